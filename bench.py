@@ -1,0 +1,197 @@
+"""Benchmark: 10-stage GGTV-GGLR image filter on sigma=25 noisy 256x256 RGB patches.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+
+One "step" = one forward of the image-domain GGTV-GGLR filter (MultiScaleGraphFilter,
+G=32 graphs x F=3, C=96, S=10 unrolled stages, v13 feature CNN; SURVEY.md §8(d) "P")
+over one per-GPU batch of B=64 synthetic noisy patches already resident in HBM.
+N>1: one process per GPU (torchrun), each rank filters its own batch (the path shards
+by patch — no data-path collective; scaling "weak"); the timed region is bracketed by
+barrier + synchronize on both sides and the max over ranks is reported.
+
+Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
+(grr_system_step, timed live with HIP events on its launch stream) and the CPU
+baseline (the oracle, timed on this host's cores on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MPix/sec + PSNR@σ=25, 10-stage GGTV-GGLR on 256×256 patches, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+G, CIN, STAGES, H, W, SIGMA = 32, 3, 10, 256, 256, 25.0
+
+
+def synthetic_patches(n, seed, h=H, w=W):
+    """Piecewise-smooth clean patches (uint8 grid) + RandomState(seed).normal(0,1)*sigma/255 noise
+    cast to fp32, as environ/data/images_pair_restoration_dataset.py:105-108."""
+    rs = np.random.RandomState(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    clean = np.empty((n, CIN, h, w), np.float32)
+    for i in range(n):
+        for c in range(CIN):
+            fy, fx, ph = rs.uniform(0.5, 4.0), rs.uniform(0.5, 4.0), rs.uniform(0, 6.28)
+            img = 0.5 + 0.3 * np.sin(2 * np.pi * fy * yy / h + ph) * np.cos(2 * np.pi * fx * xx / w)
+            for _ in range(3):
+                r0, c0 = rs.randint(0, h - h // 4), rs.randint(0, w - w // 4)
+                img[r0:r0 + rs.randint(8, h // 3), c0:c0 + rs.randint(8, w // 3)] += rs.uniform(-0.3, 0.3)
+            clean[i, c] = img
+    clean = np.round(np.clip(clean, 0, 1) * 255.0) / 255.0
+    noise = (rs.normal(0, 1, clean.shape) * (SIGMA / 255.0)).astype(np.float32)
+    return torch.from_numpy(clean.astype(np.float32)), torch.from_numpy(clean.astype(np.float32) + noise)
+
+
+def build_model(device, seed=2204):
+    import irdu_amd
+    torch.manual_seed(seed)  # reference init: default conv init + the reference's solver init constants
+    return irdu_amd.MultiScaleGraphFilter(CIN, CIN, ngraphs=G, n_cgd_iters=STAGES).to(device).eval()
+
+
+def load_traffic():
+    """Per-launch HBM bytes of grr_system_step from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "traffic_system_step.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(model_cpu_state, n_img=4):
+    """The oracle (reference op sequence, PyTorch-CPU fp32) on a bounded sample of the workload."""
+    from oracle import graph_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    clean, noisy = synthetic_patches(n_img, seed=99)
+    # warm-up on a small crop (allocator / thread pool), then the timed sample
+    O.multiscale_graph_filter(noisy[:1, :, :32, :32], model_cpu_state, G)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref = O.multiscale_graph_filter(noisy, model_cpu_state, G)
+    dt = time.perf_counter() - t0
+    mpix = n_img * H * W / dt / 1e6
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": mpix, "unit": "MPix/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} patches {H}x{W} RGB sigma=25, S={STAGES}, G={G}: {dt:.1f} s on {cpu}",
+            "seconds": dt}, clean, noisy, ref
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="patches per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import irdu_amd
+    from irdu_amd import kernels as K
+    irdu_amd.load_native()
+    model = build_model(dev)
+    b = args.batch
+    # each rank its own shard of patches (seed by rank): resident in HBM before timing
+    _, noisy = synthetic_patches(b, seed=2204 + rank)
+    noisy = noisy.to(dev)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = model(noisy)
+        barrier()
+        timer = K.LaunchTimer()
+        K.set_timer(timer)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = model(noisy)
+        barrier()
+        dt = time.perf_counter() - t0
+        K.set_timer(None)
+    kern = timer.summary()
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    px_total = world * b * H * W * args.steps
+    value = px_total / dt / 1e6
+    step = kern["system_step"]
+    achieved = step["gbps"]
+    traffic = load_traffic()
+    roofline = {"bound": "hbm", "kernel": "grr_system_step (graph_op_kernel<GLR,GTV_PAIR,EPI_STEP>)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "bytes_per_launch": step["bytes_per_launch"], "mean_launch_ms": round(step["mean_ms"], 4),
+                "launches": step["launches"]}
+    res = {"metric": METRIC, "value": round(value, 3), "unit": "MPix/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": "MultiScaleGraphFilter (image-domain GGTV-GGLR, v13 feature CNN) "
+                                  f"G={G} F={CIN} C={G * CIN}, S={STAGES} stages, {H}x{W} RGB sigma=25, "
+                                  f"random-init weights (reference init constants)",
+                      "global_batch": world * b, "per_gpu_batch": b, "image": f"{H}x{W}x{CIN}",
+                      "parallelism": f"batch-sharded x{world}, no collective in the data path"},
+           "roofline": roofline}
+    kernels_ms = {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}
+    res["kernel_ms_per_step"] = kernels_ms
+    if args.breakdown:
+        for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
+            print(f"{k:18s} launches/step={v['launches'] / args.steps:5.1f} mean={v['mean_ms']:8.3f} ms "
+                  f"algo={v['gbps']:8.1f} GB/s", file=sys.stderr)
+    if not args.no_cpu_baseline:
+        from oracle import graph_oracle as O
+        state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        cb, clean, cnoisy, ref = cpu_baseline(state)
+        with torch.no_grad():
+            got = model(cnoisy.to(dev)).cpu()
+        rel = float((got.double() - ref.double()).abs().max() / ref.double().abs().max())
+        p_gpu, p_cpu = O.psnr_ubyte(got, clean), O.psnr_ubyte(ref, clean)
+        res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()
+                               if k != "seconds"}
+        res["psnr"] = {"gpu_db": round(p_gpu, 4), "oracle_db": round(p_cpu, 4), "delta_db": round(abs(p_gpu - p_cpu), 5),
+                       "rel_err_vs_oracle": rel, "note": "random-init weights: PSNR is a parity check, not quality"}
+        res["speedup_vs_cpu"] = round(value / world / cb["value"], 1)
+    print(json.dumps(res))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

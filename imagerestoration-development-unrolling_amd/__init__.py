@@ -1,0 +1,28 @@
+"""irdu_amd — MI355X-native engine for the GGTV/GGLR unrolled graph-filter path of
+tamthuc1995/ImageRestoration-Development-Unrolling.
+
+Import as ``irdu_amd`` (the root-level ``irdu_amd.py`` loader maps this hyphenated
+directory to that package name).  The public surface mirrors the reference's
+module ``deep_multiscale_GGLR_GGTV_v1x0`` so callers can swap the import:
+
+    import irdu_amd as model_structure
+    model = model_structure.AbtractMultiScaleGraphFilter(...).cuda()
+"""
+from ._native import GrrError, NativeUnavailable, load as load_native  # noqa: F401
+from .graph_filter import (  # noqa: F401
+    AbtractMultiScaleGraphFilter,
+    CustomLayerNorm,
+    Downsampling,
+    GLRFast,
+    GTVFast,
+    LocalGatedLinearBlock,
+    LocalLowpassFilteringBlock,
+    LocalNonLinearBlock,
+    MixtureGTVGLR,
+    MultiScaleGraphFilter,
+    ReginalPixelEmbeding,
+    Upsampling,
+)
+from . import kernels  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,90 @@
+"""ctypes binding of libgrr.so (include/grr.h).
+
+The product path has exactly one implementation: the HIP kernels in this library.
+If the library is missing or cannot be loaded, every op raises NativeUnavailable —
+there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_int, c_int64, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GRR_LIB", os.path.join(HERE, "libgrr.so"))
+
+
+class NativeUnavailable(RuntimeError):
+    """libgrr.so could not be loaded (build it with build_native.py)."""
+
+
+class GrrError(RuntimeError):
+    """A libgrr.so call returned a non-OK grr_status."""
+
+    def __init__(self, fn: str, status: int, msg: str):
+        super().__init__(f"{fn} failed (status {status}): {msg}")
+        self.status = status
+
+
+STATUS_NAMES = {0: "GRR_OK", 1: "GRR_ERR_INVALID_ARG", 2: "GRR_ERR_SHAPE", 3: "GRR_ERR_UNSUPPORTED", 4: "GRR_ERR_HIP"}
+
+
+class Stencil(ctypes.Structure):
+    """grr_stencil: the four [C] stencil parameter vectors of one GLR/GTV module."""
+    _fields_ = [("p01", c_void_p), ("p02a", c_void_p), ("p02b", c_void_p), ("p03", c_void_p)]
+
+
+P = c_void_p
+I = c_int
+L = c_int64
+
+# name -> argtypes (restype is grr_status == int unless listed in _RESTYPES)
+SIGNATURES = {
+    "grr_version": [],
+    "grr_last_error": [],
+    "grr_neighbor_table": [P, I, I, P],
+    "grr_edge_weights": [P, L, P, P, P, I, I, I, I, I, P],
+    "grr_gtv_pair_weights": [P, P, I, I, I, I, P],
+    "grr_pool2": [P, P, I, I, I, I, P],
+    "grr_system_half": [P, P, P, Stencil, Stencil, P, P, P, I, I, I, I, I, P],
+    "grr_gtv_rhs_half": [P, P, Stencil, I, P, P, I, I, I, I, I, P],
+    "grr_gtv_rhs_full": [P, P, P, Stencil, I, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_system_step": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_conv1x1": [P, P, P, I, I, I, L, P],
+    "grr_conv2x2s2": [P, P, P, I, I, I, I, I, P],
+    "grr_lnb_workspace_bytes": [I, I, I, I, I],
+    "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_repeat_graphs": [P, P, I, I, I, L, P],
+}
+_RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libgrr.so once and bind every symbol of include/grr.h."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable(
+            f"{LIB_PATH} not found: build it with `python imagerestoration-development-unrolling_amd/build_native.py`")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the host
+        raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, c_int)
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    """Call a status-returning entry point; raise GrrError on failure."""
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != 0:
+        msg = lib.grr_last_error()
+        raise GrrError(name, st, (msg or b"").decode(errors="replace"))

@@ -1,0 +1,298 @@
+// gfx950 kernels of the feature CNN that produces the graph features
+// (a13 of SURVEY.md §8; REF13 = lib/model_GLR_GTV_deep_v13_no_latent.py).
+//
+// Dense channel mixing (1x1 and 2x2/s2 convolutions) is a batched GEMM
+//   out[b] (M x P) = Wt (M x K) * Bop[b] (K x P),   P = pixels,
+// computed on the matrix cores with the exact-fp32 MFMA v_mfma_f32_32x32x2_f32
+// (gfx950 has no xf32; f32-in MFMA is bit-for-bit an fmaf chain, so the result
+// stays within fp32 rounding of the reference's CPU conv).  The B-operand loader
+// fuses CustomLayerNorm's normalisation (LN GEMM) or the 2x2/s2 im2col gather.
+// Depthwise 3x3 + gating and the LayerNorm statistics are memory-bound kernels.
+#include "grr_common.h"
+
+namespace grr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int GT = 256;             // threads per GEMM workgroup (4 waves)
+constexpr int BM = 64, BN = 64, BK = 32;
+constexpr int APAD = BM + 4, BPAD = BN + 4;
+
+enum { LD_PLAIN = 0, LD_LN = 1, LD_IM2COL = 2 };
+enum { EP_STORE = 0, EP_SKIP = 1 };
+
+struct GemmArgs {
+  const float* x;      // activations [B, K, P]  (im2col: [B, Cin, H, W])
+  const float* wt;     // [M, K]
+  const float* ln_sd;  // LD_LN: [B, P] sqrt(var + eps)
+  const float* ln_w;   // LD_LN: [K]
+  const float* res;    // EP_SKIP: [B, M, P]
+  const float* skip;   // EP_SKIP: [2]
+  float* out;          // [B, M, P]
+  int K, M;
+  int64_t P;
+  int Hin, Win, Wo;    // im2col geometry
+  int mt, nt;
+  uint32_t nblk;
+};
+
+template <int LOADER, int EPI>
+__global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
+  __shared__ float As[BK][APAD];
+  __shared__ float Bs[BK][BPAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int mtile = lb % a.mt; lb /= a.mt;       // M tiles of one pixel tile are neighbours
+  const int ntile = lb % a.nt;
+  const int b = lb / a.nt;
+  const int m0 = mtile * BM;
+  const int64_t n0 = (int64_t)ntile * BN;
+  const int K = a.K, M = a.M;
+  const int64_t P = a.P;
+  const float* xb = a.x + (int64_t)b * (LOADER == LD_IM2COL ? (int64_t)(K / 4) * a.Hin * a.Win : (int64_t)K * P);
+
+  float sdv[4] = {1.f, 1.f, 1.f, 1.f};
+  if constexpr (LOADER == LD_LN) {
+    // this thread's 4 B-tile columns are fixed across the K loop
+    const int nn = (tid & 15) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t n = n0 + nn + q;
+      sdv[q] = n < P ? a.ln_sd[(int64_t)b * P + n] : 1.f;
+    }
+  }
+  f32x16 acc = {};
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    // A tile: wt[m0..m0+63][k0..k0+31] -> As[k][m]
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * GT;          // 512 float4 slots
+      const int m = idx >> 3, kq = (idx & 7) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = k0 + kq + q, mm = m0 + m;
+        As[kq + q][m] = (mm < M && k < K) ? a.wt[(int64_t)mm * K + k] : 0.f;
+      }
+    }
+    // B tile: Bop[k0..k0+31][n0..n0+63] -> Bs[k][n]
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * GT;
+      const int kk = idx >> 4, nn = (idx & 15) * 4;
+      const int k = k0 + kk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t n = n0 + nn + q;
+        float v = 0.f;
+        if (k < K && n < P) {
+          if constexpr (LOADER == LD_IM2COL) {
+            const int ci = k >> 2, ay = (k >> 1) & 1, ax = k & 1;
+            const int oy = (int)(n / a.Wo), ox = (int)(n - (int64_t)oy * a.Wo);
+            v = xb[((int64_t)ci * a.Hin + 2 * oy + ay) * a.Win + 2 * ox + ax];
+          } else {
+            v = xb[(int64_t)k * P + n];
+            if constexpr (LOADER == LD_LN) v = (v / sdv[q]) * a.ln_w[k];   // REF:921-925
+          }
+        }
+        Bs[kk][nn + q] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const float av = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float bv = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float s0 = 0.f, s1 = 1.f;
+  if constexpr (EPI == EP_SKIP) { s0 = a.skip[0]; s1 = a.skip[1]; }
+  const int64_t n = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (m < M && n < P) {
+      const int64_t o = ((int64_t)b * M + m) * P + n;
+      float v = acc[r];
+      if constexpr (EPI == EP_SKIP) v = s0 * a.res[o] + s1 * v;          // REF:962-964
+      a.out[o] = v;
+    }
+  }
+}
+
+template <int LOADER, int EPI>
+static grr_status launch_gemm(GemmArgs a, int B, hipStream_t s, const char* name) {
+  a.mt = (a.M + BM - 1) / BM;
+  const int64_t nt = (a.P + BN - 1) / BN;
+  GRR_REQUIRE(nt < (1ll << 30), GRR_ERR_UNSUPPORTED, "%s: too many pixels", name);
+  a.nt = (int)nt;
+  const uint64_t n = (uint64_t)B * a.mt * a.nt;
+  GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
+  a.nblk = (uint32_t)n;
+  hipLaunchKernelGGL((gemm_f32_kernel<LOADER, EPI>), dim3(a.nblk), dim3(GT), 0, s, a);
+  return launch_status(name);
+}
+
+// CustomLayerNorm statistics: sd[b,p] = sqrt(var_c x[b,c,p] + 1e-5), unbiased (REF:919-922)
+__global__ void ln_stats_kernel(const float* __restrict__ x, float* __restrict__ sd, int B, int C, int64_t P) {
+  const int64_t n = (int64_t)B * P;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / P, p = i - b * P;
+    const float* xp = x + b * C * P + p;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += xp[(int64_t)c * P];
+    const float mean = s / (float)C;
+    float q = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float d = xp[(int64_t)c * P] - mean;
+      q += d * d;
+    }
+    sd[i] = sqrtf(q / (float)(C - 1) + 1e-5f);
+  }
+}
+
+// depthwise 3x3 (replicate pad) on the 2*hid GEMM output, then the gate
+// g = sigmoid(mask) * mask * value  (REF:934-947).  One workgroup = (b, j, 32x32 tile).
+constexpr int DT = 32, DS = DT + 2, DA = DS * DS;
+__global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ h, const float* __restrict__ wdw,
+                                                      float* __restrict__ gout, int hid, int H, int W,
+                                                      int tiles_x, int tiles_y, uint32_t nblk) {
+  __shared__ float Ms[DA];
+  __shared__ float Vs[DA];
+  uint32_t lb = xcd_remap(blockIdx.x, nblk);
+  const int tx = lb % tiles_x; lb /= tiles_x;
+  const int ty = lb % tiles_y; lb /= tiles_y;
+  const int j = lb % hid;
+  const int b = lb / hid;
+  const int y0 = ty * DT, x0 = tx * DT;
+  const int64_t HW = (int64_t)H * W;
+  const float* mp = h + ((int64_t)b * 2 * hid + j) * HW;
+  const float* vp = h + ((int64_t)b * 2 * hid + hid + j) * HW;
+  for (int i = threadIdx.x; i < DA; i += 256) {
+    const int ry = i / DS, rx = i - ry * DS;
+    const int64_t o = (int64_t)clampi(y0 - 1 + ry, 0, H - 1) * W + clampi(x0 - 1 + rx, 0, W - 1);
+    Ms[i] = mp[o];
+    Vs[i] = vp[o];
+  }
+  float km[9], kv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    km[t] = wdw[j * 9 + t];
+    kv[t] = wdw[(hid + j) * 9 + t];
+  }
+  __syncthreads();
+  float* gp = gout + ((int64_t)b * hid + j) * HW;
+  for (int i = threadIdx.x; i < DT * DT; i += 256) {
+    const int oy = i / DT, ox = i - oy * DT;
+    const int gy = y0 + oy, gx = x0 + ox;
+    if (gy >= H || gx >= W) continue;
+    float m = 0.f, v = 0.f;
+#pragma unroll
+    for (int ay = 0; ay < 3; ++ay)
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        const int li = (oy + ay) * DS + ox + ax;
+        m += km[ay * 3 + ax] * Ms[li];
+        v += kv[ay * 3 + ax] * Vs[li];
+      }
+    const float sg = 1.0f / (1.0f + expf(-m));
+    gp[(int64_t)gy * W + gx] = (sg * m) * v;
+  }
+}
+
+__global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __restrict__ out, int Cin, int G,
+                                     int64_t P, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i % P;
+    const int64_t r = i / P;              // b * (G*Cin) + g*Cin + c
+    const int c = (int)(r % Cin);
+    const int64_t b = r / ((int64_t)G * Cin);
+    out[i] = img[(b * Cin + c) * P + p];
+  }
+}
+
+}  // namespace grr
+
+using namespace grr;
+
+extern "C" {
+
+grr_status grr_conv1x1(const float* x, const float* wt, float* out, int B, int K, int M, int64_t P, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && wt && out && B > 0 && K > 0 && M > 0 && P > 0, GRR_ERR_INVALID_ARG, "grr_conv1x1: bad args");
+  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_conv1x1: out aliases x");
+  GemmArgs a{};
+  a.x = x; a.wt = wt; a.out = out; a.K = K; a.M = M; a.P = P;
+  return launch_gemm<LD_PLAIN, EP_STORE>(a, B, (hipStream_t)stream, "grr_conv1x1");
+}
+
+grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int K, int M, int H, int W,
+                         void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && wt && out && B > 0 && K > 0 && M > 0 && H > 1 && W > 1, GRR_ERR_INVALID_ARG,
+              "grr_conv2x2s2: bad args");
+  GemmArgs a{};
+  a.x = x; a.wt = wt; a.out = out; a.K = 4 * K; a.M = M; a.P = (int64_t)(H / 2) * (W / 2);
+  a.Hin = H; a.Win = W; a.Wo = W / 2;
+  return launch_gemm<LD_IM2COL, EP_STORE>(a, B, (hipStream_t)stream, "grr_conv2x2s2");
+}
+
+int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
+  (void)C;
+  const int64_t P = (int64_t)H * W;
+  const int64_t sd = ((int64_t)B * P + 63) / 64 * 64;
+  return (sd + (int64_t)B * 3 * hid * P) * (int64_t)sizeof(float);
+}
+
+grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
+                           const float* skip, float* out, void* workspace, int B, int C, int hid, int H, int W,
+                           void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && C > 1 && hid > 0 && H > 0 &&
+                  W > 0,
+              GRR_ERR_INVALID_ARG, "grr_lnb_forward: bad args");
+  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward: out aliases x");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t P = (int64_t)H * W;
+  float* sd = (float*)workspace;
+  float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;   // [B, 2hid, P]
+  float* gbuf = hbuf + (int64_t)B * 2 * hid * P;        // [B, hid, P]
+  {
+    const int64_t n = (int64_t)B * P;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
+    hipLaunchKernelGGL(ln_stats_kernel, dim3(blocks), dim3(256), 0, s, x, sd, B, C, P);
+    grr_status st = launch_status("grr_lnb_forward/ln_stats");
+    if (st != GRR_OK) return st;
+  }
+  {
+    GemmArgs a{};
+    a.x = x; a.wt = w1; a.ln_sd = sd; a.ln_w = ln_w; a.out = hbuf; a.K = C; a.M = 2 * hid; a.P = P;
+    grr_status st = launch_gemm<LD_LN, EP_STORE>(a, B, s, "grr_lnb_forward/gemm1");
+    if (st != GRR_OK) return st;
+  }
+  {
+    const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
+    const uint64_t n = (uint64_t)B * hid * tx * ty;
+    GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+    hipLaunchKernelGGL(dw_gate_kernel, dim3((uint32_t)n), dim3(256), 0, s, hbuf, wdw, gbuf, hid, H, W, tx, ty,
+                       (uint32_t)n);
+    grr_status st = launch_status("grr_lnb_forward/dw_gate");
+    if (st != GRR_OK) return st;
+  }
+  GemmArgs a{};
+  a.x = gbuf; a.wt = w2; a.res = x; a.skip = skip; a.out = out; a.K = hid; a.M = C; a.P = P;
+  return launch_gemm<LD_PLAIN, EP_SKIP>(a, B, s, "grr_lnb_forward/gemm2");
+}
+
+grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {
+  clear_error();
+  GRR_REQUIRE(img && out && B > 0 && Cin > 0 && G > 0 && P > 0, GRR_ERR_INVALID_ARG, "grr_repeat_graphs: bad args");
+  const int64_t n = (int64_t)B * G * Cin * P;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
+  hipLaunchKernelGGL(repeat_graphs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, img, out, Cin, G, P, n);
+  return launch_status("grr_repeat_graphs");
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+// Shared helpers for the gfx950 kernels of libgrr.so (status plumbing, indexing,
+// XCD-aware block remap).  Written for CDNA4 only: wave64, 8 XCDs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <string>
+
+#include "../../include/grr.h"
+
+namespace grr {
+
+// thread-local last error (grr_last_error)
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define GRR_REQUIRE(cond, code, ...)        \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::grr::set_error(__VA_ARGS__);        \
+      return code;                          \
+    }                                       \
+  } while (0)
+
+// Check the launch that was just queued on the stream.
+grr_status launch_status(const char* what);
+
+constexpr int kWave = 64;
+constexpr int kXcd = 8;
+
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch);
+// re-label them so each XCD walks one contiguous chunk of the logical grid, i.e.
+// neighbouring tiles (which share halo lines) share that XCD's L2.  Bijective for
+// any n (cdna_hip_programming.md, "XCD swizzle must be bijective").  Speed only.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t n) {
+  const uint32_t xcd = bid % kXcd, q = n / kXcd, r = n % kXcd;
+  const uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / kXcd;
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+}  // namespace grr

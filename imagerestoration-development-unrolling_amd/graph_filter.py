@@ -1,0 +1,410 @@
+"""Drop-in nn.Modules for the reference's graph-filter path, executed by libgrr.so.
+
+Class names, constructor signatures, parameter names/shapes and therefore
+``state_dict`` keys match the reference (REF = exploration/GGTV_GGLR_v1.0/
+deep_multiscale_GGLR_GGTV_v1x0.py, REF13 = exploration/model_multiscale_mixture_GLR/
+lib/model_GLR_GTV_deep_v13_no_latent.py), so reference checkpoints load unchanged.
+The reference's plain-tensor constants (stats_kernel01..03, scaling_kernel01,
+edge_delta, pad_dim_hw — REF:52-118, :613) become non-persistent buffers: they
+follow ``.to()`` and stay out of the state_dict, as in the reference.
+
+Forward passes of the graph filter run only through the HIP kernels (kernels.py);
+GPU tensors are required.  Backward kernels are not part of this build yet: the
+solver is wrapped in an autograd Function whose backward raises, so training can
+never silently skip gradients.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+from torch.nn.parameter import Parameter
+
+from . import kernels as K
+
+EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, down)
+
+
+def _basis(c: int):
+    z = torch.zeros(3, 3)
+    k01 = z.clone(); k01[1, 1] = 1.0
+    k02a = z.clone(); k02a[1, 1] = -1.0; k02a[1, 2] = 1.0
+    k02b = z.clone(); k02b[1, 1] = -1.0; k02b[2, 1] = 1.0
+    k03 = torch.tensor([[0.0, -1.0, 0.0], [-1.0, 4.0, -1.0], [0.0, -1.0, 0.0]])
+    return [k.expand(c, 1, 3, 3).clone() for k in (k01, k02a, k02b, k03)]
+
+
+class _GraphModule(nn.Module):
+    """Parameters shared by GLRFast and GTVFast (REF:14-125 / :243-356)."""
+
+    def __init__(self, n_node_fts: int, n_graphs: int, M_diag_init: float = 0.4):
+        super().__init__()
+        self.n_channels = n_node_fts * n_graphs
+        self.n_node_fts = n_node_fts
+        self.n_graphs = n_graphs
+        self.n_edges = len(EDGE_DELTA)
+        self.buffer_size = self.n_edges
+        c = self.n_channels
+        self.register_buffer("edge_delta", torch.tensor(EDGE_DELTA, dtype=torch.int32), persistent=False)
+        self.register_buffer("pad_dim_hw", torch.tensor([1, 1], dtype=torch.int32), persistent=False)
+        b01, b02a, b02b, b03 = _basis(c)
+        # parameters in the reference's registration order (state_dict order)
+        self.stats_kernel_p01 = Parameter(torch.full((c, 1, 1, 1), 1.0))
+        self.register_buffer("stats_kernel01", b01, persistent=False)
+        self.stats_kernel_p02a = Parameter(torch.full((c, 1, 1, 1), 0.5))
+        self.register_buffer("stats_kernel02a", b02a, persistent=False)
+        self.stats_kernel_p02b = Parameter(torch.full((c, 1, 1, 1), 0.5))
+        self.register_buffer("stats_kernel02b", b02b, persistent=False)
+        self.stats_kernel_p03 = Parameter(torch.full((c, 1, 1, 1), 0.5))
+        self.register_buffer("stats_kernel03", b03, persistent=False)
+        self.multiM = Parameter(torch.full((n_graphs, n_node_fts), float(M_diag_init)))
+
+    def extract_edge_weights(self, img_features: torch.Tensor):
+        """[B,G,F,H,W] features -> (w [B,G,4,H,W], degree [B,G,H,W]) (REF:160-175)."""
+        b, g, f, h, w = img_features.shape
+        x = img_features.reshape(b, g * f, h, w).contiguous()
+        return K.edge_weights(x, 0, g, f, self.multiM.data.contiguous(), with_degree=True)
+
+    def neighbor_table(self, h: int, w: int) -> torch.Tensor:
+        """int32 [4,H,W] flat indices of the neighbours each edge reads (REF:128-144)."""
+        return K.neighbor_table(h, w, self.multiM.device)
+
+
+class GLRFast(_GraphModule):
+    """Graph-Laplacian regulariser S^T (I - W) S (REF:13-237)."""
+
+    def forward(self, patchs, edge_weights, node_degree=None):
+        b, g, f, h, w = patchs.shape
+        out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), edge_weights.contiguous(), None,
+                            K.stencil(self), K.NO_STENCIL, None, None, g)
+        return out.view(b, g, f, h, w)
+
+
+class GTVFast(_GraphModule):
+    """Graph total variation C^T C with C = W (S - S shifted) (REF:242-523)."""
+
+    def forward(self, patchs, edge_weights, node_degree=None):
+        b, g, f, h, w = patchs.shape
+        c = K.gtv_pair_weights(edge_weights.contiguous())
+        out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), None, c,
+                            K.NO_STENCIL, K.stencil(self), None, None, g)
+        return out.view(b, g, f, h, w)
+
+
+# ---------------------------------------------------------------------------
+# Feature CNN building blocks (REF:911-964; REF13:541-575)
+# ---------------------------------------------------------------------------
+class CustomLayerNorm(nn.Module):
+    def __init__(self, nchannels, nsubnets):
+        super().__init__()
+        self.nsubnets = nsubnets
+        self.nchannels = nchannels
+        self.weighted_transform = nn.Conv2d(nchannels, nchannels, kernel_size=1, stride=1, groups=nchannels,
+                                            bias=False)
+
+    def forward(self, x):  # stock PyTorch (encoder/decoder use; hot path goes through LocalNonLinearBlock)
+        b, c, h, w = x.shape
+        xs = x.reshape(b, self.nsubnets, c // self.nsubnets, h, w)
+        xs = xs / torch.sqrt(xs.var(dim=2, keepdim=True, correction=1) + 1e-5)
+        return self.weighted_transform(xs.reshape(b, c, h, w))
+
+
+class LocalGatedLinearBlock(nn.Module):
+    def __init__(self, dim, hidden_dim, nsubnets):
+        super().__init__()
+        self.channels_linear_op = nn.Conv2d(dim, hidden_dim * 2, kernel_size=1, bias=False, groups=nsubnets)
+        self.channels_local_linear_op = nn.Conv2d(hidden_dim * 2, hidden_dim * 2, kernel_size=3, stride=1, padding=1,
+                                                  padding_mode="replicate", groups=hidden_dim * 2, bias=False)
+        self.project_out = nn.Conv2d(hidden_dim, dim, kernel_size=1, bias=False, groups=nsubnets)
+
+    def forward(self, x):
+        x = self.channels_linear_op(x)
+        mask, x = self.channels_local_linear_op(x).chunk(2, dim=1)
+        return self.project_out(torch.sigmoid(mask) * mask * x)
+
+
+class LocalNonLinearBlock(nn.Module):
+    """skip0 * x + skip1 * GatedLinear(LayerNorm(x)).  nsubnets == 1 runs the fused HIP block."""
+
+    def __init__(self, dim, hidden_dim, nsubnets):
+        super().__init__()
+        self.dim, self.hidden_dim, self.nsubnets = dim, hidden_dim, nsubnets
+        self.norm = CustomLayerNorm(dim, nsubnets)
+        self.local_linear = LocalGatedLinearBlock(dim, hidden_dim, nsubnets)
+        self.skip_weight = Parameter(torch.tensor([1.0, 1.0], dtype=torch.float32))
+
+    def forward(self, x):
+        if self.nsubnets != 1:
+            # grouped variant: only used by encoder/decoder configs (out of the hot path)
+            return self.skip_weight[0] * x + self.skip_weight[1] * self.local_linear(self.norm(x))
+        ll = self.local_linear
+        c, hid = self.dim, self.hidden_dim
+        return K.lnb_forward(x.contiguous(), self.norm.weighted_transform.weight.data.view(c),
+                             ll.channels_linear_op.weight.data.view(2 * hid, c),
+                             ll.channels_local_linear_op.weight.data.view(2 * hid, 9),
+                             ll.project_out.weight.data.view(c, hid), self.skip_weight.data)
+
+
+# ---------------------------------------------------------------------------
+# The solver block
+# ---------------------------------------------------------------------------
+class _NoBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, run, x, *params):
+        return run()
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError("irdu_amd: HIP backward kernels are not built yet; "
+                                  "run the graph filter under torch.no_grad()")
+
+
+class MixtureGTVGLR(nn.Module):
+    """Two-scale GGTV+GGLR unrolled solver (REF:526-811).
+
+    ``n_cgd_iters`` (default 3 = the reference) sets the number S of unrolled
+    stages; S > 3 follows the reference's extension pattern (REF:797-807).
+    ``feature_extractor``: "v1" = the v1.0 1x1 / 2x2 convs (REF:556-612);
+    "v13" = the image-domain 3x LocalNonLinearBlock CNN of REF13:612-698.
+    """
+
+    def __init__(self, n_graphs, n_node_fts, alpha_init, beta_init, muy_init, ro_init, gamma_init,
+                 n_cgd_iters: int = 3, feature_extractor: str = "v1"):
+        super().__init__()
+        self.n_graphs = n_graphs
+        self.n_node_fts = n_node_fts
+        self.n_channels = c = n_graphs * n_node_fts
+        self.n_cgd_iters = n_cgd_iters
+        self.feature_extractor = feature_extractor
+        muy_init, ro_init, gamma_init = (torch.as_tensor(v, dtype=torch.float32) for v in (muy_init, ro_init, gamma_init))
+        self.alphaCGD = Parameter(torch.ones((n_cgd_iters, n_graphs)) * alpha_init)
+        self.betaCGD = Parameter(torch.ones((n_cgd_iters, n_graphs)) * beta_init)
+        if feature_extractor == "v1":
+            self.patchs_features_extraction00 = nn.Sequential(nn.Conv2d(c, 2 * c, 1, bias=False))
+        else:
+            hid = int(c * 8 / 3)
+            self.patchs_features_extraction00 = nn.Sequential(
+                *[LocalNonLinearBlock(c, hid, 1) for _ in range(3)], nn.Conv2d(c, 2 * c, 1, bias=False))
+        self.ro00 = Parameter(torch.ones(n_graphs) * torch.log(ro_init[0]))
+        self.gamma00 = Parameter(torch.ones(n_graphs) * torch.log(gamma_init[0]))
+        self.GTVmodule00 = GTVFast(n_node_fts, n_graphs, M_diag_init=1.0)
+        self.muys00 = Parameter(torch.ones(n_graphs) * torch.log(muy_init[0]))
+        self.GLRmodule00 = GLRFast(n_node_fts, n_graphs, M_diag_init=1.0)
+        if feature_extractor == "v1":
+            self.patchs_features_extraction01 = nn.Sequential(nn.Conv2d(c, c, 2, stride=2, bias=False),
+                                                              nn.Conv2d(c, 2 * c, 1, bias=False))
+        else:
+            hid = int(c * 8 / 3)
+            self.patchs_features_extraction01 = nn.Sequential(
+                nn.Conv2d(c, c, 2, stride=2, bias=False), *[LocalNonLinearBlock(c, hid, 1) for _ in range(3)],
+                nn.Conv2d(c, 2 * c, 1, bias=False))
+        self.register_buffer("scaling_kernel01", torch.full((c, 1, 2, 2), 0.25), persistent=False)
+        self.ro01 = Parameter(torch.ones(n_graphs) * torch.log(ro_init[1]))
+        self.gamma01 = Parameter(torch.ones(n_graphs) * torch.log(gamma_init[1]))
+        self.GTVmodule01 = GTVFast(n_node_fts, n_graphs, M_diag_init=1.0)
+        self.muys01 = Parameter(torch.ones(n_graphs) * torch.log(muy_init[1]))
+        self.GLRmodule01 = GLRFast(n_node_fts, n_graphs, M_diag_init=1.0)
+
+    # -- feature maps (a13) --------------------------------------------------
+    def features(self, y: torch.Tensor):
+        s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
+        if self.feature_extractor == "v1":
+            f0 = K.conv1x1(y, s0[0].weight.data)
+            f1 = K.conv1x1(K.conv2x2s2(y, s1[0].weight.data), s1[1].weight.data)
+            return f0, f1
+        f0 = y
+        for blk in list(s0)[:3]:
+            f0 = blk(f0)
+        f0 = K.conv1x1(f0, s0[3].weight.data)
+        f1 = K.conv2x2s2(y, s1[0].weight.data)
+        for blk in list(s1)[1:4]:
+            f1 = blk(f1)
+        f1 = K.conv1x1(f1, s1[4].weight.data)
+        return f0, f1
+
+    # -- solver (a3-a17) -----------------------------------------------------
+    def _solve(self, y: torch.Tensor, skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+        b, c, h, w = y.shape
+        g, f = self.n_graphs, self.n_node_fts
+        if c != self.n_channels:
+            raise ValueError(f"MixtureGTVGLR: expected {self.n_channels} channels, got {c}")
+        if h % 2 or w % 2:
+            raise ValueError(f"MixtureGTVGLR: H, W must be even for the 2x2 scale (got {h}x{w})")
+        f0, f1 = self.features(y)
+        d = lambda p: p.data  # noqa: E731  (parameters are read by the kernels through raw pointers)
+        wG0, _ = K.edge_weights(f0, 0, g, f, d(self.GTVmodule00.multiM))
+        wL0, _ = K.edge_weights(f0, c, g, f, d(self.GLRmodule00.multiM))
+        wG1, _ = K.edge_weights(f1, 0, g, f, d(self.GTVmodule01.multiM))
+        wL1, _ = K.edge_weights(f1, c, g, f, d(self.GLRmodule01.multiM))
+        del f0, f1
+        cG0 = K.gtv_pair_weights(wG0)
+        cG1 = K.gtv_pair_weights(wG1)
+        sG0, sL0 = K.stencil(self.GTVmodule00), K.stencil(self.GLRmodule00)
+        sG1, sL1 = K.stencil(self.GTVmodule01), K.stencil(self.GLRmodule01)
+        mu0, mu1, ro0, ro1 = d(self.muys00), d(self.muys01), d(self.ro00), d(self.ro01)
+        alpha, beta = d(self.alphaCGD), d(self.betaCGD)
+        n_st = alpha.shape[0]
+
+        # rhs A: b_A = y + ro0 G0 y + ro1 U(G1 D y)                     (REF:738-749)
+        t = K.gtv_rhs_half(K.pool2(y), cG1, sG1, False, None, g)
+        b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+        # stage 0: x1 = b_A + alpha0 (b_A - A b_A)                     (REF:751-753)
+        last = n_st == 1
+        t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
+        x, _, xd = K.system_step(b_a, b_a, None, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[0], None, g,
+                                 want_u=False, want_pool=not last, skip=skip if last else None,
+                                 y_skip=y if last else None)
+        del b_a
+        if last:
+            return x
+        # GTV proximal step -> rhs B                                   (REF:757-781)
+        t = K.gtv_rhs_half(xd, wG1, sG1, True, d(self.gamma01), g)
+        b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, d(self.gamma00), ro0, t, ro1, g)
+        del wG0, wG1
+        u = None
+        for k in range(1, n_st):                                     # (REF:784-790, :797-807)
+            last = k == n_st - 1
+            t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
+            x, u, xd = K.system_step(x, b_b, u, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[k],
+                                     beta[k] if k >= 2 else None, g, want_u=not last, want_pool=not last,
+                                     skip=skip if last else None, y_skip=y if last else None, u_out=u)
+        return x
+
+    def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+        y = patchs.contiguous()
+        if torch.is_grad_enabled() and (y.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return _NoBackward.apply(lambda: self._solve(y, _skip), y, *[p for p in self.parameters()])
+        return self._solve(y, _skip)
+
+
+class LocalLowpassFilteringBlock(nn.Module):
+    """skip0 * x + skip1 * MixtureGTVGLR(x), the skip fused into the last stage (REF:967-988)."""
+
+    def __init__(self, dim, nsubnets, ngraphs, n_cgd_iters: int = 3):
+        super().__init__()
+        self.local_filter = MixtureGTVGLR(
+            n_graphs=ngraphs, n_node_fts=dim // ngraphs, alpha_init=0.5, beta_init=0.1,
+            muy_init=torch.tensor([[0.001], [0.0001]]), ro_init=torch.tensor([[0.0001], [0.0001]]),
+            gamma_init=torch.tensor([[0.0001], [0.0001]]), n_cgd_iters=n_cgd_iters)
+        self.skip_weight = Parameter(torch.tensor([0.5, 0.5], dtype=torch.float32))
+
+    def forward(self, x):
+        return self.local_filter(x, _skip=self.skip_weight.data)
+
+
+class MultiScaleGraphFilter(nn.Module):
+    """Image-domain GGTV-GGLR filter (REF13:887-926): RGB replicated over G graphs,
+    MixtureGTVGLR with the v13 feature CNN, then a 1x1 projection to the output."""
+
+    def __init__(self, n_channels_in=3, n_channels_out=3, ngraphs=16, n_cgd_iters: int = 3):
+        super().__init__()
+        self.ngraphs = ngraphs
+        self.n_channels_in = n_channels_in
+        self.localfilter = MixtureGTVGLR(
+            n_graphs=ngraphs, n_node_fts=n_channels_in, alpha_init=0.5, beta_init=0.1,
+            muy_init=torch.tensor([[0.001], [0.0001]]), ro_init=torch.tensor([[0.0001], [0.0001]]),
+            gamma_init=torch.tensor([[0.0001], [0.0001]]), n_cgd_iters=n_cgd_iters, feature_extractor="v13")
+        self.linear_combination = nn.Conv2d(ngraphs * n_channels_in, n_channels_out, 1, bias=False)
+
+    def forward(self, img):
+        x = K.repeat_graphs(img.contiguous(), self.ngraphs)
+        y = self.localfilter(x)
+        return K.conv1x1(y, self.linear_combination.weight.data)
+
+
+# ---------------------------------------------------------------------------
+# v1.0 end-to-end model (REF:991-1174).  Encoder/decoder are outside the hot path:
+# their convolutions run as stock PyTorch-ROCm ops; LocalNonLinearBlocks with
+# nsubnets == 1 and the four filter blocks run on the HIP kernels.
+# ---------------------------------------------------------------------------
+class ReginalPixelEmbeding(nn.Module):
+    def __init__(self, n_channels_in=3, dim=48, bias=False):
+        super().__init__()
+        self.channels_local_linear_op01 = nn.Conv2d(n_channels_in, dim, kernel_size=3, stride=1, padding=1,
+                                                    padding_mode="replicate", bias=False)
+
+    def forward(self, x):
+        return self.channels_local_linear_op01(x)
+
+
+class Downsampling(nn.Module):
+    def __init__(self, dim_in, dim_out, nsubnets):
+        super().__init__()
+        self.local_linear = nn.Conv2d(dim_in, dim_out, kernel_size=2, stride=2, padding=0, groups=nsubnets, bias=False)
+
+    def forward(self, x):
+        return self.local_linear(x)
+
+
+class Upsampling(nn.Module):
+    def __init__(self, dim_in, dim_out, nsubnets):
+        super().__init__()
+        self.local_linear = nn.ConvTranspose2d(dim_in, dim_out, kernel_size=2, stride=2, padding=0, groups=nsubnets,
+                                               bias=False)
+
+    def forward(self, x):
+        return self.local_linear(x)
+
+
+class AbtractMultiScaleGraphFilter(nn.Module):
+    def __init__(self, n_channels_in=3, n_channels_out=3, dims=(48, 64, 96, 128), hidden_dims=(128, 192, 256, 384),
+                 nsubnets=(1, 1, 1, 1), ngraphs=(4, 4, 8, 8), num_blocks=(4, 6, 6, 8), num_blocks_out=4,
+                 n_cgd_iters: int = 3):
+        super().__init__()
+        dims, hidden_dims, nsubnets, ngraphs, num_blocks = map(list, (dims, hidden_dims, nsubnets, ngraphs, num_blocks))
+
+        def blocks(i, n):
+            return nn.Sequential(*[LocalNonLinearBlock(dims[i], hidden_dims[i], nsubnets[i]) for _ in range(n)])
+
+        self.patch_3x3_embeding = ReginalPixelEmbeding(n_channels_in, dims[0])
+        self.encoder_scale_00 = blocks(0, num_blocks[0])
+        self.down_sample_00_01 = Downsampling(dims[0], dims[1], nsubnets[0])
+        self.encoder_scale_01 = blocks(1, num_blocks[1])
+        self.down_sample_01_02 = Downsampling(dims[1], dims[2], nsubnets[1])
+        self.encoder_scale_02 = blocks(2, num_blocks[2])
+        self.down_sample_02_03 = Downsampling(dims[2], dims[3], nsubnets[2])
+        self.encoder_scale_03 = blocks(3, num_blocks[3])
+        self.localfilter_scale_00 = LocalLowpassFilteringBlock(dims[0], nsubnets[0], ngraphs[0], n_cgd_iters)
+        self.localfilter_scale_01 = LocalLowpassFilteringBlock(dims[1], nsubnets[1], ngraphs[1], n_cgd_iters)
+        self.localfilter_scale_02 = LocalLowpassFilteringBlock(dims[2], nsubnets[2], ngraphs[2], n_cgd_iters)
+        self.localfilter_scale_03 = LocalLowpassFilteringBlock(dims[3], nsubnets[3], ngraphs[3], n_cgd_iters)
+        self.up_sample_03_02 = Upsampling(dims[3], dims[2], nsubnets[3])
+        self.combine_channels_02 = nn.Conv2d(dims[2] * 2, dims[2], kernel_size=1, bias=False, groups=nsubnets[2])
+        self.decoder_scale_02 = blocks(2, num_blocks[2])
+        self.up_sample_02_01 = Upsampling(dims[2], dims[1], nsubnets[2])
+        self.combine_channels_01 = nn.Conv2d(dims[1] * 2, dims[1], kernel_size=1, bias=False, groups=nsubnets[1])
+        self.decoder_scale_01 = blocks(1, num_blocks[1])
+        self.up_sample_01_00 = Upsampling(dims[1], dims[0], nsubnets[1])
+        self.combine_channels_00 = nn.Conv2d(dims[0] * 2, dims[0], kernel_size=1, bias=False, groups=nsubnets[0])
+        self.decoder_scale_00 = blocks(0, num_blocks[0])
+        self.refining_block = blocks(0, num_blocks_out)
+        self.linear_output = nn.Conv2d(dims[0], n_channels_out, kernel_size=1, bias=False)
+
+    def encode(self, img):
+        e0 = self.encoder_scale_00(self.patch_3x3_embeding(img))
+        e1 = self.encoder_scale_01(self.down_sample_00_01(e0))
+        e2 = self.encoder_scale_02(self.down_sample_01_02(e1))
+        e3 = self.encoder_scale_03(self.down_sample_02_03(e2))
+        return e0, e1, e2, e3
+
+    def filtering(self, coefs):
+        e0, e1, e2, e3 = coefs
+        return (self.localfilter_scale_00(e0), self.localfilter_scale_01(e1),
+                self.localfilter_scale_02(e2), self.localfilter_scale_03(e3))
+
+    def decode(self, coefs):
+        e0, e1, e2, e3 = coefs
+        d = self.combine_channels_02(torch.cat([self.up_sample_03_02(e3), e2], 1))
+        d = self.decoder_scale_02(d)
+        d = self.combine_channels_01(torch.cat([self.up_sample_02_01(d), e1], 1))
+        d = self.decoder_scale_01(d)
+        d = self.combine_channels_00(torch.cat([self.up_sample_01_00(d), e0], 1))
+        d = self.decoder_scale_00(d)
+        return self.linear_output(self.refining_block(d))
+
+    def enc_dec(self, img):
+        return self.decode(self.encode(img))
+
+    def forward(self, img):
+        return self.decode(self.filtering(self.encode(img)))

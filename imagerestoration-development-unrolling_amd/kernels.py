@@ -1,0 +1,262 @@
+"""Torch-tensor front end of the HIP kernels (one function per C-ABI entry point).
+
+Every function checks that its tensors are fp32, contiguous and on the GPU,
+allocates its outputs with ``torch.empty`` (the C ABI never allocates), and
+launches on the current torch stream of that device.  There is no fallback: a CPU
+tensor or a missing libgrr.so raises.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _native
+from ._native import Stencil, call
+
+Tensor = torch.Tensor
+
+
+def _ptr(t: Optional[Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _check(name: str, *ts: Optional[Tensor]) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(f"{name}: tensors must be on the GPU (got {t.device}); "
+                               "the HIP engine has no CPU path")
+        if t.dtype != torch.float32:
+            raise TypeError(f"{name}: expected float32, got {t.dtype}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: expected a contiguous tensor")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"{name}: tensors on different devices ({dev} vs {t.device})")
+    return dev
+
+
+def _stream(dev: torch.device):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class LaunchTimer:
+    """Brackets each launch with HIP events on the stream it is queued on.
+
+    ``records[kind]`` collects (start, end, algorithmic_bytes) per launch; ``summary()``
+    synchronises and returns per-kind launch count, mean duration and achieved GB/s.
+    """
+
+    def __init__(self):
+        self.records = {}
+
+    def run(self, kind: str, nbytes: int, fn):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        self.records.setdefault(kind, []).append((s, e, nbytes))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, recs in self.records.items():
+            ms = [s.elapsed_time(e) for s, e, _ in recs]
+            nb = sum(b for _, _, b in recs)
+            tot = sum(ms)
+            out[kind] = {"launches": len(recs), "total_ms": tot, "mean_ms": tot / len(recs),
+                         "bytes_per_launch": nb / len(recs), "gbps": nb / (tot * 1e-3) / 1e9 if tot > 0 else 0.0}
+        return out
+
+
+_TIMER = None
+
+
+def set_timer(timer):
+    """Install (or clear, with None) a LaunchTimer for subsequent launches."""
+    global _TIMER
+    _TIMER = timer
+
+
+def _launch(kind: str, nbytes: int, name: str, *args):
+    if _TIMER is None:
+        call(name, *args)
+    else:
+        _TIMER.run(kind, int(nbytes), lambda: call(name, *args))
+
+
+def stencil(module) -> Stencil:
+    """grr_stencil of a GLRFast/GTVFast module (its stats_kernel_p* parameters)."""
+    ps = [module.stats_kernel_p01, module.stats_kernel_p02a, module.stats_kernel_p02b, module.stats_kernel_p03]
+    _check("stencil", *[p.data for p in ps])
+    return Stencil(*[p.data_ptr() for p in ps])
+
+
+NO_STENCIL = Stencil(None, None, None, None)
+
+
+# ---------------------------------------------------------------------------
+def neighbor_table(h: int, w: int, device) -> Tensor:
+    out = torch.empty((4, h, w), dtype=torch.int32, device=device)
+    call("grr_neighbor_table", out.data_ptr(), h, w, _stream(out.device))
+    return out
+
+
+def edge_weights(feat: Tensor, channel_offset: int, n_graphs: int, n_fts: int, multiM: Tensor,
+                 with_degree: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+    """Edge weights of the [n_graphs*n_fts] channel slab starting at ``channel_offset`` of feat [B,Ctot,H,W]."""
+    dev = _check("edge_weights", feat, multiM)
+    b, ctot, h, w = feat.shape
+    if channel_offset + n_graphs * n_fts > ctot:
+        raise ValueError("edge_weights: channel slab out of range")
+    wt = torch.empty((b, n_graphs, 4, h, w), dtype=torch.float32, device=dev)
+    deg = torch.empty((b, n_graphs, h, w), dtype=torch.float32, device=dev) if with_degree else None
+    base = feat.data_ptr() + channel_offset * h * w * feat.element_size()
+    nbytes = 4 * b * h * w * (n_graphs * n_fts + 4 * n_graphs + (n_graphs if with_degree else 0))
+    _launch("edge_weights", nbytes, "grr_edge_weights", base, ctot * h * w, multiM.data_ptr(), wt.data_ptr(),
+            _ptr(deg), b, n_graphs, n_fts, h, w, _stream(dev))
+    return wt, deg
+
+
+def gtv_pair_weights(w: Tensor) -> Tensor:
+    dev = _check("gtv_pair_weights", w)
+    b, g, four, h, ww = w.shape
+    assert four == 4
+    c = torch.empty((b, g, 2, h, ww), dtype=torch.float32, device=dev)
+    _launch("gtv_pair_weights", 4 * b * g * h * ww * 6, "grr_gtv_pair_weights", w.data_ptr(), c.data_ptr(),
+            b, g, h, ww, _stream(dev))
+    return c
+
+
+def pool2(x: Tensor) -> Tensor:
+    dev = _check("pool2", x)
+    b, c, h, w = x.shape
+    out = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev)
+    _launch("pool2", 4 * b * c * h * w * 5 // 4, "grr_pool2", x.data_ptr(), out.data_ptr(), b, c, h, w, _stream(dev))
+    return out
+
+
+def system_half(xd: Tensor, wL: Optional[Tensor], cG: Optional[Tensor], sL: Stencil, sG: Stencil,
+                log_mu: Optional[Tensor], log_ro: Optional[Tensor], n_graphs: int) -> Tensor:
+    dev = _check("system_half", xd, wL, cG, log_mu, log_ro)
+    b, c, h, w = xd.shape
+    t = torch.empty_like(xd)
+    nbytes = 4 * b * h * w * (2 * c + (4 * n_graphs if wL is not None else 0) + (2 * n_graphs if cG is not None else 0))
+    _launch("system_half", nbytes, "grr_system_half", xd.data_ptr(), _ptr(wL), _ptr(cG), sL, sG, _ptr(log_mu),
+            _ptr(log_ro), t.data_ptr(), b, n_graphs, c // n_graphs, h, w, _stream(dev))
+    return t
+
+
+def gtv_rhs_half(xd: Tensor, wG: Tensor, sG: Stencil, prox: bool, log_gamma: Optional[Tensor],
+                 n_graphs: int) -> Tensor:
+    dev = _check("gtv_rhs_half", xd, wG, log_gamma)
+    b, c, h, w = xd.shape
+    t = torch.empty_like(xd)
+    nbytes = 4 * b * h * w * (2 * c + (4 if prox else 2) * n_graphs)
+    _launch("gtv_rhs_half", nbytes, "grr_gtv_rhs_half", xd.data_ptr(), wG.data_ptr(), sG, int(prox),
+            _ptr(log_gamma), t.data_ptr(), b, n_graphs, c // n_graphs, h, w, _stream(dev))
+    return t
+
+
+def gtv_rhs_full(x: Tensor, y: Tensor, wG: Tensor, sG: Stencil, prox: bool, log_gamma: Optional[Tensor],
+                 log_ro0: Tensor, t_half: Optional[Tensor], log_ro1: Optional[Tensor], n_graphs: int,
+                 want_pool: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+    dev = _check("gtv_rhs_full", x, y, wG, log_gamma, log_ro0, t_half, log_ro1)
+    b, c, h, w = x.shape
+    out = torch.empty_like(x)
+    xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_pool else None
+    px = b * h * w
+    nbytes = 4 * (px * (3 * c if x.data_ptr() != y.data_ptr() else 2 * c) + px * (4 if prox else 2) * n_graphs
+                  + (px * c // 4 if t_half is not None else 0) + (px * c // 4 if want_pool else 0))
+    _launch("gtv_rhs_full", nbytes, "grr_gtv_rhs_full", x.data_ptr(), y.data_ptr(), wG.data_ptr(), sG, int(prox),
+            _ptr(log_gamma), log_ro0.data_ptr(), _ptr(t_half), _ptr(log_ro1), out.data_ptr(), _ptr(xd),
+            b, n_graphs, c // n_graphs, h, w, _stream(dev))
+    return out, xd
+
+
+def system_step(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Optional[Tensor],
+                wL: Optional[Tensor], cG: Optional[Tensor], sL: Stencil, sG: Stencil,
+                log_mu0: Optional[Tensor], log_ro0: Optional[Tensor], alpha: Tensor, beta: Optional[Tensor],
+                n_graphs: int, want_u: bool, want_pool: bool, skip: Optional[Tensor] = None,
+                y_skip: Optional[Tensor] = None, u_out: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor], Optional[Tensor]]:
+    dev = _check("system_step", x, rhs, u_prev, t_half, wL, cG, log_mu0, log_ro0, alpha, beta, skip, y_skip)
+    b, c, h, w = x.shape
+    out = torch.empty_like(x)
+    if want_u and u_out is None:
+        u_out = torch.empty_like(x)
+    if not want_u:
+        u_out = None
+    xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_pool else None
+    _launch("system_step", step_bytes(b, c, n_graphs, h, w, rhs is not x, u_prev is not None, t_half is not None,
+                                      wL is not None, cG is not None, u_out is not None, want_pool, skip is not None),
+            "grr_system_step", x.data_ptr(), rhs.data_ptr(), _ptr(u_prev), _ptr(t_half), _ptr(wL), _ptr(cG), sL, sG,
+            _ptr(log_mu0), _ptr(log_ro0), alpha.data_ptr(), _ptr(beta), _ptr(skip), _ptr(y_skip),
+            out.data_ptr(), _ptr(u_out), _ptr(xd), b, n_graphs, c // n_graphs, h, w, _stream(dev))
+    return out, u_out, xd
+
+
+def step_bytes(b, c, g, h, w, has_rhs, has_u_prev, has_half, has_glr, has_gtv, has_u_out, has_pool, has_skip):
+    """Compulsory HBM bytes of one grr_system_step launch (each input read once, each output written once)."""
+    f = c * (1 + int(has_rhs) + int(has_u_prev) + int(has_u_out) + 1 + int(has_skip))  # x, b, u_prev, u, x_out, y
+    f += (c // 4) * (int(has_half) + int(has_pool))                                     # half-level in / out
+    f += g * (4 * int(has_glr) + 2 * int(has_gtv))                                      # edge / pair weights
+    return 4 * b * h * w * f
+
+
+# ---- feature CNN -----------------------------------------------------------
+def conv1x1(x: Tensor, weight: Tensor) -> Tensor:
+    """nn.Conv2d(K, M, 1, bias=False) with weight [M,K,1,1]."""
+    dev = _check("conv1x1", x, weight)
+    b, k, h, w = x.shape
+    m = weight.shape[0]
+    if weight.shape[1] != k:
+        raise ValueError(f"conv1x1: weight {tuple(weight.shape)} vs input channels {k}")
+    out = torch.empty((b, m, h, w), dtype=torch.float32, device=dev)
+    _launch("conv1x1", 4 * b * h * w * (k + m), "grr_conv1x1", x.data_ptr(), weight.data_ptr(), out.data_ptr(),
+            b, k, m, h * w, _stream(dev))
+    return out
+
+
+def conv2x2s2(x: Tensor, weight: Tensor) -> Tensor:
+    """nn.Conv2d(K, M, 2, stride=2, bias=False) with weight [M,K,2,2]."""
+    dev = _check("conv2x2s2", x, weight)
+    b, k, h, w = x.shape
+    m = weight.shape[0]
+    if tuple(weight.shape[1:]) != (k, 2, 2):
+        raise ValueError(f"conv2x2s2: weight {tuple(weight.shape)} vs input channels {k}")
+    out = torch.empty((b, m, h // 2, w // 2), dtype=torch.float32, device=dev)
+    _launch("conv2x2s2", 4 * b * (h * w * k + (h // 2) * (w // 2) * m), "grr_conv2x2s2", x.data_ptr(),
+            weight.data_ptr(), out.data_ptr(), b, k, m, h, w, _stream(dev))
+    return out
+
+
+_WS_CACHE = {}
+
+
+def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor) -> Tensor:
+    """LocalNonLinearBlock (nsubnets = 1) forward."""
+    dev = _check("lnb_forward", x, ln_w, w1, wdw, w2, skip)
+    b, c, h, w = x.shape
+    hid = w2.shape[1]
+    nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
+    ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+    out = torch.empty_like(x)
+    # unfused LNB: x, h(2hid) round trip, g(hid) round trip, residual x, out
+    _launch("lnb", 4 * b * h * w * (3 * c + 2 * (2 * hid) + 2 * hid), "grr_lnb_forward", x.data_ptr(),
+            ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(), out.data_ptr(),
+            ws.data_ptr(), b, c, hid, h, w, _stream(dev))
+    return out
+
+
+def repeat_graphs(img: Tensor, n_graphs: int) -> Tensor:
+    dev = _check("repeat_graphs", img)
+    b, cin, h, w = img.shape
+    out = torch.empty((b, n_graphs * cin, h, w), dtype=torch.float32, device=dev)
+    _launch("repeat_graphs", 4 * b * h * w * cin * (1 + n_graphs), "grr_repeat_graphs", img.data_ptr(),
+            out.data_ptr(), b, cin, n_graphs, h * w, _stream(dev))
+    return out

@@ -1,0 +1,148 @@
+/*
+ * grr.h — C ABI of the MI355X (gfx950) graph-regularizer restoration engine.
+ *
+ * One shared library (libgrr.so) built with hipcc for gfx950.  Every entry point
+ * takes raw DEVICE pointers (fp32, contiguous NCHW unless stated), explicit sizes
+ * and the caller's hipStream_t (passed as void*).  The caller allocates every
+ * tensor; the library keeps no state, never allocates, never synchronises, and
+ * is safe to call from several host threads (re-entrant).  Each call returns a
+ * grr_status; on failure grr_last_error() (thread-local) holds a message.
+ *
+ * Reference interfaces replaced (REF = exploration/GGTV_GGLR_v1.0/
+ * deep_multiscale_GGLR_GGTV_v1x0.py; REF13 = exploration/model_multiscale_mixture_GLR/
+ * lib/model_GLR_GTV_deep_v13_no_latent.py) are cited per function.
+ *
+ * Shapes: B batch, G graphs, F node features per graph, C = G*F channels,
+ * H x W the resolution of the level a call runs at.  Edge order is the
+ * reference's: 0 up (-1,0), 1 left (0,-1), 2 right (0,+1), 3 down (+1,0).
+ */
+#ifndef GRR_H
+#define GRR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum grr_status {
+  GRR_OK = 0,
+  GRR_ERR_INVALID_ARG = 1, /* null pointer / non-positive size            */
+  GRR_ERR_SHAPE = 2,       /* shape the reference itself cannot run (odd H at a pooled level, ...) */
+  GRR_ERR_UNSUPPORTED = 3, /* outside this build's limits (e.g. F > GRR_MAX_NODE_FTS) */
+  GRR_ERR_HIP = 4          /* HIP launch error                           */
+} grr_status;
+
+#define GRR_MAX_NODE_FTS 24
+
+/* Library / error plumbing. */
+int grr_version(void);
+const char* grr_last_error(void);
+
+/* a1 — integer neighbour table (bit-exact target).  out[e*H*W + p] = flat index
+ * of clamp(p + delta_e): the pixel the reference's replicate-padded gather reads
+ * for edge e (REF:128-144, GLRFast.get_neighbors_pixels).  out: int32 [4,H,W]. */
+grr_status grr_neighbor_table(int32_t* out, int H, int W, void* stream);
+
+/* a3+a4 — edge weights of one graph module (REF:146-175, GLRFast/GTVFast
+ * .extract_edge_weights).  feat points at channel 0 of the module's [G*F] channel
+ * slab inside a feature tensor whose batch stride is feat_bstride elements
+ * (so the GTV/GLR halves of the 2C feature conv output need no copy, REF:714).
+ * multiM [G,F].  Writes w [B,G,4,H,W] and, if deg != NULL, deg [B,G,H,W]. */
+grr_status grr_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM,
+                            float* w, float* deg, int B, int G, int F, int H, int W, void* stream);
+
+/* Symmetric pair weights of the linear graph-TV operator C^T C: for the edge
+ * between p and its right / lower neighbour, c[.,0,p] = w_right(p)^2 + w_left(p+right)^2,
+ * c[.,1,p] = w_down(p)^2 + w_up(p+down)^2 (0 where that neighbour is outside).
+ * Algebraically identical to REF:452-516 (op_C then op_C_transpose with the
+ * frame-dropped scatter).  w [B,G,4,H,W] -> c [B,G,2,H,W]. */
+grr_status grr_gtv_pair_weights(const float* w, float* c, int B, int G, int H, int W, void* stream);
+
+/* D — 2x2 mean pool, stride 2 (REF:613, :662-665).  x [B,C,H,W] -> xd [B,C,H/2,W/2]. */
+grr_status grr_pool2(const float* x, float* xd, int B, int C, int H, int W, void* stream);
+
+/* Per-module stencil parameters: the four [C] vectors stats_kernel_p01, _p02a,
+ * _p02b, _p03 of one GLRFast/GTVFast module (REF:66-118, :177-215). */
+typedef struct grr_stencil {
+  const float* p01;
+  const float* p02a;
+  const float* p02b;
+  const float* p03;
+} grr_stencil;
+
+/* Half-resolution system term (REF:661-675, inside apply_lightweight_transformer):
+ *   t = exp(log_mu[g]) * S_L^T (I - W_L) S_L xd  +  exp(log_ro[g]) * G(xd)
+ * G = graph-TV C^T C with pair weights cG.  Either term may be disabled by a NULL
+ * weight pointer.  xd [B,C,h,w], wL [B,G,4,h,w], cG [B,G,2,h,w] -> t [B,C,h,w]. */
+grr_status grr_system_half(const float* xd, const float* wL, const float* cG,
+                           grr_stencil sL, grr_stencil sG,
+                           const float* log_mu, const float* log_ro,
+                           float* t, int B, int G, int F, int h, int w, void* stream);
+
+/* Half-resolution GTV right-hand-side term: t = C^T phi(C xd), unscaled.
+ * prox == 0: phi = identity, wG are pair weights [B,G,2,h,w] (rhs A, REF:739-747).
+ * prox != 0: phi(t) = eps - (t - eps), eps = soft_threshold(t, exp(log_gamma[g])),
+ *            wG are raw edge weights [B,G,4,h,w] (rhs B, REF:758-779; REF:684-704). */
+grr_status grr_gtv_rhs_half(const float* xd, const float* wG, grr_stencil sG, int prox,
+                            const float* log_gamma, float* t,
+                            int B, int G, int F, int h, int w, void* stream);
+
+/* Full-resolution GTV right-hand side (REF:744-749 rhs A, REF:776-781 rhs B):
+ *   b = (y + exp(log_ro0[g]) * C^T phi(C x))  +  exp(log_ro1[g]) * U(t_half)
+ * U = 2x2 nearest * 0.25 (conv_transpose2d of scaling_kernel01).  t_half may be NULL
+ * (single-scale).  If xd_out != NULL also writes D(b).  prox/wG as grr_gtv_rhs_half. */
+grr_status grr_gtv_rhs_full(const float* x, const float* y, const float* wG, grr_stencil sG,
+                            int prox, const float* log_gamma, const float* log_ro0,
+                            const float* t_half, const float* log_ro1,
+                            float* b_out, float* xd_out,
+                            int B, int G, int F, int H, int W, void* stream);
+
+/* One unrolled CG / heavy-ball stage (REF:751-753, :784-790, extension :797-807):
+ *   A x   = ((x + exp(log_mu0) L0 x) + exp(log_ro0) G0 x) + U(t_half)
+ *   r     = b - A x
+ *   u     = r + beta[g] * u_prev      (u = r when u_prev == NULL or beta == NULL)
+ *   x_out = x + alpha[g] * u
+ * optional: u_out (u), xd_out (D x_out), and the LocalLowpassFilteringBlock skip
+ * x_out <- skip[0] * y_skip + skip[1] * x_out when skip != NULL (REF:985-988).
+ * alpha/beta point at row k of alphaCGD/betaCGD ([G]).  t_half from grr_system_half. */
+grr_status grr_system_step(const float* x, const float* b, const float* u_prev, const float* t_half,
+                           const float* wL, const float* cG, grr_stencil sL, grr_stencil sG,
+                           const float* log_mu0, const float* log_ro0,
+                           const float* alpha, const float* beta,
+                           const float* skip, const float* y_skip,
+                           float* x_out, float* u_out, float* xd_out,
+                           int B, int G, int F, int H, int W, void* stream);
+
+/* ---- feature CNN (MFMA fp32) ------------------------------------------------ */
+
+/* 1x1 convolution, no bias (nn.Conv2d(k=1, groups=1, bias=False); REF:556-566, REF13:623-632):
+ * out[b,m,p] = sum_k wt[m,k] * x[b,k,p].  x [B,K,P], wt [M,K], out [B,M,P] (P = H*W). */
+grr_status grr_conv1x1(const float* x, const float* wt, float* out, int B, int K, int M, int64_t P,
+                       void* stream);
+
+/* 2x2 stride-2 convolution, no bias (REF:593-602): x [B,K,H,W], wt [M,K,2,2] -> out [B,M,H/2,W/2]. */
+grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int K, int M, int H, int W,
+                         void* stream);
+
+/* LocalNonLinearBlock forward, nsubnets = 1 (REF:911-964; REF13:564-575):
+ *   n   = gamma_c * x / sqrt(var_c(x) + 1e-5)          (CustomLayerNorm, unbiased var over C)
+ *   h   = dwconv3x3_replicate(W1 n)                     (C -> 2*hid -> 2*hid)
+ *   g   = sigmoid(h_mask) * h_mask * h_value            (hid)
+ *   out = skip[0] * x + skip[1] * (W2 g)               (hid -> C)
+ * ln_w [C] (norm.weighted_transform), w1 [2hid,C], wdw [2hid,9], w2 [C,hid], skip [2].
+ * workspace: grr_lnb_workspace_bytes(B,C,hid,H,W) bytes of device memory. out may not alias x. */
+int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W);
+grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw,
+                           const float* w2, const float* skip, float* out, void* workspace,
+                           int B, int C, int hid, int H, int W, void* stream);
+
+/* Channel replication of MultiScaleGraphFilter.forward (REF13:918-921):
+ * img [B,Cin,H,W] -> out [B,G*Cin,H,W], out[b, g*Cin + c] = img[b, c]. */
+grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GRR_H */

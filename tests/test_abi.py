@@ -1,0 +1,98 @@
+"""CPU-only checks of the C ABI and the drop-in module surface (no kernel launches)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import irdu_amd
+from irdu_amd import _native
+from tests.golden_io import load_golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "grr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(grr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = _native.load()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), f"libgrr.so does not export {s}"
+    assert set(syms) == set(_native.SIGNATURES), "ctypes signature table out of sync with include/grr.h"
+    assert lib.grr_version() >= 1
+    assert lib.grr_lnb_workspace_bytes(2, 96, 256, 64, 64) > 0
+
+
+def test_invalid_args_report_status_without_gpu():
+    lib = _native.load()
+    st = lib.grr_pool2(None, None, 1, 1, 4, 4, None)
+    assert st == 1  # GRR_ERR_INVALID_ARG, validated before any launch
+    assert b"bad args" in lib.grr_last_error()
+    with pytest.raises(_native.GrrError):
+        _native.call("grr_neighbor_table", None, 4, 4, None)
+
+
+def test_odd_shape_rejected_like_the_reference():
+    lib = _native.load()
+    # grr_pool2 with odd H: the reference's view() after the 2x2 conv fails too (REF:665)
+    st = lib.grr_pool2(ctypes_ptr(), ctypes_ptr(), 1, 1, 5, 4, None)
+    assert st == 2
+
+
+def ctypes_ptr():
+    return 0x1000  # never dereferenced: validation fails first
+
+
+def test_cpu_tensors_fail_loudly():
+    m = irdu_amd.GLRFast(3, 2, M_diag_init=1.0)
+    with pytest.raises(RuntimeError, match="GPU"):
+        m.extract_edge_weights(torch.randn(1, 2, 3, 8, 8))
+
+
+def _keys_from_golden(name):
+    d = load_golden(name)
+    return [k[2:] for k in d.files if k.startswith("p/")], d
+
+
+def test_state_dict_keys_match_reference_mixture():
+    keys, d = _keys_from_golden("mixture_v1.npz")
+    g = int(d["meta/n_graphs"])
+    m = irdu_amd.MixtureGTVGLR(g, 12 // g, 0.5, 0.1, torch.tensor([[0.001], [0.0001]]),
+                               torch.tensor([[0.0001], [0.0001]]), torch.tensor([[0.0001], [0.0001]]))
+    sd = m.state_dict()
+    assert list(sd.keys()) == keys
+    m.load_state_dict({k: torch.from_numpy(d["p/" + k]) for k in keys})
+    for k in keys:
+        assert tuple(sd[k].shape) == d["p/" + k].shape
+
+
+def test_state_dict_keys_match_reference_abstract_and_msgf():
+    keys, d = _keys_from_golden("abstract_v1.npz")
+    cfg = {k[5:]: d[k] for k in d.files if k.startswith("meta/") and k != "meta/n_state_keys"}
+    m = irdu_amd.AbtractMultiScaleGraphFilter(
+        n_channels_in=3, n_channels_out=3, dims=cfg["dims"].tolist(), hidden_dims=cfg["hidden_dims"].tolist(),
+        nsubnets=cfg["nsubnets"].tolist(), ngraphs=cfg["ngraphs"].tolist(), num_blocks=cfg["num_blocks"].tolist(),
+        num_blocks_out=int(cfg["num_blocks_out"]))
+    assert list(m.state_dict().keys()) == keys
+    m.load_state_dict({k: torch.from_numpy(d["p/" + k]) for k in keys}, strict=True)
+
+    keys, d = _keys_from_golden("msgf_v13.npz")
+    m = irdu_amd.MultiScaleGraphFilter(3, 3, ngraphs=int(d["meta/n_graphs"]))
+    assert list(m.state_dict().keys()) == keys
+
+
+def test_stage_count_parameter_shapes():
+    m = irdu_amd.MultiScaleGraphFilter(3, 3, ngraphs=32, n_cgd_iters=10)
+    assert tuple(m.localfilter.alphaCGD.shape) == (10, 32)
+    assert tuple(m.localfilter.betaCGD.shape) == (10, 32)
+    # non-persistent constants follow .to() but stay out of the state_dict
+    assert "localfilter.scaling_kernel01" not in m.state_dict()
+    assert m.localfilter.GLRmodule00.edge_delta.dtype == torch.int32
+    assert np.array_equal(m.localfilter.GLRmodule00.edge_delta.numpy(), [[-1, 0], [0, -1], [0, 1], [1, 0]])

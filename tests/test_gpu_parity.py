@@ -1,0 +1,284 @@
+"""GPU parity: the HIP path (libgrr.so through irdu_amd) against the CPU oracle.
+
+Tolerance (north_star): fp32 outputs within 1e-4 relative, measured normwise as
+max|hip - oracle| / max|oracle| over the tensor; the neighbour table is bit-exact;
+PSNR within 0.01 dB.  Inputs are seeded; the oracle is pinned to the reference by
+tests/test_oracle_golden.py, and the golden fixtures are also compared directly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import graph_oracle as O
+from tests.golden_io import load_golden, params_of
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def irdu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import irdu_amd
+    irdu_amd.load_native()
+    return irdu_amd
+
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float((a - b).abs().max()) / max(float(b.abs().max()), 1e-30)
+
+
+def assert_close(a, b, rtol=RTOL):
+    e = rel_err(a, b)
+    assert e <= rtol, f"relative error {e:.3e} > {rtol:.1e}"
+
+
+def rand(*shape, seed=0, scale=1.0, offset=0.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale + offset
+
+
+def perturbed_graph_module(mod, seed):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in (mod.stats_kernel_p01, mod.stats_kernel_p02a, mod.stats_kernel_p02b, mod.stats_kernel_p03):
+            p.mul_(1 + 0.25 * torch.randn(p.shape, generator=g))
+        mod.multiM.copy_(1 + 0.3 * torch.randn(mod.multiM.shape, generator=g))
+    return mod
+
+
+def perturb_mixture(mix, seed):
+    g = torch.Generator().manual_seed(seed)
+    u = lambda shape, lo, hi: lo + (hi - lo) * torch.rand(shape, generator=g)  # noqa: E731
+    with torch.no_grad():
+        mix.alphaCGD.copy_(u(mix.alphaCGD.shape, 0.2, 0.8))
+        mix.betaCGD.copy_(u(mix.betaCGD.shape, 0.05, 0.4))
+        for p in (mix.muys00, mix.muys01, mix.ro00, mix.ro01):
+            p.copy_(torch.log(u(p.shape, 0.05, 0.6)))
+        for p in (mix.gamma00, mix.gamma01):
+            p.copy_(torch.log(u(p.shape, 0.002, 0.05)))
+        for i, m in enumerate((mix.GLRmodule00, mix.GLRmodule01, mix.GTVmodule00, mix.GTVmodule01)):
+            perturbed_graph_module(m, seed + 10 + i)
+
+
+def sd_cpu(module):
+    return {k: v.detach().cpu() for k, v in module.state_dict().items()}
+
+
+# ---------------------------------------------------------------------------
+# a1/a2: neighbour table, bit-exact
+@pytest.mark.parametrize("hw", [(1, 1), (1, 7), (5, 1), (16, 20), (37, 45), (256, 256)])
+def test_neighbor_table_bit_exact(irdu, hw):
+    h, w = hw
+    got = irdu.kernels.neighbor_table(h, w, DEV).cpu()
+    assert torch.equal(got, O.neighbor_table(h, w))
+
+
+def test_neighbor_table_matches_golden(irdu):
+    d = load_golden("ops_small.npz")
+    h, w = d["out/neighbor_table"].shape[-2:]
+    assert np.array_equal(irdu.kernels.neighbor_table(h, w, DEV).cpu().numpy(), d["out/neighbor_table"])
+
+
+# ---------------------------------------------------------------------------
+# a3/a4 edge weights; a5-a10 operators — against the reference's golden vectors
+def test_ops_golden(irdu):
+    d = load_golden("ops_small.npz")
+    feat = torch.from_numpy(d["in/feat"])
+    x = torch.from_numpy(d["in/x"])
+    b, g, f, h, w = x.shape
+    glr = irdu.GLRFast(f, g, 1.0)
+    gtv = irdu.GTVFast(f, g, 1.0)
+    glr.load_state_dict(params_of(d, "glr."))
+    gtv.load_state_dict(params_of(d, "gtv."))
+    glr, gtv = glr.to(DEV), gtv.to(DEV)
+    with torch.no_grad():
+        wl, dl = glr.extract_edge_weights(feat.to(DEV))
+        wg, dg = gtv.extract_edge_weights(feat.to(DEV))
+        assert_close(wl, d["out/glr_w"], 1e-5)
+        assert_close(dl, d["out/glr_deg"], 1e-5)
+        assert_close(wg, d["out/gtv_w"], 1e-5)
+        assert_close(glr(x.to(DEV), wl, dl), d["out/glr_forward"])
+        assert_close(gtv(x.to(DEV), wg, dg), d["out/gtv_forward"])
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 37, 45), (2, 3, 12, 20, 70), (1, 2, 1, 64, 96)])
+def test_edge_weights_random(irdu, shape):
+    b, g, f, h, w = shape
+    feat = rand(b, g, f, h, w, seed=1)
+    m = perturbed_graph_module(irdu.GLRFast(f, g, 1.0), 3)
+    wt, deg = m.to(DEV).extract_edge_weights(feat.to(DEV))
+    ow, od = O.edge_weights(feat, m.multiM.detach().cpu())
+    assert_close(wt, ow, 1e-5)
+    assert_close(deg, od, 1e-5)
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 37, 45), (1, 3, 2, 9, 70)])
+def test_glr_gtv_operators_random(irdu, shape):
+    b, g, f, h, w = shape
+    x = rand(b, g, f, h, w, seed=2)
+    wl = torch.softmax(rand(b, g, 4, h, w, seed=3), dim=2)
+    wg = torch.softmax(rand(b, g, 4, h, w, seed=4), dim=2)
+    glr = perturbed_graph_module(irdu.GLRFast(f, g, 1.0), 5)
+    gtv = perturbed_graph_module(irdu.GTVFast(f, g, 1.0), 6)
+    kl = O.stats_kernel(sd_cpu(glr), "")
+    kg = O.stats_kernel(sd_cpu(gtv), "")
+    glr, gtv = glr.to(DEV), gtv.to(DEV)
+    with torch.no_grad():
+        assert_close(glr(x.to(DEV), wl.to(DEV)), O.glr_apply(x, wl, kl))
+        assert_close(gtv(x.to(DEV), wg.to(DEV)), O.gtv_apply(x, wg, kg))
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 21, 31)])
+def test_gtv_prox_rhs_half(irdu, shape):
+    """C^T phi(C x) with the soft-threshold phi of the proximal step (a12, a16)."""
+    b, g, f, h, w = shape
+    x = rand(b, g, f, h, w, seed=7)
+    wg = torch.softmax(rand(b, g, 4, h, w, seed=8), dim=2)
+    gtv = perturbed_graph_module(irdu.GTVFast(f, g, 1.0), 9)
+    kg = O.stats_kernel(sd_cpu(gtv), "")
+    log_gamma = torch.log(torch.linspace(0.01, 0.2, g))
+    t = O.gtv_C(x, wg, kg)
+    e = O.soft_threshold(t, torch.exp(log_gamma))
+    ref = O.gtv_Ct(e - (t - e), wg, kg)
+    gtv = gtv.to(DEV)
+    got = irdu.kernels.gtv_rhs_half(x.reshape(b, g * f, h, w).to(DEV), wg.to(DEV), irdu.kernels.stencil(gtv),
+                                    True, log_gamma.to(DEV), g)
+    assert_close(got.view(b, g, f, h, w), ref)
+    # enough entries are thresholded for the test to mean something
+    assert 0.05 < float((e == 0).double().mean()) < 0.95
+
+
+# ---------------------------------------------------------------------------
+# feature CNN
+@pytest.mark.parametrize("bkmp", [(2, 12, 24, (8, 8)), (1, 96, 192, (33, 40)), (2, 7, 3, (5, 6))])
+def test_conv1x1(irdu, bkmp):
+    b, k, m, (h, w) = bkmp
+    x = rand(b, k, h, w, seed=11)
+    wt = rand(m, k, 1, 1, seed=12) * 0.2
+    assert_close(irdu.kernels.conv1x1(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt), 1e-5)
+
+
+@pytest.mark.parametrize("bkmhw", [(2, 12, 12, 16, 16), (1, 96, 96, 34, 50)])
+def test_conv2x2s2(irdu, bkmhw):
+    b, k, m, h, w = bkmhw
+    x = rand(b, k, h, w, seed=13)
+    wt = rand(m, k, 2, 2, seed=14) * 0.2
+    assert_close(irdu.kernels.conv2x2s2(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt, stride=2), 1e-5)
+
+
+@pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 40, 36)])
+def test_local_nonlinear_block(irdu, chw):
+    c, hid, h, w = chw
+    torch.manual_seed(0)
+    blk = irdu.LocalNonLinearBlock(c, hid, 1)
+    with torch.no_grad():
+        blk.skip_weight.copy_(torch.tensor([0.9, 1.3]))
+        blk.norm.weighted_transform.weight.mul_(1.0 + 0.2 * torch.randn_like(blk.norm.weighted_transform.weight))
+    x = rand(2, c, h, w, seed=15)
+    ref = O.local_nonlinear_block(x, sd_cpu(blk), "")
+    with torch.no_grad():
+        got = blk.to(DEV)(x.to(DEV))
+    assert_close(got, ref)
+
+
+# ---------------------------------------------------------------------------
+# full solver against the reference's golden vectors
+@pytest.mark.parametrize("name", ["mixture_v1.npz", "mixture_v1_rect.npz"])
+def test_mixture_golden(irdu, name):
+    d = load_golden(name)
+    g = int(d["meta/n_graphs"])
+    x = torch.from_numpy(d["in/x"])
+    c = x.shape[1]
+    m = irdu.MixtureGTVGLR(g, c // g, 0.5, 0.1, [[0.001], [0.0001]], [[0.0001], [0.0001]], [[0.0001], [0.0001]])
+    m.load_state_dict(params_of(d, ""))
+    with torch.no_grad():
+        y = m.to(DEV)(x.to(DEV))
+    assert_close(y, d["out/y"])
+
+
+def test_msgf_v13_golden(irdu):
+    d = load_golden("msgf_v13.npz")
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=int(d["meta/n_graphs"]))
+    m.load_state_dict(params_of(d, ""))
+    with torch.no_grad():
+        y = m.to(DEV)(torch.from_numpy(d["in/noisy"]).to(DEV))
+    assert_close(y, d["out/y"])
+    clean = torch.from_numpy(d["in/clean"])
+    assert abs(O.psnr_ubyte(y.cpu(), clean) - O.psnr_ubyte(torch.from_numpy(d["out/y"]), clean)) <= 0.01
+
+
+def test_abstract_model_golden(irdu):
+    d = load_golden("abstract_v1.npz")
+    cfg = {k[5:]: d[k] for k in d.files if k.startswith("meta/") and k != "meta/n_state_keys"}
+    m = irdu.AbtractMultiScaleGraphFilter(
+        n_channels_in=3, n_channels_out=3, dims=cfg["dims"].tolist(), hidden_dims=cfg["hidden_dims"].tolist(),
+        nsubnets=cfg["nsubnets"].tolist(), ngraphs=cfg["ngraphs"].tolist(), num_blocks=cfg["num_blocks"].tolist(),
+        num_blocks_out=int(cfg["num_blocks_out"]))
+    m.load_state_dict(params_of(d, ""))
+    m = m.to(DEV)
+    img = torch.from_numpy(d["in/noisy"]).to(DEV)
+    with torch.no_grad():
+        coefs = m.encode(img)
+        filt = m.filtering(coefs)
+        y = m(img)
+    for i in range(4):
+        assert_close(filt[i], d[f"out/filtered{i}"])
+    assert_close(y, d["out/y"])
+
+
+# ---------------------------------------------------------------------------
+# S = 10 stages (the metric's configuration) against the oracle
+@pytest.mark.parametrize("case", [dict(g=4, b=2, h=32, w=32), dict(g=32, b=1, h=64, w=96)])
+def test_msgf_ten_stages_vs_oracle(irdu, case):
+    g, b, h, w = case["g"], case["b"], case["h"], case["w"]
+    torch.manual_seed(2204)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=g, n_cgd_iters=10)
+    perturb_mixture(m.localfilter, 21)
+    clean = torch.rand(b, 3, h, w)
+    noisy = clean + torch.randn(b, 3, h, w) * (25.0 / 255.0)
+    ref = O.multiscale_graph_filter(noisy, sd_cpu(m), g)
+    with torch.no_grad():
+        got = m.to(DEV)(noisy.to(DEV))
+    assert_close(got, ref)
+    assert abs(O.psnr_ubyte(got.cpu(), clean) - O.psnr_ubyte(ref, clean)) <= 0.01
+
+
+def test_lowpass_block_ten_stages_vs_oracle(irdu):
+    torch.manual_seed(7)
+    blk = irdu.LocalLowpassFilteringBlock(dim=48, nsubnets=1, ngraphs=8, n_cgd_iters=10)
+    perturb_mixture(blk.local_filter, 31)
+    with torch.no_grad():
+        blk.skip_weight.copy_(torch.tensor([0.3, 0.8]))
+    x = rand(2, 48, 48, 64, seed=17)
+    ref = O.lowpass_block(x, sd_cpu(blk), 8)
+    with torch.no_grad():
+        got = blk.to(DEV)(x.to(DEV))
+    assert_close(got, ref)
+
+
+def test_single_stage_and_odd_half_level(irdu):
+    """S = 1 (the example.yaml plumbing config) and a half level with odd size (42x62 -> 21x31)."""
+    torch.manual_seed(3)
+    blk = irdu.LocalLowpassFilteringBlock(dim=12, nsubnets=1, ngraphs=4, n_cgd_iters=1)
+    perturb_mixture(blk.local_filter, 41)
+    x = rand(1, 12, 42, 62, seed=18)
+    ref = O.lowpass_block(x, sd_cpu(blk), 4)
+    with torch.no_grad():
+        got = blk.to(DEV)(x.to(DEV))
+    assert_close(got, ref)
+
+
+def test_backward_fails_loudly(irdu):
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=2).to(DEV)
+    y = m(torch.rand(1, 3, 16, 16, device=DEV))
+    with pytest.raises(NotImplementedError):
+        y.sum().backward()
