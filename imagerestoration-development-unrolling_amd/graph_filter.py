@@ -26,6 +26,31 @@ from . import kernels as K
 EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, down)
 
 
+class _NoBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, run, *tensors):
+        out = run()
+        return out if isinstance(out, torch.Tensor) else tuple(out)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError("irdu_amd: HIP backward kernels are not built yet; "
+                                  "run the graph filter under torch.no_grad()")
+
+
+def hip_forward(fn):
+    """Run a HIP-backed forward; when autograd is recording, attach a node whose
+    backward raises, so a training loop can never silently drop gradients."""
+    def wrapper(self, *args, **kwargs):
+        tensors = [a for a in args if isinstance(a, torch.Tensor)]
+        if torch.is_grad_enabled() and (any(t.requires_grad for t in tensors)
+                                        or any(p.requires_grad for p in self.parameters())):
+            return _NoBackward.apply(lambda: fn(self, *args, **kwargs), *tensors, *self.parameters())
+        return fn(self, *args, **kwargs)
+    wrapper.__name__, wrapper.__doc__ = fn.__name__, fn.__doc__
+    return wrapper
+
+
 def _basis(c: int):
     z = torch.zeros(3, 3)
     k01 = z.clone(); k01[1, 1] = 1.0
@@ -60,6 +85,7 @@ class _GraphModule(nn.Module):
         self.register_buffer("stats_kernel03", b03, persistent=False)
         self.multiM = Parameter(torch.full((n_graphs, n_node_fts), float(M_diag_init)))
 
+    @hip_forward
     def extract_edge_weights(self, img_features: torch.Tensor):
         """[B,G,F,H,W] features -> (w [B,G,4,H,W], degree [B,G,H,W]) (REF:160-175)."""
         b, g, f, h, w = img_features.shape
@@ -74,6 +100,7 @@ class _GraphModule(nn.Module):
 class GLRFast(_GraphModule):
     """Graph-Laplacian regulariser S^T (I - W) S (REF:13-237)."""
 
+    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
         b, g, f, h, w = patchs.shape
         out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), edge_weights.contiguous(), None,
@@ -84,6 +111,7 @@ class GLRFast(_GraphModule):
 class GTVFast(_GraphModule):
     """Graph total variation C^T C with C = W (S - S shifted) (REF:242-523)."""
 
+    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
         b, g, f, h, w = patchs.shape
         c = K.gtv_pair_weights(edge_weights.contiguous())
@@ -138,6 +166,10 @@ class LocalNonLinearBlock(nn.Module):
         if self.nsubnets != 1:
             # grouped variant: only used by encoder/decoder configs (out of the hot path)
             return self.skip_weight[0] * x + self.skip_weight[1] * self.local_linear(self.norm(x))
+        return self._forward_hip(x)
+
+    @hip_forward
+    def _forward_hip(self, x):
         ll = self.local_linear
         c, hid = self.dim, self.hidden_dim
         return K.lnb_forward(x.contiguous(), self.norm.weighted_transform.weight.data.view(c),
@@ -149,17 +181,6 @@ class LocalNonLinearBlock(nn.Module):
 # ---------------------------------------------------------------------------
 # The solver block
 # ---------------------------------------------------------------------------
-class _NoBackward(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, run, x, *params):
-        return run()
-
-    @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError("irdu_amd: HIP backward kernels are not built yet; "
-                                  "run the graph filter under torch.no_grad()")
-
-
 class MixtureGTVGLR(nn.Module):
     """Two-scale GGTV+GGLR unrolled solver (REF:526-811).
 
@@ -271,11 +292,9 @@ class MixtureGTVGLR(nn.Module):
                                      skip=skip if last else None, y_skip=y if last else None, u_out=u)
         return x
 
+    @hip_forward
     def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None) -> torch.Tensor:
-        y = patchs.contiguous()
-        if torch.is_grad_enabled() and (y.requires_grad or any(p.requires_grad for p in self.parameters())):
-            return _NoBackward.apply(lambda: self._solve(y, _skip), y, *[p for p in self.parameters()])
-        return self._solve(y, _skip)
+        return self._solve(patchs.contiguous(), _skip)
 
 
 class LocalLowpassFilteringBlock(nn.Module):
@@ -307,6 +326,7 @@ class MultiScaleGraphFilter(nn.Module):
             gamma_init=torch.tensor([[0.0001], [0.0001]]), n_cgd_iters=n_cgd_iters, feature_extractor="v13")
         self.linear_combination = nn.Conv2d(ngraphs * n_channels_in, n_channels_out, 1, bias=False)
 
+    @hip_forward
     def forward(self, img):
         x = K.repeat_graphs(img.contiguous(), self.ngraphs)
         y = self.localfilter(x)
