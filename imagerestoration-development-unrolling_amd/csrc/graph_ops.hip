@@ -7,12 +7,14 @@
 //   half level    [B, C, H/2, W/2]       (2x2 mean pool D, REF:613)
 //
 // Work decomposition of the fused operator kernel: one 256-thread workgroup = one
-// (batch b, graph g, 32x32 output tile); it walks the graph's F channels so the
-// tile's edge weights are loaded from HBM once into registers and reused F times.
-// Per channel the input tile (halo 3, replicate-clamped) is staged in LDS and the
-// chain  x -> s = S x (halo 2) -> {l = (I-W) s, o = C^T C s} (halo 1) -> S^T  is
-// evaluated LDS-to-LDS, followed by a fused epilogue (rhs / CG stage / half-level
-// term).  Everything is memory-bound (≈3.5 flop/B), so the design goal is HBM
+// (batch b, channel, 32x32 output tile).  All of its global loads (input tile with
+// a 3-pixel replicate halo, the graph's edge weights at the 34x34 pass-B points,
+// the epilogue operands) are issued up front, so their latency overlaps; the F
+// channel-workgroups of one (b, graph, tile) are consecutive logical blocks placed
+// on one XCD, so the shared edge weights come from HBM once and from L2 F-1 times.
+// The chain  x -> s = S x (halo 2) -> {l = (I-W) s, o = C^T C s} (halo 1) -> S^T
+// is evaluated LDS-to-LDS, followed by a fused epilogue (rhs / CG stage /
+// half-level term).  Everything is memory-bound (≈3.5 flop/B), so the design goal is HBM
 // bytes: each launch reads each of its inputs once and writes each output once.
 #include <cstdarg>
 
@@ -244,18 +246,41 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   __shared__ float Ls[GLR ? LA : 1];
   __shared__ float Gs[GTV ? LA : 1];
   constexpr int NW = GTV == GTV_PROX ? 8 : 4;
+  constexpr int NXL = (XA + NT - 1) / NT;  // input-tile loads per thread (6)
 
+  // One workgroup = one (b, channel, 32x32 tile).  The F channel-workgroups of a
+  // (b, graph, tile) are consecutive logical blocks, so after the XCD remap they run
+  // together on one XCD and the graph's edge weights are fetched from HBM once.
   const int tid = threadIdx.x;
+  const int F = a.F;
   uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int f = lb % F; lb /= F;
   const int tx = lb % a.tiles_x; lb /= a.tiles_x;
   const int ty = lb % a.tiles_y; lb /= a.tiles_y;
   const int g = lb % a.G;
   const int b = lb / a.G;
-  const int H = a.H, W = a.W, F = a.F, C = a.G * a.F;
+  const int H = a.H, W = a.W, C = a.G * F;
   const int64_t HW = (int64_t)H * W;
   const int y0 = ty * TILE, x0 = tx * TILE;
+  const int ch = g * F + f;
+  const int64_t plane = ((int64_t)b * C + ch) * HW;
+  const int hh = H / 2, hw = W / 2;
 
-  // ---- edge weights of this (b, g) at the pass-B points: loaded once, reused F times
+  // ---- issue every global load of the workgroup up front ----------------------
+  // (1) input tile, halo 3, replicate-clamped (REF:186 replicate pad)
+  float xr[NXL];
+  {
+    const float* xp = a.x + plane;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const int i = tid + j * NT;
+      const int ii = i < XA ? i : XA - 1;
+      const int ry = ii / XS, rx = ii - ry * XS;
+      const int gy = clampi(y0 - 3 + ry, 0, H - 1), gx = clampi(x0 - 3 + rx, 0, W - 1);
+      xr[j] = xp[(int64_t)gy * W + gx];
+    }
+  }
+  // (2) this graph's edge weights at the pass-B points
   float wl[NPB][4];
   float wg[NPB][NW];
   {
@@ -293,6 +318,30 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
       }
     }
   }
+  // (3) epilogue operands of this thread's 2x2 output block
+  const int by = tid >> 4, bx = tid & 15;
+  const int gy0 = y0 + 2 * by, gx0 = x0 + 2 * bx;
+  float eb[2][2] = {}, eu[2][2] = {}, ey[2][2] = {};
+  float th = 0.f;
+  const bool has_half = EPI != EPI_HALF && a.t_half != nullptr;
+  const bool use_beta = EPI == EPI_STEP && a.beta != nullptr && a.u_prev != nullptr;
+  const bool need_y = (EPI == EPI_RHS) || (EPI == EPI_STEP && a.skip != nullptr);
+  if (EPI != EPI_HALF) {
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int gy = gy0 + dy, gx = gx0 + dx;
+        if (gy < H && gx < W) {
+          const int64_t o = plane + (int64_t)gy * W + gx;
+          if (EPI == EPI_STEP) eb[dy][dx] = a.b[o];
+          if (use_beta) eu[dy][dx] = a.u_prev[o];
+          if (need_y) ey[dy][dx] = a.y[o];
+        }
+      }
+    if (has_half && gy0 < H && gx0 < W)
+      th = 0.25f * a.t_half[((int64_t)b * C + ch) * hh * hw + (int64_t)(gy0 >> 1) * hw + (gx0 >> 1)];
+  }
   float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
   if (a.log_l) sc_l = expf(a.log_l[g]);
   if (a.log_g) sc_g = expf(a.log_g[g]);
@@ -300,172 +349,136 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   if constexpr (GTV == GTV_PROX) gam = expf(a.log_gamma[g]);
   if constexpr (EPI == EPI_STEP) {
     alpha = a.alpha[g];
-    if (a.beta && a.u_prev) beta = a.beta[g];
+    if (use_beta) beta = a.beta[g];
     if (a.skip) { sk0 = a.skip[0]; sk1 = a.skip[1]; }
   }
-  const bool use_beta = EPI == EPI_STEP && a.beta != nullptr && a.u_prev != nullptr;
-  const int hh = H / 2, hw = W / 2;
+  Taps tL{}, tG{};
+  if constexpr (GLR) tL = make_taps(a.sL, ch);
+  if constexpr (GTV != GTV_NONE) tG = make_taps(a.sG, ch);
 
-  for (int f = 0; f < F; ++f) {
-    const int ch = g * F + f;
-    const int64_t plane = ((int64_t)b * C + ch) * HW;
-    const float* xp = a.x + plane;
-    // ---- pass 0: input tile, halo 3, replicate-clamped (REF:186 replicate pad)
-    for (int i = tid; i < XA; i += NT) {
-      const int ry = i / XS, rx = i - ry * XS;
-      const int gy = clampi(y0 - 3 + ry, 0, H - 1), gx = clampi(x0 - 3 + rx, 0, W - 1);
-      Xs[i] = xp[(int64_t)gy * W + gx];
-    }
-    Taps tL{}, tG{};
-    if constexpr (GLR) tL = make_taps(a.sL, ch);
-    if constexpr (GTV != GTV_NONE) tG = make_taps(a.sG, ch);
-    __syncthreads();
-    // ---- pass A: s = S x on the halo-2 region (values outside the image are never read)
-    for (int i = tid; i < SA; i += NT) {
-      const int ry = i / SS, rx = i - ry * SS;
-      const int xi = (ry + 1) * XS + rx + 1;
-      if constexpr (GLR) SLs[i] = stencil(tL, Xs, xi, XS);
-      if constexpr (GTV != GTV_NONE) SGs[i] = stencil(tG, Xs, xi, XS);
-    }
-    __syncthreads();
-    // ---- pass B: l = s - W s (GLR, REF:218-228) and o = C^T phi(C s) (GTV, REF:452-516)
+  // ---- pass 0: input tile to LDS
 #pragma unroll
-    for (int j = 0; j < NPB; ++j) {
-      const int i = tid + j * NT;
-      if (i < LA) {
-        const int ry = i / LS, rx = i - ry * LS;
-        const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
-        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        const int si = (ry + 1) * SS + rx + 1;
-        if constexpr (GLR) {
-          float l = 0.f;
-          if (in) {
-            const int nu = gy > 0 ? si - SS : si, nl = gx > 0 ? si - 1 : si;
-            const int nr = gx < W - 1 ? si + 1 : si, nd = gy < H - 1 ? si + SS : si;
-            const float wx = ((wl[j][0] * SLs[nu] + wl[j][1] * SLs[nl]) + wl[j][2] * SLs[nr]) + wl[j][3] * SLs[nd];
-            l = SLs[si] - wx;
-          }
-          Ls[i] = l;
-        }
-        if constexpr (GTV == GTV_PAIR) {
-          float o = 0.f;
-          if (in) {
-            const float s = SGs[si];
-            o = wg[j][0] * (s - SGs[si + 1]) + wg[j][1] * (s - SGs[si - 1]) +
-                wg[j][2] * (s - SGs[si + SS]) + wg[j][3] * (s - SGs[si - SS]);
-          }
-          Gs[i] = o;
-        }
-        if constexpr (GTV == GTV_PROX) {
-          float o = 0.f;
-          if (in) {
-            const float s = SGs[si];
-            const int nb[4] = {si - SS, si - 1, si + 1, si + SS};
-            float z[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float we = wg[j][e];
-              z[e] = prox_phi(we * s - we * SGs[nb[e]], gam) * we;   // z_e(q)
-            }
-            o = ((z[0] + z[1]) + z[2]) + z[3];
-            // subtract z_e(q - delta_e) in edge order (REF:482-500)
-            const int pb[4] = {si + SS, si + 1, si - 1, si - SS};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float we = wg[j][4 + e];
-              o = o - prox_phi(we * SGs[pb[e]] - we * s, gam) * we;
-            }
-          }
-          Gs[i] = o;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- pass C: S^T and the epilogue, one 2x2 output block per thread
-    {
-      const int by = tid >> 4, bx = tid & 15;
-      float v[2][2];
-      float xv[2][2];
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          const int oy = 2 * by + dy, ox = 2 * bx + dx;
-          const int li = (oy + 1) * LS + ox + 1;
-          float tl = 0.f, tg = 0.f;
-          if constexpr (GLR) tl = stencil_t(tL, Ls, li, LS);
-          if constexpr (GTV != GTV_NONE) tg = stencil_t(tG, Gs, li, LS);
-          xv[dy][dx] = Xs[(oy + 3) * XS + ox + 3];
-          if constexpr (EPI == EPI_HALF) {
-            float r = 0.f;
-            if constexpr (GLR) r = tl * sc_l;
-            if constexpr (GTV != GTV_NONE) r = GLR ? r + tg * sc_g : tg * sc_g;
-            v[dy][dx] = r;
-          } else {
-            v[dy][dx] = 0.f;
-            (void)tl;
-            (void)tg;
-            // stash the operator terms; combined below with the global inputs
-            if constexpr (EPI == EPI_STEP) {
-              float ax = xv[dy][dx];
-              if constexpr (GLR) ax = ax + tl * sc_l;
-              if constexpr (GTV != GTV_NONE) ax = ax + tg * sc_g;
-              v[dy][dx] = ax;
-            } else {
-              v[dy][dx] = tg * sc_g;
-            }
-          }
-        }
-      const int gy0 = y0 + 2 * by, gx0 = x0 + 2 * bx;
-      float th = 0.f;
-      const bool has_half = EPI != EPI_HALF && a.t_half != nullptr;
-      if (has_half && gy0 < H && gx0 < W)
-        th = 0.25f * a.t_half[((int64_t)b * C + ch) * hh * hw + (int64_t)(gy0 >> 1) * hw + (gx0 >> 1)];
-      float outv[2][2];
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          const int gy = gy0 + dy, gx = gx0 + dx;
-          const bool in = gy < H && gx < W;
-          const int64_t o = plane + (int64_t)gy * W + gx;
-          float r = v[dy][dx];
-          if constexpr (EPI == EPI_RHS) {
-            // (y + ro0 * C^T phi(C x)) + ro1 * U(t_half)   (REF:744-749 / :776-781)
-            const float yv = in ? a.y[o] : 0.f;
-            r = yv + r;
-            if (has_half) r = r + th * sc_h;
-          } else if constexpr (EPI == EPI_STEP) {
-            if (has_half) r = r + th;                       // A x complete (REF:680)
-            const float bv = in ? a.b[o] : 0.f;
-            float u = bv - r;                               // residual
-            if (use_beta) u = u + beta * (in ? a.u_prev[o] : 0.f);
-            const float xn = xv[dy][dx] + alpha * u;
-            if (a.u_out && in) a.u_out[o] = u;
-            r = xn;
-          }
-          outv[dy][dx] = r;
-        }
-      // D of the (pre-skip) result for the next stage's half level
-      if (a.xd_out && gy0 + 1 < H && gx0 + 1 < W) {
-        const float d = 0.25f * outv[0][0] + 0.25f * outv[0][1] + 0.25f * outv[1][0] + 0.25f * outv[1][1];
-        a.xd_out[((int64_t)b * C + ch) * hh * hw + (int64_t)(gy0 >> 1) * hw + (gx0 >> 1)] = d;
-      }
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          const int gy = gy0 + dy, gx = gx0 + dx;
-          if (gy < H && gx < W) {
-            const int64_t o = plane + (int64_t)gy * W + gx;
-            float r = outv[dy][dx];
-            if (EPI == EPI_STEP && a.skip) r = sk0 * a.y[o] + sk1 * r;   // REF:987
-            a.out[o] = r;
-          }
-        }
-    }
-    __syncthreads();
+  for (int j = 0; j < NXL; ++j) {
+    const int i = tid + j * NT;
+    if (i < XA) Xs[i] = xr[j];
   }
+  __syncthreads();
+  // ---- pass A: s = S x on the halo-2 region (values outside the image are never read)
+  for (int i = tid; i < SA; i += NT) {
+    const int ry = i / SS, rx = i - ry * SS;
+    const int xi = (ry + 1) * XS + rx + 1;
+    if constexpr (GLR) SLs[i] = stencil(tL, Xs, xi, XS);
+    if constexpr (GTV != GTV_NONE) SGs[i] = stencil(tG, Xs, xi, XS);
+  }
+  __syncthreads();
+  // ---- pass B: l = s - W s (GLR, REF:218-228) and o = C^T phi(C s) (GTV, REF:452-516)
+#pragma unroll
+  for (int j = 0; j < NPB; ++j) {
+    const int i = tid + j * NT;
+    if (i < LA) {
+      const int ry = i / LS, rx = i - ry * LS;
+      const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
+      const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+      const int si = (ry + 1) * SS + rx + 1;
+      if constexpr (GLR) {
+        float l = 0.f;
+        if (in) {
+          const int nu = gy > 0 ? si - SS : si, nl = gx > 0 ? si - 1 : si;
+          const int nr = gx < W - 1 ? si + 1 : si, nd = gy < H - 1 ? si + SS : si;
+          const float wx = ((wl[j][0] * SLs[nu] + wl[j][1] * SLs[nl]) + wl[j][2] * SLs[nr]) + wl[j][3] * SLs[nd];
+          l = SLs[si] - wx;
+        }
+        Ls[i] = l;
+      }
+      if constexpr (GTV == GTV_PAIR) {
+        float o = 0.f;
+        if (in) {
+          const float s = SGs[si];
+          o = wg[j][0] * (s - SGs[si + 1]) + wg[j][1] * (s - SGs[si - 1]) +
+              wg[j][2] * (s - SGs[si + SS]) + wg[j][3] * (s - SGs[si - SS]);
+        }
+        Gs[i] = o;
+      }
+      if constexpr (GTV == GTV_PROX) {
+        float o = 0.f;
+        if (in) {
+          const float s = SGs[si];
+          const int nb[4] = {si - SS, si - 1, si + 1, si + SS};
+          float z[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float we = wg[j][e];
+            z[e] = prox_phi(we * s - we * SGs[nb[e]], gam) * we;   // z_e(q)
+          }
+          o = ((z[0] + z[1]) + z[2]) + z[3];
+          // subtract z_e(q - delta_e) in edge order (REF:482-500)
+          const int pb[4] = {si + SS, si + 1, si - 1, si - SS};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float we = wg[j][4 + e];
+            o = o - prox_phi(we * SGs[pb[e]] - we * s, gam) * we;
+          }
+        }
+        Gs[i] = o;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- pass C: S^T and the epilogue, one 2x2 output block per thread
+  float outv[2][2];
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int oy = 2 * by + dy, ox = 2 * bx + dx;
+      const int li = (oy + 1) * LS + ox + 1;
+      float tl = 0.f, tg = 0.f;
+      if constexpr (GLR) tl = stencil_t(tL, Ls, li, LS);
+      if constexpr (GTV != GTV_NONE) tg = stencil_t(tG, Gs, li, LS);
+      const float xv = Xs[(oy + 3) * XS + ox + 3];
+      float r;
+      if constexpr (EPI == EPI_HALF) {
+        // mu * S_L^T l + ro * S_G^T o   (REF:666-675)
+        r = 0.f;
+        if constexpr (GLR) r = tl * sc_l;
+        if constexpr (GTV != GTV_NONE) r = GLR ? r + tg * sc_g : tg * sc_g;
+      } else if constexpr (EPI == EPI_RHS) {
+        // (y + ro0 * C^T phi(C x)) + ro1 * U(t_half)   (REF:744-749 / :776-781)
+        r = ey[dy][dx] + tg * sc_g;
+        if (has_half) r = r + th * sc_h;
+      } else {
+        // A x = ((x + mu0 L0 x) + ro0 G0 x) + U(t_half)   (REF:648-680)
+        float ax = xv;
+        if constexpr (GLR) ax = ax + tl * sc_l;
+        if constexpr (GTV != GTV_NONE) ax = ax + tg * sc_g;
+        if (has_half) ax = ax + th;
+        float u = eb[dy][dx] - ax;                    // residual b - A x
+        if (use_beta) u = u + beta * eu[dy][dx];      // heavy-ball direction (REF:789)
+        eu[dy][dx] = u;
+        r = xv + alpha * u;                           // x_{k+1}
+      }
+      outv[dy][dx] = r;
+    }
+  // D of the (pre-skip) result for the next stage's half level
+  if (a.xd_out && gy0 + 1 < H && gx0 + 1 < W) {
+    const float d = 0.25f * outv[0][0] + 0.25f * outv[0][1] + 0.25f * outv[1][0] + 0.25f * outv[1][1];
+    a.xd_out[((int64_t)b * C + ch) * hh * hw + (int64_t)(gy0 >> 1) * hw + (gx0 >> 1)] = d;
+  }
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int gy = gy0 + dy, gx = gx0 + dx;
+      if (gy < H && gx < W) {
+        const int64_t o = plane + (int64_t)gy * W + gx;
+        float r = outv[dy][dx];
+        if (EPI == EPI_STEP) {
+          if (a.u_out) a.u_out[o] = eu[dy][dx];
+          if (a.skip) r = sk0 * ey[dy][dx] + sk1 * r;   // REF:987
+        }
+        a.out[o] = r;
+      }
+    }
 }
 
 template <bool GLR, int GTV, int EPI>
@@ -473,7 +486,7 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
   OpArgs a = a0;
   a.tiles_x = (a.W + TILE - 1) / TILE;
   a.tiles_y = (a.H + TILE - 1) / TILE;
-  const uint64_t n = (uint64_t)B * a.G * a.tiles_x * a.tiles_y;
+  const uint64_t n = (uint64_t)B * a.G * a.F * a.tiles_x * a.tiles_y;
   GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   a.nblk = (uint32_t)n;
   hipLaunchKernelGGL((graph_op_kernel<GLR, GTV, EPI>), dim3(a.nblk), dim3(NT), 0, s, a);
