@@ -14,9 +14,10 @@ namespace grr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int GT = 256;             // threads per GEMM workgroup (4 waves)
-constexpr int BM = 64, BN = 64, BK = 32;
-constexpr int APAD = BM + 4, BPAD = BN + 4;
+constexpr int GT = 256;                    // threads per GEMM workgroup (4 waves, 2x2)
+constexpr int BM = 128, BN = 128, BK = 16;  // block tile; each wave owns a 64x64 quadrant
+constexpr int APAD = BM + 2;                // 130: conflict-free transposed A stores (8*130 = 16 mod 32)
+constexpr int BPAD = BN + 4;
 
 enum { LD_PLAIN = 0, LD_LN = 1, LD_IM2COL = 2 };
 enum { EP_STORE = 0, EP_SKIP = 1 };
@@ -36,14 +37,17 @@ struct GemmArgs {
   uint32_t nblk;
 };
 
-template <int LOADER, int EPI>
+// Block tile 128 (out channels) x 128 (pixels), K in chunks of 16 staged through a
+// double-buffered LDS image; the next chunk is fetched into registers while the
+// current one feeds the matrix cores (v_mfma_f32_32x32x2_f32, 4 accumulators/wave).
+template <int LOADER, int EPI, bool VEC>
 __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
-  __shared__ float As[BK][APAD];
-  __shared__ float Bs[BK][BPAD];
+  __shared__ float As[2][BK][APAD];
+  __shared__ float Bs[2][BK][BPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
-  const int mtile = lb % a.mt; lb /= a.mt;       // M tiles of one pixel tile are neighbours
+  const int mtile = lb % a.mt; lb /= a.mt;       // M tiles of one pixel tile are neighbours (shared B)
   const int ntile = lb % a.nt;
   const int b = lb / a.nt;
   const int m0 = mtile * BM;
@@ -52,74 +56,118 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
   const int64_t P = a.P;
   const float* xb = a.x + (int64_t)b * (LOADER == LD_IM2COL ? (int64_t)(K / 4) * a.Hin * a.Win : (int64_t)K * P);
 
-  float sdv[4] = {1.f, 1.f, 1.f, 1.f};
+  // A staging: thread -> row am, 8 consecutive k;  B staging: thread -> row bk, 8 consecutive n
+  const int am = tid >> 1, ak = (tid & 1) * 8;
+  const int bk = tid >> 4, bn = (tid & 15) * 8;
+  float ra[8], rb[8];
+  float sd[8];
   if constexpr (LOADER == LD_LN) {
-    // this thread's 4 B-tile columns are fixed across the K loop
-    const int nn = (tid & 15) * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t n = n0 + nn + q;
-      sdv[q] = n < P ? a.ln_sd[(int64_t)b * P + n] : 1.f;
+    for (int q = 0; q < 8; ++q) {
+      const int64_t n = n0 + bn + q;
+      sd[q] = n < P ? a.ln_sd[(int64_t)b * P + n] : 1.f;
     }
   }
-  f32x16 acc = {};
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    // A tile: wt[m0..m0+63][k0..k0+31] -> As[k][m]
+  auto load_chunk = [&](int k0) {
+    const int mm = m0 + am;
+    if (VEC && mm < M && k0 + ak + 8 <= K) {
+      const float4* src = reinterpret_cast<const float4*>(a.wt + (int64_t)mm * K + k0 + ak);
+      const float4 v0 = src[0], v1 = src[1];
+      ra[0] = v0.x; ra[1] = v0.y; ra[2] = v0.z; ra[3] = v0.w;
+      ra[4] = v1.x; ra[5] = v1.y; ra[6] = v1.z; ra[7] = v1.w;
+    } else {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = tid + it * GT;          // 512 float4 slots
-      const int m = idx >> 3, kq = (idx & 7) * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int k = k0 + kq + q, mm = m0 + m;
-        As[kq + q][m] = (mm < M && k < K) ? a.wt[(int64_t)mm * K + k] : 0.f;
+      for (int q = 0; q < 8; ++q) {
+        const int k = k0 + ak + q;
+        ra[q] = (mm < M && k < K) ? a.wt[(int64_t)mm * K + k] : 0.f;
       }
     }
-    // B tile: Bop[k0..k0+31][n0..n0+63] -> Bs[k][n]
+    const int k = k0 + bk;
+    if constexpr (LOADER == LD_IM2COL) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = tid + it * GT;
-      const int kk = idx >> 4, nn = (idx & 15) * 4;
-      const int k = k0 + kk;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t n = n0 + nn + q;
+      for (int q = 0; q < 8; ++q) {
+        const int64_t n = n0 + bn + q;
         float v = 0.f;
         if (k < K && n < P) {
-          if constexpr (LOADER == LD_IM2COL) {
-            const int ci = k >> 2, ay = (k >> 1) & 1, ax = k & 1;
-            const int oy = (int)(n / a.Wo), ox = (int)(n - (int64_t)oy * a.Wo);
-            v = xb[((int64_t)ci * a.Hin + 2 * oy + ay) * a.Win + 2 * ox + ax];
-          } else {
-            v = xb[(int64_t)k * P + n];
-            if constexpr (LOADER == LD_LN) v = (v / sdv[q]) * a.ln_w[k];   // REF:921-925
-          }
+          const int ci = k >> 2, ay = (k >> 1) & 1, ax = k & 1;
+          const int oy = (int)(n / a.Wo), ox = (int)(n - (int64_t)oy * a.Wo);
+          v = xb[((int64_t)ci * a.Hin + 2 * oy + ay) * a.Win + 2 * ox + ax];
         }
-        Bs[kk][nn + q] = v;
+        rb[q] = v;
+      }
+    } else {
+      if (VEC && k < K && n0 + bn + 8 <= P) {
+        const float4* src = reinterpret_cast<const float4*>(xb + (int64_t)k * P + n0 + bn);
+        const float4 v0 = src[0], v1 = src[1];
+        rb[0] = v0.x; rb[1] = v0.y; rb[2] = v0.z; rb[3] = v0.w;
+        rb[4] = v1.x; rb[5] = v1.y; rb[6] = v1.z; rb[7] = v1.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int64_t n = n0 + bn + q;
+          rb[q] = (k < K && n < P) ? xb[(int64_t)k * P + n] : 0.f;
+        }
+      }
+      if constexpr (LOADER == LD_LN) {
+        const float g = k < K ? a.ln_w[k] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rb[q] = (rb[q] / sd[q]) * g;   // REF:921-925
       }
     }
-    __syncthreads();
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) As[buf][ak + q][am] = ra[q];
+    *reinterpret_cast<float4*>(&Bs[buf][bk][bn]) = make_float4(rb[0], rb[1], rb[2], rb[3]);
+    *reinterpret_cast<float4*>(&Bs[buf][bk][bn + 4]) = make_float4(rb[4], rb[5], rb[6], rb[7]);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int nchunks = (K + BK - 1) / BK;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunks) load_chunk((c + 1) * BK);   // in flight during this chunk's MFMAs
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      const float av = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
-      const float bv = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      const int kr = kk + (lane >> 5);
+      const float a0 = As[buf][kr][wm * 64 + (lane & 31)];
+      const float a1 = As[buf][kr][wm * 64 + 32 + (lane & 31)];
+      const float b0 = Bs[buf][kr][wn * 64 + (lane & 31)];
+      const float b1 = Bs[buf][kr][wn * 64 + 32 + (lane & 31)];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
+    if (c + 1 < nchunks) store_chunk(buf ^ 1);
     __syncthreads();
   }
   float s0 = 0.f, s1 = 1.f;
   if constexpr (EPI == EP_SKIP) { s0 = a.skip[0]; s1 = a.skip[1]; }
-  const int64_t n = n0 + wn * 32 + (lane & 31);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (m < M && n < P) {
-      const int64_t o = ((int64_t)b * M + m) * P + n;
-      float v = acc[r];
-      if constexpr (EPI == EP_SKIP) v = s0 * a.res[o] + s1 * v;          // REF:962-964
-      a.out[o] = v;
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M && n < P) {
+          const int64_t o = ((int64_t)b * M + m) * P + n;
+          float v = acc[i][j][r];
+          if constexpr (EPI == EP_SKIP) v = s0 * a.res[o] + s1 * v;          // REF:962-964
+          a.out[o] = v;
+        }
+      }
     }
-  }
 }
 
 template <int LOADER, int EPI>
@@ -131,7 +179,10 @@ static grr_status launch_gemm(GemmArgs a, int B, hipStream_t s, const char* name
   const uint64_t n = (uint64_t)B * a.mt * a.nt;
   GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   a.nblk = (uint32_t)n;
-  hipLaunchKernelGGL((gemm_f32_kernel<LOADER, EPI>), dim3(a.nblk), dim3(GT), 0, s, a);
+  // 16-byte vector staging needs 4-aligned row strides (and base pointers, which torch provides)
+  const bool vec = (a.K % 4 == 0) && (a.P % 4 == 0) && ((uintptr_t)a.x % 16 == 0) && ((uintptr_t)a.wt % 16 == 0);
+  if (vec) hipLaunchKernelGGL((gemm_f32_kernel<LOADER, EPI, true>), dim3(a.nblk), dim3(GT), 0, s, a);
+  else hipLaunchKernelGGL((gemm_f32_kernel<LOADER, EPI, false>), dim3(a.nblk), dim3(GT), 0, s, a);
   return launch_status(name);
 }
 

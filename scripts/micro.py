@@ -1,0 +1,75 @@
+"""Micro-benchmark of single HIP kernels at the bench shape (P: B=64, G=32, F=3, 256x256).
+
+    python scripts/micro.py [--kernel step|half|lnb|conv1x1|edge] [--iters N] [--batch B]
+
+Used under rocprofv3 (kernel trace / PMC passes) to profile one kernel in isolation.
+Prints mean milliseconds per launch and algorithmic GB/s from HIP events.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import irdu_amd  # noqa: E402
+from irdu_amd import kernels as K  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="step")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--size", type=int, default=256)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    b, g, f, h, w = args.batch, 32, 3, args.size, args.size
+    c = g * f
+    torch.manual_seed(0)
+    mix = irdu_amd.MixtureGTVGLR(g, f, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]],
+                                 n_cgd_iters=10).to(dev)
+    x = torch.rand(b, c, h, w, device=dev)
+    rhs = torch.rand(b, c, h, w, device=dev)
+    u = torch.rand(b, c, h, w, device=dev)
+    th = torch.rand(b, c, h // 2, w // 2, device=dev)
+    wl = torch.softmax(torch.rand(b, g, 4, h, w, device=dev), 2)
+    cg = torch.rand(b, g, 2, h, w, device=dev)
+    sl, sg = K.stencil(mix.GLRmodule00), K.stencil(mix.GTVmodule00)
+    p = lambda t: t.data  # noqa: E731
+
+    if args.kernel == "step":
+        fn = lambda: K.system_step(x, rhs, u, th, wl, cg, sl, sg, p(mix.muys00), p(mix.ro00), p(mix.alphaCGD)[2],  # noqa: E731
+                                   p(mix.betaCGD)[2], g, want_u=True, want_pool=True)
+    elif args.kernel == "half":
+        xd = torch.rand(b, c, h // 2, w // 2, device=dev)
+        wl1 = torch.softmax(torch.rand(b, g, 4, h // 2, w // 2, device=dev), 2)
+        cg1 = torch.rand(b, g, 2, h // 2, w // 2, device=dev)
+        fn = lambda: K.system_half(xd, wl1, cg1, sl, sg, p(mix.muys01), p(mix.ro01), g)  # noqa: E731
+    elif args.kernel == "lnb":
+        blk = irdu_amd.LocalNonLinearBlock(c, 256, 1).to(dev)
+        fn = lambda: blk(x)  # noqa: E731
+    elif args.kernel == "conv1x1":
+        wt = torch.rand(2 * c, c, 1, 1, device=dev)
+        fn = lambda: K.conv1x1(x, wt)  # noqa: E731
+    elif args.kernel == "edge":
+        feat = torch.rand(b, 2 * c, h, w, device=dev)
+        fn = lambda: K.edge_weights(feat, 0, g, f, p(mix.GTVmodule00.multiM))  # noqa: E731
+    else:
+        raise SystemExit(f"unknown kernel {args.kernel}")
+    with torch.no_grad():
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        timer = K.LaunchTimer()
+        K.set_timer(timer)
+        for _ in range(args.iters):
+            fn()
+        K.set_timer(None)
+        for kind, v in timer.summary().items():
+            print(f"{args.kernel}: {kind:16s} launches={v['launches']} mean={v['mean_ms']:.4f} ms "
+                  f"algo={v['gbps']:.1f} GB/s bytes/launch={v['bytes_per_launch']:.4e}")
+
+
+if __name__ == "__main__":
+    main()
