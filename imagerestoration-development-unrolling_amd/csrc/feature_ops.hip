@@ -253,6 +253,143 @@ __global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ 
   }
 }
 
+// LocalNonLinearBlock tail, fused: out = skip0*x + skip1 * W2 . gate(dw3x3(h))
+// (REF:943-948, :962-964).  A workgroup owns a 4x32 pixel tile and ALL M <= 128 output
+// channels (wave w: pixels 32w..32w+31 of the tile, MT 32-row MFMA tiles).  The hidden
+// channels are walked in chunks of KC: the mask / value planes of the chunk are staged
+// with a 1-pixel replicate halo (double-buffered, next chunk's loads in flight), the
+// depthwise 3x3 and the gate are evaluated into the MFMA B image, and the chunk's W2
+// columns are applied on the matrix cores.  The gated activations never reach HBM.
+constexpr int FT = 256;             // threads
+constexpr int FTR = 4, FTC = 32;    // pixel tile rows x cols (128 pixels)
+constexpr int FKC = 8;              // hidden channels per chunk
+constexpr int FHR = FTR + 2, FHC = FTC + 2, FHA = FHR * FHC;   // halo tile 6 x 34
+constexpr int FSTAGE = 2 * FKC * FHA;                          // mask + value halo tiles per chunk
+constexpr int FLD = (FSTAGE + FT - 1) / FT;                    // staging loads per thread (13)
+
+struct LnbTailArgs {
+  const float* h;      // [B, 2hid, H, W]
+  const float* wdw;    // [2hid, 9]
+  const float* w2;     // [M, hid]
+  const float* x;      // [B, M, H, W] residual
+  const float* skip;   // [2]
+  float* out;          // [B, M, H, W]
+  int hid, M, H, W, tiles_x, tiles_y;
+  uint32_t nblk;
+};
+
+template <int MT>
+__global__ __launch_bounds__(FT) void lnb_tail_kernel(LnbTailArgs a) {
+  __shared__ float Hs[2][FSTAGE];
+  __shared__ float Bs[FKC][FTR * FTC + 4];
+  __shared__ float As[FKC][MT * 32 + 2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int tx = lb % a.tiles_x; lb /= a.tiles_x;
+  const int ty = lb % a.tiles_y;
+  const int b = lb / a.tiles_y;
+  const int H = a.H, W = a.W, hid = a.hid, M = a.M;
+  const int64_t HW = (int64_t)H * W;
+  const int y0 = ty * FTR, x0 = tx * FTC;
+  const float* hb = a.h + (int64_t)b * 2 * hid * HW;
+
+  float st[FLD];
+  auto load_chunk = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < FLD; ++j) {
+      const int i = tid + j * FT;
+      const int ii = i < FSTAGE ? i : FSTAGE - 1;
+      const int plane = ii / FHA, r = ii - plane * FHA;      // plane: [0,KC) mask, [KC,2KC) value
+      const int kk = plane < FKC ? plane : plane - FKC;
+      const int ch = (plane < FKC ? 0 : hid) + k0 + kk;
+      const int ry = r / FHC, rx = r - ry * FHC;
+      const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 1 + rx, 0, W - 1);
+      st[j] = (k0 + kk < hid) ? hb[(int64_t)ch * HW + (int64_t)gy * W + gx] : 0.f;
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < FLD; ++j) {
+      const int i = tid + j * FT;
+      if (i < FSTAGE) Hs[buf][i] = st[j];
+    }
+  };
+
+  f32x16 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x16{};
+  const int nchunks = (hid + FKC - 1) / FKC;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1, k0 = c * FKC;
+    if (c + 1 < nchunks) load_chunk(k0 + FKC);
+    // W2 columns of this chunk -> As[k][m]
+    for (int i = tid; i < FKC * MT * 32; i += FT) {
+      const int kk = i / (MT * 32), m = i - kk * (MT * 32);
+      As[kk][m] = (m < M && k0 + kk < hid) ? a.w2[(int64_t)m * hid + k0 + kk] : 0.f;
+    }
+    // depthwise 3x3 (replicate pad) + gate: 8 channels x 128 pixels, 4 per thread.
+    // The channel of each pass is wave-uniform (readfirstlane), so the taps are scalar loads.
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const int p = tid & (FTR * FTC - 1);
+    const int py = p / FTC, px = p - py * FTC;
+#pragma unroll
+    for (int q = 0; q < (FKC * FTR * FTC) / FT; ++q) {
+      const int kk = (wave_u >> 1) + 2 * q;
+      const int k = k0 + kk;
+      float g = 0.f;
+      if (k < hid) {
+        const float* mt = &Hs[buf][kk * FHA];
+        const float* vt = &Hs[buf][(FKC + kk) * FHA];
+        const float* km = a.wdw + k * 9;
+        const float* kv = a.wdw + (hid + k) * 9;
+        float m = 0.f, v = 0.f;
+#pragma unroll
+        for (int ay = 0; ay < 3; ++ay)
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) {
+            const int li = (py + ay) * FHC + px + ax;
+            m += km[ay * 3 + ax] * mt[li];
+            v += kv[ay * 3 + ax] * vt[li];
+          }
+        const float sg = 1.0f / (1.0f + expf(-m));
+        g = (sg * m) * v;
+      }
+      Bs[kk][p] = g;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < FKC; kk += 2) {
+      const int kr = kk + (lane >> 5);
+      const float bv = Bs[kr][wave * 32 + (lane & 31)];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const float av = As[kr][t * 32 + (lane & 31)];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+      }
+    }
+    if (c + 1 < nchunks) store_chunk(buf ^ 1);
+    __syncthreads();
+  }
+  const float s0 = a.skip[0], s1 = a.skip[1];
+  const int p = wave * 32 + (lane & 31);
+  const int gy = y0 + p / FTC, gx = x0 + (p % FTC);
+  if (gy < H && gx < W) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M) {
+          const int64_t o = ((int64_t)b * M + m) * HW + (int64_t)gy * W + gx;
+          a.out[o] = s0 * a.x[o] + s1 * acc[t][r];      // REF:962-964
+        }
+      }
+  }
+}
+
 __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __restrict__ out, int Cin, int G,
                                      int64_t P, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -294,7 +431,7 @@ int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
   (void)C;
   const int64_t P = (int64_t)H * W;
   const int64_t sd = ((int64_t)B * P + 63) / 64 * 64;
-  return (sd + (int64_t)B * 3 * hid * P) * (int64_t)sizeof(float);
+  return (sd + (int64_t)B * 2 * hid * P) * (int64_t)sizeof(float);
 }
 
 grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
@@ -309,7 +446,6 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
   const int64_t P = (int64_t)H * W;
   float* sd = (float*)workspace;
   float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;   // [B, 2hid, P]
-  float* gbuf = hbuf + (int64_t)B * 2 * hid * P;        // [B, hid, P]
   {
     const int64_t n = (int64_t)B * P;
     const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
@@ -323,18 +459,21 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
     grr_status st = launch_gemm<LD_LN, EP_STORE>(a, B, s, "grr_lnb_forward/gemm1");
     if (st != GRR_OK) return st;
   }
-  {
-    const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
-    const uint64_t n = (uint64_t)B * hid * tx * ty;
-    GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
-    hipLaunchKernelGGL(dw_gate_kernel, dim3((uint32_t)n), dim3(256), 0, s, hbuf, wdw, gbuf, hid, H, W, tx, ty,
-                       (uint32_t)n);
-    grr_status st = launch_status("grr_lnb_forward/dw_gate");
-    if (st != GRR_OK) return st;
-  }
-  GemmArgs a{};
-  a.x = gbuf; a.wt = w2; a.res = x; a.skip = skip; a.out = out; a.K = hid; a.M = C; a.P = P;
-  return launch_gemm<LD_PLAIN, EP_SKIP>(a, B, s, "grr_lnb_forward/gemm2");
+  GRR_REQUIRE(C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 128", C);
+  LnbTailArgs t{};
+  t.h = hbuf; t.wdw = wdw; t.w2 = w2; t.x = x; t.skip = skip; t.out = out;
+  t.hid = hid; t.M = C; t.H = H; t.W = W;
+  t.tiles_x = (W + FTC - 1) / FTC;
+  t.tiles_y = (H + FTR - 1) / FTR;
+  const uint64_t n = (uint64_t)B * t.tiles_x * t.tiles_y;
+  GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+  t.nblk = (uint32_t)n;
+  const int mt = (C + 31) / 32;
+  if (mt == 1) hipLaunchKernelGGL((lnb_tail_kernel<1>), dim3(t.nblk), dim3(FT), 0, s, t);
+  else if (mt == 2) hipLaunchKernelGGL((lnb_tail_kernel<2>), dim3(t.nblk), dim3(FT), 0, s, t);
+  else if (mt == 3) hipLaunchKernelGGL((lnb_tail_kernel<3>), dim3(t.nblk), dim3(FT), 0, s, t);
+  else hipLaunchKernelGGL((lnb_tail_kernel<4>), dim3(t.nblk), dim3(FT), 0, s, t);
+  return launch_status("grr_lnb_forward/tail");
 }
 
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {
