@@ -190,7 +190,8 @@ struct OpArgs {
   float* u_out;
   float* xd_out;
   int G, F, H, W, tiles_x, tiles_y;
-  uint32_t nblk;
+  int nstrips, nsegs;
+  uint32_t nunits, nblk;
 };
 
 struct Taps {
@@ -238,110 +239,103 @@ __device__ __forceinline__ float prox_phi(float t, float gm) {
   return eps - (t - eps);
 }
 
+// ---------------------------------------------------------------------------
+// Streaming fused graph operator.
+//
+// One wave = one (b, channel) plane, one 64-column strip, one segment of SSEG output
+// rows.  Lane = column.  The wave marches down the rows; each iteration loads one
+// input row and advances a 4-stage pipeline held entirely in registers:
+//     x row t  ->  s = S x at row t-1  ->  {l, o} at row t-2  ->  S^T + epilogue at row t-3
+// Vertical neighbours are the previous iteration's registers; horizontal neighbours
+// come from the adjacent lanes through DPP wave shifts (v_mov_b32_dpp wave_shr/shl:1).
+// No LDS and no barriers.  Each stage needs one column of halo on each side, so a
+// 64-lane strip produces SVALID = 58 output columns.  Row loads (one 256-B coalesced
+// line per wave and operand) are issued two iterations ahead of their use (register
+// ring of depth 2).
+// ---------------------------------------------------------------------------
+constexpr int SVALID = 58;   // output columns per strip (3-column halo each side)
+constexpr int SSEG = 64;     // output rows per segment (pipeline fill: 6 rows)
+
+// Cross-lane reads must execute with the whole wave active: a DPP read of a lane that
+// is masked off returns 0.  The empty asm pins each result at its definition, so the
+// compiler cannot sink the v_mov_b32_dpp into a divergent branch (it turned
+// `c > 0 ? lane_prev(v) : 0` into an exec-masked branch before this was added).
+__device__ __forceinline__ float lane_prev(float v) {  // value of lane-1 (column c-1)
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ float lane_next(float v) {  // value of lane+1 (column c+1)
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+// plain global addressing: base pointer (uniform) + per-lane column offset (bytes) +
+// per-row offset (floats, uniform)
+struct rsrc_t {
+  const float* p;
+};
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t) { return rsrc_t{p}; }
+__device__ __forceinline__ float bload(rsrc_t r, int voff_bytes, int soff_floats) {
+  return r.p[soff_floats + (voff_bytes >> 2)];
+}
+__device__ __forceinline__ void bstore(float v, rsrc_t r, int voff_bytes, int soff_floats) {
+  const_cast<float*>(r.p)[soff_floats + (voff_bytes >> 2)] = v;
+}
+
+// loads consumed by one pipeline iteration t (issued two iterations earlier)
+struct RowLoads {
+  float x;        // x row t
+  float wl[4];    // GLR edge weights, row t-2
+  float wg[4];    // GTV pair weights (2) or raw weights (4), row t-2
+  float wup;      // prox: w_up at row t-1 (the scatter source below)
+  float eb, eu, ey, th;  // epilogue operands at row t-3
+};
+
 template <bool GLR, int GTV, int EPI>
 __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
-  __shared__ float Xs[XA];
-  __shared__ float SLs[GLR ? SA : 1];
-  __shared__ float SGs[GTV ? SA : 1];
-  __shared__ float Ls[GLR ? LA : 1];
-  __shared__ float Gs[GTV ? LA : 1];
-  constexpr int NW = GTV == GTV_PROX ? 8 : 4;
-  constexpr int NXL = (XA + NT - 1) / NT;  // input-tile loads per thread (6)
-
-  // One workgroup = one (b, channel, 32x32 tile).  The F channel-workgroups of a
-  // (b, graph, tile) are consecutive logical blocks, so after the XCD remap they run
-  // together on one XCD and the graph's edge weights are fetched from HBM once.
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * 4 + wave;
+  if (unit >= a.nunits) return;   // whole wave (uniform)
   const int F = a.F;
-  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
-  const int f = lb % F; lb /= F;
-  const int tx = lb % a.tiles_x; lb /= a.tiles_x;
-  const int ty = lb % a.tiles_y; lb /= a.tiles_y;
-  const int g = lb % a.G;
-  const int b = lb / a.G;
-  const int H = a.H, W = a.W, C = a.G * F;
-  const int64_t HW = (int64_t)H * W;
-  const int y0 = ty * TILE, x0 = tx * TILE;
-  const int ch = g * F + f;
-  const int64_t plane = ((int64_t)b * C + ch) * HW;
+  const int strip = unit % a.nstrips; unit /= a.nstrips;
+  const int f = unit % F; unit /= F;
+  const int seg = unit % a.nsegs; unit /= a.nsegs;
+  const int g = unit % a.G;
+  const int b = unit / a.G;
+  const int H = a.H, W = a.W, C = a.G * F, ch = g * F + f;
   const int hh = H / 2, hw = W / 2;
+  const int64_t HW = (int64_t)H * W;
+  const int c = strip * SVALID - 3 + lane;
+  const int cc = clampi(c, 0, W - 1);
+  const bool cin = c >= 0 && c < W;
+  const bool owner = lane >= 3 && lane < 3 + SVALID && cin;
+  const int r0 = seg * SSEG, r1 = min(r0 + SSEG, H);
+  const int vo = cc * 4, vo_half = (cc >> 1) * 4;
 
-  // ---- issue every global load of the workgroup up front ----------------------
-  // (1) input tile, halo 3, replicate-clamped (REF:186 replicate pad)
-  float xr[NXL];
-  {
-    const float* xp = a.x + plane;
-#pragma unroll
-    for (int j = 0; j < NXL; ++j) {
-      const int i = tid + j * NT;
-      const int ii = i < XA ? i : XA - 1;
-      const int ry = ii / XS, rx = ii - ry * XS;
-      const int gy = clampi(y0 - 3 + ry, 0, H - 1), gx = clampi(x0 - 3 + rx, 0, W - 1);
-      xr[j] = xp[(int64_t)gy * W + gx];
-    }
-  }
-  // (2) this graph's edge weights at the pass-B points
-  float wl[NPB][4];
-  float wg[NPB][NW];
-  {
-    const float* wLb = GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
-    const float* wGb = GTV ? a.wG + (int64_t)(b * a.G + g) * (GTV == GTV_PROX ? 4 : 2) * HW : nullptr;
-#pragma unroll
-    for (int j = 0; j < NPB; ++j) {
-      const int i = tid + j * NT;
-      const int ry = i / LS, rx = i - ry * LS;
-      const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
-      const bool in = i < LA && gy >= 0 && gy < H && gx >= 0 && gx < W;
-      const int64_t o = (int64_t)gy * W + gx;
-      if constexpr (GLR) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) wl[j][e] = in ? wLb[e * HW + o] : 0.f;
-      }
-      if constexpr (GTV == GTV_PAIR) {
-        wg[j][0] = in ? wGb[o] : 0.f;                              // c_h(q)      right edge
-        wg[j][1] = (in && gx > 0) ? wGb[o - 1] : 0.f;              // c_h(q-1)    left edge
-        wg[j][2] = in ? wGb[HW + o] : 0.f;                         // c_v(q)      down edge
-        wg[j][3] = (in && gy > 0) ? wGb[HW + o - W] : 0.f;         // c_v(q-W)    up edge
-      }
-      if constexpr (GTV == GTV_PROX) {
-        // own edges e at q (zero where q+delta_e leaves the image: the reference's
-        // clamped neighbour is q itself, so E_e = w*s(q) - w*s(q) = 0)
-        wg[j][0] = (in && gy > 0) ? wGb[o] : 0.f;
-        wg[j][1] = (in && gx > 0) ? wGb[HW + o] : 0.f;
-        wg[j][2] = (in && gx < W - 1) ? wGb[2 * HW + o] : 0.f;
-        wg[j][3] = (in && gy < H - 1) ? wGb[3 * HW + o] : 0.f;
-        // edges e of the pixel p = q - delta_e whose scatter lands on q (REF:482-500)
-        wg[j][4] = (in && gy < H - 1) ? wGb[o + W] : 0.f;               // w_up(q+down)
-        wg[j][5] = (in && gx < W - 1) ? wGb[HW + o + 1] : 0.f;          // w_left(q+right)
-        wg[j][6] = (in && gx > 0) ? wGb[2 * HW + o - 1] : 0.f;          // w_right(q-right)
-        wg[j][7] = (in && gy > 0) ? wGb[3 * HW + o - W] : 0.f;          // w_down(q-down)
-      }
-    }
-  }
-  // (3) epilogue operands of this thread's 2x2 output block
-  const int by = tid >> 4, bx = tid & 15;
-  const int gy0 = y0 + 2 * by, gx0 = x0 + 2 * bx;
-  float eb[2][2] = {}, eu[2][2] = {}, ey[2][2] = {};
-  float th = 0.f;
+  const int64_t plane = ((int64_t)b * C + ch) * HW;
+  const int64_t hplane = ((int64_t)b * C + ch) * (int64_t)hh * hw;
+  const rsrc_t rx = make_rsrc(a.x + plane, HW);
   const bool has_half = EPI != EPI_HALF && a.t_half != nullptr;
   const bool use_beta = EPI == EPI_STEP && a.beta != nullptr && a.u_prev != nullptr;
   const bool need_y = (EPI == EPI_RHS) || (EPI == EPI_STEP && a.skip != nullptr);
-  if (EPI != EPI_HALF) {
-#pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const int gy = gy0 + dy, gx = gx0 + dx;
-        if (gy < H && gx < W) {
-          const int64_t o = plane + (int64_t)gy * W + gx;
-          if (EPI == EPI_STEP) eb[dy][dx] = a.b[o];
-          if (use_beta) eu[dy][dx] = a.u_prev[o];
-          if (need_y) ey[dy][dx] = a.y[o];
-        }
-      }
-    if (has_half && gy0 < H && gx0 < W)
-      th = 0.25f * a.t_half[((int64_t)b * C + ch) * hh * hw + (int64_t)(gy0 >> 1) * hw + (gx0 >> 1)];
-  }
+  const bool want_u = EPI == EPI_STEP && a.u_out != nullptr;
+  const bool want_xd = a.xd_out != nullptr;
+  // descriptors of absent operands get 0 records (never read: their loads are compiled out
+  // or guarded by the same uniform flags)
+  const int np = GTV == GTV_PROX ? 4 : 2;
+  const rsrc_t rwl = make_rsrc(GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : a.x, GLR ? 4 * HW : 0);
+  const rsrc_t rwg = make_rsrc(GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : a.x, GTV ? np * HW : 0);
+  const rsrc_t rb = make_rsrc(EPI == EPI_STEP ? a.b + plane : a.x, EPI == EPI_STEP ? HW : 0);
+  const rsrc_t ru = make_rsrc(use_beta ? a.u_prev + plane : a.x, use_beta ? HW : 0);
+  const rsrc_t ry = make_rsrc(need_y ? a.y + plane : a.x, need_y ? HW : 0);
+  const rsrc_t rth = make_rsrc(has_half ? a.t_half + hplane : a.x, has_half ? (int64_t)hh * hw : 0);
+  const rsrc_t rout = make_rsrc(a.out + plane, HW);
+  const rsrc_t ruo = make_rsrc(want_u ? a.u_out + plane : a.out, want_u ? HW : 0);
+  const rsrc_t rxd = make_rsrc(want_xd ? a.xd_out + hplane : a.out, want_xd ? (int64_t)hh * hw : 0);
+
   float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
   if (a.log_l) sc_l = expf(a.log_l[g]);
   if (a.log_g) sc_g = expf(a.log_g[g]);
@@ -356,139 +350,180 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   if constexpr (GLR) tL = make_taps(a.sL, ch);
   if constexpr (GTV != GTV_NONE) tG = make_taps(a.sG, ch);
 
-  // ---- pass 0: input tile to LDS
+  auto issue = [&](int t, RowLoads& S) {
+    S.x = bload(rx, vo, clampi(t, 0, H - 1) * W);
+    const int rw = clampi(t - 2, 0, H - 1) * W;
+    if constexpr (GLR) {
 #pragma unroll
-  for (int j = 0; j < NXL; ++j) {
-    const int i = tid + j * NT;
-    if (i < XA) Xs[i] = xr[j];
-  }
-  __syncthreads();
-  // ---- pass A: s = S x on the halo-2 region (values outside the image are never read)
-  for (int i = tid; i < SA; i += NT) {
-    const int ry = i / SS, rx = i - ry * SS;
-    const int xi = (ry + 1) * XS + rx + 1;
-    if constexpr (GLR) SLs[i] = stencil(tL, Xs, xi, XS);
-    if constexpr (GTV != GTV_NONE) SGs[i] = stencil(tG, Xs, xi, XS);
-  }
-  __syncthreads();
-  // ---- pass B: l = s - W s (GLR, REF:218-228) and o = C^T phi(C s) (GTV, REF:452-516)
+      for (int e = 0; e < 4; ++e) S.wl[e] = bload(rwl, vo, (int)(e * HW) + rw);
+    }
+    if constexpr (GTV == GTV_PAIR) {
+      S.wg[0] = bload(rwg, vo, rw);
+      S.wg[1] = bload(rwg, vo, (int)HW + rw);
+    }
+    if constexpr (GTV == GTV_PROX) {
 #pragma unroll
-  for (int j = 0; j < NPB; ++j) {
-    const int i = tid + j * NT;
-    if (i < LA) {
-      const int ry = i / LS, rx = i - ry * LS;
-      const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
-      const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-      const int si = (ry + 1) * SS + rx + 1;
+      for (int e = 0; e < 4; ++e) S.wg[e] = bload(rwg, vo, (int)(e * HW) + rw);
+      S.wup = bload(rwg, vo, clampi(t - 1, 0, H - 1) * W);
+    }
+    const int re = clampi(t - 3, 0, H - 1);
+    if (EPI == EPI_STEP) S.eb = bload(rb, vo, re * W);
+    if (use_beta) S.eu = bload(ru, vo, re * W);
+    if (need_y) S.ey = bload(ry, vo, re * W);
+    if (has_half) S.th = bload(rth, vo_half, (re >> 1) * hw);
+  };
+
+  // pipeline registers (rows relative to the current iteration t)
+  float X0 = 0.f, X1 = 0.f, X2 = 0.f, X3 = 0.f;   // x rows t-3 .. t
+  float SL0 = 0.f, SL1 = 0.f, SL2 = 0.f;          // S_L x rows t-3 .. t-1
+  float SG0 = 0.f, SG1 = 0.f, SG2 = 0.f;          // S_G x rows t-3 .. t-1
+  float L0 = 0.f, L1 = 0.f, L2 = 0.f;             // l rows t-4 .. t-2
+  float O0 = 0.f, O1 = 0.f, O2 = 0.f;             // o rows t-4 .. t-2
+  float cv_prev = 0.f, wdn_prev = 0.f, xn_prev = 0.f;
+
+  auto consume = [&](int t, const RowLoads& S) {
+    // ---- stage 1: input row t
+    X0 = X1; X1 = X2; X2 = X3; X3 = S.x;
+    // ---- stage 2: s at row t-1 (replicate: X rows are clamped loads)
+    {
+      const float xl = lane_prev(X2), xr = lane_next(X2);
       if constexpr (GLR) {
-        float l = 0.f;
-        if (in) {
-          const int nu = gy > 0 ? si - SS : si, nl = gx > 0 ? si - 1 : si;
-          const int nr = gx < W - 1 ? si + 1 : si, nd = gy < H - 1 ? si + SS : si;
-          const float wx = ((wl[j][0] * SLs[nu] + wl[j][1] * SLs[nl]) + wl[j][2] * SLs[nr]) + wl[j][3] * SLs[nd];
-          l = SLs[si] - wx;
-        }
-        Ls[i] = l;
+        float sv = tL.u * X1;
+        sv += tL.l * xl; sv += tL.c * X2; sv += tL.r * xr; sv += tL.d * X3;
+        SL0 = SL1; SL1 = SL2; SL2 = sv;
+      }
+      if constexpr (GTV != GTV_NONE) {
+        float sv = tG.u * X1;
+        sv += tG.l * xl; sv += tG.c * X2; sv += tG.r * xr; sv += tG.d * X3;
+        SG0 = SG1; SG1 = SG2; SG2 = sv;
+      }
+    }
+    // ---- stage 3: l and o at row r = t-2 (zero outside the image: S^T's zero boundary)
+    {
+      const int r = t - 2;
+      const bool rin = r >= 0 && r < H;
+      if constexpr (GLR) {
+        // (I - W) s with the replicate-clamped neighbour s(clamp(q + delta_e))  (REF:218-228)
+        const float up = r > 0 ? SL0 : SL1;
+        const float dn = r < H - 1 ? SL2 : SL1;
+        const float pv = lane_prev(SL1), nx = lane_next(SL1);
+        const float lf = c > 0 ? pv : SL1;
+        const float rt = c < W - 1 ? nx : SL1;
+        const float wx = ((S.wl[0] * up + S.wl[1] * lf) + S.wl[2] * rt) + S.wl[3] * dn;
+        const float l = (rin && cin) ? SL1 - wx : 0.f;
+        L0 = L1; L1 = L2; L2 = l;
       }
       if constexpr (GTV == GTV_PAIR) {
-        float o = 0.f;
-        if (in) {
-          const float s = SGs[si];
-          o = wg[j][0] * (s - SGs[si + 1]) + wg[j][1] * (s - SGs[si - 1]) +
-              wg[j][2] * (s - SGs[si + SS]) + wg[j][3] * (s - SGs[si - SS]);
-        }
-        Gs[i] = o;
+        // C^T C s with symmetrised pair weights (zero on edges leaving the image)
+        const float chp = lane_prev(S.wg[0]);
+        const float chl = c > 0 ? chp : 0.f;
+        const float cvu = r > 0 ? cv_prev : 0.f;
+        const float sv = SG1;
+        const float o = S.wg[0] * (sv - lane_next(SG1)) + chl * (sv - lane_prev(SG1)) +
+                        S.wg[1] * (sv - SG2) + cvu * (sv - SG0);
+        cv_prev = S.wg[1];
+        const float ov = (rin && cin) ? o : 0.f;
+        O0 = O1; O1 = O2; O2 = ov;
       }
       if constexpr (GTV == GTV_PROX) {
-        float o = 0.f;
-        if (in) {
-          const float s = SGs[si];
-          const int nb[4] = {si - SS, si - 1, si + 1, si + SS};
-          float z[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float we = wg[j][e];
-            z[e] = prox_phi(we * s - we * SGs[nb[e]], gam) * we;   // z_e(q)
-          }
-          o = ((z[0] + z[1]) + z[2]) + z[3];
-          // subtract z_e(q - delta_e) in edge order (REF:482-500)
-          const int pb[4] = {si + SS, si + 1, si - 1, si - SS};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float we = wg[j][4 + e];
-            o = o - prox_phi(we * SGs[pb[e]] - we * s, gam) * we;
-          }
-        }
-        Gs[i] = o;
+        // o = sum_e z_e(q) - sum_e z_e(q - delta_e),  z_e = phi(E_e) w_e  (REF:452-516, :765-781)
+        const float sv = SG1;
+        const float su = r > 0 ? SG0 : sv, sd = r < H - 1 ? SG2 : sv;
+        const float spv = lane_prev(SG1), snx = lane_next(SG1);
+        const float sl = c > 0 ? spv : sv, sr = c < W - 1 ? snx : sv;
+        const float w0 = S.wg[0], w1 = S.wg[1], w2 = S.wg[2], w3 = S.wg[3];
+        const float z0 = prox_phi(w0 * sv - w0 * su, gam) * w0;
+        const float z1 = prox_phi(w1 * sv - w1 * sl, gam) * w1;
+        const float z2 = prox_phi(w2 * sv - w2 * sr, gam) * w2;
+        const float z3 = prox_phi(w3 * sv - w3 * sd, gam) * w3;
+        float o = ((z0 + z1) + z2) + z3;
+        // scatters landing on q, in edge order; frame-dropped when the source is outside
+        const float wupb = S.wup;                       // w_up(q + down)
+        const float wlfr = lane_next(w1);               // w_left(q + right)
+        const float wrtl = lane_prev(w2);               // w_right(q - right)
+        const float wdna = wdn_prev;                    // w_down(q - down)
+        if (r < H - 1) o = o - prox_phi(wupb * SG2 - wupb * sv, gam) * wupb;
+        if (c < W - 1) o = o - prox_phi(wlfr * snx - wlfr * sv, gam) * wlfr;
+        if (c > 0) o = o - prox_phi(wrtl * spv - wrtl * sv, gam) * wrtl;
+        if (r > 0) o = o - prox_phi(wdna * SG0 - wdna * sv, gam) * wdna;
+        wdn_prev = w3;
+        const float ov = (rin && cin) ? o : 0.f;
+        O0 = O1; O1 = O2; O2 = ov;
       }
+    }
+    // ---- stage 4: S^T and the epilogue at row y = t-3
+    const int y = t - 3;
+    float tl = 0.f, tg = 0.f;
+    if constexpr (GLR) {
+      float v = tL.u * L2;
+      v += tL.l * lane_next(L1); v += tL.c * L1; v += tL.r * lane_prev(L1); v += tL.d * L0;
+      tl = v;
+    }
+    if constexpr (GTV != GTV_NONE) {
+      float v = tG.u * O2;
+      v += tG.l * lane_next(O1); v += tG.c * O1; v += tG.r * lane_prev(O1); v += tG.d * O0;
+      tg = v;
+    }
+    const float th = has_half ? 0.25f * S.th : 0.f;
+    float res, xn = 0.f, u = 0.f;
+    if constexpr (EPI == EPI_HALF) {
+      res = 0.f;                                        // mu * S_L^T l + ro * S_G^T o (REF:666-675)
+      if constexpr (GLR) res = tl * sc_l;
+      if constexpr (GTV != GTV_NONE) res = GLR ? res + tg * sc_g : tg * sc_g;
+      xn = res;
+    } else if constexpr (EPI == EPI_RHS) {
+      res = S.ey + tg * sc_g;                           // (y + ro0 C^T phi(C x)) + ro1 U(t)
+      if (has_half) res = res + th * sc_h;
+      xn = res;
+    } else {
+      float ax = X0;                                    // A x = ((x + mu0 L x) + ro0 G x) + U(t)
+      if constexpr (GLR) ax = ax + tl * sc_l;
+      if constexpr (GTV != GTV_NONE) ax = ax + tg * sc_g;
+      if (has_half) ax = ax + th;
+      u = S.eb - ax;                                    // residual
+      if (use_beta) u = u + beta * S.eu;                // heavy-ball direction (REF:789)
+      xn = X0 + alpha * u;                              // x_{k+1}
+      res = a.skip ? sk0 * S.ey + sk1 * xn : xn;        // block skip (REF:987)
+    }
+    if (y >= r0 && y < r1) {
+      if (owner) {
+        bstore(res, rout, vo, y * W);
+        if (want_u) bstore(u, ruo, vo, y * W);
+      }
+      if (want_xd && (y & 1)) {
+        // D of x_{k+1} (pre-skip): 2x2 block = rows y-1, y x columns c, c+1
+        const float pn = lane_next(xn_prev), cn = lane_next(xn);
+        const float d = 0.25f * xn_prev + 0.25f * pn + 0.25f * xn + 0.25f * cn;
+        if (owner && (c & 1) == 0 && c + 1 < W) bstore(d, rxd, vo_half, (y >> 1) * hw);
+      }
+    }
+    xn_prev = xn;
+  };
+
+  const int ts = r0 - 3, te = r1 + 3;
+  RowLoads A, B;
+  issue(ts, A);
+  issue(ts + 1, B);
+  for (int t = ts; t < te; t += 2) {
+    consume(t, A);
+    if (t + 2 < te) issue(t + 2, A);
+    if (t + 1 < te) {
+      consume(t + 1, B);
+      if (t + 3 < te) issue(t + 3, B);
     }
   }
-  __syncthreads();
-  // ---- pass C: S^T and the epilogue, one 2x2 output block per thread
-  float outv[2][2];
-#pragma unroll
-  for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-    for (int dx = 0; dx < 2; ++dx) {
-      const int oy = 2 * by + dy, ox = 2 * bx + dx;
-      const int li = (oy + 1) * LS + ox + 1;
-      float tl = 0.f, tg = 0.f;
-      if constexpr (GLR) tl = stencil_t(tL, Ls, li, LS);
-      if constexpr (GTV != GTV_NONE) tg = stencil_t(tG, Gs, li, LS);
-      const float xv = Xs[(oy + 3) * XS + ox + 3];
-      float r;
-      if constexpr (EPI == EPI_HALF) {
-        // mu * S_L^T l + ro * S_G^T o   (REF:666-675)
-        r = 0.f;
-        if constexpr (GLR) r = tl * sc_l;
-        if constexpr (GTV != GTV_NONE) r = GLR ? r + tg * sc_g : tg * sc_g;
-      } else if constexpr (EPI == EPI_RHS) {
-        // (y + ro0 * C^T phi(C x)) + ro1 * U(t_half)   (REF:744-749 / :776-781)
-        r = ey[dy][dx] + tg * sc_g;
-        if (has_half) r = r + th * sc_h;
-      } else {
-        // A x = ((x + mu0 L0 x) + ro0 G0 x) + U(t_half)   (REF:648-680)
-        float ax = xv;
-        if constexpr (GLR) ax = ax + tl * sc_l;
-        if constexpr (GTV != GTV_NONE) ax = ax + tg * sc_g;
-        if (has_half) ax = ax + th;
-        float u = eb[dy][dx] - ax;                    // residual b - A x
-        if (use_beta) u = u + beta * eu[dy][dx];      // heavy-ball direction (REF:789)
-        eu[dy][dx] = u;
-        r = xv + alpha * u;                           // x_{k+1}
-      }
-      outv[dy][dx] = r;
-    }
-  // D of the (pre-skip) result for the next stage's half level
-  if (a.xd_out && gy0 + 1 < H && gx0 + 1 < W) {
-    const float d = 0.25f * outv[0][0] + 0.25f * outv[0][1] + 0.25f * outv[1][0] + 0.25f * outv[1][1];
-    a.xd_out[((int64_t)b * C + ch) * hh * hw + (int64_t)(gy0 >> 1) * hw + (gx0 >> 1)] = d;
-  }
-#pragma unroll
-  for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-    for (int dx = 0; dx < 2; ++dx) {
-      const int gy = gy0 + dy, gx = gx0 + dx;
-      if (gy < H && gx < W) {
-        const int64_t o = plane + (int64_t)gy * W + gx;
-        float r = outv[dy][dx];
-        if (EPI == EPI_STEP) {
-          if (a.u_out) a.u_out[o] = eu[dy][dx];
-          if (a.skip) r = sk0 * ey[dy][dx] + sk1 * r;   // REF:987
-        }
-        a.out[o] = r;
-      }
-    }
 }
 
 template <bool GLR, int GTV, int EPI>
 static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* name) {
   OpArgs a = a0;
-  a.tiles_x = (a.W + TILE - 1) / TILE;
-  a.tiles_y = (a.H + TILE - 1) / TILE;
-  const uint64_t n = (uint64_t)B * a.G * a.F * a.tiles_x * a.tiles_y;
-  GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
-  a.nblk = (uint32_t)n;
+  a.nstrips = (a.W + SVALID - 1) / SVALID;
+  a.nsegs = (a.H + SSEG - 1) / SSEG;
+  const uint64_t units = (uint64_t)B * a.G * a.F * a.nsegs * a.nstrips;
+  GRR_REQUIRE(units < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
+  GRR_REQUIRE((int64_t)a.H * a.W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "%s: plane too large", name);
+  a.nunits = (uint32_t)units;
+  a.nblk = (uint32_t)((units + 3) / 4);
   hipLaunchKernelGGL((graph_op_kernel<GLR, GTV, EPI>), dim3(a.nblk), dim3(NT), 0, s, a);
   return launch_status(name);
 }
