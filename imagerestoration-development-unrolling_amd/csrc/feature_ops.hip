@@ -25,7 +25,7 @@ enum { EP_STORE = 0, EP_SKIP = 1 };
 struct GemmArgs {
   const float* x;      // activations [B, K, P]  (im2col: [B, Cin, H, W])
   const float* wt;     // [M, K]
-  const float* ln_sd;  // LD_LN: [B, P] sqrt(var + eps)
+  const float* ln_sd;  // LD_LN: [B, P] 1 / sqrt(var + eps)
   const float* ln_w;   // LD_LN: [K]
   const float* res;    // EP_SKIP: [B, M, P]
   const float* skip;   // EP_SKIP: [2]
@@ -42,8 +42,11 @@ struct GemmArgs {
 // current one feeds the matrix cores (v_mfma_f32_32x32x2_f32, 4 accumulators/wave).
 template <int LOADER, int EPI, bool VEC>
 __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
-  __shared__ float As[2][BK][APAD];
-  __shared__ float Bs[2][BK][BPAD];
+  // one LDS image: double-buffered A / B staging during the K loop, reused by the epilogue
+  __shared__ __attribute__((aligned(16))) float smem[2 * BK * APAD + 2 * BK * BPAD + 512];
+  auto As = reinterpret_cast<float(*)[BK][APAD]>(smem);
+  auto Bs = reinterpret_cast<float(*)[BK][BPAD]>(smem + 2 * BK * APAD);
+  float* lnw = smem + 2 * BK * APAD + 2 * BK * BPAD;   // LD_LN: CustomLayerNorm scale, K <= 512
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
@@ -60,14 +63,6 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
   const int am = tid >> 1, ak = (tid & 1) * 8;
   const int bk = tid >> 4, bn = (tid & 15) * 8;
   float ra[8], rb[8];
-  float sd[8];
-  if constexpr (LOADER == LD_LN) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int64_t n = n0 + bn + q;
-      sd[q] = n < P ? a.ln_sd[(int64_t)b * P + n] : 1.f;
-    }
-  }
   auto load_chunk = [&](int k0) {
     const int mm = m0 + am;
     if (VEC && mm < M && k0 + ak + 8 <= K) {
@@ -81,6 +76,12 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
         const int k = k0 + ak + q;
         ra[q] = (mm < M && k < K) ? a.wt[(int64_t)mm * K + k] : 0.f;
       }
+    }
+    if constexpr (LOADER == LD_LN) {
+      // CustomLayerNorm's per-channel scale folded into W1's columns (REF:925); the per-pixel
+      // 1/sigma is applied in the epilogue: W1 (g * x / sigma) = (W1 diag g) x / sigma
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ra[q] *= lnw[k0 + ak + q];
     }
     const int k = k0 + bk;
     if constexpr (LOADER == LD_IM2COL) {
@@ -108,11 +109,6 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
           rb[q] = (k < K && n < P) ? xb[(int64_t)k * P + n] : 0.f;
         }
       }
-      if constexpr (LOADER == LD_LN) {
-        const float g = k < K ? a.ln_w[k] : 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) rb[q] = (rb[q] / sd[q]) * g;   // REF:921-925
-      }
     }
   };
   auto store_chunk = [&](int buf) {
@@ -129,6 +125,10 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
   const int nchunks = (K + BK - 1) / BK;
+  if constexpr (LOADER == LD_LN) {
+    for (int k = tid; k < nchunks * BK; k += GT) lnw[k] = k < K ? a.ln_w[k] : 0.f;
+    __syncthreads();
+  }
   load_chunk(0);
   store_chunk(0);
   __syncthreads();
@@ -150,23 +150,61 @@ __global__ __launch_bounds__(GT) void gemm_f32_kernel(GemmArgs a) {
     if (c + 1 < nchunks) store_chunk(buf ^ 1);
     __syncthreads();
   }
+  // Epilogue: each 32x32 accumulator tile goes through a per-wave LDS slab (rows m, 32
+  // columns n, padded) and leaves as 16-byte row segments: 4 dwordx4 stores per lane
+  // instead of 16 dword stores (the store-issue rate, not HBM, bounds a scalar epilogue).
   float s0 = 0.f, s1 = 1.f;
   if constexpr (EPI == EP_SKIP) { s0 = a.skip[0]; s1 = a.skip[1]; }
+  constexpr int TP = 36;                                   // slab row pitch (floats)
+  float* slab = smem + wave * 32 * TP;                     // 4 x 4.5 KB, inside the A/B image
+  const int rr = lane >> 3, cq = (lane & 7) * 4;           // read-back: row group, 4-column chunk
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int64_t n = n0 + wn * 64 + j * 32 + (lane & 31);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M && n < P) {
-          const int64_t o = ((int64_t)b * M + m) * P + n;
-          float v = acc[i][j][r];
-          if constexpr (EPI == EP_SKIP) v = s0 * a.res[o] + s1 * v;          // REF:962-964
-          a.out[o] = v;
+      for (int r = 0; r < 16; ++r)
+        slab[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP + (lane & 31)] = acc[i][j][r];
+      __builtin_amdgcn_s_waitcnt(0xc07f);                   // lgkmcnt(0): this wave's slab writes
+      const int64_t nb = n0 + wn * 64 + j * 32 + cq;
+      float cs[4] = {1.f, 1.f, 1.f, 1.f};
+      if constexpr (LOADER == LD_LN) {                     // 1/sigma per pixel column (REF:921-922)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cs[q] = nb + q < P ? a.ln_sd[(int64_t)b * P + nb + q] : 0.f;
+      }
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+        const int row = pass * 8 + rr;
+        const int m = m0 + wm * 64 + i * 32 + row;
+        const float4 v4 = *reinterpret_cast<const float4*>(&slab[row * TP + cq]);
+        float v[4] = {v4.x, v4.y, v4.z, v4.w};
+        if (m < M) {
+          const int64_t o = ((int64_t)b * M + m) * P + nb;
+          if (VEC && nb + 4 <= P) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if constexpr (LOADER == LD_LN) v[q] *= cs[q];
+            }
+            if constexpr (EPI == EP_SKIP) {
+              const float4 r4 = *reinterpret_cast<const float4*>(a.res + o);
+              v[0] = s0 * r4.x + s1 * v[0]; v[1] = s0 * r4.y + s1 * v[1];
+              v[2] = s0 * r4.z + s1 * v[2]; v[3] = s0 * r4.w + s1 * v[3];   // REF:962-964
+            }
+            *reinterpret_cast<float4*>(a.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (nb + q < P) {
+                float w = v[q];
+                if constexpr (LOADER == LD_LN) w *= cs[q];
+                if constexpr (EPI == EP_SKIP) w = s0 * a.res[o + q] + s1 * w;
+                a.out[o + q] = w;
+              }
+            }
+          }
         }
       }
+      __builtin_amdgcn_s_waitcnt(0xc07f);                   // slab reads done before reuse
     }
 }
 
@@ -186,7 +224,7 @@ static grr_status launch_gemm(GemmArgs a, int B, hipStream_t s, const char* name
   return launch_status(name);
 }
 
-// CustomLayerNorm statistics: sd[b,p] = sqrt(var_c x[b,c,p] + 1e-5), unbiased (REF:919-922)
+// CustomLayerNorm statistics: sd[b,p] = 1/sqrt(var_c x[b,c,p] + 1e-5), unbiased (REF:919-922)
 __global__ void ln_stats_kernel(const float* __restrict__ x, float* __restrict__ sd, int B, int C, int64_t P) {
   const int64_t n = (int64_t)B * P;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -200,7 +238,7 @@ __global__ void ln_stats_kernel(const float* __restrict__ x, float* __restrict__
       const float d = xp[(int64_t)c * P] - mean;
       q += d * d;
     }
-    sd[i] = sqrtf(q / (float)(C - 1) + 1e-5f);
+    sd[i] = 1.0f / sqrtf(q / (float)(C - 1) + 1e-5f);
   }
 }
 
@@ -293,19 +331,26 @@ __global__ __launch_bounds__(FT) void lnb_tail_kernel(LnbTailArgs a) {
   const int y0 = ty * FTR, x0 = tx * FTC;
   const float* hb = a.h + (int64_t)b * 2 * hid * HW;
 
+  // per-thread staging slots: element i = tid + j*FT of the chunk's [2*KC][6x34] halo image;
+  // its plane / clamped pixel offset does not depend on the chunk, only the channel base does
   float st[FLD];
-  auto load_chunk = [&](int k0) {
+  int soff[FLD];   // pixel offset + (value plane ? hid*HW : 0) + kk*HW
+  int skk[FLD];    // channel within the chunk (for the hid bound)
 #pragma unroll
-    for (int j = 0; j < FLD; ++j) {
-      const int i = tid + j * FT;
-      const int ii = i < FSTAGE ? i : FSTAGE - 1;
-      const int plane = ii / FHA, r = ii - plane * FHA;      // plane: [0,KC) mask, [KC,2KC) value
-      const int kk = plane < FKC ? plane : plane - FKC;
-      const int ch = (plane < FKC ? 0 : hid) + k0 + kk;
-      const int ry = r / FHC, rx = r - ry * FHC;
-      const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 1 + rx, 0, W - 1);
-      st[j] = (k0 + kk < hid) ? hb[(int64_t)ch * HW + (int64_t)gy * W + gx] : 0.f;
-    }
+  for (int j = 0; j < FLD; ++j) {
+    const int i = tid + j * FT;
+    const int ii = i < FSTAGE ? i : FSTAGE - 1;
+    const int plane = ii / FHA, r = ii - plane * FHA;      // plane: [0,KC) mask, [KC,2KC) value
+    const int kk = plane < FKC ? plane : plane - FKC;
+    const int ry = r / FHC, rx = r - ry * FHC;
+    const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 1 + rx, 0, W - 1);
+    soff[j] = (plane < FKC ? 0 : hid * (int)HW) + kk * (int)HW + gy * W + gx;
+    skk[j] = kk;
+  }
+  auto load_chunk = [&](int k0) {
+    const float* hk = hb + (int64_t)k0 * HW;
+#pragma unroll
+    for (int j = 0; j < FLD; ++j) st[j] = (k0 + skk[j] < hid) ? hk[soff[j]] : 0.f;
   };
   auto store_chunk = [&](int buf) {
 #pragma unroll

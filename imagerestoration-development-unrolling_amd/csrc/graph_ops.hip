@@ -17,6 +17,7 @@
 // half-level term).  Everything is memory-bound (≈3.5 flop/B), so the design goal is HBM
 // bytes: each launch reads each of its inputs once and writes each output once.
 #include <cstdarg>
+#include <type_traits>
 
 #include "grr_common.h"
 
@@ -271,18 +272,21 @@ __device__ __forceinline__ float lane_next(float v) {  // value of lane+1 (colum
   return r;
 }
 
-// plain global addressing: base pointer (uniform) + per-lane column offset (bytes) +
-// per-row offset (floats, uniform)
-struct rsrc_t {
-  const float* p;
-};
-__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t) { return rsrc_t{p}; }
-__device__ __forceinline__ float bload(rsrc_t r, int voff_bytes, int soff_floats) {
-  return r.p[soff_floats + (voff_bytes >> 2)];
+// Addressing: a wave-uniform row base (SGPRs) + a per-lane 32-bit byte offset, so the
+// compiler can use the global_load/store "saddr" form with no per-access 64-bit VALU math.
+__device__ __forceinline__ float gload(const float* row_base, uint32_t off_bytes) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(row_base) + off_bytes);
 }
-__device__ __forceinline__ void bstore(float v, rsrc_t r, int voff_bytes, int soff_floats) {
-  const_cast<float*>(r.p)[soff_floats + (voff_bytes >> 2)] = v;
+__device__ __forceinline__ void gstore(float* row_base, uint32_t off_bytes, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(row_base) + off_bytes) = v;
 }
+
+// Every pipeline iteration issues the same sequence of memory operations, so hipcc's
+// s_waitcnt bookkeeping stays exact across the loop and the loads issued two
+// iterations ahead remain in flight: absent operands are read from this small
+// device-resident line, and stores that must not land (halo lanes, pipeline-fill
+// rows, outputs the caller did not ask for) go to a per-lane slot of it.
+__device__ float g_grr_scratch[64];
 
 // loads consumed by one pipeline iteration t (issued two iterations earlier)
 struct RowLoads {
@@ -313,28 +317,33 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   const bool cin = c >= 0 && c < W;
   const bool owner = lane >= 3 && lane < 3 + SVALID && cin;
   const int r0 = seg * SSEG, r1 = min(r0 + SSEG, H);
-  const int vo = cc * 4, vo_half = (cc >> 1) * 4;
+  float* const scratch = g_grr_scratch;
+  const uint32_t vo = (uint32_t)cc * 4u, vo_half = (uint32_t)(cc >> 1) * 4u, vo_lane = (uint32_t)lane * 4u;
+  const bool owner_xd = owner && (c & 1) == 0 && c + 1 < W;                       // D(x) writer
 
   const int64_t plane = ((int64_t)b * C + ch) * HW;
   const int64_t hplane = ((int64_t)b * C + ch) * (int64_t)hh * hw;
-  const rsrc_t rx = make_rsrc(a.x + plane, HW);
   const bool has_half = EPI != EPI_HALF && a.t_half != nullptr;
   const bool use_beta = EPI == EPI_STEP && a.beta != nullptr && a.u_prev != nullptr;
   const bool need_y = (EPI == EPI_RHS) || (EPI == EPI_STEP && a.skip != nullptr);
   const bool want_u = EPI == EPI_STEP && a.u_out != nullptr;
   const bool want_xd = a.xd_out != nullptr;
-  // descriptors of absent operands get 0 records (never read: their loads are compiled out
-  // or guarded by the same uniform flags)
   const int np = GTV == GTV_PROX ? 4 : 2;
-  const rsrc_t rwl = make_rsrc(GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : a.x, GLR ? 4 * HW : 0);
-  const rsrc_t rwg = make_rsrc(GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : a.x, GTV ? np * HW : 0);
-  const rsrc_t rb = make_rsrc(EPI == EPI_STEP ? a.b + plane : a.x, EPI == EPI_STEP ? HW : 0);
-  const rsrc_t ru = make_rsrc(use_beta ? a.u_prev + plane : a.x, use_beta ? HW : 0);
-  const rsrc_t ry = make_rsrc(need_y ? a.y + plane : a.x, need_y ? HW : 0);
-  const rsrc_t rth = make_rsrc(has_half ? a.t_half + hplane : a.x, has_half ? (int64_t)hh * hw : 0);
-  const rsrc_t rout = make_rsrc(a.out + plane, HW);
-  const rsrc_t ruo = make_rsrc(want_u ? a.u_out + plane : a.out, want_u ? HW : 0);
-  const rsrc_t rxd = make_rsrc(want_xd ? a.xd_out + hplane : a.out, want_xd ? (int64_t)hh * hw : 0);
+  // plane bases (uniform); absent operands point at the scratch line with row stride 0
+  const float* px = a.x + plane;
+  const float* pwl = GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
+  const float* pwg = GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : nullptr;
+  const float* pb = EPI == EPI_STEP ? a.b + plane : scratch;
+  const float* pu = use_beta ? a.u_prev + plane : scratch;
+  const float* py = need_y ? a.y + plane : scratch;
+  const float* pth = has_half ? a.t_half + hplane : scratch;
+  float* pout = a.out + plane;
+  float* puo = want_u ? a.u_out + plane : scratch;
+  float* pxd = want_xd ? a.xd_out + hplane : scratch;
+  const int ws_b = EPI == EPI_STEP ? W : 0, ws_u = use_beta ? W : 0, ws_y = need_y ? W : 0;
+  const int ws_th = has_half ? hw : 0, ws_uo = want_u ? W : 0, ws_xd = want_xd ? hw : 0;
+  const uint32_t vo_b = EPI == EPI_STEP ? vo : vo_lane, vo_u = use_beta ? vo : vo_lane;
+  const uint32_t vo_y = need_y ? vo : vo_lane, vo_th = has_half ? vo_half : vo_lane;
 
   float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
   if (a.log_l) sc_l = expf(a.log_l[g]);
@@ -346,31 +355,36 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
     if (use_beta) beta = a.beta[g];
     if (a.skip) { sk0 = a.skip[0]; sk1 = a.skip[1]; }
   }
+  const bool use_skip = EPI == EPI_STEP && a.skip != nullptr;
   Taps tL{}, tG{};
   if constexpr (GLR) tL = make_taps(a.sL, ch);
   if constexpr (GTV != GTV_NONE) tG = make_taps(a.sG, ch);
 
   auto issue = [&](int t, RowLoads& S) {
-    S.x = bload(rx, vo, clampi(t, 0, H - 1) * W);
+    S.x = gload(px + clampi(t, 0, H - 1) * W, vo);
     const int rw = clampi(t - 2, 0, H - 1) * W;
     if constexpr (GLR) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) S.wl[e] = bload(rwl, vo, (int)(e * HW) + rw);
+      for (int e = 0; e < 4; ++e) S.wl[e] = gload(pwl + e * HW + rw, vo);
     }
     if constexpr (GTV == GTV_PAIR) {
-      S.wg[0] = bload(rwg, vo, rw);
-      S.wg[1] = bload(rwg, vo, (int)HW + rw);
+      S.wg[0] = gload(pwg + rw, vo);
+      S.wg[1] = gload(pwg + HW + rw, vo);
     }
     if constexpr (GTV == GTV_PROX) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) S.wg[e] = bload(rwg, vo, (int)(e * HW) + rw);
-      S.wup = bload(rwg, vo, clampi(t - 1, 0, H - 1) * W);
+      for (int e = 0; e < 4; ++e) S.wg[e] = gload(pwg + e * HW + rw, vo);
+      S.wup = gload(pwg + clampi(t - 1, 0, H - 1) * W, vo);
     }
     const int re = clampi(t - 3, 0, H - 1);
-    if (EPI == EPI_STEP) S.eb = bload(rb, vo, re * W);
-    if (use_beta) S.eu = bload(ru, vo, re * W);
-    if (need_y) S.ey = bload(ry, vo, re * W);
-    if (has_half) S.th = bload(rth, vo_half, (re >> 1) * hw);
+    if constexpr (EPI == EPI_STEP) {
+      S.eb = gload(pb + re * ws_b, vo_b);
+      S.eu = gload(pu + re * ws_u, vo_u);
+    }
+    if constexpr (EPI != EPI_HALF) {
+      S.ey = gload(py + re * ws_y, vo_y);
+      S.th = gload(pth + (re >> 1) * ws_th, vo_th);
+    }
   };
 
   // pipeline registers (rows relative to the current iteration t)
@@ -381,7 +395,10 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   float O0 = 0.f, O1 = 0.f, O2 = 0.f;             // o rows t-4 .. t-2
   float cv_prev = 0.f, wdn_prev = 0.f, xn_prev = 0.f;
 
-  auto consume = [&](int t, const RowLoads& S) {
+  // ODD_Y: output row y = t-3 is odd in this body (segments start at even rows), so the
+  // 2x2 pool of rows (y-1, y) is completed here.
+  auto consume = [&](int t, const RowLoads& S, auto odd_tag) {
+    constexpr bool ODD_Y = decltype(odd_tag)::value;
     // ---- stage 1: input row t
     X0 = X1; X1 = X2; X2 = X3; X3 = S.x;
     // ---- stage 2: s at row t-1 (replicate: X rows are clamped loads)
@@ -419,8 +436,8 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
         const float chl = c > 0 ? chp : 0.f;
         const float cvu = r > 0 ? cv_prev : 0.f;
         const float sv = SG1;
-        const float o = S.wg[0] * (sv - lane_next(SG1)) + chl * (sv - lane_prev(SG1)) +
-                        S.wg[1] * (sv - SG2) + cvu * (sv - SG0);
+        const float snx = lane_next(SG1), spv = lane_prev(SG1);
+        const float o = S.wg[0] * (sv - snx) + chl * (sv - spv) + S.wg[1] * (sv - SG2) + cvu * (sv - SG0);
         cv_prev = S.wg[1];
         const float ov = (rin && cin) ? o : 0.f;
         O0 = O1; O1 = O2; O2 = ov;
@@ -442,10 +459,14 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
         const float wlfr = lane_next(w1);               // w_left(q + right)
         const float wrtl = lane_prev(w2);               // w_right(q - right)
         const float wdna = wdn_prev;                    // w_down(q - down)
-        if (r < H - 1) o = o - prox_phi(wupb * SG2 - wupb * sv, gam) * wupb;
-        if (c < W - 1) o = o - prox_phi(wlfr * snx - wlfr * sv, gam) * wlfr;
-        if (c > 0) o = o - prox_phi(wrtl * spv - wrtl * sv, gam) * wrtl;
-        if (r > 0) o = o - prox_phi(wdna * SG0 - wdna * sv, gam) * wdna;
+        const float o1 = o - prox_phi(wupb * SG2 - wupb * sv, gam) * wupb;
+        o = r < H - 1 ? o1 : o;
+        const float o2 = o - prox_phi(wlfr * snx - wlfr * sv, gam) * wlfr;
+        o = c < W - 1 ? o2 : o;
+        const float o3 = o - prox_phi(wrtl * spv - wrtl * sv, gam) * wrtl;
+        o = c > 0 ? o3 : o;
+        const float o4 = o - prox_phi(wdna * SG0 - wdna * sv, gam) * wdna;
+        o = r > 0 ? o4 : o;
         wdn_prev = w3;
         const float ov = (rin && cin) ? o : 0.f;
         O0 = O1; O1 = O2; O2 = ov;
@@ -455,16 +476,18 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
     const int y = t - 3;
     float tl = 0.f, tg = 0.f;
     if constexpr (GLR) {
+      const float ln = lane_next(L1), lp = lane_prev(L1);
       float v = tL.u * L2;
-      v += tL.l * lane_next(L1); v += tL.c * L1; v += tL.r * lane_prev(L1); v += tL.d * L0;
+      v += tL.l * ln; v += tL.c * L1; v += tL.r * lp; v += tL.d * L0;
       tl = v;
     }
     if constexpr (GTV != GTV_NONE) {
+      const float on = lane_next(O1), op = lane_prev(O1);
       float v = tG.u * O2;
-      v += tG.l * lane_next(O1); v += tG.c * O1; v += tG.r * lane_prev(O1); v += tG.d * O0;
+      v += tG.l * on; v += tG.c * O1; v += tG.r * op; v += tG.d * O0;
       tg = v;
     }
-    const float th = has_half ? 0.25f * S.th : 0.f;
+    const float th = 0.25f * S.th;
     float res, xn = 0.f, u = 0.f;
     if constexpr (EPI == EPI_HALF) {
       res = 0.f;                                        // mu * S_L^T l + ro * S_G^T o (REF:666-675)
@@ -483,34 +506,36 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
       u = S.eb - ax;                                    // residual
       if (use_beta) u = u + beta * S.eu;                // heavy-ball direction (REF:789)
       xn = X0 + alpha * u;                              // x_{k+1}
-      res = a.skip ? sk0 * S.ey + sk1 * xn : xn;        // block skip (REF:987)
+      res = use_skip ? sk0 * S.ey + sk1 * xn : xn;      // block skip (REF:987)
     }
-    if (y >= r0 && y < r1) {
-      if (owner) {
-        bstore(res, rout, vo, y * W);
-        if (want_u) bstore(u, ruo, vo, y * W);
-      }
-      if (want_xd && (y & 1)) {
-        // D of x_{k+1} (pre-skip): 2x2 block = rows y-1, y x columns c, c+1
-        const float pn = lane_next(xn_prev), cn = lane_next(xn);
-        const float d = 0.25f * xn_prev + 0.25f * pn + 0.25f * xn + 0.25f * cn;
-        if (owner && (c & 1) == 0 && c + 1 < W) bstore(d, rxd, vo_half, (y >> 1) * hw);
-      }
+    // stores: same sequence every iteration; fill rows / halo lanes land in the scratch line
+    const bool yv = y >= r0 && y < r1;
+    const int yr = yv ? y : 0;
+    if (owner) gstore(yv ? pout + yr * W : scratch, yv ? vo : vo_lane, res);
+    if constexpr (EPI == EPI_STEP) {
+      if (owner) gstore(yv ? puo + yr * ws_uo : scratch, yv ? (want_u ? vo : vo_lane) : vo_lane, u);
+    }
+    if constexpr (ODD_Y) {
+      // D of the (pre-skip) result: 2x2 block = rows y-1, y x columns c, c+1
+      const float pn = lane_next(xn_prev), cn = lane_next(xn);
+      const float d = 0.25f * xn_prev + 0.25f * pn + 0.25f * xn + 0.25f * cn;
+      if (owner_xd) gstore(yv ? pxd + (yr >> 1) * ws_xd : scratch, yv ? (want_xd ? vo_half : vo_lane) : vo_lane, d);
     }
     xn_prev = xn;
   };
 
-  const int ts = r0 - 3, te = r1 + 3;
+  // ts = r0 - 3 is odd (r0 even): body A handles even y, body B odd y.  The trip count is
+  // padded to even; the extra row only writes to the scratch line.
+  const int ts = r0 - 3;
+  const int te = ts + ((r1 + 3 - ts + 1) & ~1);
   RowLoads A, B;
   issue(ts, A);
   issue(ts + 1, B);
   for (int t = ts; t < te; t += 2) {
-    consume(t, A);
-    if (t + 2 < te) issue(t + 2, A);
-    if (t + 1 < te) {
-      consume(t + 1, B);
-      if (t + 3 < te) issue(t + 3, B);
-    }
+    consume(t, A, std::false_type{});
+    issue(t + 2, A);
+    consume(t + 1, B, std::true_type{});
+    issue(t + 3, B);
   }
 }
 
