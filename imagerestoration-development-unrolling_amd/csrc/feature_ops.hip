@@ -294,21 +294,34 @@ __global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ 
 // LocalNonLinearBlock tail, fused: out = skip0*x + skip1 * W2 . gate(dw3x3(h))
 // (REF:943-948, :962-964).  A workgroup owns a 4x32 pixel tile and ALL M <= 128 output
 // channels (wave w: pixels 32w..32w+31 of the tile, MT 32-row MFMA tiles).  The hidden
-// channels are walked in chunks of KC: the mask / value planes of the chunk are staged
-// with a 1-pixel replicate halo (double-buffered, next chunk's loads in flight), the
-// depthwise 3x3 and the gate are evaluated into the MFMA B image, and the chunk's W2
-// columns are applied on the matrix cores.  The gated activations never reach HBM.
+// channels are walked in chunks of FKC.  Each chunk's operands -- the mask / value planes
+// with a 1-pixel halo, and the chunk's packed W2 columns + depthwise taps (lnb_pack_kernel)
+// -- are fetched by LDS-DMA (global_load_lds) into a 3-slot ring, two chunks ahead of their
+// use; a chunk is consumed after a counted s_waitcnt vmcnt + raw s_barrier.  The depthwise
+// 3x3 and the gate are evaluated from the ring into the MFMA B image; the gated activations
+// never reach HBM.
+//
+// V4 (W % 4 == 0): a halo plane is 6 rows x 10 float4 (columns x0-4 .. x0+35), ONE 16-byte
+// DMA wave-instruction; replicate padding at the left / right image edge is applied when the
+// 3x3 window is read.  Otherwise a plane is 204 dwords (columns x0-1 .. x0+32, clamped at
+// load time), four 4-byte DMA wave-instructions.
+#ifndef GRR_TAIL_EXP
+#define GRR_TAIL_EXP 0   // ablation builds only (scripts/build_ablation.sh); 0 = the product kernel
+#endif
 constexpr int FT = 256;             // threads
 constexpr int FTR = 4, FTC = 32;    // pixel tile rows x cols (128 pixels)
 constexpr int FKC = 8;              // hidden channels per chunk
-constexpr int FHR = FTR + 2, FHC = FTC + 2, FHA = FHR * FHC;   // halo tile 6 x 34
-constexpr int FSTAGE = 2 * FKC * FHA;                          // mask + value halo tiles per chunk
-constexpr int FLD = (FSTAGE + FT - 1) / FT;                    // staging loads per thread (13)
+constexpr int FPL = 256;            // LDS pitch of one halo plane
+constexpr int FNS = 3;              // ring slots (two chunks in flight + the one being consumed)
+constexpr int FBP = FTR * FTC + 4;  // pitch of the gated-activation image Bs[FKC][FBP]
+constexpr int FTAPS = 2 * FKC * 9;  // depthwise taps per chunk: mask [kk][9], value [kk][9]
+// packed per-chunk auxiliaries: W2^T [kk][MT*32] (zero padded), then the taps
+__host__ __device__ constexpr int lnb_aux_instr(int mt) { return (mt * 32 * FKC + FTAPS + 1023) / 1024; }
+__host__ __device__ constexpr int lnb_aux_floats(int mt) { return lnb_aux_instr(mt) * 1024; }
 
 struct LnbTailArgs {
   const float* h;      // [B, 2hid, H, W]
-  const float* wdw;    // [2hid, 9]
-  const float* w2;     // [M, hid]
+  const float* aux;    // [nchunks][lnb_aux_floats(MT)]
   const float* x;      // [B, M, H, W] residual
   const float* skip;   // [2]
   float* out;          // [B, M, H, W]
@@ -316,12 +329,50 @@ struct LnbTailArgs {
   uint32_t nblk;
 };
 
-template <int MT>
+// Pack W2 [M, hid] and the depthwise taps [2hid, 9] chunk-major for 16-byte LDS-DMA.
+__global__ void lnb_pack_kernel(const float* __restrict__ w2, const float* __restrict__ wdw,
+                                float* __restrict__ aux, int M, int hid, int mpad, int auxf, int nchunks) {
+  const int n = nchunks * auxf;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c = i / auxf, e = i - c * auxf;
+    float v = 0.f;
+    if (e < FKC * mpad) {
+      const int kk = e / mpad, m = e - kk * mpad, k = c * FKC + kk;
+      if (m < M && k < hid) v = w2[(int64_t)m * hid + k];
+    } else if (e < FKC * mpad + FTAPS) {
+      const int t = e - FKC * mpad, half = t / (FKC * 9), r = t - half * FKC * 9;
+      const int kk = r / 9, k = c * FKC + kk;
+      if (k < hid) v = wdw[((half ? hid : 0) + k) * 9 + (r - kk * 9)];
+    }
+    aux[i] = v;
+  }
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// One LDS-DMA per lane: LDS[wave_base + BYTES*lane] = *(base + byte_off), `base` wave-uniform
+// (SGPRs), byte_off a per-lane 32-bit offset.
+template <int BYTES>
+__device__ __forceinline__ void dma(const float* base, uint32_t byte_off, float* lds_wave_base) {
+  const float* src = (const float*)((const char*)base + byte_off);
+  if constexpr (BYTES == 16) __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+  else __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 4, 0, 0);
+}
+
+template <int MT, bool V4>
 __global__ __launch_bounds__(FT) void lnb_tail_kernel(LnbTailArgs a) {
-  __shared__ float Hs[2][FSTAGE];
-  __shared__ float Bs[FKC][FTR * FTC + 4];
-  __shared__ float As[FKC][MT * 32 + 2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int HPI = V4 ? 1 : 4;                    // DMA instructions per halo plane
+  constexpr int HP = V4 ? 40 : FTC + 2;              // halo row pitch (floats)
+  constexpr int HX = V4 ? 3 : 0;                     // halo column of x = x0 - 1
+  constexpr int AUXI = lnb_aux_instr(MT);            // 16-byte aux instructions per wave
+  constexpr int AUXF = lnb_aux_floats(MT);
+  constexpr int SLOT = 2 * FKC * FPL + AUXF;
+  constexpr int PER_CHUNK = 4 * HPI + AUXI;          // VMEM ops per wave per chunk
+  // a single LDS array (a second __shared__ object can make hipcc drain vmcnt at ds_reads)
+  __shared__ __attribute__((aligned(16))) float smem[FNS * SLOT + FKC * FBP];
+  float* Bs = smem + FNS * SLOT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
   const int tx = lb % a.tiles_x; lb /= a.tiles_x;
   const int ty = lb % a.tiles_y;
@@ -331,106 +382,151 @@ __global__ __launch_bounds__(FT) void lnb_tail_kernel(LnbTailArgs a) {
   const int y0 = ty * FTR, x0 = tx * FTC;
   const float* hb = a.h + (int64_t)b * 2 * hid * HW;
 
-  // per-thread staging slots: element i = tid + j*FT of the chunk's [2*KC][6x34] halo image;
-  // its plane / clamped pixel offset does not depend on the chunk, only the channel base does
-  float st[FLD];
-  int soff[FLD];   // pixel offset + (value plane ? hid*HW : 0) + kk*HW
-  int skk[FLD];    // channel within the chunk (for the hid bound)
+  // per-lane byte offsets of this tile's halo elements inside a plane (fixed for the kernel)
+  uint32_t hofs[HPI];
+  if constexpr (V4) {
+    const int l = min(lane, 59), ry = l / 10, c4 = l - ry * 10;
+    const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 4 + 4 * c4, 0, W - 4);
+    hofs[0] = (uint32_t)(gy * W + gx) * 4u;
+  } else {
 #pragma unroll
-  for (int j = 0; j < FLD; ++j) {
-    const int i = tid + j * FT;
-    const int ii = i < FSTAGE ? i : FSTAGE - 1;
-    const int plane = ii / FHA, r = ii - plane * FHA;      // plane: [0,KC) mask, [KC,2KC) value
-    const int kk = plane < FKC ? plane : plane - FKC;
-    const int ry = r / FHC, rx = r - ry * FHC;
-    const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 1 + rx, 0, W - 1);
-    soff[j] = (plane < FKC ? 0 : hid * (int)HW) + kk * (int)HW + gy * W + gx;
-    skk[j] = kk;
-  }
-  auto load_chunk = [&](int k0) {
-    const float* hk = hb + (int64_t)k0 * HW;
-#pragma unroll
-    for (int j = 0; j < FLD; ++j) st[j] = (k0 + skk[j] < hid) ? hk[soff[j]] : 0.f;
-  };
-  auto store_chunk = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < FLD; ++j) {
-      const int i = tid + j * FT;
-      if (i < FSTAGE) Hs[buf][i] = st[j];
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(64 * i + lane, 6 * HP - 1);
+      const int ry = r / HP, rx = r - ry * HP;
+      const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 1 + rx, 0, W - 1);
+      hofs[i] = (uint32_t)(gy * W + gx) * 4u;
     }
+  }
+  const uint32_t aofs = (uint32_t)lane * 16u;
+
+  auto issue = [&](int c) {
+    const int k0 = c * FKC;
+    float* slot = smem + (c % FNS) * SLOT;
+#if GRR_TAIL_EXP >= 6
+    // timing-only: channel-blocked h ([chunk][H][W][16]); 6 rows x 40 px x 16 ch contiguous per row
+    if constexpr (V4) {
+#pragma unroll
+      for (int pi = 0; pi < 4; ++pi) {
+        const int L = (wave * 4 + pi) * 64 + lane;
+        const int row = min(L / 160, 5), within = L % 160;
+        const int gy = clampi(y0 - 1 + row, 0, H - 1);
+        const uint32_t off = (uint32_t)((gy * W + max(x0 - 4, 0)) * 16 + within * 4) * 4u;
+        dma<16>(hb + (int64_t)c * 16 * HW, off, slot + (wave * 4 + pi) * FPL);
+      }
+    }
+    if (0)
+#endif
+#pragma unroll
+    for (int pi = 0; pi < 4; ++pi) {
+      const int pl = wave * 4 + pi;                    // plane 0..15: [0,8) mask, [8,16) value
+      const int ch = (pl < FKC ? 0 : hid) + min(k0 + (pl & (FKC - 1)), hid - 1);   // k >= hid: gate zeroed
+      const float* base = hb + (int64_t)ch * HW;
+#pragma unroll
+      for (int i = 0; i < HPI; ++i) dma<V4 ? 16 : 4>(base, hofs[i], slot + pl * FPL + 64 * i);
+    }
+    const float* abase = a.aux + (int64_t)c * AUXF;
+#pragma unroll
+    for (int i = 0; i < AUXI; ++i)
+      dma<16>(abase + (i * 4 + wave) * 256, aofs, slot + 2 * FKC * FPL + (i * 4 + wave) * 256);
   };
 
   f32x16 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x16{};
   const int nchunks = (hid + FKC - 1) / FKC;
-  load_chunk(0);
-  store_chunk(0);
-  __syncthreads();
+  issue(0);
+  if (nchunks > 1) issue(1);
+  // gate mapping: thread = (channel kk = tid / 32, column px), computing the 4-pixel column
+  // strip px of the tile, so the 6 halo rows it reads are shared by its 4 outputs
+  const int gk = tid >> 5, px = tid & 31;
+  // window columns of x-1, x, x+1 (replicate padding at the image edges for V4)
+  const int cm = HX + px;
+  const int cl = (V4 && x0 + px == 0) ? cm + 1 : cm;
+  const int cr = (V4 && x0 + px + 1 >= W) ? cm + 1 : cm + 2;
   for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1, k0 = c * FKC;
-    if (c + 1 < nchunks) load_chunk(k0 + FKC);
-    // W2 columns of this chunk -> As[k][m]
-    for (int i = tid; i < FKC * MT * 32; i += FT) {
-      const int kk = i / (MT * 32), m = i - kk * (MT * 32);
-      As[kk][m] = (m < M && k0 + kk < hid) ? a.w2[(int64_t)m * hid + k0 + kk] : 0.f;
-    }
-    // depthwise 3x3 (replicate pad) + gate: 8 channels x 128 pixels, 4 per thread.
-    // The channel of each pass is wave-uniform (readfirstlane), so the taps are scalar loads.
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    const int p = tid & (FTR * FTC - 1);
-    const int py = p / FTC, px = p - py * FTC;
+    const int k0 = c * FKC;
+    const float* slot = smem + (c % FNS) * SLOT;
+    // chunk c landed (this wave's DMAs), then every wave's (barrier)
+    if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER_CHUNK) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#if GRR_TAIL_EXP != 3 && GRR_TAIL_EXP != 5
+    if (c + 2 < nchunks) issue(c + 2);                 // slot (c+2)%3 was last read in chunk c-1
+#endif
+    const float* wsl = slot + 2 * FKC * FPL;
+    {
+      // depthwise 3x3 (REF:946) on mask and value planes + gate sigmoid(m)*m*v (REF:947)
+      const float* taps = wsl + FKC * MT * 32;
+      const float* mt = slot + gk * FPL;
+      const float* vt = slot + (FKC + gk) * FPL;
+      float km[9], kv[9];
 #pragma unroll
-    for (int q = 0; q < (FKC * FTR * FTC) / FT; ++q) {
-      const int kk = (wave_u >> 1) + 2 * q;
-      const int k = k0 + kk;
-      float g = 0.f;
-      if (k < hid) {
-        const float* mt = &Hs[buf][kk * FHA];
-        const float* vt = &Hs[buf][(FKC + kk) * FHA];
-        const float* km = a.wdw + k * 9;
-        const float* kv = a.wdw + (hid + k) * 9;
+      for (int i = 0; i < 9; ++i) {
+        km[i] = taps[gk * 9 + i];
+        kv[i] = taps[FKC * 9 + gk * 9 + i];
+      }
+      float mr[FTR + 2][3], vr[FTR + 2][3];
+#pragma unroll
+      for (int r = 0; r < FTR + 2; ++r) {
+        mr[r][0] = mt[r * HP + cl]; mr[r][1] = mt[r * HP + cm + 1]; mr[r][2] = mt[r * HP + cr];
+        vr[r][0] = vt[r * HP + cl]; vr[r][1] = vt[r * HP + cm + 1]; vr[r][2] = vt[r * HP + cr];
+      }
+      const bool live = k0 + gk < hid;
+#pragma unroll
+      for (int py = 0; py < FTR; ++py) {
         float m = 0.f, v = 0.f;
+#if GRR_TAIL_EXP == 1 || GRR_TAIL_EXP == 4 || GRR_TAIL_EXP == 5 || GRR_TAIL_EXP == 6
+        m = mr[py][1]; v = vr[py][1];
+#else
 #pragma unroll
         for (int ay = 0; ay < 3; ++ay)
 #pragma unroll
           for (int ax = 0; ax < 3; ++ax) {
-            const int li = (py + ay) * FHC + px + ax;
-            m += km[ay * 3 + ax] * mt[li];
-            v += kv[ay * 3 + ax] * vt[li];
+            m += km[ay * 3 + ax] * mr[py + ay][ax];
+            v += kv[ay * 3 + ax] * vr[py + ay][ax];
           }
-        const float sg = 1.0f / (1.0f + expf(-m));
-        g = (sg * m) * v;
+#endif
+        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
+        Bs[gk * FBP + py * FTC + px] = live ? (sg * m) * v : 0.f;
       }
-      Bs[kk][p] = g;
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#if GRR_TAIL_EXP == 2 || GRR_TAIL_EXP == 4 || GRR_TAIL_EXP == 5 || GRR_TAIL_EXP == 6
+    if (c >= 0) continue;
+#endif
 #pragma unroll
     for (int kk = 0; kk < FKC; kk += 2) {
       const int kr = kk + (lane >> 5);
-      const float bv = Bs[kr][wave * 32 + (lane & 31)];
+      const float bv = Bs[kr * FBP + wave * 32 + (lane & 31)];
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        const float av = As[kr][t * 32 + (lane & 31)];
+        const float av = wsl[kr * (MT * 32) + t * 32 + (lane & 31)];
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
       }
     }
-    if (c + 1 < nchunks) store_chunk(buf ^ 1);
-    __syncthreads();
   }
   const float s0 = a.skip[0], s1 = a.skip[1];
-  const int p = wave * 32 + (lane & 31);
-  const int gy = y0 + p / FTC, gx = x0 + (p % FTC);
-  if (gy < H && gx < W) {
+  const int pp = wave * 32 + (lane & 31);
+  const int gy = y0 + pp / FTC, gx = x0 + (pp % FTC);
+  const bool pix = gy < H && gx < W;
+  const int64_t pofs = (int64_t)b * M * HW + (int64_t)min(gy, H - 1) * W + min(gx, W - 1);
+  // residual loads first, all in flight together (clamped addresses), then one wait
+  float xv[MT][16];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = min(t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), M - 1);
+      xv[t][r] = a.x[pofs + (int64_t)m * HW];
+    }
+  if (pix) {
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M) {
-          const int64_t o = ((int64_t)b * M + m) * HW + (int64_t)gy * W + gx;
-          a.out[o] = s0 * a.x[o] + s1 * acc[t][r];      // REF:962-964
-        }
+        if (m < M) a.out[pofs + (int64_t)m * HW] = s0 * xv[t][r] + s1 * acc[t][r];   // REF:962-964
       }
   }
 }
@@ -444,6 +540,18 @@ __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __res
     const int64_t b = r / ((int64_t)G * Cin);
     out[i] = img[(b * Cin + c) * P + p];
   }
+}
+
+static int64_t lnb_aux_offset(int B, int hid, int H, int W) {
+  const int64_t P = (int64_t)H * W;
+  const int64_t sd = ((int64_t)B * P + 63) / 64 * 64;
+  return (sd + (int64_t)B * 2 * hid * P + 63) / 64 * 64;   // floats; 256-byte aligned
+}
+
+template <int MT>
+static void launch_tail(const LnbTailArgs& t, bool v4, hipStream_t s) {
+  if (v4) hipLaunchKernelGGL((lnb_tail_kernel<MT, true>), dim3(t.nblk), dim3(FT), 0, s, t);
+  else hipLaunchKernelGGL((lnb_tail_kernel<MT, false>), dim3(t.nblk), dim3(FT), 0, s, t);
 }
 
 }  // namespace grr
@@ -473,10 +581,10 @@ grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int
 }
 
 int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
-  (void)C;
-  const int64_t P = (int64_t)H * W;
-  const int64_t sd = ((int64_t)B * P + 63) / 64 * 64;
-  return (sd + (int64_t)B * 2 * hid * P) * (int64_t)sizeof(float);
+  const int nchunks = (hid + FKC - 1) / FKC;
+  const int mt = (C + 31) / 32;
+  return (lnb_aux_offset(B, hid, H, W) + (int64_t)nchunks * lnb_aux_floats(mt < 1 ? 1 : mt)) *
+         (int64_t)sizeof(float);
 }
 
 grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
@@ -487,15 +595,26 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
                   W > 0,
               GRR_ERR_INVALID_ARG, "grr_lnb_forward: bad args");
   GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward: out aliases x");
+  GRR_REQUIRE(C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 128", C);
+  GRR_REQUIRE(((uintptr_t)workspace & 15) == 0, GRR_ERR_INVALID_ARG, "grr_lnb_forward: workspace not 16-B aligned");
+  GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: plane too large");
   hipStream_t s = (hipStream_t)stream;
   const int64_t P = (int64_t)H * W;
   float* sd = (float*)workspace;
   float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;   // [B, 2hid, P]
+  float* aux = sd + lnb_aux_offset(B, hid, H, W);
+  const int mt = (C + 31) / 32;
+  const int nchunks = (hid + FKC - 1) / FKC;
   {
     const int64_t n = (int64_t)B * P;
     const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
     hipLaunchKernelGGL(ln_stats_kernel, dim3(blocks), dim3(256), 0, s, x, sd, B, C, P);
     grr_status st = launch_status("grr_lnb_forward/ln_stats");
+    if (st != GRR_OK) return st;
+    const int na = nchunks * lnb_aux_floats(mt);
+    hipLaunchKernelGGL(lnb_pack_kernel, dim3((na + 255) / 256), dim3(256), 0, s, w2, wdw, aux, C, hid, mt * 32,
+                       lnb_aux_floats(mt), nchunks);
+    st = launch_status("grr_lnb_forward/pack");
     if (st != GRR_OK) return st;
   }
   {
@@ -504,20 +623,19 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
     grr_status st = launch_gemm<LD_LN, EP_STORE>(a, B, s, "grr_lnb_forward/gemm1");
     if (st != GRR_OK) return st;
   }
-  GRR_REQUIRE(C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 128", C);
   LnbTailArgs t{};
-  t.h = hbuf; t.wdw = wdw; t.w2 = w2; t.x = x; t.skip = skip; t.out = out;
+  t.h = hbuf; t.aux = aux; t.x = x; t.skip = skip; t.out = out;
   t.hid = hid; t.M = C; t.H = H; t.W = W;
   t.tiles_x = (W + FTC - 1) / FTC;
   t.tiles_y = (H + FTR - 1) / FTR;
   const uint64_t n = (uint64_t)B * t.tiles_x * t.tiles_y;
   GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
   t.nblk = (uint32_t)n;
-  const int mt = (C + 31) / 32;
-  if (mt == 1) hipLaunchKernelGGL((lnb_tail_kernel<1>), dim3(t.nblk), dim3(FT), 0, s, t);
-  else if (mt == 2) hipLaunchKernelGGL((lnb_tail_kernel<2>), dim3(t.nblk), dim3(FT), 0, s, t);
-  else if (mt == 3) hipLaunchKernelGGL((lnb_tail_kernel<3>), dim3(t.nblk), dim3(FT), 0, s, t);
-  else hipLaunchKernelGGL((lnb_tail_kernel<4>), dim3(t.nblk), dim3(FT), 0, s, t);
+  const bool v4 = (W % 4 == 0) && W >= 4;
+  if (mt == 1) launch_tail<1>(t, v4, s);
+  else if (mt == 2) launch_tail<2>(t, v4, s);
+  else if (mt == 3) launch_tail<3>(t, v4, s);
+  else launch_tail<4>(t, v4, s);
   return launch_status("grr_lnb_forward/tail");
 }
 

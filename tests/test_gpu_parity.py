@@ -175,7 +175,10 @@ def test_conv2x2s2(irdu, bkmhw):
     assert_close(irdu.kernels.conv2x2s2(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt, stride=2), 1e-5)
 
 
-@pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 40, 36)])
+# (C, hid, H, W): full/partial 4x32 tiles, W % 4 == 0 (16-byte halo DMA) and not (dword DMA),
+# hid % 8 != 0 (partial last chunk), C up to 128 (4 MFMA row tiles), W = 4 (both edges in one float4)
+@pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 40, 36), (33, 20, 9, 44), (24, 64, 13, 30),
+                                 (128, 24, 8, 68), (6, 16, 5, 4)])
 def test_local_nonlinear_block(irdu, chw):
     c, hid, h, w = chw
     torch.manual_seed(0)
