@@ -42,6 +42,7 @@ L = c_int64
 SIGNATURES = {
     "grr_version": [],
     "grr_last_error": [],
+    "grr_set_kernel_variant": [I],
     "grr_neighbor_table": [P, I, I, P],
     "grr_edge_weights": [P, L, P, P, P, I, I, I, I, I, P],
     "grr_gtv_pair_weights": [P, P, I, I, I, I, P],

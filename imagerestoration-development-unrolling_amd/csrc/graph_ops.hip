@@ -24,6 +24,7 @@
 namespace grr {
 
 static thread_local std::string g_err;
+static int g_kernel_variant = 0;   // grr_set_kernel_variant: 0 auto, 1 strip kernels only
 
 void set_error(const char* fmt, ...) {
   char buf[512];
@@ -286,7 +287,7 @@ __device__ __forceinline__ void gstore(float* row_base, uint32_t off_bytes, floa
 // iterations ahead remain in flight: absent operands are read from this small
 // device-resident line, and stores that must not land (halo lanes, pipeline-fill
 // rows, outputs the caller did not ask for) go to a per-lane slot of it.
-__device__ float g_grr_scratch[64];
+__device__ __attribute__((aligned(16))) float g_grr_scratch[256];   // 64 lanes x up to 16 B
 
 // loads consumed by one pipeline iteration t (issued two iterations earlier)
 struct RowLoads {
@@ -539,8 +540,373 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-wave variant (W <= 64 V, W % V == 0): one wave = one (b, channel) plane, one
+// segment of SSEG output rows and ALL W columns; lane l holds columns V l .. V l + V-1.
+// Same 4-stage register pipeline as graph_op_kernel, but no halo columns: every row
+// operand is one coalesced V*256-byte wave-load (global_load_dwordx4 for V = 4) and
+// horizontal neighbours are in-lane except a lane's first / last column (one DPP
+// shift per row array and direction).  Image-edge columns apply the operators'
+// boundary rules explicitly (replicate for S, zero outside for S^T / C^T C).
+// ---------------------------------------------------------------------------
+template <int V> struct VecT;
+template <> struct VecT<1> { typedef float type; };
+template <> struct VecT<2> { typedef float __attribute__((ext_vector_type(2))) type; };
+template <> struct VecT<4> { typedef float __attribute__((ext_vector_type(4))) type; };
+
+template <int N>
+__device__ __forceinline__ void vload(float (&d)[N], const float* row_base, uint32_t off_bytes) {
+  typedef typename VecT<N>::type T;
+  const T t = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(row_base) + off_bytes);
+  if constexpr (N == 1) {
+    d[0] = t;
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) d[j] = t[j];
+  }
+}
+template <int N>
+__device__ __forceinline__ void vstore(float* row_base, uint32_t off_bytes, const float (&v)[N]) {
+  typedef typename VecT<N>::type T;
+  T t;
+  if constexpr (N == 1) {
+    t = v[0];
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) t[j] = v[j];
+  }
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(row_base) + off_bytes) = t;
+}
+
+template <int V>
+struct RowLoadsV {
+  float x[V];          // x row t
+  float wl[4][V];      // GLR edge weights, row t-2
+  float wg[4][V];      // GTV pair (2) or raw (4) weights, row t-2
+  float wup[V];        // prox: w_up at row t-1
+  float eb[V], eu[V], ey[V];
+  float th[(V + 1) / 2];   // half-resolution operand at row (t-3)/2
+};
+
+template <bool GLR, int GTV, int EPI, int V>
+__global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
+  constexpr int NH = (V + 1) / 2;    // half-resolution values per lane
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * 4 + wave;
+  if (unit >= a.nunits) return;   // whole wave (uniform)
+  const int F = a.F;
+  const int f = unit % F; unit /= F;
+  const int seg = unit % a.nsegs; unit /= a.nsegs;
+  const int g = unit % a.G;
+  const int b = unit / a.G;
+  const int H = a.H, W = a.W, C = a.G * F, ch = g * F + f;
+  const int hh = H / 2, hw = W / 2;
+  const int64_t HW = (int64_t)H * W;
+  const int c0 = V * lane;                       // first column of this lane
+  const bool lane_on = c0 < W;                   // W % V == 0: a lane is all-in or all-out
+  const int cl0 = lane_on ? c0 : W - V;          // clamped (loads of idle lanes duplicate)
+  const int r0 = seg * SSEG, r1 = min(r0 + SSEG, H);
+  float* const scratch = g_grr_scratch;
+  const uint32_t vo = (uint32_t)cl0 * 4u, vo_lane = (uint32_t)lane * 4u * V;
+  // half-resolution column(s) of this lane: V=4 -> 2l, 2l+1; V=2 -> l; V=1 -> l/2
+  const uint32_t vo_half = (uint32_t)(V == 1 ? (cl0 >> 1) : (cl0 >> 1)) * 4u;
+  const bool owner_xd = lane_on && (V > 1 || ((c0 & 1) == 0 && c0 + 1 < W));
+
+  const int64_t plane = ((int64_t)b * C + ch) * HW;
+  const int64_t hplane = ((int64_t)b * C + ch) * (int64_t)hh * hw;
+  const bool has_half = EPI != EPI_HALF && a.t_half != nullptr;
+  const bool use_beta = EPI == EPI_STEP && a.beta != nullptr && a.u_prev != nullptr;
+  const bool need_y = (EPI == EPI_RHS) || (EPI == EPI_STEP && a.skip != nullptr);
+  const bool want_u = EPI == EPI_STEP && a.u_out != nullptr;
+  const bool want_xd = a.xd_out != nullptr;
+  const int np = GTV == GTV_PROX ? 4 : 2;
+  const float* px = a.x + plane;
+  const float* pwl = GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
+  const float* pwg = GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : nullptr;
+  const float* pb = EPI == EPI_STEP ? a.b + plane : scratch;
+  const float* pu = use_beta ? a.u_prev + plane : scratch;
+  const float* py = need_y ? a.y + plane : scratch;
+  const float* pth = has_half ? a.t_half + hplane : scratch;
+  float* pout = a.out + plane;
+  float* puo = want_u ? a.u_out + plane : scratch;
+  float* pxd = want_xd ? a.xd_out + hplane : scratch;
+  const int ws_b = EPI == EPI_STEP ? W : 0, ws_u = use_beta ? W : 0, ws_y = need_y ? W : 0;
+  const int ws_th = has_half ? hw : 0, ws_uo = want_u ? W : 0, ws_xd = want_xd ? hw : 0;
+  const uint32_t vo_b = EPI == EPI_STEP ? vo : vo_lane, vo_u = use_beta ? vo : vo_lane;
+  const uint32_t vo_y = need_y ? vo : vo_lane, vo_th = has_half ? vo_half : vo_lane;
+
+  float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
+  if (a.log_l) sc_l = expf(a.log_l[g]);
+  if (a.log_g) sc_g = expf(a.log_g[g]);
+  if (a.log_half) sc_h = expf(a.log_half[g]);
+  if constexpr (GTV == GTV_PROX) gam = expf(a.log_gamma[g]);
+  if constexpr (EPI == EPI_STEP) {
+    alpha = a.alpha[g];
+    if (use_beta) beta = a.beta[g];
+    if (a.skip) { sk0 = a.skip[0]; sk1 = a.skip[1]; }
+  }
+  const bool use_skip = EPI == EPI_STEP && a.skip != nullptr;
+  Taps tL{}, tG{};
+  if constexpr (GLR) tL = make_taps(a.sL, ch);
+  if constexpr (GTV != GTV_NONE) tG = make_taps(a.sG, ch);
+
+  auto issue = [&](int t, RowLoadsV<V>& S) {
+    vload(S.x, px + clampi(t, 0, H - 1) * W, vo);
+    const int rw = clampi(t - 2, 0, H - 1) * W;
+    if constexpr (GLR) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vload(S.wl[e], pwl + e * HW + rw, vo);
+    }
+    if constexpr (GTV == GTV_PAIR) {
+      vload(S.wg[0], pwg + rw, vo);
+      vload(S.wg[1], pwg + HW + rw, vo);
+    }
+    if constexpr (GTV == GTV_PROX) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vload(S.wg[e], pwg + e * HW + rw, vo);
+      vload(S.wup, pwg + clampi(t - 1, 0, H - 1) * W, vo);
+    }
+    const int re = clampi(t - 3, 0, H - 1);
+    if constexpr (EPI == EPI_STEP) {
+      vload(S.eb, pb + re * ws_b, vo_b);
+      vload(S.eu, pu + re * ws_u, vo_u);
+    }
+    if constexpr (EPI != EPI_HALF) {
+      vload(S.ey, py + re * ws_y, vo_y);
+      vload(S.th, pth + (re >> 1) * ws_th, vo_th);
+    }
+  };
+
+  // pipeline registers, [V] per row (rows relative to the current iteration t)
+  float X0[V] = {}, X1[V] = {}, X2[V] = {}, X3[V] = {};
+  float SL0[V] = {}, SL1[V] = {}, SL2[V] = {};
+  float SG0[V] = {}, SG1[V] = {}, SG2[V] = {};
+  float L0[V] = {}, L1[V] = {}, L2[V] = {};
+  float O0[V] = {}, O1[V] = {}, O2[V] = {};
+  float cv_prev[V] = {}, wdn_prev[V] = {}, xn_prev[V] = {};
+
+  auto consume = [&](int t, const RowLoadsV<V>& S, auto odd_tag) {
+    constexpr bool ODD_Y = decltype(odd_tag)::value;
+#pragma unroll
+    for (int j = 0; j < V; ++j) { X0[j] = X1[j]; X1[j] = X2[j]; X2[j] = X3[j]; X3[j] = S.x[j]; }
+    // ---- stage 2: s at row t-1 (rows replicate-clamped by the loads, columns here)
+    {
+      const float xp = lane_prev(X2[V - 1]), xq = lane_next(X2[0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        const float xl = col > 0 ? (j > 0 ? X2[j - 1] : xp) : X2[j];
+        const float xr = col < W - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
+        if constexpr (GLR) {
+          float sv = tL.u * X1[j];
+          sv += tL.l * xl; sv += tL.c * X2[j]; sv += tL.r * xr; sv += tL.d * X3[j];
+          SL0[j] = SL1[j]; SL1[j] = SL2[j]; SL2[j] = sv;
+        }
+        if constexpr (GTV != GTV_NONE) {
+          float sv = tG.u * X1[j];
+          sv += tG.l * xl; sv += tG.c * X2[j]; sv += tG.r * xr; sv += tG.d * X3[j];
+          SG0[j] = SG1[j]; SG1[j] = SG2[j]; SG2[j] = sv;
+        }
+      }
+    }
+    // ---- stage 3: l and o at row r = t-2 (zero outside the image)
+    {
+      const int r = t - 2;
+      const bool rin = r >= 0 && r < H;
+      if constexpr (GLR) {
+        const float pv = lane_prev(SL1[V - 1]), nx = lane_next(SL1[0]);
+        float l[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int col = c0 + j;
+          const float up = r > 0 ? SL0[j] : SL1[j];
+          const float dn = r < H - 1 ? SL2[j] : SL1[j];
+          const float lf = col > 0 ? (j > 0 ? SL1[j - 1] : pv) : SL1[j];
+          const float rt = col < W - 1 ? (j < V - 1 ? SL1[j + 1] : nx) : SL1[j];
+          const float wx = ((S.wl[0][j] * up + S.wl[1][j] * lf) + S.wl[2][j] * rt) + S.wl[3][j] * dn;
+          l[j] = (rin && col < W) ? SL1[j] - wx : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) { L0[j] = L1[j]; L1[j] = L2[j]; L2[j] = l[j]; }
+      }
+      if constexpr (GTV == GTV_PAIR) {
+        const float sp = lane_prev(SG1[V - 1]), sn = lane_next(SG1[0]);
+        const float wp = lane_prev(S.wg[0][V - 1]);
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int col = c0 + j;
+          const float sv = SG1[j];
+          const float snx = j < V - 1 ? SG1[j + 1] : sn;     // x c_h = 0 at the last column
+          const float spv = j > 0 ? SG1[j - 1] : sp;
+          const float chl = col > 0 ? (j > 0 ? S.wg[0][j - 1] : wp) : 0.f;
+          const float cvu = r > 0 ? cv_prev[j] : 0.f;
+          const float ov = S.wg[0][j] * (sv - snx) + chl * (sv - spv) + S.wg[1][j] * (sv - SG2[j]) +
+                           cvu * (sv - SG0[j]);
+          o[j] = (rin && col < W) ? ov : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) { cv_prev[j] = S.wg[1][j]; O0[j] = O1[j]; O1[j] = O2[j]; O2[j] = o[j]; }
+      }
+      if constexpr (GTV == GTV_PROX) {
+        const float sp = lane_prev(SG1[V - 1]), sn = lane_next(SG1[0]);
+        const float w1n = lane_next(S.wg[1][0]), w2p = lane_prev(S.wg[2][V - 1]);
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int col = c0 + j;
+          const float sv = SG1[j];
+          const float su = r > 0 ? SG0[j] : sv, sd = r < H - 1 ? SG2[j] : sv;
+          const float spv = j > 0 ? SG1[j - 1] : sp, snx = j < V - 1 ? SG1[j + 1] : sn;
+          const float sl = col > 0 ? spv : sv, sr = col < W - 1 ? snx : sv;
+          const float w0 = S.wg[0][j], w1 = S.wg[1][j], w2 = S.wg[2][j], w3 = S.wg[3][j];
+          const float z0 = prox_phi(w0 * sv - w0 * su, gam) * w0;
+          const float z1 = prox_phi(w1 * sv - w1 * sl, gam) * w1;
+          const float z2 = prox_phi(w2 * sv - w2 * sr, gam) * w2;
+          const float z3 = prox_phi(w3 * sv - w3 * sd, gam) * w3;
+          float ov = ((z0 + z1) + z2) + z3;
+          const float wupb = S.wup[j];                                 // w_up(q + down)
+          const float wlfr = j < V - 1 ? S.wg[1][j + 1] : w1n;         // w_left(q + right)
+          const float wrtl = j > 0 ? S.wg[2][j - 1] : w2p;             // w_right(q - right)
+          const float wdna = wdn_prev[j];                              // w_down(q - down)
+          const float o1 = ov - prox_phi(wupb * SG2[j] - wupb * sv, gam) * wupb;
+          ov = r < H - 1 ? o1 : ov;
+          const float o2 = ov - prox_phi(wlfr * snx - wlfr * sv, gam) * wlfr;
+          ov = col < W - 1 ? o2 : ov;
+          const float o3 = ov - prox_phi(wrtl * spv - wrtl * sv, gam) * wrtl;
+          ov = col > 0 ? o3 : ov;
+          const float o4 = ov - prox_phi(wdna * SG0[j] - wdna * sv, gam) * wdna;
+          ov = r > 0 ? o4 : ov;
+          o[j] = (rin && col < W) ? ov : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) { wdn_prev[j] = S.wg[3][j]; O0[j] = O1[j]; O1[j] = O2[j]; O2[j] = o[j]; }
+      }
+    }
+    // ---- stage 4: S^T and the epilogue at row y = t-3 (neighbours outside are 0)
+    const int y = t - 3;
+    float tl[V] = {}, tg[V] = {};
+    if constexpr (GLR) {
+      const float lp = lane_prev(L1[V - 1]), ln = lane_next(L1[0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float nx = j < V - 1 ? L1[j + 1] : ln, pv = j > 0 ? L1[j - 1] : lp;
+        float v = tL.u * L2[j];
+        v += tL.l * nx; v += tL.c * L1[j]; v += tL.r * pv; v += tL.d * L0[j];
+        tl[j] = v;
+      }
+    }
+    if constexpr (GTV != GTV_NONE) {
+      const float op = lane_prev(O1[V - 1]), on = lane_next(O1[0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float nx = j < V - 1 ? O1[j + 1] : on, pv = j > 0 ? O1[j - 1] : op;
+        float v = tG.u * O2[j];
+        v += tG.l * nx; v += tG.c * O1[j]; v += tG.r * pv; v += tG.d * O0[j];
+        tg[j] = v;
+      }
+    }
+    float res[V], xn[V], u[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float th = 0.25f * S.th[V == 4 ? (j >> 1) : 0];
+      xn[j] = 0.f; u[j] = 0.f;
+      if constexpr (EPI == EPI_HALF) {
+        float rv = 0.f;                                   // mu * S_L^T l + ro * S_G^T o (REF:666-675)
+        if constexpr (GLR) rv = tl[j] * sc_l;
+        if constexpr (GTV != GTV_NONE) rv = GLR ? rv + tg[j] * sc_g : tg[j] * sc_g;
+        res[j] = rv; xn[j] = rv;
+      } else if constexpr (EPI == EPI_RHS) {
+        float rv = S.ey[j] + tg[j] * sc_g;                // (y + ro0 C^T phi(C x)) + ro1 U(t)
+        if (has_half) rv = rv + th * sc_h;
+        res[j] = rv; xn[j] = rv;
+      } else {
+        float ax = X0[j];                                 // A x = ((x + mu0 L x) + ro0 G x) + U(t)
+        if constexpr (GLR) ax = ax + tl[j] * sc_l;
+        if constexpr (GTV != GTV_NONE) ax = ax + tg[j] * sc_g;
+        if (has_half) ax = ax + th;
+        float uv = S.eb[j] - ax;                          // residual
+        if (use_beta) uv = uv + beta * S.eu[j];           // heavy-ball direction (REF:789)
+        u[j] = uv;
+        xn[j] = X0[j] + alpha * uv;                       // x_{k+1}
+        res[j] = use_skip ? sk0 * S.ey[j] + sk1 * xn[j] : xn[j];   // block skip (REF:987)
+      }
+    }
+    const bool yv = y >= r0 && y < r1;
+    const int yr = yv ? y : 0;
+    if (lane_on) vstore(yv ? pout + yr * W : scratch, yv ? vo : vo_lane, res);
+    if constexpr (EPI == EPI_STEP) {
+      if (lane_on) vstore(yv ? puo + yr * ws_uo : scratch, yv ? (want_u ? vo : vo_lane) : vo_lane, u);
+    }
+    if constexpr (ODD_Y) {
+      // D of the (pre-skip) result: 2x2 blocks of rows y-1, y
+      float d[NH];
+      if constexpr (V == 1) {
+        const float pn = lane_next(xn_prev[0]), cn = lane_next(xn[0]);
+        d[0] = 0.25f * xn_prev[0] + 0.25f * pn + 0.25f * xn[0] + 0.25f * cn;
+      } else {
+#pragma unroll
+        for (int k = 0; k < NH; ++k)
+          d[k] = 0.25f * xn_prev[2 * k] + 0.25f * xn_prev[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+      }
+      if (owner_xd)
+        vstore(yv ? pxd + (yr >> 1) * ws_xd : scratch, yv ? (want_xd ? vo_half : vo_lane) : vo_lane, d);
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) xn_prev[j] = xn[j];
+  };
+
+  const int ts = r0 - 3;
+  const int te = ts + ((r1 + 3 - ts + 1) & ~1);
+  RowLoadsV<V> A, B;
+  issue(ts, A);
+  issue(ts + 1, B);
+  for (int t = ts; t < te; t += 2) {
+    consume(t, A, std::false_type{});
+    issue(t + 2, A);
+    consume(t + 1, B, std::true_type{});
+    issue(t + 3, B);
+  }
+}
+
+// W <= 64 V with W % V == 0 -> row kernel with V columns per lane; otherwise 0 (strips)
+static int row_vec(int W) {
+  if (W <= 64) return 1;
+  if (W <= 128 && W % 2 == 0) return 2;
+  if (W <= 256 && W % 4 == 0) return 4;
+  return 0;
+}
+
+template <bool GLR, int GTV, int EPI, int V>
+static void launch_row(OpArgs a, int B, hipStream_t s) {
+  a.nsegs = (a.H + SSEG - 1) / SSEG;
+  const uint64_t units = (uint64_t)B * a.G * a.F * a.nsegs;
+  a.nunits = (uint32_t)units;
+  a.nblk = (uint32_t)((units + 3) / 4);
+  hipLaunchKernelGGL((graph_row_kernel<GLR, GTV, EPI, V>), dim3(a.nblk), dim3(NT), 0, s, a);
+}
+
 template <bool GLR, int GTV, int EPI>
 static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* name) {
+  GRR_REQUIRE((int64_t)a0.H * a0.W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "%s: plane too large", name);
+  GRR_REQUIRE((uint64_t)B * a0.G * a0.F * ((a0.H + SSEG - 1) / SSEG) * ((a0.W + SVALID - 1) / SVALID) <
+                  (1ull << 32) - 4,
+              GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
+  int vec = g_kernel_variant == 1 ? 0 : row_vec(a0.W);
+  if (vec > 1) {   // vector row loads need every operand base aligned to 4V bytes
+    const void* ptrs[] = {a0.x, a0.wL, a0.wG, a0.y, a0.b, a0.u_prev, a0.t_half, a0.out, a0.u_out, a0.xd_out};
+    for (const void* q : ptrs)
+      if ((uintptr_t)q % (4u * vec) != 0) vec = 0;
+    // half-resolution rows are read / written as V/2-float vectors
+    if (vec == 4 && (a0.t_half || a0.xd_out) && (((int64_t)(a0.H / 2) * (a0.W / 2)) % 2 != 0)) vec = 0;
+  }
+  switch (vec) {
+    case 1: launch_row<GLR, GTV, EPI, 1>(a0, B, s); return launch_status(name);
+    case 2: launch_row<GLR, GTV, EPI, 2>(a0, B, s); return launch_status(name);
+    case 4: launch_row<GLR, GTV, EPI, 4>(a0, B, s); return launch_status(name);
+    default: break;
+  }
   OpArgs a = a0;
   a.nstrips = (a.W + SVALID - 1) / SVALID;
   a.nsegs = (a.H + SSEG - 1) / SSEG;
@@ -562,6 +928,13 @@ using namespace grr;
 extern "C" {
 
 int grr_version(void) { return 1; }
+
+grr_status grr_set_kernel_variant(int variant) {
+  clear_error();
+  GRR_REQUIRE(variant == 0 || variant == 1, GRR_ERR_INVALID_ARG, "grr_set_kernel_variant: %d", variant);
+  g_kernel_variant = variant;
+  return GRR_OK;
+}
 const char* grr_last_error(void) { return g_err.c_str(); }
 
 grr_status grr_neighbor_table(int32_t* out, int H, int W, void* stream) {

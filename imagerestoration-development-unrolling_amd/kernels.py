@@ -101,6 +101,12 @@ NO_STENCIL = Stencil(None, None, None, None)
 
 
 # ---------------------------------------------------------------------------
+def set_kernel_variant(variant: str) -> None:
+    """Select the graph-operator kernels: "auto" (row waves for W <= 256) or "strips"
+    (column strips at every width).  Test / benchmark knob; process-wide."""
+    _native.call("grr_set_kernel_variant", {"auto": 0, "strips": 1}[variant])
+
+
 def neighbor_table(h: int, w: int, device) -> Tensor:
     out = torch.empty((4, h, w), dtype=torch.int32, device=device)
     call("grr_neighbor_table", out.data_ptr(), h, w, _stream(out.device))

@@ -39,6 +39,11 @@ typedef enum grr_status {
 int grr_version(void);
 const char* grr_last_error(void);
 
+/* Kernel-variant knob for tests and benchmarks (no reference counterpart): 0 = automatic
+ * (row-wave graph operators for W <= 256, column strips above), 1 = column-strip graph
+ * operators at every width.  Process-wide; results agree to fp32 rounding either way. */
+grr_status grr_set_kernel_variant(int variant);
+
 /* a1 — integer neighbour table (bit-exact target).  out[e*H*W + p] = flat index
  * of clamp(p + delta_e): the pixel the reference's replicate-padded gather reads
  * for edge e (REF:128-144, GLRFast.get_neighbors_pixels).  out: int32 [4,H,W]. */

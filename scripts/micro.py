@@ -22,7 +22,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--variant", default="auto", choices=["auto", "strips"])
     args = ap.parse_args()
+    K.set_kernel_variant(args.variant)
     dev = torch.device("cuda", 0)
     b, g, f, h, w = args.batch, 32, 3, args.size, args.size
     c = g * f

@@ -29,6 +29,15 @@ def irdu():
 DEV = "cuda"
 
 
+@pytest.fixture(params=["auto", "strips"])
+def variant(irdu, request):
+    """Run a test with the row-wave graph kernels (auto, W <= 256) and with the column-strip
+    kernels forced at every width."""
+    irdu.kernels.set_kernel_variant(request.param)
+    yield request.param
+    irdu.kernels.set_kernel_variant("auto")
+
+
 def rel_err(a, b):
     a = a.detach().double().cpu()
     b = torch.as_tensor(b).double().cpu()
@@ -121,8 +130,10 @@ def test_edge_weights_random(irdu, shape):
     assert_close(deg, od, 1e-5)
 
 
-@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 37, 45), (1, 3, 2, 9, 70)])
-def test_glr_gtv_operators_random(irdu, shape):
+# widths: <= 64 (1 column per lane), 70 (2), 200 / 256 (4), 130 (W % 4 != 0 -> strips)
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 37, 45), (1, 3, 2, 9, 70), (1, 2, 3, 12, 200),
+                                   (1, 1, 3, 10, 256), (1, 2, 3, 7, 130)])
+def test_glr_gtv_operators_random(irdu, variant, shape):
     b, g, f, h, w = shape
     x = rand(b, g, f, h, w, seed=2)
     wl = torch.softmax(rand(b, g, 4, h, w, seed=3), dim=2)
@@ -137,8 +148,8 @@ def test_glr_gtv_operators_random(irdu, shape):
         assert_close(gtv(x.to(DEV), wg.to(DEV)), O.gtv_apply(x, wg, kg))
 
 
-@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 21, 31)])
-def test_gtv_prox_rhs_half(irdu, shape):
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 21, 31), (1, 2, 3, 10, 100), (1, 2, 3, 13, 132)])
+def test_gtv_prox_rhs_half(irdu, variant, shape):
     """C^T phi(C x) with the soft-threshold phi of the proximal step (a12, a16)."""
     b, g, f, h, w = shape
     x = rand(b, g, f, h, w, seed=7)
@@ -196,7 +207,7 @@ def test_local_nonlinear_block(irdu, chw):
 # ---------------------------------------------------------------------------
 # full solver against the reference's golden vectors
 @pytest.mark.parametrize("name", ["mixture_v1.npz", "mixture_v1_rect.npz"])
-def test_mixture_golden(irdu, name):
+def test_mixture_golden(irdu, variant, name):
     d = load_golden(name)
     g = int(d["meta/n_graphs"])
     x = torch.from_numpy(d["in/x"])
@@ -240,8 +251,9 @@ def test_abstract_model_golden(irdu):
 
 # ---------------------------------------------------------------------------
 # S = 10 stages (the metric's configuration) against the oracle
-@pytest.mark.parametrize("case", [dict(g=4, b=2, h=32, w=32), dict(g=32, b=1, h=64, w=96)])
-def test_msgf_ten_stages_vs_oracle(irdu, case):
+@pytest.mark.parametrize("case", [dict(g=4, b=2, h=32, w=32), dict(g=32, b=1, h=64, w=96),
+                                  dict(g=4, b=1, h=24, w=256)])
+def test_msgf_ten_stages_vs_oracle(irdu, variant, case):
     g, b, h, w = case["g"], case["b"], case["h"], case["w"]
     torch.manual_seed(2204)
     m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=g, n_cgd_iters=10)
@@ -268,7 +280,7 @@ def test_lowpass_block_ten_stages_vs_oracle(irdu):
     assert_close(got, ref)
 
 
-def test_single_stage_and_odd_half_level(irdu):
+def test_single_stage_and_odd_half_level(irdu, variant):
     """S = 1 (the example.yaml plumbing config) and a half level with odd size (42x62 -> 21x31)."""
     torch.manual_seed(3)
     blk = irdu.LocalLowpassFilteringBlock(dim=12, nsubnets=1, ngraphs=4, n_cgd_iters=1)
