@@ -68,13 +68,20 @@ def build_model(device, seed=2204):
     return m.to(device).eval()
 
 
+# the kernel grr_system_step launches at the bench shape (W = 256: row waves, 4 columns per lane)
+STEP_KERNEL = "graph_row_kernel<true, 1, 2, 4>"
+
+
 def load_traffic():
-    """Per-launch HBM bytes of grr_system_step from the committed rocprofv3 PMC summary (or None)."""
+    """Per-launch HBM bytes of grr_system_step from the committed rocprofv3 PMC summary (or None
+    when the summary was collected on a different kernel)."""
     path = os.path.join(ROOT, "profiles", "traffic_system_step.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
+    if d.get("kernel") != STEP_KERNEL:
+        return None
     return d.get("hbm_bytes_per_launch")
 
 
@@ -165,7 +172,7 @@ def main():
     step = kern["system_step"]
     achieved = step["gbps"]
     traffic = load_traffic()
-    roofline = {"bound": "hbm", "kernel": "grr_system_step (graph_op_kernel<GLR,GTV_PAIR,EPI_STEP>)",
+    roofline = {"bound": "hbm", "kernel": f"grr_system_step ({STEP_KERNEL})",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "bytes_per_launch": step["bytes_per_launch"], "mean_launch_ms": round(step["mean_ms"], 4),

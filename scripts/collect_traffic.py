@@ -1,6 +1,6 @@
 """Turn rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of a bench run into per-launch HBM bytes.
 
-    python scripts/collect_traffic.py <fetch_dir> <write_dir> [--kernel graph_op_kernel<true, 1, 2>]
+    python scripts/collect_traffic.py <fetch_dir> <write_dir> [--kernel "graph_row_kernel<true, 1, 2, 4>"]
                                       [--out profiles/traffic_system_step.json]
 
 Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): on gfx950 FETCH_SIZE
@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--kernel", default="graph_op_kernel<true, 1, 2>")
+    ap.add_argument("--kernel", default="graph_row_kernel<true, 1, 2, 4>")
     ap.add_argument("--out", default="profiles/traffic_system_step.json")
     args = ap.parse_args()
     fetch = per_dispatch(args.fetch_dir, "FETCH_SIZE", args.kernel)
