@@ -531,6 +531,242 @@ __global__ __launch_bounds__(FT) void lnb_tail_kernel(LnbTailArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32-accurate 1x1 convolution on bf16 MFMA ("x3 split").
+//
+// Every fp32 operand is split EXACTLY into three bf16 terms, v = v0 + v1 + v2
+// (v0 = rne(v), v1 = rne(v - v0), v2 = v - v0 - v1: the 24 significand bits as 3 x 8),
+// and the six products above 2^-24 |a b| are accumulated in fp32 by
+// v_mfma_f32_32x32x16_bf16: a0b0 + a0b1 + a1b0 + a0b2 + a2b0 + a1b1 (the dropped
+// a1b2 + a2b1 + a2b2 are below fp32 rounding).  Six bf16 MFMAs cost 6 x 32 cycles per
+// 32x32x16 block against 8 x 64 for v_mfma_f32_32x32x2_f32: 2.7x the fp32 MFMA rate.
+//
+// out[b][m][p] = rstd(b,p) * sum_k A[m][k] x[b][k][p]   (rstd = 1 without LN)
+// With LN (CustomLayerNorm folded, REF:911-925): A = W1 . diag(ln_w) and
+// rstd = 1 / sqrt(var_unbiased_k(x[b][:][p]) + 1e-5), computed in-kernel from the
+// x column the wave already holds.
+//
+// Workgroup = 4 waves x 32 pixels; every wave keeps its pixels' K-column as split B
+// fragments in registers and walks ALL M rows in chunks of 64 (two 32-row MFMA
+// tiles).  A (pre-split, fragment order, lnb_x3_pack_kernel) streams through a 2-slot
+// LDS-DMA ring shared by the 4 waves.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t bf16_rne(float v) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_val(uint32_t h) { return __builtin_bit_cast(float, h << 16); }
+// exact 3-term split: returns the bf16 bit patterns of v0, v1, v2
+__device__ __forceinline__ void split3(float v, uint32_t& h0, uint32_t& h1, uint32_t& h2) {
+  h0 = bf16_rne(v);
+  const float r1 = v - bf16_val(h0);
+  h1 = bf16_rne(r1);
+  const float r2 = r1 - bf16_val(h1);
+  h2 = bf16_rne(r2);
+}
+
+#ifndef GRR_X3_TILES
+#define GRR_X3_TILES 2
+#endif
+constexpr int X3_NT = GRR_X3_TILES;  // 32-row MFMA tiles per chunk
+constexpr int X3_MCH = 32 * X3_NT;   // output rows per chunk
+
+// frag images per chunk: [tile t][k-step s][term q] x 64 lanes x 8 bf16 (1 KB each),
+// padded to a whole number of 16-byte DMA instructions per wave (4 waves)
+__host__ __device__ inline int x3_imgs(int KS) { return X3_NT * KS * 3; }
+__host__ __device__ inline int x3_niw(int KS) { return (x3_imgs(KS) + 3) / 4; }
+__host__ __device__ inline int64_t x3_chunk_bytes(int KS) { return (int64_t)x3_niw(KS) * 4 * 1024; }
+
+// A[m][k] = W[m][k] * (ln_w ? ln_w[k] : 1), split and laid out in fragment order
+__global__ void x3_pack_kernel(const float* __restrict__ w, const float* __restrict__ ln_w,
+                               uint16_t* __restrict__ frag, int M, int K, int KS, int nch) {
+  const int64_t per = x3_chunk_bytes(KS) / 2;        // bf16 per chunk image
+  const int64_t n = per * nch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i / per);
+    const int e = (int)(i - (int64_t)c * per);
+    const int img = e >> 9, lane = (e >> 3) & 63, j = e & 7;
+    uint16_t out = 0;
+    if (img < x3_imgs(KS)) {
+      const int q = img % 3, s = (img / 3) % KS, t = img / (3 * KS);
+      const int m = c * X3_MCH + t * 32 + (lane & 31), k = 16 * s + 8 * (lane >> 5) + j;
+      if (m < M && k < K) {
+        const float v = ln_w ? w[(int64_t)m * K + k] * ln_w[k] : w[(int64_t)m * K + k];
+        uint32_t h0, h1, h2;
+        split3(v, h0, h1, h2);
+        out = (uint16_t)(q == 0 ? h0 : q == 1 ? h1 : h2);
+      }
+    }
+    frag[i] = out;
+  }
+}
+
+struct X3Args {
+  const float* x;          // [B, K, P]
+  const uint16_t* frag;    // [nch][x3_chunk_bytes / 2]
+  float* out;              // [B, M, P]
+  int64_t P;
+  int K, M, nch, tiles;    // tiles: 128-pixel tiles per image
+  uint32_t nblk;
+};
+
+__device__ float g_x3_scratch[64];
+
+template <int KS, bool LN>
+__global__ __launch_bounds__(256) void gemm_x3_kernel(X3Args a) {
+  extern __shared__ __attribute__((aligned(16))) float x3_lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int b = lb / a.tiles, tile = lb - b * a.tiles;
+  const int64_t P = a.P;
+  const int K = a.K, M = a.M, r = lane & 31, hf = lane >> 5;
+  const int64_t p = (int64_t)tile * 128 + wave * 32 + r;
+  const bool pin = p < P;
+  const int64_t pc = pin ? p : P - 1;
+  const int NIW = x3_niw(KS);
+  const int64_t CB = x3_chunk_bytes(KS);
+  const int nch = a.nch;
+  const char* fragb = reinterpret_cast<const char*>(a.frag);
+
+  auto issue = [&](int c) {        // chunk c -> slot c & 1 (16-byte LDS-DMA, lane-linear)
+    float* slot = x3_lds + (c & 1) * (CB / 4);
+    const char* src = fragb + (int64_t)c * CB;
+    for (int i = 0; i < NIW; ++i) {
+      const int img = i * 4 + wave;
+      __builtin_amdgcn_global_load_lds((const void*)(src + img * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(slot + img * 256), 16, 0, 0);
+    }
+  };
+  issue(0);
+
+  // this lane's K column: k = 16 s + 8 hf + j
+  float xv[KS][8];
+  const float* xb = a.x + (int64_t)b * K * P + pc;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * hf + j;
+      xv[s][j] = k < K ? xb[(int64_t)k * P] : 0.f;
+    }
+  float rstd = 1.f;
+  if constexpr (LN) {                          // CustomLayerNorm statistics (REF:916-922)
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += xv[s][j];
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / (float)K;
+    float sq = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = 16 * s + 8 * hf + j < K ? xv[s][j] - mean : 0.f;
+        sq += d * d;
+      }
+    sq += __shfl_xor(sq, 32);
+    rstd = 1.0f / sqrtf(sq / (float)(K - 1) + 1e-5f);
+  }
+  bf16x8 bq[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint32_t h0, h1, h2;
+      split3(xv[s][j], h0, h1, h2);
+      bq[s][0][j] = __builtin_bit_cast(__bf16, (uint16_t)h0);
+      bq[s][1][j] = __builtin_bit_cast(__bf16, (uint16_t)h1);
+      bq[s][2][j] = __builtin_bit_cast(__bf16, (uint16_t)h2);
+    }
+
+  float* const obase = a.out + (int64_t)b * M * P;
+  // full tile: every lane's pixel in range -> stores through a uniform row base + 32-bit offset
+  const bool full_px = (int64_t)tile * 128 + 128 <= P;
+  const uint32_t so = (uint32_t)((4 * hf) * P + r) * 4u;
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed (this wave's DMAs; later ops: the previous chunk's stores), then all waves'
+    if (c == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(16 * X3_NT) : "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + 1 < nch) issue(c + 1);             // slot (c+1)&1 was last read in chunk c-1
+    const float* slot = x3_lds + (c & 1) * (CB / 4);
+    f32x16 acc[X3_NT];
+#pragma unroll
+    for (int t = 0; t < X3_NT; ++t) {
+      acc[t] = f32x16{};
+      const float* im = slot + (t * KS * 3) * 256 + lane * 4;
+      bf16x8 a0 = *reinterpret_cast<const bf16x8*>(im);
+      bf16x8 a1 = *reinterpret_cast<const bf16x8*>(im + 256);
+      bf16x8 a2 = *reinterpret_cast<const bf16x8*>(im + 512);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        // prefetch the next k-step's fragments behind this step's six MFMAs
+        bf16x8 n0 = a0, n1 = a1, n2 = a2;
+        if (s + 1 < KS) {
+          n0 = *reinterpret_cast<const bf16x8*>(im + (s + 1) * 768);
+          n1 = *reinterpret_cast<const bf16x8*>(im + (s + 1) * 768 + 256);
+          n2 = *reinterpret_cast<const bf16x8*>(im + (s + 1) * 768 + 512);
+        }
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[s][1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, bq[s][0], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[s][2], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[s][0], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[s][1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[s][0], acc[t], 0, 0, 0);
+        a0 = n0; a1 = n1; a2 = n2;
+      }
+    }
+    // epilogue: 16 stores per tile, every one issued (rows >= M / pixels >= P -> scratch)
+    if (full_px && (c + 1) * X3_MCH <= M) {
+#pragma unroll
+      for (int t = 0; t < X3_NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m0 = c * X3_MCH + t * 32 + (i & 3) + 8 * (i >> 2);
+          float* row = obase + (int64_t)m0 * P + (int64_t)tile * 128 + wave * 32;
+          *reinterpret_cast<float*>(reinterpret_cast<char*>(row) + so) = acc[t][i] * rstd;
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < X3_NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = c * X3_MCH + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          float* dst = (m < M && pin) ? obase + (int64_t)m * P + p : g_x3_scratch + lane;
+          *dst = acc[t][i] * rstd;
+        }
+    }
+  }
+}
+
+template <bool LN>
+static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
+                            hipStream_t s, const char* name) {
+  GRR_REQUIRE(K >= 1 && K <= 128, GRR_ERR_UNSUPPORTED, "%s: K=%d outside [1, 128]", name, K);
+  X3Args a{};
+  a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M;
+  a.nch = (M + X3_MCH - 1) / X3_MCH;
+  a.tiles = (int)((P + 127) / 128);
+  const uint64_t n = (uint64_t)B * a.tiles;
+  GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
+  a.nblk = (uint32_t)n;
+  const int KS = (K + 15) / 16;
+  const size_t lds = 2 * (size_t)x3_chunk_bytes(KS);
+  switch (KS) {
+#define GRR_X3_CASE(ks) \
+    case ks: hipLaunchKernelGGL((gemm_x3_kernel<ks, LN>), dim3(a.nblk), dim3(256), lds, s, a); break;
+    GRR_X3_CASE(1) GRR_X3_CASE(2) GRR_X3_CASE(3) GRR_X3_CASE(4)
+    GRR_X3_CASE(5) GRR_X3_CASE(6) GRR_X3_CASE(7) GRR_X3_CASE(8)
+#undef GRR_X3_CASE
+  }
+  return launch_status(name);
+}
+
 __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __restrict__ out, int Cin, int G,
                                      int64_t P, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -542,10 +778,15 @@ __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __res
   }
 }
 
+// LNB workspace (floats): [h: B*2hid*P][tail aux: nchunks*aux][W1 x3 fragments], 256-B aligned
 static int64_t lnb_aux_offset(int B, int hid, int H, int W) {
   const int64_t P = (int64_t)H * W;
-  const int64_t sd = ((int64_t)B * P + 63) / 64 * 64;
-  return (sd + (int64_t)B * 2 * hid * P + 63) / 64 * 64;   // floats; 256-byte aligned
+  return ((int64_t)B * 2 * hid * P + 63) / 64 * 64;
+}
+static int64_t lnb_frag_offset(int B, int C, int hid, int H, int W) {
+  const int nchunks = (hid + FKC - 1) / FKC;
+  const int mt = (C + 31) / 32;
+  return lnb_aux_offset(B, hid, H, W) + ((int64_t)nchunks * lnb_aux_floats(mt < 1 ? 1 : mt) + 63) / 64 * 64;
 }
 
 template <int MT>
@@ -581,10 +822,9 @@ grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int
 }
 
 int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
-  const int nchunks = (hid + FKC - 1) / FKC;
-  const int mt = (C + 31) / 32;
-  return (lnb_aux_offset(B, hid, H, W) + (int64_t)nchunks * lnb_aux_floats(mt < 1 ? 1 : mt)) *
-         (int64_t)sizeof(float);
+  const int KS = (C + 15) / 16;
+  const int nch = (2 * hid + X3_MCH - 1) / X3_MCH;
+  return lnb_frag_offset(B, C, hid, H, W) * (int64_t)sizeof(float) + (int64_t)nch * x3_chunk_bytes(KS);
 }
 
 grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
@@ -596,33 +836,32 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
               GRR_ERR_INVALID_ARG, "grr_lnb_forward: bad args");
   GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward: out aliases x");
   GRR_REQUIRE(C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 128", C);
-  GRR_REQUIRE(((uintptr_t)workspace & 15) == 0, GRR_ERR_INVALID_ARG, "grr_lnb_forward: workspace not 16-B aligned");
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_lnb_forward: workspace not 256-B aligned");
   GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: plane too large");
   hipStream_t s = (hipStream_t)stream;
   const int64_t P = (int64_t)H * W;
-  float* sd = (float*)workspace;
-  float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;   // [B, 2hid, P]
-  float* aux = sd + lnb_aux_offset(B, hid, H, W);
+  float* hbuf = (float*)workspace;                                     // [B, 2hid, P]
+  float* aux = hbuf + lnb_aux_offset(B, hid, H, W);
+  uint16_t* frag = (uint16_t*)(hbuf + lnb_frag_offset(B, C, hid, H, W));
   const int mt = (C + 31) / 32;
   const int nchunks = (hid + FKC - 1) / FKC;
   {
-    const int64_t n = (int64_t)B * P;
-    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
-    hipLaunchKernelGGL(ln_stats_kernel, dim3(blocks), dim3(256), 0, s, x, sd, B, C, P);
-    grr_status st = launch_status("grr_lnb_forward/ln_stats");
-    if (st != GRR_OK) return st;
+    // weights: tail W2 / taps chunks, and W1 . diag(ln_w) split for the x3 GEMM
     const int na = nchunks * lnb_aux_floats(mt);
     hipLaunchKernelGGL(lnb_pack_kernel, dim3((na + 255) / 256), dim3(256), 0, s, w2, wdw, aux, C, hid, mt * 32,
                        lnb_aux_floats(mt), nchunks);
-    st = launch_status("grr_lnb_forward/pack");
+    grr_status st = launch_status("grr_lnb_forward/pack");
+    if (st != GRR_OK) return st;
+    const int KS = (C + 15) / 16, nch = (2 * hid + X3_MCH - 1) / X3_MCH;
+    const int64_t nf = (int64_t)nch * x3_chunk_bytes(KS) / 2;
+    hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 1 << 16)), dim3(256), 0, s,
+                       w1, ln_w, frag, 2 * hid, C, KS, nch);
+    st = launch_status("grr_lnb_forward/pack_w1");
     if (st != GRR_OK) return st;
   }
-  {
-    GemmArgs a{};
-    a.x = x; a.wt = w1; a.ln_sd = sd; a.ln_w = ln_w; a.out = hbuf; a.K = C; a.M = 2 * hid; a.P = P;
-    grr_status st = launch_gemm<LD_LN, EP_STORE>(a, B, s, "grr_lnb_forward/gemm1");
-    if (st != GRR_OK) return st;
-  }
+  // LayerNorm + 1x1 C -> 2hid (REF:916-941), statistics in-kernel
+  grr_status st = launch_x3<true>(x, frag, hbuf, B, C, 2 * hid, P, s, "grr_lnb_forward/gemm1");
+  if (st != GRR_OK) return st;
   LnbTailArgs t{};
   t.h = hbuf; t.aux = aux; t.x = x; t.skip = skip; t.out = out;
   t.hid = hid; t.M = C; t.H = H; t.W = W;
