@@ -52,12 +52,15 @@ SIGNATURES = {
     "grr_gtv_rhs_full": [P, P, P, Stencil, I, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_system_step": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_conv1x1": [P, P, P, I, I, I, L, P],
+    "grr_conv1x1_workspace_bytes": [I, I],
+    "grr_conv1x1_ws": [P, P, P, P, I, I, I, L, P],
     "grr_conv2x2s2": [P, P, P, I, I, I, I, I, P],
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
 }
-_RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64}
+_RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
+             "grr_conv1x1_workspace_bytes": c_int64}
 
 _lib = None
 

@@ -810,6 +810,32 @@ grr_status grr_conv1x1(const float* x, const float* wt, float* out, int B, int K
   return launch_gemm<LD_PLAIN, EP_STORE>(a, B, (hipStream_t)stream, "grr_conv1x1");
 }
 
+int64_t grr_conv1x1_workspace_bytes(int K, int M) {
+  if (K < 1 || K > 128 || M < 1) return 0;
+  const int KS = (K + 15) / 16, nch = (M + X3_MCH - 1) / X3_MCH;
+  return (int64_t)nch * x3_chunk_bytes(KS);
+}
+
+grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* workspace, int B, int K, int M,
+                          int64_t P, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && wt && out && workspace && B > 0 && K > 0 && M > 0 && P > 0, GRR_ERR_INVALID_ARG,
+              "grr_conv1x1_ws: bad args");
+  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_conv1x1_ws: out aliases x");
+  GRR_REQUIRE(K <= 128, GRR_ERR_UNSUPPORTED, "grr_conv1x1_ws: K=%d > 128", K);
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_conv1x1_ws: workspace not 256-B aligned");
+  GRR_REQUIRE(P * 16 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_conv1x1_ws: P too large");
+  hipStream_t s = (hipStream_t)stream;
+  const int KS = (K + 15) / 16, nch = (M + X3_MCH - 1) / X3_MCH;
+  uint16_t* frag = (uint16_t*)workspace;
+  const int64_t nf = (int64_t)nch * x3_chunk_bytes(KS) / 2;
+  hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 1 << 16)), dim3(256), 0, s,
+                     wt, nullptr, frag, M, K, KS, nch);
+  grr_status st = launch_status("grr_conv1x1_ws/pack");
+  if (st != GRR_OK) return st;
+  return launch_x3<false>(x, frag, out, B, K, M, P, s, "grr_conv1x1_ws");
+}
+
 grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int K, int M, int H, int W,
                          void* stream) {
   clear_error();

@@ -223,8 +223,14 @@ def conv1x1(x: Tensor, weight: Tensor) -> Tensor:
     if weight.shape[1] != k:
         raise ValueError(f"conv1x1: weight {tuple(weight.shape)} vs input channels {k}")
     out = torch.empty((b, m, h, w), dtype=torch.float32, device=dev)
-    _launch("conv1x1", 4 * b * h * w * (k + m), "grr_conv1x1", x.data_ptr(), weight.data_ptr(), out.data_ptr(),
-            b, k, m, h * w, _stream(dev))
+    ws_bytes = _native.load().grr_conv1x1_workspace_bytes(k, m)
+    if ws_bytes > 0:   # K <= 128: split-bf16 MFMA path (fp32-accurate)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)  # allocator: 512-B aligned
+        _launch("conv1x1", 4 * b * h * w * (k + m), "grr_conv1x1_ws", x.data_ptr(), weight.data_ptr(),
+                out.data_ptr(), ws.data_ptr(), b, k, m, h * w, _stream(dev))
+    else:
+        _launch("conv1x1", 4 * b * h * w * (k + m), "grr_conv1x1", x.data_ptr(), weight.data_ptr(),
+                out.data_ptr(), b, k, m, h * w, _stream(dev))
     return out
 
 
@@ -252,8 +258,8 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty_like(x)
-    # unfused LNB: x, h(2hid) round trip, g(hid) round trip, residual x, out
-    _launch("lnb", 4 * b * h * w * (3 * c + 2 * (2 * hid) + 2 * hid), "grr_lnb_forward", x.data_ptr(),
+    # x (GEMM1), h (2hid) written and read back once, residual x, out
+    _launch("lnb", 4 * b * h * w * (3 * c + 2 * (2 * hid)), "grr_lnb_forward", x.data_ptr(),
             ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(), out.data_ptr(),
             ws.data_ptr(), b, c, hid, h, w, _stream(dev))
     return out

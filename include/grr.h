@@ -126,6 +126,13 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
 grr_status grr_conv1x1(const float* x, const float* wt, float* out, int B, int K, int M, int64_t P,
                        void* stream);
 
+/* The same 1x1 convolution on bf16 MFMA with an exact 3-term split of both fp32 operands
+ * (six products, fp32-accurate; see DESIGN.md "x3 GEMM").  K <= 128.  workspace: device
+ * memory of grr_conv1x1_workspace_bytes(K, M) bytes, 256-B aligned (the split weights). */
+int64_t grr_conv1x1_workspace_bytes(int K, int M);
+grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* workspace, int B, int K, int M,
+                          int64_t P, void* stream);
+
 /* 2x2 stride-2 convolution, no bias (REF:593-602): x [B,K,H,W], wt [M,K,2,2] -> out [B,M,H/2,W/2]. */
 grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int K, int M, int H, int W,
                          void* stream);

@@ -170,12 +170,36 @@ def test_gtv_prox_rhs_half(irdu, variant, shape):
 
 # ---------------------------------------------------------------------------
 # feature CNN
-@pytest.mark.parametrize("bkmp", [(2, 12, 24, (8, 8)), (1, 96, 192, (33, 40)), (2, 7, 3, (5, 6))])
+# K <= 128: split-bf16 MFMA path (grr_conv1x1_ws); K = 160: fp32 MFMA path (grr_conv1x1)
+@pytest.mark.parametrize("bkmp", [(2, 12, 24, (8, 8)), (1, 96, 192, (33, 40)), (2, 7, 3, (5, 6)),
+                                  (1, 96, 3, (16, 24)), (1, 160, 40, (9, 10))])
 def test_conv1x1(irdu, bkmp):
     b, k, m, (h, w) = bkmp
     x = rand(b, k, h, w, seed=11)
     wt = rand(m, k, 1, 1, seed=12) * 0.2
     assert_close(irdu.kernels.conv1x1(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt), 1e-5)
+
+
+def test_x3_gemm_is_fp32_accurate(irdu):
+    """The split-bf16 GEMM (3 exact bf16 terms per operand, 6 products) against a float64
+    reference: its error must be of the order of a plain fp32 evaluation's, not bf16's."""
+    x = rand(2, 96, 40, 36, seed=31, scale=3.0, offset=0.5)
+    wt = rand(192, 96, 1, 1, seed=32) * 0.2
+    ref64 = torch.nn.functional.conv2d(x.double(), wt.double())
+    err32 = rel_err(torch.nn.functional.conv2d(x, wt), ref64)
+    got = irdu.kernels.conv1x1(x.to(DEV), wt.to(DEV))
+    err = rel_err(got, ref64)
+    assert err <= 4 * err32 + 1e-7, (err, err32)
+    # and the LayerNorm-folded variant inside the LNB (fp32 CPU oracle vs float64 oracle)
+    torch.manual_seed(5)
+    blk = irdu.LocalNonLinearBlock(96, 256, 1)
+    p64 = {k: v.double() for k, v in sd_cpu(blk).items()}
+    x = rand(1, 96, 24, 40, seed=33)
+    ref64 = O.local_nonlinear_block(x.double(), p64, "")
+    err32 = rel_err(O.local_nonlinear_block(x, sd_cpu(blk), ""), ref64)
+    with torch.no_grad():
+        err = rel_err(blk.to(DEV)(x.to(DEV)), ref64)
+    assert err <= 4 * err32 + 1e-7, (err, err32)
 
 
 @pytest.mark.parametrize("bkmhw", [(2, 12, 12, 16, 16), (1, 96, 96, 34, 50)])
