@@ -23,7 +23,7 @@ step() {  # step <name> <limit-seconds> <allow-exit-1> cmd...
 
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests 900 1 python -m pytest tests -m gpu -q -rf
+  step gpu_tests 900 1 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = smoke ]; then
   step smoke 300 0 python -c "import __graft_entry__ as g; g.smoke()"
