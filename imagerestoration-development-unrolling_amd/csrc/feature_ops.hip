@@ -291,246 +291,6 @@ __global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ 
   }
 }
 
-// LocalNonLinearBlock tail, fused: out = skip0*x + skip1 * W2 . gate(dw3x3(h))
-// (REF:943-948, :962-964).  A workgroup owns a 4x32 pixel tile and ALL M <= 128 output
-// channels (wave w: pixels 32w..32w+31 of the tile, MT 32-row MFMA tiles).  The hidden
-// channels are walked in chunks of FKC.  Each chunk's operands -- the mask / value planes
-// with a 1-pixel halo, and the chunk's packed W2 columns + depthwise taps (lnb_pack_kernel)
-// -- are fetched by LDS-DMA (global_load_lds) into a 3-slot ring, two chunks ahead of their
-// use; a chunk is consumed after a counted s_waitcnt vmcnt + raw s_barrier.  The depthwise
-// 3x3 and the gate are evaluated from the ring into the MFMA B image; the gated activations
-// never reach HBM.
-//
-// V4 (W % 4 == 0): a halo plane is 6 rows x 10 float4 (columns x0-4 .. x0+35), ONE 16-byte
-// DMA wave-instruction; replicate padding at the left / right image edge is applied when the
-// 3x3 window is read.  Otherwise a plane is 204 dwords (columns x0-1 .. x0+32, clamped at
-// load time), four 4-byte DMA wave-instructions.
-#ifndef GRR_TAIL_EXP
-#define GRR_TAIL_EXP 0   // ablation builds only (scripts/build_ablation.sh); 0 = the product kernel
-#endif
-constexpr int FT = 256;             // threads
-constexpr int FTR = 4, FTC = 32;    // pixel tile rows x cols (128 pixels)
-constexpr int FKC = 8;              // hidden channels per chunk
-constexpr int FPL = 256;            // LDS pitch of one halo plane
-constexpr int FNS = 3;              // ring slots (two chunks in flight + the one being consumed)
-constexpr int FBP = FTR * FTC + 4;  // pitch of the gated-activation image Bs[FKC][FBP]
-constexpr int FTAPS = 2 * FKC * 9;  // depthwise taps per chunk: mask [kk][9], value [kk][9]
-// packed per-chunk auxiliaries: W2^T [kk][MT*32] (zero padded), then the taps
-__host__ __device__ constexpr int lnb_aux_instr(int mt) { return (mt * 32 * FKC + FTAPS + 1023) / 1024; }
-__host__ __device__ constexpr int lnb_aux_floats(int mt) { return lnb_aux_instr(mt) * 1024; }
-
-struct LnbTailArgs {
-  const float* h;      // [B, 2hid, H, W]
-  const float* aux;    // [nchunks][lnb_aux_floats(MT)]
-  const float* x;      // [B, M, H, W] residual
-  const float* skip;   // [2]
-  float* out;          // [B, M, H, W]
-  int hid, M, H, W, tiles_x, tiles_y;
-  uint32_t nblk;
-};
-
-// Pack W2 [M, hid] and the depthwise taps [2hid, 9] chunk-major for 16-byte LDS-DMA.
-__global__ void lnb_pack_kernel(const float* __restrict__ w2, const float* __restrict__ wdw,
-                                float* __restrict__ aux, int M, int hid, int mpad, int auxf, int nchunks) {
-  const int n = nchunks * auxf;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int c = i / auxf, e = i - c * auxf;
-    float v = 0.f;
-    if (e < FKC * mpad) {
-      const int kk = e / mpad, m = e - kk * mpad, k = c * FKC + kk;
-      if (m < M && k < hid) v = w2[(int64_t)m * hid + k];
-    } else if (e < FKC * mpad + FTAPS) {
-      const int t = e - FKC * mpad, half = t / (FKC * 9), r = t - half * FKC * 9;
-      const int kk = r / 9, k = c * FKC + kk;
-      if (k < hid) v = wdw[((half ? hid : 0) + k) * 9 + (r - kk * 9)];
-    }
-    aux[i] = v;
-  }
-}
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-// One LDS-DMA per lane: LDS[wave_base + BYTES*lane] = *(base + byte_off), `base` wave-uniform
-// (SGPRs), byte_off a per-lane 32-bit offset.
-template <int BYTES>
-__device__ __forceinline__ void dma(const float* base, uint32_t byte_off, float* lds_wave_base) {
-  const float* src = (const float*)((const char*)base + byte_off);
-  if constexpr (BYTES == 16) __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
-  else __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 4, 0, 0);
-}
-
-template <int MT, bool V4>
-__global__ __launch_bounds__(FT) void lnb_tail_kernel(LnbTailArgs a) {
-  constexpr int HPI = V4 ? 1 : 4;                    // DMA instructions per halo plane
-  constexpr int HP = V4 ? 40 : FTC + 2;              // halo row pitch (floats)
-  constexpr int HX = V4 ? 3 : 0;                     // halo column of x = x0 - 1
-  constexpr int AUXI = lnb_aux_instr(MT);            // 16-byte aux instructions per wave
-  constexpr int AUXF = lnb_aux_floats(MT);
-  constexpr int SLOT = 2 * FKC * FPL + AUXF;
-  constexpr int PER_CHUNK = 4 * HPI + AUXI;          // VMEM ops per wave per chunk
-  // a single LDS array (a second __shared__ object can make hipcc drain vmcnt at ds_reads)
-  __shared__ __attribute__((aligned(16))) float smem[FNS * SLOT + FKC * FBP];
-  float* Bs = smem + FNS * SLOT;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
-  const int tx = lb % a.tiles_x; lb /= a.tiles_x;
-  const int ty = lb % a.tiles_y;
-  const int b = lb / a.tiles_y;
-  const int H = a.H, W = a.W, hid = a.hid, M = a.M;
-  const int64_t HW = (int64_t)H * W;
-  const int y0 = ty * FTR, x0 = tx * FTC;
-  const float* hb = a.h + (int64_t)b * 2 * hid * HW;
-
-  // per-lane byte offsets of this tile's halo elements inside a plane (fixed for the kernel)
-  uint32_t hofs[HPI];
-  if constexpr (V4) {
-    const int l = min(lane, 59), ry = l / 10, c4 = l - ry * 10;
-    const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 4 + 4 * c4, 0, W - 4);
-    hofs[0] = (uint32_t)(gy * W + gx) * 4u;
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = min(64 * i + lane, 6 * HP - 1);
-      const int ry = r / HP, rx = r - ry * HP;
-      const int gy = clampi(y0 - 1 + ry, 0, H - 1), gx = clampi(x0 - 1 + rx, 0, W - 1);
-      hofs[i] = (uint32_t)(gy * W + gx) * 4u;
-    }
-  }
-  const uint32_t aofs = (uint32_t)lane * 16u;
-
-  auto issue = [&](int c) {
-    const int k0 = c * FKC;
-    float* slot = smem + (c % FNS) * SLOT;
-#if GRR_TAIL_EXP >= 6
-    // timing-only: channel-blocked h ([chunk][H][W][16]); 6 rows x 40 px x 16 ch contiguous per row
-    if constexpr (V4) {
-#pragma unroll
-      for (int pi = 0; pi < 4; ++pi) {
-        const int L = (wave * 4 + pi) * 64 + lane;
-        const int row = min(L / 160, 5), within = L % 160;
-        const int gy = clampi(y0 - 1 + row, 0, H - 1);
-        const uint32_t off = (uint32_t)((gy * W + max(x0 - 4, 0)) * 16 + within * 4) * 4u;
-        dma<16>(hb + (int64_t)c * 16 * HW, off, slot + (wave * 4 + pi) * FPL);
-      }
-    }
-    if (0)
-#endif
-#pragma unroll
-    for (int pi = 0; pi < 4; ++pi) {
-      const int pl = wave * 4 + pi;                    // plane 0..15: [0,8) mask, [8,16) value
-      const int ch = (pl < FKC ? 0 : hid) + min(k0 + (pl & (FKC - 1)), hid - 1);   // k >= hid: gate zeroed
-      const float* base = hb + (int64_t)ch * HW;
-#pragma unroll
-      for (int i = 0; i < HPI; ++i) dma<V4 ? 16 : 4>(base, hofs[i], slot + pl * FPL + 64 * i);
-    }
-    const float* abase = a.aux + (int64_t)c * AUXF;
-#pragma unroll
-    for (int i = 0; i < AUXI; ++i)
-      dma<16>(abase + (i * 4 + wave) * 256, aofs, slot + 2 * FKC * FPL + (i * 4 + wave) * 256);
-  };
-
-  f32x16 acc[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = f32x16{};
-  const int nchunks = (hid + FKC - 1) / FKC;
-  issue(0);
-  if (nchunks > 1) issue(1);
-  // gate mapping: thread = (channel kk = tid / 32, column px), computing the 4-pixel column
-  // strip px of the tile, so the 6 halo rows it reads are shared by its 4 outputs
-  const int gk = tid >> 5, px = tid & 31;
-  // window columns of x-1, x, x+1 (replicate padding at the image edges for V4)
-  const int cm = HX + px;
-  const int cl = (V4 && x0 + px == 0) ? cm + 1 : cm;
-  const int cr = (V4 && x0 + px + 1 >= W) ? cm + 1 : cm + 2;
-  for (int c = 0; c < nchunks; ++c) {
-    const int k0 = c * FKC;
-    const float* slot = smem + (c % FNS) * SLOT;
-    // chunk c landed (this wave's DMAs), then every wave's (barrier)
-    if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER_CHUNK) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#if GRR_TAIL_EXP != 3 && GRR_TAIL_EXP != 5
-    if (c + 2 < nchunks) issue(c + 2);                 // slot (c+2)%3 was last read in chunk c-1
-#endif
-    const float* wsl = slot + 2 * FKC * FPL;
-    {
-      // depthwise 3x3 (REF:946) on mask and value planes + gate sigmoid(m)*m*v (REF:947)
-      const float* taps = wsl + FKC * MT * 32;
-      const float* mt = slot + gk * FPL;
-      const float* vt = slot + (FKC + gk) * FPL;
-      float km[9], kv[9];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        km[i] = taps[gk * 9 + i];
-        kv[i] = taps[FKC * 9 + gk * 9 + i];
-      }
-      float mr[FTR + 2][3], vr[FTR + 2][3];
-#pragma unroll
-      for (int r = 0; r < FTR + 2; ++r) {
-        mr[r][0] = mt[r * HP + cl]; mr[r][1] = mt[r * HP + cm + 1]; mr[r][2] = mt[r * HP + cr];
-        vr[r][0] = vt[r * HP + cl]; vr[r][1] = vt[r * HP + cm + 1]; vr[r][2] = vt[r * HP + cr];
-      }
-      const bool live = k0 + gk < hid;
-#pragma unroll
-      for (int py = 0; py < FTR; ++py) {
-        float m = 0.f, v = 0.f;
-#if GRR_TAIL_EXP == 1 || GRR_TAIL_EXP == 4 || GRR_TAIL_EXP == 5 || GRR_TAIL_EXP == 6
-        m = mr[py][1]; v = vr[py][1];
-#else
-#pragma unroll
-        for (int ay = 0; ay < 3; ++ay)
-#pragma unroll
-          for (int ax = 0; ax < 3; ++ax) {
-            m += km[ay * 3 + ax] * mr[py + ay][ax];
-            v += kv[ay * 3 + ax] * vr[py + ay][ax];
-          }
-#endif
-        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
-        Bs[gk * FBP + py * FTC + px] = live ? (sg * m) * v : 0.f;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#if GRR_TAIL_EXP == 2 || GRR_TAIL_EXP == 4 || GRR_TAIL_EXP == 5 || GRR_TAIL_EXP == 6
-    if (c >= 0) continue;
-#endif
-#pragma unroll
-    for (int kk = 0; kk < FKC; kk += 2) {
-      const int kr = kk + (lane >> 5);
-      const float bv = Bs[kr * FBP + wave * 32 + (lane & 31)];
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const float av = wsl[kr * (MT * 32) + t * 32 + (lane & 31)];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
-      }
-    }
-  }
-  const float s0 = a.skip[0], s1 = a.skip[1];
-  const int pp = wave * 32 + (lane & 31);
-  const int gy = y0 + pp / FTC, gx = x0 + (pp % FTC);
-  const bool pix = gy < H && gx < W;
-  const int64_t pofs = (int64_t)b * M * HW + (int64_t)min(gy, H - 1) * W + min(gx, W - 1);
-  // residual loads first, all in flight together (clamped addresses), then one wait
-  float xv[MT][16];
-#pragma unroll
-  for (int t = 0; t < MT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = min(t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), M - 1);
-      xv[t][r] = a.x[pofs + (int64_t)m * HW];
-    }
-  if (pix) {
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M) a.out[pofs + (int64_t)m * HW] = s0 * xv[t][r] + s1 * acc[t][r];   // REF:962-964
-      }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // fp32-accurate 1x1 convolution on bf16 MFMA ("x3 split").
 //
@@ -778,23 +538,6 @@ __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __res
   }
 }
 
-// LNB workspace (floats): [h: B*2hid*P][tail aux: nchunks*aux][W1 x3 fragments], 256-B aligned
-static int64_t lnb_aux_offset(int B, int hid, int H, int W) {
-  const int64_t P = (int64_t)H * W;
-  return ((int64_t)B * 2 * hid * P + 63) / 64 * 64;
-}
-static int64_t lnb_frag_offset(int B, int C, int hid, int H, int W) {
-  const int nchunks = (hid + FKC - 1) / FKC;
-  const int mt = (C + 31) / 32;
-  return lnb_aux_offset(B, hid, H, W) + ((int64_t)nchunks * lnb_aux_floats(mt < 1 ? 1 : mt) + 63) / 64 * 64;
-}
-
-template <int MT>
-static void launch_tail(const LnbTailArgs& t, bool v4, hipStream_t s) {
-  if (v4) hipLaunchKernelGGL((lnb_tail_kernel<MT, true>), dim3(t.nblk), dim3(FT), 0, s, t);
-  else hipLaunchKernelGGL((lnb_tail_kernel<MT, false>), dim3(t.nblk), dim3(FT), 0, s, t);
-}
-
 }  // namespace grr
 
 using namespace grr;
@@ -847,61 +590,71 @@ grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int
   return launch_gemm<LD_IM2COL, EP_STORE>(a, B, (hipStream_t)stream, "grr_conv2x2s2");
 }
 
+}  // extern "C"
+
+namespace grr {
+
+// LNB fp32 path (C > 128): LN statistics, W1 on fp32 MFMA with the LN folded in, depthwise
+// 3x3 + gate, W2 + skip.  Workspace (floats): [sd: B*P][h: B*2hid*P][g: B*hid*P].
+static int64_t lnb_fp32_workspace_floats(int B, int hid, int H, int W) {
+  const int64_t P = (int64_t)H * W, a64 = 64;
+  return ((int64_t)B * P + a64 - 1) / a64 * a64 + ((int64_t)B * 2 * hid * P + a64 - 1) / a64 * a64 +
+         (int64_t)B * hid * P;
+}
+
+static grr_status lnb_forward_fp32(const float* x, const float* ln_w, const float* w1, const float* wdw,
+                                   const float* w2, const float* skip, float* out, float* ws, int B, int C, int hid,
+                                   int H, int W, hipStream_t s) {
+  GRR_REQUIRE(C <= 512, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 512", C);
+  const int64_t P = (int64_t)H * W;
+  float* sd = ws;
+  float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;
+  float* gbuf = hbuf + ((int64_t)B * 2 * hid * P + 63) / 64 * 64;
+  const int64_t n = (int64_t)B * P;
+  hipLaunchKernelGGL(ln_stats_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1 << 16)), dim3(256), 0, s,
+                     x, sd, B, C, P);
+  grr_status st = launch_status("grr_lnb_forward/ln_stats");
+  if (st != GRR_OK) return st;
+  GemmArgs g1{};
+  g1.x = x; g1.wt = w1; g1.ln_sd = sd; g1.ln_w = ln_w; g1.out = hbuf; g1.K = C; g1.M = 2 * hid; g1.P = P;
+  st = launch_gemm<LD_LN, EP_STORE>(g1, B, s, "grr_lnb_forward/w1");
+  if (st != GRR_OK) return st;
+  const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
+  const uint64_t nb = (uint64_t)B * hid * tx * ty;
+  GRR_REQUIRE(nb < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+  hipLaunchKernelGGL(dw_gate_kernel, dim3((unsigned)nb), dim3(256), 0, s, hbuf, wdw, gbuf, hid, H, W, tx, ty,
+                     (uint32_t)nb);
+  st = launch_status("grr_lnb_forward/dw_gate");
+  if (st != GRR_OK) return st;
+  GemmArgs g2{};
+  g2.x = gbuf; g2.wt = w2; g2.res = x; g2.skip = skip; g2.out = out; g2.K = hid; g2.M = C; g2.P = P;
+  return launch_gemm<LD_PLAIN, EP_SKIP>(g2, B, s, "grr_lnb_forward/w2");
+}
+
+}  // namespace grr
+
+extern "C" {
+
 int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
-  const int KS = (C + 15) / 16;
-  const int nch = (2 * hid + X3_MCH - 1) / X3_MCH;
-  return lnb_frag_offset(B, C, hid, H, W) * (int64_t)sizeof(float) + (int64_t)nch * x3_chunk_bytes(KS);
+  if (B <= 0 || C <= 0 || hid <= 0 || H <= 0 || W <= 0) return 0;
+  const int64_t f = C <= 128 ? grr::lnb_mfma_workspace_floats(B, C, hid, H, W)
+                             : grr::lnb_fp32_workspace_floats(B, hid, H, W);
+  return f * (int64_t)sizeof(float);
 }
 
 grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                            const float* skip, float* out, void* workspace, int B, int C, int hid, int H, int W,
                            void* stream) {
-  clear_error();
+  grr::clear_error();
   GRR_REQUIRE(x && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && C > 1 && hid > 0 && H > 0 &&
                   W > 0,
               GRR_ERR_INVALID_ARG, "grr_lnb_forward: bad args");
   GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward: out aliases x");
-  GRR_REQUIRE(C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 128", C);
   GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_lnb_forward: workspace not 256-B aligned");
-  GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: plane too large");
   hipStream_t s = (hipStream_t)stream;
-  const int64_t P = (int64_t)H * W;
-  float* hbuf = (float*)workspace;                                     // [B, 2hid, P]
-  float* aux = hbuf + lnb_aux_offset(B, hid, H, W);
-  uint16_t* frag = (uint16_t*)(hbuf + lnb_frag_offset(B, C, hid, H, W));
-  const int mt = (C + 31) / 32;
-  const int nchunks = (hid + FKC - 1) / FKC;
-  {
-    // weights: tail W2 / taps chunks, and W1 . diag(ln_w) split for the x3 GEMM
-    const int na = nchunks * lnb_aux_floats(mt);
-    hipLaunchKernelGGL(lnb_pack_kernel, dim3((na + 255) / 256), dim3(256), 0, s, w2, wdw, aux, C, hid, mt * 32,
-                       lnb_aux_floats(mt), nchunks);
-    grr_status st = launch_status("grr_lnb_forward/pack");
-    if (st != GRR_OK) return st;
-    const int KS = (C + 15) / 16, nch = (2 * hid + X3_MCH - 1) / X3_MCH;
-    const int64_t nf = (int64_t)nch * x3_chunk_bytes(KS) / 2;
-    hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 1 << 16)), dim3(256), 0, s,
-                       w1, ln_w, frag, 2 * hid, C, KS, nch);
-    st = launch_status("grr_lnb_forward/pack_w1");
-    if (st != GRR_OK) return st;
-  }
-  // LayerNorm + 1x1 C -> 2hid (REF:916-941), statistics in-kernel
-  grr_status st = launch_x3<true>(x, frag, hbuf, B, C, 2 * hid, P, s, "grr_lnb_forward/gemm1");
-  if (st != GRR_OK) return st;
-  LnbTailArgs t{};
-  t.h = hbuf; t.aux = aux; t.x = x; t.skip = skip; t.out = out;
-  t.hid = hid; t.M = C; t.H = H; t.W = W;
-  t.tiles_x = (W + FTC - 1) / FTC;
-  t.tiles_y = (H + FTR - 1) / FTR;
-  const uint64_t n = (uint64_t)B * t.tiles_x * t.tiles_y;
-  GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
-  t.nblk = (uint32_t)n;
-  const bool v4 = (W % 4 == 0) && W >= 4;
-  if (mt == 1) launch_tail<1>(t, v4, s);
-  else if (mt == 2) launch_tail<2>(t, v4, s);
-  else if (mt == 3) launch_tail<3>(t, v4, s);
-  else launch_tail<4>(t, v4, s);
-  return launch_status("grr_lnb_forward/tail");
+  if (C <= 128)
+    return grr::lnb_forward_mfma(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
+  return grr::lnb_forward_fp32(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
 }
 
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {

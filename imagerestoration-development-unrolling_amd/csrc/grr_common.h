@@ -40,6 +40,12 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t n) {
   return base + bid / kXcd;
 }
 
+// LocalNonLinearBlock on the split-bf16 MFMA kernels (lnb_ops.hip), C <= 128
+int64_t lnb_mfma_workspace_floats(int B, int C, int hid, int H, int W);
+grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
+                            const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
+                            hipStream_t s);
+
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 }  // namespace grr

@@ -258,8 +258,9 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty_like(x)
-    # x (GEMM1), h (2hid) written and read back once, residual x, out
-    _launch("lnb", 4 * b * h * w * (3 * c + 2 * (2 * hid)), "grr_lnb_forward", x.data_ptr(),
+    # C <= 128: x (head), gated g (hid) written and read back once, residual x, out
+    nbytes_algo = 4 * b * h * w * (3 * c + 2 * hid) if c <= 128 else 4 * b * h * w * (3 * c + 2 * (2 * hid) + 2 * hid)
+    _launch("lnb", nbytes_algo, "grr_lnb_forward", x.data_ptr(),
             ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(), out.data_ptr(),
             ws.data_ptr(), b, c, hid, h, w, _stream(dev))
     return out

@@ -210,10 +210,14 @@ def test_conv2x2s2(irdu, bkmhw):
     assert_close(irdu.kernels.conv2x2s2(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt, stride=2), 1e-5)
 
 
-# (C, hid, H, W): full/partial 4x32 tiles, W % 4 == 0 (16-byte halo DMA) and not (dword DMA),
-# hid % 8 != 0 (partial last chunk), C up to 128 (4 MFMA row tiles), W = 4 (both edges in one float4)
+# (C, hid, H, W): C <= 128 runs the split-bf16 head (32 x 13 / 32 x 9 output tiles with halo
+# recompute) + mix kernels: full / partial tiles, H*W % 4 == 0 (16-byte g DMA) and not (dword
+# DMA), hid % 8 != 0 and hid % 16 != 0 (partial chunk / k-step), C = 33 (partial k-step and
+# row tile), C = 128 (4 k-steps: 3 blocks per wave), tiny images (tile wider than the image);
+# C = 160 / 192 run the fp32 MFMA path (v1.0 encoder/decoder widths).
 @pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 40, 36), (33, 20, 9, 44), (24, 64, 13, 30),
-                                 (128, 24, 8, 68), (6, 16, 5, 4)])
+                                 (128, 24, 8, 68), (6, 16, 5, 4), (96, 256, 27, 70), (64, 40, 1, 3),
+                                 (160, 48, 12, 20), (192, 64, 9, 11)])
 def test_local_nonlinear_block(irdu, chw):
     c, hid, h, w = chw
     torch.manual_seed(0)
