@@ -21,6 +21,9 @@ LIB = os.path.join(HERE, "libgrr.so")
 SOURCES = ["graph_ops.hip", "feature_ops.hip", "lnb_ops.hip"]
 HEADERS = [os.path.join(CSRC, "grr_common.h"), os.path.join(ROOT, "include", "grr.h")]
 ARCH = "gfx950"
+# lnb_ops: no SLP packing of the gate's independent f32 FMAs into v_pk_fma_f32 (the packing
+# needs register-pair moves that cost more than it saves, MI355X_MICROARCH.md)
+EXTRA_FLAGS = {"lnb_ops.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:
@@ -46,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         obj = os.path.join(CSRC, src.replace(".hip", ".o"))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                "-Wno-unused-variable", "-I", os.path.join(ROOT, "include"), "-c",
-               os.path.join(CSRC, src), "-o", obj]
+               os.path.join(CSRC, src), "-o", obj] + EXTRA_FLAGS.get(src, [])
         if verbose:
             cmd.insert(2, "-Rpass-analysis=kernel-resource-usage")
             print(" ".join(cmd), flush=True)

@@ -80,6 +80,20 @@ __device__ __forceinline__ uint16_t split_term(float v, int q) {
 __device__ __forceinline__ void dma16(const void* src, float* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
 }
+// The same 16-byte LDS-DMA as an asm statement.  hipcc answers every LDS-DMA builtin with
+// lgkmcnt(0) waits at all later LDS reads (it cannot order the DMA's LDS write against them);
+// the head kernel orders its ring itself (counted vmcnt + barrier), so it issues the DMA
+// opaquely and keeps the compiler's counted lgkmcnt waits.  The compiler does not count these
+// operations: they are only issued where no compiler-visible vector-memory load is pending
+// behind them.
+typedef __attribute__((address_space(3))) float* lds_f32_t;
+__device__ __forceinline__ void dma16_opaque(const void* src, float* lds_wave_base) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)lds_wave_base;
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v)) : "memory");
+}
+#ifndef GRR_HEAD_OPAQUE_DMA
+#define GRR_HEAD_OPAQUE_DMA 1
+#endif
 
 // ---------------------------------------------------------------------------
 // head: LN + W1 + dw3x3 + gate
@@ -164,7 +178,8 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
       const int img = min(i * 8 + wave, NI - 1);   // surplus waves repeat the last image
-      dma16(src + img * 1024, slot + img * 256);
+      if constexpr (GRR_HEAD_OPAQUE_DMA) dma16_opaque(src + img * 1024, slot + img * 256);
+      else dma16(src + img * 1024, slot + img * 256);
     }
   };
   issue(0, 0);
@@ -220,72 +235,85 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
       a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
   const int gx = x0 + col;
 
+  auto gemm1 = [&](int c) {
+    if (c >= nch) return;
+    const float* slot = ring + (c % NSLOT) * SLOTF + lane * 4;
+    f32x4 acc[NB];
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) acc[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 0) * 256);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 1) * 256);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 2) * 256);
+#pragma unroll
+      for (int blk = 0; blk < NB; ++blk)
+        GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_16x16x32_bf16, acc[blk], a0, a1, a2, xf[blk][s][0],
+                    xf[blk][s][1], xf[blk][s][2]);
+    }
+    // h rows 4 kq + i (0..7 mask, 8..15 value) of the halo pixels -> LDS plane set c & 1
+    float* hb = smem + (c & 1) * HBUF;
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      const int q = (wave * NB + blk) * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
+    }
+  };
+  // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1
+  auto gate = [&](int c) {
+    const int jj = LH_JC * (c - 1) + wave;
+    const bool live = c >= 1 && jj < hid;
+    const float* hb = smem + ((c + 1) & 1) * HBUF;
+    const float* mp = hb + wave * Geo::HP + col;
+    const float* vp = hb + (LH_JC + wave) * Geo::HP + col;
+    const float* taps = ring + ((c + NSLOT - 1) % NSLOT) * SLOTF + KS * 3 * 256 + wave * 18;
+    float km[9], kv[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      km[t] = taps[t];
+      kv[t] = taps[9 + t];
+    }
+    float mw[3][3], vw[3][3];
+#pragma unroll
+    for (int i = 0; i < RA + 2; ++i) {
+      const int hrow = min(r0 + i, Geo::HR - 1) * LH_HWD;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        mw[i % 3][d] = mp[hrow + d];
+        vw[i % 3][d] = vp[hrow + d];
+      }
+      if (i >= 2) {
+        float m = 0.f, v = 0.f;
+#pragma unroll
+        for (int ay = 0; ay < 3; ++ay)
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) {
+            m += km[ay * 3 + ax] * mw[(i - 2 + ay) % 3][ax];
+            v += kv[ay * 3 + ax] * vw[(i - 2 + ay) % 3][ax];
+          }
+        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
+        const int orow = r0 + i - 2, gy = y0 + orow;
+        const bool ok = live && orow < Geo::TH && gy < H && gx < W;
+        const uint32_t off = ok ? (uint32_t)(jj * HW + gy * W + gx) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((sg * m) * v), grs, off, 0, 0);
+      }
+    }
+  };
+
+  // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (independent LDS planes).  The two
+  // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work
+  // overlaps the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).
+  const bool gate_first = wave < 4;
   for (int c = 0; c <= nch; ++c) {
     // chunk c + 2 -> slot (c + 2) % 4, last read (gate of chunk c - 2) before the previous barrier
     issue(min(c + 2, nch - 1), (c + 2) % NSLOT);
-    if (c < nch) {
-      const float* slot = ring + (c % NSLOT) * SLOTF + lane * 4;
-      f32x4 acc[NB];
-#pragma unroll
-      for (int blk = 0; blk < NB; ++blk) acc[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 0) * 256);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 1) * 256);
-        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 2) * 256);
-#pragma unroll
-        for (int blk = 0; blk < NB; ++blk)
-          GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_16x16x32_bf16, acc[blk], a0, a1, a2, xf[blk][s][0],
-                      xf[blk][s][1], xf[blk][s][2]);
-      }
-      // h rows 4 kq + i (0..7 mask, 8..15 value) of the halo pixels -> LDS plane set c & 1
-      float* hb = smem + (c & 1) * HBUF;
-#pragma unroll
-      for (int blk = 0; blk < NB; ++blk) {
-        const int q = (wave * NB + blk) * 16 + (lane & 15);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
-      }
-    }
-    // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1
-    {
-      const int jj = LH_JC * (c - 1) + wave;
-      const bool live = c >= 1 && jj < hid;
-      const float* hb = smem + ((c + 1) & 1) * HBUF;
-      const float* mp = hb + wave * Geo::HP + col;
-      const float* vp = hb + (LH_JC + wave) * Geo::HP + col;
-      const float* taps = ring + ((c + NSLOT - 1) % NSLOT) * SLOTF + KS * 3 * 256 + wave * 18;
-      float km[9], kv[9];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        km[t] = taps[t];
-        kv[t] = taps[9 + t];
-      }
-      float mw[3][3], vw[3][3];
-#pragma unroll
-      for (int i = 0; i < RA + 2; ++i) {
-        const int hrow = min(r0 + i, Geo::HR - 1) * LH_HWD;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          mw[i % 3][d] = mp[hrow + d];
-          vw[i % 3][d] = vp[hrow + d];
-        }
-        if (i >= 2) {
-          float m = 0.f, v = 0.f;
-#pragma unroll
-          for (int ay = 0; ay < 3; ++ay)
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-              m += km[ay * 3 + ax] * mw[(i - 2 + ay) % 3][ax];
-              v += kv[ay * 3 + ax] * vw[(i - 2 + ay) % 3][ax];
-            }
-          const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
-          const int orow = r0 + i - 2, gy = y0 + orow;
-          const bool ok = live && orow < Geo::TH && gy < H && gx < W;
-          const uint32_t off = ok ? (uint32_t)(jj * HW + gy * W + gx) * 4u : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((sg * m) * v), grs, off, 0, 0);
-        }
-      }
+    if (gate_first) {
+      gate(c);
+      gemm1(c);
+    } else {
+      gemm1(c);
+      gate(c);
     }
     // chunk c + 1 landed: after its DMA this wave issued RA stores (iteration c - 1),
     // DPW DMAs and RA stores (iteration c); then every wave's part (barrier)

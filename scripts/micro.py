@@ -71,6 +71,18 @@ def main():
         for kind, v in timer.summary().items():
             print(f"{args.kernel}: {kind:16s} launches={v['launches']} mean={v['mean_ms']:.4f} ms "
                   f"algo={v['gbps']:.1f} GB/s bytes/launch={v['bytes_per_launch']:.4e}")
+        lib = irdu_amd._native.load()
+        if hasattr(lib, "grr_debug_head_stamps"):   # GRR_HEAD_STAMP timing builds
+            import ctypes
+            import numpy as np
+            buf = (ctypes.c_ulonglong * (64 * 8 * 8))()
+            lib.grr_debug_head_stamps(buf)
+            a = np.frombuffer(buf, dtype=np.uint64).reshape(64 * 8, 8).astype(np.float64)
+            tot = a[:, 1] - a[:, 0]
+            print(f"head stamps (cycles per wave, mean of {len(a)}): total {tot.mean():.0f}  "
+                  f"steady work {a[:, 2].mean():.0f}  vmcnt wait {a[:, 3].mean():.0f}  barrier {a[:, 4].mean():.0f}  "
+                  f"per steady chunk: work {a[:, 2].mean() / (a[0, 5] - 1):.0f} wait {a[:, 3].mean() / (a[0, 5] - 1):.0f} "
+                  f"barrier {a[:, 4].mean() / (a[0, 5] - 1):.0f}")
 
 
 if __name__ == "__main__":
