@@ -527,14 +527,26 @@ static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, in
   return launch_status(name);
 }
 
+// out[b, g Cin + c] = img[b, c]: one thread per 4 consecutive pixels of one (b, c) plane reads
+// them once (16-byte load) and writes the G copies (16-byte stores); store-bandwidth bound.
 __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __restrict__ out, int Cin, int G,
-                                     int64_t P, int64_t n) {
+                                     int64_t P, int64_t nq) {
+  const int64_t P4 = P / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nq; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t plane = i / P4, q = i - plane * P4;      // plane = b Cin + c
+    const int64_t b = plane / Cin, c = plane - b * Cin;
+    const float4 v = reinterpret_cast<const float4*>(img + plane * P)[q];
+    float4* o = reinterpret_cast<float4*>(out + (b * G * Cin + c) * P) + q;
+    for (int g = 0; g < G; ++g) o[g * Cin * P4] = v;
+  }
+}
+__global__ void repeat_graphs_scalar_kernel(const float* __restrict__ img, float* __restrict__ out, int Cin, int G,
+                                            int64_t P, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p = i % P;
-    const int64_t r = i / P;              // b * (G*Cin) + g*Cin + c
-    const int c = (int)(r % Cin);
-    const int64_t b = r / ((int64_t)G * Cin);
-    out[i] = img[(b * Cin + c) * P + p];
+    const int64_t p = i % P, plane = i / P;
+    const int64_t b = plane / Cin, c = plane - b * Cin;
+    const float v = img[i];
+    for (int g = 0; g < G; ++g) out[((b * G + g) * Cin + c) * P + p] = v;
   }
 }
 
@@ -660,9 +672,16 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {
   clear_error();
   GRR_REQUIRE(img && out && B > 0 && Cin > 0 && G > 0 && P > 0, GRR_ERR_INVALID_ARG, "grr_repeat_graphs: bad args");
-  const int64_t n = (int64_t)B * G * Cin * P;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
-  hipLaunchKernelGGL(repeat_graphs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, img, out, Cin, G, P, n);
+  const int64_t n = (int64_t)B * Cin * P;   // input elements
+  if (P % 4 == 0 && (uintptr_t)img % 16 == 0 && (uintptr_t)out % 16 == 0) {
+    const int64_t nq = n / 4;
+    const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 1 << 16);
+    hipLaunchKernelGGL(repeat_graphs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, img, out, Cin, G, P, nq);
+  } else {
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1 << 16);
+    hipLaunchKernelGGL(repeat_graphs_scalar_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, img, out, Cin,
+                       G, P, n);
+  }
   return launch_status("grr_repeat_graphs");
 }
 

@@ -228,31 +228,48 @@ class MixtureGTVGLR(nn.Module):
         self.GLRmodule01 = GLRFast(n_node_fts, n_graphs, M_diag_init=1.0)
 
     # -- feature maps (a13) --------------------------------------------------
-    def features(self, y: torch.Tensor):
+    @staticmethod
+    def _down(y: torch.Tensor, weight: torch.Tensor, src: Optional[torch.Tensor]) -> torch.Tensor:
+        """2x2/s2 conv of y.  When y is src replicated over the graphs (MultiScaleGraphFilter),
+        the conv of the replicas equals the conv of src with the weights summed over the
+        replicas: K = 4 Cin instead of 4 G Cin (same value up to fp32 summation order)."""
+        if src is None:
+            return K.conv2x2s2(y, weight)
+        m, c = weight.shape[:2]
+        cin = src.shape[1]
+        folded = weight.reshape(m, c // cin, cin, 2, 2).sum(1).contiguous()
+        return K.conv2x2s2(src, folded)
+
+    def features(self, y: torch.Tensor, src: Optional[torch.Tensor] = None):
         s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
         if self.feature_extractor == "v1":
             f0 = K.conv1x1(y, s0[0].weight.data)
-            f1 = K.conv1x1(K.conv2x2s2(y, s1[0].weight.data), s1[1].weight.data)
+            f1 = K.conv1x1(self._down(y, s1[0].weight.data, src), s1[1].weight.data)
             return f0, f1
         f0 = y
         for blk in list(s0)[:3]:
             f0 = blk(f0)
         f0 = K.conv1x1(f0, s0[3].weight.data)
-        f1 = K.conv2x2s2(y, s1[0].weight.data)
+        f1 = self._down(y, s1[0].weight.data, src)
         for blk in list(s1)[1:4]:
             f1 = blk(f1)
         f1 = K.conv1x1(f1, s1[4].weight.data)
         return f0, f1
 
     # -- solver (a3-a17) -----------------------------------------------------
-    def _solve(self, y: torch.Tensor, skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def _solve(self, y: torch.Tensor, skip: Optional[torch.Tensor] = None,
+               src: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """src: optional [B, F, H, W] image that y replicates over the G graphs (y[:, gF + i] =
+        src[:, i]); lets the replicated-input steps run on src."""
         b, c, h, w = y.shape
         g, f = self.n_graphs, self.n_node_fts
         if c != self.n_channels:
             raise ValueError(f"MixtureGTVGLR: expected {self.n_channels} channels, got {c}")
         if h % 2 or w % 2:
             raise ValueError(f"MixtureGTVGLR: H, W must be even for the 2x2 scale (got {h}x{w})")
-        f0, f1 = self.features(y)
+        if src is not None and (src.shape[1] != f or src.shape[0] != b or tuple(src.shape[2:]) != (h, w)):
+            raise ValueError("MixtureGTVGLR: src must be [B, F, H, W]")
+        f0, f1 = self.features(y, src)
         d = lambda p: p.data  # noqa: E731  (parameters are read by the kernels through raw pointers)
         wG0, _ = K.edge_weights(f0, 0, g, f, d(self.GTVmodule00.multiM))
         wL0, _ = K.edge_weights(f0, c, g, f, d(self.GLRmodule00.multiM))
@@ -268,7 +285,9 @@ class MixtureGTVGLR(nn.Module):
         n_st = alpha.shape[0]
 
         # rhs A: b_A = y + ro0 G0 y + ro1 U(G1 D y)                     (REF:738-749)
-        t = K.gtv_rhs_half(K.pool2(y), cG1, sG1, False, None, g)
+        yd = K.pool2(y) if src is None else K.repeat_graphs(K.pool2(src), g)   # D y
+        t = K.gtv_rhs_half(yd, cG1, sG1, False, None, g)
+        del yd
         b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
         # stage 0: x1 = b_A + alpha0 (b_A - A b_A)                     (REF:751-753)
         last = n_st == 1
@@ -293,8 +312,9 @@ class MixtureGTVGLR(nn.Module):
         return x
 
     @hip_forward
-    def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None) -> torch.Tensor:
-        return self._solve(patchs.contiguous(), _skip)
+    def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None,
+                _src: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self._solve(patchs.contiguous(), _skip, None if _src is None else _src.contiguous())
 
 
 class LocalLowpassFilteringBlock(nn.Module):
@@ -328,8 +348,9 @@ class MultiScaleGraphFilter(nn.Module):
 
     @hip_forward
     def forward(self, img):
-        x = K.repeat_graphs(img.contiguous(), self.ngraphs)
-        y = self.localfilter(x)
+        img = img.contiguous()
+        x = K.repeat_graphs(img, self.ngraphs)
+        y = self.localfilter(x, _src=img)
         return K.conv1x1(y, self.linear_combination.weight.data)
 
 

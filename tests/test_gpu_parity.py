@@ -210,6 +210,31 @@ def test_conv2x2s2(irdu, bkmhw):
     assert_close(irdu.kernels.conv2x2s2(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt, stride=2), 1e-5)
 
 
+@pytest.mark.parametrize("bchw", [(2, 3, 16, 20), (1, 3, 5, 7)])   # 16-byte path / scalar path
+def test_repeat_graphs(irdu, bchw):
+    b, c, h, w = bchw
+    img = rand(b, c, h, w, seed=16)
+    got = irdu.kernels.repeat_graphs(img.to(DEV), 5).cpu()
+    assert torch.equal(got, img.repeat(1, 5, 1, 1))
+
+
+def test_replicated_input_folding(irdu):
+    """The image filter runs the 2x2/s2 conv and the pooled rhs on the un-replicated image
+    (weights summed over the G replicas); the result must match the plain replicated path."""
+    torch.manual_seed(3)
+    g = 8
+    mix = irdu.MixtureGTVGLR(g, 3, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]],
+                             n_cgd_iters=4, feature_extractor="v13")
+    perturb_mixture(mix, 7)
+    img = rand(2, 3, 24, 32, seed=17).to(DEV)
+    mix = mix.to(DEV)
+    with torch.no_grad():
+        y = irdu.kernels.repeat_graphs(img, g)
+        plain = mix(y)
+        folded = mix(y, _src=img)
+    assert_close(folded, plain, 1e-5)
+
+
 # (C, hid, H, W): C <= 128 runs the split-bf16 head (32 x 13 / 32 x 9 output tiles with halo
 # recompute) + mix kernels: full / partial tiles, H*W % 4 == 0 (16-byte g DMA) and not (dword
 # DMA), hid % 8 != 0 and hid % 16 != 0 (partial chunk / k-step), C = 33 (partial k-step and
