@@ -37,6 +37,7 @@ class Stencil(ctypes.Structure):
 P = c_void_p
 I = c_int
 L = c_int64
+Fl = ctypes.c_float
 
 # name -> argtypes (restype is grr_status == int unless listed in _RESTYPES)
 SIGNATURES = {
@@ -58,6 +59,18 @@ SIGNATURES = {
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
+    # reverse pass
+    "grr_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
+    "grr_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],
+    "grr_bwd_glr": [P, P, P, P, Fl, P, P, P, P, I, I, I, I, I, P],
+    "grr_bwd_pair": [P, P, P, P, Fl, P, P, P, P, I, I, I, I, I, P],
+    "grr_bwd_prox": [P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_bwd_pair_weights": [P, P, P, I, I, I, I, P],
+    "grr_bwd_edge_weights": [P, L, P, P, P, P, L, P, I, I, I, I, I, P],
+    "grr_bwd_graph_dot": [P, P, Fl, P, I, I, I, I, I, P],
+    "grr_bwd_lincomb": [P, P, P, P, P, I, I, I, I, I, I, P],
+    "grr_bwd_unpool2_acc": [P, P, I, I, I, I, P],
+    "grr_conv2x2s2_bwd_data": [P, P, P, I, I, I, I, I, P],
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64}

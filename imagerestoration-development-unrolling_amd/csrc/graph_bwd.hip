@@ -1,0 +1,627 @@
+// Backward (adjoint) kernels of the GGTV/GGLR solver for training (config C4).
+//
+// The forward solver (graph_ops.hip) fuses whole operator applications into streaming
+// kernels.  Its reverse pass is written here as a small set of per-pixel kernels that
+// the host (irdu_amd/solver_grad.py) composes into the reverse of every operator
+// application (REF = exploration/GGTV_GGLR_v1.0/deep_multiscale_GGLR_GGTV_v1x0.py):
+//
+//   stencil_kernel       S = replicate-pad 3x3 cross correlation (REF:177-195), its
+//                        conv_transpose partner S^T (zero frame, REF:197-215) and the
+//                        exact adjoints of both (4 modes)
+//   tapgrad_kernel       d/d(tap) of S or S^T, reduced per channel
+//   glr_bwd_kernel       reverse of (I - W) inside GLR  (REF:218-237)
+//   pair_bwd_kernel      reverse of the symmetric pair Laplacian inside C^T C (REF:452-523)
+//   prox_bwd_kernel      reverse of C^T phi(C s) with the soft-threshold prox (REF:684-704, :757-781)
+//   pair_weights_bwd     c = w_right^2 + w_left(p+1)^2 ... -> raw edge weights
+//   edge_weights_bwd     softmax + normalise + multiM (REF:146-175)
+//   graph_dot / lincomb / unpool2_acc / conv2x2s2_bwd_data: recurrence and feature-conv glue
+//
+// All are HBM-bound streaming passes with one thread per pixel; the F node features of
+// one graph are looped inside the thread so the graph's edge weights are read once.
+// Reductions (per-graph scalars, per-channel taps, multiM) are accumulated in registers
+// over a grid-strided pixel range, reduced across the wave with DPP shuffles, and folded
+// with one float atomic per wave.
+//
+// Tap order (host computes taps [C,5] from stats_kernel_p01/p02a/p02b/p03):
+//   0 centre (0,0), 1 up (-1,0), 2 left (0,-1), 3 right (0,+1), 4 down (+1,0).
+// Edge order (REF:42-53): 0 up, 1 left, 2 right, 3 down; opposite(e) = 3 - e.
+#include <algorithm>
+
+#include "grr_common.h"
+
+namespace grr {
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAX_CHUNKS = 32;   // pixel chunks per (b, plane) for reduction kernels
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// one atomic per wave (lane 0); every lane of the wave must call it
+__device__ __forceinline__ void wave_atomic_add(float* dst, float v) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(dst, v);
+}
+
+__device__ __forceinline__ bool inside_e(int e, int r, int c, int H, int W) {
+  switch (e) {
+    case 0: return r > 0;
+    case 1: return c > 0;
+    case 2: return c + 1 < W;
+    default: return r + 1 < H;
+  }
+}
+__device__ __forceinline__ int off_e(int e, int W) {
+  switch (e) {
+    case 0: return -W;
+    case 1: return -1;
+    case 2: return 1;
+    default: return W;
+  }
+}
+// tap t: offsets (dy, dx)
+__device__ __forceinline__ int tap_dy(int t) { return t == 1 ? -1 : (t == 4 ? 1 : 0); }
+__device__ __forceinline__ int tap_dx(int t) { return t == 2 ? -1 : (t == 3 ? 1 : 0); }
+
+// ---------------------------------------------------------------------------
+// Stencil apply.  mode 0 P:  y(p) = sum_t k_t x(clamp(p + t))            (S, REF:177-195)
+//                 mode 1 T:  y(q) = sum_t k_t x(q - t) [q - t inside]     (S^T, REF:197-215)
+//                 mode 2 Tt: y(p) = sum_t k_t x(p + t) [p + t inside]     (adjoint of T)
+//                 mode 3 Pt: y(q) = sum_t k_t ([q - t in] x(q - t) + [t != 0, q + t out] x(q))  (adjoint of P)
+// out = (acc ? out : 0) + (scale ? scale[g] : 1) * y.   grid (ceil(HW/NT), B*C).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void stencil_kernel(const float* __restrict__ x, const float* __restrict__ taps,
+                                                     int mode, const float* __restrict__ scale, int acc,
+                                                     float* __restrict__ out, int C, int F, int H, int W) {
+  const int HW = H * W;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  if (p >= HW) return;
+  const int plane = blockIdx.y, ch = plane % C;
+  const int r = p / W, col = p - r * W;
+  const float* xp = x + (int64_t)plane * HW;
+  float k[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) k[t] = taps[ch * 5 + t];
+  float y = 0.f;
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const int dy = tap_dy(t), dx = tap_dx(t);
+    if (mode == 0) {
+      y += k[t] * xp[clampi(r + dy, 0, H - 1) * W + clampi(col + dx, 0, W - 1)];
+    } else if (mode == 1) {
+      const int rr = r - dy, cc = col - dx;
+      if (rr >= 0 && rr < H && cc >= 0 && cc < W) y += k[t] * xp[rr * W + cc];
+    } else if (mode == 2) {
+      const int rr = r + dy, cc = col + dx;
+      if (rr >= 0 && rr < H && cc >= 0 && cc < W) y += k[t] * xp[rr * W + cc];
+    } else {
+      const int rr = r - dy, cc = col - dx;
+      if (rr >= 0 && rr < H && cc >= 0 && cc < W) y += k[t] * xp[rr * W + cc];
+      const int ro = r + dy, co = col + dx;
+      if (t != 0 && (ro < 0 || ro >= H || co < 0 || co >= W)) y += k[t] * xp[p];
+    }
+  }
+  if (scale) y *= scale[ch / F];
+  float* o = out + (int64_t)plane * HW + p;
+  *o = acc ? *o + y : y;
+}
+
+// Tap gradients of y = mode(z) contracted with u: gt[c, t] += scale[g] * sum_{b,q} u(q) dy(q)/dk_t.
+// mode 0 (P): dy(q)/dk_t = z(clamp(q + t));  mode 1 (T): z(q - t) [inside].   grid (chunks, B*C).
+__global__ __launch_bounds__(NT) void tapgrad_kernel(const float* __restrict__ u, const float* __restrict__ z,
+                                                     int mode, const float* __restrict__ scale,
+                                                     float* __restrict__ gt, int C, int F, int H, int W) {
+  const int HW = H * W;
+  const int plane = blockIdx.y, ch = plane % C;
+  const float* up = u + (int64_t)plane * HW;
+  const float* zp = z + (int64_t)plane * HW;
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = blockIdx.x * NT + threadIdx.x; p < HW; p += gridDim.x * NT) {
+    const int r = p / W, col = p - r * W;
+    const float uv = up[p];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int dy = tap_dy(t), dx = tap_dx(t);
+      if (mode == 0) {
+        acc[t] += uv * zp[clampi(r + dy, 0, H - 1) * W + clampi(col + dx, 0, W - 1)];
+      } else {
+        const int rr = r - dy, cc = col - dx;
+        if (rr >= 0 && rr < H && cc >= 0 && cc < W) acc[t] += uv * zp[rr * W + cc];
+      }
+    }
+  }
+  const float sc = scale ? scale[ch / F] : 1.f;
+#pragma unroll
+  for (int t = 0; t < 5; ++t) wave_atomic_add(gt + ch * 5 + t, sc * acc[t]);
+}
+
+// ---------------------------------------------------------------------------
+// GLR reverse.  Forward inside GLR: z = (I - W) s,  (W s)(p) = sum_e w_e(p) s(nb_e(p)),
+// nb_e(p) = clamp(p + delta_e) (REF:218-237).  Given s = P x and a = Tt(g):
+//   z_out  = (I - W) s                      (for the T-tap gradient)
+//   ap_out = (I - W)^T a                    (then x-gradient = Pt(ap), P-tap gradient)
+//   gw[e](p) += scale[g] * (-sum_f a_f(p) s_f(nb_e p))
+//   gdot[g]  += coef * sum a . z            (d/d mu of <g, T z>)
+// grid (ceil(HW/NT), B*G)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void glr_bwd_kernel(const float* __restrict__ s, const float* __restrict__ a,
+                                                     const float* __restrict__ w, const float* __restrict__ scale,
+                                                     float coef, float* __restrict__ z_out,
+                                                     float* __restrict__ ap_out, float* __restrict__ gw,
+                                                     float* __restrict__ gdot, int G, int F, int H, int W) {
+  const int HW = H * W;
+  const int bg = blockIdx.y, g = bg % G;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  float dot = 0.f;
+  if (p < HW) {
+    const int r = p / W, col = p - r * W;
+    const float* wb = w + (int64_t)bg * 4 * HW;
+    float we[4], wn[4];
+    bool in[4];
+    int nb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      in[e] = inside_e(e, r, col, H, W);
+      nb[e] = in[e] ? p + off_e(e, W) : p;
+      we[e] = wb[e * HW + p];
+    }
+    // w_e(p - delta_e) = w of edge e at the opposite neighbour (exists iff that neighbour is inside)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wn[e] = in[3 - e] ? wb[e * HW + nb[3 - e]] : 0.f;
+    float gwa[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < F; ++f) {
+      const int64_t base = ((int64_t)bg * F + f) * HW;
+      const float* sp = s + base;
+      const float* ap = a + base;
+      const float sv = sp[p], av = ap[p];
+      float z = sv, wta = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sn = sp[nb[e]];
+        z -= we[e] * sn;
+        gwa[e] -= av * sn;
+        wta += in[3 - e] ? wn[e] * ap[nb[3 - e]] : 0.f;   // scatter-adjoint, interior part
+        wta += in[e] ? 0.f : we[e] * av;                  // clamped (self) reads at the frame
+      }
+      z_out[base + p] = z;
+      ap_out[base + p] = av - wta;
+      dot += av * z;
+    }
+    const float sc = scale ? scale[g] : 1.f;
+    float* gwb = gw + (int64_t)bg * 4 * HW + p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gwb[e * HW] += sc * gwa[e];
+  }
+  if (gdot) wave_atomic_add(gdot + g, coef * dot);
+}
+
+// Pair-Laplacian reverse (GTV C^T C, linear part).  K s(p) = sum over the 4 incident edges
+// of c_edge (s(p) - s(other)); c[0] = edge (p, p+right), c[1] = edge (p, p+down).  K is
+// symmetric, so ap_out = K a.  gc[d](p) += scale[g] sum_f (a(p) - a(p+d)) (s(p) - s(p+d)).
+__global__ __launch_bounds__(NT) void pair_bwd_kernel(const float* __restrict__ s, const float* __restrict__ a,
+                                                      const float* __restrict__ cw, const float* __restrict__ scale,
+                                                      float coef, float* __restrict__ z_out,
+                                                      float* __restrict__ ap_out, float* __restrict__ gc,
+                                                      float* __restrict__ gdot, int G, int F, int H, int W) {
+  const int HW = H * W;
+  const int bg = blockIdx.y, g = bg % G;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  float dot = 0.f;
+  if (p < HW) {
+    const int r = p / W, col = p - r * W;
+    const float* cb = cw + (int64_t)bg * 2 * HW;
+    const bool hr = col + 1 < W, hl = col > 0, vd = r + 1 < H, vu = r > 0;
+    const float cr = hr ? cb[p] : 0.f, cl = hl ? cb[p - 1] : 0.f;
+    const float cd = vd ? cb[HW + p] : 0.f, cu = vu ? cb[HW + p - W] : 0.f;
+    const int pr = hr ? p + 1 : p, pl = hl ? p - 1 : p, pd = vd ? p + W : p, pu = vu ? p - W : p;
+    float gh = 0.f, gv = 0.f;
+    for (int f = 0; f < F; ++f) {
+      const int64_t base = ((int64_t)bg * F + f) * HW;
+      const float* sp = s + base;
+      const float* ap = a + base;
+      const float sv = sp[p], av = ap[p];
+      const float sr = sp[pr], sl = sp[pl], sd = sp[pd], su = sp[pu];
+      const float ar = ap[pr], al = ap[pl], ad = ap[pd], au = ap[pu];
+      const float z = cr * (sv - sr) + cl * (sv - sl) + cd * (sv - sd) + cu * (sv - su);
+      const float ka = cr * (av - ar) + cl * (av - al) + cd * (av - ad) + cu * (av - au);
+      z_out[base + p] = z;
+      ap_out[base + p] = ka;
+      gh += (av - ar) * (sv - sr);
+      gv += (av - ad) * (sv - sd);
+      dot += av * z;
+    }
+    const float sc = scale ? scale[g] : 1.f;
+    float* gcb = gc + (int64_t)bg * 2 * HW + p;
+    if (hr) gcb[0] += sc * gh;
+    if (vd) gcb[HW] += sc * gv;
+  }
+  if (gdot) wave_atomic_add(gdot + g, coef * dot);
+}
+
+// ---------------------------------------------------------------------------
+// Prox reverse: o = Ct(phi(C s)) before the final S^T, with
+//   t_e(p) = w_e(p) (s(p) - s(p + delta_e))  (0 when p + delta_e is outside)      REF:452-467
+//   phi(t) = 2 soft(t, gamma) - t,  soft = the reference's two wheres               REF:684-704, :766-771
+//   o(q)   = sum_e w_e(q) phi_e(q) - sum_e [q - delta_e in] w_e(q - delta_e) phi_e(q - delta_e)   REF:469-516
+// Given a = Tt(g):
+//   o_out(q), gs_out(q) = d<a, o>/ds(q),  gw[e](q) += scale * d<a,o>/dw_e(q),
+//   ggam[g] += scale * d<a,o>/dgamma,     gdot[g] += coef * <a, o>
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float soft_t(float t, float gm) { return t < -gm ? t + gm : (t > gm ? t - gm : 0.f); }
+
+__global__ __launch_bounds__(NT) void prox_bwd_kernel(const float* __restrict__ s, const float* __restrict__ a,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ log_gamma,
+                                                      const float* __restrict__ scale, float coef,
+                                                      float* __restrict__ o_out, float* __restrict__ gs_out,
+                                                      float* __restrict__ gw, float* __restrict__ ggam,
+                                                      float* __restrict__ gdot, int G, int F, int H, int W) {
+  const int HW = H * W;
+  const int bg = blockIdx.y, g = bg % G;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  float dot = 0.f, dgam = 0.f;
+  const float gm = expf(log_gamma[g]);
+  if (p < HW) {
+    const int r = p / W, col = p - r * W;
+    const float* wb = w + (int64_t)bg * 4 * HW;
+    float we[4], wn[4];
+    bool in[4];
+    int nb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      in[e] = inside_e(e, r, col, H, W);
+      nb[e] = in[e] ? p + off_e(e, W) : p;
+      we[e] = wb[e * HW + p];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wn[e] = in[3 - e] ? wb[e * HW + nb[3 - e]] : 0.f;   // w_e(p - delta_e)
+    float gwa[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < F; ++f) {
+      const int64_t base = ((int64_t)bg * F + f) * HW;
+      const float* sp = s + base;
+      const float* ap = a + base;
+      const float sv = sp[p], av = ap[p];
+      float o = 0.f, gs = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // edge e leaving p
+        if (in[e]) {
+          const float sn = sp[nb[e]], an = ap[nb[e]];
+          const float ds = sv - sn, t = we[e] * ds;
+          const float ph = 2.f * soft_t(t, gm) - t;
+          const float da = av - an;
+          const float gph = we[e] * da;
+          const bool beyond = t < -gm || t > gm;
+          const float gt = beyond ? gph : -gph;
+          o += we[e] * ph;
+          gs += gt * we[e];
+          gwa[e] += ph * da + gt * ds;
+          dgam += gph * (t < -gm ? 2.f : (t > gm ? -2.f : 0.f));
+        }   // else t = 0, phi = 0: no contribution to o, w or gamma
+        // edge e arriving at p from q' = p - delta_e (neighbour in direction 3-e)
+        if (in[3 - e]) {
+          const int q = nb[3 - e];
+          const float sq = sp[q], aq = ap[q];
+          const float t = wn[e] * (sq - sv);
+          const float ph = 2.f * soft_t(t, gm) - t;
+          const float gph = wn[e] * (aq - av);
+          const bool beyond = t < -gm || t > gm;
+          const float gt = beyond ? gph : -gph;
+          o -= wn[e] * ph;
+          gs -= gt * wn[e];
+        }
+      }
+      o_out[base + p] = o;
+      gs_out[base + p] = gs;
+      dot += av * o;
+    }
+    const float sc = scale ? scale[g] : 1.f;
+    float* gwb = gw + (int64_t)bg * 4 * HW + p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gwb[e * HW] += sc * gwa[e];
+    dgam *= sc;
+  }
+  if (gdot) wave_atomic_add(gdot + g, coef * dot);
+  if (ggam) wave_atomic_add(ggam + g, dgam);
+}
+
+// c[0](p) = w_right(p)^2 + w_left(p+1)^2, c[1](p) = w_down(p)^2 + w_up(p+W)^2 (0 at the frame):
+// gw[right](p) += 2 w_right(p) gc0(p);  gw[left](q) += 2 w_left(q) gc0(q-1);
+// gw[down](p)  += 2 w_down(p) gc1(p);   gw[up](q)   += 2 w_up(q) gc1(q-W).      grid (ceil(HW/NT), B*G)
+__global__ __launch_bounds__(NT) void pair_weights_bwd_kernel(const float* __restrict__ w, const float* __restrict__ gc,
+                                                              float* __restrict__ gw, int H, int W) {
+  const int HW = H * W;
+  const int bg = blockIdx.y;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  if (p >= HW) return;
+  const int r = p / W, col = p - r * W;
+  const float* wb = w + (int64_t)bg * 4 * HW;
+  const float* gcb = gc + (int64_t)bg * 2 * HW;
+  float* gwb = gw + (int64_t)bg * 4 * HW;
+  if (r > 0) gwb[p] += 2.f * wb[p] * gcb[HW + p - W];
+  if (col > 0) gwb[HW + p] += 2.f * wb[HW + p] * gcb[p - 1];
+  if (col + 1 < W) gwb[2 * HW + p] += 2.f * wb[2 * HW + p] * gcb[p];
+  if (r + 1 < H) gwb[3 * HW + p] += 2.f * wb[3 * HW + p] * gcb[HW + p];
+}
+
+// ---------------------------------------------------------------------------
+// Edge-weight reverse (REF:146-175): fh_f = M_f f_f / max(|f|, 1e-12);
+// sim_e(p) = sum_f fh_f(p) fh_f(nb_e p);  w = softmax_e(sim).
+//   gsim_e(p) = w_e(p) (gw_e(p) - sum_e' w_e'(p) gw_e'(p))
+//   gfh_f(q)  = sum_e gsim_e(q) fh_f(nb_e q) + sum_e [q - delta_e in] gsim_e(q - delta_e) fh_f(q - delta_e)
+//             + sum_e [q + delta_e out] gsim_e(q) fh_f(q)
+//   gM[g,f]  += gfh_f n_f ;  gf = (gn - n (n . gn)) / |f|  (gn / eps below eps), gn = M gfh
+// feat / gfeat: channel-0 pointers of the module's [G*F] slab, batch strides in elements.
+// grid (chunks, B*G)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float inv_den(const float* fp, int64_t HW, int F, int p) {
+  float ss = 0.f;
+  for (int f = 0; f < F; ++f) {
+    const float v = fp[f * HW + p];
+    ss += v * v;
+  }
+  return 1.f / fmaxf(sqrtf(ss), 1e-12f);
+}
+__device__ __forceinline__ float gsim_at(const float* wb, const float* gwb, int64_t HW, int e, int p) {
+  const float w0 = wb[p], w1 = wb[HW + p], w2 = wb[2 * HW + p], w3 = wb[3 * HW + p];
+  const float s = w0 * gwb[p] + w1 * gwb[HW + p] + w2 * gwb[2 * HW + p] + w3 * gwb[3 * HW + p];
+  return wb[e * HW + p] * (gwb[e * HW + p] - s);
+}
+
+__global__ __launch_bounds__(NT) void edge_weights_bwd_kernel(const float* __restrict__ feat, int64_t fstride,
+                                                              const float* __restrict__ multiM,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ gw,
+                                                              float* __restrict__ gfeat, int64_t gstride,
+                                                              float* __restrict__ gM, int G, int F, int H, int W) {
+  const int HW = H * W;
+  const int bg = blockIdx.y, g = bg % G, b = bg / G;
+  const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW;
+  float* gfp = gfeat + (int64_t)b * gstride + (int64_t)g * F * HW;
+  const float* wb = w + (int64_t)bg * 4 * HW;
+  const float* gwb = gw + (int64_t)bg * 4 * HW;
+  const float* M = multiM + g * F;
+  // per-thread multiM gradient partials in LDS (F <= GRR_MAX_NODE_FTS), reduced once per block
+  __shared__ float gm_sm[GRR_MAX_NODE_FTS * NT];
+  for (int f = 0; f < F; ++f) gm_sm[f * NT + threadIdx.x] = 0.f;
+  for (int p = blockIdx.x * NT + threadIdx.x; p < HW; p += gridDim.x * NT) {
+    const int r = p / W, col = p - r * W;
+    bool in[4];
+    int nb[4];
+    float inb[4], gs_out[4], gs_in[4];
+    const float ic = inv_den(fp, HW, F, p);
+    float gsum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      in[e] = inside_e(e, r, col, H, W);
+      nb[e] = in[e] ? p + off_e(e, W) : p;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      inb[e] = in[e] ? inv_den(fp, HW, F, nb[e]) : ic;
+      gs_out[e] = gsim_at(wb, gwb, HW, e, p);
+      // gsim of edge e at q' = p - delta_e (the neighbour in direction 3-e), whose e-neighbour is p
+      gs_in[e] = in[3 - e] ? gsim_at(wb, gwb, HW, e, nb[3 - e]) : 0.f;
+      gsum += in[e] ? 0.f : gs_out[e];          // self term at the frame
+    }
+    // pass A: n . gn
+    float ndg = 0.f;
+    for (int f = 0; f < F; ++f) {
+      const float* ff = fp + (int64_t)f * HW;
+      const float m = M[f];
+      const float n = ff[p] * ic;
+      float gfh = gsum * n * m;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gfh += gs_out[e] * ff[nb[e]] * inb[e] * m;
+        if (in[3 - e]) gfh += gs_in[e] * ff[nb[3 - e]] * inb[3 - e] * m;
+      }
+      gm_sm[f * NT + threadIdx.x] += gfh * n;
+      ndg += n * (gfh * m);
+    }
+    // pass B: gf
+    const bool small = 1.f / ic <= 1e-12f;
+    for (int f = 0; f < F; ++f) {
+      const float* ff = fp + (int64_t)f * HW;
+      const float m = M[f];
+      const float n = ff[p] * ic;
+      float gfh = gsum * n * m;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gfh += gs_out[e] * ff[nb[e]] * inb[e] * m;
+        if (in[3 - e]) gfh += gs_in[e] * ff[nb[3 - e]] * inb[3 - e] * m;
+      }
+      const float gn = gfh * m;
+      gfp[(int64_t)f * HW + p] = small ? gn * ic : (gn - n * ndg) * ic;
+    }
+  }
+  for (int f = 0; f < F; ++f) wave_atomic_add(gM + g * F + f, gm_sm[f * NT + threadIdx.x]);
+}
+
+// gdot[g] += coef * sum_{b,f,p} u v.      grid (chunks, B*G)
+__global__ __launch_bounds__(NT) void graph_dot_kernel(const float* __restrict__ u, const float* __restrict__ v,
+                                                       float coef, float* __restrict__ gdot, int G, int F,
+                                                       int64_t HW) {
+  const int bg = blockIdx.y, g = bg % G;
+  const int64_t n = (int64_t)F * HW;
+  const float* up = u + (int64_t)bg * n;
+  const float* vp = v + (int64_t)bg * n;
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) acc += up[i] * vp[i];
+  wave_atomic_add(gdot + g, coef * acc);
+}
+
+// out = sa[g] * x + sb[g] * y  (sa/sb NULL -> 1; y NULL -> term dropped); acc: out += ...
+__global__ __launch_bounds__(NT) void lincomb_kernel(const float* __restrict__ x, const float* __restrict__ sa,
+                                                     const float* __restrict__ y, const float* __restrict__ sb,
+                                                     float* __restrict__ out, int acc, int C, int F, int64_t HW,
+                                                     int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int g = (int)((i / HW) % C) / F;
+    float v = (sa ? sa[g] : 1.f) * x[i];
+    if (y) v += (sb ? sb[g] : 1.f) * y[i];
+    out[i] = acc ? out[i] + v : v;
+  }
+}
+
+// out(q) += 0.25 * xd(q / 2)   (U = conv_transpose2d of the 0.25 2x2 kernel, stride 2; REF:676-679)
+__global__ __launch_bounds__(NT) void unpool2_acc_kernel(const float* __restrict__ xd, float* __restrict__ out, int H,
+                                                         int W, int64_t n) {
+  const int h = H / 2, w = W / 2;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int64_t plane = i / ((int64_t)H * W);
+    const int p = (int)(i - plane * H * W);
+    const int r = p / W, c = p - r * W;
+    out[i] += 0.25f * xd[plane * h * w + (r >> 1) * w + (c >> 1)];
+  }
+}
+
+// data gradient of the 2x2 stride-2 conv (REF:593-602):
+// gx[b,k,2i+di,2j+dj] = sum_m wt[m,k,di,dj] g[b,m,i,j]
+__global__ __launch_bounds__(NT) void conv2x2s2_bwd_data_kernel(const float* __restrict__ g,
+                                                                const float* __restrict__ wt,
+                                                                float* __restrict__ gx, int K, int M, int H, int W) {
+  const int HW = H * W, h = H / 2, w = W / 2;
+  const int p = blockIdx.x * NT + threadIdx.x;
+  if (p >= HW) return;
+  const int bk = blockIdx.y, b = bk / K, k = bk % K;
+  const int r = p / W, c = p - r * W;
+  const int tap = (r & 1) * 2 + (c & 1);
+  const float* gp = g + (int64_t)b * M * h * w + (r >> 1) * w + (c >> 1);
+  float acc = 0.f;
+  for (int m = 0; m < M; ++m) acc += wt[(m * K + k) * 4 + tap] * gp[(int64_t)m * h * w];
+  gx[(int64_t)bk * HW + p] = acc;
+}
+
+int chunks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, MAX_CHUNKS); }
+int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
+
+}  // namespace
+}  // namespace grr
+
+using namespace grr;
+
+extern "C" {
+
+grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,
+                           float* out, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && taps && out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 && mode >= 0 && mode <= 3,
+              GRR_ERR_INVALID_ARG, "grr_bwd_stencil: bad args");
+  const int C = G * F;
+  GRR_REQUIRE((int64_t)B * C < 65536 * 16 && (int64_t)H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_bwd_stencil: grid too large");
+  hipLaunchKernelGGL(stencil_kernel, dim3((H * W + NT - 1) / NT, B * C), dim3(NT), 0, (hipStream_t)stream, x, taps,
+                     mode, scale, accumulate, out, C, F, H, W);
+  return launch_status("grr_bwd_stencil");
+}
+
+grr_status grr_bwd_tapgrad(const float* u, const float* z, int mode, const float* scale, float* gtaps, int B, int G,
+                           int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(u && z && gtaps && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 && (mode == 0 || mode == 1),
+              GRR_ERR_INVALID_ARG, "grr_bwd_tapgrad: bad args");
+  hipLaunchKernelGGL(tapgrad_kernel, dim3(chunks_for((int64_t)H * W), B * G * F), dim3(NT), 0, (hipStream_t)stream, u,
+                     z, mode, scale, gtaps, G * F, F, H, W);
+  return launch_status("grr_bwd_tapgrad");
+}
+
+grr_status grr_bwd_glr(const float* s, const float* a, const float* w, const float* scale, float coef, float* z_out,
+                       float* ap_out, float* gw, float* gdot, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(s && a && w && z_out && ap_out && gw && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_bwd_glr: bad args");
+  hipLaunchKernelGGL(glr_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
+                     scale, coef, z_out, ap_out, gw, gdot, G, F, H, W);
+  return launch_status("grr_bwd_glr");
+}
+
+grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const float* scale, float coef, float* z_out,
+                        float* ap_out, float* gc, float* gdot, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(s && a && c && z_out && ap_out && gc && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_bwd_pair: bad args");
+  hipLaunchKernelGGL(pair_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, c,
+                     scale, coef, z_out, ap_out, gc, gdot, G, F, H, W);
+  return launch_status("grr_bwd_pair");
+}
+
+grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const float* log_gamma, const float* scale,
+                        float coef, float* o_out, float* gs_out, float* gw, float* ggamma, float* gdot, int B, int G,
+                        int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(s && a && w && log_gamma && o_out && gs_out && gw && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_bwd_prox: bad args");
+  hipLaunchKernelGGL(prox_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
+                     log_gamma, scale, coef, o_out, gs_out, gw, ggamma, gdot, G, F, H, W);
+  return launch_status("grr_bwd_prox");
+}
+
+grr_status grr_bwd_pair_weights(const float* w, const float* gc, float* gw, int B, int G, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(w && gc && gw && B > 0 && G > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
+              "grr_bwd_pair_weights: bad args");
+  hipLaunchKernelGGL(pair_weights_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, w,
+                     gc, gw, H, W);
+  return launch_status("grr_bwd_pair_weights");
+}
+
+grr_status grr_bwd_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM, const float* w,
+                                const float* gw, float* gfeat, int64_t gfeat_bstride, float* gmultiM, int B, int G,
+                                int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(feat && multiM && w && gw && gfeat && gmultiM && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_bwd_edge_weights: bad args");
+  GRR_REQUIRE(F <= GRR_MAX_NODE_FTS, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: F=%d > %d", F, GRR_MAX_NODE_FTS);
+  hipLaunchKernelGGL(edge_weights_bwd_kernel, dim3(chunks_for((int64_t)H * W), B * G), dim3(NT), 0,
+                     (hipStream_t)stream, feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, G, F, H,
+                     W);
+  return launch_status("grr_bwd_edge_weights");
+}
+
+grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* gdot, int B, int G, int F, int H,
+                             int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(u && v && gdot && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
+              "grr_bwd_graph_dot: bad args");
+  hipLaunchKernelGGL(graph_dot_kernel, dim3(chunks_for((int64_t)F * H * W), B * G), dim3(NT), 0, (hipStream_t)stream,
+                     u, v, coef, gdot, G, F, (int64_t)H * W);
+  return launch_status("grr_bwd_graph_dot");
+}
+
+grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,
+                           int accumulate, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
+              "grr_bwd_lincomb: bad args");
+  const int64_t HW = (int64_t)H * W, n = (int64_t)B * G * F * HW;
+  hipLaunchKernelGGL(lincomb_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, x, sa, y, sb, out,
+                     accumulate, G * F, F, HW, n);
+  return launch_status("grr_bwd_lincomb");
+}
+
+grr_status grr_bwd_unpool2_acc(const float* xd, float* out, int B, int C, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(xd && out && B > 0 && C > 0 && H > 1 && W > 1, GRR_ERR_INVALID_ARG, "grr_bwd_unpool2_acc: bad args");
+  GRR_REQUIRE(H % 2 == 0 && W % 2 == 0, GRR_ERR_SHAPE, "grr_bwd_unpool2_acc: H, W must be even");
+  const int64_t n = (int64_t)B * C * H * W;
+  hipLaunchKernelGGL(unpool2_acc_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, xd, out, H, W, n);
+  return launch_status("grr_bwd_unpool2_acc");
+}
+
+grr_status grr_conv2x2s2_bwd_data(const float* g, const float* wt, float* gx, int B, int K, int M, int H, int W,
+                                  void* stream) {
+  clear_error();
+  GRR_REQUIRE(g && wt && gx && B > 0 && K > 0 && M > 0 && H > 1 && W > 1, GRR_ERR_INVALID_ARG,
+              "grr_conv2x2s2_bwd_data: bad args");
+  GRR_REQUIRE(H % 2 == 0 && W % 2 == 0, GRR_ERR_SHAPE, "grr_conv2x2s2_bwd_data: H, W must be even");
+  GRR_REQUIRE((int64_t)B * K < 65536 * 16, GRR_ERR_UNSUPPORTED, "grr_conv2x2s2_bwd_data: grid too large");
+  hipLaunchKernelGGL(conv2x2s2_bwd_data_kernel, dim3((H * W + NT - 1) / NT, B * K), dim3(NT), 0, (hipStream_t)stream,
+                     g, wt, gx, K, M, H, W);
+  return launch_status("grr_conv2x2s2_bwd_data");
+}
+
+}  // extern "C"

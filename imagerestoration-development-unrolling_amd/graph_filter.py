@@ -9,9 +9,11 @@ edge_delta, pad_dim_hw — REF:52-118, :613) become non-persistent buffers: they
 follow ``.to()`` and stay out of the state_dict, as in the reference.
 
 Forward passes of the graph filter run only through the HIP kernels (kernels.py);
-GPU tensors are required.  Backward kernels are not part of this build yet: the
-solver is wrapped in an autograd Function whose backward raises, so training can
-never silently skip gradients.
+GPU tensors are required.  When autograd records (training), MixtureGTVGLR and the
+filter blocks switch to the differentiable path of solver_grad.py (HIP forward that
+keeps the iterates + hand-written HIP reverse sweep).  Entry points without a reverse
+kernel yet (the GLRFast/GTVFast sub-API) attach a node whose backward raises, so
+training can never silently skip gradients.
 """
 from __future__ import annotations
 
@@ -22,6 +24,7 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
+from . import solver_grad as SG
 
 EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, down)
 
@@ -36,6 +39,12 @@ class _NoBackward(torch.autograd.Function):
     def backward(ctx, *grads):
         raise NotImplementedError("irdu_amd: HIP backward kernels are not built yet; "
                                   "run the graph filter under torch.no_grad()")
+
+
+def records_grad(module: nn.Module, *tensors) -> bool:
+    """True when autograd would record this call (training)."""
+    return torch.is_grad_enabled() and (any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors)
+                                        or any(p.requires_grad for p in module.parameters()))
 
 
 def hip_forward(fn):
@@ -163,8 +172,9 @@ class LocalNonLinearBlock(nn.Module):
         self.skip_weight = Parameter(torch.tensor([1.0, 1.0], dtype=torch.float32))
 
     def forward(self, x):
-        if self.nsubnets != 1:
-            # grouped variant: only used by encoder/decoder configs (out of the hot path)
+        if self.nsubnets != 1 or records_grad(self, x):
+            # grouped variant (encoder/decoder configs) and the training path: stock PyTorch-ROCm
+            # ops (the fused HIP block has no reverse kernel yet)
             return self.skip_weight[0] * x + self.skip_weight[1] * self.local_linear(self.norm(x))
         return self._forward_hip(x)
 
@@ -256,6 +266,23 @@ class MixtureGTVGLR(nn.Module):
         f1 = K.conv1x1(f1, s1[4].weight.data)
         return f0, f1
 
+    def features_train(self, y: torch.Tensor):
+        """Differentiable feature maps (training): HIP convs with autograd reverses."""
+        s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
+        if self.feature_extractor == "v1":
+            f0 = SG.Conv1x1Fn.apply(y, s0[0].weight)
+            f1 = SG.Conv1x1Fn.apply(SG.Conv2x2s2Fn.apply(y, s1[0].weight), s1[1].weight)
+            return f0, f1
+        f0 = y
+        for blk in list(s0)[:3]:
+            f0 = blk(f0)
+        f0 = SG.Conv1x1Fn.apply(f0.contiguous(), s0[3].weight)
+        f1 = SG.Conv2x2s2Fn.apply(y, s1[0].weight)
+        for blk in list(s1)[1:4]:
+            f1 = blk(f1)
+        f1 = SG.Conv1x1Fn.apply(f1.contiguous(), s1[4].weight)
+        return f0, f1
+
     # -- solver (a3-a17) -----------------------------------------------------
     def _solve(self, y: torch.Tensor, skip: Optional[torch.Tensor] = None,
                src: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -311,10 +338,19 @@ class MixtureGTVGLR(nn.Module):
                                      skip=skip if last else None, y_skip=y if last else None, u_out=u)
         return x
 
-    @hip_forward
     def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None,
                 _src: Optional[torch.Tensor] = None) -> torch.Tensor:
-        return self._solve(patchs.contiguous(), _skip, None if _src is None else _src.contiguous())
+        if records_grad(self, patchs, _skip):
+            y = patchs.contiguous()
+            b, c, h, w = y.shape
+            if c != self.n_channels or h % 2 or w % 2:
+                raise ValueError(f"MixtureGTVGLR: expected [B,{self.n_channels},H,W] with even H, W, "
+                                 f"got {tuple(y.shape)}")
+            f0, f1 = self.features_train(y)
+            x = SG.mixture_solve(self, y, f0, f1)
+            return x if _skip is None else _skip[0] * y + _skip[1] * x
+        with torch.no_grad():
+            return self._solve(patchs.contiguous(), _skip, None if _src is None else _src.contiguous())
 
 
 class LocalLowpassFilteringBlock(nn.Module):
@@ -329,6 +365,8 @@ class LocalLowpassFilteringBlock(nn.Module):
         self.skip_weight = Parameter(torch.tensor([0.5, 0.5], dtype=torch.float32))
 
     def forward(self, x):
+        if records_grad(self, x):
+            return self.local_filter(x, _skip=self.skip_weight)
         return self.local_filter(x, _skip=self.skip_weight.data)
 
 
@@ -346,9 +384,15 @@ class MultiScaleGraphFilter(nn.Module):
             gamma_init=torch.tensor([[0.0001], [0.0001]]), n_cgd_iters=n_cgd_iters, feature_extractor="v13")
         self.linear_combination = nn.Conv2d(ngraphs * n_channels_in, n_channels_out, 1, bias=False)
 
-    @hip_forward
     def forward(self, img):
         img = img.contiguous()
+        if records_grad(self, img):
+            y = self.localfilter(SG.RepeatGraphsFn.apply(img, self.ngraphs))
+            return SG.Conv1x1Fn.apply(y.contiguous(), self.linear_combination.weight)
+        return self._forward_inference(img)
+
+    @torch.no_grad()
+    def _forward_inference(self, img):
         x = K.repeat_graphs(img, self.ngraphs)
         y = self.localfilter(x, _src=img)
         return K.conv1x1(y, self.linear_combination.weight.data)

@@ -273,3 +273,132 @@ def repeat_graphs(img: Tensor, n_graphs: int) -> Tensor:
     _launch("repeat_graphs", 4 * b * h * w * cin * (1 + n_graphs), "grr_repeat_graphs", img.data_ptr(),
             out.data_ptr(), b, cin, n_graphs, h * w, _stream(dev))
     return out
+
+
+# ---- reverse pass (training) ------------------------------------------------
+# Modes of grr_bwd_stencil / grr_bwd_tapgrad
+ST_P, ST_T, ST_T_ADJ, ST_P_ADJ = 0, 1, 2, 3
+
+
+def stencil_taps(p01: Tensor, p02a: Tensor, p02b: Tensor, p03: Tensor) -> Tensor:
+    """[C,5] taps (centre, up, left, right, down) of the 3x3 cross stencil
+    p01*k01 + p02a*k02a + p02b*k02b + p03*k03 (REF:56-118, :178-183)."""
+    a, b, c, d = (t.reshape(-1) for t in (p01, p02a, p02b, p03))
+    return torch.stack([a - b - c + 4 * d, -d, -d, b - d, c - d], dim=1).contiguous()
+
+
+def stencil_taps_backward(gt: Tensor):
+    """Chain [C,5] tap gradients back to (p01, p02a, p02b, p03) gradients, each [C,1,1,1]."""
+    dc, du, dl, dr, dd = gt.unbind(1)
+    out = (dc, dr - dc, dd - dc, 4 * dc - du - dl - dr - dd)
+    return tuple(t.reshape(-1, 1, 1, 1) for t in out)
+
+
+def _bgfhw(x: Tensor, n_graphs: int):
+    b, c, h, w = x.shape
+    if c % n_graphs:
+        raise ValueError(f"{c} channels not divisible by {n_graphs} graphs")
+    return b, n_graphs, c // n_graphs, h, w
+
+
+def bwd_stencil(x: Tensor, taps: Tensor, mode: int, n_graphs: int, scale: Optional[Tensor] = None,
+                out: Optional[Tensor] = None) -> Tensor:
+    """out = [out +] scale[g] * mode(x)  (out given -> accumulate)."""
+    dev = _check("bwd_stencil", x, taps, scale, out)
+    acc = out is not None
+    if out is None:
+        out = torch.empty_like(x)
+    _launch("bwd_stencil", 4 * x.numel() * (3 if acc else 2), "grr_bwd_stencil", x.data_ptr(), taps.data_ptr(), mode,
+            _ptr(scale), int(acc), out.data_ptr(), *_bgfhw(x, n_graphs), _stream(dev))
+    return out
+
+
+def bwd_tapgrad(u: Tensor, z: Tensor, mode: int, n_graphs: int, scale: Optional[Tensor], gtaps: Tensor) -> None:
+    dev = _check("bwd_tapgrad", u, z, scale, gtaps)
+    _launch("bwd_tapgrad", 8 * u.numel(), "grr_bwd_tapgrad", u.data_ptr(), z.data_ptr(), mode, _ptr(scale),
+            gtaps.data_ptr(), *_bgfhw(u, n_graphs), _stream(dev))
+
+
+def bwd_glr(s: Tensor, a: Tensor, w: Tensor, scale: Tensor, coef: float, gw: Tensor, gdot: Tensor, n_graphs: int):
+    dev = _check("bwd_glr", s, a, w, scale, gw, gdot)
+    z, ap = torch.empty_like(s), torch.empty_like(s)
+    _launch("bwd_glr", 4 * (4 * s.numel() + 3 * w.numel()), "grr_bwd_glr", s.data_ptr(), a.data_ptr(), w.data_ptr(),
+            scale.data_ptr(), float(coef), z.data_ptr(), ap.data_ptr(), gw.data_ptr(), gdot.data_ptr(),
+            *_bgfhw(s, n_graphs), _stream(dev))
+    return z, ap
+
+
+def bwd_pair(s: Tensor, a: Tensor, c: Tensor, scale: Tensor, coef: float, gc: Tensor, gdot: Tensor, n_graphs: int):
+    dev = _check("bwd_pair", s, a, c, scale, gc, gdot)
+    z, ap = torch.empty_like(s), torch.empty_like(s)
+    _launch("bwd_pair", 4 * (4 * s.numel() + 3 * c.numel()), "grr_bwd_pair", s.data_ptr(), a.data_ptr(), c.data_ptr(),
+            scale.data_ptr(), float(coef), z.data_ptr(), ap.data_ptr(), gc.data_ptr(), gdot.data_ptr(),
+            *_bgfhw(s, n_graphs), _stream(dev))
+    return z, ap
+
+
+def bwd_prox(s: Tensor, a: Tensor, w: Tensor, log_gamma: Tensor, scale: Tensor, coef: float, gw: Tensor,
+             ggamma: Tensor, gdot: Tensor, n_graphs: int):
+    dev = _check("bwd_prox", s, a, w, log_gamma, scale, gw, ggamma, gdot)
+    o, gs = torch.empty_like(s), torch.empty_like(s)
+    _launch("bwd_prox", 4 * (4 * s.numel() + 3 * w.numel()), "grr_bwd_prox", s.data_ptr(), a.data_ptr(),
+            w.data_ptr(), log_gamma.data_ptr(), scale.data_ptr(), float(coef), o.data_ptr(), gs.data_ptr(),
+            gw.data_ptr(), ggamma.data_ptr(), gdot.data_ptr(), *_bgfhw(s, n_graphs), _stream(dev))
+    return o, gs
+
+
+def bwd_pair_weights(w: Tensor, gc: Tensor, gw: Tensor) -> None:
+    dev = _check("bwd_pair_weights", w, gc, gw)
+    b, g, _, h, ww = w.shape
+    _launch("bwd_pair_weights", 4 * (3 * w.numel() + gc.numel()), "grr_bwd_pair_weights", w.data_ptr(),
+            gc.data_ptr(), gw.data_ptr(), b, g, h, ww, _stream(dev))
+
+
+def bwd_edge_weights(feat: Tensor, channel_offset: int, n_graphs: int, n_fts: int, multiM: Tensor, w: Tensor,
+                     gw: Tensor, gfeat: Tensor, gmultiM: Tensor) -> None:
+    """Writes the gradient of the [G*F] slab at channel_offset of gfeat (same shape as feat)."""
+    dev = _check("bwd_edge_weights", feat, multiM, w, gw, gfeat, gmultiM)
+    b, ctot, h, ww = feat.shape
+    if gfeat.shape != feat.shape or channel_offset + n_graphs * n_fts > ctot:
+        raise ValueError("bwd_edge_weights: bad slab")
+    off = channel_offset * h * ww * 4
+    _launch("bwd_edge_weights", 4 * b * h * ww * (2 * n_graphs * n_fts + 8 * n_graphs), "grr_bwd_edge_weights",
+            feat.data_ptr() + off, ctot * h * ww, multiM.data_ptr(), w.data_ptr(), gw.data_ptr(),
+            gfeat.data_ptr() + off, ctot * h * ww, gmultiM.data_ptr(), b, n_graphs, n_fts, h, ww, _stream(dev))
+
+
+def bwd_graph_dot(u: Tensor, v: Tensor, out: Tensor, n_graphs: int, coef: float = 1.0) -> None:
+    """out[g] += coef * sum over (b, f, pixels) of u * v."""
+    dev = _check("bwd_graph_dot", u, v, out)
+    _launch("bwd_graph_dot", 8 * u.numel(), "grr_bwd_graph_dot", u.data_ptr(), v.data_ptr(), float(coef),
+            out.data_ptr(), *_bgfhw(u, n_graphs), _stream(dev))
+
+
+def bwd_lincomb(x: Tensor, sa: Optional[Tensor], y: Optional[Tensor], sb: Optional[Tensor], n_graphs: int,
+                out: Optional[Tensor] = None, accumulate: bool = False) -> Tensor:
+    """out = [out +] sa[g] x + sb[g] y (per-graph coefficient vectors; None = 1)."""
+    dev = _check("bwd_lincomb", x, sa, y, sb, out)
+    if out is None:
+        out = torch.empty_like(x)
+        accumulate = False
+    _launch("bwd_lincomb", 4 * x.numel() * (2 + int(y is not None) + int(accumulate)), "grr_bwd_lincomb",
+            x.data_ptr(), _ptr(sa), _ptr(y), _ptr(sb), out.data_ptr(), int(accumulate), *_bgfhw(x, n_graphs),
+            _stream(dev))
+    return out
+
+
+def bwd_unpool2_acc(xd: Tensor, out: Tensor) -> None:
+    dev = _check("bwd_unpool2_acc", xd, out)
+    b, c, h, w = out.shape
+    _launch("bwd_unpool2_acc", 4 * (2 * out.numel() + xd.numel()), "grr_bwd_unpool2_acc", xd.data_ptr(),
+            out.data_ptr(), b, c, h, w, _stream(dev))
+
+
+def conv2x2s2_bwd_data(g: Tensor, weight: Tensor, h: int, w: int) -> Tensor:
+    dev = _check("conv2x2s2_bwd_data", g, weight)
+    b, m = g.shape[:2]
+    k = weight.shape[1]
+    gx = torch.empty((b, k, h, w), dtype=torch.float32, device=dev)
+    _launch("conv2x2s2_bwd", 4 * (g.numel() + gx.numel()), "grr_conv2x2s2_bwd_data", g.data_ptr(),
+            weight.data_ptr(), gx.data_ptr(), b, k, m, h, w, _stream(dev))
+    return gx

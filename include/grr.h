@@ -153,6 +153,57 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
  * img [B,Cin,H,W] -> out [B,G*Cin,H,W], out[b, g*Cin + c] = img[b, c]. */
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream);
 
+/* ---- reverse pass (training, config C4) -------------------------------------
+ * Adjoint building blocks of the solver; the host composes them into the reverse of
+ * every operator application of MixtureGTVGLR.forward (REF:707-811), the autograd
+ * graph the reference gets from PyTorch.  Layouts as above; taps [C,5] are the 3x3
+ * cross stencil of one module in the order centre, up, left, right, down (built from
+ * stats_kernel_p01/p02a/p02b/p03, REF:178-183).  scale: per-graph [G] multiplier or
+ * NULL (=1); "accumulate"/"+=" outputs are read-modify-write, all others overwritten.
+ * Reductions (gtaps, gdot, ggamma, gmultiM) are float atomics: run-to-run order may vary. */
+
+/* mode 0: S x (replicate, REF:177-195); 1: S^T x (conv_transpose zero frame, REF:197-215);
+ * 2: adjoint of mode 1; 3: adjoint of mode 0.  out = [out +] scale[g] * mode(x). */
+grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,
+                           float* out, int B, int G, int F, int H, int W, void* stream);
+/* gtaps[c,t] += scale[g] * sum u(q) d(mode(z))(q)/dk_t, mode 0 (S) or 1 (S^T). */
+grr_status grr_bwd_tapgrad(const float* u, const float* z, int mode, const float* scale, float* gtaps,
+                           int B, int G, int F, int H, int W, void* stream);
+/* GLR (I - W) reverse (REF:218-237): s = S x, a = adjoint-S^T(g).
+ * z_out = (I-W) s, ap_out = (I-W)^T a, gw += scale * d<a,(I-W)s>/dw, gdot[g] += coef * <a, z>. */
+grr_status grr_bwd_glr(const float* s, const float* a, const float* w, const float* scale, float coef,
+                       float* z_out, float* ap_out, float* gw, float* gdot,
+                       int B, int G, int F, int H, int W, void* stream);
+/* Pair-Laplacian (linear C^T C, REF:452-523) reverse with pair weights c [B,G,2,H,W]:
+ * z_out = K s, ap_out = K a, gc += scale * d<a,Ks>/dc, gdot[g] += coef * <a, z>. */
+grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const float* scale, float coef,
+                        float* z_out, float* ap_out, float* gc, float* gdot,
+                        int B, int G, int F, int H, int W, void* stream);
+/* Prox rhs reverse, o = C^T-part(phi(C s)) with phi(t) = 2 soft(t, exp(log_gamma)) - t
+ * (REF:684-704, :757-781): o_out, gs_out = d<a,o>/ds, gw += scale * d<a,o>/dw (raw weights),
+ * ggamma[g] += scale * d<a,o>/dgamma, gdot[g] += coef * <a, o>. */
+grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const float* log_gamma,
+                        const float* scale, float coef, float* o_out, float* gs_out, float* gw,
+                        float* ggamma, float* gdot, int B, int G, int F, int H, int W, void* stream);
+/* Reverse of grr_gtv_pair_weights: gw [B,G,4,H,W] += d<gc, c(w)>/dw. */
+grr_status grr_bwd_pair_weights(const float* w, const float* gc, float* gw, int B, int G, int H, int W,
+                                void* stream);
+/* Reverse of grr_edge_weights (REF:146-175): gfeat (slab, overwritten) and gmultiM [G,F] (+=). */
+grr_status grr_bwd_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM, const float* w,
+                                const float* gw, float* gfeat, int64_t gfeat_bstride, float* gmultiM,
+                                int B, int G, int F, int H, int W, void* stream);
+/* gdot[g] += coef * sum_{b,f,p} u v  (per-graph inner product; alpha/beta/gamma gradients). */
+grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* gdot,
+                             int B, int G, int F, int H, int W, void* stream);
+/* out = [out +] sa[g] x + sb[g] y  (sa/sb NULL = 1, y NULL = no second term). */
+grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,
+                           int accumulate, int B, int G, int F, int H, int W, void* stream);
+/* out [B,C,H,W] += U(xd): 0.25 * xd(q/2) (conv_transpose2d of scaling_kernel01, REF:676-679). */
+grr_status grr_bwd_unpool2_acc(const float* xd, float* out, int B, int C, int H, int W, void* stream);
+/* Data gradient of grr_conv2x2s2: g [B,M,H/2,W/2], wt [M,K,2,2] -> gx [B,K,H,W]. */
+grr_status grr_conv2x2s2_bwd_data(const float* g, const float* wt, float* gx, int B, int K, int M, int H, int W,
+                                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

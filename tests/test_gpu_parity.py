@@ -346,7 +346,11 @@ def test_single_stage_and_odd_half_level(irdu, variant):
 
 
 def test_backward_fails_loudly(irdu):
-    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=2).to(DEV)
-    y = m(torch.rand(1, 3, 16, 16, device=DEV))
+    """Entry points without a reverse kernel (the GLRFast/GTVFast sub-API) raise in backward
+    instead of silently dropping gradients."""
+    m = irdu.GLRFast(3, 2, M_diag_init=1.0).to(DEV)
+    x = torch.rand(1, 2, 3, 16, 16, device=DEV, requires_grad=True)
+    w = torch.softmax(torch.rand(1, 2, 4, 16, 16, device=DEV), dim=2)
+    y = m(x, w)
     with pytest.raises(NotImplementedError):
         y.sum().backward()
