@@ -24,5 +24,7 @@ from .graph_filter import (  # noqa: F401
     Upsampling,
 )
 from . import kernels  # noqa: F401
+from . import glr_v10 as v10  # noqa: F401  (GLR-only drop-ins of lib/model_GLR_GTV_deep_v10.py)
+from .glr_v10 import GLRImageFilter, MixtureGLR  # noqa: F401
 
 __version__ = "0.1.0"

@@ -52,6 +52,7 @@ SIGNATURES = {
     "grr_gtv_rhs_half": [P, P, Stencil, I, P, P, I, I, I, I, I, P],
     "grr_gtv_rhs_full": [P, P, P, Stencil, I, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_system_step": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_glr_stage": [P, P, P, P, Stencil, P, P, P, P, P, I, I, I, I, I, P],
     "grr_conv1x1": [P, P, P, I, I, I, L, P],
     "grr_conv1x1_workspace_bytes": [I, I],
     "grr_conv1x1_ws": [P, P, P, P, I, I, I, L, P],

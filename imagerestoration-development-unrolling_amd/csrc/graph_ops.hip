@@ -177,7 +177,7 @@ struct OpArgs {
   const float* wL;      // GLR edge weights [B,G,4,H,W]
   const float* wG;      // GTV pair weights [B,G,2,H,W] or raw [B,G,4,H,W] (prox)
   grr_stencil sL, sG;
-  const float* log_l;   // GLR term scale (log), NULL -> 1
+  const float* log_l;   // GLR term scale (log, or linear when lin_l), NULL -> 1
   const float* log_g;   // GTV term scale (log), NULL -> 1
   const float* log_gamma;
   const float* log_half;  // scale of U(t_half) (log), NULL -> 1
@@ -193,6 +193,7 @@ struct OpArgs {
   float* xd_out;
   int G, F, H, W, tiles_x, tiles_y;
   int nstrips, nsegs, sseg;
+  int lin_l;            // log_l holds the scale itself (v10 MixtureGLR stores mu linearly)
   uint32_t nunits, nblk;
 };
 
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   const uint32_t vo_y = need_y ? vo : vo_lane, vo_th = has_half ? vo_half : vo_lane;
 
   float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
-  if (a.log_l) sc_l = expf(a.log_l[g]);
+  if (a.log_l) sc_l = a.lin_l ? a.log_l[g] : expf(a.log_l[g]);
   if (a.log_g) sc_g = expf(a.log_g[g]);
   if (a.log_half) sc_h = expf(a.log_half[g]);
   if constexpr (GTV == GTV_PROX) gam = expf(a.log_gamma[g]);
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
   const uint32_t vo_y = need_y ? vo : vo_lane, vo_th = has_half ? vo_half : vo_lane;
 
   float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
-  if (a.log_l) sc_l = expf(a.log_l[g]);
+  if (a.log_l) sc_l = a.lin_l ? a.log_l[g] : expf(a.log_l[g]);
   if (a.log_g) sc_g = expf(a.log_g[g]);
   if (a.log_half) sc_h = expf(a.log_half[g]);
   if constexpr (GTV == GTV_PROX) gam = expf(a.log_gamma[g]);
@@ -1069,6 +1070,23 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
   if (wL && cG) return launch_op<true, GTV_PAIR, EPI_STEP>(a, B, s, "grr_system_step");
   if (wL) return launch_op<true, GTV_NONE, EPI_STEP>(a, B, s, "grr_system_step");
   return launch_op<false, GTV_PAIR, EPI_STEP>(a, B, s, "grr_system_step");
+}
+
+grr_status grr_glr_stage(const float* x, const float* b, const float* u_prev, const float* wL, grr_stencil sL,
+                         const float* mu, const float* alpha, const float* beta, float* x_out, float* u_out, int B,
+                         int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && b && wL && mu && alpha && x_out && stencil_ok(sL) && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_glr_stage: bad args");
+  GRR_REQUIRE(!u_prev || beta, GRR_ERR_INVALID_ARG, "grr_glr_stage: u_prev needs beta");
+  GRR_REQUIRE(x_out != x && x_out != b && (!u_prev || x_out != u_prev) && (!u_out || u_out != x),
+              GRR_ERR_INVALID_ARG, "grr_glr_stage: outputs must not alias the stencil inputs");
+  OpArgs a{};
+  a.x = x; a.b = b; a.u_prev = u_prev; a.wL = wL; a.sL = sL;
+  a.log_l = mu; a.lin_l = 1; a.alpha = alpha; a.beta = beta;
+  a.out = x_out; a.u_out = u_out;
+  a.G = G; a.F = F; a.H = H; a.W = W;
+  return launch_op<true, GTV_NONE, EPI_STEP>(a, B, (hipStream_t)stream, "grr_glr_stage");
 }
 
 }  // extern "C"

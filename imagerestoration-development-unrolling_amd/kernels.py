@@ -402,3 +402,22 @@ def conv2x2s2_bwd_data(g: Tensor, weight: Tensor, h: int, w: int) -> Tensor:
     _launch("conv2x2s2_bwd", 4 * (g.numel() + gx.numel()), "grr_conv2x2s2_bwd_data", g.data_ptr(),
             weight.data_ptr(), gx.data_ptr(), b, k, m, h, w, _stream(dev))
     return gx
+
+
+def glr_stage(x: Tensor, b: Tensor, u_prev: Optional[Tensor], wL: Tensor, sL: Stencil, mu: Tensor, alpha: Tensor,
+              beta: Optional[Tensor], n_graphs: int, want_u: bool = True,
+              u_out: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """One v10 MixtureGLR stage (grr_glr_stage): returns (x_out, u)."""
+    dev = _check("glr_stage", x, b, u_prev, wL, mu, alpha, beta, u_out)
+    bb, c, h, w = x.shape
+    out = torch.empty_like(x)
+    if want_u and u_out is None:
+        u_out = torch.empty_like(x)
+    if not want_u:
+        u_out = None
+    nbytes = 4 * bb * h * w * (c * (2 + int(b is not x) + int(u_prev is not None) + int(u_out is not None))
+                               + 4 * n_graphs)
+    _launch("glr_stage", nbytes, "grr_glr_stage", x.data_ptr(), b.data_ptr(), _ptr(u_prev), wL.data_ptr(), sL,
+            mu.data_ptr(), alpha.data_ptr(), _ptr(beta), out.data_ptr(), _ptr(u_out), bb, n_graphs, c // n_graphs,
+            h, w, _stream(dev))
+    return out, u_out

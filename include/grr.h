@@ -119,6 +119,15 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
                            float* x_out, float* u_out, float* xd_out,
                            int B, int G, int F, int H, int W, void* stream);
 
+/* One unrolled stage of the GLR-only v10 block (exploration/model_multiscale_mixture_GLR/lib/
+ * model_GLR_GTV_deep_v10.py:241-335, MixtureGLR): single scale, A x = x + mu[g] L x with mu
+ * stored LINEARLY (not as a log, :283-286, :296-305):
+ *   r = b - A x;  u = r + beta[g] u_prev (u = r when u_prev == NULL);  x_out = x + alpha[g] u.
+ * u_out may be NULL.  With x = b = y and u_prev = NULL this is stage 0 (:316-318). */
+grr_status grr_glr_stage(const float* x, const float* b, const float* u_prev, const float* wL, grr_stencil sL,
+                         const float* mu, const float* alpha, const float* beta, float* x_out, float* u_out,
+                         int B, int G, int F, int H, int W, void* stream);
+
 /* ---- feature CNN (MFMA fp32) ------------------------------------------------ */
 
 /* 1x1 convolution, no bias (nn.Conv2d(k=1, groups=1, bias=False); REF:556-566, REF13:623-632):

@@ -348,6 +348,36 @@ def features_v13(y4: Tensor, p: Params) -> Tuple[Tensor, Tensor]:
     return f0, f1
 
 
+def mixture_glr_forward(y4: Tensor, p: Params, n_graphs: int, n_stages: Optional[int] = None) -> Tensor:
+    """GLR-only single-scale MixtureGLR.forward of lib/model_GLR_GTV_deep_v10.py:241-335 (REF10).
+
+    features = 1x1 conv C->C (REF10:270-281); one GLR graph (REF10:302-305); A x = x + mu L x with
+    mu = muys00 used linearly (REF10:283-286, :296-305).  Recurrence (REF10:313-328):
+    u_0 = r_0 = y - A y, x_1 = y + a_0 u_0;  u_k = (y - A x_k) + b_k u_{k-1}, x_{k+1} = x_k + a_k u_k.
+    S = alphaCGD.shape[0] (3 in the reference) unless given.
+    """
+    b, c, h, w = y4.shape
+    g = n_graphs
+    nf = c // g
+    feat = Fn.conv2d(y4, p["patchs_features_extraction.0.weight"])
+    wgt, _ = edge_weights(feat.reshape(b, g, nf, h, w), p["GLRmodule00.multiM"])
+    k = stats_kernel(p, "GLRmodule00.")
+    mu = p["muys00"]
+    alpha, beta = p["alphaCGD"], p["betaCGD"]
+    s_count = alpha.shape[0] if n_stages is None else n_stages
+    y5 = y4.reshape(b, g, nf, h, w)
+
+    def system(x5):
+        return x5 + _scale(glr_apply(x5, wgt, k), mu)
+
+    u = y5 - system(y5)
+    x = y5 + _scale(u, alpha[0])
+    for i in range(1, s_count):
+        u = (y5 - system(x)) + _scale(u, beta[i])
+        x = x + _scale(u, alpha[i])
+    return x.reshape(b, c, h, w)
+
+
 def sub_params(p: Params, prefix: str) -> Params:
     n = len(prefix)
     return {k[n:]: v for k, v in p.items() if k.startswith(prefix)}

@@ -14,6 +14,8 @@ Fixtures:
   mixture_v1_rect.npz same on a non-square, non-multiple-of-32 image
   msgf_v13.npz        v13_no_latent MultiScaleGraphFilter forward (lib/..._v13_no_latent.py:887-926)
   abstract_v1.npz     AbtractMultiScaleGraphFilter (small dims) forward + filtering (REF:1028-1174)
+  mixture_glr_v10.npz / mixture_glr_v10_f1.npz
+                      GLR-only MixtureGLR (lib/model_GLR_GTV_deep_v10.py:241-335) forward + L1 gradients
 """
 from __future__ import annotations
 
@@ -36,6 +38,37 @@ def _import_ref(ref_root: str):
     import deep_multiscale_GGLR_GGTV_v1x0 as v1  # noqa: E402
     import model_GLR_GTV_deep_v13_no_latent as v13  # noqa: E402
     return v1, v13
+
+
+def _import_v10(ref_root: str):
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, os.path.join(ref_root, "exploration", "model_multiscale_mixture_GLR", "lib"))
+    import model_GLR_GTV_deep_v10 as v10  # noqa: E402
+    return v10
+
+
+def make_mixture_glr(v10, gen, name, shape, g):
+    b, c, h, w = shape
+    mix = v10.MixtureGLR(n_graphs=g, n_node_fts=c // g, alpha_init=0.5, beta_init=0.1,
+                         muy_init=torch.tensor([[0.001], [0.0], [0.0], [0.0]]))
+    with torch.no_grad():
+        mix.alphaCGD.copy_(0.2 + 0.6 * torch.rand(mix.alphaCGD.shape, generator=gen))
+        mix.betaCGD.copy_(0.05 + 0.35 * torch.rand(mix.betaCGD.shape, generator=gen))
+        mix.muys00.copy_(0.05 + 0.55 * torch.rand(mix.muys00.shape, generator=gen))
+    _perturb_graph_module(mix.GLRmodule00, gen)
+    x = torch.randn(shape, generator=gen) * 0.5 + 0.5
+    target = torch.randn(shape, generator=gen) * 0.1
+    out = {"in/x": _np(x), "in/target": _np(target), "meta/n_graphs": np.array(g)}
+    _state(out, mix)
+    with torch.no_grad():
+        out["out/y"] = _np(mix(x))
+    xg = x.clone().requires_grad_(True)
+    loss = torch.nn.functional.l1_loss(mix(xg), target)
+    loss.backward()
+    out["grad/x"] = _np(xg.grad)
+    for k, p in mix.named_parameters():
+        out["grad/" + k] = _np(p.grad)
+    np.savez_compressed(os.path.join(HERE, name), **out)
 
 
 def _np(t: torch.Tensor) -> np.ndarray:
@@ -201,7 +234,15 @@ def make_abstract(v1, gen):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", choices=["all", "v10"], default="all")
     args = ap.parse_args()
+    if args.only in ("all", "v10"):   # own generator: (re)making these leaves the others untouched
+        v10 = _import_v10(args.ref)
+        gen10 = torch.Generator().manual_seed(2210)
+        make_mixture_glr(v10, gen10, "mixture_glr_v10.npz", (2, 12, 24, 32), 4)
+        make_mixture_glr(v10, gen10, "mixture_glr_v10_f1.npz", (1, 8, 20, 28), 8)
+        if args.only == "v10":
+            return
     v1, v13 = _import_ref(args.ref)
     torch.manual_seed(2204)
     gen = torch.Generator().manual_seed(2204)

@@ -354,3 +354,61 @@ def test_backward_fails_loudly(irdu):
     y = m(x, w)
     with pytest.raises(NotImplementedError):
         y.sum().backward()
+
+
+# ---------------------------------------------------------------------------
+# GLR-only v10 MixtureGLR (config C2 pattern)
+@pytest.mark.parametrize("name", ["mixture_glr_v10.npz", "mixture_glr_v10_f1.npz"])
+def test_mixture_glr_v10_golden(irdu, variant, name):
+    d = load_golden(name)
+    g = int(d["meta/n_graphs"])
+    x = torch.from_numpy(d["in/x"])
+    mix = irdu.MixtureGLR(g, x.shape[1] // g, 0.5, 0.1, [[0.001]])
+    mix.load_state_dict(params_of(d, ""))
+    with torch.no_grad():
+        got = mix.to(DEV)(x.to(DEV))
+    assert_close(got, d["out/y"])
+
+
+@pytest.mark.parametrize("case", [dict(b=2, h=64, w=64), dict(b=1, h=40, w=300)])
+def test_glr_image_filter_five_stages(irdu, variant, case):
+    """Config C2 shape family: gray image, G = 8 graphs x F = 1, S = 5 stages, vs the oracle."""
+    torch.manual_seed(12)
+    m = irdu.GLRImageFilter(1, 1, ngraphs=8, n_cgd_iters=5)
+    gen = torch.Generator().manual_seed(13)
+    with torch.no_grad():
+        lf = m.localfilter
+        lf.alphaCGD.copy_(0.2 + 0.6 * torch.rand(lf.alphaCGD.shape, generator=gen))
+        lf.betaCGD.copy_(0.05 + 0.35 * torch.rand(lf.betaCGD.shape, generator=gen))
+        lf.muys00.copy_(0.05 + 0.55 * torch.rand(lf.muys00.shape, generator=gen))
+    perturbed_graph_module(lf.GLRmodule00, 14)
+    clean = torch.rand(case["b"], 1, case["h"], case["w"])
+    noisy = clean + torch.randn(clean.shape) * (25.0 / 255.0)
+    p = sd_cpu(m)
+    x = noisy.repeat(1, 8, 1, 1)
+    ref = torch.nn.functional.conv2d(O.mixture_glr_forward(x, O.sub_params(p, "localfilter."), 8),
+                                     p["linear_combination.weight"])
+    with torch.no_grad():
+        got = m.to(DEV)(noisy.to(DEV))
+    assert_close(got, ref)
+
+
+# ---------------------------------------------------------------------------
+# training parity against the reference's own autograd gradients (golden)
+@pytest.mark.parametrize("name", ["mixture_v1.npz", "mixture_v1_rect.npz"])
+def test_mixture_grad_vs_reference_golden(irdu, name):
+    """L1-loss gradients of MixtureGTVGLR (input + every parameter) from the HIP reverse
+    sweep vs the gradients the reference's PyTorch autograd produced (fixture)."""
+    d = load_golden(name)
+    g = int(d["meta/n_graphs"])
+    x = torch.from_numpy(d["in/x"])
+    mix = irdu.MixtureGTVGLR(g, x.shape[1] // g, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]])
+    mix.load_state_dict(params_of(d, ""))
+    mix = mix.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    loss = torch.nn.functional.l1_loss(mix(xg), torch.from_numpy(d["in/target"]).to(DEV))
+    loss.backward()
+    assert abs(float(loss.detach()) - float(d["out/loss"])) <= 1e-5 * abs(float(d["out/loss"]))
+    assert_close(xg.grad, d["grad/x"], 2e-4)
+    for k, p in mix.named_parameters():
+        assert_close(p.grad, d["grad/" + k], 2e-4)

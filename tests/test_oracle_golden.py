@@ -128,3 +128,19 @@ def test_psnr_helper():
     assert O.psnr_ubyte(clean, clean) == float("inf")
     noisy = clean + 2.2 / 255.0  # quantises to exactly +2 grey levels
     assert abs(O.psnr_ubyte(noisy, clean) - 20 * np.log10(255 / 2.0)) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["mixture_glr_v10.npz", "mixture_glr_v10_f1.npz"])
+def test_mixture_glr_v10_forward_and_grads(name):
+    """GLR-only v10 MixtureGLR (lib/model_GLR_GTV_deep_v10.py:241-335): forward and the
+    reference's own L1-loss autograd gradients."""
+    d = load_golden(name)
+    g = int(d["meta/n_graphs"])
+    p = {k: v.clone().requires_grad_(True) for k, v in params_of(d, "").items()}
+    x = torch.from_numpy(d["in/x"]).requires_grad_(True)
+    y = O.mixture_glr_forward(x, p, g)
+    close(y.detach(), d["out/y"])
+    torch.nn.functional.l1_loss(y, torch.from_numpy(d["in/target"])).backward()
+    close(x.grad, d["grad/x"], 1e-4)
+    for k, v in p.items():
+        close(v.grad, d["grad/" + k], 1e-4)
