@@ -1,0 +1,339 @@
+"""Training engine: the reference's run_train.py / experiment_conf YAML surface on the HIP path.
+
+Mirrors (reference paths):
+  run_train.py:20-121                      parse_options, checkpoint discovery, logger, dataset/dataloader
+  environ/utils/custom_parser.py:23-30     YAML -> dict
+  environ/data/__init__.py:29-69           create_dataset (by ``type``), create_dataloader
+  environ/data/data_sampler.py:6-31        ResumeableSampler (resume inside an epoch)
+  environ/data/images_pair_restoration_dataset.py:15-116
+                                           AddictiveGaussianNoiseImagePair (patch grid, permute, noise)
+  exploration/model_multiscale_mixture_GLR/scripts_v2/run_abtract_lightformer_GGTV_GGLR_sigma25.py
+    :120-151  model / losses (L1 + 0.1 MSE(enc-dec) + 0.5 MSE(latent-perturbed decode))
+    :153-171  Adam(4e-4, eps 1e-8), MultiStepLR(gamma = 0.5**0.25) -> CosineAnnealingLR (SequentialLR)
+    :186-224  training step, checkpoint dict {'i', 'model', 'optimizer', 'lr_scheduler'}
+
+The reference's run_train.py stops after building the dataloader; the YAML here adds
+``model:`` and ``train:`` sections so the same entry point runs the training loop of the
+v2 scripts.  Multi-GPU: one process per GPU (torchrun); every rank trains on its own
+slice of each global batch and gradients are averaged with bucketed RCCL all-reduces
+(sharding.allreduce_gradients) — the only collective of the path.
+
+Datasets: no image data ships with the reference, so ``SyntheticNoisyPatches`` (seeded
+procedural clean patches, the same noise law) is the default; the CSV/PNG dataset type
+is kept for real data.  Samples are (noisy, clean) HWC float32 like the reference's.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import math
+import os
+import random
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import yaml
+from torch.utils.data import Dataset, Sampler
+
+from . import sharding
+
+LOG = logging.getLogger("irdu_amd.train")
+
+
+# ---------------------------------------------------------------------------
+# options (run_train.py:20-36, custom_parser.py:23-30, small_utils.py:12-18)
+# ---------------------------------------------------------------------------
+def parse(yaml_file_path: str) -> dict:
+    with open(yaml_file_path) as f:
+        return yaml.safe_load(f)
+
+
+def set_random_seed(seed: int = 2204) -> None:
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+def parse_options(yaml_path: str) -> dict:
+    conf = parse(yaml_path)
+    if conf.get("manual_seed") is None:
+        conf["manual_seed"] = random.randint(1, 10000)
+    set_random_seed(conf["manual_seed"])
+    return conf
+
+
+# ---------------------------------------------------------------------------
+# data (environ/data/*)
+# ---------------------------------------------------------------------------
+def _noisy(patch: np.ndarray, rs: np.random.RandomState, dist_mode: str, lambda_noise: float) -> np.ndarray:
+    """images_pair_restoration_dataset.py:101-110: additive Gaussian noise, sigma = lambda/255."""
+    if dist_mode == "addictive_noise":
+        noise = rs.normal(loc=0.0, scale=lambda_noise / 255.0, size=patch.shape)
+    elif dist_mode == "addictive_noise_scale":
+        noise = rs.normal(loc=0.0, scale=1.0, size=patch.shape) * (lambda_noise / 255.0)
+    else:
+        raise ValueError(f"unknown dist_mode {dist_mode!r}")
+    return patch + noise.astype(np.float32)
+
+
+class AddictiveGaussianNoiseImagePair(Dataset):
+    """CSV-indexed image patches + noise (images_pair_restoration_dataset.py:15-116).
+    csv columns: index, path, height, width (as the reference's *_info.csv)."""
+
+    def __init__(self, csv_path, dist_mode="", lambda_noise=None, patch_size=64, patch_overlap_size=32,
+                 max_num_patchs=100000, root_folder="", logger_name=None, device_str="cpu", n_channels=3):
+        import pandas as pd
+        self.img_infos = pd.read_csv(csv_path, index_col="index")
+        self.patch_size, self.patch_overlap_size = patch_size, patch_overlap_size
+        self.root_folder, self.lambda_noise, self.dist_mode = root_folder, lambda_noise, dist_mode
+        self.n_channels = n_channels
+        rows = []
+        step = patch_size - patch_overlap_size
+        for i in range(self.img_infos.shape[0]):
+            info = self.img_infos.iloc[i]
+            path = os.path.join(root_folder, info["path"])
+            for r in np.arange(0, info["height"] - patch_size, step):
+                for c in np.arange(0, info["width"] - patch_size, step):
+                    rows.append((int(r), int(c), path))
+        self.patchs_data_all = rows
+        self.max_num_patchs = min(max_num_patchs, len(rows))
+        self.random_permute(seed=2204)
+
+    def random_permute(self, seed=2204):
+        self.random_state = np.random.RandomState(seed=seed)
+        ind = self.random_state.permutation(self.max_num_patchs)
+        self.patchs_data = [self.patchs_data_all[i] for i in ind]
+
+    def __len__(self):
+        return len(self.patchs_data)
+
+    def __getitem__(self, idx):
+        from PIL import Image
+        row, col, path = self.patchs_data[idx]
+        img = np.array(Image.open(path))
+        patch = img[row:row + self.patch_size, col:col + self.patch_size, :]
+        h, w = (patch.shape[0] // 16) * 16, (patch.shape[1] // 16) * 16
+        patch = patch[:h, :w].astype(np.float32) / 255.0
+        dist = _noisy(patch, self.random_state, self.dist_mode, self.lambda_noise)
+        return torch.from_numpy(dist), torch.from_numpy(patch)
+
+
+def synthetic_clean_patch(rs: np.random.RandomState, h: int, w: int, c: int) -> np.ndarray:
+    """Piecewise-smooth clean patch on the uint8 grid (sinusoid background + rectangles), HWC."""
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    out = np.empty((h, w, c), np.float32)
+    for ch in range(c):
+        fy, fx, ph = rs.uniform(0.5, 4.0), rs.uniform(0.5, 4.0), rs.uniform(0, 6.28)
+        img = 0.5 + 0.3 * np.sin(2 * np.pi * fy * yy / h + ph) * np.cos(2 * np.pi * fx * xx / w)
+        for _ in range(3):
+            r0, c0 = rs.randint(0, max(1, h - h // 4)), rs.randint(0, max(1, w - w // 4))
+            img[r0:r0 + rs.randint(4, max(5, h // 3)), c0:c0 + rs.randint(4, max(5, w // 3))] += rs.uniform(-0.3, 0.3)
+        out[..., ch] = img
+    return (np.round(np.clip(out, 0, 1) * 255.0) / 255.0).astype(np.float32)
+
+
+class SyntheticNoisyPatches(Dataset):
+    """Deterministic synthetic (noisy, clean) patch pairs: sample i is a function of (seed, i)."""
+
+    def __init__(self, dist_mode="addictive_noise_scale", lambda_noise=25.0, patch_size=64, max_num_patchs=1000,
+                 n_channels=3, seed=2204, **_ignored):
+        self.dist_mode, self.lambda_noise = dist_mode, lambda_noise
+        self.patch_size, self.n_channels, self.seed = patch_size, n_channels, seed
+        self.max_num_patchs = max_num_patchs
+        self.random_permute(seed=2204)
+
+    def random_permute(self, seed=2204):
+        self.order = np.random.RandomState(seed).permutation(self.max_num_patchs)
+
+    def __len__(self):
+        return self.max_num_patchs
+
+    def __getitem__(self, idx):
+        rs = np.random.RandomState((self.seed * 1000003 + int(self.order[idx])) % (2 ** 32))
+        clean = synthetic_clean_patch(rs, self.patch_size, self.patch_size, self.n_channels)
+        return torch.from_numpy(_noisy(clean, rs, self.dist_mode, self.lambda_noise)), torch.from_numpy(clean)
+
+
+DATASETS = {c.__name__: c for c in (AddictiveGaussianNoiseImagePair, SyntheticNoisyPatches)}
+
+
+class ResumeableSampler(Sampler):
+    """Deterministic in-order sampling that resumes after ``current_sample`` (data_sampler.py:6-31).
+    With world_size > 1 each rank yields its own contiguous slice of every global batch."""
+
+    def __init__(self, dataset, batch_size: int = 1, rank: int = 0, world_size: int = 1):
+        self.dataset = dataset
+        self.epoch = 0
+        self.current_sample = -1
+        self.num_samples = len(dataset)
+        self.batch_size, self.rank, self.world_size = batch_size, rank, world_size
+
+    def _mine(self, i: int) -> bool:
+        if self.world_size == 1:
+            return True
+        gb = self.batch_size * self.world_size
+        return (i % gb) // self.batch_size == self.rank
+
+    def __iter__(self) -> Iterator[int]:
+        for sample_i in range(self.num_samples):
+            if sample_i > self.current_sample:
+                self.current_sample += 1
+                if self._mine(sample_i):
+                    yield sample_i
+
+    def __len__(self):
+        return self.num_samples // self.world_size
+
+    def set_epoch_and_current_sample(self, current_epoch, current_sample):
+        self.current_epoch = current_epoch
+        self.current_sample = current_sample
+        self.dataset.random_permute(seed=2024 + current_epoch)
+
+
+def create_dataset(dataset_conf: dict, environ_conf: dict):
+    cls = DATASETS.get(dataset_conf["type"])
+    if cls is None:
+        raise ValueError(f"Dataset {dataset_conf['type']} is not found.")
+    return cls(**dataset_conf["dataset_args"])
+
+
+def create_dataloader(dataset, sampler, dataset_conf: dict, environ_conf: dict):
+    args = dict(dataset_conf["dataloader_args"])
+    return torch.utils.data.DataLoader(dataset=dataset, sampler=sampler, **args)
+
+
+# ---------------------------------------------------------------------------
+# model / optimiser / schedule (v2 script :120-171)
+# ---------------------------------------------------------------------------
+def build_model(model_conf: dict) -> nn.Module:
+    import irdu_amd
+    kind = model_conf.get("type", "AbtractMultiScaleGraphFilter")
+    cls = {"AbtractMultiScaleGraphFilter": irdu_amd.AbtractMultiScaleGraphFilter,
+           "MultiScaleGraphFilter": irdu_amd.MultiScaleGraphFilter}.get(kind)
+    if cls is None:
+        raise ValueError(f"model type {kind!r} has no training path")
+    return cls(**model_conf.get("args", {}))
+
+
+def build_optimizer(model: nn.Module, tconf: dict):
+    """Adam + MultiStepLR(gamma=sqrt(sqrt(0.5))) -> CosineAnnealingLR (base lr 5e-5) via SequentialLR."""
+    from torch.optim.lr_scheduler import CosineAnnealingLR, MultiStepLR, SequentialLR
+    opt = torch.optim.Adam(model.parameters(), lr=tconf.get("lr", 4e-4), eps=tconf.get("eps", 1e-8))
+    switch = tconf.get("cosine_from", 600000)
+    s1 = MultiStepLR(opt, milestones=list(tconf.get("milestones", range(50000, 600001, 50000))),
+                     gamma=float(np.sqrt(np.sqrt(0.5))))
+    s2 = CosineAnnealingLR(opt, T_max=tconf.get("cosine_T_max", 701000), eta_min=tconf.get("eta_min", 1e-6))
+    s2.base_lrs = [tconf.get("cosine_base_lr", 5e-5) for _ in opt.param_groups]
+    return opt, SequentialLR(opt, schedulers=[s1, s2], milestones=[switch])
+
+
+class Trainer:
+    """One optimisation step = the v2 script's loop body (:186-207) + the DDP gradient average."""
+
+    def __init__(self, model: nn.Module, tconf: dict, device):
+        self.model, self.device = model.to(device), device
+        self.optimizer, self.lr_scheduler = build_optimizer(self.model, tconf)
+        self.w_encdec = float(tconf.get("loss02_weight", 0.1))
+        self.w_perturb = float(tconf.get("loss03_weight", 0.5))
+        self.latent_noise = float(tconf.get("latent_noise", 0.05))
+        self.bucket_mb = float(tconf.get("allreduce_bucket_mb", 32.0))
+        self.i = 0
+
+    def loss(self, noisy: torch.Tensor, clean: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        loss = nn.functional.l1_loss(m(noisy), clean)
+        if hasattr(m, "encode") and (self.w_encdec or self.w_perturb):
+            latent = m.encode(clean)
+            rec = m.decode(latent)
+            disturbed = m.decode(tuple(t + torch.normal(0.0, self.latent_noise, size=t.shape, device=t.device)
+                                       for t in latent))
+            loss = loss + self.w_encdec * nn.functional.mse_loss(rec, clean)
+            loss = loss + self.w_perturb * nn.functional.mse_loss(rec, disturbed)
+        return loss
+
+    def step(self, noisy_hwc: torch.Tensor, clean_hwc: torch.Tensor) -> float:
+        """noisy/clean: [B,H,W,C] batches as the dataset yields them (permuted like :191-193)."""
+        self.model.train()
+        self.optimizer.zero_grad(set_to_none=True)
+        noisy = noisy_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
+        clean = clean_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
+        loss = self.loss(noisy, clean)
+        loss.backward()
+        sharding.allreduce_gradients(self.model.parameters(), bucket_mb=self.bucket_mb)
+        self.optimizer.step()
+        self.lr_scheduler.step()
+        self.i += 1
+        return float(loss.detach())
+
+    def state_dict(self) -> dict:
+        return {"i": self.i, "model": self.model.state_dict(), "optimizer": self.optimizer.state_dict(),
+                "lr_scheduler": self.lr_scheduler.state_dict()}
+
+    def load_state_dict(self, ckpt: dict) -> None:
+        self.model.load_state_dict(ckpt["model"])
+        self.optimizer.load_state_dict(ckpt["optimizer"])
+        self.lr_scheduler.load_state_dict(ckpt["lr_scheduler"])
+        self.i = int(ckpt["i"])
+
+
+def checkpoint_dir(conf: dict) -> str:
+    return os.path.join(conf["path"]["root_dir"], "experiments", conf["name"], "learning_checkpoints")
+
+
+def latest_checkpoint(conf: dict) -> Optional[str]:
+    """run_train.py:42-55: the last file of the sorted checkpoint folder."""
+    d = checkpoint_dir(conf)
+    files = sorted(os.listdir(d)) if os.path.isdir(d) else []
+    return os.path.join(d, files[-1]) if files else None
+
+
+def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
+    """Build everything from the YAML dict, resume from the latest checkpoint, train."""
+    rank, world = sharding.world()
+    if device is None:
+        device = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', 0))}") if torch.cuda.is_available() \
+            else torch.device("cpu")
+    tconf = conf.get("train", {})
+    ds_conf = conf["datasets"]["train"]
+    dataset = create_dataset(ds_conf, conf)
+    bs = int(ds_conf["dataloader_args"].get("batch_size", 1))
+    sampler = ResumeableSampler(dataset, bs, rank, world)
+    loader = create_dataloader(dataset, sampler, ds_conf, conf)
+    trainer = Trainer(build_model(conf.get("model", {})), tconf, device)
+    ckpt_path = conf["path"].get("latest_checkpoint_path") or latest_checkpoint(conf)
+    if ckpt_path:
+        trainer.load_state_dict(torch.load(ckpt_path, map_location=device, weights_only=True))
+        sampler.set_epoch_and_current_sample(0, trainer.i * bs * world - 1)
+        LOG.info("resumed from %s at iteration %d", ckpt_path, trainer.i)
+    os.makedirs(checkpoint_dir(conf), exist_ok=True)
+    total = max_iters if max_iters is not None else int(tconf.get("total_iters", len(sampler) // bs))
+    every = int(tconf.get("checkpoint_every", 5000))
+    verbose = int(tconf.get("verbose_every", 100))
+    for noisy, clean in loader:
+        if trainer.i >= total:
+            break
+        loss = trainer.step(noisy, clean)
+        if rank == 0 and trainer.i % verbose == 0:
+            LOG.info("iter=%d loss=%.6f lr=%.3e", trainer.i, loss, trainer.optimizer.param_groups[0]["lr"])
+        if rank == 0 and (trainer.i % every == 0 or trainer.i == total):
+            torch.save(trainer.state_dict(), os.path.join(checkpoint_dir(conf), f"checkpoint_iter{trainer.i:08d}.pt"))
+    return trainer
+
+
+def main(argv: Optional[Sequence[str]] = None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-yaml_path", type=str, required=True, help="Path to option YAML file.")
+    ap.add_argument("-max_iters", type=int, default=None)
+    args = ap.parse_args(argv)
+    conf = parse_options(args.yaml_path)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s: %(message)s")
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1 and not torch.distributed.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+        torch.distributed.init_process_group(backend)
+    run(conf, max_iters=args.max_iters)

@@ -1,0 +1,149 @@
+"""Host logic of the training engine (irdu_amd/training.py) on CPU: YAML surface, datasets,
+ResumeableSampler semantics (environ/data/data_sampler.py:6-31), the reference's LR schedule
+(scripts_v2/...sigma25.py:153-171), checkpoint/resume, and the data-parallel step over gloo.
+The graph filter itself needs the GPU (tests/test_gpu_training.py); here a small stock
+PyTorch model stands in, since the engine is model-agnostic."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from irdu_amd import training as T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class TinyModel(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Conv2d(3, 4, 3, padding=1, bias=False)
+        self.b = torch.nn.Conv2d(4, 3, 1, bias=False)
+
+    def encode(self, x):
+        return (self.a(x),)
+
+    def decode(self, lat):
+        return self.b(lat[0])
+
+    def forward(self, x):
+        return self.decode(self.encode(x))
+
+
+def test_example_yaml_parses_with_reference_keys():
+    conf = T.parse_options(os.path.join(ROOT, "experiment_conf", "example.yaml"))
+    for key in ("name", "manual_seed", "path", "datasets"):
+        assert key in conf
+    ds = conf["datasets"]["train"]
+    assert ds["type"] in T.DATASETS and ds["dataloader_args"]["batch_size"] == 4
+    c4 = T.parse(os.path.join(ROOT, "experiment_conf", "c4_train.yaml"))
+    assert c4["model"]["args"]["n_cgd_iters"] == 10 and c4["datasets"]["train"]["dataset_args"]["patch_size"] == 512
+
+
+def test_synthetic_dataset_deterministic_and_noise_law():
+    ds = T.SyntheticNoisyPatches(lambda_noise=25.0, patch_size=32, max_num_patchs=8)
+    n0, c0 = ds[3]
+    n1, c1 = ds[3]
+    assert torch.equal(n0, n1) and torch.equal(c0, c1)
+    assert n0.shape == (32, 32, 3) and c0.min() >= 0 and c0.max() <= 1
+    assert torch.allclose(c0 * 255, torch.round(c0 * 255), atol=1e-4)      # uint8 grid
+    noise = (n0 - c0).flatten()
+    assert abs(float(noise.std()) - 25.0 / 255.0) < 0.15 * 25.0 / 255.0
+
+
+def test_resumeable_sampler_resumes_and_shards():
+    ds = T.SyntheticNoisyPatches(patch_size=16, max_num_patchs=10)
+    s = T.ResumeableSampler(ds)
+    assert list(s) == list(range(10))
+    s = T.ResumeableSampler(ds)
+    s.set_epoch_and_current_sample(0, 3)
+    assert list(s) == list(range(4, 10))                 # resumes after sample 3
+    parts = [list(T.ResumeableSampler(ds, batch_size=2, rank=r, world_size=2)) for r in range(2)]
+    assert parts[0] == [0, 1, 4, 5, 8, 9] and parts[1] == [2, 3, 6, 7]
+    assert sorted(parts[0] + parts[1]) == list(range(10))
+
+
+def test_lr_schedule_matches_reference_formula():
+    m = TinyModel()
+    opt, sched = T.build_optimizer(m, {"milestones": [3, 6], "cosine_from": 8, "cosine_T_max": 10,
+                                       "cosine_base_lr": 5e-5, "eta_min": 1e-6})
+    lrs = []
+    for _ in range(12):
+        lrs.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sched.step()
+    g = math.sqrt(math.sqrt(0.5))
+    assert lrs[0] == pytest.approx(4e-4) and lrs[3] == pytest.approx(4e-4 * g) and lrs[6] == pytest.approx(4e-4 * g * g)
+    # after the switch: cosine from the reset base lr 5e-5 towards 1e-6
+    for k in range(8, 12):
+        t = k - 8
+        assert lrs[k] == pytest.approx(1e-6 + (5e-5 - 1e-6) * (1 + math.cos(math.pi * t / 10)) / 2, rel=1e-6)
+
+
+def test_checkpoint_roundtrip_and_resume(tmp_path):
+    torch.manual_seed(0)
+    tr = T.Trainer(TinyModel(), {"milestones": [2]}, torch.device("cpu"))
+    ds = T.SyntheticNoisyPatches(patch_size=16, max_num_patchs=8, lambda_noise=25.0)
+    batch = [torch.stack(x) for x in zip(*[ds[i] for i in range(4)])]
+    losses = [tr.step(*batch) for _ in range(3)]
+    assert all(np.isfinite(losses))
+    path = tmp_path / "ck.pt"
+    torch.save(tr.state_dict(), path)
+    ck = torch.load(path, weights_only=True)
+    assert set(ck) == {"i", "model", "optimizer", "lr_scheduler"} and ck["i"] == 3
+    tr2 = T.Trainer(TinyModel(), {"milestones": [2]}, torch.device("cpu"))
+    tr2.load_state_dict(ck)
+    torch.manual_seed(5)          # the latent-perturbation loss draws noise
+    a = tr.step(*batch)
+    torch.manual_seed(5)
+    b = tr2.step(*batch)
+    assert a == pytest.approx(b, rel=1e-6)
+    assert tr2.optimizer.param_groups[0]["lr"] == pytest.approx(tr.optimizer.param_groups[0]["lr"])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        tr = T.Trainer(TinyModel(), {"loss03_weight": 0.0}, torch.device("cpu"))
+        ds = T.SyntheticNoisyPatches(patch_size=16, max_num_patchs=8)
+        idx = [i for i in T.ResumeableSampler(ds, batch_size=2, rank=rank, world_size=world)][:2]
+        batch = [torch.stack(x) for x in zip(*[ds[i] for i in idx])]
+        tr.step(*batch)
+        q.put((rank, {k: v.detach().numpy() for k, v in tr.model.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_step_equals_full_batch_step():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    tr = T.Trainer(TinyModel(), {"loss03_weight": 0.0}, torch.device("cpu"))
+    ds = T.SyntheticNoisyPatches(patch_size=16, max_num_patchs=8)
+    batch = [torch.stack(x) for x in zip(*[ds[i] for i in range(4)])]
+    tr.step(*batch)
+    for k, v in tr.model.state_dict().items():
+        for r in (0, 1):
+            assert np.allclose(res[r][k], v.numpy(), rtol=1e-5, atol=1e-7), (k, r)
