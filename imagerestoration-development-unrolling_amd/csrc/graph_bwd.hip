@@ -33,17 +33,27 @@ namespace grr {
 namespace {
 
 constexpr int NT = 256;
-constexpr int MAX_CHUNKS = 32;   // pixel chunks per (b, plane) for reduction kernels
+constexpr int TARGET_BLOCKS = 4096;   // grid size of the pixel-looping reduction kernels
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// one atomic per wave (lane 0); every lane of the wave must call it
-__device__ __forceinline__ void wave_atomic_add(float* dst, float v) {
+// one atomic per block: wave sums -> LDS -> thread 0.  Every thread of the block must call it
+// (it synchronises); consecutive calls reuse the LDS slots safely.
+__device__ __forceinline__ void block_atomic_add(float* dst, float v) {
+  __shared__ float red[NT / 64];
   v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(dst, v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    if (t != 0.f) atomicAdd(dst, t);
+  }
 }
 
 __device__ __forceinline__ bool inside_e(int e, int r, int c, int H, int W) {
@@ -73,8 +83,9 @@ __device__ __forceinline__ int tap_dx(int t) { return t == 2 ? -1 : (t == 3 ? 1 
 //                 mode 3 Pt: y(q) = sum_t k_t ([q - t in] x(q - t) + [t != 0, q + t out] x(q))  (adjoint of P)
 // out = (acc ? out : 0) + (scale ? scale[g] : 1) * y.   grid (ceil(HW/NT), B*C).
 // ---------------------------------------------------------------------------
+template <int mode>
 __global__ __launch_bounds__(NT) void stencil_kernel(const float* __restrict__ x, const float* __restrict__ taps,
-                                                     int mode, const float* __restrict__ scale, int acc,
+                                                     const float* __restrict__ scale, int acc,
                                                      float* __restrict__ out, int C, int F, int H, int W) {
   const int HW = H * W;
   const int p = blockIdx.x * NT + threadIdx.x;
@@ -89,12 +100,12 @@ __global__ __launch_bounds__(NT) void stencil_kernel(const float* __restrict__ x
 #pragma unroll
   for (int t = 0; t < 5; ++t) {
     const int dy = tap_dy(t), dx = tap_dx(t);
-    if (mode == 0) {
+    if constexpr (mode == 0) {
       y += k[t] * xp[clampi(r + dy, 0, H - 1) * W + clampi(col + dx, 0, W - 1)];
-    } else if (mode == 1) {
+    } else if constexpr (mode == 1) {
       const int rr = r - dy, cc = col - dx;
       if (rr >= 0 && rr < H && cc >= 0 && cc < W) y += k[t] * xp[rr * W + cc];
-    } else if (mode == 2) {
+    } else if constexpr (mode == 2) {
       const int rr = r + dy, cc = col + dx;
       if (rr >= 0 && rr < H && cc >= 0 && cc < W) y += k[t] * xp[rr * W + cc];
     } else {
@@ -111,8 +122,9 @@ __global__ __launch_bounds__(NT) void stencil_kernel(const float* __restrict__ x
 
 // Tap gradients of y = mode(z) contracted with u: gt[c, t] += scale[g] * sum_{b,q} u(q) dy(q)/dk_t.
 // mode 0 (P): dy(q)/dk_t = z(clamp(q + t));  mode 1 (T): z(q - t) [inside].   grid (chunks, B*C).
+template <int mode>
 __global__ __launch_bounds__(NT) void tapgrad_kernel(const float* __restrict__ u, const float* __restrict__ z,
-                                                     int mode, const float* __restrict__ scale,
+                                                     const float* __restrict__ scale,
                                                      float* __restrict__ gt, int C, int F, int H, int W) {
   const int HW = H * W;
   const int plane = blockIdx.y, ch = plane % C;
@@ -125,7 +137,7 @@ __global__ __launch_bounds__(NT) void tapgrad_kernel(const float* __restrict__ u
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
       const int dy = tap_dy(t), dx = tap_dx(t);
-      if (mode == 0) {
+      if constexpr (mode == 0) {
         acc[t] += uv * zp[clampi(r + dy, 0, H - 1) * W + clampi(col + dx, 0, W - 1)];
       } else {
         const int rr = r - dy, cc = col - dx;
@@ -135,7 +147,7 @@ __global__ __launch_bounds__(NT) void tapgrad_kernel(const float* __restrict__ u
   }
   const float sc = scale ? scale[ch / F] : 1.f;
 #pragma unroll
-  for (int t = 0; t < 5; ++t) wave_atomic_add(gt + ch * 5 + t, sc * acc[t]);
+  for (int t = 0; t < 5; ++t) block_atomic_add(gt + ch * 5 + t, sc * acc[t]);
 }
 
 // ---------------------------------------------------------------------------
@@ -154,9 +166,8 @@ __global__ __launch_bounds__(NT) void glr_bwd_kernel(const float* __restrict__ s
                                                      float* __restrict__ gdot, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G;
-  const int p = blockIdx.x * NT + threadIdx.x;
   float dot = 0.f;
-  if (p < HW) {
+  for (int p = blockIdx.x * NT + threadIdx.x; p < HW; p += gridDim.x * NT) {
     const int r = p / W, col = p - r * W;
     const float* wb = w + (int64_t)bg * 4 * HW;
     float we[4], wn[4];
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(NT) void glr_bwd_kernel(const float* __restrict__ s
 #pragma unroll
     for (int e = 0; e < 4; ++e) gwb[e * HW] += sc * gwa[e];
   }
-  if (gdot) wave_atomic_add(gdot + g, coef * dot);
+  if (gdot) block_atomic_add(gdot + g, coef * dot);
 }
 
 // Pair-Laplacian reverse (GTV C^T C, linear part).  K s(p) = sum over the 4 incident edges
@@ -208,9 +219,8 @@ __global__ __launch_bounds__(NT) void pair_bwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ gdot, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G;
-  const int p = blockIdx.x * NT + threadIdx.x;
   float dot = 0.f;
-  if (p < HW) {
+  for (int p = blockIdx.x * NT + threadIdx.x; p < HW; p += gridDim.x * NT) {
     const int r = p / W, col = p - r * W;
     const float* cb = cw + (int64_t)bg * 2 * HW;
     const bool hr = col + 1 < W, hl = col > 0, vd = r + 1 < H, vu = r > 0;
@@ -238,7 +248,7 @@ __global__ __launch_bounds__(NT) void pair_bwd_kernel(const float* __restrict__ 
     if (hr) gcb[0] += sc * gh;
     if (vd) gcb[HW] += sc * gv;
   }
-  if (gdot) wave_atomic_add(gdot + g, coef * dot);
+  if (gdot) block_atomic_add(gdot + g, coef * dot);
 }
 
 // ---------------------------------------------------------------------------
@@ -261,10 +271,9 @@ __global__ __launch_bounds__(NT) void prox_bwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ gdot, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G;
-  const int p = blockIdx.x * NT + threadIdx.x;
   float dot = 0.f, dgam = 0.f;
   const float gm = expf(log_gamma[g]);
-  if (p < HW) {
+  for (int p = blockIdx.x * NT + threadIdx.x; p < HW; p += gridDim.x * NT) {
     const int r = p / W, col = p - r * W;
     const float* wb = w + (int64_t)bg * 4 * HW;
     float we[4], wn[4];
@@ -322,10 +331,10 @@ __global__ __launch_bounds__(NT) void prox_bwd_kernel(const float* __restrict__ 
     float* gwb = gw + (int64_t)bg * 4 * HW + p;
 #pragma unroll
     for (int e = 0; e < 4; ++e) gwb[e * HW] += sc * gwa[e];
-    dgam *= sc;
   }
-  if (gdot) wave_atomic_add(gdot + g, coef * dot);
-  if (ggam) wave_atomic_add(ggam + g, dgam);
+  dgam *= scale ? scale[g] : 1.f;
+  if (gdot) block_atomic_add(gdot + g, coef * dot);
+  if (ggam) block_atomic_add(ggam + g, dgam);
 }
 
 // c[0](p) = w_right(p)^2 + w_left(p+1)^2, c[1](p) = w_down(p)^2 + w_up(p+W)^2 (0 at the frame):
@@ -438,7 +447,7 @@ __global__ __launch_bounds__(NT) void edge_weights_bwd_kernel(const float* __res
       gfp[(int64_t)f * HW + p] = small ? gn * ic : (gn - n * ndg) * ic;
     }
   }
-  for (int f = 0; f < F; ++f) wave_atomic_add(gM + g * F + f, gm_sm[f * NT + threadIdx.x]);
+  for (int f = 0; f < F; ++f) block_atomic_add(gM + g * F + f, gm_sm[f * NT + threadIdx.x]);
 }
 
 // gdot[g] += coef * sum_{b,f,p} u v.      grid (chunks, B*G)
@@ -451,7 +460,7 @@ __global__ __launch_bounds__(NT) void graph_dot_kernel(const float* __restrict__
   const float* vp = v + (int64_t)bg * n;
   float acc = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) acc += up[i] * vp[i];
-  wave_atomic_add(gdot + g, coef * acc);
+  block_atomic_add(gdot + g, coef * acc);
 }
 
 // out = sa[g] * x + sb[g] * y  (sa/sb NULL -> 1; y NULL -> term dropped); acc: out += ...
@@ -496,7 +505,12 @@ __global__ __launch_bounds__(NT) void conv2x2s2_bwd_data_kernel(const float* __r
   gx[(int64_t)bk * HW + p] = acc;
 }
 
-int chunks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, MAX_CHUNKS); }
+// pixel chunks per plane for the reduction kernels: ~TARGET_BLOCKS blocks in total, so each
+// block loops over many pixels and issues few atomics
+int chunks_for(int64_t n, int64_t planes) {
+  const int64_t want = (TARGET_BLOCKS + planes - 1) / planes;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, (n + NT - 1) / NT));
+}
 int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
 
 }  // namespace
@@ -512,10 +526,16 @@ grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const fl
   GRR_REQUIRE(x && taps && out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 && mode >= 0 && mode <= 3,
               GRR_ERR_INVALID_ARG, "grr_bwd_stencil: bad args");
   const int C = G * F;
-  GRR_REQUIRE((int64_t)B * C < 65536 * 16 && (int64_t)H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
+  GRR_REQUIRE((int64_t)B * C <= 65535 && (int64_t)H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_bwd_stencil: grid too large");
-  hipLaunchKernelGGL(stencil_kernel, dim3((H * W + NT - 1) / NT, B * C), dim3(NT), 0, (hipStream_t)stream, x, taps,
-                     mode, scale, accumulate, out, C, F, H, W);
+  const dim3 grid((H * W + NT - 1) / NT, B * C);
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(stencil_kernel<0>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
+    case 1: hipLaunchKernelGGL(stencil_kernel<1>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
+    case 2: hipLaunchKernelGGL(stencil_kernel<2>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
+    default: hipLaunchKernelGGL(stencil_kernel<3>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W);
+  }
   return launch_status("grr_bwd_stencil");
 }
 
@@ -524,8 +544,12 @@ grr_status grr_bwd_tapgrad(const float* u, const float* z, int mode, const float
   clear_error();
   GRR_REQUIRE(u && z && gtaps && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 && (mode == 0 || mode == 1),
               GRR_ERR_INVALID_ARG, "grr_bwd_tapgrad: bad args");
-  hipLaunchKernelGGL(tapgrad_kernel, dim3(chunks_for((int64_t)H * W), B * G * F), dim3(NT), 0, (hipStream_t)stream, u,
-                     z, mode, scale, gtaps, G * F, F, H, W);
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_tapgrad: B*G*F > 65535");
+  const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G * F), B * G * F);
+  if (mode == 0)
+    hipLaunchKernelGGL(tapgrad_kernel<0>, grid, dim3(NT), 0, (hipStream_t)stream, u, z, scale, gtaps, G * F, F, H, W);
+  else
+    hipLaunchKernelGGL(tapgrad_kernel<1>, grid, dim3(NT), 0, (hipStream_t)stream, u, z, scale, gtaps, G * F, F, H, W);
   return launch_status("grr_bwd_tapgrad");
 }
 
@@ -534,7 +558,8 @@ grr_status grr_bwd_glr(const float* s, const float* a, const float* w, const flo
   clear_error();
   GRR_REQUIRE(s && a && w && z_out && ap_out && gw && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_glr: bad args");
-  hipLaunchKernelGGL(glr_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_glr: B*G*F > 65535");
+  hipLaunchKernelGGL(glr_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
                      scale, coef, z_out, ap_out, gw, gdot, G, F, H, W);
   return launch_status("grr_bwd_glr");
 }
@@ -544,7 +569,8 @@ grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const fl
   clear_error();
   GRR_REQUIRE(s && a && c && z_out && ap_out && gc && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_pair: bad args");
-  hipLaunchKernelGGL(pair_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, c,
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_pair: B*G*F > 65535");
+  hipLaunchKernelGGL(pair_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream, s, a, c,
                      scale, coef, z_out, ap_out, gc, gdot, G, F, H, W);
   return launch_status("grr_bwd_pair");
 }
@@ -555,7 +581,8 @@ grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const fl
   clear_error();
   GRR_REQUIRE(s && a && w && log_gamma && o_out && gs_out && gw && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_prox: bad args");
-  hipLaunchKernelGGL(prox_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_prox: B*G*F > 65535");
+  hipLaunchKernelGGL(prox_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
                      log_gamma, scale, coef, o_out, gs_out, gw, ggamma, gdot, G, F, H, W);
   return launch_status("grr_bwd_prox");
 }
@@ -564,6 +591,7 @@ grr_status grr_bwd_pair_weights(const float* w, const float* gc, float* gw, int 
   clear_error();
   GRR_REQUIRE(w && gc && gw && B > 0 && G > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_bwd_pair_weights: bad args");
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_pair_weights: B*G > 65535");
   hipLaunchKernelGGL(pair_weights_bwd_kernel, dim3((H * W + NT - 1) / NT, B * G), dim3(NT), 0, (hipStream_t)stream, w,
                      gc, gw, H, W);
   return launch_status("grr_bwd_pair_weights");
@@ -575,8 +603,9 @@ grr_status grr_bwd_edge_weights(const float* feat, int64_t feat_bstride, const f
   clear_error();
   GRR_REQUIRE(feat && multiM && w && gw && gfeat && gmultiM && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_edge_weights: bad args");
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: B*G*F > 65535");
   GRR_REQUIRE(F <= GRR_MAX_NODE_FTS, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: F=%d > %d", F, GRR_MAX_NODE_FTS);
-  hipLaunchKernelGGL(edge_weights_bwd_kernel, dim3(chunks_for((int64_t)H * W), B * G), dim3(NT), 0,
+  hipLaunchKernelGGL(edge_weights_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0,
                      (hipStream_t)stream, feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, G, F, H,
                      W);
   return launch_status("grr_bwd_edge_weights");
@@ -587,7 +616,8 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   clear_error();
   GRR_REQUIRE(u && v && gdot && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_bwd_graph_dot: bad args");
-  hipLaunchKernelGGL(graph_dot_kernel, dim3(chunks_for((int64_t)F * H * W), B * G), dim3(NT), 0, (hipStream_t)stream,
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_graph_dot: B*G*F > 65535");
+  hipLaunchKernelGGL(graph_dot_kernel, dim3(chunks_for((int64_t)F * H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream,
                      u, v, coef, gdot, G, F, (int64_t)H * W);
   return launch_status("grr_bwd_graph_dot");
 }
@@ -618,7 +648,7 @@ grr_status grr_conv2x2s2_bwd_data(const float* g, const float* wt, float* gx, in
   GRR_REQUIRE(g && wt && gx && B > 0 && K > 0 && M > 0 && H > 1 && W > 1, GRR_ERR_INVALID_ARG,
               "grr_conv2x2s2_bwd_data: bad args");
   GRR_REQUIRE(H % 2 == 0 && W % 2 == 0, GRR_ERR_SHAPE, "grr_conv2x2s2_bwd_data: H, W must be even");
-  GRR_REQUIRE((int64_t)B * K < 65536 * 16, GRR_ERR_UNSUPPORTED, "grr_conv2x2s2_bwd_data: grid too large");
+  GRR_REQUIRE((int64_t)B * K <= 65535, GRR_ERR_UNSUPPORTED, "grr_conv2x2s2_bwd_data: grid too large");
   hipLaunchKernelGGL(conv2x2s2_bwd_data_kernel, dim3((H * W + NT - 1) / NT, B * K), dim3(NT), 0, (hipStream_t)stream,
                      g, wt, gx, K, M, H, W);
   return launch_status("grr_conv2x2s2_bwd_data");
