@@ -194,6 +194,7 @@ struct OpArgs {
   int G, F, H, W, tiles_x, tiles_y;
   int nstrips, nsegs, sseg;
   int lin_l;            // log_l holds the scale itself (v10 MixtureGLR stores mu linearly)
+  int wpb;              // row kernel: waves per block = channels of one graph walked in lockstep
   uint32_t nunits, nblk;
 };
 
@@ -603,8 +604,11 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
   constexpr int NH = (V + 1) / 2;    // half-resolution values per lane
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * 4 + wave;
-  if (unit >= a.nunits) return;   // whole wave (uniform)
+  // a block = wpb channel waves of one (b, graph, segment): they walk the rows in lockstep
+  // (one barrier per two rows), so the graph's edge-weight rows are fetched from HBM once
+  // and served to the other channel waves by L1/L2 (the grid divides exactly: no wave
+  // leaves early, every wave reaches every barrier)
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * a.wpb + wave;
   const int F = a.F;
   const int f = unit % F; unit /= F;
   const int seg = unit % a.nsegs; unit /= a.nsegs;
@@ -872,11 +876,13 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
   RowLoadsV<V> A, B;
   issue(ts, A);
   issue(ts + 1, B);
+  const bool lockstep = a.wpb > 1;
   for (int t = ts; t < te; t += 2) {
     consume(t, A, std::false_type{});
     issue(t + 2, A);
     consume(t + 1, B, std::true_type{});
     issue(t + 3, B);
+    if (lockstep) __builtin_amdgcn_s_barrier();
   }
 }
 
@@ -894,8 +900,12 @@ static void launch_row(OpArgs a, int B, hipStream_t s) {
   a.nsegs = (a.H + a.sseg - 1) / a.sseg;
   const uint64_t units = (uint64_t)B * a.G * a.F * a.nsegs;
   a.nunits = (uint32_t)units;
-  a.nblk = (uint32_t)((units + 3) / 4);
-  hipLaunchKernelGGL((graph_row_kernel<GLR, GTV, EPI, V>), dim3(a.nblk), dim3(NT), 0, s, a);
+  // channels of a graph per block: the largest divisor of F that fits NT threads
+  int wpb = g_kernel_variant == 2 ? 1 : NT / 64;
+  while (a.F % wpb) --wpb;
+  a.wpb = wpb;
+  a.nblk = (uint32_t)(units / wpb);
+  hipLaunchKernelGGL((graph_row_kernel<GLR, GTV, EPI, V>), dim3(a.nblk), dim3(64 * wpb), 0, s, a);
 }
 
 template <bool GLR, int GTV, int EPI>
@@ -943,7 +953,7 @@ int grr_version(void) { return 1; }
 
 grr_status grr_set_kernel_variant(int variant) {
   clear_error();
-  GRR_REQUIRE(variant == 0 || variant == 1, GRR_ERR_INVALID_ARG, "grr_set_kernel_variant: %d", variant);
+  GRR_REQUIRE(variant >= 0 && variant <= 2, GRR_ERR_INVALID_ARG, "grr_set_kernel_variant: %d", variant);
   g_kernel_variant = variant;
   return GRR_OK;
 }

@@ -102,9 +102,10 @@ NO_STENCIL = Stencil(None, None, None, None)
 
 # ---------------------------------------------------------------------------
 def set_kernel_variant(variant: str) -> None:
-    """Select the graph-operator kernels: "auto" (row waves for W <= 256) or "strips"
-    (column strips at every width).  Test / benchmark knob; process-wide."""
-    _native.call("grr_set_kernel_variant", {"auto": 0, "strips": 1}[variant])
+    """Select the graph-operator kernels: "auto" (row waves for W <= 256, the channel waves
+    of a graph in lockstep), "strips" (column strips at every width) or "independent" (row
+    waves, channel waves unsynchronised).  Test / benchmark knob; process-wide."""
+    _native.call("grr_set_kernel_variant", {"auto": 0, "strips": 1, "independent": 2}[variant])
 
 
 def neighbor_table(h: int, w: int, device) -> Tensor:

@@ -22,11 +22,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--variant", default="auto", choices=["auto", "strips"])
+    ap.add_argument("--variant", default="auto", choices=["auto", "strips", "independent"])
+    ap.add_argument("--graphs", type=int, default=32)
+    ap.add_argument("--fts", type=int, default=3)
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
     dev = torch.device("cuda", 0)
-    b, g, f, h, w = args.batch, 32, 3, args.size, args.size
+    b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.size
     c = g * f
     torch.manual_seed(0)
     mix = irdu_amd.MixtureGTVGLR(g, f, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]],

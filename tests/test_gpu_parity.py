@@ -29,7 +29,7 @@ def irdu():
 DEV = "cuda"
 
 
-@pytest.fixture(params=["auto", "strips"])
+@pytest.fixture(params=["auto", "strips", "independent"])
 def variant(irdu, request):
     """Run a test with the row-wave graph kernels (auto, W <= 256) and with the column-strip
     kernels forced at every width."""
