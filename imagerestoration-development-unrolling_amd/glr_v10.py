@@ -12,8 +12,8 @@ residual + heavy-ball update); the edge weights are built once.  ``n_cgd_iters``
 5-stage GLR, gray 256x256, G=8 graphs, F=1): the image replicated over the G graphs
 (as REF13:918-921 does for RGB), MixtureGLR, then a 1x1 projection back.
 
-State-dict keys match the reference.  Training through these blocks is not wired to a
-reverse kernel yet: autograd recording attaches a node whose backward raises.
+State-dict keys match the reference.  Training: when autograd records, the solver runs
+``solver_grad._GLRSolve`` (HIP forward keeping the iterates + HIP reverse sweep).
 """
 from __future__ import annotations
 
@@ -22,7 +22,8 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
-from .graph_filter import GLRFast, hip_forward
+from . import solver_grad as SG
+from .graph_filter import GLRFast, records_grad
 
 
 class MixtureGLR(nn.Module):
@@ -39,13 +40,17 @@ class MixtureGLR(nn.Module):
         self.muys00 = Parameter(torch.ones(n_graphs) * muy_init[0])
         self.GLRmodule00 = GLRFast(n_node_fts, n_graphs, M_diag_init=1.0)
 
-    @hip_forward
     def forward(self, patchs):
         y = patchs.contiguous()
-        b, c, h, w = y.shape
+        if y.shape[1] != self.n_channels:
+            raise ValueError(f"MixtureGLR: expected {self.n_channels} channels, got {y.shape[1]}")
+        if records_grad(self, y):
+            return SG.glr_solve(self, y, SG.Conv1x1Fn.apply(y, self.patchs_features_extraction[0].weight))
+        return self._solve(y)
+
+    @torch.no_grad()
+    def _solve(self, y):
         g, f = self.n_graphs, self.n_node_fts
-        if c != self.n_channels:
-            raise ValueError(f"MixtureGLR: expected {self.n_channels} channels, got {c}")
         feat = K.conv1x1(y, self.patchs_features_extraction[0].weight.data)
         wL, _ = K.edge_weights(feat, 0, g, f, self.GLRmodule00.multiM.data)
         del feat
@@ -80,7 +85,11 @@ class GLRImageFilter(nn.Module):
                                       n_cgd_iters=n_cgd_iters)
         self.linear_combination = nn.Conv2d(ngraphs * n_channels_in, n_channels_out, 1, bias=False)
 
-    @hip_forward
     def forward(self, img):
-        x = K.repeat_graphs(img.contiguous(), self.ngraphs)
-        return K.conv1x1(self.localfilter(x), self.linear_combination.weight.data)
+        img = img.contiguous()
+        if records_grad(self, img):
+            y = self.localfilter(SG.RepeatGraphsFn.apply(img, self.ngraphs))
+            return SG.Conv1x1Fn.apply(y.contiguous(), self.linear_combination.weight)
+        with torch.no_grad():
+            x = K.repeat_graphs(img, self.ngraphs)
+            return K.conv1x1(self.localfilter(x), self.linear_combination.weight.data)

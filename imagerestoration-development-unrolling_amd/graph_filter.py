@@ -94,9 +94,14 @@ class _GraphModule(nn.Module):
         self.register_buffer("stats_kernel03", b03, persistent=False)
         self.multiM = Parameter(torch.full((n_graphs, n_node_fts), float(M_diag_init)))
 
-    @hip_forward
     def extract_edge_weights(self, img_features: torch.Tensor):
         """[B,G,F,H,W] features -> (w [B,G,4,H,W], degree [B,G,H,W]) (REF:160-175)."""
+        if records_grad(self, img_features):
+            return SG.edge_weights(self, img_features)
+        return self._edge_weights(img_features)
+
+    @torch.no_grad()
+    def _edge_weights(self, img_features: torch.Tensor):
         b, g, f, h, w = img_features.shape
         x = img_features.reshape(b, g * f, h, w).contiguous()
         return K.edge_weights(x, 0, g, f, self.multiM.data.contiguous(), with_degree=True)
@@ -109,8 +114,13 @@ class _GraphModule(nn.Module):
 class GLRFast(_GraphModule):
     """Graph-Laplacian regulariser S^T (I - W) S (REF:13-237)."""
 
-    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
+        if records_grad(self, patchs, edge_weights):
+            return SG.graph_apply(self, "glr", patchs, edge_weights)
+        return self._hip_apply(patchs, edge_weights)
+
+    @torch.no_grad()
+    def _hip_apply(self, patchs, edge_weights):
         b, g, f, h, w = patchs.shape
         out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), edge_weights.contiguous(), None,
                             K.stencil(self), K.NO_STENCIL, None, None, g)
@@ -120,8 +130,13 @@ class GLRFast(_GraphModule):
 class GTVFast(_GraphModule):
     """Graph total variation C^T C with C = W (S - S shifted) (REF:242-523)."""
 
-    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
+        if records_grad(self, patchs, edge_weights):
+            return SG.graph_apply(self, "gtv", patchs, edge_weights)
+        return self._hip_apply(patchs, edge_weights)
+
+    @torch.no_grad()
+    def _hip_apply(self, patchs, edge_weights):
         b, g, f, h, w = patchs.shape
         c = K.gtv_pair_weights(edge_weights.contiguous())
         out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), None, c,

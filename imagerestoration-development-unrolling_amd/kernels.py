@@ -324,7 +324,7 @@ def bwd_glr(s: Tensor, a: Tensor, w: Tensor, scale: Tensor, coef: float, gw: Ten
     dev = _check("bwd_glr", s, a, w, scale, gw, gdot)
     z, ap = torch.empty_like(s), torch.empty_like(s)
     _launch("bwd_glr", 4 * (4 * s.numel() + 3 * w.numel()), "grr_bwd_glr", s.data_ptr(), a.data_ptr(), w.data_ptr(),
-            scale.data_ptr(), float(coef), z.data_ptr(), ap.data_ptr(), gw.data_ptr(), gdot.data_ptr(),
+            scale.data_ptr(), float(coef), z.data_ptr(), ap.data_ptr(), gw.data_ptr(), _ptr(gdot),
             *_bgfhw(s, n_graphs), _stream(dev))
     return z, ap
 
@@ -333,7 +333,7 @@ def bwd_pair(s: Tensor, a: Tensor, c: Tensor, scale: Tensor, coef: float, gc: Te
     dev = _check("bwd_pair", s, a, c, scale, gc, gdot)
     z, ap = torch.empty_like(s), torch.empty_like(s)
     _launch("bwd_pair", 4 * (4 * s.numel() + 3 * c.numel()), "grr_bwd_pair", s.data_ptr(), a.data_ptr(), c.data_ptr(),
-            scale.data_ptr(), float(coef), z.data_ptr(), ap.data_ptr(), gc.data_ptr(), gdot.data_ptr(),
+            scale.data_ptr(), float(coef), z.data_ptr(), ap.data_ptr(), gc.data_ptr(), _ptr(gdot),
             *_bgfhw(s, n_graphs), _stream(dev))
     return z, ap
 

@@ -22,7 +22,7 @@ are differentiated as the reference stores them (logs of mu, ro, gamma).
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -49,6 +49,33 @@ def solver_params(mod) -> List[Tensor]:
     return out
 
 
+def glr_term_bwd(x: Tensor, g: Tensor, taps: Tensor, w: Tensor, scale: Tensor, coef: float, n_graphs: int,
+                 out: Tensor, gw: Tensor, gscale: Optional[Tensor], gtaps: Tensor) -> None:
+    """Reverse of the GLR term  scale[g] * T((I - W) P x)  (REF:218-237) contracted with coef * g:
+    out += coef*scale * P*(I-W)^T T* g; gw, gtaps += coef*scale * d/d(.); gscale += coef * <g, T(I-W)Px>."""
+    sc = scale * coef
+    s = K.bwd_stencil(x, taps, K.ST_P, n_graphs)
+    a = K.bwd_stencil(g, taps, K.ST_T_ADJ, n_graphs)
+    z, ap = K.bwd_glr(s, a, w, sc, coef, gw, gscale, n_graphs)
+    del s, a
+    K.bwd_tapgrad(g, z, K.ST_T, n_graphs, sc, gtaps)
+    K.bwd_tapgrad(ap, x, K.ST_P, n_graphs, sc, gtaps)
+    K.bwd_stencil(ap, taps, K.ST_P_ADJ, n_graphs, sc, out=out)
+
+
+def gtv_term_bwd(x: Tensor, g: Tensor, taps: Tensor, c: Tensor, scale: Tensor, coef: float, n_graphs: int,
+                 out: Tensor, gc: Tensor, gscale: Optional[Tensor], gtaps: Tensor) -> None:
+    """Reverse of the linear GTV term  scale[g] * T(K_c P x)  (C^T C with pair weights, REF:452-523)."""
+    sc = scale * coef
+    s = K.bwd_stencil(x, taps, K.ST_P, n_graphs)
+    a = K.bwd_stencil(g, taps, K.ST_T_ADJ, n_graphs)
+    z, ap = K.bwd_pair(s, a, c, sc, coef, gc, gscale, n_graphs)
+    del s, a
+    K.bwd_tapgrad(g, z, K.ST_T, n_graphs, sc, gtaps)
+    K.bwd_tapgrad(ap, x, K.ST_P, n_graphs, sc, gtaps)
+    K.bwd_stencil(ap, taps, K.ST_P_ADJ, n_graphs, sc, out=out)
+
+
 class _Level:
     """One resolution level of the operator: its graphs, stencils, scalars and gradient buffers."""
 
@@ -66,25 +93,9 @@ class _Level:
 
     def terms_bwd(self, x: Tensor, g: Tensor, coef: float, out: Tensor, glr: bool = True) -> None:
         """out += coef * (mu L^T + ro G^T) g, and coef * d<g, mu L x + ro G x>/d(params) into the buffers."""
-        G = self.g
         if glr:
-            sc = self.mu * coef
-            s = K.bwd_stencil(x, self.tapsL, K.ST_P, G)
-            a = K.bwd_stencil(g, self.tapsL, K.ST_T_ADJ, G)
-            z, ap = K.bwd_glr(s, a, self.wL, sc, coef, self.gwL, self.gmu, G)
-            del s, a
-            K.bwd_tapgrad(g, z, K.ST_T, G, sc, self.gtapL)
-            K.bwd_tapgrad(ap, x, K.ST_P, G, sc, self.gtapL)
-            K.bwd_stencil(ap, self.tapsL, K.ST_P_ADJ, G, sc, out=out)
-            del z, ap
-        sc = self.ro * coef
-        s = K.bwd_stencil(x, self.tapsG, K.ST_P, G)
-        a = K.bwd_stencil(g, self.tapsG, K.ST_T_ADJ, G)
-        z, ap = K.bwd_pair(s, a, self.cG, sc, coef, self.gcG, self.gro, G)
-        del s, a
-        K.bwd_tapgrad(g, z, K.ST_T, G, sc, self.gtapG)
-        K.bwd_tapgrad(ap, x, K.ST_P, G, sc, self.gtapG)
-        K.bwd_stencil(ap, self.tapsG, K.ST_P_ADJ, G, sc, out=out)
+            glr_term_bwd(x, g, self.tapsL, self.wL, self.mu, coef, self.g, out, self.gwL, self.gmu, self.gtapL)
+        gtv_term_bwd(x, g, self.tapsG, self.cG, self.ro, coef, self.g, out, self.gcG, self.gro, self.gtapG)
 
     def prox_bwd(self, x: Tensor, g: Tensor, out: Tensor) -> None:
         """out += ro C^T-part reverse of the prox rhs term ro T(Ct phi(C P x)); parameter gradients."""
@@ -291,3 +302,149 @@ class RepeatGraphsFn(torch.autograd.Function):
     def backward(ctx, g: Tensor):
         b, c, h, w = g.shape
         return g.reshape(b, ctx.n_graphs, c // ctx.n_graphs, h, w).sum(1), None
+
+
+# ---- GLRFast / GTVFast / extract_edge_weights sub-API (REF:146-237, :391-523) ----------
+def _taps_params(module) -> Tuple[Tensor, ...]:
+    return (module.stats_kernel_p01, module.stats_kernel_p02a, module.stats_kernel_p02b, module.stats_kernel_p03)
+
+
+class _GraphApply(torch.autograd.Function):
+    """GLRFast.forward (kind 'glr': S^T (I - W) S x) or GTVFast.forward (kind 'gtv': C^T C x)."""
+
+    @staticmethod
+    def forward(ctx, kind: str, n_graphs: int, x: Tensor, w: Tensor, p01, p02a, p02b, p03) -> Tensor:
+        st = Stencil(*[t.data_ptr() for t in (p01, p02a, p02b, p03)])
+        if kind == "glr":
+            out = K.system_half(x, w, None, st, K.NO_STENCIL, None, None, n_graphs)
+            ctx.save_for_backward(x, w, p01, p02a, p02b, p03)
+        else:
+            c = K.gtv_pair_weights(w)
+            out = K.system_half(x, None, c, K.NO_STENCIL, st, None, None, n_graphs)
+            ctx.save_for_backward(x, w, p01, p02a, p02b, p03, c)
+        ctx.kind, ctx.n_graphs = kind, n_graphs
+        return out
+
+    @staticmethod
+    def backward(ctx, gout: Tensor):
+        x, w, p01, p02a, p02b, p03 = ctx.saved_tensors[:6]
+        g, gout = ctx.n_graphs, gout.contiguous()
+        taps = K.stencil_taps(p01, p02a, p02b, p03)
+        one = torch.ones(g, dtype=torch.float32, device=x.device)
+        gx, gw, gtaps = torch.zeros_like(x), torch.zeros_like(w), torch.zeros_like(taps)
+        if ctx.kind == "glr":
+            glr_term_bwd(x, gout, taps, w, one, 1.0, g, gx, gw, None, gtaps)
+        else:
+            c = ctx.saved_tensors[6]
+            gc = torch.zeros_like(c)
+            gtv_term_bwd(x, gout, taps, c, one, 1.0, g, gx, gc, None, gtaps)
+            K.bwd_pair_weights(w, gc, gw)
+        return (None, None, gx, gw, *K.stencil_taps_backward(gtaps))
+
+
+def graph_apply(module, kind: str, x5: Tensor, w: Tensor) -> Tensor:
+    b, g, f, h, ww = x5.shape
+    out = _GraphApply.apply(kind, g, x5.reshape(b, g * f, h, ww).contiguous(), w.contiguous(), *_taps_params(module))
+    return out.view(b, g, f, h, ww)
+
+
+class _EdgeWeights(torch.autograd.Function):
+    """extract_edge_weights: features [B,G*F,H,W] -> (w [B,G,4,H,W], degree [B,G,H,W])."""
+
+    @staticmethod
+    def forward(ctx, n_graphs: int, feat: Tensor, multiM: Tensor):
+        w, deg = K.edge_weights(feat, 0, n_graphs, feat.shape[1] // n_graphs, multiM, with_degree=True)
+        ctx.save_for_backward(feat, multiM, w)
+        ctx.n_graphs = n_graphs
+        return w, deg
+
+    @staticmethod
+    def backward(ctx, gw: Optional[Tensor], gdeg: Optional[Tensor]):
+        feat, multiM, w = ctx.saved_tensors
+        g = ctx.n_graphs
+        gw_t = torch.zeros_like(w) if gw is None else gw.contiguous().clone()
+        if gdeg is not None:                      # degree = sum_e w_e
+            gw_t += gdeg.unsqueeze(2)
+        gfeat, gM = torch.empty_like(feat), torch.zeros_like(multiM)
+        K.bwd_edge_weights(feat, 0, g, feat.shape[1] // g, multiM, w, gw_t, gfeat, gM)
+        return None, gfeat, gM
+
+
+def edge_weights(module, f5: Tensor):
+    b, g, f, h, w = f5.shape
+    return _EdgeWeights.apply(g, f5.reshape(b, g * f, h, w).contiguous(), module.multiM)
+
+
+# ---- v10 MixtureGLR (lib/model_GLR_GTV_deep_v10.py:241-335) -----------------------------
+V10_PARAMS = ("GLRmodule00.multiM",) + tuple(f"GLRmodule00.{q}" for q in STENCIL_PARAMS) + (
+    "muys00", "alphaCGD", "betaCGD")
+
+
+class _GLRSolve(torch.autograd.Function):
+    """(y, feat, params) -> x_S of the GLR-only heavy-ball solver, A = I + mu L with mu linear."""
+
+    @staticmethod
+    def forward(ctx, n_graphs: int, y: Tensor, feat: Tensor, *params: Tensor) -> Tensor:
+        p = dict(zip(V10_PARAMS, params))
+        g = n_graphs
+        wL, _ = K.edge_weights(feat, 0, g, y.shape[1] // g, p["GLRmodule00.multiM"])
+        st = Stencil(*[p[f"GLRmodule00.{q}"].data_ptr() for q in STENCIL_PARAMS])
+        mu, alpha, beta = p["muys00"], p["alphaCGD"], p["betaCGD"]
+        n_st = alpha.shape[0]
+        x, u = K.glr_stage(y, y, None, wL, st, mu, alpha[0], None, g)       # u_0 = r_0, x_1
+        xs, us = [y, x], [u]
+        for k in range(1, n_st):
+            x, u = K.glr_stage(x, y, u, wL, st, mu, alpha[k], beta[k], g)
+            xs.append(x)
+            us.append(u)
+        ctx.n_graphs, ctx.n_st = g, n_st
+        ctx.save_for_backward(y, feat, wL, *params, *xs[1:-1], *us)
+        return xs[-1]
+
+    @staticmethod
+    def backward(ctx, gout: Tensor):
+        g, n_st = ctx.n_graphs, ctx.n_st
+        sv = ctx.saved_tensors
+        y, feat, wL = sv[:3]
+        npar = len(V10_PARAMS)
+        params = sv[3:3 + npar]
+        xs = (y,) + tuple(sv[3 + npar:3 + npar + n_st - 1])      # x_0 = y, x_1 .. x_{S-1}
+        us = sv[3 + npar + n_st - 1:]                             # u_0 .. u_{S-1}
+        p = dict(zip(V10_PARAMS, params))
+        mu, alpha, beta = p["muys00"], p["alphaCGD"], p["betaCGD"]
+        taps = K.stencil_taps(*[p[f"GLRmodule00.{q}"] for q in STENCIL_PARAMS])
+        gw, gtaps, gmu = torch.zeros_like(wL), torch.zeros_like(taps), torch.zeros_like(mu)
+        galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
+        gy = torch.zeros_like(y)
+        gx = gout.contiguous()
+        gu_next = None
+        neg = torch.full_like(mu, -1.0)
+        for k in range(n_st - 1, -1, -1):
+            # x_{k+1} = x_k + a_k u_k,  u_k = (y - A x_k) + b_k u_{k-1}   (u_{-1} = 0; x_0 = y)
+            K.bwd_graph_dot(gx, us[k], galpha[k], g)
+            if gu_next is not None:
+                gu = K.bwd_lincomb(gx, alpha[k], gu_next, beta[k + 1], g)
+            else:
+                gu = K.bwd_lincomb(gx, alpha[k], None, None, g)
+            if k >= 1:
+                K.bwd_graph_dot(gu, us[k - 1], gbeta[k], g)
+            K.bwd_lincomb(gu, None, None, None, g, out=gy, accumulate=True)
+            if k >= 1:
+                gx = K.bwd_lincomb(gx, None, gu, neg, g)                   # gx_{k+1} - gu
+                glr_term_bwd(xs[k], gu, taps, wL, mu, -1.0, g, gx, gw, gmu, gtaps)
+            else:                                                           # x_0 = y
+                K.bwd_lincomb(gx, None, gu, neg, g, out=gy, accumulate=True)
+                glr_term_bwd(y, gu, taps, wL, mu, -1.0, g, gy, gw, gmu, gtaps)
+            gu_next = gu
+        gfeat, gM = torch.empty_like(feat), torch.zeros_like(p["GLRmodule00.multiM"])
+        K.bwd_edge_weights(feat, 0, g, y.shape[1] // g, p["GLRmodule00.multiM"], wL, gw, gfeat, gM)
+        grads = {"GLRmodule00.multiM": gM, "muys00": gmu, "alphaCGD": galpha, "betaCGD": gbeta}
+        for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gtaps)):
+            grads[f"GLRmodule00.{q}"] = gq
+        return (None, gy, gfeat, *[grads[n] for n in V10_PARAMS])
+
+
+def glr_solve(mod, y: Tensor, feat: Tensor) -> Tensor:
+    params = [mod.GLRmodule00.multiM] + [getattr(mod.GLRmodule00, q) for q in STENCIL_PARAMS] + [
+        mod.muys00, mod.alphaCGD, mod.betaCGD]
+    return _GLRSolve.apply(mod.n_graphs, y, feat.contiguous(), *params)

@@ -346,12 +346,12 @@ def test_single_stage_and_odd_half_level(irdu, variant):
 
 
 def test_backward_fails_loudly(irdu):
-    """Entry points without a reverse kernel (the GLRFast/GTVFast sub-API) raise in backward
-    instead of silently dropping gradients."""
-    m = irdu.GLRFast(3, 2, M_diag_init=1.0).to(DEV)
-    x = torch.rand(1, 2, 3, 16, 16, device=DEV, requires_grad=True)
-    w = torch.softmax(torch.rand(1, 2, 4, 16, 16, device=DEV), dim=2)
-    y = m(x, w)
+    """A HIP forward without a reverse kernel (the fused LocalNonLinearBlock, whose training
+    pass runs on stock ops) raises in backward if reached with autograd on, instead of
+    silently dropping gradients."""
+    blk = irdu.LocalNonLinearBlock(8, 16, 1).to(DEV)
+    x = torch.rand(1, 8, 16, 16, device=DEV, requires_grad=True)
+    y = blk._forward_hip(x)
     with pytest.raises(NotImplementedError):
         y.sum().backward()
 
@@ -412,3 +412,56 @@ def test_mixture_grad_vs_reference_golden(irdu, name):
     assert_close(xg.grad, d["grad/x"], 2e-4)
     for k, p in mix.named_parameters():
         assert_close(p.grad, d["grad/" + k], 2e-4)
+
+
+@pytest.mark.parametrize("name", ["mixture_glr_v10.npz", "mixture_glr_v10_f1.npz"])
+def test_mixture_glr_v10_grad_vs_reference_golden(irdu, name):
+    """v10 MixtureGLR L1-loss gradients (HIP reverse) vs the reference's autograd gradients."""
+    d = load_golden(name)
+    g = int(d["meta/n_graphs"])
+    x = torch.from_numpy(d["in/x"])
+    mix = irdu.MixtureGLR(g, x.shape[1] // g, 0.5, 0.1, [[0.001]])
+    mix.load_state_dict(params_of(d, ""))
+    mix = mix.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    torch.nn.functional.l1_loss(mix(xg), torch.from_numpy(d["in/target"]).to(DEV)).backward()
+    assert_close(xg.grad, d["grad/x"], 2e-4)
+    # with F = 1 the normalised feature is sign(f) (REF:146-157): the feature-conv gradient is 0
+    # analytically and both sides hold rounding noise (~1e-9), so errors are measured against
+    # max(|ref|, 1e-4 x the largest parameter gradient)
+    floor = 1e-4 * max(float(abs(d["grad/" + k]).max()) for k, _ in mix.named_parameters())
+    for k, p in mix.named_parameters():
+        ref = torch.from_numpy(d["grad/" + k]).double()
+        err = float((p.grad.detach().double().cpu() - ref).abs().max()) / max(float(ref.abs().max()), floor)
+        assert err <= 2e-4, (k, err)
+
+
+def test_graph_module_sub_api_grads(irdu):
+    """GLRFast / GTVFast forward and extract_edge_weights (the reference's sub-API) under
+    autograd vs the fp64 oracle: gradients of input, edge weights and every parameter."""
+    from tests.test_gpu_grad import weights_r
+    torch.manual_seed(21)
+    b, g, f, h, w = 2, 3, 4, 14, 18
+    feat = rand(b, g, f, h, w, seed=22)
+    x = rand(b, g, f, h, w, seed=23)
+    for cls, apply in ((irdu.GLRFast, O.glr_apply), (irdu.GTVFast, O.gtv_apply)):
+        m = perturbed_graph_module(cls(f, g, M_diag_init=1.0), 24)
+        torch.set_default_dtype(torch.float64)
+        try:
+            p = {k: v.detach().double().requires_grad_(True) for k, v in m.state_dict().items()}
+            fd, xd = feat.double().requires_grad_(True), x.double().requires_grad_(True)
+            wgt, _ = O.edge_weights(fd, p["multiM"])
+            out = apply(xd, wgt, O.stats_kernel(p, ""))
+            (out * weights_r(out.shape).double()).sum().backward()
+        finally:
+            torch.set_default_dtype(torch.float32)
+        m = m.to(DEV)
+        fg, xg = feat.to(DEV).requires_grad_(True), x.to(DEV).requires_grad_(True)
+        wg, _ = m.extract_edge_weights(fg)
+        og = m(xg, wg)
+        (og * weights_r(og.shape).to(DEV)).sum().backward()
+        assert_close(og, out.detach(), 1e-5)
+        assert_close(xg.grad, xd.grad, 2e-4)
+        assert_close(fg.grad, fd.grad, 2e-4)
+        for k, prm in m.named_parameters():
+            assert_close(prm.grad, p[k].grad, 2e-4)
