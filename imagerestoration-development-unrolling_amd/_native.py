@@ -72,6 +72,11 @@ SIGNATURES = {
     "grr_bwd_lincomb": [P, P, P, P, P, I, I, I, I, I, I, P],
     "grr_bwd_unpool2_acc": [P, P, I, I, I, I, P],
     "grr_conv2x2s2_bwd_data": [P, P, P, I, I, I, I, I, P],
+    "grr_lnb_norm": [P, P, P, P, I, I, L, P],
+    "grr_lnb_norm_bwd": [P, P, P, P, P, P, I, I, L, P],
+    "grr_dwconv3": [P, P, P, I, I, I, I, P],
+    "grr_dwconv3_bwd": [P, P, P, P, P, I, I, I, I, P],
+    "grr_lnb_gate": [P, P, P, P, I, I, L, P],
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64}

@@ -187,10 +187,13 @@ class LocalNonLinearBlock(nn.Module):
         self.skip_weight = Parameter(torch.tensor([1.0, 1.0], dtype=torch.float32))
 
     def forward(self, x):
-        if self.nsubnets != 1 or records_grad(self, x):
-            # grouped variant (encoder/decoder configs) and the training path: stock PyTorch-ROCm
-            # ops (the fused HIP block has no reverse kernel yet)
+        if self.nsubnets != 1:
+            # grouped variant (encoder/decoder configs only, outside the hot path): stock PyTorch-ROCm ops
             return self.skip_weight[0] * x + self.skip_weight[1] * self.local_linear(self.norm(x))
+        if records_grad(self, x):
+            ll = self.local_linear
+            return SG.LNBFn.apply(x.contiguous(), self.norm.weighted_transform.weight, ll.channels_linear_op.weight,
+                                  ll.channels_local_linear_op.weight, ll.project_out.weight, self.skip_weight)
         return self._forward_hip(x)
 
     @hip_forward

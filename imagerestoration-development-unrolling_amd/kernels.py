@@ -422,3 +422,51 @@ def glr_stage(x: Tensor, b: Tensor, u_prev: Optional[Tensor], wL: Tensor, sL: St
             mu.data_ptr(), alpha.data_ptr(), _ptr(beta), out.data_ptr(), _ptr(u_out), bb, n_graphs, c // n_graphs,
             h, w, _stream(dev))
     return out, u_out
+
+
+# ---- LocalNonLinearBlock reverse pieces ---------------------------------------
+def lnb_norm(x: Tensor, ln_w: Tensor) -> Tuple[Tensor, Tensor]:
+    dev = _check("lnb_norm", x, ln_w)
+    b, c, h, w = x.shape
+    n = torch.empty_like(x)
+    isd = torch.empty((b, h, w), dtype=torch.float32, device=dev)
+    _launch("lnb_bwd", 8 * x.numel(), "grr_lnb_norm", x.data_ptr(), ln_w.data_ptr(), n.data_ptr(), isd.data_ptr(),
+            b, c, h * w, _stream(dev))
+    return n, isd
+
+
+def lnb_norm_bwd(x: Tensor, ln_w: Tensor, isd: Tensor, gn: Tensor, gx: Tensor, gln_w: Tensor) -> None:
+    dev = _check("lnb_norm_bwd", x, ln_w, isd, gn, gx, gln_w)
+    b, c, h, w = x.shape
+    _launch("lnb_bwd", 20 * x.numel(), "grr_lnb_norm_bwd", x.data_ptr(), ln_w.data_ptr(), isd.data_ptr(),
+            gn.data_ptr(), gx.data_ptr(), gln_w.data_ptr(), b, c, h * w, _stream(dev))
+
+
+def dwconv3(h: Tensor, wdw: Tensor) -> Tensor:
+    dev = _check("dwconv3", h, wdw)
+    b, c, hh, ww = h.shape
+    out = torch.empty_like(h)
+    _launch("lnb_bwd", 8 * h.numel(), "grr_dwconv3", h.data_ptr(), wdw.data_ptr(), out.data_ptr(), b, c, hh, ww,
+            _stream(dev))
+    return out
+
+
+def dwconv3_bwd(g: Tensor, h: Tensor, wdw: Tensor, gwdw: Tensor) -> Tensor:
+    dev = _check("dwconv3_bwd", g, h, wdw, gwdw)
+    b, c, hh, ww = h.shape
+    gh = torch.empty_like(h)
+    _launch("lnb_bwd", 16 * h.numel(), "grr_dwconv3_bwd", g.data_ptr(), h.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
+            gwdw.data_ptr(), b, c, hh, ww, _stream(dev))
+    return gh
+
+
+def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True):
+    """gate = sigmoid(m) m v of hp = [m; v]; with ggate also the reverse ghp.  Returns (gate, ghp)."""
+    dev = _check("lnb_gate", hp, ggate)
+    b, c2, h, w = hp.shape
+    hid = c2 // 2
+    gate = torch.empty((b, hid, h, w), dtype=torch.float32, device=dev) if want_gate else None
+    ghp = torch.empty_like(hp) if ggate is not None else None
+    _launch("lnb_bwd", 4 * hp.numel() * 2, "grr_lnb_gate", hp.data_ptr(), _ptr(ggate), _ptr(gate), _ptr(ghp), b, hid,
+            h * w, _stream(dev))
+    return gate, ghp

@@ -448,3 +448,57 @@ def glr_solve(mod, y: Tensor, feat: Tensor) -> Tensor:
     params = [mod.GLRmodule00.multiM] + [getattr(mod.GLRmodule00, q) for q in STENCIL_PARAMS] + [
         mod.muys00, mod.alphaCGD, mod.betaCGD]
     return _GLRSolve.apply(mod.n_graphs, y, feat.contiguous(), *params)
+
+
+# ---- LocalNonLinearBlock (nsubnets = 1; REF:911-964, REF13:541-575) ---------------------
+def _mat(w: Tensor, rows: int) -> Tensor:
+    return w.reshape(rows, -1)
+
+
+class LNBFn(torch.autograd.Function):
+    """out = s0 x + s1 W2 gate(dw3x3(W1 LN(x))): fused HIP forward; the reverse recomputes
+    n, h, h', gate with HIP kernels and runs the adjoints (GEMMs: HIP conv1x1 for the data
+    gradients, one library GEMM per weight gradient)."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor) -> Tensor:
+        c, hid2 = x.shape[1], w1.shape[0]
+        out = K.lnb_forward(x, ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(),
+                            _mat(wdw, hid2).contiguous(), _mat(w2, c).contiguous(), skip.contiguous())
+        ctx.save_for_backward(x, ln_w, w1, wdw, w2, skip)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout: Tensor):
+        x, ln_w, w1, wdw, w2, skip = ctx.saved_tensors
+        gout = gout.contiguous()
+        b, c, h, w = x.shape
+        hid2 = w1.shape[0]
+        hid = hid2 // 2
+        lnw, W1, Wdw, W2 = ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(), _mat(wdw, hid2).contiguous(), \
+            _mat(w2, c).contiguous()
+        n, isd = K.lnb_norm(x, lnw)
+        hh = K.conv1x1(n, W1.view(hid2, c, 1, 1))
+        hp = K.dwconv3(hh, Wdw)
+        gate, _ = K.lnb_gate(hp)
+        o = K.conv1x1(gate, W2.view(c, hid, 1, 1))
+        gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
+        K.bwd_graph_dot(gout, x, gskip[0:1], 1)
+        K.bwd_graph_dot(gout, o, gskip[1:2], 1)
+        del o
+        go = K.bwd_lincomb(gout, skip[1:2].contiguous(), None, None, 1)          # s1 * gout
+        gw2 = torch.matmul(go.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0)
+        ggate = K.conv1x1(go, W2.t().contiguous().view(hid, c, 1, 1))
+        del go, gate
+        _, ghp = K.lnb_gate(hp, ggate, want_gate=False)
+        del hp, ggate
+        gwdw = torch.zeros_like(Wdw)
+        gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
+        del ghp, hh
+        gw1 = torch.matmul(gh.reshape(b, hid2, -1), n.reshape(b, c, -1).transpose(1, 2)).sum(0)
+        gn = K.conv1x1(gh, W1.t().contiguous().view(c, hid2, 1, 1))
+        del gh, n
+        gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
+        glnw = torch.zeros_like(lnw)
+        K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
+        return gx, glnw.view_as(ln_w), gw1.view_as(w1), gwdw.view_as(wdw), gw2.view_as(w2), gskip

@@ -213,6 +213,22 @@ grr_status grr_bwd_unpool2_acc(const float* xd, float* out, int B, int C, int H,
 grr_status grr_conv2x2s2_bwd_data(const float* g, const float* wt, float* gx, int B, int K, int M, int H, int W,
                                   void* stream);
 
+/* ---- LocalNonLinearBlock reverse (training; REF:911-964) ---------------------------------
+ * n = ln_w * x * isd with isd[b,p] = 1/sqrt(var_c x + 1e-5) (unbiased, uncentred x, REF:919-925). */
+grr_status grr_lnb_norm(const float* x, const float* ln_w, float* n, float* isd, int B, int C, int64_t P,
+                        void* stream);
+/* gx [B,C,P] += d<gn, n>/dx;  gln_w [C] += sum gn x isd. */
+grr_status grr_lnb_norm_bwd(const float* x, const float* ln_w, const float* isd, const float* gn, float* gx,
+                            float* gln_w, int B, int C, int64_t P, void* stream);
+/* depthwise 3x3 with replicate padding (channels_local_linear_op, REF:934-940): wdw [C,9]. */
+grr_status grr_dwconv3(const float* h, const float* wdw, float* out, int B, int C, int H, int W, void* stream);
+/* its reverse: gh = exact adjoint of the clamped gather applied to g; gwdw [C,9] += weight gradient. */
+grr_status grr_dwconv3_bwd(const float* g, const float* h, const float* wdw, float* gh, float* gwdw, int B, int C,
+                           int H, int W, void* stream);
+/* gate = sigmoid(m) m v of hp = [m; v] [B,2hid,P] (if gate); ghp from ggate (if ggate) (REF:941-947). */
+grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -149,3 +149,16 @@ def test_training_step_reduces_loss(irdu):
         losses.append(float(loss.detach()))
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 20, 24), (33, 20, 9, 44), (160, 64, 8, 12)])
+def test_local_nonlinear_block_grad(irdu, chw):
+    """LocalNonLinearBlock reverse on HIP (LN, W1, depthwise 3x3, gate, W2, skip) vs fp64 oracle."""
+    c, hid, h, w = chw
+    torch.manual_seed(31)
+    blk = irdu.LocalNonLinearBlock(c, hid, 1)
+    with torch.no_grad():
+        blk.norm.weighted_transform.weight.mul_(1 + 0.2 * torch.randn_like(blk.norm.weighted_transform.weight))
+        blk.skip_weight.copy_(torch.tensor([0.7, 1.3]))
+    x = rand(2, c, h, w, seed=32)
+    check(blk, lambda xd, p: O.local_nonlinear_block(xd, p, ""), x)
