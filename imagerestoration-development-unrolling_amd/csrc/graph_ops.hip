@@ -313,11 +313,13 @@ template <bool GLR, int GTV, int EPI>
 __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // channels fastest, then strips: a graph's channel waves are dispatch-adjacent (weights
+  // shared through L2) and neighbouring strips (shared halo columns) stay on one XCD.
   uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * 4 + wave;
-  if (unit >= a.nunits) return;   // whole wave (uniform)
+  if (unit >= a.nunits) return;   // whole wave (uniform); wpb == 1 here, no barrier is met
   const int F = a.F;
-  const int strip = unit % a.nstrips; unit /= a.nstrips;
   const int f = unit % F; unit /= F;
+  const int strip = unit % a.nstrips; unit /= a.nstrips;
   const int seg = unit % a.nsegs; unit /= a.nsegs;
   const int g = unit % a.G;
   const int b = unit / a.G;
@@ -543,11 +545,13 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   RowLoads A, B;
   issue(ts, A);
   issue(ts + 1, B);
+  const bool lockstep = a.wpb > 1;
   for (int t = ts; t < te; t += 2) {
     consume(t, A, std::false_type{});
     issue(t + 2, A);
     consume(t + 1, B, std::true_type{});
     issue(t + 3, B);
+    if (lockstep) __builtin_amdgcn_s_barrier();
   }
 }
 
@@ -936,6 +940,9 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
   GRR_REQUIRE(units < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   GRR_REQUIRE((int64_t)a.H * a.W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "%s: plane too large", name);
   a.nunits = (uint32_t)units;
+  // lockstep channel waves measured neutral for the 58-column strips (W = 512: 3.27 vs 3.19 ms;
+  // the strip halo re-reads dominate), so strips run one wave per channel, 4 waves per block
+  a.wpb = 1;
   a.nblk = (uint32_t)((units + 3) / 4);
   hipLaunchKernelGGL((graph_op_kernel<GLR, GTV, EPI>), dim3(a.nblk), dim3(NT), 0, s, a);
   return launch_status(name);
