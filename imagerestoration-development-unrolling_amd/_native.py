@@ -47,6 +47,7 @@ SIGNATURES = {
     "grr_neighbor_table": [P, I, I, P],
     "grr_edge_weights": [P, L, P, P, P, I, I, I, I, I, P],
     "grr_gtv_pair_weights": [P, P, I, I, I, I, P],
+    "grr_edge_weights_block": [P, L, I, P, I, P, P, P, P, I, I, I, I, I, P],
     "grr_pool2": [P, P, I, I, I, I, P],
     "grr_system_half": [P, P, P, Stencil, Stencil, P, P, P, I, I, I, I, I, P],
     "grr_gtv_rhs_half": [P, P, Stencil, I, P, P, I, I, I, I, I, P],

@@ -948,6 +948,174 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
   return launch_status(name);
 }
 
+
+// ---------------------------------------------------------------------------
+// a3+a4 as a row-wave stream (W <= 256): the GTV slab (raw weights + pair weights) and
+// the GLR slab (raw weights) of one feature tensor in ONE launch.  One wave = one
+// (b, slab, graph) plane set; lane = V adjacent columns (dwordx4 loads for V = 4); the
+// normalised features of rows r-1, r, r+1 stay in registers (vertical neighbours),
+// horizontal neighbours come from DPP wave shifts.  Row r's pair weight c_v needs
+// w_up of row r+1, so it is written one row late.  Same arithmetic order as
+// edge_weights_kernel (REF:146-175).
+// ---------------------------------------------------------------------------
+struct EdgeArgs {
+  const float* feat;
+  int64_t bstride;
+  int slab_off[2];          // first channel of each slab in feat
+  const float* multiM[2];   // [G,F] per slab
+  float* w[2];              // raw weights [B,G,4,H,W] per slab
+  float* c[2];              // pair weights [B,G,2,H,W] per slab, or NULL
+  int nslab, G, H, W;
+  uint32_t nunits, nblk;
+};
+
+template <int F, int V>
+__global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * 4 + wave;
+  if (unit >= a.nunits) return;   // whole wave (uniform)
+  const int g = unit % a.G; unit /= a.G;
+  const int slab = unit % a.nslab;
+  const int b = unit / a.nslab;
+  const int H = a.H, W = a.W;
+  const int64_t HW = (int64_t)H * W;
+  const float* fb = a.feat + (int64_t)b * a.bstride + (int64_t)(a.slab_off[slab] + g * F) * HW;
+  const float* Mp = a.multiM[slab] + g * F;
+  float M[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) M[f] = Mp[f];
+  const int c0 = V * lane;
+  const bool lane_on = c0 < W;
+  const int cl0 = lane_on ? c0 : W - V;
+  const uint32_t vo = (uint32_t)cl0 * 4u;
+  float* wb = a.w[slab] + (int64_t)(b * a.G + g) * 4 * HW;
+  float* cb = a.c[slab] ? a.c[slab] + (int64_t)(b * a.G + g) * 2 * HW : nullptr;
+
+  float fP[F][V], fC[F][V], fN[F][V], raw[F][V];
+  auto load_raw = [&](int row) {
+    const int rr = clampi(row, 0, H - 1);
+#pragma unroll
+    for (int f = 0; f < F; ++f) vload(raw[f], fb + f * HW + (int64_t)rr * W, vo);
+  };
+  auto normalise = [&](float (&dst)[F][V]) {   // F.normalize(dim=F, eps 1e-12) * multiM (REF:146-157)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float ss = 0.f;
+#pragma unroll
+      for (int f = 0; f < F; ++f) ss += raw[f][j] * raw[f][j];
+      const float den = fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+      for (int f = 0; f < F; ++f) dst[f][j] = (raw[f][j] / den) * M[f];
+    }
+  };
+  load_raw(0);
+  normalise(fC);
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int j = 0; j < V; ++j) fP[f][j] = fC[f][j];
+  load_raw(1);
+  normalise(fN);
+  float wdn_prev[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) wdn_prev[j] = 0.f;
+
+  for (int r = 0; r < H; ++r) {
+    load_raw(r + 2);                                   // consumed at the bottom of the iteration
+    float fl[F], fr[F];                                // lane-edge neighbours (whole wave active)
+#pragma unroll
+    for (int f = 0; f < F; ++f) { fl[f] = lane_prev(fC[f][V - 1]); fr[f] = lane_next(fC[f][0]); }
+    float w0[V], w1[V], w2[V], w3[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int col = c0 + j;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const float v = fC[f][j];
+        const float lv = col > 0 ? (j > 0 ? fC[f][j - 1] : fl[f]) : v;
+        const float rv = col < W - 1 ? (j < V - 1 ? fC[f][j + 1] : fr[f]) : v;
+        s0 += v * fP[f][j];
+        s1 += v * lv;
+        s2 += v * rv;
+        s3 += v * fN[f][j];
+      }
+      const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
+      const float e0 = expf(s0 - m), e1 = expf(s1 - m), e2 = expf(s2 - m), e3 = expf(s3 - m);
+      const float sum = ((e0 + e1) + e2) + e3;
+      w0[j] = e0 / sum; w1[j] = e1 / sum; w2[j] = e2 / sum; w3[j] = e3 / sum;
+    }
+    const int64_t ro = (int64_t)r * W;
+    if (lane_on) {
+      vstore(wb + ro, vo, w0);
+      vstore(wb + HW + ro, vo, w1);
+      vstore(wb + 2 * HW + ro, vo, w2);
+      vstore(wb + 3 * HW + ro, vo, w3);
+    }
+    if (cb) {   // wave-uniform
+      const float wl_next = lane_next(w1[0]);
+      float ch[V], cv[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        const float wln = j < V - 1 ? w1[j + 1] : wl_next;     // w_left(p + right)
+        ch[j] = col + 1 < W ? w2[j] * w2[j] + wln * wln : 0.f;
+        cv[j] = wdn_prev[j] * wdn_prev[j] + w0[j] * w0[j];     // row r-1: w_down(p)^2 + w_up(p + down)^2
+        wdn_prev[j] = w3[j];
+      }
+      if (lane_on) {
+        vstore(cb + ro, vo, ch);
+        if (r > 0) vstore(cb + HW + ro - W, vo, cv);
+      }
+    }
+    // advance the row window (the down neighbour of the last row is itself: clamped load)
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+      for (int j = 0; j < V; ++j) { fP[f][j] = fC[f][j]; fC[f][j] = fN[f][j]; }
+    normalise(fN);
+  }
+  if (cb && lane_on) {   // last row: no lower neighbour
+    float z[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) z[j] = 0.f;
+    vstore(cb + HW + (int64_t)(H - 1) * W, vo, z);
+  }
+}
+
+template <int F>
+static void launch_edge_row_f(const EdgeArgs& a, int V, hipStream_t s) {
+  const dim3 grid(a.nblk), block(NT);
+  if (V == 4) hipLaunchKernelGGL((edge_row_kernel<F, 4>), grid, block, 0, s, a);
+  else if (V == 2) hipLaunchKernelGGL((edge_row_kernel<F, 2>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((edge_row_kernel<F, 1>), grid, block, 0, s, a);
+}
+
+// true when the row-wave kernel took the launch
+static bool launch_edge_row(EdgeArgs a, int B, int F, hipStream_t s) {
+  const int V = g_kernel_variant == 1 ? 0 : row_vec(a.W);
+  if (V == 0) return false;
+  if ((uintptr_t)a.feat % (4u * V) || (a.bstride * 4) % (4 * V) || ((int64_t)a.H * a.W) % V) return false;
+  for (int k = 0; k < a.nslab; ++k)
+    if ((uintptr_t)a.w[k] % (4u * V) || (a.c[k] && (uintptr_t)a.c[k] % (4u * V))) return false;
+  const uint64_t units = (uint64_t)B * a.nslab * a.G;
+  if (units >= (1ull << 32) - 4) return false;
+  a.nunits = (uint32_t)units;
+  a.nblk = (uint32_t)((units + 3) / 4);
+  switch (F) {
+    case 1: launch_edge_row_f<1>(a, V, s); return true;
+    case 2: launch_edge_row_f<2>(a, V, s); return true;
+    case 3: launch_edge_row_f<3>(a, V, s); return true;
+    case 4: launch_edge_row_f<4>(a, V, s); return true;
+    case 6: launch_edge_row_f<6>(a, V, s); return true;
+    case 8: launch_edge_row_f<8>(a, V, s); return true;
+    case 12: launch_edge_row_f<12>(a, V, s); return true;
+    case 16: launch_edge_row_f<16>(a, V, s); return true;
+    default: return false;
+  }
+}
+
 static bool stencil_ok(const grr_stencil& s) { return s.p01 && s.p02a && s.p02b && s.p03; }
 
 }  // namespace grr
@@ -998,6 +1166,30 @@ grr_status grr_gtv_pair_weights(const float* w, float* c, int B, int G, int H, i
   hipLaunchKernelGGL(gtv_pair_weights_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, c,
                      (int64_t)B * G, H, W);
   return launch_status("grr_gtv_pair_weights");
+}
+
+grr_status grr_edge_weights_block(const float* feat, int64_t feat_bstride, int gtv_off, const float* multiM_gtv,
+                                  int glr_off, const float* multiM_glr, float* wG, float* cG, float* wL, int B,
+                                  int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(feat && multiM_gtv && multiM_glr && wG && cG && wL && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 &&
+                  gtv_off >= 0 && glr_off >= 0,
+              GRR_ERR_INVALID_ARG, "grr_edge_weights_block: bad args");
+  GRR_REQUIRE(F <= GRR_MAX_NODE_FTS, GRR_ERR_UNSUPPORTED, "grr_edge_weights_block: F=%d > %d", F, GRR_MAX_NODE_FTS);
+  hipStream_t s = (hipStream_t)stream;
+  EdgeArgs a{};
+  a.feat = feat; a.bstride = feat_bstride;
+  a.slab_off[0] = gtv_off; a.multiM[0] = multiM_gtv; a.w[0] = wG; a.c[0] = cG;
+  a.slab_off[1] = glr_off; a.multiM[1] = multiM_glr; a.w[1] = wL; a.c[1] = nullptr;
+  a.nslab = 2; a.G = G; a.H = H; a.W = W;
+  if (launch_edge_row(a, B, F, s)) return launch_status("grr_edge_weights_block");
+  const int64_t HW = (int64_t)H * W;
+  grr_status st = grr_edge_weights(feat + (int64_t)gtv_off * HW, feat_bstride, multiM_gtv, wG, nullptr, B, G, F, H,
+                                   W, stream);
+  if (st != GRR_OK) return st;
+  st = grr_gtv_pair_weights(wG, cG, B, G, H, W, stream);
+  if (st != GRR_OK) return st;
+  return grr_edge_weights(feat + (int64_t)glr_off * HW, feat_bstride, multiM_glr, wL, nullptr, B, G, F, H, W, stream);
 }
 
 grr_status grr_pool2(const float* x, float* xd, int B, int C, int H, int W, void* stream) {

@@ -316,13 +316,9 @@ class MixtureGTVGLR(nn.Module):
             raise ValueError("MixtureGTVGLR: src must be [B, F, H, W]")
         f0, f1 = self.features(y, src)
         d = lambda p: p.data  # noqa: E731  (parameters are read by the kernels through raw pointers)
-        wG0, _ = K.edge_weights(f0, 0, g, f, d(self.GTVmodule00.multiM))
-        wL0, _ = K.edge_weights(f0, c, g, f, d(self.GLRmodule00.multiM))
-        wG1, _ = K.edge_weights(f1, 0, g, f, d(self.GTVmodule01.multiM))
-        wL1, _ = K.edge_weights(f1, c, g, f, d(self.GLRmodule01.multiM))
+        wG0, cG0, wL0 = K.edge_weights_block(f0, g, f, d(self.GTVmodule00.multiM), d(self.GLRmodule00.multiM))
+        wG1, cG1, wL1 = K.edge_weights_block(f1, g, f, d(self.GTVmodule01.multiM), d(self.GLRmodule01.multiM))
         del f0, f1
-        cG0 = K.gtv_pair_weights(wG0)
-        cG1 = K.gtv_pair_weights(wG1)
         sG0, sL0 = K.stencil(self.GTVmodule00), K.stencil(self.GLRmodule00)
         sG1, sL1 = K.stencil(self.GTVmodule01), K.stencil(self.GLRmodule01)
         mu0, mu1, ro0, ro1 = d(self.muys00), d(self.muys01), d(self.ro00), d(self.ro01)

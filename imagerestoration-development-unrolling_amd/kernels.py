@@ -130,6 +130,25 @@ def edge_weights(feat: Tensor, channel_offset: int, n_graphs: int, n_fts: int, m
     return wt, deg
 
 
+def edge_weights_block(feat: Tensor, n_graphs: int, n_fts: int, multiM_gtv: Tensor,
+                       multiM_glr: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """Both graph modules of a level from one [B, 2C, H, W] feature map (GTV half first, REF:714):
+    returns (wG raw [B,G,4,H,W], cG pair [B,G,2,H,W], wL [B,G,4,H,W])."""
+    dev = _check("edge_weights_block", feat, multiM_gtv, multiM_glr)
+    b, ctot, h, w = feat.shape
+    c = n_graphs * n_fts
+    if ctot != 2 * c:
+        raise ValueError(f"edge_weights_block: expected {2 * c} feature channels, got {ctot}")
+    wG = torch.empty((b, n_graphs, 4, h, w), dtype=torch.float32, device=dev)
+    wL = torch.empty_like(wG)
+    cG = torch.empty((b, n_graphs, 2, h, w), dtype=torch.float32, device=dev)
+    nbytes = 4 * b * h * w * (2 * c + 10 * n_graphs)
+    _launch("edge_weights", nbytes, "grr_edge_weights_block", feat.data_ptr(), ctot * h * w, 0,
+            multiM_gtv.data_ptr(), c, multiM_glr.data_ptr(), wG.data_ptr(), cG.data_ptr(), wL.data_ptr(),
+            b, n_graphs, n_fts, h, w, _stream(dev))
+    return wG, cG, wL
+
+
 def gtv_pair_weights(w: Tensor) -> Tensor:
     dev = _check("gtv_pair_weights", w)
     b, g, four, h, ww = w.shape

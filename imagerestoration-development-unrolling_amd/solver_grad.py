@@ -132,11 +132,8 @@ class _MixtureSolve(torch.autograd.Function):
         g = n_graphs
         b, c, h, w = y.shape
         nf = c // g
-        wG0, _ = K.edge_weights(f0, 0, g, nf, p["GTVmodule00.multiM"])
-        wL0, _ = K.edge_weights(f0, c, g, nf, p["GLRmodule00.multiM"])
-        wG1, _ = K.edge_weights(f1, 0, g, nf, p["GTVmodule01.multiM"])
-        wL1, _ = K.edge_weights(f1, c, g, nf, p["GLRmodule01.multiM"])
-        cG0, cG1 = K.gtv_pair_weights(wG0), K.gtv_pair_weights(wG1)
+        wG0, cG0, wL0 = K.edge_weights_block(f0, g, nf, p["GTVmodule00.multiM"], p["GLRmodule00.multiM"])
+        wG1, cG1, wL1 = K.edge_weights_block(f1, g, nf, p["GTVmodule01.multiM"], p["GLRmodule01.multiM"])
         st = {m: tuple(p[f"{m}.{q}"] for q in STENCIL_PARAMS) for m in MODULES}
         sG0, sL0, sG1, sL1 = (_stencil(st[m]) for m in MODULES)
         mu0, mu1, ro0, ro1 = p["muys00"], p["muys01"], p["ro00"], p["ro01"]

@@ -64,6 +64,14 @@ grr_status grr_edge_weights(const float* feat, int64_t feat_bstride, const float
  * frame-dropped scatter).  w [B,G,4,H,W] -> c [B,G,2,H,W]. */
 grr_status grr_gtv_pair_weights(const float* w, float* c, int B, int G, int H, int W, void* stream);
 
+/* Both graph modules of one MixtureGTVGLR level in one call (REF:712-729): the GTV slab
+ * (channels [gtv_off, gtv_off + G*F) of feat) -> raw weights wG [B,G,4,H,W] and pair
+ * weights cG [B,G,2,H,W] (= grr_gtv_pair_weights(wG)); the GLR slab -> wL.  Same values as
+ * grr_edge_weights (+ grr_gtv_pair_weights); a single row-wave launch where W <= 256. */
+grr_status grr_edge_weights_block(const float* feat, int64_t feat_bstride, int gtv_off, const float* multiM_gtv,
+                                  int glr_off, const float* multiM_glr, float* wG, float* cG, float* wL,
+                                  int B, int G, int F, int H, int W, void* stream);
+
 /* D — 2x2 mean pool, stride 2 (REF:613, :662-665).  x [B,C,H,W] -> xd [B,C,H/2,W/2]. */
 grr_status grr_pool2(const float* x, float* xd, int B, int C, int H, int W, void* stream);
 

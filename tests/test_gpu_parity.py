@@ -130,6 +130,25 @@ def test_edge_weights_random(irdu, shape):
     assert_close(deg, od, 1e-5)
 
 
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 20, 64), (2, 3, 12, 9, 256), (1, 2, 1, 7, 40),
+                                   (1, 2, 5, 12, 48), (1, 2, 3, 10, 300)])
+def test_edge_weights_block(irdu, variant, shape):
+    """The fused two-module edge weights (row-wave kernel for W <= 256 and F in {1,2,3,4,6,8,12,16},
+    tile kernels otherwise) equal the per-module kernels + pair weights, and the oracle."""
+    b, g, f, h, w = shape
+    feat = rand(b, 2 * g * f, h, w, seed=41).to(DEV)
+    mG, mL = ((1 + 0.3 * rand(g, f, seed=s)).to(DEV) for s in (42, 43))
+    wG, cG, wL = irdu.kernels.edge_weights_block(feat, g, f, mG, mL)
+    rG, _ = irdu.kernels.edge_weights(feat, 0, g, f, mG)
+    rL, _ = irdu.kernels.edge_weights(feat, g * f, g, f, mL)
+    assert_close(wG, rG, 1e-6)
+    assert_close(wL, rL, 1e-6)
+    assert_close(cG, irdu.kernels.gtv_pair_weights(rG), 1e-6)
+    fo = feat.cpu().reshape(b, 2, g, f, h, w)
+    assert_close(wG, O.edge_weights(fo[:, 0], mG.cpu())[0], 1e-5)
+    assert_close(wL, O.edge_weights(fo[:, 1], mL.cpu())[0], 1e-5)
+
+
 # widths: <= 64 (1 column per lane), 70 (2), 200 / 256 (4), 130 (W % 4 != 0 -> strips)
 @pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 37, 45), (1, 3, 2, 9, 70), (1, 2, 3, 12, 200),
                                    (1, 1, 3, 10, 256), (1, 2, 3, 7, 130)])
