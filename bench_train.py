@@ -40,10 +40,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GRR_BENCH_BACKEND=gloo + fewer GPUs than ranks: multi-rank rehearsal on a one-GPU box
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("GRR_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
 
     import irdu_amd
     from irdu_amd import kernels as K

@@ -505,6 +505,190 @@ __global__ __launch_bounds__(NT) void conv2x2s2_bwd_data_kernel(const float* __r
   gx[(int64_t)bk * HW + p] = acc;
 }
 
+// ---------------------------------------------------------------------------
+// Fused term reverse: one pass per operator term instead of five.  s = P x and a = T* g
+// are recomputed on the fly at the pixel and its four neighbours (radius-2 reads that hit
+// L1/L2), the term's reverse runs as in glr_bwd / pair_bwd / prox_bwd above, and both
+// tap gradients are accumulated in the same pass in their gather forms:
+//   T taps:  sum_q g(q) z(q - t) [inside]  = sum_p z(p) g(p + t) [p + t inside]
+//   P taps:  sum_q v(q) x(clamp(q + t))     with v = (I-W)^T a, K a or d<a,o>/ds
+// Output v_out = that v (the x-gradient is then one adjoint-stencil pass, P* v).
+// MODE 0: GLR (w raw),  1: pair Laplacian (w = pair weights),  2: prox (w raw, gamma).
+// F is a template parameter so the per-channel tap partials stay in registers.
+// grid (chunks, B*G)
+// ---------------------------------------------------------------------------
+template <int MODE, int F>
+__global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
+    const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
+    const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
+    float* __restrict__ v_out, float* __restrict__ gw, float* __restrict__ ggam, float* __restrict__ gdot,
+    float* __restrict__ gtaps, int G, int H, int W) {
+  const int HW = H * W;
+  const int bg = blockIdx.y, gi = bg % G;
+  const float sc = scale ? scale[gi] : 1.f;
+  const float gm = MODE == 2 ? expf(log_gamma[gi]) : 0.f;
+  float k[F][5];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) k[f][t] = taps[(gi * F + f) * 5 + t];
+  float accT[F][5], accP[F][5];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) { accT[f][t] = 0.f; accP[f][t] = 0.f; }
+  float dot = 0.f, dgam = 0.f;
+  const int wplanes = MODE == 1 ? 2 : 4;
+  const float* wb = w + (int64_t)bg * wplanes * HW;
+  float* gwb = gw + (int64_t)bg * wplanes * HW;
+
+  for (int p = blockIdx.x * NT + threadIdx.x; p < HW; p += gridDim.x * NT) {
+    const int r = p / W, col = p - r * W;
+    bool in[4];
+    int nb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      in[e] = inside_e(e, r, col, H, W);
+      nb[e] = in[e] ? p + off_e(e, W) : p;
+    }
+    // neighbour coordinates of the 5 positions {p, up, left, right, down} (clamped)
+    const int pr[5] = {r, in[0] ? r - 1 : r, r, r, in[3] ? r + 1 : r};
+    const int pc[5] = {col, col, in[1] ? col - 1 : col, in[2] ? col + 1 : col, col};
+    float we[4] = {0.f, 0.f, 0.f, 0.f}, wn[4] = {0.f, 0.f, 0.f, 0.f};
+    float cr = 0.f, cl = 0.f, cd = 0.f, cu = 0.f;
+    if constexpr (MODE == 1) {
+      cr = in[2] ? wb[p] : 0.f; cl = in[1] ? wb[p - 1] : 0.f;
+      cd = in[3] ? wb[HW + p] : 0.f; cu = in[0] ? wb[HW + p - W] : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) we[e] = wb[e * HW + p];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wn[e] = in[3 - e] ? wb[e * HW + nb[3 - e]] : 0.f;
+    }
+    float gwa[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const int64_t base = ((int64_t)bg * F + f) * HW;
+      const float* xp = x + base;
+      const float* gp = g + base;
+      // s = P x (replicate) and a = T* g (zero frame) at the 5 positions
+      float s5[5], a5[5], xt[5], gt5[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int rr = pr[i], cc = pc[i];
+        const float* xr = xp + rr * W;
+        const float xc = xr[cc];
+        const float xu = xp[max(rr - 1, 0) * W + cc], xd = xp[min(rr + 1, H - 1) * W + cc];
+        const float xl = xr[max(cc - 1, 0)], xrr = xr[min(cc + 1, W - 1)];
+        s5[i] = k[f][0] * xc + k[f][1] * xu + k[f][2] * xl + k[f][3] * xrr + k[f][4] * xd;
+        const float* gr = gp + rr * W;
+        const float gc = gr[cc];
+        const float gu = rr > 0 ? gp[(rr - 1) * W + cc] : 0.f, gd = rr + 1 < H ? gp[(rr + 1) * W + cc] : 0.f;
+        const float gl = cc > 0 ? gr[cc - 1] : 0.f, grr = cc + 1 < W ? gr[cc + 1] : 0.f;
+        a5[i] = k[f][0] * gc + k[f][1] * gu + k[f][2] * gl + k[f][3] * grr + k[f][4] * gd;
+        if (i == 0) {
+          xt[0] = xc; xt[1] = xu; xt[2] = xl; xt[3] = xrr; xt[4] = xd;   // x(clamp(p + t))
+          gt5[0] = gc; gt5[1] = gu; gt5[2] = gl; gt5[3] = grr; gt5[4] = gd;   // g(p + t), 0 outside
+        }
+      }
+      const float sv = s5[0], av = a5[0];
+      float z = 0.f, v = 0.f;
+      if constexpr (MODE == 0) {
+        float wta = 0.f;
+        z = sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sn = s5[e + 1];            // s(nb_e p): positions 1..4 are up, left, right, down
+          z -= we[e] * sn;
+          gwa[e] -= av * sn;
+          wta += in[3 - e] ? wn[e] * a5[(3 - e) + 1] : 0.f;
+          wta += in[e] ? 0.f : we[e] * av;
+        }
+        v = av - wta;
+      } else if constexpr (MODE == 1) {
+        const float su = s5[1], sl = s5[2], sr = s5[3], sd = s5[4];
+        const float au = a5[1], al = a5[2], ar = a5[3], ad = a5[4];
+        z = cr * (sv - sr) + cl * (sv - sl) + cd * (sv - sd) + cu * (sv - su);
+        v = cr * (av - ar) + cl * (av - al) + cd * (av - ad) + cu * (av - au);
+        gwa[0] += (av - ar) * (sv - sr);
+        gwa[1] += (av - ad) * (sv - sd);
+      } else {
+        float o = 0.f, gs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (in[e]) {
+            const float sn = s5[e + 1], an = a5[e + 1];
+            const float ds = sv - sn, t = we[e] * ds;
+            const float ph = 2.f * soft_t(t, gm) - t;
+            const float da = av - an;
+            const float gph = we[e] * da;
+            const float gtv = (t < -gm || t > gm) ? gph : -gph;
+            o += we[e] * ph;
+            gs += gtv * we[e];
+            gwa[e] += ph * da + gtv * ds;
+            dgam += gph * (t < -gm ? 2.f : (t > gm ? -2.f : 0.f));
+          }
+          if (in[3 - e]) {
+            const float sq = s5[(3 - e) + 1], aq = a5[(3 - e) + 1];
+            const float t = wn[e] * (sq - sv);
+            const float ph = 2.f * soft_t(t, gm) - t;
+            const float gph = wn[e] * (aq - av);
+            const float gtv = (t < -gm || t > gm) ? gph : -gph;
+            o -= wn[e] * ph;
+            gs -= gtv * wn[e];
+          }
+        }
+        z = o;
+        v = gs;
+      }
+      v_out[base + p] = v;
+      dot += av * z;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        accT[f][t] += z * gt5[t];
+        accP[f][t] += v * xt[t];
+      }
+    }
+    if constexpr (MODE == 1) {
+      if (in[2]) gwb[p] += sc * gwa[0];
+      if (in[3]) gwb[HW + p] += sc * gwa[1];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gwb[e * HW + p] += sc * gwa[e];
+    }
+  }
+  if (gdot) block_atomic_add(gdot + gi, coef * dot);
+  if constexpr (MODE == 2) {
+    if (ggam) block_atomic_add(ggam + gi, sc * dgam);
+  }
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) block_atomic_add(gtaps + (gi * F + f) * 5 + t, sc * (accT[f][t] + accP[f][t]));
+}
+
+template <int MODE>
+bool launch_term_fused(int F, dim3 grid, hipStream_t s, const float* x, const float* g, const float* taps,
+                       const float* w, const float* lg, const float* scale, float coef, float* v, float* gw,
+                       float* ggam, float* gdot, float* gtaps, int G, int H, int W) {
+#define GRR_TERM_CASE(FF)                                                                                      \
+  case FF:                                                                                                     \
+    hipLaunchKernelGGL((term_bwd_fused_kernel<MODE, FF>), grid, dim3(NT), 0, s, x, g, taps, w, lg, scale, coef, \
+                       v, gw, ggam, gdot, gtaps, G, H, W);                                                     \
+    return true;
+  switch (F) {
+    GRR_TERM_CASE(1)
+    GRR_TERM_CASE(2)
+    GRR_TERM_CASE(3)
+    GRR_TERM_CASE(4)
+    GRR_TERM_CASE(6)
+    GRR_TERM_CASE(8)
+    GRR_TERM_CASE(12)
+    default: return false;
+  }
+#undef GRR_TERM_CASE
+}
+
 // pixel chunks per plane for the reduction kernels: ~TARGET_BLOCKS blocks in total, so each
 // block loops over many pixels and issues few atomics
 int chunks_for(int64_t n, int64_t planes) {
@@ -519,6 +703,27 @@ int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 <
 using namespace grr;
 
 extern "C" {
+
+grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const float* taps, const float* w,
+                              const float* log_gamma, const float* scale, float coef, float* v_out, float* gw,
+                              float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
+                              void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && g && taps && w && v_out && gw && gtaps && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 &&
+                  mode >= 0 && mode <= 2 && (mode != 2 || log_gamma),
+              GRR_ERR_INVALID_ARG, "grr_bwd_term_fused: bad args");
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: B*G > 65535");
+  const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G), B * G);
+  hipStream_t s = (hipStream_t)stream;
+  bool ok = false;
+  switch (mode) {
+    case 0: ok = launch_term_fused<0>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W); break;
+    case 1: ok = launch_term_fused<1>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W); break;
+    default: ok = launch_term_fused<2>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W);
+  }
+  GRR_REQUIRE(ok, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: F=%d has no fused instance", F);
+  return launch_status("grr_bwd_term_fused");
+}
 
 grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,
                            float* out, int B, int G, int F, int H, int W, void* stream) {

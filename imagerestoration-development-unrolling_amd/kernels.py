@@ -367,6 +367,23 @@ def bwd_prox(s: Tensor, a: Tensor, w: Tensor, log_gamma: Tensor, scale: Tensor, 
     return o, gs
 
 
+FUSED_TERM_FTS = (1, 2, 3, 4, 6, 8, 12)   # node-feature counts with a fused reverse instance
+TERM_GLR, TERM_PAIR, TERM_PROX = 0, 1, 2
+
+
+def bwd_term_fused(mode: int, x: Tensor, g: Tensor, taps: Tensor, w: Tensor, log_gamma: Optional[Tensor],
+                   scale: Tensor, coef: float, gw: Tensor, ggamma: Optional[Tensor], gdot: Optional[Tensor],
+                   gtaps: Tensor, n_graphs: int) -> Tensor:
+    """One-pass reverse of an operator term (grr_bwd_term_fused); returns v for the P* pass."""
+    dev = _check("bwd_term_fused", x, g, taps, w, log_gamma, scale, gw, ggamma, gdot, gtaps)
+    v = torch.empty_like(x)
+    _launch("bwd_term_fused", 4 * (3 * x.numel() + 3 * w.numel()), "grr_bwd_term_fused", mode, x.data_ptr(),
+            g.data_ptr(), taps.data_ptr(), w.data_ptr(), _ptr(log_gamma), scale.data_ptr(), float(coef),
+            v.data_ptr(), gw.data_ptr(), _ptr(ggamma), _ptr(gdot), gtaps.data_ptr(), *_bgfhw(x, n_graphs),
+            _stream(dev))
+    return v
+
+
 def bwd_pair_weights(w: Tensor, gc: Tensor, gw: Tensor) -> None:
     dev = _check("bwd_pair_weights", w, gc, gw)
     b, g, _, h, ww = w.shape

@@ -49,11 +49,22 @@ def solver_params(mod) -> List[Tensor]:
     return out
 
 
+FUSED = True   # one-pass term reverses (grr_bwd_term_fused) where F has an instance; False: 5-pass path
+
+
+def _use_fused(x: Tensor, n_graphs: int) -> bool:
+    return FUSED and (x.shape[1] // n_graphs) in K.FUSED_TERM_FTS
+
+
 def glr_term_bwd(x: Tensor, g: Tensor, taps: Tensor, w: Tensor, scale: Tensor, coef: float, n_graphs: int,
                  out: Tensor, gw: Tensor, gscale: Optional[Tensor], gtaps: Tensor) -> None:
     """Reverse of the GLR term  scale[g] * T((I - W) P x)  (REF:218-237) contracted with coef * g:
     out += coef*scale * P*(I-W)^T T* g; gw, gtaps += coef*scale * d/d(.); gscale += coef * <g, T(I-W)Px>."""
     sc = scale * coef
+    if _use_fused(x, n_graphs):
+        v = K.bwd_term_fused(K.TERM_GLR, x, g, taps, w, None, sc, coef, gw, None, gscale, gtaps, n_graphs)
+        K.bwd_stencil(v, taps, K.ST_P_ADJ, n_graphs, sc, out=out)
+        return
     s = K.bwd_stencil(x, taps, K.ST_P, n_graphs)
     a = K.bwd_stencil(g, taps, K.ST_T_ADJ, n_graphs)
     z, ap = K.bwd_glr(s, a, w, sc, coef, gw, gscale, n_graphs)
@@ -67,6 +78,10 @@ def gtv_term_bwd(x: Tensor, g: Tensor, taps: Tensor, c: Tensor, scale: Tensor, c
                  out: Tensor, gc: Tensor, gscale: Optional[Tensor], gtaps: Tensor) -> None:
     """Reverse of the linear GTV term  scale[g] * T(K_c P x)  (C^T C with pair weights, REF:452-523)."""
     sc = scale * coef
+    if _use_fused(x, n_graphs):
+        v = K.bwd_term_fused(K.TERM_PAIR, x, g, taps, c, None, sc, coef, gc, None, gscale, gtaps, n_graphs)
+        K.bwd_stencil(v, taps, K.ST_P_ADJ, n_graphs, sc, out=out)
+        return
     s = K.bwd_stencil(x, taps, K.ST_P, n_graphs)
     a = K.bwd_stencil(g, taps, K.ST_T_ADJ, n_graphs)
     z, ap = K.bwd_pair(s, a, c, sc, coef, gc, gscale, n_graphs)
@@ -101,6 +116,11 @@ class _Level:
         """out += ro C^T-part reverse of the prox rhs term ro T(Ct phi(C P x)); parameter gradients."""
         G = self.g
         sc = self.ro
+        if _use_fused(x, G):
+            v = K.bwd_term_fused(K.TERM_PROX, x, g, self.tapsG, self.wG, self.log_gamma, sc, 1.0, self.gwG,
+                                 self.ggam, self.gro, self.gtapG, G)
+            K.bwd_stencil(v, self.tapsG, K.ST_P_ADJ, G, sc, out=out)
+            return
         s = K.bwd_stencil(x, self.tapsG, K.ST_P, G)
         a = K.bwd_stencil(g, self.tapsG, K.ST_T_ADJ, G)
         o, gs = K.bwd_prox(s, a, self.wG, self.log_gamma, sc, 1.0, self.gwG, self.ggam, self.gro, G)

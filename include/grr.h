@@ -202,6 +202,15 @@ grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const fl
 grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const float* log_gamma,
                         const float* scale, float coef, float* o_out, float* gs_out, float* gw,
                         float* ggamma, float* gdot, int B, int G, int F, int H, int W, void* stream);
+/* The three reverses above in one pass each, from x and g directly (s = S x and a = adjoint-S^T g
+ * recomputed on the fly) with both tap gradients fused: mode 0 GLR (w raw), 1 pair Laplacian
+ * (w = pair weights), 2 prox (w raw, log_gamma).  Writes v_out = (I-W)^T a, K a or d<a,o>/ds
+ * (x-gradient = adjoint-S of v); gw, ggamma, gdot, gtaps (+=) as the multi-pass path, whose
+ * results it reproduces.  GRR_ERR_UNSUPPORTED for F outside {1,2,3,4,6,8,12}. */
+grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const float* taps, const float* w,
+                              const float* log_gamma, const float* scale, float coef, float* v_out, float* gw,
+                              float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
+                              void* stream);
 /* Reverse of grr_gtv_pair_weights: gw [B,G,4,H,W] += d<gc, c(w)>/dw. */
 grr_status grr_bwd_pair_weights(const float* w, const float* gc, float* gw, int B, int G, int H, int W,
                                 void* stream);

@@ -73,9 +73,19 @@ def check(module, fn, x, tol=GTOL, loose=()):
     return errs
 
 
+@pytest.fixture(params=[True, False], ids=["fused", "multipass"])
+def term_path(irdu, request):
+    """Run a test with the one-pass fused term reverses and with the five-pass path."""
+    from irdu_amd import solver_grad as SG
+    SG.FUSED = request.param
+    yield request.param
+    SG.FUSED = True
+
+
 @pytest.mark.parametrize("case", [dict(g=2, f=3, b=2, h=16, w=16, s=3), dict(g=4, f=2, b=1, h=12, w=20, s=5),
-                                  dict(g=2, f=6, b=1, h=10, w=14, s=1), dict(g=3, f=3, b=1, h=18, w=8, s=10)])
-def test_lowpass_block_grad(irdu, case):
+                                  dict(g=2, f=6, b=1, h=10, w=14, s=1), dict(g=3, f=3, b=1, h=18, w=8, s=10),
+                                  dict(g=2, f=5, b=1, h=12, w=12, s=3)])    # F = 5: no fused instance
+def test_lowpass_block_grad(irdu, term_path, case):
     """LocalLowpassFilteringBlock (v1 feature convs + two-scale solver + skip), every parameter."""
     torch.manual_seed(5)
     c = case["g"] * case["f"]
