@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--aux-losses", action="store_true", help="add the enc-dec / latent-perturbation losses")
     ap.add_argument("--breakdown", action="store_true")
+    ap.add_argument("--fused-fts", type=str, default=None,
+                    help="comma list of F that use the one-pass term reverses (default: all instances)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -55,6 +57,8 @@ def main():
     from irdu_amd import training as T
     from bench import synthetic_patches
     irdu_amd.load_native()
+    if args.fused_fts is not None:
+        K.FUSED_TERM_FTS = tuple(int(v) for v in args.fused_fts.split(",") if v)
     torch.manual_seed(2204)
     if args.model == "abstract":
         model = irdu_amd.AbtractMultiScaleGraphFilter(3, 3, n_cgd_iters=args.stages, **D_ARGS)

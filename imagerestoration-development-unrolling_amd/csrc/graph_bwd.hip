@@ -681,10 +681,8 @@ bool launch_term_fused(int F, dim3 grid, hipStream_t s, const float* x, const fl
     GRR_TERM_CASE(2)
     GRR_TERM_CASE(3)
     GRR_TERM_CASE(4)
-    GRR_TERM_CASE(6)
-    GRR_TERM_CASE(8)
-    GRR_TERM_CASE(12)
-    default: return false;
+    default: return false;   // F > 4: the tap partials spill registers; the multi-pass path is faster there
+
   }
 #undef GRR_TERM_CASE
 }

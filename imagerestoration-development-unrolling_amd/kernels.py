@@ -367,7 +367,9 @@ def bwd_prox(s: Tensor, a: Tensor, w: Tensor, log_gamma: Tensor, scale: Tensor, 
     return o, gs
 
 
-FUSED_TERM_FTS = (1, 2, 3, 4, 6, 8, 12)   # node-feature counts with a fused reverse instance
+# node-feature counts with a fused reverse instance (measured slower than the multi-pass path
+# for F = 6 and 12: 49.6 vs 46.5 ms of term reverses per v1.0 training step at 8 x 256^2)
+FUSED_TERM_FTS = (1, 2, 3, 4)
 TERM_GLR, TERM_PAIR, TERM_PROX = 0, 1, 2
 
 
@@ -466,7 +468,7 @@ def lnb_norm(x: Tensor, ln_w: Tensor) -> Tuple[Tensor, Tensor]:
     b, c, h, w = x.shape
     n = torch.empty_like(x)
     isd = torch.empty((b, h, w), dtype=torch.float32, device=dev)
-    _launch("lnb_bwd", 8 * x.numel(), "grr_lnb_norm", x.data_ptr(), ln_w.data_ptr(), n.data_ptr(), isd.data_ptr(),
+    _launch("lnb_norm", 8 * x.numel(), "grr_lnb_norm", x.data_ptr(), ln_w.data_ptr(), n.data_ptr(), isd.data_ptr(),
             b, c, h * w, _stream(dev))
     return n, isd
 
@@ -474,7 +476,7 @@ def lnb_norm(x: Tensor, ln_w: Tensor) -> Tuple[Tensor, Tensor]:
 def lnb_norm_bwd(x: Tensor, ln_w: Tensor, isd: Tensor, gn: Tensor, gx: Tensor, gln_w: Tensor) -> None:
     dev = _check("lnb_norm_bwd", x, ln_w, isd, gn, gx, gln_w)
     b, c, h, w = x.shape
-    _launch("lnb_bwd", 20 * x.numel(), "grr_lnb_norm_bwd", x.data_ptr(), ln_w.data_ptr(), isd.data_ptr(),
+    _launch("lnb_norm_bwd", 20 * x.numel(), "grr_lnb_norm_bwd", x.data_ptr(), ln_w.data_ptr(), isd.data_ptr(),
             gn.data_ptr(), gx.data_ptr(), gln_w.data_ptr(), b, c, h * w, _stream(dev))
 
 
@@ -482,7 +484,7 @@ def dwconv3(h: Tensor, wdw: Tensor) -> Tensor:
     dev = _check("dwconv3", h, wdw)
     b, c, hh, ww = h.shape
     out = torch.empty_like(h)
-    _launch("lnb_bwd", 8 * h.numel(), "grr_dwconv3", h.data_ptr(), wdw.data_ptr(), out.data_ptr(), b, c, hh, ww,
+    _launch("dwconv3", 8 * h.numel(), "grr_dwconv3", h.data_ptr(), wdw.data_ptr(), out.data_ptr(), b, c, hh, ww,
             _stream(dev))
     return out
 
@@ -491,7 +493,7 @@ def dwconv3_bwd(g: Tensor, h: Tensor, wdw: Tensor, gwdw: Tensor) -> Tensor:
     dev = _check("dwconv3_bwd", g, h, wdw, gwdw)
     b, c, hh, ww = h.shape
     gh = torch.empty_like(h)
-    _launch("lnb_bwd", 16 * h.numel(), "grr_dwconv3_bwd", g.data_ptr(), h.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
+    _launch("dwconv3_bwd", 16 * h.numel(), "grr_dwconv3_bwd", g.data_ptr(), h.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
             gwdw.data_ptr(), b, c, hh, ww, _stream(dev))
     return gh
 
@@ -503,6 +505,6 @@ def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True)
     hid = c2 // 2
     gate = torch.empty((b, hid, h, w), dtype=torch.float32, device=dev) if want_gate else None
     ghp = torch.empty_like(hp) if ggate is not None else None
-    _launch("lnb_bwd", 4 * hp.numel() * 2, "grr_lnb_gate", hp.data_ptr(), _ptr(ggate), _ptr(gate), _ptr(ghp), b, hid,
+    _launch("lnb_gate", 4 * hp.numel() * 2, "grr_lnb_gate", hp.data_ptr(), _ptr(ggate), _ptr(gate), _ptr(ghp), b, hid,
             h * w, _stream(dev))
     return gate, ghp

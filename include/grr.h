@@ -40,8 +40,9 @@ int grr_version(void);
 const char* grr_last_error(void);
 
 /* Kernel-variant knob for tests and benchmarks (no reference counterpart): 0 = automatic
- * (row-wave graph operators for W <= 256, column strips above), 1 = column-strip graph
- * operators at every width.  Process-wide; results agree to fp32 rounding either way. */
+ * (row-wave graph operators for W <= 256 with the channel waves of a graph in lockstep,
+ * column strips above), 1 = column-strip graph operators at every width, 2 = automatic
+ * without the lockstep.  Process-wide; results agree to fp32 rounding either way. */
 grr_status grr_set_kernel_variant(int variant);
 
 /* a1 — integer neighbour table (bit-exact target).  out[e*H*W + p] = flat index
@@ -206,7 +207,7 @@ grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const fl
  * recomputed on the fly) with both tap gradients fused: mode 0 GLR (w raw), 1 pair Laplacian
  * (w = pair weights), 2 prox (w raw, log_gamma).  Writes v_out = (I-W)^T a, K a or d<a,o>/ds
  * (x-gradient = adjoint-S of v); gw, ggamma, gdot, gtaps (+=) as the multi-pass path, whose
- * results it reproduces.  GRR_ERR_UNSUPPORTED for F outside {1,2,3,4,6,8,12}. */
+ * results it reproduces.  GRR_ERR_UNSUPPORTED for F outside {1,2,3,4}. */
 grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const float* taps, const float* w,
                               const float* log_gamma, const float* scale, float coef, float* v_out, float* gw,
                               float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
