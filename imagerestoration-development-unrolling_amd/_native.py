@@ -61,6 +61,7 @@ SIGNATURES = {
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
+    "grr_lnb_forward_rep": [P, I, I, P, P, P, P, P, P, P, P, I, I, I, I, P],
     # reverse pass
     "grr_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
     "grr_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],

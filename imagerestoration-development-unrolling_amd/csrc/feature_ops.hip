@@ -669,6 +669,21 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
   return grr::lnb_forward_fp32(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
 }
 
+grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, const float* ln_w, const float* w1,
+                               const float* wdw, const float* w2, const float* skip, float* out, void* workspace,
+                               int B, int hid, int H, int W, void* stream) {
+  grr::clear_error();
+  GRR_REQUIRE(src && x && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && Cs > 0 && R > 0 &&
+                  hid > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_lnb_forward_rep: bad args");
+  GRR_REQUIRE(out != x && out != src, GRR_ERR_INVALID_ARG, "grr_lnb_forward_rep: out aliases an input");
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG,
+              "grr_lnb_forward_rep: workspace not 256-B aligned");
+  GRR_REQUIRE(R * Cs <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward_rep: R*Cs=%d > 128", R * Cs);
+  return grr::lnb_forward_mfma_rep(src, Cs, R, x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, hid, H, W,
+                                   (hipStream_t)stream);
+}
+
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {
   clear_error();
   GRR_REQUIRE(img && out && B > 0 && Cin > 0 && G > 0 && P > 0, GRR_ERR_INVALID_ARG, "grr_repeat_graphs: bad args");

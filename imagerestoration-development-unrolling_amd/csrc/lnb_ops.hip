@@ -114,6 +114,7 @@ struct LnbHeadArgs {
   const float* x;        // [B, C, H, W]
   const char* w1f;       // [nch][KS*3 + 1] images of 1 KB: W1 diag(ln_w) fragments, then the chunk's taps
   float* g;              // [B, hid, H, W]
+  float var_den;         // unbiased-variance denominator: C - 1, or (R C - 1) / R for an R-fold replicated x
   int C, hid, H, W, tiles_x, tiles_y, nch;
   uint32_t nblk;
 };
@@ -124,9 +125,12 @@ struct LnbHeadArgs {
 // the depthwise taps: [w][0..8] of mask channel 8c + w, [w][9..17] of value channel hid + 8c + w.
 __host__ __device__ inline int head_images(int KS) { return KS * 3 + 1; }
 
+// R > 1: the block's input is R stacked copies of a C-channel image (MultiScaleGraphFilter's
+// graph replicas, REF13:918-921); W1 diag(ln_w) is folded over the copies (w1 rows have R*C
+// entries), so GEMM1 runs with K = C instead of R*C.
 __global__ void lnb_w1_pack_kernel(const float* __restrict__ w1, const float* __restrict__ ln_w,
                                    const float* __restrict__ wdw, char* __restrict__ out, int C, int hid, int KS,
-                                   int nch) {
+                                   int nch, int R) {
   const int NI = head_images(KS);
   const int64_t n = (int64_t)nch * NI * 256;        // 32-bit words
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -139,7 +143,12 @@ __global__ void lnb_w1_pack_kernel(const float* __restrict__ w1, const float* __
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int k = 32 * s + 8 * (l >> 4) + 2 * (e & 3) + u;
-        if (jj < hid && k < C) h[u] = split_term(w1[(int64_t)((r < 8 ? 0 : hid) + jj) * C + k] * ln_w[k], q);
+        if (jj < hid && k < C) {
+          const float* wr = w1 + (int64_t)((r < 8 ? 0 : hid) + jj) * (R * C);
+          float v = wr[k] * ln_w[k];
+          for (int rep = 1; rep < R; ++rep) v += wr[rep * C + k] * ln_w[rep * C + k];
+          h[u] = split_term(v, q);
+        }
       }
       word = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
     } else if (e < LH_JC * 18) {
@@ -224,7 +233,7 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
       }
     sq += __shfl_xor(sq, 16);
     sq += __shfl_xor(sq, 32);
-    rstd[blk] = 1.0f / sqrtf(sq / (float)(C - 1) + 1e-5f);
+    rstd[blk] = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
 #pragma unroll
     for (int s = 0; s < KS; ++s) split3x8(xv[blk][s], xf[blk][s][0], xf[blk][s][1], xf[blk][s][2]);
   }
@@ -503,27 +512,35 @@ static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                             const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
                             hipStream_t s) {
-  GRR_REQUIRE(C >= 2 && C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d outside [2, 128]", C);
+  return lnb_forward_mfma_rep(x, C, 1, x, ln_w, w1, wdw, w2, skip, out, ws, B, hid, H, W, s);
+}
+
+grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
+                                const float* wdw, const float* w2, const float* skip, float* out, float* ws, int B,
+                                int hid, int H, int W, hipStream_t s) {
+  const int C = R * Ch;   // channels of x / out; the head reads the Ch-channel xh
+  GRR_REQUIRE(C >= 2 && C <= 128 && Ch >= 1, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d outside [2, 128]", C);
   GRR_REQUIRE((int64_t)std::max(hid, C) * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_lnb_forward: max(hid, C)*H*W too large for one image's 32-bit offsets");
-  const int KS = head_ks(C), NB = head_nb(KS), nch = (hid + LH_JC - 1) / LH_JC;
+  const int KS = head_ks(Ch), NB = head_nb(KS), nch = (hid + LH_JC - 1) / LH_JC;
   const int MT = (C + 31) / 32, KS2 = (hid + LM_KD - 1) / LM_KD;
   const int64_t P = (int64_t)H * W;
   float* g = ws;
   char* w1f = reinterpret_cast<char*>(ws + align64((int64_t)B * hid * P));
-  uint16_t* w2f = reinterpret_cast<uint16_t*>(ws + align64((int64_t)B * hid * P) + head_pack_floats(C, hid));
+  uint16_t* w2f = reinterpret_cast<uint16_t*>(ws + align64((int64_t)B * hid * P) + head_pack_floats(Ch, hid));
   {
     const int64_t n1 = (int64_t)nch * head_images(KS) * 256, n2 = (int64_t)KS2 * MT * 3 * 512;
     hipLaunchKernelGGL(lnb_w1_pack_kernel, dim3((unsigned)std::min<int64_t>((n1 + 255) / 256, 4096)), dim3(256), 0,
-                       s, w1, ln_w, wdw, w1f, C, hid, KS, nch);
+                       s, w1, ln_w, wdw, w1f, Ch, hid, KS, nch, R);
     hipLaunchKernelGGL(lnb_w2_pack_kernel, dim3((unsigned)std::min<int64_t>((n2 + 255) / 256, 4096)), dim3(256), 0,
                        s, w2, w2f, C, hid, MT, KS2);
     grr_status st = launch_status("grr_lnb_forward/pack");
     if (st != GRR_OK) return st;
   }
   LnbHeadArgs h{};
-  h.x = x; h.w1f = w1f; h.g = g;
-  h.C = C; h.hid = hid; h.H = H; h.W = W; h.nch = nch;
+  h.x = xh; h.w1f = w1f; h.g = g;
+  h.var_den = R == 1 ? (float)(C - 1) : (float)(C - 1) / (float)R;
+  h.C = Ch; h.hid = hid; h.H = H; h.W = W; h.nch = nch;
   const int TH = NB == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH;
   h.tiles_x = (W + LH_TW - 1) / LH_TW;
   h.tiles_y = (H + TH - 1) / TH;

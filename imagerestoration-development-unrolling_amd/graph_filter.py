@@ -196,6 +196,18 @@ class LocalNonLinearBlock(nn.Module):
                                   ll.channels_local_linear_op.weight, ll.project_out.weight, self.skip_weight)
         return self._forward_hip(x)
 
+    @torch.no_grad()
+    def forward_replicated(self, src, x):
+        """Inference forward when x is copies of src along channels (C <= 128): GEMM1 on src."""
+        ll = self.local_linear
+        c, hid = self.dim, self.hidden_dim
+        if c > 128 or self.nsubnets != 1:
+            return self._forward_hip(x)
+        return K.lnb_forward_rep(src, x, self.norm.weighted_transform.weight.data.view(c),
+                                 ll.channels_linear_op.weight.data.view(2 * hid, c),
+                                 ll.channels_local_linear_op.weight.data.view(2 * hid, 9),
+                                 ll.project_out.weight.data.view(c, hid), self.skip_weight.data)
+
     @hip_forward
     def _forward_hip(self, x):
         ll = self.local_linear
@@ -274,8 +286,10 @@ class MixtureGTVGLR(nn.Module):
             f0 = K.conv1x1(y, s0[0].weight.data)
             f1 = K.conv1x1(self._down(y, s1[0].weight.data, src), s1[1].weight.data)
             return f0, f1
-        f0 = y
-        for blk in list(s0)[:3]:
+        blocks = list(s0)[:3]
+        # the first block's input replicates src over the graphs: its GEMM1 runs on src (K = F)
+        f0 = blocks[0].forward_replicated(src, y) if src is not None else blocks[0](y)
+        for blk in blocks[1:]:
             f0 = blk(f0)
         f0 = K.conv1x1(f0, s0[3].weight.data)
         f1 = self._down(y, s1[0].weight.data, src)

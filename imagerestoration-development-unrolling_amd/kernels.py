@@ -286,6 +286,24 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     return out
 
 
+def lnb_forward_rep(src: Tensor, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
+                    skip: Tensor) -> Tensor:
+    """LocalNonLinearBlock forward when x [B, R*Cs, H, W] is R copies of src [B, Cs, H, W]."""
+    dev = _check("lnb_forward_rep", src, x, ln_w, w1, wdw, w2, skip)
+    b, c, h, w = x.shape
+    cs = src.shape[1]
+    if c % cs or src.shape[0] != b or tuple(src.shape[2:]) != (h, w):
+        raise ValueError("lnb_forward_rep: x must be copies of src")
+    hid = w2.shape[1]
+    nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
+    ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+    out = torch.empty_like(x)
+    _launch("lnb", 4 * b * h * w * (cs + 2 * c + 2 * hid), "grr_lnb_forward_rep", src.data_ptr(), cs, c // cs,
+            x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
+            out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev))
+    return out
+
+
 def repeat_graphs(img: Tensor, n_graphs: int) -> Tensor:
     dev = _check("repeat_graphs", img)
     b, cin, h, w = img.shape

@@ -167,6 +167,15 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
                            const float* w2, const float* skip, float* out, void* workspace,
                            int B, int C, int hid, int H, int W, void* stream);
 
+/* grr_lnb_forward for an input x [B, R*Cs, H, W] that is R stacked copies of src [B, Cs, H, W]
+ * (the first feature block of MultiScaleGraphFilter, whose input replicates RGB over the graphs,
+ * REF13:918-921): LN statistics and W1 are evaluated on src with W1 diag(ln_w) folded over the
+ * copies (GEMM1 depth Cs instead of R*Cs); the skip reads x.  R*Cs <= 128.  workspace:
+ * grr_lnb_workspace_bytes(B, R*Cs, hid, H, W). */
+grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, const float* ln_w, const float* w1,
+                               const float* wdw, const float* w2, const float* skip, float* out, void* workspace,
+                               int B, int hid, int H, int W, void* stream);
+
 /* Channel replication of MultiScaleGraphFilter.forward (REF13:918-921):
  * img [B,Cin,H,W] -> out [B,G*Cin,H,W], out[b, g*Cin + c] = img[b, c]. */
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream);
