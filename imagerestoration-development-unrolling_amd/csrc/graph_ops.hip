@@ -904,8 +904,10 @@ static void launch_row(OpArgs a, int B, hipStream_t s) {
   a.nsegs = (a.H + a.sseg - 1) / a.sseg;
   const uint64_t units = (uint64_t)B * a.G * a.F * a.nsegs;
   a.nunits = (uint32_t)units;
-  // channels of a graph per block: the largest divisor of F that fits NT threads
-  int wpb = g_kernel_variant == 2 ? 1 : NT / 64;
+  // channels of a graph per block: the largest divisor of F that fits NT threads.  Only for
+  // V = 4 (W > 128): on 128-wide half-resolution planes the unsynchronised waves measured 4 %
+  // faster (0.408 vs 0.426 ms, scripts/micro.py --kernel half), the weight rows being short
+  int wpb = (g_kernel_variant == 2 || V < 4) ? 1 : NT / 64;
   while (a.F % wpb) --wpb;
   a.wpb = wpb;
   a.nblk = (uint32_t)(units / wpb);
