@@ -46,9 +46,11 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const float* __restrict__ x,
     const int64_t b = i / P, p = i - b * P;
     const float* xp = x + b * C * P + p;
     float s = 0.f;
+#pragma unroll 8
     for (int c = 0; c < C; ++c) s += xp[(int64_t)c * P];
     const float mean = s / (float)C;
     float q = 0.f;
+#pragma unroll 8
     for (int c = 0; c < C; ++c) {
       const float d = xp[(int64_t)c * P] - mean;
       q += d * d;
@@ -56,6 +58,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const float* __restrict__ x,
     const float r = 1.0f / sqrtf(q / (float)(C - 1) + 1e-5f);
     isd[i] = r;
     float* np_ = n + b * C * P + p;
+#pragma unroll 8
     for (int c = 0; c < C; ++c) np_[(int64_t)c * P] = lnw[c] * xp[(int64_t)c * P] * r;
   }
 }
@@ -69,6 +72,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const float* __restrict__ x,
     const float* xp = x + b * C * P + p;
     const float* gp = gn + b * C * P + p;
     float s = 0.f, dot = 0.f;
+#pragma unroll 8
     for (int c = 0; c < C; ++c) {
       const float xv = xp[(int64_t)c * P];
       s += xv;
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const float* __restrict__ x,
     const float mean = s / (float)C, r = isd[i];
     const float k = dot * r * r * r / (float)(C - 1);
     float* gxp = gx + b * C * P + p;
+#pragma unroll 8
     for (int c = 0; c < C; ++c) {
       const int64_t o = (int64_t)c * P;
       gxp[o] += lnw[c] * gp[o] * r - (xp[o] - mean) * k;
@@ -135,6 +140,14 @@ __global__ __launch_bounds__(NT) void dw3_bwd_data_kernel(const float* __restric
   const int r = p / W, col = p - r * W;
   const float* gp = g + (int64_t)plane * HW;
   float acc = 0.f;
+  if (r > 0 && r < H - 1 && col > 0 && col < W - 1) {   // interior: correlation with the flipped taps
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) acc += wdw[c * 9 + (dy + 1) * 3 + dx + 1] * gp[(r - dy) * W + col - dx];
+    gh[(int64_t)plane * HW + p] = acc;
+    return;
+  }
   for (int dy = -1; dy <= 1; ++dy) {
     int sy[2];
     const int ny = axis_sources(r, dy, H, sy);
