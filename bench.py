@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MPix/sec + PSNR@σ=25, 10-stage GGTV-GGLR on 256×256 patches, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix rate (the arithmetic the LNB GEMMs reproduce exactly)
 G, CIN, STAGES, H, W, SIGMA = 32, 3, 10, 256, 256, 25.0
 
 
@@ -193,6 +194,16 @@ def main():
                       "global_batch": world * b, "per_gpu_batch": b, "image": f"{H}x{W}x{CIN}",
                       "parallelism": f"batch-sharded x{world}, no collective in the data path"},
            "roofline": roofline}
+    if "lnb" in kern:   # the MFMA-bound feature CNN: fp32-accurate split-bf16 GEMMs + depthwise + gate
+        lnb = kern["lnb"]
+        res["roofline_secondary"] = {
+            "bound": "mfma", "kernel": "LocalNonLinearBlock (lnb_head_kernel + lnb_mix_kernel)",
+            "achieved": round(lnb["tflops"], 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(lnb["tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
+            "flops_per_launch": lnb["flops_per_launch"], "mean_launch_ms": round(lnb["mean_ms"], 4),
+            "launches": lnb["launches"],
+            "note": "algorithmic fp32 flops (kernels.lnb_flops) / HIP-event time; each fp32 product runs as 6 "
+                    "bf16 MFMA products (exact 3-term split), so the bf16 rate used is 6x this"}
     kernels_ms = {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms
     if args.breakdown:

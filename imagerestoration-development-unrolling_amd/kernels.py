@@ -54,23 +54,26 @@ class LaunchTimer:
     def __init__(self):
         self.records = {}
 
-    def run(self, kind: str, nbytes: int, fn):
+    def run(self, kind: str, nbytes: int, fn, flops: int = 0):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         fn()
         e.record()
-        self.records.setdefault(kind, []).append((s, e, nbytes))
+        self.records.setdefault(kind, []).append((s, e, nbytes, flops))
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
         for kind, recs in self.records.items():
-            ms = [s.elapsed_time(e) for s, e, _ in recs]
-            nb = sum(b for _, _, b in recs)
+            ms = [s.elapsed_time(e) for s, e, _, _ in recs]
+            nb = sum(r[2] for r in recs)
+            fl = sum(r[3] for r in recs)
             tot = sum(ms)
             out[kind] = {"launches": len(recs), "total_ms": tot, "mean_ms": tot / len(recs),
-                         "bytes_per_launch": nb / len(recs), "gbps": nb / (tot * 1e-3) / 1e9 if tot > 0 else 0.0}
+                         "bytes_per_launch": nb / len(recs), "gbps": nb / (tot * 1e-3) / 1e9 if tot > 0 else 0.0,
+                         "flops_per_launch": fl / len(recs),
+                         "tflops": fl / (tot * 1e-3) / 1e12 if tot > 0 else 0.0}
         return out
 
 
@@ -83,11 +86,18 @@ def set_timer(timer):
     _TIMER = timer
 
 
-def _launch(kind: str, nbytes: int, name: str, *args):
+def _launch(kind: str, nbytes: int, name: str, *args, flops: int = 0):
     if _TIMER is None:
         call(name, *args)
     else:
-        _TIMER.run(kind, int(nbytes), lambda: call(name, *args))
+        _TIMER.run(kind, int(nbytes), lambda: call(name, *args), int(flops))
+
+
+def lnb_flops(px: int, c_head: int, c: int, hid: int) -> int:
+    """Algorithmic fp32 flops of one LocalNonLinearBlock (REF:911-964) over px pixels: LN (4 per
+    input channel), W1 (2 c_head 2hid), depthwise 3x3 (18 per hidden channel), gate (4 per
+    gated channel), W2 (2 hid c), skip (3 per output channel)."""
+    return px * (4 * c_head + 2 * c_head * 2 * hid + 18 * 2 * hid + 4 * hid + 2 * hid * c + 3 * c)
 
 
 def stencil(module) -> Stencil:
@@ -282,7 +292,7 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     nbytes_algo = 4 * b * h * w * (3 * c + 2 * hid) if c <= 128 else 4 * b * h * w * (3 * c + 2 * (2 * hid) + 2 * hid)
     _launch("lnb", nbytes_algo, "grr_lnb_forward", x.data_ptr(),
             ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(), out.data_ptr(),
-            ws.data_ptr(), b, c, hid, h, w, _stream(dev))
+            ws.data_ptr(), b, c, hid, h, w, _stream(dev), flops=lnb_flops(b * h * w, c, c, hid))
     return out
 
 
@@ -300,7 +310,7 @@ def lnb_forward_rep(src: Tensor, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tenso
     out = torch.empty_like(x)
     _launch("lnb", 4 * b * h * w * (cs + 2 * c + 2 * hid), "grr_lnb_forward_rep", src.data_ptr(), cs, c // cs,
             x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
-            out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev))
+            out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev), flops=lnb_flops(b * h * w, cs, c, hid))
     return out
 
 
