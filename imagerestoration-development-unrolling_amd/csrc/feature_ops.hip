@@ -673,7 +673,7 @@ grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, 
                                const float* wdw, const float* w2, const float* skip, float* out, void* workspace,
                                int B, int hid, int H, int W, void* stream) {
   grr::clear_error();
-  GRR_REQUIRE(src && x && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && Cs > 0 && R > 0 &&
+  GRR_REQUIRE(src && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && Cs > 0 && R > 0 &&
                   hid > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_lnb_forward_rep: bad args");
   GRR_REQUIRE(out != x && out != src, GRR_ERR_INVALID_ARG, "grr_lnb_forward_rep: out aliases an input");

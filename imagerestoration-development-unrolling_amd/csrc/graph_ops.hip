@@ -195,6 +195,7 @@ struct OpArgs {
   int nstrips, nsegs, sseg;
   int lin_l;            // log_l holds the scale itself (v10 MixtureGLR stores mu linearly)
   int wpb;              // row kernel: waves per block = channels of one graph walked in lockstep
+  int x_rep, y_rep;     // operand is [B, F, H, W], replicated over the G graphs (channel g F + f reads f)
   uint32_t nunits, nblk;
 };
 
@@ -344,12 +345,13 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
   const bool want_xd = a.xd_out != nullptr;
   const int np = GTV == GTV_PROX ? 4 : 2;
   // plane bases (uniform); absent operands point at the scratch line with row stride 0
-  const float* px = a.x + plane;
+  const int64_t rplane = ((int64_t)b * F + f) * HW;   // plane of a graph-replicated operand
+  const float* px = a.x + (a.x_rep ? rplane : plane);
   const float* pwl = GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
   const float* pwg = GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : nullptr;
   const float* pb = EPI == EPI_STEP ? a.b + plane : scratch;
   const float* pu = use_beta ? a.u_prev + plane : scratch;
-  const float* py = need_y ? a.y + plane : scratch;
+  const float* py = need_y ? a.y + (a.y_rep ? rplane : plane) : scratch;
   const float* pth = has_half ? a.t_half + hplane : scratch;
   float* pout = a.out + plane;
   float* puo = want_u ? a.u_out + plane : scratch;
@@ -639,12 +641,13 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
   const bool want_u = EPI == EPI_STEP && a.u_out != nullptr;
   const bool want_xd = a.xd_out != nullptr;
   const int np = GTV == GTV_PROX ? 4 : 2;
-  const float* px = a.x + plane;
+  const int64_t rplane = ((int64_t)b * F + f) * HW;   // plane of a graph-replicated operand
+  const float* px = a.x + (a.x_rep ? rplane : plane);
   const float* pwl = GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
   const float* pwg = GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : nullptr;
   const float* pb = EPI == EPI_STEP ? a.b + plane : scratch;
   const float* pu = use_beta ? a.u_prev + plane : scratch;
-  const float* py = need_y ? a.y + plane : scratch;
+  const float* py = need_y ? a.y + (a.y_rep ? rplane : plane) : scratch;
   const float* pth = has_half ? a.t_half + hplane : scratch;
   float* pout = a.out + plane;
   float* puo = want_u ? a.u_out + plane : scratch;
@@ -1254,6 +1257,25 @@ grr_status grr_gtv_rhs_full(const float* x, const float* y, const float* wG, grr
   hipStream_t s = (hipStream_t)stream;
   if (prox) return launch_op<false, GTV_PROX, EPI_RHS>(a, B, s, "grr_gtv_rhs_full");
   return launch_op<false, GTV_PAIR, EPI_RHS>(a, B, s, "grr_gtv_rhs_full");
+}
+
+grr_status grr_gtv_rhs_full_rep(const float* x, int x_rep, const float* y, int y_rep, const float* wG, grr_stencil sG, int prox,
+                            const float* log_gamma, const float* log_ro0, const float* t_half, const float* log_ro1,
+                            float* b_out, float* xd_out, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && y && wG && b_out && log_ro0 && stencil_ok(sG) && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_gtv_rhs_full_rep: bad args");
+  GRR_REQUIRE(!prox || log_gamma, GRR_ERR_INVALID_ARG, "grr_gtv_rhs_full_rep: prox needs log_gamma");
+  GRR_REQUIRE(!t_half || log_ro1, GRR_ERR_INVALID_ARG, "grr_gtv_rhs_full_rep: t_half needs log_ro1");
+  GRR_REQUIRE(!(t_half || xd_out) || (H % 2 == 0 && W % 2 == 0), GRR_ERR_SHAPE,
+              "grr_gtv_rhs_full_rep: two-scale operator needs even H, W (got %dx%d)", H, W);
+  OpArgs a{};
+  a.x = x; a.y = y; a.x_rep = x_rep != 0; a.y_rep = y_rep != 0; a.wG = wG; a.sG = sG; a.log_gamma = log_gamma; a.log_g = log_ro0;
+  a.t_half = t_half; a.log_half = log_ro1; a.out = b_out; a.xd_out = xd_out;
+  a.G = G; a.F = F; a.H = H; a.W = W;
+  hipStream_t s = (hipStream_t)stream;
+  if (prox) return launch_op<false, GTV_PROX, EPI_RHS>(a, B, s, "grr_gtv_rhs_full_rep");
+  return launch_op<false, GTV_PAIR, EPI_RHS>(a, B, s, "grr_gtv_rhs_full_rep");
 }
 
 grr_status grr_system_step(const float* x, const float* b, const float* u_prev, const float* t_half, const float* wL,

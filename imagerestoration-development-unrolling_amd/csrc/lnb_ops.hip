@@ -340,7 +340,8 @@ constexpr int LM_KD = 16;                 // hidden channels per k-step
 struct LnbMixArgs {
   const float* g;         // [B, hid, P]
   const char* w2f;        // [KS2][MT][3] fragment images of W2
-  const float* x;         // [B, C, P]
+  const float* x;         // [B, C, P], or [B, xs_c, P] read at channel m mod xs_c when xs_c > 0
+  int xs_c;
   const float* skip;      // [2]
   float* out;             // [B, C, P]
   int64_t P;
@@ -454,8 +455,9 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArg
   // x / out through buffer descriptors (32-bit offsets; rows >= C or pixels >= P not stored)
   const float s0 = a.skip[0], s1 = a.skip[1];
   const int img_bytes = (int)((int64_t)C * P * 4);
-  const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x + (int64_t)b * C * P), 0, img_bytes, 0x00020000);
+  const int XC = a.xs_c > 0 ? a.xs_c : C;   // skip operand: x, or the image x replicates (channel m mod XC)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x + (int64_t)b * XC * P), 0, (int)((int64_t)XC * P * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * C * P, 0, img_bytes,
                                                                         0x00020000);
   const int Pi = (int)P;
@@ -469,7 +471,8 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArg
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = min(32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh, C - 1);
-        xv[t][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (m * Pi + pc) * 4, 0, 0));
+        const int mx = XC == C ? m : m % XC;
+        xv[t][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (mx * Pi + pc) * 4, 0, 0));
       }
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -556,7 +559,9 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   grr_status st = launch_status("grr_lnb_forward/head");
   if (st != GRR_OK) return st;
   LnbMixArgs m{};
-  m.g = g; m.w2f = reinterpret_cast<const char*>(w2f); m.x = x; m.skip = skip; m.out = out;
+  m.g = g; m.w2f = reinterpret_cast<const char*>(w2f); m.skip = skip; m.out = out;
+  m.x = x ? x : xh;           // x == NULL: the skip reads the replicated image itself
+  m.xs_c = x ? 0 : Ch;
   m.P = P; m.C = C; m.hid = hid; m.KS2 = KS2;
   m.tiles = (int)((P + LM_PX - 1) / LM_PX);
   const uint64_t nm = (uint64_t)B * m.tiles;

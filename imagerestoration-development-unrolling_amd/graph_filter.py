@@ -197,11 +197,14 @@ class LocalNonLinearBlock(nn.Module):
         return self._forward_hip(x)
 
     @torch.no_grad()
-    def forward_replicated(self, src, x):
-        """Inference forward when x is copies of src along channels (C <= 128): GEMM1 on src."""
+    def forward_replicated(self, src, x=None):
+        """Inference forward when the block input is copies of src along channels (C <= 128):
+        GEMM1 on src; x (the materialised copies) may be None, the skip then reads src."""
         ll = self.local_linear
         c, hid = self.dim, self.hidden_dim
         if c > 128 or self.nsubnets != 1:
+            if x is None:
+                x = src.repeat(1, c // src.shape[1], 1, 1)
             return self._forward_hip(x)
         return K.lnb_forward_rep(src, x, self.norm.weighted_transform.weight.data.view(c),
                                  ll.channels_linear_op.weight.data.view(2 * hid, c),
@@ -316,13 +319,21 @@ class MixtureGTVGLR(nn.Module):
         return f0, f1
 
     # -- solver (a3-a17) -----------------------------------------------------
-    def _solve(self, y: torch.Tensor, skip: Optional[torch.Tensor] = None,
+    def _solve(self, y: Optional[torch.Tensor], skip: Optional[torch.Tensor] = None,
                src: Optional[torch.Tensor] = None) -> torch.Tensor:
         """src: optional [B, F, H, W] image that y replicates over the G graphs (y[:, gF + i] =
-        src[:, i]); lets the replicated-input steps run on src."""
-        b, c, h, w = y.shape
+        src[:, i]); lets the replicated-input steps run on src.  With src, y may be None: the
+        replicated input is then never materialised (first feature block, 2x2 conv and both
+        right-hand sides read src; REF13:918-921)."""
         g, f = self.n_graphs, self.n_node_fts
-        if c != self.n_channels:
+        if y is None:
+            if src is None:
+                raise ValueError("MixtureGTVGLR: need y or src")
+            if self.feature_extractor != "v13" or skip is not None:   # those paths read y itself
+                y = K.repeat_graphs(src, g)
+        ref = y if y is not None else src
+        b, c, h, w = ref.shape
+        if y is not None and c != self.n_channels:
             raise ValueError(f"MixtureGTVGLR: expected {self.n_channels} channels, got {c}")
         if h % 2 or w % 2:
             raise ValueError(f"MixtureGTVGLR: H, W must be even for the 2x2 scale (got {h}x{w})")
@@ -343,7 +354,10 @@ class MixtureGTVGLR(nn.Module):
         yd = K.pool2(y) if src is None else K.repeat_graphs(K.pool2(src), g)   # D y
         t = K.gtv_rhs_half(yd, cG1, sG1, False, None, g)
         del yd
-        b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+        if y is None:
+            b_a, xd = K.gtv_rhs_full_rep(src, True, src, True, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+        else:
+            b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
         # stage 0: x1 = b_A + alpha0 (b_A - A b_A)                     (REF:751-753)
         last = n_st == 1
         t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
@@ -355,7 +369,10 @@ class MixtureGTVGLR(nn.Module):
             return x
         # GTV proximal step -> rhs B                                   (REF:757-781)
         t = K.gtv_rhs_half(xd, wG1, sG1, True, d(self.gamma01), g)
-        b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, d(self.gamma00), ro0, t, ro1, g)
+        if y is None:
+            b_b, _ = K.gtv_rhs_full_rep(x, False, src, True, wG0, sG0, True, d(self.gamma00), ro0, t, ro1, g)
+        else:
+            b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, d(self.gamma00), ro0, t, ro1, g)
         del wG0, wG1
         u = None
         for k in range(1, n_st):                                     # (REF:784-790, :797-807)
@@ -421,8 +438,8 @@ class MultiScaleGraphFilter(nn.Module):
 
     @torch.no_grad()
     def _forward_inference(self, img):
-        x = K.repeat_graphs(img, self.ngraphs)
-        y = self.localfilter(x, _src=img)
+        # the G-fold replicated input (REF13:918-921) is never materialised: the solver reads img
+        y = self.localfilter._solve(None, None, img)
         return K.conv1x1(y, self.linear_combination.weight.data)
 
 

@@ -215,6 +215,26 @@ def gtv_rhs_full(x: Tensor, y: Tensor, wG: Tensor, sG: Stencil, prox: bool, log_
     return out, xd
 
 
+def gtv_rhs_full_rep(x: Tensor, x_rep: bool, y: Tensor, y_rep: bool, wG: Tensor, sG: Stencil, prox: bool,
+                     log_gamma: Optional[Tensor], log_ro0: Tensor, t_half: Optional[Tensor],
+                     log_ro1: Optional[Tensor], n_graphs: int, want_pool: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+    """grr_gtv_rhs_full with x and/or y given as the [B, F, H, W] image they replicate over the graphs."""
+    dev = _check("gtv_rhs_full", x, y, wG, log_gamma, log_ro0, t_half, log_ro1)
+    full = y if not y_rep else (x if not x_rep else None)
+    b, f, h, w = (x if x_rep else y).shape if full is None else (full.shape[0], full.shape[1] // n_graphs,
+                                                                  full.shape[2], full.shape[3])
+    c = n_graphs * f
+    out = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
+    xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_pool else None
+    px = b * h * w
+    nbytes = 4 * (px * (f if x_rep else c) + px * (f if y_rep else c) + px * c + px * (4 if prox else 2) * n_graphs
+                  + (px * c // 4 if t_half is not None else 0) + (px * c // 4 if want_pool else 0))
+    _launch("gtv_rhs_full", nbytes, "grr_gtv_rhs_full_rep", x.data_ptr(), int(x_rep), y.data_ptr(), int(y_rep),
+            wG.data_ptr(), sG, int(prox), _ptr(log_gamma), log_ro0.data_ptr(), _ptr(t_half), _ptr(log_ro1),
+            out.data_ptr(), _ptr(xd), b, n_graphs, f, h, w, _stream(dev))
+    return out, xd
+
+
 def system_step(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Optional[Tensor],
                 wL: Optional[Tensor], cG: Optional[Tensor], sL: Stencil, sG: Stencil,
                 log_mu0: Optional[Tensor], log_ro0: Optional[Tensor], alpha: Tensor, beta: Optional[Tensor],
@@ -296,20 +316,21 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     return out
 
 
-def lnb_forward_rep(src: Tensor, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
+def lnb_forward_rep(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
                     skip: Tensor) -> Tensor:
-    """LocalNonLinearBlock forward when x [B, R*Cs, H, W] is R copies of src [B, Cs, H, W]."""
+    """LocalNonLinearBlock forward when its input [B, R*Cs, H, W] is R copies of src [B, Cs, H, W];
+    x is that replicated input (read by the skip) or None (the skip reads src)."""
     dev = _check("lnb_forward_rep", src, x, ln_w, w1, wdw, w2, skip)
-    b, c, h, w = x.shape
-    cs = src.shape[1]
-    if c % cs or src.shape[0] != b or tuple(src.shape[2:]) != (h, w):
-        raise ValueError("lnb_forward_rep: x must be copies of src")
+    b, cs, h, w = src.shape
+    c = ln_w.numel()
+    if c % cs or (x is not None and tuple(x.shape) != (b, c, h, w)):
+        raise ValueError("lnb_forward_rep: the block input must be copies of src")
     hid = w2.shape[1]
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
-    out = torch.empty_like(x)
+    out = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
     _launch("lnb", 4 * b * h * w * (cs + 2 * c + 2 * hid), "grr_lnb_forward_rep", src.data_ptr(), cs, c // cs,
-            x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
+            _ptr(x), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
             out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev), flops=lnb_flops(b * h * w, cs, c, hid))
     return out
 

@@ -112,6 +112,14 @@ grr_status grr_gtv_rhs_full(const float* x, const float* y, const float* wG, grr
                             float* b_out, float* xd_out,
                             int B, int G, int F, int H, int W, void* stream);
 
+/* grr_gtv_rhs_full where x and/or y are given un-replicated, [B, F, H, W], standing for their
+ * copies over the G graphs (MultiScaleGraphFilter's input, REF13:918-921; x_rep / y_rep != 0):
+ * channel g*F + f reads plane f.  b_out / xd_out stay [B, G*F, ...]. */
+grr_status grr_gtv_rhs_full_rep(const float* x, int x_rep, const float* y, int y_rep, const float* wG,
+                                grr_stencil sG, int prox, const float* log_gamma, const float* log_ro0,
+                                const float* t_half, const float* log_ro1, float* b_out, float* xd_out,
+                                int B, int G, int F, int H, int W, void* stream);
+
 /* One unrolled CG / heavy-ball stage (REF:751-753, :784-790, extension :797-807):
  *   A x   = ((x + exp(log_mu0) L0 x) + exp(log_ro0) G0 x) + U(t_half)
  *   r     = b - A x
@@ -170,7 +178,8 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
 /* grr_lnb_forward for an input x [B, R*Cs, H, W] that is R stacked copies of src [B, Cs, H, W]
  * (the first feature block of MultiScaleGraphFilter, whose input replicates RGB over the graphs,
  * REF13:918-921): LN statistics and W1 are evaluated on src with W1 diag(ln_w) folded over the
- * copies (GEMM1 depth Cs instead of R*Cs); the skip reads x.  R*Cs <= 128.  workspace:
+ * copies (GEMM1 depth Cs instead of R*Cs); the skip reads x, or src at channel c mod Cs when
+ * x == NULL (then no replicated copy needs to exist).  R*Cs <= 128.  workspace:
  * grr_lnb_workspace_bytes(B, R*Cs, hid, H, W). */
 grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, const float* ln_w, const float* w1,
                                const float* wdw, const float* w2, const float* skip, float* out, void* workspace,
