@@ -113,6 +113,45 @@ def cpu_baseline(model_cpu_state, n_img=4):
             "seconds": dt}, clean, noisy, ref
 
 
+D_CFG = dict(dims=[48, 96, 192, 384], hidden_dims=[96, 192, 384, 768], nsubnets=[1, 1, 1, 1],
+             ngraphs=[8, 16, 16, 32], num_blocks=[4, 6, 6, 8], num_blocks_out=4)
+
+
+def bench_abstract(dev, b, steps=3):
+    """SURVEY.md §8(d) 'D': the drop-in v1.0 AbtractMultiScaleGraphFilter (trained dims of
+    README.ipynb:74-84) with S = 10 in all four filter blocks: end-to-end forward and the
+    filtering() part alone, on b synthetic 256x256 patches (rank 0 only, after the main timing)."""
+    import irdu_amd
+    torch.manual_seed(2204)
+    m = irdu_amd.AbtractMultiScaleGraphFilter(3, 3, n_cgd_iters=STAGES, **D_CFG).to(dev).eval()
+    _, noisy = synthetic_patches(b, seed=7)
+    noisy = noisy.to(dev)
+    with torch.no_grad():
+        for _ in range(2):
+            m(noisy)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m(noisy)
+        torch.cuda.synchronize(dev)
+        t_full = (time.perf_counter() - t0) / steps
+        coefs = m.encode(noisy)
+        m.filtering(coefs)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m.filtering(coefs)
+        torch.cuda.synchronize(dev)
+        t_filt = (time.perf_counter() - t0) / steps
+    px = b * H * W
+    return {"workload": f"AbtractMultiScaleGraphFilter v1.0 dims {D_CFG['dims']} ngraphs {D_CFG['ngraphs']} "
+                        f"blocks {D_CFG['num_blocks']}, S={STAGES} in all 4 filter blocks, {H}x{W} RGB",
+            "per_gpu_batch": b, "mpix_per_s": round(px / t_full / 1e6, 3), "ms_per_step": round(t_full * 1e3, 2),
+            "filtering_mpix_per_s": round(px / t_filt / 1e6, 3), "filtering_ms": round(t_filt * 1e3, 2),
+            "note": "encoder/decoder plain convs on stock PyTorch-ROCm; every LocalNonLinearBlock and filter "
+                    "block on HIP"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +159,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="patches per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary workload (v1.0 AbtractMultiScaleGraphFilter, SURVEY.md §8d 'D')")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
     args = ap.parse_args()
 
@@ -210,6 +251,8 @@ def main():
         for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
             print(f"{k:18s} launches/step={v['launches'] / args.steps:5.1f} mean={v['mean_ms']:8.3f} ms "
                   f"algo={v['gbps']:8.1f} GB/s", file=sys.stderr)
+    if not args.no_secondary and rank == 0:
+        res["secondary_workload"] = bench_abstract(dev, min(b, 16))
     if not args.no_cpu_baseline:
         from oracle import graph_oracle as O
         state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
