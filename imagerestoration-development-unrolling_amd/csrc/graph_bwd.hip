@@ -120,6 +120,62 @@ __global__ __launch_bounds__(NT) void stencil_kernel(const float* __restrict__ x
   *o = acc ? *o + y : y;
 }
 
+// The same four stencils, four adjacent columns per thread (W % 4 == 0, 16-byte aligned planes):
+// rows r-1, r, r+1 as float4 plus the two flanking columns of row r.  grid (ceil(HW/4/NT), B*C).
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <int mode>
+__global__ __launch_bounds__(NT) void stencil4_kernel(const float* __restrict__ x, const float* __restrict__ taps,
+                                                      const float* __restrict__ scale, int acc,
+                                                      float* __restrict__ out, int C, int F, int H, int W) {
+  const int HW = H * W, W4 = W / 4;
+  const int q4 = blockIdx.x * NT + threadIdx.x;
+  if (q4 >= HW / 4) return;
+  const int plane = blockIdx.y, ch = plane % C;
+  const int r = q4 / W4, c0 = (q4 - r * W4) * 4;
+  const float* xp = x + (int64_t)plane * HW;
+  const float k0 = taps[ch * 5], ku = taps[ch * 5 + 1], kl = taps[ch * 5 + 2], kr = taps[ch * 5 + 3],
+              kd = taps[ch * 5 + 4];
+  const bool top = r == 0, bot = r == H - 1, lft = c0 == 0, rgt = c0 + 4 == W;
+  const f4 cv = *reinterpret_cast<const f4*>(xp + r * W + c0);
+  f4 uv, dv;
+  float lv, rv;
+  if constexpr (mode == 0) {   // replicate
+    uv = *reinterpret_cast<const f4*>(xp + (top ? r : r - 1) * W + c0);
+    dv = *reinterpret_cast<const f4*>(xp + (bot ? r : r + 1) * W + c0);
+    lv = lft ? cv[0] : xp[r * W + c0 - 1];
+    rv = rgt ? cv[3] : xp[r * W + c0 + 4];
+  } else {                     // zero frame
+    uv = top ? f4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f4*>(xp + (r - 1) * W + c0);
+    dv = bot ? f4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f4*>(xp + (r + 1) * W + c0);
+    lv = lft ? 0.f : xp[r * W + c0 - 1];
+    rv = rgt ? 0.f : xp[r * W + c0 + 4];
+  }
+  f4 y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float l = j > 0 ? cv[j - 1] : lv, rr = j < 3 ? cv[j + 1] : rv;
+    float v;
+    if constexpr (mode == 0 || mode == 2) {   // sum_t k_t x(p + t)
+      v = k0 * cv[j];
+      v += ku * uv[j]; v += kl * l; v += kr * rr; v += kd * dv[j];
+    } else {                                  // sum_t k_t x(q - t)
+      v = k0 * cv[j];
+      v += ku * dv[j]; v += kl * rr; v += kr * l; v += kd * uv[j];
+      if constexpr (mode == 3) {              // replicate adjoint: clamped reads at the frame land on q
+        const int col = c0 + j;
+        if (top) v += ku * cv[j];
+        if (bot) v += kd * cv[j];
+        if (col == 0) v += kl * cv[j];
+        if (col == W - 1) v += kr * cv[j];
+      }
+    }
+    y[j] = v;
+  }
+  if (scale) y *= scale[ch / F];
+  f4* o = reinterpret_cast<f4*>(out + (int64_t)plane * HW + r * W + c0);
+  *o = acc ? *o + y : y;
+}
+
 // Tap gradients of y = mode(z) contracted with u: gt[c, t] += scale[g] * sum_{b,q} u(q) dy(q)/dk_t.
 // mode 0 (P): dy(q)/dk_t = z(clamp(q + t));  mode 1 (T): z(q - t) [inside].   grid (chunks, B*C).
 template <int mode>
@@ -731,8 +787,18 @@ grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const fl
   const int C = G * F;
   GRR_REQUIRE((int64_t)B * C <= 65535 && (int64_t)H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_bwd_stencil: grid too large");
-  const dim3 grid((H * W + NT - 1) / NT, B * C);
   hipStream_t s = (hipStream_t)stream;
+  if (W % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)out % 16 == 0) {
+    const dim3 g4((H * W / 4 + NT - 1) / NT, B * C);
+    switch (mode) {
+      case 0: hipLaunchKernelGGL(stencil4_kernel<0>, g4, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
+      case 1: hipLaunchKernelGGL(stencil4_kernel<1>, g4, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
+      case 2: hipLaunchKernelGGL(stencil4_kernel<2>, g4, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
+      default: hipLaunchKernelGGL(stencil4_kernel<3>, g4, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W);
+    }
+    return launch_status("grr_bwd_stencil");
+  }
+  const dim3 grid((H * W + NT - 1) / NT, B * C);
   switch (mode) {
     case 0: hipLaunchKernelGGL(stencil_kernel<0>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
     case 1: hipLaunchKernelGGL(stencil_kernel<1>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W); break;
