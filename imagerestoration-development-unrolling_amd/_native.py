@@ -81,6 +81,10 @@ SIGNATURES = {
     "grr_dwconv3": [P, P, P, I, I, I, I, P],
     "grr_dwconv3_bwd": [P, P, P, P, P, I, I, I, I, P],
     "grr_lnb_gate": [P, P, P, P, I, I, L, P],
+    # window graphs (REF7 / REF1)
+    "grr_win_edge_weights": [P, L, P, P, I, P, P, I, I, I, I, I, P],
+    "grr_win_solver": [I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, I, I, I, I, I, P],
+    "grr_win_mix": [P, P, P, P, I, I, I, I, I, P],
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64}

@@ -557,3 +557,115 @@ def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True)
     _launch("lnb_gate", 4 * hp.numel() * 2, "grr_lnb_gate", hp.data_ptr(), _ptr(ggate), _ptr(gate), _ptr(ghp), b, hid,
             h * w, _stream(dev))
     return gate, ghp
+
+
+# ---- window graphs (REF7 = lib/model_GLR_GTV_deep_v7.py, REF1 = lib/model_GLR_GTV_deep_v1.py) ----
+_DELTA_CACHE = {}
+
+
+def _delta_arg(edge_delta) -> Tuple[object, int]:
+    """Host int32 [K,2] (dy, dx) array for the window entry points (cached per window)."""
+    key = tuple((int(a), int(b)) for a, b in edge_delta)
+    arr = _DELTA_CACHE.get(key)
+    if arr is None:
+        import ctypes
+        flat = [v for e in key for v in e]
+        arr = (ctypes.c_int32 * len(flat))(*flat)
+        _DELTA_CACHE[key] = arr
+    return arr, len(key)
+
+
+def win_edge_weights(feat: Tensor, channel_offset: int, n_graphs: int, n_fts: int, multiM: Tensor, edge_delta,
+                     with_degree: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+    """Window-graph edge weights (grr_win_edge_weights, REF7:418-446) of the [n_graphs*n_fts] channel
+    slab at ``channel_offset`` of feat [B,Ctot,H,W] -> (w [B,G,K,H,W], degree or None)."""
+    dev = _check("win_edge_weights", feat, multiM)
+    b, ctot, h, w = feat.shape
+    if channel_offset + n_graphs * n_fts > ctot:
+        raise ValueError("win_edge_weights: channel slab out of range")
+    delta, k = _delta_arg(edge_delta)
+    wt = torch.empty((b, n_graphs, k, h, w), dtype=torch.float32, device=dev)
+    deg = torch.empty((b, n_graphs, h, w), dtype=torch.float32, device=dev) if with_degree else None
+    base = feat.data_ptr() + channel_offset * h * w * feat.element_size()
+    nbytes = 4 * b * h * w * (n_graphs * n_fts + k * n_graphs + (n_graphs if with_degree else 0))
+    _launch("win_edge_weights", nbytes, "grr_win_edge_weights", base, ctot * h * w, multiM.data_ptr(), delta, k,
+            wt.data_ptr(), _ptr(deg), b, n_graphs, n_fts, h, w, _stream(dev))
+    return wt, deg
+
+
+def win_taps(p01: Tensor, p02a: Tensor, p02b: Tensor, p03: Tensor) -> Tensor:
+    """(centre, up, left, right, down) of the stats stencil p01 k01 + p02a k02a + p02b k02b + p03 k03
+    (REF7:300-358, scalar parameters): centre p01 - p02a - p02b + 4 p03, right p02a - p03,
+    down p02b - p03, up = left = -p03."""
+    p01, p02a, p02b, p03 = (t.reshape(()) for t in (p01, p02a, p02b, p03))
+    return torch.stack([p01 - p02a - p02b + 4.0 * p03, -p03, -p03, p02a - p03, p02b - p03]).float().contiguous()
+
+
+IDENTITY_TAPS = (1.0, 0.0, 0.0, 0.0, 0.0)
+
+
+def win_solver(mode: int, x: Tensor, y: Tensor, wG: Tensor, tapsG: Tensor, ro: Tensor, edge_delta, n_graphs: int,
+               n_sig: int, *, wL: Optional[Tensor] = None, tapsL: Optional[Tensor] = None, mu: Optional[Tensor] = None,
+               log_gamma: Optional[Tensor] = None, alpha: Optional[Tensor] = None, beta: Optional[Tensor] = None,
+               u_prev: Optional[Tensor] = None, want_u: bool = True) -> Tuple[Tensor, Optional[Tensor]]:
+    """One fused pass of the window-graph MixtureGTV solver (grr_win_solver, REF7:892-1004).
+
+    mode 0: CG step, x [B,G,Fs,H,W], y = rhs [B,G,Fs,H,W] -> (x_next, u);
+    mode 1/2: (prox) right-hand side, y [B,Fs,H,W] shared by the graphs, x per graph or
+    [B,Fs,H,W] (shared) -> (rhs [B,G,Fs,H,W], None)."""
+    dev = _check("win_solver", x, y, wG, tapsG, ro, wL, tapsL, mu, log_gamma, alpha, beta, u_prev)
+    delta, k = _delta_arg(edge_delta)
+    b, h, w = x.shape[0], x.shape[-2], x.shape[-1]
+    x_rep = int(x.dim() == 4)
+    if x_rep and x.shape[1] != n_sig or not x_rep and tuple(x.shape[1:3]) != (n_graphs, n_sig):
+        raise ValueError(f"win_solver: x has shape {tuple(x.shape)}")
+    if tuple(wG.shape) != (b, n_graphs, k, h, w):
+        raise ValueError(f"win_solver: wG has shape {tuple(wG.shape)}, expected {(b, n_graphs, k, h, w)}")
+    out = torch.empty((b, n_graphs, n_sig, h, w), dtype=torch.float32, device=dev)
+    u_out = torch.empty_like(out) if (mode == 0 and want_u) else None
+    planes = b * n_graphs * n_sig
+    if mode == 0:
+        if tuple(wL.shape) != tuple(wG.shape) or tuple(y.shape) != tuple(out.shape):
+            raise ValueError("win_solver: wL / rhs shapes do not match")
+        nbytes = 4 * h * w * (planes * (2 + int(u_prev is not None) + 1 + int(u_out is not None))
+                              + 2 * k * b * n_graphs)
+    else:
+        if tuple(y.shape) != (b, n_sig, h, w):
+            raise ValueError(f"win_solver: y has shape {tuple(y.shape)}, expected {(b, n_sig, h, w)}")
+        nbytes = 4 * h * w * (planes * (1 + int(not x_rep)) + b * n_sig * (1 + x_rep) + k * b * n_graphs)
+    _launch("win_solver", nbytes, "grr_win_solver", mode, x.data_ptr(), x_rep, y.data_ptr(), _ptr(u_prev), _ptr(wL),
+            wG.data_ptr(), _ptr(tapsL), tapsG.data_ptr(), _ptr(mu), ro.data_ptr(), _ptr(log_gamma), _ptr(alpha),
+            _ptr(beta), delta, k, out.data_ptr(), _ptr(u_out), b, n_graphs, n_sig, h, w, _stream(dev))
+    return out, u_out
+
+
+def win_mix(x: Tensor, score: Tensor, dc: Optional[Tensor] = None) -> Tensor:
+    """sum_g x[b,g,c] score[b,g] (+ dc[b,c]) (grr_win_mix, REF7:1006-1009)."""
+    dev = _check("win_mix", x, score, dc)
+    b, g, c, h, w = x.shape
+    if tuple(score.shape) != (b, g, h, w) or (dc is not None and tuple(dc.shape) != (b, c, h, w)):
+        raise ValueError("win_mix: score / dc shapes do not match")
+    out = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
+    nbytes = 4 * h * w * (x[0].numel() // (h * w) * b + b * g + b * c * (1 + int(dc is not None)))
+    _launch("win_mix", nbytes, "grr_win_mix", x.data_ptr(), score.data_ptr(), _ptr(dc), out.data_ptr(), b, g, c, h, w,
+            _stream(dev))
+    return out
+
+
+def win_apply(x: Tensor, edge_delta, n_graphs: int, n_sig: int, *, wL: Optional[Tensor] = None,
+              tapsL: Optional[Tensor] = None, mu: Optional[Tensor] = None, wG: Optional[Tensor] = None,
+              tapsG: Optional[Tensor] = None, ro: Optional[Tensor] = None) -> Tensor:
+    """mu S_L^T (I - W_L) S_L x [wL] + ro S_G^T C^T C S_G x [wG] (grr_win_solver mode 3; the
+    GLRFast / GTVFast.forward of REF7:503-511, :776-782).  x [B,G,Fs,H,W]."""
+    dev = _check("win_apply", x, wL, tapsL, mu, wG, tapsG, ro)
+    delta, k = _delta_arg(edge_delta)
+    b, g, c, h, w = x.shape
+    for t in (wL, wG):
+        if t is not None and tuple(t.shape) != (b, n_graphs, k, h, w):
+            raise ValueError(f"win_apply: edge weights of shape {tuple(t.shape)}, expected {(b, n_graphs, k, h, w)}")
+    out = torch.empty_like(x)
+    nbytes = 4 * h * w * (2 * x.numel() // (h * w) + k * b * n_graphs * (int(wL is not None) + int(wG is not None)))
+    _launch("win_solver", nbytes, "grr_win_solver", 3, x.data_ptr(), 0, None, None, _ptr(wL), _ptr(wG), _ptr(tapsL),
+            _ptr(tapsG), _ptr(mu), _ptr(ro), None, None, None, delta, k, out.data_ptr(), None, b, n_graphs, n_sig, h, w,
+            _stream(dev))
+    return out

@@ -265,6 +265,46 @@ grr_status grr_dwconv3_bwd(const float* g, const float* h, const float* wdw, flo
 grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,
                         void* stream);
 
+/* ---- window graphs (older image-domain models) ------------------------------
+ * REF7 = exploration/model_multiscale_mixture_GLR/lib/model_GLR_GTV_deep_v7.py,
+ * REF1 = .../lib/model_GLR_GTV_deep_v1.py.  Graphs connect each pixel to the K
+ * neighbours of a connection window; delta is a HOST array int32 [K,2] of (dy, dx)
+ * offsets in the reference's edge order (itertools.product over the window, REF7:285-296),
+ * |dy|, |dx| <= 2, K <= 24.  Signals x [B,G,Fs,H,W] (Fs = signal channels, 3 for RGB);
+ * edge weights [B,G,K,H,W]; taps device [5] = (centre, up, left, right, down) of the
+ * module's stats stencil (identity (1,0,0,0,0) for REF1, which has none). */
+
+/* Edge weights of a window graph (GLRFast/GTVFast.extract_edge_weights, REF7:418-446):
+ * feat channels [g*F, (g+1)*F) of each batch item (batch stride feat_bstride floats),
+ * normalised over F, scaled by multiM [G,F], K dot products with the (replicate-clamped)
+ * neighbours, softmax over the K edges -> w [B,G,K,H,W]; deg [B,G,H,W] (may be NULL). */
+grr_status grr_win_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM, const int32_t* delta,
+                                int K, float* w, float* deg, int B, int G, int F, int H, int W, void* stream);
+
+/* One fused pass of MixtureGTV's solver (REF7:892-1004; REF1:558-676), edge tensors never
+ * materialised.  mu, ro [G] linear, log_gamma [G] (gamma = exp), alpha/beta [G] = one row.
+ *  mode 0, CG step: A x = x + mu S_L^T(S_L x - W_L S_L x) + ro S_G^T C^T C S_G x (REF7:892-911),
+ *          u = (y - A x) + beta u_prev (u = y - A x when u_prev == NULL), out = x + alpha u,
+ *          u_out = u (may be NULL); y is the right-hand side [B,G,Fs,H,W].
+ *  mode 1, rhs:      out = ro S_G^T C^T (C S_G x) + y        (first ADMM rhs, bias 0, REF7:945-949)
+ *  mode 2, prox rhs: out = ro S_G^T C^T (2 soft(C S_G x, gamma) - C S_G x) + y
+ *                    (one ADMM bias update from 0, REF7:958-967);
+ *          modes 1/2: y [B,Fs,H,W] shared by the graphs, x per graph or (x_rep) [B,Fs,H,W].
+ *  mode 3, module apply (GLRFast/GTVFast.forward, REF7:503-511, :776-782):
+ *          out = mu S_L^T(S_L x - W_L S_L x) [wL != NULL] + ro S_G^T C^T C S_G x [wG != NULL];
+ *          mu / ro may be NULL (= 1); y unused.
+ * S reads x with a reflect frame (REF7:449-467); L/C neighbours clamp to the frame; S^T and
+ * the C^T scatter drop what lands outside (REF7:469-488, :748-774). */
+grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, const float* u_prev, const float* wL,
+                          const float* wG, const float* tapsL, const float* tapsG, const float* mu, const float* ro,
+                          const float* log_gamma, const float* alpha, const float* beta, const int32_t* delta, int K,
+                          float* out, float* u_out, int B, int G, int Fs, int H, int W, void* stream);
+
+/* Graph mixture (REF7:1006-1009): out[b,c] = sum_g x[b,g,c] score[b,g] + dc[b,c] (dc may be NULL).
+ * x [B,G,Fs,H,W], score [B,G,H,W], dc/out [B,Fs,H,W]. */
+grr_status grr_win_mix(const float* x, const float* score, const float* dc, float* out, int B, int G, int Fs, int H,
+                       int W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

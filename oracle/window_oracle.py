@@ -1,0 +1,225 @@
+"""CPU oracle for the window-graph MixtureGTV denoiser of the older reference models.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/`` and ``bench_window.py``'s CPU-baseline leg
+may import this module, as the checker / the timed CPU baseline.  The product path
+(``irdu_amd.window_graph``) never calls it.
+
+A functional (no nn.Module) PyTorch-CPU fp32 restatement of
+REF7 = exploration/model_multiscale_mixture_GLR/lib/model_GLR_GTV_deep_v7.py
+(GLRFast :274-511, GTVFast :514-782, MixtureGTV :802-1016, FeatureExtraction :195-270,
+MultiScaleSequenceDenoiser :1019-1087), following its op sequence: replicate-padded
+neighbour stacks, reflect-padded stats stencil, materialised edge tensors [B,G,F,K,H,W],
+pad-subtract-crop transpose.  ``stats=False`` drops the stats stencils (REF1 =
+lib/model_GLR_GTV_deep_v1.py, whose GLRFast/GTVFast have none, :187-470).
+
+Parameters come as a flat dict keyed like the reference's ``state_dict``.
+Pinning: ``tests/golden/make_golden_window.py`` imports REF7 in the build container and
+records inputs / parameters / outputs (``tests/golden/window_v7*.npz``), checked against
+this module by ``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import itertools
+from typing import Dict, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as Fn
+
+Tensor = torch.Tensor
+Params = Dict[str, Tensor]
+
+
+def window_edges(connection_window) -> np.ndarray:
+    """(dy, dx) of the window's edges in itertools.product order (REF7:285-296)."""
+    cw = np.asarray(connection_window)
+    m = np.arange(cw.shape[0]) - cw.shape[0] // 2
+    delta = np.array(list(itertools.product(m, m)), dtype=np.int32)
+    return delta[cw.reshape(-1) == 1]
+
+
+def _pad(delta: np.ndarray) -> Tuple[int, int]:
+    ph, pw = np.abs(delta.min(axis=0))           # REF7:297
+    return int(ph), int(pw)
+
+
+def neighbors(x4: Tensor, delta: np.ndarray) -> Tensor:
+    """[B,C,H,W] -> [B,C,K,H,W] replicate-padded shifted views (REF7:374-415)."""
+    _, _, h, w = x4.shape
+    ph, pw = _pad(delta)
+    fr = Fn.pad(x4, (pw, pw, ph, ph), "replicate")
+    return torch.stack([fr[:, :, ph + dy:ph + dy + h, pw + dx:pw + dx + w] for dy, dx in delta], dim=-3)
+
+
+def stats_kernel(p: Params, prefix: str, n_channels: int) -> Tensor:
+    """p01 k01 + p02a k02a + p02b k02b + p03 k03, one copy per channel (REF7:300-358, :449-456)."""
+    z = torch.zeros(3, 3)
+    k01 = z.clone(); k01[1, 1] = 1.0
+    k02a = z.clone(); k02a[1, 1] = -1.0; k02a[1, 2] = 1.0
+    k02b = z.clone(); k02b[1, 1] = -1.0; k02b[2, 1] = 1.0
+    k03 = torch.tensor([[0.0, -1.0, 0.0], [-1.0, 4.0, -1.0], [0.0, -1.0, 0.0]])
+    ks = [k.expand(n_channels, 1, 3, 3) for k in (k01, k02a, k02b, k03)]
+    return (p[prefix + "stats_kernel_p01"] * ks[0] + p[prefix + "stats_kernel_p02a"] * ks[1]
+            + p[prefix + "stats_kernel_p02b"] * ks[2] + p[prefix + "stats_kernel_p03"] * ks[3])
+
+
+def stats_conv(x5: Tensor, k: Tensor) -> Tensor:
+    b, g, c, h, w = x5.shape                     # REF7:449-467 (reflect frame)
+    t = Fn.pad(x5.reshape(b * g, c, h, w), (1, 1, 1, 1), "reflect")
+    return Fn.conv2d(t, k, stride=1, padding=0, groups=c).view(b, g, c, h, w)
+
+
+def stats_conv_t(x5: Tensor, k: Tensor) -> Tensor:
+    b, g, c, h, w = x5.shape                     # REF7:469-488
+    return Fn.conv_transpose2d(x5.reshape(b * g, c, h, w), k, stride=1, padding=1, groups=c).view(b, g, c, h, w)
+
+
+def edge_weights(f5: Tensor, multiM: Tensor, delta: np.ndarray) -> Tuple[Tensor, Tensor]:
+    """REF7:418-446: normalise over F, x multiM, K similarities, softmax over edges."""
+    b, g, f, h, w = f5.shape
+    fn = Fn.normalize(f5, dim=2)
+    ft = torch.einsum("bhcHW, hc -> bhcHW", fn, multiM).reshape(b, g * f, h, w)
+    nb = neighbors(ft, delta)
+    k = len(delta)
+    sim = (ft[:, :, None] * nb).view(b, g, f, k, h, w).sum(dim=2)
+    wgt = Fn.softmax(sim, dim=2)
+    return wgt, wgt.sum(dim=2)
+
+
+def glr_apply(x5: Tensor, wgt: Tensor, k, delta: np.ndarray) -> Tensor:
+    """S^T (x - W x) S (REF7:490-511); k None = no stats stencil (REF1)."""
+    s = stats_conv(x5, k) if k is not None else x5
+    b, g, c, h, w = s.shape
+    nb = neighbors(s.reshape(b, g * c, h, w), delta).view(b, g, c, len(delta), h, w)
+    out = s - torch.einsum("bhceHW, bheHW -> bhcHW", nb, wgt)
+    return stats_conv_t(out, k) if k is not None else out
+
+
+def gtv_C(x5: Tensor, wgt: Tensor, k, delta: np.ndarray) -> Tensor:
+    s = stats_conv(x5, k) if k is not None else x5     # REF7:730-746
+    b, g, c, h, w = s.shape
+    nb = neighbors(s.reshape(b, g * c, h, w), delta).view(b, g, c, len(delta), h, w)
+    return s[:, :, :, None] * wgt[:, :, None] - nb * wgt[:, :, None]
+
+
+def gtv_Ct(e6: Tensor, wgt: Tensor, k, delta: np.ndarray) -> Tensor:
+    b, g, c, ne, h, w = e6.shape                        # REF7:748-774
+    e6 = e6 * wgt[:, :, None]
+    out = e6.sum(dim=3)
+    ph, pw = _pad(delta)
+    out = Fn.pad(out.reshape(b, g * c, h, w), (pw, pw, ph, ph), "replicate").view(b, g, c, h + 2 * ph, w + 2 * pw)
+    for i, (dy, dx) in enumerate(delta):
+        sl = (slice(None), slice(None), slice(None), slice(ph + dy, ph + dy + h), slice(pw + dx, pw + dx + w))
+        out[sl] = out[sl] - e6[:, :, :, i]
+    out = out[:, :, :, ph:ph + h, pw:pw + w]
+    return stats_conv_t(out, k) if k is not None else out
+
+
+def soft_threshold(d: Tensor, gamma: Tensor) -> Tensor:
+    gm = gamma[None, :, None, None, None, None]          # REF7:913-933
+    return torch.where(d < -gm, d + gm, 0.0) + torch.where(d > gm, d - gm, 0.0)
+
+
+def _bc(v: Tensor) -> Tensor:
+    return v[None, :, None, None, None]
+
+
+def mixture_solve(y4: Tensor, gfeat: Tensor, p: Params, n_graphs: int, n_fts: int, delta: np.ndarray,
+                  n_cgd_iters: int = 4, stats: bool = True) -> Tensor:
+    """The ADMM / CG solver of MixtureGTV.forward (REF7:936-1004; REF1:602-670) -> [B,G,Fs,H,W]."""
+    b, fs, h, w = y4.shape
+    f5 = gfeat.reshape(b, n_graphs, n_fts, h, w)
+    wG, _ = edge_weights(f5, p["GTVmodule00.multiM"], delta)
+    wL, _ = edge_weights(f5, p["GLRmodule00.multiM"], delta)
+    kG = stats_kernel(p, "GTVmodule00.", fs) if stats else None
+    kL = stats_kernel(p, "GLRmodule00.", fs) if stats else None
+    ro, mu = p["ro00"], p["muys00"]
+    al, be = p["alphaCGD"], p["betaCGD"]
+    gam = torch.exp(p["gamma00"])
+    y5 = y4[:, None]
+
+    def A(x):                                            # REF7:892-911
+        return x + glr_apply(x, wL, kL, delta) * _bc(mu) + gtv_Ct(gtv_C(x, wG, kG, delta), wG, kG, delta) * _bc(ro)
+
+    eps = gtv_C(y5, wG, kG, delta)
+    bias = torch.zeros_like(eps)
+    lhs = gtv_Ct(eps - bias, wG, kG, delta) * _bc(ro) + y5
+    x = lhs
+    upd = lhs - A(x)
+    x = x + al[0][None, :, None, None, None] * upd
+    upd = (lhs - A(x)) + be[1][None, :, None, None, None] * upd
+    x = x + al[1][None, :, None, None, None] * upd
+    cx = gtv_C(x, wG, kG, delta)
+    eps = soft_threshold(cx + bias, gam)
+    bias = bias + (gtv_C(x, wG, kG, delta) - eps)
+    lhs = gtv_Ct(eps - bias, wG, kG, delta) * _bc(ro) + y5
+    x = lhs
+    for i, kk in enumerate(range(2, n_cgd_iters)):
+        r = lhs - A(x)
+        upd = r if i == 0 else r + be[kk][None, :, None, None, None] * upd
+        x = x + al[kk][None, :, None, None, None] * upd
+    return x
+
+
+# ---- feature CNN (REF7:13-270, :785-799) ----------------------------------
+def _conv(x, p, key, **kw):
+    return Fn.conv2d(x, p[key], **kw)
+
+
+def ff_block(x: Tensor, p: Params, pre: str) -> Tensor:
+    sigma = x.var(dim=1, keepdim=True, correction=1)     # CustomLayerNorm REF7:13-26
+    n = _conv(x / torch.sqrt(sigma + 1e-5), p, pre + "norm.weighted_transform.weight", groups=x.shape[1])
+    hcat = _conv(n, p, pre + "ffn.project_in.weight")
+    hcat = _conv(hcat, p, pre + "ffn.dwconv.weight", padding=1, groups=hcat.shape[1])
+    x1, x2 = hcat.chunk(2, dim=1)
+    out = _conv(Fn.gelu(x1) * x2, p, pre + "ffn.project_out.weight")
+    s = p[pre + "skip_connect_weight_final"]
+    return s[0] * x + s[1] * out
+
+
+def _seq(x, p, pre, n):
+    for i in range(n):
+        x = ff_block(x, p, f"{pre}.{i}.")
+    return x
+
+
+def feature_extraction(img: Tensor, p: Params, pre: str, num_blocks: Sequence[int], n_ref: int) -> Tensor:
+    e1 = _seq(_conv(img, p, pre + "patch_embed.proj.weight", padding=1), p, pre + "encoder_level1", num_blocks[0])
+    lat = Fn.pixel_unshuffle(_conv(e1, p, pre + "down1_2.body.0.weight", padding=1), 2)
+    lat = _seq(lat, p, pre + "encoder_level2", num_blocks[1])
+    up = Fn.pixel_shuffle(_conv(lat, p, pre + "up2_1.body.0.weight", padding=1), 2)
+    d1 = _seq(torch.cat([up, e1], 1), p, pre + "decoder_level1", num_blocks[0])
+    d1 = _seq(d1, p, pre + "refinement", n_ref)
+    return _conv(d1, p, pre + "output.weight", padding=1)
+
+
+def dc_estimator(x: Tensor, p: Params, pre: str) -> Tensor:
+    h = _conv(x, p, pre + "project_in.weight")
+    h = _conv(h, p, pre + "dwconv.weight", padding=1, groups=h.shape[1])
+    a, b = h.chunk(2, dim=1)
+    return _conv(Fn.gelu(a) * b, p, pre + "project_out.weight")
+
+
+def mixture_gtv_v7(img: Tensor, p: Params, n_graphs: int, n_fts: int, connection_window,
+                   n_cgd_iters: int = 4) -> Tensor:
+    """MixtureGTV.forward (REF7:936-1011)."""
+    delta = window_edges(connection_window)
+    feats = feature_extraction(img, p, "patchs_features_extraction.", [4, 3, 3], 4)
+    gfeat = feats[:, :-12]
+    dc = dc_estimator(feats[:, -12:], p, "dc_estimator.")
+    y = img - dc
+    x = mixture_solve(y, gfeat, p, n_graphs, n_fts, delta, n_cgd_iters)
+    score = Fn.softmax(_conv(gfeat, p, "combination_weight.0.weight"), dim=1)
+    return torch.einsum("bgchw, bghw -> bchw", x, score) + dc
+
+
+def sub_params(p: Params, prefix: str) -> Params:
+    return {k[len(prefix):]: v for k, v in p.items() if k.startswith(prefix)}
+
+
+def sequence_denoiser_v7(img: Tensor, p: Params, n_cgd_iters: int = 4) -> Tensor:
+    """MultiScaleSequenceDenoiser.forward (REF7:1083-1087): 24 graphs x 3 fts, 5x5 diamond."""
+    cw = np.array([0, 0, 1, 0, 0, 0, 1, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0]).reshape(5, 5)
+    s = p["skip_connect_weight03"]
+    inner = mixture_gtv_v7(img, sub_params(p, "mixtureGLR_block03."), 24, 3, cw, n_cgd_iters)
+    return s[0] * img + s[1] * inner
