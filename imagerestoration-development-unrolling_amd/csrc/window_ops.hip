@@ -146,19 +146,27 @@ __device__ __forceinline__ int reflect1(int v, int n) {   // one-pixel reflect f
   return v > n - 1 ? 2 * (n - 1) - v : v;
 }
 
-template <int R, int MODE>
-__global__ __launch_bounds__(NTW) void win_solver_kernel(WinArgs a) {
+// Block = NTS threads; all Fs <= FSMAX signal channels of the graph stay in LDS together so
+// each edge weight is fetched once per position and applied to every channel.  KT = K at
+// compile time (8, 12, 24: the edge loops unroll and every weight load is issued up front;
+// 0 = runtime K).
+constexpr int NTS = 512, FSMAX = 3;
+
+template <int R, int MODE, int KT>
+__global__ __launch_bounds__(NTS) void win_solver_kernel(WinArgs a) {
   constexpr bool GLR = MODE == 0 || MODE == 3;
   constexpr int HX = R + 2, XH = TH + 2 * HX, XW = TW + 2 * HX;   // x region
   constexpr int HS = R + 1, SH = TH + 2 * HS, SW = TW + 2 * HS;   // s region
   constexpr int LH = TH + 2, LW = TW + 2;                          // l / o region (halo 1)
+  constexpr int NS = SH * SW, NL = LH * LW;
   __shared__ float xs[XH * XW];
-  __shared__ float sg[SH * SW];
-  __shared__ float sl[GLR ? SH * SW : 1];
-  __shared__ float os[LH * LW];
-  __shared__ float ls[GLR ? LH * LW : 1];
+  __shared__ float sg[FSMAX * NS];
+  __shared__ float sl[GLR ? FSMAX * NS : 1];
+  __shared__ float os[FSMAX * NL];
+  __shared__ float ls[GLR ? FSMAX * NL : 1];
 
-  const int H = a.H, W = a.W, K = a.K, G = a.G, Fs = a.Fs;
+  const int H = a.H, W = a.W, G = a.G, Fs = a.Fs;
+  const int K = KT > 0 ? KT : a.K;
   const int64_t HW = (int64_t)H * W;
   const int tile = blockIdx.x, bg = blockIdx.y;
   const int g = bg % G, b = bg / G;
@@ -185,109 +193,149 @@ __global__ __launch_bounds__(NTW) void win_solver_kernel(WinArgs a) {
   const float* wLp = has_glr ? a.wL + (int64_t)bg * K * HW : nullptr;
   const float* wGp = has_gtv ? a.wG + (int64_t)bg * K * HW : nullptr;
 
+  // ---- per channel: x region (reflect-mapped one pixel outside the frame, clamped beyond),
+  //      then s = S x on the s region (out-of-frame entries are never read)
   for (int c = 0; c < Fs; ++c) {
-    const int64_t plane = ((int64_t)bg * Fs + c) * HW;
-    const float* xp = a.x + (a.x_rep ? ((int64_t)b * Fs + c) * HW : plane);
-    if (c > 0) __syncthreads();   // previous channel's epilogue done with xs / ls / os
-    // ---- x region, reflect-mapped one pixel outside the frame, clamped beyond
-    for (int i = tid; i < XH * XW; i += NTW) {
+    const float* xp = a.x + (a.x_rep ? ((int64_t)b * Fs + c) * HW : ((int64_t)bg * Fs + c) * HW);
+    if (c > 0) __syncthreads();
+    for (int i = tid; i < XH * XW; i += NTS) {
       const int ry = i / XW, rx = i - ry * XW;
-      int gy = y0 - HX + ry, gx = x0 - HX + rx;
-      gy = clampi(reflect1(gy, H), 0, H - 1);
-      gx = clampi(reflect1(gx, W), 0, W - 1);
+      const int gy = clampi(reflect1(y0 - HX + ry, H), 0, H - 1);
+      const int gx = clampi(reflect1(x0 - HX + rx, W), 0, W - 1);
       xs[i] = xp[(int64_t)gy * W + gx];
     }
     __syncthreads();
-    // ---- s = S x at in-frame positions of the s region (others are never read)
-    for (int i = tid; i < SH * SW; i += NTW) {
+    for (int i = tid; i < NS; i += NTS) {
       const int ry = i / SW, rx = i - ry * SW;
       const int xi = (ry + 1) * XW + (rx + 1);
       const float xc = xs[xi], xu = xs[xi - XW], xl = xs[xi - 1], xr = xs[xi + 1], xd = xs[xi + XW];
       float v = kG[0] * xc;
       v += kG[1] * xu; v += kG[2] * xl; v += kG[3] * xr; v += kG[4] * xd;
-      sg[i] = v;
+      sg[c * NS + i] = v;
       if constexpr (GLR) {
         float w = kL[0] * xc;
         w += kL[1] * xu; w += kL[2] * xl; w += kL[3] * xr; w += kL[4] * xd;
-        sl[i] = w;
+        sl[c * NS + i] = w;
       }
     }
-    __syncthreads();
-    // ---- l and o on the tile + 1-pixel halo (zero outside the frame)
-    for (int i = tid; i < LH * LW; i += NTW) {
-      const int ry = i / LW, rx = i - ry * LW;
-      const int qy = y0 - 1 + ry, qx = x0 - 1 + rx;
-      float ov = 0.f, lv = 0.f;
-      if (qy >= 0 && qy < H && qx >= 0 && qx < W && has_gtv) {
-        const int64_t q = (int64_t)qy * W + qx;
-        auto sidx = [&](int gy, int gx) { return (gy - (y0 - HS)) * SW + (gx - (x0 - HS)); };
-        const float sq = sg[sidx(qy, qx)];
-        // sum_e z_e(q), z_e = w_e phi(w_e s(q) - w_e s(clamp(q + delta_e)))
-        float acc = 0.f;
-        for (int e = 0; e < K; ++e) {
-          const int ny = clampi(qy + a.d.dy[e], 0, H - 1), nx = clampi(qx + a.d.dx[e], 0, W - 1);
-          const float we = wGp[e * HW + q];
-          float t = we * sq - we * sg[sidx(ny, nx)];
-          if constexpr (MODE == 2) t = soft_phi(t, gam);
-          acc += t * we;
-        }
-        // - z_e(q - delta_e) for sources inside the frame, in edge order
-        for (int e = 0; e < K; ++e) {
-          const int py = qy - a.d.dy[e], px = qx - a.d.dx[e];
-          if (py >= 0 && py < H && px >= 0 && px < W) {
-            const float we = wGp[e * HW + (int64_t)py * W + px];
-            float t = we * sg[sidx(py, px)] - we * sq;   // its neighbour p + delta_e is q itself
+  }
+  __syncthreads();
+  // ---- l and o of every channel on the tile + 1-pixel halo (zero outside the frame)
+  for (int i = tid; i < NL; i += NTS) {
+    const int ry = i / LW, rx = i - ry * LW;
+    const int qy = y0 - 1 + ry, qx = x0 - 1 + rx;
+    const bool in = qy >= 0 && qy < H && qx >= 0 && qx < W;
+    const int64_t q = (int64_t)qy * W + qx;
+    const int sq = (qy - (y0 - HS)) * SW + (qx - (x0 - HS));
+    float ov[FSMAX] = {0.f, 0.f, 0.f}, lv[FSMAX] = {0.f, 0.f, 0.f};
+    constexpr int KE = KT > 0 ? KT : kMaxEdges;
+    if (in && has_gtv) {
+      // every weight of this position first (one batch of loads in flight), then the math:
+      // sum_e z_e(q) - sum_e [q - delta_e inside] z_e(q - delta_e), z_e = w_e phi(w_e s - w_e s(+delta_e))
+      float wf[KE], wb[KE];
+      int sn[KE], sp[KE];
+#pragma unroll
+      for (int e = 0; e < KE; ++e) {
+        if (KT == 0 && e >= K) break;
+        const int ny = clampi(qy + a.d.dy[e], 0, H - 1), nx = clampi(qx + a.d.dx[e], 0, W - 1);
+        sn[e] = (ny - (y0 - HS)) * SW + (nx - (x0 - HS));
+        const int py = qy - a.d.dy[e], px = qx - a.d.dx[e];
+        const bool pin = py >= 0 && py < H && px >= 0 && px < W;
+        const int cy = pin ? py : qy, cx = pin ? px : qx;
+        sp[e] = pin ? (cy - (y0 - HS)) * SW + (cx - (x0 - HS)) : -1;
+        wf[e] = wGp[e * HW + q];
+        wb[e] = wGp[e * HW + (int64_t)cy * W + cx];
+      }
+#pragma unroll
+      for (int c = 0; c < FSMAX; ++c) {
+        if (c < Fs) {
+          const float* sc = sg + c * NS;
+          const float sv = sc[sq];
+          float acc = 0.f;
+#pragma unroll
+          for (int e = 0; e < KE; ++e) {
+            if (KT == 0 && e >= K) break;
+            float t = wf[e] * sv - wf[e] * sc[sn[e]];
             if constexpr (MODE == 2) t = soft_phi(t, gam);
-            acc -= t * we;
+            acc += t * wf[e];
           }
-        }
-        ov = acc;
-      }
-      if (qy >= 0 && qy < H && qx >= 0 && qx < W && has_glr) {
-        {
-          const int64_t q = (int64_t)qy * W + qx;
-          auto sidx = [&](int gy, int gx) { return (gy - (y0 - HS)) * SW + (gx - (x0 - HS)); };
-          const float lq = sl[sidx(qy, qx)];
-          float wx = 0.f;
-          for (int e = 0; e < K; ++e) {
-            const int ny = clampi(qy + a.d.dy[e], 0, H - 1), nx = clampi(qx + a.d.dx[e], 0, W - 1);
-            wx += wLp[e * HW + q] * sl[sidx(ny, nx)];
+#pragma unroll
+          for (int e = 0; e < KE; ++e) {
+            if (KT == 0 && e >= K) break;
+            if (sp[e] >= 0) {
+              float t = wb[e] * sc[sp[e]] - wb[e] * sv;   // its neighbour p + delta_e is q
+              if constexpr (MODE == 2) t = soft_phi(t, gam);
+              acc -= t * wb[e];
+            }
           }
-          lv = lq - wx;
+          ov[c] = acc;
         }
       }
-      os[i] = ov;
-      if constexpr (GLR) ls[i] = lv;
     }
-    __syncthreads();
-    // ---- S^T (zero frame) and the epilogue on the tile
-    for (int i = tid; i < TH * TW; i += NTW) {
-      const int ry = i / TW, rx = i - ry * TW;
-      const int py = y0 + ry, px = x0 + rx;
-      if (py >= H || px >= W) continue;
-      const int li = (ry + 1) * LW + (rx + 1);
-      // sum_t k_t v(p - t): up tap reads p + down, left tap p + right, ...
-      float tg = kG[0] * os[li];
-      tg += kG[1] * os[li + LW]; tg += kG[2] * os[li + 1]; tg += kG[3] * os[li - 1]; tg += kG[4] * os[li - LW];
-      const int64_t p = (int64_t)py * W + px;
-      if constexpr (MODE == 0) {
-        float tl = kL[0] * ls[li];
-        tl += kL[1] * ls[li + LW]; tl += kL[2] * ls[li + 1]; tl += kL[3] * ls[li - 1]; tl += kL[4] * ls[li - LW];
-        const float xv = xs[(ry + HX) * XW + (rx + HX)];
-        const float ax = (xv + tl * mu) + tg * ro;
-        float u = a.y[plane + p] - ax;
-        if (use_beta) u = u + beta * a.u_prev[plane + p];
-        a.out[plane + p] = xv + alpha * u;
-        if (a.u_out) a.u_out[plane + p] = u;
-      } else if constexpr (MODE == 3) {
-        float tl = kL[0] * ls[li];
-        tl += kL[1] * ls[li + LW]; tl += kL[2] * ls[li + 1]; tl += kL[3] * ls[li - 1]; tl += kL[4] * ls[li - LW];
-        float v = has_glr ? tl * mu : 0.f;
-        if (has_gtv) v = has_glr ? v + tg * ro : tg * ro;
-        a.out[plane + p] = v;
-      } else {
-        a.out[plane + p] = tg * ro + a.y[((int64_t)b * Fs + c) * HW + p];
+    if constexpr (GLR) {
+      if (in && has_glr) {
+        float wl[KE];
+        int sn[KE];
+#pragma unroll
+        for (int e = 0; e < KE; ++e) {
+          if (KT == 0 && e >= K) break;
+          const int ny = clampi(qy + a.d.dy[e], 0, H - 1), nx = clampi(qx + a.d.dx[e], 0, W - 1);
+          sn[e] = (ny - (y0 - HS)) * SW + (nx - (x0 - HS));
+          wl[e] = wLp[e * HW + q];
+        }
+#pragma unroll
+        for (int c = 0; c < FSMAX; ++c) {
+          if (c < Fs) {
+            const float* sc = sl + c * NS;
+            float wx = 0.f;
+#pragma unroll
+            for (int e = 0; e < KE; ++e) {
+              if (KT == 0 && e >= K) break;
+              wx += wl[e] * sc[sn[e]];
+            }
+            lv[c] = sc[sq] - wx;
+          }
+        }
       }
+    }
+#pragma unroll
+    for (int c = 0; c < FSMAX; ++c) {
+      if (c < Fs) {
+        os[c * NL + i] = ov[c];
+        if constexpr (GLR) ls[c * NL + i] = lv[c];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- S^T (zero frame) and the epilogue on the tile, every channel
+  for (int i = tid; i < Fs * TH * TW; i += NTS) {
+    const int c = i / (TH * TW), j = i - c * (TH * TW);
+    const int ry = j / TW, rx = j - ry * TW;
+    const int py = y0 + ry, px = x0 + rx;
+    if (py >= H || px >= W) continue;
+    const int li = c * NL + (ry + 1) * LW + (rx + 1);
+    // sum_t k_t v(p - t): up tap reads p + down, left tap p + right, ...
+    float tg = kG[0] * os[li];
+    tg += kG[1] * os[li + LW]; tg += kG[2] * os[li + 1]; tg += kG[3] * os[li - 1]; tg += kG[4] * os[li - LW];
+    const int64_t plane = ((int64_t)bg * Fs + c) * HW;
+    const int64_t p = (int64_t)py * W + px;
+    if constexpr (MODE == 0) {
+      float tl = kL[0] * ls[li];
+      tl += kL[1] * ls[li + LW]; tl += kL[2] * ls[li + 1]; tl += kL[3] * ls[li - 1]; tl += kL[4] * ls[li - LW];
+      const float xv = a.x[plane + p];
+      const float ax = (xv + tl * mu) + tg * ro;
+      float u = a.y[plane + p] - ax;
+      if (use_beta) u = u + beta * a.u_prev[plane + p];
+      a.out[plane + p] = xv + alpha * u;
+      if (a.u_out) a.u_out[plane + p] = u;
+    } else if constexpr (MODE == 3) {
+      float tl = kL[0] * ls[li];
+      tl += kL[1] * ls[li + LW]; tl += kL[2] * ls[li + 1]; tl += kL[3] * ls[li - 1]; tl += kL[4] * ls[li - LW];
+      float v = has_glr ? tl * mu : 0.f;
+      if (has_gtv) v = has_glr ? v + tg * ro : tg * ro;
+      a.out[plane + p] = v;
+    } else {
+      a.out[plane + p] = tg * ro + a.y[((int64_t)b * Fs + c) * HW + p];
     }
   }
 }
@@ -369,6 +417,7 @@ grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, c
   GRR_REQUIRE(mode != 2 || log_gamma, GRR_ERR_INVALID_ARG, "grr_win_solver: prox needs log_gamma");
   GRR_REQUIRE(!(mode == 0 && x_rep), GRR_ERR_INVALID_ARG, "grr_win_solver: the CG step needs a per-graph x");
   GRR_REQUIRE(H >= 2 && W >= 2, GRR_ERR_SHAPE, "grr_win_solver: reflect padding needs H, W >= 2");
+  GRR_REQUIRE(Fs <= FSMAX, GRR_ERR_UNSUPPORTED, "grr_win_solver: at most %d signal channels (got %d)", FSMAX, Fs);
   GRR_REQUIRE((int64_t)B * G <= 65535 && (int64_t)H * W * K < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_win_solver: grid too large");
   WinArgs a{};
@@ -383,14 +432,20 @@ grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, c
   const int tiles = a.tiles_x * ((H + TH - 1) / TH);
   const dim3 grid(tiles, B * G);
   hipStream_t s = (hipStream_t)stream;
-#define WIN_LAUNCH(R_, M_) hipLaunchKernelGGL((win_solver_kernel<R_, M_>), grid, dim3(NTW), 0, s, a)
+#define WIN_LAUNCH(R_, M_, K_) hipLaunchKernelGGL((win_solver_kernel<R_, M_, K_>), grid, dim3(NTS), 0, s, a)
+#define WIN_MODES(R_, K_)                                  \
+  do {                                                     \
+    if (mode == 0) WIN_LAUNCH(R_, 0, K_);                  \
+    else if (mode == 1) WIN_LAUNCH(R_, 1, K_);             \
+    else if (mode == 2) WIN_LAUNCH(R_, 2, K_);             \
+    else WIN_LAUNCH(R_, 3, K_);                            \
+  } while (0)
   if (reach <= 1) {
-    if (mode == 0) WIN_LAUNCH(1, 0); else if (mode == 1) WIN_LAUNCH(1, 1); else if (mode == 2) WIN_LAUNCH(1, 2);
-    else WIN_LAUNCH(1, 3);
+    if (K == 8) WIN_MODES(1, 8); else WIN_MODES(1, 0);
   } else {
-    if (mode == 0) WIN_LAUNCH(2, 0); else if (mode == 1) WIN_LAUNCH(2, 1); else if (mode == 2) WIN_LAUNCH(2, 2);
-    else WIN_LAUNCH(2, 3);
+    if (K == 12) WIN_MODES(2, 12); else if (K == 24) WIN_MODES(2, 24); else WIN_MODES(2, 0);
   }
+#undef WIN_MODES
 #undef WIN_LAUNCH
   return launch_status("grr_win_solver");
 }
