@@ -223,3 +223,51 @@ def sequence_denoiser_v7(img: Tensor, p: Params, n_cgd_iters: int = 4) -> Tensor
     s = p["skip_connect_weight03"]
     inner = mixture_gtv_v7(img, sub_params(p, "mixtureGLR_block03."), 24, 3, cw, n_cgd_iters)
     return s[0] * img + s[1] * inner
+
+
+# ---- REF1 = lib/model_GLR_GTV_deep_v1.py (no stats stencils, 4-level U-Net, sharpening) ----
+def feature_extraction_v1(img: Tensor, p: Params, pre: str, num_blocks: Sequence[int], n_ref: int) -> Tensor:
+    """REF1:108-184; returns the first output (the graph features)."""
+    e1 = _seq(_conv(img, p, pre + "patch_embed.proj.weight", padding=1), p, pre + "encoder_level1", num_blocks[0])
+    e2 = _seq(Fn.pixel_unshuffle(_conv(e1, p, pre + "down1_2.body.0.weight", padding=1), 2), p,
+              pre + "encoder_level2", num_blocks[1])
+    e3 = _seq(Fn.pixel_unshuffle(_conv(e2, p, pre + "down2_3.body.0.weight", padding=1), 2), p,
+              pre + "encoder_level3", num_blocks[2])
+    lat = _seq(Fn.pixel_unshuffle(_conv(e3, p, pre + "down3_4.body.0.weight", padding=1), 2), p,
+               pre + "latent", num_blocks[3])
+    d3 = torch.cat([Fn.pixel_shuffle(_conv(lat, p, pre + "up4_3.body.0.weight", padding=1), 2), e3], 1)
+    d3 = _seq(_conv(d3, p, pre + "reduce_chan_level3.weight"), p, pre + "decoder_level3", num_blocks[2])
+    d2 = torch.cat([Fn.pixel_shuffle(_conv(d3, p, pre + "up3_2.body.0.weight", padding=1), 2), e2], 1)
+    d2 = _seq(_conv(d2, p, pre + "reduce_chan_level2.weight"), p, pre + "decoder_level2", num_blocks[1])
+    d1 = torch.cat([Fn.pixel_shuffle(_conv(d2, p, pre + "up2_1.body.0.weight", padding=1), 2), e1], 1)
+    d1 = _seq(_seq(d1, p, pre + "decoder_level1", num_blocks[0]), p, pre + "refinement", n_ref)
+    return _conv(d1, p, pre + "output.weight", padding=1)
+
+
+def mixture_gtv_v1(img: Tensor, p: Params, n_graphs: int, n_fts: int, connection_window,
+                   n_cgd_iters: int = 6) -> Tensor:
+    """MixtureGTV.forward of REF1 (:602-676)."""
+    delta = window_edges(connection_window)
+    feats = feature_extraction_v1(img, p, "patchs_features_extraction.", [2, 2, 2, 2], 4)
+    x = mixture_solve(img, feats, p, n_graphs, n_fts, delta, n_cgd_iters, stats=False)
+    score = Fn.softmax(_conv(feats, p, "combination_weight.0.weight"), dim=1)
+    return torch.einsum("bgchw, bghw -> bchw", x, score)
+
+
+def sharpening(x: Tensor, p: Params, pre: str) -> Tensor:
+    """SharpeningBlock (REF1:768-787)."""
+    out = dc_estimator(x, p, pre)
+    s = p[pre + "skip_connect_weight"]
+    return s[0] * x + s[1] * out
+
+
+def sequence_denoiser_v1(img: Tensor, p: Params) -> Tensor:
+    """MultiScaleSequenceDenoiser.forward (REF1:869-884)."""
+    ring3 = np.array([1, 1, 1, 1, 0, 1, 1, 1, 1]).reshape(3, 3)
+    full5 = np.array([1] * 12 + [0] + [1] * 12).reshape(5, 5)
+    x = img
+    for i, (f, cw) in enumerate(((6, ring3), (6, ring3), (12, full5)), start=1):
+        s = p[f"skip_connect_weight0{i}"]
+        x = s[0] * x + s[1] * mixture_gtv_v1(x, sub_params(p, f"mixtureGLR_block0{i}."), 4, f, cw)
+        x = sharpening(x, p, f"sharp0{i}.")
+    return x

@@ -11,6 +11,8 @@ scalars away from their near-zero inits so every term is exercised, and stores i
                       3x3 ring (K=8), the 5x5 diamond (K=12) and the full 5x5 window (K=24)
   window_v7.npz       MixtureGTV forward (REF7:802-1016; small CNN width) + its solver input
                       (features, y~) and the solver's graph-mixed output
+  window_v1.npz       REF1 = lib/model_GLR_GTV_deep_v1.py MixtureGTV blocks (:472-676: 3x3 ring and full
+                      5x5 window, no stats stencils, 6 CG stages) + SharpeningBlock (:768-787) forwards
 """
 from __future__ import annotations
 
@@ -108,6 +110,51 @@ def make_mixture(v7, gen):
     np.savez_compressed(os.path.join(HERE, "window_v7.npz"), **out)
 
 
+def _import_v1(ref_root: str):
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, os.path.join(ref_root, "exploration", "model_multiscale_mixture_GLR", "lib"))
+    import model_GLR_GTV_deep_v1 as v1  # noqa: E402
+    return v1
+
+
+def make_blocks_v1(v1, gen):
+    """Two REF1 MixtureGTV blocks (3x3 ring K=8, full 5x5 K=24; 6 CG stages) + a SharpeningBlock at small
+    widths (the full MultiScaleSequenceDenoiser's state_dict is 30 MB; its composition is checked
+    against the oracle, which these blocks pin)."""
+    torch.manual_seed(2201)
+    out = {}
+    for name, g, f, cw in (("ring3", 2, 3, WINDOWS["ring3"]), ("full5", 2, 2, WINDOWS["full5"])):
+        mix = v1.MixtureGTV(nchannels_in=3, n_graphs=g, n_node_fts=f, connection_window=cw, n_cgd_iters=6,
+                            alpha_init=0.5, beta_init=0.1, muy_init=torch.tensor([[0.1], [0.0], [0.0], [0.0]]),
+                            ro_init=torch.tensor([[0.1], [0.0], [0.0], [0.0]]),
+                            gamma_init=torch.tensor([[0.001], [0.0], [0.0], [0.0]]), device="cpu")
+        with torch.no_grad():
+            mix.alphaCGD.copy_(0.2 + 0.6 * torch.rand(mix.alphaCGD.shape, generator=gen))
+            mix.betaCGD.copy_(0.05 + 0.35 * torch.rand(mix.betaCGD.shape, generator=gen))
+            mix.muys00.copy_(0.1 + 0.5 * torch.rand(mix.muys00.shape, generator=gen))
+            mix.ro00.copy_(0.1 + 0.5 * torch.rand(mix.ro00.shape, generator=gen))
+            mix.gamma00.copy_(torch.log(0.002 + 0.01 * torch.rand(mix.gamma00.shape, generator=gen)))
+            for mod in (mix.GLRmodule00, mix.GTVmodule00):
+                mod.multiM.copy_(0.5 + torch.rand(mod.multiM.shape, generator=gen))
+        clean = torch.rand((2, 3, 24, 40), generator=gen)
+        noisy = clean + torch.randn(clean.shape, generator=gen) * (25.0 / 255.0)
+        with torch.no_grad():
+            out[f"{name}/in"] = _np(noisy)
+            out[f"{name}/out"] = _np(mix(noisy))
+        for k, v in mix.state_dict().items():
+            out[f"{name}/p/{k}"] = _np(v)
+        out[f"{name}/meta/n_state_keys"] = np.array(len(mix.state_dict()))
+    sharp = v1.SharpeningBlock(3, 3, 24)
+    with torch.no_grad():
+        sharp.skip_connect_weight.copy_(torch.tensor([0.3, 0.8]))
+        x = torch.rand((1, 3, 16, 20), generator=gen)
+        out["sharp/in"] = _np(x)
+        out["sharp/out"] = _np(sharp(x))
+    for k, v in sharp.state_dict().items():
+        out["sharp/p/" + k] = _np(v)
+    np.savez_compressed(os.path.join(HERE, "window_v1.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -116,7 +163,8 @@ def main():
     gen = torch.Generator().manual_seed(2207)
     make_ops(v7, gen)
     make_mixture(v7, gen)
-    for fn in ("window_ops_v7.npz", "window_v7.npz"):
+    make_blocks_v1(_import_v1(args.ref), torch.Generator().manual_seed(2201))
+    for fn in ("window_ops_v7.npz", "window_v7.npz", "window_v1.npz"):
         print(fn, os.path.getsize(os.path.join(HERE, fn)))
 
 

@@ -156,3 +156,39 @@ def test_window_grad_mode_raises(wg):
     out = m(torch.from_numpy(g["in/noisy"]).to(DEV))
     with pytest.raises(NotImplementedError):
         out.sum().backward()
+
+
+V1_WINDOWS = {"ring3": (2, 3, np.array([1, 1, 1, 1, 0, 1, 1, 1, 1]).reshape(3, 3)),
+              "full5": (2, 2, np.array([1] * 12 + [0] + [1] * 12).reshape(5, 5))}
+
+
+@pytest.mark.parametrize("name", sorted(V1_WINDOWS))
+def test_window_v1_block_vs_reference_golden(wg, name):
+    from irdu_amd import window_graph_v1 as W1
+    d = load_golden("window_v1.npz")
+    g, f, cw = V1_WINDOWS[name]
+    m = W1.MixtureGTV(3, g, f, cw, 6, 0.5, 0.1, torch.tensor([[0.1]]), torch.tensor([[0.1]]), torch.tensor([[0.001]]))
+    pre = f"{name}/p/"
+    m.load_state_dict({k[len(pre):]: torch.from_numpy(d[k].copy()) for k in d.files if k.startswith(pre)})
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        out = m(torch.from_numpy(d[f"{name}/in"]).to(DEV))
+    assert rel_err(out, d[f"{name}/out"]) <= RTOL
+
+
+def test_window_v1_sequence_denoiser_vs_oracle(wg):
+    """REF1 MultiScaleSequenceDenoiser (three blocks: K=8, K=8, K=24; 6 CG stages) end to end."""
+    from irdu_amd import window_graph_v1 as W1
+    torch.manual_seed(2201)
+    model = W1.MultiScaleSequenceDenoiser()
+    with torch.no_grad():
+        for i in (1, 2, 3):
+            mix = getattr(model, f"mixtureGLR_block0{i}")
+            mix.muys00.fill_(0.3); mix.ro00.fill_(0.2); mix.gamma00.fill_(float(np.log(0.005)))
+    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    img = torch.rand((2, 3, 32, 40))
+    ref = O.sequence_denoiser_v1(img, p)
+    model = model.to(DEV).eval()
+    with torch.no_grad():
+        out = model(img.to(DEV))
+    assert rel_err(out, ref) <= RTOL
