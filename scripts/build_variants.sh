@@ -7,12 +7,16 @@ mkdir -p exp
 H=/opt/rocm/bin/hipcc
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I include"
 S=imagerestoration-development-unrolling_amd/csrc
+SRCS="graph_ops feature_ops lnb_ops graph_bwd lnb_bwd window_ops"
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
-  $H $F $defs -c $S/graph_ops.hip -o exp/g_$name.o &
-  $H $F $defs -c $S/feature_ops.hip -o exp/f_$name.o &
-  $H $F -fno-slp-vectorize $defs -c $S/lnb_ops.hip -o exp/l_$name.o &
+  objs=""
+  for src in $SRCS; do
+    extra=""; [ "$src" = lnb_ops ] && extra=-fno-slp-vectorize
+    $H $F $extra $defs -c $S/$src.hip -o exp/${src}_$name.o &
+    objs="$objs exp/${src}_$name.o"
+  done
   wait
-  $H --offload-arch=gfx950 -shared -fPIC -o exp/libgrr_$name.so exp/g_$name.o exp/f_$name.o exp/l_$name.o
-  rm -f exp/g_$name.o exp/f_$name.o exp/l_$name.o
+  $H --offload-arch=gfx950 -shared -fPIC -o exp/libgrr_$name.so $objs
+  rm -f $objs
 done
