@@ -151,15 +151,14 @@ __device__ __forceinline__ int reflect1(int v, int n) {   // one-pixel reflect f
 // compile time (8, 12, 24: the edge loops unroll and every weight load is issued up front;
 // 0 = runtime K).
 constexpr int NTS = 512, FSMAX = 3;
+static_assert(FSMAX * TH * TW % NTS == 0, "epilogue slots");
 
 template <int R, int MODE, int KT>
-__global__ __launch_bounds__(NTS) void win_solver_kernel(WinArgs a) {
+__global__ __launch_bounds__(NTS, KT == 24 ? 2 : 4) void win_solver_kernel(WinArgs a) {
   constexpr bool GLR = MODE == 0 || MODE == 3;
-  constexpr int HX = R + 2, XH = TH + 2 * HX, XW = TW + 2 * HX;   // x region
   constexpr int HS = R + 1, SH = TH + 2 * HS, SW = TW + 2 * HS;   // s region
   constexpr int LH = TH + 2, LW = TW + 2;                          // l / o region (halo 1)
   constexpr int NS = SH * SW, NL = LH * LW;
-  __shared__ float xs[XH * XW];
   __shared__ float sg[FSMAX * NS];
   __shared__ float sl[GLR ? FSMAX * NS : 1];
   __shared__ float os[FSMAX * NL];
@@ -193,29 +192,55 @@ __global__ __launch_bounds__(NTS) void win_solver_kernel(WinArgs a) {
   const float* wLp = has_glr ? a.wL + (int64_t)bg * K * HW : nullptr;
   const float* wGp = has_gtv ? a.wG + (int64_t)bg * K * HW : nullptr;
 
-  // ---- per channel: x region (reflect-mapped one pixel outside the frame, clamped beyond),
-  //      then s = S x on the s region (out-of-frame entries are never read)
-  for (int c = 0; c < Fs; ++c) {
-    const float* xp = a.x + (a.x_rep ? ((int64_t)b * Fs + c) * HW : ((int64_t)bg * Fs + c) * HW);
-    if (c > 0) __syncthreads();
-    for (int i = tid; i < XH * XW; i += NTS) {
-      const int ry = i / XW, rx = i - ry * XW;
-      const int gy = clampi(reflect1(y0 - HX + ry, H), 0, H - 1);
-      const int gx = clampi(reflect1(x0 - HX + rx, W), 0, W - 1);
-      xs[i] = xp[(int64_t)gy * W + gx];
+  // ---- epilogue operands of this thread's outputs, loaded now so their latency hides
+  //      behind the s / l / o phases
+  constexpr int EPT = FSMAX * TH * TW / NTS;
+  float ex[EPT], eb[EPT], eu[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int i = tid + k * NTS;
+    const int c = i / (TH * TW), j = i - c * (TH * TW);
+    const int py = y0 + j / TW, px = x0 + (j % TW);
+    const bool ok = c < Fs && py < H && px < W;
+    const int64_t off = ok ? ((int64_t)bg * Fs + c) * HW + (int64_t)py * W + px : 0;
+    ex[k] = eb[k] = eu[k] = 0.f;
+    if constexpr (MODE == 0) {
+      if (ok) {
+        ex[k] = a.x[off];
+        eb[k] = a.y[off];
+        if (use_beta) eu[k] = a.u_prev[off];
+      }
+    } else if constexpr (MODE == 1 || MODE == 2) {
+      if (ok) eb[k] = a.y[((int64_t)b * Fs + c) * HW + (int64_t)py * W + px];
     }
-    __syncthreads();
-    for (int i = tid; i < NS; i += NTS) {
-      const int ry = i / SW, rx = i - ry * SW;
-      const int xi = (ry + 1) * XW + (rx + 1);
-      const float xc = xs[xi], xu = xs[xi - XW], xl = xs[xi - 1], xr = xs[xi + 1], xd = xs[xi + XW];
-      float v = kG[0] * xc;
-      v += kG[1] * xu; v += kG[2] * xl; v += kG[3] * xr; v += kG[4] * xd;
-      sg[c * NS + i] = v;
-      if constexpr (GLR) {
-        float w = kL[0] * xc;
-        w += kL[1] * xu; w += kL[2] * xl; w += kL[3] * xr; w += kL[4] * xd;
-        sl[c * NS + i] = w;
+  }
+  // ---- s = S x of every channel on the s region, straight from global memory (the five
+  //      taps of all channels in flight together; reflect frame; out-of-frame s is never read)
+  for (int i = tid; i < NS; i += NTS) {
+    const int ry = i / SW, rx = i - ry * SW;
+    const int gy = y0 - HS + ry, gx = x0 - HS + rx;
+    const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const int cy = clampi(gy, 0, H - 1), cx = clampi(gx, 0, W - 1);
+    const int ru = reflect1(cy - 1, H), rd = reflect1(cy + 1, H), rl = reflect1(cx - 1, W), rr = reflect1(cx + 1, W);
+    const int oc = cy * W + cx, ou = ru * W + cx, od = rd * W + cx, ol = cy * W + rl, orr = cy * W + rr;
+    float xv[FSMAX][5];
+#pragma unroll
+    for (int c = 0; c < FSMAX; ++c) {
+      const float* xp = a.x + (a.x_rep ? ((int64_t)b * Fs + min(c, Fs - 1)) * HW
+                                       : ((int64_t)bg * Fs + min(c, Fs - 1)) * HW);
+      xv[c][0] = xp[oc]; xv[c][1] = xp[ou]; xv[c][2] = xp[ol]; xv[c][3] = xp[orr]; xv[c][4] = xp[od];
+    }
+#pragma unroll
+    for (int c = 0; c < FSMAX; ++c) {
+      if (c < Fs) {
+        float v = kG[0] * xv[c][0];
+        v += kG[1] * xv[c][1]; v += kG[2] * xv[c][2]; v += kG[3] * xv[c][3]; v += kG[4] * xv[c][4];
+        sg[c * NS + i] = in ? v : 0.f;
+        if constexpr (GLR) {
+          float w = kL[0] * xv[c][0];
+          w += kL[1] * xv[c][1]; w += kL[2] * xv[c][2]; w += kL[3] * xv[c][3]; w += kL[4] * xv[c][4];
+          sl[c * NS + i] = in ? w : 0.f;
+        }
       }
     }
   }
@@ -308,11 +333,13 @@ __global__ __launch_bounds__(NTS) void win_solver_kernel(WinArgs a) {
   }
   __syncthreads();
   // ---- S^T (zero frame) and the epilogue on the tile, every channel
-  for (int i = tid; i < Fs * TH * TW; i += NTS) {
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int i = tid + k * NTS;
     const int c = i / (TH * TW), j = i - c * (TH * TW);
     const int ry = j / TW, rx = j - ry * TW;
     const int py = y0 + ry, px = x0 + rx;
-    if (py >= H || px >= W) continue;
+    if (c >= Fs || py >= H || px >= W) continue;
     const int li = c * NL + (ry + 1) * LW + (rx + 1);
     // sum_t k_t v(p - t): up tap reads p + down, left tap p + right, ...
     float tg = kG[0] * os[li];
@@ -322,10 +349,10 @@ __global__ __launch_bounds__(NTS) void win_solver_kernel(WinArgs a) {
     if constexpr (MODE == 0) {
       float tl = kL[0] * ls[li];
       tl += kL[1] * ls[li + LW]; tl += kL[2] * ls[li + 1]; tl += kL[3] * ls[li - 1]; tl += kL[4] * ls[li - LW];
-      const float xv = a.x[plane + p];
+      const float xv = ex[k];
       const float ax = (xv + tl * mu) + tg * ro;
-      float u = a.y[plane + p] - ax;
-      if (use_beta) u = u + beta * a.u_prev[plane + p];
+      float u = eb[k] - ax;
+      if (use_beta) u = u + beta * eu[k];
       a.out[plane + p] = xv + alpha * u;
       if (a.u_out) a.u_out[plane + p] = u;
     } else if constexpr (MODE == 3) {
@@ -335,7 +362,7 @@ __global__ __launch_bounds__(NTS) void win_solver_kernel(WinArgs a) {
       if (has_gtv) v = has_glr ? v + tg * ro : tg * ro;
       a.out[plane + p] = v;
     } else {
-      a.out[plane + p] = tg * ro + a.y[((int64_t)b * Fs + c) * HW + p];
+      a.out[plane + p] = tg * ro + eb[k];
     }
   }
 }
