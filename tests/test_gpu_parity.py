@@ -341,6 +341,38 @@ def test_msgf_ten_stages_vs_oracle(irdu, variant, case):
     assert abs(O.psnr_ubyte(got.cpu(), clean) - O.psnr_ubyte(ref, clean)) <= 0.01
 
 
+def test_c3_full_patch_sigma50_vs_oracle(irdu):
+    """Config C3's per-patch workload at full size: one 256x256 RGB patch, sigma = 50, G = 32,
+    S = 10 (the oracle finishes in seconds for one patch)."""
+    torch.manual_seed(2250)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=32, n_cgd_iters=10)
+    perturb_mixture(m.localfilter, 50)
+    clean = torch.rand(1, 3, 256, 256)
+    noisy = clean + torch.randn(1, 3, 256, 256) * (50.0 / 255.0)
+    ref = O.multiscale_graph_filter(noisy, sd_cpu(m), 32)
+    with torch.no_grad():
+        got = m.to(DEV)(noisy.to(DEV))
+    assert_close(got, ref)
+    assert abs(O.psnr_ubyte(got.cpu(), clean) - O.psnr_ubyte(ref, clean)) <= 0.01
+
+
+def test_full_batch_is_patch_independent(irdu):
+    """Size-independent property at the bench's full shape (64 x 256x256, G = 32, S = 10): every
+    patch of the batch filters exactly as it does alone, which is what batch sharding over GPUs
+    relies on (no collective in the data path).  Bit-exact: no kernel mixes batch items."""
+    torch.manual_seed(2251)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=32, n_cgd_iters=10)
+    perturb_mixture(m.localfilter, 51)
+    m = m.to(DEV)
+    noisy = (torch.rand(64, 3, 256, 256) + torch.randn(64, 3, 256, 256) * (25.0 / 255.0)).to(DEV)
+    with torch.no_grad():
+        full = m(noisy)
+        for i in (0, 17, 63):
+            assert torch.equal(m(noisy[i:i + 1].contiguous())[0], full[i])
+        assert torch.equal(m(noisy[32:40].contiguous()), full[32:40])
+    assert torch.isfinite(full).all()
+
+
 def test_lowpass_block_ten_stages_vs_oracle(irdu):
     torch.manual_seed(7)
     blk = irdu.LocalLowpassFilteringBlock(dim=48, nsubnets=1, ngraphs=8, n_cgd_iters=10)
