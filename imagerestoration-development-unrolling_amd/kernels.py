@@ -584,6 +584,8 @@ def win_edge_weights(feat: Tensor, channel_offset: int, n_graphs: int, n_fts: in
     if channel_offset + n_graphs * n_fts > ctot:
         raise ValueError("win_edge_weights: channel slab out of range")
     delta, k = _delta_arg(edge_delta)
+    if multiM.numel() != n_graphs * n_fts:
+        raise ValueError(f"win_edge_weights: multiM has {multiM.numel()} entries, expected {n_graphs * n_fts}")
     wt = torch.empty((b, n_graphs, k, h, w), dtype=torch.float32, device=dev)
     deg = torch.empty((b, n_graphs, h, w), dtype=torch.float32, device=dev) if with_degree else None
     base = feat.data_ptr() + channel_offset * h * w * feat.element_size()
@@ -604,6 +606,16 @@ def win_taps(p01: Tensor, p02a: Tensor, p02b: Tensor, p03: Tensor) -> Tensor:
 IDENTITY_TAPS = (1.0, 0.0, 0.0, 0.0, 0.0)
 
 
+def _check_win_scalars(n_graphs: int, **ts) -> None:
+    """Host-side size checks of the per-graph scalars / stencil taps the window kernels index."""
+    for name, t in ts.items():
+        if t is None:
+            continue
+        need = 5 if name.startswith("taps") else n_graphs
+        if t.numel() < need:
+            raise ValueError(f"window graph: {name} has {t.numel()} entries, needs {need}")
+
+
 def win_solver(mode: int, x: Tensor, y: Tensor, wG: Tensor, tapsG: Tensor, ro: Tensor, edge_delta, n_graphs: int,
                n_sig: int, *, wL: Optional[Tensor] = None, tapsL: Optional[Tensor] = None, mu: Optional[Tensor] = None,
                log_gamma: Optional[Tensor] = None, alpha: Optional[Tensor] = None, beta: Optional[Tensor] = None,
@@ -621,7 +633,10 @@ def win_solver(mode: int, x: Tensor, y: Tensor, wG: Tensor, tapsG: Tensor, ro: T
         raise ValueError(f"win_solver: x has shape {tuple(x.shape)}")
     if tuple(wG.shape) != (b, n_graphs, k, h, w):
         raise ValueError(f"win_solver: wG has shape {tuple(wG.shape)}, expected {(b, n_graphs, k, h, w)}")
+    _check_win_scalars(n_graphs, tapsG=tapsG, tapsL=tapsL, ro=ro, mu=mu, log_gamma=log_gamma, alpha=alpha, beta=beta)
     out = torch.empty((b, n_graphs, n_sig, h, w), dtype=torch.float32, device=dev)
+    if u_prev is not None and tuple(u_prev.shape) != tuple(out.shape):
+        raise ValueError(f"win_solver: u_prev has shape {tuple(u_prev.shape)}, expected {tuple(out.shape)}")
     u_out = torch.empty_like(out) if (mode == 0 and want_u) else None
     planes = b * n_graphs * n_sig
     if mode == 0:
@@ -663,6 +678,9 @@ def win_apply(x: Tensor, edge_delta, n_graphs: int, n_sig: int, *, wL: Optional[
     for t in (wL, wG):
         if t is not None and tuple(t.shape) != (b, n_graphs, k, h, w):
             raise ValueError(f"win_apply: edge weights of shape {tuple(t.shape)}, expected {(b, n_graphs, k, h, w)}")
+    if g != n_graphs or c > 3:
+        raise ValueError(f"win_apply: x has shape {tuple(x.shape)} (graphs {n_graphs}, at most 3 signal channels)")
+    _check_win_scalars(n_graphs, tapsG=tapsG, tapsL=tapsL, ro=ro, mu=mu)
     out = torch.empty_like(x)
     nbytes = 4 * h * w * (2 * x.numel() // (h * w) + k * b * n_graphs * (int(wL is not None) + int(wG is not None)))
     _launch("win_solver", nbytes, "grr_win_solver", 3, x.data_ptr(), 0, None, None, _ptr(wL), _ptr(wG), _ptr(tapsL),

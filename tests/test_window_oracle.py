@@ -108,3 +108,16 @@ def test_window_v1_state_dict_keys_match_reference():
     W1.SharpeningBlock(3, 3, 24).load_state_dict(_v1_params(d, "sharp/p/"), strict=True)
     seq = W1.MultiScaleSequenceDenoiser()
     assert sum(1 for k in seq.state_dict() if k.endswith("alphaCGD")) == 3
+
+
+def test_window_host_checks_reject_bad_shapes_without_gpu():
+    """Shape errors surface on the host before any launch (CPU tensors would also be refused)."""
+    from irdu_amd import kernels as K
+    from irdu_amd import window_graph as WG
+    delta = WG.window_edges(WG.CONNECTION_FLAGS_3x3)
+    assert delta.shape == (8, 2)
+    with pytest.raises(ValueError):
+        K._check_win_scalars(4, ro=torch.zeros(3))
+    with pytest.raises(ValueError):
+        K._check_win_scalars(4, tapsG=torch.zeros(4))
+    K._check_win_scalars(4, ro=torch.zeros(4), tapsG=torch.zeros(5), beta=None)
