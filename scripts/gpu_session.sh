@@ -33,13 +33,13 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = prof ]; then
   step rocprof 900 0 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+    python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary
 fi
 if [ "$MODE" = traffic ]; then
   step pmc_fetch 600 0 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+    python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary
   step pmc_write 600 0 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+    python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary
   python scripts/collect_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --out "$OUT/traffic_system_step.json"
 fi
 echo "session done"
