@@ -224,21 +224,53 @@ static grr_status launch_gemm(GemmArgs a, int B, hipStream_t s, const char* name
   return launch_status(name);
 }
 
-// CustomLayerNorm statistics: sd[b,p] = 1/sqrt(var_c x[b,c,p] + 1e-5), unbiased (REF:919-922)
-__global__ void ln_stats_kernel(const float* __restrict__ x, float* __restrict__ sd, int B, int C, int64_t P) {
-  const int64_t n = (int64_t)B * P;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = i / P, p = i - b * P;
-    const float* xp = x + b * C * P + p;
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s += xp[(int64_t)c * P];
-    const float mean = s / (float)C;
+// CustomLayerNorm statistics: sd[b,p] = 1/sqrt(var_c x[b,c,p] + 1e-5), unbiased (REF:919-922).
+// One workgroup = 64 consecutive pixels x LN_G channel groups (one wave each, channels
+// c = grp, grp + LN_G, ...; 256-B coalesced row loads, 4 independent accumulators per lane);
+// two passes (mean, then squared deviations) as the reference's var, partials via LDS.
+constexpr int LN_G = 4;
+__global__ __launch_bounds__(64 * LN_G) void ln_stats_kernel(const float* __restrict__ x, float* __restrict__ sd,
+                                                             int B, int C, int64_t P) {
+  __shared__ float part[LN_G][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t tiles = (P + 63) / 64;
+  const int64_t b = blockIdx.x / tiles, p = (blockIdx.x - b * tiles) * 64 + lane;
+  const bool ok = p < P;
+  const float* xp = x + b * C * P + (ok ? p : 0);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int c = grp;
+  for (; c + 3 * LN_G < C; c += 4 * LN_G) {
+    a0 += xp[(int64_t)c * P];
+    a1 += xp[(int64_t)(c + LN_G) * P];
+    a2 += xp[(int64_t)(c + 2 * LN_G) * P];
+    a3 += xp[(int64_t)(c + 3 * LN_G) * P];
+  }
+  for (; c < C; c += LN_G) a0 += xp[(int64_t)c * P];
+  part[grp][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int g = 0; g < LN_G; ++g) s += part[g][lane];
+  const float mean = s / (float)C;
+  __syncthreads();
+  a0 = a1 = a2 = a3 = 0.f;
+  c = grp;
+  for (; c + 3 * LN_G < C; c += 4 * LN_G) {
+    const float d0 = xp[(int64_t)c * P] - mean, d1 = xp[(int64_t)(c + LN_G) * P] - mean;
+    const float d2 = xp[(int64_t)(c + 2 * LN_G) * P] - mean, d3 = xp[(int64_t)(c + 3 * LN_G) * P] - mean;
+    a0 += d0 * d0; a1 += d1 * d1; a2 += d2 * d2; a3 += d3 * d3;
+  }
+  for (; c < C; c += LN_G) {
+    const float d = xp[(int64_t)c * P] - mean;
+    a0 += d * d;
+  }
+  part[grp][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && ok) {
     float q = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const float d = xp[(int64_t)c * P] - mean;
-      q += d * d;
-    }
-    sd[i] = 1.0f / sqrtf(q / (float)(C - 1) + 1e-5f);
+#pragma unroll
+    for (int g = 0; g < LN_G; ++g) q += part[g][lane];
+    sd[b * P + p] = 1.0f / sqrtf(q / (float)(C - 1) + 1e-5f);
   }
 }
 
@@ -623,8 +655,9 @@ static grr_status lnb_forward_fp32(const float* x, const float* ln_w, const floa
   float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;
   float* gbuf = hbuf + ((int64_t)B * 2 * hid * P + 63) / 64 * 64;
   const int64_t n = (int64_t)B * P;
-  hipLaunchKernelGGL(ln_stats_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1 << 16)), dim3(256), 0, s,
-                     x, sd, B, C, P);
+  GRR_REQUIRE((int64_t)B * ((P + 63) / 64) < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+  hipLaunchKernelGGL(ln_stats_kernel, dim3((unsigned)((int64_t)B * ((P + 63) / 64))), dim3(64 * LN_G), 0, s, x, sd, B,
+                     C, P);
   grr_status st = launch_status("grr_lnb_forward/ln_stats");
   if (st != GRR_OK) return st;
   GemmArgs g1{};

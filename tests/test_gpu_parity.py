@@ -263,7 +263,7 @@ def test_replicated_input_folding(irdu):
 # C = 160 / 192 run the fp32 MFMA path (v1.0 encoder/decoder widths).
 @pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 40, 36), (33, 20, 9, 44), (24, 64, 13, 30),
                                  (128, 24, 8, 68), (6, 16, 5, 4), (96, 256, 27, 70), (64, 40, 1, 3),
-                                 (160, 48, 12, 20), (192, 64, 9, 11)])
+                                 (160, 48, 12, 20), (192, 64, 9, 11), (384, 96, 6, 10)])
 def test_local_nonlinear_block(irdu, chw):
     c, hid, h, w = chw
     torch.manual_seed(0)
