@@ -566,6 +566,7 @@ __global__ __launch_bounds__(NT) void graph_op_kernel(OpArgs a) {
 // shift per row array and direction).  Image-edge columns apply the operators'
 // boundary rules explicitly (replicate for S, zero outside for S^T / C^T C).
 // ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) float* lds_f32_t;
 template <int V> struct VecT;
 template <> struct VecT<1> { typedef float type; };
 template <> struct VecT<2> { typedef float __attribute__((ext_vector_type(2))) type; };
@@ -605,16 +606,31 @@ struct RowLoadsV {
   float th[(V + 1) / 2];   // half-resolution operand at row (t-3)/2
 };
 
+// Minimum waves per SIMD asked of the LDS-ring step kernel (LW below).  Without its weight
+// registers it needs 178 VGPRs (2 waves/SIMD); forcing 3 (168 VGPRs) spills 10-12 VGPRs of
+// store addresses into the row loop and measured 2.37 -> 2.81 ms per launch, so 1 (no bound).
+#ifndef GRR_ROW_WPE
+#define GRR_ROW_WPE 1
+#endif
 template <bool GLR, int GTV, int EPI, int V>
-__global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((
+    amdgpu_waves_per_eu((GLR && GTV == GTV_PAIR && EPI == EPI_STEP && V == 4) ? GRR_ROW_WPE : 1)))
+void graph_row_kernel(OpArgs a) {
   constexpr int NH = (V + 1) / 2;    // half-resolution values per lane
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // LW: the step kernel's edge-weight rows (4 GLR + 2 GTV pair rows per image row) reach the
+  // block through an LDS ring filled by one extra producer wave with LDS-DMA, four rows
+  // ahead; the channel waves read them with ds_read_b128 and hold no weight registers
+  constexpr bool LW = GLR && GTV == GTV_PAIR && EPI == EPI_STEP && V == 4;
+  constexpr int LW_ROWS = 6;                     // weight rows per image row
+  __shared__ __attribute__((aligned(16))) float wring[LW ? 3 * 2 * LW_ROWS * 256 : 4];
+  const bool producer = LW && wave == a.wpb;
   // a block = wpb channel waves of one (b, graph, segment): they walk the rows in lockstep
   // (one barrier per two rows), so the graph's edge-weight rows are fetched from HBM once
   // and served to the other channel waves by L1/L2 (the grid divides exactly: no wave
   // leaves early, every wave reaches every barrier)
-  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * a.wpb + wave;
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * a.wpb + (producer ? 0 : wave);
   const int F = a.F;
   const int f = unit % F; unit /= F;
   const int seg = unit % a.nsegs; unit /= a.nsegs;
@@ -675,11 +691,11 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
   auto issue = [&](int t, RowLoadsV<V>& S) {
     vload(S.x, px + clampi(t, 0, H - 1) * W, vo);
     const int rw = clampi(t - 2, 0, H - 1) * W;
-    if constexpr (GLR) {
+    if constexpr (GLR && !LW) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) vload(S.wl[e], pwl + e * HW + rw, vo);
     }
-    if constexpr (GTV == GTV_PAIR) {
+    if constexpr (GTV == GTV_PAIR && !LW) {
       vload(S.wg[0], pwg + rw, vo);
       vload(S.wg[1], pwg + HW + rw, vo);
     }
@@ -707,8 +723,29 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
   float O0[V] = {}, O1[V] = {}, O2[V] = {};
   float cv_prev[V] = {}, wdn_prev[V] = {}, xn_prev[V] = {};
 
-  auto consume = [&](int t, const RowLoadsV<V>& S, auto odd_tag) {
+  auto consume = [&](int t, const RowLoadsV<V>& S, const float* lwrow, auto odd_tag) {
     constexpr bool ODD_Y = decltype(odd_tag)::value;
+    // edge weights of row t-2: registers, or (LW) this lane's 4 columns of the LDS ring slot
+    float WL[4][V], WG[2][V];
+    if constexpr (LW) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 q = *reinterpret_cast<const float4*>(lwrow + e * 256);
+        WL[e][0] = q.x; WL[e][1] = q.y; WL[e][2] = q.z; WL[e][3] = q.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float4 q = *reinterpret_cast<const float4*>(lwrow + (4 + e) * 256);
+        WG[e][0] = q.x; WG[e][1] = q.y; WG[e][2] = q.z; WG[e][3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) WL[e][j] = S.wl[e][j];
+        WG[0][j] = S.wg[0][j]; WG[1][j] = S.wg[1][j];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < V; ++j) { X0[j] = X1[j]; X1[j] = X2[j]; X2[j] = X3[j]; X3[j] = S.x[j]; }
     // ---- stage 2: s at row t-1 (rows replicate-clamped by the loads, columns here)
@@ -745,7 +782,7 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
           const float dn = r < H - 1 ? SL2[j] : SL1[j];
           const float lf = col > 0 ? (j > 0 ? SL1[j - 1] : pv) : SL1[j];
           const float rt = col < W - 1 ? (j < V - 1 ? SL1[j + 1] : nx) : SL1[j];
-          const float wx = ((S.wl[0][j] * up + S.wl[1][j] * lf) + S.wl[2][j] * rt) + S.wl[3][j] * dn;
+          const float wx = ((WL[0][j] * up + WL[1][j] * lf) + WL[2][j] * rt) + WL[3][j] * dn;
           l[j] = (rin && col < W) ? SL1[j] - wx : 0.f;
         }
 #pragma unroll
@@ -753,7 +790,7 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
       }
       if constexpr (GTV == GTV_PAIR) {
         const float sp = lane_prev(SG1[V - 1]), sn = lane_next(SG1[0]);
-        const float wp = lane_prev(S.wg[0][V - 1]);
+        const float wp = lane_prev(WG[0][V - 1]);
         float o[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) {
@@ -761,14 +798,14 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
           const float sv = SG1[j];
           const float snx = j < V - 1 ? SG1[j + 1] : sn;     // x c_h = 0 at the last column
           const float spv = j > 0 ? SG1[j - 1] : sp;
-          const float chl = col > 0 ? (j > 0 ? S.wg[0][j - 1] : wp) : 0.f;
+          const float chl = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
           const float cvu = r > 0 ? cv_prev[j] : 0.f;
-          const float ov = S.wg[0][j] * (sv - snx) + chl * (sv - spv) + S.wg[1][j] * (sv - SG2[j]) +
+          const float ov = WG[0][j] * (sv - snx) + chl * (sv - spv) + WG[1][j] * (sv - SG2[j]) +
                            cvu * (sv - SG0[j]);
           o[j] = (rin && col < W) ? ov : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < V; ++j) { cv_prev[j] = S.wg[1][j]; O0[j] = O1[j]; O1[j] = O2[j]; O2[j] = o[j]; }
+        for (int j = 0; j < V; ++j) { cv_prev[j] = WG[1][j]; O0[j] = O1[j]; O1[j] = O2[j]; O2[j] = o[j]; }
       }
       if constexpr (GTV == GTV_PROX) {
         const float sp = lane_prev(SG1[V - 1]), sn = lane_next(SG1[0]);
@@ -880,16 +917,62 @@ __global__ __launch_bounds__(NT) void graph_row_kernel(OpArgs a) {
 
   const int ts = r0 - 3;
   const int te = ts + ((r1 + 3 - ts + 1) & ~1);
+  if constexpr (LW) {
+    // ring slot (pair q, parity) holds the weight rows of step t = ts + 2 q' + parity, q = q' mod 3
+    if (producer) {
+      const uint32_t vsrc = (uint32_t)cl0;
+      auto dma_pair = [&](int t, int q) {
+#pragma unroll
+        for (int par = 0; par < 2; ++par) {
+          const int rw = clampi(t + par - 2, 0, H - 1) * W;
+          float* slot = wring + (q * 2 + par) * LW_ROWS * 256;
+#pragma unroll
+          for (int e = 0; e < LW_ROWS; ++e) {
+            const float* src = e < 4 ? pwl + e * HW + rw + vsrc : pwg + (e - 4) * HW + rw + vsrc;
+            const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)(slot + e * 256);
+            asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
+                         : "memory");
+          }
+        }
+      };
+      dma_pair(ts, 0);
+      dma_pair(ts + 2, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * LW_ROWS) : "memory");   // pair 0 landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      int q = 0;
+      for (int t = ts; t < te; t += 2) {
+        dma_pair(t + 4, q == 0 ? 2 : q - 1);       // the slot the channel waves read last iteration
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * LW_ROWS) : "memory");  // pair of t + 2 landed
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        q = q == 2 ? 0 : q + 1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
   RowLoadsV<V> A, B;
   issue(ts, A);
   issue(ts + 1, B);
-  const bool lockstep = a.wpb > 1;
+  if constexpr (LW) {
+    __builtin_amdgcn_s_barrier();                  // the producer's first ring pair has landed
+    asm volatile("" ::: "memory");
+  }
+  const bool lockstep = LW || a.wpb > 1;
+  const float* lwl = wring + lane * 4;
+  int q = 0;
   for (int t = ts; t < te; t += 2) {
-    consume(t, A, std::false_type{});
+    consume(t, A, lwl + (q * 2) * LW_ROWS * 256, std::false_type{});
     issue(t + 2, A);
-    consume(t + 1, B, std::true_type{});
+    consume(t + 1, B, lwl + (q * 2 + 1) * LW_ROWS * 256, std::true_type{});
     issue(t + 3, B);
-    if (lockstep) __builtin_amdgcn_s_barrier();
+    if (lockstep) {
+      if constexpr (LW) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ring reads done
+      __builtin_amdgcn_s_barrier();
+      if constexpr (LW) asm volatile("" ::: "memory");
+    }
+    q = q == 2 ? 0 : q + 1;
   }
 }
 
@@ -910,11 +993,14 @@ static void launch_row(OpArgs a, int B, hipStream_t s) {
   // channels of a graph per block: the largest divisor of F that fits NT threads.  Only for
   // V = 4 (W > 128): on 128-wide half-resolution planes the unsynchronised waves measured 4 %
   // faster (0.408 vs 0.426 ms, scripts/micro.py --kernel half), the weight rows being short
-  int wpb = (g_kernel_variant == 2 || V < 4) ? 1 : NT / 64;
+  // The step kernel (LW) adds one producer wave per block that streams the edge-weight rows
+  // into an LDS ring, so at most NT / 64 - 1 channel waves
+  constexpr bool LW = GLR && GTV == GTV_PAIR && EPI == EPI_STEP && V == 4;
+  int wpb = (g_kernel_variant == 2 || V < 4) ? 1 : NT / 64 - (LW ? 1 : 0);
   while (a.F % wpb) --wpb;
   a.wpb = wpb;
   a.nblk = (uint32_t)(units / wpb);
-  hipLaunchKernelGGL((graph_row_kernel<GLR, GTV, EPI, V>), dim3(a.nblk), dim3(64 * wpb), 0, s, a);
+  hipLaunchKernelGGL((graph_row_kernel<GLR, GTV, EPI, V>), dim3(a.nblk), dim3(64 * (wpb + (LW ? 1 : 0))), 0, s, a);
 }
 
 template <bool GLR, int GTV, int EPI>
