@@ -596,6 +596,48 @@ __device__ __forceinline__ void vstore(float* row_base, uint32_t off_bytes, cons
   *reinterpret_cast<T*>(reinterpret_cast<char*>(row_base) + off_bytes) = t;
 }
 
+// Buffer-resource row access for the row kernels: a wave-uniform resource per operand plane
+// (base + byte size in SGPRs) and one 32-bit VGPR offset per access, instead of 64-bit VGPR
+// row pointers.  Reads past num_records return 0 and writes there are dropped by the
+// hardware range check, so absent operands use num_records = 0 and rows / lanes that must
+// not be written get an offset past the end (GRR_OOB).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t GRR_OOB = 0x80000000u;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, p ? (int)bytes : 0, 0x00020000);
+}
+template <int N>
+__device__ __forceinline__ void bload(float (&d)[N], rsrc_t r, uint32_t off) {
+  if constexpr (N == 1) {
+    d[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  } else {
+    typedef typename VecT<N>::type T;
+    T t;
+    if constexpr (N == 2) t = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    else t = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+#pragma unroll
+    for (int j = 0; j < N; ++j) d[j] = t[j];
+  }
+}
+template <int N>
+__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, const float (&v)[N]) {
+  if constexpr (N == 1) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[0]), r, off, 0, 0);
+  } else {
+    typedef typename VecT<N>::type T;
+    T t;
+#pragma unroll
+    for (int j = 0; j < N; ++j) t[j] = v[j];
+    if constexpr (N == 2) {
+      typedef uint32_t U2 __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, t), r, off, 0, 0);
+    } else {
+      typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, t), r, off, 0, 0);
+    }
+  }
+}
+
 template <int V>
 struct RowLoadsV {
   float x[V];          // x row t
@@ -643,10 +685,9 @@ void graph_row_kernel(OpArgs a) {
   const bool lane_on = c0 < W;                   // W % V == 0: a lane is all-in or all-out
   const int cl0 = lane_on ? c0 : W - V;          // clamped (loads of idle lanes duplicate)
   const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
-  float* const scratch = g_grr_scratch;
-  const uint32_t vo = (uint32_t)cl0 * 4u, vo_lane = (uint32_t)lane * 4u * V;
+  const uint32_t vo = (uint32_t)cl0 * 4u;
   // half-resolution column(s) of this lane: V=4 -> 2l, 2l+1; V=2 -> l; V=1 -> l/2
-  const uint32_t vo_half = (uint32_t)(V == 1 ? (cl0 >> 1) : (cl0 >> 1)) * 4u;
+  const uint32_t vo_half = (uint32_t)(cl0 >> 1) * 4u;
   const bool owner_xd = lane_on && (V > 1 || ((c0 & 1) == 0 && c0 + 1 < W));
 
   const int64_t plane = ((int64_t)b * C + ch) * HW;
@@ -658,20 +699,19 @@ void graph_row_kernel(OpArgs a) {
   const bool want_xd = a.xd_out != nullptr;
   const int np = GTV == GTV_PROX ? 4 : 2;
   const int64_t rplane = ((int64_t)b * F + f) * HW;   // plane of a graph-replicated operand
-  const float* px = a.x + (a.x_rep ? rplane : plane);
+  const int64_t PB = HW * 4, HPB = (int64_t)hh * hw * 4;   // plane bytes (launch_op: < 2^31 / 4)
   const float* pwl = GLR ? a.wL + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
   const float* pwg = GTV ? a.wG + (int64_t)(b * a.G + g) * np * HW : nullptr;
-  const float* pb = EPI == EPI_STEP ? a.b + plane : scratch;
-  const float* pu = use_beta ? a.u_prev + plane : scratch;
-  const float* py = need_y ? a.y + (a.y_rep ? rplane : plane) : scratch;
-  const float* pth = has_half ? a.t_half + hplane : scratch;
-  float* pout = a.out + plane;
-  float* puo = want_u ? a.u_out + plane : scratch;
-  float* pxd = want_xd ? a.xd_out + hplane : scratch;
-  const int ws_b = EPI == EPI_STEP ? W : 0, ws_u = use_beta ? W : 0, ws_y = need_y ? W : 0;
-  const int ws_th = has_half ? hw : 0, ws_uo = want_u ? W : 0, ws_xd = want_xd ? hw : 0;
-  const uint32_t vo_b = EPI == EPI_STEP ? vo : vo_lane, vo_u = use_beta ? vo : vo_lane;
-  const uint32_t vo_y = need_y ? vo : vo_lane, vo_th = has_half ? vo_half : vo_lane;
+  const rsrc_t rx = make_rsrc(a.x + (a.x_rep ? rplane : plane), PB);
+  const rsrc_t rwl = make_rsrc(pwl, 4 * PB), rwg = make_rsrc(pwg, np * PB);
+  const rsrc_t rb = make_rsrc(EPI == EPI_STEP ? a.b + plane : nullptr, PB);
+  const rsrc_t ru = make_rsrc(use_beta ? a.u_prev + plane : nullptr, PB);
+  const rsrc_t ry = make_rsrc(need_y ? a.y + (a.y_rep ? rplane : plane) : nullptr, PB);
+  const rsrc_t rth = make_rsrc(has_half ? a.t_half + hplane : nullptr, HPB);
+  const rsrc_t rout = make_rsrc(a.out + plane, PB);
+  const rsrc_t ruo = make_rsrc(want_u ? a.u_out + plane : nullptr, PB);
+  const rsrc_t rxd = make_rsrc(want_xd ? a.xd_out + hplane : nullptr, HPB);
+  const uint32_t RB = (uint32_t)W * 4u, HRB = (uint32_t)hw * 4u;   // row bytes
 
   float sc_l = 1.f, sc_g = 1.f, sc_h = 1.f, gam = 0.f, alpha = 0.f, beta = 0.f, sk0 = 0.f, sk1 = 1.f;
   if (a.log_l) sc_l = a.lin_l ? a.log_l[g] : expf(a.log_l[g]);
@@ -689,29 +729,29 @@ void graph_row_kernel(OpArgs a) {
   if constexpr (GTV != GTV_NONE) tG = make_taps(a.sG, ch);
 
   auto issue = [&](int t, RowLoadsV<V>& S) {
-    vload(S.x, px + clampi(t, 0, H - 1) * W, vo);
-    const int rw = clampi(t - 2, 0, H - 1) * W;
+    bload(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
+    const uint32_t rw = clampi(t - 2, 0, H - 1) * RB;
     if constexpr (GLR && !LW) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) vload(S.wl[e], pwl + e * HW + rw, vo);
+      for (int e = 0; e < 4; ++e) bload(S.wl[e], rwl, vo + e * (uint32_t)PB + rw);
     }
     if constexpr (GTV == GTV_PAIR && !LW) {
-      vload(S.wg[0], pwg + rw, vo);
-      vload(S.wg[1], pwg + HW + rw, vo);
+      bload(S.wg[0], rwg, vo + rw);
+      bload(S.wg[1], rwg, vo + (uint32_t)PB + rw);
     }
     if constexpr (GTV == GTV_PROX) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) vload(S.wg[e], pwg + e * HW + rw, vo);
-      vload(S.wup, pwg + clampi(t - 1, 0, H - 1) * W, vo);
+      for (int e = 0; e < 4; ++e) bload(S.wg[e], rwg, vo + e * (uint32_t)PB + rw);
+      bload(S.wup, rwg, vo + clampi(t - 1, 0, H - 1) * RB);
     }
     const int re = clampi(t - 3, 0, H - 1);
     if constexpr (EPI == EPI_STEP) {
-      vload(S.eb, pb + re * ws_b, vo_b);
-      vload(S.eu, pu + re * ws_u, vo_u);
+      bload(S.eb, rb, vo + re * RB);
+      bload(S.eu, ru, vo + re * RB);
     }
     if constexpr (EPI != EPI_HALF) {
-      vload(S.ey, py + re * ws_y, vo_y);
-      vload(S.th, pth + (re >> 1) * ws_th, vo_th);
+      bload(S.ey, ry, vo + re * RB);
+      bload(S.th, rth, vo_half + (re >> 1) * HRB);
     }
   };
 
@@ -893,10 +933,9 @@ void graph_row_kernel(OpArgs a) {
     }
     const bool yv = y >= r0 && y < r1;
     const int yr = yv ? y : 0;
-    if (lane_on) vstore(yv ? pout + yr * W : scratch, yv ? vo : vo_lane, res);
-    if constexpr (EPI == EPI_STEP) {
-      if (lane_on) vstore(yv ? puo + yr * ws_uo : scratch, yv ? (want_u ? vo : vo_lane) : vo_lane, u);
-    }
+    const uint32_t so = (yv && lane_on) ? vo + yr * RB : GRR_OOB;
+    bstore(rout, so, res);
+    if constexpr (EPI == EPI_STEP) bstore(ruo, so, u);
     if constexpr (ODD_Y) {
       // D of the (pre-skip) result: 2x2 blocks of rows y-1, y
       float d[NH];
@@ -908,8 +947,7 @@ void graph_row_kernel(OpArgs a) {
         for (int k = 0; k < NH; ++k)
           d[k] = 0.25f * xn_prev[2 * k] + 0.25f * xn_prev[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
       }
-      if (owner_xd)
-        vstore(yv ? pxd + (yr >> 1) * ws_xd : scratch, yv ? (want_xd ? vo_half : vo_lane) : vo_lane, d);
+      bstore(rxd, (yv && owner_xd) ? vo_half + (yr >> 1) * HRB : GRR_OOB, d);
     }
 #pragma unroll
     for (int j = 0; j < V; ++j) xn_prev[j] = xn[j];
@@ -1010,6 +1048,8 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
                   (1ull << 32) - 4,
               GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   int vec = g_kernel_variant == 1 ? 0 : row_vec(a0.W);
+  // row kernels address a graph's 4 weight planes through one buffer resource (int range)
+  if ((int64_t)a0.H * a0.W * 16 >= (1ll << 31)) vec = 0;
   if (vec > 1) {   // vector row loads need every operand base aligned to 4V bytes
     const void* ptrs[] = {a0.x, a0.wL, a0.wG, a0.y, a0.b, a0.u_prev, a0.t_half, a0.out, a0.u_out, a0.xd_out};
     for (const void* q : ptrs)
@@ -1213,9 +1253,33 @@ static bool stencil_ok(const grr_stencil& s) { return s.p01 && s.p02a && s.p02b 
 
 using namespace grr;
 
+// Streaming copy (one float4 per lane, non-temporal): the HBM ceiling the bench reports
+// beside the step kernel's rate (measured on the same GPU in the same run).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void stream_copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                                          int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) {
+    const f32x4 v = __builtin_nontemporal_load(src + i);
+    __builtin_nontemporal_store(v, dst + i);
+  }
+}
+
 extern "C" {
 
 int grr_version(void) { return 1; }
+
+grr_status grr_stream_copy(const float* src, float* dst, int64_t n, void* stream) {
+  clear_error();
+  GRR_REQUIRE(src && dst && n > 0 && n % 4 == 0 && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0,
+              GRR_ERR_INVALID_ARG, "grr_stream_copy: bad args");
+  const int64_t n4 = n / 4;
+  GRR_REQUIRE(n4 / 256 < (1ll << 31) - 1, GRR_ERR_UNSUPPORTED, "grr_stream_copy: too large");
+  const int blocks = (int)((n4 + 255) / 256);
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const f32x4*>(src), reinterpret_cast<f32x4*>(dst), n4);
+  return launch_status("grr_stream_copy");
+}
 
 grr_status grr_set_kernel_variant(int variant) {
   clear_error();

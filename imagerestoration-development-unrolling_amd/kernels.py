@@ -118,6 +118,12 @@ def set_kernel_variant(variant: str) -> None:
     _native.call("grr_set_kernel_variant", {"auto": 0, "strips": 1, "independent": 2}[variant])
 
 
+def stream_copy(src: Tensor, dst: Tensor) -> None:
+    """float4 streaming copy (bench's measured HBM ceiling)."""
+    assert src.is_contiguous() and dst.is_contiguous() and src.numel() == dst.numel()
+    call("grr_stream_copy", src.data_ptr(), dst.data_ptr(), src.numel(), _stream(src.device))
+
+
 def neighbor_table(h: int, w: int, device) -> Tensor:
     out = torch.empty((4, h, w), dtype=torch.int32, device=device)
     call("grr_neighbor_table", out.data_ptr(), h, w, _stream(out.device))

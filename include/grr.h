@@ -45,6 +45,10 @@ const char* grr_last_error(void);
  * without the lockstep.  Process-wide; results agree to fp32 rounding either way. */
 grr_status grr_set_kernel_variant(int variant);
 
+/* Measurement helper (not a reference interface): float4 streaming copy of n floats
+ * (n % 4 == 0, 16-byte aligned), the HBM ceiling bench.py reports beside the step kernel. */
+grr_status grr_stream_copy(const float* src, float* dst, int64_t n, void* stream);
+
 /* a1 — integer neighbour table (bit-exact target).  out[e*H*W + p] = flat index
  * of clamp(p + delta_e): the pixel the reference's replicate-padded gather reads
  * for edge e (REF:128-144, GLRFast.get_neighbors_pixels).  out: int32 [4,H,W]. */

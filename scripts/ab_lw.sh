@@ -11,6 +11,8 @@ for L in "$@"; do
 done
 for r in 1 2; do
   for L in "$@"; do
-    echo "== micro $L"; GRR_LIB=$L timeout -k 10 120 python scripts/micro.py --kernel step --iters 30 2>&1 | tail -1 || exit 1
+    for K in step half; do
+      echo "== micro $K $L"; GRR_LIB=$L timeout -k 10 120 python scripts/micro.py --kernel $K --iters 30 2>&1 | tail -1 || exit 1
+    done
   done
 done
