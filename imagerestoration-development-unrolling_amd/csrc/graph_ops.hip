@@ -237,10 +237,11 @@ __device__ __forceinline__ float stencil_t(const Taps& t, const float* a, int i,
 }
 
 // phi of the GTV proximal rhs: eps - (t - eps), eps = soft_threshold(t, gamma) (REF:684-704, :765-774)
+// soft_threshold(t) = t - clamp(t, -gamma, gamma) is the same fp32 value as the reference's
+// where(t < -g, t + g, 0) + where(t > g, t - g, 0) (t - (-g) == t + g exactly; t - t == +0),
+// so one v_med3_f32 + a subtraction replaces two compares, two selects and two adds
 __device__ __forceinline__ float prox_phi(float t, float gm) {
-  const float lo = t < -gm ? t + gm : 0.f;
-  const float hi = t > gm ? t - gm : 0.f;
-  const float eps = lo + hi;
+  const float eps = t - __builtin_amdgcn_fmed3f(t, -gm, gm);
   return eps - (t - eps);
 }
 
