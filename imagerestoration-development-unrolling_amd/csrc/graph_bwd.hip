@@ -316,7 +316,8 @@ __global__ __launch_bounds__(NT) void pair_bwd_kernel(const float* __restrict__ 
 //   o_out(q), gs_out(q) = d<a, o>/ds(q),  gw[e](q) += scale * d<a,o>/dw_e(q),
 //   ggam[g] += scale * d<a,o>/dgamma,     gdot[g] += coef * <a, o>
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float soft_t(float t, float gm) { return t < -gm ? t + gm : (t > gm ? t - gm : 0.f); }
+// soft threshold as t - clamp(t, -gm, gm): the same fp32 value as the two-sided select (one v_med3)
+__device__ __forceinline__ float soft_t(float t, float gm) { return t - __builtin_amdgcn_fmed3f(t, -gm, gm); }
 
 __global__ __launch_bounds__(NT) void prox_bwd_kernel(const float* __restrict__ s, const float* __restrict__ a,
                                                       const float* __restrict__ w,
