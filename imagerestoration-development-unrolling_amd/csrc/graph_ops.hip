@@ -665,9 +665,16 @@ void graph_row_kernel(OpArgs a) {
   // LW: the step kernel's edge-weight rows (4 GLR + 2 GTV pair rows per image row) reach the
   // block through an LDS ring filled by one extra producer wave with LDS-DMA, four rows
   // ahead; the channel waves read them with ds_read_b128 and hold no weight registers
-  constexpr bool LW = GLR && GTV == GTV_PAIR && EPI == EPI_STEP && V == 4;
+  // The half-level operator (system_half, V = 2, W = 128) uses the same ring: there one
+  // 1 KiB DMA (lanes 0-31 row t-2, lanes 32-63 row t-1) moves a weight plane's row pair.
+  constexpr bool LW = GLR && GTV == GTV_PAIR && ((EPI == EPI_STEP && V == 4) || (EPI == EPI_HALF && V == 2));
   constexpr int LW_ROWS = 6;                     // weight rows per image row
-  __shared__ __attribute__((aligned(16))) float wring[LW ? 3 * 2 * LW_ROWS * 256 : 4];
+  // ring of 3 row pairs; a plane's rows sit 256 floats apart: V = 4 slot [pair][parity][plane][256],
+  // V = 2 slot [pair][plane][parity][128]
+  constexpr int LW_PAIR = V == 4 ? 2 * LW_ROWS * 256 : LW_ROWS * 256;   // floats per pair
+  constexpr int LW_PAR = V == 4 ? LW_ROWS * 256 : 128;                   // parity offset
+  constexpr int LW_NDMA = V == 4 ? 2 * LW_ROWS : LW_ROWS;                // DMAs per pair
+  __shared__ __attribute__((aligned(16))) float wring[LW ? 3 * LW_PAIR : 4];
   const bool producer = LW && wave == a.wpb;
   // a block = wpb channel waves of one (b, graph, segment): they walk the rows in lockstep
   // (one barrier per two rows), so the graph's edge-weight rows are fetched from HBM once
@@ -769,15 +776,18 @@ void graph_row_kernel(OpArgs a) {
     // edge weights of row t-2: registers, or (LW) this lane's 4 columns of the LDS ring slot
     float WL[4][V], WG[2][V];
     if constexpr (LW) {
+      typedef typename VecT<V>::type T;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float4 q = *reinterpret_cast<const float4*>(lwrow + e * 256);
-        WL[e][0] = q.x; WL[e][1] = q.y; WL[e][2] = q.z; WL[e][3] = q.w;
+        const T q = *reinterpret_cast<const T*>(lwrow + e * 256);
+#pragma unroll
+        for (int j = 0; j < V; ++j) WL[e][j] = q[j];
       }
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const float4 q = *reinterpret_cast<const float4*>(lwrow + (4 + e) * 256);
-        WG[e][0] = q.x; WG[e][1] = q.y; WG[e][2] = q.z; WG[e][3] = q.w;
+        const T q = *reinterpret_cast<const T*>(lwrow + (4 + e) * 256);
+#pragma unroll
+        for (int j = 0; j < V; ++j) WG[e][j] = q[j];
       }
     } else {
 #pragma unroll
@@ -959,30 +969,38 @@ void graph_row_kernel(OpArgs a) {
   if constexpr (LW) {
     // ring slot (pair q, parity) holds the weight rows of step t = ts + 2 q' + parity, q = q' mod 3
     if (producer) {
-      const uint32_t vsrc = (uint32_t)cl0;
+      auto dma = [&](const float* src, float* dst) {
+        const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)dst;
+        asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
+                     : "memory");
+      };
       auto dma_pair = [&](int t, int q) {
+        if constexpr (V == 4) {
 #pragma unroll
-        for (int par = 0; par < 2; ++par) {
-          const int rw = clampi(t + par - 2, 0, H - 1) * W;
-          float* slot = wring + (q * 2 + par) * LW_ROWS * 256;
+          for (int par = 0; par < 2; ++par) {
+            const int rw = clampi(t + par - 2, 0, H - 1) * W + cl0;
+            float* slot = wring + q * LW_PAIR + par * LW_PAR;
 #pragma unroll
-          for (int e = 0; e < LW_ROWS; ++e) {
-            const float* src = e < 4 ? pwl + e * HW + rw + vsrc : pwg + (e - 4) * HW + rw + vsrc;
-            const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)(slot + e * 256);
-            asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
-                         : "memory");
+            for (int e = 0; e < LW_ROWS; ++e)
+              dma(e < 4 ? pwl + e * HW + rw : pwg + (e - 4) * HW + rw, slot + e * 256);
           }
+        } else {   // W == 128: lanes 0-31 row t-2, lanes 32-63 row t-1, 4 columns each
+          const int rw = clampi(t + (lane >> 5) - 2, 0, H - 1) * W + (lane & 31) * 4;
+          float* slot = wring + q * LW_PAIR;
+#pragma unroll
+          for (int e = 0; e < LW_ROWS; ++e)
+            dma(e < 4 ? pwl + e * HW + rw : pwg + (e - 4) * HW + rw, slot + e * 256);
         }
       };
       dma_pair(ts, 0);
       dma_pair(ts + 2, 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * LW_ROWS) : "memory");   // pair 0 landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LW_NDMA) : "memory");   // pair 0 landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       int q = 0;
       for (int t = ts; t < te; t += 2) {
         dma_pair(t + 4, q == 0 ? 2 : q - 1);       // the slot the channel waves read last iteration
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * LW_ROWS) : "memory");  // pair of t + 2 landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LW_NDMA) : "memory");  // pair of t + 2 landed
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         q = q == 2 ? 0 : q + 1;
@@ -999,12 +1017,12 @@ void graph_row_kernel(OpArgs a) {
     asm volatile("" ::: "memory");
   }
   const bool lockstep = LW || a.wpb > 1;
-  const float* lwl = wring + lane * 4;
+  const float* lwl = wring + lane * V;
   int q = 0;
   for (int t = ts; t < te; t += 2) {
-    consume(t, A, lwl + (q * 2) * LW_ROWS * 256, std::false_type{});
+    consume(t, A, lwl + q * LW_PAIR, std::false_type{});
     issue(t + 2, A);
-    consume(t + 1, B, lwl + (q * 2 + 1) * LW_ROWS * 256, std::true_type{});
+    consume(t + 1, B, lwl + q * LW_PAIR + LW_PAR, std::true_type{});
     issue(t + 3, B);
     if (lockstep) {
       if constexpr (LW) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ring reads done
@@ -1032,10 +1050,11 @@ static void launch_row(OpArgs a, int B, hipStream_t s) {
   // channels of a graph per block: the largest divisor of F that fits NT threads.  Only for
   // V = 4 (W > 128): on 128-wide half-resolution planes the unsynchronised waves measured 4 %
   // faster (0.408 vs 0.426 ms, scripts/micro.py --kernel half), the weight rows being short
-  // The step kernel (LW) adds one producer wave per block that streams the edge-weight rows
-  // into an LDS ring, so at most NT / 64 - 1 channel waves
-  constexpr bool LW = GLR && GTV == GTV_PAIR && EPI == EPI_STEP && V == 4;
-  int wpb = (g_kernel_variant == 2 || V < 4) ? 1 : NT / 64 - (LW ? 1 : 0);
+  // The LDS-ring kernels (LW: the step kernel and the 128-wide half-level operator) add one
+  // producer wave per block that streams the edge-weight rows into an LDS ring, so at most
+  // NT / 64 - 1 channel waves
+  constexpr bool LW = GLR && GTV == GTV_PAIR && ((EPI == EPI_STEP && V == 4) || (EPI == EPI_HALF && V == 2));
+  int wpb = (g_kernel_variant == 2 || (V < 4 && !LW)) ? 1 : NT / 64 - (LW ? 1 : 0);
   while (a.F % wpb) --wpb;
   a.wpb = wpb;
   a.nblk = (uint32_t)(units / wpb);
@@ -1057,6 +1076,10 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
       if ((uintptr_t)q % (4u * vec) != 0) vec = 0;
     // half-resolution rows are read / written as V/2-float vectors
     if (vec == 4 && (a0.t_half || a0.xd_out) && (((int64_t)(a0.H / 2) * (a0.W / 2)) % 2 != 0)) vec = 0;
+    // the LDS-ring half-level operator moves whole 128-float weight row pairs with 16-byte DMAs
+    if (vec == 2 && GLR && GTV == GTV_PAIR && EPI == EPI_HALF &&
+        (a0.W != 128 || (uintptr_t)a0.wL % 16 != 0 || (uintptr_t)a0.wG % 16 != 0))
+      vec = 0;
   }
   switch (vec) {
     case 1: launch_row<GLR, GTV, EPI, 1>(a0, B, s); return launch_status(name);
