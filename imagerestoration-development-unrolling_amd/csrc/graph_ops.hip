@@ -1113,6 +1113,10 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
 // w_up of row r+1, so it is written one row late.  Same arithmetic order as
 // edge_weights_kernel (REF:146-175).
 // ---------------------------------------------------------------------------
+#ifndef GRR_EDGE_MIN_WAVES
+#define GRR_EDGE_MIN_WAVES 8192
+#endif
+constexpr uint64_t EDGE_MIN_WAVES = GRR_EDGE_MIN_WAVES;
 struct EdgeArgs {
   const float* feat;
   int64_t bstride;
@@ -1121,6 +1125,7 @@ struct EdgeArgs {
   float* w[2];              // raw weights [B,G,4,H,W] per slab
   float* c[2];              // pair weights [B,G,2,H,W] per slab, or NULL
   int nslab, G, H, W;
+  int sseg, nsegs;          // rows per wave segment, segments per plane
   uint32_t nunits, nblk;
 };
 
@@ -1130,10 +1135,15 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t unit = xcd_remap(blockIdx.x, a.nblk) * 4 + wave;
   if (unit >= a.nunits) return;   // whole wave (uniform)
+  const int seg = unit % a.nsegs; unit /= a.nsegs;
   const int g = unit % a.G; unit /= a.G;
   const int slab = unit % a.nslab;
   const int b = unit / a.nslab;
   const int H = a.H, W = a.W;
+  // rows [r0, r1) of the plane; a segment that ends inside the image runs one extra row
+  // (weights not stored) for the w_up its last row's pair weight c_v needs
+  const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
+  const int rend = r1 < H ? r1 + 1 : H;
   const int64_t HW = (int64_t)H * W;
   const float* fb = a.feat + (int64_t)b * a.bstride + (int64_t)(a.slab_off[slab] + g * F) * HW;
   const float* Mp = a.multiM[slab] + g * F;
@@ -1158,25 +1168,26 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
     for (int j = 0; j < V; ++j) {
       float ss = 0.f;
 #pragma unroll
-      for (int f = 0; f < F; ++f) ss += raw[f][j] * raw[f][j];
+      // explicit fma: the prologue's and the row loop's copies of this code must round alike
+      // (a segment's first rows are normalised by the prologue, elsewhere by the loop)
+      for (int f = 0; f < F; ++f) ss = __builtin_fmaf(raw[f][j], raw[f][j], ss);
       const float den = fmaxf(sqrtf(ss), 1e-12f);
 #pragma unroll
       for (int f = 0; f < F; ++f) dst[f][j] = (raw[f][j] / den) * M[f];
     }
   };
-  load_raw(0);
+  load_raw(r0 - 1);                                  // clamped: row 0 is its own up neighbour
+  normalise(fP);
+  load_raw(r0);
   normalise(fC);
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-#pragma unroll
-    for (int j = 0; j < V; ++j) fP[f][j] = fC[f][j];
-  load_raw(1);
+  load_raw(r0 + 1);
   normalise(fN);
   float wdn_prev[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) wdn_prev[j] = 0.f;
 
-  for (int r = 0; r < H; ++r) {
+  for (int r = r0; r < rend; ++r) {
+    const bool own = r < r1;                           // wave-uniform: row r belongs to this segment
     load_raw(r + 2);                                   // consumed at the bottom of the iteration
     float fl[F], fr[F];                                // lane-edge neighbours (whole wave active)
 #pragma unroll
@@ -1202,7 +1213,7 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
       w0[j] = e0 / sum; w1[j] = e1 / sum; w2[j] = e2 / sum; w3[j] = e3 / sum;
     }
     const int64_t ro = (int64_t)r * W;
-    if (lane_on) {
+    if (lane_on && own) {
       vstore(wb + ro, vo, w0);
       vstore(wb + HW + ro, vo, w1);
       vstore(wb + 2 * HW + ro, vo, w2);
@@ -1220,8 +1231,8 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
         wdn_prev[j] = w3[j];
       }
       if (lane_on) {
-        vstore(cb + ro, vo, ch);
-        if (r > 0) vstore(cb + HW + ro - W, vo, cv);
+        if (own) vstore(cb + ro, vo, ch);
+        if (r > r0) vstore(cb + HW + ro - W, vo, cv);
       }
     }
     // advance the row window (the down neighbour of the last row is itself: clamped load)
@@ -1231,7 +1242,7 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
       for (int j = 0; j < V; ++j) { fP[f][j] = fC[f][j]; fC[f][j] = fN[f][j]; }
     normalise(fN);
   }
-  if (cb && lane_on) {   // last row: no lower neighbour
+  if (cb && lane_on && r1 == H) {   // last row: no lower neighbour
     float z[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) z[j] = 0.f;
@@ -1254,7 +1265,14 @@ static bool launch_edge_row(EdgeArgs a, int B, int F, hipStream_t s) {
   if ((uintptr_t)a.feat % (4u * V) || (a.bstride * 4) % (4 * V) || ((int64_t)a.H * a.W) % V) return false;
   for (int k = 0; k < a.nslab; ++k)
     if ((uintptr_t)a.w[k] % (4u * V) || (a.c[k] && (uintptr_t)a.c[k] % (4u * V))) return false;
-  const uint64_t units = (uint64_t)B * a.nslab * a.G;
+  // row segments: at least EDGE_MIN_WAVES waves (the row loop is latency-bound with one row
+  // of prefetch), segments of >= 32 rows (each costs 2 extra normalised rows + 1 extra row)
+  const uint64_t planes = (uint64_t)B * a.nslab * a.G;
+  int nsegs = 1;
+  while (planes * nsegs < EDGE_MIN_WAVES && a.H / (2 * nsegs) >= 32) nsegs *= 2;
+  a.sseg = (a.H + nsegs - 1) / nsegs;
+  a.nsegs = (a.H + a.sseg - 1) / a.sseg;
+  const uint64_t units = planes * a.nsegs;
   if (units >= (1ull << 32) - 4) return false;
   a.nunits = (uint32_t)units;
   a.nblk = (uint32_t)((units + 3) / 4);
