@@ -25,7 +25,7 @@ from .graph_filter import (  # noqa: F401
 )
 from . import kernels  # noqa: F401
 from . import glr_v10 as v10  # noqa: F401  (GLR-only drop-ins of lib/model_GLR_GTV_deep_v10.py)
-from .glr_v10 import GLRImageFilter, MixtureGLR  # noqa: F401
+from .glr_v10 import GLRImageFilter, MixtureGLR, MultiScaleGLRImageFilter, MultiScaleMixtureGLR  # noqa: F401
 from . import window_graph  # noqa: F401  (window-graph MixtureGTV of lib/model_GLR_GTV_deep_v7.py)
 from . import window_graph_v1  # noqa: F401  (multiblock window denoiser of lib/model_GLR_GTV_deep_v1.py)
 

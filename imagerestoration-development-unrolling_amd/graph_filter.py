@@ -9,10 +9,12 @@ edge_delta, pad_dim_hw — REF:52-118, :613) become non-persistent buffers: they
 follow ``.to()`` and stay out of the state_dict, as in the reference.
 
 Forward passes of the graph filter run only through the HIP kernels (kernels.py);
-GPU tensors are required.  When autograd records (training), MixtureGTVGLR and the
-filter blocks switch to the differentiable path of solver_grad.py (HIP forward that
-keeps the iterates + hand-written HIP reverse sweep).  Entry points without a reverse
-kernel yet (the GLRFast/GTVFast sub-API) attach a node whose backward raises, so
+GPU tensors are required.  When autograd records (training), every module here switches
+to the differentiable path of solver_grad.py (HIP forward that keeps what the reverse
+needs + hand-written HIP reverse kernels): MixtureGTVGLR / LocalLowpassFilteringBlock
+(_MixtureSolve), the GLRFast/GTVFast sub-API and extract_edge_weights (_GraphApply,
+_EdgeWeights), LocalNonLinearBlock (LNBFn).  A HIP forward entered directly without a
+reverse (``hip_forward``-wrapped internals) attaches a node whose backward raises, so
 training can never silently skip gradients.
 """
 from __future__ import annotations

@@ -306,11 +306,37 @@ def conv2x2s2(x: Tensor, weight: Tensor) -> Tensor:
 _WS_CACHE = {}
 
 
+# the LNB kernels address one image's [max(hid, C), H, W] planes with 32-bit byte offsets
+_LNB_MAX_BYTES = 1 << 31
+
+
+def _lnb_band_rows(c: int, hid: int, h: int, w: int) -> int:
+    """Rows per band so one band (+ its two halo rows) fits the kernels' 32-bit image offsets."""
+    per_row = max(hid, c) * w * 4
+    return h if per_row * h < _LNB_MAX_BYTES else max(1, (_LNB_MAX_BYTES - 1) // per_row - 2)
+
+
+def _lnb_banded(run, xs, h: int, rows: int) -> Tensor:
+    """Run an LNB forward on row bands of a tall image: the block's only spatial op is the
+    depthwise 3x3 (replicate pad), so output rows [r0, r1) need input rows [r0-1, r1+1), and the
+    band's own edge padding only reaches the halo rows, which are dropped."""
+    outs = []
+    for r0 in range(0, h, rows):
+        r1 = min(r0 + rows, h)
+        a, e = max(r0 - 1, 0), min(r1 + 1, h)
+        y = run(*[None if t is None else t[:, :, a:e].contiguous() for t in xs])
+        outs.append(y[:, :, r0 - a:r1 - a])
+    return torch.cat(outs, 2)
+
+
 def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor) -> Tensor:
     """LocalNonLinearBlock (nsubnets = 1) forward."""
     dev = _check("lnb_forward", x, ln_w, w1, wdw, w2, skip)
     b, c, h, w = x.shape
     hid = w2.shape[1]
+    rows = _lnb_band_rows(c, hid, h, w)
+    if rows < h:
+        return _lnb_banded(lambda xb: lnb_forward(xb, ln_w, w1, wdw, w2, skip), [x], h, rows)
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty_like(x)
@@ -332,6 +358,9 @@ def lnb_forward_rep(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, 
     if c % cs or (x is not None and tuple(x.shape) != (b, c, h, w)):
         raise ValueError("lnb_forward_rep: the block input must be copies of src")
     hid = w2.shape[1]
+    rows = _lnb_band_rows(c, hid, h, w)
+    if rows < h:
+        return _lnb_banded(lambda sb, xb: lnb_forward_rep(sb, xb, ln_w, w1, wdw, w2, skip), [src, x], h, rows)
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)

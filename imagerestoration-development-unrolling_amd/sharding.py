@@ -67,6 +67,24 @@ def global_psnr_ubyte(restored_local: torch.Tensor, clean_local: torch.Tensor) -
     return float(acc[0] / acc[1])
 
 
+@torch.no_grad()
+def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Copy rank src's parameters and buffers to every rank (one flattened broadcast per dtype)."""
+    if world()[1] == 1:
+        return
+    tensors = [t for t in list(module.parameters()) + list(module.buffers()) if t.numel()]
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.broadcast(flat, src, group=group)
+        off = 0
+        for t in ts:
+            t.copy_(flat[off:off + t.numel()].view_as(t))
+            off += t.numel()
+
+
 def _buckets(params: Sequence[torch.Tensor], bucket_bytes: int) -> List[List[torch.Tensor]]:
     out, cur, size = [], [], 0
     for p in params:

@@ -467,6 +467,107 @@ def glr_solve(mod, y: Tensor, feat: Tensor) -> Tensor:
     return _GLRSolve.apply(mod.n_graphs, y, feat.contiguous(), *params)
 
 
+# ---- two-scale GLR-only solver (config C2; glr_v10.MultiScaleMixtureGLR) ---------------------
+GLR2_PARAMS = ("GLRmodule00.multiM", "GLRmodule01.multiM") + tuple(
+    f"{m}.{q}" for m in ("GLRmodule00", "GLRmodule01") for q in STENCIL_PARAMS) + (
+    "muys00", "muys01", "alphaCGD", "betaCGD")
+
+
+class _GLR2Solve(torch.autograd.Function):
+    """(y, f0, f1, params) -> x_S of  A = I + e^mu0 L0 + U e^mu1 L1 D  under the v10 recurrence."""
+
+    @staticmethod
+    def forward(ctx, n_graphs: int, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor) -> Tensor:
+        p = dict(zip(GLR2_PARAMS, params))
+        g = n_graphs
+        nf = y.shape[1] // g
+        wL0, _ = K.edge_weights(f0, 0, g, nf, p["GLRmodule00.multiM"])
+        wL1, _ = K.edge_weights(f1, 0, g, nf, p["GLRmodule01.multiM"])
+        sL0 = Stencil(*[p[f"GLRmodule00.{q}"].data_ptr() for q in STENCIL_PARAMS])
+        sL1 = Stencil(*[p[f"GLRmodule01.{q}"].data_ptr() for q in STENCIL_PARAMS])
+        mu0, mu1, alpha, beta = p["muys00"], p["muys01"], p["alphaCGD"], p["betaCGD"]
+        n_st = alpha.shape[0]
+        x, u, xd = y, None, K.pool2(y)
+        xs, us = [y], []
+        for k in range(n_st):
+            t = K.system_half(xd, wL1, None, sL1, K.NO_STENCIL, mu1, None, g)
+            x, u, xd = K.system_step(x, y, u, t, wL0, None, sL0, K.NO_STENCIL, mu0, None, alpha[k],
+                                     beta[k] if k >= 1 else None, g, want_u=True, want_pool=k < n_st - 1)
+            xs.append(x)
+            us.append(u)
+        ctx.n_graphs, ctx.n_st = g, n_st
+        ctx.save_for_backward(y, f0, f1, wL0, wL1, *params, *xs[1:-1], *us)
+        return xs[-1]
+
+    @staticmethod
+    def backward(ctx, gout: Tensor):
+        g, n_st = ctx.n_graphs, ctx.n_st
+        sv = ctx.saved_tensors
+        y, f0, f1, wL0, wL1 = sv[:5]
+        npar = len(GLR2_PARAMS)
+        params = sv[5:5 + npar]
+        xs = (y,) + tuple(sv[5 + npar:5 + npar + n_st - 1])      # x_0 = y, x_1 .. x_{S-1}
+        us = sv[5 + npar + n_st - 1:]                             # u_0 .. u_{S-1}
+        p = dict(zip(GLR2_PARAMS, params))
+        mu0, mu1 = torch.exp(p["muys00"]), torch.exp(p["muys01"])
+        alpha, beta = p["alphaCGD"], p["betaCGD"]
+        taps0 = K.stencil_taps(*[p[f"GLRmodule00.{q}"] for q in STENCIL_PARAMS])
+        taps1 = K.stencil_taps(*[p[f"GLRmodule01.{q}"] for q in STENCIL_PARAMS])
+        gw0, gw1 = torch.zeros_like(wL0), torch.zeros_like(wL1)
+        gt0, gt1 = torch.zeros_like(taps0), torch.zeros_like(taps1)
+        gm0, gm1 = torch.zeros_like(mu0), torch.zeros_like(mu1)
+        galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
+        gy = torch.zeros_like(y)
+        neg = torch.full_like(mu0, -1.0)
+
+        def a_bwd(x: Tensor, gu: Tensor, out: Tensor) -> None:     # out -= (A - I)^T gu (+ params)
+            glr_term_bwd(x, gu, taps0, wL0, mu0, -1.0, g, out, gw0, gm0, gt0)
+            xd, gd = K.pool2(x), K.pool2(gu)                       # U^T = D
+            gxd = torch.zeros_like(xd)
+            glr_term_bwd(xd, gd, taps1, wL1, mu1, -1.0, g, gxd, gw1, gm1, gt1)
+            K.bwd_unpool2_acc(gxd, out)                            # D^T = U
+
+        gx = gout.contiguous()
+        gu_next = None
+        for k in range(n_st - 1, -1, -1):
+            K.bwd_graph_dot(gx, us[k], galpha[k], g)
+            if gu_next is not None:
+                gu = K.bwd_lincomb(gx, alpha[k], gu_next, beta[k + 1], g)
+            else:
+                gu = K.bwd_lincomb(gx, alpha[k], None, None, g)
+            if k >= 1:
+                K.bwd_graph_dot(gu, us[k - 1], gbeta[k], g)
+            K.bwd_lincomb(gu, None, None, None, g, out=gy, accumulate=True)
+            if k >= 1:
+                gx = K.bwd_lincomb(gx, None, gu, neg, g)                   # gx_{k+1} - gu
+                a_bwd(xs[k], gu, gx)
+            else:                                                           # x_0 = y
+                K.bwd_lincomb(gx, None, gu, neg, g, out=gy, accumulate=True)
+                a_bwd(y, gu, gy)
+            gu_next = gu
+        nf = y.shape[1] // g
+        gf0, gf1 = torch.empty_like(f0), torch.empty_like(f1)
+        gM0, gM1 = torch.zeros_like(p["GLRmodule00.multiM"]), torch.zeros_like(p["GLRmodule01.multiM"])
+        K.bwd_edge_weights(f0, 0, g, nf, p["GLRmodule00.multiM"], wL0, gw0, gf0, gM0)
+        K.bwd_edge_weights(f1, 0, g, nf, p["GLRmodule01.multiM"], wL1, gw1, gf1, gM1)
+        grads = {"GLRmodule00.multiM": gM0, "GLRmodule01.multiM": gM1, "muys00": gm0 * mu0, "muys01": gm1 * mu1,
+                 "alphaCGD": galpha, "betaCGD": gbeta}
+        for m, gt in (("GLRmodule00", gt0), ("GLRmodule01", gt1)):
+            for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gt)):
+                grads[f"{m}.{q}"] = gq
+        return (None, gy, gf0, gf1, *[grads[n] for n in GLR2_PARAMS])
+
+
+def glr2_solve(mod, y: Tensor, f0: Tensor, f1: Tensor) -> Tensor:
+    params = []
+    for name in GLR2_PARAMS:
+        obj = mod
+        for part in name.split("."):
+            obj = getattr(obj, part)
+        params.append(obj)
+    return _GLR2Solve.apply(mod.n_graphs, y, f0.contiguous(), f1.contiguous(), *params)
+
+
 # ---- LocalNonLinearBlock (nsubnets = 1; REF:911-964, REF13:541-575) ---------------------
 def _mat(w: Tensor, rows: int) -> Tensor:
     return w.reshape(rows, -1)

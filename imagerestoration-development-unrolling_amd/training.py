@@ -163,14 +163,18 @@ DATASETS = {c.__name__: c for c in (AddictiveGaussianNoiseImagePair, SyntheticNo
 
 class ResumeableSampler(Sampler):
     """Deterministic in-order sampling that resumes after ``current_sample`` (data_sampler.py:6-31).
-    With world_size > 1 each rank yields its own contiguous slice of every global batch."""
+    With world_size > 1 each rank yields its own contiguous slice of every global batch, and the
+    epoch is cut to whole global batches (the tail of num_samples % (batch_size * world_size) is
+    dropped) so every rank runs the same number of full steps — a rank with one more batch would
+    block forever in the gradient all-reduce."""
 
     def __init__(self, dataset, batch_size: int = 1, rank: int = 0, world_size: int = 1):
         self.dataset = dataset
         self.epoch = 0
         self.current_sample = -1
-        self.num_samples = len(dataset)
         self.batch_size, self.rank, self.world_size = batch_size, rank, world_size
+        n = len(dataset)
+        self.num_samples = n if world_size == 1 else n - n % (batch_size * world_size)
 
     def _mine(self, i: int) -> bool:
         if self.world_size == 1:
@@ -189,9 +193,13 @@ class ResumeableSampler(Sampler):
         return self.num_samples // self.world_size
 
     def set_epoch_and_current_sample(self, current_epoch, current_sample):
-        self.current_epoch = current_epoch
+        self.epoch = self.current_epoch = current_epoch
         self.current_sample = current_sample
         self.dataset.random_permute(seed=2024 + current_epoch)
+
+    def steps_per_epoch(self) -> int:
+        """Optimisation steps one epoch holds (a partial last batch counts when world_size == 1)."""
+        return -(-(self.num_samples // self.world_size) // self.batch_size)
 
 
 def create_dataset(dataset_conf: dict, environ_conf: dict):
@@ -213,7 +221,9 @@ def build_model(model_conf: dict) -> nn.Module:
     import irdu_amd
     kind = model_conf.get("type", "AbtractMultiScaleGraphFilter")
     cls = {"AbtractMultiScaleGraphFilter": irdu_amd.AbtractMultiScaleGraphFilter,
-           "MultiScaleGraphFilter": irdu_amd.MultiScaleGraphFilter}.get(kind)
+           "MultiScaleGraphFilter": irdu_amd.MultiScaleGraphFilter,
+           "GLRImageFilter": irdu_amd.GLRImageFilter,
+           "MultiScaleGLRImageFilter": irdu_amd.MultiScaleGLRImageFilter}.get(kind)
     if cls is None:
         raise ValueError(f"model type {kind!r} has no training path")
     return cls(**model_conf.get("args", {}))
@@ -305,22 +315,44 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
     loader = create_dataloader(dataset, sampler, ds_conf, conf)
     trainer = Trainer(build_model(conf.get("model", {})), tconf, device)
     ckpt_path = conf["path"].get("latest_checkpoint_path") or latest_checkpoint(conf)
+    spe = sampler.steps_per_epoch()
+    if spe <= 0:
+        raise ValueError(f"dataset of {len(dataset)} samples holds no batch of {bs} x {world} ranks")
     if ckpt_path:
         trainer.load_state_dict(torch.load(ckpt_path, map_location=device, weights_only=True))
-        sampler.set_epoch_and_current_sample(0, trainer.i * bs * world - 1)
         LOG.info("resumed from %s at iteration %d", ckpt_path, trainer.i)
+    # replicas start identical whatever each rank's seed was (data-parallel averaging never
+    # reconciles diverged weights); rank 0's weights are the ones checkpointed
+    sharding.broadcast_module(trainer.model)
     os.makedirs(checkpoint_dir(conf), exist_ok=True)
-    total = max_iters if max_iters is not None else int(tconf.get("total_iters", len(sampler) // bs))
+    total = max_iters if max_iters is not None else int(tconf.get("total_iters", spe))
     every = int(tconf.get("checkpoint_every", 5000))
     verbose = int(tconf.get("verbose_every", 100))
-    for noisy, clean in loader:
-        if trainer.i >= total:
-            break
-        loss = trainer.step(noisy, clean)
-        if rank == 0 and trainer.i % verbose == 0:
-            LOG.info("iter=%d loss=%.6f lr=%.3e", trainer.i, loss, trainer.optimizer.param_groups[0]["lr"])
-        if rank == 0 and (trainer.i % every == 0 or trainer.i == total):
+
+    def save():
+        if rank == 0:
             torch.save(trainer.state_dict(), os.path.join(checkpoint_dir(conf), f"checkpoint_iter{trainer.i:08d}.pt"))
+
+    # epoch e visits the dataset permuted with seed 2024 + e (data_sampler.py:28-31), for a fresh
+    # run and a resumed one alike, so resuming at iteration i continues exactly the order the
+    # uninterrupted run would have seen (the reference permutes a fresh run with 2204 instead,
+    # images_pair_restoration_dataset.py:41, which makes its resume skip a different order)
+    epoch, done_in_epoch = divmod(trainer.i, spe)
+    start_i, saved_at = trainer.i, None
+    while trainer.i < total:
+        sampler.set_epoch_and_current_sample(epoch, done_in_epoch * bs * world - 1)
+        for noisy, clean in loader:
+            if trainer.i >= total:
+                break
+            loss = trainer.step(noisy, clean)
+            if rank == 0 and trainer.i % verbose == 0:
+                LOG.info("iter=%d loss=%.6f lr=%.3e", trainer.i, loss, trainer.optimizer.param_groups[0]["lr"])
+            if trainer.i % every == 0:
+                save()
+                saved_at = trainer.i
+        epoch, done_in_epoch = epoch + 1, 0
+    if trainer.i > start_i and saved_at != trainer.i:     # the final state is always on disk
+        save()
     return trainer
 
 

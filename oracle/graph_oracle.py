@@ -378,6 +378,57 @@ def mixture_glr_forward(y4: Tensor, p: Params, n_graphs: int, n_stages: Optional
     return x.reshape(b, c, h, w)
 
 
+def multiscale_glr_forward(y4: Tensor, p: Params, n_graphs: int, n_stages: Optional[int] = None) -> Tensor:
+    """Two-scale GLR-only solver of config C2 (irdu_amd.MultiScaleMixtureGLR), composed from the
+    pinned ops above.  No literal reference instance exists (SURVEY.md §8d "GLR-only, v10
+    pattern, 2 scales"): the operator is REF:642-682 with its GTV / ro terms removed,
+        A x = x + e^{mu0} L0 x + U(e^{mu1} L1 D x),
+    features 1x1 C->C at full resolution (REF10:270-281) and 2x2/s2 + 1x1 at half resolution
+    (REF:593-612), and the recurrence is REF10:313-328 with b = y.
+    """
+    b, c, h, w = y4.shape
+    g = n_graphs
+    nf = c // g
+    f0 = Fn.conv2d(y4, p["patchs_features_extraction00.0.weight"])
+    f1 = Fn.conv2d(Fn.conv2d(y4, p["patchs_features_extraction01.0.weight"], stride=2),
+                   p["patchs_features_extraction01.1.weight"])
+    w0, _ = edge_weights(f0.reshape(b, g, nf, h, w), p["GLRmodule00.multiM"])
+    w1, _ = edge_weights(f1.reshape(b, g, nf, h // 2, w // 2), p["GLRmodule01.multiM"])
+    k0, k1 = stats_kernel(p, "GLRmodule00."), stats_kernel(p, "GLRmodule01.")
+    mu0, mu1 = torch.exp(p["muys00"]), torch.exp(p["muys01"])
+    alpha, beta = p["alphaCGD"], p["betaCGD"]
+    s_count = alpha.shape[0] if n_stages is None else n_stages
+    y5 = y4.reshape(b, g, nf, h, w)
+
+    def system(x5):
+        xd = pool2(x5.reshape(b, c, h, w)).view(b, g, nf, h // 2, w // 2)
+        t = _scale(glr_apply(xd, w1, k1), mu1)
+        return x5 + _scale(glr_apply(x5, w0, k0), mu0) + unpool2(t.reshape(b, c, h // 2, w // 2)).view(b, g, nf, h, w)
+
+    u = y5 - system(y5)
+    x = y5 + _scale(u, alpha[0])
+    for i in range(1, s_count):
+        u = (y5 - system(x)) + _scale(u, beta[i])
+        x = x + _scale(u, alpha[i])
+    return x.reshape(b, c, h, w)
+
+
+def multiscale_glr_image_filter(img: Tensor, p: Params, n_graphs: int, n_stages: Optional[int] = None) -> Tensor:
+    """Config C2 image filter: gray image replicated over G graphs -> two-scale GLR -> 1x1."""
+    b, cin, h, w = img.shape
+    x = img[:, None].repeat(1, n_graphs, 1, 1, 1).reshape(b, n_graphs * cin, h, w)
+    y = multiscale_glr_forward(x, sub_params(p, "localfilter."), n_graphs, n_stages)
+    return Fn.conv2d(y, p["linear_combination.weight"])
+
+
+def glr_image_filter(img: Tensor, p: Params, n_graphs: int, n_stages: Optional[int] = None) -> Tensor:
+    """Single-scale GLR image filter (config C1): image replicated over G graphs -> v10 MixtureGLR -> 1x1."""
+    b, cin, h, w = img.shape
+    x = img[:, None].repeat(1, n_graphs, 1, 1, 1).reshape(b, n_graphs * cin, h, w)
+    y = mixture_glr_forward(x, sub_params(p, "localfilter."), n_graphs, n_stages)
+    return Fn.conv2d(y, p["linear_combination.weight"])
+
+
 def sub_params(p: Params, prefix: str) -> Params:
     n = len(prefix)
     return {k[n:]: v for k, v in p.items() if k.startswith(prefix)}

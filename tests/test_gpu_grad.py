@@ -84,7 +84,9 @@ def term_path(irdu, request):
 
 @pytest.mark.parametrize("case", [dict(g=2, f=3, b=2, h=16, w=16, s=3), dict(g=4, f=2, b=1, h=12, w=20, s=5),
                                   dict(g=2, f=6, b=1, h=10, w=14, s=1), dict(g=3, f=3, b=1, h=18, w=8, s=10),
-                                  dict(g=2, f=5, b=1, h=12, w=12, s=3)])    # F = 5: no fused instance
+                                  dict(g=2, f=5, b=1, h=12, w=12, s=3),      # F = 5: no fused instance
+                                  dict(g=2, f=12, b=1, h=12, w=16, s=3),     # F = 12: v1.0 scales 2-3
+                                  dict(g=1, f=12, b=2, h=8, w=8, s=10)])
 def test_lowpass_block_grad(irdu, term_path, case):
     """LocalLowpassFilteringBlock (v1 feature convs + two-scale solver + skip), every parameter."""
     torch.manual_seed(5)
@@ -98,8 +100,8 @@ def test_lowpass_block_grad(irdu, term_path, case):
 
 
 def test_msgf_grad(irdu):
-    """MultiScaleGraphFilter with the v13 feature CNN (LocalNonLinearBlocks on the stock
-    autograd path, convs and solver on HIP), S = 10."""
+    """MultiScaleGraphFilter with the v13 feature CNN, S = 10: LocalNonLinearBlocks (LNBFn),
+    convs and solver all on their HIP forward + reverse kernels."""
     torch.manual_seed(6)
     m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=4, n_cgd_iters=10)
     perturb_mixture(m.localfilter, 61)

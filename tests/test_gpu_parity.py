@@ -399,9 +399,9 @@ def test_single_stage_and_odd_half_level(irdu, variant):
 
 
 def test_backward_fails_loudly(irdu):
-    """A HIP forward without a reverse kernel (the fused LocalNonLinearBlock, whose training
-    pass runs on stock ops) raises in backward if reached with autograd on, instead of
-    silently dropping gradients."""
+    """The fused inference forward of LocalNonLinearBlock (``_forward_hip``, no saved state for a
+    reverse; training goes through LNBFn instead) raises in backward if reached with autograd
+    on, instead of silently dropping gradients."""
     blk = irdu.LocalNonLinearBlock(8, 16, 1).to(DEV)
     x = torch.rand(1, 8, 16, 16, device=DEV, requires_grad=True)
     y = blk._forward_hip(x)
@@ -518,3 +518,22 @@ def test_graph_module_sub_api_grads(irdu):
         assert_close(fg.grad, fd.grad, 2e-4)
         for k, prm in m.named_parameters():
             assert_close(prm.grad, p[k].grad, 2e-4)
+
+
+@pytest.mark.parametrize("bgfhw", [(64, 32, 3, 256, 256), (64, 32, 3, 128, 128), (16, 8, 3, 100, 128),
+                                   (4, 8, 6, 96, 64), (2, 4, 1, 130, 200)])
+def test_edge_weights_block_batch_independent_bitwise(irdu, bgfhw):
+    """The edge-weight row kernel splits planes into row segments by a count that depends on the
+    batch (>= 8192 waves), so a patch's weights come from different segment boundaries alone and
+    in a batch; the prologue normalises a segment's first rows with the same explicit-fma
+    arithmetic as the row loop, so the results must be bit-identical (H = 100 / 130: segments of
+    unequal length; the single patch runs 8 segments, the full batch 1-2)."""
+    b, g, f, h, w = bgfhw
+    gen = torch.Generator().manual_seed(h + w)
+    feat = torch.randn(b, 2 * g * f, h, w, generator=gen).to(DEV)
+    mg, ml = ((torch.rand(g, f, generator=gen) + 0.5).to(DEV) for _ in range(2))
+    full = irdu.kernels.edge_weights_block(feat, g, f, mg, ml)
+    for i in (0, b - 1):
+        one = irdu.kernels.edge_weights_block(feat[i:i + 1].contiguous(), g, f, mg, ml)
+        for name, a, o in zip(("wG", "cG", "wL"), full, one):
+            assert torch.equal(a[i], o[0]), (name, i)

@@ -39,7 +39,13 @@ def test_example_yaml_parses_with_reference_keys():
     for key in ("name", "manual_seed", "path", "datasets"):
         assert key in conf
     ds = conf["datasets"]["train"]
-    assert ds["type"] in T.DATASETS and ds["dataloader_args"]["batch_size"] == 4
+    # config C1 as BASELINE.json states it: single-scale GLR, 1 stage, 64x64 gray, sigma 25, batch 1
+    assert ds["type"] in T.DATASETS and ds["dataloader_args"]["batch_size"] == 1
+    assert ds["dataset_args"]["patch_size"] == 64 and ds["dataset_args"]["lambda_noise"] == 25.0
+    assert ds["dataset_args"]["n_channels"] == 1
+    assert conf["model"]["type"] == "GLRImageFilter" and conf["model"]["args"]["n_cgd_iters"] == 1
+    small = T.parse(os.path.join(ROOT, "experiment_conf", "example_v1x0_small.yaml"))
+    assert small["datasets"]["train"]["dataloader_args"]["batch_size"] == 4
     c4 = T.parse(os.path.join(ROOT, "experiment_conf", "c4_train.yaml"))
     assert c4["model"]["args"]["n_cgd_iters"] == 10 and c4["datasets"]["train"]["dataset_args"]["patch_size"] == 512
 
@@ -63,8 +69,10 @@ def test_resumeable_sampler_resumes_and_shards():
     s.set_epoch_and_current_sample(0, 3)
     assert list(s) == list(range(4, 10))                 # resumes after sample 3
     parts = [list(T.ResumeableSampler(ds, batch_size=2, rank=r, world_size=2)) for r in range(2)]
-    assert parts[0] == [0, 1, 4, 5, 8, 9] and parts[1] == [2, 3, 6, 7]
-    assert sorted(parts[0] + parts[1]) == list(range(10))
+    # the epoch is cut to whole global batches (10 -> 8 samples): both ranks take 2 full steps
+    assert parts[0] == [0, 1, 4, 5] and parts[1] == [2, 3, 6, 7]
+    assert T.ResumeableSampler(ds, batch_size=2, rank=0, world_size=2).steps_per_epoch() == 2
+    assert T.ResumeableSampler(ds, batch_size=4).steps_per_epoch() == 3      # partial last batch (1 rank)
 
 
 def test_lr_schedule_matches_reference_formula():
@@ -147,3 +155,69 @@ def test_data_parallel_step_equals_full_batch_step():
     for k, v in tr.model.state_dict().items():
         for r in (0, 1):
             assert np.allclose(res[r][k], v.numpy(), rtol=1e-5, atol=1e-7), (k, r)
+
+
+def _tiny_conf(root, total, bs=4, n=10):
+    return {"name": "tiny", "manual_seed": 1, "path": {"root_dir": str(root)},
+            "datasets": {"train": {"type": "SyntheticNoisyPatches",
+                                   "dataset_args": {"patch_size": 16, "max_num_patchs": n, "lambda_noise": 25.0},
+                                   "dataloader_args": {"batch_size": bs}}},
+            "train": {"total_iters": total, "checkpoint_every": 1000, "verbose_every": 1000,
+                      "loss03_weight": 0.0, "milestones": [100]}}
+
+
+def _run_tiny(monkeypatch, conf, seed=0):
+    def build(_conf):
+        torch.manual_seed(seed)
+        return TinyModel()
+    monkeypatch.setattr(T, "build_model", build)
+    return T.run(conf, device=torch.device("cpu"))
+
+
+def test_run_trains_past_one_epoch_and_saves_final(tmp_path, monkeypatch):
+    """total_iters beyond one epoch (3 steps of 4, 4, 2 samples) keeps training over epochs and the
+    final state is checkpointed even when it is not a multiple of checkpoint_every."""
+    tr = _run_tiny(monkeypatch, _tiny_conf(tmp_path, 7))
+    assert tr.i == 7
+    files = sorted(os.listdir(T.checkpoint_dir(_tiny_conf(tmp_path, 7))))
+    assert files == ["checkpoint_iter00000007.pt"]
+
+
+def test_resume_continues_the_same_sample_order(tmp_path, monkeypatch):
+    """Interrupted at iteration 4 (inside epoch 1) and resumed to 7 == one uninterrupted run to 7."""
+    full = _run_tiny(monkeypatch, _tiny_conf(tmp_path / "a", 7))
+    _run_tiny(monkeypatch, _tiny_conf(tmp_path / "b", 4))
+    resumed = _run_tiny(monkeypatch, _tiny_conf(tmp_path / "b", 7), seed=123)   # weights come from the ckpt
+    assert resumed.i == 7
+    for (k, v), (k2, v2) in zip(full.model.state_dict().items(), resumed.model.state_dict().items()):
+        assert k == k2 and torch.allclose(v, v2, rtol=1e-6, atol=1e-8), k
+
+
+def _run_worker(rank, world, port, root, q):
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        T.build_model = lambda _c: (torch.manual_seed(rank), TinyModel())[1]   # replicas start different
+        tr = T.run(_tiny_conf(root, 5, bs=2, n=10), device=torch.device("cpu"))
+        q.put((rank, tr.i, {k: v.detach().numpy() for k, v in tr.model.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_run_over_epochs_stays_in_sync(tmp_path):
+    """2 gloo ranks, 10 samples, batch 2 per rank: each epoch is cut to 2 whole global batches, the
+    run crosses two epoch boundaries without a rank blocking in the all-reduce, and the replicas
+    (built from different seeds) are broadcast from rank 0 and stay identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (i, sd) for r, i, sd in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0] == 5
+    for k in res[0][1]:
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k
