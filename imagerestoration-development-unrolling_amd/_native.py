@@ -64,6 +64,13 @@ SIGNATURES = {
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
     "grr_lnb_forward_rep": [P, I, I, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    # GLRFast / GTVFast sub-API
+    "grr_neighbor_gather": [P, P, I, I, I, I, P],
+    "grr_normalize_features": [P, P, P, I, I, I, I, I, P],
+    "grr_stats_conv": [P, Stencil, I, P, I, I, I, I, I, P],
+    "grr_glr_op_l_norm": [P, P, P, I, I, I, I, I, P],
+    "grr_gtv_op_c": [P, P, Stencil, P, I, I, I, I, I, P],
+    "grr_gtv_op_c_transpose": [P, P, Stencil, P, P, I, I, I, I, I, P],
     # reverse pass
     "grr_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
     "grr_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],

@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 from torch.nn.parameter import Parameter
 
-from . import kernels as K
+from . import ops as OPS
 from . import solver_grad as SG
 from .graph_filter import GLRFast, records_grad
 
@@ -54,16 +54,16 @@ class MixtureGLR(nn.Module):
     @torch.no_grad()
     def _solve(self, y):
         g, f = self.n_graphs, self.n_node_fts
-        feat = K.conv1x1(y, self.patchs_features_extraction[0].weight.data)
-        wL, _ = K.edge_weights(feat, 0, g, f, self.GLRmodule00.multiM.data)
+        feat = OPS.conv1x1(y, self.patchs_features_extraction[0].weight)
+        wL, _ = OPS.edge_weights(feat, 0, g, f, self.GLRmodule00.multiM)
         del feat
-        mu, alpha, beta = self.muys00.data, self.alphaCGD.data, self.betaCGD.data
-        st = K.stencil(self.GLRmodule00)
+        mu, alpha, beta = self.muys00, self.alphaCGD, self.betaCGD
+        L0 = self.GLRmodule00
         # stage 0: u0 = r0 = y - A y, x1 = y + a0 u0                      (REF10:316-318)
-        x, u = K.glr_stage(y, y, None, wL, st, mu, alpha[0], None, g)
+        x, u = OPS.glr_stage(y, y, None, wL, L0, mu, alpha[0], None, g, want_u=self.n_cgd_iters > 1)
         for k in range(1, self.n_cgd_iters):                          # (REF10:320-328)
-            x, u = K.glr_stage(x, y, u, wL, st, mu, alpha[k], beta[k], g, want_u=k < self.n_cgd_iters - 1,
-                               u_out=u)
+            x, u = OPS.glr_stage(x, y, u, wL, L0, mu, alpha[k], beta[k], g, want_u=k < self.n_cgd_iters - 1,
+                                 u_out=u)
         return x
 
 
@@ -130,22 +130,22 @@ class MultiScaleMixtureGLR(nn.Module):
     def _solve(self, y):
         g, f = self.n_graphs, self.n_node_fts
         s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
-        f0 = K.conv1x1(y, s0[0].weight.data)
-        f1 = K.conv1x1(K.conv2x2s2(y, s1[0].weight.data), s1[1].weight.data)
-        wL0, _ = K.edge_weights(f0, 0, g, f, self.GLRmodule00.multiM.data)
-        wL1, _ = K.edge_weights(f1, 0, g, f, self.GLRmodule01.multiM.data)
+        f0 = OPS.conv1x1(y, s0[0].weight)
+        f1 = OPS.conv1x1(OPS.conv2x2s2(y, s1[0].weight), s1[1].weight)
+        wL0, _ = OPS.edge_weights(f0, 0, g, f, self.GLRmodule00.multiM)
+        wL1, _ = OPS.edge_weights(f1, 0, g, f, self.GLRmodule01.multiM)
         del f0, f1
-        sL0, sL1 = K.stencil(self.GLRmodule00), K.stencil(self.GLRmodule01)
-        mu0, mu1 = self.muys00.data, self.muys01.data
-        alpha, beta = self.alphaCGD.data, self.betaCGD.data
+        L0, L1 = self.GLRmodule00, self.GLRmodule01
+        mu0, mu1 = self.muys00, self.muys01
+        alpha, beta = self.alphaCGD, self.betaCGD
         n_st = alpha.shape[0]
-        x, u, xd = y, None, K.pool2(y)
+        x, u, xd = y, None, OPS.pool2(y)
         for k in range(n_st):                                         # (REF10:316-328)
             last = k == n_st - 1
-            t = K.system_half(xd, wL1, None, sL1, K.NO_STENCIL, mu1, None, g)
-            x, u, xd = K.system_step(x, y, u, t, wL0, None, sL0, K.NO_STENCIL, mu0, None, alpha[k],
-                                     beta[k] if k >= 1 else None, g, want_u=not last, want_pool=not last,
-                                     u_out=u)
+            t = OPS.system_half(xd, wL1, None, L1, None, mu1, None, g)
+            x, u, xd = OPS.system_step(x, y, u, t, wL0, None, L0, None, mu0, None, alpha[k],
+                                       beta[k] if k >= 1 else None, g, want_u=not last, want_pool=not last,
+                                       u_out=u)
         return x
 
 
@@ -165,8 +165,8 @@ class MultiScaleGLRImageFilter(nn.Module):
             y = self.localfilter(SG.RepeatGraphsFn.apply(img, self.ngraphs))
             return SG.Conv1x1Fn.apply(y.contiguous(), self.linear_combination.weight)
         with torch.no_grad():
-            x = K.repeat_graphs(img, self.ngraphs)
-            return K.conv1x1(self.localfilter(x), self.linear_combination.weight.data)
+            x = OPS.repeat_graphs(img, self.ngraphs)
+            return OPS.conv1x1(self.localfilter(x), self.linear_combination.weight)
 
 
 class GLRImageFilter(nn.Module):
@@ -186,5 +186,5 @@ class GLRImageFilter(nn.Module):
             y = self.localfilter(SG.RepeatGraphsFn.apply(img, self.ngraphs))
             return SG.Conv1x1Fn.apply(y.contiguous(), self.linear_combination.weight)
         with torch.no_grad():
-            x = K.repeat_graphs(img, self.ngraphs)
-            return K.conv1x1(self.localfilter(x), self.linear_combination.weight.data)
+            x = OPS.repeat_graphs(img, self.ngraphs)
+            return OPS.conv1x1(self.localfilter(x), self.linear_combination.weight)

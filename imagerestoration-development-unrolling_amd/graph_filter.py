@@ -26,6 +26,7 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
+from . import ops as OPS
 from . import solver_grad as SG
 
 EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, down)
@@ -106,11 +107,33 @@ class _GraphModule(nn.Module):
     def _edge_weights(self, img_features: torch.Tensor):
         b, g, f, h, w = img_features.shape
         x = img_features.reshape(b, g * f, h, w).contiguous()
-        return K.edge_weights(x, 0, g, f, self.multiM.data.contiguous(), with_degree=True)
+        return OPS.edge_weights(x, 0, g, f, self.multiM, with_degree=True)
 
     def neighbor_table(self, h: int, w: int) -> torch.Tensor:
         """int32 [4,H,W] flat indices of the neighbours each edge reads (REF:128-144)."""
         return K.neighbor_table(h, w, self.multiM.device)
+
+    # -- the reference's module methods, standalone (the solver fuses them; csrc/subapi_ops.hip) --
+    # Their HIP forwards carry no reverse: under autograd, backward raises (hip_forward).
+    @hip_forward
+    def get_neighbors_pixels(self, img_features):
+        """[B,C,H,W] -> [B,C,4,H,W]: the replicate-clamped up/left/right/down neighbours (REF:128-144)."""
+        return OPS.neighbor_gather(img_features.contiguous())
+
+    @hip_forward
+    def normalize_and_transform_features(self, img_features):
+        """[B,G,F,H,W] -> [B,G*F,H,W]: L2-normalised over F (eps 1e-12), scaled by multiM (REF:146-157)."""
+        return OPS.normalize_features(img_features.contiguous(), self.multiM)
+
+    @hip_forward
+    def stats_conv(self, patchs):
+        """S x, depthwise 3x3 cross stencil with a replicate frame (REF:177-195)."""
+        return OPS.stats_conv(patchs.contiguous(), self, False)
+
+    @hip_forward
+    def stats_conv_transpose(self, patchs):
+        """S^T x, conv_transpose2d(padding=1) of the same stencil, zero frame (REF:197-215)."""
+        return OPS.stats_conv(patchs.contiguous(), self, True)
 
 
 class GLRFast(_GraphModule):
@@ -121,11 +144,16 @@ class GLRFast(_GraphModule):
             return SG.graph_apply(self, "glr", patchs, edge_weights)
         return self._hip_apply(patchs, edge_weights)
 
+    @hip_forward
+    def op_L_norm(self, img_signals, edge_weights, node_degree=None):
+        """x - sum_e w_e x(clamp(p + delta_e)) (REF:218-228); x [B,G,F,H,W], w [B,G,4,H,W]."""
+        return OPS.glr_op_L_norm(img_signals.contiguous(), edge_weights.contiguous())
+
     @torch.no_grad()
     def _hip_apply(self, patchs, edge_weights):
         b, g, f, h, w = patchs.shape
-        out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), edge_weights.contiguous(), None,
-                            K.stencil(self), K.NO_STENCIL, None, None, g)
+        out = OPS.system_half(patchs.reshape(b, g * f, h, w).contiguous(), edge_weights.contiguous(), None,
+                              self, None, None, None, g)
         return out.view(b, g, f, h, w)
 
 
@@ -137,12 +165,21 @@ class GTVFast(_GraphModule):
             return SG.graph_apply(self, "gtv", patchs, edge_weights)
         return self._hip_apply(patchs, edge_weights)
 
+    @hip_forward
+    def op_C(self, img_signals, edge_weights, node_degree=None):
+        """Edge signals E_e = w_e (S x - (S x)(clamp(p + delta_e))), [B,G,F,4,H,W] (REF:452-467)."""
+        return OPS.gtv_op_C(img_signals.contiguous(), edge_weights.contiguous(), self)
+
+    @hip_forward
+    def op_C_transpose(self, edge_signals, edge_weights, node_degree=None):
+        """S^T of the frame-dropped scatter of w_e E_e (REF:469-516) -> [B,G,F,H,W]."""
+        return OPS.gtv_op_C_transpose(edge_signals.contiguous(), edge_weights.contiguous(), self)
+
     @torch.no_grad()
     def _hip_apply(self, patchs, edge_weights):
         b, g, f, h, w = patchs.shape
-        c = K.gtv_pair_weights(edge_weights.contiguous())
-        out = K.system_half(patchs.reshape(b, g * f, h, w).contiguous(), None, c,
-                            K.NO_STENCIL, K.stencil(self), None, None, g)
+        c = OPS.gtv_pair_weights(edge_weights.contiguous())
+        out = OPS.system_half(patchs.reshape(b, g * f, h, w).contiguous(), None, c, None, self, None, None, g)
         return out.view(b, g, f, h, w)
 
 
@@ -206,21 +243,21 @@ class LocalNonLinearBlock(nn.Module):
         c, hid = self.dim, self.hidden_dim
         if c > 128 or self.nsubnets != 1:
             if x is None:
-                x = src.repeat(1, c // src.shape[1], 1, 1)
+                x = OPS.repeat_graphs(src, c // src.shape[1])
             return self._forward_hip(x)
-        return K.lnb_forward_rep(src, x, self.norm.weighted_transform.weight.data.view(c),
-                                 ll.channels_linear_op.weight.data.view(2 * hid, c),
-                                 ll.channels_local_linear_op.weight.data.view(2 * hid, 9),
-                                 ll.project_out.weight.data.view(c, hid), self.skip_weight.data)
+        return OPS.lnb_forward_rep(src, x, self.norm.weighted_transform.weight.view(c),
+                                   ll.channels_linear_op.weight.view(2 * hid, c),
+                                   ll.channels_local_linear_op.weight.view(2 * hid, 9),
+                                   ll.project_out.weight.view(c, hid), self.skip_weight)
 
     @hip_forward
     def _forward_hip(self, x):
         ll = self.local_linear
         c, hid = self.dim, self.hidden_dim
-        return K.lnb_forward(x.contiguous(), self.norm.weighted_transform.weight.data.view(c),
-                             ll.channels_linear_op.weight.data.view(2 * hid, c),
-                             ll.channels_local_linear_op.weight.data.view(2 * hid, 9),
-                             ll.project_out.weight.data.view(c, hid), self.skip_weight.data)
+        return OPS.lnb_forward(x.contiguous(), self.norm.weighted_transform.weight.view(c),
+                               ll.channels_linear_op.weight.view(2 * hid, c),
+                               ll.channels_local_linear_op.weight.view(2 * hid, 9),
+                               ll.project_out.weight.view(c, hid), self.skip_weight)
 
 
 # ---------------------------------------------------------------------------
@@ -279,28 +316,25 @@ class MixtureGTVGLR(nn.Module):
         the conv of the replicas equals the conv of src with the weights summed over the
         replicas: K = 4 Cin instead of 4 G Cin (same value up to fp32 summation order)."""
         if src is None:
-            return K.conv2x2s2(y, weight)
-        m, c = weight.shape[:2]
-        cin = src.shape[1]
-        folded = weight.reshape(m, c // cin, cin, 2, 2).sum(1).contiguous()
-        return K.conv2x2s2(src, folded)
+            return OPS.conv2x2s2(y, weight)
+        return OPS.conv2x2s2(src, weight, fold=True)
 
     def features(self, y: torch.Tensor, src: Optional[torch.Tensor] = None):
         s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
         if self.feature_extractor == "v1":
-            f0 = K.conv1x1(y, s0[0].weight.data)
-            f1 = K.conv1x1(self._down(y, s1[0].weight.data, src), s1[1].weight.data)
+            f0 = OPS.conv1x1(y, s0[0].weight)
+            f1 = OPS.conv1x1(self._down(y, s1[0].weight, src), s1[1].weight)
             return f0, f1
         blocks = list(s0)[:3]
         # the first block's input replicates src over the graphs: its GEMM1 runs on src (K = F)
         f0 = blocks[0].forward_replicated(src, y) if src is not None else blocks[0](y)
         for blk in blocks[1:]:
             f0 = blk(f0)
-        f0 = K.conv1x1(f0, s0[3].weight.data)
-        f1 = self._down(y, s1[0].weight.data, src)
+        f0 = OPS.conv1x1(f0, s0[3].weight)
+        f1 = self._down(y, s1[0].weight, src)
         for blk in list(s1)[1:4]:
             f1 = blk(f1)
-        f1 = K.conv1x1(f1, s1[4].weight.data)
+        f1 = OPS.conv1x1(f1, s1[4].weight)
         return f0, f1
 
     def features_train(self, y: torch.Tensor):
@@ -332,7 +366,7 @@ class MixtureGTVGLR(nn.Module):
             if src is None:
                 raise ValueError("MixtureGTVGLR: need y or src")
             if self.feature_extractor != "v13" or skip is not None:   # those paths read y itself
-                y = K.repeat_graphs(src, g)
+                y = OPS.repeat_graphs(src, g)
         ref = y if y is not None else src
         b, c, h, w = ref.shape
         if y is not None and c != self.n_channels:
@@ -342,47 +376,45 @@ class MixtureGTVGLR(nn.Module):
         if src is not None and (src.shape[1] != f or src.shape[0] != b or tuple(src.shape[2:]) != (h, w)):
             raise ValueError("MixtureGTVGLR: src must be [B, F, H, W]")
         f0, f1 = self.features(y, src)
-        d = lambda p: p.data  # noqa: E731  (parameters are read by the kernels through raw pointers)
-        wG0, cG0, wL0 = K.edge_weights_block(f0, g, f, d(self.GTVmodule00.multiM), d(self.GLRmodule00.multiM))
-        wG1, cG1, wL1 = K.edge_weights_block(f1, g, f, d(self.GTVmodule01.multiM), d(self.GLRmodule01.multiM))
+        G0, L0, G1, L1 = self.GTVmodule00, self.GLRmodule00, self.GTVmodule01, self.GLRmodule01
+        wG0, cG0, wL0 = OPS.edge_weights_block(f0, g, f, G0.multiM, L0.multiM)
+        wG1, cG1, wL1 = OPS.edge_weights_block(f1, g, f, G1.multiM, L1.multiM)
         del f0, f1
-        sG0, sL0 = K.stencil(self.GTVmodule00), K.stencil(self.GLRmodule00)
-        sG1, sL1 = K.stencil(self.GTVmodule01), K.stencil(self.GLRmodule01)
-        mu0, mu1, ro0, ro1 = d(self.muys00), d(self.muys01), d(self.ro00), d(self.ro01)
-        alpha, beta = d(self.alphaCGD), d(self.betaCGD)
+        mu0, mu1, ro0, ro1 = self.muys00, self.muys01, self.ro00, self.ro01
+        alpha, beta = self.alphaCGD, self.betaCGD
         n_st = alpha.shape[0]
 
         # rhs A: b_A = y + ro0 G0 y + ro1 U(G1 D y)                     (REF:738-749)
-        yd = K.pool2(y) if src is None else K.repeat_graphs(K.pool2(src), g)   # D y
-        t = K.gtv_rhs_half(yd, cG1, sG1, False, None, g)
+        yd = OPS.pool2(y) if src is None else OPS.repeat_graphs(OPS.pool2(src), g)   # D y
+        t = OPS.gtv_rhs_half(yd, cG1, G1, False, None, g)
         del yd
         if y is None:
-            b_a, xd = K.gtv_rhs_full_rep(src, True, src, True, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+            b_a, xd = OPS.gtv_rhs_full(src, True, src, True, cG0, G0, False, None, ro0, t, ro1, g, want_pool=True)
         else:
-            b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+            b_a, xd = OPS.gtv_rhs_full(y, False, y, False, cG0, G0, False, None, ro0, t, ro1, g, want_pool=True)
         # stage 0: x1 = b_A + alpha0 (b_A - A b_A)                     (REF:751-753)
         last = n_st == 1
-        t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
-        x, _, xd = K.system_step(b_a, b_a, None, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[0], None, g,
-                                 want_u=False, want_pool=not last, skip=skip if last else None,
-                                 y_skip=y if last else None)
+        t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
+        x, _, xd = OPS.system_step(b_a, b_a, None, t, wL0, cG0, L0, G0, mu0, ro0, alpha[0], None, g,
+                                   want_u=False, want_pool=not last, skip=skip if last else None,
+                                   y_skip=y if last else None)
         del b_a
         if last:
             return x
         # GTV proximal step -> rhs B                                   (REF:757-781)
-        t = K.gtv_rhs_half(xd, wG1, sG1, True, d(self.gamma01), g)
+        t = OPS.gtv_rhs_half(xd, wG1, G1, True, self.gamma01, g)
         if y is None:
-            b_b, _ = K.gtv_rhs_full_rep(x, False, src, True, wG0, sG0, True, d(self.gamma00), ro0, t, ro1, g)
+            b_b, _ = OPS.gtv_rhs_full(x, False, src, True, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
         else:
-            b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, d(self.gamma00), ro0, t, ro1, g)
+            b_b, _ = OPS.gtv_rhs_full(x, False, y, False, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
         del wG0, wG1
         u = None
         for k in range(1, n_st):                                     # (REF:784-790, :797-807)
             last = k == n_st - 1
-            t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
-            x, u, xd = K.system_step(x, b_b, u, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[k],
-                                     beta[k] if k >= 2 else None, g, want_u=not last, want_pool=not last,
-                                     skip=skip if last else None, y_skip=y if last else None, u_out=u)
+            t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
+            x, u, xd = OPS.system_step(x, b_b, u, t, wL0, cG0, L0, G0, mu0, ro0, alpha[k],
+                                       beta[k] if k >= 2 else None, g, want_u=not last, want_pool=not last,
+                                       skip=skip if last else None, y_skip=y if last else None, u_out=u)
         return x
 
     def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None,
@@ -414,7 +446,7 @@ class LocalLowpassFilteringBlock(nn.Module):
     def forward(self, x):
         if records_grad(self, x):
             return self.local_filter(x, _skip=self.skip_weight)
-        return self.local_filter(x, _skip=self.skip_weight.data)
+        return self.local_filter(x, _skip=self.skip_weight.detach())
 
 
 class MultiScaleGraphFilter(nn.Module):
@@ -442,7 +474,7 @@ class MultiScaleGraphFilter(nn.Module):
     def _forward_inference(self, img):
         # the G-fold replicated input (REF13:918-921) is never materialised: the solver reads img
         y = self.localfilter._solve(None, None, img)
-        return K.conv1x1(y, self.linear_combination.weight.data)
+        return OPS.conv1x1(y, self.linear_combination.weight)
 
 
 # ---------------------------------------------------------------------------

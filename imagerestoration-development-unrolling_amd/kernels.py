@@ -270,6 +270,75 @@ def step_bytes(b, c, g, h, w, has_rhs, has_u_prev, has_half, has_glr, has_gtv, h
     return 4 * b * h * w * f
 
 
+# ---- GLRFast / GTVFast sub-API (REF:128-228, :452-516) ---------------------------------
+def neighbor_gather(x: Tensor) -> Tensor:
+    """get_neighbors_pixels: [B,C,H,W] -> [B,C,4,H,W] replicate-clamped neighbours (REF:128-144)."""
+    dev = _check("neighbor_gather", x)
+    b, c, h, w = x.shape
+    out = torch.empty((b, c, 4, h, w), dtype=torch.float32, device=dev)
+    _launch("subapi", 4 * x.numel() * 5, "grr_neighbor_gather", x.data_ptr(), out.data_ptr(), b, c, h, w, _stream(dev))
+    return out
+
+
+def normalize_features(f5: Tensor, multiM: Tensor) -> Tensor:
+    """normalize_and_transform_features: [B,G,F,H,W] -> [B,G*F,H,W] (REF:146-157)."""
+    dev = _check("normalize_features", f5, multiM)
+    b, g, f, h, w = f5.shape
+    if tuple(multiM.shape) != (g, f):
+        raise ValueError(f"normalize_features: multiM {tuple(multiM.shape)} vs ({g}, {f})")
+    out = torch.empty((b, g * f, h, w), dtype=torch.float32, device=dev)
+    _launch("subapi", 8 * f5.numel(), "grr_normalize_features", f5.data_ptr(), multiM.data_ptr(), out.data_ptr(),
+            b, g, f, h, w, _stream(dev))
+    return out
+
+
+def stats_conv(x5: Tensor, st: Stencil, transpose: bool) -> Tensor:
+    """stats_conv (replicate) / stats_conv_transpose (zero frame) of [B,G,F,H,W] (REF:177-215)."""
+    dev = _check("stats_conv", x5)
+    b, g, f, h, w = x5.shape
+    out = torch.empty_like(x5)
+    _launch("subapi", 8 * x5.numel(), "grr_stats_conv", x5.data_ptr(), st, int(transpose), out.data_ptr(),
+            b, g, f, h, w, _stream(dev))
+    return out
+
+
+def glr_op_L_norm(x5: Tensor, w: Tensor) -> Tensor:
+    """GLRFast.op_L_norm: x - sum_e w_e x(clamp(p + delta_e)) (REF:218-228)."""
+    dev = _check("glr_op_L_norm", x5, w)
+    b, g, f, h, ww = x5.shape
+    if tuple(w.shape) != (b, g, 4, h, ww):
+        raise ValueError(f"glr_op_L_norm: edge weights {tuple(w.shape)} vs {(b, g, 4, h, ww)}")
+    out = torch.empty_like(x5)
+    _launch("subapi", 4 * (2 * x5.numel() + w.numel()), "grr_glr_op_l_norm", x5.data_ptr(), w.data_ptr(),
+            out.data_ptr(), b, g, f, h, ww, _stream(dev))
+    return out
+
+
+def gtv_op_C(x5: Tensor, w: Tensor, st: Stencil) -> Tensor:
+    """GTVFast.op_C: [B,G,F,H,W] -> edge signals [B,G,F,4,H,W] (REF:452-467)."""
+    dev = _check("gtv_op_C", x5, w)
+    b, g, f, h, ww = x5.shape
+    if tuple(w.shape) != (b, g, 4, h, ww):
+        raise ValueError(f"gtv_op_C: edge weights {tuple(w.shape)} vs {(b, g, 4, h, ww)}")
+    out = torch.empty((b, g, f, 4, h, ww), dtype=torch.float32, device=dev)
+    _launch("subapi", 4 * (5 * x5.numel() + w.numel()), "grr_gtv_op_c", x5.data_ptr(), w.data_ptr(), st,
+            out.data_ptr(), b, g, f, h, ww, _stream(dev))
+    return out
+
+
+def gtv_op_C_transpose(e6: Tensor, w: Tensor, st: Stencil) -> Tensor:
+    """GTVFast.op_C_transpose: edge signals [B,G,F,4,H,W] -> [B,G,F,H,W] (REF:469-516)."""
+    dev = _check("gtv_op_C_transpose", e6, w)
+    b, g, f, four, h, ww = e6.shape
+    if four != 4 or tuple(w.shape) != (b, g, 4, h, ww):
+        raise ValueError(f"gtv_op_C_transpose: edges {tuple(e6.shape)} / weights {tuple(w.shape)}")
+    work = torch.empty((b, g, f, h, ww), dtype=torch.float32, device=dev)
+    out = torch.empty_like(work)
+    _launch("subapi", 4 * (e6.numel() + w.numel() + 3 * work.numel()), "grr_gtv_op_c_transpose", e6.data_ptr(),
+            w.data_ptr(), st, work.data_ptr(), out.data_ptr(), b, g, f, h, ww, _stream(dev))
+    return out
+
+
 # ---- feature CNN -----------------------------------------------------------
 def conv1x1(x: Tensor, weight: Tensor) -> Tensor:
     """nn.Conv2d(K, M, 1, bias=False) with weight [M,K,1,1]."""

@@ -149,6 +149,32 @@ grr_status grr_glr_stage(const float* x, const float* b, const float* u_prev, co
                          const float* mu, const float* alpha, const float* beta, float* x_out, float* u_out,
                          int B, int G, int F, int H, int W, void* stream);
 
+/* ---- GLRFast / GTVFast sub-API (module methods outside the fused solver) -------------
+ * Standalone versions of the reference module methods, for callers of the module API (the
+ * solver itself fuses the same arithmetic into the operator kernels above).  Layouts as above;
+ * edge signals are [B,G,F,4,H,W] (REF:452-467). */
+
+/* get_neighbors_pixels (REF:128-144): out[b,c,e,p] = x[b,c,clamp(p + delta_e)], out [B,C,4,H,W]. */
+grr_status grr_neighbor_gather(const float* x, float* out, int B, int C, int H, int W, void* stream);
+/* normalize_and_transform_features (REF:146-157): out[b, g*F + f] = f / max(|f|_2 over F, 1e-12) * multiM[g,f]. */
+grr_status grr_normalize_features(const float* f, const float* multiM, float* out, int B, int G, int F, int H, int W,
+                                  void* stream);
+/* stats_conv (transpose == 0, replicate frame, REF:177-195) / stats_conv_transpose (transpose != 0,
+ * conv_transpose2d padding 1 = zero frame, REF:197-215) with the module's stencil. */
+grr_status grr_stats_conv(const float* x, grr_stencil s, int transpose, float* out, int B, int G, int F, int H, int W,
+                          void* stream);
+/* GLRFast.op_L_norm (REF:218-228): out = x - sum_e w_e x(clamp(p + delta_e)); x [B,G,F,H,W], w [B,G,4,H,W]. */
+grr_status grr_glr_op_l_norm(const float* x, const float* w, float* out, int B, int G, int F, int H, int W,
+                             void* stream);
+/* GTVFast.op_C (REF:452-467): edges[b,g,f,e,p] = w_e(p) (S x)(p) - w_e(p) (S x)(clamp(p + delta_e)). */
+grr_status grr_gtv_op_c(const float* x, const float* w, grr_stencil s, float* edges, int B, int G, int F, int H, int W,
+                        void* stream);
+/* GTVFast.op_C_transpose (REF:469-516): z_e = edges_e w_e; o(q) = sum_e z_e(q) - sum_e z_e(q - delta_e) for
+ * q - delta_e inside the image (scatters into the pad frame are dropped); out = S^T o.  work [B,G,F,H,W]
+ * is caller scratch (o). */
+grr_status grr_gtv_op_c_transpose(const float* edges, const float* w, grr_stencil s, float* work, float* out, int B,
+                                  int G, int F, int H, int W, void* stream);
+
 /* ---- feature CNN (MFMA fp32) ------------------------------------------------ */
 
 /* 1x1 convolution, no bias (nn.Conv2d(k=1, groups=1, bias=False); REF:556-566, REF13:623-632):

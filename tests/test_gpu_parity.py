@@ -537,3 +537,66 @@ def test_edge_weights_block_batch_independent_bitwise(irdu, bgfhw):
         one = irdu.kernels.edge_weights_block(feat[i:i + 1].contiguous(), g, f, mg, ml)
         for name, a, o in zip(("wG", "cG", "wL"), full, one):
             assert torch.equal(a[i], o[0]), (name, i)
+
+
+# ---------------------------------------------------------------------------
+# GLRFast / GTVFast sub-API methods (REF:128-228, :452-516) against the reference's own outputs
+def test_sub_api_golden(irdu):
+    d = load_golden("ops_small.npz")
+    feat = torch.from_numpy(d["in/feat"]).to(DEV)
+    x = torch.from_numpy(d["in/x"]).to(DEV)
+    b, g, f, h, w = x.shape
+    glr = irdu.GLRFast(f, g, 1.0)
+    gtv = irdu.GTVFast(f, g, 1.0)
+    glr.load_state_dict(params_of(d, "glr."))
+    gtv.load_state_dict(params_of(d, "gtv."))
+    glr, gtv = glr.to(DEV), gtv.to(DEV)
+    with torch.no_grad():
+        wl, dl = glr.extract_edge_weights(feat)
+        wg, dg = gtv.extract_edge_weights(feat)
+        assert_close(glr.stats_conv(x), d["out/glr_stats_conv"], 1e-5)
+        assert_close(glr.stats_conv_transpose(x), d["out/glr_stats_conv_t"], 1e-5)
+        assert_close(glr.op_L_norm(x, wl, dl), d["out/glr_op_L_norm"], 1e-5)
+        e = gtv.op_C(x, wg, dg)
+        assert_close(e, d["out/gtv_op_C"], 1e-5)
+        # op_C_transpose on the reference's own edge signals and on ours
+        assert_close(gtv.op_C_transpose(torch.from_numpy(d["out/gtv_op_C"]).to(DEV), wg, dg),
+                     d["out/gtv_op_C_transpose"], 1e-5)
+        assert_close(gtv.op_C_transpose(e, wg, dg), d["out/gtv_op_C_transpose"], 1e-5)
+        # composition = forward (REF:518-523, :231-237)
+        assert_close(gtv.op_C_transpose(gtv.op_C(x, wg), wg), gtv(x, wg), 1e-5)
+        assert_close(glr.stats_conv_transpose(glr.op_L_norm(glr.stats_conv(x), wl)), glr(x, wl), 1e-5)
+        # neighbour gather: the golden table is the gather of the flat index image
+        idx = torch.arange(h * w, dtype=torch.float32, device=DEV).view(1, 1, h, w)
+        nb = glr.get_neighbors_pixels(idx)
+        assert np.array_equal(nb[0, 0].to(torch.int32).cpu().numpy(), d["out/neighbor_table"])
+        # normalise + transform: the edge weights are its 4-way softmax of neighbour dot products
+        fn = glr.normalize_and_transform_features(feat).cpu()
+        assert_close(fn, O.normalize_features(feat.cpu(), glr.multiM.detach().cpu()), 1e-6)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 4, 17, 23), (1, 2, 6, 40, 300), (1, 1, 1, 1, 5)])
+def test_sub_api_random_vs_oracle(irdu, shape):
+    """Odd sizes, one-row images and W > 256 against the oracle restatement of the same methods."""
+    b, g, f, h, w = shape
+    x = rand(b, g, f, h, w, seed=61)
+    feat = rand(b, g, f, h, w, seed=62)
+    wl = torch.softmax(rand(b, g, 4, h, w, seed=63), dim=2)
+    glr = perturbed_graph_module(irdu.GLRFast(f, g, 1.0), 64)
+    gtv = perturbed_graph_module(irdu.GTVFast(f, g, 1.0), 65)
+    kl, kg = O.stats_kernel(sd_cpu(glr), ""), O.stats_kernel(sd_cpu(gtv), "")
+    glr, gtv = glr.to(DEV), gtv.to(DEV)
+    xd, wd = x.to(DEV), wl.to(DEV)
+    with torch.no_grad():
+        assert_close(glr.stats_conv(xd), O.stats_conv(x, kl), 1e-5)
+        assert_close(glr.stats_conv_transpose(xd), O.stats_conv_t(x, kl), 1e-5)
+        ref_l = x - torch.einsum("bgfehw,bgehw->bgfhw", O.gather_neighbors(x.reshape(b, g * f, h, w)).view(
+            b, g, f, 4, h, w), wl)
+        assert_close(glr.op_L_norm(xd, wd), ref_l, 1e-5)
+        e = gtv.op_C(xd, wd)
+        assert_close(e, O.gtv_C(x, wl, kg), 1e-5)
+        assert_close(gtv.op_C_transpose(e, wd), O.gtv_Ct(e.cpu(), wl, kg), 1e-5)
+        assert torch.equal(glr.get_neighbors_pixels(xd.reshape(b, g * f, h, w)).cpu(),
+                           O.gather_neighbors(x.reshape(b, g * f, h, w)))
+        assert_close(glr.normalize_and_transform_features(feat.to(DEV)),
+                     O.normalize_features(feat, glr.multiM.detach().cpu()), 1e-6)
