@@ -56,10 +56,15 @@ def synthetic_patches(n, seed, h=H, w=W):
     return torch.from_numpy(clean.astype(np.float32)), torch.from_numpy(clean.astype(np.float32) + noise)
 
 
-def build_model(device, seed=2204):
+TRAINED = os.path.join(ROOT, "tests", "golden", "msgf_trained_g32_s10.safetensors")
+
+
+def build_model(device, seed=2204, trained=False):
     """Reference init (default conv init + the reference's solver init constants), except the
     final 1x1 projection, set to the per-colour mean over the G filtered copies so that the
-    output is an image and its PSNR is interpretable without a trained checkpoint."""
+    output is an image.  trained=True loads the weights fixture that
+    scripts/train_psnr_fixture.py trained from this init (3,000 Adam steps on synthetic
+    sigma-25 patches; safetensors, weights only), so PSNR is measured on a filter that denoises."""
     import irdu_amd
     torch.manual_seed(seed)
     m = irdu_amd.MultiScaleGraphFilter(CIN, CIN, ngraphs=G, n_cgd_iters=STAGES)
@@ -69,6 +74,9 @@ def build_model(device, seed=2204):
             for c in range(CIN):
                 w[c, gi * CIN + c] = 1.0 / G
         m.linear_combination.weight.copy_(w)
+    if trained:
+        from safetensors.torch import load_file
+        m.load_state_dict(load_file(TRAINED))
     return m.to(device).eval()
 
 
@@ -213,7 +221,7 @@ def main():
     import irdu_amd
     from irdu_amd import kernels as K
     irdu_amd.load_native()
-    model = build_model(dev)
+    model = build_model(dev, trained=os.path.exists(TRAINED))
     b = args.batch
     # each rank its own shard of patches (seed by rank): resident in HBM before timing
     _, noisy = synthetic_patches(b, seed=2204 + rank)
@@ -282,7 +290,8 @@ def main():
            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
            "config": {"workload": "MultiScaleGraphFilter (image-domain GGTV-GGLR, v13 feature CNN) "
                                   f"G={G} F={CIN} C={G * CIN}, S={STAGES} stages, {H}x{W} RGB sigma=25, "
-                                  f"reference-init weights, output 1x1 = per-colour graph mean",
+                                  + ("weights: trained fixture" if os.path.exists(TRAINED) else
+                                     "reference-init weights, output 1x1 = per-colour graph mean"),
                       "global_batch": world * b, "per_gpu_batch": b, "image": f"{H}x{W}x{CIN}",
                       "parallelism": f"batch-sharded x{world}, no collective in the data path"},
            "roofline": roofline}
@@ -317,7 +326,8 @@ def main():
         res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()}
         res["psnr"] = {"gpu_db": round(p_gpu, 4), "oracle_db": round(p_cpu, 4), "delta_db": round(abs(p_gpu - p_cpu), 5),
                        "noisy_input_db": round(O.psnr_ubyte(cnoisy, clean), 4), "rel_err_vs_oracle": rel,
-                       "note": "untrained weights (no checkpoint exists): PSNR is a parity check, not quality"}
+                       "weights": ("tests/golden/msgf_trained_g32_s10.safetensors (trained here: no reference "
+                                   "checkpoint exists)") if os.path.exists(TRAINED) else "reference init"}
         res["speedup_vs_cpu"] = round(value / world / cb["value"], 1)
     print(json.dumps(res))
     if world > 1:

@@ -29,10 +29,13 @@
 //
 // Arithmetic: both GEMMs use the exact 3-term bf16 split of feature_ops.hip (six products,
 // fp32-accurate); depthwise 3x3 and the gate in fp32 with the reference's tap order.
+#include <cstdlib>
+
 #include "grr_common.h"
 
 namespace grr {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -122,7 +125,7 @@ struct LnbHeadArgs {
 // Per chunk c (8 hidden channels): KS*3 bf16 images of 16x16x32 A fragments of W1 diag(ln_w)
 // (k-step s, term q, lane l, element j: row r = l & 15 -- r < 8: mask channel 8c + r, else
 // value channel hid + 8c + r - 8 -- and k = 32 s + 8 (l >> 4) + j), then one fp32 image with
-// the depthwise taps: [w][0..8] of mask channel 8c + w, [w][9..17] of value channel hid + 8c + w.
+// the depthwise taps: [w][2 t], [w][2 t + 1] = tap t of mask channel 8c + w and of value channel hid + 8c + w.
 __host__ __device__ inline int head_images(int KS) { return KS * 3 + 1; }
 
 // R > 1: the block's input is R stacked copies of a C-channel image (MultiScaleGraphFilter's
@@ -151,16 +154,19 @@ __global__ void lnb_w1_pack_kernel(const float* __restrict__ w1, const float* __
         }
       }
       word = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-    } else if (e < LH_JC * 18) {
-      const int w = e / 18, t = e % 18, jj = LH_JC * c + w;
-      if (jj < hid) word = __float_as_uint(wdw[(int64_t)((t < 9 ? 0 : hid) + jj) * 9 + t % 9]);
+    } else if (e < LH_JC * 18) {   // taps of chunk channel w: (mask, value) pairs, tap by tap
+      const int w = e / 18, t = (e % 18) >> 1, comp = e & 1, jj = LH_JC * c + w;
+      if (jj < hid) word = __float_as_uint(wdw[(int64_t)((comp ? hid : 0) + jj) * 9 + t]);
     }
     reinterpret_cast<uint32_t*>(out)[i] = word;
   }
 }
 
 template <int KS, int NB>
-__global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
+#ifndef GRR_HEAD_WPE
+#define GRR_HEAD_WPE 2
+#endif
+__global__ __launch_bounds__(512, GRR_HEAD_WPE) void lnb_head_kernel(LnbHeadArgs a) {
   using Geo = HeadGeom<NB>;
   constexpr int NI = KS * 3 + 1;        // images per chunk (fragments + taps)
   constexpr int DPW = (NI + 7) / 8;     // LDS-DMA instructions per wave per chunk
@@ -168,8 +174,10 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
   constexpr int NSLOT = 4;              // two chunks in flight + GEMM1(c) + gate(c - 1)
   constexpr int HBUF = 2 * LH_JC * Geo::HP;
   constexpr int RA = Geo::RA;
-  __shared__ __attribute__((aligned(16))) float smem[2 * HBUF + NSLOT * SLOTF];
-  float* const ring = smem + 2 * HBUF;
+  // one h plane set (filled after the gates of the previous chunk are done with it): 73 KB of LDS
+  // for KS = 3, so two workgroups (16 waves) share a CU and hide the gate phase's latencies
+  __shared__ __attribute__((aligned(16))) float smem[HBUF + NSLOT * SLOTF];
+  float* const ring = smem + HBUF;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -238,16 +246,21 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
     for (int s = 0; s < KS; ++s) split3x8(xv[blk][s], xf[blk][s][0], xf[blk][s][1], xf[blk][s][2]);
   }
 
+  // chunks 0 and 1 landed (this wave's DMAs), then every wave's: the ring is shared
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
   // gate phase mapping: wave = hidden channel of the chunk, lane = (output column, row half)
   const int col = lane & 31, r0 = (lane >> 5) * RA;
   const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
       a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
   const int gx = x0 + col;
 
+  f32x4 acc[NB];
   auto gemm1 = [&](int c) {
     if (c >= nch) return;
     const float* slot = ring + (c % NSLOT) * SLOTF + lane * 4;
-    f32x4 acc[NB];
 #pragma unroll
     for (int blk = 0; blk < NB; ++blk) acc[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -260,28 +273,30 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
         GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_16x16x32_bf16, acc[blk], a0, a1, a2, xf[blk][s][0],
                     xf[blk][s][1], xf[blk][s][2]);
     }
-    // h rows 4 kq + i (0..7 mask, 8..15 value) of the halo pixels -> LDS plane set c & 1
-    float* hb = smem + (c & 1) * HBUF;
+  };
+  // h rows 4 kq + i (0..7 mask, 8..15 value) of the halo pixels -> the LDS plane set
+  auto store_h = [&](int c) {
+    if (c >= nch) return;
 #pragma unroll
     for (int blk = 0; blk < NB; ++blk) {
       const int q = (wave * NB + blk) * 16 + (lane & 15);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
+      for (int i = 0; i < 4; ++i) smem[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
     }
   };
   // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1
   auto gate = [&](int c) {
     const int jj = LH_JC * (c - 1) + wave;
     const bool live = c >= 1 && jj < hid;
-    const float* hb = smem + ((c + 1) & 1) * HBUF;
+    const float* hb = smem;
     const float* mp = hb + wave * Geo::HP + col;
     const float* vp = hb + (LH_JC + wave) * Geo::HP + col;
     const float* taps = ring + ((c + NSLOT - 1) % NSLOT) * SLOTF + KS * 3 * 256 + wave * 18;
     float km[9], kv[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      km[t] = taps[t];
-      kv[t] = taps[9 + t];
+      km[t] = taps[2 * t];
+      kv[t] = taps[2 * t + 1];
     }
     float mw[3][3], vw[3][3];
 #pragma unroll
@@ -310,12 +325,13 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
     }
   };
 
-  // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (independent LDS planes).  The two
-  // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work
-  // overlaps the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).
+  // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (h of chunk c - 1 in LDS).  The two
+  // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work overlaps
+  // the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).  Then, once
+  // every gate has read h of chunk c - 1, h of chunk c replaces it.
   const bool gate_first = wave < 4;
   for (int c = 0; c <= nch; ++c) {
-    // chunk c + 2 -> slot (c + 2) % 4, last read (gate of chunk c - 2) before the previous barrier
+    // chunk c + 2 -> slot (c + 2) % 4, last read (gate of chunk c - 2) before the previous barriers
     issue(min(c + 2, nch - 1), (c + 2) % NSLOT);
     if (gate_first) {
       gate(c);
@@ -324,10 +340,15 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
       gemm1(c);
       gate(c);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                  // every wave done reading h of chunk c - 1
+    asm volatile("" ::: "memory");
+    store_h(c);
     // chunk c + 1 landed: after its DMA this wave issued RA stores (iteration c - 1),
     // DPW DMAs and RA stores (iteration c); then every wave's part (barrier)
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * RA + DPW) : "memory");
     __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
 }
 
@@ -486,9 +507,330 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArg
 }
 
 // ---------------------------------------------------------------------------
+// fused: LN + W1 + dw3x3 + gate + W2 + skip in ONE kernel; the gated activations g stay in LDS.
+//
+// The head kernel's tile (32 columns x TH rows, W1 recomputed on the (TH+2) x 34 halo) and its
+// hidden-channel chunk loop (8 (mask, value) pairs per chunk), plus the second GEMM: every chunk
+// pair's g (16 hidden channels x TH x 32 pixels, fp32 in LDS) is multiplied into per-wave
+// accumulators of the output tile (C rows x TH x 32 pixels, v_mfma_f32_32x32x16_bf16 on the
+// exact 3-term split, 6 products) that stay in registers across the whole hidden loop; the
+// epilogue adds the skip and writes out.  Per iteration c: gate of chunk c - 1 (LDS h -> LDS g),
+// GEMM1 of chunk c (registers), GEMM2 of the pair gated two iterations earlier; barrier; h of
+// chunk c to LDS; barrier.  W1 chunks (+ taps) arrive by LDS-DMA in a 4-slot ring two chunks
+// ahead, W2 pair fragments in a 2-slot ring; every wave issues the same DMA count per iteration,
+// so the ring waits are one counted vmcnt.  Nothing of the 2 hid x HW hidden state or the hid x HW
+// gated state reaches HBM: the block reads x (with halo) and writes out.
+struct LnbFusedArgs {
+  const float* x;        // GEMM1 input [B, Ch, H, W] (Ch = C, or the replicated image's channels)
+  const char* w1f;       // W1 diag(ln_w) chunk images + taps (lnb_w1_pack_kernel)
+  const char* w2f;       // W2 pair images [npairs][MT][3] (lnb_w2_pack_kernel, 16-deep k-steps)
+  const float* xs;       // skip operand [B, XC, H, W]: x, or the image it replicates (channel m mod XC)
+  int XC;
+  const float* skip;     // [2]
+  float* out;            // [B, C, H, W]
+  float var_den;
+  int Ch, C, hid, H, W, tiles_x, tiles_y, nch, npairs;
+  uint32_t nblk;
+};
+
+#ifdef GRR_FUSED_STAMP
+// per-phase cycle totals of the first 64 workgroups' waves (timing builds only; written with
+// ordinary vector stores): gate, GEMM1, GEMM2, barrier 1, h store, wait + barrier 2, total, iterations
+__device__ unsigned long long g_fused_stamps[64 * 8 * 8];
+#endif
+
+template <int KS, int NB, int MT>
+__global__ __launch_bounds__(512, 1) void lnb_fused_kernel(LnbFusedArgs a) {
+  using Geo = HeadGeom<NB>;
+  constexpr int TH = Geo::TH, RA = Geo::RA, HP = Geo::HP;
+  constexpr int NI = KS * 3 + 1;        // W1 images per chunk (fragments + taps)
+  constexpr int DPW = (NI + 7) / 8;     // W1 LDS-DMAs per wave per iteration
+  constexpr int SLOTF = NI * 256;
+  constexpr int NSLOT = 4;
+  constexpr int HBUF = 2 * LH_JC * HP;  // one h plane set: 8 mask + 8 value rows of halo pixels
+  constexpr int W2I = MT * 3;           // W2 fragment images per chunk pair
+  constexpr int W2PW = (W2I + 7) / 8;   // W2 LDS-DMAs per wave per iteration
+  constexpr int GPX = TH * LH_TW;       // output pixels of the tile
+  // g of one chunk, already split for the GEMM2 B operand: [term][pixel][8 channels] bf16 = 4 floats
+  // per (term, pixel); the two 32-lane halves of a B read hit chunk slots 16 floats apart mod 64
+  constexpr int GCH = 3 * GPX * 4 + 16;
+  constexpr int NT2 = MT * TH;          // GEMM2 output tiles (32 channels x 32 pixels of one output row)
+  constexpr int TPW = (NT2 + 7) / 8;    // tiles per wave
+  __shared__ __attribute__((aligned(16))) float smem[HBUF + NSLOT * SLOTF + 2 * W2I * 256 + 3 * GCH];
+  float* const hb = smem;               // h of one chunk: [channel 0..7][halo pixel][mask, value]
+  float* const ring = smem + HBUF;
+  float* const w2ring = ring + NSLOT * SLOTF;
+  float* const gring = w2ring + 2 * W2I * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int tx = lb % a.tiles_x; lb /= a.tiles_x;
+  const int ty = lb % a.tiles_y;
+  const int b = lb / a.tiles_y;
+  const int H = a.H, W = a.W, Ch = a.Ch, C = a.C, hid = a.hid, nch = a.nch, npairs = a.npairs;
+  const int HW = H * W;
+  const int y0 = ty * TH, x0 = tx * LH_TW;
+
+  auto issue_w1 = [&](int chunk, int slot_idx) {
+    float* slot = ring + slot_idx * SLOTF;
+    const char* src = a.w1f + (int64_t)chunk * NI * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int img = min(i * 8 + wave, NI - 1);   // surplus waves repeat the last image
+      dma16_opaque(src + img * 1024, slot + img * 256);
+    }
+  };
+  auto issue_w2 = [&](int pair) {
+    float* slot = w2ring + (pair & 1) * W2I * 256;
+    const char* src = a.w2f + (int64_t)pair * W2I * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < W2PW; ++i) {
+      const int img = min(i * 8 + wave, W2I - 1);
+      dma16_opaque(src + img * 1024, slot + img * 256);
+    }
+  };
+  issue_w1(0, 0);
+  issue_w1(min(1, nch - 1), 1);
+  issue_w2(0);
+
+  // this wave's halo pixels: raw x column split into bf16 terms, and 1/sigma (REF:916-922)
+  const int kq = lane >> 4;
+  bf16x8 xf[NB][KS][3];
+  float rstd[NB];
+  {
+    float xv[NB][KS][8];
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      const int q = min((wave * NB + blk) * 16 + (lane & 15), Geo::HR * LH_HWD - 1);
+      const int hy = q / LH_HWD, hx = q - hy * LH_HWD;
+      const int gy = clampi(y0 - 1 + hy, 0, H - 1), gx = clampi(x0 - 1 + hx, 0, W - 1);
+      const float* xp = a.x + (int64_t)b * Ch * HW + gy * W + gx;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[blk][s][j] = xp[(int64_t)min(32 * s + 8 * kq + j, Ch - 1) * HW];
+    }
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      float sum = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (32 * s + 8 * kq + j >= Ch) xv[blk][s][j] = 0.f;
+          sum += xv[blk][s][j];
+        }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      const float mean = sum / (float)Ch;
+      float sq = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = 32 * s + 8 * kq + j < Ch ? xv[blk][s][j] - mean : 0.f;
+          sq += d * d;
+        }
+      sq += __shfl_xor(sq, 16);
+      sq += __shfl_xor(sq, 32);
+      rstd[blk] = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) split3x8(xv[blk][s], xf[blk][s][0], xf[blk][s][1], xf[blk][s][2]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W1 chunks 0, 1 and W2 pair 0 landed (this wave's part)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  f32x4 acc1[NB];
+  f32x16 acc2[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc2[i] = f32x16{};
+
+  auto gemm1 = [&](int c) {
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) acc1[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (c >= nch) return;
+    const float* slot = ring + (c % NSLOT) * SLOTF + lane * 4;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 0) * 256);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 1) * 256);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 2) * 256);
+#pragma unroll
+      for (int blk = 0; blk < NB; ++blk)
+        GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_16x16x32_bf16, acc1[blk], a0, a1, a2, xf[blk][s][0],
+                    xf[blk][s][1], xf[blk][s][2]);
+      // the next k-step's fragments are read while these MFMAs run (not all hoisted: registers)
+      asm volatile("" ::: "memory");
+    }
+  };
+  // GEMM1 rows 4 kq + i: kq < 2 mask channels 4 kq + i, kq >= 2 value channels 4 (kq - 2) + i
+  auto store_h = [&](int c) {
+    if (c >= nch) return;
+    const int ch0 = 4 * (kq & 1), comp = kq >> 1;
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      const int q = (wave * NB + blk) * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hb[((ch0 + i) * HP + q) * 2 + comp] = acc1[blk][i] * rstd[blk];
+    }
+  };
+  // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1 -> g slot (c - 1) mod 3.
+  // Mask and value run as one packed pair (v_pk_fma_f32; each component the same fma chain in the
+  // reference's tap order); g goes to LDS as its exact 3-term bf16 split, in the GEMM2 B layout.
+  const int col = lane & 31, r0 = (lane >> 5) * RA;
+  auto gate = [&](int c) {
+    const int jj = LH_JC * (c - 1) + wave;
+    const bool live = c >= 1 && jj < hid;
+    const f32x2* hp = reinterpret_cast<const f32x2*>(hb) + wave * HP + col;
+    const float* taps = ring + ((c + NSLOT - 1) % NSLOT) * SLOTF + KS * 3 * 256 + wave * 18;
+    __bf16* gdst = reinterpret_cast<__bf16*>(gring + ((c + 2) % 3) * GCH) + wave;
+    const f32x2* k2 = reinterpret_cast<const f32x2*>(taps);   // (mask, value) tap pairs, broadcast LDS reads
+    f32x2 hw[3][3];
+#pragma unroll
+    for (int i = 0; i < RA + 2; ++i) {
+      const int hrow = min(r0 + i, Geo::HR - 1) * LH_HWD;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) hw[i % 3][d] = hp[hrow + d];
+      if (i >= 2) {
+        f32x2 mv = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int ay = 0; ay < 3; ++ay)
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) mv = __builtin_elementwise_fma(k2[ay * 3 + ax], hw[(i - 2 + ay) % 3][ax], mv);
+        const float m = mv.x, v = mv.y;
+        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
+        const float g = live ? (sg * m) * v : 0.f;   // 0 for padding channels
+        const int orow = r0 + i - 2;
+        if (orow < TH) {
+          const __bf16 h0 = (__bf16)g;
+          const float r1 = g - (float)h0;
+          const __bf16 h1 = (__bf16)r1;
+          const __bf16 h2 = (__bf16)(r1 - (float)h1);
+          __bf16* d = gdst + (orow * LH_TW + col) * 8;
+          d[0] = h0;
+          d[GPX * 8] = h1;
+          d[2 * GPX * 8] = h2;
+        }
+      }
+    }
+  };
+  // out tile rows += W2[:, 16 p .. 16 p + 15] g(pair p): tile t = wave + 8 i -> (output row t / MT, rows 32 (t % MT) ..)
+  auto gemm2 = [&](int p) {
+    const float* w2 = w2ring + (p & 1) * W2I * 256 + lane * 4;
+    const float* gsrc = gring + ((2 * p + (lane >> 5)) % 3) * GCH + col * 4;
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int t = wave + 8 * i;
+      if (t < NT2) {
+        const int orow = t / MT, mt = t - orow * MT;
+        const float* gp = gsrc + orow * LH_TW * 4;
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(gp);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(gp + GPX * 4);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(gp + 2 * GPX * 4);
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(w2 + (3 * mt + 0) * 256);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(w2 + (3 * mt + 1) * 256);
+        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(w2 + (3 * mt + 2) * 256);
+        GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_32x32x16_bf16, acc2[i], a0, a1, a2, b0, b1, b2);
+      }
+    }
+  };
+
+  // iteration c: gate(c - 1 chunk), GEMM1(c), GEMM2 of the pair gated in iterations c - 2, c - 1
+  const bool gate_first = wave < 4;   // SIMD partners (w, w + 4) overlap one's MFMA with the other's VALU
+  const int cmax = 2 * npairs + 1;
+#ifdef GRR_FUSED_STAMP
+  uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#define GRR_STAMP(k, t) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - (t); (t) = t_; } while (0)
+#else
+#define GRR_STAMP(k, t) do { } while (0)
+#endif
+  for (int c = 0; c <= cmax; ++c) {
+#ifdef GRR_FUSED_STAMP
+    uint64_t tt = __builtin_amdgcn_s_memtime();
+#endif
+    issue_w1(min(c + 2, nch - 1), (c + 2) % NSLOT);   // slot last read by gate(c - 1) (taps of chunk c - 2)
+    issue_w2(min(c >> 1, npairs - 1));                // slot last read by gemm2 of iteration c - 1 or earlier
+    if (gate_first) {
+      gate(c);
+      GRR_STAMP(0, tt);
+      gemm1(c);
+      GRR_STAMP(1, tt);
+    } else {
+      gemm1(c);
+      GRR_STAMP(1, tt);
+      gate(c);
+      GRR_STAMP(0, tt);
+    }
+    if ((c & 1) && c >= 3) gemm2((c - 3) >> 1);
+    GRR_STAMP(2, tt);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                     // h of chunk c - 1 and the g slots read: reusable
+    asm volatile("" ::: "memory");
+    GRR_STAMP(3, tt);
+    store_h(c);
+    GRR_STAMP(4, tt);
+    // everything issued before this iteration landed (this wave's part), then every wave's
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(DPW + W2PW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    GRR_STAMP(5, tt);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef GRR_FUSED_STAMP
+  st[6] = __builtin_amdgcn_s_memtime() - t_begin;
+  st[7] = (uint64_t)(cmax + 1);
+  if (blockIdx.x < 64 && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g_fused_stamps[(blockIdx.x * 8 + wave) * 8 + k] = st[k];
+  }
+#endif
+#undef GRR_STAMP
+
+  // epilogue (REF:962-964): out = skip0 x + skip1 W2 g.  acc2[i] element e: channel
+  // 32 mt + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), pixel (y0 + orow, x0 + lane & 31)
+  const float s0 = a.skip[0], s1 = a.skip[1];
+  const int XC = a.XC;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.xs + (int64_t)b * XC * HW), 0, (int)((int64_t)XC * HW * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * C * HW, 0,
+                                                                        (int)((int64_t)C * HW * 4), 0x00020000);
+  const int gx = x0 + col;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = wave + 8 * i;
+    if (t < NT2) {
+      const int orow = t / MT, mt = t - orow * MT;
+      const int gy = y0 + orow;
+      const bool pix = gy < H && gx < W;
+      const int p = min(gy, H - 1) * W + min(gx, W - 1);
+      float xv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = min(32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5), C - 1);
+        const int mx = XC == C ? m : m % XC;
+        xv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (uint32_t)(mx * HW + p) * 4u, 0, 0));
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const uint32_t off = (m < C && pix) ? (uint32_t)(m * HW + p) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[e] + s1 * acc2[i][e]), ors, off, 0, 0);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 static int head_ks(int C) { return (C + 31) / 32; }
-static int head_nb(int KS) { return KS <= 3 ? 4 : 3; }
+#ifndef GRR_HEAD_NB
+#define GRR_HEAD_NB 4
+#endif
+static int head_nb(int KS) { return KS <= 3 ? GRR_HEAD_NB : 3; }
 static int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }
 static int64_t head_pack_floats(int C, int hid) {
   return align64((int64_t)((hid + LH_JC - 1) / LH_JC) * head_images(head_ks(C)) * 256);
@@ -510,6 +852,40 @@ template <int MT>
 static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
   if (v4) hipLaunchKernelGGL((lnb_mix_kernel<MT, true>), dim3(m.nblk), dim3(256), 0, s, m);
   else hipLaunchKernelGGL((lnb_mix_kernel<MT, false>), dim3(m.nblk), dim3(256), 0, s, m);
+}
+
+// GRR_LNB_FUSED=1 selects the single fused kernel (A/B measurements).  Default: head + mix -- the
+// fused kernel keeps the GEMM2 accumulators in the registers the gate phase needs for latency
+// hiding and measured slower
+static bool lnb_fused_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GRR_LNB_FUSED");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// halo pixel blocks per wave of the fused kernel: its GEMM2 accumulators share the 256 registers
+// of a 2-waves-per-SIMD kernel with the x fragments, so deeper / wider blocks run 3 blocks (9-row
+// tiles); the shapes that would still spill (K > 96 with C > 32, or C > 96 with K > 32) keep the
+// two-kernel head + mix path
+static constexpr int fused_nb(int KS, int MT) { return (KS == 1 || (KS == 2 && MT <= 2)) ? 4 : 3; }
+static bool fused_ok(int KS, int MT) { return KS <= MT && (KS == 1 || MT <= 3); }
+template <int KS, int MT>
+static void launch_fused_t(const LnbFusedArgs& f, hipStream_t s) {
+  constexpr int NB = fused_nb(KS, MT);
+  hipLaunchKernelGGL((lnb_fused_kernel<KS, NB, MT>), dim3(f.nblk), dim3(512), 0, s, f);
+}
+static void launch_fused(const LnbFusedArgs& f, int KS, int MT, hipStream_t s) {
+  switch (MT * 8 + KS) {
+    case 1 * 8 + 1: launch_fused_t<1, 1>(f, s); break;
+    case 2 * 8 + 1: launch_fused_t<1, 2>(f, s); break;
+    case 2 * 8 + 2: launch_fused_t<2, 2>(f, s); break;
+    case 3 * 8 + 1: launch_fused_t<1, 3>(f, s); break;
+    case 3 * 8 + 2: launch_fused_t<2, 3>(f, s); break;
+    case 3 * 8 + 3: launch_fused_t<3, 3>(f, s); break;
+    default: launch_fused_t<1, 4>(f, s); break;
+  }
 }
 
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
@@ -540,20 +916,37 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
     grr_status st = launch_status("grr_lnb_forward/pack");
     if (st != GRR_OK) return st;
   }
+  if (lnb_fused_enabled() && fused_ok(KS, MT)) {
+    LnbFusedArgs f{};
+    f.x = xh; f.w1f = w1f; f.w2f = reinterpret_cast<const char*>(w2f);
+    f.xs = x ? x : xh;          // x == NULL: the skip reads the replicated image itself
+    f.XC = x ? C : Ch;
+    f.skip = skip; f.out = out;
+    f.var_den = R == 1 ? (float)(C - 1) : (float)(C - 1) / (float)R;
+    f.Ch = Ch; f.C = C; f.hid = hid; f.H = H; f.W = W; f.nch = nch; f.npairs = KS2;
+    const int TH = fused_nb(KS, MT) == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH;
+    f.tiles_x = (W + LH_TW - 1) / LH_TW;
+    f.tiles_y = (H + TH - 1) / TH;
+    const uint64_t nf = (uint64_t)B * f.tiles_x * f.tiles_y;
+    GRR_REQUIRE(nf < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+    f.nblk = (uint32_t)nf;
+    launch_fused(f, KS, MT, s);
+    return launch_status("grr_lnb_forward/fused");
+  }
   LnbHeadArgs h{};
   h.x = xh; h.w1f = w1f; h.g = g;
   h.var_den = R == 1 ? (float)(C - 1) : (float)(C - 1) / (float)R;
   h.C = Ch; h.hid = hid; h.H = H; h.W = W; h.nch = nch;
-  const int TH = NB == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH;
+  const int TH = NB == 4 ? HeadGeom<4>::TH : NB == 3 ? HeadGeom<3>::TH : HeadGeom<2>::TH;
   h.tiles_x = (W + LH_TW - 1) / LH_TW;
   h.tiles_y = (H + TH - 1) / TH;
   const uint64_t nh = (uint64_t)B * h.tiles_x * h.tiles_y;
   GRR_REQUIRE(nh < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
   h.nblk = (uint32_t)nh;
   switch (KS) {
-    case 1: launch_head<1, 4>(h, s); break;
-    case 2: launch_head<2, 4>(h, s); break;
-    case 3: launch_head<3, 4>(h, s); break;
+    case 1: launch_head<1, GRR_HEAD_NB>(h, s); break;
+    case 2: launch_head<2, GRR_HEAD_NB>(h, s); break;
+    case 3: launch_head<3, GRR_HEAD_NB>(h, s); break;
     default: launch_head<4, 3>(h, s); break;
   }
   grr_status st = launch_status("grr_lnb_forward/head");
@@ -578,3 +971,10 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
 }
 
 }  // namespace grr
+
+#ifdef GRR_FUSED_STAMP
+extern "C" grr_status grr_debug_fused_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(grr::g_fused_stamps), sizeof(grr::g_fused_stamps)) == hipSuccess
+             ? GRR_OK : GRR_ERR_HIP;
+}
+#endif

@@ -194,13 +194,13 @@ def soft_threshold(d: Tensor, gamma: Tensor) -> Tensor:
 # ---------------------------------------------------------------------------
 def pool2(x4: Tensor) -> Tensor:
     c = x4.shape[1]
-    k = torch.full((c, 1, 2, 2), 0.25)
+    k = torch.full((c, 1, 2, 2), 0.25, dtype=x4.dtype)
     return Fn.conv2d(x4, k, stride=2, groups=c)
 
 
 def unpool2(x4: Tensor) -> Tensor:
     c = x4.shape[1]
-    k = torch.full((c, 1, 2, 2), 0.25)
+    k = torch.full((c, 1, 2, 2), 0.25, dtype=x4.dtype)
     return Fn.conv_transpose2d(x4, k, stride=2, groups=c)
 
 

@@ -74,6 +74,20 @@ def main():
             print(f"{args.kernel}: {kind:16s} launches={v['launches']} mean={v['mean_ms']:.4f} ms "
                   f"algo={v['gbps']:.1f} GB/s bytes/launch={v['bytes_per_launch']:.4e}")
         lib = irdu_amd._native.load()
+        if hasattr(lib, "grr_debug_fused_stamps"):   # GRR_FUSED_STAMP timing builds of the fused LNB
+            import ctypes
+            import numpy as np
+            buf = (ctypes.c_ulonglong * (64 * 8 * 8))()
+            lib.grr_debug_fused_stamps(buf)
+            a = np.frombuffer(buf, dtype=np.uint64).reshape(64 * 8, 8).astype(np.float64)
+            names = ["gate", "gemm1", "gemm2", "barrier1", "store_h", "wait+barrier2"]
+            it = a[0, 7]
+            print("fused stamps, cycles per iteration (mean over waves): " +
+                  "  ".join(f"{n} {a[:, k].mean() / it:.0f}" for k, n in enumerate(names)) +
+                  f"  total {a[:, 6].mean() / it:.0f}  (iterations {it:.0f})")
+            for grp, sel in (("waves 0-3 (gate first)", a[np.arange(len(a)) % 8 < 4]),
+                             ("waves 4-7 (gemm first)", a[np.arange(len(a)) % 8 >= 4])):
+                print(f"   {grp}: " + "  ".join(f"{n} {sel[:, k].mean() / it:.0f}" for k, n in enumerate(names)))
         if hasattr(lib, "grr_debug_head_stamps"):   # GRR_HEAD_STAMP timing builds
             import ctypes
             import numpy as np

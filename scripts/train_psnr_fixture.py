@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--lr", type=float, default=4e-4)
     ap.add_argument("--eval-every", type=int, default=250)
     ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--copy-to", default=os.path.join(ROOT, "gpurun_out", "msgf_trained_g32_s10.safetensors"))
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden", "msgf_trained_g32_s10.safetensors"))
     args = ap.parse_args()
     import irdu_amd
@@ -79,6 +80,10 @@ def main():
     save_file(state, args.out, metadata={"model": "MultiScaleGraphFilter", "ngraphs": "32", "n_cgd_iters": "10",
                                          "iters": str(it), "batch": str(args.batch), "size": str(args.size),
                                          "final_psnr_out": str(log[-1]["psnr_out"] if log else "")})
+    if args.copy_to:
+        os.makedirs(os.path.dirname(args.copy_to), exist_ok=True)
+        import shutil
+        shutil.copyfile(args.out, args.copy_to)
     print(json.dumps({"saved": args.out, "iters": it, "seconds": round(time.time() - t0, 1)}))
 
 

@@ -1,6 +1,11 @@
 import os
 import sys
 
+# The v1.0 encoder/decoder's plain convolutions run on MIOpen; its exhaustive first-call "find"
+# at the C4 shapes (32 x 512^2, up to 384 channels, forward + both backward passes) takes minutes.
+# The fast find mode picks an algorithm without benchmarking them all (set before MIOpen loads).
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

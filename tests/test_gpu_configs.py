@@ -134,6 +134,7 @@ C4_CFG = dict(dims=(48, 96, 192, 384), hidden_dims=(96, 192, 384, 768), nsubnets
               ngraphs=(8, 16, 16, 32), num_blocks=(4, 6, 6, 8), num_blocks_out=4)
 
 
+@pytest.mark.timeout(900)
 def test_c4_per_rank_training_step(irdu):
     """One training step of config C4's per-rank shard: 32 x 512x512 RGB sigma 25 through the v1.0
     model with S = 10 in all four filter blocks and the v2 script's losses (L1 + 0.1 MSE(enc-dec)
@@ -172,25 +173,32 @@ def test_c4_per_rank_training_step(irdu):
 
 # ---------------------------------------------------------------------------
 # C5: 2048x2048 tiled inference
+@pytest.mark.timeout(600)
 def test_c5_tiled_2048_vs_whole_image_and_oracle(irdu):
-    """C5: a 2048x2048 RGB sigma-25 image filtered as 256x256 overlap-save windows (halo 32, the
-    bench default) equals the whole-image HIP filter to fp32 rounding; the whole-image output on a
-    central 128x128 region equals the CPU oracle run on a 320x320 crop around it (96-px margin ->
-    beyond the filter's receptive field, see tiling.py)."""
+    """C5: a 2048x2048 RGB sigma-25 image filtered as 256x256 overlap-save windows equals the
+    whole-image HIP filter to within 1e-5 relative at the bench's halo (32 px), with the trained
+    weights fixture (trained-scale solver coefficients; tests/test_gpu_psnr.py).  The analytic
+    receptive field is far wider (tiling.py: ~130 px), so the error is measured at halos 16 / 32 /
+    64 and printed.  The whole-image output on a central 128x128 region equals the CPU oracle run
+    on a 320x320 crop around it (96-px margin: the filter's influence at that distance is below
+    fp32 rounding, shown by the halo sweep)."""
     from irdu_amd import tiling
     from bench import build_model, synthetic_patches
-    m = build_model(torch.device("cpu"))
-    perturb_mixture(m.localfilter, 90)
+    m = build_model(torch.device("cpu"), trained=True)
+    state = sd_cpu(m)
     m = m.to(DEV)
     _, noisy = synthetic_patches(1, seed=2205, h=2048, w=2048)
     x = noisy.to(DEV)
     with torch.no_grad():
         whole = m(x)
-    tiled = tiling.tiled_forward(m, x, tile=256, halo=32, align=16, micro_batch=64)
-    err = rel_err(tiled, whole)
-    print(f"\nC5 tiled (halo 32) vs whole image: rel err {err:.2e}")
-    assert err <= 1e-4
+    errs = {}
+    for halo in (16, 32, 64):
+        tiled = tiling.tiled_forward(m, x, tile=256, halo=halo, align=16, micro_batch=64)
+        errs[halo] = rel_err(tiled, whole)
+        del tiled
+    print(f"\nC5 tiled vs whole image (trained weights), rel err by halo: {errs}")
+    assert errs[32] <= 1e-5 and errs[64] <= errs[16]
     r0, c0 = 960, 960
     crop = noisy[:, :, r0 - 96:r0 + 128 + 96, c0 - 96:c0 + 128 + 96].contiguous()
-    ref = O.multiscale_graph_filter(crop, sd_cpu(m), 32)[:, :, 96:96 + 128, 96:96 + 128]
+    ref = O.multiscale_graph_filter(crop, state, 32)[:, :, 96:96 + 128, 96:96 + 128]
     assert_close(whole[:, :, r0:r0 + 128, c0:c0 + 128], ref)
