@@ -98,6 +98,13 @@ __device__ __forceinline__ void dma16_opaque(const void* src, float* lds_wave_ba
 #define GRR_HEAD_OPAQUE_DMA 1
 #endif
 
+#ifdef GRR_FUSED_STAMP
+// per-phase cycle totals of the first 64 workgroups' waves of the head or fused kernel (timing builds
+// only; ordinary vector stores): gate, GEMM1, GEMM2, barrier 1 / vmcnt wait, h store, (wait +) barrier,
+// total, iterations
+__device__ unsigned long long g_fused_stamps[64 * 8 * 8];
+#endif
+
 // ---------------------------------------------------------------------------
 // head: LN + W1 + dw3x3 + gate
 constexpr int LH_TW = 32;           // output columns per tile
@@ -163,10 +170,7 @@ __global__ void lnb_w1_pack_kernel(const float* __restrict__ w1, const float* __
 }
 
 template <int KS, int NB>
-#ifndef GRR_HEAD_WPE
-#define GRR_HEAD_WPE 2
-#endif
-__global__ __launch_bounds__(512, GRR_HEAD_WPE) void lnb_head_kernel(LnbHeadArgs a) {
+__global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
   using Geo = HeadGeom<NB>;
   constexpr int NI = KS * 3 + 1;        // images per chunk (fragments + taps)
   constexpr int DPW = (NI + 7) / 8;     // LDS-DMA instructions per wave per chunk
@@ -174,10 +178,8 @@ __global__ __launch_bounds__(512, GRR_HEAD_WPE) void lnb_head_kernel(LnbHeadArgs
   constexpr int NSLOT = 4;              // two chunks in flight + GEMM1(c) + gate(c - 1)
   constexpr int HBUF = 2 * LH_JC * Geo::HP;
   constexpr int RA = Geo::RA;
-  // one h plane set (filled after the gates of the previous chunk are done with it): 73 KB of LDS
-  // for KS = 3, so two workgroups (16 waves) share a CU and hide the gate phase's latencies
-  __shared__ __attribute__((aligned(16))) float smem[HBUF + NSLOT * SLOTF];
-  float* const ring = smem + HBUF;
+  __shared__ __attribute__((aligned(16))) float smem[2 * HBUF + NSLOT * SLOTF];
+  float* const ring = smem + 2 * HBUF;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -257,10 +259,10 @@ __global__ __launch_bounds__(512, GRR_HEAD_WPE) void lnb_head_kernel(LnbHeadArgs
       a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
   const int gx = x0 + col;
 
-  f32x4 acc[NB];
   auto gemm1 = [&](int c) {
     if (c >= nch) return;
     const float* slot = ring + (c % NSLOT) * SLOTF + lane * 4;
+    f32x4 acc[NB];
 #pragma unroll
     for (int blk = 0; blk < NB; ++blk) acc[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -273,22 +275,20 @@ __global__ __launch_bounds__(512, GRR_HEAD_WPE) void lnb_head_kernel(LnbHeadArgs
         GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_16x16x32_bf16, acc[blk], a0, a1, a2, xf[blk][s][0],
                     xf[blk][s][1], xf[blk][s][2]);
     }
-  };
-  // h rows 4 kq + i (0..7 mask, 8..15 value) of the halo pixels -> the LDS plane set
-  auto store_h = [&](int c) {
-    if (c >= nch) return;
+    // h rows 4 kq + i (0..7 mask, 8..15 value) of the halo pixels -> LDS plane set c & 1
+    float* hb = smem + (c & 1) * HBUF;
 #pragma unroll
     for (int blk = 0; blk < NB; ++blk) {
       const int q = (wave * NB + blk) * 16 + (lane & 15);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) smem[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
+      for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
     }
   };
   // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1
   auto gate = [&](int c) {
     const int jj = LH_JC * (c - 1) + wave;
     const bool live = c >= 1 && jj < hid;
-    const float* hb = smem;
+    const float* hb = smem + ((c + 1) & 1) * HBUF;
     const float* mp = hb + wave * Geo::HP + col;
     const float* vp = hb + (LH_JC + wave) * Geo::HP + col;
     const float* taps = ring + ((c + NSLOT - 1) % NSLOT) * SLOTF + KS * 3 * 256 + wave * 18;
@@ -325,31 +325,50 @@ __global__ __launch_bounds__(512, GRR_HEAD_WPE) void lnb_head_kernel(LnbHeadArgs
     }
   };
 
-  // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (h of chunk c - 1 in LDS).  The two
-  // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work overlaps
-  // the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).  Then, once
-  // every gate has read h of chunk c - 1, h of chunk c replaces it.
+  // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (independent LDS planes).  The two
+  // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work
+  // overlaps the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).
   const bool gate_first = wave < 4;
+#ifdef GRR_FUSED_STAMP
+  uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#define GRR_STAMP(k, t) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - (t); (t) = t_; } while (0)
+#else
+#define GRR_STAMP(k, t) do { } while (0)
+#endif
   for (int c = 0; c <= nch; ++c) {
-    // chunk c + 2 -> slot (c + 2) % 4, last read (gate of chunk c - 2) before the previous barriers
+#ifdef GRR_FUSED_STAMP
+    uint64_t tt = __builtin_amdgcn_s_memtime();
+#endif
+    // chunk c + 2 -> slot (c + 2) % 4, last read (gate of chunk c - 2) before the previous barrier
     issue(min(c + 2, nch - 1), (c + 2) % NSLOT);
     if (gate_first) {
       gate(c);
+      GRR_STAMP(0, tt);
       gemm1(c);
+      GRR_STAMP(1, tt);
     } else {
       gemm1(c);
+      GRR_STAMP(1, tt);
       gate(c);
+      GRR_STAMP(0, tt);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                  // every wave done reading h of chunk c - 1
-    asm volatile("" ::: "memory");
-    store_h(c);
     // chunk c + 1 landed: after its DMA this wave issued RA stores (iteration c - 1),
     // DPW DMAs and RA stores (iteration c); then every wave's part (barrier)
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * RA + DPW) : "memory");
+    GRR_STAMP(3, tt);
     __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    GRR_STAMP(5, tt);
   }
+#ifdef GRR_FUSED_STAMP
+  st[6] = __builtin_amdgcn_s_memtime() - t_begin;
+  st[7] = (uint64_t)(nch + 1);
+  if (blockIdx.x < 64 && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g_fused_stamps[(blockIdx.x * 8 + wave) * 8 + k] = st[k];
+  }
+#endif
+#undef GRR_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -533,11 +552,6 @@ struct LnbFusedArgs {
   uint32_t nblk;
 };
 
-#ifdef GRR_FUSED_STAMP
-// per-phase cycle totals of the first 64 workgroups' waves (timing builds only; written with
-// ordinary vector stores): gate, GEMM1, GEMM2, barrier 1, h store, wait + barrier 2, total, iterations
-__device__ unsigned long long g_fused_stamps[64 * 8 * 8];
-#endif
 
 template <int KS, int NB, int MT>
 __global__ __launch_bounds__(512, 1) void lnb_fused_kernel(LnbFusedArgs a) {
@@ -827,10 +841,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused_kernel(LnbFusedArgs a) {
 // ---------------------------------------------------------------------------
 // host side
 static int head_ks(int C) { return (C + 31) / 32; }
-#ifndef GRR_HEAD_NB
-#define GRR_HEAD_NB 4
-#endif
-static int head_nb(int KS) { return KS <= 3 ? GRR_HEAD_NB : 3; }
+static int head_nb(int KS) { return KS <= 3 ? 4 : 3; }
 static int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }
 static int64_t head_pack_floats(int C, int hid) {
   return align64((int64_t)((hid + LH_JC - 1) / LH_JC) * head_images(head_ks(C)) * 256);
@@ -937,16 +948,16 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   h.x = xh; h.w1f = w1f; h.g = g;
   h.var_den = R == 1 ? (float)(C - 1) : (float)(C - 1) / (float)R;
   h.C = Ch; h.hid = hid; h.H = H; h.W = W; h.nch = nch;
-  const int TH = NB == 4 ? HeadGeom<4>::TH : NB == 3 ? HeadGeom<3>::TH : HeadGeom<2>::TH;
+  const int TH = NB == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH;
   h.tiles_x = (W + LH_TW - 1) / LH_TW;
   h.tiles_y = (H + TH - 1) / TH;
   const uint64_t nh = (uint64_t)B * h.tiles_x * h.tiles_y;
   GRR_REQUIRE(nh < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
   h.nblk = (uint32_t)nh;
   switch (KS) {
-    case 1: launch_head<1, GRR_HEAD_NB>(h, s); break;
-    case 2: launch_head<2, GRR_HEAD_NB>(h, s); break;
-    case 3: launch_head<3, GRR_HEAD_NB>(h, s); break;
+    case 1: launch_head<1, 4>(h, s); break;
+    case 2: launch_head<2, 4>(h, s); break;
+    case 3: launch_head<3, 4>(h, s); break;
     default: launch_head<4, 3>(h, s); break;
   }
   grr_status st = launch_status("grr_lnb_forward/head");
