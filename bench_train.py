@@ -25,6 +25,63 @@ D_ARGS = dict(dims=[48, 96, 192, 384], hidden_dims=[96, 192, 384, 768], nsubnets
               ngraphs=[8, 16, 16, 32], num_blocks=[4, 6, 6, 8], num_blocks_out=4)
 
 
+HBM_PEAK_GBPS = 8000.0
+
+
+def reverse_roofline(kern):
+    """Roofline of the dominant reverse-sweep kernel kind: algorithmic bytes per launch
+    (kernels.py byte model of each reverse pass) / its mean HIP-event launch time."""
+    cands = {k: v for k, v in kern.items() if k.startswith("bwd") and v["bytes_per_launch"] > 0}
+    if not cands:
+        return None
+    k, v = max(cands.items(), key=lambda kv: kv[1]["total_ms"])
+    return {"bound": "hbm", "kernel": k, "achieved": round(v["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(v["gbps"] / HBM_PEAK_GBPS, 4), "traffic": None,
+            "bytes_per_launch": v["bytes_per_launch"], "mean_launch_ms": round(v["mean_ms"], 4),
+            "launches": v["launches"]}
+
+
+def cpu_baseline(model, model_kind, size, runs=3):
+    """The oracle's differentiable restatement of the same model (PyTorch-CPU fp32, the
+    reference's op sequence) for one optimisation step -- forward, L1 loss, autograd reverse,
+    Adam -- on one size x size patch; threads = the CPUs this process may use; median of runs."""
+    import statistics
+    from bench import cpu_model, host_cpus, synthetic_patches
+    from oracle import graph_oracle as O
+    n_cpu, usable = host_cpus()
+    threads = min(n_cpu, usable)
+    torch.set_num_threads(threads)
+    names = {k for k, _ in model.named_parameters()}
+    state = {k: v.detach().cpu().clone().requires_grad_(k in names) for k, v in model.state_dict().items()}
+    params = [v for v in state.values() if v.requires_grad]
+    opt = torch.optim.Adam(params, lr=4e-4, eps=1e-8)
+    clean, noisy = synthetic_patches(1, seed=99, h=size, w=size)
+
+    def fwd(x):
+        if model_kind == "msgf":
+            return O.multiscale_graph_filter(x, state, 32)
+        return O.abstract_forward(x, state, D_ARGS["ngraphs"], D_ARGS["num_blocks"], D_ARGS["num_blocks_out"],
+                                  D_ARGS["nsubnets"])
+
+    def step(x, c):
+        opt.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.l1_loss(fwd(x), c)
+        loss.backward()
+        opt.step()
+
+    step(noisy[..., :32, :32], clean[..., :32, :32])   # warm-up
+    times = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        step(noisy, clean)
+        times.append(time.perf_counter() - t0)
+    dt = statistics.median(times)
+    return {"value": round(size * size / dt / 1e6, 6), "unit": "MPix/s", "cores": threads, "kind": "port",
+            "sample": f"1 patch {size}x{size} RGB sigma=25, forward + L1 + autograd reverse + Adam: median of "
+                      f"{runs} steps {dt:.2f} s (runs {', '.join(f'{t:.2f}' for t in times)}) on {cpu_model()}",
+            "os_cpu_count": n_cpu, "usable_cpus": usable}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", choices=["abstract", "msgf"], default="abstract")
@@ -35,6 +92,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--aux-losses", action="store_true", help="add the enc-dec / latent-perturbation losses")
     ap.add_argument("--breakdown", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-size", type=int, default=None,
+                    help="CPU-baseline patch side (default: --size for msgf, 128 for the v1.0 model)")
     ap.add_argument("--fused-fts", type=str, default=None,
                     help="comma list of F that use the one-pass term reverses (default: all instances)")
     args = ap.parse_args()
@@ -107,6 +167,11 @@ def main():
                "loss": loss, "hip_kernel_ms_per_step": round(hip_ms, 2),
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                "kernel_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}}
+        res["roofline"] = reverse_roofline(kern)
+        if not args.no_cpu_baseline and world == 1:
+            cb = cpu_baseline(model, args.model, args.cpu_size or (args.size if args.model == "msgf" else 128))
+            res["cpu_baseline"] = cb
+            res["speedup_vs_cpu"] = round(res["value"] / cb["value"], 1)
         if args.breakdown:
             for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
                 print(f"{k:20s} launches/step={v['launches'] / args.steps:6.1f} mean={v['mean_ms']:8.3f} ms "

@@ -118,10 +118,83 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], bucket_mb: float =
     for bucket in buckets:
         flat = torch.cat([p.grad.reshape(-1) for p in bucket])
         dist.all_reduce(flat, group=group)
-        flat.div_(ws)
-        off = 0
-        for p in bucket:
-            n = p.numel()
-            p.grad.copy_(flat[off:off + n].view_as(p.grad))
-            off += n
+        _unflatten_mean(flat, bucket, ws)
     return len(buckets)
+
+
+def _unflatten_mean(flat: torch.Tensor, bucket: Sequence[torch.Tensor], ws: int) -> None:
+    flat.div_(ws)
+    off = 0
+    for p in bucket:
+        n = p.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        off += n
+
+
+class OverlappedGradReducer:
+    """Gradient average whose all-reduces run while the backward pass is still producing
+    gradients (the DDP reducer's schedule, written for this path).
+
+    Parameters are bucketed in REVERSE registration order -- the order the reverse sweep
+    finishes them: the solver's scalars and edge stencils (whose gradients the one-Function
+    HIP solver reverse returns first) before the feature CNN's weights.  A
+    post-accumulate-grad hook counts each parameter in; when a bucket is complete it is
+    flattened and handed to an asynchronous all_reduce (RCCL runs it on its own stream,
+    ordered after the producing kernels), so the collective overlaps the CNN's reverse.
+    Buckets launch strictly in index order on every rank (a bucket that completes early
+    waits for its predecessors), so ranks issue identical collective sequences.
+    ``finish()`` launches what backward never reached (parameters without a gradient this
+    step contribute zeros), waits, and writes the averages back into ``.grad``.
+    """
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 32.0, group=None):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.ws = world()[1]
+        self.buckets = _buckets(self.params[::-1], int(bucket_mb * 2 ** 20))
+        self._bucket_of = {id(p): i for i, bk in enumerate(self.buckets) for p in bk}
+        self._hooks = []
+        if self.ws > 1:
+            self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self.launched_in_backward = 0
+        self._reset()
+
+    def _reset(self):
+        self._pending = [len(bk) for bk in self.buckets]
+        self._next = 0
+        self._work = [None] * len(self.buckets)
+        self._flat = [None] * len(self.buckets)
+
+    def _on_grad(self, p):
+        i = self._bucket_of[id(p)]
+        self._pending[i] -= 1
+        while self._next < len(self.buckets) and self._pending[self._next] <= 0:
+            self._launch(self._next)
+            self.launched_in_backward += 1
+
+    def _launch(self, i: int):
+        bk = self.buckets[i]
+        for p in bk:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self._flat[i] = torch.cat([p.grad.reshape(-1) for p in bk])
+        self._work[i] = dist.all_reduce(self._flat[i], group=self.group, async_op=True)
+        self._next = i + 1
+
+    def finish(self) -> int:
+        """Complete this step's average; returns the bucket count (0 on one rank)."""
+        if self.ws == 1 or not self.buckets:
+            return 0
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+        for i, bk in enumerate(self.buckets):
+            self._work[i].wait()
+            _unflatten_mean(self._flat[i], bk, self.ws)
+        n = len(self.buckets)
+        self._reset()
+        return n
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -16,7 +16,8 @@ The reference's run_train.py stops after building the dataloader; the YAML here 
 ``model:`` and ``train:`` sections so the same entry point runs the training loop of the
 v2 scripts.  Multi-GPU: one process per GPU (torchrun); every rank trains on its own
 slice of each global batch and gradients are averaged with bucketed RCCL all-reduces
-(sharding.allreduce_gradients) — the only collective of the path.
+(sharding.OverlappedGradReducer, launched from backward hooks so they overlap the
+reverse sweep) — the only collective of the path.
 
 Datasets: no image data ships with the reference, so ``SyntheticNoisyPatches`` (seeded
 procedural clean patches, the same noise law) is the default; the CSV/PNG dataset type
@@ -251,6 +252,8 @@ class Trainer:
         self.w_perturb = float(tconf.get("loss03_weight", 0.5))
         self.latent_noise = float(tconf.get("latent_noise", 0.05))
         self.bucket_mb = float(tconf.get("allreduce_bucket_mb", 32.0))
+        # all-reduces overlapped with the reverse sweep (post-accumulate-grad hooks); inert on one rank
+        self.reducer = sharding.OverlappedGradReducer(self.model.parameters(), bucket_mb=self.bucket_mb)
         self.i = 0
 
     def loss(self, noisy: torch.Tensor, clean: torch.Tensor) -> torch.Tensor:
@@ -273,7 +276,7 @@ class Trainer:
         clean = clean_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
         loss = self.loss(noisy, clean)
         loss.backward()
-        sharding.allreduce_gradients(self.model.parameters(), bucket_mb=self.bucket_mb)
+        self.reducer.finish()
         self.optimizer.step()
         self.lr_scheduler.step()
         self.i += 1

@@ -63,11 +63,18 @@ def _worker(rank, world_size, port, result_q):
         _loss(params, xs, ts).backward()
         nb = sharding.allreduce_gradients(params.values(), bucket_mb=0.001)
         grads = {k: (p.grad * world_size).clone() for k, p in params.items()}
+        # the same average with the all-reduces launched from backward hooks
+        params2 = {k: torch.nn.Parameter(v.clone()) for k, v in base.items()}
+        red = sharding.OverlappedGradReducer(list(params2.values()), bucket_mb=0.001)
+        _loss(params2, xs, ts).backward()
+        nb2 = red.finish()
+        early = red.launched_in_backward
+        grads2 = {k: (p.grad * world_size).numpy() for k, p in params2.items()}
         # PSNR reduction across ranks
         clean = torch.rand(4, 3, 8, 8)
         rest = (clean + 0.02 * torch.randn(4, 3, 8, 8)).clamp(0, 1)
         psnr = sharding.global_psnr_ubyte(sharding.shard_batch(rest), sharding.shard_batch(clean))
-        result_q.put((rank, nb, {k: v.numpy() for k, v in grads.items()}, psnr))
+        result_q.put((rank, nb, {k: v.numpy() for k, v in grads.items()}, psnr, nb2, early, grads2))
     finally:
         dist.destroy_process_group()
 
@@ -93,10 +100,12 @@ def test_data_parallel_gradients_match_single_process():
     clean = torch.rand(4, 3, 8, 8)
     rest = (clean + 0.02 * torch.randn(4, 3, 8, 8)).clamp(0, 1)
     full_psnr = sharding.global_psnr_ubyte(rest, clean)
-    for rank, nb, grads, psnr in results:
-        assert nb > 1  # several buckets exercised
+    for rank, nb, grads, psnr, nb2, early, grads2 in results:
+        assert nb > 1 and nb2 == nb  # several buckets exercised
+        assert early >= 1            # buckets were reduced while backward was still running
         for k, p in params.items():
             ref = p.grad.numpy()
-            err = abs(grads[k] - ref).max() / max(abs(ref).max(), 1e-12)
-            assert err < 1e-5, (k, err)
+            for gr in (grads, grads2):
+                err = abs(gr[k] - ref).max() / max(abs(ref).max(), 1e-12)
+                assert err < 1e-5, (k, err)
         assert abs(psnr - full_psnr) < 1e-9
