@@ -55,6 +55,8 @@ SIGNATURES = {
     "grr_gtv_rhs_full": [P, P, P, Stencil, I, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_gtv_rhs_full_rep": [P, I, P, I, P, Stencil, I, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_system_step": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_system_step2": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P,
+                         P, P, P, I, I, I, I, I, P],
     "grr_glr_stage": [P, P, P, P, Stencil, P, P, P, P, P, I, I, I, I, I, P],
     "grr_conv1x1": [P, P, P, I, I, I, L, P],
     "grr_conv1x1_workspace_bytes": [I, I],

@@ -1291,6 +1291,452 @@ static bool launch_edge_row(EdgeArgs a, int B, int F, hipStream_t s) {
 
 static bool stencil_ok(const grr_stencil& s) { return s.p01 && s.p02a && s.p02b && s.p03; }
 
+// ---------------------------------------------------------------------------
+// Two CG stages per pass: temporal blocking of grr_system_step (GLR + GTV pair, W = 256).
+//
+// Stage k+1 consumes stage k's rows a few rows behind inside the same workgroup, so
+// x_{k+1} and u_{k+1} never reach HBM and the full-level edge weights are read once for
+// both stages.  One workgroup = the F channel waves of one (b, graph, row segment) + one
+// producer wave; one workgroup per CU (≈156 KiB of LDS), one wave per SIMD.  Per iteration
+// (two image rows) each channel wave runs three register pipelines of the operator
+// (OpPipe: x -> s = S x -> {l, o} -> S^T, the arithmetic of graph_row_kernel's consume):
+//   stage A   = stage k at full resolution: x_k rows from HBM, t_k (the half-level term of
+//               x_k, from the preceding grr_system_half) from HBM; writes x_{k+1} and u_{k+1}
+//               rows into private LDS rings and D x_{k+1} half rows into a third ring;
+//   half      = the half-level operator (mu1 L1 + ro1 G1) of D x_{k+1}, 128-wide rows, two
+//               half columns per lane: t_{k+1}, kept in registers;
+//   stage B   = stage k+1 at full resolution, 8 rows behind stage A: x_{k+1} / u_{k+1} from the
+//               rings, t_{k+1} from registers; writes x_{k+2}, u_{k+2} and D x_{k+2} to HBM.
+// Row timeline at step t (two steps per iteration): stage A loads x_k row t and emits row
+// t-3; the half pipeline reads D x half row (t-4)/2 - 1 (one row late, so its replicate
+// clamp at the top reads a row that exists) and emits half row (t-11)/2; stage B reads
+// x_{k+1} row t-8 and emits row t-11.  The rings are read with the rows clamped to the
+// image (the replicate boundary the HBM loads apply), and rows outside the image are never
+// written into them.  A segment's stage A starts 6 rows before its stage B needs exact
+// rows (ts = r0 - 9).  The producer wave streams the full-level weight row pairs (7-pair
+// ring: stage A uses pair i, stage B pair i-4, pairs i+1, i+2 in flight) and the half-level
+// weight rows (4-row ring) with LDS-DMA, two iterations ahead.
+// ---------------------------------------------------------------------------
+struct Step2Args {
+  const float* x;
+  const float* b;
+  const float* u_prev;
+  const float* t_half;
+  const float* wL0;
+  const float* cG0;
+  const float* wL1;
+  const float* cG1;
+  grr_stencil sL0, sG0, sL1, sG1;
+  const float* log_mu0;
+  const float* log_ro0;
+  const float* log_mu1;
+  const float* log_ro1;
+  const float* alpha_a;
+  const float* beta_a;
+  const float* alpha_b;
+  const float* beta_b;
+  const float* skip;
+  const float* y;
+  float* out;
+  float* u_out;
+  float* xd_out;
+  int G, F, H, nsegs, sseg;
+  uint32_t nblk;
+};
+
+template <int V>
+struct OpPipe {
+  float X0[V], X1[V], X2[V], X3[V];
+  float SL0[V], SL1[V], SL2[V], SG0[V], SG1[V], SG2[V];
+  float L0[V], L1[V], L2[V], O0[V], O1[V], O2[V];
+  float cv[V];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      X0[j] = X1[j] = X2[j] = X3[j] = 0.f;
+      SL0[j] = SL1[j] = SL2[j] = SG0[j] = SG1[j] = SG2[j] = 0.f;
+      L0[j] = L1[j] = L2[j] = O0[j] = O1[j] = O2[j] = 0.f;
+      cv[j] = 0.f;
+    }
+  }
+
+  // push input row t (replicate-clamped by the caller) and the edge-weight row t-2 (4 GLR
+  // planes, 2 pair planes); returns S_L^T (I - W) S_L x and S_G^T C^T C S_G x at row t-3
+  // (before the mu / ro scales).  Lane = V adjacent columns starting at c0.
+  __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
+                                          int t, int H, int W, int c0, const Taps& tL, const Taps& tG,
+                                          float (&tl)[V], float (&tg)[V]) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) { X0[j] = X1[j]; X1[j] = X2[j]; X2[j] = X3[j]; X3[j] = xin[j]; }
+    {  // s at row t-1
+      const float xp = lane_prev(X2[V - 1]), xq = lane_next(X2[0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        const float xl = col > 0 ? (j > 0 ? X2[j - 1] : xp) : X2[j];
+        const float xr = col < W - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
+        float sv = tL.u * X1[j];
+        sv += tL.l * xl; sv += tL.c * X2[j]; sv += tL.r * xr; sv += tL.d * X3[j];
+        SL0[j] = SL1[j]; SL1[j] = SL2[j]; SL2[j] = sv;
+        float sg = tG.u * X1[j];
+        sg += tG.l * xl; sg += tG.c * X2[j]; sg += tG.r * xr; sg += tG.d * X3[j];
+        SG0[j] = SG1[j]; SG1[j] = SG2[j]; SG2[j] = sg;
+      }
+    }
+    {  // l and o at row r = t-2 (zero outside the image)
+      const int r = t - 2;
+      const bool rin = r >= 0 && r < H;
+      const float pv = lane_prev(SL1[V - 1]), nx = lane_next(SL1[0]);
+      const float sp = lane_prev(SG1[V - 1]), sn = lane_next(SG1[0]);
+      const float wp = lane_prev(WG[0][V - 1]);
+      float l[V], o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        const float up = r > 0 ? SL0[j] : SL1[j];
+        const float dn = r < H - 1 ? SL2[j] : SL1[j];
+        const float lf = col > 0 ? (j > 0 ? SL1[j - 1] : pv) : SL1[j];
+        const float rt = col < W - 1 ? (j < V - 1 ? SL1[j + 1] : nx) : SL1[j];
+        const float wx = ((WL[0][j] * up + WL[1][j] * lf) + WL[2][j] * rt) + WL[3][j] * dn;
+        l[j] = (rin && col < W) ? SL1[j] - wx : 0.f;
+        const float sv = SG1[j];
+        const float snx = j < V - 1 ? SG1[j + 1] : sn;
+        const float spv = j > 0 ? SG1[j - 1] : sp;
+        const float chl = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
+        const float cvu = r > 0 ? cv[j] : 0.f;
+        const float ov = WG[0][j] * (sv - snx) + chl * (sv - spv) + WG[1][j] * (sv - SG2[j]) + cvu * (sv - SG0[j]);
+        o[j] = (rin && col < W) ? ov : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        L0[j] = L1[j]; L1[j] = L2[j]; L2[j] = l[j];
+        cv[j] = WG[1][j]; O0[j] = O1[j]; O1[j] = O2[j]; O2[j] = o[j];
+      }
+    }
+    {  // S^T at row t-3 (neighbours outside are 0)
+      const float lp = lane_prev(L1[V - 1]), ln = lane_next(L1[0]);
+      const float op = lane_prev(O1[V - 1]), on = lane_next(O1[0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float nx = j < V - 1 ? L1[j + 1] : ln, pv = j > 0 ? L1[j - 1] : lp;
+        float v = tL.u * L2[j];
+        v += tL.l * nx; v += tL.c * L1[j]; v += tL.r * pv; v += tL.d * L0[j];
+        tl[j] = v;
+        const float gx = j < V - 1 ? O1[j + 1] : on, gp = j > 0 ? O1[j - 1] : op;
+        float w = tG.u * O2[j];
+        w += tG.l * gx; w += tG.c * O1[j]; w += tG.r * gp; w += tG.d * O0[j];
+        tg[j] = w;
+      }
+    }
+  }
+};
+
+constexpr int S2_W = 256, S2_HW = 128;    // full / half row width
+constexpr int S2_WP = 7;                   // weight-ring row pairs
+constexpr int S2_HR = 4;                   // half-weight ring rows
+constexpr int S2_XR = 8;                   // x_{k+1} ring rows (per channel)
+constexpr int S2_UR = 10;                  // u_{k+1} ring rows (per channel)
+constexpr int S2_DR = 4;                   // D x_{k+1} ring half rows (per channel)
+constexpr int S2_FMAX = 3;                 // channel waves per graph
+constexpr int S2_PAIR = 2 * 6 * S2_W;      // floats per weight-ring pair
+constexpr int S2_HROW = 6 * S2_HW;         // floats per half-weight ring row
+constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW + S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW);
+static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
+
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void graph_step2_kernel(Step2Args a) {
+  constexpr int V = 4, VH = 2;
+  typedef typename VecT<4>::type F4;
+  typedef typename VecT<2>::type F2;
+  __shared__ __attribute__((aligned(16))) float lds[S2_LDS];
+  float* const wring = lds;
+  float* const hring = wring + S2_WP * S2_PAIR;
+  float* const xring = hring + S2_HR * S2_HROW;
+  float* const uring = xring + S2_FMAX * S2_XR * S2_W;
+  float* const dring = uring + S2_FMAX * S2_UR * S2_W;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int F = a.F;
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk);
+  const int seg = unit % a.nsegs; unit /= a.nsegs;
+  const int g = unit % a.G;
+  const int b = unit / a.G;
+  const int H = a.H, W = S2_W, h = H / 2, hw = S2_HW;
+  const int64_t HW = (int64_t)H * W, hHW = (int64_t)h * hw;
+  const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
+  const int ts = r0 - 9;                 // first step (odd offset from r0: step t emits stage-A row t-3)
+  const int NI = (r1 + 11 - ts) / 2;     // stage B emits rows up to r1 - 1
+
+  if (wave == F) {   // producer: weight rows -> LDS rings (LDS-DMA), two iterations ahead
+    const float* pwl0 = a.wL0 + (int64_t)(b * a.G + g) * 4 * HW;
+    const float* pcg0 = a.cG0 + (int64_t)(b * a.G + g) * 2 * HW;
+    const float* pwl1 = a.wL1 + (int64_t)(b * a.G + g) * 4 * hHW;
+    const float* pcg1 = a.cG1 + (int64_t)(b * a.G + g) * 2 * hHW;
+    auto dma = [&](const float* src, float* dst) {
+      const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)dst;
+      asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
+                   : "memory");
+    };
+    auto dma_pair = [&](int p) {   // full-level weight rows of steps ts+2p, ts+2p+1 (rows t-2)
+      float* slot = wring + (p % S2_WP) * S2_PAIR;
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        const int64_t rw = (int64_t)clampi(ts + 2 * p + par - 2, 0, H - 1) * W + 4 * lane;
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+          dma(e < 4 ? pwl0 + e * HW + rw : pcg0 + (e - 4) * HW + rw, slot + (par * 6 + e) * S2_W);
+      }
+    };
+    auto dma_half = [&](int p) {   // half-level weight row of iteration p (its l/o row)
+      const int hr = clampi((ts + 2 * p - 3) / 2 - 3, 0, h - 1);
+      float* slot = hring + (p % S2_HR) * S2_HROW;
+      const int pl = lane >> 5;   // lanes 0-31: plane 2e, lanes 32-63: plane 2e+1
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int plane = 2 * e + pl;
+        const float* src = (plane < 4 ? pwl1 + plane * hHW : pcg1 + (plane - 4) * hHW) + (int64_t)hr * hw +
+                           (lane & 31) * 4;
+        dma(src, slot + e * 2 * S2_HW);
+      }
+    };
+    dma_pair(0);
+    dma_half(0);
+    dma_pair(1);
+    dma_half(1);
+    asm volatile("s_waitcnt vmcnt(15)" ::: "memory");   // iteration 0's rows landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int i = 0; i < NI; ++i) {
+      dma_pair(i + 2);
+      dma_half(i + 2);
+      asm volatile("s_waitcnt vmcnt(15)" ::: "memory");  // iteration i+1's rows landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---- channel wave f
+  const int f = wave;
+  const int C = a.G * F, ch = g * F + f;
+  const int64_t plane = ((int64_t)b * C + ch) * HW, hplane = ((int64_t)b * C + ch) * hHW;
+  const int64_t PB = HW * 4, HPB = hHW * 4;
+  const bool use_beta_a = a.beta_a != nullptr && a.u_prev != nullptr;
+  const bool use_beta_b = a.beta_b != nullptr;
+  const bool use_skip = a.skip != nullptr;
+  const rsrc_t rx = make_rsrc(a.x + plane, PB);
+  const rsrc_t rb = make_rsrc(a.b + plane, PB);
+  const rsrc_t ru = make_rsrc(use_beta_a ? a.u_prev + plane : nullptr, PB);
+  const rsrc_t rth = make_rsrc(a.t_half + hplane, HPB);
+  const rsrc_t ry = make_rsrc(use_skip ? a.y + plane : nullptr, PB);
+  const rsrc_t rout = make_rsrc(a.out + plane, PB);
+  const rsrc_t ruo = make_rsrc(a.u_out ? a.u_out + plane : nullptr, PB);
+  const rsrc_t rxd = make_rsrc(a.xd_out ? a.xd_out + hplane : nullptr, HPB);
+  const uint32_t RB = (uint32_t)W * 4u, HRB = (uint32_t)hw * 4u;
+  const int c0 = 4 * lane, ch0 = 2 * lane;
+  const uint32_t vo = (uint32_t)c0 * 4u, vo_half = (uint32_t)ch0 * 4u;
+
+  const float scl0 = expf(a.log_mu0[g]), scg0 = expf(a.log_ro0[g]);
+  const float scl1 = expf(a.log_mu1[g]), scg1 = expf(a.log_ro1[g]);
+  const float alpha_a = a.alpha_a[g], beta_a = use_beta_a ? a.beta_a[g] : 0.f;
+  const float alpha_b = a.alpha_b[g], beta_b = use_beta_b ? a.beta_b[g] : 0.f;
+  float sk0 = 0.f, sk1 = 1.f;
+  if (use_skip) { sk0 = a.skip[0]; sk1 = a.skip[1]; }
+  const Taps tL0 = make_taps(a.sL0, ch), tG0 = make_taps(a.sG0, ch);
+  const Taps tL1 = make_taps(a.sL1, ch), tG1 = make_taps(a.sG1, ch);
+
+  float* const xr = xring + f * S2_XR * S2_W + c0;
+  float* const ur = uring + f * S2_UR * S2_W + c0;
+  float* const dr = dring + f * S2_DR * S2_HW + ch0;
+  const float* const wl_lane = wring + c0;
+  const float* const hw_lane = hring + ch0;
+
+  struct Ld {
+    float x[V], eb[V], eu[V], th[VH], b2[V], y2[V];
+  };
+  auto issue = [&](int t, Ld& S) {
+    bload(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
+    const int re = clampi(t - 3, 0, H - 1);
+    bload(S.eb, rb, vo + re * RB);
+    bload(S.eu, ru, vo + re * RB);
+    bload(S.th, rth, vo_half + (re >> 1) * HRB);
+    const int r2 = clampi(t - 11, 0, H - 1);
+    bload(S.b2, rb, vo + r2 * RB);
+    bload(S.y2, ry, vo + r2 * RB);
+  };
+  auto ring_w = [&](const float* row, float (&WL)[4][V], float (&WG)[2][V]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const F4 q = *reinterpret_cast<const F4*>(row + e * S2_W);
+#pragma unroll
+      for (int j = 0; j < V; ++j) WL[e][j] = q[j];
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const F4 q = *reinterpret_cast<const F4*>(row + (4 + e) * S2_W);
+#pragma unroll
+      for (int j = 0; j < V; ++j) WG[e][j] = q[j];
+    }
+  };
+  auto st4 = [&](float* p, const float (&v)[V]) {
+    F4 q;
+#pragma unroll
+    for (int j = 0; j < V; ++j) q[j] = v[j];
+    *reinterpret_cast<F4*>(p) = q;
+  };
+  auto ld4 = [&](const float* p, float (&v)[V]) {
+    const F4 q = *reinterpret_cast<const F4*>(p);
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = q[j];
+  };
+
+  OpPipe<V> PA, PQ;
+  OpPipe<VH> PH;
+  PA.zero();
+  PQ.zero();
+  PH.zero();
+  float xa_prev[V] = {}, xb_prev[V] = {}, TH[VH] = {};
+  int hA = 0;
+
+  // stage A (stage k) at step t: emits row t-3 into the x / u rings, D x half rows at odd rows
+  auto stage_a = [&](int t, const Ld& S, int q, int par) {
+    float WL[4][V], WG[2][V], tl[V], tg[V];
+    ring_w(wl_lane + q * S2_PAIR + par * 6 * S2_W, WL, WG);
+    PA.advance(S.x, WL, WG, t, H, W, c0, tL0, tG0, tl, tg);
+    const int y = t - 3;
+    float xn[V], u[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float th = 0.25f * S.th[j >> 1];
+      float ax = PA.X0[j];
+      ax = ax + tl[j] * scl0;
+      ax = ax + tg[j] * scg0;
+      ax = ax + th;
+      float uv = S.eb[j] - ax;
+      if (use_beta_a) uv = uv + beta_a * S.eu[j];
+      u[j] = uv;
+      xn[j] = PA.X0[j] + alpha_a * uv;
+    }
+    if (y >= 0 && y < H) {
+      st4(xr + (y & (S2_XR - 1)) * S2_W, xn);
+      st4(ur + (y % S2_UR) * S2_W, u);
+    }
+    if (par) {
+      float d[VH];
+#pragma unroll
+      for (int k = 0; k < VH; ++k)
+        d[k] = 0.25f * xa_prev[2 * k] + 0.25f * xa_prev[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+      hA = (y - 1) / 2;
+      if (hA >= 0 && hA < h) {
+        F2 q;
+        q[0] = d[0]; q[1] = d[1];
+        *reinterpret_cast<F2*>(dr + (hA & (S2_DR - 1)) * S2_HW) = q;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) xa_prev[j] = xn[j];
+  };
+
+  // half level of D x_{k+1}: input half row hA - 1 (clamped), emits t_{k+1} half row hA - 4
+  auto stage_h = [&](int qh) {
+    const int hin = hA - 1;
+    float xh[VH], WL[4][VH], WG[2][VH], tl[VH], tg[VH];
+    {
+      const F2 q = *reinterpret_cast<const F2*>(dr + (clampi(hin, 0, h - 1) & (S2_DR - 1)) * S2_HW);
+      xh[0] = q[0]; xh[1] = q[1];
+    }
+    const float* row = hw_lane + qh * S2_HROW;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const F2 q = *reinterpret_cast<const F2*>(row + e * S2_HW);
+      WL[e][0] = q[0]; WL[e][1] = q[1];
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const F2 q = *reinterpret_cast<const F2*>(row + (4 + e) * S2_HW);
+      WG[e][0] = q[0]; WG[e][1] = q[1];
+    }
+    PH.advance(xh, WL, WG, hin, h, hw, ch0, tL1, tG1, tl, tg);
+#pragma unroll
+    for (int k = 0; k < VH; ++k) {
+      float rv = tl[k] * scl1;
+      rv = rv + tg[k] * scg1;
+      TH[k] = rv;
+    }
+  };
+
+  // stage B (stage k+1) at step t: input x_{k+1} row t-8, emits row t-11 to HBM
+  auto stage_b = [&](int t, const Ld& S, int q, int par) {
+    const int tb = t - 8;
+    float xin[V], WL[4][V], WG[2][V], tl[V], tg[V];
+    ld4(xr + (clampi(tb, 0, H - 1) & (S2_XR - 1)) * S2_W, xin);
+    ring_w(wl_lane + q * S2_PAIR + par * 6 * S2_W, WL, WG);
+    PQ.advance(xin, WL, WG, tb, H, W, c0, tL0, tG0, tl, tg);
+    const int y = t - 11;
+    float up[V] = {};
+    if (use_beta_b) ld4(ur + (((y % S2_UR) + S2_UR) % S2_UR) * S2_W, up);
+    float res[V], xn[V], u[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float th = 0.25f * TH[j >> 1];
+      float ax = PQ.X0[j];
+      ax = ax + tl[j] * scl0;
+      ax = ax + tg[j] * scg0;
+      ax = ax + th;
+      float uv = S.b2[j] - ax;
+      if (use_beta_b) uv = uv + beta_b * up[j];
+      u[j] = uv;
+      xn[j] = PQ.X0[j] + alpha_b * uv;
+      res[j] = use_skip ? sk0 * S.y2[j] + sk1 * xn[j] : xn[j];
+    }
+    const bool yv = y >= r0 && y < r1;
+    const uint32_t so = yv ? vo + (uint32_t)y * RB : GRR_OOB;
+    bstore(rout, so, res);
+    bstore(ruo, so, u);
+    if (par) {
+      float d[VH];
+#pragma unroll
+      for (int k = 0; k < VH; ++k)
+        d[k] = 0.25f * xb_prev[2 * k] + 0.25f * xb_prev[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+      bstore(rxd, yv ? vo_half + (uint32_t)(y >> 1) * HRB : GRR_OOB, d);
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) xb_prev[j] = xn[j];
+  };
+
+  Ld LA, LB;
+  issue(ts, LA);
+  issue(ts + 1, LB);
+  __builtin_amdgcn_s_barrier();   // the producer's first ring rows have landed
+  asm volatile("" ::: "memory");
+  int qa = 0, qh = 0;
+  for (int i = 0; i < NI; ++i) {
+    const int t = ts + 2 * i;
+    const int qb = qa >= 4 ? qa - 4 : qa + 3;   // pair i - 4 (mod 7)
+    stage_a(t, LA, qa, 0);
+    stage_a(t + 1, LB, qa, 1);
+    stage_h(qh);
+    stage_b(t, LA, qb, 0);
+    issue(t + 2, LA);
+    stage_b(t + 1, LB, qb, 1);
+    issue(t + 3, LB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ring reads done before the producer refills
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    qa = qa == S2_WP - 1 ? 0 : qa + 1;
+    qh = (qh + 1) & (S2_HR - 1);
+  }
+}
+
+static int step2_seg_rows(int H, uint64_t blocks_per_seg) {
+  // one workgroup per CU: at least 2 workgroups per CU where the batch allows, segments of >= 64 rows
+  int sseg = H;
+  while (sseg > 64 && blocks_per_seg * (uint64_t)((H + sseg - 1) / sseg) < 512) sseg = ((sseg / 2) + 1) & ~1;
+  return sseg;
+}
+
 }  // namespace grr
 
 using namespace grr;
@@ -1495,6 +1941,46 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
   if (wL && cG) return launch_op<true, GTV_PAIR, EPI_STEP>(a, B, s, "grr_system_step");
   if (wL) return launch_op<true, GTV_NONE, EPI_STEP>(a, B, s, "grr_system_step");
   return launch_op<false, GTV_PAIR, EPI_STEP>(a, B, s, "grr_system_step");
+}
+
+grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* t_half,
+                            const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
+                            const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
+                            grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
+                            const float* alpha_a, const float* beta_a, const float* alpha_b, const float* beta_b,
+                            const float* skip, const float* y_skip, float* x_out, float* u_out, float* xd_out,
+                            int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && b && t_half && wL0 && cG0 && wL1 && cG1 && log_mu0 && log_ro0 && log_mu1 && log_ro1 && alpha_a &&
+                  alpha_b && x_out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_system_step2: bad args");
+  GRR_REQUIRE(stencil_ok(sL0) && stencil_ok(sG0) && stencil_ok(sL1) && stencil_ok(sG1), GRR_ERR_INVALID_ARG,
+              "grr_system_step2: stencil missing");
+  GRR_REQUIRE(!skip || y_skip, GRR_ERR_INVALID_ARG, "grr_system_step2: skip needs y_skip");
+  GRR_REQUIRE(!beta_a || u_prev, GRR_ERR_INVALID_ARG, "grr_system_step2: beta_a needs u_prev");
+  GRR_REQUIRE(W == S2_W && H % 2 == 0 && H >= 2 && F <= S2_FMAX, GRR_ERR_UNSUPPORTED,
+              "grr_system_step2: needs W = %d, even H and F <= %d (got H %d, W %d, F %d)", S2_W, S2_FMAX, H, W, F);
+  GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_system_step2: plane too large");
+  GRR_REQUIRE(x_out != x && x_out != b && x_out != u_prev && (!u_out || (u_out != u_prev && u_out != x && u_out != b)),
+              GRR_ERR_INVALID_ARG, "grr_system_step2: outputs must not alias the inputs (rows are read ahead)");
+  const void* ptrs[] = {x, b, u_prev, t_half, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out};
+  for (const void* q : ptrs)
+    GRR_REQUIRE((uintptr_t)q % 16 == 0, GRR_ERR_INVALID_ARG, "grr_system_step2: operands must be 16-byte aligned");
+  Step2Args a{};
+  a.x = x; a.b = b; a.u_prev = u_prev; a.t_half = t_half;
+  a.wL0 = wL0; a.cG0 = cG0; a.wL1 = wL1; a.cG1 = cG1;
+  a.sL0 = sL0; a.sG0 = sG0; a.sL1 = sL1; a.sG1 = sG1;
+  a.log_mu0 = log_mu0; a.log_ro0 = log_ro0; a.log_mu1 = log_mu1; a.log_ro1 = log_ro1;
+  a.alpha_a = alpha_a; a.beta_a = beta_a; a.alpha_b = alpha_b; a.beta_b = beta_b;
+  a.skip = skip; a.y = y_skip; a.out = x_out; a.u_out = u_out; a.xd_out = xd_out;
+  a.G = G; a.F = F; a.H = H;
+  a.sseg = step2_seg_rows(H, (uint64_t)B * G);
+  a.nsegs = (H + a.sseg - 1) / a.sseg;
+  const uint64_t nblk = (uint64_t)B * G * a.nsegs;
+  GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_step2: grid too large");
+  a.nblk = (uint32_t)nblk;
+  hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(64 * (F + 1)), 0, (hipStream_t)stream, a);
+  return launch_status("grr_system_step2");
 }
 
 grr_status grr_glr_stage(const float* x, const float* b, const float* u_prev, const float* wL, grr_stencil sL,

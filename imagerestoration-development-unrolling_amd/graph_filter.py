@@ -408,13 +408,26 @@ class MixtureGTVGLR(nn.Module):
         else:
             b_b, _ = OPS.gtv_rhs_full(x, False, y, False, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
         del wG0, wG1
-        u = None
-        for k in range(1, n_st):                                     # (REF:784-790, :797-807)
-            last = k == n_st - 1
+        u, u_spare = None, None
+        pair = OPS.step2_supported(x, g)
+        k = 1
+        while k < n_st:                                              # (REF:784-790, :797-807)
             t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
+            if pair and k + 1 < n_st:
+                # stages k, k+1 in one pass: x_{k+1}, u_{k+1}, t_{k+1} stay on chip
+                last = k + 1 == n_st - 1
+                x, u_new, xd = OPS.system_step2(x, b_b, u, t, wL0, cG0, L0, G0, mu0, ro0, wL1, cG1, L1, G1, mu1,
+                                                ro1, alpha[k], beta[k] if k >= 2 else None, alpha[k + 1], beta[k + 1],
+                                                g, want_u=not last, want_pool=not last, skip=skip if last else None,
+                                                y_skip=y if last else None, u_out=u_spare)
+                u_spare, u = u, u_new
+                k += 2
+                continue
+            last = k == n_st - 1
             x, u, xd = OPS.system_step(x, b_b, u, t, wL0, cG0, L0, G0, mu0, ro0, alpha[k],
                                        beta[k] if k >= 2 else None, g, want_u=not last, want_pool=not last,
                                        skip=skip if last else None, y_skip=y if last else None, u_out=u)
+            k += 1
         return x
 
     def forward(self, patchs: torch.Tensor, _skip: Optional[torch.Tensor] = None,

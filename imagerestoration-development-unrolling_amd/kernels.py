@@ -9,6 +9,8 @@ from __future__ import annotations
 
 from typing import Optional, Sequence, Tuple
 
+import os
+
 import torch
 
 from . import _native
@@ -260,6 +262,53 @@ def system_step(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Option
             _ptr(log_mu0), _ptr(log_ro0), alpha.data_ptr(), _ptr(beta), _ptr(skip), _ptr(y_skip),
             out.data_ptr(), _ptr(u_out), _ptr(xd), b, n_graphs, c // n_graphs, h, w, _stream(dev))
     return out, u_out, xd
+
+
+def system_step2(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Tensor,
+                 wL0: Tensor, cG0: Tensor, sL0: Stencil, sG0: Stencil, log_mu0: Tensor, log_ro0: Tensor,
+                 wL1: Tensor, cG1: Tensor, sL1: Stencil, sG1: Stencil, log_mu1: Tensor, log_ro1: Tensor,
+                 alpha_a: Tensor, beta_a: Optional[Tensor], alpha_b: Tensor, beta_b: Optional[Tensor],
+                 n_graphs: int, want_u: bool, want_pool: bool, skip: Optional[Tensor] = None,
+                 y_skip: Optional[Tensor] = None, u_out: Optional[Tensor] = None
+                 ) -> Tuple[Tensor, Optional[Tensor], Optional[Tensor]]:
+    """Stages k and k+1 in one pass (grr_system_step2): returns (x_{k+2}, u_{k+2}, D x_{k+2})."""
+    dev = _check("system_step2", x, rhs, u_prev, t_half, wL0, cG0, log_mu0, log_ro0, wL1, cG1, log_mu1, log_ro1,
+                 alpha_a, beta_a, alpha_b, beta_b, skip, y_skip)
+    b, c, h, w = x.shape
+    out = torch.empty_like(x)
+    if want_u and (u_out is None or (u_prev is not None and u_out.data_ptr() == u_prev.data_ptr())):
+        u_out = torch.empty_like(x)
+    if not want_u:
+        u_out = None
+    xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_pool else None
+    _launch("system_step2", step2_bytes(b, c, n_graphs, h, w, u_prev is not None, u_out is not None, want_pool,
+                                        skip is not None),
+            "grr_system_step2", x.data_ptr(), rhs.data_ptr(), _ptr(u_prev), t_half.data_ptr(), wL0.data_ptr(),
+            cG0.data_ptr(), sL0, sG0, log_mu0.data_ptr(), log_ro0.data_ptr(), wL1.data_ptr(), cG1.data_ptr(), sL1, sG1,
+            log_mu1.data_ptr(), log_ro1.data_ptr(), alpha_a.data_ptr(), _ptr(beta_a), alpha_b.data_ptr(),
+            _ptr(beta_b), _ptr(skip), _ptr(y_skip), out.data_ptr(), _ptr(u_out), _ptr(xd), b, n_graphs,
+            c // n_graphs, h, w, _stream(dev))
+    return out, u_out, xd
+
+
+# two CG stages per launch where the shape allows (GRR_STEP2=0: one launch per stage, for A/B runs)
+STEP2 = os.environ.get("GRR_STEP2", "1") != "0"
+
+
+def step2_supported(x: Tensor, n_graphs: int) -> bool:
+    """grr_system_step2's shape limits: W = 256, even H, F <= 3."""
+    b, c, h, w = x.shape
+    return w == 256 and h % 2 == 0 and c % n_graphs == 0 and c // n_graphs <= 3
+
+
+def step2_bytes(b, c, g, h, w, has_u_prev, has_u_out, has_pool, has_skip):
+    """Compulsory HBM bytes of one grr_system_step2 launch: x, b, u_prev, t_half, the full- and
+    half-level GLR + pair weights read once; x_out, u_out, D x_out written once (x_{k+1}, u_{k+1},
+    t_{k+1} stay on chip; the second read of b rows is an L2 hit by construction)."""
+    f = c * (2 + int(has_u_prev) + 1 + int(has_u_out) + int(has_skip))    # x, b, u_prev, x_out, u_out, y
+    f += (c // 4) * (1 + int(has_pool))                                   # t_half in, D x_out
+    f += 6 * g + (6 * g) // 4                                             # full + half-level weights
+    return 4 * b * h * w * f
 
 
 def step_bytes(b, c, g, h, w, has_rhs, has_u_prev, has_half, has_glr, has_gtv, has_u_out, has_pool, has_skip):

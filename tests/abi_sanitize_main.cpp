@@ -38,6 +38,8 @@ int main() {
   EXPECT_ERR(grr_gtv_rhs_full(n, n, n, ns, 0, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_gtv_rhs_full_rep(n, 1, n, 1, n, ns, 0, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_system_step(n, n, n, n, n, n, ns, ns, n, n, n, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_system_step2(n, n, n, n, n, n, ns, ns, n, n, n, n, ns, ns, n, n, n, n, n, n, n, n, n, n, n, 1, 1, 1,
+                              8, 256, s));
   EXPECT_ERR(grr_glr_stage(n, n, n, n, ns, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_neighbor_gather(n, n, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_normalize_features(n, n, n, 1, 1, 1, 8, 8, s));

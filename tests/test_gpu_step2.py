@@ -1,0 +1,145 @@
+"""grr_system_step2 (two CG stages per pass, temporal blocking) against the one-stage-per-launch
+sequence grr_system_step -> grr_system_half -> grr_system_step and against the CPU oracle.
+
+The fused kernel computes the same values with the same per-row arithmetic; the tolerance
+below (2e-6 relative to the largest output) covers fp32 contraction differences between the
+two code paths.  Shapes cover one row segment per (b, graph) (B*G >= 512 workgroups) and the
+segmented grid of small batches (64-row segments, the stage-A lead of 9 rows crossing the
+segment boundary), the top / bottom replicate clamps of the in-kernel rings at short H, the
+first pair (no u_prev / beta_a) and the last pair (skip, no u / D x outputs).
+"""
+import pytest
+import torch
+
+from oracle import graph_oracle as O
+from tests.test_gpu_parity import DEV, perturb_mixture, rel_err, sd_cpu
+
+pytestmark = pytest.mark.gpu
+TIGHT = 2e-6
+
+
+@pytest.fixture(scope="module")
+def irdu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import irdu_amd
+    irdu_amd.load_native()
+    return irdu_amd
+
+
+def _setup(irdu, B, G, F, H, seed):
+    from irdu_amd import kernels as K
+    torch.manual_seed(seed)
+    mix = irdu.MixtureGTVGLR(G, F, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]], n_cgd_iters=4)
+    perturb_mixture(mix, seed)
+    with torch.no_grad():   # scales large enough that both levels matter
+        mix.muys00.fill_(-1.0)
+        mix.ro00.fill_(-1.5)
+        mix.muys01.fill_(-1.2)
+        mix.ro01.fill_(-1.6)
+    mix = mix.to(DEV)
+    W = 256
+    f0 = torch.randn(B, 2 * G * F, H, W, device=DEV)
+    f1 = torch.randn(B, 2 * G * F, H // 2, W // 2, device=DEV)
+    _, cG0, wL0 = K.edge_weights_block(f0, G, F, mix.GTVmodule00.multiM, mix.GLRmodule00.multiM)
+    _, cG1, wL1 = K.edge_weights_block(f1, G, F, mix.GTVmodule01.multiM, mix.GLRmodule01.multiM)
+    C = G * F
+    x = torch.rand(B, C, H, W, device=DEV)
+    b = x + 0.1 * torch.randn(B, C, H, W, device=DEV)
+    u = 0.05 * torch.randn(B, C, H, W, device=DEV)
+    return mix, x, b, u, (wL0, cG0, wL1, cG1)
+
+
+def _two_steps(irdu, mix, x, b, u, w, k, g, skip=None, y_skip=None, last=False):
+    from irdu_amd import ops as OPS
+    wL0, cG0, wL1, cG1 = w
+    m = mix
+    alpha, beta = m.alphaCGD, m.betaCGD
+    xd = OPS.pool2(x)
+    t = OPS.system_half(xd, wL1, cG1, m.GLRmodule01, m.GTVmodule01, m.muys01, m.ro01, g)
+    ref1, u1, xd1 = OPS.system_step(x, b, u, t, wL0, cG0, m.GLRmodule00, m.GTVmodule00, m.muys00, m.ro00, alpha[k],
+                                    beta[k] if u is not None else None, g, want_u=True, want_pool=True)
+    t1 = OPS.system_half(xd1, wL1, cG1, m.GLRmodule01, m.GTVmodule01, m.muys01, m.ro01, g)
+    ref2, u2, xd2 = OPS.system_step(ref1, b, u1, t1, wL0, cG0, m.GLRmodule00, m.GTVmodule00, m.muys00, m.ro00,
+                                    alpha[k + 1], beta[k + 1], g, want_u=not last, want_pool=not last,
+                                    skip=skip, y_skip=y_skip)
+    got, gu, gxd = OPS.system_step2(x, b, u, t, wL0, cG0, m.GLRmodule00, m.GTVmodule00, m.muys00, m.ro00, wL1, cG1,
+                                    m.GLRmodule01, m.GTVmodule01, m.muys01, m.ro01, alpha[k],
+                                    beta[k] if u is not None else None, alpha[k + 1], beta[k + 1], g,
+                                    want_u=not last, want_pool=not last, skip=skip, y_skip=y_skip)
+    return (ref2, u2, xd2), (got, gu, gxd)
+
+
+CASES = [
+    dict(B=2, G=4, F=3, H=256),     # segmented grid: 64-row segments
+    dict(B=16, G=32, F=3, H=256),   # one segment per (b, graph): the bench's workgroup shape
+    dict(B=3, G=2, F=3, H=16),      # shorter than the pipeline lag
+    dict(B=2, G=3, F=2, H=130),     # H not a multiple of the segment, F = 2
+    dict(B=1, G=4, F=1, H=64),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{B}g{G}f{F}h{H}".format(**c))
+@pytest.mark.parametrize("with_u", [True, False])
+def test_step2_equals_two_steps(irdu, case, with_u):
+    B, G, F, H = case["B"], case["G"], case["F"], case["H"]
+    mix, x, b, u, w = _setup(irdu, B, G, F, H, seed=B * 100 + H + F)
+    with torch.no_grad():
+        (r, ru, rxd), (o, ou, oxd) = _two_steps(irdu, mix, x, b, u if with_u else None, w, k=2, g=G)
+    torch.cuda.synchronize()
+    for name, a, bb in (("x", o, r), ("u", ou, ru), ("xd", oxd, rxd)):
+        e = rel_err(a, bb)
+        assert e <= TIGHT, (name, e)
+        assert torch.isfinite(a).all()
+
+
+def test_step2_last_pair_with_skip(irdu):
+    mix, x, b, u, w = _setup(irdu, 2, 4, 3, 256, seed=77)
+    y = torch.rand_like(x)
+    skip = torch.tensor([0.7, 0.4], device=DEV)
+    with torch.no_grad():
+        (r, ru, rxd), (o, ou, oxd) = _two_steps(irdu, mix, x, b, u, w, k=2, g=4, skip=skip, y_skip=y, last=True)
+    assert ou is None and oxd is None and ru is None and rxd is None
+    assert rel_err(o, r) <= TIGHT
+
+
+def test_step2_rejects_unsupported_shapes(irdu):
+    from irdu_amd import kernels as K
+    from irdu_amd._native import GrrError
+    mix, x, b, u, w = _setup(irdu, 1, 2, 3, 16, seed=5)
+    xs = x[..., :128].contiguous()
+    wL0, cG0, wL1, cG1 = w
+    m = mix
+    with pytest.raises(GrrError):
+        K.system_step2(xs, xs, None, torch.zeros(1, 6, 8, 64, device=DEV), wL0[..., :128].contiguous(),
+                       cG0[..., :128].contiguous(), K.stencil(m.GLRmodule00), K.stencil(m.GTVmodule00), m.muys00,
+                       m.ro00, wL1[..., :64].contiguous(), cG1[..., :64].contiguous(), K.stencil(m.GLRmodule01),
+                       K.stencil(m.GTVmodule01), m.muys01, m.ro01, m.alphaCGD[0], None, m.alphaCGD[1],
+                       m.betaCGD[1], 2, True, True)
+    assert not K.step2_supported(xs, 2)
+
+
+@pytest.mark.parametrize("b", [1, 3])
+def test_filter_with_step2_matches_per_stage_launches_and_oracle(irdu, b):
+    """The image filter (S = 10: stage 0, then pairs (1,2) ... (7,8) and stage 9) with and without
+    two-stage launches, and against the CPU oracle at the PSNR tolerance."""
+    from irdu_amd import kernels as K
+    torch.manual_seed(2300 + b)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=10)
+    perturb_mixture(m.localfilter, 23 + b)
+    clean = torch.rand(b, 3, 256, 256)
+    noisy = clean + torch.randn(b, 3, 256, 256) * (25.0 / 255.0)
+    md = m.to(DEV)
+    saved = K.STEP2
+    try:
+        with torch.no_grad():
+            K.STEP2 = True
+            fused = md(noisy.to(DEV)).cpu()
+            K.STEP2 = False
+            single = md(noisy.to(DEV)).cpu()
+    finally:
+        K.STEP2 = saved
+    assert rel_err(fused, single) <= 1e-5
+    ref = O.multiscale_graph_filter(noisy, sd_cpu(m), 8)
+    assert rel_err(fused, ref) <= 1e-4
+    assert abs(O.psnr_ubyte(fused, clean) - O.psnr_ubyte(ref, clean)) <= 0.01
