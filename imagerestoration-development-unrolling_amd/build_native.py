@@ -21,9 +21,10 @@ LIB = os.path.join(HERE, "libgrr.so")
 SOURCES = ["graph_ops.hip", "feature_ops.hip", "lnb_ops.hip", "graph_bwd.hip", "lnb_bwd.hip", "window_ops.hip", "subapi_ops.hip"]
 HEADERS = [os.path.join(CSRC, "grr_common.h"), os.path.join(ROOT, "include", "grr.h")]
 ARCH = "gfx950"
-# lnb_ops: no SLP packing of the gate's independent f32 FMAs into v_pk_fma_f32 (the packing
-# needs register-pair moves that cost more than it saves, MI355X_MICROARCH.md)
-EXTRA_FLAGS = {"lnb_ops.hip": ["-fno-slp-vectorize"]}
+# lnb_ops, graph_ops: no SLP packing of independent f32 FMAs into v_pk_fma_f32 (the packing
+# needs register-pair moves that cost more than it saves, MI355X_MICROARCH.md; graph_step2_kernel:
+# 1149 -> 1055 VALU instructions per iteration)
+EXTRA_FLAGS = {"lnb_ops.hip": ["-fno-slp-vectorize"], "graph_ops.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:

@@ -1346,30 +1346,41 @@ struct Step2Args {
 
 template <int V>
 struct OpPipe {
-  float X0[V], X1[V], X2[V], X3[V];
-  float SL0[V], SL1[V], SL2[V], SG0[V], SG1[V], SG2[V];
-  float L0[V], L1[V], L2[V], O0[V], O1[V], O2[V];
-  float cv[V];
+  // Register slots of the row pipeline, 4-periodic: at phase P (step t with t = P mod 4 in
+  // the caller's unrolled loop) input row t lands in X[(P+3)&3]; X[P&3] holds row t-3.
+  // S (s = S x), L (l) and O (o) keep rows t-3..t-1 / t-4..t-2 in slots (P+1..P+3)&3.
+  // Static slot indices: no register moves for the pipeline shifts.
+  float X[4][V], SL[4][V], SG[4][V], L[4][V], O[4][V];
+  float cv[2][V];   // pair weight c_v of the previous row (parity slots)
 
   __device__ __forceinline__ void zero() {
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      X0[j] = X1[j] = X2[j] = X3[j] = 0.f;
-      SL0[j] = SL1[j] = SL2[j] = SG0[j] = SG1[j] = SG2[j] = 0.f;
-      L0[j] = L1[j] = L2[j] = O0[j] = O1[j] = O2[j] = 0.f;
-      cv[j] = 0.f;
-    }
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < V; ++j) X[k][j] = SL[k][j] = SG[k][j] = L[k][j] = O[k][j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) cv[0][j] = cv[1][j] = 0.f;
   }
+
+  // x row t-3 (the epilogue's x at the output row)
+  template <int P>
+  __device__ __forceinline__ const float (&x_out() const)[V] { return X[P & 3]; }
 
   // push input row t (replicate-clamped by the caller) and the edge-weight row t-2 (4 GLR
   // planes, 2 pair planes); returns S_L^T (I - W) S_L x and S_G^T C^T C S_G x at row t-3
-  // (before the mu / ro scales).  Lane = V adjacent columns starting at c0.
+  // (before the mu / ro scales).  Lane = V adjacent columns starting at c0.  The arithmetic
+  // of graph_row_kernel's consume (stages 2-4).
+  template <int P, int W>
   __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
-                                          int t, int H, int W, int c0, const Taps& tL, const Taps& tG,
+                                          int t, int H, int c0, const Taps& tL, const Taps& tG,
                                           float (&tl)[V], float (&tg)[V]) {
+    constexpr int K0 = P & 3, K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
 #pragma unroll
-    for (int j = 0; j < V; ++j) { X0[j] = X1[j]; X1[j] = X2[j]; X2[j] = X3[j]; X3[j] = xin[j]; }
-    {  // s at row t-1
+    for (int j = 0; j < V; ++j) X[K3][j] = xin[j];
+    const float (&X1)[V] = X[K1];
+    const float (&X2)[V] = X[K2];
+    const float (&X3)[V] = X[K3];
+    {  // s at row t-1 -> slot K3 (rows t-3, t-2 in K1, K2)
       const float xp = lane_prev(X2[V - 1]), xq = lane_next(X2[0]);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
@@ -1378,43 +1389,53 @@ struct OpPipe {
         const float xr = col < W - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
         float sv = tL.u * X1[j];
         sv += tL.l * xl; sv += tL.c * X2[j]; sv += tL.r * xr; sv += tL.d * X3[j];
-        SL0[j] = SL1[j]; SL1[j] = SL2[j]; SL2[j] = sv;
+        SL[K3][j] = sv;
         float sg = tG.u * X1[j];
         sg += tG.l * xl; sg += tG.c * X2[j]; sg += tG.r * xr; sg += tG.d * X3[j];
-        SG0[j] = SG1[j]; SG1[j] = SG2[j]; SG2[j] = sg;
+        SG[K3][j] = sg;
       }
     }
-    {  // l and o at row r = t-2 (zero outside the image)
+    {  // l and o at row r = t-2 -> slot K3 (zero outside the image); s rows t-3, t-2, t-1 = K1, K2, K3
       const int r = t - 2;
       const bool rin = r >= 0 && r < H;
-      const float pv = lane_prev(SL1[V - 1]), nx = lane_next(SL1[0]);
-      const float sp = lane_prev(SG1[V - 1]), sn = lane_next(SG1[0]);
+      const float (&S0)[V] = SL[K1];
+      const float (&S1)[V] = SL[K2];
+      const float (&S2)[V] = SL[K3];
+      const float (&G0)[V] = SG[K1];
+      const float (&G1)[V] = SG[K2];
+      const float (&G2)[V] = SG[K3];
+      const float pv = lane_prev(S1[V - 1]), nx = lane_next(S1[0]);
+      const float sp = lane_prev(G1[V - 1]), sn = lane_next(G1[0]);
       const float wp = lane_prev(WG[0][V - 1]);
-      float l[V], o[V];
+      const float (&cvp)[V] = cv[(P + 1) & 1];
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const int col = c0 + j;
-        const float up = r > 0 ? SL0[j] : SL1[j];
-        const float dn = r < H - 1 ? SL2[j] : SL1[j];
-        const float lf = col > 0 ? (j > 0 ? SL1[j - 1] : pv) : SL1[j];
-        const float rt = col < W - 1 ? (j < V - 1 ? SL1[j + 1] : nx) : SL1[j];
+        const float up = r > 0 ? S0[j] : S1[j];
+        const float dn = r < H - 1 ? S2[j] : S1[j];
+        const float lf = col > 0 ? (j > 0 ? S1[j - 1] : pv) : S1[j];
+        const float rt = col < W - 1 ? (j < V - 1 ? S1[j + 1] : nx) : S1[j];
         const float wx = ((WL[0][j] * up + WL[1][j] * lf) + WL[2][j] * rt) + WL[3][j] * dn;
-        l[j] = (rin && col < W) ? SL1[j] - wx : 0.f;
-        const float sv = SG1[j];
-        const float snx = j < V - 1 ? SG1[j + 1] : sn;
-        const float spv = j > 0 ? SG1[j - 1] : sp;
+        const float lv = S1[j] - wx;
+        const float sv = G1[j];
+        const float snx = j < V - 1 ? G1[j + 1] : sn;
+        const float spv = j > 0 ? G1[j - 1] : sp;
         const float chl = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
-        const float cvu = r > 0 ? cv[j] : 0.f;
-        const float ov = WG[0][j] * (sv - snx) + chl * (sv - spv) + WG[1][j] * (sv - SG2[j]) + cvu * (sv - SG0[j]);
-        o[j] = (rin && col < W) ? ov : 0.f;
+        const float cvu = r > 0 ? cvp[j] : 0.f;
+        const float ov = WG[0][j] * (sv - snx) + chl * (sv - spv) + WG[1][j] * (sv - G2[j]) + cvu * (sv - G0[j]);
+        L[K3][j] = rin ? lv : 0.f;
+        O[K3][j] = rin ? ov : 0.f;
       }
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        L0[j] = L1[j]; L1[j] = L2[j]; L2[j] = l[j];
-        cv[j] = WG[1][j]; O0[j] = O1[j]; O1[j] = O2[j]; O2[j] = o[j];
-      }
+      for (int j = 0; j < V; ++j) cv[P & 1][j] = WG[1][j];
     }
-    {  // S^T at row t-3 (neighbours outside are 0)
+    {  // S^T at row t-3 from l / o rows t-4, t-3, t-2 = slots K1, K2, K3
+      const float (&L0)[V] = L[K1];
+      const float (&L1)[V] = L[K2];
+      const float (&L2)[V] = L[K3];
+      const float (&O0)[V] = O[K1];
+      const float (&O1)[V] = O[K2];
+      const float (&O2)[V] = O[K3];
       const float lp = lane_prev(L1[V - 1]), ln = lane_next(L1[0]);
       const float op = lane_prev(O1[V - 1]), on = lane_next(O1[0]);
 #pragma unroll
@@ -1441,12 +1462,14 @@ constexpr int S2_DR = 4;                   // D x_{k+1} ring half rows (per chan
 constexpr int S2_FMAX = 3;                 // channel waves per graph
 constexpr int S2_PAIR = 2 * 6 * S2_W;      // floats per weight-ring pair
 constexpr int S2_HROW = 6 * S2_HW;         // floats per half-weight ring row
-constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW + S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW);
+constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW + S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW) +
+                       S2_W + S2_HW;       // + one dummy row (writes of rows outside the image)
+constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipelines' slot period)
 static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
 
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void graph_step2_kernel(Step2Args a) {
-  constexpr int V = 4, VH = 2;
+  constexpr int V = 4, VH = 2, W = S2_W, hw = S2_HW;
   typedef typename VecT<4>::type F4;
   typedef typename VecT<2>::type F2;
   __shared__ __attribute__((aligned(16))) float lds[S2_LDS];
@@ -1455,6 +1478,7 @@ void graph_step2_kernel(Step2Args a) {
   float* const xring = hring + S2_HR * S2_HROW;
   float* const uring = xring + S2_FMAX * S2_XR * S2_W;
   float* const dring = uring + S2_FMAX * S2_UR * S2_W;
+  float* const dummy = dring + S2_FMAX * S2_DR * S2_HW;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int F = a.F;
@@ -1462,11 +1486,12 @@ void graph_step2_kernel(Step2Args a) {
   const int seg = unit % a.nsegs; unit /= a.nsegs;
   const int g = unit % a.G;
   const int b = unit / a.G;
-  const int H = a.H, W = S2_W, h = H / 2, hw = S2_HW;
+  const int H = a.H, h = H / 2;
   const int64_t HW = (int64_t)H * W, hHW = (int64_t)h * hw;
   const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
   const int ts = r0 - 9;                 // first step (odd offset from r0: step t emits stage-A row t-3)
-  const int NI = (r1 + 11 - ts) / 2;     // stage B emits rows up to r1 - 1
+  const int NI0 = (r1 + 11 - ts) / 2;    // stage B emits rows up to r1 - 1
+  const int NI = (NI0 + S2_UNROLL - 1) / S2_UNROLL * S2_UNROLL;   // extra iterations store nothing
 
   if (wave == F) {   // producer: weight rows -> LDS rings (LDS-DMA), two iterations ahead
     const float* pwl0 = a.wL0 + (int64_t)(b * a.G + g) * 4 * HW;
@@ -1524,11 +1549,10 @@ void graph_step2_kernel(Step2Args a) {
   const int64_t plane = ((int64_t)b * C + ch) * HW, hplane = ((int64_t)b * C + ch) * hHW;
   const int64_t PB = HW * 4, HPB = hHW * 4;
   const bool use_beta_a = a.beta_a != nullptr && a.u_prev != nullptr;
-  const bool use_beta_b = a.beta_b != nullptr;
   const bool use_skip = a.skip != nullptr;
   const rsrc_t rx = make_rsrc(a.x + plane, PB);
   const rsrc_t rb = make_rsrc(a.b + plane, PB);
-  const rsrc_t ru = make_rsrc(use_beta_a ? a.u_prev + plane : nullptr, PB);
+  const rsrc_t ru = make_rsrc(use_beta_a ? a.u_prev + plane : nullptr, PB);   // absent: reads 0
   const rsrc_t rth = make_rsrc(a.t_half + hplane, HPB);
   const rsrc_t ry = make_rsrc(use_skip ? a.y + plane : nullptr, PB);
   const rsrc_t rout = make_rsrc(a.out + plane, PB);
@@ -1540,8 +1564,9 @@ void graph_step2_kernel(Step2Args a) {
 
   const float scl0 = expf(a.log_mu0[g]), scg0 = expf(a.log_ro0[g]);
   const float scl1 = expf(a.log_mu1[g]), scg1 = expf(a.log_ro1[g]);
+  // absent terms enter as exact zeros / ones: u_prev reads 0 (beta 0), y reads 0 (skip 0, 1)
   const float alpha_a = a.alpha_a[g], beta_a = use_beta_a ? a.beta_a[g] : 0.f;
-  const float alpha_b = a.alpha_b[g], beta_b = use_beta_b ? a.beta_b[g] : 0.f;
+  const float alpha_b = a.alpha_b[g], beta_b = a.beta_b ? a.beta_b[g] : 0.f;
   float sk0 = 0.f, sk1 = 1.f;
   if (use_skip) { sk0 = a.skip[0]; sk1 = a.skip[1]; }
   const Taps tL0 = make_taps(a.sL0, ch), tG0 = make_taps(a.sG0, ch);
@@ -1550,6 +1575,8 @@ void graph_step2_kernel(Step2Args a) {
   float* const xr = xring + f * S2_XR * S2_W + c0;
   float* const ur = uring + f * S2_UR * S2_W + c0;
   float* const dr = dring + f * S2_DR * S2_HW + ch0;
+  float* const dmy = dummy + c0;
+  float* const dmyh = dummy + S2_W + ch0;
   const float* const wl_lane = wring + c0;
   const float* const hw_lane = hring + ch0;
 
@@ -1597,50 +1624,51 @@ void graph_step2_kernel(Step2Args a) {
   PA.zero();
   PQ.zero();
   PH.zero();
-  float xa_prev[V] = {}, xb_prev[V] = {}, TH[VH] = {};
-  int hA = 0;
+  float TH[VH] = {};
+  float xa0[V], xb0[V];   // the even row of the current iteration (2x2 pooling)
 
   // stage A (stage k) at step t: emits row t-3 into the x / u rings, D x half rows at odd rows
-  auto stage_a = [&](int t, const Ld& S, int q, int par) {
+  auto stage_a = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag) {
+    constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
     float WL[4][V], WG[2][V], tl[V], tg[V];
-    ring_w(wl_lane + q * S2_PAIR + par * 6 * S2_W, WL, WG);
-    PA.advance(S.x, WL, WG, t, H, W, c0, tL0, tG0, tl, tg);
+    ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
+    PA.template advance<P, W>(S.x, WL, WG, t, H, c0, tL0, tG0, tl, tg);
+    const float (&x0)[V] = PA.template x_out<P>();
     const int y = t - 3;
     float xn[V], u[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float th = 0.25f * S.th[j >> 1];
-      float ax = PA.X0[j];
+      float ax = x0[j];
       ax = ax + tl[j] * scl0;
       ax = ax + tg[j] * scg0;
       ax = ax + th;
       float uv = S.eb[j] - ax;
-      if (use_beta_a) uv = uv + beta_a * S.eu[j];
+      uv = uv + beta_a * S.eu[j];
       u[j] = uv;
-      xn[j] = PA.X0[j] + alpha_a * uv;
+      xn[j] = x0[j] + alpha_a * uv;
     }
-    if (y >= 0 && y < H) {
-      st4(xr + (y & (S2_XR - 1)) * S2_W, xn);
-      st4(ur + (y % S2_UR) * S2_W, u);
-    }
-    if (par) {
+    const bool yin = y >= 0 && y < H;
+    st4(yin ? xr + (y & (S2_XR - 1)) * S2_W : dmy, xn);
+    st4(yin ? ur + (y % S2_UR) * S2_W : dmy, u);
+    if constexpr (PAR == 0) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) xa0[j] = xn[j];
+    } else {
       float d[VH];
 #pragma unroll
       for (int k = 0; k < VH; ++k)
-        d[k] = 0.25f * xa_prev[2 * k] + 0.25f * xa_prev[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
-      hA = (y - 1) / 2;
-      if (hA >= 0 && hA < h) {
-        F2 q;
-        q[0] = d[0]; q[1] = d[1];
-        *reinterpret_cast<F2*>(dr + (hA & (S2_DR - 1)) * S2_HW) = q;
-      }
+        d[k] = 0.25f * xa0[2 * k] + 0.25f * xa0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+      const int hA = (y - 1) / 2;
+      F2 qv;
+      qv[0] = d[0]; qv[1] = d[1];
+      *reinterpret_cast<F2*>((hA >= 0 && hA < h) ? dr + (hA & (S2_DR - 1)) * S2_HW : dmyh) = qv;
     }
-#pragma unroll
-    for (int j = 0; j < V; ++j) xa_prev[j] = xn[j];
   };
 
   // half level of D x_{k+1}: input half row hA - 1 (clamped), emits t_{k+1} half row hA - 4
-  auto stage_h = [&](int qh) {
+  auto stage_h = [&](int hA, int qh, auto ph_tag) {
+    constexpr int P = decltype(ph_tag)::value;
     const int hin = hA - 1;
     float xh[VH], WL[4][VH], WG[2][VH], tl[VH], tg[VH];
     {
@@ -1658,7 +1686,7 @@ void graph_step2_kernel(Step2Args a) {
       const F2 q = *reinterpret_cast<const F2*>(row + (4 + e) * S2_HW);
       WG[e][0] = q[0]; WG[e][1] = q[1];
     }
-    PH.advance(xh, WL, WG, hin, h, hw, ch0, tL1, tG1, tl, tg);
+    PH.template advance<P, hw>(xh, WL, WG, hin, h, ch0, tL1, tG1, tl, tg);
 #pragma unroll
     for (int k = 0; k < VH; ++k) {
       float rv = tl[k] * scl1;
@@ -1668,65 +1696,94 @@ void graph_step2_kernel(Step2Args a) {
   };
 
   // stage B (stage k+1) at step t: input x_{k+1} row t-8, emits row t-11 to HBM
-  auto stage_b = [&](int t, const Ld& S, int q, int par) {
+  auto stage_b = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag) {
+    constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
     const int tb = t - 8;
-    float xin[V], WL[4][V], WG[2][V], tl[V], tg[V];
+    float xin[V], WL[4][V], WG[2][V], tl[V], tg[V], up[V];
     ld4(xr + (clampi(tb, 0, H - 1) & (S2_XR - 1)) * S2_W, xin);
-    ring_w(wl_lane + q * S2_PAIR + par * 6 * S2_W, WL, WG);
-    PQ.advance(xin, WL, WG, tb, H, W, c0, tL0, tG0, tl, tg);
+    ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
     const int y = t - 11;
-    float up[V] = {};
-    if (use_beta_b) ld4(ur + (((y % S2_UR) + S2_UR) % S2_UR) * S2_W, up);
+    ld4(ur + (((y % S2_UR) + S2_UR) % S2_UR) * S2_W, up);
+    PQ.template advance<P, W>(xin, WL, WG, tb, H, c0, tL0, tG0, tl, tg);
+    const float (&x0)[V] = PQ.template x_out<P>();
     float res[V], xn[V], u[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float th = 0.25f * TH[j >> 1];
-      float ax = PQ.X0[j];
+      float ax = x0[j];
       ax = ax + tl[j] * scl0;
       ax = ax + tg[j] * scg0;
       ax = ax + th;
       float uv = S.b2[j] - ax;
-      if (use_beta_b) uv = uv + beta_b * up[j];
+      uv = uv + beta_b * up[j];
       u[j] = uv;
-      xn[j] = PQ.X0[j] + alpha_b * uv;
-      res[j] = use_skip ? sk0 * S.y2[j] + sk1 * xn[j] : xn[j];
+      xn[j] = x0[j] + alpha_b * uv;
+      res[j] = sk0 * S.y2[j] + sk1 * xn[j];
     }
     const bool yv = y >= r0 && y < r1;
     const uint32_t so = yv ? vo + (uint32_t)y * RB : GRR_OOB;
     bstore(rout, so, res);
     bstore(ruo, so, u);
-    if (par) {
+    if constexpr (PAR == 0) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) xb0[j] = xn[j];
+    } else {
       float d[VH];
 #pragma unroll
       for (int k = 0; k < VH; ++k)
-        d[k] = 0.25f * xb_prev[2 * k] + 0.25f * xb_prev[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+        d[k] = 0.25f * xb0[2 * k] + 0.25f * xb0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
       bstore(rxd, yv ? vo_half + (uint32_t)(y >> 1) * HRB : GRR_OOB, d);
     }
-#pragma unroll
-    for (int j = 0; j < V; ++j) xb_prev[j] = xn[j];
   };
 
   Ld LA, LB;
   issue(ts, LA);
   issue(ts + 1, LB);
+  // Ring rows the pipelines read before their first write (rows above the image / before the
+  // segment, weight pairs of stage B's fill) only feed rows that are never stored, but through
+  // products with a 0 weight: zero them so the garbage is finite.  Weight slots 2..6 are first
+  // filled after the barrier below.
+  {
+    const float zero4[V] = {};
+#pragma unroll
+    for (int r = 0; r < S2_XR; ++r) st4(xr + r * S2_W, zero4);
+#pragma unroll
+    for (int r = 0; r < S2_UR; ++r) st4(ur + r * S2_W, zero4);
+    *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + S2_W + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
+    for (int r = f; r < (S2_WP - 2) * 12; r += F) st4(wring + 2 * S2_PAIR + r * S2_W + c0, zero4);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // the producer's first ring rows have landed
   asm volatile("" ::: "memory");
-  int qa = 0, qh = 0;
-  for (int i = 0; i < NI; ++i) {
+  int qa = 0;
+  // one iteration = two steps of stage A, one half-level row, two steps of stage B; PI = the
+  // iteration's phase in the unrolled body (pipelines A, B advance two slots per iteration, the
+  // half level one)
+  auto iteration = [&](int i, auto pi_tag) {
+    constexpr int PI = decltype(pi_tag)::value;
+    using P0 = std::integral_constant<int, (2 * PI) & 3>;
+    using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
+    using PHh = std::integral_constant<int, PI & 3>;
     const int t = ts + 2 * i;
     const int qb = qa >= 4 ? qa - 4 : qa + 3;   // pair i - 4 (mod 7)
-    stage_a(t, LA, qa, 0);
-    stage_a(t + 1, LB, qa, 1);
-    stage_h(qh);
-    stage_b(t, LA, qb, 0);
+    stage_a(t, LA, qa, std::integral_constant<int, 0>{}, P0{});
+    stage_a(t + 1, LB, qa, std::integral_constant<int, 1>{}, P1{});
+    stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{});   // hA: the half row stage A just pooled
+    stage_b(t, LA, qb, std::integral_constant<int, 0>{}, P0{});
     issue(t + 2, LA);
-    stage_b(t + 1, LB, qb, 1);
+    stage_b(t + 1, LB, qb, std::integral_constant<int, 1>{}, P1{});
     issue(t + 3, LB);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ring reads done before the producer refills
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     qa = qa == S2_WP - 1 ? 0 : qa + 1;
-    qh = (qh + 1) & (S2_HR - 1);
+  };
+  for (int i = 0; i < NI; i += S2_UNROLL) {
+    iteration(i, std::integral_constant<int, 0>{});
+    iteration(i + 1, std::integral_constant<int, 1>{});
+    iteration(i + 2, std::integral_constant<int, 2>{});
+    iteration(i + 3, std::integral_constant<int, 3>{});
   }
 }
 

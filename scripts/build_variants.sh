@@ -12,7 +12,7 @@ while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   objs=""
   for src in $SRCS; do
-    extra=""; [ "$src" = lnb_ops ] && extra=-fno-slp-vectorize
+    extra=""; { [ "$src" = lnb_ops ] || [ "$src" = graph_ops ]; } && extra=-fno-slp-vectorize
     $H $F $extra $defs -c $S/$src.hip -o exp/${src}_$name.o &
     objs="$objs exp/${src}_$name.o"
   done
