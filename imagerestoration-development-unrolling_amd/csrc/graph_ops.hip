@@ -276,12 +276,12 @@ static int seg_rows(int H, uint64_t units_per_seg) {
 // compiler cannot sink the v_mov_b32_dpp into a divergent branch (it turned
 // `c > 0 ? lane_prev(v) : 0` into an exec-masked branch before this was added).
 __device__ __forceinline__ float lane_prev(float v) {  // value of lane-1 (column c-1)
-  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
   asm volatile("" : "+v"(r));
   return r;
 }
 __device__ __forceinline__ float lane_next(float v) {  // value of lane+1 (column c+1)
-  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
   asm volatile("" : "+v"(r));
   return r;
 }
@@ -1370,7 +1370,10 @@ struct OpPipe {
   // planes, 2 pair planes); returns S_L^T (I - W) S_L x and S_G^T C^T C S_G x at row t-3
   // (before the mu / ro scales).  Lane = V adjacent columns starting at c0.  The arithmetic
   // of graph_row_kernel's consume (stages 2-4).
-  template <int P, int W>
+  // EDGE = false: the caller guarantees 1 <= t-2 <= H-2 (no row-boundary selects).  An
+  // interior-block copy of the step2 loop measured no gain: the duplicated body raised the
+  // register pressure into AGPR spills that cost what the selects did.
+  template <int P, int W, bool EDGE = true>
   __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
                                           int t, int H, int c0, const Taps& tL, const Taps& tG,
                                           float (&tl)[V], float (&tg)[V]) {
@@ -1411,8 +1414,8 @@ struct OpPipe {
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const int col = c0 + j;
-        const float up = r > 0 ? S0[j] : S1[j];
-        const float dn = r < H - 1 ? S2[j] : S1[j];
+        const float up = (!EDGE || r > 0) ? S0[j] : S1[j];
+        const float dn = (!EDGE || r < H - 1) ? S2[j] : S1[j];
         const float lf = col > 0 ? (j > 0 ? S1[j - 1] : pv) : S1[j];
         const float rt = col < W - 1 ? (j < V - 1 ? S1[j + 1] : nx) : S1[j];
         const float wx = ((WL[0][j] * up + WL[1][j] * lf) + WL[2][j] * rt) + WL[3][j] * dn;
@@ -1421,10 +1424,10 @@ struct OpPipe {
         const float snx = j < V - 1 ? G1[j + 1] : sn;
         const float spv = j > 0 ? G1[j - 1] : sp;
         const float chl = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
-        const float cvu = r > 0 ? cvp[j] : 0.f;
+        const float cvu = (!EDGE || r > 0) ? cvp[j] : 0.f;
         const float ov = WG[0][j] * (sv - snx) + chl * (sv - spv) + WG[1][j] * (sv - G2[j]) + cvu * (sv - G0[j]);
-        L[K3][j] = rin ? lv : 0.f;
-        O[K3][j] = rin ? ov : 0.f;
+        L[K3][j] = (!EDGE || rin) ? lv : 0.f;
+        O[K3][j] = (!EDGE || rin) ? ov : 0.f;
       }
 #pragma unroll
       for (int j = 0; j < V; ++j) cv[P & 1][j] = WG[1][j];
@@ -1628,11 +1631,12 @@ void graph_step2_kernel(Step2Args a) {
   float xa0[V], xb0[V];   // the even row of the current iteration (2x2 pooling)
 
   // stage A (stage k) at step t: emits row t-3 into the x / u rings, D x half rows at odd rows
-  auto stage_a = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag) {
+  auto stage_a = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag, auto edge_tag) {
     constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
+    constexpr bool EDGE = decltype(edge_tag)::value;
     float WL[4][V], WG[2][V], tl[V], tg[V];
     ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
-    PA.template advance<P, W>(S.x, WL, WG, t, H, c0, tL0, tG0, tl, tg);
+    PA.template advance<P, W, EDGE>(S.x, WL, WG, t, H, c0, tL0, tG0, tl, tg);
     const float (&x0)[V] = PA.template x_out<P>();
     const int y = t - 3;
     float xn[V], u[V];
@@ -1667,8 +1671,9 @@ void graph_step2_kernel(Step2Args a) {
   };
 
   // half level of D x_{k+1}: input half row hA - 1 (clamped), emits t_{k+1} half row hA - 4
-  auto stage_h = [&](int hA, int qh, auto ph_tag) {
+  auto stage_h = [&](int hA, int qh, auto ph_tag, auto edge_tag) {
     constexpr int P = decltype(ph_tag)::value;
+    constexpr bool EDGE = decltype(edge_tag)::value;
     const int hin = hA - 1;
     float xh[VH], WL[4][VH], WG[2][VH], tl[VH], tg[VH];
     {
@@ -1686,7 +1691,7 @@ void graph_step2_kernel(Step2Args a) {
       const F2 q = *reinterpret_cast<const F2*>(row + (4 + e) * S2_HW);
       WG[e][0] = q[0]; WG[e][1] = q[1];
     }
-    PH.template advance<P, hw>(xh, WL, WG, hin, h, ch0, tL1, tG1, tl, tg);
+    PH.template advance<P, hw, EDGE>(xh, WL, WG, hin, h, ch0, tL1, tG1, tl, tg);
 #pragma unroll
     for (int k = 0; k < VH; ++k) {
       float rv = tl[k] * scl1;
@@ -1696,15 +1701,16 @@ void graph_step2_kernel(Step2Args a) {
   };
 
   // stage B (stage k+1) at step t: input x_{k+1} row t-8, emits row t-11 to HBM
-  auto stage_b = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag) {
+  auto stage_b = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag, auto edge_tag) {
     constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
+    constexpr bool EDGE = decltype(edge_tag)::value;
     const int tb = t - 8;
     float xin[V], WL[4][V], WG[2][V], tl[V], tg[V], up[V];
     ld4(xr + (clampi(tb, 0, H - 1) & (S2_XR - 1)) * S2_W, xin);
     ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
     const int y = t - 11;
     ld4(ur + (((y % S2_UR) + S2_UR) % S2_UR) * S2_W, up);
-    PQ.template advance<P, W>(xin, WL, WG, tb, H, c0, tL0, tG0, tl, tg);
+    PQ.template advance<P, W, EDGE>(xin, WL, WG, tb, H, c0, tL0, tG0, tl, tg);
     const float (&x0)[V] = PQ.template x_out<P>();
     float res[V], xn[V], u[V];
 #pragma unroll
@@ -1760,31 +1766,33 @@ void graph_step2_kernel(Step2Args a) {
   // one iteration = two steps of stage A, one half-level row, two steps of stage B; PI = the
   // iteration's phase in the unrolled body (pipelines A, B advance two slots per iteration, the
   // half level one)
-  auto iteration = [&](int i, auto pi_tag) {
+  auto iteration = [&](int i, auto pi_tag, auto edge_tag) {
     constexpr int PI = decltype(pi_tag)::value;
     using P0 = std::integral_constant<int, (2 * PI) & 3>;
     using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
     using PHh = std::integral_constant<int, PI & 3>;
+    using E = decltype(edge_tag);
     const int t = ts + 2 * i;
     const int qb = qa >= 4 ? qa - 4 : qa + 3;   // pair i - 4 (mod 7)
-    stage_a(t, LA, qa, std::integral_constant<int, 0>{}, P0{});
-    stage_a(t + 1, LB, qa, std::integral_constant<int, 1>{}, P1{});
-    stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{});   // hA: the half row stage A just pooled
-    stage_b(t, LA, qb, std::integral_constant<int, 0>{}, P0{});
+    stage_a(t, LA, qa, std::integral_constant<int, 0>{}, P0{}, E{});
+    stage_a(t + 1, LB, qa, std::integral_constant<int, 1>{}, P1{}, E{});
+    stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{}, E{});   // hA: the half row stage A just pooled
+    stage_b(t, LA, qb, std::integral_constant<int, 0>{}, P0{}, E{});
     issue(t + 2, LA);
-    stage_b(t + 1, LB, qb, std::integral_constant<int, 1>{}, P1{});
+    stage_b(t + 1, LB, qb, std::integral_constant<int, 1>{}, P1{}, E{});
     issue(t + 3, LB);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ring reads done before the producer refills
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     qa = qa == S2_WP - 1 ? 0 : qa + 1;
   };
-  for (int i = 0; i < NI; i += S2_UNROLL) {
-    iteration(i, std::integral_constant<int, 0>{});
-    iteration(i + 1, std::integral_constant<int, 1>{});
-    iteration(i + 2, std::integral_constant<int, 2>{});
-    iteration(i + 3, std::integral_constant<int, 3>{});
-  }
+  auto block = [&](int i, auto edge_tag) {
+    iteration(i, std::integral_constant<int, 0>{}, edge_tag);
+    iteration(i + 1, std::integral_constant<int, 1>{}, edge_tag);
+    iteration(i + 2, std::integral_constant<int, 2>{}, edge_tag);
+    iteration(i + 3, std::integral_constant<int, 3>{}, edge_tag);
+  };
+  for (int i = 0; i < NI; i += S2_UNROLL) block(i, std::true_type{});
 }
 
 static int step2_seg_rows(int H, uint64_t blocks_per_seg) {
