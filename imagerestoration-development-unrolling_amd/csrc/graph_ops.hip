@@ -607,23 +607,23 @@ constexpr uint32_t GRR_OOB = 0x80000000u;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, p ? (int)bytes : 0, 0x00020000);
 }
-template <int N>
+template <int N, int AUX = 0>   // AUX: cache-policy bits (2 = nt)
 __device__ __forceinline__ void bload(float (&d)[N], rsrc_t r, uint32_t off) {
   if constexpr (N == 1) {
-    d[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    d[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
   } else {
     typedef typename VecT<N>::type T;
     T t;
-    if constexpr (N == 2) t = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-    else t = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    if constexpr (N == 2) t = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX));
+    else t = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
 #pragma unroll
     for (int j = 0; j < N; ++j) d[j] = t[j];
   }
 }
-template <int N>
+template <int N, int AUX = 0>
 __device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, const float (&v)[N]) {
   if constexpr (N == 1) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[0]), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[0]), r, off, 0, AUX);
   } else {
     typedef typename VecT<N>::type T;
     T t;
@@ -631,10 +631,10 @@ __device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, const float (&v)[
     for (int j = 0; j < N; ++j) t[j] = v[j];
     if constexpr (N == 2) {
       typedef uint32_t U2 __attribute__((ext_vector_type(2)));
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, t), r, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, t), r, off, 0, AUX);
     } else {
       typedef uint32_t U4 __attribute__((ext_vector_type(4)));
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, t), r, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, t), r, off, 0, AUX);
     }
   }
 }
@@ -1467,6 +1467,10 @@ constexpr int S2_PAIR = 2 * 6 * S2_W;      // floats per weight-ring pair
 constexpr int S2_HROW = 6 * S2_HW;         // floats per half-weight ring row
 constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW + S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW) +
                        S2_W + S2_HW;       // + one dummy row (writes of rows outside the image)
+#ifndef GRR_STEP2_NT
+#define GRR_STEP2_NT 1
+#endif
+constexpr int S2_NT = GRR_STEP2_NT ? 2 : 0;   // cache policy of step2's read-once / write-once streams
 constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipelines' slot period)
 static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
 
@@ -1503,8 +1507,13 @@ void graph_step2_kernel(Step2Args a) {
     const float* pcg1 = a.cG1 + (int64_t)(b * a.G + g) * 2 * hHW;
     auto dma = [&](const float* src, float* dst) {
       const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)dst;
+#if GRR_STEP2_NT
+      asm volatile("global_load_lds_dwordx4 %0, off nt" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
+                   : "memory");
+#else
       asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
                    : "memory");
+#endif
     };
     auto dma_pair = [&](int p) {   // full-level weight rows of steps ts+2p, ts+2p+1 (rows t-2)
       float* slot = wring + (p % S2_WP) * S2_PAIR;
@@ -1586,12 +1595,14 @@ void graph_step2_kernel(Step2Args a) {
   struct Ld {
     float x[V], eb[V], eu[V], th[VH], b2[V], y2[V];
   };
+  // read-once streams (x_k, u_k, t_k, weights) are non-temporal so that b's rows stay in L2
+  // for stage B's second read 8 rows later (one HBM read of b per launch)
   auto issue = [&](int t, Ld& S) {
-    bload(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
+    bload<V, S2_NT>(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
     const int re = clampi(t - 3, 0, H - 1);
     bload(S.eb, rb, vo + re * RB);
-    bload(S.eu, ru, vo + re * RB);
-    bload(S.th, rth, vo_half + (re >> 1) * HRB);
+    bload<V, S2_NT>(S.eu, ru, vo + re * RB);
+    bload<VH, S2_NT>(S.th, rth, vo_half + (re >> 1) * HRB);
     const int r2 = clampi(t - 11, 0, H - 1);
     bload(S.b2, rb, vo + r2 * RB);
     bload(S.y2, ry, vo + r2 * RB);
@@ -1728,8 +1739,8 @@ void graph_step2_kernel(Step2Args a) {
     }
     const bool yv = y >= r0 && y < r1;
     const uint32_t so = yv ? vo + (uint32_t)y * RB : GRR_OOB;
-    bstore(rout, so, res);
-    bstore(ruo, so, u);
+    bstore<V, S2_NT>(rout, so, res);
+    bstore<V, S2_NT>(ruo, so, u);
     if constexpr (PAR == 0) {
 #pragma unroll
       for (int j = 0; j < V; ++j) xb0[j] = xn[j];
@@ -1738,7 +1749,7 @@ void graph_step2_kernel(Step2Args a) {
 #pragma unroll
       for (int k = 0; k < VH; ++k)
         d[k] = 0.25f * xb0[2 * k] + 0.25f * xb0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
-      bstore(rxd, yv ? vo_half + (uint32_t)(y >> 1) * HRB : GRR_OOB, d);
+      bstore<VH, S2_NT>(rxd, yv ? vo_half + (uint32_t)(y >> 1) * HRB : GRR_OOB, d);
     }
   };
 

@@ -1,6 +1,6 @@
 """Micro-benchmark of single HIP kernels at the bench shape (P: B=64, G=32, F=3, 256x256).
 
-    python scripts/micro.py [--kernel step|half|lnb|conv1x1|edge] [--iters N] [--batch B]
+    python scripts/micro.py [--kernel step|step2|half|lnb|conv1x1|edge] [--iters N] [--batch B]
 
 Used under rocprofv3 (kernel trace / PMC passes) to profile one kernel in isolation.
 Prints mean milliseconds per launch and algorithmic GB/s from HIP events.
@@ -45,6 +45,15 @@ def main():
     if args.kernel == "step":
         fn = lambda: K.system_step(x, rhs, u, th, wl, cg, sl, sg, p(mix.muys00), p(mix.ro00), p(mix.alphaCGD)[2],  # noqa: E731
                                    p(mix.betaCGD)[2], g, want_u=True, want_pool=True)
+    elif args.kernel == "step2":
+        wl1 = torch.softmax(torch.rand(b, g, 4, h // 2, w // 2, device=dev), 2)
+        cg1 = torch.rand(b, g, 2, h // 2, w // 2, device=dev)
+        sl1, sg1 = K.stencil(mix.GLRmodule01), K.stencil(mix.GTVmodule01)
+        u_out = torch.empty_like(u)
+        fn = lambda: K.system_step2(x, rhs, u, th, wl, cg, sl, sg, p(mix.muys00), p(mix.ro00), wl1, cg1, sl1, sg1,  # noqa: E731
+                                    p(mix.muys01), p(mix.ro01), p(mix.alphaCGD)[2], p(mix.betaCGD)[2],
+                                    p(mix.alphaCGD)[3], p(mix.betaCGD)[3], g, want_u=True, want_pool=True,
+                                    u_out=u_out)
     elif args.kernel == "half":
         xd = torch.rand(b, c, h // 2, w // 2, device=dev)
         wl1 = torch.softmax(torch.rand(b, g, 4, h // 2, w // 2, device=dev), 2)
