@@ -9,9 +9,9 @@ N>1: one process per GPU (torchrun), each rank filters its own batch (the path s
 by patch — no data-path collective; scaling "weak"); the timed region is bracketed by
 barrier + synchronize on both sides and the max over ranks is reported.
 
-Rank 0 prints ONE JSON line with the metric, the roofline of the dominant kernel
-(grr_system_step, timed live with HIP events on its launch stream) and the CPU
-baseline (the oracle, timed on this host's cores on a bounded sample).
+Rank 0 prints ONE JSON line with the metric, the roofline of the dominant solver kernel
+(grr_system_step2: two CG stages per launch; timed live with HIP events on its launch
+stream) and the CPU baseline (the oracle, timed on this host's cores on a bounded sample).
 """
 from __future__ import annotations
 
@@ -80,19 +80,22 @@ def build_model(device, seed=2204, trained=False):
     return m.to(device).eval()
 
 
-# the kernel grr_system_step launches at the bench shape (W = 256: row waves, 4 columns per lane)
+# the solver kernels at the bench shape: grr_system_step2 (two CG stages per launch, stages 1-8)
+# and grr_system_step (W = 256 row waves: stages 0 and 9, or every stage with GRR_STEP2=0)
+STEP2_KERNEL = "graph_step2_kernel"
 STEP_KERNEL = "graph_row_kernel<true, 1, 2, 4>"
+TRAFFIC_FILES = {STEP2_KERNEL: "traffic_system_step2.json", STEP_KERNEL: "traffic_system_step.json"}
 
 
-def load_traffic():
-    """Per-launch HBM bytes of grr_system_step from the committed rocprofv3 PMC summary (or None
-    when the summary was collected on a different kernel)."""
-    path = os.path.join(ROOT, "profiles", "traffic_system_step.json")
+def load_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC summary under profiles/
+    (None when there is none for that kernel)."""
+    path = os.path.join(ROOT, "profiles", TRAFFIC_FILES[kernel])
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
-    if d.get("kernel") != STEP_KERNEL:
+    if d.get("kernel") != kernel:
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -262,14 +265,19 @@ def main():
 
     px_total = world * b * H * W * args.steps
     value = px_total / dt / 1e6
-    step = kern["system_step"]
+    # the dominant solver kernel: the two-stage launch where the filter uses it
+    kind, kname = ("system_step2", STEP2_KERNEL) if "system_step2" in kern else ("system_step", STEP_KERNEL)
+    step = kern[kind]
     achieved = step["gbps"]
-    traffic = load_traffic()
-    roofline = {"bound": "hbm", "kernel": f"grr_system_step ({STEP_KERNEL})",
+    traffic = load_traffic(kname)
+    roofline = {"bound": "hbm", "kernel": f"grr_{kind} ({kname})",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "bytes_per_launch": step["bytes_per_launch"], "mean_launch_ms": round(step["mean_ms"], 4),
                 "launches": step["launches"]}
+    if kind == "system_step2":
+        roofline["stages_per_launch"] = 2
+        roofline["ms_per_stage"] = round(step["mean_ms"] / 2, 4)
     # context for frac: a float4 streaming copy's rate on this GPU (read + write bytes / time),
     # i.e. what a pure streaming kernel reaches here; measured after the timed region
     src = torch.empty(1 << 30, dtype=torch.float32, device=dev)
