@@ -193,6 +193,7 @@ struct OpArgs {
   float* xd_out;
   int G, F, H, W, tiles_x, tiles_y;
   int nstrips, nsegs, sseg;
+  int sw;               // row kernel, wide images: output columns per strip (W when one strip)
   int lin_l;            // log_l holds the scale itself (v10 MixtureGLR stores mu linearly)
   int wpb;              // row kernel: waves per block = channels of one graph walked in lockstep
   int x_rep, y_rep;     // operand is [B, F, H, W], replicated over the G graphs (channel g F + f reads f)
@@ -684,18 +685,25 @@ void graph_row_kernel(OpArgs a) {
   const int F = a.F;
   const int f = unit % F; unit /= F;
   const int seg = unit % a.nsegs; unit /= a.nsegs;
+  const int strip = unit % a.nstrips; unit /= a.nstrips;
   const int g = unit % a.G;
   const int b = unit / a.G;
   const int H = a.H, W = a.W, C = a.G * F, ch = g * F + f;
   const int hh = H / 2, hw = W / 2;
   const int64_t HW = (int64_t)H * W;
-  const int c0 = V * lane;                       // first column of this lane
-  const bool lane_on = c0 < W;                   // W % V == 0: a lane is all-in or all-out
-  const int cl0 = lane_on ? c0 : W - V;          // clamped (loads of idle lanes duplicate)
+  // Wide rows (W > 64 V): strips of output columns [xs, xe); a strip's wave covers 64 V columns
+  // from x0 = xs - 4 (4 halo columns each side, whole lanes; strip 0 starts at the image edge).
+  // Lanes past the right halo or the image read nothing (out-of-range offsets read 0).
+  const int xs = strip * a.sw, xe = min(xs + a.sw, W);
+  const int x0 = strip > 0 ? xs - 4 : 0;
+  const int c0 = x0 + V * lane;                  // first column of this lane
+  const bool lane_on = c0 >= xs && c0 < xe;      // W % V == 0: a lane is all-in or all-out
+  const bool lane_ld = c0 < min(xe + 4, W);      // lanes with columns this strip reads
+  const int cl0 = lane_ld ? c0 : W - V;          // clamped column for the weight-row DMAs
   const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
-  const uint32_t vo = (uint32_t)cl0 * 4u;
+  const uint32_t vo = lane_ld ? (uint32_t)c0 * 4u : GRR_OOB;
   // half-resolution column(s) of this lane: V=4 -> 2l, 2l+1; V=2 -> l; V=1 -> l/2
-  const uint32_t vo_half = (uint32_t)(cl0 >> 1) * 4u;
+  const uint32_t vo_half = lane_ld ? (uint32_t)(c0 >> 1) * 4u : GRR_OOB;
   const bool owner_xd = lane_on && (V > 1 || ((c0 & 1) == 0 && c0 + 1 < W));
 
   const int64_t plane = ((int64_t)b * C + ch) * HW;
@@ -1043,9 +1051,16 @@ static int row_vec(int W) {
 
 template <bool GLR, int GTV, int EPI, int V>
 static void launch_row(OpArgs a, int B, hipStream_t s) {
-  a.sseg = seg_rows(a.H, (uint64_t)B * a.G * a.F);
+  // wide images: strips of at most 64 V - 8 output columns (a multiple of V), 4 halo columns each side
+  a.nstrips = 1;
+  a.sw = a.W;
+  if (a.W > 64 * V) {
+    a.nstrips = (a.W + 64 * V - 9) / (64 * V - 8);
+    a.sw = ((a.W + a.nstrips - 1) / a.nstrips + V - 1) / V * V;
+  }
+  a.sseg = seg_rows(a.H, (uint64_t)B * a.G * a.F * a.nstrips);
   a.nsegs = (a.H + a.sseg - 1) / a.sseg;
-  const uint64_t units = (uint64_t)B * a.G * a.F * a.nsegs;
+  const uint64_t units = (uint64_t)B * a.G * a.F * a.nsegs * a.nstrips;
   a.nunits = (uint32_t)units;
   // channels of a graph per block: the largest divisor of F that fits NT threads.  Only for
   // V = 4 (W > 128): on 128-wide half-resolution planes the unsynchronised waves measured 4 %
@@ -1068,6 +1083,8 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
                   (1ull << 32) - 4,
               GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   int vec = g_kernel_variant == 1 ? 0 : row_vec(a0.W);
+  // wider rows: the V = 4 row kernel in column strips (4 halo columns per side)
+  if (vec == 0 && g_kernel_variant != 1 && a0.W > 256 && a0.W % 4 == 0) vec = 4;
   // row kernels address a graph's 4 weight planes through one buffer resource (int range)
   if ((int64_t)a0.H * a0.W * 16 >= (1ll << 31)) vec = 0;
   if (vec > 1) {   // vector row loads need every operand base aligned to 4V bytes

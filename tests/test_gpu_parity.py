@@ -149,9 +149,11 @@ def test_edge_weights_block(irdu, variant, shape):
     assert_close(wL, O.edge_weights(fo[:, 1], mL.cpu())[0], 1e-5)
 
 
-# widths: <= 64 (1 column per lane), 70 (2), 200 / 256 (4), 130 (W % 4 != 0 -> strips)
+# widths: <= 64 (1 column per lane), 70 (2), 200 / 256 (4), 130 (W % 4 != 0 -> strips),
+# 300 / 512 / 1000 (4 columns per lane in 248-column strips with 4 halo columns)
 @pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 37, 45), (1, 3, 2, 9, 70), (1, 2, 3, 12, 200),
-                                   (1, 1, 3, 10, 256), (1, 2, 3, 7, 130)])
+                                   (1, 1, 3, 10, 256), (1, 2, 3, 7, 130), (1, 1, 3, 11, 300), (1, 2, 3, 9, 512),
+                                   (1, 1, 2, 6, 1000)])
 def test_glr_gtv_operators_random(irdu, variant, shape):
     b, g, f, h, w = shape
     x = rand(b, g, f, h, w, seed=2)
@@ -167,7 +169,8 @@ def test_glr_gtv_operators_random(irdu, variant, shape):
         assert_close(gtv(x.to(DEV), wg.to(DEV)), O.gtv_apply(x, wg, kg))
 
 
-@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 21, 31), (1, 2, 3, 10, 100), (1, 2, 3, 13, 132)])
+@pytest.mark.parametrize("shape", [(2, 4, 3, 32, 32), (1, 2, 6, 21, 31), (1, 2, 3, 10, 100), (1, 2, 3, 13, 132),
+                                   (1, 2, 3, 8, 520)])
 def test_gtv_prox_rhs_half(irdu, variant, shape):
     """C^T phi(C x) with the soft-threshold phi of the proximal step (a12, a16)."""
     b, g, f, h, w = shape
@@ -326,7 +329,8 @@ def test_abstract_model_golden(irdu):
 # ---------------------------------------------------------------------------
 # S = 10 stages (the metric's configuration) against the oracle
 @pytest.mark.parametrize("case", [dict(g=4, b=2, h=32, w=32), dict(g=32, b=1, h=64, w=96),
-                                  dict(g=4, b=1, h=24, w=256), dict(g=4, b=1, h=16, w=300)])
+                                  dict(g=4, b=1, h=24, w=256), dict(g=4, b=1, h=16, w=300),
+                                  dict(g=4, b=1, h=20, w=512)])
 def test_msgf_ten_stages_vs_oracle(irdu, variant, case):
     g, b, h, w = case["g"], case["b"], case["h"], case["w"]
     torch.manual_seed(2204)
