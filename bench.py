@@ -63,7 +63,7 @@ def build_model(device, seed=2204, trained=False):
     """Reference init (default conv init + the reference's solver init constants), except the
     final 1x1 projection, set to the per-colour mean over the G filtered copies so that the
     output is an image.  trained=True loads the weights fixture that
-    scripts/train_psnr_fixture.py trained from this init (3,000 Adam steps on synthetic
+    scripts/train_psnr_fixture.py trained from this init (4,000 Adam steps on synthetic
     sigma-25 patches; safetensors, weights only), so PSNR is measured on a filter that denoises."""
     import irdu_amd
     torch.manual_seed(seed)

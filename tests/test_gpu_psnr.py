@@ -1,7 +1,7 @@
 """PSNR parity on weights that denoise (the metric's "PSNR within 0.01 dB of reference").
 
 No reference checkpoint exists, so scripts/train_psnr_fixture.py trained the bench's image filter
-(MultiScaleGraphFilter G=32 F=3 S=10) on the HIP training path for 3,000 Adam steps on synthetic
+(MultiScaleGraphFilter G=32 F=3 S=10) on the HIP training path for 4,000 Adam steps on synthetic
 sigma-25 patches; the weights are the committed fixture tests/golden/msgf_trained_g32_s10.safetensors
 (loaded weights-only).  On held-out patches (a different generator and seed than the training
 data) the HIP forward must match the CPU oracle within 1e-4 relative and 0.01 dB, while actually
