@@ -203,6 +203,255 @@ __global__ __launch_bounds__(NT) void gate_kernel(const float* __restrict__ hp, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-streaming depthwise 3x3 (W <= 64 V, W % V == 0): one wave = one (b, channel) plane and a
+// segment of rows, lane = V adjacent columns; rows r-1, r, r+1 of the operands stay in
+// registers (one row load per row and operand, prefetched one row ahead), horizontal
+// neighbours come from DPP lane shifts.  The per-pixel kernels above issue nine scalar
+// loads per output pixel and are L1-bound (dwconv3 2.3 TB/s, dwconv3_bwd 1.6 TB/s).
+// ---------------------------------------------------------------------------
+template <int V> struct RowVec;
+template <> struct RowVec<1> { typedef float T; };
+template <> struct RowVec<2> { typedef float __attribute__((ext_vector_type(2))) T; };
+template <> struct RowVec<4> { typedef float __attribute__((ext_vector_type(4))) T; };
+
+template <int V>
+__device__ __forceinline__ void row_load(float (&d)[V], const float* p) {
+  const typename RowVec<V>::T t = *reinterpret_cast<const typename RowVec<V>::T*>(p);
+  if constexpr (V == 1) {
+    d[0] = t;
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) d[j] = t[j];
+  }
+}
+template <int V>
+__device__ __forceinline__ void row_store(float* p, const float (&v)[V]) {
+  typename RowVec<V>::T t;
+  if constexpr (V == 1) {
+    t = v[0];
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) t[j] = v[j];
+  }
+  *reinterpret_cast<typename RowVec<V>::T*>(p) = t;
+}
+// value of lane -1 / +1 (0 past the wave's ends); the asm pins the DPP at its definition
+__device__ __forceinline__ float dpp_prev(float v) {
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ float dpp_next(float v) {
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+struct Dw3RowGeom {
+  int lane, c0, cl0;
+  bool on;
+  int plane, c, r0, r1;
+};
+template <int V>
+__device__ __forceinline__ bool dw3_row_geom(Dw3RowGeom& q, int C, int H, int W, int sseg, int nsegs, uint32_t nwaves) {
+  q.lane = threadIdx.x & 63;
+  const uint32_t wid = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (wid >= nwaves) return false;   // whole waves only
+  const int seg = (int)(wid % nsegs);
+  q.plane = (int)(wid / nsegs);
+  q.c = q.plane % C;
+  q.r0 = seg * sseg;
+  q.r1 = min(q.r0 + sseg, H);
+  q.c0 = V * q.lane;
+  q.on = q.c0 < W;
+  q.cl0 = q.on ? q.c0 : W - V;
+  return true;
+}
+
+// out(r, c) = sum_t w_t h(clamp(r + dy), clamp(c + dx))  (same taps and order as dw3_fwd_kernel)
+template <int V>
+__global__ __launch_bounds__(NT) void dw3_row_fwd_kernel(const float* __restrict__ h, const float* __restrict__ wdw,
+                                                         float* __restrict__ out, int C, int H, int W, int sseg,
+                                                         int nsegs, uint32_t nwaves) {
+  Dw3RowGeom q;
+  if (!dw3_row_geom<V>(q, C, H, W, sseg, nsegs, nwaves)) return;
+  const int64_t HW = (int64_t)H * W;
+  const float* hp = h + q.plane * HW + q.cl0;
+  float* op = out + q.plane * HW + q.cl0;
+  float wt[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wt[t] = wdw[q.c * 9 + t];
+  float R[3][V], N[V];
+  row_load<V>(R[0], hp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load<V>(R[1], hp + (int64_t)q.r0 * W);
+  row_load<V>(N, hp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  for (int r = q.r0; r < q.r1; ++r) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) R[2][j] = N[j];
+    row_load<V>(N, hp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    float o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float pv = dpp_prev(R[dy][V - 1]), nx = dpp_next(R[dy][0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = q.c0 + j;
+        const float l = col > 0 ? (j > 0 ? R[dy][j - 1] : pv) : R[dy][j];
+        const float rr = col < W - 1 ? (j < V - 1 ? R[dy][j + 1] : nx) : R[dy][j];
+        o[j] += wt[dy * 3 + 0] * l;
+        o[j] += wt[dy * 3 + 1] * R[dy][j];
+        o[j] += wt[dy * 3 + 2] * rr;
+      }
+    }
+    if (q.on) row_store<V>(op + (int64_t)r * W, o);
+#pragma unroll
+    for (int j = 0; j < V; ++j) { R[0][j] = R[1][j]; R[1][j] = R[2][j]; }
+  }
+}
+
+// One pass for both gradients of the depthwise conv:
+//   gh(q) = sum_t w_t sum_{p: clamp(p + t) = q} g(p)   (adjoint of the clamped gather, separable:
+//           rows then columns; along an axis the sources of q for offset d are q - d when inside,
+//           plus q itself at the edge the clamp folds onto)
+//   gw[c, t] += sum_p g(p) h(clamp(p + t))              (wave sums, one atomic per tap and wave)
+template <int V>
+__global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict__ g, const float* __restrict__ h,
+                                                         const float* __restrict__ wdw, float* __restrict__ gh,
+                                                         float* __restrict__ gw, int C, int H, int W, int sseg,
+                                                         int nsegs, uint32_t nwaves) {
+  Dw3RowGeom q;
+  if (!dw3_row_geom<V>(q, C, H, W, sseg, nsegs, nwaves)) return;
+  const int64_t HW = (int64_t)H * W;
+  const float* gp = g + q.plane * HW + q.cl0;
+  const float* hp = h + q.plane * HW + q.cl0;
+  float* ghp = gh + q.plane * HW + q.cl0;
+  float wt[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wt[t] = wdw[q.c * 9 + t];
+  float acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+  // g rows r-1, r, r+1 (zero outside the image: the adjoint has no sources there), h rows clamped
+  float G[3][V], Hh[3][V], NG[V], NH[V];
+  auto gload = [&](float (&d)[V], int rr) {
+    if (rr >= 0 && rr < H) {
+      row_load<V>(d, gp + (int64_t)rr * W);
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) d[j] = 0.f;
+    }
+  };
+  gload(G[0], q.r0 - 1);
+  gload(G[1], q.r0);
+  gload(NG, q.r0 + 1);
+  row_load<V>(Hh[0], hp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load<V>(Hh[1], hp + (int64_t)q.r0 * W);
+  row_load<V>(NH, hp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  for (int r = q.r0; r < q.r1; ++r) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) { G[2][j] = NG[j]; Hh[2][j] = NH[j]; }
+    gload(NG, r + 2);
+    row_load<V>(NH, hp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    // row adjoint: tap row dy (0: -1, 1: 0, 2: +1) reads g at row r - (dy - 1)
+    float A[3][V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      A[0][j] = r == 0 ? G[2][j] + G[1][j] : G[2][j];        // dy = -1: sources r + 1, and r at the top
+      A[1][j] = G[1][j];
+      A[2][j] = r == H - 1 ? G[0][j] + G[1][j] : G[0][j];    // dy = +1: sources r - 1, and r at the bottom
+    }
+    float o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float pv = dpp_prev(A[dy][V - 1]), nx = dpp_next(A[dy][0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = q.c0 + j;
+        const float a = A[dy][j];
+        const float al = j > 0 ? A[dy][j - 1] : pv;      // column c - 1 (0 left of the image)
+        const float ar = j < V - 1 ? A[dy][j + 1] : nx;  // column c + 1
+        const float sm = col + 1 < W ? (col == 0 ? ar + a : ar) : (col == 0 ? a : 0.f);   // dx = -1
+        const float sp = col >= 1 ? (col == W - 1 ? al + a : al) : (col == W - 1 ? a : 0.f);  // dx = +1
+        o[j] += wt[dy * 3 + 0] * sm;
+        o[j] += wt[dy * 3 + 1] * a;
+        o[j] += wt[dy * 3 + 2] * sp;
+      }
+    }
+    if (q.on) row_store<V>(ghp + (int64_t)r * W, o);
+    // weight gradient: g(r, c) h(clamp(r + dy), clamp(c + dx))
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float pv = dpp_prev(Hh[dy][V - 1]), nx = dpp_next(Hh[dy][0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = q.c0 + j;
+        const float gv = q.on ? G[1][j] : 0.f;
+        const float l = col > 0 ? (j > 0 ? Hh[dy][j - 1] : pv) : Hh[dy][j];
+        const float rr = col < W - 1 ? (j < V - 1 ? Hh[dy][j + 1] : nx) : Hh[dy][j];
+        acc[dy * 3 + 0] += gv * l;
+        acc[dy * 3 + 1] += gv * Hh[dy][j];
+        acc[dy * 3 + 2] += gv * rr;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      G[0][j] = G[1][j]; G[1][j] = G[2][j];
+      Hh[0][j] = Hh[1][j]; Hh[1][j] = Hh[2][j];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const float s = wave_sum(acc[t]);
+    if (q.lane == 0 && s != 0.f) atomicAdd(gw + q.c * 9 + t, s);
+  }
+}
+
+// V for the row kernels (0: not applicable -> per-pixel kernels)
+int dw3_row_vec(int W) {
+  if (W <= 64) return 1;
+  if (W <= 128 && W % 2 == 0) return 2;
+  if (W <= 256 && W % 4 == 0) return 4;
+  return 0;
+}
+// rows per wave: whole planes while the grid has >= 4096 waves, else segments of >= 32 rows
+int dw3_row_seg(int H, int64_t planes) {
+  int sseg = H;
+  while (sseg > 32 && planes * ((H + sseg - 1) / sseg) < 4096) sseg = (sseg + 1) / 2;
+  return sseg;
+}
+template <int V>
+void launch_dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gw, int B, int C,
+                    int H, int W, hipStream_t s) {
+  const int64_t planes = (int64_t)B * C;
+  const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
+  const uint32_t nwaves = (uint32_t)(planes * nsegs);
+  const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+  if (bwd)
+    hipLaunchKernelGGL(dw3_row_bwd_kernel<V>, grid, dim3(NT), 0, s, g, h, wdw, out, gw, C, H, W, sseg, nsegs, nwaves);
+  else
+    hipLaunchKernelGGL(dw3_row_fwd_kernel<V>, grid, dim3(NT), 0, s, h, wdw, out, C, H, W, sseg, nsegs, nwaves);
+}
+bool dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gw, int B, int C, int H,
+             int W, hipStream_t s) {
+  const int V = dw3_row_vec(W);
+  // vector row loads: plane bases aligned to 4 V bytes
+  const void* ptrs[] = {g, h, out};
+  for (const void* p : ptrs)
+    if (p && (uintptr_t)p % (4u * V) != 0) return false;
+  if ((int64_t)B * C * ((H + 31) / 32) >= (1ll << 31)) return false;
+  switch (V) {
+    case 1: launch_dw3_row<1>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
+    case 2: launch_dw3_row<2>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
+    case 4: launch_dw3_row<4>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
+    default: return false;
+  }
+}
+
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
 int chunks_for(int64_t n, int64_t planes) {
   const int64_t want = (4096 + planes - 1) / planes;
@@ -244,6 +493,7 @@ grr_status grr_lnb_norm_bwd(const float* x, const float* ln_w, const float* isd,
 grr_status grr_dwconv3(const float* h, const float* wdw, float* out, int B, int C, int H, int W, void* stream) {
   clear_error();
   GRR_REQUIRE(h && wdw && out && B > 0 && C > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG, "grr_dwconv3: bad args");
+  if (dw3_row(false, nullptr, h, wdw, out, nullptr, B, C, H, W, (hipStream_t)stream)) return launch_status("grr_dwconv3");
   GRR_REQUIRE((int64_t)B * C <= 65535, GRR_ERR_UNSUPPORTED, "grr_dwconv3: B*C > 65535");
   hipLaunchKernelGGL(dw3_fwd_kernel, dim3((H * W + NT - 1) / NT, B * C), dim3(NT), 0, (hipStream_t)stream, h, wdw,
                      out, C, H, W);
@@ -255,6 +505,7 @@ grr_status grr_dwconv3_bwd(const float* g, const float* h, const float* wdw, flo
   clear_error();
   GRR_REQUIRE(g && h && wdw && gh && gwdw && B > 0 && C > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_dwconv3_bwd: bad args");
+  if (dw3_row(true, g, h, wdw, gh, gwdw, B, C, H, W, (hipStream_t)stream)) return launch_status("grr_dwconv3_bwd");
   GRR_REQUIRE((int64_t)B * C <= 65535, GRR_ERR_UNSUPPORTED, "grr_dwconv3_bwd: B*C > 65535");
   hipLaunchKernelGGL(dw3_bwd_data_kernel, dim3((H * W + NT - 1) / NT, B * C), dim3(NT), 0, (hipStream_t)stream, g,
                      wdw, gh, C, H, W);

@@ -695,7 +695,8 @@ def dwconv3_bwd(g: Tensor, h: Tensor, wdw: Tensor, gwdw: Tensor) -> Tensor:
     dev = _check("dwconv3_bwd", g, h, wdw, gwdw)
     b, c, hh, ww = h.shape
     gh = torch.empty_like(h)
-    _launch("dwconv3_bwd", 16 * h.numel(), "grr_dwconv3_bwd", g.data_ptr(), h.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
+    # compulsory bytes: g and h read once, gh written once (one fused pass for W <= 256)
+    _launch("dwconv3_bwd", 12 * h.numel(), "grr_dwconv3_bwd", g.data_ptr(), h.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
             gwdw.data_ptr(), b, c, hh, ww, _stream(dev))
     return gh
 
