@@ -724,6 +724,356 @@ __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
     for (int t = 0; t < 5; ++t) block_atomic_add(gtaps + (gi * F + f) * 5 + t, sc * (accT[f][t] + accP[f][t]));
 }
 
+// ---------------------------------------------------------------------------
+// The same term reverse as a row-streaming kernel (W <= 64 V, W % V == 0): one workgroup = the
+// F channel waves of one (b, graph, row segment), lane = V adjacent columns.  Each wave keeps
+// x and g rows t-3..t, s = P x and a = T* g rows t-3..t-1 in registers (vertical neighbours)
+// and takes horizontal neighbours by DPP lane shifts; per output row r = t-2 it evaluates the
+// per-pixel arithmetic of term_bwd_fused_kernel (same expressions, same order) for its
+// channel.  The weight gradient sums over the F channels of the graph: each wave writes its
+// row of partials to LDS (double-buffered by row parity, one barrier per row) and the sum in
+// channel order is added to gw by the wave that owns the plane.  x, g, w are read once and v,
+// gw written once per launch (the per-pixel kernel re-reads every operand 5-25 times from
+// L1/L2 and runs at ≈ 1.7 TB/s).
+// ---------------------------------------------------------------------------
+int g_term_rows = 1;   // grr_bwd_set_term_rows: 0 = per-pixel term reverses (A/B and tests)
+
+template <int V> struct RowT;
+template <> struct RowT<1> { typedef float T; };
+template <> struct RowT<2> { typedef float __attribute__((ext_vector_type(2))) T; };
+template <> struct RowT<4> { typedef float __attribute__((ext_vector_type(4))) T; };
+template <int V>
+__device__ __forceinline__ void rload(float (&d)[V], const float* p) {
+  const typename RowT<V>::T t = *reinterpret_cast<const typename RowT<V>::T*>(p);
+  if constexpr (V == 1) {
+    d[0] = t;
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) d[j] = t[j];
+  }
+}
+template <int V>
+__device__ __forceinline__ void rstore(float* p, const float (&v)[V]) {
+  typename RowT<V>::T t;
+  if constexpr (V == 1) {
+    t = v[0];
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) t[j] = v[j];
+  }
+  *reinterpret_cast<typename RowT<V>::T*>(p) = t;
+}
+__device__ __forceinline__ float lprev(float v) {   // lane - 1 (0 at lane 0)
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ float lnext(float v) {   // lane + 1 (0 at lane 63)
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+constexpr int TR_FMAX = 4;
+template <int MODE, int V>
+__global__ __launch_bounds__(NT) void term_row_kernel(
+    const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
+    const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
+    float* __restrict__ v_out, float* __restrict__ gw, float* __restrict__ ggam, float* __restrict__ gdot,
+    float* __restrict__ gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
+  constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
+  __shared__ __attribute__((aligned(16))) float part[2][TR_FMAX][WPL][64 * V];
+  const int lane = threadIdx.x & 63;
+  const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t unit = xcd_remap(blockIdx.x, nblk);
+  const int seg = unit % nsegs;
+  const int bg = unit / nsegs, gi = bg % G;
+  const int r0 = seg * sseg, r1 = min(r0 + sseg, H);
+  const int c0 = V * lane;
+  const bool on = c0 < W;
+  const int cl0 = on ? c0 : W - V;
+  const int64_t HW = (int64_t)H * W;
+  const float sc = scale ? scale[gi] : 1.f;
+  const float gm = MODE == 2 ? expf(log_gamma[gi]) : 0.f;
+  float k[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) k[t] = taps[(gi * F + f) * 5 + t];
+  const int64_t base = ((int64_t)bg * F + f) * HW + cl0;
+  const float* xp = x + base;
+  const float* gp = g + base;
+  float* vp = v_out + base;
+  const float* wb = w + (int64_t)bg * WPL * HW + cl0;
+  float* gwb = gw + (int64_t)bg * WPL * HW + cl0;
+
+  float X[4][V], Gr[4][V], S[3][V], A[3][V];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) X[i][j] = Gr[i][j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) S[i][j] = A[i][j] = 0.f;
+  // weight rows: MODE 0/2: plane 0 rows r, r+1; plane 3 rows r-1, r; planes 1, 2 row r.
+  //              MODE 1:   plane 0 row r; plane 1 rows r-1, r.
+  float W0[2][V], W3[2][V], W1[V], W2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) W0[0][j] = W0[1][j] = W3[0][j] = W3[1][j] = W1[j] = W2[j] = 0.f;
+  float accT[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accP[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float dot = 0.f, dgam = 0.f;
+
+  auto xrow = [&](float (&d)[V], int rr) { rload<V>(d, xp + (int64_t)clampi(rr, 0, H - 1) * W); };
+  auto grow = [&](float (&d)[V], int rr) {
+    if (rr >= 0 && rr < H) {
+      rload<V>(d, gp + (int64_t)rr * W);
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) d[j] = 0.f;
+    }
+  };
+  auto wrow = [&](float (&d)[V], int e, int rr) {   // rows outside the image are never used (selects)
+    rload<V>(d, wb + e * HW + (int64_t)clampi(rr, 0, H - 1) * W);
+  };
+  // prefetched operands of the next step
+  float NX[V], NG[V], NW0[V], NW3[V], NW1[V], NW2[V];
+  const int t0 = r0 - 1;
+  auto prefetch = [&](int t) {   // step t: x, g row t; weights of output row t - 2 (plane 0 row t - 1)
+    xrow(NX, t);
+    grow(NG, t);
+    if constexpr (MODE == 1) {
+      wrow(NW0, 0, t - 2);
+      wrow(NW3, 1, t - 2);
+    } else {
+      wrow(NW0, 0, t - 1);
+      wrow(NW1, 1, t - 2);
+      wrow(NW2, 2, t - 2);
+      wrow(NW3, 3, t - 2);
+    }
+  };
+  // fill: steps r0 - 3 .. r0 - 2 (x, g rows; no output)
+  xrow(X[2], r0 - 3);
+  grow(Gr[2], r0 - 3);
+  xrow(X[3], r0 - 2);
+  grow(Gr[3], r0 - 2);
+  if constexpr (MODE != 1) wrow(W0[1], 0, r0 - 2);
+  prefetch(t0);
+  int par = 0;
+  for (int t = t0; t <= r1 + 1; ++t) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      X[0][j] = X[1][j]; X[1][j] = X[2][j]; X[2][j] = X[3][j]; X[3][j] = NX[j];
+      Gr[0][j] = Gr[1][j]; Gr[1][j] = Gr[2][j]; Gr[2][j] = Gr[3][j]; Gr[3][j] = NG[j];
+      if constexpr (MODE == 1) {
+        W0[0][j] = NW0[j];
+        W3[0][j] = W3[1][j]; W3[1][j] = NW3[j];
+      } else {
+        W0[0][j] = W0[1][j]; W0[1][j] = NW0[j];
+        W3[0][j] = W3[1][j]; W3[1][j] = NW3[j];
+        W1[j] = NW1[j]; W2[j] = NW2[j];
+      }
+    }
+    if (t + 1 <= r1 + 1) prefetch(t + 1);
+    // s = P x (replicate) and a = T* g (zero frame) at row t - 1
+    {
+      const float xp_ = lprev(X[2][V - 1]), xn_ = lnext(X[2][0]);
+      const float gp_ = lprev(Gr[2][V - 1]), gn_ = lnext(Gr[2][0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        const float xl = col > 0 ? (j > 0 ? X[2][j - 1] : xp_) : X[2][j];
+        const float xr = col < W - 1 ? (j < V - 1 ? X[2][j + 1] : xn_) : X[2][j];
+        const float gl = col > 0 ? (j > 0 ? Gr[2][j - 1] : gp_) : 0.f;
+        const float gr = col + 1 < W ? (j < V - 1 ? Gr[2][j + 1] : gn_) : 0.f;
+        S[0][j] = S[1][j]; S[1][j] = S[2][j];
+        A[0][j] = A[1][j]; A[1][j] = A[2][j];
+        S[2][j] = k[0] * X[2][j] + k[1] * X[1][j] + k[2] * xl + k[3] * xr + k[4] * X[3][j];
+        A[2][j] = k[0] * Gr[2][j] + k[1] * Gr[1][j] + k[2] * gl + k[3] * gr + k[4] * Gr[3][j];
+      }
+    }
+    const int r = t - 2;
+    if (r < r0) continue;   // pipeline fill (uniform over the workgroup)
+    // output row r: s, a rows r-1, r, r+1 = S[0..2]; x, g rows r-1, r, r+1 = X[0..2], Gr[0..2]
+    const bool in0 = r > 0, in3 = r + 1 < H;
+    const float s_p = lprev(S[1][V - 1]), s_n = lnext(S[1][0]);
+    const float a_p = lprev(A[1][V - 1]), a_n = lnext(A[1][0]);
+    const float x_p = lprev(X[1][V - 1]), x_n = lnext(X[1][0]);
+    const float g_p = lprev(Gr[1][V - 1]), g_n = lnext(Gr[1][0]);
+    float w1n = 0.f, w2p = 0.f, c0p = 0.f;
+    if constexpr (MODE == 1) c0p = lprev(W0[0][V - 1]);
+    else { w1n = lnext(W1[0]); w2p = lprev(W2[V - 1]); }
+    float vrow[V], gwa[WPL][V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int col = c0 + j;
+      const bool in1 = col > 0, in2 = col + 1 < W;
+      const float sv = S[1][j], av = A[1][j];
+      float s5[5], a5[5], xt[5], gt5[5];
+      s5[0] = sv;
+      s5[1] = in0 ? S[0][j] : sv;
+      s5[2] = in1 ? (j > 0 ? S[1][j - 1] : s_p) : sv;
+      s5[3] = in2 ? (j < V - 1 ? S[1][j + 1] : s_n) : sv;
+      s5[4] = in3 ? S[2][j] : sv;
+      a5[0] = av;
+      a5[1] = in0 ? A[0][j] : av;
+      a5[2] = in1 ? (j > 0 ? A[1][j - 1] : a_p) : av;
+      a5[3] = in2 ? (j < V - 1 ? A[1][j + 1] : a_n) : av;
+      a5[4] = in3 ? A[2][j] : av;
+      xt[0] = X[1][j]; xt[1] = X[0][j]; xt[4] = X[2][j];
+      xt[2] = in1 ? (j > 0 ? X[1][j - 1] : x_p) : X[1][j];
+      xt[3] = in2 ? (j < V - 1 ? X[1][j + 1] : x_n) : X[1][j];
+      gt5[0] = Gr[1][j]; gt5[1] = Gr[0][j]; gt5[4] = Gr[2][j];
+      gt5[2] = in1 ? (j > 0 ? Gr[1][j - 1] : g_p) : 0.f;
+      gt5[3] = in2 ? (j < V - 1 ? Gr[1][j + 1] : g_n) : 0.f;
+      float z = 0.f, v = 0.f;
+      if constexpr (MODE == 0) {
+        const bool in[4] = {in0, in1, in2, in3};
+        const float we[4] = {W0[0][j], W1[j], W2[j], W3[1][j]};
+        const float wn[4] = {in3 ? W0[1][j] : 0.f, in2 ? (j < V - 1 ? W1[j + 1] : w1n) : 0.f,
+                             in1 ? (j > 0 ? W2[j - 1] : w2p) : 0.f, in0 ? W3[0][j] : 0.f};
+        float wta = 0.f;
+        z = sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sn = s5[e + 1];
+          z -= we[e] * sn;
+          gwa[e][j] = -(av * sn);
+          wta += in[3 - e] ? wn[e] * a5[(3 - e) + 1] : 0.f;
+          wta += in[e] ? 0.f : we[e] * av;
+        }
+        v = av - wta;
+      } else if constexpr (MODE == 1) {
+        const float cr = in2 ? W0[0][j] : 0.f, cl = in1 ? (j > 0 ? W0[0][j - 1] : c0p) : 0.f;
+        const float cd = in3 ? W3[1][j] : 0.f, cu = in0 ? W3[0][j] : 0.f;
+        const float su = s5[1], sl = s5[2], sr = s5[3], sd = s5[4];
+        const float au = a5[1], al = a5[2], ar = a5[3], ad = a5[4];
+        z = cr * (sv - sr) + cl * (sv - sl) + cd * (sv - sd) + cu * (sv - su);
+        v = cr * (av - ar) + cl * (av - al) + cd * (av - ad) + cu * (av - au);
+        gwa[0][j] = (av - ar) * (sv - sr);
+        gwa[1][j] = (av - ad) * (sv - sd);
+      } else {
+        const bool in[4] = {in0, in1, in2, in3};
+        const float we[4] = {W0[0][j], W1[j], W2[j], W3[1][j]};
+        const float wn[4] = {in3 ? W0[1][j] : 0.f, in2 ? (j < V - 1 ? W1[j + 1] : w1n) : 0.f,
+                             in1 ? (j > 0 ? W2[j - 1] : w2p) : 0.f, in0 ? W3[0][j] : 0.f};
+        float o = 0.f, gs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gwa[e][j] = 0.f;
+          if (in[e]) {
+            const float sn = s5[e + 1], an = a5[e + 1];
+            const float ds = sv - sn, tt = we[e] * ds;
+            const float ph = 2.f * soft_t(tt, gm) - tt;
+            const float da = av - an;
+            const float gph = we[e] * da;
+            const float gtv = (tt < -gm || tt > gm) ? gph : -gph;
+            o += we[e] * ph;
+            gs += gtv * we[e];
+            gwa[e][j] = ph * da + gtv * ds;
+            if (on) dgam += gph * (tt < -gm ? 2.f : (tt > gm ? -2.f : 0.f));
+          }
+          if (in[3 - e]) {
+            const float sq = s5[(3 - e) + 1], aq = a5[(3 - e) + 1];
+            const float tt = wn[e] * (sq - sv);
+            const float ph = 2.f * soft_t(tt, gm) - tt;
+            const float gph = wn[e] * (aq - av);
+            const float gtv = (tt < -gm || tt > gm) ? gph : -gph;
+            o -= wn[e] * ph;
+            gs -= gtv * wn[e];
+          }
+        }
+        z = o;
+        v = gs;
+      }
+      const float zz = on ? z : 0.f, vv = on ? v : 0.f;
+      vrow[j] = v;
+      dot += av * zz;
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        accT[tt] += zz * gt5[tt];
+        accP[tt] += vv * xt[tt];
+      }
+    }
+    if (on) rstore<V>(vp + (int64_t)r * W, vrow);
+    // weight gradient: partials of the F channels -> LDS -> sum in channel order -> gw
+#pragma unroll
+    for (int e = 0; e < WPL; ++e) rstore<V>(&part[par][f][e][c0], gwa[e]);
+    __syncthreads();
+    for (int e = f; e < WPL; e += F) {
+      float sum[V];
+      rload<V>(sum, &part[par][0][e][c0]);
+      for (int ff = 1; ff < F; ++ff) {
+        float pv[V];
+        rload<V>(pv, &part[par][ff][e][c0]);
+#pragma unroll
+        for (int j = 0; j < V; ++j) sum[j] += pv[j];
+      }
+      if (on) {
+        float* dst = gwb + e * HW + (int64_t)r * W;
+        float cur[V];
+        rload<V>(cur, dst);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int col = c0 + j;
+          const bool keep = MODE != 1 || (e == 0 ? col + 1 < W : r + 1 < H);
+          if (keep) cur[j] += sc * sum[j];
+        }
+        rstore<V>(dst, cur);
+      }
+    }
+    par ^= 1;
+  }
+  // per-graph / per-channel reductions: wave sums, one atomic per value and wave
+  {
+    const float d = wave_sum(dot);
+    if (lane == 0 && gdot && d != 0.f) atomicAdd(gdot + gi, coef * d);
+  }
+  if constexpr (MODE == 2) {
+    const float d = wave_sum(dgam);
+    if (lane == 0 && ggam && d != 0.f) atomicAdd(ggam + gi, sc * d);
+  }
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt) {
+    const float d = wave_sum(accT[tt] + accP[tt]);
+    if (lane == 0 && d != 0.f) atomicAdd(gtaps + (gi * F + f) * 5 + tt, sc * d);
+  }
+}
+
+int term_row_vec(int W) {
+  if (W <= 64) return 1;
+  if (W <= 128 && W % 2 == 0) return 2;
+  if (W <= 256 && W % 4 == 0) return 4;
+  return 0;
+}
+template <int MODE, int V>
+void launch_term_row(int B, int F, const float* x, const float* g, const float* taps, const float* w, const float* lg,
+                     const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot, float* gtaps,
+                     int G, int H, int W, hipStream_t s) {
+  // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
+  int sseg = H;
+  const int64_t graphs = (int64_t)B * G;
+  while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
+  const int nsegs = (H + sseg - 1) / sseg;
+  const uint32_t nblk = (uint32_t)(graphs * nsegs);
+  hipLaunchKernelGGL((term_row_kernel<MODE, V>), dim3(nblk), dim3(64 * F), 0, s, x, g, taps, w, lg, scale, coef, v,
+                     gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
+}
+template <int MODE>
+bool launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
+                       const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot,
+                       float* gtaps, int G, int H, int W, hipStream_t s) {
+  const int V = term_row_vec(W);
+  if (F > TR_FMAX || V == 0) return false;
+  const void* ptrs[] = {x, g, w, v, gw};
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % (4u * V) != 0) return false;
+  switch (V) {
+    case 1: launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s); break;
+    case 2: launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s); break;
+    default: launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
+  }
+  return true;
+}
+
 template <int MODE>
 bool launch_term_fused(int F, dim3 grid, hipStream_t s, const float* x, const float* g, const float* taps,
                        const float* w, const float* lg, const float* scale, float coef, float* v, float* gw,
@@ -759,6 +1109,13 @@ using namespace grr;
 
 extern "C" {
 
+grr_status grr_bwd_set_term_rows(int enable) {
+  clear_error();
+  GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_rows: 0 or 1");
+  g_term_rows = enable;
+  return GRR_OK;
+}
+
 grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const float* taps, const float* w,
                               const float* log_gamma, const float* scale, float coef, float* v_out, float* gw,
                               float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
@@ -768,8 +1125,17 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
                   mode >= 0 && mode <= 2 && (mode != 2 || log_gamma),
               GRR_ERR_INVALID_ARG, "grr_bwd_term_fused: bad args");
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: B*G > 65535");
-  const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G), B * G);
   hipStream_t s = (hipStream_t)stream;
+  if (g_term_rows) {   // row-streaming kernel where the width allows (W <= 256)
+    bool rows = false;
+    switch (mode) {
+      case 0: rows = launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s); break;
+      case 1: rows = launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s); break;
+      default: rows = launch_term_row_v<2>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
+    }
+    if (rows) return launch_status("grr_bwd_term_fused");
+  }
+  const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G), B * G);
   bool ok = false;
   switch (mode) {
     case 0: ok = launch_term_fused<0>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W); break;

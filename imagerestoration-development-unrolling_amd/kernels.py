@@ -113,6 +113,11 @@ NO_STENCIL = Stencil(None, None, None, None)
 
 
 # ---------------------------------------------------------------------------
+def set_term_rows(enable: bool) -> None:
+    """Row-streaming (True, default) or per-pixel (False) term reverses (grr_bwd_term_fused)."""
+    _native.call("grr_bwd_set_term_rows", int(bool(enable)))
+
+
 def set_kernel_variant(variant: str) -> None:
     """Select the graph-operator kernels: "auto" (row waves for W <= 256, the channel waves
     of a graph in lockstep), "strips" (column strips at every width) or "independent" (row

@@ -268,6 +268,11 @@ grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const fl
 grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const float* log_gamma,
                         const float* scale, float coef, float* o_out, float* gs_out, float* gw,
                         float* ggamma, float* gdot, int B, int G, int F, int H, int W, void* stream);
+/* Kernel knob for tests and benchmarks (no reference counterpart): 1 (default) runs
+ * grr_bwd_term_fused as a row-streaming kernel where W <= 256, 0 always as the per-pixel kernel.
+ * Process-wide; results agree to fp32 rounding. */
+grr_status grr_bwd_set_term_rows(int enable);
+
 /* The three reverses above in one pass each, from x and g directly (s = S x and a = adjoint-S^T g
  * recomputed on the fly) with both tap gradients fused: mode 0 GLR (w raw), 1 pair Laplacian
  * (w = pair weights), 2 prox (w raw, log_gamma).  Writes v_out = (I-W)^T a, K a or d<a,o>/ds

@@ -1,0 +1,60 @@
+"""grr_bwd_term_fused's row-streaming kernel (W <= 256) against its per-pixel kernel, for the three
+operator terms (GLR, pair Laplacian, prox) and every instantiated F: the v output, the weight
+gradient (summed over the graph's channels through LDS), and the per-graph / per-channel
+reductions (<a, z>, gamma, taps).  The per-pixel kernel is itself pinned by the gradient tests
+(reference autograd golden + float64 oracle autograd, test_gpu_grad.py)."""
+import pytest
+import torch
+
+from tests.test_gpu_parity import DEV, rel_err
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(2, 4, 3, 20, 256), (1, 3, 1, 9, 32), (1, 2, 2, 17, 100), (1, 2, 4, 70, 200), (3, 2, 3, 2, 64),
+         (1, 1, 3, 300, 128)]
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import irdu_amd
+    irdu_amd.load_native()
+    from irdu_amd import kernels
+    yield kernels
+    kernels.set_term_rows(True)
+
+
+def _run(K, mode, x, g, taps, w, lg, scale, G, rows):
+    K.set_term_rows(rows)
+    gw = torch.full_like(w, 0.5)           # accumulated into (+=)
+    gdot = torch.zeros(G, device=DEV)
+    ggam = torch.zeros(G, device=DEV) if mode == 2 else None
+    gtaps = torch.zeros_like(taps)
+    v = K.bwd_term_fused(mode, x, g, taps, w, lg, scale, 0.7, gw, ggam, gdot, gtaps, G)
+    torch.cuda.synchronize()
+    return v.cpu(), gw.cpu(), gdot.cpu(), None if ggam is None else ggam.cpu(), gtaps.cpu()
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_term_rows_equal_per_pixel(K, case, mode):
+    b, G, F, h, w_ = case
+    torch.manual_seed(mode * 100 + h + w_)
+    C = G * F
+    x = torch.randn(b, C, h, w_, device=DEV)
+    g = torch.randn(b, C, h, w_, device=DEV)
+    taps = torch.randn(C, 5, device=DEV) * 0.5
+    planes = 2 if mode == 1 else 4
+    w = torch.rand(b, G, planes, h, w_, device=DEV)
+    lg = torch.log(torch.linspace(0.05, 0.5, G, device=DEV)) if mode == 2 else None
+    scale = torch.rand(G, device=DEV) + 0.5
+    ref = _run(K, mode, x, g, taps, w, lg, scale, G, rows=False)
+    got = _run(K, mode, x, g, taps, w, lg, scale, G, rows=True)
+    names = ["v", "gw", "gdot", "ggamma", "gtaps"]
+    for name, a, r in zip(names, got, ref):
+        if r is None:
+            continue
+        assert torch.isfinite(a).all(), name
+        tol = 2e-6 if name in ("v", "gw") else 2e-5
+        assert rel_err(a, r) <= tol, (name, rel_err(a, r))
