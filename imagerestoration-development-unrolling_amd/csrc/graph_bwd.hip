@@ -775,8 +775,14 @@ __device__ __forceinline__ float lnext(float v) {   // lane + 1 (0 at lane 63)
 }
 
 constexpr int TR_FMAX = 4;
+#ifndef GRR_TERM_ROW_WPE
+#define GRR_TERM_ROW_WPE 3
+#endif
+// 3 waves per SIMD (<= 168 VGPRs): 4 three-wave workgroups per CU instead of 2 at the 176-182
+// VGPRs the compiler picks unconstrained
 template <int MODE, int V>
-__global__ __launch_bounds__(NT) void term_row_kernel(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(V == 4 ? GRR_TERM_ROW_WPE : 1)))
+void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
     float* __restrict__ v_out, float* __restrict__ gw, float* __restrict__ ggam, float* __restrict__ gdot,
