@@ -774,21 +774,20 @@ __device__ __forceinline__ float lnext(float v) {   // lane + 1 (0 at lane 63)
   return r;
 }
 
-constexpr int TR_FMAX = 4;
-#ifndef GRR_TERM_ROW_WPE
-#define GRR_TERM_ROW_WPE 3
-#endif
-// 3 waves per SIMD (<= 168 VGPRs): 4 three-wave workgroups per CU instead of 2 at the 176-182
-// VGPRs the compiler picks unconstrained
+// Workgroup = F channel waves: up to 12 for V = 4 (a 768-thread bound caps the kernel at 168
+// VGPRs = 3 waves per SIMD, which also gives 4 three-wave workgroups per CU instead of 2 at the
+// 176-182 VGPRs the compiler picks unconstrained), up to 16 for V <= 2 (128 VGPRs).
+template <int V> struct TermRowMax { static constexpr int F = V == 4 ? 12 : 16; };
 template <int MODE, int V>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(V == 4 ? GRR_TERM_ROW_WPE : 1)))
-void term_row_kernel(
+__global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
     float* __restrict__ v_out, float* __restrict__ gw, float* __restrict__ ggam, float* __restrict__ gdot,
     float* __restrict__ gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
-  __shared__ __attribute__((aligned(16))) float part[2][TR_FMAX][WPL][64 * V];
+  // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats)
+  extern __shared__ __attribute__((aligned(16))) float part_dyn[];
+  auto part = [&](int pr, int ff, int e) { return part_dyn + ((pr * F + ff) * WPL + e) * (64 * V); };
   const int lane = threadIdx.x & 63;
   const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t unit = xcd_remap(blockIdx.x, nblk);
@@ -1002,14 +1001,14 @@ void term_row_kernel(
     if (on) rstore<V>(vp + (int64_t)r * W, vrow);
     // weight gradient: partials of the F channels -> LDS -> sum in channel order -> gw
 #pragma unroll
-    for (int e = 0; e < WPL; ++e) rstore<V>(&part[par][f][e][c0], gwa[e]);
+    for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + c0, gwa[e]);
     __syncthreads();
     for (int e = f; e < WPL; e += F) {
       float sum[V];
-      rload<V>(sum, &part[par][0][e][c0]);
+      rload<V>(sum, part(par, 0, e) + c0);
       for (int ff = 1; ff < F; ++ff) {
         float pv[V];
-        rload<V>(pv, &part[par][ff][e][c0]);
+        rload<V>(pv, part(par, ff, e) + c0);
 #pragma unroll
         for (int j = 0; j < V; ++j) sum[j] += pv[j];
       }
@@ -1060,7 +1059,8 @@ void launch_term_row(int B, int F, const float* x, const float* g, const float* 
   while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
-  hipLaunchKernelGGL((term_row_kernel<MODE, V>), dim3(nblk), dim3(64 * F), 0, s, x, g, taps, w, lg, scale, coef, v,
+  const size_t lds = (size_t)2 * F * (MODE == 1 ? 2 : 4) * 64 * V * sizeof(float);
+  hipLaunchKernelGGL((term_row_kernel<MODE, V>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale, coef, v,
                      gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
 }
 template <int MODE>
@@ -1068,7 +1068,7 @@ bool launch_term_row_v(int B, int F, const float* x, const float* g, const float
                        const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot,
                        float* gtaps, int G, int H, int W, hipStream_t s) {
   const int V = term_row_vec(W);
-  if (F > TR_FMAX || V == 0) return false;
+  if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return false;
   const void* ptrs[] = {x, g, w, v, gw};
   for (const void* p : ptrs)
     if ((uintptr_t)p % (4u * V) != 0) return false;
@@ -1130,9 +1130,8 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
   GRR_REQUIRE(x && g && taps && w && v_out && gw && gtaps && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 &&
                   mode >= 0 && mode <= 2 && (mode != 2 || log_gamma),
               GRR_ERR_INVALID_ARG, "grr_bwd_term_fused: bad args");
-  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: B*G > 65535");
   hipStream_t s = (hipStream_t)stream;
-  if (g_term_rows) {   // row-streaming kernel where the width allows (W <= 256)
+  if (g_term_rows && (int64_t)B * G * H < (1ll << 31)) {   // row-streaming kernel where the width allows (W <= 256)
     bool rows = false;
     switch (mode) {
       case 0: rows = launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s); break;
@@ -1141,6 +1140,7 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
     }
     if (rows) return launch_status("grr_bwd_term_fused");
   }
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: B*G > 65535");
   const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G), B * G);
   bool ok = false;
   switch (mode) {
@@ -1148,7 +1148,8 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
     case 1: ok = launch_term_fused<1>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W); break;
     default: ok = launch_term_fused<2>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W);
   }
-  GRR_REQUIRE(ok, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: F=%d has no fused instance", F);
+  GRR_REQUIRE(ok, GRR_ERR_UNSUPPORTED,
+              "grr_bwd_term_fused: F=%d needs the row kernel (W <= 256 with W %% V == 0, F <= 12 / 16) or F <= 4", F);
   return launch_status("grr_bwd_term_fused");
 }
 

@@ -113,9 +113,23 @@ NO_STENCIL = Stencil(None, None, None, None)
 
 
 # ---------------------------------------------------------------------------
+TERM_ROWS = True
+
+
 def set_term_rows(enable: bool) -> None:
     """Row-streaming (True, default) or per-pixel (False) term reverses (grr_bwd_term_fused)."""
+    global TERM_ROWS
     _native.call("grr_bwd_set_term_rows", int(bool(enable)))
+    TERM_ROWS = bool(enable)
+
+
+def term_rows_ok(w: int, f: int) -> bool:
+    """Widths / channel counts the row-streaming term reverse takes (16-byte aligned planes assumed)."""
+    if w <= 64:
+        return f <= 16
+    if w <= 128 and w % 2 == 0:
+        return f <= 16
+    return w <= 256 and w % 4 == 0 and f <= 12
 
 
 def set_kernel_variant(variant: str) -> None:

@@ -53,7 +53,9 @@ FUSED = True   # one-pass term reverses (grr_bwd_term_fused) where F has an inst
 
 
 def _use_fused(x: Tensor, n_graphs: int) -> bool:
-    return FUSED and (x.shape[1] // n_graphs) in K.FUSED_TERM_FTS
+    """One-pass term reverse: the row-streaming kernel (W <= 256, F <= 12) or the per-pixel one (F <= 4)."""
+    f = x.shape[1] // n_graphs
+    return FUSED and (f in K.FUSED_TERM_FTS or (K.TERM_ROWS and K.term_rows_ok(x.shape[3], f)))
 
 
 def glr_term_bwd(x: Tensor, g: Tensor, taps: Tensor, w: Tensor, scale: Tensor, coef: float, n_graphs: int,

@@ -58,3 +58,58 @@ def test_term_rows_equal_per_pixel(K, case, mode):
         assert torch.isfinite(a).all(), name
         tol = 2e-6 if name in ("v", "gw") else 2e-5
         assert rel_err(a, r) <= tol, (name, rel_err(a, r))
+
+
+WIDE_F = [(2, 2, 6, 18, 256), (1, 2, 12, 9, 256), (1, 2, 16, 7, 128), (2, 1, 12, 12, 64), (1, 1, 6, 5, 32)]
+
+
+@pytest.mark.parametrize("case", WIDE_F, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
+def test_term_rows_large_f_equal_five_pass(K, case):
+    """F > 4 (the v1.0 model's F = 6 and 12 levels): the row kernel against the five-pass reverse
+    (stencils, Z-reverse, tap gradients, adjoint stencil) on all three terms, through solver_grad."""
+    from irdu_amd import solver_grad as SG
+    b, G, F, h, w_ = case
+    torch.manual_seed(F * 10 + h)
+    C = G * F
+    # x at a scale where |C x| sits far from gamma (0.05..0.5) except on a set of measure ~0: the two
+    # paths round s = P x differently in the last place, which could flip an edge's soft-threshold
+    # branch if |C x| were within rounding of gamma (DESIGN.md §5)
+    x = 100.0 * torch.randn(b, C, h, w_, device=DEV)
+    g = torch.randn(b, C, h, w_, device=DEV)
+    taps = torch.randn(C, 5, device=DEV) * 0.5
+    wl = torch.rand(b, G, 4, h, w_, device=DEV)
+    cg = torch.rand(b, G, 2, h, w_, device=DEV)
+    scale = torch.rand(G, device=DEV) + 0.5
+    lg = torch.log(torch.linspace(0.05, 0.5, G, device=DEV))
+    res = {}
+    saved = SG.FUSED
+    try:
+        for fused in (False, True):
+            SG.FUSED = fused
+            outs = []
+            for term in ("glr", "gtv", "prox"):
+                out = torch.zeros_like(x)
+                gw = torch.zeros_like(cg if term == "gtv" else wl)
+                gs = torch.zeros(G, device=DEV)
+                gt = torch.zeros_like(taps)
+                if term == "glr":
+                    SG.glr_term_bwd(x, g, taps, wl, scale, 0.7, G, out, gw, gs, gt)
+                    outs.append((out, gw, gs, gt))
+                elif term == "gtv":
+                    SG.gtv_term_bwd(x, g, taps, cg, scale, 0.7, G, out, gw, gs, gt)
+                    outs.append((out, gw, gs, gt))
+                else:
+                    assert SG._use_fused(x, G) == fused
+                    st = tuple(taps[:, 0].contiguous() for _ in range(4))
+                    lvl = SG._Level(wl, cg, wl, st, st, lg, torch.log(scale), lg, G)
+                    lvl.tapsG = taps
+                    lvl.prox_bwd(x, g, out)
+                    outs.append((out, lvl.gwG, lvl.gro, lvl.ggam, lvl.gtapG))
+            res[fused] = outs
+    finally:
+        SG.FUSED = saved
+    torch.cuda.synchronize()
+    for t, (a_set, r_set) in enumerate(zip(res[True], res[False])):
+        for i, (a, r) in enumerate(zip(a_set, r_set)):
+            assert torch.isfinite(a).all()
+            assert rel_err(a.cpu(), r.cpu()) <= 2e-5, (t, i, rel_err(a.cpu(), r.cpu()))
