@@ -1049,6 +1049,178 @@ int term_row_vec(int W) {
   if (W <= 256 && W % 4 == 0) return 4;
   return 0;
 }
+// The same reverse as a row-streaming kernel (W <= 64 V, F in {1, 2, 3, 4, 6}): one wave = one
+// (b, graph) and a segment of rows, lane = V adjacent columns.  Feature rows r-1..r+1 of the F
+// channels, their inverse norms and gsim (4 planes) stay in registers; horizontal neighbours
+// come from DPP lane shifts.  feat, w, gw read once, gfeat written once (the per-pixel kernel
+// re-reads each feature plane ~12 times through L1/L2, 1.1 TB/s).
+template <int F, int V>
+__global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restrict__ feat, int64_t fstride,
+                                                          const float* __restrict__ multiM,
+                                                          const float* __restrict__ w, const float* __restrict__ gw,
+                                                          float* __restrict__ gfeat, int64_t gstride,
+                                                          float* __restrict__ gM, int G, int H, int W, int sseg,
+                                                          int nsegs, uint32_t nwaves) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wid = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (wid >= nwaves) return;   // whole waves; no barriers below
+  const int seg = (int)(wid % nsegs);
+  const int bg = (int)(wid / nsegs), g = bg % G, b = bg / G;
+  const int r0 = seg * sseg, r1 = min(r0 + sseg, H);
+  const int c0 = V * lane;
+  const bool on = c0 < W;
+  const int cl0 = on ? c0 : W - V;
+  const int64_t HW = (int64_t)H * W;
+  const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW + cl0;
+  float* gfp = gfeat + (int64_t)b * gstride + (int64_t)g * F * HW + cl0;
+  const float* wb = w + (int64_t)bg * 4 * HW + cl0;
+  const float* gwb = gw + (int64_t)bg * 4 * HW + cl0;
+  float M[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) M[f] = multiM[g * F + f];
+  float gm[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) gm[f] = 0.f;
+
+  // windows: rows t-2, t-1, t (slot 0, 1, 2)
+  float FE[3][F][V], IC[3][V], GS[3][4][V];
+  auto load_row = [&](int slot, int rr) {
+    const int64_t ro = (int64_t)clampi(rr, 0, H - 1) * W;
+    float ss[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) ss[j] = 0.f;
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      rload<V>(FE[slot][f], fp + f * HW + ro);
+#pragma unroll
+      for (int j = 0; j < V; ++j) ss[j] += FE[slot][f][j] * FE[slot][f][j];
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) IC[slot][j] = 1.f / fmaxf(sqrtf(ss[j]), 1e-12f);
+    float wv[4][V], gv[4][V];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      rload<V>(wv[e], wb + e * HW + ro);
+      rload<V>(gv[e], gwb + e * HW + ro);
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float s = wv[0][j] * gv[0][j] + wv[1][j] * gv[1][j] + wv[2][j] * gv[2][j] + wv[3][j] * gv[3][j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) GS[slot][e][j] = wv[e][j] * (gv[e][j] - s);
+    }
+  };
+  auto shift = [&]() {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        IC[k][j] = IC[k + 1][j];
+#pragma unroll
+        for (int f = 0; f < F; ++f) FE[k][f][j] = FE[k + 1][f][j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) GS[k][e][j] = GS[k + 1][e][j];
+      }
+    }
+  };
+  load_row(1, r0 - 1);
+  load_row(2, r0);
+  for (int r = r0; r < r1; ++r) {
+    shift();
+    load_row(2, r + 1);
+    // output row r: rows r-1, r, r+1 in slots 0, 1, 2
+    const bool in0 = r > 0, in3 = r + 1 < H;
+    float gout[F][V];
+    const float icp = lprev(IC[1][V - 1]), icn = lnext(IC[1][0]);
+    const float g1n = lnext(GS[1][1][0]), g2p = lprev(GS[1][2][V - 1]);
+    float fpv[F], fnx[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) { fpv[f] = lprev(FE[1][f][V - 1]); fnx[f] = lnext(FE[1][f][0]); }
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int col = c0 + j;
+      const bool in1 = col > 0, in2 = col + 1 < W;
+      const bool in[4] = {in0, in1, in2, in3};
+      const float ic = IC[1][j];
+      const float icl = j > 0 ? IC[1][j - 1] : icp, icr = j < V - 1 ? IC[1][j + 1] : icn;
+      const float inb[4] = {in0 ? IC[0][j] : ic, in1 ? icl : ic, in2 ? icr : ic, in3 ? IC[2][j] : ic};
+      float gs_out[4], gs_in[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gs_out[e] = GS[1][e][j];
+      gs_in[0] = in3 ? GS[2][0][j] : 0.f;                                  // edge up of the pixel below
+      gs_in[1] = in2 ? (j < V - 1 ? GS[1][1][j + 1] : g1n) : 0.f;          // edge left of the right pixel
+      gs_in[2] = in1 ? (j > 0 ? GS[1][2][j - 1] : g2p) : 0.f;              // edge right of the left pixel
+      gs_in[3] = in0 ? GS[0][3][j] : 0.f;                                  // edge down of the pixel above
+      float gsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gsum += in[e] ? 0.f : gs_out[e];
+      float gfh[F], ndg = 0.f;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const float m = M[f];
+        const float xc = FE[1][f][j];
+        const float n = xc * ic;
+        // feature f at the 4 (clamped) neighbours: up, left, right, down
+        const float xl = j > 0 ? FE[1][f][j - 1] : fpv[f], xr = j < V - 1 ? FE[1][f][j + 1] : fnx[f];
+        const float xn[4] = {in0 ? FE[0][f][j] : xc, in1 ? xl : xc, in2 ? xr : xc, in3 ? FE[2][f][j] : xc};
+        float v = gsum * n * m;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v += gs_out[e] * xn[e] * inb[e] * m;
+          if (in[3 - e]) v += gs_in[e] * xn[3 - e] * inb[3 - e] * m;
+        }
+        gfh[f] = v;
+        if (on) gm[f] += v * n;
+        ndg += n * (v * m);
+      }
+      const bool small = 1.f / ic <= 1e-12f;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const float n = FE[1][f][j] * ic;
+        const float gn = gfh[f] * M[f];
+        gout[f][j] = small ? gn * ic : (gn - n * ndg) * ic;
+      }
+    }
+    if (on) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) rstore<V>(gfp + f * HW + (int64_t)r * W, gout[f]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const float s = wave_sum(gm[f]);
+    if (lane == 0 && s != 0.f) atomicAdd(gM + g * F + f, s);
+  }
+}
+
+bool launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM, const float* w, const float* gw,
+                         float* gfeat, int64_t gstride, float* gM, int B, int G, int F, int H, int W, hipStream_t s) {
+  const int V = term_row_vec(W);
+  if (V == 0) return false;
+  if (fstride % V != 0 || gstride % V != 0 || ((int64_t)H * W) % V != 0) return false;
+  const void* ptrs[] = {feat, w, gw, gfeat};
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % (4u * V) != 0) return false;
+  const int64_t planes = (int64_t)B * G;
+  int sseg = H;
+  while (sseg > 32 && planes * ((H + sseg - 1) / sseg) < 4096) sseg = (sseg + 1) / 2;
+  const int nsegs = (H + sseg - 1) / sseg;
+  const uint32_t nwaves = (uint32_t)(planes * nsegs);
+  const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+#define GRR_EDGE_BWD_CASE(FF, VV)                                                                              \
+  if (F == FF && V == VV) {                                                                                    \
+    hipLaunchKernelGGL((edge_row_bwd_kernel<FF, VV>), grid, dim3(NT), 0, s, feat, fstride, multiM, w, gw, gfeat, \
+                       gstride, gM, G, H, W, sseg, nsegs, nwaves);                                             \
+    return true;                                                                                               \
+  }
+  GRR_EDGE_BWD_CASE(1, 4) GRR_EDGE_BWD_CASE(2, 4) GRR_EDGE_BWD_CASE(3, 4) GRR_EDGE_BWD_CASE(4, 4)
+  GRR_EDGE_BWD_CASE(6, 4) GRR_EDGE_BWD_CASE(1, 2) GRR_EDGE_BWD_CASE(2, 2) GRR_EDGE_BWD_CASE(3, 2)
+  GRR_EDGE_BWD_CASE(4, 2) GRR_EDGE_BWD_CASE(6, 2) GRR_EDGE_BWD_CASE(1, 1) GRR_EDGE_BWD_CASE(2, 1)
+  GRR_EDGE_BWD_CASE(3, 1) GRR_EDGE_BWD_CASE(4, 1) GRR_EDGE_BWD_CASE(6, 1)
+#undef GRR_EDGE_BWD_CASE
+  return false;
+}
+
 template <int MODE, int V>
 void launch_term_row(int B, int F, const float* x, const float* g, const float* taps, const float* w, const float* lg,
                      const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot, float* gtaps,
@@ -1246,8 +1418,11 @@ grr_status grr_bwd_edge_weights(const float* feat, int64_t feat_bstride, const f
   clear_error();
   GRR_REQUIRE(feat && multiM && w && gw && gfeat && gmultiM && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_edge_weights: bad args");
-  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: B*G*F > 65535");
   GRR_REQUIRE(F <= GRR_MAX_NODE_FTS, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: F=%d > %d", F, GRR_MAX_NODE_FTS);
+  if (g_term_rows && launch_edge_row_bwd(feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, B, G, F,
+                                         H, W, (hipStream_t)stream))
+    return launch_status("grr_bwd_edge_weights");
+  GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: B*G*F > 65535");
   hipLaunchKernelGGL(edge_weights_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0,
                      (hipStream_t)stream, feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, G, F, H,
                      W);

@@ -269,7 +269,8 @@ grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const fl
                         const float* scale, float coef, float* o_out, float* gs_out, float* gw,
                         float* ggamma, float* gdot, int B, int G, int F, int H, int W, void* stream);
 /* Kernel knob for tests and benchmarks (no reference counterpart): 1 (default) runs
- * grr_bwd_term_fused as a row-streaming kernel where W <= 256, 0 always as the per-pixel kernel.
+ * grr_bwd_term_fused and grr_bwd_edge_weights as row-streaming kernels where W <= 256, 0 always as
+ * the per-pixel kernels.
  * Process-wide; results agree to fp32 rounding. */
 grr_status grr_bwd_set_term_rows(int enable);
 

@@ -113,3 +113,35 @@ def test_term_rows_large_f_equal_five_pass(K, case):
         for i, (a, r) in enumerate(zip(a_set, r_set)):
             assert torch.isfinite(a).all()
             assert rel_err(a.cpu(), r.cpu()) <= 2e-5, (t, i, rel_err(a.cpu(), r.cpu()))
+
+
+EDGE_CASES = [(2, 4, 3, 20, 256), (1, 3, 1, 9, 32), (1, 2, 2, 17, 100), (1, 2, 6, 33, 200), (3, 2, 4, 2, 64),
+              (1, 1, 3, 140, 128), (1, 2, 12, 9, 64)]
+
+
+@pytest.mark.parametrize("case", EDGE_CASES, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
+def test_edge_weights_reverse_rows_equal_per_pixel(K, case):
+    """grr_bwd_edge_weights' row kernel (F in {1, 2, 3, 4, 6}, W <= 256; F = 12 falls back) against the
+    per-pixel kernel, on a GTV/GLR slab at a channel offset of a wider feature tensor."""
+    b, G, F, h, w_ = case
+    torch.manual_seed(F * 7 + h)
+    C = G * F
+    feat = torch.randn(b, 2 * C, h, w_, device=DEV)
+    feat[:, C:C + 1, :2, :3] = 0.0                      # some zero-norm pixels (the 1e-12 floor)
+    multiM = torch.rand(G, F, device=DEV) + 0.5
+    wts = K.edge_weights(feat, C, G, F, multiM)
+    w = wts[0] if isinstance(wts, tuple) else wts
+    gw = torch.randn_like(w)
+    outs = []
+    for rows in (False, True):
+        K.set_term_rows(rows)
+        gfeat = torch.zeros_like(feat)
+        gM = torch.zeros_like(multiM)
+        K.bwd_edge_weights(feat, C, G, F, multiM, w, gw, gfeat, gM)
+        torch.cuda.synchronize()
+        outs.append((gfeat.cpu(), gM.cpu()))
+    K.set_term_rows(True)
+    (rf, rm), (af, am) = outs
+    assert torch.isfinite(af).all()
+    assert rel_err(af, rf) <= 2e-6
+    assert rel_err(am, rm) <= 2e-5
