@@ -96,6 +96,13 @@ SIGNATURES = {
     "grr_win_edge_weights": [P, L, P, P, I, P, P, I, I, I, I, I, P],
     "grr_win_solver": [I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, I, I, I, I, I, P],
     "grr_win_mix": [P, P, P, P, I, I, I, I, I, P],
+    "grr_win_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
+    "grr_win_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],
+    "grr_win_bwd_glr": [P, P, P, P, I, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_win_bwd_gtv": [P, P, P, P, I, I, P, P, Fl, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_win_bwd_gather": [P, P, P, I, P, P, I, I, I, I, I, P],
+    "grr_win_bwd_edge_weights": [P, L, P, P, P, P, I, P, L, P, I, I, I, I, I, P],
+    "grr_win_bwd_mix": [P, P, P, P, P, I, I, I, I, I, P],
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64}

@@ -860,3 +860,125 @@ def win_apply(x: Tensor, edge_delta, n_graphs: int, n_sig: int, *, wL: Optional[
             _ptr(tapsG), _ptr(mu), _ptr(ro), None, None, None, delta, k, out.data_ptr(), None, b, n_graphs, n_sig, h, w,
             _stream(dev))
     return out
+
+
+# ---- window-graph reverse (window_bwd.hip; training through MixtureGTV of REF7 / REF1) ----
+WST_P, WST_T_ADJ, WST_P_ADJ = 0, 1, 2      # S x (reflect) / S^T* g (zero-frame correlation) / S* g
+WTAP_P, WTAP_T = 0, 1
+
+
+def _win5(x: Tensor, n_graphs: int):
+    """(B, G, Fs, H, W) of a [B,G,Fs,H,W] window signal."""
+    if x.dim() != 5 or x.shape[1] != n_graphs:
+        raise ValueError(f"window reverse: expected [B,{n_graphs},Fs,H,W], got {tuple(x.shape)}")
+    b, g, fs, h, w = x.shape
+    if h < 2 or w < 2:
+        raise ValueError("window reverse: the reflect frame needs H, W >= 2")
+    return b, g, fs, h, w
+
+
+def win_bwd_stencil(x: Tensor, taps: Tensor, mode: int, n_graphs: int, scale: Optional[Tensor] = None,
+                    out: Optional[Tensor] = None) -> Tensor:
+    """out = [out +] scale[g] * mode(x)  (out given -> accumulate)."""
+    dev = _check("win_bwd_stencil", x, taps, scale, out)
+    dims = _win5(x, n_graphs)
+    acc = out is not None
+    if out is None:
+        out = torch.empty_like(x)
+    elif out.shape != x.shape:
+        raise ValueError("win_bwd_stencil: out shape")
+    _check_win_scalars(n_graphs, taps=taps, scale=scale)
+    _launch("win_bwd_stencil", 4 * x.numel() * (2 + int(acc)), "grr_win_bwd_stencil", x.data_ptr(), taps.data_ptr(),
+            mode, _ptr(scale), int(acc), out.data_ptr(), *dims, _stream(dev))
+    return out
+
+
+def win_bwd_tapgrad(u: Tensor, z: Tensor, mode: int, n_graphs: int, scale: Optional[Tensor], gtaps: Tensor) -> None:
+    dev = _check("win_bwd_tapgrad", u, z, scale, gtaps)
+    dims = _win5(u, n_graphs)
+    if z.shape != u.shape or gtaps.numel() < 5:
+        raise ValueError("win_bwd_tapgrad: shapes")
+    _launch("win_bwd_tapgrad", 8 * u.numel(), "grr_win_bwd_tapgrad", u.data_ptr(), z.data_ptr(), mode, _ptr(scale),
+            gtaps.data_ptr(), *dims, _stream(dev))
+
+
+def _edge_shape_ok(w: Tensor, dims, k: int) -> None:
+    b, g, _, h, ww = dims
+    if tuple(w.shape) != (b, g, k, h, ww):
+        raise ValueError(f"window reverse: edge weights of shape {tuple(w.shape)}, expected {(b, g, k, h, ww)}")
+
+
+def win_bwd_glr(s: Tensor, bt: Tensor, w: Tensor, edge_delta, sc: Tensor, coef: float, gw: Tensor,
+                gdot: Optional[Tensor], n_graphs: int) -> Tuple[Tensor, Tensor]:
+    """GLR term reverse, both passes: returns (l = (I - W) s, gs = (I - W)^T (sc * bt))."""
+    dev = _check("win_bwd_glr", s, bt, w, sc, gw, gdot)
+    dims = _win5(s, n_graphs)
+    delta, k = _delta_arg(edge_delta)
+    _edge_shape_ok(w, dims, k)
+    if bt.shape != s.shape or gw.shape != w.shape:
+        raise ValueError("win_bwd_glr: shapes")
+    _check_win_scalars(n_graphs, sc=sc, gdot=gdot)
+    b, g, fs, h, ww = dims
+    l_out, gs = torch.empty_like(s), torch.empty_like(s)
+    E = torch.empty((b, g, fs, k, h, ww), dtype=torch.float32, device=dev)
+    _launch("win_bwd_glr", 4 * (3 * s.numel() + 3 * w.numel() + (k + 2) * s.numel()), "grr_win_bwd_glr",
+            s.data_ptr(), bt.data_ptr(), w.data_ptr(), delta, k, sc.data_ptr(), float(coef), l_out.data_ptr(),
+            E.data_ptr(), gs.data_ptr(), gw.data_ptr(), _ptr(gdot), *dims, _stream(dev))
+    _launch("win_bwd_gather", 4 * (k + 2) * s.numel(), "grr_win_bwd_gather", E.data_ptr(), None, delta, k,
+            gs.data_ptr(), None, *dims, _stream(dev))
+    return l_out, gs
+
+
+def win_bwd_gtv(s: Tensor, bt: Tensor, w: Tensor, edge_delta, prox: bool, log_gamma: Optional[Tensor], sc: Tensor,
+                coef: float, gw: Tensor, gdot: Optional[Tensor], ggamma: Optional[Tensor],
+                n_graphs: int) -> Tuple[Tensor, Tensor]:
+    """GTV term (C^T C or C^T phi(C .)) reverse, both passes: returns (o, gs)."""
+    dev = _check("win_bwd_gtv", s, bt, w, log_gamma, sc, gw, gdot, ggamma)
+    dims = _win5(s, n_graphs)
+    delta, k = _delta_arg(edge_delta)
+    _edge_shape_ok(w, dims, k)
+    if bt.shape != s.shape or gw.shape != w.shape or (prox and log_gamma is None):
+        raise ValueError("win_bwd_gtv: shapes / log_gamma")
+    _check_win_scalars(n_graphs, sc=sc, gdot=gdot, log_gamma=log_gamma, ggamma=ggamma)
+    b, g, fs, h, ww = dims
+    o, gs = torch.empty_like(s), torch.empty_like(s)
+    E = torch.empty((b, g, fs, k, h, ww), dtype=torch.float32, device=dev)
+    PW = torch.empty_like(E)
+    _launch("win_bwd_gtv", 4 * (3 * s.numel() + 3 * w.numel() + (2 * k + 1) * s.numel()), "grr_win_bwd_gtv",
+            s.data_ptr(), bt.data_ptr(), w.data_ptr(), delta, k, int(prox), _ptr(log_gamma), sc.data_ptr(),
+            float(coef), PW.data_ptr(), E.data_ptr(), gs.data_ptr(), gw.data_ptr(), _ptr(gdot), _ptr(ggamma), *dims,
+            _stream(dev))
+    _launch("win_bwd_gather", 4 * (2 * k + 3) * s.numel(), "grr_win_bwd_gather", E.data_ptr(), PW.data_ptr(), delta,
+            k, gs.data_ptr(), o.data_ptr(), *dims, _stream(dev))
+    return o, gs
+
+
+def win_bwd_edge_weights(feat: Tensor, channel_offset: int, n_graphs: int, n_fts: int, multiM: Tensor, w: Tensor,
+                         gw: Tensor, edge_delta, gfeat: Tensor, gmultiM: Tensor) -> None:
+    """Accumulates into the [G*F] slab at channel_offset of gfeat (same shape as feat) and gmultiM;
+    gw is consumed (overwritten by the softmax reverse)."""
+    dev = _check("win_bwd_edge_weights", feat, multiM, w, gw, gfeat, gmultiM)
+    b, ctot, h, ww = feat.shape
+    delta, k = _delta_arg(edge_delta)
+    if gfeat.shape != feat.shape or channel_offset + n_graphs * n_fts > ctot:
+        raise ValueError("win_bwd_edge_weights: bad slab")
+    if tuple(w.shape) != (b, n_graphs, k, h, ww) or gw.shape != w.shape or multiM.numel() != n_graphs * n_fts \
+            or gmultiM.numel() != n_graphs * n_fts:
+        raise ValueError("win_bwd_edge_weights: shapes")
+    off = channel_offset * h * ww * 4
+    _launch("win_bwd_edge_weights", 4 * b * h * ww * n_graphs * (3 * n_fts + 3 * k), "grr_win_bwd_edge_weights",
+            feat.data_ptr() + off, ctot * h * ww, multiM.data_ptr(), w.data_ptr(), gw.data_ptr(), delta, k,
+            gfeat.data_ptr() + off, ctot * h * ww, gmultiM.data_ptr(), b, n_graphs, n_fts, h, ww, _stream(dev))
+
+
+def win_bwd_mix(gout: Tensor, x: Tensor, score: Tensor) -> Tuple[Tensor, Tensor]:
+    """Reverse of win_mix: (gx [B,G,Fs,H,W], gscore [B,G,H,W]); gdc = gout."""
+    dev = _check("win_bwd_mix", gout, x, score)
+    b, g, c, h, w = x.shape
+    if tuple(score.shape) != (b, g, h, w) or tuple(gout.shape) != (b, c, h, w):
+        raise ValueError("win_bwd_mix: shapes")
+    gx, gscore = torch.empty_like(x), torch.empty_like(score)
+    _launch("win_bwd_mix", 4 * (2 * x.numel() + 2 * score.numel() + gout.numel()), "grr_win_bwd_mix",
+            gout.data_ptr(), x.data_ptr(), score.data_ptr(), gx.data_ptr(), gscore.data_ptr(), b, g, c, h, w,
+            _stream(dev))
+    return gx, gscore

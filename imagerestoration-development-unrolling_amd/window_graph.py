@@ -19,7 +19,10 @@ run on stock PyTorch-ROCm convolutions.
 
 Class names, constructor signatures and ``state_dict`` keys match REF7, so its
 checkpoints load unchanged (the ``device`` argument is accepted and used for placement).
-Inference only: under autograd the solver attaches a node whose backward raises.
+Training: when autograd records, ``MixtureGTV`` runs the solver through
+``window_grad._WindowSolve`` (HIP forward keeping the iterates + HIP reverse sweep of
+window_bwd.hip) and the mixture through ``window_grad.WinMixFn``.  The GLRFast / GTVFast
+module calls stay inference-only (under autograd they attach a node whose backward raises).
 """
 from __future__ import annotations
 
@@ -32,7 +35,8 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
-from .graph_filter import hip_forward
+from . import window_grad as WG
+from .graph_filter import hip_forward, records_grad
 
 CONNECTION_FLAGS_5x5_small = np.array([
     0, 0, 1, 0, 0,
@@ -259,8 +263,20 @@ class MixtureGTV(nn.Module):
         self.muys00 = Parameter((torch.ones(n_graphs) * muy_init[0]).to(device))
         self.GLRmodule00 = GLRFast(nchannels_in, n_node_fts, n_graphs, connection_window, device, M_diag_init=1.0)
 
-    @hip_forward
     def forward(self, patchs):
+        if records_grad(self, patchs):
+            # training: the solver and mixture run window_grad's HIP forward + HIP reverse;
+            # the feature CNN / DC estimator / combination conv stay on PyTorch autograd
+            feats = self.patchs_features_extraction(patchs)[0]
+            graph_feats = feats[:, :-12]
+            dc_term = self.dc_estimator(feats[:, -12:])
+            x = WG.window_solve(self, patchs - dc_term, feats, with_taps=True)
+            score = self.combination_weight(graph_feats)
+            return WG.WinMixFn.apply(x, score.contiguous(), dc_term.contiguous())
+        return self._forward_hip(patchs)
+
+    @hip_forward
+    def _forward_hip(self, patchs):
         feats = self.patchs_features_extraction(patchs)[0].contiguous()
         graph_feats = feats[:, :-12].contiguous()
         dc_term = self.dc_estimator(feats[:, -12:]).contiguous()

@@ -8,7 +8,8 @@ Differences from REF7 (window_graph.py): the graph modules have no stats stencil
 5x5 window (K = 24) — each behind a skip mix and a ``SharpeningBlock`` (REF1:768-884), with
 6 CG stages (2 before the prox update, 4 after).
 
-Class names, constructor signatures and ``state_dict`` keys match REF1.  Inference only.
+Class names, constructor signatures and ``state_dict`` keys match REF1.  Training runs the
+solver through ``window_grad`` (HIP forward + HIP reverse, identity stencil: no tap gradients).
 """
 from __future__ import annotations
 
@@ -18,7 +19,8 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
-from .graph_filter import hip_forward
+from . import window_grad as WG
+from .graph_filter import hip_forward, records_grad
 from .window_graph import (CONNECTION_FLAGS_3x3, CONNECTION_FLAGS_5x5, Downsample, FFBlock, MixtureGTV as _MixV7,
                            OverlapPatchEmbed, Upsample, window_edges)
 
@@ -148,8 +150,15 @@ class MixtureGTV(nn.Module):
         self.muys00 = Parameter((torch.ones(n_graphs) * muy_init[0]).to(device))
         self.GLRmodule00 = GLRFast(nchannels_in, n_node_fts, n_graphs, connection_window, device, M_diag_init=1.0)
 
-    @hip_forward
     def forward(self, patchs):
+        if records_grad(self, patchs):          # training: window_grad's HIP forward + reverse
+            feats = self.patchs_features_extraction(patchs)[0]
+            x = WG.window_solve(self, patchs, feats, with_taps=False)
+            return WG.WinMixFn.apply(x, self.combination_weight(feats).contiguous(), None)
+        return self._forward_hip(patchs)
+
+    @hip_forward
+    def _forward_hip(self, patchs):
         y = patchs.contiguous()
         feats = self.patchs_features_extraction(y)[0].contiguous()
         x = self.solve(y, feats)

@@ -358,6 +358,43 @@ grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, c
 grr_status grr_win_mix(const float* x, const float* score, const float* dc, float* out, int B, int G, int Fs, int H,
                        int W, void* stream);
 
+/* ---- window-graph reverse (training): replaces torch autograd through MixtureGTV's solver,
+ * edge weights and mixture (REF7:418-446, :449-488, :892-1011 under loss.backward() of the
+ * multiblocks training script).  Planes [B,G,Fs,H,W]; per-graph scale vectors [G] may be
+ * NULL (= 1); every reduction output (gw, gdot, ggamma, gtaps, gmultiM) ACCUMULATES.
+ * H, W >= 2 (the reflect frame). */
+
+/* Stencil of the reverse: mode 0 S x (reflect frame), 1 S^T* g (zero-frame correlation),
+ * 2 S* g (adjoint of the reflect-frame stencil).  out = [out +] scale[g] y. */
+grr_status grr_win_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,
+                               float* out, int B, int G, int Fs, int H, int W, void* stream);
+/* gtaps[t] += sum scale[g] u(p) z(src_t(p)); mode 0 src = reflect(p + d_t) (S), 1 src = p - d_t (S^T). */
+grr_status grr_win_bwd_tapgrad(const float* u, const float* z, int mode, const float* scale, float* gtaps, int B,
+                               int G, int Fs, int H, int W, void* stream);
+/* GLR term reverse, pass 1 (s = S x, b = S^T* g): l_out = (I - W) s, gsd = scale b,
+ * E [B,G,Fs,K,H,W] = scale b w_e (gathered by grr_win_bwd_gather), gw += -scale b s(n_e),
+ * gdot[g] += coef <b, l>. */
+grr_status grr_win_bwd_glr(const float* s, const float* b, const float* w, const int32_t* delta, int K,
+                           const float* scale, float coef, float* l_out, float* E, float* gsd, float* gw, float* gdot,
+                           int B, int G, int Fs, int H, int W, void* stream);
+/* GTV term reverse, pass 1 (C^T C, or with prox C^T phi(C .)): gsd, E as above, PW [B,G,Fs,K,H,W]
+ * = w_e phi(z_e) (the gather rebuilds o = C^T phi from it), gw, gdot[g] += coef <b, o>,
+ * ggamma[g] += dL/dgamma (prox). */
+grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const int32_t* delta, int K, int prox,
+                           const float* log_gamma, const float* scale, float coef, float* PW, float* E, float* gsd,
+                           float* gw, float* gdot, float* ggamma, int B, int G, int Fs, int H, int W, void* stream);
+/* Pass 2: gs -= sum_e sum_{p: clamp(p + delta_e) = q} E_e(p) (in place); with PW also o_out. */
+grr_status grr_win_bwd_gather(const float* E, const float* PW, const int32_t* delta, int K, float* gs, float* o_out,
+                              int B, int G, int Fs, int H, int W, void* stream);
+/* Edge-weight reverse of grr_win_edge_weights: gw is overwritten (softmax reverse in place);
+ * the [G*F] slab of gfeat and gmultiM [G,F] accumulate (the GTV and GLR graphs share features). */
+grr_status grr_win_bwd_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM, const float* w,
+                                    float* gw, const int32_t* delta, int K, float* gfeat, int64_t gfeat_bstride,
+                                    float* gmultiM, int B, int G, int F, int H, int W, void* stream);
+/* Mixture reverse: gx[b,g,c] = gout[b,c] score[b,g], gscore[b,g] = sum_c gout[b,c] x[b,g,c]. */
+grr_status grr_win_bwd_mix(const float* gout, const float* x, const float* score, float* gx, float* gscore, int B,
+                           int G, int Fs, int H, int W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

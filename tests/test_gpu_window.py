@@ -150,10 +150,15 @@ def test_window_sequence_denoiser_small(wg):
     assert rel_err(out, ref) <= RTOL
 
 
-def test_window_grad_mode_raises(wg):
-    g = load_golden("window_v7.npz")
-    m = _load_mixture(wg, g)
-    out = m(torch.from_numpy(g["in/noisy"]).to(DEV))
+def test_window_module_grad_mode_raises(wg):
+    """The GLRFast / GTVFast module calls have no reverse: under autograd they must raise, not
+    drop gradients (MixtureGTV itself trains: tests/test_gpu_window_grad.py)."""
+    d = load_golden("window_ops_v7.npz")
+    x = torch.from_numpy(d["diamond5/x"]).to(DEV).requires_grad_(True)
+    wgt = torch.from_numpy(d["diamond5/wG"]).to(DEV)
+    b, g, f, h, w = torch.from_numpy(d["diamond5/feat"]).shape
+    gtv = wg.GTVFast(3, f, g, _window("diamond5")).to(DEV)
+    out = gtv(x, wgt)
     with pytest.raises(NotImplementedError):
         out.sum().backward()
 
