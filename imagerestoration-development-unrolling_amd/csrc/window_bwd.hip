@@ -144,17 +144,17 @@ __global__ __launch_bounds__(NTB) void win_glr_bwd_kernel(const float* __restric
                                                           const float* __restrict__ scale, float coef,
                                                           float* __restrict__ l_out, float* __restrict__ E,
                                                           float* __restrict__ gsd, float* __restrict__ gw,
-                                                          float* __restrict__ gdot, int G, int Fs, int H, int W,
-                                                          int64_t npix) {
+                                                          float* __restrict__ gdot, int G, int Fs, int H, int W) {
+  // grid (x, B*G): every lane of a block works on the same graph, so the per-graph
+  // reduction is one wave sum after the loop, with every lane active
   const int64_t HW = (int64_t)H * W;
-  for (int64_t i = blockIdx.x * (int64_t)NTB + threadIdx.x; i < npix; i += (int64_t)gridDim.x * NTB) {
-    const int64_t bg = i / HW;
-    const int q = (int)(i - bg * HW);
-    const int g = (int)(bg % G);
+  const int64_t bg = blockIdx.y;
+  const int g = (int)(bg % G);
+  const float sc = scale ? scale[g] : 1.f;
+  float dot = 0.f;
+  for (int q = blockIdx.x * NTB + threadIdx.x; q < HW; q += gridDim.x * NTB) {
     const int r = q / W, c = q - r * W;
-    const float sc = scale ? scale[g] : 1.f;
     const float* wq = w + bg * K * HW + q;
-    float dot = 0.f;
     float gwa[kWinMaxEdges];
     for (int e = 0; e < K; ++e) gwa[e] = 0.f;
     for (int ch = 0; ch < Fs; ++ch) {
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(NTB) void win_glr_bwd_kernel(const float* __restric
       dot += bv * lv;
     }
     for (int e = 0; e < K; ++e) gw[bg * K * HW + e * HW + q] += gwa[e];
-    if (gdot) wave_atomic(gdot + g, coef * dot);
   }
+  if (gdot) wave_atomic(gdot + g, coef * dot);
 }
 
 // ---- GTV pass 1 (linear C^T C or the prox C^T phi(C .)).  sc = scale[g] (ro coef):
@@ -191,17 +191,16 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
                                                           float* __restrict__ PW, float* __restrict__ E,
                                                           float* __restrict__ gsd, float* __restrict__ gw,
                                                           float* __restrict__ gdot, float* __restrict__ ggam, int G,
-                                                          int Fs, int H, int W, int64_t npix) {
-  const int64_t HW = (int64_t)H * W;
-  for (int64_t i = blockIdx.x * (int64_t)NTB + threadIdx.x; i < npix; i += (int64_t)gridDim.x * NTB) {
-    const int64_t bg = i / HW;
-    const int p = (int)(i - bg * HW);
-    const int g = (int)(bg % G);
+                                                          int Fs, int H, int W) {
+  const int64_t HW = (int64_t)H * W;                 // grid (x, B*G) as the GLR kernel
+  const int64_t bg = blockIdx.y;
+  const int g = (int)(bg % G);
+  const float sc = scale ? scale[g] : 1.f;
+  const float gm = prox ? expf(log_gamma[g]) : 0.f;
+  float dot = 0.f, dgam = 0.f;
+  for (int p = blockIdx.x * NTB + threadIdx.x; p < HW; p += gridDim.x * NTB) {
     const int r = p / W, c = p - r * W;
-    const float sc = scale ? scale[g] : 1.f;
-    const float gm = prox ? expf(log_gamma[g]) : 0.f;
     const float* wp = w + bg * K * HW + p;
-    float dot = 0.f, dgam = 0.f;
     float gwa[kWinMaxEdges];
     for (int e = 0; e < K; ++e) gwa[e] = 0.f;
     for (int ch = 0; ch < Fs; ++ch) {
@@ -238,9 +237,9 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
       gsd[plane + p] = gs;
     }
     for (int e = 0; e < K; ++e) gw[bg * K * HW + e * HW + p] += gwa[e];
-    if (gdot) wave_atomic(gdot + g, coef * dot);
-    if (prox && ggam) wave_atomic(ggam + g, dgam);
   }
+  if (gdot) wave_atomic(gdot + g, coef * dot);
+  if (prox && ggam) wave_atomic(ggam + g, dgam);
 }
 
 // ---- pass 2 (gather):  gs(q) = gsd(q) - sum_e sum_{p: clamp(p + d_e) = q} E_e(p)
@@ -372,6 +371,9 @@ __global__ __launch_bounds__(NTB) void win_mix_bwd_kernel(const float* __restric
 }
 
 int grid_1d(int64_t n) { return (int)std::min<int64_t>((n + NTB - 1) / NTB, 1 << 16); }
+dim3 plane_grid(int H, int W, int planes) {
+  return dim3((unsigned)std::min<int64_t>(((int64_t)H * W + NTB - 1) / NTB, 65535), (unsigned)planes);
+}
 
 // delta: int32 [K,2] (dy, dx), the layout grr_win_edge_weights / grr_win_solver take
 bool fill_delta(const int32_t* delta, int K, WinDeltaB& d) {
@@ -430,9 +432,9 @@ grr_status grr_win_bwd_glr(const float* s, const float* b, const float* w, const
   GRR_REQUIRE(s && b && w && l_out && E && gsd && gw && B > 0 && G > 0 && Fs > 0 && H > 1 && W > 1 &&
                   fill_delta(delta, K, d),
               GRR_ERR_INVALID_ARG, "grr_win_bwd_glr: bad args");
-  const int64_t npix = (int64_t)B * G * H * W;
-  hipLaunchKernelGGL(win_glr_bwd_kernel, dim3(grid_1d(npix)), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K, scale,
-                     coef, l_out, E, gsd, gw, gdot, G, Fs, H, W, npix);
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_glr: B*G > 65535");
+  hipLaunchKernelGGL(win_glr_bwd_kernel, plane_grid(H, W, B * G), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K,
+                     scale, coef, l_out, E, gsd, gw, gdot, G, Fs, H, W);
   return launch_status("grr_win_bwd_glr");
 }
 
@@ -445,9 +447,9 @@ grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const
   GRR_REQUIRE(s && b && w && PW && E && gsd && gw && B > 0 && G > 0 && Fs > 0 && H > 1 && W > 1 &&
                   (!prox || log_gamma) && fill_delta(delta, K, d),
               GRR_ERR_INVALID_ARG, "grr_win_bwd_gtv: bad args");
-  const int64_t npix = (int64_t)B * G * H * W;
-  hipLaunchKernelGGL(win_gtv_bwd_kernel, dim3(grid_1d(npix)), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K, prox,
-                     log_gamma, scale, coef, PW, E, gsd, gw, gdot, ggamma, G, Fs, H, W, npix);
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_gtv: B*G > 65535");
+  hipLaunchKernelGGL(win_gtv_bwd_kernel, plane_grid(H, W, B * G), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K,
+                     prox, log_gamma, scale, coef, PW, E, gsd, gw, gdot, ggamma, G, Fs, H, W);
   return launch_status("grr_win_bwd_gtv");
 }
 

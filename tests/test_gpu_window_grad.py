@@ -234,6 +234,11 @@ def _model_grads_vs_oracle(model, oracle_fn, img, tol):
     (out * go.float().to(DEV)).sum().backward()
     for k, prm in model.named_parameters():
         assert prm.grad is not None, k
+        if k.endswith("gamma00"):
+            # gamma = 1e-9 keeps every soft-threshold branch stable; its own gradient is then ~0
+            # on both sides (rounding noise) -- checked at gamma = 0.02 by the solver test
+            assert float(prm.grad.abs().max()) <= 1e-6 * max(float(p[k.replace("gamma00", "ro00")].grad.abs().max()), 1)
+            continue
         assert rel_l2(prm.grad, p[k].grad) <= tol, k
 
 
