@@ -36,7 +36,11 @@ def main():
     ap.add_argument("--stages", type=int, default=4, help="n_cgd_iters (the reference runs 4)")
     ap.add_argument("--breakdown", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train", action="store_true",
+                    help="time a training step (L1 loss, backward through window_bwd.hip, Adam) instead")
     args = ap.parse_args()
+    if args.train:
+        return train_main(args)
 
     import irdu_amd
     from irdu_amd import kernels as K
@@ -105,6 +109,68 @@ def main():
         res["cpu_baseline"] = {"value": round(hw * hw / cdt / 1e6, 5), "unit": "MPix/s", "cores": threads,
                                "kind": "port", "sample": f"1 patch {hw}x{hw}: {cdt:.1f} s"}
         res["rel_err_vs_oracle"] = float((got.double() - ref.double()).abs().max() / ref.double().abs().max())
+    print(json.dumps(res))
+
+
+def train_main(args):
+    """Training step of the multiblocks script (run_lightformer_GGTV_GGLR_multiblocks.py:186-193):
+    L1 loss, backward (feature CNN on PyTorch autograd, solver / edge weights / mixture on the
+    window_bwd.hip reverse), Adam step."""
+    import irdu_amd
+    from irdu_amd import kernels as K
+    from irdu_amd import window_graph as WG
+    from bench import synthetic_patches
+    irdu_amd.load_native()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(2207)
+    model = WG.MultiScaleSequenceDenoiser(n_cgd_iters=args.stages)
+    mix = model.mixtureGLR_block03
+    with torch.no_grad():
+        mix.muys00.fill_(0.4); mix.ro00.fill_(0.3); mix.gamma00.fill_(float(np.log(0.005)))
+    model = model.to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=4e-4, eps=1e-8)
+    b, hw = args.batch, args.size
+    clean, noisy = synthetic_patches(b, seed=2207, h=hw, w=hw)
+    clean, noisy = clean.to(dev), noisy.to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.l1_loss(model(noisy), clean)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    timer = K.LaunchTimer()
+    K.set_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    K.set_timer(None)
+    kern = timer.summary()
+    hip_ms = sum(v["total_ms"] for v in kern.values()) / args.steps
+    rev = {k: v for k, v in kern.items() if k.startswith("win_bwd") or k.startswith("bwd_")}
+    top = max(rev, key=lambda k: rev[k]["total_ms"])
+    res = {"metric": "MPix/s, window-graph MixtureGTV training step (REF7 MultiScaleSequenceDenoiser)",
+           "value": round(b * hw * hw * args.steps / dt / 1e6, 3), "unit": "MPix/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "higher_is_better": True, "dtype": "f32", "data": "synthetic", "loss": float(loss),
+           "config": {"workload": f"MultiScaleSequenceDenoiser v7 training step: G=24 F=3, K=12, n_cnn_fts=128, "
+                                  f"{args.stages} CG stages + 1 ADMM prox, {hw}x{hw} RGB, L1 + Adam",
+                      "per_gpu_batch": b},
+           "hip_ms_per_step": round(hip_ms, 3),
+           "dominant_reverse_kernel": {"kind": top, "achieved": round(rev[top]["gbps"], 1), "peak": HBM_PEAK_GBPS,
+                                       "unit": "GB/s", "frac": round(rev[top]["gbps"] / HBM_PEAK_GBPS, 4),
+                                       "mean_launch_ms": round(rev[top]["mean_ms"], 4)},
+           "kernel_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}}
+    if args.breakdown:
+        for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
+            print(f"{k:22s} launches/step={v['launches'] / args.steps:5.1f} mean={v['mean_ms']:8.3f} ms "
+                  f"algo={v['gbps']:8.1f} GB/s", file=sys.stderr)
     print(json.dumps(res))
 
 

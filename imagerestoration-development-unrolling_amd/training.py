@@ -70,10 +70,15 @@ def parse_options(yaml_path: str) -> dict:
 # ---------------------------------------------------------------------------
 # data (environ/data/*)
 # ---------------------------------------------------------------------------
-def _noisy(patch: np.ndarray, rs: np.random.RandomState, dist_mode: str, lambda_noise: float) -> np.ndarray:
-    """images_pair_restoration_dataset.py:101-110: additive Gaussian noise, sigma = lambda/255."""
+def _noisy(patch: np.ndarray, rs: np.random.RandomState, dist_mode: str, lambda_noise) -> np.ndarray:
+    """images_pair_restoration_dataset.py:101-110: additive Gaussian noise, sigma = lambda/255;
+    vary_addictive_noise (model_multiscale_mixture_GLR/lib/dataloader.py:165-169): lambda_noise =
+    [levels, probabilities], one level drawn per patch."""
     if dist_mode == "addictive_noise":
         noise = rs.normal(loc=0.0, scale=lambda_noise / 255.0, size=patch.shape)
+    elif dist_mode == "vary_addictive_noise":
+        level = rs.choice(lambda_noise[0], p=lambda_noise[1])
+        noise = rs.normal(loc=0.0, scale=level / 255.0, size=patch.shape)
     elif dist_mode == "addictive_noise_scale":
         noise = rs.normal(loc=0.0, scale=1.0, size=patch.shape) * (lambda_noise / 255.0)
     else:
@@ -221,19 +226,28 @@ def create_dataloader(dataset, sampler, dataset_conf: dict, environ_conf: dict):
 def build_model(model_conf: dict) -> nn.Module:
     import irdu_amd
     kind = model_conf.get("type", "AbtractMultiScaleGraphFilter")
+    from irdu_amd import window_graph, window_graph_v1
     cls = {"AbtractMultiScaleGraphFilter": irdu_amd.AbtractMultiScaleGraphFilter,
            "MultiScaleGraphFilter": irdu_amd.MultiScaleGraphFilter,
            "GLRImageFilter": irdu_amd.GLRImageFilter,
-           "MultiScaleGLRImageFilter": irdu_amd.MultiScaleGLRImageFilter}.get(kind)
+           "MultiScaleGLRImageFilter": irdu_amd.MultiScaleGLRImageFilter,
+           # window-graph denoisers of the multiblocks scripts (REF7 v7 / REF1 v1)
+           "MultiScaleSequenceDenoiser": window_graph.MultiScaleSequenceDenoiser,
+           "MultiScaleSequenceDenoiserV1": window_graph_v1.MultiScaleSequenceDenoiser}.get(kind)
     if cls is None:
         raise ValueError(f"model type {kind!r} has no training path")
     return cls(**model_conf.get("args", {}))
 
 
 def build_optimizer(model: nn.Module, tconf: dict):
-    """Adam + MultiStepLR(gamma=sqrt(sqrt(0.5))) -> CosineAnnealingLR (base lr 5e-5) via SequentialLR."""
+    """Adam + MultiStepLR(gamma=sqrt(sqrt(0.5))) -> CosineAnnealingLR (base lr 5e-5) via SequentialLR;
+    ``lr_schedule: multistep`` is the multiblocks scripts' Adam + MultiStepLR(milestones, lr_gamma)
+    (run_lightformer_GGTV_GGLR_multiblocks.py:166-174)."""
     from torch.optim.lr_scheduler import CosineAnnealingLR, MultiStepLR, SequentialLR
     opt = torch.optim.Adam(model.parameters(), lr=tconf.get("lr", 4e-4), eps=tconf.get("eps", 1e-8))
+    if tconf.get("lr_schedule", "v2") == "multistep":
+        return opt, MultiStepLR(opt, milestones=list(tconf.get("milestones", [200000, 500000, 650000])),
+                                gamma=float(tconf.get("lr_gamma", 0.5)))
     switch = tconf.get("cosine_from", 600000)
     s1 = MultiStepLR(opt, milestones=list(tconf.get("milestones", range(50000, 600001, 50000))),
                      gamma=float(np.sqrt(np.sqrt(0.5))))

@@ -69,3 +69,27 @@ def test_c1_example_yaml_trains_and_matches_oracle(T, tmp_path):
     err = float((got.double() - ref.double()).abs().max() / ref.double().abs().max())
     assert err <= 1e-4, err
     assert abs(O.psnr_ubyte(got, clean) - O.psnr_ubyte(ref, clean)) <= 0.01
+
+
+def test_run_train_multiblocks_v7_yaml(T, tmp_path):
+    """The multiblocks script's model (REF7 MultiScaleSequenceDenoiser: 24 graphs x 3 features,
+    5x5 diamond, feature CNN 128 wide) trains through run_train on the window-graph HIP reverse:
+    finite loss, every solver parameter receives a gradient, the reference's checkpoint dict."""
+    conf = T.parse_options(os.path.join(ROOT, "experiment_conf", "multiblocks_v7.yaml"))
+    assert conf["model"]["type"] == "MultiScaleSequenceDenoiser"
+    conf["path"]["root_dir"] = str(tmp_path)
+    conf["train"].update(total_iters=3, checkpoint_every=3, verbose_every=1)
+    conf["datasets"]["train"]["dataset_args"].update(max_num_patchs=16, patch_size=32)
+    conf["datasets"]["train"]["dataloader_args"]["batch_size"] = 2
+    tr = T.run(conf, device=torch.device("cuda:0"))
+    assert tr.i == 3
+    mix = tr.model.mixtureGLR_block03
+    for name in ("alphaCGD", "betaCGD", "ro00", "muys00", "gamma00"):
+        g = getattr(mix, name).grad
+        assert g is not None and bool(torch.isfinite(g).all()), name
+    for mod in (mix.GTVmodule00, mix.GLRmodule00):
+        assert mod.multiM.grad is not None and float(mod.multiM.grad.abs().sum()) > 0
+        assert mod.stats_kernel_p03.grad is not None
+    saved = torch.load(os.path.join(T.checkpoint_dir(conf), "checkpoint_iter00000003.pt"), weights_only=True)
+    assert set(saved) == {"i", "model", "optimizer", "lr_scheduler"}
+    assert all(np.isfinite(v.float().cpu().numpy()).all() for v in saved["model"].values())

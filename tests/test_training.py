@@ -61,6 +61,26 @@ def test_synthetic_dataset_deterministic_and_noise_law():
     assert abs(float(noise.std()) - 25.0 / 255.0) < 0.15 * 25.0 / 255.0
 
 
+def test_multiblocks_yaml_noise_mix_and_schedule():
+    """experiment_conf/multiblocks_v7.yaml: the multiblocks script's noise mix
+    (lib/dataloader.py:165-169, one sigma per patch) and Adam + MultiStepLR(0.5)."""
+    conf = T.parse_options(os.path.join(ROOT, "experiment_conf", "multiblocks_v7.yaml"))
+    args = dict(conf["datasets"]["train"]["dataset_args"], patch_size=16, max_num_patchs=400)
+    ds = T.SyntheticNoisyPatches(**args)
+    sig = np.array([float((ds[i][0] - ds[i][1]).std()) * 255.0 for i in range(400)])
+    levels = np.array([1.0, 10.0, 15.0, 20.0, 25.0])
+    picked = levels[np.abs(sig[:, None] - levels[None]).argmin(1)]
+    assert abs(float((picked == 25.0).mean()) - 0.6) < 0.1
+    assert set(np.unique(picked)) <= set(levels)
+    opt, sched = T.build_optimizer(TinyModel(), dict(conf["train"], milestones=[2, 4]))
+    lrs = []
+    for _ in range(6):
+        lrs.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sched.step()
+    assert lrs == pytest.approx([4e-4, 4e-4, 2e-4, 2e-4, 1e-4, 1e-4])
+
+
 def test_resumeable_sampler_resumes_and_shards():
     ds = T.SyntheticNoisyPatches(patch_size=16, max_num_patchs=10)
     s = T.ResumeableSampler(ds)
