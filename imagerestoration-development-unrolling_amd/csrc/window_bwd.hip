@@ -36,9 +36,28 @@ __device__ __forceinline__ float wsum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ void wave_atomic(float* dst, float v) {
-  v = wsum(v);
-  if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(dst, v);
+// Block-wide sums of N per-thread values, one float atomic per value per block: dst[idx[i]] += sum.
+// Every thread of the block must call it (the grid-stride loops end before it).
+template <int N>
+__device__ __forceinline__ void block_atomic(float (&v)[N], float* const (&dst)[N]) {
+  __shared__ float red[NTB / 64][N];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float s = wsum(v[i]);
+    if (lane == 0) red[wave][i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NTB / 64; ++w) t += red[w][threadIdx.x];
+    float* d = nullptr;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (i == (int)threadIdx.x) d = dst[i];
+    if (d && t != 0.f) atomicAdd(d, t);
+  }
 }
 __device__ __forceinline__ int refl(int v, int n) {   // one-pixel reflect frame
   v = v < 0 ? -v : v;
@@ -132,8 +151,8 @@ __global__ __launch_bounds__(NTB) void win_tapgrad_kernel(const float* __restric
       }
     }
   }
-#pragma unroll
-  for (int t = 0; t < 5; ++t) wave_atomic(gt + t, acc[t]);
+  float* const dst[5] = {gt, gt + 1, gt + 2, gt + 3, gt + 4};
+  block_atomic<5>(acc, dst);
 }
 
 // ---- GLR pass 1.  Per (b, g) and pixel q, channels in turn; sc = scale[g] (mu coef):
@@ -176,7 +195,9 @@ __global__ __launch_bounds__(NTB) void win_glr_bwd_kernel(const float* __restric
     }
     for (int e = 0; e < K; ++e) gw[bg * K * HW + e * HW + q] += gwa[e];
   }
-  if (gdot) wave_atomic(gdot + g, coef * dot);
+  float v[1] = {coef * dot};
+  float* const dst[1] = {gdot ? gdot + g : nullptr};
+  block_atomic<1>(v, dst);
 }
 
 // ---- GTV pass 1 (linear C^T C or the prox C^T phi(C .)).  sc = scale[g] (ro coef):
@@ -238,8 +259,9 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
     }
     for (int e = 0; e < K; ++e) gw[bg * K * HW + e * HW + p] += gwa[e];
   }
-  if (gdot) wave_atomic(gdot + g, coef * dot);
-  if (prox && ggam) wave_atomic(ggam + g, dgam);
+  float v[2] = {coef * dot, dgam};
+  float* const dst[2] = {gdot ? gdot + g : nullptr, prox && ggam ? ggam + g : nullptr};
+  block_atomic<2>(v, dst);
 }
 
 // ---- pass 2 (gather):  gs(q) = gsd(q) - sum_e sum_{p: clamp(p + d_e) = q} E_e(p)
@@ -294,60 +316,74 @@ __global__ __launch_bounds__(NTB) void win_feat_bwd_kernel(const float* __restri
                                                            const float* __restrict__ multiM,
                                                            const float* __restrict__ gsim, WinDeltaB d, int K,
                                                            float* __restrict__ gfeat, int64_t gstride,
-                                                           float* __restrict__ gM, int G, int F, int H, int W,
-                                                           int64_t npix) {
+                                                           float* __restrict__ gM, int G, int F, int H, int W) {
+  // grid (x, B*G): the graph is fixed per block, so gM reduces per block (one atomic per f)
   const int64_t HW = (int64_t)H * W;
-  for (int64_t i = blockIdx.x * (int64_t)NTB + threadIdx.x; i < npix; i += (int64_t)gridDim.x * NTB) {
-    const int64_t bg = i / HW;
-    const int q = (int)(i - bg * HW);
-    const int g = (int)(bg % G), b = (int)(bg / G);
-    const int r = q / W, c = q - r * W;
-    const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW;
-    float* gfp = gfeat + (int64_t)b * gstride + (int64_t)g * F * HW;
-    const float* gsp = gsim + bg * K * HW;
-    float M[FMAX], inv_at_q, nrm = 0.f;
-    for (int f = 0; f < F; ++f) {
-      M[f] = multiM[g * F + f];
-      const float v = fp[f * HW + q];
-      nrm += v * v;
+  const int bg = blockIdx.y, g = bg % G, b = bg / G;
+  const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW;
+  float* gfp = gfeat + (int64_t)b * gstride + (int64_t)g * F * HW;
+  const float* gsp = gsim + (int64_t)bg * K * HW;
+  float M[FMAX], gMa[FMAX];
+#pragma unroll
+  for (int f = 0; f < FMAX; ++f) {
+    M[f] = f < F ? multiM[g * F + f] : 0.f;
+    gMa[f] = 0.f;
+  }
+  // fh(pix) = M f(pix) / max(|f(pix)|, eps), accumulated as  acc += wt * fh(pix)
+  auto add_fh = [&](float (&acc)[FMAX], int pix, float wt) {
+    float v[FMAX], ss = 0.f;
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) {
+      v[f] = f < F ? fp[f * HW + pix] : 0.f;
+      ss += v[f] * v[f];
     }
-    inv_at_q = 1.f / fmaxf(sqrtf(nrm), 1e-12f);
-    auto inv_at = [&](int pix) {
-      float ss = 0.f;
-      for (int f = 0; f < F; ++f) {
-        const float v = fp[f * HW + pix];
-        ss += v * v;
-      }
-      return 1.f / fmaxf(sqrtf(ss), 1e-12f);
-    };
+    const float c = wt / fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) acc[f] += c * (v[f] * M[f]);
+  };
+  for (int q = blockIdx.x * NTB + threadIdx.x; q < HW; q += gridDim.x * NTB) {
+    const int r = q / W, c = q - r * W;
     float gfh[FMAX];
-    for (int f = 0; f < F; ++f) gfh[f] = 0.f;
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) gfh[f] = 0.f;
     for (int e = 0; e < K; ++e) {
       const int nq = clampi(r + d.dy[e], 0, H - 1) * W + clampi(c + d.dx[e], 0, W - 1);
-      const float gs = gsp[e * HW + q], in_ = inv_at(nq);
-      for (int f = 0; f < F; ++f) gfh[f] += gs * (fp[f * HW + nq] * in_ * M[f]);
+      add_fh(gfh, nq, gsp[e * HW + q]);
       int sy[3], sx[3];
       const int ny = clamp_sources(r, d.dy[e], H, sy), nx = clamp_sources(c, d.dx[e], W, sx);
       for (int a = 0; a < ny; ++a)
         for (int bb = 0; bb < nx; ++bb) {
           const int pp = sy[a] * W + sx[bb];
-          const float gp = gsp[e * HW + pp], ip = inv_at(pp);
-          for (int f = 0; f < F; ++f) gfh[f] += gp * (fp[f * HW + pp] * ip * M[f]);
+          add_fh(gfh, pp, gsp[e * HW + pp]);
         }
     }
+    float v[FMAX], nrm = 0.f;
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) {
+      v[f] = f < F ? fp[f * HW + q] : 0.f;
+      nrm += v[f] * v[f];
+    }
+    const float inv = 1.f / fmaxf(sqrtf(nrm), 1e-12f);
+    const bool small = sqrtf(nrm) <= 1e-12f;
     float ndg = 0.f;
-    for (int f = 0; f < F; ++f) {
-      const float n = fp[f * HW + q] * inv_at_q;
-      atomicAdd(gM + g * F + f, gfh[f] * n);
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) {
+      const float n = v[f] * inv;
+      gMa[f] += gfh[f] * n;
       ndg += n * (gfh[f] * M[f]);
     }
-    const bool small = 1.f / inv_at_q <= 1e-12f;
-    for (int f = 0; f < F; ++f) {
-      const float n = fp[f * HW + q] * inv_at_q;
-      const float gn = gfh[f] * M[f];
-      gfp[f * HW + q] += small ? gn * inv_at_q : (gn - n * ndg) * inv_at_q;   // GTV and GLR share a slab
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) {
+      if (f < F) {
+        const float n = v[f] * inv, gn = gfh[f] * M[f];
+        gfp[f * HW + q] += small ? gn * inv : (gn - n * ndg) * inv;   // GTV and GLR share a slab
+      }
     }
   }
+  float* dst[FMAX];
+#pragma unroll
+  for (int f = 0; f < FMAX; ++f) dst[f] = f < F ? gM + g * F + f : nullptr;
+  block_atomic<FMAX>(gMa, dst);
 }
 
 // ---- mixture reverse (REF7:1006-1009): out[b,c] = sum_g score[b,g] x[b,g,c] + dc[b,c]
@@ -371,8 +407,12 @@ __global__ __launch_bounds__(NTB) void win_mix_bwd_kernel(const float* __restric
 }
 
 int grid_1d(int64_t n) { return (int)std::min<int64_t>((n + NTB - 1) / NTB, 1 << 16); }
+// reduction kernels: about 4096 blocks in all (16 per CU), grid-stride beyond, so the per-block
+// atomics stay few
+int grid_red(int64_t n) { return (int)std::min<int64_t>((n + NTB - 1) / NTB, 4096); }
 dim3 plane_grid(int H, int W, int planes) {
-  return dim3((unsigned)std::min<int64_t>(((int64_t)H * W + NTB - 1) / NTB, 65535), (unsigned)planes);
+  const int64_t per = std::max<int64_t>(1, 4096 / std::max(planes, 1));
+  return dim3((unsigned)std::min<int64_t>(((int64_t)H * W + NTB - 1) / NTB, per), (unsigned)planes);
 }
 
 // delta: int32 [K,2] (dy, dx), the layout grr_win_edge_weights / grr_win_solver take
@@ -418,9 +458,9 @@ grr_status grr_win_bwd_tapgrad(const float* u, const float* z, int mode, const f
   const int64_t n = (int64_t)B * G * Fs * H * W;
   hipStream_t s = (hipStream_t)stream;
   if (mode == 0)
-    hipLaunchKernelGGL(win_tapgrad_kernel<0>, dim3(grid_1d(n)), dim3(NTB), 0, s, u, z, scale, gtaps, G, Fs, H, W, n);
+    hipLaunchKernelGGL(win_tapgrad_kernel<0>, dim3(grid_red(n)), dim3(NTB), 0, s, u, z, scale, gtaps, G, Fs, H, W, n);
   else
-    hipLaunchKernelGGL(win_tapgrad_kernel<1>, dim3(grid_1d(n)), dim3(NTB), 0, s, u, z, scale, gtaps, G, Fs, H, W, n);
+    hipLaunchKernelGGL(win_tapgrad_kernel<1>, dim3(grid_red(n)), dim3(NTB), 0, s, u, z, scale, gtaps, G, Fs, H, W, n);
   return launch_status("grr_win_bwd_tapgrad");
 }
 
@@ -479,9 +519,10 @@ grr_status grr_win_bwd_edge_weights(const float* feat, int64_t feat_bstride, con
   const int64_t npix = (int64_t)B * G * H * W;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(win_softmax_bwd_kernel, dim3(grid_1d(npix)), dim3(NTB), 0, s, w, gw, K, (int64_t)H * W, npix);
-#define WIN_FEAT_BWD(FM_)                                                                                     \
-  hipLaunchKernelGGL(win_feat_bwd_kernel<FM_>, dim3(grid_1d(npix)), dim3(NTB), 0, s, feat, feat_bstride, multiM, gw, \
-                     d, K, gfeat, gfeat_bstride, gmultiM, G, F, H, W, npix)
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_edge_weights: B*G > 65535");
+#define WIN_FEAT_BWD(FM_)                                                                                          \
+  hipLaunchKernelGGL(win_feat_bwd_kernel<FM_>, plane_grid(H, W, B * G), dim3(NTB), 0, s, feat, feat_bstride, multiM, \
+                     gw, d, K, gfeat, gfeat_bstride, gmultiM, G, F, H, W)
   if (F <= 4)
     WIN_FEAT_BWD(4);
   else if (F <= 12)
