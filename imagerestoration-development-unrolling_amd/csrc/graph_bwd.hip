@@ -533,6 +533,55 @@ __global__ __launch_bounds__(NT) void lincomb_kernel(const float* __restrict__ x
   }
 }
 
+// One reverse step of the stage recurrence x' = x + alpha u, u = r - A x + beta u_prev, without
+// the operator term (REF:784-807), in one pass over the (b, g) slab:
+//   galpha[g] += <gx', u>;  gu = alpha[g] gx' + beta_next[g] gu_next;  gbeta[g] += <gu, u_prev>;
+//   gbb += gu;  gx_out = gx' - gu  (gx_out may alias gx).                 grid (chunks, B*G)
+template <bool V4>
+__global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const float* __restrict__ u,
+                                                     const float* __restrict__ gun, const float* __restrict__ up,
+                                                     const float* __restrict__ alpha,
+                                                     const float* __restrict__ beta_next, float* __restrict__ gu_out,
+                                                     float* __restrict__ gbb, float* gx_out, float* __restrict__ galpha,
+                                                     float* __restrict__ gbeta, int G, int64_t n) {
+  const int bg = blockIdx.y, g = bg % G;
+  const int64_t base = (int64_t)bg * n;
+  const float al = alpha[g], be = gun ? beta_next[g] : 0.f;
+  float da = 0.f, db = 0.f;
+  if constexpr (V4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int64_t n4 = n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+      const int64_t o = base + 4 * i;
+      const f4 x = *reinterpret_cast<const f4*>(gx + o), uv = *reinterpret_cast<const f4*>(u + o);
+      f4 gu = al * x;
+      if (gun) gu += be * *reinterpret_cast<const f4*>(gun + o);
+      da += x.x * uv.x + x.y * uv.y + x.z * uv.z + x.w * uv.w;
+      if (up) {
+        const f4 pv = *reinterpret_cast<const f4*>(up + o);
+        db += gu.x * pv.x + gu.y * pv.y + gu.z * pv.z + gu.w * pv.w;
+      }
+      if (gbb) *reinterpret_cast<f4*>(gbb + o) += gu;
+      *reinterpret_cast<f4*>(gu_out + o) = gu;
+      *reinterpret_cast<f4*>(gx_out + o) = x - gu;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+      const int64_t o = base + i;
+      const float x = gx[o];
+      float gu = al * x;
+      if (gun) gu += be * gun[o];
+      da += x * u[o];
+      if (up) db += gu * up[o];
+      if (gbb) gbb[o] += gu;
+      gu_out[o] = gu;
+      gx_out[o] = x - gu;
+    }
+  }
+  block_atomic_add(galpha + g, da);
+  if (up) block_atomic_add(gbeta + g, db);
+}
+
 // out(q) += 0.25 * xd(q / 2)   (U = conv_transpose2d of the 0.25 2x2 kernel, stride 2; REF:676-679)
 __global__ __launch_bounds__(NT) void unpool2_acc_kernel(const float* __restrict__ xd, float* __restrict__ out, int H,
                                                          int W, int64_t n) {
@@ -1438,6 +1487,28 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   hipLaunchKernelGGL(graph_dot_kernel, dim3(chunks_for((int64_t)F * H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream,
                      u, v, coef, gdot, G, F, (int64_t)H * W);
   return launch_status("grr_bwd_graph_dot");
+}
+
+grr_status grr_bwd_cg_glue(const float* gx, const float* u, const float* gu_next, const float* u_prev,
+                           const float* alpha, const float* beta_next, float* gu, float* gbb, float* gx_out,
+                           float* galpha, float* gbeta, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(gx && u && alpha && gu && gx_out && galpha && (!gu_next || beta_next) && (!u_prev || gbeta) && B > 0 &&
+                  G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_bwd_cg_glue: bad args");
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_cg_glue: B*G > 65535");
+  const int64_t n = (int64_t)F * H * W;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool v4 = n % 4 == 0 && al16(gx) && al16(u) && al16(gu) && al16(gx_out) && (!gu_next || al16(gu_next)) &&
+                  (!u_prev || al16(u_prev)) && (!gbb || al16(gbb));
+  const dim3 grid(chunks_for(v4 ? n / 4 : n, (int64_t)B * G), B * G);
+  if (v4)
+    hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, u, gu_next, u_prev, alpha,
+                       beta_next, gu, gbb, gx_out, galpha, gbeta, G, n);
+  else
+    hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, u, gu_next, u_prev, alpha,
+                       beta_next, gu, gbb, gx_out, galpha, gbeta, G, n);
+  return launch_status("grr_bwd_cg_glue");
 }
 
 grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,

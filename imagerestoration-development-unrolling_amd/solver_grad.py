@@ -141,6 +141,17 @@ def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn) ->
     K.bwd_unpool2_acc(gxd, out)               # D^T = U
 
 
+def cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Optional[Tensor], alpha: Tensor, beta: Tensor,
+            gbb: Optional[Tensor], galpha: Tensor, gbeta: Tensor, k: int, g: int, owned: bool) -> Tuple[Tensor, Tensor]:
+    """Reverse of stage k's recurrence glue (x' = x + a_k u_k, u_k = r - A x + b_k u_{k-1}) without the
+    operator term: returns (gu_k, gx' - gu_k); ga_k, gb_k (when u_prev) and gbb accumulate.  owned: gx
+    is this sweep's own buffer and is overwritten."""
+    gu, gx2 = K.bwd_cg_glue(gx, u, gu_next, u_prev, alpha[k].contiguous(),
+                            beta[k + 1].contiguous() if gu_next is not None else None, gbb, galpha[k],
+                            gbeta[k] if u_prev is not None else None, g, inplace=owned)
+    return gu, gx2
+
+
 def _stencil(t4) -> Stencil:
     return Stencil(*[t.data_ptr() for t in t4])
 
@@ -211,16 +222,9 @@ class _MixtureSolve(torch.autograd.Function):
             gbb = torch.zeros_like(y)
             gu_next = None
             for k in range(n_st - 1, 0, -1):
-                K.bwd_graph_dot(gx, us[k], galpha[k], g)
-                if gu_next is not None and k + 1 >= 2:
-                    gu = K.bwd_lincomb(gx, alpha[k], gu_next, beta[k + 1], g)
-                else:
-                    gu = K.bwd_lincomb(gx, alpha[k], None, None, g)
-                if k >= 2:
-                    K.bwd_graph_dot(gu, us[k - 1], gbeta[k], g)
-                K.bwd_lincomb(gu, None, None, None, g, out=gbb, accumulate=True)
-                neg = torch.full_like(alpha[k], -1.0)
-                gx = K.bwd_lincomb(gx, None, gu, neg, g)            # gx_{k+1} - gu
+                # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue)
+                gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
+                                 galpha, gbeta, k, g, owned=k < n_st - 1)
                 a_bwd(xs[k], gu, -1.0, gx)                          #   - (A - I)^T gu
                 gu_next = gu
             # b_B = y + prox terms(x_1)
@@ -437,22 +441,14 @@ class _GLRSolve(torch.autograd.Function):
         gy = torch.zeros_like(y)
         gx = gout.contiguous()
         gu_next = None
-        neg = torch.full_like(mu, -1.0)
         for k in range(n_st - 1, -1, -1):
             # x_{k+1} = x_k + a_k u_k,  u_k = (y - A x_k) + b_k u_{k-1}   (u_{-1} = 0; x_0 = y)
-            K.bwd_graph_dot(gx, us[k], galpha[k], g)
-            if gu_next is not None:
-                gu = K.bwd_lincomb(gx, alpha[k], gu_next, beta[k + 1], g)
-            else:
-                gu = K.bwd_lincomb(gx, alpha[k], None, None, g)
+            gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 1 else None, alpha, beta, gy, galpha, gbeta,
+                             k, g, owned=k < n_st - 1)                     # gx <- gx_{k+1} - gu
             if k >= 1:
-                K.bwd_graph_dot(gu, us[k - 1], gbeta[k], g)
-            K.bwd_lincomb(gu, None, None, None, g, out=gy, accumulate=True)
-            if k >= 1:
-                gx = K.bwd_lincomb(gx, None, gu, neg, g)                   # gx_{k+1} - gu
                 glr_term_bwd(xs[k], gu, taps, wL, mu, -1.0, g, gx, gw, gmu, gtaps)
             else:                                                           # x_0 = y
-                K.bwd_lincomb(gx, None, gu, neg, g, out=gy, accumulate=True)
+                gy.add_(gx)
                 glr_term_bwd(y, gu, taps, wL, mu, -1.0, g, gy, gw, gmu, gtaps)
             gu_next = gu
         gfeat, gM = torch.empty_like(feat), torch.zeros_like(p["GLRmodule00.multiM"])
@@ -520,7 +516,6 @@ class _GLR2Solve(torch.autograd.Function):
         gm0, gm1 = torch.zeros_like(mu0), torch.zeros_like(mu1)
         galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
         gy = torch.zeros_like(y)
-        neg = torch.full_like(mu0, -1.0)
 
         def a_bwd(x: Tensor, gu: Tensor, out: Tensor) -> None:     # out -= (A - I)^T gu (+ params)
             glr_term_bwd(x, gu, taps0, wL0, mu0, -1.0, g, out, gw0, gm0, gt0)
@@ -532,19 +527,12 @@ class _GLR2Solve(torch.autograd.Function):
         gx = gout.contiguous()
         gu_next = None
         for k in range(n_st - 1, -1, -1):
-            K.bwd_graph_dot(gx, us[k], galpha[k], g)
-            if gu_next is not None:
-                gu = K.bwd_lincomb(gx, alpha[k], gu_next, beta[k + 1], g)
-            else:
-                gu = K.bwd_lincomb(gx, alpha[k], None, None, g)
+            gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 1 else None, alpha, beta, gy, galpha, gbeta,
+                             k, g, owned=k < n_st - 1)                     # gx <- gx_{k+1} - gu
             if k >= 1:
-                K.bwd_graph_dot(gu, us[k - 1], gbeta[k], g)
-            K.bwd_lincomb(gu, None, None, None, g, out=gy, accumulate=True)
-            if k >= 1:
-                gx = K.bwd_lincomb(gx, None, gu, neg, g)                   # gx_{k+1} - gu
                 a_bwd(xs[k], gu, gx)
             else:                                                           # x_0 = y
-                K.bwd_lincomb(gx, None, gu, neg, g, out=gy, accumulate=True)
+                gy.add_(gx)
                 a_bwd(y, gu, gy)
             gu_next = gu
         nf = y.shape[1] // g

@@ -92,10 +92,6 @@ class _Terms:
         self.gtv_bwd(x, gg, coef, out)
 
 
-def _row(v: Tensor) -> Tensor:
-    return v.contiguous()
-
-
 class _WindowSolve(torch.autograd.Function):
     """(y [B,Fs,H,W], feat [B,Ctot,H,W], params) -> x_S [B,G,Fs,H,W] of MixtureGTV's solver
     (REF7:936-1004), the graph features being channels [0, G*F) of feat."""
@@ -152,7 +148,6 @@ class _WindowSolve(torch.autograd.Function):
         T = _Terms(wG, wL, tG, tL, ro, mu, lg, delta, g)
         b, fs, h, w = y.shape
         galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
-        neg = torch.full_like(ro, -1.0)
 
         def flat(t):                                   # [B,G,Fs,H,W] viewed as [B, G*Fs, H, W]
             return t.view(b, g * fs, h, w)
@@ -161,17 +156,15 @@ class _WindowSolve(torch.autograd.Function):
         gy = torch.zeros_like(y)
         grhs = torch.zeros_like(gx)
         gu_next = None
+        owned = False
         for k in range(n_st - 1, -1, -1):
             first = k in (0, 2)
-            K.bwd_graph_dot(flat(gx), flat(us[k]), galpha[k], g)
-            if gu_next is not None:
-                gu = K.bwd_lincomb(flat(gx), alpha[k], flat(gu_next), beta[k + 1], g).view_as(gx)
-            else:
-                gu = K.bwd_lincomb(flat(gx), alpha[k], None, None, g).view_as(gx)
-            if not first:
-                K.bwd_graph_dot(flat(gu), flat(us[k - 1]), gbeta[k], g)
-            K.bwd_lincomb(flat(gu), None, None, None, g, out=flat(grhs), accumulate=True)
-            gx = K.bwd_lincomb(flat(gx), None, flat(gu), neg, g).view_as(gx)     # gx' - gu
+            # ga_k, gu_k, gb_k, grhs += gu_k, gx' - gu_k in one pass (grr_bwd_cg_glue)
+            gu, gxf = K.bwd_cg_glue(flat(gx), flat(us[k]), None if gu_next is None else flat(gu_next),
+                                    None if first else flat(us[k - 1]), alpha[k],
+                                    None if gu_next is None else beta[k + 1], flat(grhs), galpha[k],
+                                    None if first else gbeta[k], g, inplace=owned)
+            gu, gx, owned = gu.view_as(gx), gxf.view_as(gx), True
             T.a_bwd(xs[k], gu, -1.0, gx)                                           #   - (A - I)^T gu
             gu_next = gu
             if first:                                   # x_in = r: its gradient joins the rhs gradient
