@@ -360,7 +360,7 @@ __device__ __forceinline__ void split3(float v, uint32_t& h0, uint32_t& h1, uint
 }
 
 #ifndef GRR_X3_TILES
-#define GRR_X3_TILES 2
+#define GRR_X3_TILES 1   // 32-row chunks: 36 KB LDS ring at K = 96 -> 4 workgroups per CU (2 tiles: 2.38 -> 1 tile: 1.88 ms per bench step)
 #endif
 constexpr int X3_NT = GRR_X3_TILES;  // 32-row MFMA tiles per chunk
 constexpr int X3_MCH = 32 * X3_NT;   // output rows per chunk
