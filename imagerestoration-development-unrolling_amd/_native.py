@@ -88,6 +88,7 @@ SIGNATURES = {
     "grr_bwd_cg_glue": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_unpool2_acc": [P, P, I, I, I, I, P],
     "grr_conv2x2s2_bwd_data": [P, P, P, I, I, I, I, I, P],
+    "grr_interleave2x2": [P, P, I, I, I, I, P],
     "grr_lnb_norm": [P, P, P, P, I, I, L, P],
     "grr_lnb_norm_bwd": [P, P, P, P, P, P, I, I, L, P],
     "grr_dwconv3": [P, P, P, I, I, I, I, P],

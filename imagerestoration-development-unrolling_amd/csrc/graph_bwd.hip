@@ -611,6 +611,26 @@ __global__ __launch_bounds__(NT) void conv2x2s2_bwd_data_kernel(const float* __r
   gx[(int64_t)bk * HW + p] = acc;
 }
 
+// gx[b,k,2i+di,2j+dj] = t[b, (2 di + dj) K + k, i, j]: the four tap planes of the 2x2 stride-2 conv's
+// data gradient, computed as one 1x1 GEMM with 4K output rows, interleaved to full resolution.
+// One thread per 4 consecutive output pixels of a row (float4 store; two float2 source reads).
+__global__ __launch_bounds__(NT) void interleave2x2_kernel(const float* __restrict__ t, float* __restrict__ gx, int K,
+                                                           int H, int W, int64_t nq) {
+  const int h = H / 2, w = W / 2, W4 = W / 4;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nq; i += (int64_t)gridDim.x * NT) {
+    const int64_t row = i / W4;                        // (b, k, r)
+    const int c4 = (int)(i - row * W4) * 4;
+    const int r = (int)(row % H);
+    const int64_t bk = row / H;
+    const int64_t b = bk / K, k = bk - b * K;
+    const int di = r & 1;
+    const float* t0 = t + ((b * 4 + 2 * di) * K + k) * h * w + (int64_t)(r >> 1) * w + c4 / 2;
+    const float* t1 = t0 + (int64_t)K * h * w;        // dj = 1
+    const float2 e = *reinterpret_cast<const float2*>(t0), o = *reinterpret_cast<const float2*>(t1);
+    *reinterpret_cast<float4*>(gx + row * W + c4) = make_float4(e.x, o.x, e.y, o.y);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Fused term reverse: one pass per operator term instead of five.  s = P x and a = T* g
 // are recomputed on the fly at the pixel and its four neighbours (radius-2 reads that hit
@@ -1529,6 +1549,18 @@ grr_status grr_bwd_unpool2_acc(const float* xd, float* out, int B, int C, int H,
   const int64_t n = (int64_t)B * C * H * W;
   hipLaunchKernelGGL(unpool2_acc_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, xd, out, H, W, n);
   return launch_status("grr_bwd_unpool2_acc");
+}
+
+grr_status grr_interleave2x2(const float* t, float* gx, int B, int K, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(t && gx && t != gx && B > 0 && K > 0 && H > 1 && W > 1, GRR_ERR_INVALID_ARG,
+              "grr_interleave2x2: bad args");
+  GRR_REQUIRE(H % 2 == 0 && W % 4 == 0, GRR_ERR_SHAPE, "grr_interleave2x2: H even and W %% 4 == 0 required");
+  GRR_REQUIRE(((uintptr_t)t & 7) == 0 && ((uintptr_t)gx & 15) == 0, GRR_ERR_INVALID_ARG,
+              "grr_interleave2x2: t 8-byte / gx 16-byte alignment required");
+  const int64_t nq = (int64_t)B * K * H * (W / 4);
+  hipLaunchKernelGGL(interleave2x2_kernel, dim3(blocks_for(nq)), dim3(NT), 0, (hipStream_t)stream, t, gx, K, H, W, nq);
+  return launch_status("grr_interleave2x2");
 }
 
 grr_status grr_conv2x2s2_bwd_data(const float* g, const float* wt, float* gx, int B, int K, int M, int H, int W,

@@ -672,6 +672,20 @@ def bwd_unpool2_acc(xd: Tensor, out: Tensor) -> None:
             out.data_ptr(), b, c, h, w, _stream(dev))
 
 
+def conv2x2s2_bwd_data_gemm(g: Tensor, weight: Tensor, h: int, w: int) -> Tensor:
+    """Data gradient of nn.Conv2d(K, M, 2, stride=2): one split-bf16 1x1 GEMM with the 4K tap rows
+    W[m, k, di, dj] -> row (2 di + dj) K + k, then grr_interleave2x2 to full resolution."""
+    dev = _check("conv2x2s2_bwd_data", g, weight)
+    b, m = g.shape[:2]
+    k = weight.shape[1]
+    w4 = weight.permute(2, 3, 1, 0).reshape(4 * k, m, 1, 1).contiguous()
+    t = conv1x1(g, w4)
+    gx = torch.empty((b, k, h, w), dtype=torch.float32, device=dev)
+    _launch("interleave2x2", 8 * gx.numel(), "grr_interleave2x2", t.data_ptr(), gx.data_ptr(), b, k, h, w,
+            _stream(dev))
+    return gx
+
+
 def conv2x2s2_bwd_data(g: Tensor, weight: Tensor, h: int, w: int) -> Tensor:
     dev = _check("conv2x2s2_bwd_data", g, weight)
     b, m = g.shape[:2]

@@ -306,7 +306,13 @@ class Conv2x2s2Fn(torch.autograd.Function):
         g = g.contiguous()
         b, k, h, w = x.shape
         m = weight.shape[0]
-        gx = K.conv2x2s2_bwd_data(g, weight.contiguous(), h, w) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            # one 4K-row GEMM (split-bf16 for M <= 128, fp32 MFMA above) + interleave (W % 4 == 0)
+            if w % 4 == 0:
+                gx = K.conv2x2s2_bwd_data_gemm(g, weight.contiguous(), h, w)
+            else:
+                gx = K.conv2x2s2_bwd_data(g, weight.contiguous(), h, w)
         patches = x.reshape(b, k, h // 2, 2, w // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(b, -1, k * 4)
         gw = torch.matmul(g.reshape(b, m, -1), patches).sum(0)
         return gx, gw.view_as(weight)

@@ -305,6 +305,10 @@ grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, cons
                            int accumulate, int B, int G, int F, int H, int W, void* stream);
 /* out [B,C,H,W] += U(xd): 0.25 * xd(q/2) (conv_transpose2d of scaling_kernel01, REF:676-679). */
 grr_status grr_bwd_unpool2_acc(const float* xd, float* out, int B, int C, int H, int W, void* stream);
+/* gx[b,k,2i+di,2j+dj] = t[b,(2di+dj)K+k,i,j] (t [B,4K,H/2,W/2]): interleaves the four tap planes of
+ * the 2x2 stride-2 conv's data gradient (REF:593-602, computed as one 1x1 GEMM with 4K rows).
+ * H even, W % 4 == 0. */
+grr_status grr_interleave2x2(const float* t, float* gx, int B, int K, int H, int W, void* stream);
 /* Data gradient of grr_conv2x2s2: g [B,M,H/2,W/2], wt [M,K,2,2] -> gx [B,K,H,W]. */
 grr_status grr_conv2x2s2_bwd_data(const float* g, const float* wt, float* gx, int B, int K, int M, int H, int W,
                                   void* stream);

@@ -67,6 +67,7 @@ int main() {
   EXPECT_ERR(grr_bwd_cg_glue(n, n, n, n, n, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_unpool2_acc(n, n, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_conv2x2s2_bwd_data(n, n, n, 1, 4, 4, 8, 8, s));
+  EXPECT_ERR(grr_interleave2x2(n, n, 1, 4, 8, 8, s));
   EXPECT_ERR(grr_lnb_norm(n, n, n, n, 1, 4, 64, s));
   EXPECT_ERR(grr_lnb_norm_bwd(n, n, n, n, n, n, 1, 4, 64, s));
   EXPECT_ERR(grr_dwconv3(n, n, n, 1, 4, 8, 8, s));

@@ -125,11 +125,12 @@ def test_abstract_model_grad(irdu):
     check(m, lambda xd, p: O.abstract_forward(xd, p, ng, (1, 1, 1, 1), 1), x, tol=5e-4, loose=("gamma",))
 
 
-@pytest.mark.parametrize("bkm", [(2, 12, 24), (1, 96, 192)])
-def test_conv_grads(irdu, bkm):
+@pytest.mark.parametrize("hw", [(10, 14), (12, 16)])      # 2x2/s2 data gradient: direct kernel / GEMM + interleave
+@pytest.mark.parametrize("bkm", [(2, 12, 24), (1, 96, 192), (1, 24, 160)])
+def test_conv_grads(irdu, bkm, hw):
     b, k, m = bkm
     from irdu_amd import solver_grad as SG
-    x = rand(b, k, 10, 14, seed=3)
+    x = rand(b, k, *hw, seed=3)
     w1 = rand(m, k, 1, 1, seed=4) * 0.2
     w2 = rand(m, k, 2, 2, seed=5) * 0.2
     for fn, ref, w in ((SG.Conv1x1Fn.apply, torch.nn.functional.conv2d, w1),
