@@ -8,6 +8,6 @@ for r in 1 2; do
     tag=$(basename $lib .so)
     GRR_LIB=$lib timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary --breakdown "$@" \
       > gpurun_out/ab_$v/$tag.json 2> gpurun_out/ab_$v/$tag.err || exit 1
-    echo "$tag $(python -c "import json;d=json.loads(open('gpurun_out/ab_$v/$tag.json').read().strip().splitlines()[-1]);k=d['kernel_ms_per_step'];print(d['value'], d['ms_per_step'], {x: k[x] for x in ('lnb','conv1x1','system_step2','edge_weights')})")"
+    echo "$tag $(python -c "import json;d=json.loads(open('gpurun_out/ab_$v/$tag.json').read().strip().splitlines()[-1]);k=d['kernel_ms_per_step'];print(d['value'], d['ms_per_step'], {x: k[x] for x in ('lnb','conv1x1','system_step2','edge_weights') if x in k})")"
   done
 done
