@@ -203,6 +203,28 @@ __global__ __launch_bounds__(NT) void gate_kernel(const float* __restrict__ hp, 
   }
 }
 
+// Reverse of the gate with the skip scale folded in: ghp = scale * d(gate)/d(hp) . gq and
+// gdot += <gq, gate>, gq = W2^T gout (so that <gout, W2 gate> = <gq, gate> needs no W2 gate).
+// Grid-stride over all elements, one atomic per block.
+__global__ __launch_bounds__(NT) void gate_bwd_scaled_kernel(const float* __restrict__ hp, const float* __restrict__ gq,
+                                                             const float* __restrict__ scale, float* __restrict__ ghp,
+                                                             float* __restrict__ gdot, int hid, int64_t P, int64_t n) {
+  const float s = scale[0];
+  float dot = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int64_t b = i / ((int64_t)hid * P), rem = i - b * hid * P;
+    const int64_t om = b * 2 * hid * P + rem, ov = om + (int64_t)hid * P;
+    const float m = hp[om], v = hp[ov];
+    const float sg = 1.0f / (1.0f + expf(-m));
+    const float q = gq[i];
+    dot += q * ((sg * m) * v);
+    const float gg = s * q;
+    ghp[om] = gg * v * (sg + m * sg * (1.0f - sg));
+    ghp[ov] = gg * sg * m;
+  }
+  block_atomic_add(gdot, dot);
+}
+
 // ---------------------------------------------------------------------------
 // Row-streaming depthwise 3x3 (W <= 64 V, W % V == 0): one wave = one (b, channel) plane and a
 // segment of rows, lane = V adjacent columns; rows r-1, r, r+1 of the operands stay in
@@ -514,6 +536,18 @@ grr_status grr_dwconv3_bwd(const float* g, const float* h, const float* wdw, flo
   hipLaunchKernelGGL(dw3_wgrad_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * C), B * C), dim3(NT), 0,
                      (hipStream_t)stream, g, h, gwdw, C, H, W);
   return launch_status("grr_dwconv3_bwd/weight");
+}
+
+grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float* scale, float* ghp, float* gdot, int B,
+                                   int hid, int64_t P, void* stream) {
+  clear_error();
+  GRR_REQUIRE(hp && gq && scale && ghp && gdot && B > 0 && hid > 0 && P > 0, GRR_ERR_INVALID_ARG,
+              "grr_lnb_gate_bwd_scaled: bad args");
+  const int64_t n = (int64_t)B * hid * P;
+  const int grid = (int)std::min<int64_t>((n + NT - 1) / NT, 4096);
+  hipLaunchKernelGGL(gate_bwd_scaled_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, hp, gq, scale, ghp, gdot, hid,
+                     P, n);
+  return launch_status("grr_lnb_gate_bwd_scaled");
 }
 
 grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,

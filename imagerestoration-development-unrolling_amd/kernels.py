@@ -752,6 +752,19 @@ def dwconv3_bwd(g: Tensor, h: Tensor, wdw: Tensor, gwdw: Tensor) -> Tensor:
     return gh
 
 
+def lnb_gate_bwd_scaled(hp: Tensor, gq: Tensor, scale: Tensor, gdot: Tensor) -> Tensor:
+    """ghp = scale * (d gate / d hp) . gq;  gdot += <gq, gate>   (grr_lnb_gate_bwd_scaled)."""
+    dev = _check("lnb_gate_bwd_scaled", hp, gq, scale, gdot)
+    b, c2, h, w = hp.shape
+    hid = c2 // 2
+    if tuple(gq.shape) != (b, hid, h, w):
+        raise ValueError("lnb_gate_bwd_scaled: gq shape")
+    ghp = torch.empty_like(hp)
+    _launch("lnb_gate", 4 * hp.numel() * 2 + 4 * gq.numel(), "grr_lnb_gate_bwd_scaled", hp.data_ptr(), gq.data_ptr(),
+            scale.data_ptr(), ghp.data_ptr(), gdot.data_ptr(), b, hid, h * w, _stream(dev))
+    return ghp
+
+
 def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True):
     """gate = sigmoid(m) m v of hp = [m; v]; with ggate also the reverse ghp.  Returns (gate, ghp)."""
     dev = _check("lnb_gate", hp, ggate)

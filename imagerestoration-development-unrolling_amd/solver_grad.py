@@ -595,17 +595,16 @@ class LNBFn(torch.autograd.Function):
         hh = K.conv1x1(n, W1.view(hid2, c, 1, 1))
         hp = K.dwconv3(hh, Wdw)
         gate, _ = K.lnb_gate(hp)
-        o = K.conv1x1(gate, W2.view(c, hid, 1, 1))
         gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
         K.bwd_graph_dot(gout, x, gskip[0:1], 1)
-        K.bwd_graph_dot(gout, o, gskip[1:2], 1)
-        del o
-        go = K.bwd_lincomb(gout, skip[1:2].contiguous(), None, None, 1)          # s1 * gout
-        gw2 = torch.matmul(go.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0)
-        ggate = K.conv1x1(go, W2.t().contiguous().view(hid, c, 1, 1))
-        del go, gate
-        _, ghp = K.lnb_gate(hp, ggate, want_gate=False)
-        del hp, ggate
+        s1 = skip[1:2].contiguous()
+        # gw2 = s1 gout gate^T; gq = W2^T gout: the gate reverse takes s1 and returns
+        # <gout, W2 gate> = <gq, gate> for the skip weight (no recomputed W2 gate)
+        gw2 = torch.matmul(gout.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0) * s1
+        del gate
+        gq = K.conv1x1(gout, W2.t().contiguous().view(hid, c, 1, 1))
+        ghp = K.lnb_gate_bwd_scaled(hp, gq, s1, gskip[1:2])
+        del hp, gq
         gwdw = torch.zeros_like(Wdw)
         gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
         del ghp, hh

@@ -328,6 +328,11 @@ grr_status grr_dwconv3_bwd(const float* g, const float* h, const float* wdw, flo
 /* gate = sigmoid(m) m v of hp = [m; v] [B,2hid,P] (if gate); ghp from ggate (if ggate) (REF:941-947). */
 grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,
                         void* stream);
+/* the gate's reverse with the skip scale folded in (autograd of REF:941-947, :962-964):
+ * ghp = scale[0] * (d gate / d hp) . gq and gdot[0] += <gq, gate>, gq = W2^T gout — so the skip
+ * weight's gradient <gout, W2 gate> needs no recomputed W2 gate. */
+grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float* scale, float* ghp, float* gdot, int B,
+                                   int hid, int64_t P, void* stream);
 
 /* ---- window graphs (older image-domain models) ------------------------------
  * REF7 = exploration/model_multiscale_mixture_GLR/lib/model_GLR_GTV_deep_v7.py,
