@@ -433,6 +433,148 @@ __global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict
   }
 }
 
+// The gate's reverse and the depthwise reverse in one row pass (LocalNonLinearBlock reverse,
+// REF:934-947): one wave = one hidden channel pair (mask plane j, value plane hid + j) of one
+// image and a segment of rows.  The ghp rows are formed in registers from hp = [m; v] and
+// gq = W2^T gout as the rows arrive (ghp_m = s gq v (sg + m sg (1 - sg)), ghp_v = s gq sg m,
+// sg = sigmoid(m)), so ghp never reaches HBM; <gq, gate> is accumulated for the skip weight
+// (rows of the wave's own segment only); then, per plane, the depthwise data adjoint and weight
+// gradient of dw3_row_bwd_kernel with the same expressions.
+template <int V>
+__global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
+    const float* __restrict__ hp, const float* __restrict__ gq, const float* __restrict__ scale,
+    const float* __restrict__ hh, const float* __restrict__ wdw, float* __restrict__ gh, float* __restrict__ gw,
+    float* __restrict__ gdot, int hid, int H, int W, int sseg, int nsegs, uint32_t nwaves) {
+  Dw3RowGeom q;
+  if (!dw3_row_geom<V>(q, hid, H, W, sseg, nsegs, nwaves)) return;   // q.plane = b hid + j, q.c = j
+  const int64_t HW = (int64_t)H * W;
+  const int64_t bq = q.plane / hid, j = q.c;
+  const int64_t pm = (bq * 2 * hid + j) * HW + q.cl0, pv = pm + (int64_t)hid * HW;
+  const float* mp = hp + pm;
+  const float* vp = hp + pv;
+  const float* qp = gq + q.plane * HW + q.cl0;
+  const float* hmp = hh + pm;
+  const float* hvp = hh + pv;
+  const float s = scale[0];
+  float wm[9], wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wm[t] = wdw[j * 9 + t];
+    wv[t] = wdw[(hid + j) * 9 + t];
+  }
+  float accm[9], accv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) accm[t] = accv[t] = 0.f;
+  float dot = 0.f;
+  // ghp rows r-1, r, r+1 of both planes (zero outside the image), hh rows clamped
+  float Gm[3][V], Gv[3][V], Hm[3][V], Hv[3][V];
+  float NM[V], NV[V], NQ[V], NHm[V], NHv[V];
+  auto raw_load = [&](int rr) {   // operands of ghp row rr (clamped; rows outside give ghp 0)
+    const int64_t o = (int64_t)clampi(rr, 0, H - 1) * W;
+    row_load<V>(NM, mp + o);
+    row_load<V>(NV, vp + o);
+    row_load<V>(NQ, qp + o);
+  };
+  auto ghp_row = [&](int rr, float (&dm)[V], float (&dv)[V]) {
+    const bool in = rr >= 0 && rr < H;
+    const bool own = q.on && rr >= q.r0 && rr < q.r1;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float m = NM[k], v = NV[k], g = NQ[k];
+      const float sg = 1.0f / (1.0f + expf(-m));
+      if (own) dot += g * ((sg * m) * v);
+      const float gg = s * g;
+      dm[k] = in ? gg * v * (sg + m * sg * (1.0f - sg)) : 0.f;
+      dv[k] = in ? gg * sg * m : 0.f;
+    }
+  };
+  raw_load(q.r0 - 1);
+  ghp_row(q.r0 - 1, Gm[0], Gv[0]);
+  raw_load(q.r0);
+  ghp_row(q.r0, Gm[1], Gv[1]);
+  raw_load(q.r0 + 1);
+  row_load<V>(Hm[0], hmp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load<V>(Hv[0], hvp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load<V>(Hm[1], hmp + (int64_t)q.r0 * W);
+  row_load<V>(Hv[1], hvp + (int64_t)q.r0 * W);
+  row_load<V>(NHm, hmp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  row_load<V>(NHv, hvp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  // one plane's data adjoint (row r) and weight-gradient contribution
+  auto plane = [&](const float (&G)[3][V], const float (&Hp)[3][V], const float (&wt)[9], float (&acc)[9], int r,
+                   float* dst) {
+    float A[3][V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      A[0][k] = r == 0 ? G[2][k] + G[1][k] : G[2][k];
+      A[1][k] = G[1][k];
+      A[2][k] = r == H - 1 ? G[0][k] + G[1][k] : G[0][k];
+    }
+    float o[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float pvv = dpp_prev(A[dy][V - 1]), nx = dpp_next(A[dy][0]);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const int col = q.c0 + k;
+        const float a = A[dy][k];
+        const float al = k > 0 ? A[dy][k - 1] : pvv;
+        const float ar = k < V - 1 ? A[dy][k + 1] : nx;
+        const float sm = col + 1 < W ? (col == 0 ? ar + a : ar) : (col == 0 ? a : 0.f);
+        const float sp = col >= 1 ? (col == W - 1 ? al + a : al) : (col == W - 1 ? a : 0.f);
+        o[k] += wt[dy * 3 + 0] * sm;
+        o[k] += wt[dy * 3 + 1] * a;
+        o[k] += wt[dy * 3 + 2] * sp;
+      }
+    }
+    if (q.on) row_store<V>(dst + (int64_t)r * W, o);
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float pvv = dpp_prev(Hp[dy][V - 1]), nx = dpp_next(Hp[dy][0]);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const int col = q.c0 + k;
+        const float gv = q.on ? G[1][k] : 0.f;
+        const float l = col > 0 ? (k > 0 ? Hp[dy][k - 1] : pvv) : Hp[dy][k];
+        const float rr = col < W - 1 ? (k < V - 1 ? Hp[dy][k + 1] : nx) : Hp[dy][k];
+        acc[dy * 3 + 0] += gv * l;
+        acc[dy * 3 + 1] += gv * Hp[dy][k];
+        acc[dy * 3 + 2] += gv * rr;
+      }
+    }
+  };
+  float* const ghm = gh + pm;
+  float* const ghv = gh + pv;
+  for (int r = q.r0; r < q.r1; ++r) {
+    ghp_row(r + 1, Gm[2], Gv[2]);
+#pragma unroll
+    for (int k = 0; k < V; ++k) { Hm[2][k] = NHm[k]; Hv[2][k] = NHv[k]; }
+    raw_load(r + 2);
+    row_load<V>(NHm, hmp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    row_load<V>(NHv, hvp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    plane(Gm, Hm, wm, accm, r, ghm);
+    plane(Gv, Hv, wv, accv, r, ghv);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      Gm[0][k] = Gm[1][k]; Gm[1][k] = Gm[2][k];
+      Gv[0][k] = Gv[1][k]; Gv[1][k] = Gv[2][k];
+      Hm[0][k] = Hm[1][k]; Hm[1][k] = Hm[2][k];
+      Hv[0][k] = Hv[1][k]; Hv[1][k] = Hv[2][k];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const float a = wave_sum(accm[t]), b = wave_sum(accv[t]);
+    if (q.lane == 0) {
+      if (a != 0.f) atomicAdd(gw + j * 9 + t, a);
+      if (b != 0.f) atomicAdd(gw + (hid + j) * 9 + t, b);
+    }
+  }
+  const float d = wave_sum(dot);
+  if (q.lane == 0 && d != 0.f) atomicAdd(gdot, d);
+}
+
 // V for the row kernels (0: not applicable -> per-pixel kernels)
 int dw3_row_vec(int W) {
   if (W <= 64) return 1;
@@ -472,6 +614,17 @@ bool dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* 
     case 4: launch_dw3_row<4>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
     default: return false;
   }
+}
+
+template <int V>
+void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, const float* hh, const float* wdw,
+                         float* gh, float* gw, float* gdot, int B, int hid, int H, int W, hipStream_t s) {
+  const int64_t planes = (int64_t)B * hid;
+  const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
+  const uint32_t nwaves = (uint32_t)(planes * nsegs);
+  const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+  hipLaunchKernelGGL(dw3_gate_row_bwd_kernel<V>, grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot, hid, H, W,
+                     sseg, nsegs, nwaves);
 }
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
@@ -548,6 +701,27 @@ grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float
   hipLaunchKernelGGL(gate_bwd_scaled_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, hp, gq, scale, ghp, gdot, hid,
                      P, n);
   return launch_status("grr_lnb_gate_bwd_scaled");
+}
+
+grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* scale, const float* hh,
+                                const float* wdw, float* gh, float* gwdw, float* gdot, int B, int hid, int H, int W,
+                                void* stream) {
+  clear_error();
+  GRR_REQUIRE(hp && gq && scale && hh && wdw && gh && gwdw && gdot && B > 0 && hid > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_lnb_gate_dw3_bwd: bad args");
+  const int V = dw3_row_vec(W);
+  const void* ptrs[] = {hp, gq, hh, gh};
+  bool aligned = true;
+  for (const void* p : ptrs) aligned = aligned && (uintptr_t)p % (4u * (V > 0 ? V : 1)) == 0;
+  GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_gate_dw3_bwd: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  hipStream_t s = (hipStream_t)stream;
+  switch (V) {
+    case 1: launch_dw3_gate_row<1>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+    case 2: launch_dw3_gate_row<2>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+    default: launch_dw3_gate_row<4>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+  }
+  return launch_status("grr_lnb_gate_dw3_bwd");
 }
 
 grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,

@@ -765,6 +765,24 @@ def lnb_gate_bwd_scaled(hp: Tensor, gq: Tensor, scale: Tensor, gdot: Tensor) -> 
     return ghp
 
 
+def lnb_gate_dw3_ok(h: int, w: int) -> bool:
+    return (w <= 64) or (w <= 128 and w % 2 == 0) or (w <= 256 and w % 4 == 0)
+
+
+def lnb_gate_dw3_bwd(hp: Tensor, gq: Tensor, scale: Tensor, hh: Tensor, wdw: Tensor, gwdw: Tensor,
+                     gdot: Tensor) -> Tensor:
+    """Gate reverse + depthwise reverse in one row pass (grr_lnb_gate_dw3_bwd): returns gh."""
+    dev = _check("lnb_gate_dw3_bwd", hp, gq, scale, hh, wdw, gwdw, gdot)
+    b, c2, h, w = hp.shape
+    if hh.shape != hp.shape or tuple(gq.shape) != (b, c2 // 2, h, w):
+        raise ValueError("lnb_gate_dw3_bwd: shapes")
+    gh = torch.empty_like(hh)
+    _launch("lnb_gate_dw3_bwd", 4 * (hp.numel() + gq.numel() + hh.numel() + gh.numel()), "grr_lnb_gate_dw3_bwd",
+            hp.data_ptr(), gq.data_ptr(), scale.data_ptr(), hh.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
+            gwdw.data_ptr(), gdot.data_ptr(), b, c2 // 2, h, w, _stream(dev))
+    return gh
+
+
 def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True):
     """gate = sigmoid(m) m v of hp = [m; v]; with ggate also the reverse ghp.  Returns (gate, ghp)."""
     dev = _check("lnb_gate", hp, ggate)

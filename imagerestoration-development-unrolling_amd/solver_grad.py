@@ -49,6 +49,7 @@ def solver_params(mod) -> List[Tensor]:
     return out
 
 
+FUSED_GATE_DW3 = True   # LNB reverse: gate + depthwise reverse in one row pass (False: two kernels; tests)
 FUSED = True   # one-pass term reverses (grr_bwd_term_fused) where F has an instance; False: 5-pass path
 
 
@@ -603,11 +604,15 @@ class LNBFn(torch.autograd.Function):
         gw2 = torch.matmul(gout.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0) * s1
         del gate
         gq = K.conv1x1(gout, W2.t().contiguous().view(hid, c, 1, 1))
-        ghp = K.lnb_gate_bwd_scaled(hp, gq, s1, gskip[1:2])
-        del hp, gq
         gwdw = torch.zeros_like(Wdw)
-        gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
-        del ghp, hh
+        if FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w):   # ghp formed in registers, never in HBM
+            gh = K.lnb_gate_dw3_bwd(hp, gq, s1, hh, Wdw, gwdw, gskip[1:2])
+            del hp, gq, hh
+        else:
+            ghp = K.lnb_gate_bwd_scaled(hp, gq, s1, gskip[1:2])
+            del hp, gq
+            gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
+            del ghp, hh
         gw1 = torch.matmul(gh.reshape(b, hid2, -1), n.reshape(b, c, -1).transpose(1, 2)).sum(0)
         gn = K.conv1x1(gh, W1.t().contiguous().view(c, hid2, 1, 1))
         del gh, n

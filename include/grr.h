@@ -333,6 +333,13 @@ grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float*
  * weight's gradient <gout, W2 gate> needs no recomputed W2 gate. */
 grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float* scale, float* ghp, float* gdot, int B,
                                    int hid, int64_t P, void* stream);
+/* grr_lnb_gate_bwd_scaled and grr_dwconv3_bwd in one row pass (ghp stays on chip): hp [B,2hid,H,W]
+ * (depthwise output), gq [B,hid,H,W], hh [B,2hid,H,W] (depthwise input), wdw [2hid,9] ->
+ * gh [B,2hid,H,W]; gwdw [2hid,9] += ; gdot[0] += <gq, gate>.  W <= 256 with W % V == 0
+ * (V = 1 / 2 / 4 for W <= 64 / 128 / 256), else GRR_ERR_UNSUPPORTED. */
+grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* scale, const float* hh,
+                                const float* wdw, float* gh, float* gwdw, float* gdot, int B, int hid, int H, int W,
+                                void* stream);
 
 /* ---- window graphs (older image-domain models) ------------------------------
  * REF7 = exploration/model_multiscale_mixture_GLR/lib/model_GLR_GTV_deep_v7.py,

@@ -164,9 +164,14 @@ def test_training_step_reduces_loss(irdu):
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 20, 24), (33, 20, 9, 44), (160, 64, 8, 12)])
-def test_local_nonlinear_block_grad(irdu, chw):
-    """LocalNonLinearBlock reverse on HIP (LN, W1, depthwise 3x3, gate, W2, skip) vs fp64 oracle."""
+@pytest.mark.parametrize("fused", [True, False])   # gate + depthwise reverse in one row pass / two kernels
+@pytest.mark.parametrize("chw", [(12, 32, 16, 16), (96, 256, 20, 24), (33, 20, 9, 44), (160, 64, 8, 12),
+                                 (8, 16, 6, 100), (8, 16, 5, 200), (8, 12, 4, 300)])
+def test_local_nonlinear_block_grad(irdu, chw, fused):
+    """LocalNonLinearBlock reverse on HIP (LN, W1, depthwise 3x3, gate, W2, skip) vs fp64 oracle;
+    W = 100 / 200 run the fused gate-depthwise row kernel at V = 2 / 4, W = 300 the two kernels."""
+    from irdu_amd import solver_grad as SG
+    SG.FUSED_GATE_DW3 = fused
     c, hid, h, w = chw
     torch.manual_seed(31)
     blk = irdu.LocalNonLinearBlock(c, hid, 1)
@@ -174,4 +179,7 @@ def test_local_nonlinear_block_grad(irdu, chw):
         blk.norm.weighted_transform.weight.mul_(1 + 0.2 * torch.randn_like(blk.norm.weighted_transform.weight))
         blk.skip_weight.copy_(torch.tensor([0.7, 1.3]))
     x = rand(2, c, h, w, seed=32)
-    check(blk, lambda xd, p: O.local_nonlinear_block(xd, p, ""), x)
+    try:
+        check(blk, lambda xd, p: O.local_nonlinear_block(xd, p, ""), x)
+    finally:
+        SG.FUSED_GATE_DW3 = True
