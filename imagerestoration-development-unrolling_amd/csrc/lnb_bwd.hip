@@ -433,6 +433,81 @@ __global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict
   }
 }
 
+// one depthwise output row from input rows r-1, r, r+1 (R[0..2], replicate-clamped by the
+// caller): the expressions and order of dw3_row_fwd_kernel
+template <int V>
+__device__ __forceinline__ void dw3_row_out(const float (&R0)[V], const float (&R1)[V], const float (&R2)[V],
+                                            const float (&wt)[9], int c0, int W, float (&o)[V]) {
+  const float* Rs[3] = {R0, R1, R2};
+#pragma unroll
+  for (int k = 0; k < V; ++k) o[k] = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const float* R = Rs[dy];
+    const float pv = dpp_prev(R[V - 1]), nx = dpp_next(R[0]);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const int col = c0 + k;
+      const float l = col > 0 ? (k > 0 ? R[k - 1] : pv) : R[k];
+      const float rr = col < W - 1 ? (k < V - 1 ? R[k + 1] : nx) : R[k];
+      o[k] += wt[dy * 3 + 0] * l;
+      o[k] += wt[dy * 3 + 1] * R[k];
+      o[k] += wt[dy * 3 + 2] * rr;
+    }
+  }
+}
+
+// depthwise 3x3 + gate in one row pass: gate = sigmoid(m) m v of (m, v) = dw3(hh)[j], [hid + j];
+// one wave = one channel pair of one image and a segment of rows (the depthwise output is not
+// written: the reverse recomputes it from hh)
+template <int V>
+__global__ __launch_bounds__(NT) void dw3_gate_row_fwd_kernel(const float* __restrict__ hh,
+                                                              const float* __restrict__ wdw, float* __restrict__ gate,
+                                                              int hid, int H, int W, int sseg, int nsegs,
+                                                              uint32_t nwaves) {
+  Dw3RowGeom q;
+  if (!dw3_row_geom<V>(q, hid, H, W, sseg, nsegs, nwaves)) return;
+  const int64_t HW = (int64_t)H * W;
+  const int64_t bq = q.plane / hid, j = q.c;
+  const int64_t pm = (bq * 2 * hid + j) * HW + q.cl0, pv = pm + (int64_t)hid * HW;
+  const float* hmp = hh + pm;
+  const float* hvp = hh + pv;
+  float* gp = gate + q.plane * HW + q.cl0;
+  float wm[9], wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wm[t] = wdw[j * 9 + t];
+    wv[t] = wdw[(hid + j) * 9 + t];
+  }
+  float Rm[3][V], Rv[3][V], Nm[V], Nv[V];
+  row_load<V>(Rm[0], hmp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load<V>(Rv[0], hvp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load<V>(Rm[1], hmp + (int64_t)q.r0 * W);
+  row_load<V>(Rv[1], hvp + (int64_t)q.r0 * W);
+  row_load<V>(Nm, hmp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  row_load<V>(Nv, hvp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  for (int r = q.r0; r < q.r1; ++r) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) { Rm[2][k] = Nm[k]; Rv[2][k] = Nv[k]; }
+    row_load<V>(Nm, hmp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    row_load<V>(Nv, hvp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    float m[V], v[V], o[V];
+    dw3_row_out<V>(Rm[0], Rm[1], Rm[2], wm, q.c0, W, m);
+    dw3_row_out<V>(Rv[0], Rv[1], Rv[2], wv, q.c0, W, v);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float sg = 1.0f / (1.0f + expf(-m[k]));
+      o[k] = (sg * m[k]) * v[k];
+    }
+    if (q.on) row_store<V>(gp + (int64_t)r * W, o);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      Rm[0][k] = Rm[1][k]; Rm[1][k] = Rm[2][k];
+      Rv[0][k] = Rv[1][k]; Rv[1][k] = Rv[2][k];
+    }
+  }
+}
+
 // The gate's reverse and the depthwise reverse in one row pass (LocalNonLinearBlock reverse,
 // REF:934-947): one wave = one hidden channel pair (mask plane j, value plane hid + j) of one
 // image and a segment of rows.  The ghp rows are formed in registers from hp = [m; v] and
@@ -440,9 +515,9 @@ __global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict
 // sg = sigmoid(m)), so ghp never reaches HBM; <gq, gate> is accumulated for the skip weight
 // (rows of the wave's own segment only); then, per plane, the depthwise data adjoint and weight
 // gradient of dw3_row_bwd_kernel with the same expressions.
-template <int V>
+template <int V, bool REC>
 __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
-    const float* __restrict__ hp, const float* __restrict__ gq, const float* __restrict__ scale,
+    const float* hp, const float* __restrict__ gq, const float* __restrict__ scale,
     const float* __restrict__ hh, const float* __restrict__ wdw, float* __restrict__ gh, float* __restrict__ gw,
     float* __restrict__ gdot, int hid, int H, int W, int sseg, int nsegs, uint32_t nwaves) {
   Dw3RowGeom q;
@@ -450,8 +525,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
   const int64_t HW = (int64_t)H * W;
   const int64_t bq = q.plane / hid, j = q.c;
   const int64_t pm = (bq * 2 * hid + j) * HW + q.cl0, pv = pm + (int64_t)hid * HW;
-  const float* mp = hp + pm;
-  const float* vp = hp + pv;
+  const float* mp = hp ? hp + pm : nullptr;
+  const float* vp = hp ? hp + pv : nullptr;
   const float* qp = gq + q.plane * HW + q.cl0;
   const float* hmp = hh + pm;
   const float* hvp = hh + pv;
@@ -469,11 +544,45 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
   // ghp rows r-1, r, r+1 of both planes (zero outside the image), hh rows clamped
   float Gm[3][V], Gv[3][V], Hm[3][V], Hv[3][V];
   float NM[V], NV[V], NQ[V], NHm[V], NHv[V];
+  // hp == nullptr: the depthwise output rows are recomputed from hh rows (ring X*: rows
+  // rr-1, rr, rr+1 of the row rr being formed), so hp never has to be stored
+  constexpr bool rec = REC;   // hp not given
+  float Xm[3][V], Xv[3][V];
+  if constexpr (REC) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) Xm[0][k] = Xv[0][k] = Xm[1][k] = Xv[1][k] = 0.f;
+  }
+  int xrow = INT32_MIN;   // hh row held in X*[2] (rows xrow-2, xrow-1, xrow in X*[0..2])
   auto raw_load = [&](int rr) {   // operands of ghp row rr (clamped; rows outside give ghp 0)
     const int64_t o = (int64_t)clampi(rr, 0, H - 1) * W;
-    row_load<V>(NM, mp + o);
-    row_load<V>(NV, vp + o);
     row_load<V>(NQ, qp + o);
+    if constexpr (!REC) {
+      row_load<V>(NM, mp + o);
+      row_load<V>(NV, vp + o);
+      return;
+    }
+    // hh rows up to rr + 1 into the ring (rows are consecutive after the first call)
+    const int want = rr + 1;
+    if (xrow == INT32_MIN) {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int64_t oo = (int64_t)clampi(want - 2 + d, 0, H - 1) * W;
+        row_load<V>(Xm[d], hmp + oo);
+        row_load<V>(Xv[d], hvp + oo);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        Xm[0][k] = Xm[1][k]; Xm[1][k] = Xm[2][k];
+        Xv[0][k] = Xv[1][k]; Xv[1][k] = Xv[2][k];
+      }
+      const int64_t oo = (int64_t)clampi(want, 0, H - 1) * W;
+      row_load<V>(Xm[2], hmp + oo);
+      row_load<V>(Xv[2], hvp + oo);
+    }
+    xrow = want;
+    dw3_row_out<V>(Xm[0], Xm[1], Xm[2], wm, q.c0, W, NM);
+    dw3_row_out<V>(Xv[0], Xv[1], Xv[2], wv, q.c0, W, NV);
   };
   auto ghp_row = [&](int rr, float (&dm)[V], float (&dv)[V]) {
     const bool in = rr >= 0 && rr < H;
@@ -623,8 +732,22 @@ void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, c
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
-  hipLaunchKernelGGL(dw3_gate_row_bwd_kernel<V>, grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot, hid, H, W,
-                     sseg, nsegs, nwaves);
+  if (hp)
+    hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, false>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot,
+                       hid, H, W, sseg, nsegs, nwaves);
+  else
+    hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, true>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot,
+                       hid, H, W, sseg, nsegs, nwaves);
+}
+
+template <int V>
+void launch_dw3_gate_fwd_row(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
+                             hipStream_t s) {
+  const int64_t planes = (int64_t)B * hid;
+  const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
+  const uint32_t nwaves = (uint32_t)(planes * nsegs);
+  const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+  hipLaunchKernelGGL(dw3_gate_row_fwd_kernel<V>, grid, dim3(NT), 0, s, hh, wdw, gate, hid, H, W, sseg, nsegs, nwaves);
 }
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
@@ -703,16 +826,34 @@ grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float
   return launch_status("grr_lnb_gate_bwd_scaled");
 }
 
+grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
+                            void* stream) {
+  clear_error();
+  GRR_REQUIRE(hh && wdw && gate && B > 0 && hid > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
+              "grr_lnb_dw3_gate: bad args");
+  const int V = dw3_row_vec(W);
+  const bool aligned = V > 0 && (uintptr_t)hh % (4u * V) == 0 && (uintptr_t)gate % (4u * V) == 0;
+  GRR_REQUIRE(aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_dw3_gate: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  hipStream_t s = (hipStream_t)stream;
+  switch (V) {
+    case 1: launch_dw3_gate_fwd_row<1>(hh, wdw, gate, B, hid, H, W, s); break;
+    case 2: launch_dw3_gate_fwd_row<2>(hh, wdw, gate, B, hid, H, W, s); break;
+    default: launch_dw3_gate_fwd_row<4>(hh, wdw, gate, B, hid, H, W, s); break;
+  }
+  return launch_status("grr_lnb_dw3_gate");
+}
+
 grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* scale, const float* hh,
                                 const float* wdw, float* gh, float* gwdw, float* gdot, int B, int hid, int H, int W,
                                 void* stream) {
   clear_error();
-  GRR_REQUIRE(hp && gq && scale && hh && wdw && gh && gwdw && gdot && B > 0 && hid > 0 && H > 0 && W > 0,
+  GRR_REQUIRE(gq && scale && hh && wdw && gh && gwdw && gdot && B > 0 && hid > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_lnb_gate_dw3_bwd: bad args");
   const int V = dw3_row_vec(W);
   const void* ptrs[] = {hp, gq, hh, gh};
   bool aligned = true;
-  for (const void* p : ptrs) aligned = aligned && (uintptr_t)p % (4u * (V > 0 ? V : 1)) == 0;
+  for (const void* p : ptrs) aligned = aligned && (uintptr_t)p % (4u * (V > 0 ? V : 1)) == 0;   // NULL hp passes
   GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_lnb_gate_dw3_bwd: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;

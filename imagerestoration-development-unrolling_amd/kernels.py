@@ -769,18 +769,30 @@ def lnb_gate_dw3_ok(h: int, w: int) -> bool:
     return (w <= 64) or (w <= 128 and w % 2 == 0) or (w <= 256 and w % 4 == 0)
 
 
-def lnb_gate_dw3_bwd(hp: Tensor, gq: Tensor, scale: Tensor, hh: Tensor, wdw: Tensor, gwdw: Tensor,
+def lnb_gate_dw3_bwd(hp: Optional[Tensor], gq: Tensor, scale: Tensor, hh: Tensor, wdw: Tensor, gwdw: Tensor,
                      gdot: Tensor) -> Tensor:
-    """Gate reverse + depthwise reverse in one row pass (grr_lnb_gate_dw3_bwd): returns gh."""
+    """Gate reverse + depthwise reverse in one row pass (grr_lnb_gate_dw3_bwd): returns gh.
+    hp None: the depthwise output is recomputed from hh in-kernel."""
     dev = _check("lnb_gate_dw3_bwd", hp, gq, scale, hh, wdw, gwdw, gdot)
-    b, c2, h, w = hp.shape
-    if hh.shape != hp.shape or tuple(gq.shape) != (b, c2 // 2, h, w):
+    b, c2, h, w = hh.shape
+    if (hp is not None and hp.shape != hh.shape) or tuple(gq.shape) != (b, c2 // 2, h, w):
         raise ValueError("lnb_gate_dw3_bwd: shapes")
     gh = torch.empty_like(hh)
-    _launch("lnb_gate_dw3_bwd", 4 * (hp.numel() + gq.numel() + hh.numel() + gh.numel()), "grr_lnb_gate_dw3_bwd",
-            hp.data_ptr(), gq.data_ptr(), scale.data_ptr(), hh.data_ptr(), wdw.data_ptr(), gh.data_ptr(),
-            gwdw.data_ptr(), gdot.data_ptr(), b, c2 // 2, h, w, _stream(dev))
+    nbytes = 4 * ((hp.numel() if hp is not None else 0) + gq.numel() + hh.numel() + gh.numel())
+    _launch("lnb_gate_dw3_bwd", nbytes, "grr_lnb_gate_dw3_bwd", _ptr(hp), gq.data_ptr(), scale.data_ptr(),
+            hh.data_ptr(), wdw.data_ptr(), gh.data_ptr(), gwdw.data_ptr(), gdot.data_ptr(), b, c2 // 2, h, w,
+            _stream(dev))
     return gh
+
+
+def lnb_dw3_gate(hh: Tensor, wdw: Tensor) -> Tensor:
+    """gate = sigmoid(m) m v of (m, v) = dwconv3(hh), the depthwise output not stored (grr_lnb_dw3_gate)."""
+    dev = _check("lnb_dw3_gate", hh, wdw)
+    b, c2, h, w = hh.shape
+    gate = torch.empty((b, c2 // 2, h, w), dtype=torch.float32, device=dev)
+    _launch("lnb_dw3_gate", 4 * (hh.numel() + gate.numel()), "grr_lnb_dw3_gate", hh.data_ptr(), wdw.data_ptr(),
+            gate.data_ptr(), b, c2 // 2, h, w, _stream(dev))
+    return gate
 
 
 def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True):

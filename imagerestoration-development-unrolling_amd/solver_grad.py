@@ -594,8 +594,15 @@ class LNBFn(torch.autograd.Function):
             _mat(w2, c).contiguous()
         n, isd = K.lnb_norm(x, lnw)
         hh = K.conv1x1(n, W1.view(hid2, c, 1, 1))
-        hp = K.dwconv3(hh, Wdw)
-        gate, _ = K.lnb_gate(hp)
+        # row-kernel widths: the depthwise output hp is never stored (gate from hh in one pass, the
+        # reverse recomputes hp from hh); else the per-stage kernels
+        rows = FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w)
+        if rows:
+            hp = None
+            gate = K.lnb_dw3_gate(hh, Wdw)
+        else:
+            hp = K.dwconv3(hh, Wdw)
+            gate, _ = K.lnb_gate(hp)
         gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
         K.bwd_graph_dot(gout, x, gskip[0:1], 1)
         s1 = skip[1:2].contiguous()
@@ -605,8 +612,8 @@ class LNBFn(torch.autograd.Function):
         del gate
         gq = K.conv1x1(gout, W2.t().contiguous().view(hid, c, 1, 1))
         gwdw = torch.zeros_like(Wdw)
-        if FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w):   # ghp formed in registers, never in HBM
-            gh = K.lnb_gate_dw3_bwd(hp, gq, s1, hh, Wdw, gwdw, gskip[1:2])
+        if rows:                                        # ghp formed in registers, never in HBM
+            gh = K.lnb_gate_dw3_bwd(None, gq, s1, hh, Wdw, gwdw, gskip[1:2])
             del hp, gq, hh
         else:
             ghp = K.lnb_gate_bwd_scaled(hp, gq, s1, gskip[1:2])

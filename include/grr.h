@@ -333,8 +333,13 @@ grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float*
  * weight's gradient <gout, W2 gate> needs no recomputed W2 gate. */
 grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float* scale, float* ghp, float* gdot, int B,
                                    int hid, int64_t P, void* stream);
+/* depthwise 3x3 + gate in one row pass: gate [B,hid,H,W] = sigmoid(m) m v of (m, v) = dw3(hh) (the
+ * depthwise output itself is not stored).  W <= 256 with W % V == 0, else GRR_ERR_UNSUPPORTED. */
+grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
+                            void* stream);
 /* grr_lnb_gate_bwd_scaled and grr_dwconv3_bwd in one row pass (ghp stays on chip): hp [B,2hid,H,W]
- * (depthwise output), gq [B,hid,H,W], hh [B,2hid,H,W] (depthwise input), wdw [2hid,9] ->
+ * (depthwise output; NULL = recomputed from hh in-kernel), gq [B,hid,H,W], hh [B,2hid,H,W]
+ * (depthwise input), wdw [2hid,9] ->
  * gh [B,2hid,H,W]; gwdw [2hid,9] += ; gdot[0] += <gq, gate>.  W <= 256 with W % V == 0
  * (V = 1 / 2 / 4 for W <= 64 / 128 / 256), else GRR_ERR_UNSUPPORTED. */
 grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* scale, const float* hh,
