@@ -1490,8 +1490,17 @@ constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW + S2_FMAX * (S2_XR * S2
 constexpr int S2_NT = GRR_STEP2_NT ? 2 : 0;   // cache policy of step2's read-once / write-once streams
 constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipelines' slot period)
 static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
+// GRR_STEP2_SPLIT: stage A and stage B of a channel run in two waves (waves S2_FMAX + 1 + f and f),
+// the producer is wave S2_FMAX: 7 waves, the two waves of channel f share one SIMD, so each SIMD
+// issues its vector work from two waves (a lone wave issues at half the VALU rate; the kernel is
+// VALU-bound at one wave per SIMD).  Everything the stages exchange already goes through the LDS
+// rings (x_{k+1}, u_{k+1}, D x_{k+1}), written at least one barrier before it is read.
+#ifndef GRR_STEP2_SPLIT
+#define GRR_STEP2_SPLIT 1
+#endif
+constexpr int S2_THREADS = GRR_STEP2_SPLIT ? 64 * (2 * S2_FMAX + 1) : NT;
 
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ __launch_bounds__(S2_THREADS) __attribute__((amdgpu_waves_per_eu(GRR_STEP2_SPLIT ? 2 : 1, GRR_STEP2_SPLIT ? 2 : 1)))
 void graph_step2_kernel(Step2Args a) {
   constexpr int V = 4, VH = 2, W = S2_W, hw = S2_HW;
   typedef typename VecT<4>::type F4;
@@ -1516,8 +1525,13 @@ void graph_step2_kernel(Step2Args a) {
   const int ts = r0 - 9;                 // first step (odd offset from r0: step t emits stage-A row t-3)
   const int NI0 = (r1 + 11 - ts) / 2;    // stage B emits rows up to r1 - 1
   const int NI = (NI0 + S2_UNROLL - 1) / S2_UNROLL * S2_UNROLL;   // extra iterations store nothing
+  // Split waves: in the iteration where stage A pools half row 0 (t = 3, top segment only), the
+  // half level reads that row as its replicate-clamped row -1 -- one extra barrier for every wave
+  // orders the stage-A write before the stage-B read (program order did it for one wave)
+  const int i_top = GRR_STEP2_SPLIT && r0 == 0 ? (3 - ts) / 2 : -1;
 
-  if (wave == F) {   // producer: weight rows -> LDS rings (LDS-DMA), two iterations ahead
+  constexpr int PRODUCER = GRR_STEP2_SPLIT ? S2_FMAX : -1;
+  if (wave == (GRR_STEP2_SPLIT ? PRODUCER : F)) {   // producer: weight rows -> LDS rings (LDS-DMA), two iterations ahead
     const float* pwl0 = a.wL0 + (int64_t)(b * a.G + g) * 4 * HW;
     const float* pcg0 = a.cG0 + (int64_t)(b * a.G + g) * 2 * HW;
     const float* pwl1 = a.wL1 + (int64_t)(b * a.G + g) * 4 * hHW;
@@ -1564,6 +1578,7 @@ void graph_step2_kernel(Step2Args a) {
     for (int i = 0; i < NI; ++i) {
       dma_pair(i + 2);
       dma_half(i + 2);
+      if (i == i_top) __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt vmcnt(15)" ::: "memory");  // iteration i+1's rows landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -1572,8 +1587,13 @@ void graph_step2_kernel(Step2Args a) {
     return;
   }
 
-  // ---- channel wave f
-  const int f = wave;
+  // ---- channel wave f (split: stage-B wave f < S2_FMAX, stage-A wave S2_FMAX + 1 + f)
+  const bool role_a = GRR_STEP2_SPLIT && wave > PRODUCER;
+  const int f = GRR_STEP2_SPLIT ? (role_a ? wave - PRODUCER - 1 : wave) : wave;
+  if (f >= F) {   // spare wave of a graph with F < S2_FMAX: the barriers only
+    for (int i = 0; i <= NI + (i_top >= 0); ++i) __builtin_amdgcn_s_barrier();
+    return;
+  }
   const int C = a.G * F, ch = g * F + f;
   const int64_t plane = ((int64_t)b * C + ch) * HW, hplane = ((int64_t)b * C + ch) * hHW;
   const int64_t PB = HW * 4, HPB = hHW * 4;
@@ -1614,15 +1634,21 @@ void graph_step2_kernel(Step2Args a) {
   };
   // read-once streams (x_k, u_k, t_k, weights) are non-temporal so that b's rows stay in L2
   // for stage B's second read 8 rows later (one HBM read of b per launch)
-  auto issue = [&](int t, Ld& S) {
+  auto issue_a = [&](int t, Ld& S) {
     bload<V, S2_NT>(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
     const int re = clampi(t - 3, 0, H - 1);
     bload(S.eb, rb, vo + re * RB);
     bload<V, S2_NT>(S.eu, ru, vo + re * RB);
     bload<VH, S2_NT>(S.th, rth, vo_half + (re >> 1) * HRB);
+  };
+  auto issue_b = [&](int t, Ld& S) {
     const int r2 = clampi(t - 11, 0, H - 1);
     bload(S.b2, rb, vo + r2 * RB);
     bload(S.y2, ry, vo + r2 * RB);
+  };
+  auto issue = [&](int t, Ld& S) {
+    if (!GRR_STEP2_SPLIT || role_a) issue_a(t, S);
+    if (!GRR_STEP2_SPLIT || !role_a) issue_b(t, S);
   };
   auto ring_w = [&](const float* row, float (&WL)[4][V], float (&WG)[2][V]) {
 #pragma unroll
@@ -1777,7 +1803,7 @@ void graph_step2_kernel(Step2Args a) {
   // segment, weight pairs of stage B's fill) only feed rows that are never stored, but through
   // products with a 0 weight: zero them so the garbage is finite.  Weight slots 2..6 are first
   // filled after the barrier below.
-  {
+  if (!GRR_STEP2_SPLIT || role_a) {
     const float zero4[V] = {};
 #pragma unroll
     for (int r = 0; r < S2_XR; ++r) st4(xr + r * S2_W, zero4);
@@ -1820,7 +1846,65 @@ void graph_step2_kernel(Step2Args a) {
     iteration(i + 2, std::integral_constant<int, 2>{}, edge_tag);
     iteration(i + 3, std::integral_constant<int, 3>{}, edge_tag);
   };
+#if GRR_STEP2_SPLIT
+  // stage-A wave: two rows of stage k per iteration; stage-B wave: the half level and two rows of
+  // stage k+1 (8 rows behind, its inputs written into the rings at least one barrier earlier)
+  auto iteration_a = [&](int i, auto pi_tag, auto edge_tag) {
+    constexpr int PI = decltype(pi_tag)::value;
+    using P0 = std::integral_constant<int, (2 * PI) & 3>;
+    using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
+    using E = decltype(edge_tag);
+    const int t = ts + 2 * i;
+    stage_a(t, LA, qa, std::integral_constant<int, 0>{}, P0{}, E{});
+    issue_a(t + 2, LA);
+    stage_a(t + 1, LB, qa, std::integral_constant<int, 1>{}, P1{}, E{});
+    issue_a(t + 3, LB);
+    if (i == i_top) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    qa = qa == S2_WP - 1 ? 0 : qa + 1;
+  };
+  auto iteration_b = [&](int i, auto pi_tag, auto edge_tag) {
+    constexpr int PI = decltype(pi_tag)::value;
+    using P0 = std::integral_constant<int, (2 * PI) & 3>;
+    using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
+    using PHh = std::integral_constant<int, PI & 3>;
+    using E = decltype(edge_tag);
+    const int t = ts + 2 * i;
+    const int qb = qa >= 4 ? qa - 4 : qa + 3;   // pair i - 4 (mod 7)
+    if (i == i_top) __builtin_amdgcn_s_barrier();
+    stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{}, E{});
+    stage_b(t, LA, qb, std::integral_constant<int, 0>{}, P0{}, E{});
+    issue_b(t + 2, LA);
+    stage_b(t + 1, LB, qb, std::integral_constant<int, 1>{}, P1{}, E{});
+    issue_b(t + 3, LB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    qa = qa == S2_WP - 1 ? 0 : qa + 1;
+  };
+  if (role_a) {
+    for (int i = 0; i < NI; i += S2_UNROLL) {
+      iteration_a(i, std::integral_constant<int, 0>{}, std::true_type{});
+      iteration_a(i + 1, std::integral_constant<int, 1>{}, std::true_type{});
+      iteration_a(i + 2, std::integral_constant<int, 2>{}, std::true_type{});
+      iteration_a(i + 3, std::integral_constant<int, 3>{}, std::true_type{});
+    }
+  } else {
+    for (int i = 0; i < NI; i += S2_UNROLL) {
+      iteration_b(i, std::integral_constant<int, 0>{}, std::true_type{});
+      iteration_b(i + 1, std::integral_constant<int, 1>{}, std::true_type{});
+      iteration_b(i + 2, std::integral_constant<int, 2>{}, std::true_type{});
+      iteration_b(i + 3, std::integral_constant<int, 3>{}, std::true_type{});
+    }
+  }
+#else
   for (int i = 0; i < NI; i += S2_UNROLL) block(i, std::true_type{});
+#endif
 }
 
 static int step2_seg_rows(int H, uint64_t blocks_per_seg) {
@@ -2072,7 +2156,8 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   const uint64_t nblk = (uint64_t)B * G * a.nsegs;
   GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_step2: grid too large");
   a.nblk = (uint32_t)nblk;
-  hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(64 * (F + 1)), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(GRR_STEP2_SPLIT ? S2_THREADS : 64 * (F + 1)), 0,
+                     (hipStream_t)stream, a);
   return launch_status("grr_system_step2");
 }
 

@@ -11,16 +11,17 @@
 //  lnb_head_kernel  LN + W1 + depthwise 3x3 + gate, x -> g [B, hid, H, W].
 //    A 512-thread workgroup owns a 32-column x TH-row output tile and recomputes W1 on
 //    its (TH+2) x 34 halo (replicate padding = clamped halo coordinates).  Every wave keeps
-//    the raw x columns of its halo pixels as an exact 3-term bf16 split in registers (B
-//    operand of v_mfma_f32_16x16x32_bf16) together with each pixel's 1/sigma (LN folded:
-//    W1 (ln_w * x / sigma) = (W1 diag ln_w) x / sigma); the hidden channels are walked in
+//    the x / sigma columns of its halo pixels as an exact 3-term bf16 split in registers (B
+//    operand of v_mfma_f32_16x16x32_bf16; LN folded: W1 (ln_w * x / sigma) = (W1 diag ln_w)
+//    (x / sigma)); the hidden channels are walked in
 //    chunks of 8 (mask, value) pairs = 16 GEMM rows.  A chunk's W1.diag(ln_w) fragments
 //    arrive by LDS-DMA in a 3-slot ring two chunks ahead; its 16 x halo h image goes to a double-buffered LDS plane set, from
 //    which the next iteration evaluates the depthwise 3x3 + gate (one wave per hidden
 //    channel, lane = output column) while the matrix cores run the following chunk.  One
 //    barrier per chunk; every wave issues a fixed sequence of memory operations per
 //    iteration (dummy DMA / out-of-range buffer stores at the edges), so the ring is
-//    waited on with a counted vmcnt.
+//    waited on with a counted vmcnt.  The K = 3 head (the image filter's replicated first block,
+//    110 VGPRs) keeps one chunk in flight instead of two and runs two workgroups per CU.
 //
 //  lnb_mix_kernel   W2 g + skip, g, x -> out.  256 pixels x all C rows per workgroup,
 //    W2 (split, fragment order) streamed through a 4-slot LDS-DMA ring per 16-deep k-step,
@@ -169,13 +170,19 @@ __global__ void lnb_w1_pack_kernel(const float* __restrict__ w1, const float* __
   }
 }
 
+// chunks of W1 fragments in flight ahead of GEMM1; the K = 3 head (110 VGPRs) runs two workgroups
+// per CU with one chunk ahead (3-slot ring: 78 KB of LDS per workgroup)
+__host__ __device__ constexpr int head_ahead(int KS) { return KS == 1 ? 1 : 2; }
+__host__ __device__ constexpr int head_wgs(int KS) { return KS == 1 ? 2 : 1; }
+
 template <int KS, int NB>
-__global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
+__global__ __launch_bounds__(512, head_wgs(KS)) void lnb_head_kernel(LnbHeadArgs a) {
   using Geo = HeadGeom<NB>;
   constexpr int NI = KS * 3 + 1;        // images per chunk (fragments + taps)
   constexpr int DPW = (NI + 7) / 8;     // LDS-DMA instructions per wave per chunk
   constexpr int SLOTF = NI * 256;       // floats per ring slot
-  constexpr int NSLOT = 4;              // two chunks in flight + GEMM1(c) + gate(c - 1)
+  constexpr int AHEAD = head_ahead(KS);
+  constexpr int NSLOT = AHEAD + 2;      // chunks in flight + GEMM1(c) + gate(c - 1)
   constexpr int HBUF = 2 * LH_JC * Geo::HP;
   constexpr int RA = Geo::RA;
   __shared__ __attribute__((aligned(16))) float smem[2 * HBUF + NSLOT * SLOTF];
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
     }
   };
   issue(0, 0);
-  issue(min(1, nch - 1), 1);
+  if constexpr (AHEAD == 2) issue(min(1, nch - 1), 1);
 
   // this wave's halo pixels: raw x column split into bf16 terms, and 1/sigma (REF:916-922)
   const int kq = lane >> 4;
@@ -244,6 +251,11 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
     sq += __shfl_xor(sq, 16);
     sq += __shfl_xor(sq, 32);
     rstd[blk] = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
+    // x / sigma first (REF:921), so h = (W1 diag ln_w) (x / sigma) leaves GEMM1 unscaled
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[blk][s][j] *= rstd[blk];
 #pragma unroll
     for (int s = 0; s < KS; ++s) split3x8(xv[blk][s], xf[blk][s][0], xf[blk][s][1], xf[blk][s][2]);
   }
@@ -281,13 +293,16 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
     for (int blk = 0; blk < NB; ++blk) {
       const int q = (wave * NB + blk) * 16 + (lane & 15);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * Geo::HP + q] = acc[blk][i] * rstd[blk];
+      for (int i = 0; i < 4; ++i) hb[(4 * kq + i) * Geo::HP + q] = acc[blk][i];
     }
   };
   // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1
   auto gate = [&](int c) {
     const int jj = LH_JC * (c - 1) + wave;
     const bool live = c >= 1 && jj < hid;
+    const bool lane_ok = live && gx < W;
+    const int nrow = min(Geo::TH, H - y0) - r0;   // output rows of this lane's half inside the tile and image
+    const uint32_t off0 = (uint32_t)(jj * HW + (y0 + r0) * W + gx) * 4u;
     const float* hb = smem + ((c + 1) & 1) * HBUF;
     const float* mp = hb + wave * Geo::HP + col;
     const float* vp = hb + (LH_JC + wave) * Geo::HP + col;
@@ -316,11 +331,10 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
             m += km[ay * 3 + ax] * mw[(i - 2 + ay) % 3][ax];
             v += kv[ay * 3 + ax] * vw[(i - 2 + ay) % 3][ax];
           }
-        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
-        const int orow = r0 + i - 2, gy = y0 + orow;
-        const bool ok = live && orow < Geo::TH && gy < H && gx < W;
-        const uint32_t off = ok ? (uint32_t)(jj * HW + gy * W + gx) * 4u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((sg * m) * v), grs, off, 0, 0);
+        const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __expf(-m));   // sigmoid(m) m v
+        const bool ok = lane_ok && i - 2 < nrow;
+        const uint32_t off = ok ? off0 + (uint32_t)((i - 2) * W) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, off, 0, 0);
       }
     }
   };
@@ -340,8 +354,8 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
 #ifdef GRR_FUSED_STAMP
     uint64_t tt = __builtin_amdgcn_s_memtime();
 #endif
-    // chunk c + 2 -> slot (c + 2) % 4, last read (gate of chunk c - 2) before the previous barrier
-    issue(min(c + 2, nch - 1), (c + 2) % NSLOT);
+    // chunk c + AHEAD -> slot (c + AHEAD) % NSLOT, last read (gate of chunk c - 2) before the previous barrier
+    issue(min(c + AHEAD, nch - 1), (c + AHEAD) % NSLOT);
     if (gate_first) {
       gate(c);
       GRR_STAMP(0, tt);
@@ -354,8 +368,9 @@ __global__ __launch_bounds__(512, 1) void lnb_head_kernel(LnbHeadArgs a) {
       GRR_STAMP(0, tt);
     }
     // chunk c + 1 landed: after its DMA this wave issued RA stores (iteration c - 1),
-    // DPW DMAs and RA stores (iteration c); then every wave's part (barrier)
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * RA + DPW) : "memory");
+    // DPW DMAs and RA stores (iteration c) -- AHEAD = 1: RA stores (iteration c); then every
+    // wave's part (barrier)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(AHEAD == 2 ? 2 * RA + DPW : RA) : "memory");
     GRR_STAMP(3, tt);
     __builtin_amdgcn_s_barrier();
     GRR_STAMP(5, tt);

@@ -62,6 +62,14 @@ def main():
     elif args.kernel == "lnb":
         blk = irdu_amd.LocalNonLinearBlock(c, 256, 1).to(dev)
         fn = lambda: blk(x)  # noqa: E731
+    elif args.kernel == "lnb_rep":   # first block of the image filter: RGB replicated over the graphs
+        blk = irdu_amd.LocalNonLinearBlock(c, 256, 1).to(dev)
+        src = torch.rand(b, 3, h, w, device=dev)
+        ll, hid = blk.local_linear, 256
+        wts = (p(blk.norm.weighted_transform.weight).view(c), p(ll.channels_linear_op.weight).view(2 * hid, c),
+               p(ll.channels_local_linear_op.weight).view(2 * hid, 9), p(ll.project_out.weight).view(c, hid),
+               p(blk.skip_weight))
+        fn = lambda: K.lnb_forward_rep(src, None, *wts)  # noqa: E731
     elif args.kernel == "conv1x1":
         wt = torch.rand(2 * c, c, 1, 1, device=dev)
         fn = lambda: K.conv1x1(x, wt)  # noqa: E731
