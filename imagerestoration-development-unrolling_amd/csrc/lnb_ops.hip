@@ -342,7 +342,10 @@ __global__ __launch_bounds__(512, head_wgs(KS)) void lnb_head_kernel(LnbHeadArgs
   // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (independent LDS planes).  The two
   // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work
   // overlaps the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).
-  const bool gate_first = wave < 4;
+#ifndef GRR_HEAD_STAGGER
+#define GRR_HEAD_STAGGER 1
+#endif
+  const bool gate_first = GRR_HEAD_STAGGER ? wave < 4 : true;
 #ifdef GRR_FUSED_STAMP
   uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t t_begin = __builtin_amdgcn_s_memtime();
