@@ -523,23 +523,23 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArg
   for (int nb = 0; nb < LM_NBB; ++nb) {
     const int p = (int)p0 + (wave * LM_NBB + nb) * 32 + r;
     const int pc = min(p, Pi - 1);
-    float xv[MT][16];
+    // one 32-row tile of x at a time (the skip operand): 16 loads in flight, not MT x 16 live registers
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) {
+      float xv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = min(32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh, C - 1);
         const int mx = XC == C ? m : m % XC;
-        xv[t][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (mx * Pi + pc) * 4, 0, 0));
+        xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (mx * Pi + pc) * 4, 0, 0));
       }
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
         const uint32_t off = (m < C && p < Pi) ? (uint32_t)(m * Pi + p) * 4u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[t][i] + s1 * acc[t][nb][i]), ors, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[i] + s1 * acc[t][nb][i]), ors, off, 0, 0);
       }
+    }
   }
 }
 
