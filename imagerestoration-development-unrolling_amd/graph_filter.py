@@ -19,6 +19,7 @@ training can never silently skip gradients.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -30,6 +31,18 @@ from . import ops as OPS
 from . import solver_grad as SG
 
 EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, down)
+
+# Inference: the half-resolution feature branch (2x2 conv, its LocalNonLinearBlocks, 1x1) runs on
+# a second HIP stream beside the full-resolution branch (GRR_FEATURE_STREAMS=0: one stream)
+FEATURE_STREAMS = os.environ.get("GRR_FEATURE_STREAMS", "1") == "1"
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev)
+    return _SIDE_STREAMS[key]
 
 
 class _NoBackward(torch.autograd.Function):
@@ -319,22 +332,43 @@ class MixtureGTVGLR(nn.Module):
             return OPS.conv2x2s2(y, weight)
         return OPS.conv2x2s2(src, weight, fold=True)
 
-    def features(self, y: torch.Tensor, src: Optional[torch.Tensor] = None):
+    def features(self, y: torch.Tensor, src: Optional[torch.Tensor] = None, half_tail=None):
+        """f0, f1 (a13).  half_tail(f1), when given, runs right after the half-resolution branch on
+        the same stream and its tuple of tensors is returned in place of f1."""
         s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
         if self.feature_extractor == "v1":
             f0 = OPS.conv1x1(y, s0[0].weight)
             f1 = OPS.conv1x1(self._down(y, s1[0].weight, src), s1[1].weight)
-            return f0, f1
+            return f0, (half_tail(f1) if half_tail is not None else f1)
+        ref = y if y is not None else src
+
+        def half():
+            f1 = self._down(y, s1[0].weight, src)
+            for blk in list(s1)[1:4]:
+                f1 = blk(f1)
+            f1 = OPS.conv1x1(f1, s1[4].weight)
+            return half_tail(f1) if half_tail is not None else f1
+
+        side = None
+        if FEATURE_STREAMS and ref.is_cuda and not torch.compiler.is_compiling() \
+                and not torch.cuda.is_current_stream_capturing():
+            main = torch.cuda.current_stream(ref.device)
+            side = _side_stream(ref.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                f1 = half()
+        else:
+            f1 = half()
         blocks = list(s0)[:3]
         # the first block's input replicates src over the graphs: its GEMM1 runs on src (K = F)
         f0 = blocks[0].forward_replicated(src, y) if src is not None else blocks[0](y)
         for blk in blocks[1:]:
             f0 = blk(f0)
         f0 = OPS.conv1x1(f0, s0[3].weight)
-        f1 = self._down(y, s1[0].weight, src)
-        for blk in list(s1)[1:4]:
-            f1 = blk(f1)
-        f1 = OPS.conv1x1(f1, s1[4].weight)
+        if side is not None:
+            main.wait_stream(side)
+            for t in (f1 if isinstance(f1, tuple) else (f1,)):
+                t.record_stream(main)
         return f0, f1
 
     def features_train(self, y: torch.Tensor):
@@ -375,19 +409,22 @@ class MixtureGTVGLR(nn.Module):
             raise ValueError(f"MixtureGTVGLR: H, W must be even for the 2x2 scale (got {h}x{w})")
         if src is not None and (src.shape[1] != f or src.shape[0] != b or tuple(src.shape[2:]) != (h, w)):
             raise ValueError("MixtureGTVGLR: src must be [B, F, H, W]")
-        f0, f1 = self.features(y, src)
         G0, L0, G1, L1 = self.GTVmodule00, self.GLRmodule00, self.GTVmodule01, self.GLRmodule01
+
+        def half_tail(f1):
+            # the half level's edge weights and its part of rhs A (ro1 G1 D y, REF:738-749)
+            wG1, cG1, wL1 = OPS.edge_weights_block(f1, g, f, G1.multiM, L1.multiM)
+            yd = OPS.pool2(y) if src is None else OPS.repeat_graphs(OPS.pool2(src), g)   # D y
+            return wG1, cG1, wL1, OPS.gtv_rhs_half(yd, cG1, G1, False, None, g)
+
+        f0, (wG1, cG1, wL1, t) = self.features(y, src, half_tail)
         wG0, cG0, wL0 = OPS.edge_weights_block(f0, g, f, G0.multiM, L0.multiM)
-        wG1, cG1, wL1 = OPS.edge_weights_block(f1, g, f, G1.multiM, L1.multiM)
-        del f0, f1
+        del f0
         mu0, mu1, ro0, ro1 = self.muys00, self.muys01, self.ro00, self.ro01
         alpha, beta = self.alphaCGD, self.betaCGD
         n_st = alpha.shape[0]
 
         # rhs A: b_A = y + ro0 G0 y + ro1 U(G1 D y)                     (REF:738-749)
-        yd = OPS.pool2(y) if src is None else OPS.repeat_graphs(OPS.pool2(src), g)   # D y
-        t = OPS.gtv_rhs_half(yd, cG1, G1, False, None, g)
-        del yd
         if y is None:
             b_a, xd = OPS.gtv_rhs_full(src, True, src, True, cG0, G0, False, None, ro0, t, ro1, g, want_pool=True)
         else:

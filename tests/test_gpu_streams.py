@@ -1,0 +1,53 @@
+"""The image filter's half-resolution feature branch (2x2 conv, LocalNonLinearBlocks, 1x1, the
+half level's edge weights and its rhs-A term) runs on a second HIP stream beside the
+full-resolution branch (graph_filter.FEATURE_STREAMS).  The kernels are deterministic, so the
+two-stream forward must equal the one-stream forward bit for bit, for the replicated-RGB
+MultiScaleGraphFilter and for a MixtureGTVGLR called on a plain signal."""
+import pytest
+import torch
+
+from tests.test_gpu_parity import DEV
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def irdu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import irdu_amd
+    irdu_amd.load_native()
+    return irdu_amd
+
+
+def _both(run):
+    from irdu_amd import graph_filter as GF
+    saved = GF.FEATURE_STREAMS
+    try:
+        outs = []
+        for on in (False, True):
+            GF.FEATURE_STREAMS = on
+            with torch.no_grad():
+                outs.append(run())
+            torch.cuda.synchronize()
+        return outs
+    finally:
+        GF.FEATURE_STREAMS = saved
+
+
+def test_msgf_two_streams_bitwise(irdu):
+    torch.manual_seed(7)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=4).to(DEV)
+    x = torch.rand(3, 3, 64, 96, device=DEV)
+    a, b = _both(lambda: m(x))
+    assert torch.equal(a, b)
+
+
+def test_mixture_two_streams_bitwise(irdu):
+    torch.manual_seed(8)
+    g, f = 4, 3
+    mix = irdu.MixtureGTVGLR(g, f, 0.5, 0.1, [[1e-1], [1e-2]], [[1e-1], [1e-2]], [[1e-2], [1e-2]],
+                             n_cgd_iters=5, feature_extractor="v13").to(DEV)
+    y = torch.rand(2, g * f, 48, 64, device=DEV)
+    a, b = _both(lambda: mix(y))
+    assert torch.equal(a, b)
