@@ -247,12 +247,18 @@ def main():
         barrier()
         dt = time.perf_counter() - t0
         # then the same steps again with HIP events around every launch (per-kernel breakdown and
-        # the roofline's kernel time); this loop's wall time is not the headline
+        # the roofline's kernel time); this loop's wall time is not the headline.  It runs on one
+        # stream (no feature side stream), so each kernel's time is its own and not shared with a
+        # concurrent kernel
+        from irdu_amd import graph_filter as GF
+        saved = GF.FEATURE_STREAMS
+        GF.FEATURE_STREAMS = False
         timer = K.LaunchTimer()
         K.set_timer(timer)
         for _ in range(max(1, min(args.steps, 5))):
             out = model(noisy)
         K.set_timer(None)
+        GF.FEATURE_STREAMS = saved
         n_inst = max(1, min(args.steps, 5))
     kern = timer.summary()
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
