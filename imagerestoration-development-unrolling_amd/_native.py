@@ -101,6 +101,7 @@ SIGNATURES = {
     "grr_win_edge_weights": [P, L, P, P, I, P, P, I, I, I, I, I, P],
     "grr_win_solver": [I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, I, I, I, I, I, P],
     "grr_win_mix": [P, P, P, P, I, I, I, I, I, P],
+    "grr_win_pair_weights": [P, P, I, P, I, I, I, I, P],
     "grr_win_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
     "grr_win_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],
     "grr_win_bwd_glr": [P, P, P, P, I, P, Fl, P, P, P, P, P, I, I, I, I, I, P],

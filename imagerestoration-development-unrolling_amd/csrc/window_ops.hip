@@ -109,6 +109,36 @@ __global__ __launch_bounds__(NTW) void win_edge_weights_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------
+// Pair weights of the linear GTV term (solver modes 0, 1, 3).  The frame-dropped C^T scatter pairs
+// each directed edge with its reverse: C^T C s (q) = sum_e c_e(q) (s(q) - s(clamp(q + d_e))) with
+// c_e(q) = w_e(q)^2 + [q + d_e inside] w_e'(q + d_e)^2, e' the edge of offset -d_e (REF7:748-774
+// for the scatter; the window offsets are symmetric).  The solver then loads K weights per
+// position instead of K plus K gathered reverse weights.   grid (ceil(HW / NTW), B*G)
+// ---------------------------------------------------------------------------
+struct WinOpp {
+  int8_t e[kMaxEdges];
+};
+__global__ __launch_bounds__(NTW) void win_pair_weights_kernel(const float* __restrict__ w, float* __restrict__ c,
+                                                               WinDelta d, WinOpp opp, int K, int H, int W) {
+  const int HW = H * W;
+  const int p = blockIdx.x * NTW + threadIdx.x;
+  if (p >= HW) return;
+  const int r = p / W, col = p - r * W;
+  const float* wp = w + (int64_t)blockIdx.y * K * HW;
+  float* cp = c + (int64_t)blockIdx.y * K * HW;
+  for (int e = 0; e < K; ++e) {
+    const float we = wp[(int64_t)e * HW + p];
+    const int ny = r + d.dy[e], nx = col + d.dx[e];
+    float v = we * we;
+    if (ny >= 0 && ny < H && nx >= 0 && nx < W) {
+      const float wr = wp[(int64_t)opp.e[e] * HW + ny * W + nx];
+      v += wr * wr;
+    }
+    cp[(int64_t)e * HW + p] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Solver kernel.  Tile TH x TW outputs of one (b, g); R = window reach (1 or 2).
 //   MODE 0 (CG step, REF7:892-911, :951-990):  A x = x + mu S_L^T (S_L x - W_L S_L x)
 //          + ro S_G^T C^T C S_G x;  u = (b - A x) [+ beta u_prev];  x' = x + alpha u
@@ -153,7 +183,8 @@ __device__ __forceinline__ int reflect1(int v, int n) {   // one-pixel reflect f
 constexpr int NTS = 512, FSMAX = 3;
 static_assert(FSMAX * TH * TW % NTS == 0, "epilogue slots");
 
-template <int R, int MODE, int KT>
+// PAIR (modes 0, 1, 3): wG holds the pair weights of win_pair_weights_kernel.
+template <int R, int MODE, int KT, bool PAIR = false>
 __global__ __launch_bounds__(NTS, KT == 24 ? 2 : 4) void win_solver_kernel(WinArgs a) {
   constexpr bool GLR = MODE == 0 || MODE == 3;
   constexpr int HS = R + 1, SH = TH + 2 * HS, SW = TW + 2 * HS;   // s region
@@ -254,7 +285,32 @@ __global__ __launch_bounds__(NTS, KT == 24 ? 2 : 4) void win_solver_kernel(WinAr
     const int sq = (qy - (y0 - HS)) * SW + (qx - (x0 - HS));
     float ov[FSMAX] = {0.f, 0.f, 0.f}, lv[FSMAX] = {0.f, 0.f, 0.f};
     constexpr int KE = KT > 0 ? KT : kMaxEdges;
-    if (in && has_gtv) {
+    if (PAIR && in && has_gtv) {
+      // sum_e c_e(q) (s(q) - s(clamp(q + delta_e))): K pair weights, no reverse-edge gathers
+      float cf[KE];
+      int sn[KE];
+#pragma unroll
+      for (int e = 0; e < KE; ++e) {
+        if (KT == 0 && e >= K) break;
+        const int ny = clampi(qy + a.d.dy[e], 0, H - 1), nx = clampi(qx + a.d.dx[e], 0, W - 1);
+        sn[e] = (ny - (y0 - HS)) * SW + (nx - (x0 - HS));
+        cf[e] = wGp[e * HW + q];
+      }
+#pragma unroll
+      for (int c = 0; c < FSMAX; ++c) {
+        if (c < Fs) {
+          const float* sc = sg + c * NS;
+          const float sv = sc[sq];
+          float acc = 0.f;
+#pragma unroll
+          for (int e = 0; e < KE; ++e) {
+            if (KT == 0 && e >= K) break;
+            acc += cf[e] * (sv - sc[sn[e]]);
+          }
+          ov[c] = acc;
+        }
+      }
+    } else if (in && has_gtv) {
       // every weight of this position first (one batch of loads in flight), then the math:
       // sum_e z_e(q) - sum_e [q - delta_e inside] z_e(q - delta_e), z_e = w_e phi(w_e s - w_e s(+delta_e))
       float wf[KE], wb[KE];
@@ -429,11 +485,37 @@ grr_status grr_win_edge_weights(const float* feat, int64_t feat_bstride, const f
   return launch_status("grr_win_edge_weights");
 }
 
+grr_status grr_win_pair_weights(const float* w, const int32_t* delta, int K, float* c, int B, int G, int H, int W,
+                                void* stream) {
+  GRR_REQUIRE(w && c && w != c && B > 0 && G > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
+              "grr_win_pair_weights: bad argument");
+  GRR_REQUIRE((int64_t)B * G <= 65535 && (int64_t)H * W * K < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_win_pair_weights: grid too large");
+  WinDelta d{};
+  int reach = 0;
+  const grr_status st = load_delta(delta, K, &d, &reach);
+  if (st != GRR_OK) return st;
+  WinOpp opp{};
+  for (int e = 0; e < K; ++e) {
+    int o = -1;
+    for (int f = 0; f < K; ++f)
+      if (d.dy[f] == -d.dy[e] && d.dx[f] == -d.dx[e]) o = f;
+    GRR_REQUIRE(o >= 0, GRR_ERR_UNSUPPORTED, "grr_win_pair_weights: edge %d = (%d, %d) has no reverse edge", e,
+                (int)d.dy[e], (int)d.dx[e]);
+    opp.e[e] = (int8_t)o;
+  }
+  const dim3 grid((H * W + NTW - 1) / NTW, B * G);
+  hipLaunchKernelGGL(win_pair_weights_kernel, grid, dim3(NTW), 0, (hipStream_t)stream, w, c, d, opp, K, H, W);
+  return launch_status("grr_win_pair_weights");
+}
+
 grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, const float* u_prev, const float* wL,
                           const float* wG, const float* tapsL, const float* tapsG, const float* mu, const float* ro,
                           const float* log_gamma, const float* alpha, const float* beta, const int32_t* delta, int K,
                           float* out, float* u_out, int B, int G, int Fs, int H, int W, void* stream) {
-  GRR_REQUIRE(mode >= 0 && mode <= 3, GRR_ERR_INVALID_ARG, "grr_win_solver: mode %d", mode);
+  const bool pair = mode >= 4;   // modes 4, 5, 7: 0, 1, 3 with wG = grr_win_pair_weights(w_G)
+  GRR_REQUIRE(mode >= 0 && mode <= 7 && mode != 6, GRR_ERR_INVALID_ARG, "grr_win_solver: mode %d", mode);
+  mode &= 3;
   GRR_REQUIRE(x && out && B > 0 && G > 0 && Fs > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_win_solver: bad argument");
   GRR_REQUIRE(mode == 3 || (y && wG && tapsG && ro), GRR_ERR_INVALID_ARG, "grr_win_solver: y, wG, tapsG, ro required");
@@ -459,13 +541,13 @@ grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, c
   const int tiles = a.tiles_x * ((H + TH - 1) / TH);
   const dim3 grid(tiles, B * G);
   hipStream_t s = (hipStream_t)stream;
-#define WIN_LAUNCH(R_, M_, K_) hipLaunchKernelGGL((win_solver_kernel<R_, M_, K_>), grid, dim3(NTS), 0, s, a)
-#define WIN_MODES(R_, K_)                                  \
-  do {                                                     \
-    if (mode == 0) WIN_LAUNCH(R_, 0, K_);                  \
-    else if (mode == 1) WIN_LAUNCH(R_, 1, K_);             \
-    else if (mode == 2) WIN_LAUNCH(R_, 2, K_);             \
-    else WIN_LAUNCH(R_, 3, K_);                            \
+#define WIN_LAUNCH(R_, M_, K_, P_) hipLaunchKernelGGL((win_solver_kernel<R_, M_, K_, P_>), grid, dim3(NTS), 0, s, a)
+#define WIN_MODES(R_, K_)                                                      \
+  do {                                                                         \
+    if (mode == 0) { if (pair) WIN_LAUNCH(R_, 0, K_, true); else WIN_LAUNCH(R_, 0, K_, false); }   \
+    else if (mode == 1) { if (pair) WIN_LAUNCH(R_, 1, K_, true); else WIN_LAUNCH(R_, 1, K_, false); } \
+    else if (mode == 2) WIN_LAUNCH(R_, 2, K_, false);                          \
+    else { if (pair) WIN_LAUNCH(R_, 3, K_, true); else WIN_LAUNCH(R_, 3, K_, false); }             \
   } while (0)
   if (reach <= 1) {
     if (K == 8) WIN_MODES(1, 8); else WIN_MODES(1, 0);

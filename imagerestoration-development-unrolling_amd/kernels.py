@@ -867,8 +867,11 @@ def _check_win_scalars(n_graphs: int, **ts) -> None:
 def win_solver(mode: int, x: Tensor, y: Tensor, wG: Tensor, tapsG: Tensor, ro: Tensor, edge_delta, n_graphs: int,
                n_sig: int, *, wL: Optional[Tensor] = None, tapsL: Optional[Tensor] = None, mu: Optional[Tensor] = None,
                log_gamma: Optional[Tensor] = None, alpha: Optional[Tensor] = None, beta: Optional[Tensor] = None,
-               u_prev: Optional[Tensor] = None, want_u: bool = True) -> Tuple[Tensor, Optional[Tensor]]:
+               u_prev: Optional[Tensor] = None, want_u: bool = True,
+               pair: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
     """One fused pass of the window-graph MixtureGTV solver (grr_win_solver, REF7:892-1004).
+    pair: wG holds win_pair_weights(w_G) (modes 0 and 1: the same linear GTV term from K weights
+    per position instead of K plus K gathered reverse-edge weights).
 
     mode 0: CG step, x [B,G,Fs,H,W], y = rhs [B,G,Fs,H,W] -> (x_next, u);
     mode 1/2: (prox) right-hand side, y [B,Fs,H,W] shared by the graphs, x per graph or
@@ -896,10 +899,27 @@ def win_solver(mode: int, x: Tensor, y: Tensor, wG: Tensor, tapsG: Tensor, ro: T
         if tuple(y.shape) != (b, n_sig, h, w):
             raise ValueError(f"win_solver: y has shape {tuple(y.shape)}, expected {(b, n_sig, h, w)}")
         nbytes = 4 * h * w * (planes * (1 + int(not x_rep)) + b * n_sig * (1 + x_rep) + k * b * n_graphs)
-    _launch("win_solver", nbytes, "grr_win_solver", mode, x.data_ptr(), x_rep, y.data_ptr(), _ptr(u_prev), _ptr(wL),
+    if pair and mode == 2:
+        raise ValueError("win_solver: the prox rhs (mode 2) needs the raw GTV weights")
+    _launch("win_solver", nbytes, "grr_win_solver", mode + (4 if pair else 0), x.data_ptr(), x_rep, y.data_ptr(),
+            _ptr(u_prev), _ptr(wL),
             wG.data_ptr(), _ptr(tapsL), tapsG.data_ptr(), _ptr(mu), ro.data_ptr(), _ptr(log_gamma), _ptr(alpha),
             _ptr(beta), delta, k, out.data_ptr(), _ptr(u_out), b, n_graphs, n_sig, h, w, _stream(dev))
     return out, u_out
+
+
+def win_pair_weights(w: Tensor, edge_delta) -> Tensor:
+    """Pair weights c_e(q) = w_e(q)^2 + [q + d_e inside] w_e'(q + d_e)^2 of the linear window GTV
+    term (grr_win_pair_weights), w [B,G,K,H,W] -> c of the same shape."""
+    dev = _check("win_pair_weights", w)
+    delta, k = _delta_arg(edge_delta)
+    b, g, kk, h, ww = w.shape
+    if kk != k:
+        raise ValueError(f"win_pair_weights: w has {kk} edge planes, the window {k}")
+    c = torch.empty_like(w)
+    _launch("win_pair_weights", 4 * w.numel() * 3, "grr_win_pair_weights", w.data_ptr(), delta, k, c.data_ptr(), b, g,
+            h, ww, _stream(dev))
+    return c
 
 
 def win_mix(x: Tensor, score: Tensor, dc: Optional[Tensor] = None) -> Tensor:

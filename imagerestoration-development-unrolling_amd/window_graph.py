@@ -27,6 +27,7 @@ module calls stay inference-only (under autograd they attach a node whose backwa
 from __future__ import annotations
 
 import itertools
+import os
 from typing import Optional
 
 import numpy as np
@@ -37,6 +38,9 @@ from torch.nn.parameter import Parameter
 from . import kernels as K
 from . import window_grad as WG
 from .graph_filter import hip_forward, records_grad
+
+# inference: the linear GTV passes on pair weights (grr_win_pair_weights); GRR_WIN_PAIR=0: raw weights (A/B)
+WIN_PAIR_WEIGHTS = os.environ.get("GRR_WIN_PAIR", "1") == "1"
 
 CONNECTION_FLAGS_5x5_small = np.array([
     0, 0, 1, 0, 0,
@@ -297,16 +301,20 @@ class MixtureGTV(nn.Module):
         tG, tL = gtv.taps(), glr.taps()
         ro, mu, lg = self.ro00.data, self.muys00.data, self.gamma00.data
         alpha, beta = self.alphaCGD.data, self.betaCGD.data
+        # the linear GTV passes (CG steps, first rhs) read pair weights (K loads per position
+        # instead of K + K reverse-edge gathers); the prox rhs needs the raw directed weights
+        pair = WIN_PAIR_WEIGHTS
+        cG = K.win_pair_weights(wG, delta) if pair else wG
 
         def stages(rhs, ks):
             x, u = rhs, None
             for i, k in enumerate(ks):
                 last = i == len(ks) - 1
-                x, u = K.win_solver(0, x, rhs, wG, tG, ro, delta, g, fs, wL=wL, tapsL=tL, mu=mu, alpha=alpha[k],
-                                    beta=beta[k] if u is not None else None, u_prev=u, want_u=not last)
+                x, u = K.win_solver(0, x, rhs, cG, tG, ro, delta, g, fs, wL=wL, tapsL=tL, mu=mu, alpha=alpha[k],
+                                    beta=beta[k] if u is not None else None, u_prev=u, want_u=not last, pair=pair)
             return x
 
-        rhs, _ = K.win_solver(1, y, y, wG, tG, ro, delta, g, fs)                        # REF7:945-949
+        rhs, _ = K.win_solver(1, y, y, cG, tG, ro, delta, g, fs, pair=pair)              # REF7:945-949
         x = stages(rhs, [0, 1])                                                           # REF7:951-958
         rhs, _ = K.win_solver(2, x, y, wG, tG, ro, delta, g, fs, log_gamma=lg)            # REF7:960-967
         return stages(rhs, list(range(2, self.n_cgd_iters)))                              # REF7:970-990

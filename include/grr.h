@@ -375,11 +375,21 @@ grr_status grr_win_edge_weights(const float* feat, int64_t feat_bstride, const f
  *          out = mu S_L^T(S_L x - W_L S_L x) [wL != NULL] + ro S_G^T C^T C S_G x [wG != NULL];
  *          mu / ro may be NULL (= 1); y unused.
  * S reads x with a reflect frame (REF7:449-467); L/C neighbours clamp to the frame; S^T and
- * the C^T scatter drop what lands outside (REF7:469-488, :748-774). */
+ * the C^T scatter drop what lands outside (REF7:469-488, :748-774).
+ *  modes 4, 5, 7: modes 0, 1, 3 with wG holding the pair weights of grr_win_pair_weights (the
+ *          same linear GTV term, K weight loads per position instead of 2 K). */
 grr_status grr_win_solver(int mode, const float* x, int x_rep, const float* y, const float* u_prev, const float* wL,
                           const float* wG, const float* tapsL, const float* tapsG, const float* mu, const float* ro,
                           const float* log_gamma, const float* alpha, const float* beta, const int32_t* delta, int K,
                           float* out, float* u_out, int B, int G, int Fs, int H, int W, void* stream);
+
+/* Pair weights of a window graph's linear GTV term: c [B,G,K,H,W] with
+ * c_e(q) = w_e(q)^2 + [q + d_e inside] w_e'(q + d_e)^2, e' the edge of offset -d_e, so that
+ * C^T C s (q) = sum_e c_e(q) (s(q) - s(clamp(q + d_e))) (the frame-dropped scatter of
+ * GTVFast.op_C_transpose, REF7:748-774, paired edge by edge).  GRR_ERR_UNSUPPORTED when an offset
+ * has no reverse in delta. */
+grr_status grr_win_pair_weights(const float* w, const int32_t* delta, int K, float* c, int B, int G, int H, int W,
+                                void* stream);
 
 /* Graph mixture (REF7:1006-1009): out[b,c] = sum_g x[b,g,c] score[b,g] + dc[b,c] (dc may be NULL).
  * x [B,G,Fs,H,W], score [B,G,H,W], dc/out [B,Fs,H,W]. */

@@ -80,6 +80,7 @@ int main() {
   EXPECT_ERR(grr_win_edge_weights(n, 0, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_solver(0, n, 0, n, n, n, n, n, n, n, n, n, n, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_mix(n, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_win_pair_weights(n, delta, 2, n, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_stencil(n, n, 0, n, 0, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_tapgrad(n, n, 0, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_glr(n, n, n, delta, 2, n, 1.f, n, n, n, n, n, 1, 1, 1, 8, 8, s));

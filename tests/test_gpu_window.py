@@ -197,3 +197,44 @@ def test_window_v1_sequence_denoiser_vs_oracle(wg):
     with torch.no_grad():
         out = model(img.to(DEV))
     assert rel_err(out, ref) <= RTOL
+
+
+@pytest.mark.parametrize("name", WINDOWS)
+def test_window_pair_weights_and_pair_solver(wg, name):
+    """grr_win_pair_weights against a torch restatement of c_e(q) = w_e(q)^2 + [q + d_e inside]
+    w_e'(q + d_e)^2, and the solver's pair-weight modes (CG step, first rhs, module apply)
+    against the raw-weight modes they replace (same linear term, different summation order)."""
+    from irdu_amd import kernels as K
+    torch.manual_seed(31)
+    b, g, fs, h, w = 2, 3, 3, 37, 70
+    delta = O.window_edges(_window(name))
+    k = len(delta)
+    wgt = torch.softmax(torch.randn(b, g, k, h, w, device=DEV), 2)
+    c = K.win_pair_weights(wgt, delta)
+    ref = wgt.double() ** 2
+    for e, (dy, dx) in enumerate(delta):
+        o = [i for i, d in enumerate(delta) if tuple(d) == (-dy, -dx)][0]
+        sh = torch.zeros_like(ref[:, :, e])
+        ys, xs = slice(max(0, -dy), h - max(0, dy)), slice(max(0, -dx), w - max(0, dx))
+        yd, xd = slice(max(0, dy), h - max(0, -dy)), slice(max(0, dx), w - max(0, -dx))
+        sh[:, :, ys, xs] = wgt.double()[:, :, o, yd, xd] ** 2
+        ref[:, :, e] += sh
+    assert rel_err(c, ref) <= 1e-6
+    x = torch.randn(b, g, fs, h, w, device=DEV)
+    y = torch.randn(b, g, fs, h, w, device=DEV)
+    y1 = torch.randn(b, fs, h, w, device=DEV)
+    wl = torch.softmax(torch.randn(b, g, k, h, w, device=DEV), 2)
+    taps = torch.tensor([1.3, -0.2, -0.15, -0.25, -0.1], device=DEV)
+    ro, mu = torch.rand(g, device=DEV) + 0.2, torch.rand(g, device=DEV) + 0.2
+    alpha, beta = torch.rand(g, device=DEV), torch.rand(g, device=DEV)
+    u0 = torch.randn_like(x)
+    raw0 = K.win_solver(0, x, y, wgt, taps, ro, delta, g, fs, wL=wl, tapsL=taps, mu=mu, alpha=alpha, beta=beta,
+                        u_prev=u0)
+    got0 = K.win_solver(0, x, y, c, taps, ro, delta, g, fs, wL=wl, tapsL=taps, mu=mu, alpha=alpha, beta=beta,
+                        u_prev=u0, pair=True)
+    assert rel_err(got0[0], raw0[0]) <= 1e-5 and rel_err(got0[1], raw0[1]) <= 1e-5
+    raw1, _ = K.win_solver(1, x, y1, wgt, taps, ro, delta, g, fs)
+    got1, _ = K.win_solver(1, x, y1, c, taps, ro, delta, g, fs, pair=True)
+    assert rel_err(got1, raw1) <= 1e-5
+    with pytest.raises(ValueError):
+        K.win_solver(2, x, y1, c, taps, ro, delta, g, fs, log_gamma=torch.zeros(g, device=DEV), pair=True)
