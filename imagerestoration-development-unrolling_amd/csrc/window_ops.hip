@@ -118,23 +118,30 @@ __global__ __launch_bounds__(NTW) void win_edge_weights_kernel(const float* __re
 struct WinOpp {
   int8_t e[kMaxEdges];
 };
+template <int KT>   // KT = K at compile time (8, 12, 24: every load issued up front), 0 = runtime K
 __global__ __launch_bounds__(NTW) void win_pair_weights_kernel(const float* __restrict__ w, float* __restrict__ c,
-                                                               WinDelta d, WinOpp opp, int K, int H, int W) {
+                                                               WinDelta d, WinOpp opp, int K_, int H, int W) {
+  constexpr int KE = KT > 0 ? KT : kMaxEdges;
+  const int K = KT > 0 ? KT : K_;
   const int HW = H * W;
   const int p = blockIdx.x * NTW + threadIdx.x;
   if (p >= HW) return;
   const int r = p / W, col = p - r * W;
   const float* wp = w + (int64_t)blockIdx.y * K * HW;
   float* cp = c + (int64_t)blockIdx.y * K * HW;
-  for (int e = 0; e < K; ++e) {
-    const float we = wp[(int64_t)e * HW + p];
+  float we[KE], wr[KE];
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    if (KT == 0 && e >= K) break;
     const int ny = r + d.dy[e], nx = col + d.dx[e];
-    float v = we * we;
-    if (ny >= 0 && ny < H && nx >= 0 && nx < W) {
-      const float wr = wp[(int64_t)opp.e[e] * HW + ny * W + nx];
-      v += wr * wr;
-    }
-    cp[(int64_t)e * HW + p] = v;
+    const bool in = ny >= 0 && ny < H && nx >= 0 && nx < W;
+    we[e] = wp[(int64_t)e * HW + p];
+    wr[e] = in ? wp[(int64_t)opp.e[e] * HW + ny * W + nx] : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    if (KT == 0 && e >= K) break;
+    cp[(int64_t)e * HW + p] = we[e] * we[e] + wr[e] * wr[e];
   }
 }
 
@@ -505,7 +512,11 @@ grr_status grr_win_pair_weights(const float* w, const int32_t* delta, int K, flo
     opp.e[e] = (int8_t)o;
   }
   const dim3 grid((H * W + NTW - 1) / NTW, B * G);
-  hipLaunchKernelGGL(win_pair_weights_kernel, grid, dim3(NTW), 0, (hipStream_t)stream, w, c, d, opp, K, H, W);
+  hipStream_t s = (hipStream_t)stream;
+  if (K == 8) hipLaunchKernelGGL(win_pair_weights_kernel<8>, grid, dim3(NTW), 0, s, w, c, d, opp, K, H, W);
+  else if (K == 12) hipLaunchKernelGGL(win_pair_weights_kernel<12>, grid, dim3(NTW), 0, s, w, c, d, opp, K, H, W);
+  else if (K == 24) hipLaunchKernelGGL(win_pair_weights_kernel<24>, grid, dim3(NTW), 0, s, w, c, d, opp, K, H, W);
+  else hipLaunchKernelGGL(win_pair_weights_kernel<0>, grid, dim3(NTW), 0, s, w, c, d, opp, K, H, W);
   return launch_status("grr_win_pair_weights");
 }
 
