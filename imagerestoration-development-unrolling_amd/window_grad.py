@@ -113,20 +113,25 @@ class _WindowSolve(torch.autograd.Function):
         n_st = alpha.shape[0]
         xs: List[Tensor] = []
         us: List[Tensor] = []
+        # linear GTV passes on pair weights (as inference, window_graph.MixtureGTV.solve); the prox
+        # rhs and the reverse use the raw directed weights
+        from .window_graph import WIN_PAIR_WEIGHTS as pair
+        cG = K.win_pair_weights(wG, delta) if pair else wG
 
         def stages(rhs, ks):
             x, u = rhs, None
             for k in ks:
                 xs.append(x)
-                x, u = K.win_solver(0, x, rhs, wG, tG, ro, delta, g, fs, wL=wL, tapsL=tL, mu=mu, alpha=alpha[k],
-                                    beta=beta[k] if u is not None else None, u_prev=u, want_u=True)
+                x, u = K.win_solver(0, x, rhs, cG, tG, ro, delta, g, fs, wL=wL, tapsL=tL, mu=mu, alpha=alpha[k],
+                                    beta=beta[k] if u is not None else None, u_prev=u, want_u=True, pair=pair)
                 us.append(u)
             return x
 
-        r0, _ = K.win_solver(1, y, y, wG, tG, ro, delta, g, fs)
+        r0, _ = K.win_solver(1, y, y, cG, tG, ro, delta, g, fs, pair=pair)
         x2 = stages(r0, [0, 1])
         r1, _ = K.win_solver(2, x2, y, wG, tG, ro, delta, g, fs, log_gamma=lg)
         out = stages(r1, list(range(2, n_st)))
+        del cG
         ctx.spec, ctx.n_st = spec, n_st
         ctx.save_for_backward(y, feat, wG, wL, tG, tL, x2, *params, *xs, *us)
         return out
