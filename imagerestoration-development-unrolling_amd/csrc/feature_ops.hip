@@ -400,14 +400,18 @@ struct X3Args {
   const uint16_t* frag;    // [nch][x3_chunk_bytes / 2]
   float* out;              // [B, M, P]
   int64_t P;
-  int K, M, nch, tiles;    // tiles: 128-pixel tiles per image
+  int K, M, nch, tiles;    // tiles: X3_PX-pixel tiles per image
   uint32_t nblk;
 };
 
 __device__ float g_x3_scratch[64];
 
+#ifndef GRR_X3_WAVES   // waves (32-pixel columns) per workgroup: the W chunk images DMA'd once serve them all
+#define GRR_X3_WAVES 8
+#endif
+constexpr int X3_WV = GRR_X3_WAVES, X3_PX = 32 * X3_WV;   // pixels per workgroup
 template <int KS, bool LN>
-__global__ __launch_bounds__(256) void gemm_x3_kernel(X3Args a) {
+__global__ __launch_bounds__(64 * X3_WV) void gemm_x3_kernel(X3Args a) {
   extern __shared__ __attribute__((aligned(16))) float x3_lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(X3Args a) {
   const int b = lb / a.tiles, tile = lb - b * a.tiles;
   const int64_t P = a.P;
   const int K = a.K, M = a.M, r = lane & 31, hf = lane >> 5;
-  const int64_t p = (int64_t)tile * 128 + wave * 32 + r;
+  const int64_t p = (int64_t)tile * X3_PX + wave * 32 + r;
   const bool pin = p < P;
   const int64_t pc = pin ? p : P - 1;
   const int NIW = x3_niw(KS);
@@ -426,8 +430,9 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(X3Args a) {
   auto issue = [&](int c) {        // chunk c -> slot c & 1 (16-byte LDS-DMA, lane-linear)
     float* slot = x3_lds + (c & 1) * (CB / 4);
     const char* src = fragb + (int64_t)c * CB;
-    for (int i = 0; i < NIW; ++i) {
-      const int img = i * 4 + wave;
+    for (int i = 0; i < (NIW * 4 + X3_WV - 1) / X3_WV; ++i) {
+      const int img = i * X3_WV + wave;
+      if (X3_WV > 4 && img >= NIW * 4) break;   // the chunk holds NIW * 4 images
       __builtin_amdgcn_global_load_lds((const void*)(src + img * 1024 + lane * 16),
                                        (__attribute__((address_space(3))) void*)(slot + img * 256), 16, 0, 0);
     }
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(X3Args a) {
 
   float* const obase = a.out + (int64_t)b * M * P;
   // full tile: every lane's pixel in range -> stores through a uniform row base + 32-bit offset
-  const bool full_px = (int64_t)tile * 128 + 128 <= P;
+  const bool full_px = (int64_t)tile * X3_PX + X3_PX <= P;
   const uint32_t so = (uint32_t)((4 * hf) * P + r) * 4u;
   for (int c = 0; c < nch; ++c) {
     // chunk c landed (this wave's DMAs; later ops: the previous chunk's stores), then all waves'
@@ -520,7 +525,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(X3Args a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int m0 = c * X3_MCH + t * 32 + (i & 3) + 8 * (i >> 2);
-          float* row = obase + (int64_t)m0 * P + (int64_t)tile * 128 + wave * 32;
+          float* row = obase + (int64_t)m0 * P + (int64_t)tile * X3_PX + wave * 32;
           *reinterpret_cast<float*>(reinterpret_cast<char*>(row) + so) = acc[t][i] * rstd;
         }
     } else {
@@ -543,7 +548,7 @@ static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, in
   X3Args a{};
   a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M;
   a.nch = (M + X3_MCH - 1) / X3_MCH;
-  a.tiles = (int)((P + 127) / 128);
+  a.tiles = (int)((P + X3_PX - 1) / X3_PX);
   const uint64_t n = (uint64_t)B * a.tiles;
   GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   a.nblk = (uint32_t)n;
@@ -551,7 +556,7 @@ static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, in
   const size_t lds = 2 * (size_t)x3_chunk_bytes(KS);
   switch (KS) {
 #define GRR_X3_CASE(ks) \
-    case ks: hipLaunchKernelGGL((gemm_x3_kernel<ks, LN>), dim3(a.nblk), dim3(256), lds, s, a); break;
+    case ks: hipLaunchKernelGGL((gemm_x3_kernel<ks, LN>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
     GRR_X3_CASE(1) GRR_X3_CASE(2) GRR_X3_CASE(3) GRR_X3_CASE(4)
     GRR_X3_CASE(5) GRR_X3_CASE(6) GRR_X3_CASE(7) GRR_X3_CASE(8)
 #undef GRR_X3_CASE
