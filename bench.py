@@ -5,7 +5,8 @@
 One "step" = one forward of the image-domain GGTV-GGLR filter (MultiScaleGraphFilter,
 G=32 graphs x F=3, C=96, S=10 unrolled stages, v13 feature CNN; SURVEY.md §8(d) "P")
 over one per-GPU batch of B=64 synthetic noisy patches already resident in HBM.
-N>1: one process per GPU (torchrun), each rank filters its own batch (the path shards
+N>1: one process per GPU (under torchrun, or spawned by this script when started plainly with
+--gpus N: benchlib.join_or_spawn), each rank filters its own batch (the path shards
 by patch — no data-path collective; scaling "weak"); the timed region is bracketed by
 barrier + synchronize on both sides and the max over ranks is reported.
 
@@ -205,22 +206,18 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary workload (v1.0 AbtractMultiScaleGraphFilter, SURVEY.md §8d 'D')")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: every rank prints its rank / world and exits (no HIP)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; GRR_BENCH_BACKEND=gloo and a device count below the rank count are
-    # only for rehearsing the multi-rank path on a one-GPU box (ranks then share cuda:0)
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % max(ndev, 1))
-    if world > 1:
-        torch.cuda.set_device(dev)
-        backend = os.environ.get("GRR_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev)
-        else:
-            torch.distributed.init_process_group(backend)
+    # --gpus N: one process per GPU.  Under torchrun the ranks exist already (WORLD_SIZE must
+    # equal N); started plainly, this process spawns the N ranks and exits with their status
+    import benchlib
+    world, rank, local = benchlib.join_or_spawn(args.gpus, dry_run=args.dry_run)
+    if args.dry_run:
+        benchlib.dry_run_report(world, rank, local)
+        return
+    dev = benchlib.init(world, local)
 
     import irdu_amd
     from irdu_amd import kernels as K
@@ -232,9 +229,7 @@ def main():
     noisy = noisy.to(dev)
 
     def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize(dev)
+        benchlib.barrier(world, dev)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -261,13 +256,10 @@ def main():
         GF.FEATURE_STREAMS = saved
         n_inst = max(1, min(args.steps, 5))
     kern = timer.summary()
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    rank_dts = [r[0] for r in benchlib.gather_floats([dt], world, dev)]
+    dt = benchlib.max_over_ranks(dt, world, dev)
     if rank != 0:
-        if world > 1:
-            torch.distributed.destroy_process_group()
+        benchlib.finish(world)
         return
 
     px_total = world * b * H * W * args.steps
@@ -310,6 +302,9 @@ def main():
                       "global_batch": world * b, "per_gpu_batch": b, "image": f"{H}x{W}x{CIN}",
                       "parallelism": f"batch-sharded x{world}, no collective in the data path"},
            "roofline": roofline}
+    if world > 1:
+        res["ranks"] = {"backend": benchlib.backend(), "visible_gpus": torch.cuda.device_count(),
+                        "ms_per_step_per_rank": [round(d / args.steps * 1e3, 3) for d in rank_dts]}
     if "lnb" in kern:   # the MFMA-bound feature CNN: fp32-accurate split-bf16 GEMMs + depthwise + gate
         lnb = kern["lnb"]
         res["roofline_secondary"] = {
@@ -344,9 +339,8 @@ def main():
                        "weights": ("tests/golden/msgf_trained_g32_s10.safetensors (trained here: no reference "
                                    "checkpoint exists)") if os.path.exists(TRAINED) else "reference init"}
         res["speedup_vs_cpu"] = round(value / world / cb["value"], 1)
-    print(json.dumps(res))
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    print(json.dumps(res), flush=True)
+    benchlib.finish(world)
 
 
 if __name__ == "__main__":

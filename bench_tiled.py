@@ -29,44 +29,43 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--gather", action="store_true")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; spawned when not under torchrun)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher check: ranks report and exit (no HIP)")
     args = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # GRR_BENCH_BACKEND=gloo + fewer GPUs than ranks: multi-rank rehearsal on a one-GPU box
-    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
-    if world > 1:
-        torch.cuda.set_device(dev)
-        backend = os.environ.get("GRR_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev)
-        else:
-            torch.distributed.init_process_group(backend)
+    import benchlib
+    world, rank, local = benchlib.join_or_spawn(args.gpus, dry_run=args.dry_run)
+    if args.dry_run:
+        benchlib.dry_run_report(world, rank, local)
+        return
+    dev = benchlib.init(world, local)
     import irdu_amd
     from irdu_amd import tiling
-    from bench import build_model, synthetic_patches
+    from bench import TRAINED, build_model, synthetic_patches
     irdu_amd.load_native()
-    model = build_model(dev)
+    trained = os.path.exists(TRAINED)
+    model = build_model(dev, trained=trained)
     _, noisy = synthetic_patches(args.images, seed=2204, h=args.size, w=args.size)
     noisy = noisy.to(dev)
     run = lambda: tiling.tiled_forward(model, noisy, tile=args.tile, halo=args.halo, align=16,  # noqa: E731
                                        micro_batch=args.micro_batch, gather=args.gather)
     run()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
+    benchlib.barrier(world, dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    benchlib.barrier(world, dev)
+    dt = benchlib.max_over_ranks(time.perf_counter() - t0, world, dev)
     nwin = len(tiling.tile_grid(args.size, args.size, args.tile, args.halo, 16))
+    parity = None
+    if world == 1:
+        # tiled vs the whole image in one launch (image 0): the halo's effect on the output
+        with torch.no_grad():
+            tiled = run()[:1]
+            whole = model(noisy[:1])
+        ref = whole.abs().max().item()
+        parity = {"image": "0 of the batch", "max_abs_err_vs_whole": (tiled - whole).abs().max().item(),
+                  "rel_err_vs_whole": (tiled - whole).abs().max().item() / ref,
+                  "weights": "trained fixture" if trained else "reference init"}
     if rank == 0:
         px = args.images * args.size * args.size * args.steps
         print(json.dumps({"metric": "tiled inference MPix/s (output pixels)", "value": round(px / dt / 1e6, 3),
@@ -75,9 +74,11 @@ def main():
                                                  f"{args.halo}, G=32 F=3 S=10 image filter",
                                      "windows_per_image": nwin,
                                      "window_overhead": round(nwin * args.tile ** 2 / args.size ** 2, 3),
-                                     "parallelism": f"windows sharded x{world}"}}))
-    if world > 1:
-        torch.distributed.destroy_process_group()
+                                     "weights": "tests/golden/msgf_trained_g32_s10.safetensors" if trained
+                                     else "reference init",
+                                     "parallelism": f"windows sharded x{world}"},
+                          "tiled_vs_whole": parity}), flush=True)
+    benchlib.finish(world)
 
 
 if __name__ == "__main__":

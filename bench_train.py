@@ -97,20 +97,16 @@ def main():
                     help="CPU-baseline patch side (default: --size for msgf, 128 for the v1.0 model)")
     ap.add_argument("--fused-fts", type=str, default=None,
                     help="comma list of F that use the one-pass term reverses (default: all instances)")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; spawned when not under torchrun)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher check: ranks report and exit (no HIP)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # GRR_BENCH_BACKEND=gloo + fewer GPUs than ranks: multi-rank rehearsal on a one-GPU box
-    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
-    if world > 1:
-        torch.cuda.set_device(dev)
-        backend = os.environ.get("GRR_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev)
-        else:
-            torch.distributed.init_process_group(backend)
+    import benchlib
+    world, rank, local = benchlib.join_or_spawn(args.gpus, dry_run=args.dry_run)
+    if args.dry_run:
+        benchlib.dry_run_report(world, rank, local)
+        return
+    dev = benchlib.init(world, local)
 
     import irdu_amd
     from irdu_amd import kernels as K
@@ -133,9 +129,7 @@ def main():
     clean_hwc = clean.permute(0, 2, 3, 1).contiguous().to(dev)
 
     def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize(dev)
+        benchlib.barrier(world, dev)
 
     for _ in range(args.warmup):
         tr.step(noisy_hwc, clean_hwc)
@@ -150,10 +144,7 @@ def main():
     dt = time.perf_counter() - t0
     K.set_timer(None)
     kern = timer.summary()
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    dt = benchlib.max_over_ranks(dt, world, dev)
     if rank == 0:
         px = world * args.batch * args.size * args.size * args.steps
         hip_ms = sum(v["total_ms"] for v in kern.values()) / args.steps
@@ -176,9 +167,8 @@ def main():
             for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
                 print(f"{k:20s} launches/step={v['launches'] / args.steps:6.1f} mean={v['mean_ms']:8.3f} ms "
                       f"algo={v['gbps']:8.1f} GB/s", file=sys.stderr)
-        print(json.dumps(res))
-    if world > 1:
-        torch.distributed.destroy_process_group()
+        print(json.dumps(res), flush=True)
+    benchlib.finish(world)
 
 
 if __name__ == "__main__":

@@ -145,6 +145,9 @@ class OverlappedGradReducer:
     waits for its predecessors), so ranks issue identical collective sequences.
     ``finish()`` launches what backward never reached (parameters without a gradient this
     step contribute zeros), waits, and writes the averages back into ``.grad``.
+    ``prepare()`` starts a step: it drains anything a step left behind (an exception between
+    backward and ``finish()``) and resets the bucket state, so a stale step can never leak into
+    the next one's averages; a second backward inside one step raises instead of reducing twice.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 32.0, group=None):
@@ -165,9 +168,19 @@ class OverlappedGradReducer:
         self._work = [None] * len(self.buckets)
         self._flat = [None] * len(self.buckets)
 
+    def prepare(self) -> None:
+        """Begin a step (call before loss.backward())."""
+        for w in self._work:
+            if w is not None:
+                w.wait()
+        self._reset()
+
     def _on_grad(self, p):
         i = self._bucket_of[id(p)]
         self._pending[i] -= 1
+        if self._pending[i] < 0:
+            raise RuntimeError("OverlappedGradReducer: a parameter's gradient arrived twice in one step "
+                               "(a second backward without finish(); call prepare() at the start of each step)")
         while self._next < len(self.buckets) and self._pending[self._next] <= 0:
             self._launch(self._next)
             self.launched_in_backward += 1

@@ -203,9 +203,11 @@ class ResumeableSampler(Sampler):
         self.current_sample = current_sample
         self.dataset.random_permute(seed=2024 + current_epoch)
 
-    def steps_per_epoch(self) -> int:
-        """Optimisation steps one epoch holds (a partial last batch counts when world_size == 1)."""
-        return -(-(self.num_samples // self.world_size) // self.batch_size)
+    def steps_per_epoch(self, drop_last: bool = False) -> int:
+        """Optimisation steps one epoch holds: a partial last batch counts unless the loader drops
+        it (dataloader_args.drop_last); with world_size > 1 there is none (whole global batches)."""
+        local = self.num_samples // self.world_size
+        return local // self.batch_size if drop_last else -(-local // self.batch_size)
 
 
 def create_dataset(dataset_conf: dict, environ_conf: dict):
@@ -286,6 +288,7 @@ class Trainer:
         """noisy/clean: [B,H,W,C] batches as the dataset yields them (permuted like :191-193)."""
         self.model.train()
         self.optimizer.zero_grad(set_to_none=True)
+        self.reducer.prepare()
         noisy = noisy_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
         clean = clean_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
         loss = self.loss(noisy, clean)
@@ -332,12 +335,24 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
     loader = create_dataloader(dataset, sampler, ds_conf, conf)
     trainer = Trainer(build_model(conf.get("model", {})), tconf, device)
     ckpt_path = conf["path"].get("latest_checkpoint_path") or latest_checkpoint(conf)
-    spe = sampler.steps_per_epoch()
+    if world > 1:
+        # every rank resumes rank 0's choice of checkpoint (ranks never pick their own latest file:
+        # without a shared view they could resume at different iterations and block forever in the
+        # gradient all-reduce)
+        choice = [ckpt_path]
+        torch.distributed.broadcast_object_list(choice, src=0)
+        ckpt_path = choice[0]
+    spe = sampler.steps_per_epoch(bool(ds_conf["dataloader_args"].get("drop_last", False)))
     if spe <= 0:
         raise ValueError(f"dataset of {len(dataset)} samples holds no batch of {bs} x {world} ranks")
     if ckpt_path:
         trainer.load_state_dict(torch.load(ckpt_path, map_location=device, weights_only=True))
         LOG.info("resumed from %s at iteration %d", ckpt_path, trainer.i)
+    if world > 1:
+        its = [None] * world
+        torch.distributed.all_gather_object(its, trainer.i)
+        if len(set(its)) != 1:
+            raise RuntimeError(f"ranks resumed at different iterations {its} from {ckpt_path!r}")
     # replicas start identical whatever each rank's seed was (data-parallel averaging never
     # reconciles diverged weights); rank 0's weights are the ones checkpointed
     sharding.broadcast_module(trainer.model)
@@ -358,15 +373,20 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
     start_i, saved_at = trainer.i, None
     while trainer.i < total:
         sampler.set_epoch_and_current_sample(epoch, done_in_epoch * bs * world - 1)
+        stepped = False
         for noisy, clean in loader:
             if trainer.i >= total:
                 break
             loss = trainer.step(noisy, clean)
+            stepped = True
             if rank == 0 and trainer.i % verbose == 0:
                 LOG.info("iter=%d loss=%.6f lr=%.3e", trainer.i, loss, trainer.optimizer.param_groups[0]["lr"])
             if trainer.i % every == 0:
                 save()
                 saved_at = trainer.i
+        if not stepped and trainer.i < total:
+            raise RuntimeError(f"epoch {epoch} yielded no batch (dataset {len(dataset)}, batch {bs}, "
+                               f"{world} ranks, drop_last {ds_conf['dataloader_args'].get('drop_last', False)})")
         epoch, done_in_epoch = epoch + 1, 0
     if trainer.i > start_i and saved_at != trainer.i:     # the final state is always on disk
         save()

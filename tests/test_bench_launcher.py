@@ -1,0 +1,74 @@
+"""bench.py / bench_train.py / bench_tiled.py --gpus N: the N ranks exist whether the script is
+started under torchrun or plainly (benchlib.join_or_spawn).  CPU-only: --dry-run ranks report
+their rank and world without loading HIP."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "GRR_BENCH_BACKEND")}
+    env.update(kw)
+    return env
+
+
+def _run(script, args, env):
+    return subprocess.run([sys.executable, os.path.join(ROOT, script)] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=180)
+
+
+@pytest.mark.parametrize("script", ["bench.py", "bench_train.py", "bench_tiled.py"])
+def test_plain_start_spawns_n_ranks(script):
+    r = _run(script, ["--gpus", "2", "--dry-run"], _env())
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 and d["local_rank"] == d["rank"] for d in lines)
+    assert len({d["master"] for d in lines}) == 1 and lines[0]["master"].startswith("127.0.0.1:")
+
+
+def test_single_gpu_dry_run_does_not_spawn():
+    r = _run("bench.py", ["--dry-run"], _env())
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines == [{"dry_run": True, "rank": 0, "local_rank": 0, "world": 1, "master": ":"}]
+
+
+def test_torchrun_world_must_match_gpus():
+    r = _run("bench.py", ["--gpus", "4", "--dry-run"], _env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def test_torchrun_rank_reports_itself():
+    r = _run("bench.py", ["--gpus", "2", "--dry-run"],
+             _env(WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29555"))
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (d["rank"], d["world"], d["master"]) == (1, 2, "127.0.0.1:29555")
+
+
+def test_more_ranks_than_gpus_is_refused():
+    # no GPU in this container: 2 RCCL ranks cannot each own a device -> refused before spawning
+    r = _run("bench.py", ["--gpus", "2"], _env())
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr
+
+
+def test_child_failure_propagates(tmp_path):
+    script = tmp_path / "child.py"
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import benchlib\n"
+        "w, r, l = benchlib.join_or_spawn(2, dry_run=True)\n"
+        "sys.exit(3 if r == 1 else 0)\n")
+    r = subprocess.run([sys.executable, str(script)], env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3
+    assert "rank exit codes [0, 3]" in r.stderr

@@ -7,6 +7,7 @@ full-batch gradients" is tested on the real path's math.
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -70,6 +71,24 @@ def _worker(rank, world_size, port, result_q):
         nb2 = red.finish()
         early = red.launched_in_backward
         grads2 = {k: (p.grad * world_size).numpy() for k, p in params2.items()}
+        # a second backward without finish() raises (no stale bucket state leaks into a step);
+        # prepare() drains the aborted step, and the next step averages exactly as before
+        for p in params2.values():
+            p.grad = None
+        red.prepare()
+        _loss(params2, xs, ts).backward()
+        raised = False
+        try:
+            _loss(params2, xs, ts).backward()
+        except RuntimeError as e:
+            raised = "arrived twice" in str(e)
+        for p in params2.values():
+            p.grad = None
+        red.prepare()
+        _loss(params2, xs, ts).backward()
+        red.finish()
+        again = max(float(abs(p.grad * world_size - torch.from_numpy(grads2[k])).max()) for k, p in params2.items())
+        grads2["_guard"] = np.array([float(raised), again])
         # PSNR reduction across ranks
         clean = torch.rand(4, 3, 8, 8)
         rest = (clean + 0.02 * torch.randn(4, 3, 8, 8)).clamp(0, 1)
@@ -101,6 +120,8 @@ def test_data_parallel_gradients_match_single_process():
     rest = (clean + 0.02 * torch.randn(4, 3, 8, 8)).clamp(0, 1)
     full_psnr = sharding.global_psnr_ubyte(rest, clean)
     for rank, nb, grads, psnr, nb2, early, grads2 in results:
+        raised, again = grads2.pop("_guard")
+        assert raised == 1.0 and again == 0.0
         assert nb > 1 and nb2 == nb  # several buckets exercised
         assert early >= 1            # buckets were reduced while backward was still running
         for k, p in params.items():

@@ -93,6 +93,21 @@ def test_resumeable_sampler_resumes_and_shards():
     assert parts[0] == [0, 1, 4, 5] and parts[1] == [2, 3, 6, 7]
     assert T.ResumeableSampler(ds, batch_size=2, rank=0, world_size=2).steps_per_epoch() == 2
     assert T.ResumeableSampler(ds, batch_size=4).steps_per_epoch() == 3      # partial last batch (1 rank)
+    assert T.ResumeableSampler(ds, batch_size=4).steps_per_epoch(drop_last=True) == 2   # loader drops it
+    assert T.ResumeableSampler(ds, batch_size=16).steps_per_epoch(drop_last=True) == 0
+
+
+def test_run_with_drop_last_counts_whole_batches(tmp_path, monkeypatch):
+    """dataloader_args.drop_last: the epoch length is floor(n / batch) (2 steps of 4 of 10 samples), so
+    resume offsets and epoch boundaries follow the loader; a dataset smaller than one batch raises."""
+    conf = _tiny_conf(tmp_path, 5)
+    conf["datasets"]["train"]["dataloader_args"]["drop_last"] = True
+    tr = _run_tiny(monkeypatch, conf)
+    assert tr.i == 5
+    small = _tiny_conf(tmp_path / "s", 3, bs=4, n=3)
+    small["datasets"]["train"]["dataloader_args"]["drop_last"] = True
+    with pytest.raises(ValueError, match="holds no batch"):
+        _run_tiny(monkeypatch, small)
 
 
 def test_lr_schedule_matches_reference_formula():
@@ -222,6 +237,37 @@ def _run_worker(rank, world, port, root, q):
         q.put((rank, tr.i, {k: v.detach().numpy() for k, v in tr.model.state_dict().items()}))
     finally:
         dist.destroy_process_group()
+
+
+def _resume_worker(rank, world, port, roots, q):
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        T.build_model = lambda _c: (torch.manual_seed(rank), TinyModel())[1]
+        tr = T.run(_tiny_conf(roots[rank], 7, bs=2, n=10), device=torch.device("cpu"))
+        q.put((rank, tr.i, {k: v.detach().numpy() for k, v in tr.model.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_resume_follows_rank0_checkpoint(tmp_path, monkeypatch):
+    """Only rank 0's checkpoint folder holds a checkpoint (iteration 4): both ranks resume from rank
+    0's file (broadcast choice), run to 7 in lock step and end with identical weights."""
+    _run_tiny(monkeypatch, _tiny_conf(tmp_path / "r0", 4, bs=2, n=10))
+    roots = [str(tmp_path / "r0"), str(tmp_path / "r1")]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resume_worker, args=(r, 2, port, roots, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (i, sd) for r, i, sd in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0] == 7
+    for k in res[0][1]:
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k
 
 
 def test_data_parallel_run_over_epochs_stays_in_sync(tmp_path):
