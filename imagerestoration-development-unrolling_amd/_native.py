@@ -73,6 +73,12 @@ SIGNATURES = {
     "grr_glr_op_l_norm": [P, P, P, I, I, I, I, I, P],
     "grr_gtv_op_c": [P, P, Stencil, P, I, I, I, I, I, P],
     "grr_gtv_op_c_transpose": [P, P, Stencil, P, P, I, I, I, I, I, P],
+    "grr_neighbor_gather_bwd": [P, P, I, I, I, I, P],
+    "grr_normalize_features_bwd": [P, P, P, P, P, I, I, I, I, I, P],
+    "grr_stats_conv_bwd": [P, Stencil, I, P, P, P, I, I, I, I, I, P],
+    "grr_glr_op_l_norm_bwd": [P, P, P, P, P, I, I, I, I, I, P],
+    "grr_gtv_op_c_bwd": [P, P, Stencil, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_gtv_op_c_transpose_bwd": [P, P, Stencil, P, P, P, P, P, P, I, I, I, I, I, P],
     # reverse pass
     "grr_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
     "grr_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],

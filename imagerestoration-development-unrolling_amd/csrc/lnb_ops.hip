@@ -390,6 +390,319 @@ __global__ __launch_bounds__(512, head_wgs(KS)) void lnb_head_kernel(LnbHeadArgs
 }
 
 // ---------------------------------------------------------------------------
+// head16: LN + W1 + dw3x3 + gate with GEMM1 on fp16 two-term splits (C <= 96)
+//
+// GEMM1 h = (W1 diag ln_w)(x / sigma) runs on v_mfma_f32_32x32x16_f16 with both operands as
+// exact two-term fp16 splits a = a_hi + a_lo (22 significant bits) and three products
+// (a_lo b_hi, a_hi b_lo, a_hi b_hi; the dropped a_lo b_lo is below 2^-22 |a b|): the products
+// are exact in the fp32 accumulator, so each term's error is the 2^-22 representation error,
+// the order of fp32 rounding in a K-deep fp32 sum (tests/test_gpu_parity.py:
+// test_x3_gemm_is_fp32_accurate bounds the block against float64).  fp16 has a narrow exponent
+// range, so both operands are power-of-two scaled, exactly: every W1 row by 2^s_row (its largest
+// entry into [2^13, 2^14)), every halo pixel's x / sigma by 2^XE (2^e_p for a pixel whose
+// largest |x / sigma| leaves [2^-10, 2^4)).  h is stored as 2^(s_row + XE) h (pixels with
+// e_p != XE are rescaled once when their h goes to LDS) and the depthwise taps are packed as
+// tap 2^-(s_row + XE), so the depthwise sums -- and everything after -- are the unscaled values.
+//
+// Against the bf16 head (lnb_head_kernel): half the MFMA products for the same fp32-class
+// accuracy, and 32x32x16 MFMAs (they hold the SIMD's vector issue 8 of 32 cycles instead of
+// 8 of 16), so the partner wave's depthwise + gate gets the issue slots.  Tile as before (32 x
+// 13 outputs, 34 x 15 halo pixels); a chunk is 16 (mask, value) pairs = 32 GEMM rows; the h of
+// a chunk lives in LDS as 16 pair planes ((m, v) interleaved per halo pixel: one ds_write_b64
+// per pair of accumulator registers, one ds_read_b64 per tap column in the gate), double
+// buffered (2 x 64 KB); the W1 fragments + taps of a chunk arrive by LDS-DMA in a 2-slot ring
+// one chunk ahead (the taps of the chunk the gate needs next are copied to registers first).
+constexpr int L6_NP = 16;                   // (mask, value) pairs per chunk
+constexpr int L6_NB = 2;                    // 32-pixel GEMM1 blocks per wave
+constexpr int L6_NH = 8 * L6_NB * 32;       // halo pixels of a tile (512; 510 used)
+constexpr int L6_HR = L6_NH / LH_HWD;       // halo rows (15)
+constexpr int L6_TH = L6_HR - 2;            // output rows (13)
+constexpr int L6_RA = (L6_TH + 1) / 2;      // output rows per lane half in the gate (7)
+constexpr int L6_PP = 2 * L6_NH;            // floats per pair plane
+constexpr int L6_HBUF = L6_NP * L6_PP;      // floats per h buffer (64 KB)
+constexpr int L6_XE = 10;                   // common power-of-two scale of the fp16 x operand
+constexpr int L6_TAPF = L6_NP * 18;         // tap floats per chunk
+__host__ __device__ constexpr int head16_images(int KS) { return 2 * KS + 2; }   // fp16 hi/lo per k-step + 2 tap images
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// largest |W1 diag(ln_w)| entry of GEMM row `row` (folded over the R replicas) -> its scale exponent
+__device__ __forceinline__ int head16_row_exp(const float* __restrict__ w1, const float* __restrict__ ln_w, int row,
+                                              int C, int R) {
+  const float* wr = w1 + (int64_t)row * (R * C);
+  float mx = 0.f;
+  for (int k = 0; k < C; ++k) {
+    float v = wr[k] * ln_w[k];
+    for (int rep = 1; rep < R; ++rep) v += wr[rep * C + k] * ln_w[rep * C + k];
+    mx = fmaxf(mx, fabsf(v));
+  }
+  if (mx == 0.f) return 0;
+  int e;
+  frexpf(mx, &e);                 // mx < 2^e
+  return clampi(14 - e, -60, 60); // mx 2^s in [2^13, 2^14)
+}
+
+// Per chunk c (16 pairs): for k-step s (16 deep) two 1-KB images of 32x32x16 A fragments
+// (term q = 0 hi, 1 lo; lane l, element j: GEMM row r = l & 31 -- pair 16 c + (r >> 1), mask
+// (r even) or value (r odd) channel -- and k = 16 s + 8 (l >> 5) + j), then two fp32 images with
+// the depthwise taps, [pair w][tap t][mask, value], scaled by 2^-(s_row + XE).
+__global__ void lnb_w1_pack16_kernel(const float* __restrict__ w1, const float* __restrict__ ln_w,
+                                     const float* __restrict__ wdw, char* __restrict__ out, int C, int hid, int KS,
+                                     int nch, int R) {
+  const int NI = head16_images(KS);
+  const int64_t n = (int64_t)nch * NI * 256;        // 32-bit words
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i >> 8;
+    const int e = (int)(i & 255), c = (int)(img / NI), im = (int)(img % NI);
+    uint32_t word = 0;
+    if (im < 2 * KS) {
+      const int q = im & 1, s = im >> 1, l = e >> 2, r = l & 31, pj = L6_NP * c + (r >> 1);
+      if (pj < hid) {
+        const int row = (r & 1 ? hid : 0) + pj;
+        const int sc = head16_row_exp(w1, ln_w, row, C, R);
+        const float* wr = w1 + (int64_t)row * (R * C);
+        uint16_t hb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int k = 16 * s + 8 * (l >> 5) + 2 * (e & 3) + u;
+          float v = 0.f;
+          if (k < C) {
+            v = wr[k] * ln_w[k];
+            for (int rep = 1; rep < R; ++rep) v += wr[rep * C + k] * ln_w[rep * C + k];
+          }
+          const float vs = ldexpf(v, sc);
+          const _Float16 h0 = (_Float16)vs;
+          const _Float16 t = q == 0 ? h0 : (_Float16)(vs - (float)h0);
+          hb[u] = __builtin_bit_cast(uint16_t, t);
+        }
+        word = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16);
+      }
+    } else {
+      const int e2 = (im - 2 * KS) * 256 + e;
+      if (e2 < L6_TAPF) {
+        const int w = e2 / 18, t = (e2 % 18) >> 1, comp = e2 & 1, pj = L6_NP * c + w;
+        if (pj < hid) {
+          const int row = (comp ? hid : 0) + pj;
+          const int sc = head16_row_exp(w1, ln_w, row, C, R);
+          word = __float_as_uint(ldexpf(wdw[(int64_t)row * 9 + t], -(sc + L6_XE)));
+        }
+      }
+    }
+    reinterpret_cast<uint32_t*>(out)[i] = word;
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
+  constexpr int NB = L6_NB, RA = L6_RA;
+  constexpr int NI = head16_images(KS);
+  constexpr int DPW = (NI + 7) / 8;      // LDS-DMA instructions per wave per chunk
+  constexpr int SLOTF = NI * 256;        // floats per ring slot
+  __shared__ __attribute__((aligned(16))) float smem[2 * L6_HBUF + 2 * SLOTF];
+  float* const ring = smem + 2 * L6_HBUF;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int tx = lb % a.tiles_x; lb /= a.tiles_x;
+  const int ty = lb % a.tiles_y;
+  const int b = lb / a.tiles_y;
+  const int H = a.H, W = a.W, C = a.C, hid = a.hid, nch = a.nch;
+  const int HW = H * W;
+  const int y0 = ty * L6_TH, x0 = tx * LH_TW;
+
+  auto issue = [&](int chunk, int slot_idx) {
+    float* slot = ring + slot_idx * SLOTF;
+    const char* src = a.w1f + (int64_t)chunk * NI * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int img = min(i * 8 + wave, NI - 1);   // surplus waves repeat the last image
+      dma16_opaque(src + img * 1024, slot + img * 256);
+    }
+  };
+  issue(0, 0);
+
+  // this wave's halo pixels (block blk: pixel q = (wave NB + blk) 32 + (lane & 31)); lane half kh
+  // holds channels 16 s + 8 kh + j of it
+  const int kh = lane >> 5;
+  f16x8 xh[NB][KS], xl[NB][KS];
+  float corr[NB];
+  bool any_corr = false;
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) {
+    const int q = min((wave * NB + blk) * 32 + (lane & 31), L6_HR * LH_HWD - 1);
+    const int hy = q / LH_HWD, hx = q - hy * LH_HWD;
+    const int gy = clampi(y0 - 1 + hy, 0, H - 1), gx = clampi(x0 - 1 + hx, 0, W - 1);
+    const float* xp = a.x + (int64_t)b * C * HW + gy * W + gx;
+    float xv[KS][8];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s + 8 * kh + j;
+        const float v = xp[(int64_t)min(k, C - 1) * HW];
+        xv[s][j] = k < C ? v : 0.f;
+      }
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += xv[s][j];
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / (float)C;
+    float sq = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = 16 * s + 8 * kh + j < C ? xv[s][j] - mean : 0.f;
+        sq += d * d;
+      }
+    sq += __shfl_xor(sq, 32);
+    const float rstd = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xv[s][j] *= rstd;                       // x / sigma (REF:921)
+        mx = fmaxf(mx, fabsf(xv[s][j]));
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    int ep = L6_XE;
+    if (mx != 0.f) {
+      int e;
+      frexpf(mx, &e);                         // mx < 2^e
+      if (e > 14 - L6_XE || e < -L6_XE) ep = clampi(14 - e, -100, 100);
+    }
+    corr[blk] = ldexpf(1.0f, L6_XE - ep);
+    any_corr |= ep != L6_XE;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = ldexpf(xv[s][j], ep);
+        const _Float16 h0 = (_Float16)v;
+        xh[blk][s][j] = h0;
+        xl[blk][s][j] = (_Float16)(v - (float)h0);
+      }
+  }
+  // wave-uniform (scalar branch at the h store; almost never taken on LayerNorm'd inputs)
+  const bool wave_corr = __builtin_amdgcn_readfirstlane((int)__any(any_corr)) != 0;
+
+  // GEMM1 of chunk c (ring slot c & 1) -> pair planes of h buffer c & 1
+  auto gemm1 = [&](int c) {
+    if (c >= nch) return;
+    const float* slot = ring + (c & 1) * SLOTF + lane * 4;
+    f32x16 acc[NB];
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) acc[blk] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(slot + (2 * s + 0) * 256);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(slot + (2 * s + 1) * 256);
+#pragma unroll
+      for (int blk = 0; blk < NB; ++blk) {
+        acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh[blk][s], acc[blk], 0, 0, 0);
+        acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl[blk][s], acc[blk], 0, 0, 0);
+        acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[blk][s], acc[blk], 0, 0, 0);
+      }
+    }
+    float* hb = smem + (c & 1) * L6_HBUF;
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      if (wave_corr) acc[blk] *= corr[blk];
+      const int q = (wave * NB + blk) * 32 + (lane & 31);
+      // registers 2u, 2u + 1 = rows r, r + 1 (r even: mask, value of pair r / 2)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = ((2 * u) & 3) + 8 * ((2 * u) >> 2) + 4 * kh;
+        *reinterpret_cast<f32x2*>(hb + (r >> 1) * L6_PP + 2 * q) = f32x2{acc[blk][2 * u], acc[blk][2 * u + 1]};
+      }
+    }
+  };
+
+  // gate phase mapping: this wave's pairs 2 wave, 2 wave + 1; lane = (output column, row half)
+  const int col = lane & 31, r0 = kh * RA;
+  const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+      a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
+  const int gx = x0 + col;
+  const int nrow = min(L6_TH, H - y0) - r0;      // output rows of this lane's half inside the tile and image
+  float tp[2][18];                               // taps of the chunk the next gate evaluates
+  auto load_taps = [&](int c) {
+    const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + 2 * wave * 18;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 18; ++i) tp[p][i] = t[p * 18 + i];
+  };
+  // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c, h buffer c & 1
+  auto gate = [&](int c) {
+    const float* hbuf = smem + (c & 1) * L6_HBUF;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int jj = L6_NP * c + 2 * wave + p;
+      const bool lane_ok = jj < hid && gx < W;
+      const uint32_t off0 = (uint32_t)(jj * HW + (y0 + r0) * W + gx) * 4u;
+      const float* hp = hbuf + (2 * wave + p) * L6_PP + 2 * col;
+      f32x2 win[3][3];                          // rows (i mod 3) x halo columns col .. col + 2
+#pragma unroll
+      for (int i = 0; i < RA + 2; ++i) {
+        const int hrow = min(r0 + i, L6_HR - 1) * LH_HWD;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
+        if (i >= 2) {
+          float m = 0.f, v = 0.f;
+#pragma unroll
+          for (int ay = 0; ay < 3; ++ay)
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+              const f32x2 hv = win[(i - 2 + ay) % 3][ax];
+              m += tp[p][2 * (ay * 3 + ax)] * hv[0];
+              v += tp[p][2 * (ay * 3 + ax) + 1] * hv[1];
+            }
+          const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __expf(-m));   // sigmoid(m) m v
+          const bool ok = lane_ok && i - 2 < nrow;
+          const uint32_t off = ok ? off0 + (uint32_t)((i - 2) * W) * 4u : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, off, 0, 0);
+        }
+      }
+    }
+  };
+
+  // prologue: chunk 0's fragments landed -> GEMM1(0), its taps, chunk 1 into slot 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  gemm1(0);
+  load_taps(0);
+  issue(min(1, nch - 1), 1);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // Iteration c: gate of chunk c - 1 (h buffer (c - 1) & 1, taps in registers) and GEMM1 of chunk c
+  // (slot c & 1 -> h buffer c & 1); the SIMD partners (w, w + 4) run them in opposite orders.  Slot
+  // (c + 1) & 1 last served GEMM1(c - 1) and load_taps(c - 1), both before the previous barrier.
+  const bool gate_first = wave < 4;
+  for (int c = 1; c <= nch; ++c) {
+    issue(min(c + 1, nch - 1), (c + 1) & 1);
+    if (gate_first) {
+      gate(c - 1);
+      gemm1(c);
+    } else {
+      gemm1(c);
+      gate(c - 1);
+    }
+    if (c < nch) load_taps(c);
+    // chunk c + 1 landed (after its DMAs this wave issued the 2 RA gate stores), then every wave's
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * RA) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+// ---------------------------------------------------------------------------
 // mix: out = skip0 x + skip1 W2 g
 constexpr int LM_NBB = 2;                 // 32-pixel blocks per wave
 constexpr int LM_PX = 4 * LM_NBB * 32;    // pixels per workgroup
@@ -544,325 +857,24 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArg
 }
 
 // ---------------------------------------------------------------------------
-// fused: LN + W1 + dw3x3 + gate + W2 + skip in ONE kernel; the gated activations g stay in LDS.
-//
-// The head kernel's tile (32 columns x TH rows, W1 recomputed on the (TH+2) x 34 halo) and its
-// hidden-channel chunk loop (8 (mask, value) pairs per chunk), plus the second GEMM: every chunk
-// pair's g (16 hidden channels x TH x 32 pixels, fp32 in LDS) is multiplied into per-wave
-// accumulators of the output tile (C rows x TH x 32 pixels, v_mfma_f32_32x32x16_bf16 on the
-// exact 3-term split, 6 products) that stay in registers across the whole hidden loop; the
-// epilogue adds the skip and writes out.  Per iteration c: gate of chunk c - 1 (LDS h -> LDS g),
-// GEMM1 of chunk c (registers), GEMM2 of the pair gated two iterations earlier; barrier; h of
-// chunk c to LDS; barrier.  W1 chunks (+ taps) arrive by LDS-DMA in a 4-slot ring two chunks
-// ahead, W2 pair fragments in a 2-slot ring; every wave issues the same DMA count per iteration,
-// so the ring waits are one counted vmcnt.  Nothing of the 2 hid x HW hidden state or the hid x HW
-// gated state reaches HBM: the block reads x (with halo) and writes out.
-struct LnbFusedArgs {
-  const float* x;        // GEMM1 input [B, Ch, H, W] (Ch = C, or the replicated image's channels)
-  const char* w1f;       // W1 diag(ln_w) chunk images + taps (lnb_w1_pack_kernel)
-  const char* w2f;       // W2 pair images [npairs][MT][3] (lnb_w2_pack_kernel, 16-deep k-steps)
-  const float* xs;       // skip operand [B, XC, H, W]: x, or the image it replicates (channel m mod XC)
-  int XC;
-  const float* skip;     // [2]
-  float* out;            // [B, C, H, W]
-  float var_den;
-  int Ch, C, hid, H, W, tiles_x, tiles_y, nch, npairs;
-  uint32_t nblk;
-};
-
-
-template <int KS, int NB, int MT>
-__global__ __launch_bounds__(512, 1) void lnb_fused_kernel(LnbFusedArgs a) {
-  using Geo = HeadGeom<NB>;
-  constexpr int TH = Geo::TH, RA = Geo::RA, HP = Geo::HP;
-  constexpr int NI = KS * 3 + 1;        // W1 images per chunk (fragments + taps)
-  constexpr int DPW = (NI + 7) / 8;     // W1 LDS-DMAs per wave per iteration
-  constexpr int SLOTF = NI * 256;
-  constexpr int NSLOT = 4;
-  constexpr int HBUF = 2 * LH_JC * HP;  // one h plane set: 8 mask + 8 value rows of halo pixels
-  constexpr int W2I = MT * 3;           // W2 fragment images per chunk pair
-  constexpr int W2PW = (W2I + 7) / 8;   // W2 LDS-DMAs per wave per iteration
-  constexpr int GPX = TH * LH_TW;       // output pixels of the tile
-  // g of one chunk, already split for the GEMM2 B operand: [term][pixel][8 channels] bf16 = 4 floats
-  // per (term, pixel); the two 32-lane halves of a B read hit chunk slots 16 floats apart mod 64
-  constexpr int GCH = 3 * GPX * 4 + 16;
-  constexpr int NT2 = MT * TH;          // GEMM2 output tiles (32 channels x 32 pixels of one output row)
-  constexpr int TPW = (NT2 + 7) / 8;    // tiles per wave
-  __shared__ __attribute__((aligned(16))) float smem[HBUF + NSLOT * SLOTF + 2 * W2I * 256 + 3 * GCH];
-  float* const hb = smem;               // h of one chunk: [channel 0..7][halo pixel][mask, value]
-  float* const ring = smem + HBUF;
-  float* const w2ring = ring + NSLOT * SLOTF;
-  float* const gring = w2ring + 2 * W2I * 256;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
-  const int tx = lb % a.tiles_x; lb /= a.tiles_x;
-  const int ty = lb % a.tiles_y;
-  const int b = lb / a.tiles_y;
-  const int H = a.H, W = a.W, Ch = a.Ch, C = a.C, hid = a.hid, nch = a.nch, npairs = a.npairs;
-  const int HW = H * W;
-  const int y0 = ty * TH, x0 = tx * LH_TW;
-
-  auto issue_w1 = [&](int chunk, int slot_idx) {
-    float* slot = ring + slot_idx * SLOTF;
-    const char* src = a.w1f + (int64_t)chunk * NI * 1024 + lane * 16;
-#pragma unroll
-    for (int i = 0; i < DPW; ++i) {
-      const int img = min(i * 8 + wave, NI - 1);   // surplus waves repeat the last image
-      dma16_opaque(src + img * 1024, slot + img * 256);
-    }
-  };
-  auto issue_w2 = [&](int pair) {
-    float* slot = w2ring + (pair & 1) * W2I * 256;
-    const char* src = a.w2f + (int64_t)pair * W2I * 1024 + lane * 16;
-#pragma unroll
-    for (int i = 0; i < W2PW; ++i) {
-      const int img = min(i * 8 + wave, W2I - 1);
-      dma16_opaque(src + img * 1024, slot + img * 256);
-    }
-  };
-  issue_w1(0, 0);
-  issue_w1(min(1, nch - 1), 1);
-  issue_w2(0);
-
-  // this wave's halo pixels: raw x column split into bf16 terms, and 1/sigma (REF:916-922)
-  const int kq = lane >> 4;
-  bf16x8 xf[NB][KS][3];
-  float rstd[NB];
-  {
-    float xv[NB][KS][8];
-#pragma unroll
-    for (int blk = 0; blk < NB; ++blk) {
-      const int q = min((wave * NB + blk) * 16 + (lane & 15), Geo::HR * LH_HWD - 1);
-      const int hy = q / LH_HWD, hx = q - hy * LH_HWD;
-      const int gy = clampi(y0 - 1 + hy, 0, H - 1), gx = clampi(x0 - 1 + hx, 0, W - 1);
-      const float* xp = a.x + (int64_t)b * Ch * HW + gy * W + gx;
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[blk][s][j] = xp[(int64_t)min(32 * s + 8 * kq + j, Ch - 1) * HW];
-    }
-#pragma unroll
-    for (int blk = 0; blk < NB; ++blk) {
-      float sum = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (32 * s + 8 * kq + j >= Ch) xv[blk][s][j] = 0.f;
-          sum += xv[blk][s][j];
-        }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
-      const float mean = sum / (float)Ch;
-      float sq = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = 32 * s + 8 * kq + j < Ch ? xv[blk][s][j] - mean : 0.f;
-          sq += d * d;
-        }
-      sq += __shfl_xor(sq, 16);
-      sq += __shfl_xor(sq, 32);
-      rstd[blk] = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) split3x8(xv[blk][s], xf[blk][s][0], xf[blk][s][1], xf[blk][s][2]);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W1 chunks 0, 1 and W2 pair 0 landed (this wave's part)
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  f32x4 acc1[NB];
-  f32x16 acc2[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) acc2[i] = f32x16{};
-
-  auto gemm1 = [&](int c) {
-#pragma unroll
-    for (int blk = 0; blk < NB; ++blk) acc1[blk] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (c >= nch) return;
-    const float* slot = ring + (c % NSLOT) * SLOTF + lane * 4;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 0) * 256);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 1) * 256);
-      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(slot + (3 * s + 2) * 256);
-#pragma unroll
-      for (int blk = 0; blk < NB; ++blk)
-        GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_16x16x32_bf16, acc1[blk], a0, a1, a2, xf[blk][s][0],
-                    xf[blk][s][1], xf[blk][s][2]);
-      // the next k-step's fragments are read while these MFMAs run (not all hoisted: registers)
-      asm volatile("" ::: "memory");
-    }
-  };
-  // GEMM1 rows 4 kq + i: kq < 2 mask channels 4 kq + i, kq >= 2 value channels 4 (kq - 2) + i
-  auto store_h = [&](int c) {
-    if (c >= nch) return;
-    const int ch0 = 4 * (kq & 1), comp = kq >> 1;
-#pragma unroll
-    for (int blk = 0; blk < NB; ++blk) {
-      const int q = (wave * NB + blk) * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hb[((ch0 + i) * HP + q) * 2 + comp] = acc1[blk][i] * rstd[blk];
-    }
-  };
-  // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c - 1 -> g slot (c - 1) mod 3.
-  // Mask and value run as one packed pair (v_pk_fma_f32; each component the same fma chain in the
-  // reference's tap order); g goes to LDS as its exact 3-term bf16 split, in the GEMM2 B layout.
-  const int col = lane & 31, r0 = (lane >> 5) * RA;
-  auto gate = [&](int c) {
-    const int jj = LH_JC * (c - 1) + wave;
-    const bool live = c >= 1 && jj < hid;
-    const f32x2* hp = reinterpret_cast<const f32x2*>(hb) + wave * HP + col;
-    const float* taps = ring + ((c + NSLOT - 1) % NSLOT) * SLOTF + KS * 3 * 256 + wave * 18;
-    __bf16* gdst = reinterpret_cast<__bf16*>(gring + ((c + 2) % 3) * GCH) + wave;
-    const f32x2* k2 = reinterpret_cast<const f32x2*>(taps);   // (mask, value) tap pairs, broadcast LDS reads
-    f32x2 hw[3][3];
-#pragma unroll
-    for (int i = 0; i < RA + 2; ++i) {
-      const int hrow = min(r0 + i, Geo::HR - 1) * LH_HWD;
-#pragma unroll
-      for (int d = 0; d < 3; ++d) hw[i % 3][d] = hp[hrow + d];
-      if (i >= 2) {
-        f32x2 mv = f32x2{0.f, 0.f};
-#pragma unroll
-        for (int ay = 0; ay < 3; ++ay)
-#pragma unroll
-          for (int ax = 0; ax < 3; ++ax) mv = __builtin_elementwise_fma(k2[ay * 3 + ax], hw[(i - 2 + ay) % 3][ax], mv);
-        const float m = mv.x, v = mv.y;
-        const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-m));
-        const float g = live ? (sg * m) * v : 0.f;   // 0 for padding channels
-        const int orow = r0 + i - 2;
-        if (orow < TH) {
-          const __bf16 h0 = (__bf16)g;
-          const float r1 = g - (float)h0;
-          const __bf16 h1 = (__bf16)r1;
-          const __bf16 h2 = (__bf16)(r1 - (float)h1);
-          __bf16* d = gdst + (orow * LH_TW + col) * 8;
-          d[0] = h0;
-          d[GPX * 8] = h1;
-          d[2 * GPX * 8] = h2;
-        }
-      }
-    }
-  };
-  // out tile rows += W2[:, 16 p .. 16 p + 15] g(pair p): tile t = wave + 8 i -> (output row t / MT, rows 32 (t % MT) ..)
-  auto gemm2 = [&](int p) {
-    const float* w2 = w2ring + (p & 1) * W2I * 256 + lane * 4;
-    const float* gsrc = gring + ((2 * p + (lane >> 5)) % 3) * GCH + col * 4;
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      const int t = wave + 8 * i;
-      if (t < NT2) {
-        const int orow = t / MT, mt = t - orow * MT;
-        const float* gp = gsrc + orow * LH_TW * 4;
-        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(gp);
-        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(gp + GPX * 4);
-        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(gp + 2 * GPX * 4);
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(w2 + (3 * mt + 0) * 256);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(w2 + (3 * mt + 1) * 256);
-        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(w2 + (3 * mt + 2) * 256);
-        GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_32x32x16_bf16, acc2[i], a0, a1, a2, b0, b1, b2);
-      }
-    }
-  };
-
-  // iteration c: gate(c - 1 chunk), GEMM1(c), GEMM2 of the pair gated in iterations c - 2, c - 1
-  const bool gate_first = wave < 4;   // SIMD partners (w, w + 4) overlap one's MFMA with the other's VALU
-  const int cmax = 2 * npairs + 1;
-#ifdef GRR_FUSED_STAMP
-  uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
-#define GRR_STAMP(k, t) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - (t); (t) = t_; } while (0)
-#else
-#define GRR_STAMP(k, t) do { } while (0)
-#endif
-  for (int c = 0; c <= cmax; ++c) {
-#ifdef GRR_FUSED_STAMP
-    uint64_t tt = __builtin_amdgcn_s_memtime();
-#endif
-    issue_w1(min(c + 2, nch - 1), (c + 2) % NSLOT);   // slot last read by gate(c - 1) (taps of chunk c - 2)
-    issue_w2(min(c >> 1, npairs - 1));                // slot last read by gemm2 of iteration c - 1 or earlier
-    if (gate_first) {
-      gate(c);
-      GRR_STAMP(0, tt);
-      gemm1(c);
-      GRR_STAMP(1, tt);
-    } else {
-      gemm1(c);
-      GRR_STAMP(1, tt);
-      gate(c);
-      GRR_STAMP(0, tt);
-    }
-    if ((c & 1) && c >= 3) gemm2((c - 3) >> 1);
-    GRR_STAMP(2, tt);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                     // h of chunk c - 1 and the g slots read: reusable
-    asm volatile("" ::: "memory");
-    GRR_STAMP(3, tt);
-    store_h(c);
-    GRR_STAMP(4, tt);
-    // everything issued before this iteration landed (this wave's part), then every wave's
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(DPW + W2PW) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    GRR_STAMP(5, tt);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef GRR_FUSED_STAMP
-  st[6] = __builtin_amdgcn_s_memtime() - t_begin;
-  st[7] = (uint64_t)(cmax + 1);
-  if (blockIdx.x < 64 && lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) g_fused_stamps[(blockIdx.x * 8 + wave) * 8 + k] = st[k];
-  }
-#endif
-#undef GRR_STAMP
-
-  // epilogue (REF:962-964): out = skip0 x + skip1 W2 g.  acc2[i] element e: channel
-  // 32 mt + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), pixel (y0 + orow, x0 + lane & 31)
-  const float s0 = a.skip[0], s1 = a.skip[1];
-  const int XC = a.XC;
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.xs + (int64_t)b * XC * HW), 0, (int)((int64_t)XC * HW * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * C * HW, 0,
-                                                                        (int)((int64_t)C * HW * 4), 0x00020000);
-  const int gx = x0 + col;
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int t = wave + 8 * i;
-    if (t < NT2) {
-      const int orow = t / MT, mt = t - orow * MT;
-      const int gy = y0 + orow;
-      const bool pix = gy < H && gx < W;
-      const int p = min(gy, H - 1) * W + min(gx, W - 1);
-      float xv[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = min(32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5), C - 1);
-        const int mx = XC == C ? m : m % XC;
-        xv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (uint32_t)(mx * HW + p) * 4u, 0, 0));
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        const uint32_t off = (m < C && pix) ? (uint32_t)(m * HW + p) * 4u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[e] + s1 * acc2[i][e]), ors, off, 0, 0);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // host side
 static int head_ks(int C) { return (C + 31) / 32; }
 static int head_nb(int KS) { return KS <= 3 ? 4 : 3; }
 static int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }
+// GEMM1 on the fp16 two-term head (lnb_head16_kernel): C <= 96 (its 2-slot ring + 2 x 64 KB of
+// h planes fill the CU's LDS at 6 k-steps); GRR_LNB_HEAD=bf16 selects the split-bf16 head (A/B)
+static int head16_ks(int C) { return (C + 15) / 16; }
+static bool head16_enabled(int C) {
+  static const bool bf16 = [] {
+    const char* e = getenv("GRR_LNB_HEAD");
+    return e && e[0] == 'b';
+  }();
+  return !bf16 && head16_ks(C) <= 6;
+}
 static int64_t head_pack_floats(int C, int hid) {
-  return align64((int64_t)((hid + LH_JC - 1) / LH_JC) * head_images(head_ks(C)) * 256);
+  const int64_t bf = (int64_t)((hid + LH_JC - 1) / LH_JC) * head_images(head_ks(C)) * 256;
+  const int64_t f16 = (int64_t)((hid + L6_NP - 1) / L6_NP) * head16_images(head16_ks(C)) * 256;
+  return align64(std::max(bf, f16));
 }
 static int64_t mix_pack_floats(int C, int hid) {
   return align64((int64_t)((hid + LM_KD - 1) / LM_KD) * ((C + 31) / 32) * 3 * 256);
@@ -877,44 +889,14 @@ template <int KS, int NB>
 static void launch_head(const LnbHeadArgs& h, hipStream_t s) {
   hipLaunchKernelGGL((lnb_head_kernel<KS, NB>), dim3(h.nblk), dim3(512), 0, s, h);
 }
+template <int KS>
+static void launch_head16(const LnbHeadArgs& h, hipStream_t s) {
+  hipLaunchKernelGGL((lnb_head16_kernel<KS>), dim3(h.nblk), dim3(512), 0, s, h);
+}
 template <int MT>
 static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
   if (v4) hipLaunchKernelGGL((lnb_mix_kernel<MT, true>), dim3(m.nblk), dim3(256), 0, s, m);
   else hipLaunchKernelGGL((lnb_mix_kernel<MT, false>), dim3(m.nblk), dim3(256), 0, s, m);
-}
-
-// GRR_LNB_FUSED=1 selects the single fused kernel (A/B measurements).  Default: head + mix -- the
-// fused kernel keeps the GEMM2 accumulators in the registers the gate phase needs for latency
-// hiding and measured slower
-static bool lnb_fused_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("GRR_LNB_FUSED");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// halo pixel blocks per wave of the fused kernel: its GEMM2 accumulators share the 256 registers
-// of a 2-waves-per-SIMD kernel with the x fragments, so deeper / wider blocks run 3 blocks (9-row
-// tiles); the shapes that would still spill (K > 96 with C > 32, or C > 96 with K > 32) keep the
-// two-kernel head + mix path
-static constexpr int fused_nb(int KS, int MT) { return (KS == 1 || (KS == 2 && MT <= 2)) ? 4 : 3; }
-static bool fused_ok(int KS, int MT) { return KS <= MT && (KS == 1 || MT <= 3); }
-template <int KS, int MT>
-static void launch_fused_t(const LnbFusedArgs& f, hipStream_t s) {
-  constexpr int NB = fused_nb(KS, MT);
-  hipLaunchKernelGGL((lnb_fused_kernel<KS, NB, MT>), dim3(f.nblk), dim3(512), 0, s, f);
-}
-static void launch_fused(const LnbFusedArgs& f, int KS, int MT, hipStream_t s) {
-  switch (MT * 8 + KS) {
-    case 1 * 8 + 1: launch_fused_t<1, 1>(f, s); break;
-    case 2 * 8 + 1: launch_fused_t<1, 2>(f, s); break;
-    case 2 * 8 + 2: launch_fused_t<2, 2>(f, s); break;
-    case 3 * 8 + 1: launch_fused_t<1, 3>(f, s); break;
-    case 3 * 8 + 2: launch_fused_t<2, 3>(f, s); break;
-    case 3 * 8 + 3: launch_fused_t<3, 3>(f, s); break;
-    default: launch_fused_t<1, 4>(f, s); break;
-  }
 }
 
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
@@ -930,53 +912,51 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   GRR_REQUIRE(C >= 2 && C <= 128 && Ch >= 1, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d outside [2, 128]", C);
   GRR_REQUIRE((int64_t)std::max(hid, C) * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_lnb_forward: max(hid, C)*H*W too large for one image's 32-bit offsets");
-  const int KS = head_ks(Ch), NB = head_nb(KS), nch = (hid + LH_JC - 1) / LH_JC;
+  const bool h16 = head16_enabled(Ch);
+  const int KS = h16 ? head16_ks(Ch) : head_ks(Ch), NB = head_nb(head_ks(Ch));
+  const int nch = h16 ? (hid + L6_NP - 1) / L6_NP : (hid + LH_JC - 1) / LH_JC;
   const int MT = (C + 31) / 32, KS2 = (hid + LM_KD - 1) / LM_KD;
   const int64_t P = (int64_t)H * W;
   float* g = ws;
   char* w1f = reinterpret_cast<char*>(ws + align64((int64_t)B * hid * P));
   uint16_t* w2f = reinterpret_cast<uint16_t*>(ws + align64((int64_t)B * hid * P) + head_pack_floats(Ch, hid));
   {
-    const int64_t n1 = (int64_t)nch * head_images(KS) * 256, n2 = (int64_t)KS2 * MT * 3 * 512;
-    hipLaunchKernelGGL(lnb_w1_pack_kernel, dim3((unsigned)std::min<int64_t>((n1 + 255) / 256, 4096)), dim3(256), 0,
-                       s, w1, ln_w, wdw, w1f, Ch, hid, KS, nch, R);
+    const int64_t n1 = (int64_t)nch * (h16 ? head16_images(KS) : head_images(KS)) * 256;
+    const int64_t n2 = (int64_t)KS2 * MT * 3 * 512;
+    const dim3 g1((unsigned)std::min<int64_t>((n1 + 255) / 256, 4096));
+    if (h16) hipLaunchKernelGGL(lnb_w1_pack16_kernel, g1, dim3(256), 0, s, w1, ln_w, wdw, w1f, Ch, hid, KS, nch, R);
+    else hipLaunchKernelGGL(lnb_w1_pack_kernel, g1, dim3(256), 0, s, w1, ln_w, wdw, w1f, Ch, hid, KS, nch, R);
     hipLaunchKernelGGL(lnb_w2_pack_kernel, dim3((unsigned)std::min<int64_t>((n2 + 255) / 256, 4096)), dim3(256), 0,
                        s, w2, w2f, C, hid, MT, KS2);
     grr_status st = launch_status("grr_lnb_forward/pack");
     if (st != GRR_OK) return st;
   }
-  if (lnb_fused_enabled() && fused_ok(KS, MT)) {
-    LnbFusedArgs f{};
-    f.x = xh; f.w1f = w1f; f.w2f = reinterpret_cast<const char*>(w2f);
-    f.xs = x ? x : xh;          // x == NULL: the skip reads the replicated image itself
-    f.XC = x ? C : Ch;
-    f.skip = skip; f.out = out;
-    f.var_den = R == 1 ? (float)(C - 1) : (float)(C - 1) / (float)R;
-    f.Ch = Ch; f.C = C; f.hid = hid; f.H = H; f.W = W; f.nch = nch; f.npairs = KS2;
-    const int TH = fused_nb(KS, MT) == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH;
-    f.tiles_x = (W + LH_TW - 1) / LH_TW;
-    f.tiles_y = (H + TH - 1) / TH;
-    const uint64_t nf = (uint64_t)B * f.tiles_x * f.tiles_y;
-    GRR_REQUIRE(nf < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
-    f.nblk = (uint32_t)nf;
-    launch_fused(f, KS, MT, s);
-    return launch_status("grr_lnb_forward/fused");
-  }
   LnbHeadArgs h{};
   h.x = xh; h.w1f = w1f; h.g = g;
   h.var_den = R == 1 ? (float)(C - 1) : (float)(C - 1) / (float)R;
   h.C = Ch; h.hid = hid; h.H = H; h.W = W; h.nch = nch;
-  const int TH = NB == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH;
+  const int TH = h16 ? L6_TH : (NB == 4 ? HeadGeom<4>::TH : HeadGeom<3>::TH);
   h.tiles_x = (W + LH_TW - 1) / LH_TW;
   h.tiles_y = (H + TH - 1) / TH;
   const uint64_t nh = (uint64_t)B * h.tiles_x * h.tiles_y;
   GRR_REQUIRE(nh < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
   h.nblk = (uint32_t)nh;
-  switch (KS) {
-    case 1: launch_head<1, 4>(h, s); break;
-    case 2: launch_head<2, 4>(h, s); break;
-    case 3: launch_head<3, 4>(h, s); break;
-    default: launch_head<4, 3>(h, s); break;
+  if (h16) {
+    switch (KS) {
+      case 1: launch_head16<1>(h, s); break;
+      case 2: launch_head16<2>(h, s); break;
+      case 3: launch_head16<3>(h, s); break;
+      case 4: launch_head16<4>(h, s); break;
+      case 5: launch_head16<5>(h, s); break;
+      default: launch_head16<6>(h, s); break;
+    }
+  } else {
+    switch (KS) {
+      case 1: launch_head<1, 4>(h, s); break;
+      case 2: launch_head<2, 4>(h, s); break;
+      case 3: launch_head<3, 4>(h, s); break;
+      default: launch_head<4, 3>(h, s); break;
+    }
   }
   grr_status st = launch_status("grr_lnb_forward/head");
   if (st != GRR_OK) return st;

@@ -11,9 +11,11 @@ follow ``.to()`` and stay out of the state_dict, as in the reference.
 Forward passes of the graph filter run only through the HIP kernels (kernels.py);
 GPU tensors are required.  When autograd records (training), every module here switches
 to the differentiable path of solver_grad.py (HIP forward that keeps what the reverse
-needs + hand-written HIP reverse kernels): MixtureGTVGLR / LocalLowpassFilteringBlock
-(_MixtureSolve), the GLRFast/GTVFast sub-API and extract_edge_weights (_GraphApply,
-_EdgeWeights), LocalNonLinearBlock (LNBFn).  A HIP forward entered directly without a
+needs + hand-written HIP reverse kernels, each an opaque irdu:: op pair under torch.compile):
+MixtureGTVGLR / LocalLowpassFilteringBlock (MIXTURE), GLRFast/GTVFast.forward and
+extract_edge_weights (GRAPH_APPLY, EDGE_WEIGHTS), the module methods get_neighbors_pixels,
+normalize_and_transform_features, stats_conv(_transpose), op_L_norm, op_C, op_C_transpose
+(csrc/subapi_bwd.hip), LocalNonLinearBlock (LNB).  A HIP forward entered directly without a
 reverse (``hip_forward``-wrapped internals) attaches a node whose backward raises, so
 training can never silently skip gradients.
 """
@@ -127,25 +129,33 @@ class _GraphModule(nn.Module):
         return K.neighbor_table(h, w, self.multiM.device)
 
     # -- the reference's module methods, standalone (the solver fuses them; csrc/subapi_ops.hip) --
-    # Their HIP forwards carry no reverse: under autograd, backward raises (hip_forward).
-    @hip_forward
+    # Differentiable like the reference's ATen compositions: under autograd they run the same HIP
+    # forwards with their reverses (csrc/subapi_bwd.hip) through solver_grad's opaque functions.
+    def _stencil_params(self):
+        return (self.stats_kernel_p01, self.stats_kernel_p02a, self.stats_kernel_p02b, self.stats_kernel_p03)
+
     def get_neighbors_pixels(self, img_features):
         """[B,C,H,W] -> [B,C,4,H,W]: the replicate-clamped up/left/right/down neighbours (REF:128-144)."""
+        if records_grad(self, img_features):
+            return SG.NEIGHBORS([], img_features.contiguous())
         return OPS.neighbor_gather(img_features.contiguous())
 
-    @hip_forward
     def normalize_and_transform_features(self, img_features):
         """[B,G,F,H,W] -> [B,G*F,H,W]: L2-normalised over F (eps 1e-12), scaled by multiM (REF:146-157)."""
+        if records_grad(self, img_features):
+            return SG.NORMALIZE([], img_features.contiguous(), self.multiM)
         return OPS.normalize_features(img_features.contiguous(), self.multiM)
 
-    @hip_forward
     def stats_conv(self, patchs):
         """S x, depthwise 3x3 cross stencil with a replicate frame (REF:177-195)."""
+        if records_grad(self, patchs):
+            return SG.STATS_CONV([0], patchs.contiguous(), *self._stencil_params())
         return OPS.stats_conv(patchs.contiguous(), self, False)
 
-    @hip_forward
     def stats_conv_transpose(self, patchs):
         """S^T x, conv_transpose2d(padding=1) of the same stencil, zero frame (REF:197-215)."""
+        if records_grad(self, patchs):
+            return SG.STATS_CONV([1], patchs.contiguous(), *self._stencil_params())
         return OPS.stats_conv(patchs.contiguous(), self, True)
 
 
@@ -157,9 +167,10 @@ class GLRFast(_GraphModule):
             return SG.graph_apply(self, "glr", patchs, edge_weights)
         return self._hip_apply(patchs, edge_weights)
 
-    @hip_forward
     def op_L_norm(self, img_signals, edge_weights, node_degree=None):
         """x - sum_e w_e x(clamp(p + delta_e)) (REF:218-228); x [B,G,F,H,W], w [B,G,4,H,W]."""
+        if records_grad(self, img_signals, edge_weights):
+            return SG.OP_L_NORM([], img_signals.contiguous(), edge_weights.contiguous())
         return OPS.glr_op_L_norm(img_signals.contiguous(), edge_weights.contiguous())
 
     @torch.no_grad()
@@ -178,14 +189,16 @@ class GTVFast(_GraphModule):
             return SG.graph_apply(self, "gtv", patchs, edge_weights)
         return self._hip_apply(patchs, edge_weights)
 
-    @hip_forward
     def op_C(self, img_signals, edge_weights, node_degree=None):
         """Edge signals E_e = w_e (S x - (S x)(clamp(p + delta_e))), [B,G,F,4,H,W] (REF:452-467)."""
+        if records_grad(self, img_signals, edge_weights):
+            return SG.OP_C([], img_signals.contiguous(), edge_weights.contiguous(), *self._stencil_params())
         return OPS.gtv_op_C(img_signals.contiguous(), edge_weights.contiguous(), self)
 
-    @hip_forward
     def op_C_transpose(self, edge_signals, edge_weights, node_degree=None):
         """S^T of the frame-dropped scatter of w_e E_e (REF:469-516) -> [B,G,F,H,W]."""
+        if records_grad(self, edge_signals, edge_weights):
+            return SG.OP_C_T([], edge_signals.contiguous(), edge_weights.contiguous(), *self._stencil_params())
         return OPS.gtv_op_C_transpose(edge_signals.contiguous(), edge_weights.contiguous(), self)
 
     @torch.no_grad()

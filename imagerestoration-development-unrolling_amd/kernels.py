@@ -394,7 +394,7 @@ def gtv_op_C(x5: Tensor, w: Tensor, st: Stencil) -> Tensor:
     return out
 
 
-def gtv_op_C_transpose(e6: Tensor, w: Tensor, st: Stencil) -> Tensor:
+def gtv_op_C_transpose(e6: Tensor, w: Tensor, st: Stencil, want_work: bool = False):
     """GTVFast.op_C_transpose: edge signals [B,G,F,4,H,W] -> [B,G,F,H,W] (REF:469-516)."""
     dev = _check("gtv_op_C_transpose", e6, w)
     b, g, f, four, h, ww = e6.shape
@@ -404,7 +404,65 @@ def gtv_op_C_transpose(e6: Tensor, w: Tensor, st: Stencil) -> Tensor:
     out = torch.empty_like(work)
     _launch("subapi", 4 * (e6.numel() + w.numel() + 3 * work.numel()), "grr_gtv_op_c_transpose", e6.data_ptr(),
             w.data_ptr(), st, work.data_ptr(), out.data_ptr(), b, g, f, h, ww, _stream(dev))
-    return out
+    return (out, work) if want_work else out
+
+
+# reverses of the sub-API (csrc/subapi_bwd.hip); gM / gtaps accumulate, gtaps is [G*F, 5]
+def neighbor_gather_bwd(g: Tensor) -> Tensor:
+    dev = _check("neighbor_gather_bwd", g)
+    b, c, four, h, w = g.shape
+    gx = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
+    _launch("subapi_bwd", 4 * g.numel() * 5 // 4, "grr_neighbor_gather_bwd", g.data_ptr(), gx.data_ptr(), b, c, h, w,
+            _stream(dev))
+    return gx
+
+
+def normalize_features_bwd(f5: Tensor, multiM: Tensor, gout: Tensor, gM: Tensor) -> Tensor:
+    dev = _check("normalize_features_bwd", f5, multiM, gout, gM)
+    b, g, f, h, w = f5.shape
+    gf = torch.empty_like(f5)
+    _launch("subapi_bwd", 12 * f5.numel(), "grr_normalize_features_bwd", f5.data_ptr(), multiM.data_ptr(),
+            gout.data_ptr(), gf.data_ptr(), gM.data_ptr(), b, g, f, h, w, _stream(dev))
+    return gf
+
+
+def stats_conv_bwd(x5: Tensor, st: Stencil, transpose: bool, g: Tensor, gtaps: Optional[Tensor]) -> Tensor:
+    dev = _check("stats_conv_bwd", x5, g, gtaps)
+    b, gg, f, h, w = x5.shape
+    gx = torch.empty_like(x5)
+    _launch("subapi_bwd", 12 * x5.numel(), "grr_stats_conv_bwd", x5.data_ptr(), st, int(transpose), g.data_ptr(),
+            gx.data_ptr(), _ptr(gtaps), b, gg, f, h, w, _stream(dev))
+    return gx
+
+
+def glr_op_L_norm_bwd(x5: Tensor, w: Tensor, g: Tensor) -> Tuple[Tensor, Tensor]:
+    dev = _check("glr_op_L_norm_bwd", x5, w, g)
+    b, gg, f, h, ww = x5.shape
+    gx, gw = torch.empty_like(x5), torch.empty_like(w)
+    _launch("subapi_bwd", 4 * (3 * x5.numel() + 3 * w.numel()), "grr_glr_op_l_norm_bwd", x5.data_ptr(), w.data_ptr(),
+            g.data_ptr(), gx.data_ptr(), gw.data_ptr(), b, gg, f, h, ww, _stream(dev))
+    return gx, gw
+
+
+def gtv_op_C_bwd(x5: Tensor, w: Tensor, st: Stencil, gE: Tensor, gtaps: Tensor) -> Tuple[Tensor, Tensor]:
+    dev = _check("gtv_op_C_bwd", x5, w, gE, gtaps)
+    b, gg, f, h, ww = x5.shape
+    work, gx, gw = torch.empty_like(x5), torch.empty_like(x5), torch.empty_like(w)
+    _launch("subapi_bwd", 4 * (gE.numel() + 6 * x5.numel() + 2 * w.numel()), "grr_gtv_op_c_bwd", x5.data_ptr(),
+            w.data_ptr(), st, gE.data_ptr(), work.data_ptr(), gx.data_ptr(), gw.data_ptr(), gtaps.data_ptr(),
+            b, gg, f, h, ww, _stream(dev))
+    return gx, gw
+
+
+def gtv_op_C_transpose_bwd(e6: Tensor, w: Tensor, st: Stencil, z: Tensor, g: Tensor,
+                           gtaps: Tensor) -> Tuple[Tensor, Tensor]:
+    dev = _check("gtv_op_C_transpose_bwd", e6, w, z, g, gtaps)
+    b, gg, f, four, h, ww = e6.shape
+    work2, gE, gw = torch.empty_like(z), torch.empty_like(e6), torch.empty_like(w)
+    _launch("subapi_bwd", 4 * (2 * e6.numel() + 4 * z.numel() + 2 * w.numel()), "grr_gtv_op_c_transpose_bwd",
+            e6.data_ptr(), w.data_ptr(), st, z.data_ptr(), g.data_ptr(), work2.data_ptr(), gE.data_ptr(),
+            gw.data_ptr(), gtaps.data_ptr(), b, gg, f, h, ww, _stream(dev))
+    return gE, gw
 
 
 # ---- feature CNN -----------------------------------------------------------

@@ -28,6 +28,7 @@ import torch
 
 from . import kernels as K
 from ._native import Stencil
+from .train_ops import OpaqueFunction
 
 Tensor = torch.Tensor
 
@@ -157,181 +158,226 @@ def _stencil(t4) -> Stencil:
     return Stencil(*[t.data_ptr() for t in t4])
 
 
-class _MixtureSolve(torch.autograd.Function):
-    """(y, f0, f1, params...) -> x_S of MixtureGTVGLR (REF:707-811), differentiable on the HIP kernels."""
+# Each differentiable HIP operation below is a pair of pure functions (forward -> outputs + the
+# tensors the reverse needs; reverse -> input gradients) wrapped by train_ops.OpaqueFunction: a
+# plain autograd.Function in eager mode, one opaque irdu:: custom op per direction under
+# torch.compile.  `consts` carries the integer arguments (graph count, kind).
 
-    @staticmethod
-    def forward(ctx, n_graphs: int, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor) -> Tensor:
-        p = dict(zip(PARAM_NAMES, params))
-        g = n_graphs
-        b, c, h, w = y.shape
-        nf = c // g
-        wG0, cG0, wL0 = K.edge_weights_block(f0, g, nf, p["GTVmodule00.multiM"], p["GLRmodule00.multiM"])
-        wG1, cG1, wL1 = K.edge_weights_block(f1, g, nf, p["GTVmodule01.multiM"], p["GLRmodule01.multiM"])
-        st = {m: tuple(p[f"{m}.{q}"] for q in STENCIL_PARAMS) for m in MODULES}
-        sG0, sL0, sG1, sL1 = (_stencil(st[m]) for m in MODULES)
-        mu0, mu1, ro0, ro1 = p["muys00"], p["muys01"], p["ro00"], p["ro01"]
-        alpha, beta = p["alphaCGD"], p["betaCGD"]
-        n_st = alpha.shape[0]
+def _new(x: Tensor, *shape) -> Tensor:
+    return x.new_empty(shape)
 
-        t = K.gtv_rhs_half(K.pool2(y), cG1, sG1, False, None, g)
-        b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
-        t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
-        x, r0, xd = K.system_step(b_a, b_a, None, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[0], None, g,
-                                  want_u=True, want_pool=n_st > 1)
-        xs, us = [b_a, x], [r0]
-        if n_st > 1:
-            t = K.gtv_rhs_half(xd, wG1, sG1, True, p["gamma01"], g)
-            b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, p["gamma00"], ro0, t, ro1, g)
-            u = None
-            for k in range(1, n_st):
-                last = k == n_st - 1
-                t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
-                x, u, xd = K.system_step(x, b_b, u, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[k],
-                                         beta[k] if k >= 2 else None, g, want_u=True, want_pool=not last)
-                xs.append(x)
-                us.append(u)
-            del b_b
-        ctx.n_graphs, ctx.n_st = g, n_st
-        ctx.save_for_backward(y, f0, f1, wG0, wL0, wG1, wL1, cG0, cG1, *params, *xs[:-1], *us)
-        return xs[-1]
 
-    @staticmethod
-    def backward(ctx, gout: Tensor):
-        g, n_st = ctx.n_graphs, ctx.n_st
-        saved = ctx.saved_tensors
-        y, f0, f1, wG0, wL0, wG1, wL1, cG0, cG1 = saved[:9]
-        npar = len(PARAM_NAMES)
-        params = saved[9:9 + npar]
-        xs = saved[9 + npar:9 + npar + n_st]          # x_0 = b_A, x_1, ..., x_{S-1}
-        us = saved[9 + npar + n_st:]                  # r_0, u_1, ..., u_{S-1}
-        p = dict(zip(PARAM_NAMES, params))
-        c = y.shape[1]
-        nf = c // g
-        st = {m: tuple(p[f"{m}.{q}"] for q in STENCIL_PARAMS) for m in MODULES}
-        l0 = _Level(wL0, cG0, wG0, st["GLRmodule00"], st["GTVmodule00"], p["muys00"], p["ro00"], p["gamma00"], g)
-        l1 = _Level(wL1, cG1, wG1, st["GLRmodule01"], st["GTVmodule01"], p["muys01"], p["ro01"], p["gamma01"], g)
-        alpha, beta = p["alphaCGD"], p["betaCGD"]
-        galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
+# ---- MixtureGTVGLR solve (REF:707-811) ----------------------------------------------------
+def _mixture_fwd(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
+    p = dict(zip(PARAM_NAMES, params))
+    g = consts[0]
+    b, c, h, w = y.shape
+    nf = c // g
+    wG0, cG0, wL0 = K.edge_weights_block(f0, g, nf, p["GTVmodule00.multiM"], p["GLRmodule00.multiM"])
+    wG1, cG1, wL1 = K.edge_weights_block(f1, g, nf, p["GTVmodule01.multiM"], p["GLRmodule01.multiM"])
+    st = {m: tuple(p[f"{m}.{q}"] for q in STENCIL_PARAMS) for m in MODULES}
+    sG0, sL0, sG1, sL1 = (_stencil(st[m]) for m in MODULES)
+    mu0, mu1, ro0, ro1 = p["muys00"], p["muys01"], p["ro00"], p["ro01"]
+    alpha, beta = p["alphaCGD"], p["betaCGD"]
+    n_st = alpha.shape[0]
 
-        def a_bwd(x, gg, coef, out, glr=True):      # out += coef * (A - I)^T gg (+ parameter gradients)
-            _two_level(l0, l1, x, gg, out, lambda lv, xx, g2, o: lv.terms_bwd(xx, g2, coef, o, glr))
+    t = K.gtv_rhs_half(K.pool2(y), cG1, sG1, False, None, g)
+    b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+    t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
+    x, r0, xd = K.system_step(b_a, b_a, None, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[0], None, g,
+                              want_u=True, want_pool=n_st > 1)
+    xs, us = [b_a, x], [r0]
+    if n_st > 1:
+        t = K.gtv_rhs_half(xd, wG1, sG1, True, p["gamma01"], g)
+        b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, p["gamma00"], ro0, t, ro1, g)
+        u = None
+        for k in range(1, n_st):
+            last = k == n_st - 1
+            t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
+            x, u, xd = K.system_step(x, b_b, u, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[k],
+                                     beta[k] if k >= 2 else None, g, want_u=True, want_pool=not last)
+            xs.append(x)
+            us.append(u)
+        del b_b
+    return [xs[-1]], [wG0, wL0, wG1, wL1, cG0, cG1, *xs[:-1], *us]
 
-        gx = gout.contiguous()
-        gy = torch.zeros_like(y)
-        if n_st > 1:
-            gbb = torch.zeros_like(y)
-            gu_next = None
-            for k in range(n_st - 1, 0, -1):
-                # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue)
-                gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
-                                 galpha, gbeta, k, g, owned=k < n_st - 1)
-                a_bwd(xs[k], gu, -1.0, gx)                          #   - (A - I)^T gu
-                gu_next = gu
-            # b_B = y + prox terms(x_1)
-            K.bwd_lincomb(gbb, None, None, None, g, out=gy, accumulate=True)
-            _two_level(l0, l1, xs[1], gbb, gx, lambda lv, xx, g2, o: lv.prox_bwd(xx, g2, o))
-            del gbb
-        # x_1 = b_A + alpha_0 r_0, r_0 = b_A - A b_A
-        K.bwd_graph_dot(gx, us[0], galpha[0], g)
-        ga = K.bwd_lincomb(gx, alpha[0], None, None, g)
-        gba = gx.clone()
-        a_bwd(xs[0], ga, -1.0, gba)                                 # gx_1 - (A - I)^T (alpha_0 gx_1)
-        del ga
-        # b_A = y + ro0 G0 y + U ro1 G1 D y
-        K.bwd_lincomb(gba, None, None, None, g, out=gy, accumulate=True)
-        a_bwd(y, gba, 1.0, gy, glr=False)
-        del gba
 
-        # weights -> features
-        K.bwd_pair_weights(wG0, l0.gcG, l0.gwG)
-        K.bwd_pair_weights(wG1, l1.gcG, l1.gwG)
-        gf0, gf1 = torch.empty_like(f0), torch.empty_like(f1)
-        gM = {m: torch.zeros_like(p[f"{m}.multiM"]) for m in MODULES}
-        K.bwd_edge_weights(f0, 0, g, nf, p["GTVmodule00.multiM"], wG0, l0.gwG, gf0, gM["GTVmodule00"])
-        K.bwd_edge_weights(f0, c, g, nf, p["GLRmodule00.multiM"], wL0, l0.gwL, gf0, gM["GLRmodule00"])
-        K.bwd_edge_weights(f1, 0, g, nf, p["GTVmodule01.multiM"], wG1, l1.gwG, gf1, gM["GTVmodule01"])
-        K.bwd_edge_weights(f1, c, g, nf, p["GLRmodule01.multiM"], wL1, l1.gwL, gf1, gM["GLRmodule01"])
+def _mixture_fake(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
+    g = consts[0]
+    b, c, h, w = y.shape
+    n_st = dict(zip(PARAM_NAMES, params))["alphaCGD"].shape[0]
+    e0, e1 = _new(y, b, g, 4, h, w), _new(y, b, g, 4, h // 2, w // 2)
+    return [_new(y, b, c, h, w)], [e0, _new(y, b, g, 4, h, w), e1, _new(y, b, g, 4, h // 2, w // 2),
+                                   _new(y, b, g, 2, h, w), _new(y, b, g, 2, h // 2, w // 2),
+                                   *[_new(y, b, c, h, w) for _ in range(2 * n_st)]]
 
-        grads = {f"{m}.multiM": gM[m] for m in MODULES}
-        for m, gt in (("GTVmodule00", l0.gtapG), ("GLRmodule00", l0.gtapL),
-                      ("GTVmodule01", l1.gtapG), ("GLRmodule01", l1.gtapL)):
-            for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gt)):
-                grads[f"{m}.{q}"] = gq
-        grads["muys00"], grads["muys01"] = l0.gmu * l0.mu, l1.gmu * l1.mu
-        grads["ro00"], grads["ro01"] = l0.gro * l0.ro, l1.gro * l1.ro
-        grads["gamma00"] = l0.ggam * torch.exp(l0.log_gamma)
-        grads["gamma01"] = l1.ggam * torch.exp(l1.log_gamma)
-        grads["alphaCGD"], grads["betaCGD"] = galpha, gbeta
-        return (None, gy, gf0, gf1, *[grads[n] for n in PARAM_NAMES])
+
+def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
+    g = consts[0]
+    y, f0, f1 = inputs[:3]
+    params = inputs[3:]
+    n_st = (len(saved) - 6) // 2
+    wG0, wL0, wG1, wL1, cG0, cG1 = saved[:6]
+    xs = saved[6:6 + n_st]          # x_0 = b_A, x_1, ..., x_{S-1}
+    us = saved[6 + n_st:]           # r_0, u_1, ..., u_{S-1}
+    p = dict(zip(PARAM_NAMES, params))
+    c = y.shape[1]
+    nf = c // g
+    st = {m: tuple(p[f"{m}.{q}"] for q in STENCIL_PARAMS) for m in MODULES}
+    l0 = _Level(wL0, cG0, wG0, st["GLRmodule00"], st["GTVmodule00"], p["muys00"], p["ro00"], p["gamma00"], g)
+    l1 = _Level(wL1, cG1, wG1, st["GLRmodule01"], st["GTVmodule01"], p["muys01"], p["ro01"], p["gamma01"], g)
+    alpha, beta = p["alphaCGD"], p["betaCGD"]
+    galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
+
+    def a_bwd(x, gg, coef, out, glr=True):      # out += coef * (A - I)^T gg (+ parameter gradients)
+        _two_level(l0, l1, x, gg, out, lambda lv, xx, g2, o: lv.terms_bwd(xx, g2, coef, o, glr))
+
+    gx = gouts[0].contiguous()
+    gy = torch.zeros_like(y)
+    if n_st > 1:
+        gbb = torch.zeros_like(y)
+        gu_next = None
+        for k in range(n_st - 1, 0, -1):
+            # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue)
+            gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
+                             galpha, gbeta, k, g, owned=k < n_st - 1)
+            a_bwd(xs[k], gu, -1.0, gx)                          #   - (A - I)^T gu
+            gu_next = gu
+        # b_B = y + prox terms(x_1)
+        K.bwd_lincomb(gbb, None, None, None, g, out=gy, accumulate=True)
+        _two_level(l0, l1, xs[1], gbb, gx, lambda lv, xx, g2, o: lv.prox_bwd(xx, g2, o))
+        del gbb
+    # x_1 = b_A + alpha_0 r_0, r_0 = b_A - A b_A
+    K.bwd_graph_dot(gx, us[0], galpha[0], g)
+    ga = K.bwd_lincomb(gx, alpha[0], None, None, g)
+    gba = gx.clone()
+    a_bwd(xs[0], ga, -1.0, gba)                                 # gx_1 - (A - I)^T (alpha_0 gx_1)
+    del ga
+    # b_A = y + ro0 G0 y + U ro1 G1 D y
+    K.bwd_lincomb(gba, None, None, None, g, out=gy, accumulate=True)
+    a_bwd(y, gba, 1.0, gy, glr=False)
+    del gba
+
+    # weights -> features
+    K.bwd_pair_weights(wG0, l0.gcG, l0.gwG)
+    K.bwd_pair_weights(wG1, l1.gcG, l1.gwG)
+    gf0, gf1 = torch.empty_like(f0), torch.empty_like(f1)
+    gM = {m: torch.zeros_like(p[f"{m}.multiM"]) for m in MODULES}
+    K.bwd_edge_weights(f0, 0, g, nf, p["GTVmodule00.multiM"], wG0, l0.gwG, gf0, gM["GTVmodule00"])
+    K.bwd_edge_weights(f0, c, g, nf, p["GLRmodule00.multiM"], wL0, l0.gwL, gf0, gM["GLRmodule00"])
+    K.bwd_edge_weights(f1, 0, g, nf, p["GTVmodule01.multiM"], wG1, l1.gwG, gf1, gM["GTVmodule01"])
+    K.bwd_edge_weights(f1, c, g, nf, p["GLRmodule01.multiM"], wL1, l1.gwL, gf1, gM["GLRmodule01"])
+
+    grads = {f"{m}.multiM": gM[m] for m in MODULES}
+    for m, gt in (("GTVmodule00", l0.gtapG), ("GLRmodule00", l0.gtapL),
+                  ("GTVmodule01", l1.gtapG), ("GLRmodule01", l1.gtapL)):
+        for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gt)):
+            grads[f"{m}.{q}"] = gq
+    grads["muys00"], grads["muys01"] = l0.gmu * l0.mu, l1.gmu * l1.mu
+    grads["ro00"], grads["ro01"] = l0.gro * l0.ro, l1.gro * l1.ro
+    grads["gamma00"] = l0.ggam * torch.exp(l0.log_gamma)
+    grads["gamma01"] = l1.ggam * torch.exp(l1.log_gamma)
+    grads["alphaCGD"], grads["betaCGD"] = galpha, gbeta
+    return (gy, gf0, gf1, *[grads[n] for n in PARAM_NAMES])
+
+
+MIXTURE = OpaqueFunction("mixture_solve_train", 1, _mixture_fwd, _mixture_bwd, _mixture_fake)
 
 
 def mixture_solve(mod, y: Tensor, f0: Tensor, f1: Tensor) -> Tensor:
     """Differentiable MixtureGTVGLR solve (features given); all work on the HIP kernels."""
-    return _MixtureSolve.apply(mod.n_graphs, y, f0.contiguous(), f1.contiguous(), *solver_params(mod))
+    return MIXTURE([mod.n_graphs], y, f0.contiguous(), f1.contiguous(), *solver_params(mod))
 
 
 # ---- feature convolutions ----------------------------------------------------
-class Conv1x1Fn(torch.autograd.Function):
-    """nn.Conv2d(K, M, 1, bias=False): forward and data gradient on the HIP GEMM; the weight
-    gradient (a reduction over B*H*W) is one plain library GEMM (rocBLAS via torch.matmul)."""
+# nn.Conv2d(K, M, 1, bias=False): forward and data gradient on the HIP GEMM; the weight gradient (a
+# reduction over B*H*W) is one plain library GEMM (rocBLAS via torch.matmul)
+def _conv1x1_fwd(consts, x: Tensor, weight: Tensor):
+    return [K.conv1x1(x.contiguous(), weight.contiguous())], []
 
+
+def _conv1x1_bwd(consts, inputs, outs, saved, gouts, needs):
+    x, weight = inputs
+    g = gouts[0].contiguous()
+    m, k = weight.shape[:2]
+    gx = K.conv1x1(g, weight.reshape(m, k).t().contiguous().view(k, m, 1, 1)) if needs[0] else None
+    b = x.shape[0]
+    gw = torch.matmul(g.reshape(b, m, -1), x.reshape(b, k, -1).transpose(1, 2)).sum(0)
+    return gx, gw.view_as(weight)
+
+
+def _conv1x1_fake(consts, x: Tensor, weight: Tensor):
+    return [_new(x, x.shape[0], weight.shape[0], x.shape[2], x.shape[3])], []
+
+
+CONV1X1 = OpaqueFunction("conv1x1_train", 1, _conv1x1_fwd, _conv1x1_bwd, _conv1x1_fake)
+
+
+# nn.Conv2d(K, M, 2, stride=2, bias=False) (REF:593-602): HIP forward and data gradient, weight gradient
+# as one library GEMM over the 2x2 patches
+def _conv2x2_fwd(consts, x: Tensor, weight: Tensor):
+    return [K.conv2x2s2(x.contiguous(), weight.contiguous())], []
+
+
+def _conv2x2_bwd(consts, inputs, outs, saved, gouts, needs):
+    x, weight = inputs
+    g = gouts[0].contiguous()
+    b, k, h, w = x.shape
+    m = weight.shape[0]
+    gx = None
+    if needs[0]:
+        # one 4K-row GEMM (split-bf16 for M <= 128, fp32 MFMA above) + interleave (W % 4 == 0)
+        if w % 4 == 0:
+            gx = K.conv2x2s2_bwd_data_gemm(g, weight.contiguous(), h, w)
+        else:
+            gx = K.conv2x2s2_bwd_data(g, weight.contiguous(), h, w)
+    patches = x.reshape(b, k, h // 2, 2, w // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(b, -1, k * 4)
+    gw = torch.matmul(g.reshape(b, m, -1), patches).sum(0)
+    return gx, gw.view_as(weight)
+
+
+def _conv2x2_fake(consts, x: Tensor, weight: Tensor):
+    return [_new(x, x.shape[0], weight.shape[0], x.shape[2] // 2, x.shape[3] // 2)], []
+
+
+CONV2X2S2 = OpaqueFunction("conv2x2s2_train", 1, _conv2x2_fwd, _conv2x2_bwd, _conv2x2_fake)
+
+
+# img [B,Cin,H,W] -> [B,G*Cin,H,W] replicated over the graphs (REF13:918-921); the reverse sums the replicas
+def _repeat_fwd(consts, img: Tensor):
+    return [K.repeat_graphs(img.contiguous(), consts[0])], []
+
+
+def _repeat_bwd(consts, inputs, outs, saved, gouts, needs):
+    g = gouts[0]
+    b, c, h, w = g.shape
+    return (g.reshape(b, consts[0], c // consts[0], h, w).sum(1),)
+
+
+def _repeat_fake(consts, img: Tensor):
+    b, c, h, w = img.shape
+    return [_new(img, b, consts[0] * c, h, w)], []
+
+
+REPEAT_GRAPHS = OpaqueFunction("repeat_graphs_train", 1, _repeat_fwd, _repeat_bwd, _repeat_fake)
+
+
+class Conv1x1Fn:
     @staticmethod
-    def forward(ctx, x: Tensor, weight: Tensor) -> Tensor:
-        ctx.save_for_backward(x, weight)
-        return K.conv1x1(x, weight.contiguous())
+    def apply(x: Tensor, weight: Tensor) -> Tensor:
+        return CONV1X1([], x, weight)
 
+
+class Conv2x2s2Fn:
     @staticmethod
-    def backward(ctx, g: Tensor):
-        x, weight = ctx.saved_tensors
-        g = g.contiguous()
-        m, k = weight.shape[:2]
-        gx = K.conv1x1(g, weight.reshape(m, k).t().contiguous().view(k, m, 1, 1)) if ctx.needs_input_grad[0] else None
-        b = x.shape[0]
-        gw = torch.matmul(g.reshape(b, m, -1), x.reshape(b, k, -1).transpose(1, 2)).sum(0)
-        return gx, gw.view_as(weight)
+    def apply(x: Tensor, weight: Tensor) -> Tensor:
+        return CONV2X2S2([], x, weight)
 
 
-class Conv2x2s2Fn(torch.autograd.Function):
-    """nn.Conv2d(K, M, 2, stride=2, bias=False) (REF:593-602): HIP forward and data gradient,
-    weight gradient as one library GEMM over the 2x2 patches."""
-
+class RepeatGraphsFn:
     @staticmethod
-    def forward(ctx, x: Tensor, weight: Tensor) -> Tensor:
-        ctx.save_for_backward(x, weight)
-        return K.conv2x2s2(x, weight.contiguous())
-
-    @staticmethod
-    def backward(ctx, g: Tensor):
-        x, weight = ctx.saved_tensors
-        g = g.contiguous()
-        b, k, h, w = x.shape
-        m = weight.shape[0]
-        gx = None
-        if ctx.needs_input_grad[0]:
-            # one 4K-row GEMM (split-bf16 for M <= 128, fp32 MFMA above) + interleave (W % 4 == 0)
-            if w % 4 == 0:
-                gx = K.conv2x2s2_bwd_data_gemm(g, weight.contiguous(), h, w)
-            else:
-                gx = K.conv2x2s2_bwd_data(g, weight.contiguous(), h, w)
-        patches = x.reshape(b, k, h // 2, 2, w // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(b, -1, k * 4)
-        gw = torch.matmul(g.reshape(b, m, -1), patches).sum(0)
-        return gx, gw.view_as(weight)
-
-
-class RepeatGraphsFn(torch.autograd.Function):
-    """img [B,Cin,H,W] -> [B,G*Cin,H,W] replicated over the graphs (REF13:918-921); the
-    reverse sums the G replicas."""
-
-    @staticmethod
-    def forward(ctx, img: Tensor, n_graphs: int) -> Tensor:
-        ctx.n_graphs = n_graphs
-        return K.repeat_graphs(img.contiguous(), n_graphs)
-
-    @staticmethod
-    def backward(ctx, g: Tensor):
-        b, c, h, w = g.shape
-        return g.reshape(b, ctx.n_graphs, c // ctx.n_graphs, h, w).sum(1), None
+    def apply(img: Tensor, n_graphs: int) -> Tensor:
+        return REPEAT_GRAPHS([n_graphs], img)
 
 
 # ---- GLRFast / GTVFast / extract_edge_weights sub-API (REF:146-237, :391-523) ----------
@@ -339,70 +385,83 @@ def _taps_params(module) -> Tuple[Tensor, ...]:
     return (module.stats_kernel_p01, module.stats_kernel_p02a, module.stats_kernel_p02b, module.stats_kernel_p03)
 
 
-class _GraphApply(torch.autograd.Function):
-    """GLRFast.forward (kind 'glr': S^T (I - W) S x) or GTVFast.forward (kind 'gtv': C^T C x)."""
+GLR_KIND, GTV_KIND = 0, 1
 
-    @staticmethod
-    def forward(ctx, kind: str, n_graphs: int, x: Tensor, w: Tensor, p01, p02a, p02b, p03) -> Tensor:
-        st = Stencil(*[t.data_ptr() for t in (p01, p02a, p02b, p03)])
-        if kind == "glr":
-            out = K.system_half(x, w, None, st, K.NO_STENCIL, None, None, n_graphs)
-            ctx.save_for_backward(x, w, p01, p02a, p02b, p03)
-        else:
-            c = K.gtv_pair_weights(w)
-            out = K.system_half(x, None, c, K.NO_STENCIL, st, None, None, n_graphs)
-            ctx.save_for_backward(x, w, p01, p02a, p02b, p03, c)
-        ctx.kind, ctx.n_graphs = kind, n_graphs
-        return out
 
-    @staticmethod
-    def backward(ctx, gout: Tensor):
-        x, w, p01, p02a, p02b, p03 = ctx.saved_tensors[:6]
-        g, gout = ctx.n_graphs, gout.contiguous()
-        taps = K.stencil_taps(p01, p02a, p02b, p03)
-        one = torch.ones(g, dtype=torch.float32, device=x.device)
-        gx, gw, gtaps = torch.zeros_like(x), torch.zeros_like(w), torch.zeros_like(taps)
-        if ctx.kind == "glr":
-            glr_term_bwd(x, gout, taps, w, one, 1.0, g, gx, gw, None, gtaps)
-        else:
-            c = ctx.saved_tensors[6]
-            gc = torch.zeros_like(c)
-            gtv_term_bwd(x, gout, taps, c, one, 1.0, g, gx, gc, None, gtaps)
-            K.bwd_pair_weights(w, gc, gw)
-        return (None, None, gx, gw, *K.stencil_taps_backward(gtaps))
+# GLRFast.forward (GLR_KIND: S^T (I - W) S x) or GTVFast.forward (GTV_KIND: C^T C x)
+def _graph_apply_fwd(consts, x: Tensor, w: Tensor, p01, p02a, p02b, p03):
+    kind, g = consts
+    st = Stencil(*[t.data_ptr() for t in (p01, p02a, p02b, p03)])
+    if kind == GLR_KIND:
+        return [K.system_half(x, w, None, st, K.NO_STENCIL, None, None, g)], []
+    c = K.gtv_pair_weights(w)
+    return [K.system_half(x, None, c, K.NO_STENCIL, st, None, None, g)], [c]
+
+
+def _graph_apply_bwd(consts, inputs, outs, saved, gouts, needs):
+    kind, g = consts
+    x, w, p01, p02a, p02b, p03 = inputs
+    gout = gouts[0].contiguous()
+    taps = K.stencil_taps(p01, p02a, p02b, p03)
+    one = torch.ones(g, dtype=torch.float32, device=x.device)
+    gx, gw, gtaps = torch.zeros_like(x), torch.zeros_like(w), torch.zeros_like(taps)
+    if kind == GLR_KIND:
+        glr_term_bwd(x, gout, taps, w, one, 1.0, g, gx, gw, None, gtaps)
+    else:
+        c = saved[0]
+        gc = torch.zeros_like(c)
+        gtv_term_bwd(x, gout, taps, c, one, 1.0, g, gx, gc, None, gtaps)
+        K.bwd_pair_weights(w, gc, gw)
+    return (gx, gw, *K.stencil_taps_backward(gtaps))
+
+
+def _graph_apply_fake(consts, x: Tensor, w: Tensor, *taps):
+    b, g, _, h, ww = w.shape
+    return [torch.empty_like(x)], ([] if consts[0] == GLR_KIND else [_new(w, b, g, 2, h, ww)])
+
+
+GRAPH_APPLY = OpaqueFunction("graph_apply_train", 1, _graph_apply_fwd, _graph_apply_bwd, _graph_apply_fake)
 
 
 def graph_apply(module, kind: str, x5: Tensor, w: Tensor) -> Tensor:
     b, g, f, h, ww = x5.shape
-    out = _GraphApply.apply(kind, g, x5.reshape(b, g * f, h, ww).contiguous(), w.contiguous(), *_taps_params(module))
+    out = GRAPH_APPLY([GLR_KIND if kind == "glr" else GTV_KIND, g], x5.reshape(b, g * f, h, ww).contiguous(),
+                      w.contiguous(), *_taps_params(module))
     return out.view(b, g, f, h, ww)
 
 
-class _EdgeWeights(torch.autograd.Function):
-    """extract_edge_weights: features [B,G*F,H,W] -> (w [B,G,4,H,W], degree [B,G,H,W])."""
+# extract_edge_weights: features [B,G*F,H,W] -> (w [B,G,4,H,W], degree [B,G,H,W])
+def _edge_weights_fwd(consts, feat: Tensor, multiM: Tensor):
+    g = consts[0]
+    w, deg = K.edge_weights(feat, 0, g, feat.shape[1] // g, multiM, with_degree=True)
+    return [w, deg], []
 
-    @staticmethod
-    def forward(ctx, n_graphs: int, feat: Tensor, multiM: Tensor):
-        w, deg = K.edge_weights(feat, 0, n_graphs, feat.shape[1] // n_graphs, multiM, with_degree=True)
-        ctx.save_for_backward(feat, multiM, w)
-        ctx.n_graphs = n_graphs
-        return w, deg
 
-    @staticmethod
-    def backward(ctx, gw: Optional[Tensor], gdeg: Optional[Tensor]):
-        feat, multiM, w = ctx.saved_tensors
-        g = ctx.n_graphs
-        gw_t = torch.zeros_like(w) if gw is None else gw.contiguous().clone()
-        if gdeg is not None:                      # degree = sum_e w_e
-            gw_t += gdeg.unsqueeze(2)
-        gfeat, gM = torch.empty_like(feat), torch.zeros_like(multiM)
-        K.bwd_edge_weights(feat, 0, g, feat.shape[1] // g, multiM, w, gw_t, gfeat, gM)
-        return None, gfeat, gM
+def _edge_weights_bwd(consts, inputs, outs, saved, gouts, needs):
+    feat, multiM = inputs
+    w = outs[0]
+    gw, gdeg = gouts
+    g = consts[0]
+    gw_t = torch.zeros_like(w) if gw is None else gw.contiguous().clone()
+    if gdeg is not None:                      # degree = sum_e w_e
+        gw_t += gdeg.unsqueeze(2)
+    gfeat, gM = torch.empty_like(feat), torch.zeros_like(multiM)
+    K.bwd_edge_weights(feat, 0, g, feat.shape[1] // g, multiM, w, gw_t, gfeat, gM)
+    return gfeat, gM
+
+
+def _edge_weights_fake(consts, feat: Tensor, multiM: Tensor):
+    b, _, h, w = feat.shape
+    g = consts[0]
+    return [_new(feat, b, g, 4, h, w), _new(feat, b, g, h, w)], []
+
+
+EDGE_WEIGHTS = OpaqueFunction("edge_weights_train", 2, _edge_weights_fwd, _edge_weights_bwd, _edge_weights_fake)
 
 
 def edge_weights(module, f5: Tensor):
     b, g, f, h, w = f5.shape
-    return _EdgeWeights.apply(g, f5.reshape(b, g * f, h, w).contiguous(), module.multiM)
+    return EDGE_WEIGHTS([g], f5.reshape(b, g * f, h, w).contiguous(), module.multiM)
 
 
 # ---- v10 MixtureGLR (lib/model_GLR_GTV_deep_v10.py:241-335) -----------------------------
@@ -410,66 +469,70 @@ V10_PARAMS = ("GLRmodule00.multiM",) + tuple(f"GLRmodule00.{q}" for q in STENCIL
     "muys00", "alphaCGD", "betaCGD")
 
 
-class _GLRSolve(torch.autograd.Function):
-    """(y, feat, params) -> x_S of the GLR-only heavy-ball solver, A = I + mu L with mu linear."""
+# (y, feat, params) -> x_S of the GLR-only heavy-ball solver, A = I + mu L with mu linear
+def _glr_fwd(consts, y: Tensor, feat: Tensor, *params: Tensor):
+    p = dict(zip(V10_PARAMS, params))
+    g = consts[0]
+    wL, _ = K.edge_weights(feat, 0, g, y.shape[1] // g, p["GLRmodule00.multiM"])
+    st = Stencil(*[p[f"GLRmodule00.{q}"].data_ptr() for q in STENCIL_PARAMS])
+    mu, alpha, beta = p["muys00"], p["alphaCGD"], p["betaCGD"]
+    n_st = alpha.shape[0]
+    x, u = K.glr_stage(y, y, None, wL, st, mu, alpha[0], None, g)       # u_0 = r_0, x_1
+    xs, us = [y, x], [u]
+    for k in range(1, n_st):
+        x, u = K.glr_stage(x, y, u, wL, st, mu, alpha[k], beta[k], g)
+        xs.append(x)
+        us.append(u)
+    return [xs[-1]], [wL, *xs[1:-1], *us]
 
-    @staticmethod
-    def forward(ctx, n_graphs: int, y: Tensor, feat: Tensor, *params: Tensor) -> Tensor:
-        p = dict(zip(V10_PARAMS, params))
-        g = n_graphs
-        wL, _ = K.edge_weights(feat, 0, g, y.shape[1] // g, p["GLRmodule00.multiM"])
-        st = Stencil(*[p[f"GLRmodule00.{q}"].data_ptr() for q in STENCIL_PARAMS])
-        mu, alpha, beta = p["muys00"], p["alphaCGD"], p["betaCGD"]
-        n_st = alpha.shape[0]
-        x, u = K.glr_stage(y, y, None, wL, st, mu, alpha[0], None, g)       # u_0 = r_0, x_1
-        xs, us = [y, x], [u]
-        for k in range(1, n_st):
-            x, u = K.glr_stage(x, y, u, wL, st, mu, alpha[k], beta[k], g)
-            xs.append(x)
-            us.append(u)
-        ctx.n_graphs, ctx.n_st = g, n_st
-        ctx.save_for_backward(y, feat, wL, *params, *xs[1:-1], *us)
-        return xs[-1]
 
-    @staticmethod
-    def backward(ctx, gout: Tensor):
-        g, n_st = ctx.n_graphs, ctx.n_st
-        sv = ctx.saved_tensors
-        y, feat, wL = sv[:3]
-        npar = len(V10_PARAMS)
-        params = sv[3:3 + npar]
-        xs = (y,) + tuple(sv[3 + npar:3 + npar + n_st - 1])      # x_0 = y, x_1 .. x_{S-1}
-        us = sv[3 + npar + n_st - 1:]                             # u_0 .. u_{S-1}
-        p = dict(zip(V10_PARAMS, params))
-        mu, alpha, beta = p["muys00"], p["alphaCGD"], p["betaCGD"]
-        taps = K.stencil_taps(*[p[f"GLRmodule00.{q}"] for q in STENCIL_PARAMS])
-        gw, gtaps, gmu = torch.zeros_like(wL), torch.zeros_like(taps), torch.zeros_like(mu)
-        galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
-        gy = torch.zeros_like(y)
-        gx = gout.contiguous()
-        gu_next = None
-        for k in range(n_st - 1, -1, -1):
-            # x_{k+1} = x_k + a_k u_k,  u_k = (y - A x_k) + b_k u_{k-1}   (u_{-1} = 0; x_0 = y)
-            gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 1 else None, alpha, beta, gy, galpha, gbeta,
-                             k, g, owned=k < n_st - 1)                     # gx <- gx_{k+1} - gu
-            if k >= 1:
-                glr_term_bwd(xs[k], gu, taps, wL, mu, -1.0, g, gx, gw, gmu, gtaps)
-            else:                                                           # x_0 = y
-                gy.add_(gx)
-                glr_term_bwd(y, gu, taps, wL, mu, -1.0, g, gy, gw, gmu, gtaps)
-            gu_next = gu
-        gfeat, gM = torch.empty_like(feat), torch.zeros_like(p["GLRmodule00.multiM"])
-        K.bwd_edge_weights(feat, 0, g, y.shape[1] // g, p["GLRmodule00.multiM"], wL, gw, gfeat, gM)
-        grads = {"GLRmodule00.multiM": gM, "muys00": gmu, "alphaCGD": galpha, "betaCGD": gbeta}
-        for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gtaps)):
-            grads[f"GLRmodule00.{q}"] = gq
-        return (None, gy, gfeat, *[grads[n] for n in V10_PARAMS])
+def _glr_fake(consts, y: Tensor, feat: Tensor, *params: Tensor):
+    b, c, h, w = y.shape
+    n_st = dict(zip(V10_PARAMS, params))["alphaCGD"].shape[0]
+    return [torch.empty_like(y)], [_new(y, b, consts[0], 4, h, w), *[torch.empty_like(y) for _ in range(2 * n_st - 1)]]
+
+
+def _glr_bwd(consts, inputs, outs, saved, gouts, needs):
+    g = consts[0]
+    y, feat = inputs[:2]
+    params = inputs[2:]
+    n_st = len(saved) // 2
+    wL = saved[0]
+    xs = (y,) + tuple(saved[1:n_st])        # x_0 = y, x_1 .. x_{S-1}
+    us = saved[n_st:]                       # u_0 .. u_{S-1}
+    p = dict(zip(V10_PARAMS, params))
+    mu, alpha, beta = p["muys00"], p["alphaCGD"], p["betaCGD"]
+    taps = K.stencil_taps(*[p[f"GLRmodule00.{q}"] for q in STENCIL_PARAMS])
+    gw, gtaps, gmu = torch.zeros_like(wL), torch.zeros_like(taps), torch.zeros_like(mu)
+    galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
+    gy = torch.zeros_like(y)
+    gx = gouts[0].contiguous()
+    gu_next = None
+    for k in range(n_st - 1, -1, -1):
+        # x_{k+1} = x_k + a_k u_k,  u_k = (y - A x_k) + b_k u_{k-1}   (u_{-1} = 0; x_0 = y)
+        gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 1 else None, alpha, beta, gy, galpha, gbeta,
+                         k, g, owned=k < n_st - 1)                     # gx <- gx_{k+1} - gu
+        if k >= 1:
+            glr_term_bwd(xs[k], gu, taps, wL, mu, -1.0, g, gx, gw, gmu, gtaps)
+        else:                                                           # x_0 = y
+            gy.add_(gx)
+            glr_term_bwd(y, gu, taps, wL, mu, -1.0, g, gy, gw, gmu, gtaps)
+        gu_next = gu
+    gfeat, gM = torch.empty_like(feat), torch.zeros_like(p["GLRmodule00.multiM"])
+    K.bwd_edge_weights(feat, 0, g, y.shape[1] // g, p["GLRmodule00.multiM"], wL, gw, gfeat, gM)
+    grads = {"GLRmodule00.multiM": gM, "muys00": gmu, "alphaCGD": galpha, "betaCGD": gbeta}
+    for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gtaps)):
+        grads[f"GLRmodule00.{q}"] = gq
+    return (gy, gfeat, *[grads[n] for n in V10_PARAMS])
+
+
+GLR_SOLVE = OpaqueFunction("glr_solve_train", 1, _glr_fwd, _glr_bwd, _glr_fake)
 
 
 def glr_solve(mod, y: Tensor, feat: Tensor) -> Tensor:
     params = [mod.GLRmodule00.multiM] + [getattr(mod.GLRmodule00, q) for q in STENCIL_PARAMS] + [
         mod.muys00, mod.alphaCGD, mod.betaCGD]
-    return _GLRSolve.apply(mod.n_graphs, y, feat.contiguous(), *params)
+    return GLR_SOLVE([mod.n_graphs], y, feat.contiguous(), *params)
 
 
 # ---- two-scale GLR-only solver (config C2; glr_v10.MultiScaleMixtureGLR) ---------------------
@@ -478,81 +541,87 @@ GLR2_PARAMS = ("GLRmodule00.multiM", "GLRmodule01.multiM") + tuple(
     "muys00", "muys01", "alphaCGD", "betaCGD")
 
 
-class _GLR2Solve(torch.autograd.Function):
-    """(y, f0, f1, params) -> x_S of  A = I + e^mu0 L0 + U e^mu1 L1 D  under the v10 recurrence."""
+# (y, f0, f1, params) -> x_S of  A = I + e^mu0 L0 + U e^mu1 L1 D  under the v10 recurrence
+def _glr2_fwd(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
+    p = dict(zip(GLR2_PARAMS, params))
+    g = consts[0]
+    nf = y.shape[1] // g
+    wL0, _ = K.edge_weights(f0, 0, g, nf, p["GLRmodule00.multiM"])
+    wL1, _ = K.edge_weights(f1, 0, g, nf, p["GLRmodule01.multiM"])
+    sL0 = Stencil(*[p[f"GLRmodule00.{q}"].data_ptr() for q in STENCIL_PARAMS])
+    sL1 = Stencil(*[p[f"GLRmodule01.{q}"].data_ptr() for q in STENCIL_PARAMS])
+    mu0, mu1, alpha, beta = p["muys00"], p["muys01"], p["alphaCGD"], p["betaCGD"]
+    n_st = alpha.shape[0]
+    x, u, xd = y, None, K.pool2(y)
+    xs, us = [y], []
+    for k in range(n_st):
+        t = K.system_half(xd, wL1, None, sL1, K.NO_STENCIL, mu1, None, g)
+        x, u, xd = K.system_step(x, y, u, t, wL0, None, sL0, K.NO_STENCIL, mu0, None, alpha[k],
+                                 beta[k] if k >= 1 else None, g, want_u=True, want_pool=k < n_st - 1)
+        xs.append(x)
+        us.append(u)
+    return [xs[-1]], [wL0, wL1, *xs[1:-1], *us]
 
-    @staticmethod
-    def forward(ctx, n_graphs: int, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor) -> Tensor:
-        p = dict(zip(GLR2_PARAMS, params))
-        g = n_graphs
-        nf = y.shape[1] // g
-        wL0, _ = K.edge_weights(f0, 0, g, nf, p["GLRmodule00.multiM"])
-        wL1, _ = K.edge_weights(f1, 0, g, nf, p["GLRmodule01.multiM"])
-        sL0 = Stencil(*[p[f"GLRmodule00.{q}"].data_ptr() for q in STENCIL_PARAMS])
-        sL1 = Stencil(*[p[f"GLRmodule01.{q}"].data_ptr() for q in STENCIL_PARAMS])
-        mu0, mu1, alpha, beta = p["muys00"], p["muys01"], p["alphaCGD"], p["betaCGD"]
-        n_st = alpha.shape[0]
-        x, u, xd = y, None, K.pool2(y)
-        xs, us = [y], []
-        for k in range(n_st):
-            t = K.system_half(xd, wL1, None, sL1, K.NO_STENCIL, mu1, None, g)
-            x, u, xd = K.system_step(x, y, u, t, wL0, None, sL0, K.NO_STENCIL, mu0, None, alpha[k],
-                                     beta[k] if k >= 1 else None, g, want_u=True, want_pool=k < n_st - 1)
-            xs.append(x)
-            us.append(u)
-        ctx.n_graphs, ctx.n_st = g, n_st
-        ctx.save_for_backward(y, f0, f1, wL0, wL1, *params, *xs[1:-1], *us)
-        return xs[-1]
 
-    @staticmethod
-    def backward(ctx, gout: Tensor):
-        g, n_st = ctx.n_graphs, ctx.n_st
-        sv = ctx.saved_tensors
-        y, f0, f1, wL0, wL1 = sv[:5]
-        npar = len(GLR2_PARAMS)
-        params = sv[5:5 + npar]
-        xs = (y,) + tuple(sv[5 + npar:5 + npar + n_st - 1])      # x_0 = y, x_1 .. x_{S-1}
-        us = sv[5 + npar + n_st - 1:]                             # u_0 .. u_{S-1}
-        p = dict(zip(GLR2_PARAMS, params))
-        mu0, mu1 = torch.exp(p["muys00"]), torch.exp(p["muys01"])
-        alpha, beta = p["alphaCGD"], p["betaCGD"]
-        taps0 = K.stencil_taps(*[p[f"GLRmodule00.{q}"] for q in STENCIL_PARAMS])
-        taps1 = K.stencil_taps(*[p[f"GLRmodule01.{q}"] for q in STENCIL_PARAMS])
-        gw0, gw1 = torch.zeros_like(wL0), torch.zeros_like(wL1)
-        gt0, gt1 = torch.zeros_like(taps0), torch.zeros_like(taps1)
-        gm0, gm1 = torch.zeros_like(mu0), torch.zeros_like(mu1)
-        galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
-        gy = torch.zeros_like(y)
+def _glr2_fake(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
+    b, c, h, w = y.shape
+    g = consts[0]
+    n_st = dict(zip(GLR2_PARAMS, params))["alphaCGD"].shape[0]
+    return [torch.empty_like(y)], [_new(y, b, g, 4, h, w), _new(y, b, g, 4, h // 2, w // 2),
+                                   *[torch.empty_like(y) for _ in range(2 * n_st - 1)]]
 
-        def a_bwd(x: Tensor, gu: Tensor, out: Tensor) -> None:     # out -= (A - I)^T gu (+ params)
-            glr_term_bwd(x, gu, taps0, wL0, mu0, -1.0, g, out, gw0, gm0, gt0)
-            xd, gd = K.pool2(x), K.pool2(gu)                       # U^T = D
-            gxd = torch.zeros_like(xd)
-            glr_term_bwd(xd, gd, taps1, wL1, mu1, -1.0, g, gxd, gw1, gm1, gt1)
-            K.bwd_unpool2_acc(gxd, out)                            # D^T = U
 
-        gx = gout.contiguous()
-        gu_next = None
-        for k in range(n_st - 1, -1, -1):
-            gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 1 else None, alpha, beta, gy, galpha, gbeta,
-                             k, g, owned=k < n_st - 1)                     # gx <- gx_{k+1} - gu
-            if k >= 1:
-                a_bwd(xs[k], gu, gx)
-            else:                                                           # x_0 = y
-                gy.add_(gx)
-                a_bwd(y, gu, gy)
-            gu_next = gu
-        nf = y.shape[1] // g
-        gf0, gf1 = torch.empty_like(f0), torch.empty_like(f1)
-        gM0, gM1 = torch.zeros_like(p["GLRmodule00.multiM"]), torch.zeros_like(p["GLRmodule01.multiM"])
-        K.bwd_edge_weights(f0, 0, g, nf, p["GLRmodule00.multiM"], wL0, gw0, gf0, gM0)
-        K.bwd_edge_weights(f1, 0, g, nf, p["GLRmodule01.multiM"], wL1, gw1, gf1, gM1)
-        grads = {"GLRmodule00.multiM": gM0, "GLRmodule01.multiM": gM1, "muys00": gm0 * mu0, "muys01": gm1 * mu1,
-                 "alphaCGD": galpha, "betaCGD": gbeta}
-        for m, gt in (("GLRmodule00", gt0), ("GLRmodule01", gt1)):
-            for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gt)):
-                grads[f"{m}.{q}"] = gq
-        return (None, gy, gf0, gf1, *[grads[n] for n in GLR2_PARAMS])
+def _glr2_bwd(consts, inputs, outs, saved, gouts, needs):
+    g = consts[0]
+    y, f0, f1 = inputs[:3]
+    params = inputs[3:]
+    n_st = (len(saved) - 1) // 2
+    wL0, wL1 = saved[:2]
+    xs = (y,) + tuple(saved[2:2 + n_st - 1])      # x_0 = y, x_1 .. x_{S-1}
+    us = saved[2 + n_st - 1:]                     # u_0 .. u_{S-1}
+    p = dict(zip(GLR2_PARAMS, params))
+    mu0, mu1 = torch.exp(p["muys00"]), torch.exp(p["muys01"])
+    alpha, beta = p["alphaCGD"], p["betaCGD"]
+    taps0 = K.stencil_taps(*[p[f"GLRmodule00.{q}"] for q in STENCIL_PARAMS])
+    taps1 = K.stencil_taps(*[p[f"GLRmodule01.{q}"] for q in STENCIL_PARAMS])
+    gw0, gw1 = torch.zeros_like(wL0), torch.zeros_like(wL1)
+    gt0, gt1 = torch.zeros_like(taps0), torch.zeros_like(taps1)
+    gm0, gm1 = torch.zeros_like(mu0), torch.zeros_like(mu1)
+    galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
+    gy = torch.zeros_like(y)
+
+    def a_bwd(x: Tensor, gu: Tensor, out: Tensor) -> None:     # out -= (A - I)^T gu (+ params)
+        glr_term_bwd(x, gu, taps0, wL0, mu0, -1.0, g, out, gw0, gm0, gt0)
+        xd, gd = K.pool2(x), K.pool2(gu)                       # U^T = D
+        gxd = torch.zeros_like(xd)
+        glr_term_bwd(xd, gd, taps1, wL1, mu1, -1.0, g, gxd, gw1, gm1, gt1)
+        K.bwd_unpool2_acc(gxd, out)                            # D^T = U
+
+    gx = gouts[0].contiguous()
+    gu_next = None
+    for k in range(n_st - 1, -1, -1):
+        gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 1 else None, alpha, beta, gy, galpha, gbeta,
+                         k, g, owned=k < n_st - 1)                     # gx <- gx_{k+1} - gu
+        if k >= 1:
+            a_bwd(xs[k], gu, gx)
+        else:                                                           # x_0 = y
+            gy.add_(gx)
+            a_bwd(y, gu, gy)
+        gu_next = gu
+    nf = y.shape[1] // g
+    gf0, gf1 = torch.empty_like(f0), torch.empty_like(f1)
+    gM0, gM1 = torch.zeros_like(p["GLRmodule00.multiM"]), torch.zeros_like(p["GLRmodule01.multiM"])
+    K.bwd_edge_weights(f0, 0, g, nf, p["GLRmodule00.multiM"], wL0, gw0, gf0, gM0)
+    K.bwd_edge_weights(f1, 0, g, nf, p["GLRmodule01.multiM"], wL1, gw1, gf1, gM1)
+    grads = {"GLRmodule00.multiM": gM0, "GLRmodule01.multiM": gM1, "muys00": gm0 * mu0, "muys01": gm1 * mu1,
+             "alphaCGD": galpha, "betaCGD": gbeta}
+    for m, gt in (("GLRmodule00", gt0), ("GLRmodule01", gt1)):
+        for q, gq in zip(STENCIL_PARAMS, K.stencil_taps_backward(gt)):
+            grads[f"{m}.{q}"] = gq
+    return (gy, gf0, gf1, *[grads[n] for n in GLR2_PARAMS])
+
+
+GLR2_SOLVE = OpaqueFunction("glr2_solve_train", 1, _glr2_fwd, _glr2_bwd, _glr2_fake)
 
 
 def glr2_solve(mod, y: Tensor, f0: Tensor, f1: Tensor) -> Tensor:
@@ -562,7 +631,7 @@ def glr2_solve(mod, y: Tensor, f0: Tensor, f1: Tensor) -> Tensor:
         for part in name.split("."):
             obj = getattr(obj, part)
         params.append(obj)
-    return _GLR2Solve.apply(mod.n_graphs, y, f0.contiguous(), f1.contiguous(), *params)
+    return GLR2_SOLVE([mod.n_graphs], y, f0.contiguous(), f1.contiguous(), *params)
 
 
 # ---- LocalNonLinearBlock (nsubnets = 1; REF:911-964, REF13:541-575) ---------------------
@@ -570,60 +639,191 @@ def _mat(w: Tensor, rows: int) -> Tensor:
     return w.reshape(rows, -1)
 
 
-class LNBFn(torch.autograd.Function):
-    """out = s0 x + s1 W2 gate(dw3x3(W1 LN(x))): fused HIP forward; the reverse recomputes
-    n, h, h', gate with HIP kernels and runs the adjoints (GEMMs: HIP conv1x1 for the data
-    gradients, one library GEMM per weight gradient)."""
+# out = s0 x + s1 W2 gate(dw3x3(W1 LN(x))): fused HIP forward; the reverse recomputes n, h, h', gate
+# with HIP kernels and runs the adjoints (GEMMs: HIP conv1x1 for the data gradients, one library GEMM
+# per weight gradient)
+def _lnb_fwd(consts, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor):
+    c, hid2 = x.shape[1], w1.shape[0]
+    out = K.lnb_forward(x.contiguous(), ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(),
+                        _mat(wdw, hid2).contiguous(), _mat(w2, c).contiguous(), skip.contiguous())
+    return [out], []
 
-    @staticmethod
-    def forward(ctx, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor) -> Tensor:
-        c, hid2 = x.shape[1], w1.shape[0]
-        out = K.lnb_forward(x, ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(),
-                            _mat(wdw, hid2).contiguous(), _mat(w2, c).contiguous(), skip.contiguous())
-        ctx.save_for_backward(x, ln_w, w1, wdw, w2, skip)
-        return out
 
+def _lnb_fake(consts, x: Tensor, *weights: Tensor):
+    return [torch.empty_like(x)], []
+
+
+def _lnb_bwd(consts, inputs, outs, saved, gouts, needs):
+    x, ln_w, w1, wdw, w2, skip = inputs
+    gout = gouts[0].contiguous()
+    b, c, h, w = x.shape
+    hid2 = w1.shape[0]
+    hid = hid2 // 2
+    lnw, W1, Wdw, W2 = ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(), _mat(wdw, hid2).contiguous(), \
+        _mat(w2, c).contiguous()
+    n, isd = K.lnb_norm(x, lnw)
+    hh = K.conv1x1(n, W1.view(hid2, c, 1, 1))
+    # row-kernel widths: the depthwise output hp is never stored (gate from hh in one pass, the
+    # reverse recomputes hp from hh); else the per-stage kernels
+    rows = FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w)
+    if rows:
+        hp = None
+        gate = K.lnb_dw3_gate(hh, Wdw)
+    else:
+        hp = K.dwconv3(hh, Wdw)
+        gate, _ = K.lnb_gate(hp)
+    gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
+    K.bwd_graph_dot(gout, x, gskip[0:1], 1)
+    s1 = skip[1:2].contiguous()
+    # gw2 = s1 gout gate^T; gq = W2^T gout: the gate reverse takes s1 and returns
+    # <gout, W2 gate> = <gq, gate> for the skip weight (no recomputed W2 gate)
+    gw2 = torch.matmul(gout.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0) * s1
+    del gate
+    gq = K.conv1x1(gout, W2.t().contiguous().view(hid, c, 1, 1))
+    gwdw = torch.zeros_like(Wdw)
+    if rows:                                        # ghp formed in registers, never in HBM
+        gh = K.lnb_gate_dw3_bwd(None, gq, s1, hh, Wdw, gwdw, gskip[1:2])
+        del hp, gq, hh
+    else:
+        ghp = K.lnb_gate_bwd_scaled(hp, gq, s1, gskip[1:2])
+        del hp, gq
+        gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
+        del ghp, hh
+    gw1 = torch.matmul(gh.reshape(b, hid2, -1), n.reshape(b, c, -1).transpose(1, 2)).sum(0)
+    gn = K.conv1x1(gh, W1.t().contiguous().view(c, hid2, 1, 1))
+    del gh, n
+    gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
+    glnw = torch.zeros_like(lnw)
+    K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
+    return gx, glnw.view_as(ln_w), gw1.view_as(w1), gwdw.view_as(wdw), gw2.view_as(w2), gskip
+
+
+LNB = OpaqueFunction("lnb_train", 1, _lnb_fwd, _lnb_bwd, _lnb_fake)
+
+
+class LNBFn:
     @staticmethod
-    def backward(ctx, gout: Tensor):
-        x, ln_w, w1, wdw, w2, skip = ctx.saved_tensors
-        gout = gout.contiguous()
-        b, c, h, w = x.shape
-        hid2 = w1.shape[0]
-        hid = hid2 // 2
-        lnw, W1, Wdw, W2 = ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(), _mat(wdw, hid2).contiguous(), \
-            _mat(w2, c).contiguous()
-        n, isd = K.lnb_norm(x, lnw)
-        hh = K.conv1x1(n, W1.view(hid2, c, 1, 1))
-        # row-kernel widths: the depthwise output hp is never stored (gate from hh in one pass, the
-        # reverse recomputes hp from hh); else the per-stage kernels
-        rows = FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w)
-        if rows:
-            hp = None
-            gate = K.lnb_dw3_gate(hh, Wdw)
-        else:
-            hp = K.dwconv3(hh, Wdw)
-            gate, _ = K.lnb_gate(hp)
-        gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
-        K.bwd_graph_dot(gout, x, gskip[0:1], 1)
-        s1 = skip[1:2].contiguous()
-        # gw2 = s1 gout gate^T; gq = W2^T gout: the gate reverse takes s1 and returns
-        # <gout, W2 gate> = <gq, gate> for the skip weight (no recomputed W2 gate)
-        gw2 = torch.matmul(gout.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0) * s1
-        del gate
-        gq = K.conv1x1(gout, W2.t().contiguous().view(hid, c, 1, 1))
-        gwdw = torch.zeros_like(Wdw)
-        if rows:                                        # ghp formed in registers, never in HBM
-            gh = K.lnb_gate_dw3_bwd(None, gq, s1, hh, Wdw, gwdw, gskip[1:2])
-            del hp, gq, hh
-        else:
-            ghp = K.lnb_gate_bwd_scaled(hp, gq, s1, gskip[1:2])
-            del hp, gq
-            gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
-            del ghp, hh
-        gw1 = torch.matmul(gh.reshape(b, hid2, -1), n.reshape(b, c, -1).transpose(1, 2)).sum(0)
-        gn = K.conv1x1(gh, W1.t().contiguous().view(c, hid2, 1, 1))
-        del gh, n
-        gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
-        glnw = torch.zeros_like(lnw)
-        K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
-        return gx, glnw.view_as(ln_w), gw1.view_as(w1), gwdw.view_as(wdw), gw2.view_as(w2), gskip
+    def apply(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor) -> Tensor:
+        return LNB([], x, ln_w, w1, wdw, w2, skip)
+
+
+# ---- the GLRFast / GTVFast module methods, differentiable (REF:128-228, :452-516) ------------
+# Forward: the standalone sub-API kernels (csrc/subapi_ops.hip); reverse: csrc/subapi_bwd.hip.
+# Stencil inputs are the module's four stats_kernel_p* parameters; tap gradients come back per
+# channel [G*F, 5] and are chained to them by kernels.stencil_taps_backward.
+def _st4(ps) -> Stencil:
+    return Stencil(*[p.data_ptr() for p in ps])
+
+
+def _neighbors_fwd(consts, x: Tensor):
+    return [K.neighbor_gather(x.contiguous())], []
+
+
+def _neighbors_bwd(consts, inputs, outs, saved, gouts, needs):
+    return (K.neighbor_gather_bwd(gouts[0].contiguous()),)
+
+
+def _neighbors_fake(consts, x: Tensor):
+    b, c, h, w = x.shape
+    return [_new(x, b, c, 4, h, w)], []
+
+
+NEIGHBORS = OpaqueFunction("neighbor_gather_train", 1, _neighbors_fwd, _neighbors_bwd, _neighbors_fake)
+
+
+def _normalize_fwd(consts, f5: Tensor, multiM: Tensor):
+    return [K.normalize_features(f5.contiguous(), multiM.contiguous())], []
+
+
+def _normalize_bwd(consts, inputs, outs, saved, gouts, needs):
+    f5, multiM = inputs
+    b, g, f, h, w = f5.shape
+    gM = torch.zeros_like(multiM)
+    gf = K.normalize_features_bwd(f5.contiguous(), multiM.contiguous(), gouts[0].contiguous().view(b, g, f, h, w), gM)
+    return gf, gM
+
+
+def _normalize_fake(consts, f5: Tensor, multiM: Tensor):
+    b, g, f, h, w = f5.shape
+    return [_new(f5, b, g * f, h, w)], []
+
+
+NORMALIZE = OpaqueFunction("normalize_features_train", 1, _normalize_fwd, _normalize_bwd, _normalize_fake)
+
+
+def _taps_grads(gtaps: Tensor, ps) -> Tuple[Tensor, ...]:
+    return tuple(gq.view_as(p) for gq, p in zip(K.stencil_taps_backward(gtaps), ps))
+
+
+def _stats_fwd(consts, x5: Tensor, *ps: Tensor):
+    return [K.stats_conv(x5.contiguous(), _st4(ps), bool(consts[0]))], []
+
+
+def _stats_bwd(consts, inputs, outs, saved, gouts, needs):
+    x5, ps = inputs[0], inputs[1:]
+    gtaps = torch.zeros((x5.shape[1] * x5.shape[2], 5), dtype=torch.float32, device=x5.device)
+    gx = K.stats_conv_bwd(x5.contiguous(), _st4(ps), bool(consts[0]), gouts[0].contiguous(), gtaps)
+    return (gx, *_taps_grads(gtaps, ps))
+
+
+def _stats_fake(consts, x5: Tensor, *ps: Tensor):
+    return [torch.empty_like(x5)], []
+
+
+STATS_CONV = OpaqueFunction("stats_conv_train", 1, _stats_fwd, _stats_bwd, _stats_fake)
+
+
+def _lnorm_fwd(consts, x5: Tensor, w: Tensor):
+    return [K.glr_op_L_norm(x5.contiguous(), w.contiguous())], []
+
+
+def _lnorm_bwd(consts, inputs, outs, saved, gouts, needs):
+    x5, w = inputs
+    return K.glr_op_L_norm_bwd(x5.contiguous(), w.contiguous(), gouts[0].contiguous())
+
+
+def _lnorm_fake(consts, x5: Tensor, w: Tensor):
+    return [torch.empty_like(x5)], []
+
+
+OP_L_NORM = OpaqueFunction("glr_op_L_norm_train", 1, _lnorm_fwd, _lnorm_bwd, _lnorm_fake)
+
+
+def _opc_fwd(consts, x5: Tensor, w: Tensor, *ps: Tensor):
+    return [K.gtv_op_C(x5.contiguous(), w.contiguous(), _st4(ps))], []
+
+
+def _opc_bwd(consts, inputs, outs, saved, gouts, needs):
+    x5, w, ps = inputs[0], inputs[1], inputs[2:]
+    gtaps = torch.zeros((x5.shape[1] * x5.shape[2], 5), dtype=torch.float32, device=x5.device)
+    gx, gw = K.gtv_op_C_bwd(x5.contiguous(), w.contiguous(), _st4(ps), gouts[0].contiguous(), gtaps)
+    return (gx, gw, *_taps_grads(gtaps, ps))
+
+
+def _opc_fake(consts, x5: Tensor, w: Tensor, *ps: Tensor):
+    b, g, f, h, ww = x5.shape
+    return [_new(x5, b, g, f, 4, h, ww)], []
+
+
+OP_C = OpaqueFunction("gtv_op_C_train", 1, _opc_fwd, _opc_bwd, _opc_fake)
+
+
+def _opct_fwd(consts, e6: Tensor, w: Tensor, *ps: Tensor):
+    out, z = K.gtv_op_C_transpose(e6.contiguous(), w.contiguous(), _st4(ps), want_work=True)
+    return [out], [z]
+
+
+def _opct_bwd(consts, inputs, outs, saved, gouts, needs):
+    e6, w, ps = inputs[0], inputs[1], inputs[2:]
+    gtaps = torch.zeros((e6.shape[1] * e6.shape[2], 5), dtype=torch.float32, device=e6.device)
+    gE, gw = K.gtv_op_C_transpose_bwd(e6.contiguous(), w.contiguous(), _st4(ps), saved[0], gouts[0].contiguous(),
+                                      gtaps)
+    return (gE, gw, *_taps_grads(gtaps, ps))
+
+
+def _opct_fake(consts, e6: Tensor, w: Tensor, *ps: Tensor):
+    b, g, f, _, h, ww = e6.shape
+    return [_new(e6, b, g, f, h, ww)], [_new(e6, b, g, f, h, ww)]
+
+
+OP_C_T = OpaqueFunction("gtv_op_C_transpose_train", 1, _opct_fwd, _opct_bwd, _opct_fake)

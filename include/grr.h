@@ -192,6 +192,30 @@ grr_status grr_gtv_op_c(const float* x, const float* w, grr_stencil s, float* ed
 grr_status grr_gtv_op_c_transpose(const float* edges, const float* w, grr_stencil s, float* work, float* out, int B,
                                   int G, int F, int H, int W, void* stream);
 
+/* Reverses of the sub-API methods above (the reference differentiates them with autograd over its
+ * ATen ops, REF:128-228, :452-516).  Gradient outputs are overwritten except gM / gtaps, which
+ * accumulate (caller zeroes); gtaps is [G*F, 5] in tap order (centre, up, left, right, down) of the
+ * stencil p01 k01 + p02a k02a + p02b k02b + p03 k03.  B*C (B*G for per-graph kernels) < 65536. */
+/* get_neighbors_pixels reverse: gx [B,C,H,W] from g [B,C,4,H,W] (adjoint of the clamped gather). */
+grr_status grr_neighbor_gather_bwd(const float* g, float* gx, int B, int C, int H, int W, void* stream);
+/* normalize_and_transform_features reverse: gf [B,G,F,H,W], gM [G,F] += ; F <= 16. */
+grr_status grr_normalize_features_bwd(const float* f, const float* multiM, const float* gout, float* gf, float* gM,
+                                      int B, int G, int F, int H, int W, void* stream);
+/* stats_conv / stats_conv_transpose reverse: gx = S* g (S^T* g), gtaps += d<g, S x>/d taps (gtaps may be NULL). */
+grr_status grr_stats_conv_bwd(const float* x, grr_stencil s, int transpose, const float* g, float* gx, float* gtaps,
+                              int B, int G, int F, int H, int W, void* stream);
+/* GLRFast.op_L_norm reverse: gx [B,G,F,H,W], gw [B,G,4,H,W]. */
+grr_status grr_glr_op_l_norm_bwd(const float* x, const float* w, const float* g, float* gx, float* gw, int B, int G,
+                                 int F, int H, int W, void* stream);
+/* GTVFast.op_C reverse from gE [B,G,F,4,H,W]: gx, gw, gtaps; work [B,G,F,H,W] caller scratch. */
+grr_status grr_gtv_op_c_bwd(const float* x, const float* w, grr_stencil s, const float* gE, float* work, float* gx,
+                            float* gw, float* gtaps, int B, int G, int F, int H, int W, void* stream);
+/* GTVFast.op_C_transpose reverse: gE [B,G,F,4,H,W], gw, gtaps; z = the forward's work buffer (the
+ * pre-S^T value o), work2 [B,G,F,H,W] caller scratch. */
+grr_status grr_gtv_op_c_transpose_bwd(const float* edges, const float* w, grr_stencil s, const float* z,
+                                      const float* g, float* work2, float* gE, float* gw, float* gtaps, int B, int G,
+                                      int F, int H, int W, void* stream);
+
 /* ---- feature CNN (MFMA fp32) ------------------------------------------------ */
 
 /* 1x1 convolution, no bias (nn.Conv2d(k=1, groups=1, bias=False); REF:556-566, REF13:623-632):

@@ -48,6 +48,12 @@ int main() {
   EXPECT_ERR(grr_glr_op_l_norm(n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_gtv_op_c(n, n, ns, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_gtv_op_c_transpose(n, n, ns, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_neighbor_gather_bwd(n, n, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_normalize_features_bwd(n, n, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_stats_conv_bwd(n, ns, 0, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_glr_op_l_norm_bwd(n, n, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_gtv_op_c_bwd(n, n, ns, n, n, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_gtv_op_c_transpose_bwd(n, n, ns, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_conv1x1(n, n, n, 1, 4, 4, 64, s));
   EXPECT_ERR(grr_conv1x1_ws(n, n, n, n, 1, 4, 4, 64, s));
   EXPECT_ERR(grr_conv2x2s2(n, n, n, 1, 4, 4, 8, 8, s));

@@ -61,3 +61,57 @@ def test_hip_graph_backend_matches_eager(irdu):
         outs = [cm(x).clone() for _ in range(3)]   # warm-up, record, replay
     for o in outs:
         assert torch.equal(o, ref)
+
+
+def _train_two_steps(m, compiled: bool):
+    """The reference's loop body (scripts_v2/...sigma25.py:186-207): L1 + 0.1 MSE(decode(encode(clean)))
+    + 0.5 MSE(decode(latent), decode(latent + N(0, 0.05))), backward, Adam(4e-4); two steps."""
+    import torch.nn.functional as F
+    if compiled:
+        m.compile()                               # as scripts_v2/...sigma25.py:130
+    opt = torch.optim.Adam(m.parameters(), lr=4e-4, eps=1e-8)
+    g = torch.Generator().manual_seed(5)
+    losses, grads = [], []
+    for step in range(2):
+        clean = torch.rand(2, 3, 32, 32, generator=g).to(DEV)
+        noisy = (clean + torch.randn(2, 3, 32, 32, generator=g).to(DEV) * (25.0 / 255.0)).contiguous()
+        opt.zero_grad(set_to_none=True)
+        torch.manual_seed(100 + step)              # the latent perturbation's noise
+        loss = F.l1_loss(m(noisy), clean)
+        latent = m.encode(clean)
+        rec = m.decode(latent)
+        disturbed = m.decode(tuple(t + torch.normal(0.0, 0.05, size=t.shape, device=t.device) for t in latent))
+        loss = loss + 0.1 * F.mse_loss(rec, clean) + 0.5 * F.mse_loss(rec, disturbed)
+        loss.backward()
+        losses.append(float(loss))
+        grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
+        opt.step()
+    return losses, grads
+
+
+def test_compiled_training_matches_eager(irdu):
+    """model.compile() then two optimisation steps of the reference's loop (S = 3 drop-in v1.0 model):
+    loss and every parameter gradient equal the eager run's; the graph-filter ops are opaque irdu::
+    nodes in both directions (tests/test_compile_training.py checks the graphs on CPU)."""
+    import torch._inductor.config as icfg
+    torch._dynamo.reset()
+
+    def make():
+        torch.manual_seed(21)
+        m = irdu.AbtractMultiScaleGraphFilter(
+            3, 3, dims=[8, 16, 16, 32], hidden_dims=[16, 32, 32, 64], nsubnets=[1, 1, 1, 1], ngraphs=[2, 4, 4, 8],
+            num_blocks=[1, 1, 1, 1], num_blocks_out=1, n_cgd_iters=3)
+        for blk in (m.localfilter_scale_00, m.localfilter_scale_01, m.localfilter_scale_02, m.localfilter_scale_03):
+            perturb_mixture(blk.local_filter, 3)
+        return m.to(DEV).train()
+
+    ref_losses, ref_grads = _train_two_steps(make(), compiled=False)
+    with icfg.patch(fallback_random=True):
+        losses, grads = _train_two_steps(make(), compiled=True)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) <= 1e-6 * abs(b), (losses, ref_losses)
+    for step in range(2):
+        for k, ref in ref_grads[step].items():
+            got = grads[step][k]
+            err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+            assert err <= 1e-5, (step, k, err)
