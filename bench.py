@@ -31,9 +31,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MPix/sec + PSNR@σ=25, 10-stage GGTV-GGLR on 256×256 patches, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-BF16_MFMA_PEAK_TFLOPS = 16 * 157.3  # dense bf16 MFMA rate (MI355X_MICROARCH.md: 1/16 of it is the f32 rate)
-# the LNB GEMMs run each fp32 product as 6 bf16 MFMA products (exact 3-term split of both operands),
-# so their ceiling in algorithmic fp32 flops is the bf16 rate / 6
+BF16_MFMA_PEAK_TFLOPS = 16 * 157.3  # dense bf16 / fp16 MFMA rate (MI355X_MICROARCH.md: 1/16 of it is the f32 rate)
+# LNB GEMM1 (head) runs each fp32 product as 3 fp16 MFMA products (exact 2-term split), GEMM2 (mix) as 6
+# bf16 products (exact 3-term split): their ceilings in algorithmic fp32 flops are the rate / 3 and / 6
+SPLIT_F16_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 SPLIT_BF16_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 G, CIN, STAGES, H, W, SIGMA = 32, 3, 10, 256, 256, 25.0
 
@@ -99,6 +100,16 @@ def load_traffic(kernel):
     if d.get("kernel") != kernel:
         return None
     return d.get("hbm_bytes_per_launch")
+
+
+def load_traffic_file(name, kernel_prefix):
+    """Per-launch HBM bytes from a committed PMC summary under profiles/r03/ (None when absent)."""
+    path = os.path.join(ROOT, "profiles", "r03", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch") if d.get("kernel", "").startswith(kernel_prefix) else None
 
 
 def host_cpus():
@@ -249,6 +260,7 @@ def main():
         saved = GF.FEATURE_STREAMS
         GF.FEATURE_STREAMS = False
         timer = K.LaunchTimer()
+        timer.split_lnb = True      # the feature CNN's head and mix kernels timed apart
         K.set_timer(timer)
         for _ in range(max(1, min(args.steps, 5))):
             out = model(noisy)
@@ -305,16 +317,26 @@ def main():
     if world > 1:
         res["ranks"] = {"backend": benchlib.backend(), "visible_gpus": torch.cuda.device_count(),
                         "ms_per_step_per_rank": [round(d / args.steps * 1e3, 3) for d in rank_dts]}
-    if "lnb" in kern:   # the MFMA-bound feature CNN: fp32-accurate split-bf16 GEMMs + depthwise + gate
-        lnb = kern["lnb"]
+    if "lnb_head" in kern:   # the feature CNN: head (LN + W1 + depthwise + gate) and mix (W2 + skip) apart
+        hd, mx = kern["lnb_head"], kern["lnb_mix"]
         res["roofline_secondary"] = {
-            "bound": "mfma", "kernel": "LocalNonLinearBlock (lnb_head_kernel + lnb_mix_kernel)",
-            "achieved": round(lnb["tflops"], 2), "peak": round(SPLIT_BF16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
-            "frac": round(lnb["tflops"] / SPLIT_BF16_PEAK_TFLOPS, 4),
-            "flops_per_launch": lnb["flops_per_launch"], "mean_launch_ms": round(lnb["mean_ms"], 4),
-            "launches": lnb["launches"],
-            "note": "algorithmic fp32 flops (kernels.lnb_flops) / HIP-event time, against the dense bf16 MFMA "
-                    "rate / 6: each fp32 product runs as 6 bf16 MFMA products (exact 3-term split)"}
+            "lnb_head": {
+                "bound": "mfma", "kernel": "lnb_head16_kernel (+ lnb_w1_pack16_kernel)",
+                "achieved": round(hd["tflops"], 2), "peak": round(SPLIT_F16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
+                "frac": round(hd["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": hd["flops_per_launch"],
+                "mean_launch_ms": round(hd["mean_ms"], 4), "launches": hd["launches"],
+                "traffic": load_traffic_file("traffic_lnb_head16.json", "lnb_head16_kernel"),
+                "note": "algorithmic fp32 flops (kernels.lnb_head_flops: LN, W1, depthwise, gate) / HIP-event time, "
+                        "against the dense fp16 MFMA rate / 3 (each W1 product = 3 fp16 products of exact 2-term "
+                        "splits); the depthwise + gate part is VALU work"},
+            "lnb_mix": {
+                "bound": "hbm", "kernel": "lnb_mix_kernel (+ lnb_w2_pack_kernel)",
+                "achieved": round(mx["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(mx["gbps"] / HBM_PEAK_GBPS, 4), "bytes_per_launch": mx["bytes_per_launch"],
+                "mean_launch_ms": round(mx["mean_ms"], 4), "launches": mx["launches"],
+                "mfma_tflops": round(mx["tflops"], 2), "mfma_peak": round(SPLIT_BF16_PEAK_TFLOPS, 1),
+                "traffic": load_traffic_file("traffic_lnb_mix.json", "lnb_mix_kernel"),
+                "note": "algorithmic bytes (g + skip operand + out) / HIP-event time; W2 on 6 bf16 products"}}
     kernels_ms = {k: round(v["total_ms"] / n_inst, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms
     if args.breakdown:

@@ -28,15 +28,30 @@ D_ARGS = dict(dims=[48, 96, 192, 384], hidden_dims=[96, 192, 384, 768], nsubnets
 HBM_PEAK_GBPS = 8000.0
 
 
-def reverse_roofline(kern):
+def load_traffic(kind, model, batch, size):
+    """Per-launch HBM bytes (PMC, scripts/pmc_train.sh) of the reverse kernel kind at this workload,
+    or None when no summary of that exact shape is committed under profiles/."""
+    path = os.path.join(ROOT, "profiles", "r03", f"traffic_{kind}_{model}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    shape = d.get("workload", {})
+    if shape and (shape.get("batch"), shape.get("size")) != (batch, size):
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def reverse_roofline(kern, model, batch, size):
     """Roofline of the dominant reverse-sweep kernel kind: algorithmic bytes per launch
-    (kernels.py byte model of each reverse pass) / its mean HIP-event launch time."""
+    (kernels.py byte model of each reverse pass) / its mean HIP-event launch time; traffic = the PMC
+    bytes per launch of the same kind (profiles/r03/traffic_<kind>_<model>.json)."""
     cands = {k: v for k, v in kern.items() if k.startswith("bwd") and v["bytes_per_launch"] > 0}
     if not cands:
         return None
     k, v = max(cands.items(), key=lambda kv: kv[1]["total_ms"])
     return {"bound": "hbm", "kernel": k, "achieved": round(v["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(v["gbps"] / HBM_PEAK_GBPS, 4), "traffic": None,
+            "frac": round(v["gbps"] / HBM_PEAK_GBPS, 4), "traffic": load_traffic(k, model, batch, size),
             "bytes_per_launch": v["bytes_per_launch"], "mean_launch_ms": round(v["mean_ms"], 4),
             "launches": v["launches"]}
 
@@ -97,10 +112,15 @@ def main():
                     help="CPU-baseline patch side (default: --size for msgf, 128 for the v1.0 model)")
     ap.add_argument("--fused-fts", type=str, default=None,
                     help="comma list of F that use the one-pass term reverses (default: all instances)")
+    ap.add_argument("--watchdog", type=float, default=0.0,
+                    help="dump every thread's Python stack to stderr each N seconds (hang diagnosis)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; spawned when not under torchrun)")
     ap.add_argument("--dry-run", action="store_true", help="launcher check: ranks report and exit (no HIP)")
     args = ap.parse_args()
 
+    if args.watchdog > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(args.watchdog, repeat=True, file=sys.stderr)
     import benchlib
     world, rank, local = benchlib.join_or_spawn(args.gpus, dry_run=args.dry_run)
     if args.dry_run:
@@ -158,7 +178,7 @@ def main():
                "loss": loss, "hip_kernel_ms_per_step": round(hip_ms, 2),
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                "kernel_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}}
-        res["roofline"] = reverse_roofline(kern)
+        res["roofline"] = reverse_roofline(kern, args.model, args.batch, args.size)
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(model, args.model, args.cpu_size or (args.size if args.model == "msgf" else 128))
             res["cpu_baseline"] = cb
@@ -169,6 +189,9 @@ def main():
                       f"algo={v['gbps']:8.1f} GB/s", file=sys.stderr)
         print(json.dumps(res), flush=True)
     benchlib.finish(world)
+    if args.watchdog > 0:
+        import faulthandler
+        faulthandler.cancel_dump_traceback_later()
 
 
 if __name__ == "__main__":

@@ -899,6 +899,10 @@ static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
   else hipLaunchKernelGGL((lnb_mix_kernel<MT, false>), dim3(m.nblk), dim3(256), 0, s, m);
 }
 
+// measurement knob (grr_lnb_set_phases): which of pack (1) / head (2) / mix (4) a forward launches, so
+// a caller can time the head and the mix of one block apart on a shared workspace
+int g_lnb_phases = 7;
+
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                             const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
                             hipStream_t s) {
@@ -920,7 +924,7 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   float* g = ws;
   char* w1f = reinterpret_cast<char*>(ws + align64((int64_t)B * hid * P));
   uint16_t* w2f = reinterpret_cast<uint16_t*>(ws + align64((int64_t)B * hid * P) + head_pack_floats(Ch, hid));
-  {
+  if (g_lnb_phases & 1) {
     const int64_t n1 = (int64_t)nch * (h16 ? head16_images(KS) : head_images(KS)) * 256;
     const int64_t n2 = (int64_t)KS2 * MT * 3 * 512;
     const dim3 g1((unsigned)std::min<int64_t>((n1 + 255) / 256, 4096));
@@ -941,7 +945,8 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   const uint64_t nh = (uint64_t)B * h.tiles_x * h.tiles_y;
   GRR_REQUIRE(nh < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
   h.nblk = (uint32_t)nh;
-  if (h16) {
+  if (!(g_lnb_phases & 2)) {
+  } else if (h16) {
     switch (KS) {
       case 1: launch_head16<1>(h, s); break;
       case 2: launch_head16<2>(h, s); break;
@@ -960,6 +965,7 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   }
   grr_status st = launch_status("grr_lnb_forward/head");
   if (st != GRR_OK) return st;
+  if (!(g_lnb_phases & 4)) return GRR_OK;
   LnbMixArgs m{};
   m.g = g; m.w2f = reinterpret_cast<const char*>(w2f); m.skip = skip; m.out = out;
   m.x = x ? x : xh;           // x == NULL: the skip reads the replicated image itself
@@ -980,6 +986,13 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
 }
 
 }  // namespace grr
+
+extern "C" grr_status grr_lnb_set_phases(int mask) {
+  grr::clear_error();
+  GRR_REQUIRE(mask >= 1 && mask <= 7, GRR_ERR_INVALID_ARG, "grr_lnb_set_phases: mask %d outside [1, 7]", mask);
+  grr::g_lnb_phases = mask;
+  return GRR_OK;
+}
 
 #ifdef GRR_FUSED_STAMP
 extern "C" grr_status grr_debug_fused_stamps(unsigned long long* host) {

@@ -37,6 +37,9 @@ EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, d
 # Inference: the half-resolution feature branch (2x2 conv, its LocalNonLinearBlocks, 1x1) runs on
 # a second HIP stream beside the full-resolution branch (GRR_FEATURE_STREAMS=0: one stream)
 FEATURE_STREAMS = os.environ.get("GRR_FEATURE_STREAMS", "1") == "1"
+# Training: the same split for the forward and (by autograd's stream replay) the reverse of the branch;
+# off by default (one of two round-2 runs of the first version stalled)
+FEATURE_STREAMS_TRAIN = os.environ.get("GRR_FEATURE_STREAMS_TRAIN", "0") == "1"
 _SIDE_STREAMS = {}
 
 
@@ -391,14 +394,35 @@ class MixtureGTVGLR(nn.Module):
             f0 = SG.Conv1x1Fn.apply(y, s0[0].weight)
             f1 = SG.Conv1x1Fn.apply(SG.Conv2x2s2Fn.apply(y, s1[0].weight), s1[1].weight)
             return f0, f1
+        def half():
+            f1 = SG.Conv2x2s2Fn.apply(y, s1[0].weight)
+            for blk in list(s1)[1:4]:
+                f1 = blk(f1)
+            return SG.Conv1x1Fn.apply(f1.contiguous(), s1[4].weight)
+
+        # the half-resolution branch on the side stream (its reverse then also runs there: autograd
+        # replays a node on the stream its forward ran on).  Cross-stream memory: y (main) is read by
+        # side kernels in both directions and f1 (side) by the main-stream solver, so each is
+        # recorded on the other stream -- the caching allocator then cannot hand either block to a
+        # new tensor while the other stream may still read it.
+        side = None
+        if FEATURE_STREAMS_TRAIN and y.is_cuda and not torch.compiler.is_compiling() \
+                and not torch.cuda.is_current_stream_capturing():
+            main = torch.cuda.current_stream(y.device)
+            side = _side_stream(y.device)
+            side.wait_stream(main)
+            y.record_stream(side)
+            with torch.cuda.stream(side):
+                f1 = half()
+        else:
+            f1 = half()
         f0 = y
         for blk in list(s0)[:3]:
             f0 = blk(f0)
         f0 = SG.Conv1x1Fn.apply(f0.contiguous(), s0[3].weight)
-        f1 = SG.Conv2x2s2Fn.apply(y, s1[0].weight)
-        for blk in list(s1)[1:4]:
-            f1 = blk(f1)
-        f1 = SG.Conv1x1Fn.apply(f1.contiguous(), s1[4].weight)
+        if side is not None:
+            main.wait_stream(side)
+            f1.record_stream(main)
         return f0, f1
 
     # -- solver (a3-a17) -----------------------------------------------------

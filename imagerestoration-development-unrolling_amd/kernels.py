@@ -52,6 +52,7 @@ class LaunchTimer:
     ``records[kind]`` collects (start, end, algorithmic_bytes) per launch; ``summary()``
     synchronises and returns per-kind launch count, mean duration and achieved GB/s.
     """
+    split_lnb = False   # True: C <= 128 LocalNonLinearBlocks timed as "lnb_head" + "lnb_mix"
 
     def __init__(self):
         self.records = {}
@@ -535,11 +536,14 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty_like(x)
+    args = (x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
+            out.data_ptr(), ws.data_ptr(), b, c, hid, h, w, _stream(dev))
+    if _lnb_split(c):
+        _lnb_timed_parts("grr_lnb_forward", args, b * h * w, c, c, hid, c)
+        return out
     # C <= 128: x (head), gated g (hid) written and read back once, residual x, out
     nbytes_algo = 4 * b * h * w * (3 * c + 2 * hid) if c <= 128 else 4 * b * h * w * (3 * c + 2 * (2 * hid) + 2 * hid)
-    _launch("lnb", nbytes_algo, "grr_lnb_forward", x.data_ptr(),
-            ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(), out.data_ptr(),
-            ws.data_ptr(), b, c, hid, h, w, _stream(dev), flops=lnb_flops(b * h * w, c, c, hid))
+    _launch("lnb", nbytes_algo, "grr_lnb_forward", *args, flops=lnb_flops(b * h * w, c, c, hid))
     return out
 
 
@@ -559,10 +563,36 @@ def lnb_forward_rep(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, 
     nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
-    _launch("lnb", 4 * b * h * w * (cs + 2 * c + 2 * hid), "grr_lnb_forward_rep", src.data_ptr(), cs, c // cs,
-            _ptr(x), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
-            out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev), flops=lnb_flops(b * h * w, cs, c, hid))
+    args = (src.data_ptr(), cs, c // cs, _ptr(x), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(),
+            skip.data_ptr(), out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev))
+    if _lnb_split(c):
+        _lnb_timed_parts("grr_lnb_forward_rep", args, b * h * w, cs, c, hid, c if x is not None else cs)
+        return out
+    _launch("lnb", 4 * b * h * w * (cs + 2 * c + 2 * hid), "grr_lnb_forward_rep", *args,
+            flops=lnb_flops(b * h * w, cs, c, hid))
     return out
+
+
+# LaunchTimer with split_lnb: the head (LN + W1 + depthwise + gate) and the mix (W2 + skip) of a C <= 128
+# block are launched and timed apart on one workspace (grr_lnb_set_phases), as kinds "lnb_head" / "lnb_mix"
+def _lnb_split(c: int) -> bool:
+    return _TIMER is not None and getattr(_TIMER, "split_lnb", False) and c <= 128
+
+
+def lnb_head_flops(px: int, c_head: int, hid: int) -> int:
+    """Algorithmic fp32 flops of the head: LN (4 per input channel), W1 (2 c_head 2hid), depthwise 3x3
+    (18 per hidden channel), gate (4 per gated channel)."""
+    return px * (4 * c_head + 2 * c_head * 2 * hid + 18 * 2 * hid + 4 * hid)
+
+
+def _lnb_timed_parts(name: str, args, px: int, c_head: int, c: int, hid: int, c_skip: int) -> None:
+    try:
+        call("grr_lnb_set_phases", 3)
+        _launch("lnb_head", 4 * px * (c_head + hid), name, *args, flops=lnb_head_flops(px, c_head, hid))
+        call("grr_lnb_set_phases", 4)
+        _launch("lnb_mix", 4 * px * (hid + c_skip + c), name, *args, flops=px * (2 * hid * c + 3 * c))
+    finally:
+        call("grr_lnb_set_phases", 7)
 
 
 def repeat_graphs(img: Tensor, n_graphs: int) -> Tensor:

@@ -53,9 +53,11 @@ class OpaqueFunction:
         _Eager.__name__ = f"{name}_fn"
         self.eager = _Eager
 
+        # the real outputs must match the fake kernels' (contiguous) metadata: AOTAutograd / Inductor
+        # assert sizes and strides of custom-op results
         def fwd_impl(inputs: List[Tensor], consts: List[int]) -> List[Tensor]:
             outs, saved = spec.fwd(list(consts), *inputs)
-            return [*outs, *saved]
+            return [t.contiguous() for t in (*outs, *saved)]
 
         def fwd_fake(inputs: List[Tensor], consts: List[int]) -> List[Tensor]:
             outs, saved = spec.fake(list(consts), *inputs)
@@ -64,11 +66,12 @@ class OpaqueFunction:
         def bwd_impl(inputs: List[Tensor], outs: List[Tensor], saved: List[Tensor], gouts: List[Tensor],
                      consts: List[int]) -> List[Tensor]:
             grads = spec.bwd(list(consts), inputs, outs, saved, gouts, [True] * len(inputs))
-            return [g if g is not None else torch.zeros_like(x) for g, x in zip(grads, inputs)]
+            return [g.contiguous().view(x.shape) if g is not None else torch.zeros(x.shape, dtype=x.dtype, device=x.device)
+                    for g, x in zip(grads, inputs)]
 
         def bwd_fake(inputs: List[Tensor], outs: List[Tensor], saved: List[Tensor], gouts: List[Tensor],
                      consts: List[int]) -> List[Tensor]:
-            return [torch.empty_like(x) for x in inputs]
+            return [x.new_empty(x.shape) for x in inputs]
 
         self.fwd_op = torch.library.custom_op(f"{NS}::{name}", fwd_impl, mutates_args=())
         self.fwd_op.register_fake(fwd_fake)

@@ -44,6 +44,11 @@ const char* grr_last_error(void);
  * column strips above), 1 = column-strip graph operators at every width, 2 = automatic
  * without the lockstep.  Process-wide; results agree to fp32 rounding either way. */
 grr_status grr_set_kernel_variant(int variant);
+/* Measurement knob (process-wide, like grr_set_kernel_variant): which phases a C <= 128 LocalNonLinearBlock
+ * forward (grr_lnb_forward / grr_lnb_forward_rep) launches -- 1 weight packing, 2 head (LN + W1 +
+ * depthwise + gate -> the workspace's g), 4 mix (W2 g + skip -> out).  7 (default) = all; a caller
+ * times head and mix apart by running mask 3 then mask 4 on the same workspace. */
+grr_status grr_lnb_set_phases(int mask);
 
 /* Measurement helper (not a reference interface): float4 streaming copy of n floats
  * (n % 4 == 0, 16-byte aligned), the HBM ceiling bench.py reports beside the step kernel. */

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--kernel", default="graph_row_kernel<true, 1, 2, 4>")
     ap.add_argument("--out", default="profiles/traffic_system_step.json")
+    ap.add_argument("--batch", type=int, default=None, help="workload batch recorded in the summary")
+    ap.add_argument("--size", type=int, default=None, help="workload image side recorded in the summary")
     args = ap.parse_args()
     fetch = per_dispatch(args.fetch_dir, "FETCH_SIZE", args.kernel)
     write = per_dispatch(args.write_dir, "WRITE_SIZE", args.kernel)
@@ -41,6 +43,8 @@ def main():
            "fetch_size_kib_mean": sum(fetch) / len(fetch), "write_size_kib_mean": sum(write) / len(write),
            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
            "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count of 128-B requests); writes = WRITE_SIZE"}
+    if args.batch is not None:
+        res["workload"] = {"batch": args.batch, "size": args.size}
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)

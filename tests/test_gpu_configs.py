@@ -178,7 +178,7 @@ def test_c5_tiled_2048_vs_whole_image_and_oracle(irdu):
     """C5: a 2048x2048 RGB sigma-25 image filtered as 256x256 overlap-save windows equals the
     whole-image HIP filter to within 1e-5 relative at the bench's halo (32 px), with the trained
     weights fixture (trained-scale solver coefficients; tests/test_gpu_psnr.py).  The analytic
-    receptive field is far wider (tiling.py: ~130 px), so the error is measured at halos 16 / 32 /
+    receptive field is wider (83 px), so the error is measured at halos 16 / 32 /
     64 and printed.  The whole-image output on a central 128x128 region equals the CPU oracle run
     on a 320x320 crop around it (96-px margin: the filter's influence at that distance is below
     fp32 rounding, shown by the halo sweep)."""

@@ -51,3 +51,40 @@ def test_mixture_two_streams_bitwise(irdu):
     y = torch.rand(2, g * f, 48, 64, device=DEV)
     a, b = _both(lambda: mix(y))
     assert torch.equal(a, b)
+
+
+def test_msgf_training_side_stream_matches_one_stream(irdu):
+    """GRR_FEATURE_STREAMS_TRAIN: the half-resolution branch's forward and (autograd's stream replay)
+    reverse on the side stream.  Three training steps (loss, backward, parameter update) per mode so
+    the caching allocator recycles the cross-stream blocks; gradients and weights equal the one-stream
+    run's (reductions use float atomics, so to 1e-5 relative, not bitwise)."""
+    import torch.nn.functional as F
+    from irdu_amd import graph_filter as GF
+
+    def run(on):
+        GF.FEATURE_STREAMS_TRAIN = on
+        torch.manual_seed(9)
+        m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=4).to(DEV).train()
+        opt = torch.optim.SGD(m.parameters(), lr=1e-3)
+        g = torch.Generator().manual_seed(3)
+        grads = []
+        for _ in range(3):
+            x = torch.rand(2, 3, 64, 64, generator=g).to(DEV)
+            t = torch.rand(2, 3, 64, 64, generator=g).to(DEV)
+            opt.zero_grad(set_to_none=True)
+            F.l1_loss(m(x), t).backward()
+            grads.append([p.grad.clone() for p in m.parameters()])
+            opt.step()
+        torch.cuda.synchronize()
+        return grads, [p.detach().clone() for p in m.parameters()]
+
+    saved = GF.FEATURE_STREAMS_TRAIN
+    try:
+        (g1, w1), (g2, w2) = run(False), run(True)
+    finally:
+        GF.FEATURE_STREAMS_TRAIN = saved
+    for step_a, step_b in zip(g1, g2):
+        for a, b in zip(step_a, step_b):
+            assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
+    for a, b in zip(w1, w2):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12

@@ -38,7 +38,7 @@ def _module(irdu, cls, seed):
 
 def _ref_params(m):
     """The module's parameters as float64 leaves keyed like the oracle's parameter dicts."""
-    return {k: v.detach().double().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    return {k: v.detach().cpu().double().clone().requires_grad_(True) for k, v in m.state_dict().items()}
 
 
 def _hip_grads(m, fn, inputs, gout):

@@ -31,10 +31,10 @@ def test_tiled_equals_whole_image_when_halo_covers_receptive_field(irdu):
 
 
 def test_tiled_msgf_ten_stages_halo(irdu):
-    """S = 10 image filter: its receptive field is finite (24 px, measured on the oracle with
-    strong coupling: outputs farther than that from a crop edge are bit-identical), so 32- and
-    64-px halos reproduce the whole image to fp32 rounding (the kernels differ between the
-    window width and the image width, hence not bit-exact)."""
+    """S = 10 image filter: its analytic receptive field is 83 px, but the
+    solver's influence decays geometrically with distance, so 32- and 64-px halos already
+    reproduce the whole image to fp32 rounding (the kernels differ between the window width and
+    the image width, hence not bit-exact)."""
     from irdu_amd import tiling
     torch.manual_seed(5)
     m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=10)
