@@ -83,6 +83,7 @@ SIGNATURES = {
     # reverse pass
     "grr_bwd_stencil": [P, P, I, P, I, P, I, I, I, I, I, P],
     "grr_bwd_tapgrad": [P, P, I, P, P, I, I, I, I, I, P],
+    "grr_bwd_padj2": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_glr": [P, P, P, P, Fl, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_pair": [P, P, P, P, Fl, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_prox": [P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],

@@ -176,6 +176,53 @@ __global__ __launch_bounds__(NT) void stencil4_kernel(const float* __restrict__ 
   *o = acc ? *o + y : y;
 }
 
+// The x-gradient pass of the GLR and the GTV term of one level in one sweep (both are P* of the
+// replicate stencil, mode 3, with the module's own taps and scale):
+//   out += s1[g] P1*(v1) + s2[g] P2*(v2)
+// reads v1, v2, out and writes out once (two stencil4_kernel<3> launches read out twice and write it
+// twice).  Four adjacent columns per thread, W % 4 == 0.  grid (ceil(HW/4/NT), B*C).
+__device__ __forceinline__ f4 padj4(const float* xp, float k0, float ku, float kl, float kr, float kd, int r, int c0,
+                                    int H, int W) {
+  const bool top = r == 0, bot = r == H - 1, lft = c0 == 0, rgt = c0 + 4 == W;
+  const f4 cv = *reinterpret_cast<const f4*>(xp + r * W + c0);
+  const f4 uv = top ? f4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f4*>(xp + (r - 1) * W + c0);
+  const f4 dv = bot ? f4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f4*>(xp + (r + 1) * W + c0);
+  const float lv = lft ? 0.f : xp[r * W + c0 - 1];
+  const float rv = rgt ? 0.f : xp[r * W + c0 + 4];
+  f4 y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {   // stencil4_kernel<3>'s expression, term by term
+    const float l = j > 0 ? cv[j - 1] : lv, rr = j < 3 ? cv[j + 1] : rv;
+    float v = k0 * cv[j];
+    v += ku * dv[j]; v += kl * rr; v += kr * l; v += kd * uv[j];
+    const int col = c0 + j;
+    if (top) v += ku * cv[j];
+    if (bot) v += kd * cv[j];
+    if (col == 0) v += kl * cv[j];
+    if (col == W - 1) v += kr * cv[j];
+    y[j] = v;
+  }
+  return y;
+}
+__global__ __launch_bounds__(NT) void padj2_kernel(const float* __restrict__ x1, const float* __restrict__ taps1,
+                                                   const float* __restrict__ scale1, const float* __restrict__ x2,
+                                                   const float* __restrict__ taps2, const float* __restrict__ scale2,
+                                                   float* __restrict__ out, int C, int F, int H, int W) {
+  const int HW = H * W, W4 = W / 4;
+  const int q4 = blockIdx.x * NT + threadIdx.x;
+  if (q4 >= HW / 4) return;
+  const int plane = blockIdx.y, ch = plane % C;
+  const int r = q4 / W4, c0 = (q4 - r * W4) * 4;
+  const float* t1 = taps1 + ch * 5;
+  const float* t2 = taps2 + ch * 5;
+  f4 y1 = padj4(x1 + (int64_t)plane * HW, t1[0], t1[1], t1[2], t1[3], t1[4], r, c0, H, W);
+  f4 y2 = padj4(x2 + (int64_t)plane * HW, t2[0], t2[1], t2[2], t2[3], t2[4], r, c0, H, W);
+  y1 *= scale1[ch / F];
+  y2 *= scale2[ch / F];
+  f4* o = reinterpret_cast<f4*>(out + (int64_t)plane * HW + r * W + c0);
+  *o = (*o + y1) + y2;   // the order of two accumulating stencil launches
+}
+
 // Tap gradients of y = mode(z) contracted with u: gt[c, t] += scale[g] * sum_{b,q} u(q) dy(q)/dk_t.
 // mode 0 (P): dy(q)/dk_t = z(clamp(q + t));  mode 1 (T): z(q - t) [inside].   grid (chunks, B*C).
 template <int mode>
@@ -1421,6 +1468,22 @@ grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const fl
     default: hipLaunchKernelGGL(stencil_kernel<3>, grid, dim3(NT), 0, s, x, taps, scale, accumulate, out, C, F, H, W);
   }
   return launch_status("grr_bwd_stencil");
+}
+
+grr_status grr_bwd_padj2(const float* v1, const float* taps1, const float* scale1, const float* v2, const float* taps2,
+                         const float* scale2, float* out, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(v1 && taps1 && scale1 && v2 && taps2 && scale2 && out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_bwd_padj2: bad args");
+  GRR_REQUIRE(W % 4 == 0 && (uintptr_t)v1 % 16 == 0 && (uintptr_t)v2 % 16 == 0 && (uintptr_t)out % 16 == 0,
+              GRR_ERR_UNSUPPORTED, "grr_bwd_padj2: W %% 4 != 0 or planes not 16-byte aligned");
+  const int C = G * F;
+  GRR_REQUIRE((int64_t)B * C <= 65535 && (int64_t)H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_bwd_padj2: grid too large");
+  const dim3 g4((H * W / 4 + NT - 1) / NT, B * C);
+  hipLaunchKernelGGL(padj2_kernel, g4, dim3(NT), 0, (hipStream_t)stream, v1, taps1, scale1, v2, taps2, scale2, out, C,
+                     F, H, W);
+  return launch_status("grr_bwd_padj2");
 }
 
 grr_status grr_bwd_tapgrad(const float* u, const float* z, int mode, const float* scale, float* gtaps, int B, int G,

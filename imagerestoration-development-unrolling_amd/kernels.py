@@ -642,6 +642,18 @@ def bwd_stencil(x: Tensor, taps: Tensor, mode: int, n_graphs: int, scale: Option
     return out
 
 
+def padj2_ok(x: Tensor) -> bool:
+    return x.shape[3] % 4 == 0
+
+
+def bwd_padj2(v1: Tensor, taps1: Tensor, scale1: Tensor, v2: Tensor, taps2: Tensor, scale2: Tensor, out: Tensor,
+              n_graphs: int) -> None:
+    """out += scale1[g] P1*(v1) + scale2[g] P2*(v2) in one pass (the two x-gradient passes of a level's terms)."""
+    dev = _check("bwd_padj2", v1, taps1, scale1, v2, taps2, scale2, out)
+    _launch("bwd_stencil", 4 * v1.numel() * 4, "grr_bwd_padj2", v1.data_ptr(), taps1.data_ptr(), scale1.data_ptr(),
+            v2.data_ptr(), taps2.data_ptr(), scale2.data_ptr(), out.data_ptr(), *_bgfhw(v1, n_graphs), _stream(dev))
+
+
 def bwd_tapgrad(u: Tensor, z: Tensor, mode: int, n_graphs: int, scale: Optional[Tensor], gtaps: Tensor) -> None:
     dev = _check("bwd_tapgrad", u, z, scale, gtaps)
     _launch("bwd_tapgrad", 8 * u.numel(), "grr_bwd_tapgrad", u.data_ptr(), z.data_ptr(), mode, _ptr(scale),

@@ -52,6 +52,7 @@ def solver_params(mod) -> List[Tensor]:
 
 FUSED_GATE_DW3 = True   # LNB reverse: gate + depthwise reverse in one row pass (False: two kernels; tests)
 FUSED = True   # one-pass term reverses (grr_bwd_term_fused) where F has an instance; False: 5-pass path
+PADJ2 = True   # the GLR and GTV terms' x-gradient passes of a level as one sweep (grr_bwd_padj2); False: two
 
 
 def _use_fused(x: Tensor, n_graphs: int) -> bool:
@@ -61,14 +62,17 @@ def _use_fused(x: Tensor, n_graphs: int) -> bool:
 
 
 def glr_term_bwd(x: Tensor, g: Tensor, taps: Tensor, w: Tensor, scale: Tensor, coef: float, n_graphs: int,
-                 out: Tensor, gw: Tensor, gscale: Optional[Tensor], gtaps: Tensor) -> None:
+                 out: Tensor, gw: Tensor, gscale: Optional[Tensor], gtaps: Tensor, defer: bool = False):
     """Reverse of the GLR term  scale[g] * T((I - W) P x)  (REF:218-237) contracted with coef * g:
-    out += coef*scale * P*(I-W)^T T* g; gw, gtaps += coef*scale * d/d(.); gscale += coef * <g, T(I-W)Px>."""
+    out += coef*scale * P*(I-W)^T T* g; gw, gtaps += coef*scale * d/d(.); gscale += coef * <g, T(I-W)Px>.
+    defer (one-pass path only): return (v, coef*scale) and leave out += coef*scale P*(v) to the caller."""
     sc = scale * coef
     if _use_fused(x, n_graphs):
         v = K.bwd_term_fused(K.TERM_GLR, x, g, taps, w, None, sc, coef, gw, None, gscale, gtaps, n_graphs)
+        if defer:
+            return v, sc
         K.bwd_stencil(v, taps, K.ST_P_ADJ, n_graphs, sc, out=out)
-        return
+        return None
     s = K.bwd_stencil(x, taps, K.ST_P, n_graphs)
     a = K.bwd_stencil(g, taps, K.ST_T_ADJ, n_graphs)
     z, ap = K.bwd_glr(s, a, w, sc, coef, gw, gscale, n_graphs)
@@ -79,13 +83,15 @@ def glr_term_bwd(x: Tensor, g: Tensor, taps: Tensor, w: Tensor, scale: Tensor, c
 
 
 def gtv_term_bwd(x: Tensor, g: Tensor, taps: Tensor, c: Tensor, scale: Tensor, coef: float, n_graphs: int,
-                 out: Tensor, gc: Tensor, gscale: Optional[Tensor], gtaps: Tensor) -> None:
+                 out: Tensor, gc: Tensor, gscale: Optional[Tensor], gtaps: Tensor, defer: bool = False):
     """Reverse of the linear GTV term  scale[g] * T(K_c P x)  (C^T C with pair weights, REF:452-523)."""
     sc = scale * coef
     if _use_fused(x, n_graphs):
         v = K.bwd_term_fused(K.TERM_PAIR, x, g, taps, c, None, sc, coef, gc, None, gscale, gtaps, n_graphs)
+        if defer:
+            return v, sc
         K.bwd_stencil(v, taps, K.ST_P_ADJ, n_graphs, sc, out=out)
-        return
+        return None
     s = K.bwd_stencil(x, taps, K.ST_P, n_graphs)
     a = K.bwd_stencil(g, taps, K.ST_T_ADJ, n_graphs)
     z, ap = K.bwd_pair(s, a, c, sc, coef, gc, gscale, n_graphs)
@@ -111,7 +117,15 @@ class _Level:
         self.gmu, self.gro, self.ggam = z(log_mu), z(log_ro), z(log_gamma)
 
     def terms_bwd(self, x: Tensor, g: Tensor, coef: float, out: Tensor, glr: bool = True) -> None:
-        """out += coef * (mu L^T + ro G^T) g, and coef * d<g, mu L x + ro G x>/d(params) into the buffers."""
+        """out += coef * (mu L^T + ro G^T) g, and coef * d<g, mu L x + ro G x>/d(params) into the buffers.
+        With both one-pass term reverses, the two x-gradient passes run as one sweep (grr_bwd_padj2)."""
+        if glr and PADJ2 and _use_fused(x, self.g) and K.padj2_ok(x):
+            vl, scl = glr_term_bwd(x, g, self.tapsL, self.wL, self.mu, coef, self.g, out, self.gwL, self.gmu,
+                                   self.gtapL, defer=True)
+            vg, scg = gtv_term_bwd(x, g, self.tapsG, self.cG, self.ro, coef, self.g, out, self.gcG, self.gro,
+                                   self.gtapG, defer=True)
+            K.bwd_padj2(vl, self.tapsL, scl, vg, self.tapsG, scg, out, self.g)
+            return
         if glr:
             glr_term_bwd(x, g, self.tapsL, self.wL, self.mu, coef, self.g, out, self.gwL, self.gmu, self.gtapL)
         gtv_term_bwd(x, g, self.tapsG, self.cG, self.ro, coef, self.g, out, self.gcG, self.gro, self.gtapG)

@@ -278,6 +278,11 @@ grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G
  * 2: adjoint of mode 1; 3: adjoint of mode 0.  out = [out +] scale[g] * mode(x). */
 grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,
                            float* out, int B, int G, int F, int H, int W, void* stream);
+/* x-gradient pass of two operator terms of one level in one sweep: out += scale1[g] P1*(v1) + scale2[g] P2*(v2),
+ * P* = the adjoint of the replicate stencil (grr_bwd_stencil mode 3) with each term's taps [C,5].
+ * W % 4 == 0, 16-byte aligned planes. */
+grr_status grr_bwd_padj2(const float* v1, const float* taps1, const float* scale1, const float* v2, const float* taps2,
+                         const float* scale2, float* out, int B, int G, int F, int H, int W, void* stream);
 /* gtaps[c,t] += scale[g] * sum u(q) d(mode(z))(q)/dk_t, mode 0 (S) or 1 (S^T). */
 grr_status grr_bwd_tapgrad(const float* u, const float* z, int mode, const float* scale, float* gtaps,
                            int B, int G, int F, int H, int W, void* stream);

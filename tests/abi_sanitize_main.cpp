@@ -62,6 +62,7 @@ int main() {
   EXPECT_ERR(grr_repeat_graphs(n, n, 1, 3, 4, 64, s));
   EXPECT_ERR(grr_bwd_stencil(n, n, 0, n, 0, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_tapgrad(n, n, 0, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_bwd_padj2(n, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_glr(n, n, n, n, 1.f, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_pair(n, n, n, n, 1.f, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_prox(n, n, n, n, n, 1.f, n, n, n, n, n, 1, 1, 1, 8, 8, s));
