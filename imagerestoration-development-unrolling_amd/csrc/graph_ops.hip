@@ -1313,32 +1313,36 @@ static bool stencil_ok(const grr_stencil& s) { return s.p01 && s.p02a && s.p02b 
 //
 // Stage k+1 consumes stage k's rows a few rows behind inside the same workgroup, so
 // x_{k+1} and u_{k+1} never reach HBM and the full-level edge weights are read once for
-// both stages.  One workgroup = the F channel waves of one (b, graph, row segment) + one
-// producer wave; one workgroup per CU (≈156 KiB of LDS), one wave per SIMD.  Per iteration
-// (two image rows) each channel wave runs three register pipelines of the operator
-// (OpPipe: x -> s = S x -> {l, o} -> S^T, the arithmetic of graph_row_kernel's consume):
-//   stage A   = stage k at full resolution: x_k rows from HBM, t_k (the half-level term of
-//               x_k, from the preceding grr_system_half) from HBM; writes x_{k+1} and u_{k+1}
-//               rows into private LDS rings and D x_{k+1} half rows into a third ring;
-//   half      = the half-level operator (mu1 L1 + ro1 G1) of D x_{k+1}, 128-wide rows, two
-//               half columns per lane: t_{k+1}, kept in registers;
+// both stages.  One workgroup = one (b, graph, row segment): per channel a stage-A and a
+// stage-B wave, one producer wave and one half-level wave; one workgroup per CU (≈159 KiB of
+// LDS), two waves per SIMD.  Per iteration (two image rows) the waves run register pipelines
+// of the operator (OpPipe: x -> s = S x -> {l, o} -> S^T, the arithmetic of graph_row_kernel's
+// consume):
+//   half A    = the half-level operator (mu1 L1 + ro1 G1) of D x_k (the previous pass's pooled
+//               output, from HBM), 128-wide rows, two half columns per lane, all channels in one
+//               wave: t_k half rows into a 2-row LDS ring per channel, one iteration ahead (what
+//               grr_system_half computed in a launch of its own before round 3);
+//   stage A   = stage k at full resolution: x_k rows from HBM, t_k from the ring; writes x_{k+1}
+//               and u_{k+1} rows into private LDS rings and D x_{k+1} half rows into a third ring;
+//   half B    = the half-level operator of D x_{k+1}: t_{k+1}, kept in registers;
 //   stage B   = stage k+1 at full resolution, 8 rows behind stage A: x_{k+1} / u_{k+1} from the
 //               rings, t_{k+1} from registers; writes x_{k+2}, u_{k+2} and D x_{k+2} to HBM.
 // Row timeline at step t (two steps per iteration): stage A loads x_k row t and emits row
-// t-3; the half pipeline reads D x half row (t-4)/2 - 1 (one row late, so its replicate
-// clamp at the top reads a row that exists) and emits half row (t-11)/2; stage B reads
-// x_{k+1} row t-8 and emits row t-11.  The rings are read with the rows clamped to the
-// image (the replicate boundary the HBM loads apply), and rows outside the image are never
-// written into them.  A segment's stage A starts 6 rows before its stage B needs exact
-// rows (ts = r0 - 9).  The producer wave streams the full-level weight row pairs (7-pair
-// ring: stage A uses pair i, stage B pair i-4, pairs i+1, i+2 in flight) and the half-level
-// weight rows (4-row ring) with LDS-DMA, two iterations ahead.
+// t-3; half B reads D x half row (t-4)/2 - 1 (one row late, so its replicate clamp at the
+// top reads a row that exists) and emits half row (t-11)/2; stage B reads x_{k+1} row t-8 and
+// emits row t-11.  The rings are read with the rows clamped to the image (the replicate
+// boundary the HBM loads apply), and rows outside the image are never written into them.
+// A segment's stage A starts 6 rows before its stage B needs exact rows (ts = r0 - 9).  The
+// producer wave streams the full-level weight row pairs (7-pair ring: stage A uses pair i,
+// stage B pair i-4, pairs i+1, i+2 in flight) and half B's weight rows (4-row ring) with
+// LDS-DMA, two iterations ahead; half A loads its weight rows itself, four half rows earlier
+// (the producer's later read of the same rows is an L2 hit).
 // ---------------------------------------------------------------------------
 struct Step2Args {
   const float* x;
   const float* b;
   const float* u_prev;
-  const float* t_half;
+  const float* xd;       // D x_k (stage A's half level runs in the kernel)
   const float* wL0;
   const float* cG0;
   const float* wL1;
@@ -1479,28 +1483,28 @@ constexpr int S2_HR = 4;                   // half-weight ring rows
 constexpr int S2_XR = 8;                   // x_{k+1} ring rows (per channel)
 constexpr int S2_UR = 10;                  // u_{k+1} ring rows (per channel)
 constexpr int S2_DR = 4;                   // D x_{k+1} ring half rows (per channel)
+constexpr int S2_TR = 2;                   // t_k ring half rows (per channel)
 constexpr int S2_FMAX = 3;                 // channel waves per graph
 constexpr int S2_PAIR = 2 * 6 * S2_W;      // floats per weight-ring pair
 constexpr int S2_HROW = 6 * S2_HW;         // floats per half-weight ring row
-constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW + S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW) +
-                       S2_W + S2_HW;       // + one dummy row (writes of rows outside the image)
+constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW +
+                       S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW + S2_TR * S2_HW);
 #ifndef GRR_STEP2_NT
 #define GRR_STEP2_NT 1
 #endif
 constexpr int S2_NT = GRR_STEP2_NT ? 2 : 0;   // cache policy of step2's read-once / write-once streams
 constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipelines' slot period)
 static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
-// GRR_STEP2_SPLIT: stage A and stage B of a channel run in two waves (waves S2_FMAX + 1 + f and f),
-// the producer is wave S2_FMAX: 7 waves, the two waves of channel f share one SIMD, so each SIMD
-// issues its vector work from two waves (a lone wave issues at half the VALU rate; the kernel is
-// VALU-bound at one wave per SIMD).  Everything the stages exchange already goes through the LDS
-// rings (x_{k+1}, u_{k+1}, D x_{k+1}), written at least one barrier before it is read.
-#ifndef GRR_STEP2_SPLIT
-#define GRR_STEP2_SPLIT 1
-#endif
-constexpr int S2_THREADS = GRR_STEP2_SPLIT ? 64 * (2 * S2_FMAX + 1) : NT;
+// Waves (wave w runs on SIMD w mod 4): stage B of channel f = wave f, the producer = wave
+// S2_FMAX, stage A of channel f = wave S2_FMAX + 1 + f, stage A's half level (all channels) =
+// wave 2 S2_FMAX + 1.  The two waves of channel f share a SIMD, so each of SIMDs 0-2 issues its
+// vector work from two waves (a lone wave issues at half the VALU rate); SIMD 3 holds the
+// producer and the half-level wave.  Everything the waves exchange goes through LDS rings
+// (x_{k+1}, u_{k+1}, D x_{k+1}, t_k), written at least one barrier before it is read.
+constexpr int S2_PRODUCER = S2_FMAX, S2_HALFW = 2 * S2_FMAX + 1;
+constexpr int S2_THREADS = 64 * (2 * S2_FMAX + 2);
 
-__global__ __launch_bounds__(S2_THREADS) __attribute__((amdgpu_waves_per_eu(GRR_STEP2_SPLIT ? 2 : 1, GRR_STEP2_SPLIT ? 2 : 1)))
+__global__ __launch_bounds__(S2_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void graph_step2_kernel(Step2Args a) {
   constexpr int V = 4, VH = 2, W = S2_W, hw = S2_HW;
   typedef typename VecT<4>::type F4;
@@ -1511,7 +1515,7 @@ void graph_step2_kernel(Step2Args a) {
   float* const xring = hring + S2_HR * S2_HROW;
   float* const uring = xring + S2_FMAX * S2_XR * S2_W;
   float* const dring = uring + S2_FMAX * S2_UR * S2_W;
-  float* const dummy = dring + S2_FMAX * S2_DR * S2_HW;
+  float* const tring = dring + S2_FMAX * S2_DR * S2_HW;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int F = a.F;
@@ -1521,17 +1525,22 @@ void graph_step2_kernel(Step2Args a) {
   const int b = unit / a.G;
   const int H = a.H, h = H / 2;
   const int64_t HW = (int64_t)H * W, hHW = (int64_t)h * hw;
+  const int64_t PB = HW * 4, HPB = hHW * 4;
+  const uint32_t RB = (uint32_t)W * 4u, HRB = (uint32_t)hw * 4u;
+  const int C = a.G * F;
+  const int c0 = 4 * lane, ch0 = 2 * lane;
+  const uint32_t vo = (uint32_t)c0 * 4u, vo_half = (uint32_t)ch0 * 4u;
   const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
   const int ts = r0 - 9;                 // first step (odd offset from r0: step t emits stage-A row t-3)
   const int NI0 = (r1 + 11 - ts) / 2;    // stage B emits rows up to r1 - 1
   const int NI = (NI0 + S2_UNROLL - 1) / S2_UNROLL * S2_UNROLL;   // extra iterations store nothing
-  // Split waves: in the iteration where stage A pools half row 0 (t = 3, top segment only), the
-  // half level reads that row as its replicate-clamped row -1 -- one extra barrier for every wave
-  // orders the stage-A write before the stage-B read (program order did it for one wave)
-  const int i_top = GRR_STEP2_SPLIT && r0 == 0 ? (3 - ts) / 2 : -1;
+  // In the iteration where stage A pools half row 0 (t = 3, top segment only), the stage-B half
+  // level reads that row as its replicate-clamped row -1: one extra barrier for every wave orders
+  // the stage-A write before the stage-B read
+  const int i_top = r0 == 0 ? (3 - ts) / 2 : -1;
+  const float scl1 = expf(a.log_mu1[g]), scg1 = expf(a.log_ro1[g]);
 
-  constexpr int PRODUCER = GRR_STEP2_SPLIT ? S2_FMAX : -1;
-  if (wave == (GRR_STEP2_SPLIT ? PRODUCER : F)) {   // producer: weight rows -> LDS rings (LDS-DMA), two iterations ahead
+  if (wave == S2_PRODUCER) {   // producer: weight rows -> LDS rings (LDS-DMA), two iterations ahead
     const float* pwl0 = a.wL0 + (int64_t)(b * a.G + g) * 4 * HW;
     const float* pcg0 = a.cG0 + (int64_t)(b * a.G + g) * 2 * HW;
     const float* pwl1 = a.wL1 + (int64_t)(b * a.G + g) * 4 * hHW;
@@ -1556,7 +1565,7 @@ void graph_step2_kernel(Step2Args a) {
           dma(e < 4 ? pwl0 + e * HW + rw : pcg0 + (e - 4) * HW + rw, slot + (par * 6 + e) * S2_W);
       }
     };
-    auto dma_half = [&](int p) {   // half-level weight row of iteration p (its l/o row)
+    auto dma_half = [&](int p) {   // half-level weight row of iteration p (the stage-B half level's l/o row)
       const int hr = clampi((ts + 2 * p - 3) / 2 - 3, 0, h - 1);
       float* slot = hring + (p % S2_HR) * S2_HROW;
       const int pl = lane >> 5;   // lanes 0-31: plane 2e, lanes 32-63: plane 2e+1
@@ -1587,32 +1596,141 @@ void graph_step2_kernel(Step2Args a) {
     return;
   }
 
-  // ---- channel wave f (split: stage-B wave f < S2_FMAX, stage-A wave S2_FMAX + 1 + f)
-  const bool role_a = GRR_STEP2_SPLIT && wave > PRODUCER;
-  const int f = GRR_STEP2_SPLIT ? (role_a ? wave - PRODUCER - 1 : wave) : wave;
+  if (wave == S2_HALFW) {
+    // Stage A's half level t_k = mu1 S_L^T l + ro1 S_G^T o of D x_k (the grr_system_half launch
+    // the per-stage path runs before each stage), one half row per iteration for every channel:
+    // iteration i emits half row hb + 1 + i into t-ring slot (i + 1) & 1 for stage A's iteration
+    // i + 1, from D x_k half row hb + 4 + i (HBM) and the half-level weight row hb + 2 + i (plain
+    // loads; the producer's LDS-DMA reads the same row for the stage-B half level four
+    // iterations later, from L2).  The pipeline is primed with 8 rows before the first barrier.
+    const int hb = (ts - 3) / 2;   // the half row stage A reads in iteration 0 (ts - 3 is even)
+    const int64_t gq = (int64_t)b * a.G + g;
+    const rsrc_t rxq = make_rsrc(a.xd + ((int64_t)b * C + (int64_t)g * F) * hHW, (int64_t)F * HPB);
+    const rsrc_t rwl = make_rsrc(a.wL1 + gq * 4 * hHW, 4 * HPB);
+    const rsrc_t rcg = make_rsrc(a.cG1 + gq * 2 * hHW, 2 * HPB);
+    Taps tLh[S2_FMAX], tGh[S2_FMAX];
+#pragma unroll
+    for (int f = 0; f < S2_FMAX; ++f) {
+      const int chf = g * F + min(f, F - 1);
+      tLh[f] = make_taps(a.sL1, chf);
+      tGh[f] = make_taps(a.sG1, chf);
+    }
+    struct LdH {
+      float xq[S2_FMAX][VH], w[6][VH];
+    };
+    // channels f >= F read past the operand's range: 0
+    auto issue_h = [&](int hin, LdH& L) {
+      const uint32_t ro = vo_half + (uint32_t)clampi(hin, 0, h - 1) * HRB;
+#pragma unroll
+      for (int f = 0; f < S2_FMAX; ++f) bload<VH, S2_NT>(L.xq[f], rxq, (uint32_t)(f * HPB) + ro);
+      const uint32_t rw = vo_half + (uint32_t)clampi(hin - 2, 0, h - 1) * HRB;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bload<VH>(L.w[e], rwl, (uint32_t)(e * HPB) + rw);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) bload<VH>(L.w[4 + e], rcg, (uint32_t)(e * HPB) + rw);
+    };
+    OpPipe<VH> PF[S2_FMAX];
+#pragma unroll
+    for (int f = 0; f < S2_FMAX; ++f) PF[f].zero();
+    float res[S2_FMAX][VH];
+    auto hadv = [&](int hin, const LdH& L, auto ph_tag) {
+      constexpr int P = decltype(ph_tag)::value;
+      float WL[4][VH], WG[2][VH];
+#pragma unroll
+      for (int k = 0; k < VH; ++k) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) WL[e][k] = L.w[e][k];
+        WG[0][k] = L.w[4][k];
+        WG[1][k] = L.w[5][k];
+      }
+#pragma unroll
+      for (int f = 0; f < S2_FMAX; ++f) {
+        if (f < F) {
+          float tl[VH], tg[VH];
+          PF[f].template advance<P, hw, true>(L.xq[f], WL, WG, hin, h, ch0, tLh[f], tGh[f], tl, tg);
+#pragma unroll
+          for (int k = 0; k < VH; ++k) {   // mu * S_L^T l + ro * S_G^T o, grr_system_half's epilogue
+            float rv = tl[k] * scl1;
+            rv = rv + tg[k] * scg1;
+            res[f][k] = rv;
+          }
+        }
+      }
+    };
+    auto put = [&](int slot) {
+#pragma unroll
+      for (int f = 0; f < S2_FMAX; ++f)
+        if (f < F) {
+          F2 q;
+          q[0] = res[f][0]; q[1] = res[f][1];
+          *reinterpret_cast<F2*>(tring + (f * S2_TR + slot) * S2_HW + ch0) = q;
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    LdH Q[4];
+    issue_h(hb - 4, Q[0]);
+    issue_h(hb - 3, Q[1]);
+    issue_h(hb - 2, Q[2]);
+    issue_h(hb - 1, Q[3]);
+    hadv(hb - 4, Q[0], I0{});
+    issue_h(hb, Q[0]);
+    hadv(hb - 3, Q[1], I1{});
+    issue_h(hb + 1, Q[1]);
+    hadv(hb - 2, Q[2], I2{});
+    issue_h(hb + 2, Q[2]);
+    hadv(hb - 1, Q[3], I3{});
+    issue_h(hb + 3, Q[3]);
+    hadv(hb, Q[0], I0{});
+    hadv(hb + 1, Q[1], I1{});
+    issue_h(hb + 4, Q[0]);
+    hadv(hb + 2, Q[2], I2{});
+    hadv(hb + 3, Q[3], I3{});   // emits half row hb
+    put(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    auto hiter = [&](int i, auto pi_tag) {
+      constexpr int PI = decltype(pi_tag)::value;
+      issue_h(hb + 5 + i, Q[(PI + 1) & 1]);
+      hadv(hb + 4 + i, Q[PI & 1], pi_tag);
+      put((PI + 1) & 1);
+      if (i == i_top) __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    for (int i = 0; i < NI; i += S2_UNROLL) {
+      hiter(i, I0{});
+      hiter(i + 1, I1{});
+      hiter(i + 2, I2{});
+      hiter(i + 3, I3{});
+    }
+    return;
+  }
+
+  // ---- channel wave f: stage B = wave f < S2_FMAX, stage A = wave S2_FMAX + 1 + f
+  const bool role_a = wave > S2_PRODUCER;
+  const int f = role_a ? wave - S2_PRODUCER - 1 : wave;
   if (f >= F) {   // spare wave of a graph with F < S2_FMAX: the barriers only
     for (int i = 0; i <= NI + (i_top >= 0); ++i) __builtin_amdgcn_s_barrier();
     return;
   }
-  const int C = a.G * F, ch = g * F + f;
+  const int ch = g * F + f;
   const int64_t plane = ((int64_t)b * C + ch) * HW, hplane = ((int64_t)b * C + ch) * hHW;
-  const int64_t PB = HW * 4, HPB = hHW * 4;
   const bool use_beta_a = a.beta_a != nullptr && a.u_prev != nullptr;
   const bool use_skip = a.skip != nullptr;
   const rsrc_t rx = make_rsrc(a.x + plane, PB);
   const rsrc_t rb = make_rsrc(a.b + plane, PB);
   const rsrc_t ru = make_rsrc(use_beta_a ? a.u_prev + plane : nullptr, PB);   // absent: reads 0
-  const rsrc_t rth = make_rsrc(a.t_half + hplane, HPB);
   const rsrc_t ry = make_rsrc(use_skip ? a.y + plane : nullptr, PB);
   const rsrc_t rout = make_rsrc(a.out + plane, PB);
   const rsrc_t ruo = make_rsrc(a.u_out ? a.u_out + plane : nullptr, PB);
   const rsrc_t rxd = make_rsrc(a.xd_out ? a.xd_out + hplane : nullptr, HPB);
-  const uint32_t RB = (uint32_t)W * 4u, HRB = (uint32_t)hw * 4u;
-  const int c0 = 4 * lane, ch0 = 2 * lane;
-  const uint32_t vo = (uint32_t)c0 * 4u, vo_half = (uint32_t)ch0 * 4u;
 
   const float scl0 = expf(a.log_mu0[g]), scg0 = expf(a.log_ro0[g]);
-  const float scl1 = expf(a.log_mu1[g]), scg1 = expf(a.log_ro1[g]);
   // absent terms enter as exact zeros / ones: u_prev reads 0 (beta 0), y reads 0 (skip 0, 1)
   const float alpha_a = a.alpha_a[g], beta_a = use_beta_a ? a.beta_a[g] : 0.f;
   const float alpha_b = a.alpha_b[g], beta_b = a.beta_b ? a.beta_b[g] : 0.f;
@@ -1624,31 +1742,25 @@ void graph_step2_kernel(Step2Args a) {
   float* const xr = xring + f * S2_XR * S2_W + c0;
   float* const ur = uring + f * S2_UR * S2_W + c0;
   float* const dr = dring + f * S2_DR * S2_HW + ch0;
-  float* const dmy = dummy + c0;
-  float* const dmyh = dummy + S2_W + ch0;
+  const float* const tr = tring + f * S2_TR * S2_HW + ch0;
   const float* const wl_lane = wring + c0;
   const float* const hw_lane = hring + ch0;
 
   struct Ld {
-    float x[V], eb[V], eu[V], th[VH], b2[V], y2[V];
+    float x[V], eb[V], eu[V], b2[V], y2[V];
   };
-  // read-once streams (x_k, u_k, t_k, weights) are non-temporal so that b's rows stay in L2
-  // for stage B's second read 8 rows later (one HBM read of b per launch)
+  // read-once streams (x_k, u_k, weights) are non-temporal so that b's rows stay in L2 for
+  // stage B's second read 8 rows later (one HBM read of b per launch)
   auto issue_a = [&](int t, Ld& S) {
     bload<V, S2_NT>(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
     const int re = clampi(t - 3, 0, H - 1);
     bload(S.eb, rb, vo + re * RB);
     bload<V, S2_NT>(S.eu, ru, vo + re * RB);
-    bload<VH, S2_NT>(S.th, rth, vo_half + (re >> 1) * HRB);
   };
   auto issue_b = [&](int t, Ld& S) {
     const int r2 = clampi(t - 11, 0, H - 1);
     bload(S.b2, rb, vo + r2 * RB);
     bload(S.y2, ry, vo + r2 * RB);
-  };
-  auto issue = [&](int t, Ld& S) {
-    if (!GRR_STEP2_SPLIT || role_a) issue_a(t, S);
-    if (!GRR_STEP2_SPLIT || !role_a) issue_b(t, S);
   };
   auto ring_w = [&](const float* row, float (&WL)[4][V], float (&WG)[2][V]) {
 #pragma unroll
@@ -1684,8 +1796,9 @@ void graph_step2_kernel(Step2Args a) {
   float TH[VH] = {};
   float xa0[V], xb0[V];   // the even row of the current iteration (2x2 pooling)
 
-  // stage A (stage k) at step t: emits row t-3 into the x / u rings, D x half rows at odd rows
-  auto stage_a = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag, auto edge_tag) {
+  // stage A (stage k) at step t: emits row t-3 into the x / u rings, D x half rows at odd rows;
+  // th = t_k at half row (t-3) >> 1 (from the t ring)
+  auto stage_a = [&](int t, const Ld& S, const float (&thv)[VH], int q, auto par_tag, auto ph_tag, auto edge_tag) {
     constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
     constexpr bool EDGE = decltype(edge_tag)::value;
     float WL[4][V], WG[2][V], tl[V], tg[V];
@@ -1696,7 +1809,7 @@ void graph_step2_kernel(Step2Args a) {
     float xn[V], u[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const float th = 0.25f * S.th[j >> 1];
+      const float th = 0.25f * thv[j >> 1];
       float ax = x0[j];
       ax = ax + tl[j] * scl0;
       ax = ax + tg[j] * scg0;
@@ -1706,21 +1819,22 @@ void graph_step2_kernel(Step2Args a) {
       u[j] = uv;
       xn[j] = x0[j] + alpha_a * uv;
     }
-    const bool yin = y >= 0 && y < H;
-    st4(yin ? xr + (y & (S2_XR - 1)) * S2_W : dmy, xn);
-    st4(yin ? ur + (y % S2_UR) * S2_W : dmy, u);
+    if (y >= 0 && y < H) {   // uniform: rows outside the image never enter the rings
+      st4(xr + (y & (S2_XR - 1)) * S2_W, xn);
+      st4(ur + (y % S2_UR) * S2_W, u);
+    }
     if constexpr (PAR == 0) {
 #pragma unroll
       for (int j = 0; j < V; ++j) xa0[j] = xn[j];
     } else {
-      float d[VH];
-#pragma unroll
-      for (int k = 0; k < VH; ++k)
-        d[k] = 0.25f * xa0[2 * k] + 0.25f * xa0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
       const int hA = (y - 1) / 2;
-      F2 qv;
-      qv[0] = d[0]; qv[1] = d[1];
-      *reinterpret_cast<F2*>((hA >= 0 && hA < h) ? dr + (hA & (S2_DR - 1)) * S2_HW : dmyh) = qv;
+      if (hA >= 0 && hA < h) {
+        F2 qv;
+#pragma unroll
+        for (int k = 0; k < VH; ++k)
+          qv[k] = 0.25f * xa0[2 * k] + 0.25f * xa0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+        *reinterpret_cast<F2*>(dr + (hA & (S2_DR - 1)) * S2_HW) = qv;
+      }
     }
   };
 
@@ -1797,13 +1911,13 @@ void graph_step2_kernel(Step2Args a) {
   };
 
   Ld LA, LB;
-  issue(ts, LA);
-  issue(ts + 1, LB);
-  // Ring rows the pipelines read before their first write (rows above the image / before the
-  // segment, weight pairs of stage B's fill) only feed rows that are never stored, but through
-  // products with a 0 weight: zero them so the garbage is finite.  Weight slots 2..6 are first
-  // filled after the barrier below.
-  if (!GRR_STEP2_SPLIT || role_a) {
+  if (role_a) {
+    issue_a(ts, LA);
+    issue_a(ts + 1, LB);
+    // Ring rows the pipelines read before their first write (rows above the image / before the
+    // segment, weight pairs of stage B's fill) only feed rows that are never stored, but through
+    // products with a 0 weight: zero them so the garbage is finite.  Weight slots 2..6 are first
+    // filled after the barrier below.
     const float zero4[V] = {};
 #pragma unroll
     for (int r = 0; r < S2_XR; ++r) st4(xr + r * S2_W, zero4);
@@ -1812,52 +1926,32 @@ void graph_step2_kernel(Step2Args a) {
     *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
     *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + S2_W + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
     for (int r = f; r < (S2_WP - 2) * 12; r += F) st4(wring + 2 * S2_PAIR + r * S2_W + c0, zero4);
+  } else {
+    issue_b(ts, LA);
+    issue_b(ts + 1, LB);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();   // the producer's first ring rows have landed
+  __builtin_amdgcn_s_barrier();   // the producer's first ring rows and the first t_k row have landed
   asm volatile("" ::: "memory");
   int qa = 0;
-  // one iteration = two steps of stage A, one half-level row, two steps of stage B; PI = the
-  // iteration's phase in the unrolled body (pipelines A, B advance two slots per iteration, the
-  // half level one)
-  auto iteration = [&](int i, auto pi_tag, auto edge_tag) {
-    constexpr int PI = decltype(pi_tag)::value;
-    using P0 = std::integral_constant<int, (2 * PI) & 3>;
-    using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
-    using PHh = std::integral_constant<int, PI & 3>;
-    using E = decltype(edge_tag);
-    const int t = ts + 2 * i;
-    const int qb = qa >= 4 ? qa - 4 : qa + 3;   // pair i - 4 (mod 7)
-    stage_a(t, LA, qa, std::integral_constant<int, 0>{}, P0{}, E{});
-    stage_a(t + 1, LB, qa, std::integral_constant<int, 1>{}, P1{}, E{});
-    stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{}, E{});   // hA: the half row stage A just pooled
-    stage_b(t, LA, qb, std::integral_constant<int, 0>{}, P0{}, E{});
-    issue(t + 2, LA);
-    stage_b(t + 1, LB, qb, std::integral_constant<int, 1>{}, P1{}, E{});
-    issue(t + 3, LB);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ring reads done before the producer refills
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    qa = qa == S2_WP - 1 ? 0 : qa + 1;
-  };
-  auto block = [&](int i, auto edge_tag) {
-    iteration(i, std::integral_constant<int, 0>{}, edge_tag);
-    iteration(i + 1, std::integral_constant<int, 1>{}, edge_tag);
-    iteration(i + 2, std::integral_constant<int, 2>{}, edge_tag);
-    iteration(i + 3, std::integral_constant<int, 3>{}, edge_tag);
-  };
-#if GRR_STEP2_SPLIT
   // stage-A wave: two rows of stage k per iteration; stage-B wave: the half level and two rows of
-  // stage k+1 (8 rows behind, its inputs written into the rings at least one barrier earlier)
+  // stage k+1 (8 rows behind, its inputs written into the rings at least one barrier earlier).
+  // PI = the iteration's phase in the unrolled body (pipelines A, B advance two slots per
+  // iteration, the half level one)
   auto iteration_a = [&](int i, auto pi_tag, auto edge_tag) {
     constexpr int PI = decltype(pi_tag)::value;
     using P0 = std::integral_constant<int, (2 * PI) & 3>;
     using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
     using E = decltype(edge_tag);
     const int t = ts + 2 * i;
-    stage_a(t, LA, qa, std::integral_constant<int, 0>{}, P0{}, E{});
+    float thv[VH];
+    {
+      const F2 q = *reinterpret_cast<const F2*>(tr + (PI & 1) * S2_HW);   // t_k half row (t-3)/2
+      thv[0] = q[0]; thv[1] = q[1];
+    }
+    stage_a(t, LA, thv, qa, std::integral_constant<int, 0>{}, P0{}, E{});
     issue_a(t + 2, LA);
-    stage_a(t + 1, LB, qa, std::integral_constant<int, 1>{}, P1{}, E{});
+    stage_a(t + 1, LB, thv, qa, std::integral_constant<int, 1>{}, P1{}, E{});
     issue_a(t + 3, LB);
     if (i == i_top) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1902,9 +1996,6 @@ void graph_step2_kernel(Step2Args a) {
       iteration_b(i + 3, std::integral_constant<int, 3>{}, std::true_type{});
     }
   }
-#else
-  for (int i = 0; i < NI; i += S2_UNROLL) block(i, std::true_type{});
-#endif
 }
 
 static int step2_seg_rows(int H, uint64_t blocks_per_seg) {
@@ -2120,7 +2211,7 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
   return launch_op<false, GTV_PAIR, EPI_STEP>(a, B, s, "grr_system_step");
 }
 
-grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* t_half,
+grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* xd,
                             const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
                             const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
                             grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
@@ -2128,7 +2219,7 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
                             const float* skip, const float* y_skip, float* x_out, float* u_out, float* xd_out,
                             int B, int G, int F, int H, int W, void* stream) {
   clear_error();
-  GRR_REQUIRE(x && b && t_half && wL0 && cG0 && wL1 && cG1 && log_mu0 && log_ro0 && log_mu1 && log_ro1 && alpha_a &&
+  GRR_REQUIRE(x && b && xd && wL0 && cG0 && wL1 && cG1 && log_mu0 && log_ro0 && log_mu1 && log_ro1 && alpha_a &&
                   alpha_b && x_out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_system_step2: bad args");
   GRR_REQUIRE(stencil_ok(sL0) && stencil_ok(sG0) && stencil_ok(sL1) && stencil_ok(sG1), GRR_ERR_INVALID_ARG,
@@ -2140,11 +2231,11 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_system_step2: plane too large");
   GRR_REQUIRE(x_out != x && x_out != b && x_out != u_prev && (!u_out || (u_out != u_prev && u_out != x && u_out != b)),
               GRR_ERR_INVALID_ARG, "grr_system_step2: outputs must not alias the inputs (rows are read ahead)");
-  const void* ptrs[] = {x, b, u_prev, t_half, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out};
+  const void* ptrs[] = {x, b, u_prev, xd, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out};
   for (const void* q : ptrs)
     GRR_REQUIRE((uintptr_t)q % 16 == 0, GRR_ERR_INVALID_ARG, "grr_system_step2: operands must be 16-byte aligned");
   Step2Args a{};
-  a.x = x; a.b = b; a.u_prev = u_prev; a.t_half = t_half;
+  a.x = x; a.b = b; a.u_prev = u_prev; a.xd = xd;
   a.wL0 = wL0; a.cG0 = cG0; a.wL1 = wL1; a.cG1 = cG1;
   a.sL0 = sL0; a.sG0 = sG0; a.sL1 = sL1; a.sG1 = sG1;
   a.log_mu0 = log_mu0; a.log_ro0 = log_ro0; a.log_mu1 = log_mu1; a.log_ro1 = log_ro1;
@@ -2156,7 +2247,7 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   const uint64_t nblk = (uint64_t)B * G * a.nsegs;
   GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_step2: grid too large");
   a.nblk = (uint32_t)nblk;
-  hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(GRR_STEP2_SPLIT ? S2_THREADS : 64 * (F + 1)), 0,
+  hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(S2_THREADS), 0,
                      (hipStream_t)stream, a);
   return launch_status("grr_system_step2");
 }

@@ -486,11 +486,11 @@ class MixtureGTVGLR(nn.Module):
         pair = OPS.step2_supported(x, g)
         k = 1
         while k < n_st:                                              # (REF:784-790, :797-807)
-            t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
             if pair and k + 1 < n_st:
-                # stages k, k+1 in one pass: x_{k+1}, u_{k+1}, t_{k+1} stay on chip
+                # stages k, k+1 in one pass, both half levels inside: t_k, x_{k+1}, u_{k+1},
+                # t_{k+1} stay on chip
                 last = k + 1 == n_st - 1
-                x, u_new, xd = OPS.system_step2(x, b_b, u, t, wL0, cG0, L0, G0, mu0, ro0, wL1, cG1, L1, G1, mu1,
+                x, u_new, xd = OPS.system_step2(x, b_b, u, xd, wL0, cG0, L0, G0, mu0, ro0, wL1, cG1, L1, G1, mu1,
                                                 ro1, alpha[k], beta[k] if k >= 2 else None, alpha[k + 1], beta[k + 1],
                                                 g, want_u=not last, want_pool=not last, skip=skip if last else None,
                                                 y_skip=y if last else None, u_out=u_spare)
@@ -498,6 +498,7 @@ class MixtureGTVGLR(nn.Module):
                 k += 2
                 continue
             last = k == n_st - 1
+            t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
             x, u, xd = OPS.system_step(x, b_b, u, t, wL0, cG0, L0, G0, mu0, ro0, alpha[k],
                                        beta[k] if k >= 2 else None, g, want_u=not last, want_pool=not last,
                                        skip=skip if last else None, y_skip=y if last else None, u_out=u)

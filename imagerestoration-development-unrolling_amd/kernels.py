@@ -284,15 +284,16 @@ def system_step(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Option
     return out, u_out, xd
 
 
-def system_step2(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Tensor,
+def system_step2(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: Tensor,
                  wL0: Tensor, cG0: Tensor, sL0: Stencil, sG0: Stencil, log_mu0: Tensor, log_ro0: Tensor,
                  wL1: Tensor, cG1: Tensor, sL1: Stencil, sG1: Stencil, log_mu1: Tensor, log_ro1: Tensor,
                  alpha_a: Tensor, beta_a: Optional[Tensor], alpha_b: Tensor, beta_b: Optional[Tensor],
                  n_graphs: int, want_u: bool, want_pool: bool, skip: Optional[Tensor] = None,
                  y_skip: Optional[Tensor] = None, u_out: Optional[Tensor] = None
                  ) -> Tuple[Tensor, Optional[Tensor], Optional[Tensor]]:
-    """Stages k and k+1 in one pass (grr_system_step2): returns (x_{k+2}, u_{k+2}, D x_{k+2})."""
-    dev = _check("system_step2", x, rhs, u_prev, t_half, wL0, cG0, log_mu0, log_ro0, wL1, cG1, log_mu1, log_ro1,
+    """Stages k and k+1 in one pass (grr_system_step2), the half level of both inside it; xd_in = D x_k
+    (the previous pass's pooled output).  Returns (x_{k+2}, u_{k+2}, D x_{k+2})."""
+    dev = _check("system_step2", x, rhs, u_prev, xd_in, wL0, cG0, log_mu0, log_ro0, wL1, cG1, log_mu1, log_ro1,
                  alpha_a, beta_a, alpha_b, beta_b, skip, y_skip)
     b, c, h, w = x.shape
     out = torch.empty_like(x)
@@ -303,7 +304,7 @@ def system_step2(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Tenso
     xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_pool else None
     _launch("system_step2", step2_bytes(b, c, n_graphs, h, w, u_prev is not None, u_out is not None, want_pool,
                                         skip is not None),
-            "grr_system_step2", x.data_ptr(), rhs.data_ptr(), _ptr(u_prev), t_half.data_ptr(), wL0.data_ptr(),
+            "grr_system_step2", x.data_ptr(), rhs.data_ptr(), _ptr(u_prev), xd_in.data_ptr(), wL0.data_ptr(),
             cG0.data_ptr(), sL0, sG0, log_mu0.data_ptr(), log_ro0.data_ptr(), wL1.data_ptr(), cG1.data_ptr(), sL1, sG1,
             log_mu1.data_ptr(), log_ro1.data_ptr(), alpha_a.data_ptr(), _ptr(beta_a), alpha_b.data_ptr(),
             _ptr(beta_b), _ptr(skip), _ptr(y_skip), out.data_ptr(), _ptr(u_out), _ptr(xd), b, n_graphs,
@@ -322,11 +323,12 @@ def step2_supported(x: Tensor, n_graphs: int) -> bool:
 
 
 def step2_bytes(b, c, g, h, w, has_u_prev, has_u_out, has_pool, has_skip):
-    """Compulsory HBM bytes of one grr_system_step2 launch: x, b, u_prev, t_half, the full- and
-    half-level GLR + pair weights read once; x_out, u_out, D x_out written once (x_{k+1}, u_{k+1},
-    t_{k+1} stay on chip; the second read of b rows is an L2 hit by construction)."""
+    """Compulsory HBM bytes of one grr_system_step2 launch: x, b, u_prev, D x_k, the full- and
+    half-level GLR + pair weights read once; x_out, u_out, D x_out written once (t_k, x_{k+1},
+    u_{k+1}, t_{k+1} stay on chip; the second reads of b rows and of half-level weight rows are
+    L2 hits by construction)."""
     f = c * (2 + int(has_u_prev) + 1 + int(has_u_out) + int(has_skip))    # x, b, u_prev, x_out, u_out, y
-    f += (c // 4) * (1 + int(has_pool))                                   # t_half in, D x_out
+    f += (c // 4) * (1 + int(has_pool))                                   # D x_k in, D x_out
     f += 6 * g + (6 * g) // 4                                             # full + half-level weights
     return 4 * b * h * w * f
 

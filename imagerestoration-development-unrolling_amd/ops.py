@@ -232,7 +232,7 @@ def _(x, rhs, u_prev, t_half, wL, cG, sL01, sL02a, sL02b, sL03, sG01, sG02a, sG0
 
 
 @custom_op(f"{NS}::system_step2", mutates_args=())
-def system_step2_op(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Tensor, wL0: Tensor, cG0: Tensor,
+def system_step2_op(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd: Tensor, wL0: Tensor, cG0: Tensor,
                     sL01: Tensor, sL02a: Tensor, sL02b: Tensor, sL03: Tensor,
                     sG01: Tensor, sG02a: Tensor, sG02b: Tensor, sG03: Tensor, log_mu0: Tensor, log_ro0: Tensor,
                     wL1: Tensor, cG1: Tensor, tL01: Tensor, tL02a: Tensor, tL02b: Tensor, tL03: Tensor,
@@ -241,7 +241,7 @@ def system_step2_op(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Te
                     n_graphs: int, want_u: bool, want_pool: bool, skip: Optional[Tensor],
                     y_skip: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
     c = lambda t: None if t is None else t.contiguous()
-    xo, u, xd = K.system_step2(x.contiguous(), rhs.contiguous(), u_prev, t_half, wL0, cG0,
+    xo, u, xd = K.system_step2(x.contiguous(), rhs.contiguous(), u_prev, xd.contiguous(), wL0, cG0,
                                _st(sL01, sL02a, sL02b, sL03), _st(sG01, sG02a, sG02b, sG03), log_mu0, log_ro0,
                                wL1, cG1, _st(tL01, tL02a, tL02b, tL03), _st(tG01, tG02a, tG02b, tG03), log_mu1, log_ro1,
                                c(alpha_a), c(beta_a), c(alpha_b), c(beta_b), n_graphs, want_u, want_pool, skip, y_skip)
@@ -249,7 +249,7 @@ def system_step2_op(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], t_half: Te
 
 
 @system_step2_op.register_fake
-def _(x, rhs, u_prev, t_half, wL0, cG0, sL01, sL02a, sL02b, sL03, sG01, sG02a, sG02b, sG03, log_mu0, log_ro0,
+def _(x, rhs, u_prev, xd, wL0, cG0, sL01, sL02a, sL02b, sL03, sG01, sG02a, sG02b, sG03, log_mu0, log_ro0,
       wL1, cG1, tL01, tL02a, tL02b, tL03, tG01, tG02a, tG02b, tG03, log_mu1, log_ro1, alpha_a, beta_a, alpha_b,
       beta_b, n_graphs, want_u, want_pool, skip, y_skip):
     return (torch.empty_like(x), torch.empty_like(x) if want_u else x.new_empty(0),
@@ -447,17 +447,18 @@ def system_step(x, rhs, u_prev, t_half, wL, cG, modL, modG, log_mu0, log_ro0, al
                          n_graphs, want_u, want_pool, skip=skip, y_skip=y_skip, u_out=u_out)
 
 
-def system_step2(x, rhs, u_prev, t_half, wL0, cG0, modL0, modG0, log_mu0, log_ro0, wL1, cG1, modL1, modG1,
+def system_step2(x, rhs, u_prev, xd, wL0, cG0, modL0, modG0, log_mu0, log_ro0, wL1, cG1, modL1, modG1,
                  log_mu1, log_ro1, alpha_a, beta_a, alpha_b, beta_b, n_graphs, want_u, want_pool, skip=None,
                  y_skip=None, u_out=None):
-    """kernels.system_step2 (stages k, k+1 in one pass); ``u_out`` must not be u_prev (eager only)."""
+    """kernels.system_step2 (stages k, k+1 in one pass, both half levels inside; xd = D x_k);
+    ``u_out`` must not be u_prev (eager only)."""
     if _tracing():
-        xo, u, xd = torch.ops.irdu.system_step2(x, rhs, u_prev, t_half, wL0, cG0, *_sp(modL0), *_sp(modG0), log_mu0,
+        xo, u, xd = torch.ops.irdu.system_step2(x, rhs, u_prev, xd, wL0, cG0, *_sp(modL0), *_sp(modG0), log_mu0,
                                                 log_ro0, wL1, cG1, *_sp(modL1), *_sp(modG1), log_mu1, log_ro1,
                                                 alpha_a, beta_a, alpha_b, beta_b, n_graphs, want_u, want_pool, skip,
                                                 y_skip)
         return xo, _opt(u), _opt(xd)
-    return K.system_step2(x, rhs, u_prev, t_half, wL0, cG0, K.stencil(modL0), K.stencil(modG0), log_mu0, log_ro0,
+    return K.system_step2(x, rhs, u_prev, xd, wL0, cG0, K.stencil(modL0), K.stencil(modG0), log_mu0, log_ro0,
                           wL1, cG1, K.stencil(modL1), K.stencil(modG1), log_mu1, log_ro1, alpha_a, beta_a, alpha_b,
                           beta_b, n_graphs, want_u, want_pool, skip=skip, y_skip=y_skip, u_out=u_out)
 

@@ -146,15 +146,17 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
                            int B, int G, int F, int H, int W, void* stream);
 
 /* Two consecutive stages k, k+1 of the loop above (REF:784-790 twice) in one pass
- * (temporal blocking; x_{k+1}, u_{k+1} and t_{k+1} never leave the chip):
- *   stage A (k):   x_{k+1}, u_{k+1} from x, u_prev (beta_a), t_half = grr_system_half(D x)
- *   half level:    t_{k+1} = exp(log_mu1) L1 (D x_{k+1}) + exp(log_ro1) G1 (D x_{k+1})
+ * (temporal blocking; t_k, x_{k+1}, u_{k+1} and t_{k+1} never leave the chip):
+ *   half level A:  t_k = exp(log_mu1) L1 xd + exp(log_ro1) G1 xd, xd = D x (the previous pass's
+ *                  xd_out; what grr_system_half computes)
+ *   stage A (k):   x_{k+1}, u_{k+1} from x, u_prev (beta_a), t_k
+ *   half level B:  t_{k+1} = exp(log_mu1) L1 (D x_{k+1}) + exp(log_ro1) G1 (D x_{k+1})
  *   stage B (k+1): x_out = x_{k+2}, u_out = u_{k+2} (beta_b with u_{k+1}), xd_out = D x_{k+2},
  *                  skip applied to x_out as in grr_system_step.
- * Same values as grr_system_step(k) -> grr_system_half -> grr_system_step(k+1) up to fp32
+ * Same values as grr_system_half -> grr_system_step(k) -> grr_system_half -> grr_system_step(k+1) up to fp32
  * rounding order.  GLR + GTV pair at both levels; W = 256, even H, F <= 3; outputs must
  * not alias inputs (u_out != u_prev).  Replaces two iterations of the loop body REF:784-790. */
-grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* t_half,
+grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* xd,
                             const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
                             const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
                             grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,

@@ -50,7 +50,8 @@ def main():
         cg1 = torch.rand(b, g, 2, h // 2, w // 2, device=dev)
         sl1, sg1 = K.stencil(mix.GLRmodule01), K.stencil(mix.GTVmodule01)
         u_out = torch.empty_like(u)
-        fn = lambda: K.system_step2(x, rhs, u, th, wl, cg, sl, sg, p(mix.muys00), p(mix.ro00), wl1, cg1, sl1, sg1,  # noqa: E731
+        xd = torch.rand(b, c, h // 2, w // 2, device=dev)
+        fn = lambda: K.system_step2(x, rhs, u, xd, wl, cg, sl, sg, p(mix.muys00), p(mix.ro00), wl1, cg1, sl1, sg1,  # noqa: E731
                                     p(mix.muys01), p(mix.ro01), p(mix.alphaCGD)[2], p(mix.betaCGD)[2],
                                     p(mix.alphaCGD)[3], p(mix.betaCGD)[3], g, want_u=True, want_pool=True,
                                     u_out=u_out)

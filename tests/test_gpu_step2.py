@@ -1,5 +1,6 @@
-"""grr_system_step2 (two CG stages per pass, temporal blocking) against the one-stage-per-launch
-sequence grr_system_step -> grr_system_half -> grr_system_step and against the CPU oracle.
+"""grr_system_step2 (two CG stages per pass, temporal blocking, both half levels inside) against the
+one-stage-per-launch sequence grr_system_half -> grr_system_step -> grr_system_half -> grr_system_step
+and against the CPU oracle.
 
 The fused kernel computes the same values with the same per-row arithmetic; the tolerance
 below (2e-6 relative to the largest output) covers fp32 contraction differences between the
@@ -63,7 +64,7 @@ def _two_steps(irdu, mix, x, b, u, w, k, g, skip=None, y_skip=None, last=False):
     ref2, u2, xd2 = OPS.system_step(ref1, b, u1, t1, wL0, cG0, m.GLRmodule00, m.GTVmodule00, m.muys00, m.ro00,
                                     alpha[k + 1], beta[k + 1], g, want_u=not last, want_pool=not last,
                                     skip=skip, y_skip=y_skip)
-    got, gu, gxd = OPS.system_step2(x, b, u, t, wL0, cG0, m.GLRmodule00, m.GTVmodule00, m.muys00, m.ro00, wL1, cG1,
+    got, gu, gxd = OPS.system_step2(x, b, u, xd, wL0, cG0, m.GLRmodule00, m.GTVmodule00, m.muys00, m.ro00, wL1, cG1,
                                     m.GLRmodule01, m.GTVmodule01, m.muys01, m.ro01, alpha[k],
                                     beta[k] if u is not None else None, alpha[k + 1], beta[k + 1], g,
                                     want_u=not last, want_pool=not last, skip=skip, y_skip=y_skip)
@@ -76,6 +77,7 @@ CASES = [
     dict(B=3, G=2, F=3, H=16),      # shorter than the pipeline lag
     dict(B=2, G=3, F=2, H=130),     # H not a multiple of the segment, F = 2
     dict(B=1, G=4, F=1, H=64),
+    dict(B=2, G=2, F=3, H=8),       # half rows fewer than the half-level pipeline's fill
 ]
 
 
