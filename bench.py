@@ -89,27 +89,29 @@ STEP_KERNEL = "graph_row_kernel<true, 1, 2, 4>"
 TRAFFIC_FILES = {STEP2_KERNEL: "traffic_system_step2.json", STEP_KERNEL: "traffic_system_step.json"}
 
 
-def load_traffic(kernel):
-    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC summary under profiles/
-    (None when there is none for that kernel)."""
-    path = os.path.join(ROOT, "profiles", TRAFFIC_FILES[kernel])
+def _traffic(path, kernel_prefix, batch):
+    """hbm_bytes_per_launch of a PMC summary (scripts/pmc_bench.sh: FETCH_SIZE / WRITE_SIZE passes
+    over this bench at the same batch), or None when absent or measured on another workload --
+    a per-launch byte count only compares with the algorithmic bytes of the same shape."""
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
-    if d.get("kernel") != kernel:
+    if not d.get("kernel", "").startswith(kernel_prefix):
+        return None
+    if d.get("workload") != {"batch": batch, "size": 256}:
         return None
     return d.get("hbm_bytes_per_launch")
 
 
-def load_traffic_file(name, kernel_prefix):
-    """Per-launch HBM bytes from a committed PMC summary under profiles/r03/ (None when absent)."""
-    path = os.path.join(ROOT, "profiles", "r03", name)
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch") if d.get("kernel", "").startswith(kernel_prefix) else None
+def load_traffic(kernel, batch):
+    """Per-launch HBM bytes of the solver kernel `kernel` at this bench's batch (profiles/)."""
+    return _traffic(os.path.join(ROOT, "profiles", TRAFFIC_FILES[kernel]), kernel, batch)
+
+
+def load_traffic_file(name, kernel_prefix, batch):
+    """Per-launch HBM bytes (mean over the bench's launches of that kernel) from profiles/r03/."""
+    return _traffic(os.path.join(ROOT, "profiles", "r03", name), kernel_prefix, batch)
 
 
 def host_cpus():
@@ -280,7 +282,7 @@ def main():
     kind, kname = ("system_step2", STEP2_KERNEL) if "system_step2" in kern else ("system_step", STEP_KERNEL)
     step = kern[kind]
     achieved = step["gbps"]
-    traffic = load_traffic(kname)
+    traffic = load_traffic(kname, b)
     roofline = {"bound": "hbm", "kernel": f"grr_{kind} ({kname})",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
@@ -325,7 +327,7 @@ def main():
                 "achieved": round(hd["tflops"], 2), "peak": round(SPLIT_F16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
                 "frac": round(hd["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": hd["flops_per_launch"],
                 "mean_launch_ms": round(hd["mean_ms"], 4), "launches": hd["launches"],
-                "traffic": load_traffic_file("traffic_lnb_head16.json", "lnb_head16_kernel"),
+                "traffic": load_traffic_file("traffic_lnb_head16.json", "lnb_head16_kernel", b),
                 "note": "algorithmic fp32 flops (kernels.lnb_head_flops: LN, W1, depthwise, gate) / HIP-event time, "
                         "against the dense fp16 MFMA rate / 3 (each W1 product = 3 fp16 products of exact 2-term "
                         "splits); the depthwise + gate part is VALU work"},
@@ -335,7 +337,7 @@ def main():
                 "frac": round(mx["gbps"] / HBM_PEAK_GBPS, 4), "bytes_per_launch": mx["bytes_per_launch"],
                 "mean_launch_ms": round(mx["mean_ms"], 4), "launches": mx["launches"],
                 "mfma_tflops": round(mx["tflops"], 2), "mfma_peak": round(SPLIT_BF16_PEAK_TFLOPS, 1),
-                "traffic": load_traffic_file("traffic_lnb_mix.json", "lnb_mix_kernel"),
+                "traffic": load_traffic_file("traffic_lnb_mix.json", "lnb_mix_kernel", b),
                 "note": "algorithmic bytes (g + skip operand + out) / HIP-event time; W2 on 6 bf16 products"}}
     kernels_ms = {k: round(v["total_ms"] / n_inst, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms

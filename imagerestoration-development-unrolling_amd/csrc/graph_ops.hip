@@ -1362,6 +1362,7 @@ struct Step2Args {
   float* u_out;
   float* xd_out;
   int G, F, H, nsegs, sseg;
+  int FG, ngrp;         // channel groups of <= S2_FMAX channels per (b, graph): FG channels each (the last may hold fewer)
   uint32_t nblk;
 };
 
@@ -1494,6 +1495,11 @@ constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW +
 #endif
 constexpr int S2_NT = GRR_STEP2_NT ? 2 : 0;   // cache policy of step2's read-once / write-once streams
 constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipelines' slot period)
+#ifndef GRR_STEP2_AHEAD
+#define GRR_STEP2_AHEAD 2
+#endif
+constexpr int S2_AHEAD = GRR_STEP2_AHEAD;  // iterations between a channel wave's row loads and their use (1 or 2)
+static_assert(S2_AHEAD == 1 || S2_AHEAD == 2, "step2 load distance");
 static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
 // Waves (wave w runs on SIMD w mod 4): stage B of channel f = wave f, the producer = wave
 // S2_FMAX, stage A of channel f = wave S2_FMAX + 1 + f, stage A's half level (all channels) =
@@ -1521,6 +1527,8 @@ void graph_step2_kernel(Step2Args a) {
   const int F = a.F;
   uint32_t unit = xcd_remap(blockIdx.x, a.nblk);
   const int seg = unit % a.nsegs; unit /= a.nsegs;
+  const int grp = unit % a.ngrp; unit /= a.ngrp;
+  const int fb = grp * a.FG, Fg = min(a.FG, F - fb);   // this workgroup's channels fb .. fb + Fg - 1 of graph g
   const int g = unit % a.G;
   const int b = unit / a.G;
   const int H = a.H, h = H / 2;
@@ -1605,20 +1613,20 @@ void graph_step2_kernel(Step2Args a) {
     // iterations later, from L2).  The pipeline is primed with 8 rows before the first barrier.
     const int hb = (ts - 3) / 2;   // the half row stage A reads in iteration 0 (ts - 3 is even)
     const int64_t gq = (int64_t)b * a.G + g;
-    const rsrc_t rxq = make_rsrc(a.xd + ((int64_t)b * C + (int64_t)g * F) * hHW, (int64_t)F * HPB);
+    const rsrc_t rxq = make_rsrc(a.xd + ((int64_t)b * C + (int64_t)g * F + fb) * hHW, (int64_t)Fg * HPB);
     const rsrc_t rwl = make_rsrc(a.wL1 + gq * 4 * hHW, 4 * HPB);
     const rsrc_t rcg = make_rsrc(a.cG1 + gq * 2 * hHW, 2 * HPB);
     Taps tLh[S2_FMAX], tGh[S2_FMAX];
 #pragma unroll
     for (int f = 0; f < S2_FMAX; ++f) {
-      const int chf = g * F + min(f, F - 1);
+      const int chf = g * F + fb + min(f, Fg - 1);
       tLh[f] = make_taps(a.sL1, chf);
       tGh[f] = make_taps(a.sG1, chf);
     }
     struct LdH {
       float xq[S2_FMAX][VH], w[6][VH];
     };
-    // channels f >= F read past the operand's range: 0
+    // channels f >= Fg read past the operand's range: 0
     auto issue_h = [&](int hin, LdH& L) {
       const uint32_t ro = vo_half + (uint32_t)clampi(hin, 0, h - 1) * HRB;
 #pragma unroll
@@ -1645,7 +1653,7 @@ void graph_step2_kernel(Step2Args a) {
       }
 #pragma unroll
       for (int f = 0; f < S2_FMAX; ++f) {
-        if (f < F) {
+        if (f < Fg) {
           float tl[VH], tg[VH];
           PF[f].template advance<P, hw, true>(L.xq[f], WL, WG, hin, h, ch0, tLh[f], tGh[f], tl, tg);
 #pragma unroll
@@ -1660,7 +1668,7 @@ void graph_step2_kernel(Step2Args a) {
     auto put = [&](int slot) {
 #pragma unroll
       for (int f = 0; f < S2_FMAX; ++f)
-        if (f < F) {
+        if (f < Fg) {
           F2 q;
           q[0] = res[f][0]; q[1] = res[f][1];
           *reinterpret_cast<F2*>(tring + (f * S2_TR + slot) * S2_HW + ch0) = q;
@@ -1714,11 +1722,11 @@ void graph_step2_kernel(Step2Args a) {
   // ---- channel wave f: stage B = wave f < S2_FMAX, stage A = wave S2_FMAX + 1 + f
   const bool role_a = wave > S2_PRODUCER;
   const int f = role_a ? wave - S2_PRODUCER - 1 : wave;
-  if (f >= F) {   // spare wave of a graph with F < S2_FMAX: the barriers only
+  if (f >= Fg) {   // spare wave of a group with Fg < S2_FMAX channels: the barriers only
     for (int i = 0; i <= NI + (i_top >= 0); ++i) __builtin_amdgcn_s_barrier();
     return;
   }
-  const int ch = g * F + f;
+  const int ch = g * F + fb + f;
   const int64_t plane = ((int64_t)b * C + ch) * HW, hplane = ((int64_t)b * C + ch) * hHW;
   const bool use_beta_a = a.beta_a != nullptr && a.u_prev != nullptr;
   const bool use_skip = a.skip != nullptr;
@@ -1910,10 +1918,14 @@ void graph_step2_kernel(Step2Args a) {
     }
   };
 
-  Ld LA, LB;
+  Ld LA, LB, LC, LD;   // rows of iterations i (A, B) and, at S2_AHEAD = 2, i + 1 (C, D) in flight
   if (role_a) {
     issue_a(ts, LA);
     issue_a(ts + 1, LB);
+    if (S2_AHEAD == 2) {
+      issue_a(ts + 2, LC);
+      issue_a(ts + 3, LD);
+    }
     // Ring rows the pipelines read before their first write (rows above the image / before the
     // segment, weight pairs of stage B's fill) only feed rows that are never stored, but through
     // products with a 0 weight: zero them so the garbage is finite.  Weight slots 2..6 are first
@@ -1925,10 +1937,14 @@ void graph_step2_kernel(Step2Args a) {
     for (int r = 0; r < S2_UR; ++r) st4(ur + r * S2_W, zero4);
     *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
     *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + S2_W + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
-    for (int r = f; r < (S2_WP - 2) * 12; r += F) st4(wring + 2 * S2_PAIR + r * S2_W + c0, zero4);
+    for (int r = f; r < (S2_WP - 2) * 12; r += Fg) st4(wring + 2 * S2_PAIR + r * S2_W + c0, zero4);
   } else {
     issue_b(ts, LA);
     issue_b(ts + 1, LB);
+    if (S2_AHEAD == 2) {
+      issue_b(ts + 2, LC);
+      issue_b(ts + 3, LD);
+    }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // the producer's first ring rows and the first t_k row have landed
@@ -1949,10 +1965,12 @@ void graph_step2_kernel(Step2Args a) {
       const F2 q = *reinterpret_cast<const F2*>(tr + (PI & 1) * S2_HW);   // t_k half row (t-3)/2
       thv[0] = q[0]; thv[1] = q[1];
     }
-    stage_a(t, LA, thv, qa, std::integral_constant<int, 0>{}, P0{}, E{});
-    issue_a(t + 2, LA);
-    stage_a(t + 1, LB, thv, qa, std::integral_constant<int, 1>{}, P1{}, E{});
-    issue_a(t + 3, LB);
+    Ld& LX = (S2_AHEAD == 2 && (PI & 1)) ? LC : LA;
+    Ld& LY = (S2_AHEAD == 2 && (PI & 1)) ? LD : LB;
+    stage_a(t, LX, thv, qa, std::integral_constant<int, 0>{}, P0{}, E{});
+    issue_a(t + 2 * S2_AHEAD, LX);
+    stage_a(t + 1, LY, thv, qa, std::integral_constant<int, 1>{}, P1{}, E{});
+    issue_a(t + 2 * S2_AHEAD + 1, LY);
     if (i == i_top) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1972,10 +1990,12 @@ void graph_step2_kernel(Step2Args a) {
     const int qb = qa >= 4 ? qa - 4 : qa + 3;   // pair i - 4 (mod 7)
     if (i == i_top) __builtin_amdgcn_s_barrier();
     stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{}, E{});
-    stage_b(t, LA, qb, std::integral_constant<int, 0>{}, P0{}, E{});
-    issue_b(t + 2, LA);
-    stage_b(t + 1, LB, qb, std::integral_constant<int, 1>{}, P1{}, E{});
-    issue_b(t + 3, LB);
+    Ld& LX = (S2_AHEAD == 2 && (PI & 1)) ? LC : LA;
+    Ld& LY = (S2_AHEAD == 2 && (PI & 1)) ? LD : LB;
+    stage_b(t, LX, qb, std::integral_constant<int, 0>{}, P0{}, E{});
+    issue_b(t + 2 * S2_AHEAD, LX);
+    stage_b(t + 1, LY, qb, std::integral_constant<int, 1>{}, P1{}, E{});
+    issue_b(t + 2 * S2_AHEAD + 1, LY);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -2226,8 +2246,8 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
               "grr_system_step2: stencil missing");
   GRR_REQUIRE(!skip || y_skip, GRR_ERR_INVALID_ARG, "grr_system_step2: skip needs y_skip");
   GRR_REQUIRE(!beta_a || u_prev, GRR_ERR_INVALID_ARG, "grr_system_step2: beta_a needs u_prev");
-  GRR_REQUIRE(W == S2_W && H % 2 == 0 && H >= 2 && F <= S2_FMAX, GRR_ERR_UNSUPPORTED,
-              "grr_system_step2: needs W = %d, even H and F <= %d (got H %d, W %d, F %d)", S2_W, S2_FMAX, H, W, F);
+  GRR_REQUIRE(W == S2_W && H % 2 == 0 && H >= 2, GRR_ERR_UNSUPPORTED,
+              "grr_system_step2: needs W = %d and even H (got H %d, W %d)", S2_W, H, W);
   GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_system_step2: plane too large");
   GRR_REQUIRE(x_out != x && x_out != b && x_out != u_prev && (!u_out || (u_out != u_prev && u_out != x && u_out != b)),
               GRR_ERR_INVALID_ARG, "grr_system_step2: outputs must not alias the inputs (rows are read ahead)");
@@ -2242,9 +2262,11 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   a.alpha_a = alpha_a; a.beta_a = beta_a; a.alpha_b = alpha_b; a.beta_b = beta_b;
   a.skip = skip; a.y = y_skip; a.out = x_out; a.u_out = u_out; a.xd_out = xd_out;
   a.G = G; a.F = F; a.H = H;
-  a.sseg = step2_seg_rows(H, (uint64_t)B * G);
+  a.ngrp = (F + S2_FMAX - 1) / S2_FMAX;   // F = 6 / 12 (v1.0 blocks): 2 / 4 groups of 3
+  a.FG = (F + a.ngrp - 1) / a.ngrp;
+  a.sseg = step2_seg_rows(H, (uint64_t)B * G * a.ngrp);
   a.nsegs = (H + a.sseg - 1) / a.sseg;
-  const uint64_t nblk = (uint64_t)B * G * a.nsegs;
+  const uint64_t nblk = (uint64_t)B * G * a.ngrp * a.nsegs;
   GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_step2: grid too large");
   a.nblk = (uint32_t)nblk;
   hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(S2_THREADS), 0,

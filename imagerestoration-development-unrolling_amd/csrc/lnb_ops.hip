@@ -591,10 +591,8 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   const bool wave_corr = __builtin_amdgcn_readfirstlane((int)__any(any_corr)) != 0;
 
   // GEMM1 of chunk c (ring slot c & 1) -> pair planes of h buffer c & 1
-  auto gemm1 = [&](int c) {
-    if (c >= nch) return;
+  auto gemm1_mma = [&](int c, f32x16 (&acc)[NB]) {
     const float* slot = ring + (c & 1) * SLOTF + lane * 4;
-    f32x16 acc[NB];
 #pragma unroll
     for (int blk = 0; blk < NB; ++blk) acc[blk] = f32x16{};
 #pragma unroll
@@ -608,6 +606,8 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
         acc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[blk][s], acc[blk], 0, 0, 0);
       }
     }
+  };
+  auto gemm1_store = [&](int c, f32x16 (&acc)[NB]) {
     float* hb = smem + (c & 1) * L6_HBUF;
 #pragma unroll
     for (int blk = 0; blk < NB; ++blk) {
@@ -620,6 +620,12 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
         *reinterpret_cast<f32x2*>(hb + (r >> 1) * L6_PP + 2 * q) = f32x2{acc[blk][2 * u], acc[blk][2 * u + 1]};
       }
     }
+  };
+  auto gemm1 = [&](int c) {
+    if (c >= nch) return;
+    f32x16 acc[NB];
+    gemm1_mma(c, acc);
+    gemm1_store(c, acc);
   };
 
   // gate phase mapping: this wave's pairs 2 wave, 2 wave + 1; lane = (output column, row half)
@@ -642,7 +648,9 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int jj = L6_NP * c + 2 * wave + p;
-      const bool lane_ok = jj < hid && gx < W;
+      // rows this lane stores (0 outside the hidden channels / image): the row test below is then
+      // one compare + select per output (no exec-masked block in the middle of the gate)
+      const uint32_t nst = (jj < hid && gx < W) ? (uint32_t)max(nrow, 0) : 0u;
       const uint32_t off0 = (uint32_t)(jj * HW + (y0 + r0) * W + gx) * 4u;
       const float* hp = hbuf + (2 * wave + p) * L6_PP + 2 * col;
       f32x2 win[3][3];                          // rows (i mod 3) x halo columns col .. col + 2
@@ -662,8 +670,8 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
               v += tp[p][2 * (ay * 3 + ax) + 1] * hv[1];
             }
           const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __expf(-m));   // sigmoid(m) m v
-          const bool ok = lane_ok && i - 2 < nrow;
-          const uint32_t off = ok ? off0 + (uint32_t)((i - 2) * W) * 4u : 0x80000000u;
+          const uint32_t msk = 0u - (uint32_t)((uint32_t)(i - 2) < nst);
+          const uint32_t off = ((off0 + (uint32_t)((i - 2) * W) * 4u) & msk) | (0x80000000u & ~msk);
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, off, 0, 0);
         }
       }

@@ -317,9 +317,9 @@ STEP2 = os.environ.get("GRR_STEP2", "1") != "0"
 
 
 def step2_supported(x: Tensor, n_graphs: int) -> bool:
-    """grr_system_step2's shape limits: W = 256, even H, F <= 3."""
+    """grr_system_step2's shape limits: W = 256, even H (F > 3: channel groups of <= 3)."""
     b, c, h, w = x.shape
-    return w == 256 and h % 2 == 0 and c % n_graphs == 0 and c // n_graphs <= 3
+    return w == 256 and h % 2 == 0 and c % n_graphs == 0
 
 
 def step2_bytes(b, c, g, h, w, has_u_prev, has_u_out, has_pool, has_skip):
@@ -329,7 +329,8 @@ def step2_bytes(b, c, g, h, w, has_u_prev, has_u_out, has_pool, has_skip):
     L2 hits by construction)."""
     f = c * (2 + int(has_u_prev) + 1 + int(has_u_out) + int(has_skip))    # x, b, u_prev, x_out, u_out, y
     f += (c // 4) * (1 + int(has_pool))                                   # D x_k in, D x_out
-    f += 6 * g + (6 * g) // 4                                             # full + half-level weights
+    ngrp = -(-(c // g) // 3)                                              # workgroups per graph (F > 3)
+    f += (6 * g + (6 * g) // 4) * ngrp                                    # full + half-level weights, per group
     return 4 * b * h * w * f
 
 

@@ -6,8 +6,8 @@ The fused kernel computes the same values with the same per-row arithmetic; the 
 below (2e-6 relative to the largest output) covers fp32 contraction differences between the
 two code paths.  Shapes cover one row segment per (b, graph) (B*G >= 512 workgroups) and the
 segmented grid of small batches (64-row segments, the stage-A lead of 9 rows crossing the
-segment boundary), the top / bottom replicate clamps of the in-kernel rings at short H, the
-first pair (no u_prev / beta_a) and the last pair (skip, no u / D x outputs).
+segment boundary), the top / bottom replicate clamps of the in-kernel rings at short H, F > 3 as
+channel groups, the first pair (no u_prev / beta_a) and the last pair (skip, no u / D x outputs).
 """
 import pytest
 import torch
@@ -78,6 +78,9 @@ CASES = [
     dict(B=2, G=3, F=2, H=130),     # H not a multiple of the segment, F = 2
     dict(B=1, G=4, F=1, H=64),
     dict(B=2, G=2, F=3, H=8),       # half rows fewer than the half-level pipeline's fill
+    dict(B=2, G=2, F=6, H=64),      # v1.0 first filter block: two channel groups of 3
+    dict(B=1, G=2, F=12, H=32),     # four groups of 3
+    dict(B=1, G=3, F=5, H=32),      # uneven groups (3 + 2)
 ]
 
 
