@@ -564,6 +564,150 @@ static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, in
   return launch_status(name);
 }
 
+// ---------------------------------------------------------------------------
+// The same fp32-accurate 1x1 convolution for deep inputs (K > 128: the training reverse's
+// W1^T gh (K = 2 hid), the v1.0 widths): a wave can no longer hold its pixels' K column, so the
+// loop order flips.  A workgroup = 8 waves x 32 pixels x one M tile of 32 TM rows; the
+// accumulators of all TM row tiles stay in registers while K streams by 16-deep k-steps: each
+// wave loads its pixels' 16 x rows two steps ahead (rows 16 s + 8 hf + j, 128-B coalesced per
+// half-wave), splits them in registers, and multiplies them with the row tiles' split W
+// fragments (x3_pack_kernel's images, [32-row group][k-step][term]), which arrive by LDS-DMA in
+// a 2-slot ring of X3K_KC k-steps shared by the 8 waves.
+// ---------------------------------------------------------------------------
+constexpr int X3K_KC = 4;   // k-steps per ring slot
+
+struct X3KArgs {
+  const float* x;          // [B, K, P]
+  const uint16_t* frag;    // x3_pack_kernel layout, X3_NT = 1: [32-row group][x3_chunk_bytes(KS) / 2]
+  float* out;              // [B, M, P]
+  int64_t P;
+  int K, M, KS, ngroups, nmt, tiles;
+  int64_t CB;              // bytes per 32-row group image
+  uint32_t nblk;
+};
+
+template <int TM>
+__global__ __launch_bounds__(64 * X3_WV) void gemm_x3k_kernel(X3KArgs a) {
+  static_assert(X3_NT == 1, "gemm_x3k_kernel reads the one-tile pack layout");
+  extern __shared__ __attribute__((aligned(16))) float x3_lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int mt = (int)(lb % (uint32_t)a.nmt);   // the M tiles of one pixel tile are neighbours (shared x rows)
+  lb /= (uint32_t)a.nmt;
+  const int tile = (int)(lb % (uint32_t)a.tiles), b = (int)(lb / (uint32_t)a.tiles);
+  const int64_t P = a.P;
+  const int K = a.K, M = a.M, KS = a.KS, r = lane & 31, hf = lane >> 5;
+  const int64_t p = (int64_t)tile * X3_PX + wave * 32 + r;
+  const bool pin = p < P;
+  const int64_t pc = pin ? p : P - 1;
+  const char* fragb = reinterpret_cast<const char*>(a.frag);
+  constexpr int SLOT = X3K_KC * TM * 3 * 256;    // floats per ring slot (1 KB images)
+  const int nch = (KS + X3K_KC - 1) / X3K_KC;
+
+  // chunk c -> slot c & 1: images [s][t][q] for k-steps c KC .. c KC + KC - 1, row tiles t < TM
+  auto issue = [&](int c) {
+    float* slot = x3_lds + (c & 1) * SLOT;
+    for (int i = wave; i < X3K_KC * TM * 3; i += X3_WV) {
+      const int q = i % 3, t = (i / 3) % TM, s = c * X3K_KC + i / (3 * TM);
+      int g = mt * TM + t;
+      if (g >= a.ngroups) g = a.ngroups - 1;     // rows past M: any valid image (never stored)
+      const int ss = s < KS ? s : KS - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(fragb + g * a.CB + (int64_t)(ss * 3 + q) * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(slot + i * 256), 16, 0, 0);
+    }
+  };
+
+  const float* xb = a.x + (int64_t)b * K * P + pc;
+  auto load = [&](int s, float (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * hf + j;
+      v[j] = k < K ? xb[(int64_t)(k < K ? k : 0) * P] : 0.f;
+    }
+  };
+
+  f32x16 acc[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) acc[t] = f32x16{};
+
+  issue(0);
+  float x0[8], x1[8];
+  load(0, x0);
+  load(1 < KS ? 1 : 0, x1);
+  for (int c = 0; c < nch; ++c) {
+    // this wave's DMAs of chunk c landed: only the x loads of the next two k-steps (16 dword loads,
+    // issued after the DMAs) may still be in flight; then every wave's (one barrier per chunk: a
+    // wave at it has finished reading the slot the next issue() overwrites)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + 1 < nch) issue(c + 1);               // slot (c + 1) & 1 was last read in chunk c - 1
+    const float* slot = x3_lds + (c & 1) * SLOT;
+#pragma unroll
+    for (int si = 0; si < X3K_KC; ++si) {
+      const int s = c * X3K_KC + si;
+      if (s >= KS) break;
+      float* cur = (si & 1) ? x1 : x0;
+      bf16x8 bq0, bq1, bq2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint32_t h0, h1, h2;
+        split3(cur[j], h0, h1, h2);
+        bq0[j] = __builtin_bit_cast(__bf16, (uint16_t)h0);
+        bq1[j] = __builtin_bit_cast(__bf16, (uint16_t)h1);
+        bq2[j] = __builtin_bit_cast(__bf16, (uint16_t)h2);
+      }
+      if (si & 1) load(s + 2 < KS ? s + 2 : KS - 1, x1);
+      else load(s + 2 < KS ? s + 2 : KS - 1, x0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const float* im = slot + (si * TM * 3 + t * 3) * 256 + lane * 4;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(im);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(im + 256);
+        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(im + 512);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq1, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, bq0, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq2, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq0, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq1, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq0, acc[t], 0, 0, 0);
+      }
+    }
+  }
+  float* const obase = a.out + (int64_t)b * M * P;
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = (mt * TM + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+      if (m < M && pin) obase[(int64_t)m * P + p] = acc[t][i];
+    }
+}
+
+static grr_status launch_x3k(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
+                             hipStream_t s, const char* name) {
+  X3KArgs a{};
+  a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M;
+  a.KS = (K + 15) / 16;
+  a.ngroups = (M + 31) / 32;
+  a.CB = x3_chunk_bytes(a.KS);
+  a.tiles = (int)((P + X3_PX - 1) / X3_PX);
+  // row tiles per workgroup: all of M up to 128 rows, else 4 (128-row M tiles)
+  const int TM = a.ngroups >= 4 ? 4 : a.ngroups;
+  a.nmt = (a.ngroups + TM - 1) / TM;
+  const uint64_t n = (uint64_t)B * a.tiles * a.nmt;
+  GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
+  a.nblk = (uint32_t)n;
+  const size_t lds = 2 * (size_t)X3K_KC * TM * 3 * 1024;
+  switch (TM) {
+    case 1: hipLaunchKernelGGL((gemm_x3k_kernel<1>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_x3k_kernel<2>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm_x3k_kernel<3>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    default: hipLaunchKernelGGL((gemm_x3k_kernel<4>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+  }
+  return launch_status(name);
+}
+
 // out[b, g Cin + c] = img[b, c]: one thread per 4 consecutive pixels of one (b, c) plane reads
 // them once (16-byte load) and writes the G copies (16-byte stores); store-bandwidth bound.
 __global__ void repeat_graphs_kernel(const float* __restrict__ img, float* __restrict__ out, int Cin, int G,
@@ -603,7 +747,7 @@ grr_status grr_conv1x1(const float* x, const float* wt, float* out, int B, int K
 }
 
 int64_t grr_conv1x1_workspace_bytes(int K, int M) {
-  if (K < 1 || K > 128 || M < 1) return 0;
+  if (K < 1 || K > 4096 || M < 1) return 0;
   const int KS = (K + 15) / 16, nch = (M + X3_MCH - 1) / X3_MCH;
   return (int64_t)nch * x3_chunk_bytes(KS);
 }
@@ -614,7 +758,7 @@ grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* wor
   GRR_REQUIRE(x && wt && out && workspace && B > 0 && K > 0 && M > 0 && P > 0, GRR_ERR_INVALID_ARG,
               "grr_conv1x1_ws: bad args");
   GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_conv1x1_ws: out aliases x");
-  GRR_REQUIRE(K <= 128, GRR_ERR_UNSUPPORTED, "grr_conv1x1_ws: K=%d > 128", K);
+  GRR_REQUIRE(K <= 4096, GRR_ERR_UNSUPPORTED, "grr_conv1x1_ws: K=%d > 4096", K);
   GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_conv1x1_ws: workspace not 256-B aligned");
   GRR_REQUIRE(P * 16 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_conv1x1_ws: P too large");
   hipStream_t s = (hipStream_t)stream;
@@ -625,6 +769,7 @@ grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* wor
                      wt, nullptr, frag, M, K, KS, nch);
   grr_status st = launch_status("grr_conv1x1_ws/pack");
   if (st != GRR_OK) return st;
+  if (K > 128) return launch_x3k(x, frag, out, B, K, M, P, s, "grr_conv1x1_ws");
   return launch_x3<false>(x, frag, out, B, K, M, P, s, "grr_conv1x1_ws");
 }
 

@@ -89,6 +89,10 @@ def set_timer(timer):
     _TIMER = timer
 
 
+# GRR_TIMER_SHAPES=1: the instrumented loops time the GEMM-like launches per operand shape
+TIMER_SHAPES = os.environ.get("GRR_TIMER_SHAPES", "0") == "1"
+
+
 def _launch(kind: str, nbytes: int, name: str, *args, flops: int = 0):
     if _TIMER is None:
         call(name, *args)
@@ -478,13 +482,14 @@ def conv1x1(x: Tensor, weight: Tensor) -> Tensor:
     if weight.shape[1] != k:
         raise ValueError(f"conv1x1: weight {tuple(weight.shape)} vs input channels {k}")
     out = torch.empty((b, m, h, w), dtype=torch.float32, device=dev)
+    kind = f"conv1x1[{k}->{m},{b}x{h}x{w}]" if TIMER_SHAPES else "conv1x1"
     ws_bytes = _native.load().grr_conv1x1_workspace_bytes(k, m)
-    if ws_bytes > 0:   # K <= 128: split-bf16 MFMA path (fp32-accurate)
+    if ws_bytes > 0:   # split-bf16 MFMA path (fp32-accurate); K > 128 streams K (gemm_x3k_kernel)
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)  # allocator: 512-B aligned
-        _launch("conv1x1", 4 * b * h * w * (k + m), "grr_conv1x1_ws", x.data_ptr(), weight.data_ptr(),
+        _launch(kind, 4 * b * h * w * (k + m), "grr_conv1x1_ws", x.data_ptr(), weight.data_ptr(),
                 out.data_ptr(), ws.data_ptr(), b, k, m, h * w, _stream(dev))
     else:
-        _launch("conv1x1", 4 * b * h * w * (k + m), "grr_conv1x1", x.data_ptr(), weight.data_ptr(),
+        _launch(kind, 4 * b * h * w * (k + m), "grr_conv1x1", x.data_ptr(), weight.data_ptr(),
                 out.data_ptr(), b, k, m, h * w, _stream(dev))
     return out
 
@@ -499,6 +504,24 @@ def conv2x2s2(x: Tensor, weight: Tensor) -> Tensor:
     out = torch.empty((b, m, h // 2, w // 2), dtype=torch.float32, device=dev)
     _launch("conv2x2s2", 4 * b * (h * w * k + (h // 2) * (w // 2) * m), "grr_conv2x2s2", x.data_ptr(),
             weight.data_ptr(), out.data_ptr(), b, k, m, h, w, _stream(dev))
+    return out
+
+
+def wgrad(a: Tensor, bop: Tensor) -> Tensor:
+    """Weight gradient out[m, k] = sum_b sum_p a[b, m, p] bop[b, k, p] (grr_wgrad): a [B, M, ...],
+    bop [B, K, ...] with the same trailing pixel extent.  The reverse of a 1x1 conv / LNB GEMM's
+    weight (REF:556-612 under autograd) without a library GEMM: fp32 MFMA, fixed summation order."""
+    dev = _check("wgrad", a, bop)
+    b, m = a.shape[:2]
+    k = bop.shape[1]
+    p = a.numel() // (b * m)
+    if bop.shape[0] != b or bop.numel() != b * k * p:
+        raise ValueError(f"wgrad: operands {tuple(a.shape)} and {tuple(bop.shape)} disagree")
+    out = torch.empty((m, k), dtype=torch.float32, device=dev)
+    ws = torch.empty((_native.load().grr_wgrad_workspace_bytes(b, m, k, p) + 3) // 4, dtype=torch.float32,
+                     device=dev)
+    _launch(f"wgrad[{m}x{k},{b}x{p}]" if TIMER_SHAPES else "wgrad", 4 * b * p * (m + k), "grr_wgrad", a.data_ptr(), bop.data_ptr(), out.data_ptr(), ws.data_ptr(),
+            b, m, k, p, _stream(dev), flops=2 * b * p * m * k)
     return out
 
 

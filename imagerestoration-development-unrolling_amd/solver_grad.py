@@ -305,7 +305,7 @@ def mixture_solve(mod, y: Tensor, f0: Tensor, f1: Tensor) -> Tensor:
 
 # ---- feature convolutions ----------------------------------------------------
 # nn.Conv2d(K, M, 1, bias=False): forward and data gradient on the HIP GEMM; the weight gradient (a
-# reduction over B*H*W) is one plain library GEMM (rocBLAS via torch.matmul)
+# reduction over B*H*W) is grr_wgrad (fp32 MFMA partial tiles per pixel chunk, added in a fixed order)
 def _conv1x1_fwd(consts, x: Tensor, weight: Tensor):
     return [K.conv1x1(x.contiguous(), weight.contiguous())], []
 
@@ -316,7 +316,7 @@ def _conv1x1_bwd(consts, inputs, outs, saved, gouts, needs):
     m, k = weight.shape[:2]
     gx = K.conv1x1(g, weight.reshape(m, k).t().contiguous().view(k, m, 1, 1)) if needs[0] else None
     b = x.shape[0]
-    gw = torch.matmul(g.reshape(b, m, -1), x.reshape(b, k, -1).transpose(1, 2)).sum(0)
+    gw = K.wgrad(g, x.contiguous())
     return gx, gw.view_as(weight)
 
 
@@ -328,7 +328,7 @@ CONV1X1 = OpaqueFunction("conv1x1_train", 1, _conv1x1_fwd, _conv1x1_bwd, _conv1x
 
 
 # nn.Conv2d(K, M, 2, stride=2, bias=False) (REF:593-602): HIP forward and data gradient, weight gradient
-# as one library GEMM over the 2x2 patches
+# on grr_wgrad over the 2x2 patches
 def _conv2x2_fwd(consts, x: Tensor, weight: Tensor):
     return [K.conv2x2s2(x.contiguous(), weight.contiguous())], []
 
@@ -345,8 +345,9 @@ def _conv2x2_bwd(consts, inputs, outs, saved, gouts, needs):
             gx = K.conv2x2s2_bwd_data_gemm(g, weight.contiguous(), h, w)
         else:
             gx = K.conv2x2s2_bwd_data(g, weight.contiguous(), h, w)
-    patches = x.reshape(b, k, h // 2, 2, w // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(b, -1, k * 4)
-    gw = torch.matmul(g.reshape(b, m, -1), patches).sum(0)
+    # patch rows in the weight's (k, dy, dx) order: [B, 4K, H/2 * W/2]
+    patches = x.reshape(b, k, h // 2, 2, w // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(b, k * 4, -1)
+    gw = K.wgrad(g, patches)
     return gx, gw.view_as(weight)
 
 
@@ -691,7 +692,7 @@ def _lnb_bwd(consts, inputs, outs, saved, gouts, needs):
     s1 = skip[1:2].contiguous()
     # gw2 = s1 gout gate^T; gq = W2^T gout: the gate reverse takes s1 and returns
     # <gout, W2 gate> = <gq, gate> for the skip weight (no recomputed W2 gate)
-    gw2 = torch.matmul(gout.reshape(b, c, -1), gate.reshape(b, hid, -1).transpose(1, 2)).sum(0) * s1
+    gw2 = K.wgrad(gout.contiguous(), gate.contiguous()) * s1
     del gate
     gq = K.conv1x1(gout, W2.t().contiguous().view(hid, c, 1, 1))
     gwdw = torch.zeros_like(Wdw)
@@ -703,7 +704,7 @@ def _lnb_bwd(consts, inputs, outs, saved, gouts, needs):
         del hp, gq
         gh = K.dwconv3_bwd(ghp, hh, Wdw, gwdw)
         del ghp, hh
-    gw1 = torch.matmul(gh.reshape(b, hid2, -1), n.reshape(b, c, -1).transpose(1, 2)).sum(0)
+    gw1 = K.wgrad(gh.contiguous(), n.contiguous())
     gn = K.conv1x1(gh, W1.t().contiguous().view(c, hid2, 1, 1))
     del gh, n
     gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout

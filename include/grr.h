@@ -232,7 +232,8 @@ grr_status grr_conv1x1(const float* x, const float* wt, float* out, int B, int K
                        void* stream);
 
 /* The same 1x1 convolution on bf16 MFMA with an exact 3-term split of both fp32 operands
- * (six products, fp32-accurate; see DESIGN.md "x3 GEMM").  K <= 128.  workspace: device
+ * (six products, fp32-accurate; see DESIGN.md "x3 GEMM").  K <= 4096 (K > 128: the K-streaming
+ * kernel).  workspace: device
  * memory of grr_conv1x1_workspace_bytes(K, M) bytes, 256-B aligned (the split weights). */
 int64_t grr_conv1x1_workspace_bytes(int K, int M);
 grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* workspace, int B, int K, int M,
@@ -241,6 +242,15 @@ grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* wor
 /* 2x2 stride-2 convolution, no bias (REF:593-602): x [B,K,H,W], wt [M,K,2,2] -> out [B,M,H/2,W/2]. */
 grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int K, int M, int H, int W,
                          void* stream);
+
+/* Weight gradient of a 1x1 / 2x2-s2 convolution or an LNB GEMM (the reverse of REF:556-612,
+ * REF13:564-575 under autograd): out[m,k] = sum_b sum_p a[b,m,p] * bop[b,k,p], a [B,M,P], bop [B,K,P],
+ * out [M,K]; fp32 MFMA, partial tiles per pixel chunk added in a fixed order (deterministic, no
+ * atomics).  Replaces the library GEMM torch.matmul(g, x^T).sum(0) of the reference's autograd.
+ * workspace: grr_wgrad_workspace_bytes(B, M, K, P) bytes of device memory; a, bop 16-B aligned. */
+int64_t grr_wgrad_workspace_bytes(int B, int M, int K, int64_t P);
+grr_status grr_wgrad(const float* a, const float* bop, float* out, void* workspace, int B, int M, int K, int64_t P,
+                     void* stream);
 
 /* LocalNonLinearBlock forward, nsubnets = 1 (REF:911-964; REF13:564-575):
  *   n   = gamma_c * x / sqrt(var_c(x) + 1e-5)          (CustomLayerNorm, unbiased var over C)

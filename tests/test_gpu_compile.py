@@ -110,8 +110,12 @@ def test_compiled_training_matches_eager(irdu):
         losses, grads = _train_two_steps(make(), compiled=True)
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) <= 1e-6 * abs(b), (losses, ref_losses)
-    for step in range(2):
+    # step 0: same weights, so only fp32 summation order differs (float atomics in the reverse
+    # reductions, Inductor's fused encoder/decoder ops): 1e-5.  Step 1 starts from weights after one
+    # Adam step, whose first update is ~lr * sign(g): an entry with |g| near eps takes an update that
+    # depends on that rounding noise, so step 1 is held to the training tolerance of DESIGN.md §5.
+    for step, tol in ((0, 1e-5), (1, 2e-4)):
         for k, ref in ref_grads[step].items():
             got = grads[step][k]
             err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
-            assert err <= 1e-5, (step, k, err)
+            assert err <= tol, (step, k, err)

@@ -192,14 +192,39 @@ def test_gtv_prox_rhs_half(irdu, variant, shape):
 
 # ---------------------------------------------------------------------------
 # feature CNN
-# K <= 128: split-bf16 MFMA path (grr_conv1x1_ws); K = 160: fp32 MFMA path (grr_conv1x1)
+# K <= 128: split-bf16 MFMA path with the K column in registers; K > 128: the K-streaming split-bf16
+# kernel (1 to 4 row tiles per workgroup, M tiles, odd K); the fp32 MFMA kernel (grr_conv1x1) directly
 @pytest.mark.parametrize("bkmp", [(2, 12, 24, (8, 8)), (1, 96, 192, (33, 40)), (2, 7, 3, (5, 6)),
-                                  (1, 96, 3, (16, 24)), (1, 160, 40, (9, 10))])
+                                  (1, 96, 3, (16, 24)), (1, 160, 40, (9, 10)), (2, 512, 96, (16, 20)),
+                                  (1, 200, 130, (7, 9)), (1, 384, 300, (12, 12)), (1, 129, 33, (5, 66)),
+                                  (1, 256, 96, (3, 5))])
 def test_conv1x1(irdu, bkmp):
     b, k, m, (h, w) = bkmp
     x = rand(b, k, h, w, seed=11)
     wt = rand(m, k, 1, 1, seed=12) * 0.2
     assert_close(irdu.kernels.conv1x1(x.to(DEV), wt.to(DEV)), torch.nn.functional.conv2d(x, wt), 1e-5)
+
+
+def test_conv1x1_fp32_kernel(irdu):
+    """grr_conv1x1 (fp32 MFMA, the ABI's plain entry point) at a deep K."""
+    x = rand(1, 160, 9, 10, seed=11)
+    wt = rand(40, 160, 1, 1, seed=12) * 0.2
+    xd, wd = x.to(DEV), wt.to(DEV).contiguous()
+    out = torch.empty(1, 40, 9, 10, device=DEV)
+    from irdu_amd._native import call
+    call("grr_conv1x1", xd.data_ptr(), wd.data_ptr(), out.data_ptr(), 1, 160, 40, 90,
+         torch.cuda.current_stream().cuda_stream)
+    assert_close(out, torch.nn.functional.conv2d(x, wt), 1e-5)
+
+
+def test_x3_gemm_deep_k_is_fp32_accurate(irdu):
+    """The K-streaming split-bf16 GEMM (K = 512, the LNB reverse's W1^T gh) against float64."""
+    x = rand(2, 512, 20, 24, seed=34, scale=3.0, offset=0.5)
+    wt = rand(96, 512, 1, 1, seed=35) * 0.1
+    ref64 = torch.nn.functional.conv2d(x.double(), wt.double())
+    err32 = rel_err(torch.nn.functional.conv2d(x, wt), ref64)
+    err = rel_err(irdu.kernels.conv1x1(x.to(DEV), wt.to(DEV)), ref64)
+    assert err <= 4 * err32 + 1e-7, (err, err32)
 
 
 def test_x3_gemm_is_fp32_accurate(irdu):
