@@ -37,9 +37,10 @@ EDGE_DELTA = ((-1, 0), (0, -1), (0, 1), (1, 0))  # REF:42-53 (up, left, right, d
 # Inference: the half-resolution feature branch (2x2 conv, its LocalNonLinearBlocks, 1x1) runs on
 # a second HIP stream beside the full-resolution branch (GRR_FEATURE_STREAMS=0: one stream)
 FEATURE_STREAMS = os.environ.get("GRR_FEATURE_STREAMS", "1") == "1"
-# Training: the same split for the forward and (by autograd's stream replay) the reverse of the branch;
-# off by default (one of two round-2 runs of the first version stalled)
-FEATURE_STREAMS_TRAIN = os.environ.get("GRR_FEATURE_STREAMS_TRAIN", "0") == "1"
+# Training: the same split for the forward and (by autograd's stream replay) the reverse of the branch
+# (GRR_FEATURE_STREAMS_TRAIN=0: one stream).  Its earlier stalls came from library stream-K weight-gradient
+# GEMMs co-resident on both streams; those reductions now run on grr_wgrad
+FEATURE_STREAMS_TRAIN = os.environ.get("GRR_FEATURE_STREAMS_TRAIN", "1") == "1"
 _SIDE_STREAMS = {}
 
 

@@ -31,11 +31,11 @@ for (m, k, hw) in [(512, 96, 256), (96, 256, 256), (192, 96, 256), (512, 96, 128
     tl = t(lambda: torch.matmul(a.reshape(B, m, -1), x.reshape(B, k, -1).transpose(1, 2)).sum(0))
     gb = 4 * B * hw * hw * (m + k) / 1e9
     tf = 2 * B * hw * hw * m * k / 1e12
-    print(f"wgrad {m}x{k} {B}x{hw}^2: grr {tw:.3f} ms ({gb / tw:.0f} GB/s, {tf / tw * 1e3:.0f} TF/s)  lib {tl:.3f} ms", flush=True)
+    print(f"wgrad {m}x{k} {B}x{hw}^2: grr {tw:.3f} ms ({gb / tw:.2f} TB/s, {tf / tw * 1e3:.0f} TF/s)  lib {tl:.3f} ms", flush=True)
 for (k, m, hw) in [(96, 512, 256), (96, 256, 256), (512, 96, 256), (256, 96, 256), (192, 96, 256), (96, 192, 256)]:
     x = torch.randn(B, k, hw, hw, device=dev)
     w = torch.randn(m, k, 1, 1, device=dev)
     tc = t(lambda: K.conv1x1(x, w))
     gb = 4 * B * hw * hw * (m + k) / 1e9
     tf = 2 * B * hw * hw * m * k / 1e12
-    print(f"conv1x1 {k}->{m} {B}x{hw}^2: {tc:.3f} ms ({gb / tc:.0f} GB/s, {tf / tc * 1e3:.0f} TF/s)", flush=True)
+    print(f"conv1x1 {k}->{m} {B}x{hw}^2: {tc:.3f} ms ({gb / tc:.2f} TB/s, {tf / tc * 1e3:.0f} TF/s)", flush=True)
