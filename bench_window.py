@@ -83,8 +83,9 @@ def main():
                       "per_gpu_batch": b},
            "graph_solver": {"ms_per_step": round(solver_ms, 3),
                             "mpix_per_s": round(b * hw * hw / (solver_ms * 1e-3) / 1e6, 2),
-                            "note": "edge weights + rhs / prox / CG passes + graph mix on HIP; the feature CNN "
-                                    "(Restormer-style FFBlocks) and DC estimator run on stock PyTorch-ROCm"},
+                            "note": "edge weights + rhs / prox / CG passes + graph mix on HIP; the feature CNN's "
+                                    "FFBlocks on grr_ffn_forward (inference), its 3x3 convs and the DC estimator "
+                                    "on stock PyTorch-ROCm"},
            "roofline": {"bound": "hbm", "kernel": "grr_win_solver (win_solver_kernel, CG-step / rhs passes)",
                         "achieved": round(step["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": round(step["gbps"] / HBM_PEAK_GBPS, 4),

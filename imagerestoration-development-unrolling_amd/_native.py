@@ -63,6 +63,8 @@ SIGNATURES = {
     "grr_conv1x1_workspace_bytes": [I, I],
     "grr_conv1x1_ws": [P, P, P, P, I, I, I, L, P],
     "grr_conv2x2s2": [P, P, P, I, I, I, I, I, P],
+    "grr_ffn_workspace_bytes": [I, I, I, I, I],
+    "grr_ffn_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_wgrad_workspace_bytes": [I, I, I, L],
     "grr_wgrad": [P, P, P, P, I, I, I, L, P],
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
@@ -121,7 +123,8 @@ SIGNATURES = {
     "grr_win_bwd_mix": [P, P, P, P, P, I, I, I, I, I, P],
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
-             "grr_conv1x1_workspace_bytes": c_int64, "grr_wgrad_workspace_bytes": c_int64}
+             "grr_conv1x1_workspace_bytes": c_int64, "grr_wgrad_workspace_bytes": c_int64,
+             "grr_ffn_workspace_bytes": c_int64}
 
 _lib = None
 

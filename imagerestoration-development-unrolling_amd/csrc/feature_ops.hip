@@ -274,9 +274,12 @@ __global__ __launch_bounds__(64 * LN_G) void ln_stats_kernel(const float* __rest
   }
 }
 
-// depthwise 3x3 (replicate pad) on the 2*hid GEMM output, then the gate
-// g = sigmoid(mask) * mask * value  (REF:934-947).  One workgroup = (b, j, 32x32 tile).
+// depthwise 3x3 on the 2*hid GEMM output, then the gate.  One workgroup = (b, j, 32x32 tile).
+//   FFN = false: LocalNonLinearBlock, replicate padding, g = sigmoid(mask) * mask * value (REF:934-947)
+//   FFN = true:  the window models' FeedForward (REF7:29-48), zero padding (Conv2d padding=1),
+//                g = gelu(x1) * x2 with the exact erf gelu of nn.functional.gelu
 constexpr int DT = 32, DS = DT + 2, DA = DS * DS;
+template <bool FFN>
 __global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ h, const float* __restrict__ wdw,
                                                       float* __restrict__ gout, int hid, int H, int W,
                                                       int tiles_x, int tiles_y, uint32_t nblk) {
@@ -293,9 +296,11 @@ __global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ 
   const float* vp = h + ((int64_t)b * 2 * hid + hid + j) * HW;
   for (int i = threadIdx.x; i < DA; i += 256) {
     const int ry = i / DS, rx = i - ry * DS;
-    const int64_t o = (int64_t)clampi(y0 - 1 + ry, 0, H - 1) * W + clampi(x0 - 1 + rx, 0, W - 1);
-    Ms[i] = mp[o];
-    Vs[i] = vp[o];
+    const int yy = y0 - 1 + ry, xx = x0 - 1 + rx;
+    const int64_t o = (int64_t)clampi(yy, 0, H - 1) * W + clampi(xx, 0, W - 1);
+    const bool in = !FFN || (yy >= 0 && yy < H && xx >= 0 && xx < W);
+    Ms[i] = in ? mp[o] : 0.f;
+    Vs[i] = in ? vp[o] : 0.f;
   }
   float km[9], kv[9];
 #pragma unroll
@@ -318,8 +323,12 @@ __global__ __launch_bounds__(256) void dw_gate_kernel(const float* __restrict__ 
         m += km[ay * 3 + ax] * Ms[li];
         v += kv[ay * 3 + ax] * Vs[li];
       }
-    const float sg = 1.0f / (1.0f + expf(-m));
-    gp[(int64_t)gy * W + gx] = (sg * m) * v;
+    if constexpr (FFN) {
+      gp[(int64_t)gy * W + gx] = (m * 0.5f * (1.0f + erff(m * 0.70710678118654752440f))) * v;
+    } else {
+      const float sg = 1.0f / (1.0f + expf(-m));
+      gp[(int64_t)gy * W + gx] = (sg * m) * v;
+    }
   }
 }
 
@@ -357,6 +366,22 @@ __device__ __forceinline__ void split3(float v, uint32_t& h0, uint32_t& h1, uint
   h1 = bf16_rne(r1);
   const float r2 = r1 - bf16_val(h1);
   h2 = bf16_rne(r2);
+}
+
+// the same exact split of 8 values with the hardware RNE conversion (v_cvt_pk_bf16_f32: two values per
+// instruction; the residuals come back through a shift / mask): about half the vector instructions of
+// the integer-rounding split3 above, the same bits for finite values
+__device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8& t0, bf16x8& t1, bf16x8& t2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h0 = (__bf16)v[j];
+    const float r1 = v[j] - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    const float r2 = r1 - (float)h1;
+    t0[j] = h0;
+    t1[j] = h1;
+    t2[j] = (__bf16)r2;
+  }
 }
 
 #ifndef GRR_X3_TILES
@@ -441,13 +466,16 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3_kernel(X3Args a) {
 
   // this lane's K column: k = 16 s + 8 hf + j
   float xv[KS][8];
-  const float* xb = a.x + (int64_t)b * K * P + pc;
+  // wave-uniform slab base + 32-bit lane offsets (K P < 2^30, checked on the host); rows past K load
+  // row K - 1 and are zeroed by a select (no per-load branches)
+  const float* xs = a.x + (int64_t)b * K * P;
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 16 * s + 8 * hf + j;
-      xv[s][j] = k < K ? xb[(int64_t)k * P] : 0.f;
+      const float v = xs[(uint32_t)(k < K ? k : K - 1) * (uint32_t)P + (uint32_t)pc];
+      xv[s][j] = k < K ? v : 0.f;
     }
   float rstd = 1.f;
   if constexpr (LN) {                          // CustomLayerNorm statistics (REF:916-922)
@@ -472,14 +500,7 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3_kernel(X3Args a) {
   bf16x8 bq[KS][3];
 #pragma unroll
   for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint32_t h0, h1, h2;
-      split3(xv[s][j], h0, h1, h2);
-      bq[s][0][j] = __builtin_bit_cast(__bf16, (uint16_t)h0);
-      bq[s][1][j] = __builtin_bit_cast(__bf16, (uint16_t)h1);
-      bq[s][2][j] = __builtin_bit_cast(__bf16, (uint16_t)h2);
-    }
+    split3x8(xv[s], bq[s][0], bq[s][1], bq[s][2]);
 
   float* const obase = a.out + (int64_t)b * M * P;
   // full tile: every lane's pixel in range -> stores through a uniform row base + 32-bit offset
@@ -545,6 +566,7 @@ template <bool LN>
 static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
                             hipStream_t s, const char* name) {
   GRR_REQUIRE(K >= 1 && K <= 128, GRR_ERR_UNSUPPORTED, "%s: K=%d outside [1, 128]", name, K);
+  GRR_REQUIRE((int64_t)K * P < (1ll << 30), GRR_ERR_UNSUPPORTED, "%s: K*P too large for 32-bit offsets", name);
   X3Args a{};
   a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M;
   a.nch = (M + X3_MCH - 1) / X3_MCH;
@@ -572,12 +594,16 @@ static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, in
 // wave loads its pixels' 16 x rows two steps ahead (rows 16 s + 8 hf + j, 128-B coalesced per
 // half-wave), splits them in registers, and multiplies them with the row tiles' split W
 // fragments (x3_pack_kernel's images, [32-row group][k-step][term]), which arrive by LDS-DMA in
-// a 2-slot ring of X3K_KC k-steps shared by the 8 waves.
+// a 3-slot ring of X3K_KC k-steps shared by the 8 waves, two chunks ahead.
 // ---------------------------------------------------------------------------
-constexpr int X3K_KC = 4;   // k-steps per ring slot
+constexpr int X3K_KC = 2;   // k-steps per ring slot (3 slots: 72 KB at 4 row tiles, two workgroups per CU)
 
+enum { X3K_STORE = 0, X3K_LN = 1, X3K_SKIP = 2 };
 struct X3KArgs {
   const float* x;          // [B, K, P]
+  const float* sd;         // X3K_LN: [B, P] per-pixel scale 1 / sqrt(var + eps) (ln_stats_kernel)
+  const float* res;        // X3K_SKIP: [B, M, P]
+  const float* skip;       // X3K_SKIP: [2], out = skip0 res + skip1 acc
   const uint16_t* frag;    // x3_pack_kernel layout, X3_NT = 1: [32-row group][x3_chunk_bytes(KS) / 2]
   float* out;              // [B, M, P]
   int64_t P;
@@ -586,8 +612,8 @@ struct X3KArgs {
   uint32_t nblk;
 };
 
-template <int TM>
-__global__ __launch_bounds__(64 * X3_WV) void gemm_x3k_kernel(X3KArgs a) {
+template <int TM, int EPI>
+__global__ __launch_bounds__(64 * X3_WV, 4) void gemm_x3k_kernel(X3KArgs a) {
   static_assert(X3_NT == 1, "gemm_x3k_kernel reads the one-tile pack layout");
   extern __shared__ __attribute__((aligned(16))) float x3_lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -605,9 +631,9 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3k_kernel(X3KArgs a) {
   constexpr int SLOT = X3K_KC * TM * 3 * 256;    // floats per ring slot (1 KB images)
   const int nch = (KS + X3K_KC - 1) / X3K_KC;
 
-  // chunk c -> slot c & 1: images [s][t][q] for k-steps c KC .. c KC + KC - 1, row tiles t < TM
+  // chunk c -> slot c % 3: images [s][t][q] for k-steps c KC .. c KC + KC - 1, row tiles t < TM
   auto issue = [&](int c) {
-    float* slot = x3_lds + (c & 1) * SLOT;
+    float* slot = x3_lds + (c % 3) * SLOT;
     for (int i = wave; i < X3K_KC * TM * 3; i += X3_WV) {
       const int q = i % 3, t = (i / 3) % TM, s = c * X3K_KC + i / (3 * TM);
       int g = mt * TM + t;
@@ -618,12 +644,20 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3k_kernel(X3KArgs a) {
     }
   };
 
-  const float* xb = a.x + (int64_t)b * K * P + pc;
+  // wave-uniform slab base + 32-bit lane offsets (K P < 2^30, checked on the host); rows past K load
+  // row K - 1 and are zeroed by a select (no per-load branches)
+  const float* xs = a.x + (int64_t)b * K * P;
+  const uint32_t P32 = (uint32_t)P, pc32 = (uint32_t)pc;
+  const uint32_t loff = (uint32_t)(8 * hf) * P32 + pc32;   // lane offset within a 16-row k-step
+  // row 16 s + j + 8 hf: a wave-uniform row base (SGPRs) plus the lane offset; rows past K read a valid
+  // row (the base clamped, the half-wave offset dropped) and are zeroed by a select -- no branches
   auto load = [&](int s, float (&v)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 16 * s + 8 * hf + j;
-      v[j] = k < K ? xb[(int64_t)(k < K ? k : 0) * P] : 0.f;
+      const int rb = 16 * s + j;
+      const float* rp = xs + (int64_t)(rb < K ? rb : K - 1) * P;
+      const float t = rp[(hf && rb + 8 < K) ? loff : pc32];
+      v[j] = rb + 8 * hf < K ? t : 0.f;
     }
   };
 
@@ -631,34 +665,37 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3k_kernel(X3KArgs a) {
 #pragma unroll
   for (int t = 0; t < TM; ++t) acc[t] = f32x16{};
 
+  // 3-slot ring, chunks two ahead.  Per wave and chunk: its DMAs of chunk c + 2 (at least DMIN),
+  // then 8 KC dword x loads (the k-steps one chunk ahead), in that order.
+  constexpr int DMIN = X3K_KC * TM * 3 / X3_WV;
   issue(0);
+  if (nch > 1) issue(1);
   float x0[8], x1[8];
   load(0, x0);
   load(1 < KS ? 1 : 0, x1);
   for (int c = 0; c < nch; ++c) {
-    // this wave's DMAs of chunk c landed: only the x loads of the next two k-steps (16 dword loads,
-    // issued after the DMAs) may still be in flight; then every wave's (one barrier per chunk: a
-    // wave at it has finished reading the slot the next issue() overwrites)
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    // this wave's DMAs of chunk c landed (younger: chunk c - 2's x loads, chunk c + 1's DMAs if any,
+    // chunk c - 1's x loads), then every wave's; one barrier per chunk: a wave at it has finished
+    // reading the slot the next issue() overwrites
+    if (c == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (c + 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(32 + DMIN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (c + 1 < nch) issue(c + 1);               // slot (c + 1) & 1 was last read in chunk c - 1
-    const float* slot = x3_lds + (c & 1) * SLOT;
+    if (c + 2 < nch) issue(c + 2);               // slot (c + 2) % 3 was last read in chunk c - 1
+    const float* slot = x3_lds + (c % 3) * SLOT;
+    static_assert(X3K_KC == 2, "two k-steps per chunk: x0 / x1 alternate by step parity");
 #pragma unroll
     for (int si = 0; si < X3K_KC; ++si) {
       const int s = c * X3K_KC + si;
-      if (s >= KS) break;
-      float* cur = (si & 1) ? x1 : x0;
+      if (s < KS) {   // wave-uniform (only the last chunk can be short)
       bf16x8 bq0, bq1, bq2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        uint32_t h0, h1, h2;
-        split3(cur[j], h0, h1, h2);
-        bq0[j] = __builtin_bit_cast(__bf16, (uint16_t)h0);
-        bq1[j] = __builtin_bit_cast(__bf16, (uint16_t)h1);
-        bq2[j] = __builtin_bit_cast(__bf16, (uint16_t)h2);
+      if (si == 0) {
+        split3x8(x0, bq0, bq1, bq2);
+        load(s + 2 < KS ? s + 2 : KS - 1, x0);
+      } else {
+        split3x8(x1, bq0, bq1, bq2);
+        load(s + 2 < KS ? s + 2 : KS - 1, x1);
       }
-      if (si & 1) load(s + 2 < KS ? s + 2 : KS - 1, x1);
-      else load(s + 2 < KS ? s + 2 : KS - 1, x0);
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
         const float* im = slot + (si * TM * 3 + t * 3) * 256 + lane * 4;
@@ -672,22 +709,39 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3k_kernel(X3KArgs a) {
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq1, acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq0, acc[t], 0, 0, 0);
       }
+      }
     }
   }
   float* const obase = a.out + (int64_t)b * M * P;
+  float cs = 1.f, s0 = 0.f, s1 = 1.f;
+  if constexpr (EPI == X3K_LN) cs = a.sd[(int64_t)b * P + pc];   // CustomLayerNorm 1/sigma (REF:921-922)
+  if constexpr (EPI == X3K_SKIP) { s0 = a.skip[0]; s1 = a.skip[1]; }
+  // row m = 32 g + (i & 3) + 8 (i >> 2) + 4 hf: a wave-uniform row base per (tile, i) plus the lane's
+  // offset 4 hf P + p (M P < 2^30, checked on the host)
+  const float* rbase = a.res + (int64_t)b * M * P;
+  const uint32_t eoff = (uint32_t)(4 * hf) * P32 + (uint32_t)p;
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int m = (mt * TM + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-      if (m < M && pin) obase[(int64_t)m * P + p] = acc[t][i];
+      const int mr = (mt * TM + t) * 32 + (i & 3) + 8 * (i >> 2);
+      if (mr + 4 * hf < M && pin) {
+        float v = acc[t][i];
+        if constexpr (EPI == X3K_LN) v *= cs;
+        if constexpr (EPI == X3K_SKIP) v = s0 * (rbase + (int64_t)mr * P)[eoff] + s1 * v;   // REF:962-964
+        (obase + (int64_t)mr * P)[eoff] = v;
+      }
     }
 }
 
+template <int EPI = X3K_STORE>
 static grr_status launch_x3k(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
-                             hipStream_t s, const char* name) {
+                             hipStream_t s, const char* name, const float* sd = nullptr, const float* res = nullptr,
+                             const float* skip = nullptr) {
+  GRR_REQUIRE((int64_t)K * P < (1ll << 30) && (int64_t)M * P < (1ll << 30), GRR_ERR_UNSUPPORTED,
+              "%s: K*P or M*P too large for 32-bit offsets", name);
   X3KArgs a{};
-  a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M;
+  a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M; a.sd = sd; a.res = res; a.skip = skip;
   a.KS = (K + 15) / 16;
   a.ngroups = (M + 31) / 32;
   a.CB = x3_chunk_bytes(a.KS);
@@ -698,12 +752,12 @@ static grr_status launch_x3k(const float* x, const uint16_t* frag, float* out, i
   const uint64_t n = (uint64_t)B * a.tiles * a.nmt;
   GRR_REQUIRE(n < (1ull << 31), GRR_ERR_UNSUPPORTED, "%s: grid too large", name);
   a.nblk = (uint32_t)n;
-  const size_t lds = 2 * (size_t)X3K_KC * TM * 3 * 1024;
+  const size_t lds = 3 * (size_t)X3K_KC * TM * 3 * 1024;
   switch (TM) {
-    case 1: hipLaunchKernelGGL((gemm_x3k_kernel<1>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
-    case 2: hipLaunchKernelGGL((gemm_x3k_kernel<2>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
-    case 3: hipLaunchKernelGGL((gemm_x3k_kernel<3>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
-    default: hipLaunchKernelGGL((gemm_x3k_kernel<4>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    case 1: hipLaunchKernelGGL((gemm_x3k_kernel<1, EPI>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_x3k_kernel<2, EPI>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm_x3k_kernel<3, EPI>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
+    default: hipLaunchKernelGGL((gemm_x3k_kernel<4, EPI>), dim3(a.nblk), dim3(64 * X3_WV), lds, s, a); break;
   }
   return launch_status(name);
 }
@@ -817,13 +871,79 @@ static grr_status lnb_forward_fp32(const float* x, const float* ln_w, const floa
   const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
   const uint64_t nb = (uint64_t)B * hid * tx * ty;
   GRR_REQUIRE(nb < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
-  hipLaunchKernelGGL(dw_gate_kernel, dim3((unsigned)nb), dim3(256), 0, s, hbuf, wdw, gbuf, hid, H, W, tx, ty,
+  hipLaunchKernelGGL(dw_gate_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, hbuf, wdw, gbuf, hid, H, W, tx, ty,
                      (uint32_t)nb);
   st = launch_status("grr_lnb_forward/dw_gate");
   if (st != GRR_OK) return st;
   GemmArgs g2{};
   g2.x = gbuf; g2.wt = w2; g2.res = x; g2.skip = skip; g2.out = out; g2.K = hid; g2.M = C; g2.P = P;
   return launch_gemm<LD_PLAIN, EP_SKIP>(g2, B, s, "grr_lnb_forward/w2");
+}
+
+// FeedForward block of the window models' feature CNN (FFBlock, REF7:13-67):
+//   n = ln_w * x / sqrt(var_c x + 1e-5);  h = W_in n;  x1, x2 = dwconv3x3_zero(h);
+//   out = s0 x + s1 W_out (gelu(x1) * x2)
+// W_in on the split-bf16 GEMM with the LN folded (K = C <= 128: statistics in-kernel; deeper: the
+// K-streaming kernel with ln_stats' per-pixel scale in its epilogue), the depthwise + gelu gate as one
+// memory-bound pass, W_out + skip on the K-streaming kernel's skip epilogue.
+// Workspace (floats, 64-aligned pieces): sd [B P], h [B 2hid P], g [B hid P], W_in / W_out fragments.
+struct FfnLayout {
+  int64_t sd, h, g, f1, f2, total;
+  int KS1, nch1, KS2, nch2;
+};
+static int64_t a64(int64_t n) { return (n + 63) / 64 * 64; }
+static FfnLayout ffn_layout(int B, int C, int hid, int64_t P) {
+  FfnLayout L{};
+  L.KS1 = (C + 15) / 16; L.nch1 = (2 * hid + 31) / 32;
+  L.KS2 = (hid + 15) / 16; L.nch2 = (C + 31) / 32;
+  L.sd = 0;
+  L.h = a64((int64_t)B * P);
+  L.g = L.h + a64((int64_t)B * 2 * hid * P);
+  L.f1 = L.g + a64((int64_t)B * hid * P);
+  L.f2 = L.f1 + a64((int64_t)L.nch1 * x3_chunk_bytes(L.KS1) / 4);
+  L.total = L.f2 + a64((int64_t)L.nch2 * x3_chunk_bytes(L.KS2) / 4);
+  return L;
+}
+
+static grr_status ffn_forward(const float* x, const float* ln_w, const float* w_in, const float* w_dw,
+                              const float* w_out, const float* skip, float* out, float* ws, int B, int C, int hid,
+                              int H, int W, hipStream_t s) {
+  const int64_t P = (int64_t)H * W;
+  const FfnLayout L = ffn_layout(B, C, hid, P);
+  float* sd = ws + L.sd;
+  float* hbuf = ws + L.h;
+  float* gbuf = ws + L.g;
+  uint16_t* f1 = reinterpret_cast<uint16_t*>(ws + L.f1);
+  uint16_t* f2 = reinterpret_cast<uint16_t*>(ws + L.f2);
+  auto pack = [&](const float* w, const float* lw, uint16_t* frag, int M, int K, int KS, int nch) {
+    const int64_t nf = (int64_t)nch * x3_chunk_bytes(KS) / 2;
+    hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 1 << 16)), dim3(256), 0, s,
+                       w, lw, frag, M, K, KS, nch);
+    return launch_status("grr_ffn_forward/pack");
+  };
+  grr_status st = pack(w_in, ln_w, f1, 2 * hid, C, L.KS1, L.nch1);
+  if (st != GRR_OK) return st;
+  st = pack(w_out, nullptr, f2, C, hid, L.KS2, L.nch2);
+  if (st != GRR_OK) return st;
+  if (C <= 128) {
+    st = launch_x3<true>(x, f1, hbuf, B, C, 2 * hid, P, s, "grr_ffn_forward/w_in");
+  } else {
+    GRR_REQUIRE((int64_t)B * ((P + 63) / 64) < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_ffn_forward: grid too large");
+    hipLaunchKernelGGL(ln_stats_kernel, dim3((unsigned)((int64_t)B * ((P + 63) / 64))), dim3(64 * LN_G), 0, s, x, sd,
+                       B, C, P);
+    st = launch_status("grr_ffn_forward/ln_stats");
+    if (st != GRR_OK) return st;
+    st = launch_x3k<X3K_LN>(x, f1, hbuf, B, C, 2 * hid, P, s, "grr_ffn_forward/w_in", sd);
+  }
+  if (st != GRR_OK) return st;
+  const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
+  const uint64_t nb = (uint64_t)B * hid * tx * ty;
+  GRR_REQUIRE(nb < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_ffn_forward: grid too large");
+  hipLaunchKernelGGL(dw_gate_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, hbuf, w_dw, gbuf, hid, H, W, tx, ty,
+                     (uint32_t)nb);
+  st = launch_status("grr_ffn_forward/dw_gate");
+  if (st != GRR_OK) return st;
+  return launch_x3k<X3K_SKIP>(gbuf, f2, out, B, hid, C, P, s, "grr_ffn_forward/w_out", nullptr, x, skip);
 }
 
 }  // namespace grr
@@ -865,6 +985,25 @@ grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, 
   GRR_REQUIRE(R * Cs <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward_rep: R*Cs=%d > 128", R * Cs);
   return grr::lnb_forward_mfma_rep(src, Cs, R, x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, hid, H, W,
                                    (hipStream_t)stream);
+}
+
+int64_t grr_ffn_workspace_bytes(int B, int C, int hid, int H, int W) {
+  if (B <= 0 || C <= 1 || hid <= 0 || H <= 0 || W <= 0) return 0;
+  return grr::ffn_layout(B, C, hid, (int64_t)H * W).total * (int64_t)sizeof(float);
+}
+
+grr_status grr_ffn_forward(const float* x, const float* ln_w, const float* w_in, const float* w_dw, const float* w_out,
+                           const float* skip, float* out, void* workspace, int B, int C, int hid, int H, int W,
+                           void* stream) {
+  grr::clear_error();
+  GRR_REQUIRE(x && ln_w && w_in && w_dw && w_out && skip && out && workspace && B > 0 && C > 1 && hid > 0 &&
+                  H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_ffn_forward: bad args");
+  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_ffn_forward: out aliases x");
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_ffn_forward: workspace not 256-B aligned");
+  GRR_REQUIRE(C <= 4096 && hid <= 4096, GRR_ERR_UNSUPPORTED, "grr_ffn_forward: C=%d, hid=%d > 4096", C, hid);
+  return grr::ffn_forward(x, ln_w, w_in, w_dw, w_out, skip, out, (float*)workspace, B, C, hid, H, W,
+                          (hipStream_t)stream);
 }
 
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {

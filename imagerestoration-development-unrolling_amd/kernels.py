@@ -507,6 +507,25 @@ def conv2x2s2(x: Tensor, weight: Tensor) -> Tensor:
     return out
 
 
+def ffn_forward(x: Tensor, ln_w: Tensor, w_in: Tensor, w_dw: Tensor, w_out: Tensor, skip: Tensor) -> Tensor:
+    """FFBlock of the window models' feature CNN (grr_ffn_forward, REF7:13-67): x [B,C,H,W]; ln_w [C];
+    w_in [2 hid, C]; w_dw [2 hid, 9]; w_out [C, hid]; skip [2]."""
+    dev = _check("ffn_forward", x, ln_w, w_in, w_dw, w_out, skip)
+    b, c, h, w = x.shape
+    hid = w_out.shape[1]
+    if tuple(w_in.shape) != (2 * hid, c) or tuple(w_dw.shape) != (2 * hid, 9) or tuple(w_out.shape) != (c, hid) \
+            or ln_w.numel() != c or skip.numel() != 2:
+        raise ValueError("ffn_forward: weight shapes disagree with x / hid")
+    out = torch.empty_like(x)
+    ws = torch.empty((_native.load().grr_ffn_workspace_bytes(b, c, hid, h, w) + 3) // 4, dtype=torch.float32,
+                     device=dev)
+    p = b * h * w
+    _launch("ffn", 4 * p * (2 * c + 3 * hid + 2 * hid), "grr_ffn_forward", x.data_ptr(), ln_w.data_ptr(),
+            w_in.data_ptr(), w_dw.data_ptr(), w_out.data_ptr(), skip.data_ptr(), out.data_ptr(), ws.data_ptr(),
+            b, c, hid, h, w, _stream(dev), flops=p * (2 * c * 2 * hid + 18 * 2 * hid + 2 * hid * c))
+    return out
+
+
 def wgrad(a: Tensor, bop: Tensor) -> Tensor:
     """Weight gradient out[m, k] = sum_b sum_p a[b, m, p] bop[b, k, p] (grr_wgrad): a [B, M, ...],
     bop [B, K, ...] with the same trailing pixel extent.  The reverse of a 1x1 conv / LNB GEMM's

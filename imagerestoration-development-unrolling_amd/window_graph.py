@@ -64,7 +64,8 @@ def window_edges(connection_window) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------
-# Feature CNN (REF7:13-270) -- stock PyTorch-ROCm convolutions
+# Feature CNN (REF7:13-270): FFBlocks on grr_ffn_forward in inference; the 3x3 convs (embedding,
+# down / up sampling, output) and the training path on stock PyTorch-ROCm convolutions
 # ---------------------------------------------------------------------------
 class CustomLayerNorm(nn.Module):
     """x / sqrt(var_c(x) + 1e-5) (unbiased, uncentred), then a per-channel scale (REF7:13-26)."""
@@ -106,6 +107,17 @@ class FFBlock(nn.Module):
         self.ffn = FeedForward(dim, ffn_expansion_factor, bias)
 
     def forward(self, x):
+        ffn = self.ffn
+        if x.is_cuda and ffn.project_in.bias is None and not records_grad(self, x) \
+                and not torch.compiler.is_compiling():
+            # inference: the whole block as one grr_ffn_forward (split-bf16 MFMA GEMMs, gelu gate)
+            c, hid = x.shape[1], ffn.project_out.weight.shape[1]
+            return K.ffn_forward(x.contiguous(), self.norm.weighted_transform.weight.reshape(c).contiguous(),
+                                 ffn.project_in.weight.reshape(2 * hid, c).contiguous(),
+                                 ffn.dwconv.weight.reshape(2 * hid, 9).contiguous(),
+                                 ffn.project_out.weight.reshape(c, hid).contiguous(),
+                                 self.skip_connect_weight_final.contiguous())
+        # training (autograd) and biased variants: stock PyTorch-ROCm ops
         return self.skip_connect_weight_final[0] * x + self.skip_connect_weight_final[1] * self.ffn(self.norm(x))
 
 

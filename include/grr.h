@@ -243,6 +243,16 @@ grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* wor
 grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int K, int M, int H, int W,
                          void* stream);
 
+/* FeedForward block of the window models' feature CNN (FFBlock, REF7:13-67, nn.Conv2d bias=False):
+ * out = skip[0] x + skip[1] W_out (gelu(d1) * d2), [d1; d2] = dwconv3x3_zero(W_in (ln_w * x / sigma)),
+ * sigma = sqrt(var_c x (unbiased) + 1e-5).  x, out [B,C,H,W]; ln_w [C]; w_in [2 hid, C]; w_dw [2 hid, 9];
+ * w_out [C, hid]; skip [2] (device).  Split-bf16 MFMA GEMMs (fp32-accurate), exact erf gelu.
+ * workspace: grr_ffn_workspace_bytes(B, C, hid, H, W) bytes, 256-B aligned. */
+int64_t grr_ffn_workspace_bytes(int B, int C, int hid, int H, int W);
+grr_status grr_ffn_forward(const float* x, const float* ln_w, const float* w_in, const float* w_dw, const float* w_out,
+                           const float* skip, float* out, void* workspace, int B, int C, int hid, int H, int W,
+                           void* stream);
+
 /* Weight gradient of a 1x1 / 2x2-s2 convolution or an LNB GEMM (the reverse of REF:556-612,
  * REF13:564-575 under autograd): out[m,k] = sum_b sum_p a[b,m,p] * bop[b,k,p], a [B,M,P], bop [B,K,P],
  * out [M,K]; fp32 MFMA, partial tiles per pixel chunk added in a fixed order (deterministic, no

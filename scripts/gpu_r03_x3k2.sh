@@ -1,0 +1,9 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+out=gpurun_out/x3k2; mkdir -p $out
+export TMPDIR=/tmp MIOPEN_FIND_MODE=FAST
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ffn.py tests/test_gpu_parity.py -k "ffn or ffblock or feature or conv or x3" -q -rf --timeout 120 --timeout-method thread -p no:cacheprovider > $out/tests.log 2>&1
+rc=$?; tail -2 $out/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u scripts/micro_wgrad.py > $out/micro.txt 2>&1; rc=$?; grep conv1x1 $out/micro.txt; [ $rc -eq 0 ] || exit $rc
+MICRO_ARGS="--batch 16" bash scripts/pmc_sq.sh conv_deep gemm_x3k x3k2/sq || exit 1

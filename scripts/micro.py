@@ -74,6 +74,10 @@ def main():
     elif args.kernel == "conv1x1":
         wt = torch.rand(2 * c, c, 1, 1, device=dev)
         fn = lambda: K.conv1x1(x, wt)  # noqa: E731
+    elif args.kernel == "conv_deep":   # the window FFBlock's W_in (K = 256 -> M = 1364), K-streaming x3 GEMM
+        xd = torch.rand(b, 256, h, w, device=dev)
+        wt = torch.rand(1364, 256, 1, 1, device=dev)
+        fn = lambda: K.conv1x1(xd, wt)  # noqa: E731
     elif args.kernel == "edge":
         feat = torch.rand(b, 2 * c, h, w, device=dev)
         fn = lambda: K.edge_weights(feat, 0, g, f, p(mix.GTVmodule00.multiM))  # noqa: E731

@@ -32,7 +32,8 @@ for (m, k, hw) in [(512, 96, 256), (96, 256, 256), (192, 96, 256), (512, 96, 128
     gb = 4 * B * hw * hw * (m + k) / 1e9
     tf = 2 * B * hw * hw * m * k / 1e12
     print(f"wgrad {m}x{k} {B}x{hw}^2: grr {tw:.3f} ms ({gb / tw:.2f} TB/s, {tf / tw * 1e3:.0f} TF/s)  lib {tl:.3f} ms", flush=True)
-for (k, m, hw) in [(96, 512, 256), (96, 256, 256), (512, 96, 256), (256, 96, 256), (192, 96, 256), (96, 192, 256)]:
+for (k, m, hw) in [(96, 512, 256), (96, 256, 256), (512, 96, 256), (256, 96, 256), (192, 96, 256), (96, 192, 256),
+                   (256, 1364, 256), (682, 256, 256)]:
     x = torch.randn(B, k, hw, hw, device=dev)
     w = torch.randn(m, k, 1, 1, device=dev)
     tc = t(lambda: K.conv1x1(x, w))

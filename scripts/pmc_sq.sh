@@ -9,7 +9,7 @@ P2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTI
 n=1
 for P in "$P1" "$P2"; do
   timeout -s KILL 90 rocprofv3 --pmc $P --kernel-include-regex "$RX" --output-format csv -d $OUT/p$n -o run -- \
-    python scripts/micro.py --kernel $MK --iters 3 > $OUT/p$n.log 2>&1 || { echo "pass $n failed"; tail -5 $OUT/p$n.log; exit 1; }
+    python scripts/micro.py --kernel $MK --iters 3 ${MICRO_ARGS:-} > $OUT/p$n.log 2>&1 || { echo "pass $n failed"; tail -5 $OUT/p$n.log; exit 1; }
   n=$((n+1))
 done
 python - "$OUT" <<'PY'
