@@ -842,49 +842,14 @@ grr_status grr_conv2x2s2(const float* x, const float* wt, float* out, int B, int
 
 namespace grr {
 
-// LNB fp32 path (C > 128): LN statistics, W1 on fp32 MFMA with the LN folded in, depthwise
-// 3x3 + gate, W2 + skip.  Workspace (floats): [sd: B*P][h: B*2hid*P][g: B*hid*P].
-static int64_t lnb_fp32_workspace_floats(int B, int hid, int H, int W) {
-  const int64_t P = (int64_t)H * W, a64 = 64;
-  return ((int64_t)B * P + a64 - 1) / a64 * a64 + ((int64_t)B * 2 * hid * P + a64 - 1) / a64 * a64 +
-         (int64_t)B * hid * P;
-}
-
-static grr_status lnb_forward_fp32(const float* x, const float* ln_w, const float* w1, const float* wdw,
-                                   const float* w2, const float* skip, float* out, float* ws, int B, int C, int hid,
-                                   int H, int W, hipStream_t s) {
-  GRR_REQUIRE(C <= 512, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d > 512", C);
-  const int64_t P = (int64_t)H * W;
-  float* sd = ws;
-  float* hbuf = sd + ((int64_t)B * P + 63) / 64 * 64;
-  float* gbuf = hbuf + ((int64_t)B * 2 * hid * P + 63) / 64 * 64;
-  const int64_t n = (int64_t)B * P;
-  GRR_REQUIRE((int64_t)B * ((P + 63) / 64) < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
-  hipLaunchKernelGGL(ln_stats_kernel, dim3((unsigned)((int64_t)B * ((P + 63) / 64))), dim3(64 * LN_G), 0, s, x, sd, B,
-                     C, P);
-  grr_status st = launch_status("grr_lnb_forward/ln_stats");
-  if (st != GRR_OK) return st;
-  GemmArgs g1{};
-  g1.x = x; g1.wt = w1; g1.ln_sd = sd; g1.ln_w = ln_w; g1.out = hbuf; g1.K = C; g1.M = 2 * hid; g1.P = P;
-  st = launch_gemm<LD_LN, EP_STORE>(g1, B, s, "grr_lnb_forward/w1");
-  if (st != GRR_OK) return st;
-  const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
-  const uint64_t nb = (uint64_t)B * hid * tx * ty;
-  GRR_REQUIRE(nb < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
-  hipLaunchKernelGGL(dw_gate_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, hbuf, wdw, gbuf, hid, H, W, tx, ty,
-                     (uint32_t)nb);
-  st = launch_status("grr_lnb_forward/dw_gate");
-  if (st != GRR_OK) return st;
-  GemmArgs g2{};
-  g2.x = gbuf; g2.wt = w2; g2.res = x; g2.skip = skip; g2.out = out; g2.K = hid; g2.M = C; g2.P = P;
-  return launch_gemm<LD_PLAIN, EP_SKIP>(g2, B, s, "grr_lnb_forward/w2");
-}
-
-// FeedForward block of the window models' feature CNN (FFBlock, REF7:13-67):
-//   n = ln_w * x / sqrt(var_c x + 1e-5);  h = W_in n;  x1, x2 = dwconv3x3_zero(h);
-//   out = s0 x + s1 W_out (gelu(x1) * x2)
+// Unfused block pipeline for the wide blocks:
+//   FFN = true:  FeedForward block of the window models' feature CNN (FFBlock, REF7:13-67):
+//                n = ln_w * x / sqrt(var_c x + 1e-5);  h = W_in n;  x1, x2 = dwconv3x3_zero(h);
+//                out = s0 x + s1 W_out (gelu(x1) * x2)
+//   FFN = false: LocalNonLinearBlock with C > 128 (the v1.0 widths 192 / 384; REF:911-964): replicate
+//                depthwise, g = sigmoid(m) m v  (C <= 128 runs the fused head / mix kernels, lnb_ops.hip)
 // W_in on the split-bf16 GEMM with the LN folded (K = C <= 128: statistics in-kernel; deeper: the
-// K-streaming kernel with ln_stats' per-pixel scale in its epilogue), the depthwise + gelu gate as one
+// K-streaming kernel with ln_stats' per-pixel scale in its epilogue), the depthwise + gate as one
 // memory-bound pass, W_out + skip on the K-streaming kernel's skip epilogue.
 // Workspace (floats, 64-aligned pieces): sd [B P], h [B 2hid P], g [B hid P], W_in / W_out fragments.
 struct FfnLayout {
@@ -905,9 +870,10 @@ static FfnLayout ffn_layout(int B, int C, int hid, int64_t P) {
   return L;
 }
 
-static grr_status ffn_forward(const float* x, const float* ln_w, const float* w_in, const float* w_dw,
-                              const float* w_out, const float* skip, float* out, float* ws, int B, int C, int hid,
-                              int H, int W, hipStream_t s) {
+template <bool FFN>
+static grr_status block_x3_forward(const float* x, const float* ln_w, const float* w_in, const float* w_dw,
+                                   const float* w_out, const float* skip, float* out, float* ws, int B, int C,
+                                   int hid, int H, int W, hipStream_t s) {
   const int64_t P = (int64_t)H * W;
   const FfnLayout L = ffn_layout(B, C, hid, P);
   float* sd = ws + L.sd;
@@ -939,7 +905,7 @@ static grr_status ffn_forward(const float* x, const float* ln_w, const float* w_
   const int tx = (W + DT - 1) / DT, ty = (H + DT - 1) / DT;
   const uint64_t nb = (uint64_t)B * hid * tx * ty;
   GRR_REQUIRE(nb < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_ffn_forward: grid too large");
-  hipLaunchKernelGGL(dw_gate_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, hbuf, w_dw, gbuf, hid, H, W, tx, ty,
+  hipLaunchKernelGGL(dw_gate_kernel<FFN>, dim3((unsigned)nb), dim3(256), 0, s, hbuf, w_dw, gbuf, hid, H, W, tx, ty,
                      (uint32_t)nb);
   st = launch_status("grr_ffn_forward/dw_gate");
   if (st != GRR_OK) return st;
@@ -953,7 +919,7 @@ extern "C" {
 int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
   if (B <= 0 || C <= 0 || hid <= 0 || H <= 0 || W <= 0) return 0;
   const int64_t f = C <= 128 ? grr::lnb_mfma_workspace_floats(B, C, hid, H, W)
-                             : grr::lnb_fp32_workspace_floats(B, hid, H, W);
+                             : grr::ffn_layout(B, C, hid, (int64_t)H * W).total;
   return f * (int64_t)sizeof(float);
 }
 
@@ -969,7 +935,8 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
   hipStream_t s = (hipStream_t)stream;
   if (C <= 128)
     return grr::lnb_forward_mfma(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
-  return grr::lnb_forward_fp32(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
+  GRR_REQUIRE(C <= 4096 && hid <= 4096, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d, hid=%d > 4096", C, hid);
+  return grr::block_x3_forward<false>(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
 }
 
 grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, const float* ln_w, const float* w1,
@@ -1002,8 +969,8 @@ grr_status grr_ffn_forward(const float* x, const float* ln_w, const float* w_in,
   GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_ffn_forward: out aliases x");
   GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_ffn_forward: workspace not 256-B aligned");
   GRR_REQUIRE(C <= 4096 && hid <= 4096, GRR_ERR_UNSUPPORTED, "grr_ffn_forward: C=%d, hid=%d > 4096", C, hid);
-  return grr::ffn_forward(x, ln_w, w_in, w_dw, w_out, skip, out, (float*)workspace, B, C, hid, H, W,
-                          (hipStream_t)stream);
+  return grr::block_x3_forward<true>(x, ln_w, w_in, w_dw, w_out, skip, out, (float*)workspace, B, C, hid, H, W,
+                                     (hipStream_t)stream);
 }
 
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream) {
