@@ -109,6 +109,8 @@ SIGNATURES = {
     "grr_lnb_gate_bwd_scaled": [P, P, P, P, P, I, I, L, P],
     "grr_lnb_gate_dw3_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "grr_lnb_dw3_gate": [P, P, P, I, I, I, I, P],
+    "grr_ffn_dw3_gate": [P, P, P, I, I, I, I, P],
+    "grr_ffn_gate_dw3_bwd": [P, P, P, P, P, P, P, I, I, I, I, P],
     # window graphs (REF7 / REF1)
     "grr_win_edge_weights": [P, L, P, P, I, P, P, I, I, I, I, I, P],
     "grr_win_solver": [I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, I, I, I, I, I, P],

@@ -435,7 +435,9 @@ __global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict
 
 // one depthwise output row from input rows r-1, r, r+1 (R[0..2], replicate-clamped by the
 // caller): the expressions and order of dw3_row_fwd_kernel
-template <int V>
+// ZERO (the window models' FeedForward, nn.Conv2d padding=1): zero padding instead of replicate -- the
+// caller passes zero rows above / below the image, the column neighbours past the edges are 0
+template <int V, bool ZERO = false>
 __device__ __forceinline__ void dw3_row_out(const float (&R0)[V], const float (&R1)[V], const float (&R2)[V],
                                             const float (&wt)[9], int c0, int W, float (&o)[V]) {
   const float* Rs[3] = {R0, R1, R2};
@@ -448,8 +450,8 @@ __device__ __forceinline__ void dw3_row_out(const float (&R0)[V], const float (&
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const int col = c0 + k;
-      const float l = col > 0 ? (k > 0 ? R[k - 1] : pv) : R[k];
-      const float rr = col < W - 1 ? (k < V - 1 ? R[k + 1] : nx) : R[k];
+      const float l = col > 0 ? (k > 0 ? R[k - 1] : pv) : (ZERO ? 0.f : R[k]);
+      const float rr = col < W - 1 ? (k < V - 1 ? R[k + 1] : nx) : (ZERO ? 0.f : R[k]);
       o[k] += wt[dy * 3 + 0] * l;
       o[k] += wt[dy * 3 + 1] * R[k];
       o[k] += wt[dy * 3 + 2] * rr;
@@ -457,10 +459,43 @@ __device__ __forceinline__ void dw3_row_out(const float (&R0)[V], const float (&
   }
 }
 
+// row rr of a plane (replicate: clamped; ZERO: zeros outside the image)
+template <int V, bool ZERO>
+__device__ __forceinline__ void row_load_pad(float (&d)[V], const float* base, int rr, int H, int W) {
+  if (ZERO && (rr < 0 || rr >= H)) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) d[k] = 0.f;
+  } else {
+    row_load<V>(d, base + (int64_t)clampi(rr, 0, H - 1) * W);
+  }
+}
+
+// the gate and its derivative: FFN (REF7:42-46) gelu(m) v with the exact erf gelu; else (REF:934-947)
+// sigmoid(m) m v.  gate_d returns d gate / dm (per unit v) and the gate factor f with gate = f v.
+template <bool FFN>
+__device__ __forceinline__ float gate_f(float m) {
+  if constexpr (FFN) return m * 0.5f * (1.0f + erff(m * 0.70710678118654752440f));
+  const float sg = 1.0f / (1.0f + expf(-m));
+  return sg * m;
+}
+template <bool FFN>
+__device__ __forceinline__ void gate_d(float m, float& f, float& df) {
+  if constexpr (FFN) {   // torch's gelu backward: cdf + x pdf
+    const float cdf = 0.5f * (1.0f + erff(m * 0.70710678118654752440f));
+    const float pdf = expf(-0.5f * m * m) * 0.39894228040143267794f;
+    f = m * cdf;
+    df = cdf + m * pdf;
+  } else {
+    const float sg = 1.0f / (1.0f + expf(-m));
+    f = sg * m;
+    df = sg + m * sg * (1.0f - sg);
+  }
+}
+
 // depthwise 3x3 + gate in one row pass: gate = sigmoid(m) m v of (m, v) = dw3(hh)[j], [hid + j];
 // one wave = one channel pair of one image and a segment of rows (the depthwise output is not
 // written: the reverse recomputes it from hh)
-template <int V>
+template <int V, bool FFN>
 __global__ __launch_bounds__(NT) void dw3_gate_row_fwd_kernel(const float* __restrict__ hh,
                                                               const float* __restrict__ wdw, float* __restrict__ gate,
                                                               int hid, int H, int W, int sseg, int nsegs,
@@ -480,25 +515,22 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_fwd_kernel(const float* __res
     wv[t] = wdw[(hid + j) * 9 + t];
   }
   float Rm[3][V], Rv[3][V], Nm[V], Nv[V];
-  row_load<V>(Rm[0], hmp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
-  row_load<V>(Rv[0], hvp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load_pad<V, FFN>(Rm[0], hmp, q.r0 - 1, H, W);
+  row_load_pad<V, FFN>(Rv[0], hvp, q.r0 - 1, H, W);
   row_load<V>(Rm[1], hmp + (int64_t)q.r0 * W);
   row_load<V>(Rv[1], hvp + (int64_t)q.r0 * W);
-  row_load<V>(Nm, hmp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
-  row_load<V>(Nv, hvp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  row_load_pad<V, FFN>(Nm, hmp, q.r0 + 1, H, W);
+  row_load_pad<V, FFN>(Nv, hvp, q.r0 + 1, H, W);
   for (int r = q.r0; r < q.r1; ++r) {
 #pragma unroll
     for (int k = 0; k < V; ++k) { Rm[2][k] = Nm[k]; Rv[2][k] = Nv[k]; }
-    row_load<V>(Nm, hmp + (int64_t)clampi(r + 2, 0, H - 1) * W);
-    row_load<V>(Nv, hvp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    row_load_pad<V, FFN>(Nm, hmp, r + 2, H, W);
+    row_load_pad<V, FFN>(Nv, hvp, r + 2, H, W);
     float m[V], v[V], o[V];
-    dw3_row_out<V>(Rm[0], Rm[1], Rm[2], wm, q.c0, W, m);
-    dw3_row_out<V>(Rv[0], Rv[1], Rv[2], wv, q.c0, W, v);
+    dw3_row_out<V, FFN>(Rm[0], Rm[1], Rm[2], wm, q.c0, W, m);
+    dw3_row_out<V, FFN>(Rv[0], Rv[1], Rv[2], wv, q.c0, W, v);
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      const float sg = 1.0f / (1.0f + expf(-m[k]));
-      o[k] = (sg * m[k]) * v[k];
-    }
+    for (int k = 0; k < V; ++k) o[k] = gate_f<FFN>(m[k]) * v[k];
     if (q.on) row_store<V>(gp + (int64_t)r * W, o);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -515,7 +547,7 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_fwd_kernel(const float* __res
 // sg = sigmoid(m)), so ghp never reaches HBM; <gq, gate> is accumulated for the skip weight
 // (rows of the wave's own segment only); then, per plane, the depthwise data adjoint and weight
 // gradient of dw3_row_bwd_kernel with the same expressions.
-template <int V, bool REC>
+template <int V, bool REC, bool FFN = false>
 __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
     const float* hp, const float* __restrict__ gq, const float* __restrict__ scale,
     const float* __restrict__ hh, const float* __restrict__ wdw, float* __restrict__ gh, float* __restrict__ gw,
@@ -566,9 +598,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
     if (xrow == INT32_MIN) {
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
-        const int64_t oo = (int64_t)clampi(want - 2 + d, 0, H - 1) * W;
-        row_load<V>(Xm[d], hmp + oo);
-        row_load<V>(Xv[d], hvp + oo);
+        row_load_pad<V, FFN>(Xm[d], hmp, want - 2 + d, H, W);
+        row_load_pad<V, FFN>(Xv[d], hvp, want - 2 + d, H, W);
       }
     } else {
 #pragma unroll
@@ -576,13 +607,12 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
         Xm[0][k] = Xm[1][k]; Xm[1][k] = Xm[2][k];
         Xv[0][k] = Xv[1][k]; Xv[1][k] = Xv[2][k];
       }
-      const int64_t oo = (int64_t)clampi(want, 0, H - 1) * W;
-      row_load<V>(Xm[2], hmp + oo);
-      row_load<V>(Xv[2], hvp + oo);
+      row_load_pad<V, FFN>(Xm[2], hmp, want, H, W);
+      row_load_pad<V, FFN>(Xv[2], hvp, want, H, W);
     }
     xrow = want;
-    dw3_row_out<V>(Xm[0], Xm[1], Xm[2], wm, q.c0, W, NM);
-    dw3_row_out<V>(Xv[0], Xv[1], Xv[2], wv, q.c0, W, NV);
+    dw3_row_out<V, FFN>(Xm[0], Xm[1], Xm[2], wm, q.c0, W, NM);
+    dw3_row_out<V, FFN>(Xv[0], Xv[1], Xv[2], wv, q.c0, W, NV);
   };
   auto ghp_row = [&](int rr, float (&dm)[V], float (&dv)[V]) {
     const bool in = rr >= 0 && rr < H;
@@ -590,11 +620,12 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const float m = NM[k], v = NV[k], g = NQ[k];
-      const float sg = 1.0f / (1.0f + expf(-m));
-      if (own) dot += g * ((sg * m) * v);
+      float gf, dgf;
+      gate_d<FFN>(m, gf, dgf);
+      if (own) dot += g * (gf * v);
       const float gg = s * g;
-      dm[k] = in ? gg * v * (sg + m * sg * (1.0f - sg)) : 0.f;
-      dv[k] = in ? gg * sg * m : 0.f;
+      dm[k] = in ? gg * v * dgf : 0.f;
+      dv[k] = in ? gg * gf : 0.f;
     }
   };
   raw_load(q.r0 - 1);
@@ -602,21 +633,21 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
   raw_load(q.r0);
   ghp_row(q.r0, Gm[1], Gv[1]);
   raw_load(q.r0 + 1);
-  row_load<V>(Hm[0], hmp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
-  row_load<V>(Hv[0], hvp + (int64_t)clampi(q.r0 - 1, 0, H - 1) * W);
+  row_load_pad<V, FFN>(Hm[0], hmp, q.r0 - 1, H, W);
+  row_load_pad<V, FFN>(Hv[0], hvp, q.r0 - 1, H, W);
   row_load<V>(Hm[1], hmp + (int64_t)q.r0 * W);
   row_load<V>(Hv[1], hvp + (int64_t)q.r0 * W);
-  row_load<V>(NHm, hmp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
-  row_load<V>(NHv, hvp + (int64_t)clampi(q.r0 + 1, 0, H - 1) * W);
+  row_load_pad<V, FFN>(NHm, hmp, q.r0 + 1, H, W);
+  row_load_pad<V, FFN>(NHv, hvp, q.r0 + 1, H, W);
   // one plane's data adjoint (row r) and weight-gradient contribution
   auto plane = [&](const float (&G)[3][V], const float (&Hp)[3][V], const float (&wt)[9], float (&acc)[9], int r,
                    float* dst) {
     float A[3][V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      A[0][k] = r == 0 ? G[2][k] + G[1][k] : G[2][k];
+    for (int k = 0; k < V; ++k) {   // zero padding: no folding of the clamped edge rows
+      A[0][k] = (!FFN && r == 0) ? G[2][k] + G[1][k] : G[2][k];
       A[1][k] = G[1][k];
-      A[2][k] = r == H - 1 ? G[0][k] + G[1][k] : G[0][k];
+      A[2][k] = (!FFN && r == H - 1) ? G[0][k] + G[1][k] : G[0][k];
     }
     float o[V];
 #pragma unroll
@@ -630,8 +661,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
         const float a = A[dy][k];
         const float al = k > 0 ? A[dy][k - 1] : pvv;
         const float ar = k < V - 1 ? A[dy][k + 1] : nx;
-        const float sm = col + 1 < W ? (col == 0 ? ar + a : ar) : (col == 0 ? a : 0.f);
-        const float sp = col >= 1 ? (col == W - 1 ? al + a : al) : (col == W - 1 ? a : 0.f);
+        const float sm = FFN ? (col + 1 < W ? ar : 0.f) : (col + 1 < W ? (col == 0 ? ar + a : ar) : (col == 0 ? a : 0.f));
+        const float sp = FFN ? (col >= 1 ? al : 0.f) : (col >= 1 ? (col == W - 1 ? al + a : al) : (col == W - 1 ? a : 0.f));
         o[k] += wt[dy * 3 + 0] * sm;
         o[k] += wt[dy * 3 + 1] * a;
         o[k] += wt[dy * 3 + 2] * sp;
@@ -645,8 +676,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
       for (int k = 0; k < V; ++k) {
         const int col = q.c0 + k;
         const float gv = q.on ? G[1][k] : 0.f;
-        const float l = col > 0 ? (k > 0 ? Hp[dy][k - 1] : pvv) : Hp[dy][k];
-        const float rr = col < W - 1 ? (k < V - 1 ? Hp[dy][k + 1] : nx) : Hp[dy][k];
+        const float l = col > 0 ? (k > 0 ? Hp[dy][k - 1] : pvv) : (FFN ? 0.f : Hp[dy][k]);
+        const float rr = col < W - 1 ? (k < V - 1 ? Hp[dy][k + 1] : nx) : (FFN ? 0.f : Hp[dy][k]);
         acc[dy * 3 + 0] += gv * l;
         acc[dy * 3 + 1] += gv * Hp[dy][k];
         acc[dy * 3 + 2] += gv * rr;
@@ -660,8 +691,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < V; ++k) { Hm[2][k] = NHm[k]; Hv[2][k] = NHv[k]; }
     raw_load(r + 2);
-    row_load<V>(NHm, hmp + (int64_t)clampi(r + 2, 0, H - 1) * W);
-    row_load<V>(NHv, hvp + (int64_t)clampi(r + 2, 0, H - 1) * W);
+    row_load_pad<V, FFN>(NHm, hmp, r + 2, H, W);
+    row_load_pad<V, FFN>(NHv, hvp, r + 2, H, W);
     plane(Gm, Hm, wm, accm, r, ghm);
     plane(Gv, Hv, wv, accv, r, ghv);
 #pragma unroll
@@ -725,13 +756,18 @@ bool dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* 
   }
 }
 
-template <int V>
+template <int V, bool FFN = false>
 void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, const float* hh, const float* wdw,
                          float* gh, float* gw, float* gdot, int B, int hid, int H, int W, hipStream_t s) {
   const int64_t planes = (int64_t)B * hid;
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+  if constexpr (FFN) {   // the FeedForward reverse always recomputes the depthwise output
+    hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, true, true>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw,
+                       gdot, hid, H, W, sseg, nsegs, nwaves);
+    return;
+  }
   if (hp)
     hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, false>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot,
                        hid, H, W, sseg, nsegs, nwaves);
@@ -740,14 +776,15 @@ void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, c
                        hid, H, W, sseg, nsegs, nwaves);
 }
 
-template <int V>
+template <int V, bool FFN = false>
 void launch_dw3_gate_fwd_row(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
                              hipStream_t s) {
   const int64_t planes = (int64_t)B * hid;
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
-  hipLaunchKernelGGL(dw3_gate_row_fwd_kernel<V>, grid, dim3(NT), 0, s, hh, wdw, gate, hid, H, W, sseg, nsegs, nwaves);
+  hipLaunchKernelGGL((dw3_gate_row_fwd_kernel<V, FFN>), grid, dim3(NT), 0, s, hh, wdw, gate, hid, H, W, sseg, nsegs,
+                     nwaves);
 }
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
@@ -863,6 +900,44 @@ grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* s
     default: launch_dw3_gate_row<4>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
   }
   return launch_status("grr_lnb_gate_dw3_bwd");
+}
+
+grr_status grr_ffn_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
+                            void* stream) {
+  clear_error();
+  GRR_REQUIRE(hh && wdw && gate && B > 0 && hid > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
+              "grr_ffn_dw3_gate: bad args");
+  const int V = dw3_row_vec(W);
+  const bool aligned = V > 0 && (uintptr_t)hh % (4u * V) == 0 && (uintptr_t)gate % (4u * V) == 0;
+  GRR_REQUIRE(aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_ffn_dw3_gate: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  hipStream_t s = (hipStream_t)stream;
+  switch (V) {
+    case 1: launch_dw3_gate_fwd_row<1, true>(hh, wdw, gate, B, hid, H, W, s); break;
+    case 2: launch_dw3_gate_fwd_row<2, true>(hh, wdw, gate, B, hid, H, W, s); break;
+    default: launch_dw3_gate_fwd_row<4, true>(hh, wdw, gate, B, hid, H, W, s); break;
+  }
+  return launch_status("grr_ffn_dw3_gate");
+}
+
+grr_status grr_ffn_gate_dw3_bwd(const float* gq, const float* scale, const float* hh, const float* wdw, float* gh,
+                                float* gwdw, float* gdot, int B, int hid, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(gq && scale && hh && wdw && gh && gwdw && gdot && B > 0 && hid > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_ffn_gate_dw3_bwd: bad args");
+  const int V = dw3_row_vec(W);
+  const void* ptrs[] = {gq, hh, gh};
+  bool aligned = true;
+  for (const void* p : ptrs) aligned = aligned && (uintptr_t)p % (4u * (V > 0 ? V : 1)) == 0;
+  GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_ffn_gate_dw3_bwd: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  hipStream_t s = (hipStream_t)stream;
+  switch (V) {
+    case 1: launch_dw3_gate_row<1, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+    case 2: launch_dw3_gate_row<2, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+    default: launch_dw3_gate_row<4, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+  }
+  return launch_status("grr_ffn_gate_dw3_bwd");
 }
 
 grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,

@@ -940,6 +940,31 @@ def lnb_dw3_gate(hh: Tensor, wdw: Tensor) -> Tensor:
     return gate
 
 
+def ffn_dw3_gate(hh: Tensor, wdw: Tensor) -> Tensor:
+    """gate = gelu(d1) d2 of [d1; d2] = zero-padded dwconv3(hh) (the window FeedForward, REF7:29-48;
+    grr_ffn_dw3_gate, the depthwise output not stored)."""
+    dev = _check("ffn_dw3_gate", hh, wdw)
+    b, c2, h, w = hh.shape
+    gate = torch.empty((b, c2 // 2, h, w), dtype=torch.float32, device=dev)
+    _launch("ffn_dw3_gate", 4 * (hh.numel() + gate.numel()), "grr_ffn_dw3_gate", hh.data_ptr(), wdw.data_ptr(),
+            gate.data_ptr(), b, c2 // 2, h, w, _stream(dev))
+    return gate
+
+
+def ffn_gate_dw3_bwd(gq: Tensor, scale: Tensor, hh: Tensor, wdw: Tensor, gwdw: Tensor, gdot: Tensor) -> Tensor:
+    """Reverse of ffn_dw3_gate with the skip scale (grr_ffn_gate_dw3_bwd): returns gh; gwdw += ;
+    gdot[0] += <gq, gate>."""
+    dev = _check("ffn_gate_dw3_bwd", gq, scale, hh, wdw, gwdw, gdot)
+    b, c2, h, w = hh.shape
+    if tuple(gq.shape) != (b, c2 // 2, h, w):
+        raise ValueError("ffn_gate_dw3_bwd: shapes")
+    gh = torch.empty_like(hh)
+    _launch("ffn_gate_dw3_bwd", 4 * (gq.numel() + hh.numel() + gh.numel()), "grr_ffn_gate_dw3_bwd", gq.data_ptr(),
+            scale.data_ptr(), hh.data_ptr(), wdw.data_ptr(), gh.data_ptr(), gwdw.data_ptr(), gdot.data_ptr(), b,
+            c2 // 2, h, w, _stream(dev))
+    return gh
+
+
 def lnb_gate(hp: Tensor, ggate: Optional[Tensor] = None, want_gate: bool = True):
     """gate = sigmoid(m) m v of hp = [m; v]; with ggate also the reverse ghp.  Returns (gate, ghp)."""
     dev = _check("lnb_gate", hp, ggate)

@@ -722,6 +722,56 @@ class LNBFn:
         return LNB([], x, ln_w, w1, wdw, w2, skip)
 
 
+# ---- FFBlock of the window models' feature CNN (REF7:13-67), training --------------------------
+# out = s0 x + s1 W_out (gelu(d1) d2), [d1; d2] = dwconv3x3_zero(W_in LN(x)): HIP forward
+# (grr_ffn_forward); the reverse recomputes n, hh and the gate and runs the adjoints on HIP kernels
+# (split-bf16 GEMMs for the data gradients, grr_wgrad for the weight gradients, one row pass for the
+# gate + depthwise reverse).  Row kernels: W <= 256 (the window models train on 64 / 256 patches).
+def _ffn_fwd(consts, x: Tensor, ln_w: Tensor, w_in: Tensor, w_dw: Tensor, w_out: Tensor, skip: Tensor):
+    c, hid2 = x.shape[1], w_in.shape[0]
+    out = K.ffn_forward(x.contiguous(), ln_w.reshape(c).contiguous(), _mat(w_in, hid2).contiguous(),
+                        _mat(w_dw, hid2).contiguous(), _mat(w_out, c).contiguous(), skip.contiguous())
+    return [out], []
+
+
+def _ffn_bwd(consts, inputs, outs, saved, gouts, needs):
+    x, ln_w, w_in, w_dw, w_out, skip = inputs
+    gout = gouts[0].contiguous()
+    b, c, h, w = x.shape
+    hid2 = w_in.shape[0]
+    hid = hid2 // 2
+    lnw, Win, Wdw, Wout = ln_w.reshape(c).contiguous(), _mat(w_in, hid2).contiguous(), \
+        _mat(w_dw, hid2).contiguous(), _mat(w_out, c).contiguous()
+    n, isd = K.lnb_norm(x, lnw)
+    hh = K.conv1x1(n, Win.view(hid2, c, 1, 1))
+    gate = K.ffn_dw3_gate(hh, Wdw)
+    gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
+    K.bwd_graph_dot(gout, x, gskip[0:1], 1)
+    s1 = skip[1:2].contiguous()
+    gw_out = K.wgrad(gout, gate) * s1                  # d/dW_out of s1 W_out gate
+    del gate
+    gq = K.conv1x1(gout, Wout.t().contiguous().view(hid, c, 1, 1))
+    gwdw = torch.zeros_like(Wdw)
+    gh = K.ffn_gate_dw3_bwd(gq, s1, hh, Wdw, gwdw, gskip[1:2])   # <gq, gate> = <gout, W_out gate>
+    del gq, hh
+    gw_in = K.wgrad(gh, n)
+    gn = K.conv1x1(gh, Win.t().contiguous().view(c, hid2, 1, 1))
+    del gh, n
+    gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
+    glnw = torch.zeros_like(lnw)
+    K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
+    return gx, glnw.view_as(ln_w), gw_in.view_as(w_in), gwdw.view_as(w_dw), gw_out.view_as(w_out), gskip
+
+
+FFN = OpaqueFunction("ffn_train", 1, _ffn_fwd, _ffn_bwd, _lnb_fake)
+
+
+class FFNFn:
+    @staticmethod
+    def apply(x: Tensor, ln_w: Tensor, w_in: Tensor, w_dw: Tensor, w_out: Tensor, skip: Tensor) -> Tensor:
+        return FFN([], x, ln_w, w_in, w_dw, w_out, skip)
+
+
 # ---- the GLRFast / GTVFast module methods, differentiable (REF:128-228, :452-516) ------------
 # Forward: the standalone sub-API kernels (csrc/subapi_ops.hip); reverse: csrc/subapi_bwd.hip.
 # Stencil inputs are the module's four stats_kernel_p* parameters; tap gradients come back per

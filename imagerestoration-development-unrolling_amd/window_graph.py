@@ -64,8 +64,9 @@ def window_edges(connection_window) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------
-# Feature CNN (REF7:13-270): FFBlocks on grr_ffn_forward in inference; the 3x3 convs (embedding,
-# down / up sampling, output) and the training path on stock PyTorch-ROCm convolutions
+# Feature CNN (REF7:13-270): FFBlocks on grr_ffn_forward in inference and on solver_grad.FFNFn (HIP
+# forward + reverse) in training; the 3x3 convs (embedding, down / up sampling, output) on stock
+# PyTorch-ROCm convolutions
 # ---------------------------------------------------------------------------
 class CustomLayerNorm(nn.Module):
     """x / sqrt(var_c(x) + 1e-5) (unbiased, uncentred), then a per-channel scale (REF7:13-26)."""
@@ -108,6 +109,11 @@ class FFBlock(nn.Module):
 
     def forward(self, x):
         ffn = self.ffn
+        if x.is_cuda and ffn.project_in.bias is None and records_grad(self, x) and K.lnb_gate_dw3_ok(*x.shape[2:]):
+            # training: HIP forward + HIP reverse (solver_grad.FFNFn)
+            from .solver_grad import FFNFn
+            return FFNFn.apply(x.contiguous(), self.norm.weighted_transform.weight, ffn.project_in.weight,
+                               ffn.dwconv.weight, ffn.project_out.weight, self.skip_connect_weight_final)
         if x.is_cuda and ffn.project_in.bias is None and not records_grad(self, x) \
                 and not torch.compiler.is_compiling():
             # inference: the whole block as one grr_ffn_forward (split-bf16 MFMA GEMMs, gelu gate)
@@ -117,7 +123,7 @@ class FFBlock(nn.Module):
                                  ffn.dwconv.weight.reshape(2 * hid, 9).contiguous(),
                                  ffn.project_out.weight.reshape(c, hid).contiguous(),
                                  self.skip_connect_weight_final.contiguous())
-        # training (autograd) and biased variants: stock PyTorch-ROCm ops
+        # biased variants, rows wider than the row kernels: stock PyTorch-ROCm ops
         return self.skip_connect_weight_final[0] * x + self.skip_connect_weight_final[1] * self.ffn(self.norm(x))
 
 

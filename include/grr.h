@@ -403,6 +403,14 @@ grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* s
                                 const float* wdw, float* gh, float* gwdw, float* gdot, int B, int hid, int H, int W,
                                 void* stream);
 
+/* The same two row passes for the window models' FeedForward (REF7:29-48): zero-padded depthwise
+ * (nn.Conv2d padding=1) and gate = gelu(d1) d2 (exact erf gelu); the reverse recomputes the depthwise
+ * output from hh (no hp operand) and adds <gq, gate> to gdot[0]. */
+grr_status grr_ffn_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
+                            void* stream);
+grr_status grr_ffn_gate_dw3_bwd(const float* gq, const float* scale, const float* hh, const float* wdw, float* gh,
+                                float* gwdw, float* gdot, int B, int hid, int H, int W, void* stream);
+
 /* ---- window graphs (older image-domain models) ------------------------------
  * REF7 = exploration/model_multiscale_mixture_GLR/lib/model_GLR_GTV_deep_v7.py,
  * REF1 = .../lib/model_GLR_GTV_deep_v1.py.  Graphs connect each pixel to the K

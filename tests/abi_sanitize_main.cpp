@@ -83,6 +83,10 @@ int main() {
   EXPECT_ERR(grr_lnb_gate_bwd_scaled(n, n, n, n, n, 1, 4, 64, s));
   EXPECT_ERR(grr_lnb_gate_dw3_bwd(n, n, n, n, n, n, n, n, 1, 4, 8, 8, s));
   EXPECT_ERR(grr_lnb_dw3_gate(n, n, n, 1, 4, 8, 8, s));
+  EXPECT_ERR(grr_ffn_dw3_gate(n, n, n, 1, 4, 8, 8, s));
+  EXPECT_ERR(grr_ffn_gate_dw3_bwd(n, n, n, n, n, n, n, 1, 4, 8, 8, s));
+  EXPECT_ERR(grr_ffn_forward(n, n, n, n, n, n, n, n, 1, 8, 16, 8, 8, s));
+  EXPECT_ERR(grr_wgrad(n, n, n, n, 1, 8, 8, 64, s));
   const int32_t delta[4] = {-1, 0, 0, -1};
   EXPECT_ERR(grr_win_edge_weights(n, 0, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_solver(0, n, 0, n, n, n, n, n, n, n, n, n, n, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));

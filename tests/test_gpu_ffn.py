@@ -66,9 +66,37 @@ def test_feature_extraction_matches_cpu(W):
     assert _rel(got, ref) <= 1e-4
 
 
-def test_ffblock_training_path_unchanged(W):
-    """With autograd recording the block stays on the PyTorch ops (gradients flow)."""
+@pytest.mark.parametrize("shape", [(2, 32, 16, 24), (1, 128, 33, 64), (1, 48, 20, 128), (1, 64, 12, 256)])
+def test_ffblock_gradients_match_float64(W, shape):
+    """Training path (solver_grad.FFNFn: HIP forward, HIP reverse with the zero-pad / gelu row kernels)
+    against float64 autograd of the module's PyTorch ops on the CPU: the input and every parameter
+    (CustomLayerNorm scale, W_in, depthwise taps, W_out, skip weights).  Row widths V = 1 / 2 / 4."""
+    b, c, h, w = shape
+    blk = _block(W, c, seed=c + w)
+    x = torch.randn(b, c, h, w, generator=torch.Generator().manual_seed(9))
+    gout = torch.randn(b, c, h, w, generator=torch.Generator().manual_seed(10))
+    ref = copy.deepcopy(blk).double()
+    xr = x.double().requires_grad_(True)
+    ref(xr).backward(gout.double())
+    dev = copy.deepcopy(blk).to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    out = dev(xd)
+    out.backward(gout.to(DEV))
+    assert _rel(xd.grad, xr.grad) <= 1e-4, "x"
+    for (k, pr), (_, pd) in zip(ref.named_parameters(), dev.named_parameters()):
+        assert _rel(pd.grad, pr.grad) <= 1e-4, k
+
+
+def test_ffblock_training_uses_hip(W):
+    """The recorded graph of a CUDA FFBlock is the opaque HIP op, not the stock conv ops."""
     blk = _block(W, 32, seed=1).to(DEV)
     x = torch.randn(1, 32, 8, 8, device=DEV, requires_grad=True)
-    blk(x).sum().backward()
+    out = blk(x)
+    names = []
+    fn = out.grad_fn
+    while fn is not None and len(names) < 8:
+        names.append(type(fn).__name__)
+        fn = fn.next_functions[0][0] if fn.next_functions else None
+    assert not any("Convolution" in n for n in names), names
+    out.sum().backward()
     assert x.grad is not None and blk.ffn.project_in.weight.grad is not None
