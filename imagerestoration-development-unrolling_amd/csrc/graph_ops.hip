@@ -1361,6 +1361,8 @@ struct Step2Args {
   float* out;
   float* u_out;
   float* xd_out;
+  float* x_mid;          // training: x_{k+1} and u_{k+1} (the reverse sweep's saved iterates), or NULL
+  float* u_mid;
   int G, F, H, nsegs, sseg;
   int FG, ngrp;         // channel groups of <= S2_FMAX channels per (b, graph): FG channels each (the last may hold fewer)
   uint32_t nblk;
@@ -1510,6 +1512,7 @@ static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
 constexpr int S2_PRODUCER = S2_FMAX, S2_HALFW = 2 * S2_FMAX + 1;
 constexpr int S2_THREADS = 64 * (2 * S2_FMAX + 2);
 
+template <bool MID>
 __global__ __launch_bounds__(S2_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void graph_step2_kernel(Step2Args a) {
   constexpr int V = 4, VH = 2, W = S2_W, hw = S2_HW;
@@ -1737,6 +1740,10 @@ void graph_step2_kernel(Step2Args a) {
   const rsrc_t rout = make_rsrc(a.out + plane, PB);
   const rsrc_t ruo = make_rsrc(a.u_out ? a.u_out + plane : nullptr, PB);
   const rsrc_t rxd = make_rsrc(a.xd_out ? a.xd_out + hplane : nullptr, HPB);
+  // MID (training): the middle iterate x_{k+1}, u_{k+1} also goes to HBM (a separate instance, so the
+  // inference kernel keeps its registers)
+  const rsrc_t rxm = make_rsrc(MID ? a.x_mid + plane : nullptr, MID ? PB : 0);
+  const rsrc_t rum = make_rsrc(MID ? a.u_mid + plane : nullptr, MID ? PB : 0);
 
   const float scl0 = expf(a.log_mu0[g]), scg0 = expf(a.log_ro0[g]);
   // absent terms enter as exact zeros / ones: u_prev reads 0 (beta 0), y reads 0 (skip 0, 1)
@@ -1830,6 +1837,11 @@ void graph_step2_kernel(Step2Args a) {
     if (y >= 0 && y < H) {   // uniform: rows outside the image never enter the rings
       st4(xr + (y & (S2_XR - 1)) * S2_W, xn);
       st4(ur + (y % S2_UR) * S2_W, u);
+    }
+    if constexpr (MID) {     // training: the middle iterate's rows of this segment to HBM
+      const uint32_t so = (y >= r0 && y < r1) ? vo + (uint32_t)y * RB : GRR_OOB;
+      bstore<V>(rxm, so, xn);
+      bstore<V>(rum, so, u);
     }
     if constexpr (PAR == 0) {
 #pragma unroll
@@ -2231,14 +2243,14 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
   return launch_op<false, GTV_PAIR, EPI_STEP>(a, B, s, "grr_system_step");
 }
 
-grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* xd,
-                            const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
-                            const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
-                            grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
-                            const float* alpha_a, const float* beta_a, const float* alpha_b, const float* beta_b,
-                            const float* skip, const float* y_skip, float* x_out, float* u_out, float* xd_out,
-                            int B, int G, int F, int H, int W, void* stream) {
-  clear_error();
+static grr_status system_step2_impl(const float* x, const float* b, const float* u_prev, const float* xd,
+                                    const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
+                                    const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
+                                    grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
+                                    const float* alpha_a, const float* beta_a, const float* alpha_b,
+                                    const float* beta_b, const float* skip, const float* y_skip, float* x_out,
+                                    float* u_out, float* xd_out, float* x_mid, float* u_mid, int B, int G, int F,
+                                    int H, int W, void* stream) {
   GRR_REQUIRE(x && b && xd && wL0 && cG0 && wL1 && cG1 && log_mu0 && log_ro0 && log_mu1 && log_ro1 && alpha_a &&
                   alpha_b && x_out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_system_step2: bad args");
@@ -2251,10 +2263,11 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_system_step2: plane too large");
   GRR_REQUIRE(x_out != x && x_out != b && x_out != u_prev && (!u_out || (u_out != u_prev && u_out != x && u_out != b)),
               GRR_ERR_INVALID_ARG, "grr_system_step2: outputs must not alias the inputs (rows are read ahead)");
-  const void* ptrs[] = {x, b, u_prev, xd, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out};
+  const void* ptrs[] = {x, b, u_prev, xd, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out, x_mid, u_mid};
   for (const void* q : ptrs)
     GRR_REQUIRE((uintptr_t)q % 16 == 0, GRR_ERR_INVALID_ARG, "grr_system_step2: operands must be 16-byte aligned");
   Step2Args a{};
+  a.x_mid = x_mid; a.u_mid = u_mid;
   a.x = x; a.b = b; a.u_prev = u_prev; a.xd = xd;
   a.wL0 = wL0; a.cG0 = cG0; a.wL1 = wL1; a.cG1 = cG1;
   a.sL0 = sL0; a.sG0 = sG0; a.sL1 = sL1; a.sG1 = sG1;
@@ -2269,9 +2282,41 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   const uint64_t nblk = (uint64_t)B * G * a.ngrp * a.nsegs;
   GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_step2: grid too large");
   a.nblk = (uint32_t)nblk;
-  hipLaunchKernelGGL(graph_step2_kernel, dim3(a.nblk), dim3(S2_THREADS), 0,
-                     (hipStream_t)stream, a);
+  if (x_mid)
+    hipLaunchKernelGGL(graph_step2_kernel<true>, dim3(a.nblk), dim3(S2_THREADS), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(graph_step2_kernel<false>, dim3(a.nblk), dim3(S2_THREADS), 0, (hipStream_t)stream, a);
   return launch_status("grr_system_step2");
+}
+
+grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* xd,
+                            const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
+                            const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
+                            grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
+                            const float* alpha_a, const float* beta_a, const float* alpha_b, const float* beta_b,
+                            const float* skip, const float* y_skip, float* x_out, float* u_out, float* xd_out,
+                            int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  return system_step2_impl(x, b, u_prev, xd, wL0, cG0, sL0, sG0, log_mu0, log_ro0, wL1, cG1, sL1, sG1, log_mu1,
+                           log_ro1, alpha_a, beta_a, alpha_b, beta_b, skip, y_skip, x_out, u_out, xd_out, nullptr,
+                           nullptr, B, G, F, H, W, stream);
+}
+
+grr_status grr_system_step2_train(const float* x, const float* b, const float* u_prev, const float* xd,
+                                  const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
+                                  const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
+                                  grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
+                                  const float* alpha_a, const float* beta_a, const float* alpha_b,
+                                  const float* beta_b, float* x_out, float* u_out, float* xd_out, float* x_mid,
+                                  float* u_mid, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x_mid && u_mid && u_out, GRR_ERR_INVALID_ARG, "grr_system_step2_train: x_mid, u_mid, u_out required");
+  GRR_REQUIRE(x_mid != x && x_mid != b && x_mid != u_prev && x_mid != x_out && x_mid != u_out && u_mid != x &&
+                  u_mid != b && u_mid != u_prev && u_mid != x_out && u_mid != u_out && x_mid != u_mid,
+              GRR_ERR_INVALID_ARG, "grr_system_step2_train: x_mid / u_mid must not alias other operands");
+  return system_step2_impl(x, b, u_prev, xd, wL0, cG0, sL0, sG0, log_mu0, log_ro0, wL1, cG1, sL1, sG1, log_mu1,
+                           log_ro1, alpha_a, beta_a, alpha_b, beta_b, nullptr, nullptr, x_out, u_out, xd_out, x_mid,
+                           u_mid, B, G, F, H, W, stream);
 }
 
 grr_status grr_glr_stage(const float* x, const float* b, const float* u_prev, const float* wL, grr_stencil sL,

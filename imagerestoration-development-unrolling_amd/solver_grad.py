@@ -205,13 +205,26 @@ def _mixture_fwd(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
         t = K.gtv_rhs_half(xd, wG1, sG1, True, p["gamma01"], g)
         b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, p["gamma00"], ro0, t, ro1, g)
         u = None
-        for k in range(1, n_st):
+        pair = K.STEP2 and K.step2_supported(x, g)
+        k = 1
+        while k < n_st:
+            if pair and k + 1 < n_st:
+                # stages k, k+1 in one pass; the middle iterate is written for the reverse sweep
+                last = k + 1 == n_st - 1
+                xm, um, x, u, xd = K.system_step2_train(x, b_b, u, xd, wL0, cG0, sL0, sG0, mu0, ro0, wL1, cG1, sL1,
+                                                        sG1, mu1, ro1, alpha[k], beta[k] if k >= 2 else None,
+                                                        alpha[k + 1], beta[k + 1], g, want_pool=not last)
+                xs += [xm, x]
+                us += [um, u]
+                k += 2
+                continue
             last = k == n_st - 1
             t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
             x, u, xd = K.system_step(x, b_b, u, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[k],
                                      beta[k] if k >= 2 else None, g, want_u=True, want_pool=not last)
             xs.append(x)
             us.append(u)
+            k += 1
         del b_b
     return [xs[-1]], [wG0, wL0, wG1, wL1, cG0, cG1, *xs[:-1], *us]
 

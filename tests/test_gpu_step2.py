@@ -148,3 +148,36 @@ def test_filter_with_step2_matches_per_stage_launches_and_oracle(irdu, b):
     ref = O.multiscale_graph_filter(noisy, sd_cpu(m), 8)
     assert rel_err(fused, ref) <= 1e-4
     assert abs(O.psnr_ubyte(fused, clean) - O.psnr_ubyte(ref, clean)) <= 0.01
+
+
+@pytest.mark.parametrize("n_st", [4, 5])
+def test_training_forward_with_step2_matches_per_stage(irdu, n_st):
+    """The training forward (grr_system_step2_train: pairs that also write the middle iterate for the
+    reverse sweep) against one stage per launch: output, loss gradient of the input and of every
+    parameter of the image filter (S = 4: pair (1,2) + stage 3; S = 5: pairs (1,2), (3,4))."""
+    from irdu_amd import kernels as K
+    torch.manual_seed(2400 + n_st)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=4, n_cgd_iters=n_st)
+    perturb_mixture(m.localfilter, 24 + n_st)
+    x = torch.rand(2, 3, 32, 256)
+    gout = torch.randn(2, 3, 32, 256)
+    md = m.to(DEV).train()
+    saved = K.STEP2
+    res = {}
+    try:
+        for flag in (True, False):
+            K.STEP2 = flag
+            md.zero_grad(set_to_none=True)
+            xd = x.to(DEV).requires_grad_(True)
+            out = md(xd)
+            out.backward(gout.to(DEV))
+            res[flag] = (out.detach().cpu(), xd.grad.cpu(),
+                         {k: p.grad.detach().cpu() for k, p in md.named_parameters() if p.grad is not None})
+    finally:
+        K.STEP2 = saved
+    (o1, g1, p1), (o0, g0, p0) = res[True], res[False]
+    assert rel_err(o1, o0) <= 1e-5
+    assert rel_err(g1, g0) <= 1e-5
+    assert p1.keys() == p0.keys()
+    for k in p0:
+        assert rel_err(p1[k], p0[k]) <= 1e-4, k
