@@ -823,6 +823,11 @@ grr_status grr_conv1x1_ws(const float* x, const float* wt, float* out, void* wor
                      wt, nullptr, frag, M, K, KS, nch);
   grr_status st = launch_status("grr_conv1x1_ws/pack");
   if (st != GRR_OK) return st;
+  if ((int64_t)K * P >= (1ll << 30) || (int64_t)M * P >= (1ll << 30)) {   // past the 32-bit lane offsets
+    GemmArgs g{};
+    g.x = x; g.wt = wt; g.out = out; g.K = K; g.M = M; g.P = P;
+    return launch_gemm<LD_PLAIN, EP_STORE>(g, B, s, "grr_conv1x1_ws/fp32");
+  }
   if (K > 128) return launch_x3k(x, frag, out, B, K, M, P, s, "grr_conv1x1_ws");
   return launch_x3<false>(x, frag, out, B, K, M, P, s, "grr_conv1x1_ws");
 }

@@ -270,6 +270,15 @@ __device__ __forceinline__ float dpp_next(float v) {
   return r;
 }
 
+// Rows wider than one wave (W > 64 V, W % V == 0) run as column strips: strip k's waves hold columns
+// [x0, x0 + 64 V), x0 = k STEP - V (0 for the first), and own the output columns [k STEP, (k + 1) STEP):
+// the V columns of each side are a halo (the depthwise reach is one column; DPP shifts stop at the
+// wave's ends), so no value the owned columns depend on crosses a wave.  Image-edge rules use the
+// global column.  Waves of neighbouring strips are neighbours in the grid (same row segment).
+__host__ __device__ inline int dw3_row_strips(int W, int V) {
+  const int step = 62 * V;
+  return W <= 64 * V ? 1 : (W + step - 1) / step;
+}
 struct Dw3RowGeom {
   int lane, c0, cl0;
   bool on;
@@ -280,14 +289,21 @@ __device__ __forceinline__ bool dw3_row_geom(Dw3RowGeom& q, int C, int H, int W,
   q.lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (wid >= nwaves) return false;   // whole waves only
-  const int seg = (int)(wid % nsegs);
-  q.plane = (int)(wid / nsegs);
+  constexpr int STEP = 62 * V;
+  const int nstrips = dw3_row_strips(W, V);
+  const int strip = (int)(wid % (uint32_t)nstrips);
+  const uint32_t rest = wid / (uint32_t)nstrips;
+  const int seg = (int)(rest % nsegs);
+  q.plane = (int)(rest / nsegs);
   q.c = q.plane % C;
   q.r0 = seg * sseg;
   q.r1 = min(q.r0 + sseg, H);
-  q.c0 = V * q.lane;
-  q.on = q.c0 < W;
-  q.cl0 = q.on ? q.c0 : W - V;
+  const int x0 = strip == 0 ? 0 : strip * STEP - V;
+  const int lo = nstrips == 1 ? 0 : strip * STEP;
+  const int hi = nstrips == 1 ? W : min(lo + STEP, W);
+  q.c0 = x0 + V * q.lane;
+  q.on = q.c0 >= lo && q.c0 < hi;
+  q.cl0 = clampi(q.c0, 0, W - V);
   return true;
 }
 
@@ -719,7 +735,7 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
 int dw3_row_vec(int W) {
   if (W <= 64) return 1;
   if (W <= 128 && W % 2 == 0) return 2;
-  if (W <= 256 && W % 4 == 0) return 4;
+  if (W % 4 == 0) return 4;   // W > 256: column strips of 4-wide lanes
   return 0;
 }
 // rows per wave: whole planes while the grid has >= 4096 waves, else segments of >= 32 rows
@@ -731,7 +747,7 @@ int dw3_row_seg(int H, int64_t planes) {
 template <int V>
 void launch_dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gw, int B, int C,
                     int H, int W, hipStream_t s) {
-  const int64_t planes = (int64_t)B * C;
+  const int64_t planes = (int64_t)B * C * dw3_row_strips(W, V);   // (plane, strip) pairs
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
@@ -747,7 +763,7 @@ bool dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* 
   const void* ptrs[] = {g, h, out};
   for (const void* p : ptrs)
     if (p && (uintptr_t)p % (4u * V) != 0) return false;
-  if ((int64_t)B * C * ((H + 31) / 32) >= (1ll << 31)) return false;
+  if ((int64_t)B * C * dw3_row_strips(W, V) * ((H + 31) / 32) >= (1ll << 31)) return false;
   switch (V) {
     case 1: launch_dw3_row<1>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
     case 2: launch_dw3_row<2>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
@@ -759,7 +775,7 @@ bool dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* 
 template <int V, bool FFN = false>
 void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, const float* hh, const float* wdw,
                          float* gh, float* gw, float* gdot, int B, int hid, int H, int W, hipStream_t s) {
-  const int64_t planes = (int64_t)B * hid;
+  const int64_t planes = (int64_t)B * hid * dw3_row_strips(W, V);   // (plane, strip) pairs
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
@@ -779,7 +795,7 @@ void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, c
 template <int V, bool FFN = false>
 void launch_dw3_gate_fwd_row(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
                              hipStream_t s) {
-  const int64_t planes = (int64_t)B * hid;
+  const int64_t planes = (int64_t)B * hid * dw3_row_strips(W, V);   // (plane, strip) pairs
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
@@ -870,8 +886,8 @@ grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int 
               "grr_lnb_dw3_gate: bad args");
   const int V = dw3_row_vec(W);
   const bool aligned = V > 0 && (uintptr_t)hh % (4u * V) == 0 && (uintptr_t)gate % (4u * V) == 0;
-  GRR_REQUIRE(aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
-              "grr_lnb_dw3_gate: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  GRR_REQUIRE(aligned && (int64_t)B * hid * dw3_row_strips(W, V > 0 ? V : 1) * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_dw3_gate: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
   switch (V) {
     case 1: launch_dw3_gate_fwd_row<1>(hh, wdw, gate, B, hid, H, W, s); break;
@@ -891,8 +907,8 @@ grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* s
   const void* ptrs[] = {hp, gq, hh, gh};
   bool aligned = true;
   for (const void* p : ptrs) aligned = aligned && (uintptr_t)p % (4u * (V > 0 ? V : 1)) == 0;   // NULL hp passes
-  GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
-              "grr_lnb_gate_dw3_bwd: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * dw3_row_strips(W, V > 0 ? V : 1) * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_gate_dw3_bwd: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
   switch (V) {
     case 1: launch_dw3_gate_row<1>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
@@ -909,8 +925,8 @@ grr_status grr_ffn_dw3_gate(const float* hh, const float* wdw, float* gate, int 
               "grr_ffn_dw3_gate: bad args");
   const int V = dw3_row_vec(W);
   const bool aligned = V > 0 && (uintptr_t)hh % (4u * V) == 0 && (uintptr_t)gate % (4u * V) == 0;
-  GRR_REQUIRE(aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
-              "grr_ffn_dw3_gate: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  GRR_REQUIRE(aligned && (int64_t)B * hid * dw3_row_strips(W, V > 0 ? V : 1) * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_ffn_dw3_gate: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
   switch (V) {
     case 1: launch_dw3_gate_fwd_row<1, true>(hh, wdw, gate, B, hid, H, W, s); break;
@@ -929,8 +945,8 @@ grr_status grr_ffn_gate_dw3_bwd(const float* gq, const float* scale, const float
   const void* ptrs[] = {gq, hh, gh};
   bool aligned = true;
   for (const void* p : ptrs) aligned = aligned && (uintptr_t)p % (4u * (V > 0 ? V : 1)) == 0;
-  GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
-              "grr_ffn_gate_dw3_bwd: needs W <= 256 (W %% V == 0) and 4V-byte aligned planes");
+  GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * dw3_row_strips(W, V > 0 ? V : 1) * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_ffn_gate_dw3_bwd: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
   switch (V) {
     case 1: launch_dw3_gate_row<1, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;

@@ -934,7 +934,8 @@ def lnb_gate_bwd_scaled(hp: Tensor, gq: Tensor, scale: Tensor, gdot: Tensor) -> 
 
 
 def lnb_gate_dw3_ok(h: int, w: int) -> bool:
-    return (w <= 64) or (w <= 128 and w % 2 == 0) or (w <= 256 and w % 4 == 0)
+    """The depthwise / gate row kernels' widths (W > 256: column strips of 4-wide lanes)."""
+    return (w <= 64) or (w <= 128 and w % 2 == 0) or (w % 4 == 0)
 
 
 def lnb_gate_dw3_bwd(hp: Optional[Tensor], gq: Tensor, scale: Tensor, hh: Tensor, wdw: Tensor, gwdw: Tensor,
