@@ -894,7 +894,7 @@ __device__ __forceinline__ float lnext(float v) {   // lane + 1 (0 at lane 63)
 // VGPRs = 3 waves per SIMD, which also gives 4 three-wave workgroups per CU instead of 2 at the
 // 176-182 VGPRs the compiler picks unconstrained), up to 16 for V <= 2 (128 VGPRs).
 template <int V> struct TermRowMax { static constexpr int F = V == 4 ? 12 : 16; };
-template <int MODE, int V>
+template <int MODE, int V, bool STRIPS = false>
 __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
@@ -907,12 +907,30 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   const int lane = threadIdx.x & 63;
   const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t unit = xcd_remap(blockIdx.x, nblk);
+  // W > 64 V: column strips owning 62 V columns with V halo columns per side (the term's reach is two
+  // columns: s = P x and a = T* g at the pixel's neighbours), as the depthwise row kernels
+  // (a separate instance, so that the one-strip kernel keeps its registers)
+  constexpr int STEP = 62 * V;
+  int strip = 0, nstrips = 1;
+  if constexpr (STRIPS) {
+    nstrips = (W + STEP - 1) / STEP;
+    strip = (int)(unit % (uint32_t)nstrips);
+    unit /= (uint32_t)nstrips;
+  }
   const int seg = unit % nsegs;
   const int bg = unit / nsegs, gi = bg % G;
   const int r0 = seg * sseg, r1 = min(r0 + sseg, H);
-  const int c0 = V * lane;
-  const bool on = c0 < W;
-  const int cl0 = on ? c0 : W - V;
+  const int lc0 = V * lane;                  // the lane's slot in the LDS partial rows
+  int c0 = lc0;                              // global column
+  bool on = c0 < W;
+  int cl0 = on ? c0 : W - V;
+  if constexpr (STRIPS) {
+    const int x0 = strip == 0 ? 0 : strip * STEP - V;
+    const int lo = strip * STEP, hi = min(lo + STEP, W);
+    c0 = x0 + lc0;
+    on = c0 >= lo && c0 < hi;
+    cl0 = clampi(c0, 0, W - V);
+  }
   const int64_t HW = (int64_t)H * W;
   const float sc = scale ? scale[gi] : 1.f;
   const float gm = MODE == 2 ? expf(log_gamma[gi]) : 0.f;
@@ -1117,14 +1135,14 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     if (on) rstore<V>(vp + (int64_t)r * W, vrow);
     // weight gradient: partials of the F channels -> LDS -> sum in channel order -> gw
 #pragma unroll
-    for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + c0, gwa[e]);
+    for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
     __syncthreads();
     for (int e = f; e < WPL; e += F) {
       float sum[V];
-      rload<V>(sum, part(par, 0, e) + c0);
+      rload<V>(sum, part(par, 0, e) + lc0);
       for (int ff = 1; ff < F; ++ff) {
         float pv[V];
-        rload<V>(pv, part(par, ff, e) + c0);
+        rload<V>(pv, part(par, ff, e) + lc0);
 #pragma unroll
         for (int j = 0; j < V; ++j) sum[j] += pv[j];
       }
@@ -1165,6 +1183,8 @@ int term_row_vec(int W) {
   if (W <= 256 && W % 4 == 0) return 4;
   return 0;
 }
+// the term reverse also runs W > 256 (W % 4 == 0) as column strips of 4-wide lanes
+int term_strip_vec(int W) { return term_row_vec(W) ? term_row_vec(W) : (W % 4 == 0 ? 4 : 0); }
 // The same reverse as a row-streaming kernel (W <= 64 V, F in {1, 2, 3, 4, 6}): one wave = one
 // (b, graph) and a segment of rows, lane = V adjacent columns.  Feature rows r-1..r+1 of the F
 // channels, their inverse norms and gsim (4 planes) stay in registers; horizontal neighbours
@@ -1343,19 +1363,24 @@ void launch_term_row(int B, int F, const float* x, const float* g, const float* 
                      int G, int H, int W, hipStream_t s) {
   // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
   int sseg = H;
-  const int64_t graphs = (int64_t)B * G;
+  const int nstrips = W <= 64 * V ? 1 : (W + 62 * V - 1) / (62 * V);
+  const int64_t graphs = (int64_t)B * G * nstrips;   // (b, graph, strip) units
   while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
   const size_t lds = (size_t)2 * F * (MODE == 1 ? 2 : 4) * 64 * V * sizeof(float);
-  hipLaunchKernelGGL((term_row_kernel<MODE, V>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale, coef, v,
-                     gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
+  if (nstrips > 1)
+    hipLaunchKernelGGL((term_row_kernel<MODE, V, true>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale,
+                       coef, v, gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
+  else
+    hipLaunchKernelGGL((term_row_kernel<MODE, V, false>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale,
+                       coef, v, gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
 }
 template <int MODE>
 bool launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
                        const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot,
                        float* gtaps, int G, int H, int W, hipStream_t s) {
-  const int V = term_row_vec(W);
+  const int V = term_strip_vec(W);
   if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return false;
   const void* ptrs[] = {x, g, w, v, gw};
   for (const void* p : ptrs)

@@ -134,7 +134,7 @@ def term_rows_ok(w: int, f: int) -> bool:
         return f <= 16
     if w <= 128 and w % 2 == 0:
         return f <= 16
-    return w <= 256 and w % 4 == 0 and f <= 12
+    return w % 4 == 0 and f <= 12   # W > 256: column strips
 
 
 def set_kernel_variant(variant: str) -> None:

@@ -1,4 +1,4 @@
-"""grr_bwd_term_fused's row-streaming kernel (W <= 256) against its per-pixel kernel, for the three
+"""grr_bwd_term_fused's row-streaming kernel (W <= 256; wider rows as column strips) against its per-pixel kernel, for the three
 operator terms (GLR, pair Laplacian, prox) and every instantiated F: the v output, the weight
 gradient (summed over the graph's channels through LDS), and the per-graph / per-channel
 reductions (<a, z>, gamma, taps).  The per-pixel kernel is itself pinned by the gradient tests
@@ -10,8 +10,9 @@ from tests.test_gpu_parity import DEV, rel_err
 
 pytestmark = pytest.mark.gpu
 
+# W > 256: column strips of 248 owned columns (300: 2 strips, 512: 3, 744: 3 whole strips)
 CASES = [(2, 4, 3, 20, 256), (1, 3, 1, 9, 32), (1, 2, 2, 17, 100), (1, 2, 4, 70, 200), (3, 2, 3, 2, 64),
-         (1, 1, 3, 300, 128)]
+         (1, 1, 3, 300, 128), (1, 2, 3, 11, 300), (1, 2, 4, 8, 512), (1, 1, 2, 6, 744)]
 
 
 @pytest.fixture(scope="module")
@@ -56,11 +57,20 @@ def test_term_rows_equal_per_pixel(K, case, mode):
         if r is None:
             continue
         assert torch.isfinite(a).all(), name
-        tol = 2e-6 if name in ("v", "gw") else 2e-5
-        assert rel_err(a, r) <= tol, (name, rel_err(a, r))
+        if name in ("v", "gw"):
+            assert rel_err(a, r) <= 2e-6, (name, rel_err(a, r))
+        else:
+            # reductions of O(1) terms in two summation orders: fp32 error grows like sqrt(N) eps,
+            # so a sum that cancels to far below sqrt(N) is held to that scale (a missing or doubled
+            # column would still be off by O(rows x channels))
+            n = b * F * h * w_
+            scale = max(float(r.abs().max()), n ** 0.5)
+            err = float((a.double() - r.double()).abs().max())
+            assert err <= 2e-5 * scale, (name, err, scale)
 
 
-WIDE_F = [(2, 2, 6, 18, 256), (1, 2, 12, 9, 256), (1, 2, 16, 7, 128), (2, 1, 12, 12, 64), (1, 1, 6, 5, 32)]
+WIDE_F = [(2, 2, 6, 18, 256), (1, 2, 12, 9, 256), (1, 2, 16, 7, 128), (2, 1, 12, 12, 64), (1, 1, 6, 5, 32),
+          (1, 2, 6, 7, 512), (1, 1, 12, 5, 300)]
 
 
 @pytest.mark.parametrize("case", WIDE_F, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
