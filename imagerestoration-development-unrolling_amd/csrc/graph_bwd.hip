@@ -1190,7 +1190,7 @@ int term_strip_vec(int W) { return term_row_vec(W) ? term_row_vec(W) : (W % 4 ==
 // channels, their inverse norms and gsim (4 planes) stay in registers; horizontal neighbours
 // come from DPP lane shifts.  feat, w, gw read once, gfeat written once (the per-pixel kernel
 // re-reads each feature plane ~12 times through L1/L2, 1.1 TB/s).
-template <int F, int V>
+template <int F, int V, bool STRIPS = false>
 __global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restrict__ feat, int64_t fstride,
                                                           const float* __restrict__ multiM,
                                                           const float* __restrict__ w, const float* __restrict__ gw,
@@ -1200,12 +1200,29 @@ __global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restric
   const int lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (wid >= nwaves) return;   // whole waves; no barriers below
-  const int seg = (int)(wid % nsegs);
-  const int bg = (int)(wid / nsegs), g = bg % G, b = bg / G;
+  // STRIPS (W > 64 V): 62 V owned columns per wave with V halo columns per side (reach: one column),
+  // as term_row_kernel
+  uint32_t unit = wid;
+  int strip = 0;
+  constexpr int STEP = 62 * V;
+  if constexpr (STRIPS) {
+    const int nstrips = (W + STEP - 1) / STEP;
+    strip = (int)(unit % (uint32_t)nstrips);
+    unit /= (uint32_t)nstrips;
+  }
+  const int seg = (int)(unit % nsegs);
+  const int bg = (int)(unit / nsegs), g = bg % G, b = bg / G;
   const int r0 = seg * sseg, r1 = min(r0 + sseg, H);
-  const int c0 = V * lane;
-  const bool on = c0 < W;
-  const int cl0 = on ? c0 : W - V;
+  int c0 = V * lane;
+  bool on = c0 < W;
+  int cl0 = on ? c0 : W - V;
+  if constexpr (STRIPS) {
+    const int x0 = strip == 0 ? 0 : strip * STEP - V;
+    const int lo = strip * STEP, hi = min(lo + STEP, W);
+    c0 = x0 + V * lane;
+    on = c0 >= lo && c0 < hi;
+    cl0 = clampi(c0, 0, W - V);
+  }
   const int64_t HW = (int64_t)H * W;
   const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW + cl0;
   float* gfp = gfeat + (int64_t)b * gstride + (int64_t)g * F * HW + cl0;
@@ -1331,13 +1348,14 @@ __global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restric
 
 bool launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM, const float* w, const float* gw,
                          float* gfeat, int64_t gstride, float* gM, int B, int G, int F, int H, int W, hipStream_t s) {
-  const int V = term_row_vec(W);
+  const int V = term_strip_vec(W);
   if (V == 0) return false;
   if (fstride % V != 0 || gstride % V != 0 || ((int64_t)H * W) % V != 0) return false;
   const void* ptrs[] = {feat, w, gw, gfeat};
   for (const void* p : ptrs)
     if ((uintptr_t)p % (4u * V) != 0) return false;
-  const int64_t planes = (int64_t)B * G;
+  const int nstrips = W <= 64 * V ? 1 : (W + 62 * V - 1) / (62 * V);
+  const int64_t planes = (int64_t)B * G * nstrips;   // (b, graph, strip) units
   int sseg = H;
   while (sseg > 32 && planes * ((H + sseg - 1) / sseg) < 4096) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
@@ -1345,8 +1363,12 @@ bool launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
 #define GRR_EDGE_BWD_CASE(FF, VV)                                                                              \
   if (F == FF && V == VV) {                                                                                    \
-    hipLaunchKernelGGL((edge_row_bwd_kernel<FF, VV>), grid, dim3(NT), 0, s, feat, fstride, multiM, w, gw, gfeat, \
-                       gstride, gM, G, H, W, sseg, nsegs, nwaves);                                             \
+    if (nstrips > 1)                                                                                           \
+      hipLaunchKernelGGL((edge_row_bwd_kernel<FF, VV, true>), grid, dim3(NT), 0, s, feat, fstride, multiM, w, gw, \
+                         gfeat, gstride, gM, G, H, W, sseg, nsegs, nwaves);                                    \
+    else                                                                                                       \
+      hipLaunchKernelGGL((edge_row_bwd_kernel<FF, VV, false>), grid, dim3(NT), 0, s, feat, fstride, multiM, w, gw, \
+                         gfeat, gstride, gM, G, H, W, sseg, nsegs, nwaves);                                    \
     return true;                                                                                               \
   }
   GRR_EDGE_BWD_CASE(1, 4) GRR_EDGE_BWD_CASE(2, 4) GRR_EDGE_BWD_CASE(3, 4) GRR_EDGE_BWD_CASE(4, 4)

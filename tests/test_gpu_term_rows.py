@@ -126,12 +126,13 @@ def test_term_rows_large_f_equal_five_pass(K, case):
 
 
 EDGE_CASES = [(2, 4, 3, 20, 256), (1, 3, 1, 9, 32), (1, 2, 2, 17, 100), (1, 2, 6, 33, 200), (3, 2, 4, 2, 64),
-              (1, 1, 3, 140, 128), (1, 2, 12, 9, 64)]
+              (1, 1, 3, 140, 128), (1, 2, 12, 9, 64),
+              (1, 2, 6, 7, 512), (2, 1, 3, 5, 300), (1, 2, 4, 6, 744)]   # W > 256: column strips
 
 
 @pytest.mark.parametrize("case", EDGE_CASES, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
 def test_edge_weights_reverse_rows_equal_per_pixel(K, case):
-    """grr_bwd_edge_weights' row kernel (F in {1, 2, 3, 4, 6}, W <= 256; F = 12 falls back) against the
+    """grr_bwd_edge_weights' row kernel (F in {1, 2, 3, 4, 6}; W > 256 in column strips; F = 12 falls back) against the
     per-pixel kernel, on a GTV/GLR slab at a channel offset of a wider feature tensor."""
     b, G, F, h, w_ = case
     torch.manual_seed(F * 7 + h)
