@@ -1364,6 +1364,7 @@ struct Step2Args {
   float* x_mid;          // training: x_{k+1} and u_{k+1} (the reverse sweep's saved iterates), or NULL
   float* u_mid;
   int G, F, H, nsegs, sseg;
+  int W, nstrips;       // image width; column strips of S2_W lanes (1 at W = S2_W)
   int FG, ngrp;         // channel groups of <= S2_FMAX channels per (b, graph): FG channels each (the last may hold fewer)
   uint32_t nblk;
 };
@@ -1397,11 +1398,14 @@ struct OpPipe {
   // EDGE = false: the caller guarantees 1 <= t-2 <= H-2 (no row-boundary selects).  An
   // interior-block copy of the step2 loop measured no gain: the duplicated body raised the
   // register pressure into AGPR spills that cost what the selects did.
-  template <int P, int W, bool EDGE = true>
+  // CE (column strips of a wider image): c0 is the image column, the image is Wr wide (columns
+  // >= Wr are lanes past the right edge: their l / o are zeroed like rows outside the image)
+  template <int P, int W, bool EDGE = true, bool CE = false>
   __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
                                           int t, int H, int c0, const Taps& tL, const Taps& tG,
-                                          float (&tl)[V], float (&tg)[V]) {
+                                          float (&tl)[V], float (&tg)[V], int Wr = W) {
     constexpr int K0 = P & 3, K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
+    const int WW = CE ? Wr : W;
 #pragma unroll
     for (int j = 0; j < V; ++j) X[K3][j] = xin[j];
     const float (&X1)[V] = X[K1];
@@ -1413,7 +1417,7 @@ struct OpPipe {
       for (int j = 0; j < V; ++j) {
         const int col = c0 + j;
         const float xl = col > 0 ? (j > 0 ? X2[j - 1] : xp) : X2[j];
-        const float xr = col < W - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
+        const float xr = col < WW - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
         float sv = tL.u * X1[j];
         sv += tL.l * xl; sv += tL.c * X2[j]; sv += tL.r * xr; sv += tL.d * X3[j];
         SL[K3][j] = sv;
@@ -1441,7 +1445,7 @@ struct OpPipe {
         const float up = (!EDGE || r > 0) ? S0[j] : S1[j];
         const float dn = (!EDGE || r < H - 1) ? S2[j] : S1[j];
         const float lf = col > 0 ? (j > 0 ? S1[j - 1] : pv) : S1[j];
-        const float rt = col < W - 1 ? (j < V - 1 ? S1[j + 1] : nx) : S1[j];
+        const float rt = col < WW - 1 ? (j < V - 1 ? S1[j + 1] : nx) : S1[j];
         const float wx = ((WL[0][j] * up + WL[1][j] * lf) + WL[2][j] * rt) + WL[3][j] * dn;
         const float lv = S1[j] - wx;
         const float sv = G1[j];
@@ -1450,8 +1454,9 @@ struct OpPipe {
         const float chl = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
         const float cvu = (!EDGE || r > 0) ? cvp[j] : 0.f;
         const float ov = WG[0][j] * (sv - snx) + chl * (sv - spv) + WG[1][j] * (sv - G2[j]) + cvu * (sv - G0[j]);
-        L[K3][j] = (!EDGE || rin) ? lv : 0.f;
-        O[K3][j] = (!EDGE || rin) ? ov : 0.f;
+        const bool in = (!EDGE || rin) && (!CE || col < WW);
+        L[K3][j] = in ? lv : 0.f;
+        O[K3][j] = in ? ov : 0.f;
       }
 #pragma unroll
       for (int j = 0; j < V; ++j) cv[P & 1][j] = WG[1][j];
@@ -1511,8 +1516,15 @@ static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
 // (x_{k+1}, u_{k+1}, D x_{k+1}, t_k), written at least one barrier before it is read.
 constexpr int S2_PRODUCER = S2_FMAX, S2_HALFW = 2 * S2_FMAX + 1;
 constexpr int S2_THREADS = 64 * (2 * S2_FMAX + 2);
+// Column strips (W != S2_W, W % 8 == 0): a workgroup covers image columns x0 .. x0 + 255,
+// x0 = S2_SOWN * strip, and stores the columns it owns, [x0 + S2_HALO, x0 + S2_W - S2_HALO)
+// (from column 0 in the first strip, to W in the last).  The lanes' neighbour exchanges are
+// wrong at the window's two outer columns; the error spreads 3 columns per operator at the full
+// level, 3 half columns at the half level: t_k 6, x_{k+1} 6, t_{k+1} 12, x_{k+2} 12 columns.  The
+// 16-column halo covers that.
+constexpr int S2_HALO = 16, S2_SOWN = S2_W - 2 * S2_HALO;
 
-template <bool MID>
+template <bool MID, bool STRIPS>
 __global__ __launch_bounds__(S2_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void graph_step2_kernel(Step2Args a) {
   constexpr int V = 4, VH = 2, W = S2_W, hw = S2_HW;
@@ -1529,18 +1541,29 @@ void graph_step2_kernel(Step2Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int F = a.F;
   uint32_t unit = xcd_remap(blockIdx.x, a.nblk);
+  int strip = 0;
+  if constexpr (STRIPS) { strip = unit % a.nstrips; unit /= a.nstrips; }
   const int seg = unit % a.nsegs; unit /= a.nsegs;
   const int grp = unit % a.ngrp; unit /= a.ngrp;
   const int fb = grp * a.FG, Fg = min(a.FG, F - fb);   // this workgroup's channels fb .. fb + Fg - 1 of graph g
   const int g = unit % a.G;
   const int b = unit / a.G;
   const int H = a.H, h = H / 2;
-  const int64_t HW = (int64_t)H * W, hHW = (int64_t)h * hw;
+  const int Wi = STRIPS ? a.W : W, hwi = Wi / 2;   // image row widths (full / half level)
+  const int64_t HW = (int64_t)H * Wi, hHW = (int64_t)h * hwi;
   const int64_t PB = HW * 4, HPB = hHW * 4;
-  const uint32_t RB = (uint32_t)W * 4u, HRB = (uint32_t)hw * 4u;
+  const uint32_t RB = (uint32_t)Wi * 4u, HRB = (uint32_t)hwi * 4u;
   const int C = a.G * F;
-  const int c0 = 4 * lane, ch0 = 2 * lane;
-  const uint32_t vo = (uint32_t)c0 * 4u, vo_half = (uint32_t)ch0 * 4u;
+  const int c0 = 4 * lane, ch0 = 2 * lane;   // the lane's columns in the LDS rows
+  // image columns of the lane (cg, chg: edge rules; loads clamp into the image) and the
+  // columns this workgroup stores
+  const int x0 = STRIPS ? S2_SOWN * strip : 0;
+  const int cg = x0 + c0, chg = x0 / 2 + ch0;
+  const uint32_t vo = (uint32_t)(STRIPS ? clampi(cg, 0, Wi - V) : c0) * 4u;
+  const uint32_t vo_half = (uint32_t)(STRIPS ? clampi(chg, 0, hwi - VH) : ch0) * 4u;
+  const int own_lo = STRIPS && strip > 0 ? x0 + S2_HALO : 0;
+  const int own_hi = STRIPS && strip < a.nstrips - 1 ? x0 + S2_W - S2_HALO : Wi;
+  const bool own = !STRIPS || (cg >= own_lo && cg < own_hi);
   const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
   const int ts = r0 - 9;                 // first step (odd offset from r0: step t emits stage-A row t-3)
   const int NI0 = (r1 + 11 - ts) / 2;    // stage B emits rows up to r1 - 1
@@ -1570,7 +1593,7 @@ void graph_step2_kernel(Step2Args a) {
       float* slot = wring + (p % S2_WP) * S2_PAIR;
 #pragma unroll
       for (int par = 0; par < 2; ++par) {
-        const int64_t rw = (int64_t)clampi(ts + 2 * p + par - 2, 0, H - 1) * W + 4 * lane;
+        const int64_t rw = (int64_t)clampi(ts + 2 * p + par - 2, 0, H - 1) * Wi + vo / 4u;
 #pragma unroll
         for (int e = 0; e < 6; ++e)
           dma(e < 4 ? pwl0 + e * HW + rw : pcg0 + (e - 4) * HW + rw, slot + (par * 6 + e) * S2_W);
@@ -1583,8 +1606,8 @@ void graph_step2_kernel(Step2Args a) {
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
         const int plane = 2 * e + pl;
-        const float* src = (plane < 4 ? pwl1 + plane * hHW : pcg1 + (plane - 4) * hHW) + (int64_t)hr * hw +
-                           (lane & 31) * 4;
+        const int hc = STRIPS ? clampi(x0 / 2 + (lane & 31) * 4, 0, hwi - 4) : (lane & 31) * 4;
+        const float* src = (plane < 4 ? pwl1 + plane * hHW : pcg1 + (plane - 4) * hHW) + (int64_t)hr * hwi + hc;
         dma(src, slot + e * 2 * S2_HW);
       }
     };
@@ -1658,7 +1681,8 @@ void graph_step2_kernel(Step2Args a) {
       for (int f = 0; f < S2_FMAX; ++f) {
         if (f < Fg) {
           float tl[VH], tg[VH];
-          PF[f].template advance<P, hw, true>(L.xq[f], WL, WG, hin, h, ch0, tLh[f], tGh[f], tl, tg);
+          PF[f].template advance<P, hw, true, STRIPS>(L.xq[f], WL, WG, hin, h, STRIPS ? chg : ch0, tLh[f], tGh[f],
+                                                      tl, tg, hwi);
 #pragma unroll
           for (int k = 0; k < VH; ++k) {   // mu * S_L^T l + ro * S_G^T o, grr_system_half's epilogue
             float rv = tl[k] * scl1;
@@ -1818,7 +1842,7 @@ void graph_step2_kernel(Step2Args a) {
     constexpr bool EDGE = decltype(edge_tag)::value;
     float WL[4][V], WG[2][V], tl[V], tg[V];
     ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
-    PA.template advance<P, W, EDGE>(S.x, WL, WG, t, H, c0, tL0, tG0, tl, tg);
+    PA.template advance<P, W, EDGE, STRIPS>(S.x, WL, WG, t, H, STRIPS ? cg : c0, tL0, tG0, tl, tg, Wi);
     const float (&x0)[V] = PA.template x_out<P>();
     const int y = t - 3;
     float xn[V], u[V];
@@ -1839,7 +1863,7 @@ void graph_step2_kernel(Step2Args a) {
       st4(ur + (y % S2_UR) * S2_W, u);
     }
     if constexpr (MID) {     // training: the middle iterate's rows of this segment to HBM
-      const uint32_t so = (y >= r0 && y < r1) ? vo + (uint32_t)y * RB : GRR_OOB;
+      const uint32_t so = (y >= r0 && y < r1 && own) ? vo + (uint32_t)y * RB : GRR_OOB;
       bstore<V>(rxm, so, xn);
       bstore<V>(rum, so, u);
     }
@@ -1879,7 +1903,7 @@ void graph_step2_kernel(Step2Args a) {
       const F2 q = *reinterpret_cast<const F2*>(row + (4 + e) * S2_HW);
       WG[e][0] = q[0]; WG[e][1] = q[1];
     }
-    PH.template advance<P, hw, EDGE>(xh, WL, WG, hin, h, ch0, tL1, tG1, tl, tg);
+    PH.template advance<P, hw, EDGE, STRIPS>(xh, WL, WG, hin, h, STRIPS ? chg : ch0, tL1, tG1, tl, tg, hwi);
 #pragma unroll
     for (int k = 0; k < VH; ++k) {
       float rv = tl[k] * scl1;
@@ -1898,7 +1922,7 @@ void graph_step2_kernel(Step2Args a) {
     ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
     const int y = t - 11;
     ld4(ur + (((y % S2_UR) + S2_UR) % S2_UR) * S2_W, up);
-    PQ.template advance<P, W, EDGE>(xin, WL, WG, tb, H, c0, tL0, tG0, tl, tg);
+    PQ.template advance<P, W, EDGE, STRIPS>(xin, WL, WG, tb, H, STRIPS ? cg : c0, tL0, tG0, tl, tg, Wi);
     const float (&x0)[V] = PQ.template x_out<P>();
     float res[V], xn[V], u[V];
 #pragma unroll
@@ -1914,7 +1938,7 @@ void graph_step2_kernel(Step2Args a) {
       xn[j] = x0[j] + alpha_b * uv;
       res[j] = sk0 * S.y2[j] + sk1 * xn[j];
     }
-    const bool yv = y >= r0 && y < r1;
+    const bool yv = y >= r0 && y < r1 && own;
     const uint32_t so = yv ? vo + (uint32_t)y * RB : GRR_OOB;
     bstore<V, S2_NT>(rout, so, res);
     bstore<V, S2_NT>(ruo, so, u);
@@ -2258,8 +2282,8 @@ static grr_status system_step2_impl(const float* x, const float* b, const float*
               "grr_system_step2: stencil missing");
   GRR_REQUIRE(!skip || y_skip, GRR_ERR_INVALID_ARG, "grr_system_step2: skip needs y_skip");
   GRR_REQUIRE(!beta_a || u_prev, GRR_ERR_INVALID_ARG, "grr_system_step2: beta_a needs u_prev");
-  GRR_REQUIRE(W == S2_W && H % 2 == 0 && H >= 2, GRR_ERR_UNSUPPORTED,
-              "grr_system_step2: needs W = %d and even H (got H %d, W %d)", S2_W, H, W);
+  GRR_REQUIRE((W == S2_W || (W % 8 == 0 && W >= 8)) && H % 2 == 0 && H >= 2, GRR_ERR_UNSUPPORTED,
+              "grr_system_step2: needs W = %d or W %% 8 == 0, and even H (got H %d, W %d)", S2_W, H, W);
   GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_system_step2: plane too large");
   GRR_REQUIRE(x_out != x && x_out != b && x_out != u_prev && (!u_out || (u_out != u_prev && u_out != x && u_out != b)),
               GRR_ERR_INVALID_ARG, "grr_system_step2: outputs must not alias the inputs (rows are read ahead)");
@@ -2274,18 +2298,24 @@ static grr_status system_step2_impl(const float* x, const float* b, const float*
   a.log_mu0 = log_mu0; a.log_ro0 = log_ro0; a.log_mu1 = log_mu1; a.log_ro1 = log_ro1;
   a.alpha_a = alpha_a; a.beta_a = beta_a; a.alpha_b = alpha_b; a.beta_b = beta_b;
   a.skip = skip; a.y = y_skip; a.out = x_out; a.u_out = u_out; a.xd_out = xd_out;
-  a.G = G; a.F = F; a.H = H;
+  a.G = G; a.F = F; a.H = H; a.W = W;
+  a.nstrips = W <= S2_W ? 1 : 1 + (W - S2_W + S2_SOWN - 1) / S2_SOWN;
   a.ngrp = (F + S2_FMAX - 1) / S2_FMAX;   // F = 6 / 12 (v1.0 blocks): 2 / 4 groups of 3
   a.FG = (F + a.ngrp - 1) / a.ngrp;
-  a.sseg = step2_seg_rows(H, (uint64_t)B * G * a.ngrp);
+  a.sseg = step2_seg_rows(H, (uint64_t)B * G * a.ngrp * a.nstrips);
   a.nsegs = (H + a.sseg - 1) / a.sseg;
-  const uint64_t nblk = (uint64_t)B * G * a.ngrp * a.nsegs;
+  const uint64_t nblk = (uint64_t)B * G * a.ngrp * a.nsegs * a.nstrips;
   GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_step2: grid too large");
   a.nblk = (uint32_t)nblk;
-  if (x_mid)
-    hipLaunchKernelGGL(graph_step2_kernel<true>, dim3(a.nblk), dim3(S2_THREADS), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(graph_step2_kernel<false>, dim3(a.nblk), dim3(S2_THREADS), 0, (hipStream_t)stream, a);
+  const dim3 grid(a.nblk), block(S2_THREADS);
+  hipStream_t s = (hipStream_t)stream;
+  if (W == S2_W) {
+    if (x_mid) hipLaunchKernelGGL((graph_step2_kernel<true, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((graph_step2_kernel<false, false>), grid, block, 0, s, a);
+  } else {   // column strips
+    if (x_mid) hipLaunchKernelGGL((graph_step2_kernel<true, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((graph_step2_kernel<false, true>), grid, block, 0, s, a);
+  }
   return launch_status("grr_system_step2");
 }
 

@@ -343,10 +343,18 @@ def system_step2_train(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: 
     return x_mid, u_mid, out, u_out, xd
 
 
+# W > 256 (W % 8 == 0) runs the two-stage pass in column strips of 256 lanes with a 16-column halo
+# (GRR_STEP2_STRIPS=0: one launch per stage there); the kernel also takes narrower W % 8 == 0
+# images as one strip with idle lanes, which the per-stage kernels run faster
+STEP2_STRIPS = os.environ.get("GRR_STEP2_STRIPS", "1") != "0"
+
+
 def step2_supported(x: Tensor, n_graphs: int) -> bool:
-    """grr_system_step2's shape limits: W = 256, even H (F > 3: channel groups of <= 3)."""
+    """Where the model loops use grr_system_step2: W = 256, or W > 256 with W % 8 == 0 (column
+    strips); even H (F > 3: channel groups of <= 3)."""
     b, c, h, w = x.shape
-    return w == 256 and h % 2 == 0 and c % n_graphs == 0
+    wide = STEP2_STRIPS and w > 256 and w % 8 == 0
+    return (w == 256 or wide) and h % 2 == 0 and c % n_graphs == 0
 
 
 def step2_bytes(b, c, g, h, w, has_u_prev, has_u_out, has_pool, has_skip):

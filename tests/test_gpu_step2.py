@@ -8,6 +8,9 @@ two code paths.  Shapes cover one row segment per (b, graph) (B*G >= 512 workgro
 segmented grid of small batches (64-row segments, the stage-A lead of 9 rows crossing the
 segment boundary), the top / bottom replicate clamps of the in-kernel rings at short H, F > 3 as
 channel groups, the first pair (no u_prev / beta_a) and the last pair (skip, no u / D x outputs).
+Widths other than 256 run the column-strip instance (256-lane windows, 16-column halo): W > 256 in
+2-4 strips (the reference's 336 x 496 evaluation pad among them), narrower W % 8 == 0 as one strip
+with lanes past the image edge.
 """
 import pytest
 import torch
@@ -28,7 +31,7 @@ def irdu():
     return irdu_amd
 
 
-def _setup(irdu, B, G, F, H, seed):
+def _setup(irdu, B, G, F, H, seed, W=256):
     from irdu_amd import kernels as K
     torch.manual_seed(seed)
     mix = irdu.MixtureGTVGLR(G, F, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]], n_cgd_iters=4)
@@ -39,7 +42,6 @@ def _setup(irdu, B, G, F, H, seed):
         mix.muys01.fill_(-1.2)
         mix.ro01.fill_(-1.6)
     mix = mix.to(DEV)
-    W = 256
     f0 = torch.randn(B, 2 * G * F, H, W, device=DEV)
     f1 = torch.randn(B, 2 * G * F, H // 2, W // 2, device=DEV)
     _, cG0, wL0 = K.edge_weights_block(f0, G, F, mix.GTVmodule00.multiM, mix.GLRmodule00.multiM)
@@ -84,11 +86,24 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{B}g{G}f{F}h{H}".format(**c))
+STRIP_CASES = [
+    dict(B=2, G=4, F=3, H=64, W=496),    # three strips (the 336 x 496 evaluation pad, landscape)
+    dict(B=1, G=3, F=3, H=96, W=336),    # two strips (portrait)
+    dict(B=2, G=2, F=6, H=32, W=512),    # C4's width, channel groups
+    dict(B=1, G=2, F=2, H=16, W=744),    # four strips
+    dict(B=2, G=4, F=3, H=256, W=480),   # two strips, last strip 32 columns short of its window
+    dict(B=2, G=2, F=3, H=32, W=128),    # one strip, half the lanes past the edge
+    dict(B=1, G=2, F=3, H=12, W=200),
+    dict(B=1, G=2, F=1, H=8, W=8),       # one lane of image
+]
+
+
+@pytest.mark.parametrize("case", CASES + STRIP_CASES, ids=lambda c: "b{B}g{G}f{F}h{H}w{W}".format(W=256, **c)
+                         if "W" not in c else "b{B}g{G}f{F}h{H}w{W}".format(**c))
 @pytest.mark.parametrize("with_u", [True, False])
 def test_step2_equals_two_steps(irdu, case, with_u):
     B, G, F, H = case["B"], case["G"], case["F"], case["H"]
-    mix, x, b, u, w = _setup(irdu, B, G, F, H, seed=B * 100 + H + F)
+    mix, x, b, u, w = _setup(irdu, B, G, F, H, seed=B * 100 + H + F, W=case.get("W", 256))
     with torch.no_grad():
         (r, ru, rxd), (o, ou, oxd) = _two_steps(irdu, mix, x, b, u if with_u else None, w, k=2, g=G)
     torch.cuda.synchronize()
@@ -112,28 +127,31 @@ def test_step2_rejects_unsupported_shapes(irdu):
     from irdu_amd import kernels as K
     from irdu_amd._native import GrrError
     mix, x, b, u, w = _setup(irdu, 1, 2, 3, 16, seed=5)
-    xs = x[..., :128].contiguous()
+    xs = x[..., :132].contiguous()   # W % 8 != 0
     wL0, cG0, wL1, cG1 = w
     m = mix
     with pytest.raises(GrrError):
-        K.system_step2(xs, xs, None, torch.zeros(1, 6, 8, 64, device=DEV), wL0[..., :128].contiguous(),
-                       cG0[..., :128].contiguous(), K.stencil(m.GLRmodule00), K.stencil(m.GTVmodule00), m.muys00,
-                       m.ro00, wL1[..., :64].contiguous(), cG1[..., :64].contiguous(), K.stencil(m.GLRmodule01),
+        K.system_step2(xs, xs, None, torch.zeros(1, 6, 8, 66, device=DEV), wL0[..., :132].contiguous(),
+                       cG0[..., :132].contiguous(), K.stencil(m.GLRmodule00), K.stencil(m.GTVmodule00), m.muys00,
+                       m.ro00, wL1[..., :66].contiguous(), cG1[..., :66].contiguous(), K.stencil(m.GLRmodule01),
                        K.stencil(m.GTVmodule01), m.muys01, m.ro01, m.alphaCGD[0], None, m.alphaCGD[1],
                        m.betaCGD[1], 2, True, True)
     assert not K.step2_supported(xs, 2)
+    assert not K.step2_supported(x[..., :128], 2)   # narrower images stay on the per-stage kernels
+    assert K.step2_supported(torch.empty(1, 6, 16, 496, device="meta"), 2) == K.STEP2_STRIPS
 
 
-@pytest.mark.parametrize("b", [1, 3])
-def test_filter_with_step2_matches_per_stage_launches_and_oracle(irdu, b):
+@pytest.mark.parametrize("b,hw", [(1, (256, 256)), (3, (256, 256)), (1, (336, 496)), (1, (496, 336))])
+def test_filter_with_step2_matches_per_stage_launches_and_oracle(irdu, b, hw):
     """The image filter (S = 10: stage 0, then pairs (1,2) ... (7,8) and stage 9) with and without
-    two-stage launches, and against the CPU oracle at the PSNR tolerance."""
+    two-stage launches, and against the CPU oracle at the PSNR tolerance; 336 x 496 / 496 x 336 is the
+    reference's CBSD68 evaluation pad (column strips)."""
     from irdu_amd import kernels as K
     torch.manual_seed(2300 + b)
     m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=10)
     perturb_mixture(m.localfilter, 23 + b)
-    clean = torch.rand(b, 3, 256, 256)
-    noisy = clean + torch.randn(b, 3, 256, 256) * (25.0 / 255.0)
+    clean = torch.rand(b, 3, *hw)
+    noisy = clean + torch.randn(b, 3, *hw) * (25.0 / 255.0)
     md = m.to(DEV)
     saved = K.STEP2
     try:
@@ -150,8 +168,8 @@ def test_filter_with_step2_matches_per_stage_launches_and_oracle(irdu, b):
     assert abs(O.psnr_ubyte(fused, clean) - O.psnr_ubyte(ref, clean)) <= 0.01
 
 
-@pytest.mark.parametrize("n_st", [4, 5])
-def test_training_forward_with_step2_matches_per_stage(irdu, n_st):
+@pytest.mark.parametrize("n_st,w", [(4, 256), (5, 256), (5, 512)])
+def test_training_forward_with_step2_matches_per_stage(irdu, n_st, w):
     """The training forward (grr_system_step2_train: pairs that also write the middle iterate for the
     reverse sweep) against one stage per launch: output, loss gradient of the input and of every
     parameter of the image filter (S = 4: pair (1,2) + stage 3; S = 5: pairs (1,2), (3,4))."""
@@ -159,8 +177,8 @@ def test_training_forward_with_step2_matches_per_stage(irdu, n_st):
     torch.manual_seed(2400 + n_st)
     m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=4, n_cgd_iters=n_st)
     perturb_mixture(m.localfilter, 24 + n_st)
-    x = torch.rand(2, 3, 32, 256)
-    gout = torch.randn(2, 3, 32, 256)
+    x = torch.rand(2, 3, 32, w)
+    gout = torch.randn(2, 3, 32, w)
     md = m.to(DEV).train()
     saved = K.STEP2
     res = {}
