@@ -343,17 +343,19 @@ def system_step2_train(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: 
     return x_mid, u_mid, out, u_out, xd
 
 
-# W > 256 (W % 8 == 0) runs the two-stage pass in column strips of 256 lanes with a 16-column halo
-# (GRR_STEP2_STRIPS=0: one launch per stage there); the kernel also takes narrower W % 8 == 0
-# images as one strip with idle lanes, which the per-stage kernels run faster
+# W != 256 (W % 8 == 0) runs the two-stage pass in column strips of 256 lanes with a 16-column halo
+# (GRR_STEP2_STRIPS=0: one launch per stage there).  Narrower images are one strip with idle lanes:
+# at W = 128 (the v1.0 model's second level) that still beats one launch per stage (v1.0 forward
+# 25.15-25.22 -> 24.75 ms at 16 x 256^2), at W = 64 it does not (25.48 ms; profiles/r03/s2strips/narrow.txt)
 STEP2_STRIPS = os.environ.get("GRR_STEP2_STRIPS", "1") != "0"
+STEP2_MIN_W = int(os.environ.get("GRR_STEP2_MIN_W", "128"))   # narrowest strip-pass width the loops use
 
 
 def step2_supported(x: Tensor, n_graphs: int) -> bool:
-    """Where the model loops use grr_system_step2: W = 256, or W > 256 with W % 8 == 0 (column
-    strips); even H (F > 3: channel groups of <= 3)."""
+    """Where the model loops use grr_system_step2: W = 256, or W >= STEP2_MIN_W with W % 8 == 0
+    (column strips); even H (F > 3: channel groups of <= 3)."""
     b, c, h, w = x.shape
-    wide = STEP2_STRIPS and w > 256 and w % 8 == 0
+    wide = STEP2_STRIPS and w >= STEP2_MIN_W and w % 8 == 0
     return (w == 256 or wide) and h % 2 == 0 and c % n_graphs == 0
 
 

@@ -137,7 +137,8 @@ def test_step2_rejects_unsupported_shapes(irdu):
                        K.stencil(m.GTVmodule01), m.muys01, m.ro01, m.alphaCGD[0], None, m.alphaCGD[1],
                        m.betaCGD[1], 2, True, True)
     assert not K.step2_supported(xs, 2)
-    assert not K.step2_supported(x[..., :128], 2)   # narrower images stay on the per-stage kernels
+    assert K.step2_supported(x[..., :128], 2) == (K.STEP2_STRIPS and K.STEP2_MIN_W <= 128)
+    assert not K.step2_supported(x[..., :64], 2) or K.STEP2_MIN_W <= 64   # W = 64: per-stage kernels
     assert K.step2_supported(torch.empty(1, 6, 16, 496, device="meta"), 2) == K.STEP2_STRIPS
 
 
