@@ -154,7 +154,8 @@ grr_status grr_system_step(const float* x, const float* b, const float* u_prev, 
  *   stage B (k+1): x_out = x_{k+2}, u_out = u_{k+2} (beta_b with u_{k+1}), xd_out = D x_{k+2},
  *                  skip applied to x_out as in grr_system_step.
  * Same values as grr_system_half -> grr_system_step(k) -> grr_system_half -> grr_system_step(k+1) up to fp32
- * rounding order.  GLR + GTV pair at both levels; W = 256, even H; F > 3 runs as groups of <= 3
+ * rounding order.  GLR + GTV pair at both levels; W = 256, or W % 8 == 0 (column strips of 256 lanes
+ * owning 224 columns with a 16-column halo), even H; F > 3 runs as groups of <= 3
  * channels (each group reads its graph's weight rows once); outputs must
  * not alias inputs (u_out != u_prev).  Replaces two iterations of the loop body REF:784-790. */
 grr_status grr_system_step2(const float* x, const float* b, const float* u_prev, const float* xd,
