@@ -554,7 +554,10 @@ __global__ __launch_bounds__(NT) void edge_weights_bwd_kernel(const float* __res
   for (int f = 0; f < F; ++f) block_atomic_add(gM + g * F + f, gm_sm[f * NT + threadIdx.x]);
 }
 
-// gdot[g] += coef * sum_{b,f,p} u v.      grid (chunks, B*G)
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// gdot[g] += coef * sum_{b,f,p} u v.      grid (chunks, B*G); V4: float4 loads (n % 4 == 0, aligned)
+template <bool V4>
 __global__ __launch_bounds__(NT) void graph_dot_kernel(const float* __restrict__ u, const float* __restrict__ v,
                                                        float coef, float* __restrict__ gdot, int G, int F,
                                                        int64_t HW) {
@@ -563,20 +566,41 @@ __global__ __launch_bounds__(NT) void graph_dot_kernel(const float* __restrict__
   const float* up = u + (int64_t)bg * n;
   const float* vp = v + (int64_t)bg * n;
   float acc = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) acc += up[i] * vp[i];
+  if constexpr (V4) {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * NT) {
+      const f4v a = *reinterpret_cast<const f4v*>(up + 4 * i), b = *reinterpret_cast<const f4v*>(vp + 4 * i);
+      acc += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) acc += up[i] * vp[i];
+  }
   block_atomic_add(gdot + g, coef * acc);
 }
 
 // out = sa[g] * x + sb[g] * y  (sa/sb NULL -> 1; y NULL -> term dropped); acc: out += ...
+// grid (chunks, B*G): one (b, graph) slab of n = F H W floats per block row; V4 as graph_dot_kernel
+template <bool V4>
 __global__ __launch_bounds__(NT) void lincomb_kernel(const float* __restrict__ x, const float* __restrict__ sa,
                                                      const float* __restrict__ y, const float* __restrict__ sb,
-                                                     float* __restrict__ out, int acc, int C, int F, int64_t HW,
-                                                     int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const int g = (int)((i / HW) % C) / F;
-    float v = (sa ? sa[g] : 1.f) * x[i];
-    if (y) v += (sb ? sb[g] : 1.f) * y[i];
-    out[i] = acc ? out[i] + v : v;
+                                                     float* __restrict__ out, int acc, int G, int64_t n) {
+  const int bg = blockIdx.y, g = bg % G;
+  const float a = sa ? sa[g] : 1.f, bb = sb ? sb[g] : 1.f;
+  const int64_t base = (int64_t)bg * n;
+  if constexpr (V4) {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * NT) {
+      const int64_t o = base + 4 * i;
+      f4v v = a * *reinterpret_cast<const f4v*>(x + o);
+      if (y) v += bb * *reinterpret_cast<const f4v*>(y + o);
+      f4v* dst = reinterpret_cast<f4v*>(out + o);
+      *dst = acc ? *dst + v : v;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+      const int64_t o = base + i;
+      float v = a * x[o];
+      if (y) v += bb * y[o];
+      out[o] = acc ? out[o] + v : v;
+    }
   }
 }
 
@@ -638,6 +662,24 @@ __global__ __launch_bounds__(NT) void unpool2_acc_kernel(const float* __restrict
     const int p = (int)(i - plane * H * W);
     const int r = p / W, c = p - r * W;
     out[i] += 0.25f * xd[plane * h * w + (r >> 1) * w + (c >> 1)];
+  }
+}
+
+// the same, four output columns per thread (W % 4 == 0, aligned): grid (chunks, planes)
+__global__ __launch_bounds__(NT) void unpool2_acc4_kernel(const float* __restrict__ xd, float* __restrict__ out,
+                                                          int H, int W) {
+  const int w = W / 2, W4 = W / 4, n4 = H * W4;
+  const int64_t plane = blockIdx.y;
+  const float* xp = xd + plane * (H / 2) * w;
+  float* op = out + plane * H * W;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < n4; i += gridDim.x * NT) {
+    const int r = i / W4, c4 = i - r * W4;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 q = *reinterpret_cast<const f2*>(xp + (r >> 1) * w + 2 * c4);
+    f4v* dst = reinterpret_cast<f4v*>(op + r * W + 4 * c4);
+    f4v v = *dst;
+    v.x += 0.25f * q.x; v.y += 0.25f * q.x; v.z += 0.25f * q.y; v.w += 0.25f * q.y;
+    *dst = v;
   }
 }
 
@@ -1614,8 +1656,15 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   GRR_REQUIRE(u && v && gdot && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_bwd_graph_dot: bad args");
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_graph_dot: B*G*F > 65535");
-  hipLaunchKernelGGL(graph_dot_kernel, dim3(chunks_for((int64_t)F * H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream,
-                     u, v, coef, gdot, G, F, (int64_t)H * W);
+  const int64_t n = (int64_t)F * H * W;
+  const bool v4 = n % 4 == 0 && ((uintptr_t)u & 15) == 0 && ((uintptr_t)v & 15) == 0;
+  const dim3 grid(chunks_for(v4 ? n / 4 : n, (int64_t)B * G), B * G);
+  if (v4)
+    hipLaunchKernelGGL(graph_dot_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, u, v, coef, gdot, G, F,
+                       (int64_t)H * W);
+  else
+    hipLaunchKernelGGL(graph_dot_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, u, v, coef, gdot, G, F,
+                       (int64_t)H * W);
   return launch_status("grr_bwd_graph_dot");
 }
 
@@ -1646,9 +1695,17 @@ grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, cons
   clear_error();
   GRR_REQUIRE(x && out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_bwd_lincomb: bad args");
-  const int64_t HW = (int64_t)H * W, n = (int64_t)B * G * F * HW;
-  hipLaunchKernelGGL(lincomb_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, x, sa, y, sb, out,
-                     accumulate, G * F, F, HW, n);
+  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_lincomb: B*G > 65535");
+  const int64_t n = (int64_t)F * H * W;   // one (b, graph) slab
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool v4 = n % 4 == 0 && al16(x) && al16(out) && (!y || al16(y));
+  const dim3 grid(chunks_for(v4 ? n / 4 : n, (int64_t)B * G), B * G);
+  if (v4)
+    hipLaunchKernelGGL(lincomb_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, x, sa, y, sb, out, accumulate, G,
+                       n);
+  else
+    hipLaunchKernelGGL(lincomb_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, x, sa, y, sb, out, accumulate,
+                       G, n);
   return launch_status("grr_bwd_lincomb");
 }
 
@@ -1657,7 +1714,13 @@ grr_status grr_bwd_unpool2_acc(const float* xd, float* out, int B, int C, int H,
   GRR_REQUIRE(xd && out && B > 0 && C > 0 && H > 1 && W > 1, GRR_ERR_INVALID_ARG, "grr_bwd_unpool2_acc: bad args");
   GRR_REQUIRE(H % 2 == 0 && W % 2 == 0, GRR_ERR_SHAPE, "grr_bwd_unpool2_acc: H, W must be even");
   const int64_t n = (int64_t)B * C * H * W;
-  hipLaunchKernelGGL(unpool2_acc_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, xd, out, H, W, n);
+  if (W % 4 == 0 && (int64_t)B * C <= 65535 && (int64_t)H * W < (1ll << 31) && ((uintptr_t)xd & 7) == 0 &&
+      ((uintptr_t)out & 15) == 0) {
+    const dim3 grid(chunks_for((int64_t)H * W / 4, (int64_t)B * C), B * C);
+    hipLaunchKernelGGL(unpool2_acc4_kernel, grid, dim3(NT), 0, (hipStream_t)stream, xd, out, H, W);
+  } else {
+    hipLaunchKernelGGL(unpool2_acc_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, xd, out, H, W, n);
+  }
   return launch_status("grr_bwd_unpool2_acc");
 }
 
