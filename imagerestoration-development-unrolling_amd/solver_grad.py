@@ -24,6 +24,8 @@ from __future__ import annotations
 
 from typing import List, Optional, Tuple
 
+import os
+
 import torch
 
 from . import kernels as K
@@ -148,8 +150,37 @@ class _Level:
         K.bwd_stencil(gs, self.tapsG, K.ST_P_ADJ, G, sc, out=out)
 
 
+# The half level's reverse runs on a second HIP stream beside the full level's (GRR_LEVEL_STREAMS=0: one
+# stream): the two touch disjoint gradient buffers until U adds the half level's x-gradient, and the
+# small launches of the deeper levels of the v1.0 model leave most of the GPU idle one at a time
+LEVEL_STREAMS = os.environ.get("GRR_LEVEL_STREAMS", "1") == "1"
+_LEVEL_SIDE = {}
+
+
+def _level_side(dev: torch.device) -> "torch.cuda.Stream":
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _LEVEL_SIDE:
+        _LEVEL_SIDE[key] = torch.cuda.Stream(device=dev)
+    return _LEVEL_SIDE[key]
+
+
 def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn) -> None:
     """Apply a per-level reverse at full resolution and, through D / U, at half resolution."""
+    if LEVEL_STREAMS and x.is_cuda and not torch.compiler.is_compiling():
+        main = torch.cuda.current_stream(x.device)
+        side = _level_side(x.device)
+        side.wait_stream(main)                # x, g (and every buffer the half level accumulates into) ready
+        with torch.cuda.stream(side):
+            xd, gd = K.pool2(x), K.pool2(g)
+            gxd = torch.zeros_like(xd)
+            fn(l1, xd, gd, gxd)
+        x.record_stream(side)
+        g.record_stream(side)
+        fn(l0, x, g, out)
+        main.wait_stream(side)
+        gxd.record_stream(main)
+        K.bwd_unpool2_acc(gxd, out)           # D^T = U
+        return
     fn(l0, x, g, out)
     xd, gd = K.pool2(x), K.pool2(g)          # half level sees D x; U^T = D
     gxd = torch.zeros_like(xd)

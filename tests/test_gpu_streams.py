@@ -53,11 +53,26 @@ def test_mixture_two_streams_bitwise(irdu):
     assert torch.equal(a, b)
 
 
+def _assert_steps_close(g1, g2, w1, w2):
+    """Per parameter: 1e-5 relative to its own largest gradient, with a floor of 1e-7 of the step's
+    largest gradient (a parameter whose gradient nearly cancels, e.g. max 1.5e-8 from terms of 1e-3,
+    carries the terms' fp32 summation noise, ~1e-12, which the atomics' order changes)."""
+    for step_a, step_b in zip(g1, g2):
+        scale = max(float(b.abs().max()) for b in step_b if b is not None)
+        for a, b in zip(step_a, step_b):
+            if a is None:
+                assert b is None
+                continue
+            assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-7 * scale
+    for a, b in zip(w1, w2):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
+
+
 def test_msgf_training_side_stream_matches_one_stream(irdu):
     """GRR_FEATURE_STREAMS_TRAIN: the half-resolution branch's forward and (autograd's stream replay)
     reverse on the side stream.  Three training steps (loss, backward, parameter update) per mode so
     the caching allocator recycles the cross-stream blocks; gradients and weights equal the one-stream
-    run's (reductions use float atomics, so to 1e-5 relative, not bitwise)."""
+    run's (reductions use float atomics, so to 1e-5 relative, not bitwise; _assert_steps_close)."""
     import torch.nn.functional as F
     from irdu_amd import graph_filter as GF
 
@@ -83,8 +98,44 @@ def test_msgf_training_side_stream_matches_one_stream(irdu):
         (g1, w1), (g2, w2) = run(False), run(True)
     finally:
         GF.FEATURE_STREAMS_TRAIN = saved
-    for step_a, step_b in zip(g1, g2):
-        for a, b in zip(step_a, step_b):
-            assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
-    for a, b in zip(w1, w2):
-        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
+    _assert_steps_close(g1, g2, w1, w2)
+
+
+@pytest.mark.parametrize("model", ["msgf", "abstract"])
+def test_training_level_streams_match_one_stream(irdu, model):
+    """solver_grad.LEVEL_STREAMS: the half level's reverse of every stage on a second stream beside the
+    full level's.  Three training steps per mode (allocator recycling across streams); gradients and
+    weights equal the one-stream run's to 1e-5 relative (float-atomic reductions)."""
+    import torch.nn.functional as F
+    from irdu_amd import solver_grad as SG
+
+    def build():
+        if model == "msgf":
+            return irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=4)
+        return irdu.AbtractMultiScaleGraphFilter(
+            3, 3, dims=[8, 16, 16, 32], hidden_dims=[16, 32, 32, 64], nsubnets=[1, 1, 1, 1], ngraphs=[2, 4, 4, 8],
+            num_blocks=[1, 1, 1, 1], num_blocks_out=1, n_cgd_iters=3)
+
+    def run(on):
+        SG.LEVEL_STREAMS = on
+        torch.manual_seed(11)
+        m = build().to(DEV).train()
+        opt = torch.optim.SGD(m.parameters(), lr=1e-3)
+        g = torch.Generator().manual_seed(5)
+        grads = []
+        for _ in range(3):
+            x = torch.rand(2, 3, 64, 64, generator=g).to(DEV)
+            t = torch.rand(2, 3, 64, 64, generator=g).to(DEV)
+            opt.zero_grad(set_to_none=True)
+            F.l1_loss(m(x), t).backward()
+            grads.append([p.grad.clone() if p.grad is not None else None for p in m.parameters()])
+            opt.step()
+        torch.cuda.synchronize()
+        return grads, [p.detach().clone() for p in m.parameters()]
+
+    saved = SG.LEVEL_STREAMS
+    try:
+        (g1, w1), (g2, w2) = run(False), run(True)
+    finally:
+        SG.LEVEL_STREAMS = saved
+    _assert_steps_close(g1, g2, w1, w2)
