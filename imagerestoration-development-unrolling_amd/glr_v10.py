@@ -25,11 +25,12 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import ops as OPS
+from .compile_backend import HipModule
 from . import solver_grad as SG
 from .graph_filter import GLRFast, records_grad
 
 
-class MixtureGLR(nn.Module):
+class MixtureGLR(HipModule):
     def __init__(self, n_graphs, n_node_fts, alpha_init, beta_init, muy_init, n_cgd_iters: int = 3):
         super().__init__()
         self.n_graphs = n_graphs
@@ -67,7 +68,7 @@ class MixtureGLR(nn.Module):
         return x
 
 
-class LocalLowpassFilteringBlock(nn.Module):
+class LocalLowpassFilteringBlock(HipModule):
     def __init__(self, dim, nsubnets, ngraphs, n_cgd_iters: int = 3):
         super().__init__()
         self.local_filter = MixtureGLR(n_graphs=ngraphs, n_node_fts=dim // ngraphs, alpha_init=0.5, beta_init=0.1,
@@ -78,7 +79,7 @@ class LocalLowpassFilteringBlock(nn.Module):
         return self.local_filter(x)
 
 
-class MultiScaleMixtureGLR(nn.Module):
+class MultiScaleMixtureGLR(HipModule):
     """Two-scale GLR-only unrolled solver (config C2, SURVEY.md §8d: "GLR-only (v10 pattern,
     2 scales)").  The reference has no literal two-scale GLR-only block, so this is the
     v1.0 system operator with its graph-TV terms removed (REF:642-682 without the ro terms),
@@ -149,7 +150,7 @@ class MultiScaleMixtureGLR(nn.Module):
         return x
 
 
-class MultiScaleGLRImageFilter(nn.Module):
+class MultiScaleGLRImageFilter(HipModule):
     """Config C2 as BASELINE.json states it: the gray image replicated over G graphs
     (as REF13:918-921 does for RGB) -> MultiScaleMixtureGLR (S = 5 two-scale stages) -> 1x1."""
 
@@ -169,7 +170,7 @@ class MultiScaleGLRImageFilter(nn.Module):
             return OPS.conv1x1(self.localfilter(x), self.linear_combination.weight)
 
 
-class GLRImageFilter(nn.Module):
+class GLRImageFilter(HipModule):
     """Single-scale GLR image filter (config C1 with S = 1): image replicated over G graphs ->
     MixtureGLR (S stages) -> 1x1 projection."""
 

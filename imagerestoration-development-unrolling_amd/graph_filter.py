@@ -29,6 +29,7 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
+from .compile_backend import HipModule
 from . import ops as OPS
 from . import solver_grad as SG
 
@@ -91,7 +92,7 @@ def _basis(c: int):
     return [k.expand(c, 1, 3, 3).clone() for k in (k01, k02a, k02b, k03)]
 
 
-class _GraphModule(nn.Module):
+class _GraphModule(HipModule):
     """Parameters shared by GLRFast and GTVFast (REF:14-125 / :243-356)."""
 
     def __init__(self, n_node_fts: int, n_graphs: int, M_diag_init: float = 0.4):
@@ -216,7 +217,7 @@ class GTVFast(_GraphModule):
 # ---------------------------------------------------------------------------
 # Feature CNN building blocks (REF:911-964; REF13:541-575)
 # ---------------------------------------------------------------------------
-class CustomLayerNorm(nn.Module):
+class CustomLayerNorm(HipModule):
     def __init__(self, nchannels, nsubnets):
         super().__init__()
         self.nsubnets = nsubnets
@@ -231,7 +232,7 @@ class CustomLayerNorm(nn.Module):
         return self.weighted_transform(xs.reshape(b, c, h, w))
 
 
-class LocalGatedLinearBlock(nn.Module):
+class LocalGatedLinearBlock(HipModule):
     def __init__(self, dim, hidden_dim, nsubnets):
         super().__init__()
         self.channels_linear_op = nn.Conv2d(dim, hidden_dim * 2, kernel_size=1, bias=False, groups=nsubnets)
@@ -245,7 +246,7 @@ class LocalGatedLinearBlock(nn.Module):
         return self.project_out(torch.sigmoid(mask) * mask * x)
 
 
-class LocalNonLinearBlock(nn.Module):
+class LocalNonLinearBlock(HipModule):
     """skip0 * x + skip1 * GatedLinear(LayerNorm(x)).  nsubnets == 1 runs the fused HIP block."""
 
     def __init__(self, dim, hidden_dim, nsubnets):
@@ -293,7 +294,7 @@ class LocalNonLinearBlock(nn.Module):
 # ---------------------------------------------------------------------------
 # The solver block
 # ---------------------------------------------------------------------------
-class MixtureGTVGLR(nn.Module):
+class MixtureGTVGLR(HipModule):
     """Two-scale GGTV+GGLR unrolled solver (REF:526-811).
 
     ``n_cgd_iters`` (default 3 = the reference) sets the number S of unrolled
@@ -521,7 +522,7 @@ class MixtureGTVGLR(nn.Module):
             return self._solve(patchs.contiguous(), _skip, None if _src is None else _src.contiguous())
 
 
-class LocalLowpassFilteringBlock(nn.Module):
+class LocalLowpassFilteringBlock(HipModule):
     """skip0 * x + skip1 * MixtureGTVGLR(x), the skip fused into the last stage (REF:967-988)."""
 
     def __init__(self, dim, nsubnets, ngraphs, n_cgd_iters: int = 3):
@@ -538,7 +539,7 @@ class LocalLowpassFilteringBlock(nn.Module):
         return self.local_filter(x, _skip=self.skip_weight.detach())
 
 
-class MultiScaleGraphFilter(nn.Module):
+class MultiScaleGraphFilter(HipModule):
     """Image-domain GGTV-GGLR filter (REF13:887-926): RGB replicated over G graphs,
     MixtureGTVGLR with the v13 feature CNN, then a 1x1 projection to the output."""
 
@@ -571,7 +572,7 @@ class MultiScaleGraphFilter(nn.Module):
 # their convolutions run as stock PyTorch-ROCm ops; LocalNonLinearBlocks with
 # nsubnets == 1 and the four filter blocks run on the HIP kernels.
 # ---------------------------------------------------------------------------
-class ReginalPixelEmbeding(nn.Module):
+class ReginalPixelEmbeding(HipModule):
     def __init__(self, n_channels_in=3, dim=48, bias=False):
         super().__init__()
         self.channels_local_linear_op01 = nn.Conv2d(n_channels_in, dim, kernel_size=3, stride=1, padding=1,
@@ -581,7 +582,7 @@ class ReginalPixelEmbeding(nn.Module):
         return self.channels_local_linear_op01(x)
 
 
-class Downsampling(nn.Module):
+class Downsampling(HipModule):
     def __init__(self, dim_in, dim_out, nsubnets):
         super().__init__()
         self.local_linear = nn.Conv2d(dim_in, dim_out, kernel_size=2, stride=2, padding=0, groups=nsubnets, bias=False)
@@ -590,7 +591,7 @@ class Downsampling(nn.Module):
         return self.local_linear(x)
 
 
-class Upsampling(nn.Module):
+class Upsampling(HipModule):
     def __init__(self, dim_in, dim_out, nsubnets):
         super().__init__()
         self.local_linear = nn.ConvTranspose2d(dim_in, dim_out, kernel_size=2, stride=2, padding=0, groups=nsubnets,
@@ -600,7 +601,7 @@ class Upsampling(nn.Module):
         return self.local_linear(x)
 
 
-class AbtractMultiScaleGraphFilter(nn.Module):
+class AbtractMultiScaleGraphFilter(HipModule):
     def __init__(self, n_channels_in=3, n_channels_out=3, dims=(48, 64, 96, 128), hidden_dims=(128, 192, 256, 384),
                  nsubnets=(1, 1, 1, 1), ngraphs=(4, 4, 8, 8), num_blocks=(4, 6, 6, 8), num_blocks_out=4,
                  n_cgd_iters: int = 3):

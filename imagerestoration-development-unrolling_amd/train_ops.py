@@ -63,15 +63,18 @@ class OpaqueFunction:
             outs, saved = spec.fake(list(consts), *inputs)
             return [*outs, *saved]
 
+        # needs[i] = 0: input i takes no gradient (ctx.needs_input_grad, as in eager mode) -- its reverse is
+        # skipped and its slot is an empty placeholder, so the compiled step runs the eager step's kernels
         def bwd_impl(inputs: List[Tensor], outs: List[Tensor], saved: List[Tensor], gouts: List[Tensor],
-                     consts: List[int]) -> List[Tensor]:
-            grads = spec.bwd(list(consts), inputs, outs, saved, gouts, [True] * len(inputs))
-            return [g.contiguous().view(x.shape) if g is not None else torch.zeros(x.shape, dtype=x.dtype, device=x.device)
-                    for g, x in zip(grads, inputs)]
+                     consts: List[int], needs: List[int]) -> List[Tensor]:
+            grads = spec.bwd(list(consts), inputs, outs, saved, gouts, [bool(n) for n in needs])
+            return [x.new_empty(0) if not n else
+                    g.contiguous().view(x.shape) if g is not None else torch.zeros(x.shape, dtype=x.dtype, device=x.device)
+                    for g, x, n in zip(grads, inputs, needs)]
 
         def bwd_fake(inputs: List[Tensor], outs: List[Tensor], saved: List[Tensor], gouts: List[Tensor],
-                     consts: List[int]) -> List[Tensor]:
-            return [x.new_empty(x.shape) for x in inputs]
+                     consts: List[int], needs: List[int]) -> List[Tensor]:
+            return [x.new_empty(x.shape) if n else x.new_empty(0) for x, n in zip(inputs, needs)]
 
         self.fwd_op = torch.library.custom_op(f"{NS}::{name}", fwd_impl, mutates_args=())
         self.fwd_op.register_fake(fwd_fake)
@@ -88,8 +91,10 @@ class OpaqueFunction:
             ins, outs = t[:ctx.n_in], t[ctx.n_in:]
             m = spec.n_out
             g = [gouts[i] if gouts[i] is not None else torch.zeros_like(outs[i]) for i in range(m)]
-            grads = spec.bwd_op(list(ins), list(outs[:m]), list(outs[m:]), g, ctx.consts)
-            return list(grads), ([] if not ctx.consts else None)   # an int list is one pytree leaf
+            needs = [int(bool(n)) for n in ctx.needs_input_grad[0]]
+            grads = spec.bwd_op(list(ins), list(outs[:m]), list(outs[m:]), g, ctx.consts, needs)
+            grads = [gr if n else None for gr, n in zip(grads, needs)]
+            return grads, ([] if not ctx.consts else None)   # an int list is one pytree leaf
 
         self.fwd_op.register_autograd(backward, setup_context=setup_context)
         OPAQUE[name] = self

@@ -36,6 +36,7 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
+from .compile_backend import HipModule
 from . import window_grad as WG
 from .graph_filter import hip_forward, records_grad
 
@@ -68,7 +69,7 @@ def window_edges(connection_window) -> np.ndarray:
 # forward + reverse) in training; the 3x3 convs (embedding, down / up sampling, output) on stock
 # PyTorch-ROCm convolutions
 # ---------------------------------------------------------------------------
-class CustomLayerNorm(nn.Module):
+class CustomLayerNorm(HipModule):
     """x / sqrt(var_c(x) + 1e-5) (unbiased, uncentred), then a per-channel scale (REF7:13-26)."""
 
     def __init__(self, nchannels):
@@ -82,7 +83,7 @@ class CustomLayerNorm(nn.Module):
         return self.weighted_transform(x / torch.sqrt(sigma + 1e-5))
 
 
-class FeedForward(nn.Module):
+class FeedForward(HipModule):
     """1x1 -> depthwise 3x3 -> gelu(x1) * x2 -> 1x1 (REF7:29-48)."""
 
     def __init__(self, dim, ffn_expansion_factor, bias):
@@ -98,7 +99,7 @@ class FeedForward(nn.Module):
         return self.project_out(nn.functional.gelu(x1) * x2)
 
 
-class FFBlock(nn.Module):
+class FFBlock(HipModule):
     """s0 x + s1 FeedForward(norm(x)) (REF7:51-67)."""
 
     def __init__(self, dim, ffn_expansion_factor, bias):
@@ -127,7 +128,7 @@ class FFBlock(nn.Module):
         return self.skip_connect_weight_final[0] * x + self.skip_connect_weight_final[1] * self.ffn(self.norm(x))
 
 
-class OverlapPatchEmbed(nn.Module):
+class OverlapPatchEmbed(HipModule):
     def __init__(self, in_c=3, embed_dim=48, bias=False):   # REF7:72-83
         super().__init__()
         self.proj = nn.Conv2d(in_c, embed_dim, kernel_size=3, stride=1, padding=1, bias=bias)
@@ -136,7 +137,7 @@ class OverlapPatchEmbed(nn.Module):
         return self.proj(x)
 
 
-class Downsample(nn.Module):
+class Downsample(HipModule):
     def __init__(self, n_feat):   # REF7:87-100
         super().__init__()
         self.body = nn.Sequential(nn.Conv2d(n_feat, n_feat // 2, kernel_size=3, stride=1, padding=1, bias=False),
@@ -146,7 +147,7 @@ class Downsample(nn.Module):
         return self.body(x)
 
 
-class Upsample(nn.Module):
+class Upsample(HipModule):
     def __init__(self, n_feat):   # REF7:102-116
         super().__init__()
         self.body = nn.Sequential(nn.Conv2d(n_feat, n_feat * 2, kernel_size=3, stride=1, padding=1, bias=False),
@@ -156,7 +157,7 @@ class Upsample(nn.Module):
         return self.body(x)
 
 
-class FeatureExtraction(nn.Module):
+class FeatureExtraction(HipModule):
     """Two-level encoder / decoder of FFBlocks (REF7:195-270); returns [features]."""
 
     def __init__(self, inp_channels=3, out_channels=48, dim=48, num_blocks=(1, 2, 2, 4), num_refinement_blocks=4,
@@ -182,7 +183,7 @@ class FeatureExtraction(nn.Module):
         return [self.output(out)]
 
 
-class DCestimator(nn.Module):
+class DCestimator(HipModule):
     def __init__(self, dim_in, dim_out, hidden_features):   # REF7:785-799
         super().__init__()
         self.project_in = nn.Conv2d(dim_in, hidden_features * 2, kernel_size=1, bias=False)
@@ -198,7 +199,7 @@ class DCestimator(nn.Module):
 # ---------------------------------------------------------------------------
 # Window graph modules (REF7:274-782)
 # ---------------------------------------------------------------------------
-class _WindowGraphModule(nn.Module):
+class _WindowGraphModule(HipModule):
     """Parameters of GLRFast / GTVFast (REF7:274-371 / :514-611): scalar stats-stencil
     weights (p01 1.0, p02a/p02b/p03 0.5) and multiM [G,F]."""
 
@@ -250,7 +251,7 @@ class GTVFast(_WindowGraphModule):
         return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wG=edge_weights.contiguous(), tapsG=self.taps())
 
 
-class MixtureGTV(nn.Module):
+class MixtureGTV(HipModule):
     """REF7:802-1016.  n_cgd_iters >= 4: two CG stages before the prox update, the rest after
     (the reference indexes rows 0..3; rows past 3 continue the same recurrence)."""
 
@@ -338,7 +339,7 @@ class MixtureGTV(nn.Module):
         return stages(rhs, list(range(2, self.n_cgd_iters)))                              # REF7:970-990
 
 
-class MultiScaleSequenceDenoiser(nn.Module):
+class MultiScaleSequenceDenoiser(HipModule):
     """REF7:1019-1087: s0 y + s1 MixtureGTV(y), 24 graphs x 3 features on the 5x5 diamond (K=12)."""
 
     def __init__(self, device=None, n_cgd_iters: int = 4):

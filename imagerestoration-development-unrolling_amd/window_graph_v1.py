@@ -19,13 +19,14 @@ import torch.nn as nn
 from torch.nn.parameter import Parameter
 
 from . import kernels as K
+from .compile_backend import HipModule
 from . import window_grad as WG
 from .graph_filter import hip_forward, records_grad
 from .window_graph import (CONNECTION_FLAGS_3x3, CONNECTION_FLAGS_5x5, Downsample, FFBlock, MixtureGTV as _MixV7,
                            OverlapPatchEmbed, Upsample, window_edges)
 
 
-class _WindowGraphModuleV1(nn.Module):
+class _WindowGraphModuleV1(HipModule):
     """GLRFast / GTVFast of REF1 (:187-221 / :293-340): multiM only, no stats stencil."""
 
     def __init__(self, n_channels, n_node_fts, n_graphs, connection_window, device=None, M_diag_init=0.4):
@@ -76,7 +77,7 @@ class GTVFast(_WindowGraphModuleV1):
         return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wG=edge_weights.contiguous(), tapsG=self.taps())
 
 
-class FeatureExtraction(nn.Module):
+class FeatureExtraction(HipModule):
     """Four-level encoder / decoder of FFBlocks (REF1:108-184); returns the four decoder levels."""
 
     def __init__(self, inp_channels=3, out_channels=48, dim=48, num_blocks=(1, 2, 2, 4), num_refinement_blocks=4,
@@ -116,7 +117,7 @@ class FeatureExtraction(nn.Module):
         return [self.output(d1), d2, d3, latent]
 
 
-class MixtureGTV(nn.Module):
+class MixtureGTV(HipModule):
     """REF1:472-676 (n_cgd_iters >= 4; the reference block runs 6)."""
 
     solve = _MixV7.solve
@@ -166,7 +167,7 @@ class MixtureGTV(nn.Module):
         return K.win_mix(x, score, None)
 
 
-class SharpeningBlock(nn.Module):
+class SharpeningBlock(HipModule):
     """s0 x + s1 project_out(gelu(a) b), [a; b] = dwconv(project_in(x)) (REF1:768-787)."""
 
     def __init__(self, dim_in, dim_out, hidden_features):
@@ -183,7 +184,7 @@ class SharpeningBlock(nn.Module):
         return self.skip_connect_weight[0] * patchs + self.skip_connect_weight[1] * out
 
 
-class MultiScaleSequenceDenoiser(nn.Module):
+class MultiScaleSequenceDenoiser(HipModule):
     """REF1:790-884: three skip-mixed MixtureGTV blocks, each followed by a SharpeningBlock."""
 
     def __init__(self, device=None):

@@ -105,9 +105,13 @@ def test_compiled_training_matches_eager(irdu):
             perturb_mixture(blk.local_filter, 3)
         return m.to(DEV).train()
 
+    import torch._inductor.metrics as metrics
     ref_losses, ref_grads = _train_two_steps(make(), compiled=False)
+    metrics.reset()
     with icfg.patch(fallback_random=True):
         losses, grads = _train_two_steps(make(), compiled=True)
+    # the stock encoder / decoder ops and losses ran on their ATen kernels: no Triton was generated
+    assert metrics.generated_kernel_count == 0, metrics.generated_kernel_count
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) <= 1e-6 * abs(b), (losses, ref_losses)
     # step 0: same weights, so only fp32 summation order differs (float atomics in the reverse
@@ -119,3 +123,25 @@ def test_compiled_training_matches_eager(irdu):
             got = grads[step][k]
             err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
             assert err <= tol, (step, k, err)
+
+
+def test_v1x0_inference_compile_without_codegen(irdu):
+    """The drop-in v1.0 model (encoder / decoder on stock ops around four HIP filter blocks, S = 10):
+    model.compile() in inference equals eager bitwise and generates no kernels."""
+    import torch._inductor.metrics as metrics
+    torch._dynamo.reset()
+    torch.manual_seed(23)
+    m = irdu.AbtractMultiScaleGraphFilter(
+        3, 3, dims=[8, 16, 16, 32], hidden_dims=[16, 32, 32, 64], nsubnets=[1, 1, 1, 1], ngraphs=[2, 4, 4, 8],
+        num_blocks=[1, 1, 1, 1], num_blocks_out=1, n_cgd_iters=10)
+    for blk in (m.localfilter_scale_00, m.localfilter_scale_01, m.localfilter_scale_02, m.localfilter_scale_03):
+        perturb_mixture(blk.local_filter, 4)
+    m = m.to(DEV).eval()
+    x = torch.rand(2, 3, 64, 64, device=DEV)
+    with torch.no_grad():
+        ref = m(x)
+        metrics.reset()
+        m.compile()
+        got = m(x)
+    assert metrics.generated_kernel_count == 0, metrics.generated_kernel_count
+    assert torch.equal(got, ref)
