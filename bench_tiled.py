@@ -1,6 +1,7 @@
 """Config C5: 2048x2048 RGB images filtered as overlap-save 256x256 windows (tiling.py) by the
-10-stage G=32 image filter; one process per GPU, windows sharded over ranks, no collective in
-the data path (gather of the output canvas only with --gather).
+10-stage G=32 image filter; one process per GPU, (image, window) units sharded over ranks -- whole
+images first -- with no collective in the data path (--gather: rank 0 also receives every rank's
+packed cores, each output pixel once).
 
     python bench_tiled.py [--images 2] [--size 2048] [--tile 256] [--halo 32] [--micro-batch 64]
 
@@ -47,7 +48,7 @@ def main():
     _, noisy = synthetic_patches(args.images, seed=2204, h=args.size, w=args.size)
     noisy = noisy.to(dev)
     run = lambda: tiling.tiled_forward(model, noisy, tile=args.tile, halo=args.halo, align=16,  # noqa: E731
-                                       micro_batch=args.micro_batch, gather=args.gather)
+                                       micro_batch=args.micro_batch, gather="rank0" if args.gather else "none")
     run()
     benchlib.barrier(world, dev)
     t0 = time.perf_counter()
@@ -76,7 +77,8 @@ def main():
                                      "window_overhead": round(nwin * args.tile ** 2 / args.size ** 2, 3),
                                      "weights": "tests/golden/msgf_trained_g32_s10.safetensors" if trained
                                      else "reference init",
-                                     "parallelism": f"windows sharded x{world}"},
+                                     "parallelism": f"(image, window) units sharded x{world}, "
+                                                    + ("cores gathered to rank 0" if args.gather else "no collective")},
                           "tiled_vs_whole": parity}), flush=True)
     benchlib.finish(world)
 

@@ -71,11 +71,35 @@ def join_or_spawn(gpus: int, argv: Optional[List[str]] = None, script: Optional[
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    if bad:
-        print(f"benchlib: rank exit codes {rcs}", file=sys.stderr)
-    raise SystemExit(bad[0] if bad else 0)
+    raise SystemExit(_wait_all(procs))
+
+
+def _wait_all(procs, poll_s: float = 0.2, grace_s: float = 10.0) -> int:
+    """Wait for every rank; when one exits non-zero, stop the others (they would block in the
+    process group's rendezvous or a collective) and return that first failing status, as torchrun does."""
+    import time
+    first_bad = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad and first_bad is None:
+            first_bad = bad[0]
+            print(f"benchlib: a rank exited with {first_bad}; stopping the others (exit codes {rcs})",
+                  file=sys.stderr)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.monotonic() + grace_s
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.0, deadline - time.monotonic()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return first_bad
+        if all(rc is not None for rc in rcs):
+            return 0
+        time.sleep(poll_s)
 
 
 def _check_devices(world: int, dry_run: bool) -> None:

@@ -38,12 +38,8 @@ struct WgArgs {
   uint32_t nblk;
 };
 
-// output tile per wave: 128 x 96 (12 accumulators, 192 registers, one wave per SIMD) or 64 x 96
-// (6 accumulators, two waves per SIMD: one wave's splits and loads overlap the other's MFMAs)
-static int wgrad_tile_variant() {
-  static const int v = [] { const char* e = getenv("GRR_WGRAD_TILE"); return e ? atoi(e) : 43; }();
-  return v;
-}
+// output tile per wave: 128 x 96 (12 accumulators in AGPRs, one wave per SIMD).  A 64 x 96 tile at two
+// waves per SIMD measured slower (1.03 vs 0.86 ms at 512 x 96) and is not built.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // exact split v = v0 + v1 + v2 of 8 values into bf16 terms (RNE casts: v_cvt_pk_bf16_f32)
@@ -253,13 +249,15 @@ struct WgPlan {
 };
 
 // chunks of whole 32-pixel steps sized for ~3 rounds of waves over the 1024 SIMDs, at most 1024
-// chunks of workspace; the operand order that pads the output tiles least
+// chunks and kWgradWsBudget bytes of workspace (the wide v1.0 LNB weights, 2 hid x C = 1536 x 384,
+// would otherwise take 1024 x 2.4 MB); the operand order that pads the output tiles least
+static constexpr int64_t kWgradWsBudget = 128ll << 20;
+
 static WgPlan wgrad_plan(int B, int M, int K, int64_t P) {
   WgPlan p{};
-  const int v = wgrad_tile_variant();
-  p.ta = v == 43 ? 4 : 2;
+  p.ta = 4;
   p.tb = 3;
-  const int wps = v == 43 ? 1 : 2;
+  const int wps = 1;
   auto padded = [&](int rows_a, int rows_b) {
     const int64_t ra = 32 * p.ta, rb = 32 * p.tb;
     return ((rows_a + ra - 1) / ra * ra) * ((rows_b + rb - 1) / rb * rb);
@@ -278,7 +276,8 @@ static WgPlan wgrad_plan(int B, int M, int K, int64_t P) {
   for (;;) {
     p.cpi = (int)((P + cp - 1) / cp);
     p.nchunk = (int64_t)B * p.cpi;
-    if (p.nchunk <= 1024 || cp >= pmax) break;
+    if ((p.nchunk <= 1024 && p.nchunk * (int64_t)M * K * (int64_t)sizeof(float) <= kWgradWsBudget) || cp >= pmax)
+      break;
     cp = std::min<int64_t>(pmax, cp * 2);
   }
   p.CP = cp;
@@ -315,13 +314,8 @@ grr_status grr_wgrad(const float* a, const float* bop, float* out, void* workspa
   w.P = P; w.CP = p.CP; w.cpi = p.cpi; w.nta = p.nta; w.ntb = p.ntb; w.nblk = (uint32_t)p.nwaves;
   // 16-byte row loads need 4-aligned rows and chunk starts (CP is a multiple of 32)
   const dim3 g(w.nblk), t(64);
-  if (p.ta == 4) {
-    if (P % 4 == 0) hipLaunchKernelGGL((wgrad_x3_kernel<4, 3, true, 1>), g, t, 0, s, w);
-    else hipLaunchKernelGGL((wgrad_x3_kernel<4, 3, false, 1>), g, t, 0, s, w);
-  } else {
-    if (P % 4 == 0) hipLaunchKernelGGL((wgrad_x3_kernel<2, 3, true, 2>), g, t, 0, s, w);
-    else hipLaunchKernelGGL((wgrad_x3_kernel<2, 3, false, 2>), g, t, 0, s, w);
-  }
+  if (P % 4 == 0) hipLaunchKernelGGL((wgrad_x3_kernel<4, 3, true, 1>), g, t, 0, s, w);
+  else hipLaunchKernelGGL((wgrad_x3_kernel<4, 3, false, 1>), g, t, 0, s, w);
   grr_status st = launch_status("grr_wgrad");
   if (st != GRR_OK) return st;
   const int64_t n = (int64_t)M * K;

@@ -148,6 +148,14 @@ class OverlappedGradReducer:
     ``prepare()`` starts a step: it drains anything a step left behind (an exception between
     backward and ``finish()``) and resets the bucket state, so a stale step can never leak into
     the next one's averages; a second backward inside one step raises instead of reducing twice.
+
+    Streams (GPU gradients): the reverse runs on several HIP streams (the feature branch's side
+    stream, the solver's level stream), and autograd runs a parameter's accumulation -- and its
+    post-accumulate hook -- on the stream that produced the gradient.  The hook therefore records
+    an event on its current stream, and a bucket is flattened and reduced on the reducer's own
+    stream after waiting on the events of every parameter in it: the flatten can never read a
+    gradient another stream is still writing.  ``finish()`` orders the caller's stream after the
+    reductions before the averages are written back.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 32.0, group=None):
@@ -160,6 +168,7 @@ class OverlappedGradReducer:
         if self.ws > 1:
             self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         self.launched_in_backward = 0
+        self._streams = {}
         self._reset()
 
     def _reset(self):
@@ -167,6 +176,12 @@ class OverlappedGradReducer:
         self._next = 0
         self._work = [None] * len(self.buckets)
         self._flat = [None] * len(self.buckets)
+        self._ready = {}            # id(param) -> event recorded on the stream that accumulated its grad
+
+    def _stream(self, dev: torch.device):
+        if dev not in self._streams:
+            self._streams[dev] = torch.cuda.Stream(device=dev)
+        return self._streams[dev]
 
     def prepare(self) -> None:
         """Begin a step (call before loss.backward())."""
@@ -177,6 +192,10 @@ class OverlappedGradReducer:
 
     def _on_grad(self, p):
         i = self._bucket_of[id(p)]
+        if p.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(p.device))
+            self._ready[id(p)] = ev
         self._pending[i] -= 1
         if self._pending[i] < 0:
             raise RuntimeError("OverlappedGradReducer: a parameter's gradient arrived twice in one step "
@@ -187,10 +206,29 @@ class OverlappedGradReducer:
 
     def _launch(self, i: int):
         bk = self.buckets[i]
-        for p in bk:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        self._flat[i] = torch.cat([p.grad.reshape(-1) for p in bk])
+        if not bk[0].is_cuda:
+            for p in bk:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            self._flat[i] = torch.cat([p.grad.reshape(-1) for p in bk])
+        else:
+            # flatten + reduce on the reducer's stream, after every producing stream's accumulation
+            red = self._stream(bk[0].device)
+            red.wait_stream(torch.cuda.current_stream(bk[0].device))    # zero-filled grads, earlier work
+            for p in bk:
+                ev = self._ready.get(id(p))
+                if ev is not None:
+                    red.wait_event(ev)
+            with torch.cuda.stream(red):
+                for p in bk:
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+                    else:
+                        p.grad.record_stream(red)
+                self._flat[i] = torch.cat([p.grad.reshape(-1) for p in bk])
+                self._work[i] = dist.all_reduce(self._flat[i], group=self.group, async_op=True)
+            self._next = i + 1
+            return
         self._work[i] = dist.all_reduce(self._flat[i], group=self.group, async_op=True)
         self._next = i + 1
 
@@ -202,6 +240,10 @@ class OverlappedGradReducer:
             self._launch(self._next)
         for i, bk in enumerate(self.buckets):
             self._work[i].wait()
+            if bk[0].is_cuda:
+                cur = torch.cuda.current_stream(bk[0].device)
+                cur.wait_stream(self._stream(bk[0].device))
+                self._flat[i].record_stream(cur)
             _unflatten_mean(self._flat[i], bk, self.ws)
         n = len(self.buckets)
         self._reset()

@@ -166,7 +166,8 @@ def _level_side(dev: torch.device) -> "torch.cuda.Stream":
 
 def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn) -> None:
     """Apply a per-level reverse at full resolution and, through D / U, at half resolution."""
-    if LEVEL_STREAMS and x.is_cuda and not torch.compiler.is_compiling():
+    if LEVEL_STREAMS and x.is_cuda and not torch.compiler.is_compiling() \
+            and not torch.cuda.is_current_stream_capturing():
         main = torch.cuda.current_stream(x.device)
         side = _level_side(x.device)
         side.wait_stream(main)                # x, g (and every buffer the half level accumulates into) ready

@@ -15,13 +15,16 @@ The reference evaluates whole images padded to a multiple of 16 (scripts_v2/...s
   geometrically with distance, so the result converges to the whole-image one as ``halo``
   grows (tests/test_gpu_tiling.py measures it).
 
-Windows are batched through the model (``micro_batch`` windows per launch).  With N ranks
-each rank filters a contiguous share of the windows (sharding.shard_range, no collective);
-``gather=True`` sums the disjoint per-rank canvases with one all-reduce.
+Windows are batched through the model (``micro_batch`` windows per launch).  The work units are
+(image, window) pairs in image-major order; with N ranks each rank filters a contiguous share of them
+(sharding.shard_range), so a batch of at least N images shards whole images and a single image
+shards its windows -- no collective in the data path either way.  Each rank
+returns its own cores; ``gather="rank0"`` additionally sends every rank's cores -- only the cores,
+each output pixel once -- to rank 0, which assembles the full canvas.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import List, Optional, Tuple, Union
 
 import torch
 
@@ -55,27 +58,70 @@ def tile_grid(h: int, w: int, tile: int = 256, halo: int = 32, align: int = 16) 
             for wc, c0, c1 in _axis(w, tile, halo, align)]
 
 
+def rank_units(b: int, n_windows: int, rank: int, world: int) -> List[Tuple[int, int]]:
+    """This rank's (image, window) units: a contiguous share of the image-major enumeration."""
+    s, e = sharding.shard_range(b * n_windows, rank, world)
+    return [divmod(u, n_windows) for u in range(s, e)]
+
+
+def _core_numel(units, wins, cout: int) -> int:
+    return sum(cout * (wins[wi][3] - wins[wi][2]) * (wins[wi][5] - wins[wi][4]) for _, wi in units)
+
+
 @torch.no_grad()
 def tiled_forward(model, img: torch.Tensor, tile: int = 256, halo: int = 32, align: int = 16,
-                  micro_batch: int = 32, out_channels: Optional[int] = None, gather: bool = True) -> torch.Tensor:
+                  micro_batch: int = 32, out_channels: Optional[int] = None,
+                  gather: Union[bool, str] = "none") -> Optional[torch.Tensor]:
     """Filter img [B,C,H,W] window by window; returns the [B,Cout,H,W] output canvas.
 
-    Multi-rank: every rank must call this with the same image; each filters its share of the
-    windows.  gather=False returns the rank's partial canvas (zeros outside its cores)."""
+    One rank: the whole canvas.  Several ranks (every rank calls this with the same image):
+    ``gather="none"`` (or False) returns the rank's canvas holding its own cores (zeros elsewhere),
+    with no communication; ``gather="rank0"`` (or True) returns the full canvas on rank 0 and None on
+    the other ranks, after one gather of the packed cores."""
+    mode = {True: "rank0", False: "none"}.get(gather, gather)
+    if mode not in ("none", "rank0"):
+        raise ValueError(f"gather must be 'none' or 'rank0' (got {gather!r})")
     b, c, h, w = img.shape
     th, tw = min(tile, h), min(tile, w)
     wins = tile_grid(h, w, tile, halo, align)
     rank, world = sharding.world()
-    s, e = sharding.shard_range(len(wins), rank, world)
-    mine = wins[s:e]
+    mine = rank_units(b, len(wins), rank, world)
     cout = out_channels if out_channels is not None else c
     canvas = torch.zeros((b, cout, h, w), dtype=img.dtype, device=img.device)
     for i in range(0, len(mine), micro_batch):
         chunk = mine[i:i + micro_batch]
-        x = torch.cat([img[:, :, wr:wr + th, wc:wc + tw] for wr, wc, *_ in chunk]).contiguous()
+        x = torch.cat([img[bi:bi + 1, :, wins[wi][0]:wins[wi][0] + th, wins[wi][1]:wins[wi][1] + tw]
+                       for bi, wi in chunk]).contiguous()
         y = model(x)
-        for j, (wr, wc, r0, r1, c0, c1) in enumerate(chunk):
-            canvas[:, :, r0:r1, c0:c1] = y[j * b:(j + 1) * b, :, r0 - wr:r1 - wr, c0 - wc:c1 - wc]
-    if gather and world > 1:
-        torch.distributed.all_reduce(canvas)
+        for j, (bi, wi) in enumerate(chunk):
+            wr, wc, r0, r1, c0, c1 = wins[wi]
+            canvas[bi, :, r0:r1, c0:c1] = y[j, :, r0 - wr:r1 - wr, c0 - wc:c1 - wc]
+    if world == 1 or mode == "none":
+        return canvas
+    return _gather_cores(canvas, wins, b, cout, rank, world)
+
+
+def _gather_cores(canvas: torch.Tensor, wins, b: int, cout: int, rank: int, world: int) -> Optional[torch.Tensor]:
+    """Rank 0 receives every rank's cores (packed, padded to the largest share) and fills its canvas."""
+    import torch.distributed as dist
+    sizes = [_core_numel(rank_units(b, len(wins), r, world), wins, cout) for r in range(world)]
+    n = max(sizes)
+    packed = canvas.new_zeros(n)
+    off = 0
+    for bi, wi in rank_units(b, len(wins), rank, world):
+        _, _, r0, r1, c0, c1 = wins[wi]
+        k = cout * (r1 - r0) * (c1 - c0)
+        packed[off:off + k] = canvas[bi, :, r0:r1, c0:c1].reshape(-1)
+        off += k
+    bufs = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+    dist.gather(packed, bufs, dst=0)
+    if rank != 0:
+        return None
+    for r in range(1, world):
+        off = 0
+        for bi, wi in rank_units(b, len(wins), r, world):
+            _, _, r0, r1, c0, c1 = wins[wi]
+            k = cout * (r1 - r0) * (c1 - c0)
+            canvas[bi, :, r0:r1, c0:c1] = bufs[r][off:off + k].view(cout, r1 - r0, c1 - c0)
+            off += k
     return canvas

@@ -38,7 +38,7 @@ import torch.nn as nn
 import yaml
 from torch.utils.data import Dataset, Sampler
 
-from . import sharding
+from . import sharding, stream_guard
 
 LOG = logging.getLogger("irdu_amd.train")
 
@@ -291,8 +291,9 @@ class Trainer:
         self.reducer.prepare()
         noisy = noisy_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
         clean = clean_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
-        loss = self.loss(noisy, clean)
-        loss.backward()
+        with stream_guard.maybe_guard():       # GRR_STREAM_GUARD=1: check the internal-stream invariant
+            loss = self.loss(noisy, clean)
+            loss.backward()
         self.reducer.finish()
         self.optimizer.step()
         self.lr_scheduler.step()

@@ -71,4 +71,23 @@ def test_child_failure_propagates(tmp_path):
         "sys.exit(3 if r == 1 else 0)\n")
     r = subprocess.run([sys.executable, str(script)], env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 3
-    assert "rank exit codes [0, 3]" in r.stderr
+    assert "a rank exited with 3" in r.stderr
+
+
+def test_failed_rank_stops_a_blocked_rank(tmp_path):
+    """Rank 1 dies while rank 0 stays blocked (as in a rendezvous or collective): the launcher stops
+    rank 0 and returns rank 1's status instead of waiting forever."""
+    import time
+    script = tmp_path / "child.py"
+    script.write_text(
+        "import os, sys, time\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import benchlib\n"
+        "w, r, l = benchlib.join_or_spawn(2, dry_run=True)\n"
+        "if r == 1:\n"
+        "    sys.exit(5)\n"
+        "time.sleep(600)\n")
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(script)], env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 5
+    assert time.monotonic() - t0 < 60

@@ -41,20 +41,33 @@ def _tile_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.manual_seed(0)
-        img = torch.rand(1, 3, 96, 128)
         conv = torch.nn.Conv2d(3, 2, 3, padding=1, padding_mode="replicate", bias=False)
         torch.nn.init.constant_(conv.weight, 0.1)
-        with torch.no_grad():
-            out = tiling.tiled_forward(conv, img, tile=64, halo=16, align=16, micro_batch=2, out_channels=2)
-            whole = conv(img)
-        q.put((rank, float((out - whole).abs().max())))
+        res = {}
+        for b in (1, 3):          # one image: windows sharded; three: whole images + a split one
+            img = torch.rand(b, 3, 96, 128)
+            with torch.no_grad():
+                whole = conv(img)
+                full = tiling.tiled_forward(conv, img, tile=64, halo=16, align=16, micro_batch=2, out_channels=2,
+                                            gather="rank0")
+                local = tiling.tiled_forward(conv, img, tile=64, halo=16, align=16, micro_batch=2, out_channels=2)
+            wins = tiling.tile_grid(96, 128, 64, 16, 16)
+            own = torch.zeros(b, 1, 96, 128)
+            for bi, wi in tiling.rank_units(b, len(wins), rank, world):
+                _, _, r0, r1, c0, c1 = wins[wi]
+                own[bi, :, r0:r1, c0:c1] = 1.0
+            res[b] = (None if full is None else float((full - whole).abs().max()),
+                      float(((local - whole) * own).abs().max()), float((local * (1 - own)).abs().max()),
+                      float(own.sum()))
+        q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-def test_window_sharding_over_ranks_gathers_whole_image():
-    """gloo world 2: each rank filters its share of the windows, the all-reduce of the disjoint
-    canvases rebuilds the whole image (a 3x3 replicate-padded conv: receptive field < halo)."""
+def test_window_sharding_over_ranks_without_collective():
+    """gloo world 2: each rank filters its share of the (image, window) units and returns its own
+    cores with no collective; gather="rank0" assembles the whole image on rank 0 from the packed cores
+    alone (a 3x3 replicate-padded conv: receptive field < halo)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -70,4 +83,16 @@ def test_window_sharding_over_ranks_gathers_whole_image():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0] <= 1e-6 and res[1] <= 1e-6
+    for b in (1, 3):
+        assert res[0][b][0] <= 1e-6 and res[1][b][0] is None
+        for r in (0, 1):
+            assert res[r][b][1] <= 1e-6 and res[r][b][2] == 0.0      # own cores right, nothing else written
+        assert res[0][b][3] + res[1][b][3] == b * 96 * 128               # the shares partition the pixels
+
+
+def test_units_shard_whole_images_first():
+    wins = tiling.tile_grid(2048, 2048, 256, 32, 16)
+    for world in (2, 4, 8):
+        for rank in range(world):
+            units = tiling.rank_units(8, len(wins), rank, world)
+            assert {bi for bi, _ in units} == set(range(rank * 8 // world, (rank + 1) * 8 // world))
