@@ -45,7 +45,7 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.replace(".hip", ".o"))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
@@ -54,8 +54,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             cmd.insert(2, "-Rpass-analysis=kernel-resource-usage")
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
         objs.append(obj)
+    # one hipcc per source, in parallel (MAX_JOBS caps it, as on the GPU box)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    with ThreadPoolExecutor(jobs) as pool:
+        for r in pool.map(lambda c: subprocess.run(c), cmds):
+            if r.returncode != 0:
+                raise subprocess.CalledProcessError(r.returncode, r.args)
     tmp = LIB + ".tmp"
     subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
     os.replace(tmp, LIB)

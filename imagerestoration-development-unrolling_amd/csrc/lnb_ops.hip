@@ -484,7 +484,11 @@ __global__ void lnb_w1_pack16_kernel(const float* __restrict__ w1, const float* 
         if (pj < hid) {
           const int row = (comp ? hid : 0) + pj;
           const int sc = head16_row_exp(w1, ln_w, row, C, R);
-          word = __float_as_uint(ldexpf(wdw[(int64_t)row * 9 + t], -(sc + L6_XE)));
+          // the gate's exp2 argument and product fold in here (lnb_head16_kernel, gate): mask taps
+          // carry -log2(e), value taps -ln(2), so m' = -log2(e) m, v' = -ln(2) v, m' v' = m v and
+          // sigmoid(m) = 1 / (1 + 2^m')
+          const float fold = comp ? -0.69314718055994531f : -1.44269504088896341f;
+          word = __float_as_uint(ldexpf(wdw[(int64_t)row * 9 + t], -(sc + L6_XE)) * fold);
         }
       }
     }
@@ -633,7 +637,15 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
       a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
   const int gx = x0 + col;
+  // g stores: the lane's byte offset of output row k of its half (row y0 + r0 + k, its column) in voffset
+  // -- out of range for rows past the tile or the image and for columns past the image, fixed for the
+  // whole kernel (vrow) -- and the channel plane and row, wave-uniform, in soffset
+  constexpr uint32_t kOut = 0x80000000u;
   const int nrow = min(L6_TH, H - y0) - r0;      // output rows of this lane's half inside the tile and image
+  const uint32_t vcol = gx < W ? (uint32_t)((y0 + r0) * W + gx) * 4u : kOut;
+  uint32_t vrow[RA];
+#pragma unroll
+  for (int k = 0; k < RA; ++k) vrow[k] = k < nrow ? vcol : kOut;
   float tp[2][18];                               // taps of the chunk the next gate evaluates
   auto load_taps = [&](int c) {
     const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + 2 * wave * 18;
@@ -642,16 +654,16 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
 #pragma unroll
       for (int i = 0; i < 18; ++i) tp[p][i] = t[p * 18 + i];
   };
-  // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c, h buffer c & 1
+  // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c, h buffer c & 1.  The taps carry
+  // the exp2 fold of lnb_w1_pack16_kernel: m' = -log2(e) m, v' = -ln(2) v, g = m' v' / (1 + 2^m').
   auto gate = [&](int c) {
     const float* hbuf = smem + (c & 1) * L6_HBUF;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int jj = L6_NP * c + 2 * wave + p;
-      // rows this lane stores (0 outside the hidden channels / image): the row test below is then
-      // one compare + select per output (no exec-masked block in the middle of the gate)
-      const uint32_t nst = (jj < hid && gx < W) ? (uint32_t)max(nrow, 0) : 0u;
-      const uint32_t off0 = (uint32_t)(jj * HW + (y0 + r0) * W + gx) * 4u;
+      // wave-uniform: past the hidden channels nothing is stored (soffset is not range-checked)
+      const int soff0 = jj < hid ? jj * HW * 4 : 0;
+      const bool live = jj < hid;
       const float* hp = hbuf + (2 * wave + p) * L6_PP + 2 * col;
       f32x2 win[3][3];                          // rows (i mod 3) x halo columns col .. col + 2
 #pragma unroll
@@ -660,19 +672,17 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
         if (i >= 2) {
-          float m = 0.f, v = 0.f;
+          const f32x2 h0 = win[(i - 2) % 3][0];
+          float m = tp[p][0] * h0[0], v = tp[p][1] * h0[1];
 #pragma unroll
-          for (int ay = 0; ay < 3; ++ay)
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {
-              const f32x2 hv = win[(i - 2 + ay) % 3][ax];
-              m += tp[p][2 * (ay * 3 + ax)] * hv[0];
-              v += tp[p][2 * (ay * 3 + ax) + 1] * hv[1];
-            }
-          const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __expf(-m));   // sigmoid(m) m v
-          const uint32_t msk = 0u - (uint32_t)((uint32_t)(i - 2) < nst);
-          const uint32_t off = ((off0 + (uint32_t)((i - 2) * W) * 4u) & msk) | (0x80000000u & ~msk);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, off, 0, 0);
+          for (int t = 1; t < 9; ++t) {
+            const f32x2 hv = win[(i - 2 + t / 3) % 3][t % 3];
+            m = __builtin_fmaf(tp[p][2 * t], hv[0], m);
+            v = __builtin_fmaf(tp[p][2 * t + 1], hv[1], v);
+          }
+          const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, live ? vrow[i - 2] : kOut,
+                                                soff0 + (i - 2) * W * 4, 0);
         }
       }
     }
@@ -870,15 +880,9 @@ static int head_ks(int C) { return (C + 31) / 32; }
 static int head_nb(int KS) { return KS <= 3 ? 4 : 3; }
 static int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }
 // GEMM1 on the fp16 two-term head (lnb_head16_kernel): C <= 96 (its 2-slot ring + 2 x 64 KB of
-// h planes fill the CU's LDS at 6 k-steps); GRR_LNB_HEAD=bf16 selects the split-bf16 head (A/B)
+// h planes fill the CU's LDS at 6 k-steps); 96 < C <= 128 runs the split-bf16 head (lnb_head_kernel)
 static int head16_ks(int C) { return (C + 15) / 16; }
-static bool head16_enabled(int C) {
-  static const bool bf16 = [] {
-    const char* e = getenv("GRR_LNB_HEAD");
-    return e && e[0] == 'b';
-  }();
-  return !bf16 && head16_ks(C) <= 6;
-}
+static bool head16_enabled(int C) { return head16_ks(C) <= 6; }
 static int64_t head_pack_floats(int C, int hid) {
   const int64_t bf = (int64_t)((hid + LH_JC - 1) / LH_JC) * head_images(head_ks(C)) * 256;
   const int64_t f16 = (int64_t)((hid + L6_NP - 1) / L6_NP) * head16_images(head16_ks(C)) * 256;

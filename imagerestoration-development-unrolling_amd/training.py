@@ -11,6 +11,7 @@ Mirrors (reference paths):
     :120-151  model / losses (L1 + 0.1 MSE(enc-dec) + 0.5 MSE(latent-perturbed decode))
     :153-171  Adam(4e-4, eps 1e-8), MultiStepLR(gamma = 0.5**0.25) -> CosineAnnealingLR (SequentialLR)
     :186-224  training step, checkpoint dict {'i', 'model', 'optimizer', 'lr_scheduler'}
+    :235-288  periodic validation: reflect-pad to x16, crop, clamp, img_as_ubyte, mean PSNR (validate)
 
 The reference's run_train.py stops after building the dataloader; the YAML here adds
 ``model:`` and ``train:`` sections so the same entry point runs the training loop of the
@@ -167,6 +168,106 @@ class SyntheticNoisyPatches(Dataset):
 DATASETS = {c.__name__: c for c in (AddictiveGaussianNoiseImagePair, SyntheticNoisyPatches)}
 
 
+# ---------------------------------------------------------------------------
+# periodic validation (scripts_v2/run_abtract_lightformer_GGTV_GGLR_sigma25.py:235-288)
+# ---------------------------------------------------------------------------
+class TestImagesCSV:
+    """Whole clean test images listed in a csv (column ``path``, as the reference's
+    dataset/CBSD68_testing_data_info.csv), HWC float32 in [0, 1] on the uint8 grid (:250-258)."""
+
+    def __init__(self, csv_path, root_folder="", **_ignored):
+        import pandas as pd
+        self.paths = [os.path.join(root_folder, p) for p in pd.read_csv(csv_path, index_col="index")["path"].tolist()]
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __getitem__(self, idx):
+        from PIL import Image
+        return np.array(Image.open(self.paths[idx])).astype(np.float32) / 255.0
+
+
+class SyntheticTestImages:
+    """Deterministic synthetic clean test images (no image data ships with the reference); the default
+    sizes are not multiples of 16, so the reflect padding of the recipe is exercised."""
+
+    def __init__(self, n_images=4, height=100, width=140, n_channels=3, seed=68, **_ignored):
+        self.n, self.h, self.w, self.c, self.seed = n_images, height, width, n_channels, seed
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, idx):
+        return synthetic_clean_patch(np.random.RandomState(self.seed * 7919 + idx), self.h, self.w, self.c)
+
+
+VAL_DATASETS = {c.__name__: c for c in (TestImagesCSV, SyntheticTestImages)}
+
+
+def _img_as_ubyte(x: np.ndarray) -> np.ndarray:
+    """skimage.util.img_as_ubyte of a float image in [0, 1] (the reference's :269): x * 255 rounded to
+    the nearest integer (half to even), as uint8."""
+    return np.clip(np.rint(x.astype(np.float64) * 255.0), 0, 255).astype(np.uint8)
+
+
+@torch.no_grad()
+def validate(model: nn.Module, images, sigma: float = 25.0, factor: int = 16, seed: int = 2204,
+             device=None) -> float:
+    """The reference's test loop (:235-288): per image, add N(0, sigma/255) noise from one
+    RandomState(seed) stream, reflect-pad the bottom / right to a multiple of ``factor`` (only a side
+    that is not already one), filter, crop, clamp to [0, 1], quantise with img_as_ubyte, MSE against
+    the clean image x 255, PSNR = 20 log10(255 / sqrt(MSE)); returns the mean PSNR over the images.
+
+    Several ranks: each filters a contiguous share of the images -- the noise draws follow the global
+    image order, as one rank would make them -- and the PSNR sum and count are all-reduced."""
+    rank, world = sharding.world()
+    was_training = model.training
+    model.eval()
+    if device is None:
+        device = next(model.parameters()).device
+    rs = np.random.RandomState(seed=seed)
+    s, e = sharding.shard_range(len(images), rank, world)
+    psnrs = []
+    for i in range(len(images)):
+        img_true = np.asarray(images[i], dtype=np.float32)
+        noisy_raw = img_true.copy()
+        noisy_raw += rs.normal(0, sigma / 255.0, img_true.shape)     # float32 += float64 draws (:258)
+        if not s <= i < e:
+            continue
+        noisy = torch.from_numpy(noisy_raw).permute(2, 0, 1).unsqueeze(0)
+        h, w = noisy.shape[2], noisy.shape[3]
+        H, W = ((h + factor) // factor) * factor, ((w + factor) // factor) * factor
+        padh = H - h if h % factor != 0 else 0
+        padw = W - w if w % factor != 0 else 0
+        noisy = nn.functional.pad(noisy, (0, padw, 0, padh), "reflect")
+        restored = model(noisy.to(device).contiguous())[:, :, :h, :w]
+        restored = torch.clamp(restored, 0, 1).cpu().permute(0, 2, 3, 1).squeeze(0).numpy()
+        restored = _img_as_ubyte(restored).astype(np.float32)
+        img_true_255 = np.rint(img_true.astype(np.float64) * 255.0).astype(np.float32)   # the uint8 image (:253)
+        mse = np.square(img_true_255 - restored).mean()                                  # float32, as :273
+        psnrs.append(float(20 * np.log10(np.float32(255.0) / np.sqrt(mse))))
+    acc = torch.tensor([float(np.sum(psnrs)), float(len(psnrs))], dtype=torch.float64)
+    if world > 1:
+        if torch.distributed.get_backend() == "nccl":
+            acc = acc.to(device)
+        torch.distributed.all_reduce(acc)
+    if was_training:
+        model.train()
+    return float(acc[0] / acc[1])
+
+
+def create_val_dataset(conf: dict):
+    """``datasets.val`` of the YAML ({type, dataset_args, sigma, factor}), or None."""
+    vconf = conf.get("datasets", {}).get("val")
+    if not vconf:
+        return None, {}
+    cls = VAL_DATASETS.get(vconf["type"])
+    if cls is None:
+        raise ValueError(f"Validation dataset {vconf['type']} is not found.")
+    return cls(**vconf.get("dataset_args", {})), {"sigma": float(vconf.get("sigma", 25.0)),
+                                                   "factor": int(vconf.get("factor", 16))}
+
+
 class ResumeableSampler(Sampler):
     """Deterministic in-order sampling that resumes after ``current_sample`` (data_sampler.py:6-31).
     With world_size > 1 each rank yields its own contiguous slice of every global batch, and the
@@ -271,6 +372,7 @@ class Trainer:
         # all-reduces overlapped with the reverse sweep (post-accumulate-grad hooks); inert on one rank
         self.reducer = sharding.OverlappedGradReducer(self.model.parameters(), bucket_mb=self.bucket_mb)
         self.i = 0
+        self.val_history: List[Tuple[int, float]] = []     # (iteration, mean test PSNR)
 
     def loss(self, noisy: torch.Tensor, clean: torch.Tensor) -> torch.Tensor:
         m = self.model
@@ -361,6 +463,8 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
     total = max_iters if max_iters is not None else int(tconf.get("total_iters", spe))
     every = int(tconf.get("checkpoint_every", 5000))
     verbose = int(tconf.get("verbose_every", 100))
+    val_set, val_args = create_val_dataset(conf)
+    val_every = int(tconf.get("val_every", 0)) if val_set is not None else 0   # the reference's VERBOSE_RATE
 
     def save():
         if rank == 0:
@@ -385,6 +489,11 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
             if trainer.i % every == 0:
                 save()
                 saved_at = trainer.i
+            if val_every and trainer.i % val_every == 0:
+                psnr = validate(trainer.model, val_set, device=device, **val_args)
+                trainer.val_history.append((trainer.i, psnr))
+                if rank == 0:
+                    LOG.info("FINISH VAL EPOCH %d - iter=%d - psnr_testing=%.4f", epoch, trainer.i, psnr)
         if not stepped and trainer.i < total:
             raise RuntimeError(f"epoch {epoch} yielded no batch (dataset {len(dataset)}, batch {bs}, "
                                f"{world} ranks, drop_last {ds_conf['dataloader_args'].get('drop_last', False)})")

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--variant", default="auto", choices=["auto", "strips", "independent"])
     ap.add_argument("--graphs", type=int, default=32)
     ap.add_argument("--fts", type=int, default=3)
+    ap.add_argument("--split", action="store_true", help="LNB: time the head and the mix apart")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
     dev = torch.device("cuda", 0)
@@ -88,6 +89,7 @@ def main():
             fn()
         torch.cuda.synchronize()
         timer = K.LaunchTimer()
+        timer.split_lnb = args.split
         K.set_timer(timer)
         for _ in range(args.iters):
             fn()

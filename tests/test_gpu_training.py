@@ -28,8 +28,11 @@ def test_run_train_example_v1x0_yaml_and_resume(T, tmp_path):
     conf["path"]["root_dir"] = str(tmp_path)
     conf["train"].update(total_iters=4, checkpoint_every=2, verbose_every=1)
     conf["datasets"]["train"]["dataset_args"]["max_num_patchs"] = 64
+    conf["train"]["val_every"] = 2
     tr = T.run(conf, device=torch.device("cuda:0"))
     assert tr.i == 4
+    # the reference's periodic test (reflect-pad to x16 of 100 x 140, crop, ubyte PSNR) ran on the HIP model
+    assert [i for i, _ in tr.val_history] == [2, 4] and all(10.0 < p < 60.0 for _, p in tr.val_history)
     ck = sorted(os.listdir(T.checkpoint_dir(conf)))
     assert ck == ["checkpoint_iter00000002.pt", "checkpoint_iter00000004.pt"]
     # the graph filters received gradients and moved

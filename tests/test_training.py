@@ -287,3 +287,83 @@ def test_data_parallel_run_over_epochs_stays_in_sync(tmp_path):
     assert res[0][0] == res[1][0] == 5
     for k in res[0][1]:
         assert np.array_equal(res[0][1][k], res[1][1][k]), k
+
+
+class _PadProbe(torch.nn.Module):
+    """Identity that records the shapes it sees (the validation recipe pads to multiples of 16)."""
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.ones(()))
+        self.seen = []
+
+    def forward(self, x):
+        self.seen.append(tuple(x.shape))
+        return x * self.w
+
+
+def _reference_val_psnr(images, sigma=25.0, seed=2204):
+    """scripts_v2/run_abtract_lightformer_GGTV_GGLR_sigma25.py:240-288 for an identity model, restated
+    in numpy: noise from one RandomState stream, pad / crop (a no-op for identity), clamp, ubyte, PSNR."""
+    rs = np.random.RandomState(seed=seed)
+    out = []
+    for img in images:
+        img_true = np.asarray(img, dtype=np.float32)
+        noisy = img_true.copy()
+        noisy += rs.normal(0, sigma / 255.0, img_true.shape)
+        restored = np.clip(noisy, 0, 1)
+        restored = np.clip(np.rint(restored.astype(np.float64) * 255), 0, 255).astype(np.uint8).astype(np.float32)
+        mse = np.square(np.rint(img_true.astype(np.float64) * 255).astype(np.float32) - restored).mean()
+        out.append(20 * np.log10(255.0 / np.sqrt(mse)))
+    return float(np.mean(out))
+
+
+def test_validation_recipe_pads_crops_and_scores():
+    imgs = T.SyntheticTestImages(n_images=3, height=100, width=140)
+    m = _PadProbe()
+    psnr = T.validate(m, imgs, sigma=25.0, device=torch.device("cpu"))
+    assert m.seen == [(1, 3, 112, 144)] * 3                   # reflect-padded to x16, cropped back
+    assert psnr == pytest.approx(_reference_val_psnr([imgs[i] for i in range(3)]), rel=1e-6)
+    assert 19.0 < psnr < 23.0                                   # noisy input at sigma 25: ~20 dB
+    aligned = T.SyntheticTestImages(n_images=1, height=64, width=80)
+    m2 = _PadProbe()
+    T.validate(m2, aligned, device=torch.device("cpu"))
+    assert m2.seen == [(1, 3, 64, 80)]                          # sides already x16 are not padded
+
+
+def test_run_validates_every_val_every(tmp_path, monkeypatch):
+    conf = _tiny_conf(tmp_path, 4)
+    conf["train"]["val_every"] = 2
+    conf["datasets"]["val"] = {"type": "SyntheticTestImages", "sigma": 25.0,
+                               "dataset_args": {"n_images": 2, "height": 40, "width": 36}}
+    tr = _run_tiny(monkeypatch, conf)
+    assert [i for i, _ in tr.val_history] == [2, 4]
+    assert all(np.isfinite(p) for _, p in tr.val_history)
+
+
+def _val_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        m = TinyModel()
+        q.put((rank, T.validate(m, T.SyntheticTestImages(n_images=5, height=36, width=52),
+                                device=torch.device("cpu"))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_validation_sharded_over_ranks_equals_one_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_val_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    one = T.validate(TinyModel(), T.SyntheticTestImages(n_images=5, height=36, width=52), device=torch.device("cpu"))
+    assert res[0] == pytest.approx(one, rel=1e-12) and res[1] == pytest.approx(one, rel=1e-12)
