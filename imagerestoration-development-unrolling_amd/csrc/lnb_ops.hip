@@ -496,11 +496,14 @@ __global__ void lnb_w1_pack16_kernel(const float* __restrict__ w1, const float* 
   }
 }
 
-template <int KS>
-__global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
-  constexpr int NB = L6_NB, RA = L6_RA;
+// NW waves per workgroup (8 or 16): each computes GEMM1 for NB = 16 / NW blocks of 32 halo pixels and the
+// gate of PPW = 16 / NW pairs per chunk
+template <int KS, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
+  static_assert(NW == 8 || NW == 16, "lnb_head16_kernel: 8 or 16 waves");
+  constexpr int NB = L6_NB * 8 / NW, RA = L6_RA, PPW = L6_NP / NW;
   constexpr int NI = head16_images(KS);
-  constexpr int DPW = (NI + 7) / 8;      // LDS-DMA instructions per wave per chunk
+  constexpr int DPW = (NI + NW - 1) / NW;  // LDS-DMA instructions per wave per chunk
   constexpr int SLOTF = NI * 256;        // floats per ring slot
   __shared__ __attribute__((aligned(16))) float smem[2 * L6_HBUF + 2 * SLOTF];
   float* const ring = smem + 2 * L6_HBUF;
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
     const char* src = a.w1f + (int64_t)chunk * NI * 1024 + lane * 16;
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
-      const int img = min(i * 8 + wave, NI - 1);   // surplus waves repeat the last image
+      const int img = min(i * NW + wave, NI - 1);   // surplus waves repeat the last image
       dma16_opaque(src + img * 1024, slot + img * 256);
     }
   };
@@ -632,7 +635,7 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
     gemm1_store(c, acc);
   };
 
-  // gate phase mapping: this wave's pairs 2 wave, 2 wave + 1; lane = (output column, row half)
+  // gate phase mapping: this wave's pairs PPW wave ... PPW wave + PPW - 1; lane = (output column, row half)
   const int col = lane & 31, r0 = kh * RA;
   const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
       a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
@@ -646,11 +649,11 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   uint32_t vrow[RA];
 #pragma unroll
   for (int k = 0; k < RA; ++k) vrow[k] = k < nrow ? vcol : kOut;
-  float tp[2][18];                               // taps of the chunk the next gate evaluates
+  float tp[PPW][18];                             // taps of the chunk the next gate evaluates
   auto load_taps = [&](int c) {
-    const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + 2 * wave * 18;
+    const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + PPW * wave * 18;
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < PPW; ++p)
 #pragma unroll
       for (int i = 0; i < 18; ++i) tp[p][i] = t[p * 18 + i];
   };
@@ -659,12 +662,12 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   auto gate = [&](int c) {
     const float* hbuf = smem + (c & 1) * L6_HBUF;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int jj = L6_NP * c + 2 * wave + p;
+    for (int p = 0; p < PPW; ++p) {
+      const int jj = L6_NP * c + PPW * wave + p;
       // wave-uniform: past the hidden channels nothing is stored (soffset is not range-checked)
       const int soff0 = jj < hid ? jj * HW * 4 : 0;
       const bool live = jj < hid;
-      const float* hp = hbuf + (2 * wave + p) * L6_PP + 2 * col;
+      const float* hp = hbuf + (PPW * wave + p) * L6_PP + 2 * col;
       f32x2 win[3][3];                          // rows (i mod 3) x halo columns col .. col + 2
 #pragma unroll
       for (int i = 0; i < RA + 2; ++i) {
@@ -700,9 +703,9 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   asm volatile("" ::: "memory");
 
   // Iteration c: gate of chunk c - 1 (h buffer (c - 1) & 1, taps in registers) and GEMM1 of chunk c
-  // (slot c & 1 -> h buffer c & 1); the SIMD partners (w, w + 4) run them in opposite orders.  Slot
-  // (c + 1) & 1 last served GEMM1(c - 1) and load_taps(c - 1), both before the previous barrier.
-  const bool gate_first = wave < 4;
+  // (slot c & 1 -> h buffer c & 1); the waves of a SIMD (w, w + 4, ...) run them in opposite orders, half
+  // each.  Slot (c + 1) & 1 last served GEMM1(c - 1) and load_taps(c - 1), both before the previous barrier.
+  const bool gate_first = wave < NW / 2;
   for (int c = 1; c <= nch; ++c) {
     issue(min(c + 1, nch - 1), (c + 1) & 1);
     if (gate_first) {
@@ -713,8 +716,8 @@ __global__ __launch_bounds__(512, 1) void lnb_head16_kernel(LnbHeadArgs a) {
       gate(c - 1);
     }
     if (c < nch) load_taps(c);
-    // chunk c + 1 landed (after its DMAs this wave issued the 2 RA gate stores), then every wave's
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(2 * RA) : "memory");
+    // chunk c + 1 landed (after its DMAs this wave issued the PPW RA gate stores), then every wave's
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(PPW * RA) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
@@ -901,9 +904,15 @@ template <int KS, int NB>
 static void launch_head(const LnbHeadArgs& h, hipStream_t s) {
   hipLaunchKernelGGL((lnb_head_kernel<KS, NB>), dim3(h.nblk), dim3(512), 0, s, h);
 }
+// GRR_HEAD16_NW=16: the 16-wave head (A/B measurement, round 4)
+static int head16_waves() {
+  static const int nw = [] { const char* e = getenv("GRR_HEAD16_NW"); return e && atoi(e) == 16 ? 16 : 8; }();
+  return nw;
+}
 template <int KS>
 static void launch_head16(const LnbHeadArgs& h, hipStream_t s) {
-  hipLaunchKernelGGL((lnb_head16_kernel<KS>), dim3(h.nblk), dim3(512), 0, s, h);
+  if (head16_waves() == 16) hipLaunchKernelGGL((lnb_head16_kernel<KS, 16>), dim3(h.nblk), dim3(1024), 0, s, h);
+  else hipLaunchKernelGGL((lnb_head16_kernel<KS, 8>), dim3(h.nblk), dim3(512), 0, s, h);
 }
 template <int MT>
 static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
