@@ -31,15 +31,17 @@ HBM_PEAK_GBPS = 8000.0
 def load_traffic(kind, model, batch, size):
     """Per-launch HBM bytes (PMC, scripts/pmc_train.sh) of the reverse kernel kind at this workload,
     or None when no summary of that exact shape is committed under profiles/."""
-    path = os.path.join(ROOT, "profiles", "r03", f"traffic_{kind}_{model}.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
-    shape = d.get("workload", {})
-    if shape and (shape.get("batch"), shape.get("size")) != (batch, size):
-        return None
-    return d.get("hbm_bytes_per_launch")
+    for rnd in ("r04", "r03"):          # the newest round's summary of this exact workload
+        path = os.path.join(ROOT, "profiles", rnd, f"traffic_{kind}_{model}.json")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            d = json.load(f)
+        shape = d.get("workload", {})
+        if shape and (shape.get("batch"), shape.get("size")) != (batch, size):
+            continue
+        return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def reverse_roofline(kern, model, batch, size):

@@ -45,6 +45,7 @@ SIGNATURES = {
     "grr_last_error": [],
     "grr_set_kernel_variant": [I],
     "grr_lnb_set_phases": [I],
+    "grr_lnb_rep_fused": [I, I, I, I],
     "grr_neighbor_table": [P, I, I, P],
     "grr_stream_copy": [P, P, L, P],
     "grr_edge_weights": [P, L, P, P, P, I, I, I, I, I, P],

@@ -426,6 +426,14 @@ __host__ __device__ constexpr int head16_images(int KS) { return 2 * KS + 2; }  
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+// whole-wave DPP lane shifts (gfx9 wave_shr:1 / wave_shl:1): lane l receives lane l - 1 / l + 1 (0 past the ends)
+__device__ __forceinline__ float dpp_shr1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float dpp_shl1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
+}
+
 // largest |W1 diag(ln_w)| entry of GEMM row `row` (folded over the R replicas) -> its scale exponent
 __device__ __forceinline__ int head16_row_exp(const float* __restrict__ w1, const float* __restrict__ ln_w, int row,
                                               int C, int R) {
@@ -646,19 +654,91 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   constexpr uint32_t kOut = 0x80000000u;
   const int nrow = min(L6_TH, H - y0) - r0;      // output rows of this lane's half inside the tile and image
   const uint32_t vcol = gx < W ? (uint32_t)((y0 + r0) * W + gx) * 4u : kOut;
+#if defined(GRR_GATE_COLPAIR)
+  // lanes = (output column, pair kh of the wave's two): every lane runs all L6_TH rows of its pair; the
+  // pair's plane offset (kh HW) lives in voffset, the wave's first pair and the row in soffset
+  static_assert(PPW == 2, "GRR_GATE_COLPAIR: two pairs per wave");
+  constexpr int GR = L6_TH;                      // output rows per lane
+  const int nrow_c = min(L6_TH, H - y0);
+  const uint32_t vcolc = gx < W ? (uint32_t)(kh * HW + y0 * W + gx) * 4u : kOut;
+  uint32_t vrow[GR];
+#pragma unroll
+  for (int k = 0; k < GR; ++k) vrow[k] = k < nrow_c ? vcolc : kOut;
+#else
+  constexpr int GR = RA;
   uint32_t vrow[RA];
 #pragma unroll
   for (int k = 0; k < RA; ++k) vrow[k] = k < nrow ? vcol : kOut;
+#endif
   float tp[PPW][18];                             // taps of the chunk the next gate evaluates
+#ifdef GRR_DIAG_NOSTORE
+  float diag_sink = 0.f;
+  constexpr int kGateStores = 0;
+#elif defined(GRR_GATE_COLPAIR)
+  constexpr int kGateStores = GR;
+#else
+  constexpr int kGateStores = PPW * RA;
+#endif
   auto load_taps = [&](int c) {
     const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + PPW * wave * 18;
+#if defined(GRR_GATE_COLPAIR)
+#pragma unroll
+    for (int i = 0; i < 18; ++i) tp[0][i] = t[kh * 18 + i];
+#else
 #pragma unroll
     for (int p = 0; p < PPW; ++p)
 #pragma unroll
       for (int i = 0; i < 18; ++i) tp[p][i] = t[p * 18 + i];
+#endif
   };
   // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c, h buffer c & 1.  The taps carry
   // the exp2 fold of lnb_w1_pack16_kernel: m' = -log2(e) m, v' = -ln(2) v, g = m' v' / (1 + 2^m').
+#if defined(GRR_GATE_COLPAIR)
+  auto gate = [&](int c) {
+    const float* hbuf = smem + (c & 1) * L6_HBUF;
+    const int jj0 = L6_NP * c + PPW * wave;        // the wave's first pair (lane half kh: pair jj0 + kh)
+    const bool all_live = jj0 + 1 < hid;           // wave-uniform
+    const bool live = jj0 + kh < hid;
+    const int soff0 = all_live || jj0 < hid ? jj0 * HW * 4 : 0;
+    const float* hp = hbuf + (PPW * wave + kh) * L6_PP + 2 * col;
+#if defined(GRR_GATE_DPP)
+    const float* hq = hbuf + (PPW * wave + kh) * L6_PP;
+    const int ecol = col == 0 ? 0 : LH_HWD - 1;
+#endif
+    const float (&tk)[18] = tp[0];
+    f32x2 win[3][3];
+#pragma unroll
+    for (int i = 0; i < GR + 2; ++i) {
+      const int hrow = i * LH_HWD;
+#if defined(GRR_GATE_DPP)
+      {
+        const f32x2 cc = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + 1));
+        const f32x2 ee = *reinterpret_cast<const f32x2*>(hq + 2 * (hrow + ecol));
+        const f32x2 lf{dpp_shr1(cc[0]), dpp_shr1(cc[1])}, rt{dpp_shl1(cc[0]), dpp_shl1(cc[1])};
+        win[i % 3][0] = col == 0 ? ee : lf;
+        win[i % 3][1] = cc;
+        win[i % 3][2] = col == 31 ? ee : rt;
+      }
+#else
+#pragma unroll
+      for (int d = 0; d < 3; ++d) win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
+#endif
+      if (i >= 2) {
+        const f32x2 h0 = win[(i - 2) % 3][0];
+        float m = tk[0] * h0[0], v = tk[1] * h0[1];
+#pragma unroll
+        for (int t = 1; t < 9; ++t) {
+          const f32x2 hv = win[(i - 2 + t / 3) % 3][t % 3];
+          m = __builtin_fmaf(tk[2 * t], hv[0], m);
+          v = __builtin_fmaf(tk[2 * t + 1], hv[1], v);
+        }
+        const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+        const uint32_t vo = all_live ? vrow[i - 2] : (live ? vrow[i - 2] : kOut);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, vo, soff0 + (i - 2) * W * 4, 0);
+      }
+    }
+  };
+#else
   auto gate = [&](int c) {
     const float* hbuf = smem + (c & 1) * L6_HBUF;
 #pragma unroll
@@ -668,12 +748,34 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
       const int soff0 = jj < hid ? jj * HW * 4 : 0;
       const bool live = jj < hid;
       const float* hp = hbuf + (PPW * wave + p) * L6_PP + 2 * col;
+#if defined(GRR_GATE_DPP)
+      const float* hq = hbuf + (PPW * wave + p) * L6_PP;
+      const int ecol = col == 0 ? 0 : LH_HWD - 1;
+#endif
       f32x2 win[3][3];                          // rows (i mod 3) x halo columns col .. col + 2
 #pragma unroll
       for (int i = 0; i < RA + 2; ++i) {
         const int hrow = min(r0 + i, L6_HR - 1) * LH_HWD;
+#if defined(GRR_GATE_DPP)
+        {  // one LDS read per lane (its centre column); the side columns from the neighbour lanes (DPP),
+           // the tile-edge lanes' outer column from a second, broadcast read (col 0 or 33 of the halo row)
+          const f32x2 cc = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + 1));
+          const f32x2 ee = *reinterpret_cast<const f32x2*>(hq + 2 * (hrow + ecol));
+          const f32x2 lf{dpp_shr1(cc[0]), dpp_shr1(cc[1])}, rt{dpp_shl1(cc[0]), dpp_shl1(cc[1])};
+          win[i % 3][0] = col == 0 ? ee : lf;
+          win[i % 3][1] = cc;
+          win[i % 3][2] = col == 31 ? ee : rt;
+        }
+#else
 #pragma unroll
-        for (int d = 0; d < 3; ++d) win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
+        for (int d = 0; d < 3; ++d) {
+#ifdef GRR_DIAG_NOLDS   // timing-only diagnostic builds (wrong results): the window without LDS reads
+          win[i % 3][d] = f32x2{tp[p][d + 2 * (i % 3)], tp[p][d + 1]};
+#else
+          win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
+#endif
+        }
+#endif
         if (i >= 2) {
           const f32x2 h0 = win[(i - 2) % 3][0];
           float m = tp[p][0] * h0[0], v = tp[p][1] * h0[1];
@@ -683,13 +785,22 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
             m = __builtin_fmaf(tp[p][2 * t], hv[0], m);
             v = __builtin_fmaf(tp[p][2 * t + 1], hv[1], v);
           }
+#ifdef GRR_DIAG_NOEXP
+          const float gv = m * v;
+#else
           const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+#endif
+#ifdef GRR_DIAG_NOSTORE
+          diag_sink += gv;
+#else
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, live ? vrow[i - 2] : kOut,
                                                 soff0 + (i - 2) * W * 4, 0);
+#endif
         }
       }
     }
   };
+#endif
 
   // prologue: chunk 0's fragments landed -> GEMM1(0), its taps, chunk 1 into slot 1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -717,10 +828,269 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
     }
     if (c < nch) load_taps(c);
     // chunk c + 1 landed (after its DMAs this wave issued the PPW RA gate stores), then every wave's
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(PPW * RA) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(kGateStores) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
+#ifdef GRR_DIAG_NOSTORE
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(diag_sink), grs, vrow[0], 0, 0);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// rep: the image filter's first block -- input = the C_s-channel image replicated over the graphs
+// (REF13:918-921), C_s * 9 <= 32 -- in one pass, LN through the skip, without g in HBM or h in LDS.
+//
+// The depthwise 3x3 is linear in h = W1' n, so it folds into GEMM1 as an im2col GEMM:
+//   d[j, p] = sum_t tap[j, t] h[j, p + delta_t] = sum_{c, t} (tap[j, t] W1'[j, c]) n[c, p + delta_t]
+// (W1' = W1 diag(ln_w) folded over the replicas, n = x / sigma, the replicate padding = clamped
+// neighbour coordinates), K = 9 C_s <= 32: two 16-deep k-steps of v_mfma_f32_32x32x16_f16 on exact
+// two-term fp16 splits (three products, head16's arithmetic and scaling: rows of the folded matrix by
+// 2^s_row, each pixel's im2col column by 2^XE, corrected per column when its largest entry leaves the
+// range).  The 32 x 32 accumulator of a chunk (16 (mask, value) pairs x 32 pixels) holds both halves
+// of every pair in one lane, so the gate runs on it in registers, and the lane's eight gated values
+// are already the B operand of GEMM2 (W2 g, 32x32x16 bf16, exact three-term split, six products) once
+// W2's k order is permuted to the accumulator's pair order (lnb_rep_pack_kernel).  A workgroup = 8
+// waves x 32 pixels; the chunk's fragments (both GEMMs) and its per-row constants arrive by LDS-DMA in
+// a 3-slot ring two chunks ahead.  Against head16 + mix for this block: no g round trip (4 KB per
+// pixel of HBM traffic), no h planes in LDS, no depthwise FMAs.
+constexpr int LR_NW = 8;                  // waves per workgroup
+constexpr int LR_PX = LR_NW * 32;         // pixels per workgroup (one 32-pixel block per wave)
+constexpr int LR_XE = 10;                 // common power-of-two scale of the im2col operand
+__host__ __device__ constexpr int rep_images(int MT) { return 4 + 3 * MT + 1; }   // A1 (2 k-steps x hi/lo), A2 (MT x 3), row constants
+
+struct LnbRepArgs {
+  const float* xs;      // [B, Cs, P]: the image the block input replicates
+  const char* pack;     // [nch][rep_images(MT)] 1-KB images
+  const float* skip;    // [2]
+  float* out;           // [B, C, P]
+  float var_den;        // (C - 1) / R: the unbiased variance over the C replicated channels from the Cs sources
+  int Cs, C, hid, H, W, nch, tiles;
+  uint32_t nblk;
+};
+
+// largest |tap[row, t] W1'[row, c]| over the folded row (C_s channels x 9 taps) -> its scale exponent
+__device__ __forceinline__ int rep_row_exp(const float* __restrict__ w1, const float* __restrict__ ln_w,
+                                           const float* __restrict__ wdw, int row, int Cs, int R) {
+  float mx = 0.f;
+  for (int c = 0; c < Cs; ++c) {
+    float w = 0.f;
+    for (int rep = 0; rep < R; ++rep) w += w1[(int64_t)row * (R * Cs) + rep * Cs + c] * ln_w[rep * Cs + c];
+    for (int t = 0; t < 9; ++t) mx = fmaxf(mx, fabsf(wdw[(int64_t)row * 9 + t] * w));
+  }
+  if (mx == 0.f) return 0;
+  int e;
+  frexpf(mx, &e);
+  return clampi(14 - e, -60, 60);
+}
+
+// Per chunk c (16 pairs): images 0..3 = A1 (k-step s = im >> 1, term hi / lo = im & 1; lane l, element j:
+// GEMM row r = l & 31 -- pair 16 c + (r >> 1), mask (r even) or value -- and k = 16 s + 8 (l >> 5) + j =
+// 9 c_s + t); images 4 + 3 mt + q = A2 (W2 rows 32 mt + (l & 31), term q; k = 8 (l >> 5) + j is pair
+// pi = 4 (j >> 1) + (j & 1) + 2 (l >> 5) of the chunk: the accumulator's pair order); the last image =
+// the gate's row constants, word 16 kh + i for accumulator register i of lane half kh (row
+// (i & 3) + 8 (i >> 2) + 4 kh): -log2(e) 2^-(s_row + XE) (mask rows), -ln(2) 2^-(s_row + XE) (value rows).
+__global__ void lnb_rep_pack_kernel(const float* __restrict__ w1, const float* __restrict__ ln_w,
+                                    const float* __restrict__ wdw, const float* __restrict__ w2,
+                                    char* __restrict__ out, int Cs, int R, int C, int hid, int MT, int nch) {
+  const int NI = rep_images(MT);
+  const int64_t n = (int64_t)nch * NI * 256;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i >> 8;
+    const int e = (int)(i & 255), c = (int)(img / NI), im = (int)(img % NI);
+    const int l = e >> 2;
+    uint32_t word = 0;
+    if (im < 4) {
+      const int s = im >> 1, q = im & 1, r = l & 31, pj = 16 * c + (r >> 1);
+      if (pj < hid) {
+        const int row = (r & 1 ? hid : 0) + pj;
+        const int sc = rep_row_exp(w1, ln_w, wdw, row, Cs, R);
+        uint16_t hb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int k = 16 * s + 8 * (l >> 5) + 2 * (e & 3) + u;
+          float v = 0.f;
+          if (k < 9 * Cs) {
+            const int cs = k / 9, t = k % 9;
+            float w = 0.f;
+            for (int rep = 0; rep < R; ++rep) w += w1[(int64_t)row * (R * Cs) + rep * Cs + cs] * ln_w[rep * Cs + cs];
+            v = wdw[(int64_t)row * 9 + t] * w;
+          }
+          const float vs = ldexpf(v, sc);
+          const _Float16 h0 = (_Float16)vs;
+          const _Float16 t16 = q == 0 ? h0 : (_Float16)(vs - (float)h0);
+          hb[u] = __builtin_bit_cast(uint16_t, t16);
+        }
+        word = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16);
+      }
+    } else if (im < 4 + 3 * MT) {
+      const int mt = (im - 4) / 3, q = (im - 4) % 3, m = 32 * mt + (l & 31);
+      uint16_t hb[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j = 2 * (e & 3) + u;
+        const int pj = 16 * c + 4 * (j >> 1) + (j & 1) + 2 * (l >> 5);
+        hb[u] = (m < C && pj < hid) ? split_term(w2[(int64_t)m * hid + pj], q) : (uint16_t)0;
+      }
+      word = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16);
+    } else if (e < 32) {
+      const int kh = e >> 4, ii = e & 15, r = (ii & 3) + 8 * (ii >> 2) + 4 * kh, pj = 16 * c + (r >> 1);
+      if (pj < hid) {
+        const int row = (r & 1 ? hid : 0) + pj;
+        const float fold = r & 1 ? -0.69314718055994531f : -1.44269504088896341f;
+        word = __float_as_uint(ldexpf(fold, -(rep_row_exp(w1, ln_w, wdw, row, Cs, R) + LR_XE)));
+      }
+    }
+    reinterpret_cast<uint32_t*>(out)[i] = word;
+  }
+}
+
+template <int MT>
+__global__ __launch_bounds__(64 * LR_NW, 1) void lnb_rep_kernel(LnbRepArgs a) {
+  constexpr int NI = rep_images(MT), SLOTF = NI * 256, NSLOT = 3;
+  constexpr int DPW = (NI + LR_NW - 1) / LR_NW;   // LDS-DMA instructions per wave per chunk
+  __shared__ __attribute__((aligned(16))) float smem[NSLOT * SLOTF];
+  const int lane = threadIdx.x & 63, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
+  const int b = (int)(lb / (uint32_t)a.tiles), tile = (int)(lb % (uint32_t)a.tiles);
+  const int H = a.H, W = a.W, Cs = a.Cs, C = a.C, nch = a.nch;
+  const int P = H * W;
+  const int p = tile * LR_PX + wave * 32 + (lane & 31);   // this lane's pixel (column of every MFMA block)
+
+  // im2col column of pixel p: n = x / sigma at the 9 replicate-clamped neighbours, k = 9 c + t; this lane
+  // half holds k = 16 s + 8 kh + j
+  const int pc = min(p, P - 1), py = pc / W, px = pc - py * W;
+  const float* xb = a.xs + (int64_t)b * Cs * P;
+  float nb[9][3];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = clampi(py + t / 3 - 1, 0, H - 1), xx = clampi(px + t % 3 - 1, 0, W - 1);
+    float v[3], sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      v[c] = c < Cs ? xb[(int64_t)c * P + yy * W + xx] : 0.f;
+      sum += v[c];
+    }
+    const float mean = sum / (float)Cs;
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float d = c < Cs ? v[c] - mean : 0.f;
+      sq += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) nb[t][c] = v[c] * rstd;   // x / sigma (REF:921)
+  }
+  float nv[2][8];
+  float mx = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s2 + 8 * kh + j;
+      float v = 0.f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          if (k == 9 * c + t && c < Cs) v = nb[t][c];
+      nv[s2][j] = v;
+      mx = fmaxf(mx, fabsf(v));
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  int ep = LR_XE;
+  if (mx != 0.f) {
+    int e;
+    frexpf(mx, &e);
+    if (e > 14 - LR_XE || e < -LR_XE) ep = clampi(14 - e, -100, 100);
+  }
+  const float corr = ldexpf(1.0f, LR_XE - ep);
+  const bool wave_corr = __builtin_amdgcn_readfirstlane((int)__any(ep != LR_XE)) != 0;
+  f16x8 xh[2], xl[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = ldexpf(nv[s2][j], ep);
+      const _Float16 h0 = (_Float16)v;
+      xh[s2][j] = h0;
+      xl[s2][j] = (_Float16)(v - (float)h0);
+    }
+
+  auto issue = [&](int c) {
+    float* slot = smem + (c % NSLOT) * SLOTF;
+    const char* src = a.pack + (int64_t)min(c, nch - 1) * NI * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int img = min(i * LR_NW + wave, NI - 1);   // surplus waves repeat the last image
+      dma16_opaque(src + img * 1024, slot + img * 256);
+    }
+  };
+  issue(0);
+  issue(1);
+
+  f32x16 acc2[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc2[t] = f32x16{};
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed (this wave's DMAs; after them only chunk c + 1's), then every wave's
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(c + 2);                                   // slot (c + 2) % 3 was last read in iteration c - 1
+    const float* slot = smem + (c % NSLOT) * SLOTF + lane * 4;
+    // GEMM1 (im2col: LN, W1, depthwise in one accumulation)
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(slot + (2 * s2 + 0) * 256);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(slot + (2 * s2 + 1) * 256);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[s2], acc, 0, 0, 0);
+    }
+    if (wave_corr) acc *= corr;
+    // gate sigmoid(m) m v (REF:947) on the accumulator: registers 2q, 2q + 1 = mask, value of chunk pair
+    // 4 (q >> 1) + (q & 1) + 2 kh; the row constants undo the scales and carry the exp2 fold
+    const float* cst = smem + (c % NSLOT) * SLOTF + (4 + 3 * MT) * 256 + kh * 16;
+    float gq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float m = acc[2 * q] * cst[2 * q], v = acc[2 * q + 1] * cst[2 * q + 1];
+      gq[q] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+    }
+    bf16x8 b0, b1, b2;
+    split3x8(gq, b0, b1, b2);
+    // GEMM2: W2 (k permuted to the accumulator's pair order) g
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + (4 + 3 * t + 0) * 256);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + (4 + 3 * t + 1) * 256);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(slot + (4 + 3 * t + 2) * 256);
+      GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_32x32x16_bf16, acc2[t], a0, a1, a2, b0, b1, b2);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue (REF:962-964): out[m, p] = skip0 x[m mod Cs, p] + skip1 (W2 g)[m, p]
+  const float s0 = a.skip[0], s1 = a.skip[1];
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * C * P, 0,
+                                                                        (int)((int64_t)C * P * 4), 0x00020000);
+  float xo[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) xo[c] = c < Cs ? xb[(int64_t)c * P + pc] : 0.f;
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * kh;
+      const int cm = m % Cs;                       // source channel of replica row m (no dynamic indexing)
+      const float xv = cm == 0 ? xo[0] : (cm == 1 ? xo[1] : xo[2]);
+      const uint32_t off = (m < C && p < P) ? (uint32_t)(m * P + p) * 4u : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv + s1 * acc2[t][i]), ors, off, 0, 0);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -897,7 +1267,9 @@ static int64_t mix_pack_floats(int C, int hid) {
 
 // workspace (floats): [g: B*hid*P][W1 images][W2 images], each 256-B aligned
 int64_t lnb_mfma_workspace_floats(int B, int C, int hid, int H, int W) {
-  return align64((int64_t)B * hid * H * W) + head_pack_floats(C, hid) + mix_pack_floats(C, hid);
+  const int64_t two_kernel = align64((int64_t)B * hid * H * W) + head_pack_floats(C, hid) + mix_pack_floats(C, hid);
+  const int64_t rep = align64((int64_t)((hid + 15) / 16) * rep_images((C + 31) / 32) * 256);   // lnb_rep_kernel's chunk images
+  return std::max(two_kernel, rep);
 }
 
 template <int KS, int NB>
@@ -911,8 +1283,11 @@ static int head16_waves() {
 }
 template <int KS>
 static void launch_head16(const LnbHeadArgs& h, hipStream_t s) {
+#if !defined(GRR_GATE_COLPAIR)
   if (head16_waves() == 16) hipLaunchKernelGGL((lnb_head16_kernel<KS, 16>), dim3(h.nblk), dim3(1024), 0, s, h);
-  else hipLaunchKernelGGL((lnb_head16_kernel<KS, 8>), dim3(h.nblk), dim3(512), 0, s, h);
+  else
+#endif
+    hipLaunchKernelGGL((lnb_head16_kernel<KS, 8>), dim3(h.nblk), dim3(512), 0, s, h);
 }
 template <int MT>
 static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
@@ -930,6 +1305,18 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
   return lnb_forward_mfma_rep(x, C, 1, x, ln_w, w1, wdw, w2, skip, out, ws, B, hid, H, W, s);
 }
 
+// the replicated first block runs as one fused pass (lnb_rep_kernel) when its im2col depth 9 Cs fits two
+// k-steps; GRR_LNB_REP=0: head16 + mix (A/B measurement, round 4)
+bool lnb_rep_fused(int Ch, int R, int C, int hid) {
+  static const bool off = [] { const char* e = getenv("GRR_LNB_REP"); return e && e[0] == '0'; }();
+  return !off && R > 1 && Ch >= 1 && Ch <= 3 && C <= 128 && hid >= 1;
+}
+
+template <int MT>
+static void launch_rep(const LnbRepArgs& r, hipStream_t s) {
+  hipLaunchKernelGGL((lnb_rep_kernel<MT>), dim3(r.nblk), dim3(64 * LR_NW), 0, s, r);
+}
+
 grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
                                 const float* wdw, const float* w2, const float* skip, float* out, float* ws, int B,
                                 int hid, int H, int W, hipStream_t s) {
@@ -937,6 +1324,34 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   GRR_REQUIRE(C >= 2 && C <= 128 && Ch >= 1, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d outside [2, 128]", C);
   GRR_REQUIRE((int64_t)std::max(hid, C) * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_lnb_forward: max(hid, C)*H*W too large for one image's 32-bit offsets");
+  if (lnb_rep_fused(Ch, R, C, hid)) {
+    // workspace: the chunk images at its start (the g region the two-kernel path would use is not needed)
+    const int MT = (C + 31) / 32, nch = (hid + 15) / 16;
+    char* pack = reinterpret_cast<char*>(ws);
+    if (g_lnb_phases & 1) {
+      const int64_t n = (int64_t)nch * rep_images(MT) * 256;
+      hipLaunchKernelGGL(lnb_rep_pack_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                         s, w1, ln_w, wdw, w2, pack, Ch, R, C, hid, MT, nch);
+      grr_status st = launch_status("grr_lnb_forward/rep_pack");
+      if (st != GRR_OK) return st;
+    }
+    if (!(g_lnb_phases & 2)) return GRR_OK;
+    LnbRepArgs r{};
+    r.xs = xh; r.pack = pack; r.skip = skip; r.out = out;
+    r.var_den = (float)(C - 1) / (float)R;
+    r.Cs = Ch; r.C = C; r.hid = hid; r.H = H; r.W = W; r.nch = nch;
+    r.tiles = (int)(((int64_t)H * W + LR_PX - 1) / LR_PX);
+    const uint64_t nb = (uint64_t)B * r.tiles;
+    GRR_REQUIRE(nb < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+    r.nblk = (uint32_t)nb;
+    switch (MT) {
+      case 1: launch_rep<1>(r, s); break;
+      case 2: launch_rep<2>(r, s); break;
+      case 3: launch_rep<3>(r, s); break;
+      default: launch_rep<4>(r, s); break;
+    }
+    return launch_status("grr_lnb_forward/rep");
+  }
   const bool h16 = head16_enabled(Ch);
   const int KS = h16 ? head16_ks(Ch) : head_ks(Ch), NB = head_nb(head_ks(Ch));
   const int nch = h16 ? (hid + L6_NP - 1) / L6_NP : (hid + LH_JC - 1) / LH_JC;
@@ -1007,6 +1422,8 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
 }
 
 }  // namespace grr
+
+extern "C" int grr_lnb_rep_fused(int Cs, int R, int C, int hid) { return grr::lnb_rep_fused(Cs, R, C, hid) ? 1 : 0; }
 
 extern "C" grr_status grr_lnb_set_phases(int mask) {
   grr::clear_error();

@@ -643,6 +643,11 @@ def lnb_forward_rep(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, 
     out = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
     args = (src.data_ptr(), cs, c // cs, _ptr(x), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(),
             skip.data_ptr(), out.data_ptr(), ws.data_ptr(), b, hid, h, w, _stream(dev))
+    if _native.load().grr_lnb_rep_fused(cs, c // cs, c, hid):
+        # one fused pass (lnb_rep_kernel): src with its 3x3 halo in, out written; no gated tensor in memory
+        _launch("lnb_rep_fused", 4 * b * h * w * (cs + 2 * c if x is not None else cs + c), "grr_lnb_forward_rep",
+                *args, flops=lnb_flops(b * h * w, cs, c, hid))
+        return out
     if _lnb_split(c):
         _lnb_timed_parts("grr_lnb_forward_rep", args, b * h * w, cs, c, hid, c if x is not None else cs)
         return out

@@ -294,6 +294,10 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
 grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, const float* ln_w, const float* w1,
                                const float* wdw, const float* w2, const float* skip, float* out, void* workspace,
                                int B, int hid, int H, int W, void* stream);
+/* 1 when grr_lnb_forward_rep runs the block as one fused pass for these sizes (R > 1, Cs <= 3: the
+ * depthwise folded into an im2col GEMM1, gate and W2 in registers, no gated tensor in memory), else 0.
+ * Phase mask 2 of grr_lnb_set_phases then launches the whole block and mask 4 nothing. */
+int grr_lnb_rep_fused(int Cs, int R, int C, int hid);
 
 /* Channel replication of MultiScaleGraphFilter.forward (REF13:918-921):
  * img [B,Cin,H,W] -> out [B,G*Cin,H,W], out[b, g*Cin + c] = img[b, c]. */

@@ -284,6 +284,39 @@ def test_replicated_input_folding(irdu):
     assert_close(unmaterialised, plain, 1e-5)
 
 
+# The replicated first block (input = Cs channels copied R times) as one fused pass (lnb_rep_kernel:
+# im2col GEMM1 with the depthwise folded in, gate + W2 in registers): against float64, with fp32-class
+# error, for Cs = 1 / 2 / 3, a partial chunk (hid = 20), a tail workgroup (H * W not a multiple of 256),
+# gray pixels (equal channels: sigma = sqrt(1e-5), the large-|x / sigma| exponent correction), and the
+# skip from src (x = None) or from the materialised replicas.
+@pytest.mark.parametrize("cs_r_hid_hw", [(3, 32, 256, (40, 36)), (3, 8, 20, (9, 13)), (1, 16, 48, (17, 30)),
+                                         (2, 12, 64, (8, 8))])
+@pytest.mark.parametrize("gray", [False, True])
+def test_replicated_lnb_fused(irdu, cs_r_hid_hw, gray):
+    cs, r, hid, (h, w) = cs_r_hid_hw
+    c = cs * r
+    assert irdu._native.load().grr_lnb_rep_fused(cs, r, c, hid) == 1
+    torch.manual_seed(9)
+    blk = irdu.LocalNonLinearBlock(c, hid, 1)
+    with torch.no_grad():
+        blk.skip_weight.copy_(torch.tensor([0.8, 1.2]))
+        blk.norm.weighted_transform.weight.mul_(1.0 + 0.2 * torch.randn_like(blk.norm.weighted_transform.weight))
+        blk.local_linear.channels_local_linear_op.weight.mul_(3.0)
+    src = rand(2, cs, h, w, seed=19)
+    if gray:
+        src[:, :, : h // 2] = src[:, :1, : h // 2]          # upper half: equal channels
+    x = src.repeat(1, r, 1, 1)
+    p64 = {k: v.double() for k, v in sd_cpu(blk).items()}
+    ref64 = O.local_nonlinear_block(x.double(), p64, "")
+    err32 = rel_err(O.local_nonlinear_block(x, sd_cpu(blk), ""), ref64)
+    blk = blk.to(DEV)
+    with torch.no_grad():
+        for xin in (None, x.to(DEV)):
+            got = blk.forward_replicated(src.to(DEV), xin)
+            err = rel_err(got, ref64)
+            assert err <= 4 * err32 + 1e-6, (err, err32)
+
+
 # (C, hid, H, W): C <= 128 runs the split-bf16 head (32 x 13 / 32 x 9 output tiles with halo
 # recompute) + mix kernels: full / partial tiles, H*W % 4 == 0 (16-byte g DMA) and not (dword
 # DMA), hid % 8 != 0 and hid % 16 != 0 (partial chunk / k-step), C = 33 (partial k-step and
