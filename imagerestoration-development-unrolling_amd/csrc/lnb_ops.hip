@@ -417,7 +417,6 @@ constexpr int L6_NB = 2;                    // 32-pixel GEMM1 blocks per wave
 constexpr int L6_NH = 8 * L6_NB * 32;       // halo pixels of a tile (512; 510 used)
 constexpr int L6_HR = L6_NH / LH_HWD;       // halo rows (15)
 constexpr int L6_TH = L6_HR - 2;            // output rows (13)
-constexpr int L6_RA = (L6_TH + 1) / 2;      // output rows per lane half in the gate (7)
 constexpr int L6_PP = 2 * L6_NH;            // floats per pair plane
 constexpr int L6_HBUF = L6_NP * L6_PP;      // floats per h buffer (64 KB)
 constexpr int L6_XE = 10;                   // common power-of-two scale of the fp16 x operand
@@ -425,14 +424,6 @@ constexpr int L6_TAPF = L6_NP * 18;         // tap floats per chunk
 __host__ __device__ constexpr int head16_images(int KS) { return 2 * KS + 2; }   // fp16 hi/lo per k-step + 2 tap images
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
-// whole-wave DPP lane shifts (gfx9 wave_shr:1 / wave_shl:1): lane l receives lane l - 1 / l + 1 (0 past the ends)
-__device__ __forceinline__ float dpp_shr1(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float dpp_shl1(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
-}
 
 // largest |W1 diag(ln_w)| entry of GEMM row `row` (folded over the R replicas) -> its scale exponent
 __device__ __forceinline__ int head16_row_exp(const float* __restrict__ w1, const float* __restrict__ ln_w, int row,
@@ -504,12 +495,12 @@ __global__ void lnb_w1_pack16_kernel(const float* __restrict__ w1, const float* 
   }
 }
 
-// NW waves per workgroup (8 or 16): each computes GEMM1 for NB = 16 / NW blocks of 32 halo pixels and the
-// gate of PPW = 16 / NW pairs per chunk
+// NW = 8 waves per workgroup: each computes GEMM1 for NB = 2 blocks of 32 halo pixels and the gate of
+// PPW = 2 pairs per chunk (a 16-wave workgroup, one block and one pair per wave, measured within 2 %)
 template <int KS, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
-  static_assert(NW == 8 || NW == 16, "lnb_head16_kernel: 8 or 16 waves");
-  constexpr int NB = L6_NB * 8 / NW, RA = L6_RA, PPW = L6_NP / NW;
+  static_assert(NW == 8, "lnb_head16_kernel: 8 waves");
+  constexpr int NB = L6_NB * 8 / NW, PPW = L6_NP / NW;
   constexpr int NI = head16_images(KS);
   constexpr int DPW = (NI + NW - 1) / NW;  // LDS-DMA instructions per wave per chunk
   constexpr int SLOTF = NI * 256;        // floats per ring slot
@@ -643,86 +634,47 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
     gemm1_store(c, acc);
   };
 
-  // gate phase mapping: this wave's pairs PPW wave ... PPW wave + PPW - 1; lane = (output column, row half)
-  const int col = lane & 31, r0 = kh * RA;
+  // gate phase mapping: lane = (output column, pair kh of the wave's two); every lane runs all L6_TH output
+  // rows of its pair (15 halo rows read for 13 outputs, against 18 for 14 with a lane per half column:
+  // 1.7 % faster at C = 96, 5.6 % on the replicated block, round 4)
+  const int col = lane & 31;
   const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
       a.g + (int64_t)b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
   const int gx = x0 + col;
-  // g stores: the lane's byte offset of output row k of its half (row y0 + r0 + k, its column) in voffset
-  // -- out of range for rows past the tile or the image and for columns past the image, fixed for the
-  // whole kernel (vrow) -- and the channel plane and row, wave-uniform, in soffset
+  // g stores: the lane's byte offset of output row k (row y0 + k, its column, its pair's plane kh HW) in
+  // voffset -- out of range for rows past the tile or the image and for columns past the image, fixed for
+  // the whole kernel (vrow) -- and the wave's first pair plane and the row, wave-uniform, in soffset
+  static_assert(PPW == 2, "lnb_head16_kernel: the gate maps the wave's two pairs to its lane halves");
   constexpr uint32_t kOut = 0x80000000u;
-  const int nrow = min(L6_TH, H - y0) - r0;      // output rows of this lane's half inside the tile and image
-  const uint32_t vcol = gx < W ? (uint32_t)((y0 + r0) * W + gx) * 4u : kOut;
-#if defined(GRR_GATE_COLPAIR)
-  // lanes = (output column, pair kh of the wave's two): every lane runs all L6_TH rows of its pair; the
-  // pair's plane offset (kh HW) lives in voffset, the wave's first pair and the row in soffset
-  static_assert(PPW == 2, "GRR_GATE_COLPAIR: two pairs per wave");
   constexpr int GR = L6_TH;                      // output rows per lane
-  const int nrow_c = min(L6_TH, H - y0);
-  const uint32_t vcolc = gx < W ? (uint32_t)(kh * HW + y0 * W + gx) * 4u : kOut;
+  const int nrow = min(L6_TH, H - y0);           // output rows inside the tile and image
+  const uint32_t vcol = gx < W ? (uint32_t)(kh * HW + y0 * W + gx) * 4u : kOut;
   uint32_t vrow[GR];
 #pragma unroll
-  for (int k = 0; k < GR; ++k) vrow[k] = k < nrow_c ? vcolc : kOut;
-#else
-  constexpr int GR = RA;
-  uint32_t vrow[RA];
-#pragma unroll
-  for (int k = 0; k < RA; ++k) vrow[k] = k < nrow ? vcol : kOut;
-#endif
-  float tp[PPW][18];                             // taps of the chunk the next gate evaluates
-#ifdef GRR_DIAG_NOSTORE
-  float diag_sink = 0.f;
-  constexpr int kGateStores = 0;
-#elif defined(GRR_GATE_COLPAIR)
-  constexpr int kGateStores = GR;
-#else
-  constexpr int kGateStores = PPW * RA;
-#endif
+  for (int k = 0; k < GR; ++k) vrow[k] = k < nrow ? vcol : kOut;
+  constexpr int kGateStores = GR;                // g stores per wave and iteration
+  float tk[18];                                  // taps of the lane's pair in the chunk the next gate evaluates
   auto load_taps = [&](int c) {
-    const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + PPW * wave * 18;
-#if defined(GRR_GATE_COLPAIR)
+    const float* t = ring + (c & 1) * SLOTF + 2 * KS * 256 + (PPW * wave + kh) * 18;
 #pragma unroll
-    for (int i = 0; i < 18; ++i) tp[0][i] = t[kh * 18 + i];
-#else
-#pragma unroll
-    for (int p = 0; p < PPW; ++p)
-#pragma unroll
-      for (int i = 0; i < 18; ++i) tp[p][i] = t[p * 18 + i];
-#endif
+    for (int i = 0; i < 18; ++i) tk[i] = t[i];
   };
   // depthwise 3x3 (REF:946) + gate sigmoid(m) m v (REF:947) of chunk c, h buffer c & 1.  The taps carry
   // the exp2 fold of lnb_w1_pack16_kernel: m' = -log2(e) m, v' = -ln(2) v, g = m' v' / (1 + 2^m').
-#if defined(GRR_GATE_COLPAIR)
   auto gate = [&](int c) {
     const float* hbuf = smem + (c & 1) * L6_HBUF;
     const int jj0 = L6_NP * c + PPW * wave;        // the wave's first pair (lane half kh: pair jj0 + kh)
     const bool all_live = jj0 + 1 < hid;           // wave-uniform
     const bool live = jj0 + kh < hid;
-    const int soff0 = all_live || jj0 < hid ? jj0 * HW * 4 : 0;
+    // soffset is not range-checked: a pair past the hidden channels stores out of range through voffset
+    const int soff0 = jj0 < hid ? jj0 * HW * 4 : 0;
     const float* hp = hbuf + (PPW * wave + kh) * L6_PP + 2 * col;
-#if defined(GRR_GATE_DPP)
-    const float* hq = hbuf + (PPW * wave + kh) * L6_PP;
-    const int ecol = col == 0 ? 0 : LH_HWD - 1;
-#endif
-    const float (&tk)[18] = tp[0];
-    f32x2 win[3][3];
+    f32x2 win[3][3];                               // rows (i mod 3) x halo columns col .. col + 2
 #pragma unroll
     for (int i = 0; i < GR + 2; ++i) {
       const int hrow = i * LH_HWD;
-#if defined(GRR_GATE_DPP)
-      {
-        const f32x2 cc = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + 1));
-        const f32x2 ee = *reinterpret_cast<const f32x2*>(hq + 2 * (hrow + ecol));
-        const f32x2 lf{dpp_shr1(cc[0]), dpp_shr1(cc[1])}, rt{dpp_shl1(cc[0]), dpp_shl1(cc[1])};
-        win[i % 3][0] = col == 0 ? ee : lf;
-        win[i % 3][1] = cc;
-        win[i % 3][2] = col == 31 ? ee : rt;
-      }
-#else
 #pragma unroll
       for (int d = 0; d < 3; ++d) win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
-#endif
       if (i >= 2) {
         const f32x2 h0 = win[(i - 2) % 3][0];
         float m = tk[0] * h0[0], v = tk[1] * h0[1];
@@ -733,74 +685,11 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
           v = __builtin_fmaf(tk[2 * t + 1], hv[1], v);
         }
         const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
-        const uint32_t vo = all_live ? vrow[i - 2] : (live ? vrow[i - 2] : kOut);
+        const uint32_t vo = all_live || live ? vrow[i - 2] : kOut;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, vo, soff0 + (i - 2) * W * 4, 0);
       }
     }
   };
-#else
-  auto gate = [&](int c) {
-    const float* hbuf = smem + (c & 1) * L6_HBUF;
-#pragma unroll
-    for (int p = 0; p < PPW; ++p) {
-      const int jj = L6_NP * c + PPW * wave + p;
-      // wave-uniform: past the hidden channels nothing is stored (soffset is not range-checked)
-      const int soff0 = jj < hid ? jj * HW * 4 : 0;
-      const bool live = jj < hid;
-      const float* hp = hbuf + (PPW * wave + p) * L6_PP + 2 * col;
-#if defined(GRR_GATE_DPP)
-      const float* hq = hbuf + (PPW * wave + p) * L6_PP;
-      const int ecol = col == 0 ? 0 : LH_HWD - 1;
-#endif
-      f32x2 win[3][3];                          // rows (i mod 3) x halo columns col .. col + 2
-#pragma unroll
-      for (int i = 0; i < RA + 2; ++i) {
-        const int hrow = min(r0 + i, L6_HR - 1) * LH_HWD;
-#if defined(GRR_GATE_DPP)
-        {  // one LDS read per lane (its centre column); the side columns from the neighbour lanes (DPP),
-           // the tile-edge lanes' outer column from a second, broadcast read (col 0 or 33 of the halo row)
-          const f32x2 cc = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + 1));
-          const f32x2 ee = *reinterpret_cast<const f32x2*>(hq + 2 * (hrow + ecol));
-          const f32x2 lf{dpp_shr1(cc[0]), dpp_shr1(cc[1])}, rt{dpp_shl1(cc[0]), dpp_shl1(cc[1])};
-          win[i % 3][0] = col == 0 ? ee : lf;
-          win[i % 3][1] = cc;
-          win[i % 3][2] = col == 31 ? ee : rt;
-        }
-#else
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-#ifdef GRR_DIAG_NOLDS   // timing-only diagnostic builds (wrong results): the window without LDS reads
-          win[i % 3][d] = f32x2{tp[p][d + 2 * (i % 3)], tp[p][d + 1]};
-#else
-          win[i % 3][d] = *reinterpret_cast<const f32x2*>(hp + 2 * (hrow + d));
-#endif
-        }
-#endif
-        if (i >= 2) {
-          const f32x2 h0 = win[(i - 2) % 3][0];
-          float m = tp[p][0] * h0[0], v = tp[p][1] * h0[1];
-#pragma unroll
-          for (int t = 1; t < 9; ++t) {
-            const f32x2 hv = win[(i - 2 + t / 3) % 3][t % 3];
-            m = __builtin_fmaf(tp[p][2 * t], hv[0], m);
-            v = __builtin_fmaf(tp[p][2 * t + 1], hv[1], v);
-          }
-#ifdef GRR_DIAG_NOEXP
-          const float gv = m * v;
-#else
-          const float gv = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
-#endif
-#ifdef GRR_DIAG_NOSTORE
-          diag_sink += gv;
-#else
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs, live ? vrow[i - 2] : kOut,
-                                                soff0 + (i - 2) * W * 4, 0);
-#endif
-        }
-      }
-    }
-  };
-#endif
 
   // prologue: chunk 0's fragments landed -> GEMM1(0), its taps, chunk 1 into slot 1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -814,8 +703,8 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
   asm volatile("" ::: "memory");
 
   // Iteration c: gate of chunk c - 1 (h buffer (c - 1) & 1, taps in registers) and GEMM1 of chunk c
-  // (slot c & 1 -> h buffer c & 1); the waves of a SIMD (w, w + 4, ...) run them in opposite orders, half
-  // each.  Slot (c + 1) & 1 last served GEMM1(c - 1) and load_taps(c - 1), both before the previous barrier.
+  // (slot c & 1 -> h buffer c & 1); the waves of a SIMD (w, w + 4) run them in opposite orders.  Slot
+  // (c + 1) & 1 last served GEMM1(c - 1) and load_taps(c - 1), both before the previous barrier.
   const bool gate_first = wave < NW / 2;
   for (int c = 1; c <= nch; ++c) {
     issue(min(c + 1, nch - 1), (c + 1) & 1);
@@ -827,19 +716,16 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
       gate(c - 1);
     }
     if (c < nch) load_taps(c);
-    // chunk c + 1 landed (after its DMAs this wave issued the PPW RA gate stores), then every wave's
+    // chunk c + 1 landed (after its DMAs this wave issued the GR gate stores), then every wave's
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(kGateStores) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-#ifdef GRR_DIAG_NOSTORE
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(diag_sink), grs, vrow[0], 0, 0);
-#endif
 }
 
 // ---------------------------------------------------------------------------
 // rep: the image filter's first block -- input = the C_s-channel image replicated over the graphs
-// (REF13:918-921), C_s * 9 <= 32 -- in one pass, LN through the skip, without g in HBM or h in LDS.
+// (REF13:918-921), C_s <= 3 -- in one pass, LN through the skip, without g in HBM or h in LDS.
 //
 // The depthwise 3x3 is linear in h = W1' n, so it folds into GEMM1 as an im2col GEMM:
 //   d[j, p] = sum_t tap[j, t] h[j, p + delta_t] = sum_{c, t} (tap[j, t] W1'[j, c]) n[c, p + delta_t]
@@ -849,15 +735,21 @@ __global__ __launch_bounds__(64 * NW, 1) void lnb_head16_kernel(LnbHeadArgs a) {
 // 2^s_row, each pixel's im2col column by 2^XE, corrected per column when its largest entry leaves the
 // range).  The 32 x 32 accumulator of a chunk (16 (mask, value) pairs x 32 pixels) holds both halves
 // of every pair in one lane, so the gate runs on it in registers, and the lane's eight gated values
-// are already the B operand of GEMM2 (W2 g, 32x32x16 bf16, exact three-term split, six products) once
-// W2's k order is permuted to the accumulator's pair order (lnb_rep_pack_kernel).  A workgroup = 8
-// waves x 32 pixels; the chunk's fragments (both GEMMs) and its per-row constants arrive by LDS-DMA in
-// a 3-slot ring two chunks ahead.  Against head16 + mix for this block: no g round trip (4 KB per
-// pixel of HBM traffic), no h planes in LDS, no depthwise FMAs.
+// are already the B operand of GEMM2 (W2 g, v_mfma_f32_32x32x16_f16 on two-term splits) once W2's k
+// order is permuted to the accumulator's pair order (lnb_rep_pack_kernel).  GEMM2's fp16 operands are
+// power-of-two scaled: W2 rows by 2^s2_row, each pixel's gated values by a running exponent E (set by
+// the first chunk's largest |g| of the pixel into [2^13, 2^14); a later chunk with larger values lowers
+// E and scales the pixel's accumulators down by the exact power of two), undone in the epilogue.
+// A workgroup = 8 waves x 32 pixels; the chunk's fragments (both GEMMs) and its per-row constants
+// arrive by LDS-DMA in a 4-slot ring three chunks ahead; four waves per SIMD (two workgroups per CU)
+// overlap one another's matrix and vector phases.  Against head16 + mix for
+// this block: no g round trip (4 KB per pixel of HBM traffic), no h planes in LDS, no depthwise FMAs.
 constexpr int LR_NW = 8;                  // waves per workgroup
 constexpr int LR_PX = LR_NW * 32;         // pixels per workgroup (one 32-pixel block per wave)
 constexpr int LR_XE = 10;                 // common power-of-two scale of the im2col operand
-__host__ __device__ constexpr int rep_images(int MT) { return 4 + 3 * MT + 1; }   // A1 (2 k-steps x hi/lo), A2 (MT x 3), row constants
+constexpr int LR_NSLOT = 4;               // ring slots (three chunks in flight ahead of GEMM2)
+// A1 (2 k-steps x hi / lo), A2 (MT row tiles x hi / lo), the gate's row constants, the W2 row scales
+__host__ __device__ constexpr int rep_images(int MT) { return 4 + 2 * MT + 1; }
 
 struct LnbRepArgs {
   const float* xs;      // [B, Cs, P]: the image the block input replicates
@@ -869,27 +761,47 @@ struct LnbRepArgs {
   uint32_t nblk;
 };
 
-// largest |tap[row, t] W1'[row, c]| over the folded row (C_s channels x 9 taps) -> its scale exponent
-__device__ __forceinline__ int rep_row_exp(const float* __restrict__ w1, const float* __restrict__ ln_w,
-                                           const float* __restrict__ wdw, int row, int Cs, int R) {
-  float mx = 0.f;
-  for (int c = 0; c < Cs; ++c) {
-    float w = 0.f;
-    for (int rep = 0; rep < R; ++rep) w += w1[(int64_t)row * (R * Cs) + rep * Cs + c] * ln_w[rep * Cs + c];
-    for (int t = 0; t < 9; ++t) mx = fmaxf(mx, fabsf(wdw[(int64_t)row * 9 + t] * w));
-  }
+// scale exponent of a row whose largest |entry| is mx: mx 2^s in [2^13, 2^14)
+__device__ __forceinline__ int rep_scale_exp(float mx) {
   if (mx == 0.f) return 0;
   int e;
   frexpf(mx, &e);
   return clampi(14 - e, -60, 60);
 }
+__device__ __forceinline__ float rep_w1f(const float* __restrict__ w1, const float* __restrict__ ln_w, int row, int c,
+                                         int Cs, int R) {
+  float w = 0.f;
+  for (int rep = 0; rep < R; ++rep) w += w1[(int64_t)row * (R * Cs) + rep * Cs + c] * ln_w[rep * Cs + c];
+  return w;
+}
+// largest |tap[row, t] W1'[row, c]| over the folded row (C_s channels x 9 taps) -> its scale exponent
+__device__ __forceinline__ int rep_row_exp(const float* __restrict__ w1, const float* __restrict__ ln_w,
+                                           const float* __restrict__ wdw, int row, int Cs, int R) {
+  float mx = 0.f;
+  for (int c = 0; c < Cs; ++c) {
+    const float w = rep_w1f(w1, ln_w, row, c, Cs, R);
+    for (int t = 0; t < 9; ++t) mx = fmaxf(mx, fabsf(wdw[(int64_t)row * 9 + t] * w));
+  }
+  return rep_scale_exp(mx);
+}
+__device__ __forceinline__ int rep_w2_exp(const float* __restrict__ w2, int m, int hid) {
+  float mx = 0.f;
+  for (int k = 0; k < hid; ++k) mx = fmaxf(mx, fabsf(w2[(int64_t)m * hid + k]));
+  return rep_scale_exp(mx);
+}
+__device__ __forceinline__ uint32_t f16_pair_word(float a, float b, int q) {   // term q (0 hi, 1 lo) of a, b
+  const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+  const _Float16 ta = q == 0 ? ha : (_Float16)(a - (float)ha), tb = q == 0 ? hb : (_Float16)(b - (float)hb);
+  return (uint32_t)__builtin_bit_cast(uint16_t, ta) | ((uint32_t)__builtin_bit_cast(uint16_t, tb) << 16);
+}
 
 // Per chunk c (16 pairs): images 0..3 = A1 (k-step s = im >> 1, term hi / lo = im & 1; lane l, element j:
 // GEMM row r = l & 31 -- pair 16 c + (r >> 1), mask (r even) or value -- and k = 16 s + 8 (l >> 5) + j =
-// 9 c_s + t); images 4 + 3 mt + q = A2 (W2 rows 32 mt + (l & 31), term q; k = 8 (l >> 5) + j is pair
-// pi = 4 (j >> 1) + (j & 1) + 2 (l >> 5) of the chunk: the accumulator's pair order); the last image =
-// the gate's row constants, word 16 kh + i for accumulator register i of lane half kh (row
-// (i & 3) + 8 (i >> 2) + 4 kh): -log2(e) 2^-(s_row + XE) (mask rows), -ln(2) 2^-(s_row + XE) (value rows).
+// 9 c_s + t), scaled by 2^s_row; images 4 + 2 mt + q = A2 (W2 rows 32 mt + (l & 31) scaled by 2^s2_row,
+// term q; k = 8 (l >> 5) + j is pair pi = 4 (j >> 1) + (j & 1) + 2 (l >> 5) of the chunk: the
+// accumulator's pair order); image 4 + 2 MT: words 16 kh + i = the gate's constant of accumulator
+// register i of lane half kh (row (i & 3) + 8 (i >> 2) + 4 kh): -log2(e) 2^-(s_row + XE) (mask rows),
+// -ln(2) 2^-(s_row + XE) (value rows); words 32 + m = 2^-s2_row of output row m (C <= 128).
 __global__ void lnb_rep_pack_kernel(const float* __restrict__ w1, const float* __restrict__ ln_w,
                                     const float* __restrict__ wdw, const float* __restrict__ w2,
                                     char* __restrict__ out, int Cs, int R, int C, int hid, int MT, int nch) {
@@ -905,34 +817,28 @@ __global__ void lnb_rep_pack_kernel(const float* __restrict__ w1, const float* _
       if (pj < hid) {
         const int row = (r & 1 ? hid : 0) + pj;
         const int sc = rep_row_exp(w1, ln_w, wdw, row, Cs, R);
-        uint16_t hb[2];
+        float v[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int k = 16 * s + 8 * (l >> 5) + 2 * (e & 3) + u;
-          float v = 0.f;
-          if (k < 9 * Cs) {
-            const int cs = k / 9, t = k % 9;
-            float w = 0.f;
-            for (int rep = 0; rep < R; ++rep) w += w1[(int64_t)row * (R * Cs) + rep * Cs + cs] * ln_w[rep * Cs + cs];
-            v = wdw[(int64_t)row * 9 + t] * w;
-          }
-          const float vs = ldexpf(v, sc);
-          const _Float16 h0 = (_Float16)vs;
-          const _Float16 t16 = q == 0 ? h0 : (_Float16)(vs - (float)h0);
-          hb[u] = __builtin_bit_cast(uint16_t, t16);
+          v[u] = 0.f;
+          if (k < 9 * Cs) v[u] = ldexpf(wdw[(int64_t)row * 9 + k % 9] * rep_w1f(w1, ln_w, row, k / 9, Cs, R), sc);
         }
-        word = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16);
+        word = f16_pair_word(v[0], v[1], q);
       }
-    } else if (im < 4 + 3 * MT) {
-      const int mt = (im - 4) / 3, q = (im - 4) % 3, m = 32 * mt + (l & 31);
-      uint16_t hb[2];
+    } else if (im < 4 + 2 * MT) {
+      const int mt = (im - 4) >> 1, q = (im - 4) & 1, m = 32 * mt + (l & 31);
+      if (m < C) {
+        const int sc = rep_w2_exp(w2, m, hid);
+        float v[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int j = 2 * (e & 3) + u;
-        const int pj = 16 * c + 4 * (j >> 1) + (j & 1) + 2 * (l >> 5);
-        hb[u] = (m < C && pj < hid) ? split_term(w2[(int64_t)m * hid + pj], q) : (uint16_t)0;
+        for (int u = 0; u < 2; ++u) {
+          const int j = 2 * (e & 3) + u;
+          const int pj = 16 * c + 4 * (j >> 1) + (j & 1) + 2 * (l >> 5);
+          v[u] = pj < hid ? ldexpf(w2[(int64_t)m * hid + pj], sc) : 0.f;
+        }
+        word = f16_pair_word(v[0], v[1], q);
       }
-      word = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16);
     } else if (e < 32) {
       const int kh = e >> 4, ii = e & 15, r = (ii & 3) + 8 * (ii >> 2) + 4 * kh, pj = 16 * c + (r >> 1);
       if (pj < hid) {
@@ -940,62 +846,75 @@ __global__ void lnb_rep_pack_kernel(const float* __restrict__ w1, const float* _
         const float fold = r & 1 ? -0.69314718055994531f : -1.44269504088896341f;
         word = __float_as_uint(ldexpf(fold, -(rep_row_exp(w1, ln_w, wdw, row, Cs, R) + LR_XE)));
       }
+    } else if (e < 32 + C) {
+      word = __float_as_uint(ldexpf(1.0f, -rep_w2_exp(w2, e - 32, hid)));
     }
     reinterpret_cast<uint32_t*>(out)[i] = word;
   }
 }
 
-template <int MT>
-__global__ __launch_bounds__(64 * LR_NW, 1) void lnb_rep_kernel(LnbRepArgs a) {
-  constexpr int NI = rep_images(MT), SLOTF = NI * 256, NSLOT = 3;
+template <int MT, int CS>
+// four waves per SIMD (two workgroups per CU): <= 128 VGPRs; the four-tile instance (C > 96) three
+__global__ __launch_bounds__(64 * LR_NW, MT <= 3 ? 4 : 3) void lnb_rep_kernel(LnbRepArgs a) {
+  constexpr int NI = rep_images(MT), SLOTF = NI * 256;
   constexpr int DPW = (NI + LR_NW - 1) / LR_NW;   // LDS-DMA instructions per wave per chunk
-  __shared__ __attribute__((aligned(16))) float smem[NSLOT * SLOTF];
+  constexpr int CI = 4 + 2 * MT;                   // the constants image
+  __shared__ __attribute__((aligned(16))) float smem[LR_NSLOT * SLOTF];
   const int lane = threadIdx.x & 63, kh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lb = xcd_remap(blockIdx.x, a.nblk);
   const int b = (int)(lb / (uint32_t)a.tiles), tile = (int)(lb % (uint32_t)a.tiles);
-  const int H = a.H, W = a.W, Cs = a.Cs, C = a.C, nch = a.nch;
+  const int H = a.H, W = a.W, C = a.C, nch = a.nch;
   const int P = H * W;
   const int p = tile * LR_PX + wave * 32 + (lane & 31);   // this lane's pixel (column of every MFMA block)
+
+  auto issue = [&](int c) {
+    float* slot = smem + (c % LR_NSLOT) * SLOTF;
+    const char* src = a.pack + (int64_t)min(c, nch - 1) * NI * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int img = min(i * LR_NW + wave, NI - 1);   // surplus waves repeat the last image
+      dma16_opaque(src + img * 1024, slot + img * 256);
+    }
+  };
 
   // im2col column of pixel p: n = x / sigma at the 9 replicate-clamped neighbours, k = 9 c + t; this lane
   // half holds k = 16 s + 8 kh + j
   const int pc = min(p, P - 1), py = pc / W, px = pc - py * W;
-  const float* xb = a.xs + (int64_t)b * Cs * P;
-  float nb[9][3];
+  const float* xb = a.xs + (int64_t)b * CS * P;
+  float nb[9][CS];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int yy = clampi(py + t / 3 - 1, 0, H - 1), xx = clampi(px + t % 3 - 1, 0, W - 1);
-    float v[3], sum = 0.f;
+    float v[CS], sum = 0.f;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      v[c] = c < Cs ? xb[(int64_t)c * P + yy * W + xx] : 0.f;
+    for (int c = 0; c < CS; ++c) {
+      v[c] = xb[(int64_t)c * P + yy * W + xx];
       sum += v[c];
     }
-    const float mean = sum / (float)Cs;
+    const float mean = sum / (float)CS;
     float sq = 0.f;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float d = c < Cs ? v[c] - mean : 0.f;
+    for (int c = 0; c < CS; ++c) {
+      const float d = v[c] - mean;
       sq += d * d;
     }
     const float rstd = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) nb[t][c] = v[c] * rstd;   // x / sigma (REF:921)
+    for (int c = 0; c < CS; ++c) nb[t][c] = v[c] * rstd;   // x / sigma (REF:921)
   }
+  // the entry of either lane half is a compile-time (c, t); one select per entry
+  auto im2col = [&](int k) -> float {
+    if (k >= 9 * CS) return 0.f;
+    return nb[k % 9][k / 9];
+  };
   float nv[2][8];
   float mx = 0.f;
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 16 * s2 + 8 * kh + j;
-      float v = 0.f;
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-          if (k == 9 * c + t && c < Cs) v = nb[t][c];
+      const float v = kh ? im2col(16 * s2 + 8 + j) : im2col(16 * s2 + j);
       nv[s2][j] = v;
       mx = fmaxf(mx, fabsf(v));
     }
@@ -1019,29 +938,13 @@ __global__ __launch_bounds__(64 * LR_NW, 1) void lnb_rep_kernel(LnbRepArgs a) {
       xl[s2][j] = (_Float16)(v - (float)h0);
     }
 
-  auto issue = [&](int c) {
-    float* slot = smem + (c % NSLOT) * SLOTF;
-    const char* src = a.pack + (int64_t)min(c, nch - 1) * NI * 1024 + lane * 16;
-#pragma unroll
-    for (int i = 0; i < DPW; ++i) {
-      const int img = min(i * LR_NW + wave, NI - 1);   // surplus waves repeat the last image
-      dma16_opaque(src + img * 1024, slot + img * 256);
-    }
-  };
   issue(0);
   issue(1);
+  issue(2);
 
-  f32x16 acc2[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) acc2[t] = f32x16{};
-  for (int c = 0; c < nch; ++c) {
-    // chunk c landed (this wave's DMAs; after them only chunk c + 1's), then every wave's
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPW) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(c + 2);                                   // slot (c + 2) % 3 was last read in iteration c - 1
-    const float* slot = smem + (c % NSLOT) * SLOTF + lane * 4;
-    // GEMM1 (im2col: LN, W1, depthwise in one accumulation)
+  // GEMM1 of chunk c (LN, W1, depthwise in one accumulation), from its ring slot
+  auto gemm1 = [&](int c) -> f32x16 {
+    const float* slot = smem + (c % LR_NSLOT) * SLOTF + lane * 4;
     f32x16 acc = f32x16{};
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -1051,45 +954,103 @@ __global__ __launch_bounds__(64 * LR_NW, 1) void lnb_rep_kernel(LnbRepArgs a) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl[s2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[s2], acc, 0, 0, 0);
     }
+    return acc;
+  };
+
+  // chunk 0 landed (this wave's DMAs; after them chunks 1 and 2's), then every wave's
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * DPW) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  f32x16 acc2[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc2[t] = f32x16{};
+  int E = 1000;                                     // the pixel's GEMM2 scale exponent (none yet)
+
+  // gate of the chunk whose GEMM1 accumulator is acc (ring slot of chunk c), then its GEMM2
+  auto gate_gemm2 = [&](int c, f32x16 acc) {
     if (wave_corr) acc *= corr;
     // gate sigmoid(m) m v (REF:947) on the accumulator: registers 2q, 2q + 1 = mask, value of chunk pair
     // 4 (q >> 1) + (q & 1) + 2 kh; the row constants undo the scales and carry the exp2 fold
-    const float* cst = smem + (c % NSLOT) * SLOTF + (4 + 3 * MT) * 256 + kh * 16;
+    const float* cslot = smem + (c % LR_NSLOT) * SLOTF;
+    const float* cst = cslot + CI * 256 + kh * 16;
     float gq[8];
+    float gm = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const float m = acc[2 * q] * cst[2 * q], v = acc[2 * q + 1] * cst[2 * q + 1];
       gq[q] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+      gm = fmaxf(gm, fabsf(gq[q]));
     }
-    bf16x8 b0, b1, b2;
-    split3x8(gq, b0, b1, b2);
-    // GEMM2: W2 (k permuted to the accumulator's pair order) g
+    // the pixel's running exponent: largest |g| so far into [2^13, 2^14); lowering it scales the
+    // accumulated sums down by the exact power of two
+    gm = fmaxf(gm, __shfl_xor(gm, 32));
+    int eg = E;
+    if (gm != 0.f) {
+      int e;
+      frexpf(gm, &e);
+      eg = min(E, clampi(14 - e, -100, 100));
+    }
+    if (__builtin_amdgcn_readfirstlane((int)__any(eg != E && E != 1000)) != 0) {
+      const float f = E != 1000 ? ldexpf(1.0f, eg - E) : 1.0f;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc2[t] *= f;
+    }
+    E = eg;
+    const int Eu = E == 1000 ? 0 : E;
+    f16x8 gh, gl;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float v = ldexpf(gq[q], Eu);
+      const _Float16 h0 = (_Float16)v;
+      gh[q] = h0;
+      gl[q] = (_Float16)(v - (float)h0);
+    }
+    // GEMM2: W2 (k permuted to the accumulator's pair order) g, three products of two-term splits
+    const float* slot = cslot + lane * 4;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + (4 + 3 * t + 0) * 256);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + (4 + 3 * t + 1) * 256);
-      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(slot + (4 + 3 * t + 2) * 256);
-      GRR_X3_MFMA(__builtin_amdgcn_mfma_f32_32x32x16_bf16, acc2[t], a0, a1, a2, b0, b1, b2);
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(slot + (4 + 2 * t + 0) * 256);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(slot + (4 + 2 * t + 1) * 256);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc2[t], 0, 0, 0);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc2[t], 0, 0, 0);
+      acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc2[t], 0, 0, 0);
     }
+  };
+
+  // (Measured on the bench shape, round 4: staggering the two waves of a SIMD -- half of them running
+  // gate(c), GEMM2(c), GEMM1(c + 1) -- spills at the 128-VGPR bound of four waves per SIMD, and GEMM1 of
+  // chunk c + 1 beside the gate of chunk c fits only three waves per SIMD: 1.73 ms against 1.52.)
+  for (int c = 0; c < nch; ++c) {
+    // chunk c + 1 landed (this wave's DMAs; after them only chunk c + 2's), then every wave's
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DPW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(c + 3);                                   // slot (c + 3) % 4 was last read in iteration c - 1
+    gate_gemm2(c, gemm1(c));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // epilogue (REF:962-964): out[m, p] = skip0 x[m mod Cs, p] + skip1 (W2 g)[m, p]
-  const float s0 = a.skip[0], s1 = a.skip[1];
+  // epilogue (REF:962-964): out[m, p] = skip0 x[m mod Cs, p] + skip1 (W2 g)[m, p] 2^-(s2_row + E).  Row m =
+  // 32 t + (i & 3) + 8 (i >> 2) + 4 kh: the wave-uniform part in soffset, the lane's 4 kh rows and its
+  // pixel in voffset (out of range past the image's pixels).  The W2 row scales come from the last
+  // chunk's slot (every slot holds them).
+  const float* rs2 = smem + ((nch - 1) % LR_NSLOT) * SLOTF + CI * 256 + 32;
+  const float s0 = a.skip[0], s1 = a.skip[1] * ldexpf(1.0f, E == 1000 ? 0 : -E);
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * C * P, 0,
                                                                         (int)((int64_t)C * P * 4), 0x00020000);
-  float xo[3];
+  float xo[CS];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) xo[c] = c < Cs ? xb[(int64_t)c * P + pc] : 0.f;
+  for (int c = 0; c < CS; ++c) xo[c] = xb[(int64_t)c * P + pc];
+  const uint32_t vb = p < P ? (uint32_t)(4 * kh * P + p) * 4u : 0x80000000u;
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * kh;
-      const int cm = m % Cs;                       // source channel of replica row m (no dynamic indexing)
-      const float xv = cm == 0 ? xo[0] : (cm == 1 ? xo[1] : xo[2]);
-      const uint32_t off = (m < C && p < P) ? (uint32_t)(m * P + p) * 4u : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv + s1 * acc2[t][i]), ors, off, 0, 0);
+      const int m0 = 32 * t + (i & 3) + 8 * (i >> 2);          // row of lane half 0; lane half 1: m0 + 4
+      const float xv = kh ? xo[(m0 + 4) % CS] : xo[m0 % CS];   // source channel of replica row m
+      const float r2 = rs2[min(m0 + 4 * kh, C - 1)];
+      const uint32_t vo = m0 + 4 < C ? vb : (m0 < C && !kh ? vb : 0x80000000u);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv + s1 * (acc2[t][i] * r2)), ors, vo, m0 * P * 4, 0);
     }
 }
 
@@ -1276,18 +1237,9 @@ template <int KS, int NB>
 static void launch_head(const LnbHeadArgs& h, hipStream_t s) {
   hipLaunchKernelGGL((lnb_head_kernel<KS, NB>), dim3(h.nblk), dim3(512), 0, s, h);
 }
-// GRR_HEAD16_NW=16: the 16-wave head (A/B measurement, round 4)
-static int head16_waves() {
-  static const int nw = [] { const char* e = getenv("GRR_HEAD16_NW"); return e && atoi(e) == 16 ? 16 : 8; }();
-  return nw;
-}
 template <int KS>
 static void launch_head16(const LnbHeadArgs& h, hipStream_t s) {
-#if !defined(GRR_GATE_COLPAIR)
-  if (head16_waves() == 16) hipLaunchKernelGGL((lnb_head16_kernel<KS, 16>), dim3(h.nblk), dim3(1024), 0, s, h);
-  else
-#endif
-    hipLaunchKernelGGL((lnb_head16_kernel<KS, 8>), dim3(h.nblk), dim3(512), 0, s, h);
+  hipLaunchKernelGGL((lnb_head16_kernel<KS, 8>), dim3(h.nblk), dim3(512), 0, s, h);
 }
 template <int MT>
 static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
@@ -1314,7 +1266,11 @@ bool lnb_rep_fused(int Ch, int R, int C, int hid) {
 
 template <int MT>
 static void launch_rep(const LnbRepArgs& r, hipStream_t s) {
-  hipLaunchKernelGGL((lnb_rep_kernel<MT>), dim3(r.nblk), dim3(64 * LR_NW), 0, s, r);
+  switch (r.Cs) {
+    case 1: hipLaunchKernelGGL((lnb_rep_kernel<MT, 1>), dim3(r.nblk), dim3(64 * LR_NW), 0, s, r); break;
+    case 2: hipLaunchKernelGGL((lnb_rep_kernel<MT, 2>), dim3(r.nblk), dim3(64 * LR_NW), 0, s, r); break;
+    default: hipLaunchKernelGGL((lnb_rep_kernel<MT, 3>), dim3(r.nblk), dim3(64 * LR_NW), 0, s, r); break;
+  }
 }
 
 grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
