@@ -46,9 +46,6 @@ SIGNATURES = {
     "grr_set_kernel_variant": [I],
     "grr_lnb_set_phases": [I],
     "grr_lnb_rep_fused": [I, I, I, I],
-    "grr_lnb_proj_supported": [I, I],
-    "grr_lnb_proj_workspace_bytes": [I, I, I, I, I, I],
-    "grr_lnb_forward_proj": [P, P, P, P, P, P, P, I, P, P, I, I, I, I, I, P],
     "grr_neighbor_table": [P, I, I, P],
     "grr_stream_copy": [P, P, L, P],
     "grr_edge_weights": [P, L, P, P, P, I, I, I, I, I, P],
@@ -132,8 +129,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64, "grr_wgrad_workspace_bytes": c_int64,
-             "grr_ffn_workspace_bytes": c_int64,
-             "grr_lnb_proj_workspace_bytes": c_int64}
+             "grr_ffn_workspace_bytes": c_int64}
 
 _lib = None
 

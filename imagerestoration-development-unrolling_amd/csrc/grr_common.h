@@ -48,7 +48,7 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
 // the same block when x holds R stacked copies of the Ch-channel image xh (GEMM1 runs on xh)
 grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
                                 const float* wdw, const float* w2, const float* skip, float* out, float* ws, int B,
-                                int hid, int H, int W, hipStream_t s, const float* wp = nullptr, int MP = 0);
+                                int hid, int H, int W, hipStream_t s);
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 

@@ -1066,69 +1066,11 @@ struct LnbMixArgs {
   const float* x;         // [B, C, P], or [B, xs_c, P] read at channel m mod xs_c when xs_c > 0
   int xs_c;
   const float* skip;      // [2]
-  float* out;             // [B, C, P], or [B, MP, P] with the projection
-  const char* wpf;        // projection (MPT > 0): [2 MT k-steps][MPT tiles][hi, lo] fragment images + row scales
-  int MP;                 // projection rows
+  float* out;             // [B, C, P]
   int64_t P;
   int C, hid, KS2, tiles;
   uint32_t nblk;
 };
-
-// The block's output is often only the input of a 1x1 convolution (the image filter's feature branches:
-// three LocalNonLinearBlocks, then C -> 2C, REF13:612-698).  With a projection Wp [MP, C] the mix kernel
-// writes f = Wp out instead of out: out stays in the accumulators, and their 32 x 32 layout (lane half kh of
-// a row tile t holds rows 32 t + (i & 3) + 8 (i >> 2) + 4 kh, i = 0..15) already is the B operand of
-// v_mfma_f32_32x32x16_f16 for two 16-deep k-steps (t, h2 = i >> 3) once Wp's columns are permuted to
-// that order: k = 8 kh + j <-> channel 32 t + 16 h2 + 8 (j >> 2) + 4 kh + (j & 3).  fp16 two-term splits
-// (three products), Wp rows scaled by 2^s_row, each pixel's out vector by 2^e_px (its largest |entry| into
-// [2^13, 2^14)), both undone at the store.  Images: k-step ks = 2 t + h2, tile tt, term q at
-// (ks MPT + tt) 2 + q; then the row scales 2^-s_row (floats).
-__host__ __device__ constexpr int proj_images(int MT, int MPT) { return 2 * MT * MPT * 2 + (32 * MPT + 255) / 256; }
-__global__ void lnb_wp_pack_kernel(const float* __restrict__ wp, uint32_t* __restrict__ out, int C, int MP, int MT,
-                                   int MPT) {
-  const int NF = 2 * MT * MPT * 2;
-  const int64_t n = (int64_t)proj_images(MT, MPT) * 256;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int img = (int)(i >> 8), e = (int)(i & 255);
-    uint32_t word = 0;
-    if (img < NF) {
-      const int q = img & 1, tt = (img >> 1) % MPT, ks = (img >> 1) / MPT, t = ks >> 1, h2 = ks & 1;
-      const int l = e >> 2, m = 32 * tt + (l & 31);
-      if (m < MP) {
-        float mx = 0.f;
-        for (int c = 0; c < C; ++c) mx = fmaxf(mx, fabsf(wp[(int64_t)m * C + c]));
-        int sc = 0;
-        if (mx != 0.f) {
-          int ex;
-          frexpf(mx, &ex);
-          sc = clampi(14 - ex, -60, 60);
-        }
-        float v[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int j = 2 * (e & 3) + u;
-          const int ch = 32 * t + 16 * h2 + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3);
-          v[u] = ch < C ? ldexpf(wp[(int64_t)m * C + ch], sc) : 0.f;
-        }
-        word = f16_pair_word(v[0], v[1], q);
-      }
-    } else {
-      const int m = (img - NF) * 256 + e;
-      if (m < MP) {
-        float mx = 0.f;
-        for (int c = 0; c < C; ++c) mx = fmaxf(mx, fabsf(wp[(int64_t)m * C + c]));
-        int sc = 0;
-        if (mx != 0.f) {
-          int ex;
-          frexpf(mx, &ex);
-          sc = clampi(14 - ex, -60, 60);
-        }
-        word = __float_as_uint(ldexpf(1.0f, -sc));
-      }
-    }
-    out[i] = word;
-  }
-}
 
 // W2 [C, hid] -> 32x32x16 A fragments.  k-step s, row tile t, term q, lane l, element j:
 // m = 32 t + (l & 31), k = 16 s + 8 (l >> 5) + j.
@@ -1144,95 +1086,9 @@ __global__ void lnb_w2_pack_kernel(const float* __restrict__ w2, uint16_t* __res
   }
 }
 
-// Projection epilogue of lnb_mix_kernel (MPT > 0): out = skip0 x + skip1 acc per pixel block, then
-// f = Wp out (see lnb_wp_pack_kernel) from the reused ring, stored as [B, MP, P].
-template <int MT, int MPT>
-__device__ __forceinline__ void mix_project(const LnbMixArgs& a, f32x16 (&acc)[MT][LM_NBB], float* smem, int b,
-                                            int64_t p0, int wave, int lane) {
-  constexpr int NF = 2 * MT * MPT * 2, NIMG = proj_images(MT, MPT);
-  const int r = lane & 31, hh = lane >> 5;
-  const int C = a.C, MP = a.MP;
-  const int Pi = (int)a.P;
-  // every wave has left the k-step loop (its last ring reads) -> the projection images into the ring
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  for (int im = wave; im < NIMG; im += 4) dma16(a.wpf + (int64_t)im * 1024 + lane * 16, smem + im * 256);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  const float* rsc = smem + NF * 256;               // 2^-s_row of projection row m
-  const float s0 = a.skip[0], s1 = a.skip[1];
-  // (the projection path has a plain C-channel skip operand: grr_lnb_forward_proj)
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.x + (int64_t)b * C * a.P), 0, (int)((int64_t)C * a.P * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * MP * a.P, 0,
-                                                                        (int)((int64_t)MP * a.P * 4), 0x00020000);
-#pragma unroll
-  for (int nb = 0; nb < LM_NBB; ++nb) {
-    const int p = (int)p0 + (wave * LM_NBB + nb) * 32 + r;
-    const int pc = min(p, Pi - 1);
-    // out = skip0 x + skip1 W2 g in the accumulators (rows >= C zero); the pixel's largest |out|
-    float mx = 0.f;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (min(m, C - 1) * Pi + pc) * 4, 0, 0));
-        const float o = m < C ? s0 * xv + s1 * acc[t][nb][i] : 0.f;
-        acc[t][nb][i] = o;
-        mx = fmaxf(mx, fabsf(o));
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    int ep = 0;
-    if (mx != 0.f) {
-      int ex;
-      frexpf(mx, &ex);
-      ep = clampi(14 - ex, -100, 100);
-    }
-    // B operands: k-step (t, h2) = registers 8 h2 .. 8 h2 + 7 of row tile t, two fp16 terms
-    f16x8 bh[2 * MT], bl[2 * MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = ldexpf(acc[t][nb][8 * h2 + j], ep);
-          const _Float16 h0 = (_Float16)v;
-          bh[2 * t + h2][j] = h0;
-          bl[2 * t + h2][j] = (_Float16)(v - (float)h0);
-        }
-    const float pxs = ldexpf(1.0f, -ep);
-    const uint32_t vb = p < Pi ? (uint32_t)(4 * hh * Pi + p) * 4u : 0x80000000u;
-#pragma unroll
-    for (int tt = 0; tt < MPT; ++tt) {
-      f32x16 f = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < 2 * MT; ++ks) {
-        const float* im = smem + ((ks * MPT + tt) * 2) * 256 + lane * 4;
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(im);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(im + 256);
-        f = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[ks], f, 0, 0, 0);
-        f = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[ks], f, 0, 0, 0);
-        f = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[ks], f, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m0 = 32 * tt + (i & 3) + 8 * (i >> 2);        // lane half 1: m0 + 4
-        const int m = m0 + 4 * hh;
-        const uint32_t vo = m0 + 4 < MP ? vb : (m < MP ? vb : 0x80000000u);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f[i] * rsc[min(m, MP - 1)] * pxs), ors, vo,
-                                              m0 * Pi * 4, 0);
-      }
-    }
-  }
-}
-
 // A k-step's operands -- the W2 fragment images and the [16][256-pixel] g tile -- arrive by
 // LDS-DMA in a 3-slot ring two k-steps ahead.  V4 (P % 4 == 0): one 16-byte DMA per g row.
-template <int MT, bool V4, int MPT = 0>
+template <int MT, bool V4>
 __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArgs a) {
   constexpr int NI = MT * 3;
   constexpr int WPW = (NI + 3) / 4;                 // W2 image DMAs per wave per k-step
@@ -1318,10 +1174,6 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void lnb_mix_kernel(LnbMixArg
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if constexpr (MPT > 0) {
-    mix_project<MT, MPT>(a, acc, smem, b, p0, wave, lane);
-    return;
-  }
   // epilogue (REF:962-964): rows m = 32 t + (i & 3) + 8 (i >> 2) + 4 hh, pixel = lane column;
   // x / out through buffer descriptors (32-bit offsets; rows >= C or pixels >= P not stored)
   const float s0 = a.skip[0], s1 = a.skip[1];
@@ -1389,33 +1241,10 @@ template <int KS>
 static void launch_head16(const LnbHeadArgs& h, hipStream_t s) {
   hipLaunchKernelGGL((lnb_head16_kernel<KS, 8>), dim3(h.nblk), dim3(512), 0, s, h);
 }
-template <int MT, int MPT = 0>
-static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
-  if (v4) hipLaunchKernelGGL((lnb_mix_kernel<MT, true, MPT>), dim3(m.nblk), dim3(256), 0, s, m);
-  else hipLaunchKernelGGL((lnb_mix_kernel<MT, false, MPT>), dim3(m.nblk), dim3(256), 0, s, m);
-}
-// the projection images must fit the mix kernel's 3-slot ring (reused after its k-step loop)
-bool lnb_proj_supported(int C, int MP) {
-  if (C < 2 || C > 96 || MP < 1) return false;
-  const int MT = (C + 31) / 32, MPT = (MP + 31) / 32;
-  const int slot_floats = MT * 3 * 256 + LM_KD * LM_PX;
-  return MPT <= 6 && (int64_t)proj_images(MT, MPT) * 256 <= 3 * slot_floats;
-}
-int64_t lnb_proj_workspace_floats(int B, int C, int hid, int H, int W, int MP) {
-  return lnb_mfma_workspace_floats(B, C, hid, H, W) + align64((int64_t)proj_images((C + 31) / 32, (MP + 31) / 32) * 256);
-}
 template <int MT>
-static grr_status launch_mix_proj(const LnbMixArgs& m, bool v4, int MPT, hipStream_t s) {
-  switch (MPT) {
-    case 1: launch_mix<MT, 1>(m, v4, s); break;
-    case 2: launch_mix<MT, 2>(m, v4, s); break;
-    case 3: launch_mix<MT, 3>(m, v4, s); break;
-    case 4: launch_mix<MT, 4>(m, v4, s); break;
-    case 5: launch_mix<MT, 5>(m, v4, s); break;
-    case 6: launch_mix<MT, 6>(m, v4, s); break;
-    default: GRR_REQUIRE(false, GRR_ERR_UNSUPPORTED, "grr_lnb_forward_proj: %d projection tiles", MPT);
-  }
-  return GRR_OK;
+static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
+  if (v4) hipLaunchKernelGGL((lnb_mix_kernel<MT, true>), dim3(m.nblk), dim3(256), 0, s, m);
+  else hipLaunchKernelGGL((lnb_mix_kernel<MT, false>), dim3(m.nblk), dim3(256), 0, s, m);
 }
 
 // measurement knob (grr_lnb_set_phases): which of pack (1) / head (2) / mix (4) a forward launches, so
@@ -1446,14 +1275,12 @@ static void launch_rep(const LnbRepArgs& r, hipStream_t s) {
 
 grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
                                 const float* wdw, const float* w2, const float* skip, float* out, float* ws, int B,
-                                int hid, int H, int W, hipStream_t s, const float* wp, int MP) {
+                                int hid, int H, int W, hipStream_t s) {
   const int C = R * Ch;   // channels of x / out; the head reads the Ch-channel xh
   GRR_REQUIRE(C >= 2 && C <= 128 && Ch >= 1, GRR_ERR_UNSUPPORTED, "grr_lnb_forward: C=%d outside [2, 128]", C);
   GRR_REQUIRE((int64_t)std::max(hid, C) * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_lnb_forward: max(hid, C)*H*W too large for one image's 32-bit offsets");
-  GRR_REQUIRE(!wp || (R == 1 && lnb_proj_supported(C, MP)), GRR_ERR_UNSUPPORTED,
-              "grr_lnb_forward_proj: C=%d, MP=%d not supported", C, MP);
-  if (!wp && lnb_rep_fused(Ch, R, C, hid)) {
+  if (lnb_rep_fused(Ch, R, C, hid)) {
     // workspace: the chunk images at its start (the g region the two-kernel path would use is not needed)
     const int MT = (C + 31) / 32, nch = (hid + 15) / 16;
     char* pack = reinterpret_cast<char*>(ws);
@@ -1489,14 +1316,7 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   float* g = ws;
   char* w1f = reinterpret_cast<char*>(ws + align64((int64_t)B * hid * P));
   uint16_t* w2f = reinterpret_cast<uint16_t*>(ws + align64((int64_t)B * hid * P) + head_pack_floats(Ch, hid));
-  // projection images after the W2 images (grr_lnb_forward_proj)
-  uint32_t* wpf = wp ? reinterpret_cast<uint32_t*>(ws + lnb_mfma_workspace_floats(B, C, hid, H, W)) : nullptr;
   if (g_lnb_phases & 1) {
-    if (wp) {
-      const int64_t n3 = (int64_t)proj_images((C + 31) / 32, (MP + 31) / 32) * 256;
-      hipLaunchKernelGGL(lnb_wp_pack_kernel, dim3((unsigned)std::min<int64_t>((n3 + 255) / 256, 4096)), dim3(256), 0, s,
-                         wp, wpf, C, MP, (C + 31) / 32, (MP + 31) / 32);
-    }
     const int64_t n1 = (int64_t)nch * (h16 ? head16_images(KS) : head_images(KS)) * 256;
     const int64_t n2 = (int64_t)KS2 * MT * 3 * 512;
     const dim3 g1((unsigned)std::min<int64_t>((n1 + 255) / 256, 4096));
@@ -1548,19 +1368,6 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
   GRR_REQUIRE(nm < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
   m.nblk = (uint32_t)nm;
   const bool v4 = P % 4 == 0;
-  if (wp) {
-    m.wpf = reinterpret_cast<const char*>(wpf);
-    m.MP = MP;
-    const int MPT = (MP + 31) / 32;
-    grr_status st2 = GRR_OK;
-    switch (MT) {
-      case 1: st2 = launch_mix_proj<1>(m, v4, MPT, s); break;
-      case 2: st2 = launch_mix_proj<2>(m, v4, MPT, s); break;
-      default: st2 = launch_mix_proj<3>(m, v4, MPT, s); break;
-    }
-    if (st2 != GRR_OK) return st2;
-    return launch_status("grr_lnb_forward_proj/mix");
-  }
   switch (MT) {
     case 1: launch_mix<1>(m, v4, s); break;
     case 2: launch_mix<2>(m, v4, s); break;
@@ -1573,29 +1380,6 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
 }  // namespace grr
 
 extern "C" int grr_lnb_rep_fused(int Cs, int R, int C, int hid) { return grr::lnb_rep_fused(Cs, R, C, hid) ? 1 : 0; }
-
-extern "C" int grr_lnb_proj_supported(int C, int MP) { return grr::lnb_proj_supported(C, MP) ? 1 : 0; }
-
-extern "C" int64_t grr_lnb_proj_workspace_bytes(int B, int C, int hid, int H, int W, int MP) {
-  if (B <= 0 || C <= 0 || hid <= 0 || H <= 0 || W <= 0 || MP <= 0) return 0;
-  return grr::lnb_proj_workspace_floats(B, C, hid, H, W, MP) * (int64_t)sizeof(float);
-}
-
-extern "C" grr_status grr_lnb_forward_proj(const float* x, const float* ln_w, const float* w1, const float* wdw,
-                                           const float* w2, const float* skip, const float* wp, int MP, float* out,
-                                           void* workspace, int B, int C, int hid, int H, int W, void* stream) {
-  grr::clear_error();
-  GRR_REQUIRE(x && ln_w && w1 && wdw && w2 && skip && wp && out && workspace && B > 0 && C > 1 && hid > 0 && MP > 0 &&
-                  H > 0 && W > 0,
-              GRR_ERR_INVALID_ARG, "grr_lnb_forward_proj: bad args");
-  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward_proj: out aliases x");
-  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG, "grr_lnb_forward_proj: workspace not 256-B aligned");
-  GRR_REQUIRE(grr::lnb_proj_supported(C, MP), GRR_ERR_UNSUPPORTED, "grr_lnb_forward_proj: C=%d, MP=%d not supported", C, MP);
-  GRR_REQUIRE((int64_t)MP * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
-              "grr_lnb_forward_proj: MP*H*W too large for one image's 32-bit offsets");
-  return grr::lnb_forward_mfma_rep(x, C, 1, x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, hid, H, W,
-                                   (hipStream_t)stream, wp, MP);
-}
 
 extern "C" grr_status grr_lnb_set_phases(int mask) {
   grr::clear_error();

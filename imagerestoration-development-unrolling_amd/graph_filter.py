@@ -43,9 +43,6 @@ FEATURE_STREAMS = os.environ.get("GRR_FEATURE_STREAMS", "1") == "1"
 # GEMMs co-resident on both streams; those reductions now run on grr_wgrad
 FEATURE_STREAMS_TRAIN = os.environ.get("GRR_FEATURE_STREAMS_TRAIN", "1") == "1"
 _SIDE_STREAMS = {}
-# Inference: a feature branch's last LocalNonLinearBlock and its 1x1 conv run as one pass
-# (grr_lnb_forward_proj; GRR_LNB_PROJ=0: the block, then the conv)
-LNB_PROJ = os.environ.get("GRR_LNB_PROJ", "1") == "1"
 
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
@@ -284,21 +281,6 @@ class LocalNonLinearBlock(HipModule):
                                    ll.channels_local_linear_op.weight.view(2 * hid, 9),
                                    ll.project_out.weight.view(c, hid), self.skip_weight)
 
-    @torch.no_grad()
-    def forward_proj(self, x, weight):
-        """Inference: conv1x1(self(x), weight) (weight [MP, C, 1, 1]) with the block's output kept in the mix
-        kernel when the sizes allow it (grr_lnb_forward_proj), else the two steps."""
-        ll = self.local_linear
-        c, hid = self.dim, self.hidden_dim
-        b, _, h, w = x.shape
-        if LNB_PROJ and self.nsubnets == 1 and K.lnb_proj_supported(c, weight.shape[0]) \
-                and K._lnb_band_rows(c, hid, h, w) >= h:
-            return OPS.lnb_forward_proj(x.contiguous(), self.norm.weighted_transform.weight.view(c),
-                                        ll.channels_linear_op.weight.view(2 * hid, c),
-                                        ll.channels_local_linear_op.weight.view(2 * hid, 9),
-                                        ll.project_out.weight.view(c, hid), self.skip_weight, weight)
-        return OPS.conv1x1(self(x), weight)
-
     @hip_forward
     def _forward_hip(self, x):
         ll = self.local_linear
@@ -380,9 +362,9 @@ class MixtureGTVGLR(HipModule):
 
         def half():
             f1 = self._down(y, s1[0].weight, src)
-            for blk in list(s1)[1:3]:
+            for blk in list(s1)[1:4]:
                 f1 = blk(f1)
-            f1 = s1[3].forward_proj(f1, s1[4].weight)       # last block + 1x1 conv in one mix pass
+            f1 = OPS.conv1x1(f1, s1[4].weight)
             return half_tail(f1) if half_tail is not None else f1
 
         side = None
@@ -398,8 +380,9 @@ class MixtureGTVGLR(HipModule):
         blocks = list(s0)[:3]
         # the first block's input replicates src over the graphs: its GEMM1 runs on src (K = F)
         f0 = blocks[0].forward_replicated(src, y) if src is not None else blocks[0](y)
-        f0 = blocks[1](f0)
-        f0 = blocks[2].forward_proj(f0, s0[3].weight)            # last block + 1x1 conv in one mix pass
+        for blk in blocks[1:]:
+            f0 = blk(f0)
+        f0 = OPS.conv1x1(f0, s0[3].weight)
         if side is not None:
             main.wait_stream(side)
             for t in (f1 if isinstance(f1, tuple) else (f1,)):

@@ -625,46 +625,6 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     return out
 
 
-def lnb_proj_supported(c: int, mp: int) -> bool:
-    """grr_lnb_proj_supported restated (pure Python, so that Dynamo traces callers): the projection images
-    must fit the mix kernel's 3-slot ring (tests/test_abi.py checks the two agree)."""
-    if c < 2 or c > 96 or mp < 1:
-        return False
-    mt, mpt = (c + 31) // 32, (mp + 31) // 32
-    images = 2 * mt * mpt * 2 + (32 * mpt + 255) // 256
-    return mpt <= 6 and images * 256 <= 3 * (mt * 3 * 256 + 16 * 256)
-
-
-def lnb_forward_proj(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor,
-                     wp: Tensor) -> Tensor:
-    """wp . LocalNonLinearBlock(x) for a 1x1 projection wp [MP, C] (the conv after a feature branch's last
-    block, REF13:612-698): the block's output never leaves the mix kernel (grr_lnb_forward_proj)."""
-    dev = _check("lnb_forward_proj", x, ln_w, w1, wdw, w2, skip, wp)
-    b, c, h, w = x.shape
-    hid, mp = w2.shape[1], wp.shape[0]
-    if not lnb_proj_supported(c, mp) or _lnb_band_rows(c, hid, h, w) < h:
-        raise ValueError(f"lnb_forward_proj: C={c}, MP={mp}, {h}x{w} not supported")
-    nbytes = _native.load().grr_lnb_proj_workspace_bytes(b, c, hid, h, w, mp)
-    ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
-    out = torch.empty((b, mp, h, w), dtype=torch.float32, device=dev)
-    args = (x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
-            wp.data_ptr(), mp, out.data_ptr(), ws.data_ptr(), b, c, hid, h, w, _stream(dev))
-    px = b * h * w
-    if _lnb_split(c):
-        try:
-            call("grr_lnb_set_phases", 3)
-            _launch("lnb_head", 4 * px * (c + hid), "grr_lnb_forward_proj", *args, flops=lnb_head_flops(px, c, hid))
-            call("grr_lnb_set_phases", 4)
-            _launch("lnb_mix_proj", 4 * px * (hid + c + mp), "grr_lnb_forward_proj", *args,
-                    flops=px * (2 * hid * c + 3 * c + 2 * c * mp))
-        finally:
-            call("grr_lnb_set_phases", 7)
-        return out
-    _launch("lnb", 4 * px * (c + 2 * hid + c + mp), "grr_lnb_forward_proj", *args,
-            flops=lnb_flops(px, c, c, hid) + 2 * px * c * mp)
-    return out
-
-
 def lnb_forward_rep(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
                     skip: Tensor) -> Tensor:
     """LocalNonLinearBlock forward when its input [B, R*Cs, H, W] is R copies of src [B, Cs, H, W];

@@ -87,18 +87,6 @@ def _(x, ln_w, w1, wdw, w2, skip):
     return torch.empty_like(x)
 
 
-@custom_op(f"{NS}::lnb_forward_proj", mutates_args=())
-def lnb_forward_proj_op(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor,
-                        wp: Tensor) -> Tensor:
-    return K.lnb_forward_proj(x.contiguous(), ln_w.contiguous(), w1.contiguous(), wdw.contiguous(), w2.contiguous(),
-                              skip.contiguous(), wp.contiguous())
-
-
-@lnb_forward_proj_op.register_fake
-def _(x, ln_w, w1, wdw, w2, skip, wp):
-    return x.new_empty((x.shape[0], wp.shape[0], x.shape[2], x.shape[3]))
-
-
 @custom_op(f"{NS}::lnb_forward_rep", mutates_args=())
 def lnb_forward_rep_op(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
                        skip: Tensor) -> Tensor:
@@ -387,12 +375,6 @@ def lnb_forward(x, ln_w, w1, wdw, w2, skip):
     if _tracing():
         return torch.ops.irdu.lnb_forward(x, ln_w, w1, wdw, w2, skip)
     return K.lnb_forward(x, ln_w, w1, wdw, w2, skip)
-
-
-def lnb_forward_proj(x, ln_w, w1, wdw, w2, skip, wp):
-    if _tracing():
-        return torch.ops.irdu.lnb_forward_proj(x, ln_w, w1, wdw, w2, skip, wp)
-    return K.lnb_forward_proj(x, ln_w, w1, wdw, w2, skip, wp)
 
 
 def lnb_forward_rep(src, x, ln_w, w1, wdw, w2, skip):

@@ -299,18 +299,6 @@ grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, 
  * Phase mask 2 of grr_lnb_set_phases then launches the whole block and mask 4 nothing. */
 int grr_lnb_rep_fused(int Cs, int R, int C, int hid);
 
-/* out [B, MP, H, W] = wp . LocalNonLinearBlock(x) for a 1x1 projection wp [MP, C] (the image filter's
- * feature branches end with a block followed by a C -> 2C convolution, REF13:612-698): the block's
- * output stays in the mix kernel's accumulators and is projected there (fp16 two-term splits with
- * power-of-two row / pixel scaling, fp32-class accuracy).  Supported when grr_lnb_proj_supported(C, MP)
- * (C <= 96, MP <= 192); workspace: grr_lnb_proj_workspace_bytes(B, C, hid, H, W, MP) bytes.  Phase
- * mask 4 of grr_lnb_set_phases launches the mix with the projection. */
-int grr_lnb_proj_supported(int C, int MP);
-int64_t grr_lnb_proj_workspace_bytes(int B, int C, int hid, int H, int W, int MP);
-grr_status grr_lnb_forward_proj(const float* x, const float* ln_w, const float* w1, const float* wdw,
-                                const float* w2, const float* skip, const float* wp, int MP, float* out,
-                                void* workspace, int B, int C, int hid, int H, int W, void* stream);
-
 /* Channel replication of MultiScaleGraphFilter.forward (REF13:918-921):
  * img [B,Cin,H,W] -> out [B,G*Cin,H,W], out[b, g*Cin + c] = img[b, c]. */
 grr_status grr_repeat_graphs(const float* img, float* out, int B, int Cin, int G, int64_t P, void* stream);

@@ -96,13 +96,3 @@ def test_stage_count_parameter_shapes():
     assert "localfilter.scaling_kernel01" not in m.state_dict()
     assert m.localfilter.GLRmodule00.edge_delta.dtype == torch.int32
     assert np.array_equal(m.localfilter.GLRmodule00.edge_delta.numpy(), [[-1, 0], [0, -1], [0, 1], [1, 0]])
-
-
-def test_lnb_projection_rule_matches_library():
-    """kernels.lnb_proj_supported (Python, traced by Dynamo) restates grr_lnb_proj_supported exactly."""
-    import irdu_amd
-    lib = irdu_amd.load_native()
-    for c in range(0, 140, 3):
-        for mp in (0, 1, 3, 40, 96, 150, 192, 193, 224, 400):
-            assert bool(lib.grr_lnb_proj_supported(c, mp)) == irdu_amd.kernels.lnb_proj_supported(c, mp), (c, mp)
-    assert irdu_amd.kernels.lnb_proj_supported(96, 192)

@@ -44,9 +44,7 @@ def test_msgf_graph_is_opaque_hip_ops():
     seen = graph_ops(m, torch.rand(2, 3, 16, 24))
     assert_only_irdu(seen)
     assert seen["irdu.system_step.default"] == 4 and seen["irdu.system_half.default"] == 4
-    assert seen["irdu.lnb_forward_rep.default"] == 1 and seen["irdu.lnb_forward.default"] == 3
-    # each feature branch's last block and its 1x1 conv: one opaque node (grr_lnb_forward_proj)
-    assert seen["irdu.lnb_forward_proj.default"] == 2
+    assert seen["irdu.lnb_forward_rep.default"] == 1 and seen["irdu.lnb_forward.default"] == 5
 
 
 @pytest.mark.parametrize("model_fn, shape", [

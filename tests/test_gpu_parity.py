@@ -317,32 +317,6 @@ def test_replicated_lnb_fused(irdu, cs_r_hid_hw, gray):
             assert err <= 4 * err32 + 1e-6, (err, err32)
 
 
-# A block followed by a 1x1 projection in one pass (grr_lnb_forward_proj: the block output projected
-# inside the mix kernel, fp16 two-term splits with row / pixel power-of-two scaling): against float64 of
-# conv1x1(block(x)), fp32-class error; the image filter's shape (C = 96 -> 192), partial row tiles and
-# pixels (C = 33, MP = 40, H W % 256 != 0), a pixel whose output is all zero.
-@pytest.mark.parametrize("c_hid_mp_hw", [(96, 256, 192, (40, 36)), (33, 20, 40, (9, 13)), (64, 48, 100, (16, 20)),
-                                         (12, 32, 24, (5, 7))])
-def test_lnb_projection_fused(irdu, c_hid_mp_hw):
-    c, hid, mp, (h, w) = c_hid_mp_hw
-    assert irdu.kernels.lnb_proj_supported(c, mp)
-    torch.manual_seed(4)
-    blk = irdu.LocalNonLinearBlock(c, hid, 1)
-    with torch.no_grad():
-        blk.skip_weight.copy_(torch.tensor([0.7, 1.1]))
-        blk.norm.weighted_transform.weight.mul_(1.0 + 0.2 * torch.randn_like(blk.norm.weighted_transform.weight))
-    wp = rand(mp, c, 1, 1, seed=41) * 0.2
-    x = rand(2, c, h, w, seed=42)
-    p64 = {k: v.double() for k, v in sd_cpu(blk).items()}
-    ref64 = torch.nn.functional.conv2d(O.local_nonlinear_block(x.double(), p64, ""), wp.double())
-    ref32 = torch.nn.functional.conv2d(O.local_nonlinear_block(x, sd_cpu(blk), ""), wp)
-    err32 = rel_err(ref32, ref64)
-    blk = blk.to(DEV)
-    got = blk.forward_proj(x.to(DEV), wp.to(DEV))
-    err = rel_err(got, ref64)
-    assert err <= 4 * err32 + 1e-6, (err, err32)
-
-
 # (C, hid, H, W): C <= 128 runs the split-bf16 head (32 x 13 / 32 x 9 output tiles with halo
 # recompute) + mix kernels: full / partial tiles, H*W % 4 == 0 (16-byte g DMA) and not (dword
 # DMA), hid % 8 != 0 and hid % 16 != 0 (partial chunk / k-step), C = 33 (partial k-step and
