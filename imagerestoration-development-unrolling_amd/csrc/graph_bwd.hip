@@ -19,13 +19,16 @@
 // All are HBM-bound streaming passes with one thread per pixel; the F node features of
 // one graph are looped inside the thread so the graph's edge weights are read once.
 // Reductions (per-graph scalars, per-channel taps, multiM) are accumulated in registers
-// over a grid-strided pixel range, reduced across the wave with DPP shuffles, and folded
-// with one float atomic per wave.
+// over a grid-strided pixel range, reduced across the wave with shuffles and across the
+// workgroup through LDS in wave order, and stored into the contributor's own slot of a
+// partials array; red_finish_kernel adds the slots in order (grr_common.h, "Fixed-order
+// reductions"): bitwise run-to-run reproducible, no float atomics.
 //
 // Tap order (host computes taps [C,5] from stats_kernel_p01/p02a/p02b/p03):
 //   0 centre (0,0), 1 up (-1,0), 2 left (0,-1), 3 right (0,+1), 4 down (+1,0).
 // Edge order (REF:42-53): 0 up, 1 left, 2 right, 3 down; opposite(e) = 3 - e.
 #include <algorithm>
+#include <mutex>
 
 #include "grr_common.h"
 
@@ -40,9 +43,10 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// one atomic per block: wave sums -> LDS -> thread 0.  Every thread of the block must call it
-// (it synchronises); consecutive calls reuse the LDS slots safely.
-__device__ __forceinline__ void block_atomic_add(float* dst, float v) {
+// one partial per block: wave sums -> LDS -> thread 0 adds them in wave order and stores the
+// block's slot.  Every thread of the block must call it (it synchronises); consecutive calls
+// reuse the LDS slots safely.
+__device__ __forceinline__ void block_red_put(const Red& r, int idx, uint32_t slot, float v) {
   __shared__ float red[NT / 64];
   v = wave_sum(v);
   __syncthreads();
@@ -52,8 +56,12 @@ __device__ __forceinline__ void block_atomic_add(float* dst, float v) {
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < NT / 64; ++i) t += red[i];
-    if (t != 0.f) atomicAdd(dst, t);
+    red_put(r, idx, slot, t);
   }
+}
+// slot of block (blockIdx.x, blockIdx.y) of a (chunks, B * per) grid: one per (b, chunk)
+__device__ __forceinline__ uint32_t chunk_slot(int per) {
+  return (uint32_t)(blockIdx.y / per) * gridDim.x + blockIdx.x;
 }
 
 __device__ __forceinline__ bool inside_e(int e, int r, int c, int H, int W) {
@@ -228,7 +236,7 @@ __global__ __launch_bounds__(NT) void padj2_kernel(const float* __restrict__ x1,
 template <int mode>
 __global__ __launch_bounds__(NT) void tapgrad_kernel(const float* __restrict__ u, const float* __restrict__ z,
                                                      const float* __restrict__ scale,
-                                                     float* __restrict__ gt, int C, int F, int H, int W) {
+                                                     Red gt, int C, int F, int H, int W) {
   const int HW = H * W;
   const int plane = blockIdx.y, ch = plane % C;
   const float* up = u + (int64_t)plane * HW;
@@ -250,7 +258,7 @@ __global__ __launch_bounds__(NT) void tapgrad_kernel(const float* __restrict__ u
   }
   const float sc = scale ? scale[ch / F] : 1.f;
 #pragma unroll
-  for (int t = 0; t < 5; ++t) block_atomic_add(gt + ch * 5 + t, sc * acc[t]);
+  for (int t = 0; t < 5; ++t) block_red_put(gt, ch * 5 + t, chunk_slot(C), sc * acc[t]);
 }
 
 // ---------------------------------------------------------------------------
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(NT) void glr_bwd_kernel(const float* __restrict__ s
                                                      const float* __restrict__ w, const float* __restrict__ scale,
                                                      float coef, float* __restrict__ z_out,
                                                      float* __restrict__ ap_out, float* __restrict__ gw,
-                                                     float* __restrict__ gdot, int G, int F, int H, int W) {
+                                                     Red gdot, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G;
   float dot = 0.f;
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(NT) void glr_bwd_kernel(const float* __restrict__ s
 #pragma unroll
     for (int e = 0; e < 4; ++e) gwb[e * HW] += sc * gwa[e];
   }
-  if (gdot) block_atomic_add(gdot + g, coef * dot);
+  if (gdot.p) block_red_put(gdot, g, chunk_slot(G), coef * dot);
 }
 
 // Pair-Laplacian reverse (GTV C^T C, linear part).  K s(p) = sum over the 4 incident edges
@@ -319,7 +327,7 @@ __global__ __launch_bounds__(NT) void pair_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ cw, const float* __restrict__ scale,
                                                       float coef, float* __restrict__ z_out,
                                                       float* __restrict__ ap_out, float* __restrict__ gc,
-                                                      float* __restrict__ gdot, int G, int F, int H, int W) {
+                                                      Red gdot, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G;
   float dot = 0.f;
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(NT) void pair_bwd_kernel(const float* __restrict__ 
     if (hr) gcb[0] += sc * gh;
     if (vd) gcb[HW] += sc * gv;
   }
-  if (gdot) block_atomic_add(gdot + g, coef * dot);
+  if (gdot.p) block_red_put(gdot, g, chunk_slot(G), coef * dot);
 }
 
 // ---------------------------------------------------------------------------
@@ -371,8 +379,8 @@ __global__ __launch_bounds__(NT) void prox_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ log_gamma,
                                                       const float* __restrict__ scale, float coef,
                                                       float* __restrict__ o_out, float* __restrict__ gs_out,
-                                                      float* __restrict__ gw, float* __restrict__ ggam,
-                                                      float* __restrict__ gdot, int G, int F, int H, int W) {
+                                                      float* __restrict__ gw, Red ggam,
+                                                      Red gdot, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G;
   float dot = 0.f, dgam = 0.f;
@@ -437,8 +445,8 @@ __global__ __launch_bounds__(NT) void prox_bwd_kernel(const float* __restrict__ 
     for (int e = 0; e < 4; ++e) gwb[e * HW] += sc * gwa[e];
   }
   dgam *= scale ? scale[g] : 1.f;
-  if (gdot) block_atomic_add(gdot + g, coef * dot);
-  if (ggam) block_atomic_add(ggam + g, dgam);
+  if (gdot.p) block_red_put(gdot, g, chunk_slot(G), coef * dot);
+  if (ggam.p) block_red_put(ggam, g, chunk_slot(G), dgam);
 }
 
 // c[0](p) = w_right(p)^2 + w_left(p+1)^2, c[1](p) = w_down(p)^2 + w_up(p+W)^2 (0 at the frame):
@@ -489,7 +497,7 @@ __global__ __launch_bounds__(NT) void edge_weights_bwd_kernel(const float* __res
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ gw,
                                                               float* __restrict__ gfeat, int64_t gstride,
-                                                              float* __restrict__ gM, int G, int F, int H, int W) {
+                                                              Red gM, int G, int F, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, g = bg % G, b = bg / G;
   const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW;
@@ -551,7 +559,7 @@ __global__ __launch_bounds__(NT) void edge_weights_bwd_kernel(const float* __res
       gfp[(int64_t)f * HW + p] = small ? gn * ic : (gn - n * ndg) * ic;
     }
   }
-  for (int f = 0; f < F; ++f) block_atomic_add(gM + g * F + f, gm_sm[f * NT + threadIdx.x]);
+  for (int f = 0; f < F; ++f) block_red_put(gM, g * F + f, chunk_slot(G), gm_sm[f * NT + threadIdx.x]);
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -559,7 +567,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // gdot[g] += coef * sum_{b,f,p} u v.      grid (chunks, B*G); V4: float4 loads (n % 4 == 0, aligned)
 template <bool V4>
 __global__ __launch_bounds__(NT) void graph_dot_kernel(const float* __restrict__ u, const float* __restrict__ v,
-                                                       float coef, float* __restrict__ gdot, int G, int F,
+                                                       float coef, Red gdot, int G, int F,
                                                        int64_t HW) {
   const int bg = blockIdx.y, g = bg % G;
   const int64_t n = (int64_t)F * HW;
@@ -574,7 +582,7 @@ __global__ __launch_bounds__(NT) void graph_dot_kernel(const float* __restrict__
   } else {
     for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) acc += up[i] * vp[i];
   }
-  block_atomic_add(gdot + g, coef * acc);
+  block_red_put(gdot, g, chunk_slot(G), coef * acc);
 }
 
 // out = sa[g] * x + sb[g] * y  (sa/sb NULL -> 1; y NULL -> term dropped); acc: out += ...
@@ -613,8 +621,8 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
                                                      const float* __restrict__ gun, const float* __restrict__ up,
                                                      const float* __restrict__ alpha,
                                                      const float* __restrict__ beta_next, float* __restrict__ gu_out,
-                                                     float* __restrict__ gbb, float* gx_out, float* __restrict__ galpha,
-                                                     float* __restrict__ gbeta, int G, int64_t n) {
+                                                     float* __restrict__ gbb, float* gx_out, Red galpha,
+                                                     Red gbeta, int G, int64_t n) {
   const int bg = blockIdx.y, g = bg % G;
   const int64_t base = (int64_t)bg * n;
   const float al = alpha[g], be = gun ? beta_next[g] : 0.f;
@@ -649,8 +657,8 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
       gx_out[o] = x - gu;
     }
   }
-  block_atomic_add(galpha + g, da);
-  if (up) block_atomic_add(gbeta + g, db);
+  block_red_put(galpha, g, chunk_slot(G), da);
+  if (up) block_red_put(gbeta, g, chunk_slot(G), db);
 }
 
 // out(q) += 0.25 * xd(q / 2)   (U = conv_transpose2d of the 0.25 2x2 kernel, stride 2; REF:676-679)
@@ -736,8 +744,8 @@ template <int MODE, int F>
 __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
-    float* __restrict__ v_out, float* __restrict__ gw, float* __restrict__ ggam, float* __restrict__ gdot,
-    float* __restrict__ gtaps, int G, int H, int W) {
+    float* __restrict__ v_out, float* __restrict__ gw, Red ggam, Red gdot,
+    Red gtaps, int G, int H, int W) {
   const int HW = H * W;
   const int bg = blockIdx.y, gi = bg % G;
   const float sc = scale ? scale[gi] : 1.f;
@@ -872,14 +880,15 @@ __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
       for (int e = 0; e < 4; ++e) gwb[e * HW + p] += sc * gwa[e];
     }
   }
-  if (gdot) block_atomic_add(gdot + gi, coef * dot);
+  const uint32_t slot = chunk_slot(G);
+  if (gdot.p) block_red_put(gdot, gi, slot, coef * dot);
   if constexpr (MODE == 2) {
-    if (ggam) block_atomic_add(ggam + gi, sc * dgam);
+    if (ggam.p) block_red_put(ggam, gi, slot, sc * dgam);
   }
 #pragma unroll
   for (int f = 0; f < F; ++f)
 #pragma unroll
-    for (int t = 0; t < 5; ++t) block_atomic_add(gtaps + (gi * F + f) * 5 + t, sc * (accT[f][t] + accP[f][t]));
+    for (int t = 0; t < 5; ++t) block_red_put(gtaps, (gi * F + f) * 5 + t, slot, sc * (accT[f][t] + accP[f][t]));
 }
 
 // ---------------------------------------------------------------------------
@@ -940,8 +949,8 @@ template <int MODE, int V, bool STRIPS = false>
 __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
-    float* __restrict__ v_out, float* __restrict__ gw, float* __restrict__ ggam, float* __restrict__ gdot,
-    float* __restrict__ gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
+    float* __restrict__ v_out, float* __restrict__ gw, Red ggam, Red gdot,
+    Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
   // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats)
   extern __shared__ __attribute__((aligned(16))) float part_dyn[];
@@ -1203,19 +1212,21 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     }
     par ^= 1;
   }
-  // per-graph / per-channel reductions: wave sums, one atomic per value and wave
+  // per-graph / per-channel reductions: wave sums into this wave's slots.  Slot of the workgroup:
+  // (b, segment, strip); the per-graph scalars take one slot per channel wave of it.
+  const uint32_t wslot = ((uint32_t)(bg / G) * nsegs + seg) * nstrips + strip;
   {
     const float d = wave_sum(dot);
-    if (lane == 0 && gdot && d != 0.f) atomicAdd(gdot + gi, coef * d);
+    if (lane == 0) red_put(gdot, gi, wslot * F + f, coef * d);
   }
   if constexpr (MODE == 2) {
     const float d = wave_sum(dgam);
-    if (lane == 0 && ggam && d != 0.f) atomicAdd(ggam + gi, sc * d);
+    if (lane == 0) red_put(ggam, gi, wslot * F + f, sc * d);
   }
 #pragma unroll
   for (int tt = 0; tt < 5; ++tt) {
     const float d = wave_sum(accT[tt] + accP[tt]);
-    if (lane == 0 && d != 0.f) atomicAdd(gtaps + (gi * F + f) * 5 + tt, sc * d);
+    if (lane == 0) red_put(gtaps, (gi * F + f) * 5 + tt, wslot, sc * d);
   }
 }
 
@@ -1237,7 +1248,7 @@ __global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restric
                                                           const float* __restrict__ multiM,
                                                           const float* __restrict__ w, const float* __restrict__ gw,
                                                           float* __restrict__ gfeat, int64_t gstride,
-                                                          float* __restrict__ gM, int G, int H, int W, int sseg,
+                                                          Red gM, int G, int H, int W, int sseg,
                                                           int nsegs, uint32_t nwaves) {
   const int lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
@@ -1245,10 +1256,10 @@ __global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restric
   // STRIPS (W > 64 V): 62 V owned columns per wave with V halo columns per side (reach: one column),
   // as term_row_kernel
   uint32_t unit = wid;
-  int strip = 0;
+  int strip = 0, nstrips = 1;
   constexpr int STEP = 62 * V;
   if constexpr (STRIPS) {
-    const int nstrips = (W + STEP - 1) / STEP;
+    nstrips = (W + STEP - 1) / STEP;
     strip = (int)(unit % (uint32_t)nstrips);
     unit /= (uint32_t)nstrips;
   }
@@ -1381,21 +1392,29 @@ __global__ __launch_bounds__(NT) void edge_row_bwd_kernel(const float* __restric
       for (int f = 0; f < F; ++f) rstore<V>(gfp + f * HW + (int64_t)r * W, gout[f]);
     }
   }
+  const uint32_t wslot = ((uint32_t)b * nsegs + seg) * nstrips + strip;   // (b, segment, strip)
 #pragma unroll
   for (int f = 0; f < F; ++f) {
     const float s = wave_sum(gm[f]);
-    if (lane == 0 && s != 0.f) atomicAdd(gM + g * F + f, s);
+    if (lane == 0) red_put(gM, g * F + f, wslot, s);
   }
 }
 
-bool launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM, const float* w, const float* gw,
-                         float* gfeat, int64_t gstride, float* gM, int B, int G, int F, int H, int W, hipStream_t s) {
+bool edge_row_bwd_ok(const float* feat, int64_t fstride, const float* w, const float* gw, float* gfeat,
+                     int64_t gstride, int F, int H, int W) {
   const int V = term_strip_vec(W);
   if (V == 0) return false;
   if (fstride % V != 0 || gstride % V != 0 || ((int64_t)H * W) % V != 0) return false;
   const void* ptrs[] = {feat, w, gw, gfeat};
   for (const void* p : ptrs)
     if ((uintptr_t)p % (4u * V) != 0) return false;
+  return F == 1 || F == 2 || F == 3 || F == 4 || F == 6;
+}
+// launches edge_row_bwd_kernel (edge_row_bwd_ok() holds); gM's partials: one slot per wave
+grr_status launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM, const float* w,
+                               const float* gw, float* gfeat, int64_t gstride, float* gMd, int B, int G, int F, int H,
+                               int W, hipStream_t s) {
+  const int V = term_strip_vec(W);
   const int nstrips = W <= 64 * V ? 1 : (W + 62 * V - 1) / (62 * V);
   const int64_t planes = (int64_t)B * G * nstrips;   // (b, graph, strip) units
   int sseg = H;
@@ -1403,6 +1422,11 @@ bool launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+  RedScratch rs(s);
+  const int im = rs.plan(gMd, G * F, (uint32_t)((int64_t)B * nsegs * nstrips));
+  grr_status st = rs.alloc("grr_bwd_edge_weights");
+  if (st != GRR_OK) return st;
+  const Red gM = rs.red(im);
 #define GRR_EDGE_BWD_CASE(FF, VV)                                                                              \
   if (F == FF && V == VV) {                                                                                    \
     if (nstrips > 1)                                                                                           \
@@ -1411,20 +1435,36 @@ bool launch_edge_row_bwd(const float* feat, int64_t fstride, const float* multiM
     else                                                                                                       \
       hipLaunchKernelGGL((edge_row_bwd_kernel<FF, VV, false>), grid, dim3(NT), 0, s, feat, fstride, multiM, w, gw, \
                          gfeat, gstride, gM, G, H, W, sseg, nsegs, nwaves);                                    \
-    return true;                                                                                               \
   }
   GRR_EDGE_BWD_CASE(1, 4) GRR_EDGE_BWD_CASE(2, 4) GRR_EDGE_BWD_CASE(3, 4) GRR_EDGE_BWD_CASE(4, 4)
   GRR_EDGE_BWD_CASE(6, 4) GRR_EDGE_BWD_CASE(1, 2) GRR_EDGE_BWD_CASE(2, 2) GRR_EDGE_BWD_CASE(3, 2)
   GRR_EDGE_BWD_CASE(4, 2) GRR_EDGE_BWD_CASE(6, 2) GRR_EDGE_BWD_CASE(1, 1) GRR_EDGE_BWD_CASE(2, 1)
   GRR_EDGE_BWD_CASE(3, 1) GRR_EDGE_BWD_CASE(4, 1) GRR_EDGE_BWD_CASE(6, 1)
 #undef GRR_EDGE_BWD_CASE
-  return false;
+  st = launch_status("grr_bwd_edge_weights");
+  if (st != GRR_OK) return st;
+  return rs.finish("grr_bwd_edge_weights");
 }
 
+// The term reverse's three reductions (gdot, ggamma: per graph; gtaps: per channel and tap), planned
+// and allocated once the launch geometry is known
+struct TermReds {
+  RedScratch rs;
+  int id = 0, ig = 0, it = 0;
+  explicit TermReds(hipStream_t s) : rs(s) {}
+  grr_status setup(int mode, float* gdot, float* ggam, float* gtaps, int G, int F, uint32_t slots_scalar,
+                   uint32_t slots_taps) {
+    id = rs.plan(gdot, G, slots_scalar);
+    ig = rs.plan(mode == 2 ? ggam : nullptr, G, slots_scalar);
+    it = rs.plan(gtaps, G * F * 5, slots_taps);
+    return rs.alloc("grr_bwd_term_fused");
+  }
+};
+
 template <int MODE, int V>
-void launch_term_row(int B, int F, const float* x, const float* g, const float* taps, const float* w, const float* lg,
-                     const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot, float* gtaps,
-                     int G, int H, int W, hipStream_t s) {
+grr_status launch_term_row(int B, int F, const float* x, const float* g, const float* taps, const float* w,
+                           const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam,
+                           float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
   // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
   int sseg = H;
   const int nstrips = W <= 64 * V ? 1 : (W + 62 * V - 1) / (62 * V);
@@ -1433,34 +1473,45 @@ void launch_term_row(int B, int F, const float* x, const float* g, const float* 
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
   const size_t lds = (size_t)2 * F * (MODE == 1 ? 2 : 4) * 64 * V * sizeof(float);
+  // slots: one per (b, segment, strip) workgroup for the taps, one per channel wave of it for the
+  // per-graph scalars
+  const uint32_t wgs = (uint32_t)((int64_t)B * nsegs * nstrips);
+  TermReds R(s);
+  grr_status st = R.setup(MODE, gdot, ggam, gtaps, G, F, wgs * F, wgs);
+  if (st != GRR_OK) return st;
   if (nstrips > 1)
     hipLaunchKernelGGL((term_row_kernel<MODE, V, true>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale,
-                       coef, v, gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
+                       coef, v, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg, nsegs, nblk);
   else
     hipLaunchKernelGGL((term_row_kernel<MODE, V, false>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale,
-                       coef, v, gw, ggam, gdot, gtaps, G, F, H, W, sseg, nsegs, nblk);
+                       coef, v, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg, nsegs, nblk);
+  st = launch_status("grr_bwd_term_fused");
+  if (st != GRR_OK) return st;
+  return R.rs.finish("grr_bwd_term_fused");
 }
-template <int MODE>
-bool launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
-                       const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam, float* gdot,
-                       float* gtaps, int G, int H, int W, hipStream_t s) {
+bool term_row_ok(int F, const float* x, const float* g, const float* w, const float* v, const float* gw, int W) {
   const int V = term_strip_vec(W);
   if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return false;
   const void* ptrs[] = {x, g, w, v, gw};
   for (const void* p : ptrs)
     if ((uintptr_t)p % (4u * V) != 0) return false;
-  switch (V) {
-    case 1: launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s); break;
-    case 2: launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s); break;
-    default: launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
-  }
   return true;
+}
+template <int MODE>
+grr_status launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
+                             const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam,
+                             float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
+  switch (term_strip_vec(W)) {
+    case 1: return launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
+    case 2: return launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
+    default: return launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
+  }
 }
 
 template <int MODE>
 bool launch_term_fused(int F, dim3 grid, hipStream_t s, const float* x, const float* g, const float* taps,
                        const float* w, const float* lg, const float* scale, float coef, float* v, float* gw,
-                       float* ggam, float* gdot, float* gtaps, int G, int H, int W) {
+                       Red ggam, Red gdot, Red gtaps, int G, int H, int W) {
 #define GRR_TERM_CASE(FF)                                                                                      \
   case FF:                                                                                                     \
     hipLaunchKernelGGL((term_bwd_fused_kernel<MODE, FF>), grid, dim3(NT), 0, s, x, g, taps, w, lg, scale, coef, \
@@ -1485,7 +1536,95 @@ int chunks_for(int64_t n, int64_t planes) {
 }
 int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
 
+// dst[i] += sum_s part[i][s], slots in order: lane l adds slots l, l + 64, ... in order, then the
+// fixed shuffle tree.   grid (n), one wave per value
+__global__ __launch_bounds__(64) void red_finish_kernel(const float* __restrict__ part, uint32_t nslot,
+                                                        float* __restrict__ dst) {
+  const float* row = part + (size_t)blockIdx.x * nslot;
+  float v = 0.f;
+  for (uint32_t s = threadIdx.x; s < nslot; s += 64) v += row[s];
+  v = wave_sum(v);
+  if (threadIdx.x == 0) dst[blockIdx.x] += v;
+}
+
 }  // namespace
+
+// ---- RedScratch (grr_common.h) ---------------------------------------------
+namespace {
+// the default pool keeps freed blocks (release threshold: unbounded), once per device
+bool pool_ready[64];
+std::mutex pool_mu;
+grr_status prepare_pool() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return GRR_ERR_HIP;
+  std::lock_guard<std::mutex> lk(pool_mu);
+  if (pool_ready[dev]) return GRR_OK;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return GRR_ERR_HIP;
+  uint64_t thr = ~0ull;
+  if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) != hipSuccess) return GRR_ERR_HIP;
+  pool_ready[dev] = true;
+  return GRR_OK;
+}
+}  // namespace
+
+int RedScratch::plan(float* dst, int n, uint32_t nslot) {
+  const int i = k_++;
+  dst_[i] = dst;
+  n_[i] = n;
+  nslot_[i] = nslot < 1 ? 1 : nslot;
+  return i;
+}
+
+grr_status RedScratch::alloc(const char* what) {
+  size_t total = 0;
+  for (int i = 0; i < k_; ++i)
+    if (dst_[i]) total += (size_t)n_[i] * nslot_[i];
+  if (total == 0) return GRR_OK;
+  if (prepare_pool() != GRR_OK) {
+    set_error("%s: reduction scratch pool unavailable", what);
+    return GRR_ERR_HIP;
+  }
+  hipError_t e = hipMallocAsync(&base_, total * sizeof(float), s_);
+  if (e != hipSuccess) {
+    base_ = nullptr;
+    set_error("%s: reduction scratch (%zu floats): %s", what, total, hipGetErrorString(e));
+    return GRR_ERR_HIP;
+  }
+  float* p = static_cast<float*>(base_);
+  for (int i = 0; i < k_; ++i)
+    if (dst_[i]) {
+      part_[i] = p;
+      p += (size_t)n_[i] * nslot_[i];
+    }
+  e = hipMemsetAsync(base_, 0, total * sizeof(float), s_);
+  if (e != hipSuccess) {
+    set_error("%s: reduction scratch fill: %s", what, hipGetErrorString(e));
+    return GRR_ERR_HIP;
+  }
+  return GRR_OK;
+}
+
+grr_status RedScratch::finish(const char* what) {
+  for (int i = 0; i < k_; ++i)
+    if (dst_[i] && part_[i] && n_[i] > 0)
+      hipLaunchKernelGGL(red_finish_kernel, dim3(n_[i]), dim3(64), 0, s_, part_[i], nslot_[i], dst_[i]);
+  grr_status st = launch_status(what);
+  if (base_) {
+    const hipError_t e = hipFreeAsync(base_, s_);
+    base_ = nullptr;
+    if (e != hipSuccess && st == GRR_OK) {
+      set_error("%s: reduction scratch free: %s", what, hipGetErrorString(e));
+      st = GRR_ERR_HIP;
+    }
+  }
+  return st;
+}
+
+RedScratch::~RedScratch() {
+  if (base_) (void)hipFreeAsync(base_, s_);   // an error path before finish(): nothing was added
+}
+
 }  // namespace grr
 
 using namespace grr;
@@ -1508,26 +1647,32 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
                   mode >= 0 && mode <= 2 && (mode != 2 || log_gamma),
               GRR_ERR_INVALID_ARG, "grr_bwd_term_fused: bad args");
   hipStream_t s = (hipStream_t)stream;
-  if (g_term_rows && (int64_t)B * G * H < (1ll << 31)) {   // row-streaming kernel where the width allows (W <= 256)
-    bool rows = false;
+  // row-streaming kernel where the shape allows
+  if (g_term_rows && (int64_t)B * G * H < (1ll << 31) && term_row_ok(F, x, g, w, v_out, gw, W)) {
     switch (mode) {
-      case 0: rows = launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s); break;
-      case 1: rows = launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s); break;
-      default: rows = launch_term_row_v<2>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
+      case 0: return launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
+      case 1: return launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
+      default: return launch_term_row_v<2>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
     }
-    if (rows) return launch_status("grr_bwd_term_fused");
   }
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: B*G > 65535");
-  const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G), B * G);
-  bool ok = false;
-  switch (mode) {
-    case 0: ok = launch_term_fused<0>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W); break;
-    case 1: ok = launch_term_fused<1>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W); break;
-    default: ok = launch_term_fused<2>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W);
-  }
-  GRR_REQUIRE(ok, GRR_ERR_UNSUPPORTED,
+  GRR_REQUIRE(F >= 1 && F <= 4, GRR_ERR_UNSUPPORTED,
               "grr_bwd_term_fused: F=%d needs the row kernel (W <= 256 with W %% V == 0, F <= 12 / 16) or F <= 4", F);
-  return launch_status("grr_bwd_term_fused");
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * G);
+  const dim3 grid(chunks, B * G);
+  TermReds R(s);
+  const uint32_t slots = (uint32_t)B * chunks;   // one per (b, chunk) workgroup
+  grr_status st = R.setup(mode, gdot, ggamma, gtaps, G, F, slots, slots);
+  if (st != GRR_OK) return st;
+  const Red rg = R.rs.red(R.ig), rd = R.rs.red(R.id), rt = R.rs.red(R.it);
+  switch (mode) {
+    case 0: launch_term_fused<0>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, rg, rd, rt, G, H, W); break;
+    case 1: launch_term_fused<1>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, rg, rd, rt, G, H, W); break;
+    default: launch_term_fused<2>(F, grid, s, x, g, taps, w, log_gamma, scale, coef, v_out, gw, rg, rd, rt, G, H, W);
+  }
+  st = launch_status("grr_bwd_term_fused");
+  if (st != GRR_OK) return st;
+  return R.rs.finish("grr_bwd_term_fused");
 }
 
 grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,
@@ -1581,12 +1726,18 @@ grr_status grr_bwd_tapgrad(const float* u, const float* z, int mode, const float
   GRR_REQUIRE(u && z && gtaps && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 && (mode == 0 || mode == 1),
               GRR_ERR_INVALID_ARG, "grr_bwd_tapgrad: bad args");
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_tapgrad: B*G*F > 65535");
-  const dim3 grid(chunks_for((int64_t)H * W, (int64_t)B * G * F), B * G * F);
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * G * F);
+  const dim3 grid(chunks, B * G * F);
+  RedScratch rs((hipStream_t)stream);
+  const int it = rs.plan(gtaps, G * F * 5, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_tapgrad");
+  if (st != GRR_OK) return st;
   if (mode == 0)
-    hipLaunchKernelGGL(tapgrad_kernel<0>, grid, dim3(NT), 0, (hipStream_t)stream, u, z, scale, gtaps, G * F, F, H, W);
+    hipLaunchKernelGGL(tapgrad_kernel<0>, grid, dim3(NT), 0, (hipStream_t)stream, u, z, scale, rs.red(it), G * F, F, H, W);
   else
-    hipLaunchKernelGGL(tapgrad_kernel<1>, grid, dim3(NT), 0, (hipStream_t)stream, u, z, scale, gtaps, G * F, F, H, W);
-  return launch_status("grr_bwd_tapgrad");
+    hipLaunchKernelGGL(tapgrad_kernel<1>, grid, dim3(NT), 0, (hipStream_t)stream, u, z, scale, rs.red(it), G * F, F, H, W);
+  st = launch_status("grr_bwd_tapgrad");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_tapgrad");
 }
 
 grr_status grr_bwd_glr(const float* s, const float* a, const float* w, const float* scale, float coef, float* z_out,
@@ -1595,9 +1746,15 @@ grr_status grr_bwd_glr(const float* s, const float* a, const float* w, const flo
   GRR_REQUIRE(s && a && w && z_out && ap_out && gw && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_glr: bad args");
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_glr: B*G*F > 65535");
-  hipLaunchKernelGGL(glr_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
-                     scale, coef, z_out, ap_out, gw, gdot, G, F, H, W);
-  return launch_status("grr_bwd_glr");
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int id = rs.plan(gdot, G, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_glr");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(glr_bwd_kernel, dim3(chunks, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w, scale, coef,
+                     z_out, ap_out, gw, rs.red(id), G, F, H, W);
+  st = launch_status("grr_bwd_glr");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_glr");
 }
 
 grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const float* scale, float coef, float* z_out,
@@ -1606,9 +1763,15 @@ grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const fl
   GRR_REQUIRE(s && a && c && z_out && ap_out && gc && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_pair: bad args");
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_pair: B*G*F > 65535");
-  hipLaunchKernelGGL(pair_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream, s, a, c,
-                     scale, coef, z_out, ap_out, gc, gdot, G, F, H, W);
-  return launch_status("grr_bwd_pair");
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int id = rs.plan(gdot, G, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_pair");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(pair_bwd_kernel, dim3(chunks, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, c, scale, coef,
+                     z_out, ap_out, gc, rs.red(id), G, F, H, W);
+  st = launch_status("grr_bwd_pair");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_pair");
 }
 
 grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const float* log_gamma, const float* scale,
@@ -1618,9 +1781,15 @@ grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const fl
   GRR_REQUIRE(s && a && w && log_gamma && o_out && gs_out && gw && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_prox: bad args");
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_prox: B*G*F > 65535");
-  hipLaunchKernelGGL(prox_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w,
-                     log_gamma, scale, coef, o_out, gs_out, gw, ggamma, gdot, G, F, H, W);
-  return launch_status("grr_bwd_prox");
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int ig = rs.plan(ggamma, G, (uint32_t)B * chunks), id = rs.plan(gdot, G, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_prox");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(prox_bwd_kernel, dim3(chunks, B * G), dim3(NT), 0, (hipStream_t)stream, s, a, w, log_gamma, scale,
+                     coef, o_out, gs_out, gw, rs.red(ig), rs.red(id), G, F, H, W);
+  st = launch_status("grr_bwd_prox");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_prox");
 }
 
 grr_status grr_bwd_pair_weights(const float* w, const float* gc, float* gw, int B, int G, int H, int W, void* stream) {
@@ -1640,14 +1809,19 @@ grr_status grr_bwd_edge_weights(const float* feat, int64_t feat_bstride, const f
   GRR_REQUIRE(feat && multiM && w && gw && gfeat && gmultiM && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_bwd_edge_weights: bad args");
   GRR_REQUIRE(F <= GRR_MAX_NODE_FTS, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: F=%d > %d", F, GRR_MAX_NODE_FTS);
-  if (g_term_rows && launch_edge_row_bwd(feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, B, G, F,
-                                         H, W, (hipStream_t)stream))
-    return launch_status("grr_bwd_edge_weights");
+  if (g_term_rows && edge_row_bwd_ok(feat, feat_bstride, w, gw, gfeat, gfeat_bstride, F, H, W))
+    return launch_edge_row_bwd(feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, B, G, F, H, W,
+                               (hipStream_t)stream);
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_edge_weights: B*G*F > 65535");
-  hipLaunchKernelGGL(edge_weights_bwd_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * G), B * G), dim3(NT), 0,
-                     (hipStream_t)stream, feat, feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, gmultiM, G, F, H,
-                     W);
-  return launch_status("grr_bwd_edge_weights");
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int im = rs.plan(gmultiM, G * F, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_edge_weights");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(edge_weights_bwd_kernel, dim3(chunks, B * G), dim3(NT), 0, (hipStream_t)stream, feat,
+                     feat_bstride, multiM, w, gw, gfeat, gfeat_bstride, rs.red(im), G, F, H, W);
+  st = launch_status("grr_bwd_edge_weights");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_edge_weights");
 }
 
 grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* gdot, int B, int G, int F, int H,
@@ -1658,14 +1832,20 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   GRR_REQUIRE((int64_t)B * G * F <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_graph_dot: B*G*F > 65535");
   const int64_t n = (int64_t)F * H * W;
   const bool v4 = n % 4 == 0 && ((uintptr_t)u & 15) == 0 && ((uintptr_t)v & 15) == 0;
-  const dim3 grid(chunks_for(v4 ? n / 4 : n, (int64_t)B * G), B * G);
+  const int chunks = chunks_for(v4 ? n / 4 : n, (int64_t)B * G);
+  const dim3 grid(chunks, B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int id = rs.plan(gdot, G, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_graph_dot");
+  if (st != GRR_OK) return st;
   if (v4)
-    hipLaunchKernelGGL(graph_dot_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, u, v, coef, gdot, G, F,
+    hipLaunchKernelGGL(graph_dot_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, u, v, coef, rs.red(id), G, F,
                        (int64_t)H * W);
   else
-    hipLaunchKernelGGL(graph_dot_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, u, v, coef, gdot, G, F,
+    hipLaunchKernelGGL(graph_dot_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, u, v, coef, rs.red(id), G, F,
                        (int64_t)H * W);
-  return launch_status("grr_bwd_graph_dot");
+  st = launch_status("grr_bwd_graph_dot");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_graph_dot");
 }
 
 grr_status grr_bwd_cg_glue(const float* gx, const float* u, const float* gu_next, const float* u_prev,
@@ -1680,14 +1860,20 @@ grr_status grr_bwd_cg_glue(const float* gx, const float* u, const float* gu_next
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   const bool v4 = n % 4 == 0 && al16(gx) && al16(u) && al16(gu) && al16(gx_out) && (!gu_next || al16(gu_next)) &&
                   (!u_prev || al16(u_prev)) && (!gbb || al16(gbb));
-  const dim3 grid(chunks_for(v4 ? n / 4 : n, (int64_t)B * G), B * G);
+  const int chunks = chunks_for(v4 ? n / 4 : n, (int64_t)B * G);
+  const dim3 grid(chunks, B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int ia = rs.plan(galpha, G, (uint32_t)B * chunks), ib = rs.plan(u_prev ? gbeta : nullptr, G, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_bwd_cg_glue");
+  if (st != GRR_OK) return st;
   if (v4)
     hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, u, gu_next, u_prev, alpha,
-                       beta_next, gu, gbb, gx_out, galpha, gbeta, G, n);
+                       beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n);
   else
     hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, u, gu_next, u_prev, alpha,
-                       beta_next, gu, gbb, gx_out, galpha, gbeta, G, n);
-  return launch_status("grr_bwd_cg_glue");
+                       beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n);
+  st = launch_status("grr_bwd_cg_glue");
+  return st != GRR_OK ? st : rs.finish("grr_bwd_cg_glue");
 }
 
 grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,

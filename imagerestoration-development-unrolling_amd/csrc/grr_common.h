@@ -52,4 +52,46 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// ---------------------------------------------------------------------------
+// Fixed-order reductions of the training reverse (per-graph scalars, stencil / depthwise taps,
+// multiM): no float atomics.  A reduced value idx has one partial slot per contributor (a wave or
+// a workgroup of the launch) in a scratch array [n][nslot]; each contributor stores its partial
+// into its own slot, and red_finish_kernel then adds each row, in slot order, to the destination
+// (dst[idx] += sum).  The result is the same on every run, whatever the schedule or the stream
+// interleaving.
+// ---------------------------------------------------------------------------
+struct Red {
+  float* p;          // [n][nslot] partials; nullptr: the value is not wanted
+  uint32_t nslot;
+};
+__device__ __forceinline__ void red_put(const Red& r, int idx, uint32_t slot, float v) {
+  if (r.p) r.p[(size_t)idx * r.nslot + slot] = v;
+}
+
+// Host side: the partial arrays of one launch, carved from one stream-ordered allocation
+// (hipMallocAsync from the device's default pool, whose release threshold is raised once, so the
+// steady state reuses pool memory; capturable in a HIP graph), zero-filled, then finished and freed
+// on the same stream.
+class RedScratch {
+ public:
+  static constexpr int kMax = 4;
+  explicit RedScratch(hipStream_t s) : s_(s) {}
+  RedScratch(const RedScratch&) = delete;
+  RedScratch& operator=(const RedScratch&) = delete;
+  ~RedScratch();
+  int plan(float* dst, int n, uint32_t nslot);   // before alloc(); dst == nullptr: not wanted
+  grr_status alloc(const char* what);
+  Red red(int i) const { return Red{dst_[i] ? part_[i] : nullptr, nslot_[i]}; }
+  grr_status finish(const char* what);            // dst[idx] += sum over slots; frees the scratch
+
+ private:
+  hipStream_t s_;
+  int k_ = 0;
+  float* dst_[kMax] = {};
+  float* part_[kMax] = {};
+  int n_[kMax] = {};
+  uint32_t nslot_[kMax] = {};
+  void* base_ = nullptr;
+};
+
 }  // namespace grr

@@ -24,7 +24,9 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ void block_atomic_add(float* dst, float v) {
+// one partial per block (grr_common.h, fixed-order reductions): wave sums -> LDS -> thread 0 adds
+// them in wave order and stores the block's slot
+__device__ __forceinline__ void block_red_put(const Red& r, int idx, uint32_t slot, float v) {
   __shared__ float red[NT / 64];
   v = wave_sum(v);
   __syncthreads();
@@ -34,8 +36,12 @@ __device__ __forceinline__ void block_atomic_add(float* dst, float v) {
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < NT / 64; ++i) t += red[i];
-    if (t != 0.f) atomicAdd(dst, t);
+    red_put(r, idx, slot, t);
   }
+}
+// slot of block (blockIdx.x, blockIdx.y) of a (chunks, B * per) grid: one per (b, chunk)
+__device__ __forceinline__ uint32_t chunk_slot(int per) {
+  return (uint32_t)(blockIdx.y / per) * gridDim.x + blockIdx.x;
 }
 
 // n = ln_w x isd, isd per pixel.   grid-stride over B*P pixels
@@ -91,8 +97,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const float* __restrict__ x,
 
 // gw[c] += sum_{b,p} u v isd(b,p)          grid (chunks, B*C)
 __global__ __launch_bounds__(NT) void ln_wgrad_kernel(const float* __restrict__ u, const float* __restrict__ v,
-                                                      const float* __restrict__ isd, float* __restrict__ gw, int C,
-                                                      int64_t P) {
+                                                      const float* __restrict__ isd, Red gw, int C, int64_t P) {
   const int plane = blockIdx.y, c = plane % C, b = plane / C;
   const float* up = u + (int64_t)plane * P;
   const float* vp = v + (int64_t)plane * P;
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(NT) void ln_wgrad_kernel(const float* __restrict__ 
   float acc = 0.f;
   for (int64_t p = blockIdx.x * (int64_t)NT + threadIdx.x; p < P; p += (int64_t)gridDim.x * NT)
     acc += up[p] * vp[p] * sp[p];
-  block_atomic_add(gw + c, acc);
+  block_red_put(gw, c, chunk_slot(C), acc);
 }
 
 // h'(p) = sum_t w_t h(clamp(p + t)), t = (dy, dx) in {-1,0,1}^2, tap index (dy+1)*3 + dx+1
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(NT) void dw3_bwd_data_kernel(const float* __restric
 
 // gw[c, t] += sum_{b,p} g(p) h(clamp(p + t))        grid (chunks, B*C)
 __global__ __launch_bounds__(NT) void dw3_wgrad_kernel(const float* __restrict__ g, const float* __restrict__ h,
-                                                       float* __restrict__ gw, int C, int H, int W) {
+                                                       Red gw, int C, int H, int W) {
   const int HW = H * W;
   const int plane = blockIdx.y, c = plane % C;
   const float* gp = g + (int64_t)plane * HW;
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(NT) void dw3_wgrad_kernel(const float* __restrict__
         acc[(dy + 1) * 3 + dx + 1] += gv * hp[clampi(r + dy, 0, H - 1) * W + clampi(col + dx, 0, W - 1)];
   }
 #pragma unroll
-  for (int t = 0; t < 9; ++t) block_atomic_add(gw + c * 9 + t, acc[t]);
+  for (int t = 0; t < 9; ++t) block_red_put(gw, c * 9 + t, chunk_slot(C), acc[t]);
 }
 
 // gate = sigmoid(m) m v (if gate != NULL); gm, gv from ggate (if ggate != NULL).   hp [B, 2hid, P]
@@ -205,10 +210,10 @@ __global__ __launch_bounds__(NT) void gate_kernel(const float* __restrict__ hp, 
 
 // Reverse of the gate with the skip scale folded in: ghp = scale * d(gate)/d(hp) . gq and
 // gdot += <gq, gate>, gq = W2^T gout (so that <gout, W2 gate> = <gq, gate> needs no W2 gate).
-// Grid-stride over all elements, one atomic per block.
+// Grid-stride over all elements, one partial per block.
 __global__ __launch_bounds__(NT) void gate_bwd_scaled_kernel(const float* __restrict__ hp, const float* __restrict__ gq,
                                                              const float* __restrict__ scale, float* __restrict__ ghp,
-                                                             float* __restrict__ gdot, int hid, int64_t P, int64_t n) {
+                                                             Red gdot, int hid, int64_t P, int64_t n) {
   const float s = scale[0];
   float dot = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(NT) void gate_bwd_scaled_kernel(const float* __rest
     ghp[om] = gg * v * (sg + m * sg * (1.0f - sg));
     ghp[ov] = gg * sg * m;
   }
-  block_atomic_add(gdot, dot);
+  block_red_put(gdot, 0, blockIdx.x, dot);
 }
 
 // ---------------------------------------------------------------------------
@@ -283,6 +288,7 @@ struct Dw3RowGeom {
   int lane, c0, cl0;
   bool on;
   int plane, c, r0, r1;
+  uint32_t wid, slot;   // wave index; slot of the per-channel reductions = (b, segment, strip)
 };
 template <int V>
 __device__ __forceinline__ bool dw3_row_geom(Dw3RowGeom& q, int C, int H, int W, int sseg, int nsegs, uint32_t nwaves) {
@@ -296,6 +302,8 @@ __device__ __forceinline__ bool dw3_row_geom(Dw3RowGeom& q, int C, int H, int W,
   const int seg = (int)(rest % nsegs);
   q.plane = (int)(rest / nsegs);
   q.c = q.plane % C;
+  q.wid = wid;
+  q.slot = ((uint32_t)(q.plane / C) * nsegs + seg) * nstrips + strip;
   q.r0 = seg * sseg;
   q.r1 = min(q.r0 + sseg, H);
   const int x0 = strip == 0 ? 0 : strip * STEP - V;
@@ -354,11 +362,11 @@ __global__ __launch_bounds__(NT) void dw3_row_fwd_kernel(const float* __restrict
 //   gh(q) = sum_t w_t sum_{p: clamp(p + t) = q} g(p)   (adjoint of the clamped gather, separable:
 //           rows then columns; along an axis the sources of q for offset d are q - d when inside,
 //           plus q itself at the edge the clamp folds onto)
-//   gw[c, t] += sum_p g(p) h(clamp(p + t))              (wave sums, one atomic per tap and wave)
+//   gw[c, t] += sum_p g(p) h(clamp(p + t))              (wave sums, one partial per tap and wave)
 template <int V>
 __global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict__ g, const float* __restrict__ h,
                                                          const float* __restrict__ wdw, float* __restrict__ gh,
-                                                         float* __restrict__ gw, int C, int H, int W, int sseg,
+                                                         Red gw, int C, int H, int W, int sseg,
                                                          int nsegs, uint32_t nwaves) {
   Dw3RowGeom q;
   if (!dw3_row_geom<V>(q, C, H, W, sseg, nsegs, nwaves)) return;
@@ -445,7 +453,7 @@ __global__ __launch_bounds__(NT) void dw3_row_bwd_kernel(const float* __restrict
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const float s = wave_sum(acc[t]);
-    if (q.lane == 0 && s != 0.f) atomicAdd(gw + q.c * 9 + t, s);
+    if (q.lane == 0) red_put(gw, q.c * 9 + t, q.slot, s);
   }
 }
 
@@ -566,8 +574,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_fwd_kernel(const float* __res
 template <int V, bool REC, bool FFN = false>
 __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
     const float* hp, const float* __restrict__ gq, const float* __restrict__ scale,
-    const float* __restrict__ hh, const float* __restrict__ wdw, float* __restrict__ gh, float* __restrict__ gw,
-    float* __restrict__ gdot, int hid, int H, int W, int sseg, int nsegs, uint32_t nwaves) {
+    const float* __restrict__ hh, const float* __restrict__ wdw, float* __restrict__ gh, Red gw,
+    Red gdot, int hid, int H, int W, int sseg, int nsegs, uint32_t nwaves) {
   Dw3RowGeom q;
   if (!dw3_row_geom<V>(q, hid, H, W, sseg, nsegs, nwaves)) return;   // q.plane = b hid + j, q.c = j
   const int64_t HW = (int64_t)H * W;
@@ -723,12 +731,12 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
   for (int t = 0; t < 9; ++t) {
     const float a = wave_sum(accm[t]), b = wave_sum(accv[t]);
     if (q.lane == 0) {
-      if (a != 0.f) atomicAdd(gw + j * 9 + t, a);
-      if (b != 0.f) atomicAdd(gw + (hid + j) * 9 + t, b);
+      red_put(gw, (int)j * 9 + t, q.slot, a);
+      red_put(gw, (hid + (int)j) * 9 + t, q.slot, b);
     }
   }
   const float d = wave_sum(dot);
-  if (q.lane == 0 && d != 0.f) atomicAdd(gdot, d);
+  if (q.lane == 0) red_put(gdot, 0, q.wid, d);
 }
 
 // V for the row kernels (0: not applicable -> per-pixel kernels)
@@ -745,51 +753,71 @@ int dw3_row_seg(int H, int64_t planes) {
   return sseg;
 }
 template <int V>
-void launch_dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gw, int B, int C,
-                    int H, int W, hipStream_t s) {
-  const int64_t planes = (int64_t)B * C * dw3_row_strips(W, V);   // (plane, strip) pairs
+grr_status launch_dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gwd, int B,
+                          int C, int H, int W, hipStream_t s, const char* what) {
+  const int nstrips = dw3_row_strips(W, V);
+  const int64_t planes = (int64_t)B * C * nstrips;   // (plane, strip) pairs
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
-  if (bwd)
-    hipLaunchKernelGGL(dw3_row_bwd_kernel<V>, grid, dim3(NT), 0, s, g, h, wdw, out, gw, C, H, W, sseg, nsegs, nwaves);
-  else
+  if (!bwd) {
     hipLaunchKernelGGL(dw3_row_fwd_kernel<V>, grid, dim3(NT), 0, s, h, wdw, out, C, H, W, sseg, nsegs, nwaves);
+    return launch_status(what);
+  }
+  RedScratch rs(s);
+  const int iw = rs.plan(gwd, C * 9, (uint32_t)((int64_t)B * nsegs * nstrips));
+  grr_status st = rs.alloc(what);
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(dw3_row_bwd_kernel<V>, grid, dim3(NT), 0, s, g, h, wdw, out, rs.red(iw), C, H, W, sseg, nsegs,
+                     nwaves);
+  st = launch_status(what);
+  return st != GRR_OK ? st : rs.finish(what);
 }
-bool dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gw, int B, int C, int H,
-             int W, hipStream_t s) {
+bool dw3_row_ok(const float* g, const float* h, const float* out, int B, int C, int H, int W) {
   const int V = dw3_row_vec(W);
+  if (V == 0) return false;
   // vector row loads: plane bases aligned to 4 V bytes
   const void* ptrs[] = {g, h, out};
   for (const void* p : ptrs)
     if (p && (uintptr_t)p % (4u * V) != 0) return false;
-  if ((int64_t)B * C * dw3_row_strips(W, V) * ((H + 31) / 32) >= (1ll << 31)) return false;
-  switch (V) {
-    case 1: launch_dw3_row<1>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
-    case 2: launch_dw3_row<2>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
-    case 4: launch_dw3_row<4>(bwd, g, h, wdw, out, gw, B, C, H, W, s); return true;
-    default: return false;
+  return (int64_t)B * C * dw3_row_strips(W, V) * ((H + 31) / 32) < (1ll << 31);
+}
+grr_status dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gw, int B, int C,
+                   int H, int W, hipStream_t s, const char* what) {
+  switch (dw3_row_vec(W)) {
+    case 1: return launch_dw3_row<1>(bwd, g, h, wdw, out, gw, B, C, H, W, s, what);
+    case 2: return launch_dw3_row<2>(bwd, g, h, wdw, out, gw, B, C, H, W, s, what);
+    default: return launch_dw3_row<4>(bwd, g, h, wdw, out, gw, B, C, H, W, s, what);
   }
 }
 
 template <int V, bool FFN = false>
-void launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, const float* hh, const float* wdw,
-                         float* gh, float* gw, float* gdot, int B, int hid, int H, int W, hipStream_t s) {
-  const int64_t planes = (int64_t)B * hid * dw3_row_strips(W, V);   // (plane, strip) pairs
+grr_status launch_dw3_gate_row(const float* hp, const float* gq, const float* scale, const float* hh, const float* wdw,
+                               float* gh, float* gwd, float* gdotd, int B, int hid, int H, int W, hipStream_t s,
+                               const char* what) {
+  const int nstrips = dw3_row_strips(W, V);
+  const int64_t planes = (int64_t)B * hid * nstrips;   // (plane, strip) pairs
   const int sseg = dw3_row_seg(H, planes), nsegs = (H + sseg - 1) / sseg;
   const uint32_t nwaves = (uint32_t)(planes * nsegs);
   const dim3 grid((nwaves + NT / 64 - 1) / (NT / 64));
+  RedScratch rs(s);
+  const int iw = rs.plan(gwd, 2 * hid * 9, (uint32_t)((int64_t)B * nsegs * nstrips));
+  const int id = rs.plan(gdotd, 1, nwaves);
+  grr_status st = rs.alloc(what);
+  if (st != GRR_OK) return st;
+  const Red gw = rs.red(iw), gdot = rs.red(id);
   if constexpr (FFN) {   // the FeedForward reverse always recomputes the depthwise output
     hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, true, true>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw,
                        gdot, hid, H, W, sseg, nsegs, nwaves);
-    return;
-  }
-  if (hp)
+  } else if (hp) {
     hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, false>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot,
                        hid, H, W, sseg, nsegs, nwaves);
-  else
+  } else {
     hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, true>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw, gdot,
                        hid, H, W, sseg, nsegs, nwaves);
+  }
+  st = launch_status(what);
+  return st != GRR_OK ? st : rs.finish(what);
 }
 
 template <int V, bool FFN = false>
@@ -836,15 +864,22 @@ grr_status grr_lnb_norm_bwd(const float* x, const float* ln_w, const float* isd,
                      P, np);
   grr_status st = launch_status("grr_lnb_norm_bwd/data");
   if (st != GRR_OK) return st;
-  hipLaunchKernelGGL(ln_wgrad_kernel, dim3(chunks_for(P, (int64_t)B * C), B * C), dim3(NT), 0, (hipStream_t)stream,
-                     gn, x, isd, gln_w, C, P);
-  return launch_status("grr_lnb_norm_bwd/weight");
+  const int chunks = chunks_for(P, (int64_t)B * C);
+  RedScratch rs((hipStream_t)stream);
+  const int iw = rs.plan(gln_w, C, (uint32_t)B * chunks);
+  st = rs.alloc("grr_lnb_norm_bwd/weight");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(ln_wgrad_kernel, dim3(chunks, B * C), dim3(NT), 0, (hipStream_t)stream, gn, x, isd, rs.red(iw), C,
+                     P);
+  st = launch_status("grr_lnb_norm_bwd/weight");
+  return st != GRR_OK ? st : rs.finish("grr_lnb_norm_bwd/weight");
 }
 
 grr_status grr_dwconv3(const float* h, const float* wdw, float* out, int B, int C, int H, int W, void* stream) {
   clear_error();
   GRR_REQUIRE(h && wdw && out && B > 0 && C > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG, "grr_dwconv3: bad args");
-  if (dw3_row(false, nullptr, h, wdw, out, nullptr, B, C, H, W, (hipStream_t)stream)) return launch_status("grr_dwconv3");
+  if (dw3_row_ok(nullptr, h, out, B, C, H, W))
+    return dw3_row(false, nullptr, h, wdw, out, nullptr, B, C, H, W, (hipStream_t)stream, "grr_dwconv3");
   GRR_REQUIRE((int64_t)B * C <= 65535, GRR_ERR_UNSUPPORTED, "grr_dwconv3: B*C > 65535");
   hipLaunchKernelGGL(dw3_fwd_kernel, dim3((H * W + NT - 1) / NT, B * C), dim3(NT), 0, (hipStream_t)stream, h, wdw,
                      out, C, H, W);
@@ -856,15 +891,22 @@ grr_status grr_dwconv3_bwd(const float* g, const float* h, const float* wdw, flo
   clear_error();
   GRR_REQUIRE(g && h && wdw && gh && gwdw && B > 0 && C > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_dwconv3_bwd: bad args");
-  if (dw3_row(true, g, h, wdw, gh, gwdw, B, C, H, W, (hipStream_t)stream)) return launch_status("grr_dwconv3_bwd");
+  if (dw3_row_ok(g, h, gh, B, C, H, W))
+    return dw3_row(true, g, h, wdw, gh, gwdw, B, C, H, W, (hipStream_t)stream, "grr_dwconv3_bwd");
   GRR_REQUIRE((int64_t)B * C <= 65535, GRR_ERR_UNSUPPORTED, "grr_dwconv3_bwd: B*C > 65535");
   hipLaunchKernelGGL(dw3_bwd_data_kernel, dim3((H * W + NT - 1) / NT, B * C), dim3(NT), 0, (hipStream_t)stream, g,
                      wdw, gh, C, H, W);
   grr_status st = launch_status("grr_dwconv3_bwd/data");
   if (st != GRR_OK) return st;
-  hipLaunchKernelGGL(dw3_wgrad_kernel, dim3(chunks_for((int64_t)H * W, (int64_t)B * C), B * C), dim3(NT), 0,
-                     (hipStream_t)stream, g, h, gwdw, C, H, W);
-  return launch_status("grr_dwconv3_bwd/weight");
+  const int chunks = chunks_for((int64_t)H * W, (int64_t)B * C);
+  RedScratch rs((hipStream_t)stream);
+  const int iw = rs.plan(gwdw, C * 9, (uint32_t)B * chunks);
+  st = rs.alloc("grr_dwconv3_bwd/weight");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(dw3_wgrad_kernel, dim3(chunks, B * C), dim3(NT), 0, (hipStream_t)stream, g, h, rs.red(iw), C, H,
+                     W);
+  st = launch_status("grr_dwconv3_bwd/weight");
+  return st != GRR_OK ? st : rs.finish("grr_dwconv3_bwd/weight");
 }
 
 grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float* scale, float* ghp, float* gdot, int B,
@@ -874,9 +916,14 @@ grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float
               "grr_lnb_gate_bwd_scaled: bad args");
   const int64_t n = (int64_t)B * hid * P;
   const int grid = (int)std::min<int64_t>((n + NT - 1) / NT, 4096);
-  hipLaunchKernelGGL(gate_bwd_scaled_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, hp, gq, scale, ghp, gdot, hid,
-                     P, n);
-  return launch_status("grr_lnb_gate_bwd_scaled");
+  RedScratch rs((hipStream_t)stream);
+  const int id = rs.plan(gdot, 1, (uint32_t)grid);
+  grr_status st = rs.alloc("grr_lnb_gate_bwd_scaled");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(gate_bwd_scaled_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, hp, gq, scale, ghp,
+                     rs.red(id), hid, P, n);
+  st = launch_status("grr_lnb_gate_bwd_scaled");
+  return st != GRR_OK ? st : rs.finish("grr_lnb_gate_bwd_scaled");
 }
 
 grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
@@ -910,12 +957,12 @@ grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* s
   GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * dw3_row_strips(W, V > 0 ? V : 1) * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_lnb_gate_dw3_bwd: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
+  const char* what = "grr_lnb_gate_dw3_bwd";
   switch (V) {
-    case 1: launch_dw3_gate_row<1>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
-    case 2: launch_dw3_gate_row<2>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
-    default: launch_dw3_gate_row<4>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+    case 1: return launch_dw3_gate_row<1>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
+    case 2: return launch_dw3_gate_row<2>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
+    default: return launch_dw3_gate_row<4>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
   }
-  return launch_status("grr_lnb_gate_dw3_bwd");
 }
 
 grr_status grr_ffn_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
@@ -948,12 +995,12 @@ grr_status grr_ffn_gate_dw3_bwd(const float* gq, const float* scale, const float
   GRR_REQUIRE(V > 0 && aligned && (int64_t)B * hid * dw3_row_strips(W, V > 0 ? V : 1) * ((H + 31) / 32) < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_ffn_gate_dw3_bwd: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
+  const char* what = "grr_ffn_gate_dw3_bwd";
   switch (V) {
-    case 1: launch_dw3_gate_row<1, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
-    case 2: launch_dw3_gate_row<2, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
-    default: launch_dw3_gate_row<4, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s); break;
+    case 1: return launch_dw3_gate_row<1, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
+    case 2: return launch_dw3_gate_row<2, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
+    default: return launch_dw3_gate_row<4, true>(nullptr, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
   }
-  return launch_status("grr_ffn_gate_dw3_bwd");
 }
 
 grr_status grr_lnb_gate(const float* hp, const float* ggate, float* gate, float* ghp, int B, int hid, int64_t P,

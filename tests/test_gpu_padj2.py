@@ -56,8 +56,7 @@ def test_reverse_with_padj2_equals_without(irdu):
             grads.append([xa.grad] + [p.grad.clone() for p in blk.parameters()])
     finally:
         SG.PADJ2 = saved
-    scale = max(float(b.abs().max()) for b in grads[1])
     for a, b in zip(*grads):
-        # parameter gradients come from float atomics in the same kernels: equal up to summation order
-        # (a gradient that nearly cancels carries the noise of its terms: floor 1e-8 of the largest)
-        assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max()) + 1e-8 * scale
+        # padj2_kernel evaluates the two accumulating stencil launches' expressions in their order and
+        # the reductions are fixed-order (no float atomics): the tight round-2 floor holds again
+        assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max()) + 1e-12
