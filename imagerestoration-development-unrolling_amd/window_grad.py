@@ -16,6 +16,10 @@ reverse sweep is written out on the adjoint kernels of window_bwd.hip:
   operator  A = I + mu S_L^T (I - W_L) S_L + ro S_G^T C^T C S_G,  mu / ro linear, gamma = exp
   weights   softmax over K similarities of normalised, multiM-scaled features (REF7:418-446)
   mixture   out = sum_g softmax(conv1x1(features))_g x_g + dc                  (REF7:1006-1009)
+
+The bare module calls differentiate the same way: ``WinEdgeWeightsFn`` is
+``GLRFast/GTVFast.extract_edge_weights`` (REF7:418-446, REF1:255-272) and ``WinOperatorFn`` their
+``forward`` (REF7:503-511 / :776-782, REF1:274-291 / :421-470), each with its HIP reverse.
 """
 from __future__ import annotations
 
@@ -225,3 +229,67 @@ class WinMixFn(torch.autograd.Function):
         gout = gout.contiguous()
         gx, gscore = K.win_bwd_mix(gout, x, score)
         return gx, gscore, (gout if ctx.has_dc else None)
+
+
+class WinEdgeWeightsFn(torch.autograd.Function):
+    """(features [B,G,F,H,W], multiM [G,F]) -> (w [B,G,K,H,W], degree [B,G,H,W]): extract_edge_weights
+    (grr_win_edge_weights) with its reverse (grr_win_bwd_edge_weights; degree = sum_k w, so its gradient
+    joins every edge's)."""
+
+    @staticmethod
+    def forward(ctx, delta, f5: Tensor, multiM: Tensor):
+        b, g, f, h, w = f5.shape
+        feat = f5.reshape(b, g * f, h, w).contiguous()
+        wt, deg = K.win_edge_weights(feat, 0, g, f, multiM.contiguous(), delta, with_degree=True)
+        ctx.delta, ctx.shape5 = delta, f5.shape
+        ctx.save_for_backward(feat, multiM, wt)
+        return wt, deg
+
+    @staticmethod
+    def backward(ctx, gw: Optional[Tensor], gdeg: Optional[Tensor]):
+        feat, multiM, wt = ctx.saved_tensors
+        b, g, f, h, w = ctx.shape5
+        gwc = torch.zeros_like(wt) if gw is None else gw.contiguous().clone()   # consumed by the reverse
+        if gdeg is not None:
+            gwc += gdeg.unsqueeze(2)
+        gfeat = torch.zeros_like(feat)
+        gM = torch.zeros_like(multiM)
+        K.win_bwd_edge_weights(feat, 0, g, f, multiM.contiguous(), wt, gwc, ctx.delta, gfeat, gM)
+        return None, gfeat.view(ctx.shape5), gM
+
+
+class WinOperatorFn(torch.autograd.Function):
+    """GLRFast.forward (kind "glr": S^T (I - W) S x) or GTVFast.forward (kind "gtv": S^T C^T C S x) on a
+    window graph (grr_win_solver mode 3), differentiable in x, the edge weights and the four stats-stencil
+    parameters (None: the identity stencil of REF1).  Reverse: _Terms.glr_bwd / gtv_bwd at unit scale."""
+
+    @staticmethod
+    def forward(ctx, kind: str, delta, x: Tensor, wt: Tensor, *stencil: Optional[Tensor]):
+        b, g, c, h, w = x.shape
+        with_taps = stencil[0] is not None
+        taps = K.win_taps(*stencil) if with_taps else \
+            torch.tensor(K.IDENTITY_TAPS, dtype=torch.float32, device=x.device)
+        xc, wc = x.contiguous(), wt.contiguous()
+        if kind == "glr":
+            out = K.win_apply(xc, delta, g, c, wL=wc, tapsL=taps)
+        else:
+            out = K.win_apply(xc, delta, g, c, wG=wc, tapsG=taps)
+        ctx.kind, ctx.delta, ctx.with_taps = kind, delta, with_taps
+        ctx.save_for_backward(xc, wc, taps)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout: Tensor):
+        x, wt, taps = ctx.saved_tensors
+        g = x.shape[1]
+        one = torch.ones(g, dtype=torch.float32, device=x.device)
+        T = _Terms(wt, wt, taps, taps, one, one, torch.zeros_like(one), ctx.delta, g)
+        gx = torch.zeros_like(x)
+        if ctx.kind == "glr":
+            T.glr_bwd(x, gout.contiguous(), 1.0, gx)
+            gw, gt = T.gwL, T.gtL
+        else:
+            T.gtv_bwd(x, gout.contiguous(), 1.0, gx)
+            gw, gt = T.gwG, T.gtG
+        gst = taps_backward(gt) if ctx.with_taps else (None, None, None, None)
+        return (None, None, gx, gw, *gst)

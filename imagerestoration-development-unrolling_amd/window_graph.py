@@ -21,8 +21,9 @@ Class names, constructor signatures and ``state_dict`` keys match REF7, so its
 checkpoints load unchanged (the ``device`` argument is accepted and used for placement).
 Training: when autograd records, ``MixtureGTV`` runs the solver through
 ``window_grad._WindowSolve`` (HIP forward keeping the iterates + HIP reverse sweep of
-window_bwd.hip) and the mixture through ``window_grad.WinMixFn``.  The GLRFast / GTVFast
-module calls stay inference-only (under autograd they attach a node whose backward raises).
+window_bwd.hip) and the mixture through ``window_grad.WinMixFn``; the bare GLRFast / GTVFast
+calls (``extract_edge_weights``, ``forward``) through ``window_grad.WinEdgeWeightsFn`` /
+``WinOperatorFn`` (the same kernels, REF7:418-446, :503-511, :776-782).
 """
 from __future__ import annotations
 
@@ -225,30 +226,46 @@ class _WindowGraphModule(HipModule):
         return K.win_taps(self.stats_kernel_p01.data, self.stats_kernel_p02a.data, self.stats_kernel_p02b.data,
                           self.stats_kernel_p03.data)
 
-    @torch.no_grad()
+    def _delta(self):
+        return tuple((int(a), int(c)) for a, c in self.edge_delta)
+
+    def _stencil(self):
+        return (self.stats_kernel_p01, self.stats_kernel_p02a, self.stats_kernel_p02b, self.stats_kernel_p03)
+
     def extract_edge_weights(self, img_features):
-        """[B,G,F,H,W] -> (w [B,G,K,H,W], degree [B,G,H,W]) (REF7:432-446)."""
-        b, g, f, h, w = img_features.shape
-        feat = img_features.reshape(b, g * f, h, w).contiguous()
-        return K.win_edge_weights(feat, 0, g, f, self.multiM.data.contiguous(), self.edge_delta, with_degree=True)
+        """[B,G,F,H,W] -> (w [B,G,K,H,W], degree [B,G,H,W]) (REF7:432-446); differentiable in the
+        features and multiM when autograd records."""
+        if records_grad(self, img_features):
+            return WG.WinEdgeWeightsFn.apply(self._delta(), img_features, self.multiM)
+        with torch.no_grad():
+            b, g, f, h, w = img_features.shape
+            feat = img_features.reshape(b, g * f, h, w).contiguous()
+            return K.win_edge_weights(feat, 0, g, f, self.multiM.contiguous(), self.edge_delta, with_degree=True)
+
+    def _graph_op(self, kind, patchs, edge_weights):
+        if records_grad(self, patchs, edge_weights):
+            return WG.WinOperatorFn.apply(kind, self._delta(), patchs, edge_weights, *self._stencil())
+        with torch.no_grad():
+            b, g, c, h, w = patchs.shape
+            if kind == "glr":
+                return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wL=edge_weights.contiguous(),
+                                   tapsL=self.taps())
+            return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wG=edge_weights.contiguous(),
+                               tapsG=self.taps())
 
 
 class GLRFast(_WindowGraphModule):
     """S^T (I - W) S on a window graph (REF7:274-511)."""
 
-    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
-        b, g, c, h, w = patchs.shape
-        return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wL=edge_weights.contiguous(), tapsL=self.taps())
+        return self._graph_op("glr", patchs, edge_weights)
 
 
 class GTVFast(_WindowGraphModule):
     """C^T C with C = W (S - S shifted) on a window graph (REF7:514-782)."""
 
-    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
-        b, g, c, h, w = patchs.shape
-        return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wG=edge_weights.contiguous(), tapsG=self.taps())
+        return self._graph_op("gtv", patchs, edge_weights)
 
 
 class MixtureGTV(HipModule):

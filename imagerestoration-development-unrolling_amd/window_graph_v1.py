@@ -51,30 +51,43 @@ class _WindowGraphModuleV1(HipModule):
             self._taps = torch.tensor(K.IDENTITY_TAPS, dtype=torch.float32, device=dev)
         return self._taps
 
-    @torch.no_grad()
+    def _delta(self):
+        return tuple((int(a), int(c)) for a, c in self.edge_delta)
+
     def extract_edge_weights(self, img_features):
-        """[B,G,F,H,W] -> (w [B,G,K,H,W], degree [B,G,H,W]) (REF1:255-272)."""
-        b, g, f, h, w = img_features.shape
-        feat = img_features.reshape(b, g * f, h, w).contiguous()
-        return K.win_edge_weights(feat, 0, g, f, self.multiM.data.contiguous(), self.edge_delta, with_degree=True)
+        """[B,G,F,H,W] -> (w [B,G,K,H,W], degree [B,G,H,W]) (REF1:255-272); differentiable in the
+        features and multiM when autograd records (window_grad.WinEdgeWeightsFn)."""
+        if records_grad(self, img_features):
+            return WG.WinEdgeWeightsFn.apply(self._delta(), img_features, self.multiM)
+        with torch.no_grad():
+            b, g, f, h, w = img_features.shape
+            feat = img_features.reshape(b, g * f, h, w).contiguous()
+            return K.win_edge_weights(feat, 0, g, f, self.multiM.contiguous(), self.edge_delta, with_degree=True)
+
+    def _graph_op(self, kind, patchs, edge_weights):
+        if records_grad(self, patchs, edge_weights):   # identity stencil: no tap parameters
+            return WG.WinOperatorFn.apply(kind, self._delta(), patchs, edge_weights, None, None, None, None)
+        with torch.no_grad():
+            b, g, c, h, w = patchs.shape
+            if kind == "glr":
+                return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wL=edge_weights.contiguous(),
+                                   tapsL=self.taps())
+            return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wG=edge_weights.contiguous(),
+                               tapsG=self.taps())
 
 
 class GLRFast(_WindowGraphModuleV1):
     """x - W x on a window graph (REF1:274-291)."""
 
-    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
-        b, g, c, h, w = patchs.shape
-        return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wL=edge_weights.contiguous(), tapsL=self.taps())
+        return self._graph_op("glr", patchs, edge_weights)
 
 
 class GTVFast(_WindowGraphModuleV1):
     """C^T C, C = W (I - shift) on a window graph (REF1:421-470)."""
 
-    @hip_forward
     def forward(self, patchs, edge_weights, node_degree=None):
-        b, g, c, h, w = patchs.shape
-        return K.win_apply(patchs.contiguous(), self.edge_delta, g, c, wG=edge_weights.contiguous(), tapsG=self.taps())
+        return self._graph_op("gtv", patchs, edge_weights)
 
 
 class FeatureExtraction(HipModule):

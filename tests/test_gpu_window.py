@@ -150,19 +150,6 @@ def test_window_sequence_denoiser_small(wg):
     assert rel_err(out, ref) <= RTOL
 
 
-def test_window_module_grad_mode_raises(wg):
-    """The GLRFast / GTVFast module calls have no reverse: under autograd they must raise, not
-    drop gradients (MixtureGTV itself trains: tests/test_gpu_window_grad.py)."""
-    d = load_golden("window_ops_v7.npz")
-    x = torch.from_numpy(d["diamond5/x"]).to(DEV).requires_grad_(True)
-    wgt = torch.from_numpy(d["diamond5/wG"]).to(DEV)
-    b, g, f, h, w = torch.from_numpy(d["diamond5/feat"]).shape
-    gtv = wg.GTVFast(3, f, g, _window("diamond5")).to(DEV)
-    out = gtv(x, wgt)
-    with pytest.raises(NotImplementedError):
-        out.sum().backward()
-
-
 V1_WINDOWS = {"ring3": (2, 3, np.array([1, 1, 1, 1, 0, 1, 1, 1, 1]).reshape(3, 3)),
               "full5": (2, 2, np.array([1] * 12 + [0] + [1] * 12).reshape(5, 5))}
 

@@ -4,7 +4,8 @@ Every gradient is checked against PyTorch autograd through the CPU oracle
 (oracle/window_oracle.py, float64; the oracle's forward is pinned to the reference's own
 outputs by tests/test_oracle_golden.py): per operator term (GLR, linear GTV, prox GTV) on the
 three windows the reference uses (3x3 ring K=8, 5x5 diamond K=12, full 5x5 K=24), the whole
-unrolled solver, the mixture, and a training step of the REF7 / REF1 MixtureGTV blocks.
+unrolled solver, the mixture, a training step of the REF7 / REF1 MixtureGTV blocks, and the bare
+GLRFast / GTVFast module calls (extract_edge_weights + forward) under autograd.
 Tolerances: max-abs error / max-abs reference <= 2e-4 where every soft-threshold branch is
 stable (gamma far from |C x| or tiny); relative L2 <= 2e-3 where a few of the millions of
 |C x| ~ gamma comparisons may legitimately flip between fp32 and fp64.
@@ -265,3 +266,61 @@ def test_window_v1_training_step_grads(wg):
                       torch.tensor([[1e-9]]))
     img = torch.rand((1, 3, 16, 24))
     _model_grads_vs_oracle(m, lambda x, p: O.mixture_gtv_v1(x, p, 2, 3, wgm.CONNECTION_FLAGS_3x3), img, 2e-3)
+
+
+@pytest.mark.parametrize("version", ["v7", "v1"])
+@pytest.mark.parametrize("name", sorted(WINDOWS))
+def test_window_module_calls_differentiable(wg, version, name):
+    """The bare module calls of REF7 (:418-511, :776-782) / REF1 (:255-291, :421-470) under autograd:
+    w = extract_edge_weights(features), then GLRFast.forward(x, w_L) and GTVFast.forward(x, w_G); the
+    loss also reads the node degree.  Feature, signal, multiM and stats-stencil gradients vs the float64
+    oracle's autograd (REF1: identity stencil, no stencil parameters)."""
+    WG, W7, W1 = wg
+    mod = W7 if version == "v7" else W1
+    cw = WINDOWS[name]
+    delta = O.window_edges(cw)
+    b, g, f, fs, h, w = 2, 3, 4, 3, 17, 29
+    gen = torch.Generator().manual_seed(301 + len(delta) + len(version))
+    feat = torch.randn((b, g, f, h, w), generator=gen, dtype=torch.float64)
+    x = torch.randn((b, g, fs, h, w), generator=gen, dtype=torch.float64)
+    ggl, ggt = torch.randn_like(x), torch.randn_like(x)
+    gd = torch.randn((b, g, h, w), generator=gen, dtype=torch.float64)
+    ML = 0.5 + torch.rand((g, f), generator=gen, dtype=torch.float64)
+    MG = 0.5 + torch.rand((g, f), generator=gen, dtype=torch.float64)
+    tpl, tpg = _taps_params(gen), _taps_params(gen)
+    glr = mod.GLRFast(fs, f, g, cw).to(DEV)
+    gtv = mod.GTVFast(fs, f, g, cw).to(DEV)
+    with torch.no_grad():
+        glr.multiM.copy_(ML)
+        gtv.multiM.copy_(MG)
+        if version == "v7":
+            for m_, tp in ((glr, tpl), (gtv, tpg)):
+                for q, v in tp.items():
+                    getattr(m_, q).copy_(v)
+    # HIP
+    fr, xr = _dev(feat).requires_grad_(True), _dev(x).requires_grad_(True)
+    wl, degl = glr.extract_edge_weights(fr)
+    wgt, _ = gtv.extract_edge_weights(fr)
+    loss = (_dev(ggl) * glr(xr, wl, degl)).sum() + (_dev(ggt) * gtv(xr, wgt)).sum() + (_dev(gd) * degl).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    # oracle (autograd, float64)
+    fo, xo = feat.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    MLo, MGo = ML.clone().requires_grad_(True), MG.clone().requires_grad_(True)
+    tlo = {q: v.clone().requires_grad_(True) for q, v in tpl.items()}
+    tgo = {q: v.clone().requires_grad_(True) for q, v in tpg.items()}
+    kl = O.stats_kernel({"m." + q: v for q, v in tlo.items()}, "m.", fs) if version == "v7" else None
+    kg = O.stats_kernel({"m." + q: v for q, v in tgo.items()}, "m.", fs) if version == "v7" else None
+    wlo, dlo = O.edge_weights(fo, MLo, delta)
+    wgo, _ = O.edge_weights(fo, MGo, delta)
+    ref = ((ggl * O.glr_apply(xo, wlo, kl, delta)).sum() + (ggt * O.gtv_Ct(O.gtv_C(xo, wgo, kg, delta), wgo, kg, delta)).sum()
+           + (gd * dlo).sum())
+    ref.backward()
+    assert rel_inf(xr.grad, xo.grad) <= 2e-4
+    assert rel_inf(fr.grad, fo.grad) <= 2e-4
+    assert rel_inf(glr.multiM.grad, MLo.grad) <= 2e-4
+    assert rel_inf(gtv.multiM.grad, MGo.grad) <= 2e-4
+    if version == "v7":
+        for m_, to in ((glr, tlo), (gtv, tgo)):
+            for q, v in to.items():
+                assert rel_inf(getattr(m_, q).grad, v.grad) <= 2e-4, q
