@@ -83,7 +83,7 @@ def build_model(device, seed=2204, trained=False):
 
 
 # the solver kernels at the bench shape: grr_system_step2 (two CG stages per launch, stages 1-8)
-# and grr_system_step (W = 256 row waves: stages 0 and 9, or every stage with GRR_STEP2=0)
+# and grr_system_step (W = 256 row waves: stages 0 and 9, or every stage with kernels.STEP2 = False)
 STEP2_KERNEL = "graph_step2_kernel"
 STEP_KERNEL = "graph_row_kernel<true, 1, 2, 4>"
 TRAFFIC_FILES = {STEP2_KERNEL: "traffic_system_step2.json", STEP_KERNEL: "traffic_system_step.json"}

@@ -5,7 +5,7 @@
 W > 256 runs the CG stage pairs as two-stage passes in column strips (grr_system_step2: 256-lane
 windows, 224 owned columns, 16 halo columns per side) and the remaining graph operators as V = 4 row
 waves in column strips (248 output columns, 4 halo columns per side, graph_row_kernel);
---compare-step2 also times one launch per stage (GRR_STEP2_STRIPS=0), --compare the 64-column strip
+--compare-step2 also times one launch per stage (kernels.STEP2_STRIPS = False), --compare the 64-column strip
 kernels (grr_set_kernel_variant(1), graph_op_kernel) on the same batch.  Not the headline metric (bench.py
 is); prints one JSON line per variant with MPix/s and the per-kernel-kind time.
 Configs: 512x512 (config C4's image size), 336x496 (the BSD68 eval crops' landscape size).

@@ -99,13 +99,6 @@ __device__ __forceinline__ void dma16_opaque(const void* src, float* lds_wave_ba
 #define GRR_HEAD_OPAQUE_DMA 1
 #endif
 
-#ifdef GRR_FUSED_STAMP
-// per-phase cycle totals of the first 64 workgroups' waves of the head or fused kernel (timing builds
-// only; ordinary vector stores): gate, GEMM1, GEMM2, barrier 1 / vmcnt wait, h store, (wait +) barrier,
-// total, iterations
-__device__ unsigned long long g_fused_stamps[64 * 8 * 8];
-#endif
-
 // ---------------------------------------------------------------------------
 // head: LN + W1 + dw3x3 + gate
 constexpr int LH_TW = 32;           // output columns per tile
@@ -346,47 +339,22 @@ __global__ __launch_bounds__(512, head_wgs(KS)) void lnb_head_kernel(LnbHeadArgs
 #define GRR_HEAD_STAGGER 1
 #endif
   const bool gate_first = GRR_HEAD_STAGGER ? wave < 4 : true;
-#ifdef GRR_FUSED_STAMP
-  uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
-#define GRR_STAMP(k, t) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - (t); (t) = t_; } while (0)
-#else
-#define GRR_STAMP(k, t) do { } while (0)
-#endif
   for (int c = 0; c <= nch; ++c) {
-#ifdef GRR_FUSED_STAMP
-    uint64_t tt = __builtin_amdgcn_s_memtime();
-#endif
     // chunk c + AHEAD -> slot (c + AHEAD) % NSLOT, last read (gate of chunk c - 2) before the previous barrier
     issue(min(c + AHEAD, nch - 1), (c + AHEAD) % NSLOT);
     if (gate_first) {
       gate(c);
-      GRR_STAMP(0, tt);
       gemm1(c);
-      GRR_STAMP(1, tt);
     } else {
       gemm1(c);
-      GRR_STAMP(1, tt);
       gate(c);
-      GRR_STAMP(0, tt);
     }
     // chunk c + 1 landed: after its DMA this wave issued RA stores (iteration c - 1),
     // DPW DMAs and RA stores (iteration c) -- AHEAD = 1: RA stores (iteration c); then every
     // wave's part (barrier)
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(AHEAD == 2 ? 2 * RA + DPW : RA) : "memory");
-    GRR_STAMP(3, tt);
     __builtin_amdgcn_s_barrier();
-    GRR_STAMP(5, tt);
   }
-#ifdef GRR_FUSED_STAMP
-  st[6] = __builtin_amdgcn_s_memtime() - t_begin;
-  st[7] = (uint64_t)(nch + 1);
-  if (blockIdx.x < 64 && lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) g_fused_stamps[(blockIdx.x * 8 + wave) * 8 + k] = st[k];
-  }
-#endif
-#undef GRR_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -1258,10 +1226,9 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
 }
 
 // the replicated first block runs as one fused pass (lnb_rep_kernel) when its im2col depth 9 Cs fits two
-// k-steps; GRR_LNB_REP=0: head16 + mix (A/B measurement, round 4)
+// k-steps (else head16 + mix on the Cs-channel source)
 bool lnb_rep_fused(int Ch, int R, int C, int hid) {
-  static const bool off = [] { const char* e = getenv("GRR_LNB_REP"); return e && e[0] == '0'; }();
-  return !off && R > 1 && Ch >= 1 && Ch <= 3 && C <= 128 && hid >= 1;
+  return R > 1 && Ch >= 1 && Ch <= 3 && C <= 128 && hid >= 1;
 }
 
 template <int MT>
@@ -1388,9 +1355,3 @@ extern "C" grr_status grr_lnb_set_phases(int mask) {
   return GRR_OK;
 }
 
-#ifdef GRR_FUSED_STAMP
-extern "C" grr_status grr_debug_fused_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(grr::g_fused_stamps), sizeof(grr::g_fused_stamps)) == hipSuccess
-             ? GRR_OK : GRR_ERR_HIP;
-}
-#endif

@@ -316,8 +316,8 @@ def system_step2(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: Tensor
     return out, u_out, xd
 
 
-# two CG stages per launch where the shape allows (GRR_STEP2=0: one launch per stage, for A/B runs)
-STEP2 = os.environ.get("GRR_STEP2", "1") != "0"
+# two CG stages per launch where the shape allows (tests set False to run one launch per stage)
+STEP2 = True
 
 
 def system_step2_train(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: Tensor,
@@ -344,11 +344,11 @@ def system_step2_train(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: 
 
 
 # W != 256 (W % 8 == 0) runs the two-stage pass in column strips of 256 lanes with a 16-column halo
-# (GRR_STEP2_STRIPS=0: one launch per stage there).  Narrower images are one strip with idle lanes:
+# (STEP2_STRIPS = False: one launch per stage there; bench_wide.py's per-stage comparison).  Narrower images are one strip with idle lanes:
 # at W = 128 (the v1.0 model's second level) that still beats one launch per stage (v1.0 forward
 # 25.15-25.22 -> 24.75 ms at 16 x 256^2), at W = 64 it does not (25.48 ms; profiles/r03/s2strips/narrow.txt)
-STEP2_STRIPS = os.environ.get("GRR_STEP2_STRIPS", "1") != "0"
-STEP2_MIN_W = int(os.environ.get("GRR_STEP2_MIN_W", "128"))   # narrowest strip-pass width the loops use
+STEP2_STRIPS = True
+STEP2_MIN_W = 128   # narrowest strip-pass width the loops use
 
 
 def step2_supported(x: Tensor, n_graphs: int) -> bool:

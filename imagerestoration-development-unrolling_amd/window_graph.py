@@ -28,7 +28,6 @@ calls (``extract_edge_weights``, ``forward``) through ``window_grad.WinEdgeWeigh
 from __future__ import annotations
 
 import itertools
-import os
 from typing import Optional
 
 import numpy as np
@@ -41,8 +40,8 @@ from .compile_backend import HipModule
 from . import window_grad as WG
 from .graph_filter import hip_forward, records_grad
 
-# inference: the linear GTV passes on pair weights (grr_win_pair_weights); GRR_WIN_PAIR=0: raw weights (A/B)
-WIN_PAIR_WEIGHTS = os.environ.get("GRR_WIN_PAIR", "1") == "1"
+# the linear GTV passes on pair weights (grr_win_pair_weights); False: on the raw directed weights
+WIN_PAIR_WEIGHTS = True
 
 CONNECTION_FLAGS_5x5_small = np.array([
     0, 0, 1, 0, 0,
