@@ -1,6 +1,6 @@
 """Micro-benchmark of single HIP kernels at the bench shape (P: B=64, G=32, F=3, 256x256).
 
-    python scripts/micro.py [--kernel step|step2|half|lnb|conv1x1|edge] [--iters N] [--batch B]
+    python scripts/micro.py [--kernel step|step2|half|lnb|lnb_rep|conv1x1|term|edge] [--iters N] [--batch B]
 
 Used under rocprofv3 (kernel trace / PMC passes) to profile one kernel in isolation.
 Prints mean milliseconds per launch and algorithmic GB/s from HIP events.
@@ -26,10 +26,12 @@ def main():
     ap.add_argument("--graphs", type=int, default=32)
     ap.add_argument("--fts", type=int, default=3)
     ap.add_argument("--split", action="store_true", help="LNB: time the head and the mix apart")
+    ap.add_argument("--mode", type=int, default=0, help="term: 0 GLR, 1 pair Laplacian, 2 prox")
+    ap.add_argument("--width", type=int, default=0, help="image width (default: --size)")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
     dev = torch.device("cuda", 0)
-    b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.size
+    b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.width or args.size
     c = g * f
     torch.manual_seed(0)
     mix = irdu_amd.MixtureGTVGLR(g, f, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]],
@@ -79,6 +81,16 @@ def main():
         xd = torch.rand(b, 256, h, w, device=dev)
         wt = torch.rand(1364, 256, 1, 1, device=dev)
         fn = lambda: K.conv1x1(xd, wt)  # noqa: E731
+    elif args.kernel == "term":   # the training reverse's operator-term pass (grr_bwd_term_fused)
+        mode = args.mode
+        gg = torch.randn(b, c, h, w, device=dev)
+        taps = torch.randn(c, 5, device=dev) * 0.5
+        wt = torch.rand(b, g, 2 if mode == 1 else 4, h, w, device=dev)
+        lg = torch.log(torch.full((g,), 0.05, device=dev)) if mode == 2 else None
+        sc = torch.rand(g, device=dev) + 0.5
+        gw, gdot, gt = torch.zeros_like(wt), torch.zeros(g, device=dev), torch.zeros_like(taps)
+        ggam = torch.zeros(g, device=dev) if mode == 2 else None
+        fn = lambda: K.bwd_term_fused(mode, x, gg, taps, wt, lg, sc, 0.5, gw, ggam, gdot, gt, g)  # noqa: E731
     elif args.kernel == "edge":
         feat = torch.rand(b, 2 * c, h, w, device=dev)
         fn = lambda: K.edge_weights(feat, 0, g, f, p(mix.GTVmodule00.multiM))  # noqa: E731
@@ -97,32 +109,6 @@ def main():
         for kind, v in timer.summary().items():
             print(f"{args.kernel}: {kind:16s} launches={v['launches']} mean={v['mean_ms']:.4f} ms "
                   f"algo={v['gbps']:.1f} GB/s bytes/launch={v['bytes_per_launch']:.4e}")
-        lib = irdu_amd._native.load()
-        if hasattr(lib, "grr_debug_fused_stamps"):   # GRR_FUSED_STAMP timing builds of the fused LNB
-            import ctypes
-            import numpy as np
-            buf = (ctypes.c_ulonglong * (64 * 8 * 8))()
-            lib.grr_debug_fused_stamps(buf)
-            a = np.frombuffer(buf, dtype=np.uint64).reshape(64 * 8, 8).astype(np.float64)
-            names = ["gate", "gemm1", "gemm2", "barrier1", "store_h", "wait+barrier2"]
-            it = a[0, 7]
-            print("fused stamps, cycles per iteration (mean over waves): " +
-                  "  ".join(f"{n} {a[:, k].mean() / it:.0f}" for k, n in enumerate(names)) +
-                  f"  total {a[:, 6].mean() / it:.0f}  (iterations {it:.0f})")
-            for grp, sel in (("waves 0-3 (gate first)", a[np.arange(len(a)) % 8 < 4]),
-                             ("waves 4-7 (gemm first)", a[np.arange(len(a)) % 8 >= 4])):
-                print(f"   {grp}: " + "  ".join(f"{n} {sel[:, k].mean() / it:.0f}" for k, n in enumerate(names)))
-        if hasattr(lib, "grr_debug_head_stamps"):   # GRR_HEAD_STAMP timing builds
-            import ctypes
-            import numpy as np
-            buf = (ctypes.c_ulonglong * (64 * 8 * 8))()
-            lib.grr_debug_head_stamps(buf)
-            a = np.frombuffer(buf, dtype=np.uint64).reshape(64 * 8, 8).astype(np.float64)
-            tot = a[:, 1] - a[:, 0]
-            print(f"head stamps (cycles per wave, mean of {len(a)}): total {tot.mean():.0f}  "
-                  f"steady work {a[:, 2].mean():.0f}  vmcnt wait {a[:, 3].mean():.0f}  barrier {a[:, 4].mean():.0f}  "
-                  f"per steady chunk: work {a[:, 2].mean() / (a[0, 5] - 1):.0f} wait {a[:, 3].mean() / (a[0, 5] - 1):.0f} "
-                  f"barrier {a[:, 4].mean() / (a[0, 5] - 1):.0f}")
 
 
 if __name__ == "__main__":
