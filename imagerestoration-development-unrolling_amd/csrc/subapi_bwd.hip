@@ -9,7 +9,8 @@
 //   op_C_transpose             gz = S^T* g;  gE_e = w_e (gz - [p + d_e inside] gz(p + d_e)), gw_e = sum_f E_e (...)
 // "scatter" is the adjoint of the replicate-clamped gather: the sources of q along edge e are
 // q - d_e (when inside) and q itself (when q + d_e falls outside, the clamp maps it back to q).
-// Per-channel tap and per-graph multiM gradients are block reductions with one atomic per block.
+// Per-channel tap and per-graph multiM gradients are block reductions with one fixed-order partial per
+// block (grr_common.h).
 // These are off the solver's path (it fuses the same arithmetic in graph_bwd.hip); one thread per
 // output pixel, HBM-bound.
 #include "grr_common.h"
@@ -46,9 +47,10 @@ __device__ __forceinline__ float clamp_adj(int y, int x, int e, int H, int W, Fn
   return v;
 }
 
-// block sum of NV floats per thread -> one atomic per value (thread 0)
+// block sum of NV floats per thread -> one partial per value (thread k: row idx0 + k of r, slot `slot`;
+// grr_common.h, fixed-order reductions)
 template <int NV>
-__device__ __forceinline__ void block_atomic(float (&v)[NV], float* dst) {
+__device__ __forceinline__ void block_red(float (&v)[NV], const Red& r, int idx0, int nv, uint32_t slot) {
   __shared__ float red[NV][SB_NT / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -59,13 +61,17 @@ __device__ __forceinline__ void block_atomic(float (&v)[NV], float* dst) {
     if (lane == 0) red[k][wv] = s;
   }
   __syncthreads();
-  if (threadIdx.x < NV) {
+  if ((int)threadIdx.x < nv) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < SB_NT / 64; ++i) s += red[threadIdx.x][i];
-    if (s != 0.f) atomicAdd(dst + threadIdx.x, s);
+    red_put(r, idx0 + (int)threadIdx.x, slot, s);
   }
   __syncthreads();
+}
+// slot of block (blockIdx.x, blockIdx.y) of a (chunks, B * per) grid: one per (b, chunk)
+__device__ __forceinline__ uint32_t chunk_slot(int per) {
+  return (uint32_t)(blockIdx.y / per) * gridDim.x + blockIdx.x;
 }
 
 // grid: (blocks per plane, planes); the pixels of one plane per block row
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(SB_NT) void neighbor_gather_bwd_kernel(const float*
 __global__ __launch_bounds__(SB_NT) void normalize_features_bwd_kernel(const float* __restrict__ f,
                                                                        const float* __restrict__ multiM,
                                                                        const float* __restrict__ gout,
-                                                                       float* __restrict__ gf, float* __restrict__ gM,
+                                                                       float* __restrict__ gf, Red gM,
                                                                        int G, int F, int64_t HW) {
   constexpr int FMAX = 16;
   const int64_t bg = blockIdx.y;
@@ -118,13 +124,13 @@ __global__ __launch_bounds__(SB_NT) void normalize_features_bwd_kernel(const flo
       gf[(bg * F + k) * HW + p] = nrm > 1e-12f ? (gy - y * dot) / den : gy / den;
     }
   }
-  block_atomic<FMAX>(acc, gM + gi * F);   // entries k >= F are zero: no atomic issued for them
+  block_red<FMAX>(acc, gM, gi * F, F, chunk_slot(G));
 }
 
 // stats_conv reverse: gx = S* g (replicate) or S^T* g (zero frame); gtaps[ch] (c, u, l, r, d) += <g, shifted x>
 __global__ __launch_bounds__(SB_NT) void stats_conv_bwd_kernel(const float* __restrict__ x, grr_stencil s,
                                                                int transpose, const float* __restrict__ g,
-                                                               float* __restrict__ gx, float* __restrict__ gtaps,
+                                                               float* __restrict__ gx, Red gtaps,
                                                                int C, int H, int W) {
   const int64_t HW = (int64_t)H * W, pl = plane_of();
   const int ch = (int)(pl % C);
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(SB_NT) void stats_conv_bwd_kernel(const float* __re
     }
     gx[pl * HW + p] = v;
   }
-  if (gtaps) block_atomic<5>(tg, gtaps + ch * 5);
+  if (gtaps.p) block_red<5>(tg, gtaps, ch * 5, 5, chunk_slot(C));
 }
 
 // op_L_norm reverse, grid (blocks, B*G): the F planes of a graph share w
@@ -295,9 +301,15 @@ grr_status grr_normalize_features_bwd(const float* f, const float* multiM, const
   GRR_REQUIRE(f && multiM && gout && gf && gM && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_normalize_features_bwd: bad args");
   GRR_REQUIRE(F <= 16 && (int64_t)B * G < 65536, GRR_ERR_UNSUPPORTED, "grr_normalize_features_bwd: F > 16");
-  hipLaunchKernelGGL(normalize_features_bwd_kernel, grid2((int64_t)H * W, (int64_t)B * G), dim3(SB_NT), 0,
-                     (hipStream_t)stream, f, multiM, gout, gf, gM, G, F, (int64_t)H * W);
-  return launch_status("grr_normalize_features_bwd");
+  const dim3 grid = grid2((int64_t)H * W, (int64_t)B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int im = rs.plan(gM, G * F, (uint32_t)B * grid.x);
+  grr_status st = rs.alloc("grr_normalize_features_bwd");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(normalize_features_bwd_kernel, grid, dim3(SB_NT), 0, (hipStream_t)stream, f, multiM, gout, gf,
+                     rs.red(im), G, F, (int64_t)H * W);
+  st = launch_status("grr_normalize_features_bwd");
+  return st != GRR_OK ? st : rs.finish("grr_normalize_features_bwd");
 }
 
 grr_status grr_stats_conv_bwd(const float* x, grr_stencil s, int transpose, const float* g, float* gx, float* gtaps,
@@ -306,9 +318,15 @@ grr_status grr_stats_conv_bwd(const float* x, grr_stencil s, int transpose, cons
   GRR_REQUIRE(x && g && gx && taps_set(s) && B > 0 && G > 0 && F > 0 && H > 0 && W > 0, GRR_ERR_INVALID_ARG,
               "grr_stats_conv_bwd: bad args");
   GRR_REQUIRE(gx != g && (int64_t)B * G * F < 65536, GRR_ERR_INVALID_ARG, "grr_stats_conv_bwd: aliasing / size");
-  hipLaunchKernelGGL(stats_conv_bwd_kernel, grid2((int64_t)H * W, (int64_t)B * G * F), dim3(SB_NT), 0,
-                     (hipStream_t)stream, x, s, transpose, g, gx, gtaps, G * F, H, W);
-  return launch_status("grr_stats_conv_bwd");
+  const dim3 grid = grid2((int64_t)H * W, (int64_t)B * G * F);
+  RedScratch rs((hipStream_t)stream);
+  const int it = rs.plan(gtaps, G * F * 5, (uint32_t)B * grid.x);
+  grr_status st = rs.alloc("grr_stats_conv_bwd");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(stats_conv_bwd_kernel, grid, dim3(SB_NT), 0, (hipStream_t)stream, x, s, transpose, g, gx,
+                     rs.red(it), G * F, H, W);
+  st = launch_status("grr_stats_conv_bwd");
+  return st != GRR_OK ? st : rs.finish("grr_stats_conv_bwd");
 }
 
 grr_status grr_glr_op_l_norm_bwd(const float* x, const float* w, const float* g, float* gx, float* gw, int B, int G,
@@ -334,9 +352,14 @@ grr_status grr_gtv_op_c_bwd(const float* x, const float* w, grr_stencil s, const
                      G, F, H, W);
   grr_status rc = launch_status("grr_gtv_op_c_bwd");
   if (rc != GRR_OK) return rc;
-  hipLaunchKernelGGL(stats_conv_bwd_kernel, grid2((int64_t)H * W, (int64_t)B * G * F), dim3(SB_NT), 0, st, x, s, 0,
-                     work, gx, gtaps, G * F, H, W);
-  return launch_status("grr_gtv_op_c_bwd");
+  const dim3 grid = grid2((int64_t)H * W, (int64_t)B * G * F);
+  RedScratch rs(st);
+  const int it = rs.plan(gtaps, G * F * 5, (uint32_t)B * grid.x);
+  rc = rs.alloc("grr_gtv_op_c_bwd");
+  if (rc != GRR_OK) return rc;
+  hipLaunchKernelGGL(stats_conv_bwd_kernel, grid, dim3(SB_NT), 0, st, x, s, 0, work, gx, rs.red(it), G * F, H, W);
+  rc = launch_status("grr_gtv_op_c_bwd");
+  return rc != GRR_OK ? rc : rs.finish("grr_gtv_op_c_bwd");
 }
 
 // z: the op_C_transpose forward's pre-S^T value (its `work` buffer); work2: caller's [B,G,F,H,W] buffer
@@ -349,9 +372,14 @@ grr_status grr_gtv_op_c_transpose_bwd(const float* edges, const float* w, grr_st
   GRR_REQUIRE(work2 != g && (int64_t)B * G * F < 65536, GRR_ERR_INVALID_ARG,
               "grr_gtv_op_c_transpose_bwd: aliasing / size");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(stats_conv_bwd_kernel, grid2((int64_t)H * W, (int64_t)B * G * F), dim3(SB_NT), 0, st, z, s, 1, g,
-                     work2, gtaps, G * F, H, W);
-  grr_status rc = launch_status("grr_gtv_op_c_transpose_bwd");
+  const dim3 grid = grid2((int64_t)H * W, (int64_t)B * G * F);
+  RedScratch rs(st);
+  const int it = rs.plan(gtaps, G * F * 5, (uint32_t)B * grid.x);
+  grr_status rc = rs.alloc("grr_gtv_op_c_transpose_bwd");
+  if (rc != GRR_OK) return rc;
+  hipLaunchKernelGGL(stats_conv_bwd_kernel, grid, dim3(SB_NT), 0, st, z, s, 1, g, work2, rs.red(it), G * F, H, W);
+  rc = launch_status("grr_gtv_op_c_transpose_bwd");
+  if (rc == GRR_OK) rc = rs.finish("grr_gtv_op_c_transpose_bwd");
   if (rc != GRR_OK) return rc;
   hipLaunchKernelGGL(op_Ct_bwd_kernel, grid2((int64_t)H * W, (int64_t)B * G), dim3(SB_NT), 0, st, edges, w, work2, gE,
                      gw, F, H, W);

@@ -16,7 +16,7 @@
 // when inside, plus the pixels the clamp folds onto the frame row / column).
 //
 // Every kernel here is a per-pixel kernel (grid-stride over the elements, reductions by wave
-// sums and one float atomic per wave); the K-edge windows (K = 8, 12, 24, reach <= 2) make the
+// sums and one fixed-order partial per block); the K-edge windows (K = 8, 12, 24, reach <= 2) make the
 // per-pixel working set large, and this path trains the older window models, not the metric's.
 #include "grr_common.h"
 
@@ -36,10 +36,11 @@ __device__ __forceinline__ float wsum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// Block-wide sums of N per-thread values, one float atomic per value per block: dst[idx[i]] += sum.
-// Every thread of the block must call it (the grid-stride loops end before it).
+// Block-wide sums of N per-thread values, one partial per value and block (grr_common.h, fixed-order
+// reductions): value i goes to row idx[i] of r[i], slot `slot`.  Every thread of the block must call
+// it (the grid-stride loops end before it).
 template <int N>
-__device__ __forceinline__ void block_atomic(float (&v)[N], float* const (&dst)[N]) {
+__device__ __forceinline__ void block_red(float (&v)[N], const Red (&r)[N], const int (&idx)[N], uint32_t slot) {
   __shared__ float red[NTB / 64][N];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -52,12 +53,17 @@ __device__ __forceinline__ void block_atomic(float (&v)[N], float* const (&dst)[
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < NTB / 64; ++w) t += red[w][threadIdx.x];
-    float* d = nullptr;
+    Red rr{nullptr, 1};
+    int ii = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i)
-      if (i == (int)threadIdx.x) d = dst[i];
-    if (d && t != 0.f) atomicAdd(d, t);
+      if (i == (int)threadIdx.x) { rr = r[i]; ii = idx[i]; }
+    red_put(rr, ii, slot, t);
   }
+}
+// slot of block (blockIdx.x, blockIdx.y) of a (chunks, B * per) grid: one per (b, chunk)
+__device__ __forceinline__ uint32_t chunk_slot(int per) {
+  return (uint32_t)(blockIdx.y / per) * gridDim.x + blockIdx.x;
 }
 __device__ __forceinline__ int refl(int v, int n) {   // one-pixel reflect frame
   v = v < 0 ? -v : v;
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(NTB) void win_stencil_bwd_kernel(const float* __res
 // mode 0 (P): z(reflect(p + d_t));  mode 1 (T): z(p - d_t) [inside]
 template <int MODE>
 __global__ __launch_bounds__(NTB) void win_tapgrad_kernel(const float* __restrict__ u, const float* __restrict__ z,
-                                                          const float* __restrict__ scale, float* __restrict__ gt,
+                                                          const float* __restrict__ scale, Red gt,
                                                           int G, int Fs, int H, int W, int64_t n) {
   const int64_t HW = (int64_t)H * W;
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -151,8 +157,9 @@ __global__ __launch_bounds__(NTB) void win_tapgrad_kernel(const float* __restric
       }
     }
   }
-  float* const dst[5] = {gt, gt + 1, gt + 2, gt + 3, gt + 4};
-  block_atomic<5>(acc, dst);
+  const Red r[5] = {gt, gt, gt, gt, gt};
+  const int idx[5] = {0, 1, 2, 3, 4};
+  block_red<5>(acc, r, idx, blockIdx.x);
 }
 
 // ---- GLR pass 1.  Per (b, g) and pixel q, channels in turn; sc = scale[g] (mu coef):
@@ -163,7 +170,7 @@ __global__ __launch_bounds__(NTB) void win_glr_bwd_kernel(const float* __restric
                                                           const float* __restrict__ scale, float coef,
                                                           float* __restrict__ l_out, float* __restrict__ E,
                                                           float* __restrict__ gsd, float* __restrict__ gw,
-                                                          float* __restrict__ gdot, int G, int Fs, int H, int W) {
+                                                          Red gdot, int G, int Fs, int H, int W) {
   // grid (x, B*G): every lane of a block works on the same graph, so the per-graph
   // reduction is one wave sum after the loop, with every lane active
   const int64_t HW = (int64_t)H * W;
@@ -196,8 +203,9 @@ __global__ __launch_bounds__(NTB) void win_glr_bwd_kernel(const float* __restric
     for (int e = 0; e < K; ++e) gw[bg * K * HW + e * HW + q] += gwa[e];
   }
   float v[1] = {coef * dot};
-  float* const dst[1] = {gdot ? gdot + g : nullptr};
-  block_atomic<1>(v, dst);
+  const Red r[1] = {gdot};
+  const int idx[1] = {g};
+  block_red<1>(v, r, idx, chunk_slot(G));
 }
 
 // ---- GTV pass 1 (linear C^T C or the prox C^T phi(C .)).  sc = scale[g] (ro coef):
@@ -211,7 +219,7 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
                                                           const float* __restrict__ scale, float coef,
                                                           float* __restrict__ PW, float* __restrict__ E,
                                                           float* __restrict__ gsd, float* __restrict__ gw,
-                                                          float* __restrict__ gdot, float* __restrict__ ggam, int G,
+                                                          Red gdot, Red ggam, int G,
                                                           int Fs, int H, int W) {
   const int64_t HW = (int64_t)H * W;                 // grid (x, B*G) as the GLR kernel
   const int64_t bg = blockIdx.y;
@@ -260,8 +268,9 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
     for (int e = 0; e < K; ++e) gw[bg * K * HW + e * HW + p] += gwa[e];
   }
   float v[2] = {coef * dot, dgam};
-  float* const dst[2] = {gdot ? gdot + g : nullptr, prox && ggam ? ggam + g : nullptr};
-  block_atomic<2>(v, dst);
+  const Red r[2] = {gdot, ggam};
+  const int idx[2] = {g, g};
+  block_red<2>(v, r, idx, chunk_slot(G));
 }
 
 // ---- pass 2 (gather):  gs(q) = gsd(q) - sum_e sum_{p: clamp(p + d_e) = q} E_e(p)
@@ -316,8 +325,8 @@ __global__ __launch_bounds__(NTB) void win_feat_bwd_kernel(const float* __restri
                                                            const float* __restrict__ multiM,
                                                            const float* __restrict__ gsim, WinDeltaB d, int K,
                                                            float* __restrict__ gfeat, int64_t gstride,
-                                                           float* __restrict__ gM, int G, int F, int H, int W) {
-  // grid (x, B*G): the graph is fixed per block, so gM reduces per block (one atomic per f)
+                                                           Red gM, int G, int F, int H, int W) {
+  // grid (x, B*G): the graph is fixed per block, so gM reduces per block (one partial per f)
   const int64_t HW = (int64_t)H * W;
   const int bg = blockIdx.y, g = bg % G, b = bg / G;
   const float* fp = feat + (int64_t)b * fstride + (int64_t)g * F * HW;
@@ -380,10 +389,14 @@ __global__ __launch_bounds__(NTB) void win_feat_bwd_kernel(const float* __restri
       }
     }
   }
-  float* dst[FMAX];
+  Red r[FMAX];
+  int idx[FMAX];
 #pragma unroll
-  for (int f = 0; f < FMAX; ++f) dst[f] = f < F ? gM + g * F + f : nullptr;
-  block_atomic<FMAX>(gMa, dst);
+  for (int f = 0; f < FMAX; ++f) {
+    r[f] = f < F ? gM : Red{nullptr, 1};
+    idx[f] = g * F + f;
+  }
+  block_red<FMAX>(gMa, r, idx, chunk_slot(G));
 }
 
 // ---- mixture reverse (REF7:1006-1009): out[b,c] = sum_g score[b,g] x[b,g,c] + dc[b,c]
@@ -408,7 +421,7 @@ __global__ __launch_bounds__(NTB) void win_mix_bwd_kernel(const float* __restric
 
 int grid_1d(int64_t n) { return (int)std::min<int64_t>((n + NTB - 1) / NTB, 1 << 16); }
 // reduction kernels: about 4096 blocks in all (16 per CU), grid-stride beyond, so the per-block
-// atomics stay few
+// partials stay few
 int grid_red(int64_t n) { return (int)std::min<int64_t>((n + NTB - 1) / NTB, 4096); }
 dim3 plane_grid(int H, int W, int planes) {
   const int64_t per = std::max<int64_t>(1, 4096 / std::max(planes, 1));
@@ -457,11 +470,17 @@ grr_status grr_win_bwd_tapgrad(const float* u, const float* z, int mode, const f
               GRR_ERR_INVALID_ARG, "grr_win_bwd_tapgrad: bad args");
   const int64_t n = (int64_t)B * G * Fs * H * W;
   hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_red(n);
+  RedScratch rs(s);
+  const int it = rs.plan(gtaps, 5, (uint32_t)grid);
+  grr_status st = rs.alloc("grr_win_bwd_tapgrad");
+  if (st != GRR_OK) return st;
   if (mode == 0)
-    hipLaunchKernelGGL(win_tapgrad_kernel<0>, dim3(grid_red(n)), dim3(NTB), 0, s, u, z, scale, gtaps, G, Fs, H, W, n);
+    hipLaunchKernelGGL(win_tapgrad_kernel<0>, dim3(grid), dim3(NTB), 0, s, u, z, scale, rs.red(it), G, Fs, H, W, n);
   else
-    hipLaunchKernelGGL(win_tapgrad_kernel<1>, dim3(grid_red(n)), dim3(NTB), 0, s, u, z, scale, gtaps, G, Fs, H, W, n);
-  return launch_status("grr_win_bwd_tapgrad");
+    hipLaunchKernelGGL(win_tapgrad_kernel<1>, dim3(grid), dim3(NTB), 0, s, u, z, scale, rs.red(it), G, Fs, H, W, n);
+  st = launch_status("grr_win_bwd_tapgrad");
+  return st != GRR_OK ? st : rs.finish("grr_win_bwd_tapgrad");
 }
 
 grr_status grr_win_bwd_glr(const float* s, const float* b, const float* w, const int32_t* delta, int K,
@@ -473,9 +492,15 @@ grr_status grr_win_bwd_glr(const float* s, const float* b, const float* w, const
                   fill_delta(delta, K, d),
               GRR_ERR_INVALID_ARG, "grr_win_bwd_glr: bad args");
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_glr: B*G > 65535");
-  hipLaunchKernelGGL(win_glr_bwd_kernel, plane_grid(H, W, B * G), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K,
-                     scale, coef, l_out, E, gsd, gw, gdot, G, Fs, H, W);
-  return launch_status("grr_win_bwd_glr");
+  const dim3 grid = plane_grid(H, W, B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int id = rs.plan(gdot, G, (uint32_t)B * grid.x);
+  grr_status st = rs.alloc("grr_win_bwd_glr");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(win_glr_bwd_kernel, grid, dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K, scale, coef, l_out, E,
+                     gsd, gw, rs.red(id), G, Fs, H, W);
+  st = launch_status("grr_win_bwd_glr");
+  return st != GRR_OK ? st : rs.finish("grr_win_bwd_glr");
 }
 
 grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const int32_t* delta, int K,
@@ -488,9 +513,15 @@ grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const
                   (!prox || log_gamma) && fill_delta(delta, K, d),
               GRR_ERR_INVALID_ARG, "grr_win_bwd_gtv: bad args");
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_gtv: B*G > 65535");
-  hipLaunchKernelGGL(win_gtv_bwd_kernel, plane_grid(H, W, B * G), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K,
-                     prox, log_gamma, scale, coef, PW, E, gsd, gw, gdot, ggamma, G, Fs, H, W);
-  return launch_status("grr_win_bwd_gtv");
+  const dim3 grid = plane_grid(H, W, B * G);
+  RedScratch rs((hipStream_t)stream);
+  const int id = rs.plan(gdot, G, (uint32_t)B * grid.x), ig = rs.plan(prox ? ggamma : nullptr, G, (uint32_t)B * grid.x);
+  grr_status st = rs.alloc("grr_win_bwd_gtv");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(win_gtv_bwd_kernel, grid, dim3(NTB), 0, (hipStream_t)stream, s, b, w, d, K, prox, log_gamma,
+                     scale, coef, PW, E, gsd, gw, rs.red(id), rs.red(ig), G, Fs, H, W);
+  st = launch_status("grr_win_bwd_gtv");
+  return st != GRR_OK ? st : rs.finish("grr_win_bwd_gtv");
 }
 
 grr_status grr_win_bwd_gather(const float* E, const float* PW, const int32_t* delta, int K, float* gs,
@@ -520,9 +551,17 @@ grr_status grr_win_bwd_edge_weights(const float* feat, int64_t feat_bstride, con
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(win_softmax_bwd_kernel, dim3(grid_1d(npix)), dim3(NTB), 0, s, w, gw, K, (int64_t)H * W, npix);
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_edge_weights: B*G > 65535");
+  grr_status st = launch_status("grr_win_bwd_edge_weights");
+  if (st != GRR_OK) return st;
+  const dim3 grid = plane_grid(H, W, B * G);
+  RedScratch rs(s);
+  const int im = rs.plan(gmultiM, G * F, (uint32_t)B * grid.x);
+  st = rs.alloc("grr_win_bwd_edge_weights");
+  if (st != GRR_OK) return st;
+  const Red rm = rs.red(im);
 #define WIN_FEAT_BWD(FM_)                                                                                          \
-  hipLaunchKernelGGL(win_feat_bwd_kernel<FM_>, plane_grid(H, W, B * G), dim3(NTB), 0, s, feat, feat_bstride, multiM, \
-                     gw, d, K, gfeat, gfeat_bstride, gmultiM, G, F, H, W)
+  hipLaunchKernelGGL(win_feat_bwd_kernel<FM_>, grid, dim3(NTB), 0, s, feat, feat_bstride, multiM, gw, d, K, gfeat, \
+                     gfeat_bstride, rm, G, F, H, W)
   if (F <= 4)
     WIN_FEAT_BWD(4);
   else if (F <= 12)
@@ -530,7 +569,8 @@ grr_status grr_win_bwd_edge_weights(const float* feat, int64_t feat_bstride, con
   else
     WIN_FEAT_BWD(GRR_MAX_NODE_FTS);
 #undef WIN_FEAT_BWD
-  return launch_status("grr_win_bwd_edge_weights");
+  st = launch_status("grr_win_bwd_edge_weights");
+  return st != GRR_OK ? st : rs.finish("grr_win_bwd_edge_weights");
 }
 
 grr_status grr_win_bwd_mix(const float* gout, const float* x, const float* score, float* gx, float* gscore, int B,

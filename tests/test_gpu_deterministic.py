@@ -164,3 +164,52 @@ def test_msgf_training_gradients_bitwise(irdu):
         runs.append([p.grad.clone() for p in m.parameters()])
     for (name, _), a, b in zip(m.named_parameters(), *runs):
         assert torch.equal(a, b), name
+
+
+def test_window_reverse_reductions_bitwise(K):
+    """The window-graph reverse (taps, per-graph scalars, multiM) and the sub-API reverses are fixed-order
+    too."""
+    torch.manual_seed(9)
+    b, G, fs, f, h, w_ = 2, 3, 3, 4, 21, 37
+    delta = ((-1, 0), (0, -1), (0, 1), (1, 0), (-1, -1), (1, 1), (-2, 0), (0, 2))
+    k = len(delta)
+    s = torch.randn(b, G, fs, h, w_, device=DEV)
+    bt = torch.randn_like(s)
+    wt = torch.softmax(torch.randn(b, G, k, h, w_, device=DEV), dim=2)
+    sc = torch.rand(G, device=DEV) + 0.5
+    lg = torch.log(torch.full((G,), 0.05, device=DEV))
+    feat = torch.randn(b, G * f, h, w_, device=DEV)
+    M = torch.rand(G, f, device=DEV) + 0.5
+
+    def run():
+        gw = torch.zeros_like(wt)
+        gdot, ggam, gt = torch.zeros(G, device=DEV), torch.zeros(G, device=DEV), torch.zeros(5, device=DEV)
+        o, gs = K.win_bwd_gtv(s, bt, wt, delta, True, lg, sc, 0.7, gw, gdot, ggam, G)
+        l, gs2 = K.win_bwd_glr(s, bt, wt, delta, sc, -1.0, gw, gdot, G)
+        K.win_bwd_tapgrad(bt, o, K.WTAP_T, G, sc, gt)
+        gfeat, gM = torch.zeros_like(feat), torch.zeros(G, f, device=DEV)
+        K.win_bwd_edge_weights(feat, 0, G, f, M, wt, gw.clone(), delta, gfeat, gM)
+        return o, gs, l, gs2, gw, gdot, ggam, gt, gfeat, gM
+
+    a, bb = _twice(run)
+    _equal(a, bb, ["o", "gs", "l", "gs2", "gw", "gdot", "ggamma", "gtaps", "gfeat", "gmultiM"])
+
+
+def test_subapi_reverse_reductions_bitwise(K):
+    torch.manual_seed(12)
+    b, G, f, h, w_ = 2, 4, 3, 19, 23
+    x5 = torch.randn(b, G, f, h, w_, device=DEV)
+    g = torch.randn_like(x5)
+    M = torch.rand(G, f, device=DEV) + 0.5
+    p = [torch.rand(G * f, device=DEV) for _ in range(4)]      # p01, p02a, p02b, p03 per channel
+    st = K.Stencil(*[t.data_ptr() for t in p])
+
+    def run():
+        gM = torch.zeros(G, f, device=DEV)
+        gf = K.normalize_features_bwd(x5, M, g, gM)
+        gt = torch.zeros(G * f, 5, device=DEV)
+        gx = K.stats_conv_bwd(x5, st, False, g, gt)
+        return gf, gM, gx, gt
+
+    a, bb = _twice(run)
+    _equal(a, bb, ["gf", "gmultiM", "gx", "gtaps"])
