@@ -625,6 +625,34 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     return out
 
 
+def lnb_gate_keepable(c: int, hid: int, h: int, w: int) -> bool:
+    """lnb_forward_keep's shapes: the C <= 128 head + mix pipeline in one band (its workspace starts
+    with the gated activation g [B, hid, H, W])."""
+    return 2 <= c <= 128 and _lnb_band_rows(c, hid, h, w) >= h
+
+
+def lnb_forward_keep(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
+                     skip: Tensor) -> Tuple[Tensor, Tensor]:
+    """lnb_forward that also returns the head's gated activation g = sigmoid(m) m v,
+    [B, hid, H, W] (a view of the launch's workspace), for the training reverse's W2 weight gradient."""
+    dev = _check("lnb_forward_keep", x, ln_w, w1, wdw, w2, skip)
+    b, c, h, w = x.shape
+    hid = w2.shape[1]
+    if not lnb_gate_keepable(c, hid, h, w):
+        raise ValueError("lnb_forward_keep: needs C <= 128 and one band")
+    nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
+    ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+    out = torch.empty_like(x)
+    args = (x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
+            out.data_ptr(), ws.data_ptr(), b, c, hid, h, w, _stream(dev))
+    if _lnb_split(c):
+        _lnb_timed_parts("grr_lnb_forward", args, b * h * w, c, c, hid, c)
+    else:
+        _launch("lnb", 4 * b * h * w * (3 * c + 2 * hid), "grr_lnb_forward", *args,
+                flops=lnb_flops(b * h * w, c, c, hid))
+    return out, ws[:b * hid * h * w].view(b, hid, h, w)
+
+
 def lnb_forward_rep(src: Tensor, x: Optional[Tensor], ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor,
                     skip: Tensor) -> Tensor:
     """LocalNonLinearBlock forward when its input [B, R*Cs, H, W] is R copies of src [B, Cs, H, W];

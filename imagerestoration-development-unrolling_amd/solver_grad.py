@@ -25,11 +25,13 @@ from __future__ import annotations
 from typing import List, Optional, Tuple
 
 import os
+import weakref
 
 import torch
 
 from . import kernels as K
 from ._native import Stencil
+from . import train_ops
 from .train_ops import OpaqueFunction
 
 Tensor = torch.Tensor
@@ -702,11 +704,38 @@ def _mat(w: Tensor, rows: int) -> Tensor:
 # out = s0 x + s1 W2 gate(dw3x3(W1 LN(x))): fused HIP forward; the reverse recomputes n, h, h', gate
 # with HIP kernels and runs the adjoints (GEMMs: HIP conv1x1 for the data gradients, one library GEMM
 # per weight gradient)
+# The eager forward keeps the head's gated activation g (a view of the launch's workspace) for the
+# reverse's W2 weight gradient, which then skips recomputing the depthwise + gate.  g costs hid floats
+# per pixel, so the gates alive at once are capped (KEEP_GATE_BYTES: all of the msgf step's, a few of
+# the C4 shape's, whose step already holds ~135 GB); a kept gate leaves the budget when its tensor is
+# freed.  Compiled graphs always recompute (the custom op's saved list is fixed).
+KEEP_GATE = True
+KEEP_GATE_BYTES = 8 << 30
+_KEPT = [0]
+
+
+def _unkeep(nbytes: int) -> None:
+    _KEPT[0] -= nbytes
+
+
+def _lnb_keeps_gate(x: Tensor, w2: Tensor) -> bool:
+    b, c, h, w = x.shape
+    return KEEP_GATE and FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w) and K.lnb_gate_keepable(c, w2.shape[1], h, w)
+
+
 def _lnb_fwd(consts, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor):
     c, hid2 = x.shape[1], w1.shape[0]
-    out = K.lnb_forward(x.contiguous(), ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(),
-                        _mat(wdw, hid2).contiguous(), _mat(w2, c).contiguous(), skip.contiguous())
-    return [out], []
+    args = (x.contiguous(), ln_w.reshape(c).contiguous(), _mat(w1, hid2).contiguous(), _mat(wdw, hid2).contiguous(),
+            _mat(w2, c).contiguous(), skip.contiguous())
+    if consts and consts[0] and _lnb_keeps_gate(x, w2):
+        b, _, h, w = x.shape
+        nbytes = 4 * b * w2.shape[1] * h * w
+        if _KEPT[0] + nbytes <= KEEP_GATE_BYTES:
+            out, gate = K.lnb_forward_keep(*args)
+            _KEPT[0] += nbytes
+            weakref.finalize(gate, _unkeep, nbytes)
+            return [out], [gate]
+    return [K.lnb_forward(*args)], []
 
 
 def _lnb_fake(consts, x: Tensor, *weights: Tensor):
@@ -728,7 +757,7 @@ def _lnb_bwd(consts, inputs, outs, saved, gouts, needs):
     rows = FUSED_GATE_DW3 and K.lnb_gate_dw3_ok(h, w)
     if rows:
         hp = None
-        gate = K.lnb_dw3_gate(hh, Wdw)
+        gate = saved[0] if saved else K.lnb_dw3_gate(hh, Wdw)
     else:
         hp = K.dwconv3(hh, Wdw)
         gate, _ = K.lnb_gate(hp)
@@ -764,7 +793,9 @@ LNB = OpaqueFunction("lnb_train", 1, _lnb_fwd, _lnb_bwd, _lnb_fake)
 class LNBFn:
     @staticmethod
     def apply(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor) -> Tensor:
-        return LNB([], x, ln_w, w1, wdw, w2, skip)
+        # consts [1]: the eager forward may keep the gate (a compiled graph's saved list must not vary)
+        eager = not (train_ops.FORCE_OPS or torch.compiler.is_compiling())
+        return LNB([1 if eager else 0], x, ln_w, w1, wdw, w2, skip)
 
 
 # ---- FFBlock of the window models' feature CNN (REF7:13-67), training --------------------------

@@ -143,3 +143,43 @@ def test_training_level_streams_match_one_stream(irdu, model):
     finally:
         SG.LEVEL_STREAMS = saved
     _assert_steps_close(g1, g2, w1, w2, bitwise=model == "msgf")
+
+
+@pytest.mark.parametrize("model", ["msgf", "abstract"])
+def test_lnb_kept_gate_matches_recompute(irdu, model):
+    """solver_grad.KEEP_GATE: the eager LocalNonLinearBlock forward keeps the head's gated activation for
+    the reverse's W2 weight gradient instead of recomputing depthwise + gate from W1 LN(x).  The kept
+    gate comes from the fused head (fp16 two-term GEMM1), the recomputed one from the split-bf16 1x1
+    GEMM: equal to fp32 accuracy, so the gradients agree to 1e-5 relative."""
+    import torch.nn.functional as F
+    from irdu_amd import solver_grad as SG
+
+    def build():
+        if model == "msgf":
+            return irdu.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=4)
+        return irdu.AbtractMultiScaleGraphFilter(
+            3, 3, dims=[8, 16, 16, 32], hidden_dims=[16, 32, 32, 64], nsubnets=[1, 1, 1, 1], ngraphs=[2, 4, 4, 8],
+            num_blocks=[1, 1, 1, 1], num_blocks_out=1, n_cgd_iters=3)
+
+    def run(keep):
+        SG.KEEP_GATE = keep
+        torch.manual_seed(13)
+        m = build().to(DEV).train()
+        g = torch.Generator().manual_seed(6)
+        x = torch.rand(2, 3, 64, 64, generator=g).to(DEV)
+        t = torch.rand(2, 3, 64, 64, generator=g).to(DEV)
+        F.l1_loss(m(x), t).backward()
+        torch.cuda.synchronize()
+        return [p.grad.clone() if p.grad is not None else None for p in m.parameters()], SG._KEPT[0]
+
+    saved = SG.KEEP_GATE
+    try:
+        (g0, _), (g1, kept_after) = run(False), run(True)
+    finally:
+        SG.KEEP_GATE = saved
+    assert kept_after == 0          # every kept gate left the budget with its saved tensor
+    for a, b in zip(g1, g0):
+        if b is None:
+            assert a is None
+            continue
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
