@@ -904,6 +904,11 @@ __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
 // L1/L2 and runs at ≈ 1.7 TB/s).
 // ---------------------------------------------------------------------------
 int g_term_rows = 1;   // grr_bwd_set_term_rows: 0 = per-pixel term reverses (A/B and tests)
+// gw planes per wave whose read-modify-write row is read before the row's arithmetic (0: after the
+// partials' barrier, round 3)
+#ifndef GRR_TERM_EARLY_GW
+#define GRR_TERM_EARLY_GW 2
+#endif
 
 template <int V> struct RowT;
 template <> struct RowT<1> { typedef float T; };
@@ -1091,6 +1096,16 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     float w1n = 0.f, w2p = 0.f, c0p = 0.f;
     if constexpr (MODE == 1) c0p = lprev(W0[0][V - 1]);
     else { w1n = lnext(W1[0]); w2p = lprev(W2[V - 1]); }
+    // the gw rows this wave adds into below (planes f, f + F < WPL), read now: their latency overlaps
+    // this row's arithmetic instead of following the partials' barrier (every row's gw is read and
+    // written by this workgroup only, in this step)
+    constexpr int KE = GRR_TERM_EARLY_GW;
+    float cur[KE > 0 ? KE : 1][V];
+#pragma unroll
+    for (int k = 0; k < KE; ++k) {
+      const int e = f + k * F;
+      if (e < WPL && on) rload<V>(cur[k], gwb + e * HW + (int64_t)r * W);
+    }
     float vrow[V], gwa[WPL][V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -1188,7 +1203,10 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
 #pragma unroll
     for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
     __syncthreads();
-    for (int e = f; e < WPL; e += F) {
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+      const int e = f + k * F;
+      if (e >= WPL) break;
       float sum[V];
       rload<V>(sum, part(par, 0, e) + lc0);
       for (int ff = 1; ff < F; ++ff) {
@@ -1199,15 +1217,20 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       }
       if (on) {
         float* dst = gwb + e * HW + (int64_t)r * W;
-        float cur[V];
-        rload<V>(cur, dst);
+        float cv[V];
+        if (k < KE) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) cv[j] = cur[k < KE ? k : 0][j];
+        } else {
+          rload<V>(cv, dst);   // F = 1: planes 2, 3 of the single wave
+        }
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           const int col = c0 + j;
           const bool keep = MODE != 1 || (e == 0 ? col + 1 < W : r + 1 < H);
-          if (keep) cur[j] += sc * sum[j];
+          if (keep) cv[j] += sc * sum[j];
         }
-        rstore<V>(dst, cur);
+        rstore<V>(dst, cv);
       }
     }
     par ^= 1;
@@ -1536,15 +1559,25 @@ int chunks_for(int64_t n, int64_t planes) {
 }
 int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + NT - 1) / NT, 1 << 16); }
 
-// dst[i] += sum_s part[i][s], slots in order: lane l adds slots l, l + 64, ... in order, then the
-// fixed shuffle tree.   grid (n), one wave per value
-__global__ __launch_bounds__(64) void red_finish_kernel(const float* __restrict__ part, uint32_t nslot,
-                                                        float* __restrict__ dst) {
-  const float* row = part + (size_t)blockIdx.x * nslot;
+// dst[i] += sum_s part[i][s] for every planned reduction of a launch, slots in order: lane l adds
+// slots l, l + 64, ... in order, then the fixed shuffle tree.   grid (sum of n), one wave per value
+struct RedFinishArgs {
+  const float* part[RedScratch::kMax];
+  float* dst[RedScratch::kMax];
+  uint32_t nslot[RedScratch::kMax];
+  int first[RedScratch::kMax + 1];   // value ranges of the reductions in the grid
+  int k;
+};
+__global__ __launch_bounds__(64) void red_finish_kernel(RedFinishArgs a) {
+  int i = 0;
+  while (i + 1 < a.k && (int)blockIdx.x >= a.first[i + 1]) ++i;
+  const int idx = blockIdx.x - a.first[i];
+  const uint32_t nslot = a.nslot[i];
+  const float* row = a.part[i] + (size_t)idx * nslot;
   float v = 0.f;
   for (uint32_t s = threadIdx.x; s < nslot; s += 64) v += row[s];
   v = wave_sum(v);
-  if (threadIdx.x == 0) dst[blockIdx.x] += v;
+  if (threadIdx.x == 0) a.dst[i][idx] += v;
 }
 
 }  // namespace
@@ -1597,18 +1630,24 @@ grr_status RedScratch::alloc(const char* what) {
       part_[i] = p;
       p += (size_t)n_[i] * nslot_[i];
     }
-  e = hipMemsetAsync(base_, 0, total * sizeof(float), s_);
-  if (e != hipSuccess) {
-    set_error("%s: reduction scratch fill: %s", what, hipGetErrorString(e));
-    return GRR_ERR_HIP;
-  }
+  // no fill: every contributor of a launch stores its slot (zero partials included)
   return GRR_OK;
 }
 
 grr_status RedScratch::finish(const char* what) {
+  RedFinishArgs a{};
+  int total = 0;
   for (int i = 0; i < k_; ++i)
-    if (dst_[i] && part_[i] && n_[i] > 0)
-      hipLaunchKernelGGL(red_finish_kernel, dim3(n_[i]), dim3(64), 0, s_, part_[i], nslot_[i], dst_[i]);
+    if (dst_[i] && part_[i] && n_[i] > 0) {
+      a.part[a.k] = part_[i];
+      a.dst[a.k] = dst_[i];
+      a.nslot[a.k] = nslot_[i];
+      a.first[a.k] = total;
+      total += n_[i];
+      ++a.k;
+    }
+  a.first[a.k] = total;
+  if (total > 0) hipLaunchKernelGGL(red_finish_kernel, dim3(total), dim3(64), 0, s_, a);
   grr_status st = launch_status(what);
   if (base_) {
     const hipError_t e = hipFreeAsync(base_, s_);

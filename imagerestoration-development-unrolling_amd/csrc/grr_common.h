@@ -70,8 +70,9 @@ __device__ __forceinline__ void red_put(const Red& r, int idx, uint32_t slot, fl
 
 // Host side: the partial arrays of one launch, carved from one stream-ordered allocation
 // (hipMallocAsync from the device's default pool, whose release threshold is raised once, so the
-// steady state reuses pool memory; capturable in a HIP graph), zero-filled, then finished and freed
-// on the same stream.
+// steady state reuses pool memory; capturable in a HIP graph), then finished (one launch for all of
+// them) and freed on the same stream.  Every kernel stores every slot of its plan (zero partials
+// included), so the scratch needs no fill.
 class RedScratch {
  public:
   static constexpr int kMax = 4;
