@@ -904,11 +904,6 @@ __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
 // L1/L2 and runs at ≈ 1.7 TB/s).
 // ---------------------------------------------------------------------------
 int g_term_rows = 1;   // grr_bwd_set_term_rows: 0 = per-pixel term reverses (A/B and tests)
-// gw planes per wave whose read-modify-write row is read before the row's arithmetic (0: after the
-// partials' barrier, round 3)
-#ifndef GRR_TERM_EARLY_GW
-#define GRR_TERM_EARLY_GW 2
-#endif
 
 template <int V> struct RowT;
 template <> struct RowT<1> { typedef float T; };
@@ -1096,16 +1091,6 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     float w1n = 0.f, w2p = 0.f, c0p = 0.f;
     if constexpr (MODE == 1) c0p = lprev(W0[0][V - 1]);
     else { w1n = lnext(W1[0]); w2p = lprev(W2[V - 1]); }
-    // the gw rows this wave adds into below (planes f, f + F < WPL), read now: their latency overlaps
-    // this row's arithmetic instead of following the partials' barrier (every row's gw is read and
-    // written by this workgroup only, in this step)
-    constexpr int KE = GRR_TERM_EARLY_GW;
-    float cur[KE > 0 ? KE : 1][V];
-#pragma unroll
-    for (int k = 0; k < KE; ++k) {
-      const int e = f + k * F;
-      if (e < WPL && on) rload<V>(cur[k], gwb + e * HW + (int64_t)r * W);
-    }
     float vrow[V], gwa[WPL][V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -1203,10 +1188,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
 #pragma unroll
     for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < WPL; ++k) {
-      const int e = f + k * F;
-      if (e >= WPL) break;
+    for (int e = f; e < WPL; e += F) {
       float sum[V];
       rload<V>(sum, part(par, 0, e) + lc0);
       for (int ff = 1; ff < F; ++ff) {
@@ -1218,12 +1200,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       if (on) {
         float* dst = gwb + e * HW + (int64_t)r * W;
         float cv[V];
-        if (k < KE) {
-#pragma unroll
-          for (int j = 0; j < V; ++j) cv[j] = cur[k < KE ? k : 0][j];
-        } else {
-          rload<V>(cv, dst);   // F = 1: planes 2, 3 of the single wave
-        }
+        rload<V>(cv, dst);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           const int col = c0 + j;
