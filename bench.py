@@ -110,8 +110,13 @@ def load_traffic(kernel, batch):
 
 
 def load_traffic_file(name, kernel_prefix, batch):
-    """Per-launch HBM bytes (mean over the bench's launches of that kernel) from profiles/r03/."""
-    return _traffic(os.path.join(ROOT, "profiles", "r03", name), kernel_prefix, batch)
+    """Per-launch HBM bytes (mean over the bench's launches of that kernel): the newest round's summary
+    under profiles/ of this workload."""
+    for rnd in ("r04", "r03"):
+        t = _traffic(os.path.join(ROOT, "profiles", rnd, name), kernel_prefix, batch)
+        if t is not None:
+            return t
+    return None
 
 
 def host_cpus():
@@ -339,6 +344,17 @@ def main():
                 "mfma_tflops": round(mx["tflops"], 2), "mfma_peak": round(SPLIT_BF16_PEAK_TFLOPS, 1),
                 "traffic": load_traffic_file("traffic_lnb_mix.json", "lnb_mix_kernel", b),
                 "note": "algorithmic bytes (g + skip operand + out) / HIP-event time; W2 on 6 bf16 products"}}
+        if "lnb_rep_fused" in kern:   # the first block, on the replicated RGB input: one fused pass
+            rp = kern["lnb_rep_fused"]
+            res["roofline_secondary"]["lnb_rep_fused"] = {
+                "bound": "mfma", "kernel": "lnb_rep_kernel (+ lnb_rep_pack_kernel)",
+                "achieved": round(rp["tflops"], 2), "peak": round(SPLIT_F16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
+                "frac": round(rp["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": rp["flops_per_launch"],
+                "mean_launch_ms": round(rp["mean_ms"], 4), "launches": rp["launches"],
+                "hbm_gbps": round(rp["gbps"], 1), "bytes_per_launch": rp["bytes_per_launch"],
+                "note": "algorithmic fp32 flops (LN, W1, depthwise, gate, W2, skip) / HIP-event time against the "
+                        "dense fp16 rate / 3 (both GEMMs on exact fp16 two-term splits; the depthwise folded into "
+                        "GEMM1 as a 27-deep im2col operand); bytes: src in, out written"}
     kernels_ms = {k: round(v["total_ms"] / n_inst, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms
     if args.breakdown:

@@ -706,11 +706,12 @@ def _mat(w: Tensor, rows: int) -> Tensor:
 # per weight gradient)
 # The eager forward keeps the head's gated activation g (a view of the launch's workspace) for the
 # reverse's W2 weight gradient, which then skips recomputing the depthwise + gate.  g costs hid floats
-# per pixel, so the gates alive at once are capped (KEEP_GATE_BYTES: all of the msgf step's, a few of
-# the C4 shape's, whose step already holds ~135 GB); a kept gate leaves the budget when its tensor is
-# freed.  Compiled graphs always recompute (the custom op's saved list is fixed).
+# per pixel, so the gates alive at once are capped (KEEP_GATE_BYTES, 32 GB: all of the msgf step's,
+# about three quarters of the C4 shape's C <= 128 blocks, whose step already holds ~142 GB of the
+# 288); a kept gate leaves the budget when its tensor is freed.  Compiled graphs always recompute (the
+# custom op's saved list is fixed).
 KEEP_GATE = True
-KEEP_GATE_BYTES = 8 << 30
+KEEP_GATE_BYTES = 32 << 30
 _KEPT = [0]
 
 

@@ -10,7 +10,7 @@ rc=$?; tail -3 $out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 bash scripts/pmc_bench.sh 64 > $out/pmc.log 2>&1 || { tail -20 $out/pmc.log; exit 1; }
 tail -14 $out/pmc.log
 cp gpurun_out/pmcb/traffic_system_step2.json profiles/traffic_system_step2.json
-cp gpurun_out/pmcb/traffic_lnb_head16.json gpurun_out/pmcb/traffic_lnb_mix.json profiles/r03/
+
 cp gpurun_out/pmcb/bench_kernel_stats.csv $out/
 timeout -k 10 600 python -u bench.py > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
 tail -c 3000 $out/bench.json

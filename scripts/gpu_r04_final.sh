@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-4 evidence: full GPU suite, smoke(), PMC HBM traffic + rocprofv3 kernel summary of the bench's own
+# launches at the bench batch, the default bench line, the training lines
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+out=gpurun_out/r04final; mkdir -p $out
+export TMPDIR=/tmp
+MIOPEN_FIND_MODE=FAST timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread \
+  -p no:cacheprovider > $out/gpu_tests.log 2>&1
+rc=$?; tail -3 $out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 \
+  || { tail -20 $out/smoke.log; exit 1; }
+tail -1 $out/smoke.log
+timeout -k 10 800 bash scripts/pmc_bench.sh 64 > $out/pmc.log 2>&1 || { tail -20 $out/pmc.log; exit 1; }
+tail -14 $out/pmc.log
+cp gpurun_out/pmcb/traffic_*.json gpurun_out/pmcb/bench_kernel_stats.csv $out/
+mkdir -p profiles/r04   # this box's tree: the bench line below reads the fresh summaries (committed afterwards)
+cp gpurun_out/pmcb/traffic_system_step2.json profiles/
+cp gpurun_out/pmcb/traffic_lnb_*.json profiles/r04/
+timeout -k 10 600 python -u bench.py > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
+tail -c 1500 $out/bench.json
+timeout -k 10 200 python -u bench_train.py --model msgf --batch 16 --steps 6 --warmup 2 --no-cpu-baseline \
+  > $out/train_msgf.json 2> $out/train_msgf.err || { tail $out/train_msgf.err; exit 1; }
+timeout -k 10 300 python -u bench_train.py --model abstract --batch 8 --steps 5 --warmup 2 --no-cpu-baseline \
+  > $out/train_abstract.json 2> $out/train_abstract.err || { tail $out/train_abstract.err; exit 1; }
+timeout -k 10 600 python -u bench_train.py --model abstract --size 512 --batch 32 --steps 3 --warmup 1 --no-cpu-baseline \
+  > $out/train_c4.json 2> $out/train_c4.err || { tail $out/train_c4.err; exit 1; }
+for f in train_msgf train_abstract train_c4; do echo "$f $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"peak_mem_gb": [0-9.]*' $out/$f.json | tr '\n' ' ')"; done
