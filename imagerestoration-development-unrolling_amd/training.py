@@ -27,6 +27,7 @@ is kept for real data.  Samples are (noisy, clean) HWC float32 like the referenc
 from __future__ import annotations
 
 import argparse
+import json
 import logging
 import math
 import os
@@ -503,13 +504,61 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
     return trainer
 
 
+def log_files_dir(conf: dict) -> str:
+    return os.path.join(conf["path"]["root_dir"], "experiments", conf["name"], "log_files")
+
+
+def plumbing(conf: dict) -> dict:
+    """The reference's run_train.py main (:38-121) as it stands, for config C1 on a host without a GPU:
+    find the latest checkpoint of the experiment (only its path: nothing is unpickled), create the
+    checkpoint and log-file folders of a fresh run, log the configuration to
+    experiments/<name>/log_files/run_train_<name>.log, and build the training dataset, the resumable
+    sampler and the dataloader.  Like the reference it builds no model; returns the pieces."""
+    ckpt = latest_checkpoint(conf)
+    if ckpt:
+        conf["path"]["latest_checkpoint_path"] = ckpt
+    else:
+        os.makedirs(checkpoint_dir(conf), exist_ok=True)
+        conf["path"]["checkpoints_folder"] = checkpoint_dir(conf)
+        os.makedirs(log_files_dir(conf), exist_ok=True)
+        conf["path"]["log_files_folder"] = log_files_dir(conf)
+    logger = logging.getLogger(conf["name"])
+    logger.setLevel(logging.INFO)
+    log_dir = conf["path"].get("log_files_folder") or log_files_dir(conf)
+    os.makedirs(log_dir, exist_ok=True)
+    fh = logging.FileHandler(os.path.join(log_dir, f"run_train_{conf['name']}.log"))
+    fh.setFormatter(logging.Formatter("%(asctime)s %(levelname)s: %(message)s"))
+    logger.addHandler(fh)
+    try:
+        logger.info("environ_conf=%s", json.dumps(conf, indent=1, default=str))
+        ds_conf = conf["datasets"]["train"]
+        dataset = create_dataset(ds_conf, conf)
+        sampler = ResumeableSampler(dataset, int(ds_conf["dataloader_args"].get("batch_size", 1)))
+        loader = create_dataloader(dataset, sampler, ds_conf, conf)
+        logger.info("train dataset: %d samples", len(dataset))
+    finally:
+        logger.removeHandler(fh)
+        fh.close()
+    return {"latest_checkpoint_path": ckpt, "dataset": dataset, "sampler": sampler, "dataloader": loader}
+
+
 def main(argv: Optional[Sequence[str]] = None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("-yaml_path", type=str, required=True, help="Path to option YAML file.")
     ap.add_argument("-max_iters", type=int, default=None)
+    ap.add_argument("-plumbing_only", action="store_true",
+                    help="the reference run_train.py's steps only (no model); the default without a GPU")
     args = ap.parse_args(argv)
     conf = parse_options(args.yaml_path)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s: %(message)s")
+    if args.plumbing_only or not torch.cuda.is_available():
+        # config C1 (BASELINE.md: PyTorch-CPU plumbing): the reference's script stops before any model;
+        # the HIP model itself needs an MI355X
+        parts = plumbing(conf)
+        LOG.info("plumbing only (%s): %d training samples, latest checkpoint %s",
+                 "no GPU" if not torch.cuda.is_available() else "-plumbing_only", len(parts["dataset"]),
+                 parts["latest_checkpoint_path"])
+        return None
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1 and not torch.distributed.is_initialized():
         backend = "nccl" if torch.cuda.is_available() else "gloo"
         if torch.cuda.is_available():

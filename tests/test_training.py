@@ -367,3 +367,25 @@ def test_validation_sharded_over_ranks_equals_one_process():
     torch.manual_seed(0)
     one = T.validate(TinyModel(), T.SyntheticTestImages(n_images=5, height=36, width=52), device=torch.device("cpu"))
     assert res[0] == pytest.approx(one, rel=1e-12) and res[1] == pytest.approx(one, rel=1e-12)
+
+
+def test_run_train_plumbing_without_gpu(tmp_path):
+    """Config C1 as BASELINE.md states it (PyTorch-CPU plumbing, no GPU): on a host without a GPU,
+    run_train.py does what the reference's run_train.py:38-121 does -- latest-checkpoint discovery,
+    experiment folders, the config logged to log_files/run_train_<name>.log, dataset + resumable sampler
+    + dataloader -- and returns without building a model."""
+    import yaml as _yaml
+    from irdu_amd import training as T
+    conf = _yaml.safe_load(open(os.path.join(ROOT, "experiment_conf", "example.yaml")))
+    conf["path"]["root_dir"] = str(tmp_path)
+    conf["datasets"]["train"]["dataset_args"]["max_num_patchs"] = 8
+    path = tmp_path / "c1.yaml"
+    path.write_text(_yaml.safe_dump(conf))
+    assert T.main(["-yaml_path", str(path), "-plumbing_only"]) is None
+    exp = tmp_path / "experiments" / conf["name"]
+    assert (exp / "learning_checkpoints").is_dir()
+    log = (exp / "log_files" / f"run_train_{conf['name']}.log").read_text()
+    assert "environ_conf=" in log and "train dataset: 8 samples" in log
+    parts = T.plumbing(T.parse_options(str(path)))
+    noisy, clean = next(iter(parts["dataloader"]))
+    assert noisy.shape == clean.shape and parts["latest_checkpoint_path"] is None
