@@ -1236,8 +1236,16 @@ int term_row_vec(int W) {
   if (W <= 256 && W % 4 == 0) return 4;
   return 0;
 }
-// the term reverse also runs W > 256 (W % 4 == 0) as column strips of 4-wide lanes
-int term_strip_vec(int W) { return term_row_vec(W) ? term_row_vec(W) : (W % 4 == 0 ? 4 : 0); }
+// the term reverse also runs W > 256 as column strips of GRR_TERM_WIDE_V-wide lanes (the term's reach is
+// two columns: V >= 2)
+#ifndef GRR_TERM_WIDE_V
+#define GRR_TERM_WIDE_V 4
+#endif
+static_assert(GRR_TERM_WIDE_V == 2 || GRR_TERM_WIDE_V == 4, "strip lanes: 2 or 4 columns");
+int term_strip_vec(int W) {
+  if (term_row_vec(W)) return term_row_vec(W);
+  return W % GRR_TERM_WIDE_V == 0 ? GRR_TERM_WIDE_V : (W % 4 == 0 ? 4 : 0);
+}
 // The same reverse as a row-streaming kernel (W <= 64 V, F in {1, 2, 3, 4, 6}): one wave = one
 // (b, graph) and a segment of rows, lane = V adjacent columns.  Feature rows r-1..r+1 of the F
 // channels, their inverse norms and gsim (4 planes) stay in registers; horizontal neighbours
