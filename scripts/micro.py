@@ -91,6 +91,14 @@ def main():
         gw, gdot, gt = torch.zeros_like(wt), torch.zeros(g, device=dev), torch.zeros_like(taps)
         ggam = torch.zeros(g, device=dev) if mode == 2 else None
         fn = lambda: K.bwd_term_fused(mode, x, gg, taps, wt, lg, sc, 0.5, gw, ggam, gdot, gt, g)  # noqa: E731
+    elif args.kernel == "gate_dw3_bwd":   # LNB training reverse: gate + depthwise adjoint, hid = --fts
+        hid = args.fts
+        hh = torch.randn(b, 2 * hid, h, w, device=dev)
+        gq = torch.randn(b, hid, h, w, device=dev)
+        wdw = torch.randn(2 * hid, 1, 3, 3, device=dev)
+        sc = torch.tensor([0.7], device=dev)
+        gwdw, gdot = torch.zeros_like(wdw), torch.zeros(1, device=dev)
+        fn = lambda: K.lnb_gate_dw3_bwd(None, gq, sc, hh, wdw, gwdw, gdot)  # noqa: E731
     elif args.kernel == "edge":
         feat = torch.rand(b, 2 * c, h, w, device=dev)
         fn = lambda: K.edge_weights(feat, 0, g, f, p(mix.GTVmodule00.multiM))  # noqa: E731
