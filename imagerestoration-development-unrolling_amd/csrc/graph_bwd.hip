@@ -1236,15 +1236,15 @@ int term_row_vec(int W) {
   if (W <= 256 && W % 4 == 0) return 4;
   return 0;
 }
-// the term reverse also runs W > 256 as column strips of GRR_TERM_WIDE_V-wide lanes (the term's reach is
-// two columns: V >= 2)
-#ifndef GRR_TERM_WIDE_V
-#define GRR_TERM_WIDE_V 4
-#endif
-static_assert(GRR_TERM_WIDE_V == 2 || GRR_TERM_WIDE_V == 4, "strip lanes: 2 or 4 columns");
-int term_strip_vec(int W) {
+// W > 256 runs as column strips (the term's reach is two columns: lanes of V >= 2 columns, a V-column
+// halo per side).  The GLR and prox terms on 2-column lanes (124 owned columns per strip: 640 columns
+// loaded for W = 512 against 768 with 4-column lanes, and 128 VGPRs, four waves per SIMD), the pair term
+// on 4-column lanes (measured, B32 G8 F6 512^2: GLR 4.15 -> 3.64 ms, prox 6.69 -> 4.61, pair 2.88 -> 3.33;
+// profiles/r04/term/ab_wide_v.txt); the edge-weight reverse on 4-column lanes
+int term_strip_vec(int W, int mode = 1) {
   if (term_row_vec(W)) return term_row_vec(W);
-  return W % GRR_TERM_WIDE_V == 0 ? GRR_TERM_WIDE_V : (W % 4 == 0 ? 4 : 0);
+  if (mode != 1 && W % 2 == 0) return 2;
+  return W % 4 == 0 ? 4 : 0;
 }
 // The same reverse as a row-streaming kernel (W <= 64 V, F in {1, 2, 3, 4, 6}): one wave = one
 // (b, graph) and a segment of rows, lane = V adjacent columns.  Feature rows r-1..r+1 of the F
@@ -1497,8 +1497,9 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
   if (st != GRR_OK) return st;
   return R.rs.finish("grr_bwd_term_fused");
 }
-bool term_row_ok(int F, const float* x, const float* g, const float* w, const float* v, const float* gw, int W) {
-  const int V = term_strip_vec(W);
+bool term_row_ok(int mode, int F, const float* x, const float* g, const float* w, const float* v, const float* gw,
+                 int W) {
+  const int V = term_strip_vec(W, mode);
   if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return false;
   const void* ptrs[] = {x, g, w, v, gw};
   for (const void* p : ptrs)
@@ -1509,7 +1510,7 @@ template <int MODE>
 grr_status launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
                              const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam,
                              float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
-  switch (term_strip_vec(W)) {
+  switch (term_strip_vec(W, MODE)) {
     case 1: return launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
     case 2: return launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
     default: return launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
@@ -1672,7 +1673,7 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
               GRR_ERR_INVALID_ARG, "grr_bwd_term_fused: bad args");
   hipStream_t s = (hipStream_t)stream;
   // row-streaming kernel where the shape allows
-  if (g_term_rows && (int64_t)B * G * H < (1ll << 31) && term_row_ok(F, x, g, w, v_out, gw, W)) {
+  if (g_term_rows && (int64_t)B * G * H < (1ll << 31) && term_row_ok(mode, F, x, g, w, v_out, gw, W)) {
     switch (mode) {
       case 0: return launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
       case 1: return launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);

@@ -18,7 +18,8 @@ for lib in $L exp/libgrr_dw2.so exp/libgrr_dw1.so; do
     --batch 32 --fts 96 --size 512 --iters 10 2>&1 | grep -v amdgpu.ids | tr '\n' ' ')" >> $out/micro.txt || exit 1
 done
 cat $out/micro.txt
-for lib in exp/libgrr_dw1.so exp/libgrr_dw2.so; do
+export MIOPEN_FIND_MODE=FAST   # the same convolution solutions for every variant, no per-box search
+for lib in $L exp/libgrr_dw1.so exp/libgrr_dw2.so; do
   n=$(basename $lib .so)
   GRR_LIB=$lib timeout -k 10 600 python -u bench_train.py --model abstract --size 512 --batch 32 --steps 3 --warmup 1 \
     --no-cpu-baseline > $out/c4_$n.json 2> $out/c4_$n.err || { tail $out/c4_$n.err; exit 1; }
