@@ -3,7 +3,7 @@
 # launches at the bench batch, the default bench line, the training lines
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-out=gpurun_out/r04final; mkdir -p $out
+out=gpurun_out/${R04_OUT:-r04final}; mkdir -p $out
 export TMPDIR=/tmp
 MIOPEN_FIND_MODE=FAST timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread \
   -p no:cacheprovider > $out/gpu_tests.log 2>&1
