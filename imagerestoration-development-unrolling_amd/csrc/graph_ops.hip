@@ -1130,6 +1130,10 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
 // w_up of row r+1, so it is written one row late.  Same arithmetic order as
 // edge_weights_kernel (REF:146-175).
 // ---------------------------------------------------------------------------
+// GRR_EDGE_FASTDIV (A/B build): hardware reciprocal and exp in the normalisation and the softmax
+#ifndef GRR_EDGE_FASTDIV
+#define GRR_EDGE_FASTDIV 0
+#endif
 #ifndef GRR_EDGE_MIN_WAVES
 #define GRR_EDGE_MIN_WAVES 8192
 #endif
@@ -1189,8 +1193,14 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
       // (a segment's first rows are normalised by the prologue, elsewhere by the loop)
       for (int f = 0; f < F; ++f) ss = __builtin_fmaf(raw[f][j], raw[f][j], ss);
       const float den = fmaxf(sqrtf(ss), 1e-12f);
+#if GRR_EDGE_FASTDIV
+      const float rd = __builtin_amdgcn_rcpf(den);
+#pragma unroll
+      for (int f = 0; f < F; ++f) dst[f][j] = (raw[f][j] * rd) * M[f];
+#else
 #pragma unroll
       for (int f = 0; f < F; ++f) dst[f][j] = (raw[f][j] / den) * M[f];
+#endif
     }
   };
   load_raw(r0 - 1);                                  // clamped: row 0 is its own up neighbour
@@ -1225,9 +1235,16 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
         s3 += v * fN[f][j];
       }
       const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
+#if GRR_EDGE_FASTDIV
+      const float e0 = __expf(s0 - m), e1 = __expf(s1 - m), e2 = __expf(s2 - m), e3 = __expf(s3 - m);
+      const float sum = ((e0 + e1) + e2) + e3;
+      const float rs = __builtin_amdgcn_rcpf(sum);
+      w0[j] = e0 * rs; w1[j] = e1 * rs; w2[j] = e2 * rs; w3[j] = e3 * rs;
+#else
       const float e0 = expf(s0 - m), e1 = expf(s1 - m), e2 = expf(s2 - m), e3 = expf(s3 - m);
       const float sum = ((e0 + e1) + e2) + e3;
       w0[j] = e0 / sum; w1[j] = e1 / sum; w2[j] = e2 / sum; w3[j] = e3 / sum;
+#endif
     }
     const int64_t ro = (int64_t)r * W;
     if (lane_on && own) {
