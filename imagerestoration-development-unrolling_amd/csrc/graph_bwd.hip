@@ -945,6 +945,24 @@ __device__ __forceinline__ float lnext(float v) {   // lane + 1 (0 at lane 63)
 // VGPRs = 3 waves per SIMD, which also gives 4 three-wave workgroups per CU instead of 2 at the
 // 176-182 VGPRs the compiler picks unconstrained), up to 16 for V <= 2 (128 VGPRs).
 template <int V> struct TermRowMax { static constexpr int F = V == 4 ? 12 : 16; };
+// gw rows of the read-modify-write through LDS-DMA one row ahead (GRR_TERM_GW_DMA, default on): the
+// summing wave copies gw row r + 1 of its planes into an LDS ring right after adding row r, so the
+// next row's read-modify-write reads LDS instead of waiting on a global load after the partials'
+// barrier; no registers are held across the step (an early global read into VGPRs spilled, §4.r4)
+#ifndef GRR_TERM_GW_DMA
+#define GRR_TERM_GW_DMA 1
+#endif
+// Only where it measured faster (profiles/r04/term/ab_gw_dma.txt): not in GGTV's instance (MODE 2, the
+// register-heaviest: the ring costs it spills) nor in the one-strip 4-column instances (W = 256, 3-4 %
+// slower); 12 % faster at W = 128, 7 % at W = 512 (strips)
+__host__ __device__ constexpr bool term_gw_dma(int mode, int v, bool strips) {
+  return GRR_TERM_GW_DMA && mode != 2 && (strips || v < 4);
+}
+typedef __attribute__((address_space(3))) float* lds_f32_t;
+__device__ __forceinline__ void dma_dword(const float* src, float* lds_wave_base) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)lds_wave_base;
+  asm volatile("global_load_lds_dword %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v)) : "memory");
+}
 template <int MODE, int V, bool STRIPS = false>
 __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
@@ -952,9 +970,12 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     float* __restrict__ v_out, float* __restrict__ gw, Red ggam, Red gdot,
     Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
-  // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats)
+  constexpr bool kGwDma = term_gw_dma(MODE, V, STRIPS);
+  // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats),
+  // then (GRR_TERM_GW_DMA) the gw row ring [row parity][plane][element j][lane] (2 WPL 64 V floats)
   extern __shared__ __attribute__((aligned(16))) float part_dyn[];
   auto part = [&](int pr, int ff, int e) { return part_dyn + ((pr * F + ff) * WPL + e) * (64 * V); };
+  auto gring = [&](int pr, int e) { return part_dyn + (2 * F * WPL + pr * WPL + e) * (64 * V); };
   const int lane = threadIdx.x & 63;
   const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t unit = xcd_remap(blockIdx.x, nblk);
@@ -1046,6 +1067,13 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   xrow(X[3], r0 - 2);
   grow(Gr[3], r0 - 2);
   if constexpr (MODE != 1) wrow(W0[1], 0, r0 - 2);
+  // element j of the lane's V columns of gw row rr, plane e -> ring slot rr & 1 (lane-contiguous)
+  auto gw_dma = [&](int rr) {
+    for (int e = f; e < WPL; e += F)
+#pragma unroll
+      for (int j = 0; j < V; ++j) dma_dword(gwb + e * HW + (int64_t)rr * W + j, gring(rr & 1, e) + j * 64);
+  };
+  if constexpr (kGwDma) gw_dma(r0);
   prefetch(t0);
   int par = 0;
   for (int t = t0; t <= r1 + 1; ++t) {
@@ -1188,6 +1216,12 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
 #pragma unroll
     for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
     __syncthreads();
+    if constexpr (kGwDma) {
+      // gw row r landed: it was copied before this step's prefetch loads (>= 2 + WPL of them with the
+      // row store, at least the store without) -- the vector memory counter drains in order
+      if (t + 1 <= r1 + 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(MODE == 1 ? 4 : 6) : "memory");
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    }
     for (int e = f; e < WPL; e += F) {
       float sum[V];
       rload<V>(sum, part(par, 0, e) + lc0);
@@ -1200,7 +1234,13 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       if (on) {
         float* dst = gwb + e * HW + (int64_t)r * W;
         float cv[V];
-        rload<V>(cv, dst);
+        if constexpr (kGwDma) {
+          const float* sl = gring(r & 1, e) + lane;
+#pragma unroll
+          for (int j = 0; j < V; ++j) cv[j] = sl[j * 64];
+        } else {
+          rload<V>(cv, dst);
+        }
 #pragma unroll
         for (int j = 0; j < V; ++j) {
           const int col = c0 + j;
@@ -1209,6 +1249,9 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
         }
         rstore<V>(dst, cv);
       }
+    }
+    if constexpr (kGwDma) {
+      if (r + 1 < r1) gw_dma(r + 1);
     }
     par ^= 1;
   }
@@ -1480,7 +1523,7 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
   while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
-  const size_t lds = (size_t)2 * F * (MODE == 1 ? 2 : 4) * 64 * V * sizeof(float);
+  const size_t lds = (size_t)(2 * F + (term_gw_dma(MODE, V, nstrips > 1) ? 2 : 0)) * (MODE == 1 ? 2 : 4) * 64 * V * sizeof(float);
   // slots: one per (b, segment, strip) workgroup for the taps, one per channel wave of it for the
   // per-graph scalars
   const uint32_t wgs = (uint32_t)((int64_t)B * nsegs * nstrips);
