@@ -120,7 +120,11 @@ def main():
                     help="dump every thread's Python stack to stderr each N seconds (hang diagnosis)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; spawned when not under torchrun)")
     ap.add_argument("--dry-run", action="store_true", help="launcher check: ranks report and exit (no HIP)")
+    ap.add_argument("--conv-benchmark", action="store_true",
+                    help="torch.backends.cudnn.benchmark: MIOpen Find for the stock convolutions")
     args = ap.parse_args()
+    if args.conv_benchmark:
+        torch.backends.cudnn.benchmark = True
 
     if args.watchdog > 0:
         import faulthandler

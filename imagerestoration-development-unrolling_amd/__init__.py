@@ -8,6 +8,17 @@ module ``deep_multiscale_GGLR_GGTV_v1x0`` so callers can swap the import:
     import irdu_amd as model_structure
     model = model_structure.AbtractMultiScaleGraphFilter(...).cuda()
 """
+import os as _os
+
+# The stock convolutions outside the graph path (the v1.0 model's embedding, down/up-sampling and
+# channel combines) run on MIOpen.  With MIOpen's user find-db filled by an earlier process, its
+# immediate mode spends host time per call: the C4 training step (v1.0, 32 x 512^2) went 1.03 s
+# (fresh box) -> 2.7-4.0 s (every later run), GPU kernel time unchanged at 1.09 s per step; with the
+# find-db off every run stays at 1.02-1.03 s (DESIGN.md §4.r4, profiles/r04/miopen/).  A default
+# only: an explicit MIOPEN_DEBUG_DISABLE_FIND_DB in the environment wins.  MIOpen reads it at its
+# first convolution, so it must be set before any runs.
+_os.environ.setdefault("MIOPEN_DEBUG_DISABLE_FIND_DB", "1")
+
 from ._native import GrrError, NativeUnavailable, load as load_native  # noqa: F401
 from .graph_filter import (  # noqa: F401
     AbtractMultiScaleGraphFilter,
