@@ -116,6 +116,8 @@ def main():
                     help="comma list of F that use the one-pass term reverses (default: all instances)")
     ap.add_argument("--keep-gate", type=int, choices=[0, 1], default=1,
                     help="LNB forward keeps the gated activation for the reverse (solver_grad.KEEP_GATE; A/B runs)")
+    ap.add_argument("--term-acc", type=int, choices=[0, 1], default=1,
+                    help="x-gradient pass inside the term reverse (solver_grad.TERM_ACC; A/B runs)")
     ap.add_argument("--watchdog", type=float, default=0.0,
                     help="dump every thread's Python stack to stderr each N seconds (hang diagnosis)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; spawned when not under torchrun)")
@@ -145,6 +147,7 @@ def main():
         K.FUSED_TERM_FTS = tuple(int(v) for v in args.fused_fts.split(",") if v)
     from irdu_amd import solver_grad as SGK
     SGK.KEEP_GATE = bool(args.keep_gate)
+    SGK.TERM_ACC = bool(args.term_acc)
     torch.manual_seed(2204)
     if args.model == "abstract":
         model = irdu_amd.AbtractMultiScaleGraphFilter(3, 3, n_cgd_iters=args.stages, **D_ARGS)

@@ -96,6 +96,8 @@ SIGNATURES = {
     "grr_bwd_prox": [P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_set_term_rows": [I],
     "grr_bwd_term_fused": [I, P, P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_bwd_term_acc_supported": [I, I, I, I],
+    "grr_bwd_term_fused_acc": [I, P, P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_pair_weights": [P, P, P, I, I, I, I, P],
     "grr_bwd_edge_weights": [P, L, P, P, P, P, L, P, I, I, I, I, I, P],
     "grr_bwd_graph_dot": [P, P, Fl, P, I, I, I, I, I, P],

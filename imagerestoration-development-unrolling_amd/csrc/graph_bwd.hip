@@ -963,11 +963,15 @@ __device__ __forceinline__ void dma_dword(const float* src, float* lds_wave_base
   const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)lds_wave_base;
   asm volatile("global_load_lds_dword %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v)) : "memory");
 }
-template <int MODE, int V, bool STRIPS = false>
+// PADJ: no v_out; the x-gradient pass that follows it (gx += scale[g] P*(v), grr_bwd_stencil mode 3 /
+// padj2) runs in the kernel one row behind v: v rows go to an LDS ring (P* reaches one row and one
+// column), gx rows come one row ahead by LDS-DMA, and each segment computes v for the rows either side
+// of it (their weight-gradient partials and reductions are not taken).
+template <int MODE, int V, bool STRIPS = false, bool PADJ = false>
 __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
-    float* __restrict__ v_out, float* __restrict__ gw, Red ggam, Red gdot,
+    float* __restrict__ v_out, float* __restrict__ gx_out, float* __restrict__ gw, Red ggam, Red gdot,
     Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
   constexpr bool kGwDma = term_gw_dma(MODE, V, STRIPS);
@@ -978,6 +982,10 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   auto gring = [&](int pr, int e) { return part_dyn + (2 * F * WPL + pr * WPL + e) * (64 * V); };
   const int lane = threadIdx.x & 63;
   const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // (PADJ) then this wave's v rows [3][64 V] (lane-major) and gx rows [2][element j][lane]
+  const int ring0 = 2 * F * WPL + (kGwDma ? 2 * WPL : 0);
+  auto vring = [&](int q) { return part_dyn + (ring0 + f * 3 + q % 3) * (64 * V); };
+  auto oring = [&](int q) { return part_dyn + (ring0 + 3 * F + f * 2 + (q & 1)) * (64 * V); };
   uint32_t unit = xcd_remap(blockIdx.x, nblk);
   // W > 64 V: column strips owning 62 V columns with V halo columns per side (the term's reach is two
   // columns: s = P x and a = T* g at the pixel's neighbours), as the depthwise row kernels
@@ -992,6 +1000,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   const int seg = unit % nsegs;
   const int bg = unit / nsegs, gi = bg % G;
   const int r0 = seg * sseg, r1 = min(r0 + sseg, H);
+  const int rs = PADJ ? max(r0 - 1, 0) : r0, re = PADJ ? min(r1 + 1, H) : r1;   // rows whose v is formed
   const int lc0 = V * lane;                  // the lane's slot in the LDS partial rows
   int c0 = lc0;                              // global column
   bool on = c0 < W;
@@ -1012,7 +1021,8 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   const int64_t base = ((int64_t)bg * F + f) * HW + cl0;
   const float* xp = x + base;
   const float* gp = g + base;
-  float* vp = v_out + base;
+  float* vp = PADJ ? nullptr : v_out + base;
+  float* gxp = PADJ ? gx_out + base : nullptr;
   const float* wb = w + (int64_t)bg * WPL * HW + cl0;
   float* gwb = gw + (int64_t)bg * WPL * HW + cl0;
 
@@ -1047,7 +1057,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   };
   // prefetched operands of the next step
   float NX[V], NG[V], NW0[V], NW3[V], NW1[V], NW2[V];
-  const int t0 = r0 - 1;
+  const int t0 = rs - 1;
   auto prefetch = [&](int t) {   // step t: x, g row t; weights of output row t - 2 (plane 0 row t - 1)
     xrow(NX, t);
     grow(NG, t);
@@ -1062,11 +1072,11 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     }
   };
   // fill: steps r0 - 3 .. r0 - 2 (x, g rows; no output)
-  xrow(X[2], r0 - 3);
-  grow(Gr[2], r0 - 3);
-  xrow(X[3], r0 - 2);
-  grow(Gr[3], r0 - 2);
-  if constexpr (MODE != 1) wrow(W0[1], 0, r0 - 2);
+  xrow(X[2], rs - 3);
+  grow(Gr[2], rs - 3);
+  xrow(X[3], rs - 2);
+  grow(Gr[3], rs - 2);
+  if constexpr (MODE != 1) wrow(W0[1], 0, rs - 2);
   // element j of the lane's V columns of gw row rr, plane e -> ring slot rr & 1 (lane-contiguous)
   auto gw_dma = [&](int rr) {
     for (int e = f; e < WPL; e += F)
@@ -1074,9 +1084,50 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       for (int j = 0; j < V; ++j) dma_dword(gwb + e * HW + (int64_t)rr * W + j, gring(rr & 1, e) + j * 64);
   };
   if constexpr (kGwDma) gw_dma(r0);
+  // (PADJ) gx row q += scale P*(v) (grr_bwd_stencil mode 3's expression, term by term), v rows q - 1 .. q + 1
+  // from the ring, gx row q from its LDS-DMA slot
+  auto padj_row = [&](int q) {
+    const float* vc = vring(q);
+    const bool top = q == 0, bot = q == H - 1;
+    float cv[V], uv[V], dv[V];
+    rload<V>(cv, vc + lc0);
+    if (top) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) uv[j] = 0.f;
+    } else {
+      rload<V>(uv, vring(q + 2) + lc0);
+    }
+    if (bot) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) dv[j] = 0.f;
+    } else {
+      rload<V>(dv, vring(q + 1) + lc0);
+    }
+    const float lv = (c0 > 0 && lane > 0) ? vc[lc0 - 1] : 0.f;
+    const float rv = (c0 + V < W && lane < 63) ? vc[lc0 + V] : 0.f;
+    const float* os = oring(q) + lane;
+    float o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int col = c0 + j;
+      const float l = j > 0 ? cv[j - 1] : lv, rr = j < V - 1 ? cv[j + 1] : rv;
+      float y = k[0] * cv[j];
+      y += k[1] * dv[j]; y += k[2] * rr; y += k[3] * l; y += k[4] * uv[j];
+      if (top) y += k[1] * cv[j];
+      if (bot) y += k[4] * cv[j];
+      if (col == 0) y += k[2] * cv[j];
+      if (col == W - 1) y += k[3] * cv[j];
+      o[j] = os[j * 64] + y * sc;
+    }
+    if (on) rstore<V>(gxp + (int64_t)q * W, o);
+  };
+  auto gx_dma = [&](int q) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) dma_dword(gxp + (int64_t)q * W + j, oring(q) + j * 64);
+  };
   prefetch(t0);
   int par = 0;
-  for (int t = t0; t <= r1 + 1; ++t) {
+  for (int t = t0; t <= re + 1; ++t) {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       X[0][j] = X[1][j]; X[1][j] = X[2][j]; X[2][j] = X[3][j]; X[3][j] = NX[j];
@@ -1090,7 +1141,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
         W1[j] = NW1[j]; W2[j] = NW2[j];
       }
     }
-    if (t + 1 <= r1 + 1) prefetch(t + 1);
+    if (t + 1 <= re + 1) prefetch(t + 1);
     // s = P x (replicate) and a = T* g (zero frame) at row t - 1
     {
       const float xp_ = lprev(X[2][V - 1]), xn_ = lnext(X[2][0]);
@@ -1109,7 +1160,8 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       }
     }
     const int r = t - 2;
-    if (r < r0) continue;   // pipeline fill (uniform over the workgroup)
+    if (r < rs) continue;   // pipeline fill (uniform over the workgroup)
+    const bool own = !PADJ || (r >= r0 && r < r1);   // (PADJ) rows r0 - 1 and r1: v only
     // output row r: s, a rows r-1, r, r+1 = S[0..2]; x, g rows r-1, r, r+1 = X[0..2], Gr[0..2]
     const bool in0 = r > 0, in3 = r + 1 < H;
     const float s_p = lprev(S[1][V - 1]), s_n = lnext(S[1][0]);
@@ -1187,7 +1239,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
             o += we[e] * ph;
             gs += gtv * we[e];
             gwa[e][j] = ph * da + gtv * ds;
-            if (on) dgam += gph * (tt < -gm ? 2.f : (tt > gm ? -2.f : 0.f));
+            if (on && own) dgam += gph * (tt < -gm ? 2.f : (tt > gm ? -2.f : 0.f));
           }
           if (in[3 - e]) {
             const float sq = s5[(3 - e) + 1], aq = a5[(3 - e) + 1];
@@ -1202,7 +1254,7 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
         z = o;
         v = gs;
       }
-      const float zz = on ? z : 0.f, vv = on ? v : 0.f;
+      const float zz = on && own ? z : 0.f, vv = on && own ? v : 0.f;
       vrow[j] = v;
       dot += av * zz;
 #pragma unroll
@@ -1211,17 +1263,23 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
         accP[tt] += vv * xt[tt];
       }
     }
-    if (on) rstore<V>(vp + (int64_t)r * W, vrow);
+    if constexpr (PADJ) rstore<V>(vring(r) + lc0, vrow);
+    else if (on) rstore<V>(vp + (int64_t)r * W, vrow);
     // weight gradient: partials of the F channels -> LDS -> sum in channel order -> gw
+    if (own) {
 #pragma unroll
-    for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
-    __syncthreads();
-    if constexpr (kGwDma) {
-      // gw row r landed: it was copied before this step's prefetch loads (>= 2 + WPL of them with the
-      // row store, at least the store without) -- the vector memory counter drains in order
-      if (t + 1 <= r1 + 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(MODE == 1 ? 4 : 6) : "memory");
-      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
+      __syncthreads();
     }
+    if constexpr (kGwDma || PADJ) {
+      // gw row r / gx row r - 1 landed: copied before this step's prefetch loads (>= 1 + WPL of them,
+      // + the v row store without PADJ; none in the last steps) -- the vector memory counter drains in
+      // order
+      constexpr int kAfter = (MODE == 1 ? 3 : 5) + (PADJ ? 0 : 1);
+      if (t + 1 <= re + 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kAfter) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PADJ ? 0 : 1) : "memory");
+    }
+    if (own) {
     for (int e = f; e < WPL; e += F) {
       float sum[V];
       rload<V>(sum, part(par, 0, e) + lc0);
@@ -1254,6 +1312,17 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       if (r + 1 < r1) gw_dma(r + 1);
     }
     par ^= 1;
+    }
+    if constexpr (PADJ) {
+      if (r - 1 >= r0 && r - 1 < r1) padj_row(r - 1);
+      if (r >= r0 && r < r1) gx_dma(r);
+    }
+  }
+  if constexpr (PADJ) {
+    if (r1 == H) {   // the image's last row: no v row below it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      padj_row(H - 1);
+    }
   }
   // per-graph / per-channel reductions: wave sums into this wave's slots.  Slot of the workgroup:
   // (b, segment, strip); the per-graph scalars take one slot per channel wave of it.
@@ -1512,10 +1581,17 @@ struct TermReds {
   }
 };
 
+// LDS of one term_row_kernel workgroup: the partials, the gw ring, (PADJ) the v and gx rings
+size_t term_row_lds(int mode, int V, int F, bool strips, bool padj) {
+  const int wpl = mode == 1 ? 2 : 4;
+  const int rows = 2 * F * wpl + (term_gw_dma(mode, V, strips) ? 2 * wpl : 0) + (padj ? 5 * F : 0);
+  return (size_t)rows * 64 * V * sizeof(float);
+}
+constexpr size_t kTermLdsMax = 160 * 1024;
 template <int MODE, int V>
 grr_status launch_term_row(int B, int F, const float* x, const float* g, const float* taps, const float* w,
-                           const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam,
-                           float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
+                           const float* lg, const float* scale, float coef, float* v, float* gx, float* gw,
+                           float* ggam, float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
   // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
   int sseg = H;
   const int nstrips = W <= 64 * V ? 1 : (W + 62 * V - 1) / (62 * V);
@@ -1523,19 +1599,26 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
   while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
-  const size_t lds = (size_t)(2 * F + (term_gw_dma(MODE, V, nstrips > 1) ? 2 : 0)) * (MODE == 1 ? 2 : 4) * 64 * V * sizeof(float);
+  const bool padj = gx != nullptr;
+  const size_t lds = term_row_lds(MODE, V, F, nstrips > 1, padj);
   // slots: one per (b, segment, strip) workgroup for the taps, one per channel wave of it for the
   // per-graph scalars
   const uint32_t wgs = (uint32_t)((int64_t)B * nsegs * nstrips);
   TermReds R(s);
   grr_status st = R.setup(MODE, gdot, ggam, gtaps, G, F, wgs * F, wgs);
   if (st != GRR_OK) return st;
-  if (nstrips > 1)
-    hipLaunchKernelGGL((term_row_kernel<MODE, V, true>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale,
-                       coef, v, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg, nsegs, nblk);
-  else
-    hipLaunchKernelGGL((term_row_kernel<MODE, V, false>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, scale,
-                       coef, v, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg, nsegs, nblk);
+#define GRR_TERM_ROW_LAUNCH(STRIPS, PADJ)                                                                   \
+  hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, PADJ>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, \
+                     scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg,   \
+                     nsegs, nblk)
+  if (padj) {
+    if constexpr (V < 4) GRR_TERM_ROW_LAUNCH(false, true);   // term_acc_shape_ok: one strip, V <= 2
+  } else if (nstrips > 1) {
+    GRR_TERM_ROW_LAUNCH(true, false);
+  } else {
+    GRR_TERM_ROW_LAUNCH(false, false);
+  }
+#undef GRR_TERM_ROW_LAUNCH
   st = launch_status("grr_bwd_term_fused");
   if (st != GRR_OK) return st;
   return R.rs.finish("grr_bwd_term_fused");
@@ -1549,14 +1632,25 @@ bool term_row_ok(int mode, int F, const float* x, const float* g, const float* w
     if ((uintptr_t)p % (4u * V) != 0) return false;
   return true;
 }
+// the row kernel with the x-gradient pass inside (PADJ) where it measured faster than the kernel + the
+// stencil / padj2 pass: one strip of 1- or 2-column lanes (W <= 128; e.g. B16 G32 F3 128^2: 0.467 against
+// 0.477 ms for GLR + pair + padj2, prox 0.339 against 0.359).  The 4-column instances (W = 256, strips)
+// are at the 168-VGPR cap and spill more with it: GLR + pair 1.75 against 1.67 ms, prox 1.36 against
+// 1.22 at B16 G32 F3 256^2 (profiles/r04/term/ab_term_acc.txt).  (Strips would also need V >= 3: P* at
+// an owned edge column reads v one halo column out.)
+bool term_acc_shape_ok(int mode, int F, int W) {
+  const int V = term_strip_vec(W, mode);
+  if (V == 0 || V == 4 || W > 64 * V || F > TermRowMax<1>::F) return false;
+  return term_row_lds(mode, V, F, false, true) <= kTermLdsMax;
+}
 template <int MODE>
 grr_status launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
-                             const float* lg, const float* scale, float coef, float* v, float* gw, float* ggam,
-                             float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
+                             const float* lg, const float* scale, float coef, float* v, float* gx, float* gw,
+                             float* ggam, float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
   switch (term_strip_vec(W, MODE)) {
-    case 1: return launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
-    case 2: return launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
-    default: return launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gw, ggam, gdot, gtaps, G, H, W, s);
+    case 1: return launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gx, gw, ggam, gdot, gtaps, G, H, W, s);
+    case 2: return launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gx, gw, ggam, gdot, gtaps, G, H, W, s);
+    default: return launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gx, gw, ggam, gdot, gtaps, G, H, W, s);
   }
 }
 
@@ -1718,9 +1812,9 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
   // row-streaming kernel where the shape allows
   if (g_term_rows && (int64_t)B * G * H < (1ll << 31) && term_row_ok(mode, F, x, g, w, v_out, gw, W)) {
     switch (mode) {
-      case 0: return launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
-      case 1: return launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
-      default: return launch_term_row_v<2>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, gw, ggamma, gdot, gtaps, G, H, W, s);
+      case 0: return launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, nullptr, gw, ggamma, gdot, gtaps, G, H, W, s);
+      case 1: return launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, nullptr, gw, ggamma, gdot, gtaps, G, H, W, s);
+      default: return launch_term_row_v<2>(B, F, x, g, taps, w, log_gamma, scale, coef, v_out, nullptr, gw, ggamma, gdot, gtaps, G, H, W, s);
     }
   }
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused: B*G > 65535");
@@ -1741,6 +1835,30 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
   st = launch_status("grr_bwd_term_fused");
   if (st != GRR_OK) return st;
   return R.rs.finish("grr_bwd_term_fused");
+}
+
+int grr_bwd_term_acc_supported(int mode, int F, int H, int W) {
+  return mode >= 0 && mode <= 2 && F > 0 && H > 0 && W > 0 && g_term_rows && term_acc_shape_ok(mode, F, W) ? 1 : 0;
+}
+
+grr_status grr_bwd_term_fused_acc(int mode, const float* x, const float* g, const float* taps, const float* w,
+                                  const float* log_gamma, const float* scale, float coef, float* gx, float* gw,
+                                  float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
+                                  void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && g && taps && w && gx && gw && gtaps && scale && B > 0 && G > 0 && F > 0 && H > 0 && W > 0 &&
+                  mode >= 0 && mode <= 2 && (mode != 2 || log_gamma),
+              GRR_ERR_INVALID_ARG, "grr_bwd_term_fused_acc: bad args");
+  GRR_REQUIRE(grr_bwd_term_acc_supported(mode, F, H, W) && (int64_t)B * G * H < (1ll << 31) &&
+                  term_row_ok(mode, F, x, g, w, gx, gw, W),
+              GRR_ERR_UNSUPPORTED, "grr_bwd_term_fused_acc: mode %d F=%d %dx%d needs the row kernel (see "
+              "grr_bwd_term_acc_supported) and 4 V-byte aligned planes", mode, F, H, W);
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode) {
+    case 0: return launch_term_row_v<0>(B, F, x, g, taps, w, log_gamma, scale, coef, nullptr, gx, gw, ggamma, gdot, gtaps, G, H, W, s);
+    case 1: return launch_term_row_v<1>(B, F, x, g, taps, w, log_gamma, scale, coef, nullptr, gx, gw, ggamma, gdot, gtaps, G, H, W, s);
+    default: return launch_term_row_v<2>(B, F, x, g, taps, w, log_gamma, scale, coef, nullptr, gx, gw, ggamma, gdot, gtaps, G, H, W, s);
+  }
 }
 
 grr_status grr_bwd_stencil(const float* x, const float* taps, int mode, const float* scale, int accumulate,

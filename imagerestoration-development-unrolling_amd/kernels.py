@@ -818,6 +818,28 @@ def bwd_term_fused(mode: int, x: Tensor, g: Tensor, taps: Tensor, w: Tensor, log
     return v
 
 
+def term_acc_ok(mode: int, x: Tensor, n_graphs: int, *planes: Tensor) -> bool:
+    """Whether grr_bwd_term_fused_acc takes this term reverse (row kernel with the P* pass inside)."""
+    b, c, h, w = x.shape
+    if not TERM_ROWS or c % n_graphs or any(t.data_ptr() % 16 for t in (x, *planes)):
+        return False
+    return bool(_native.load().grr_bwd_term_acc_supported(mode, c // n_graphs, h, w))
+
+
+def bwd_term_fused_acc(mode: int, x: Tensor, g: Tensor, taps: Tensor, w: Tensor, log_gamma: Optional[Tensor],
+                       scale: Tensor, coef: float, gx: Tensor, gw: Tensor, ggamma: Optional[Tensor],
+                       gdot: Optional[Tensor], gtaps: Tensor, n_graphs: int) -> None:
+    """bwd_term_fused + bwd_stencil(v, taps, ST_P_ADJ, scale, out=gx) in one pass (grr_bwd_term_fused_acc):
+    gx += scale[g] P*(v), v never written (term_acc_ok must hold)."""
+    dev = _check("bwd_term_fused", x, g, taps, w, log_gamma, scale, gx, gw, ggamma, gdot, gtaps)
+    if gx.shape != x.shape:
+        raise ValueError(f"bwd_term_fused_acc: gx {tuple(gx.shape)} vs x {tuple(x.shape)}")
+    _launch("bwd_term_fused", 4 * (4 * x.numel() + 3 * w.numel()), "grr_bwd_term_fused_acc", mode, x.data_ptr(),
+            g.data_ptr(), taps.data_ptr(), w.data_ptr(), _ptr(log_gamma), scale.data_ptr(), float(coef),
+            gx.data_ptr(), gw.data_ptr(), _ptr(ggamma), _ptr(gdot), gtaps.data_ptr(), *_bgfhw(x, n_graphs),
+            _stream(dev))
+
+
 def bwd_pair_weights(w: Tensor, gc: Tensor, gw: Tensor) -> None:
     dev = _check("bwd_pair_weights", w, gc, gw)
     b, g, _, h, ww = w.shape

@@ -65,12 +65,24 @@ def _use_fused(x: Tensor, n_graphs: int) -> bool:
     return FUSED and (f in K.FUSED_TERM_FTS or (K.TERM_ROWS and K.term_rows_ok(x.shape[3], f)))
 
 
+# The x-gradient pass P*(v) inside the row-streaming term reverse (grr_bwd_term_fused_acc) wherever it
+# takes the shape: v is never written and the padj2 / stencil pass that read it back is gone
+TERM_ACC = True
+
+
+def _acc_ok(mode: int, x: Tensor, g: Tensor, out: Tensor, n_graphs: int) -> bool:
+    return TERM_ACC and FUSED and x.is_cuda and K.term_acc_ok(mode, x, n_graphs, g, out)
+
+
 def glr_term_bwd(x: Tensor, g: Tensor, taps: Tensor, w: Tensor, scale: Tensor, coef: float, n_graphs: int,
                  out: Tensor, gw: Tensor, gscale: Optional[Tensor], gtaps: Tensor, defer: bool = False):
     """Reverse of the GLR term  scale[g] * T((I - W) P x)  (REF:218-237) contracted with coef * g:
     out += coef*scale * P*(I-W)^T T* g; gw, gtaps += coef*scale * d/d(.); gscale += coef * <g, T(I-W)Px>.
     defer (one-pass path only): return (v, coef*scale) and leave out += coef*scale P*(v) to the caller."""
     sc = scale * coef
+    if not defer and _acc_ok(K.TERM_GLR, x, g, out, n_graphs):
+        K.bwd_term_fused_acc(K.TERM_GLR, x, g, taps, w, None, sc, coef, out, gw, None, gscale, gtaps, n_graphs)
+        return None
     if _use_fused(x, n_graphs):
         v = K.bwd_term_fused(K.TERM_GLR, x, g, taps, w, None, sc, coef, gw, None, gscale, gtaps, n_graphs)
         if defer:
@@ -90,6 +102,9 @@ def gtv_term_bwd(x: Tensor, g: Tensor, taps: Tensor, c: Tensor, scale: Tensor, c
                  out: Tensor, gc: Tensor, gscale: Optional[Tensor], gtaps: Tensor, defer: bool = False):
     """Reverse of the linear GTV term  scale[g] * T(K_c P x)  (C^T C with pair weights, REF:452-523)."""
     sc = scale * coef
+    if not defer and _acc_ok(K.TERM_PAIR, x, g, out, n_graphs):
+        K.bwd_term_fused_acc(K.TERM_PAIR, x, g, taps, c, None, sc, coef, out, gc, None, gscale, gtaps, n_graphs)
+        return None
     if _use_fused(x, n_graphs):
         v = K.bwd_term_fused(K.TERM_PAIR, x, g, taps, c, None, sc, coef, gc, None, gscale, gtaps, n_graphs)
         if defer:
@@ -123,7 +138,8 @@ class _Level:
     def terms_bwd(self, x: Tensor, g: Tensor, coef: float, out: Tensor, glr: bool = True) -> None:
         """out += coef * (mu L^T + ro G^T) g, and coef * d<g, mu L x + ro G x>/d(params) into the buffers.
         With both one-pass term reverses, the two x-gradient passes run as one sweep (grr_bwd_padj2)."""
-        if glr and PADJ2 and _use_fused(x, self.g) and K.padj2_ok(x):
+        acc = _acc_ok(K.TERM_PAIR, x, g, out, self.g) and (not glr or _acc_ok(K.TERM_GLR, x, g, out, self.g))
+        if glr and PADJ2 and not acc and _use_fused(x, self.g) and K.padj2_ok(x):
             vl, scl = glr_term_bwd(x, g, self.tapsL, self.wL, self.mu, coef, self.g, out, self.gwL, self.gmu,
                                    self.gtapL, defer=True)
             vg, scg = gtv_term_bwd(x, g, self.tapsG, self.cG, self.ro, coef, self.g, out, self.gcG, self.gro,
@@ -138,6 +154,10 @@ class _Level:
         """out += ro C^T-part reverse of the prox rhs term ro T(Ct phi(C P x)); parameter gradients."""
         G = self.g
         sc = self.ro
+        if _acc_ok(K.TERM_PROX, x, g, out, G):
+            K.bwd_term_fused_acc(K.TERM_PROX, x, g, self.tapsG, self.wG, self.log_gamma, sc, 1.0, out, self.gwG,
+                                 self.ggam, self.gro, self.gtapG, G)
+            return
         if _use_fused(x, G):
             v = K.bwd_term_fused(K.TERM_PROX, x, g, self.tapsG, self.wG, self.log_gamma, sc, 1.0, self.gwG,
                                  self.ggam, self.gro, self.gtapG, G)

@@ -355,6 +355,17 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
                               const float* log_gamma, const float* scale, float coef, float* v_out, float* gw,
                               float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
                               void* stream);
+/* grr_bwd_term_fused and the x-gradient pass that consumes its v (grr_bwd_stencil mode 3 with the
+ * same taps and scale, accumulating) in one row-streaming pass: gx += scale[g] * adjoint-S(v), v never
+ * written; gw, ggamma, gdot, gtaps as grr_bwd_term_fused.  Two calls on one gx (GLR, then pair) equal
+ * grr_bwd_padj2 of the two v's.  GRR_ERR_UNSUPPORTED where grr_bwd_term_acc_supported says 0 (the
+ * caller keeps the two-pass path) or a plane is not 4V-byte aligned.  The reference computes these
+ * gradients by autograd through REF:218-237, :452-523, :684-704. */
+int grr_bwd_term_acc_supported(int mode, int F, int H, int W);
+grr_status grr_bwd_term_fused_acc(int mode, const float* x, const float* g, const float* taps, const float* w,
+                                  const float* log_gamma, const float* scale, float coef, float* gx, float* gw,
+                                  float* ggamma, float* gdot, float* gtaps, int B, int G, int F, int H, int W,
+                                  void* stream);
 /* Reverse of grr_gtv_pair_weights: gw [B,G,4,H,W] += d<gc, c(w)>/dw. */
 grr_status grr_bwd_pair_weights(const float* w, const float* gc, float* gw, int B, int G, int H, int W,
                                 void* stream);

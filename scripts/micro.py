@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--split", action="store_true", help="LNB: time the head and the mix apart")
     ap.add_argument("--mode", type=int, default=0, help="term: 0 GLR, 1 pair Laplacian, 2 prox")
     ap.add_argument("--width", type=int, default=0, help="image width (default: --size)")
+    ap.add_argument("--acc", type=int, default=0, choices=[0, 1, 2],
+                    help="term: 0 the term pass, 1 with the x-gradient pass inside (grr_bwd_term_fused_acc), "
+                         "2 the term pass + the stencil x-gradient pass")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
     dev = torch.device("cuda", 0)
@@ -90,7 +93,14 @@ def main():
         sc = torch.rand(g, device=dev) + 0.5
         gw, gdot, gt = torch.zeros_like(wt), torch.zeros(g, device=dev), torch.zeros_like(taps)
         ggam = torch.zeros(g, device=dev) if mode == 2 else None
-        fn = lambda: K.bwd_term_fused(mode, x, gg, taps, wt, lg, sc, 0.5, gw, ggam, gdot, gt, g)  # noqa: E731
+        gx = torch.zeros_like(x)
+        if args.acc == 1:
+            fn = lambda: K.bwd_term_fused_acc(mode, x, gg, taps, wt, lg, sc, 0.5, gx, gw, ggam, gdot, gt, g)  # noqa: E731
+        elif args.acc == 2:
+            fn = lambda: K.bwd_stencil(K.bwd_term_fused(mode, x, gg, taps, wt, lg, sc, 0.5, gw, ggam, gdot, gt, g),  # noqa: E731
+                                       taps, K.ST_P_ADJ, g, sc, out=gx)
+        else:
+            fn = lambda: K.bwd_term_fused(mode, x, gg, taps, wt, lg, sc, 0.5, gw, ggam, gdot, gt, g)  # noqa: E731
     elif args.kernel == "gate_dw3_bwd":   # LNB training reverse: gate + depthwise adjoint, hid = --fts
         hid = args.fts
         hh = torch.randn(b, 2 * hid, h, w, device=dev)

@@ -1,0 +1,122 @@
+"""grr_bwd_term_fused_acc (the row-streaming term reverse with the x-gradient pass P*(v) inside) against
+grr_bwd_term_fused + grr_bwd_stencil mode 3 on the same inputs, for the three operator terms: the
+accumulated x-gradient, the weight gradient and the per-graph / per-channel reductions.  Shapes cover
+one- and two-column lanes (W <= 128, where the fused pass runs), row segments with a ragged last segment
+(the segment's halo rows), the image's first and last rows, F up to 16.  The two-pass path
+is itself pinned by test_gpu_term_rows.py and the gradient tests."""
+import pytest
+import torch
+
+from tests.test_gpu_parity import DEV, rel_err
+
+pytestmark = pytest.mark.gpu
+
+# (B, G, F, H, W): H = 70 / 100 / 300 split into row segments (32 rows) with a ragged last one; W = 256 / 512
+# check that the fused pass declines them
+CASES = [(2, 4, 3, 64, 64), (1, 3, 3, 70, 128), (2, 2, 6, 100, 100), (1, 2, 3, 300, 128), (3, 2, 3, 2, 64),
+         (1, 1, 12, 40, 128), (1, 2, 4, 9, 32), (1, 1, 1, 1, 64), (2, 1, 16, 33, 96), (1, 2, 6, 37, 512),
+         (1, 2, 3, 20, 256)]
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import irdu_amd
+    irdu_amd.load_native()
+    from irdu_amd import kernels
+    kernels.set_term_rows(True)
+    return kernels
+
+
+def _inputs(mode, case):
+    b, G, F, h, w_ = case
+    torch.manual_seed(mode * 1000 + h * 7 + w_)
+    C = G * F
+    x = torch.randn(b, C, h, w_, device=DEV)
+    g = torch.randn(b, C, h, w_, device=DEV)
+    taps = torch.randn(C, 5, device=DEV) * 0.5
+    w = torch.rand(b, G, 2 if mode == 1 else 4, h, w_, device=DEV)
+    lg = torch.log(torch.linspace(0.05, 0.5, G, device=DEV)) if mode == 2 else None
+    scale = torch.rand(G, device=DEV) + 0.5
+    gx0 = torch.randn(b, C, h, w_, device=DEV)
+    return x, g, taps, w, lg, scale, gx0
+
+
+def _bufs(mode, w, taps, G):
+    return (torch.full_like(w, 0.5), torch.zeros(G, device=DEV) if mode == 2 else None,
+            torch.zeros(G, device=DEV), torch.zeros_like(taps))
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_term_acc_equals_two_pass(K, case, mode):
+    b, G, F, h, w_ = case
+    x, g, taps, w, lg, scale, gx0 = _inputs(mode, case)
+    if not K.term_acc_ok(mode, x, G, g, gx0):
+        # W > 128 (4-column lanes, strips) stays on the two-pass path (measured slower fused)
+        assert w_ > 128, (mode, case)
+        return
+    gw_r, gg_r, gd_r, gt_r = _bufs(mode, w, taps, G)
+    v = K.bwd_term_fused(mode, x, g, taps, w, lg, scale, 0.7, gw_r, gg_r, gd_r, gt_r, G)
+    gx_r = gx0.clone()
+    K.bwd_stencil(v, taps, K.ST_P_ADJ, G, scale, out=gx_r)
+    gw_a, gg_a, gd_a, gt_a = _bufs(mode, w, taps, G)
+    gx_a = gx0.clone()
+    K.bwd_term_fused_acc(mode, x, g, taps, w, lg, scale, 0.7, gx_a, gw_a, gg_a, gd_a, gt_a, G)
+    torch.cuda.synchronize()
+    # gx: the same expression in the same order as the stencil pass; the rest: the same kernel arithmetic
+    assert rel_err(gx_a.cpu(), gx_r.cpu()) <= 1e-6, rel_err(gx_a.cpu(), gx_r.cpu())
+    assert rel_err(gw_a.cpu(), gw_r.cpu()) <= 1e-6
+    for name, a, r in (("gdot", gd_a, gd_r), ("ggamma", gg_a, gg_r), ("gtaps", gt_a, gt_r)):
+        if r is None:
+            continue
+        err = float((a.double() - r.double()).abs().max())
+        assert err <= 1e-5 * max(float(r.abs().max()), 1.0), (name, err)
+
+
+def test_glr_then_pair_equals_padj2(K):
+    """Two accumulating calls on one gx (GLR, then pair: the level's terms_bwd) equal the padj2 sweep."""
+    case = (2, 4, 3, 70, 128)
+    b, G, F, h, w_ = case
+    x, g, taps0, w0, _, s0, gx0 = _inputs(0, case)
+    _, _, taps1, w1, _, s1, _ = _inputs(1, case)
+    gx_r, gx_a = gx0.clone(), gx0.clone()
+    b0, b1 = _bufs(0, w0, taps0, G), _bufs(1, w1, taps1, G)
+    v0 = K.bwd_term_fused(0, x, g, taps0, w0, None, s0, -1.0, *b0, G)
+    v1 = K.bwd_term_fused(1, x, g, taps1, w1, None, s1, -1.0, *b1, G)
+    K.bwd_padj2(v0, taps0, s0, v1, taps1, s1, gx_r, G)
+    b0, b1 = _bufs(0, w0, taps0, G), _bufs(1, w1, taps1, G)
+    K.bwd_term_fused_acc(0, x, g, taps0, w0, None, s0, -1.0, gx_a, *b0, G)
+    K.bwd_term_fused_acc(1, x, g, taps1, w1, None, s1, -1.0, gx_a, *b1, G)
+    torch.cuda.synchronize()
+    assert rel_err(gx_a.cpu(), gx_r.cpu()) <= 1e-6
+
+
+def test_training_gradients_with_and_without_acc(K):
+    """msgf's mixture reverse with the fused x-gradient passes against the two-pass path."""
+    import irdu_amd
+    from irdu_amd import solver_grad as SG
+    from tests.test_gpu_parity import perturb_mixture
+    torch.manual_seed(5)
+    m = irdu_amd.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=4)
+    perturb_mixture(m.localfilter, 9)
+    m = m.to(DEV)
+    y = torch.rand(2, 3, 64, 64, device=DEV)
+
+    def grads(acc):
+        SG.TERM_ACC = acc
+        try:
+            m.zero_grad(set_to_none=True)
+            m(y).square().mean().backward()
+            return {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+        finally:
+            SG.TERM_ACC = True
+
+    ref, got = grads(False), grads(True)
+    assert ref.keys() == got.keys()
+    # the x-gradient passes agree to fp32 rounding (test_term_acc_equals_two_pass: 1e-6); through four
+    # stages, the feature CNN's reverse and image-wide sums that cancel (a skip weight's gradient: 3.5 from
+    # terms far larger) that rounding reaches a few 1e-5 of the largest gradient entry
+    for k in ref:
+        assert rel_err(got[k].cpu(), ref[k].cpu()) <= 2e-4, (k, rel_err(got[k].cpu(), ref[k].cpu()))
