@@ -616,23 +616,38 @@ __global__ __launch_bounds__(NT) void lincomb_kernel(const float* __restrict__ x
 // the operator term (REF:784-807), in one pass over the (b, g) slab:
 //   galpha[g] += <gx', u>;  gu = alpha[g] gx' + beta_next[g] gu_next;  gbeta[g] += <gu, u_prev>;
 //   gbb += gu;  gx_out = gx' - gu  (gx_out may alias gx).                 grid (chunks, B*G)
+// gxh (optional): the previous stage's half-level x-gradient not yet added, gx' = gx + U gxh (the 2x2
+// unpool-accumulate, unpool2_acc_kernel's arithmetic) -- one read of gx instead of U's read + write.
 template <bool V4>
-__global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const float* __restrict__ u,
+__global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const float* __restrict__ gxh,
+                                                     const float* __restrict__ u,
                                                      const float* __restrict__ gun, const float* __restrict__ up,
                                                      const float* __restrict__ alpha,
                                                      const float* __restrict__ beta_next, float* __restrict__ gu_out,
                                                      float* __restrict__ gbb, float* gx_out, Red galpha,
-                                                     Red gbeta, int G, int64_t n) {
+                                                     Red gbeta, int G, int64_t n, int H, int W) {
   const int bg = blockIdx.y, g = bg % G;
   const int64_t base = (int64_t)bg * n;
   const float al = alpha[g], be = gun ? beta_next[g] : 0.f;
+  const int HW = H * W, w2 = W / 2;
+  const int64_t hbase = (int64_t)bg * (n / 4);   // the slab's half-level planes: F (H/2) (W/2) floats
+  auto half_at = [&](int li) {   // offset of the half-level value under slab element li
+    const int f = li / HW, p = li - f * HW, r = p / W, c = p - r * W;
+    return hbase + (int64_t)f * (HW / 4) + (r >> 1) * w2 + (c >> 1);
+  };
   float da = 0.f, db = 0.f;
   if constexpr (V4) {
     typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
     const int64_t n4 = n / 4;
     for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
       const int64_t o = base + 4 * i;
-      const f4 x = *reinterpret_cast<const f4*>(gx + o), uv = *reinterpret_cast<const f4*>(u + o);
+      f4 x = *reinterpret_cast<const f4*>(gx + o);
+      const f4 uv = *reinterpret_cast<const f4*>(u + o);
+      if (gxh) {   // W % 4 == 0: the four columns sit over two half-level columns
+        const f2 q = *reinterpret_cast<const f2*>(gxh + half_at((int)(4 * i)));
+        x.x += 0.25f * q.x; x.y += 0.25f * q.x; x.z += 0.25f * q.y; x.w += 0.25f * q.y;
+      }
       f4 gu = al * x;
       if (gun) gu += be * *reinterpret_cast<const f4*>(gun + o);
       da += x.x * uv.x + x.y * uv.y + x.z * uv.z + x.w * uv.w;
@@ -647,7 +662,8 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
   } else {
     for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
       const int64_t o = base + i;
-      const float x = gx[o];
+      float x = gx[o];
+      if (gxh) x += 0.25f * gxh[half_at((int)i)];
       float gu = al * x;
       if (gun) gu += be * gun[o];
       da += x * u[o];
@@ -2034,18 +2050,21 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   return st != GRR_OK ? st : rs.finish("grr_bwd_graph_dot");
 }
 
-grr_status grr_bwd_cg_glue(const float* gx, const float* u, const float* gu_next, const float* u_prev,
-                           const float* alpha, const float* beta_next, float* gu, float* gbb, float* gx_out,
-                           float* galpha, float* gbeta, int B, int G, int F, int H, int W, void* stream) {
+grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* u, const float* gu_next,
+                           const float* u_prev, const float* alpha, const float* beta_next, float* gu, float* gbb,
+                           float* gx_out, float* galpha, float* gbeta, int B, int G, int F, int H, int W,
+                           void* stream) {
   clear_error();
   GRR_REQUIRE(gx && u && alpha && gu && gx_out && galpha && (!gu_next || beta_next) && (!u_prev || gbeta) && B > 0 &&
-                  G > 0 && F > 0 && H > 0 && W > 0,
+                  G > 0 && F > 0 && H > 0 && W > 0 && (!gx_half || (H % 2 == 0 && W % 2 == 0)),
               GRR_ERR_INVALID_ARG, "grr_bwd_cg_glue: bad args");
-  GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_bwd_cg_glue: B*G > 65535");
+  GRR_REQUIRE((int64_t)B * G <= 65535 && (int64_t)F * H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_bwd_cg_glue: B*G > 65535 or a (b, graph) slab of 2^31 floats");
   const int64_t n = (int64_t)F * H * W;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   const bool v4 = n % 4 == 0 && al16(gx) && al16(u) && al16(gu) && al16(gx_out) && (!gu_next || al16(gu_next)) &&
-                  (!u_prev || al16(u_prev)) && (!gbb || al16(gbb));
+                  (!u_prev || al16(u_prev)) && (!gbb || al16(gbb)) &&
+                  (!gx_half || (W % 4 == 0 && ((uintptr_t)gx_half & 7) == 0));
   const int chunks = chunks_for(v4 ? n / 4 : n, (int64_t)B * G);
   const dim3 grid(chunks, B * G);
   RedScratch rs((hipStream_t)stream);
@@ -2053,11 +2072,11 @@ grr_status grr_bwd_cg_glue(const float* gx, const float* u, const float* gu_next
   grr_status st = rs.alloc("grr_bwd_cg_glue");
   if (st != GRR_OK) return st;
   if (v4)
-    hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, u, gu_next, u_prev, alpha,
-                       beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n);
+    hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, u, gu_next, u_prev,
+                       alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
   else
-    hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, u, gu_next, u_prev, alpha,
-                       beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n);
+    hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, u, gu_next, u_prev,
+                       alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
   st = launch_status("grr_bwd_cg_glue");
   return st != GRR_OK ? st : rs.finish("grr_bwd_cg_glue");
 }

@@ -186,8 +186,17 @@ def _level_side(dev: torch.device) -> "torch.cuda.Stream":
     return _LEVEL_SIDE[key]
 
 
-def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn) -> None:
-    """Apply a per-level reverse at full resolution and, through D / U, at half resolution."""
+# The half level's x-gradient of stage k's operator reverse is added by the next stage's glue pass
+# (grr_bwd_cg_glue's gx_half: U folded into the pass that reads gx next) instead of its own
+# unpool-accumulate pass (a read + write of the full-resolution gradient)
+UNPOOL_GLUE = True
+
+
+def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
+               defer: bool = False) -> Optional[Tensor]:
+    """Apply a per-level reverse at full resolution and, through D / U, at half resolution.
+    defer: return the half level's x-gradient instead of adding U of it to out (the caller passes it
+    to the next bwd_cg_glue)."""
     if LEVEL_STREAMS and x.is_cuda and not torch.compiler.is_compiling() \
             and not torch.cuda.is_current_stream_capturing():
         main = torch.cuda.current_stream(x.device)
@@ -202,23 +211,29 @@ def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn) ->
         fn(l0, x, g, out)
         main.wait_stream(side)
         gxd.record_stream(main)
+        if defer:
+            return gxd
         K.bwd_unpool2_acc(gxd, out)           # D^T = U
-        return
+        return None
     fn(l0, x, g, out)
     xd, gd = K.pool2(x), K.pool2(g)          # half level sees D x; U^T = D
     gxd = torch.zeros_like(xd)
     fn(l1, xd, gd, gxd)
+    if defer:
+        return gxd
     K.bwd_unpool2_acc(gxd, out)               # D^T = U
+    return None
 
 
 def cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Optional[Tensor], alpha: Tensor, beta: Tensor,
-            gbb: Optional[Tensor], galpha: Tensor, gbeta: Tensor, k: int, g: int, owned: bool) -> Tuple[Tensor, Tensor]:
+            gbb: Optional[Tensor], galpha: Tensor, gbeta: Tensor, k: int, g: int, owned: bool,
+            gx_half: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     """Reverse of stage k's recurrence glue (x' = x + a_k u_k, u_k = r - A x + b_k u_{k-1}) without the
     operator term: returns (gu_k, gx' - gu_k); ga_k, gb_k (when u_prev) and gbb accumulate.  owned: gx
     is this sweep's own buffer and is overwritten."""
     gu, gx2 = K.bwd_cg_glue(gx, u, gu_next, u_prev, alpha[k].contiguous(),
                             beta[k + 1].contiguous() if gu_next is not None else None, gbb, galpha[k],
-                            gbeta[k] if u_prev is not None else None, g, inplace=owned)
+                            gbeta[k] if u_prev is not None else None, g, inplace=owned, gx_half=gx_half)
     return gu, gx2
 
 
@@ -310,19 +325,20 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
     alpha, beta = p["alphaCGD"], p["betaCGD"]
     galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
 
-    def a_bwd(x, gg, coef, out, glr=True):      # out += coef * (A - I)^T gg (+ parameter gradients)
-        _two_level(l0, l1, x, gg, out, lambda lv, xx, g2, o: lv.terms_bwd(xx, g2, coef, o, glr))
+    def a_bwd(x, gg, coef, out, glr=True, defer=False):   # out += coef * (A - I)^T gg (+ parameter gradients)
+        return _two_level(l0, l1, x, gg, out, lambda lv, xx, g2, o: lv.terms_bwd(xx, g2, coef, o, glr), defer)
 
     gx = gouts[0].contiguous()
     gy = torch.zeros_like(y)
     if n_st > 1:
         gbb = torch.zeros_like(y)
-        gu_next = None
+        gu_next, gxh = None, None
         for k in range(n_st - 1, 0, -1):
-            # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue)
+            # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue), with the
+            # previous stage's half-level x-gradient added on the way in
             gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
-                             galpha, gbeta, k, g, owned=k < n_st - 1)
-            a_bwd(xs[k], gu, -1.0, gx)                          #   - (A - I)^T gu
+                             galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh)
+            gxh = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1)   #   - (A - I)^T gu
             gu_next = gu
         # b_B = y + prox terms(x_1)
         K.bwd_lincomb(gbb, None, None, None, g, out=gy, accumulate=True)

@@ -380,10 +380,13 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
 /* One reverse step of the CG / heavy-ball recurrence glue (autograd of REF:784-807 without the
  * operator term): galpha[g] += <gx, u>; gu = alpha[g] gx + beta_next[g] gu_next (gu_next may be
  * NULL); gbeta[g] += <gu, u_prev> (u_prev may be NULL); gbb += gu (gbb may be NULL);
- * gx_out = gx - gu (may alias gx).  Signals [B, G*F, H, W]; alpha, beta_next, galpha, gbeta [G]. */
-grr_status grr_bwd_cg_glue(const float* gx, const float* u, const float* gu_next, const float* u_prev,
-                           const float* alpha, const float* beta_next, float* gu, float* gbb, float* gx_out,
-                           float* galpha, float* gbeta, int B, int G, int F, int H, int W, void* stream);
+ * gx_out = gx - gu (may alias gx).  Signals [B, G*F, H, W]; alpha, beta_next, galpha, gbeta [G].
+ * gx_half (may be NULL): a half-level x-gradient [B, G*F, H/2, W/2] still to be added, gx taken as
+ * gx + U gx_half (grr_bwd_unpool2_acc folded into the pass; H, W even). */
+grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* u, const float* gu_next,
+                           const float* u_prev, const float* alpha, const float* beta_next, float* gu, float* gbb,
+                           float* gx_out, float* galpha, float* gbeta, int B, int G, int F, int H, int W,
+                           void* stream);
 grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,
                            int accumulate, int B, int G, int F, int H, int W, void* stream);
 /* out [B,C,H,W] += U(xd): 0.25 * xd(q/2) (conv_transpose2d of scaling_kernel01, REF:676-679). */

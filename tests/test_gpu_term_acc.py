@@ -1,9 +1,12 @@
-"""grr_bwd_term_fused_acc (the row-streaming term reverse with the x-gradient pass P*(v) inside) against
+"""Fused reverse passes against the unfused ones they replace.
+
+grr_bwd_term_fused_acc (the row-streaming term reverse with the x-gradient pass P*(v) inside) against
 grr_bwd_term_fused + grr_bwd_stencil mode 3 on the same inputs, for the three operator terms: the
 accumulated x-gradient, the weight gradient and the per-graph / per-channel reductions.  Shapes cover
 one- and two-column lanes (W <= 128, where the fused pass runs), row segments with a ragged last segment
 (the segment's halo rows), the image's first and last rows, F up to 16.  The two-pass path
-is itself pinned by test_gpu_term_rows.py and the gradient tests."""
+is itself pinned by test_gpu_term_rows.py and the gradient tests.  grr_bwd_cg_glue with the half level's
+x-gradient folded in (gx_half) against grr_bwd_unpool2_acc + the plain glue."""
 import pytest
 import torch
 
@@ -120,3 +123,54 @@ def test_training_gradients_with_and_without_acc(K):
     # terms far larger) that rounding reaches a few 1e-5 of the largest gradient entry
     for k in ref:
         assert rel_err(got[k].cpu(), ref[k].cpu()) <= 2e-4, (k, rel_err(got[k].cpu(), ref[k].cpu()))
+
+
+@pytest.mark.parametrize("shape", [(2, 6, 8, 12), (1, 3, 6, 10), (2, 12, 32, 64)], ids=str)
+def test_cg_glue_with_half_level_equals_unpool_then_glue(K, shape):
+    """grr_bwd_cg_glue's gx_half (U of the half level's x-gradient folded into the glue pass) against
+    grr_bwd_unpool2_acc followed by the plain glue; W % 4 != 0 takes the scalar path."""
+    b, c, h, w = shape
+    G = 3
+    torch.manual_seed(h * w)
+    t = lambda *s: torch.randn(*s, device=DEV)  # noqa: E731
+    gx, u, gun, up, gbb = (t(b, c, h, w) for _ in range(5))
+    gxh = t(b, c, h // 2, w // 2)
+    alpha, beta = torch.rand(G, device=DEV), torch.rand(G, device=DEV)
+
+    def run(fold):
+        ga, gb, bb = torch.zeros(G, device=DEV), torch.zeros(G, device=DEV), gbb.clone()
+        x = gx.clone()
+        if not fold:
+            K.bwd_unpool2_acc(gxh, x)
+        gu, gxo = K.bwd_cg_glue(x, u, gun, up, alpha, beta, bb, ga, gb, G, gx_half=gxh if fold else None)
+        torch.cuda.synchronize()
+        return [v.cpu() for v in (gu, gxo, bb, ga, gb)]
+
+    for a, r in zip(run(True), run(False)):
+        assert torch.equal(a, r) or rel_err(a, r) <= 1e-6, rel_err(a, r)
+
+
+def test_training_gradients_with_and_without_unpool_glue(K):
+    """msgf's mixture reverse with the half level's U folded into the next glue pass against the separate
+    unpool-accumulate pass: the same arithmetic, so the same gradients."""
+    import irdu_amd
+    from irdu_amd import solver_grad as SG
+    from tests.test_gpu_parity import perturb_mixture
+    torch.manual_seed(6)
+    m = irdu_amd.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=5)
+    perturb_mixture(m.localfilter, 11)
+    m = m.to(DEV)
+    y = torch.rand(2, 3, 64, 64, device=DEV)
+
+    def grads(fold):
+        SG.UNPOOL_GLUE = fold
+        try:
+            m.zero_grad(set_to_none=True)
+            m(y).square().mean().backward()
+            return {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
+        finally:
+            SG.UNPOOL_GLUE = True
+
+    ref, got = grads(False), grads(True)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]) or rel_err(got[k], ref[k]) <= 1e-6, (k, rel_err(got[k], ref[k]))
