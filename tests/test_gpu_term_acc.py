@@ -174,3 +174,17 @@ def test_training_gradients_with_and_without_unpool_glue(K):
     ref, got = grads(False), grads(True)
     for k in ref:
         assert torch.equal(got[k], ref[k]) or rel_err(got[k], ref[k]) <= 1e-6, (k, rel_err(got[k], ref[k]))
+
+
+@pytest.mark.parametrize("shape", [(2, 5, 8, 12), (3, 4, 6, 10), (16, 96, 64, 128), (1, 1, 2, 4), (2, 3, 256, 256)],
+                         ids=str)
+def test_pool2_equals_oracle_mean(K, shape):
+    """grr_pool2 (the D the reverse applies to each stage's iterate and gradient) against the oracle's D in
+    float64."""
+    from oracle import graph_oracle as O
+    torch.manual_seed(sum(shape))
+    x = torch.randn(*shape)
+    got = K.pool2(x.to(DEV)).cpu()
+    want = O.pool2(x.double())
+    assert got.shape == want.shape
+    assert rel_err(got, want) <= 1e-6
