@@ -618,9 +618,14 @@ __global__ __launch_bounds__(NT) void lincomb_kernel(const float* __restrict__ x
 //   gbb += gu;  gx_out = gx' - gu  (gx_out may alias gx).                 grid (chunks, B*G)
 // gxh (optional): the previous stage's half-level x-gradient not yet added, gx' = gx + U gxh (the 2x2
 // unpool-accumulate, unpool2_acc_kernel's arithmetic) -- one read of gx instead of U's read + write.
+// pj (optional, V4 only): the previous stage's full-level x-gradient pass not yet applied,
+// gx' = (gx + s1 P1*(v1)) + s2 P2*(v2) before U -- padj2_kernel's arithmetic and order.
+struct GluePadj {
+  const float *v1, *t1, *s1, *v2, *t2, *s2;
+};
 template <bool V4>
-__global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const float* __restrict__ gxh,
-                                                     const float* __restrict__ u,
+__global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const float* __restrict__ gxh, GluePadj pj,
+                                                     int F, const float* __restrict__ u,
                                                      const float* __restrict__ gun, const float* __restrict__ up,
                                                      const float* __restrict__ alpha,
                                                      const float* __restrict__ beta_next, float* __restrict__ gu_out,
@@ -644,6 +649,17 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
       const int64_t o = base + 4 * i;
       f4 x = *reinterpret_cast<const f4*>(gx + o);
       const f4 uv = *reinterpret_cast<const f4*>(u + o);
+      if (pj.v1) {   // W % 4 == 0
+        const int li = (int)(4 * i), f = li / HW, p = li - f * HW, r = p / W, c = p - r * W;
+        const int ch = g * F + f;
+        const int64_t po = ((int64_t)bg * F + f) * HW;
+        const float *k1 = pj.t1 + ch * 5, *k2 = pj.t2 + ch * 5;
+        f4 y1 = padj4(pj.v1 + po, k1[0], k1[1], k1[2], k1[3], k1[4], r, c, H, W);
+        f4 y2 = padj4(pj.v2 + po, k2[0], k2[1], k2[2], k2[3], k2[4], r, c, H, W);
+        y1 *= pj.s1[g];
+        y2 *= pj.s2[g];
+        x = (x + y1) + y2;
+      }
       if (gxh) {   // W % 4 == 0: the four columns sit over two half-level columns
         const f2 q = *reinterpret_cast<const f2*>(gxh + half_at((int)(4 * i)));
         x.x += 0.25f * q.x; x.y += 0.25f * q.x; x.z += 0.25f * q.y; x.w += 0.25f * q.y;
@@ -2050,21 +2066,28 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   return st != GRR_OK ? st : rs.finish("grr_bwd_graph_dot");
 }
 
-grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* u, const float* gu_next,
-                           const float* u_prev, const float* alpha, const float* beta_next, float* gu, float* gbb,
-                           float* gx_out, float* galpha, float* gbeta, int B, int G, int F, int H, int W,
-                           void* stream) {
+grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v1, const float* taps1,
+                           const float* scale1, const float* v2, const float* taps2, const float* scale2,
+                           const float* u, const float* gu_next, const float* u_prev, const float* alpha,
+                           const float* beta_next, float* gu, float* gbb, float* gx_out, float* galpha, float* gbeta,
+                           int B, int G, int F, int H, int W, void* stream) {
   clear_error();
   GRR_REQUIRE(gx && u && alpha && gu && gx_out && galpha && (!gu_next || beta_next) && (!u_prev || gbeta) && B > 0 &&
                   G > 0 && F > 0 && H > 0 && W > 0 && (!gx_half || (H % 2 == 0 && W % 2 == 0)),
               GRR_ERR_INVALID_ARG, "grr_bwd_cg_glue: bad args");
+  GRR_REQUIRE(!v1 == !v2 && (!v1 || (taps1 && scale1 && taps2 && scale2)), GRR_ERR_INVALID_ARG,
+              "grr_bwd_cg_glue: v1, v2 with their taps and scales, or neither");
   GRR_REQUIRE((int64_t)B * G <= 65535 && (int64_t)F * H * W < (1ll << 31), GRR_ERR_UNSUPPORTED,
               "grr_bwd_cg_glue: B*G > 65535 or a (b, graph) slab of 2^31 floats");
   const int64_t n = (int64_t)F * H * W;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   const bool v4 = n % 4 == 0 && al16(gx) && al16(u) && al16(gu) && al16(gx_out) && (!gu_next || al16(gu_next)) &&
                   (!u_prev || al16(u_prev)) && (!gbb || al16(gbb)) &&
-                  (!gx_half || (W % 4 == 0 && ((uintptr_t)gx_half & 7) == 0));
+                  (!gx_half || (W % 4 == 0 && ((uintptr_t)gx_half & 7) == 0)) &&
+                  (!v1 || (W % 4 == 0 && al16(v1) && al16(v2)));
+  GRR_REQUIRE(!v1 || v4, GRR_ERR_UNSUPPORTED,
+              "grr_bwd_cg_glue: the x-gradient pass needs W %% 4 == 0 and 16-byte aligned planes (W = %d)", W);
+  const GluePadj pj{v1, taps1, scale1, v2, taps2, scale2};
   const int chunks = chunks_for(v4 ? n / 4 : n, (int64_t)B * G);
   const dim3 grid(chunks, B * G);
   RedScratch rs((hipStream_t)stream);
@@ -2072,11 +2095,11 @@ grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* u
   grr_status st = rs.alloc("grr_bwd_cg_glue");
   if (st != GRR_OK) return st;
   if (v4)
-    hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, u, gu_next, u_prev,
-                       alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
+    hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, pj, F, u, gu_next,
+                       u_prev, alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
   else
-    hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, u, gu_next, u_prev,
-                       alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
+    hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, pj, F, u, gu_next,
+                       u_prev, alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
   st = launch_status("grr_bwd_cg_glue");
   return st != GRR_OK ? st : rs.finish("grr_bwd_cg_glue");
 }

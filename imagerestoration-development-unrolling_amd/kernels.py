@@ -882,11 +882,18 @@ def bwd_lincomb(x: Tensor, sa: Optional[Tensor], y: Optional[Tensor], sb: Option
 
 def bwd_cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Optional[Tensor], alpha: Tensor,
                 beta_next: Optional[Tensor], gbb: Optional[Tensor], galpha: Tensor, gbeta: Optional[Tensor],
-                n_graphs: int, inplace: bool = False, gx_half: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+                n_graphs: int, inplace: bool = False, gx_half: Optional[Tensor] = None,
+                padj: Optional[tuple] = None) -> Tuple[Tensor, Tensor]:
     """One reverse step of the stage recurrence glue (grr_bwd_cg_glue): returns (gu, gx - gu);
     galpha / gbeta accumulate <gx, u> / <gu, u_prev>, gbb += gu.  inplace: gx - gu overwrites gx.
-    gx_half: a half-level x-gradient still to be added (gx taken as gx + U gx_half, one pass)."""
-    dev = _check("bwd_cg_glue", gx, gx_half, u, gu_next, u_prev, alpha, beta_next, gbb, galpha, gbeta)
+    Passes of the previous stage folded in (gx taken as ((gx + s1 P1*(v1)) + s2 P2*(v2)) + U gx_half):
+    padj = (v1, taps1, s1, v2, taps2, s2), bwd_padj2's operands (padj2_ok); gx_half, bwd_unpool2_acc's."""
+    v1, t1, s1, v2, t2, s2 = padj if padj is not None else (None,) * 6
+    dev = _check("bwd_cg_glue", gx, gx_half, v1, t1, s1, v2, t2, s2, u, gu_next, u_prev, alpha, beta_next, gbb,
+                 galpha, gbeta)
+    for t in (v1, v2):
+        if t is not None and t.shape != gx.shape:
+            raise ValueError("bwd_cg_glue: padj shapes")
     for t in (u, gu_next, u_prev, gbb):
         if t is not None and t.shape != gx.shape:
             raise ValueError("bwd_cg_glue: shapes")
@@ -896,8 +903,10 @@ def bwd_cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Option
     gu = torch.empty_like(gx)
     gx_out = gx if inplace else torch.empty_like(gx)
     n_rw = 2 + int(gu_next is not None) + int(u_prev is not None) + 2 * int(gbb is not None) + 2
+    n_rw += 2 * int(v1 is not None)
     _launch("bwd_cg_glue", 4 * (gx.numel() * n_rw + (0 if gx_half is None else gx_half.numel())), "grr_bwd_cg_glue",
-            gx.data_ptr(), _ptr(gx_half), u.data_ptr(), _ptr(gu_next), _ptr(u_prev), alpha.data_ptr(),
+            gx.data_ptr(), _ptr(gx_half), _ptr(v1), _ptr(t1), _ptr(s1), _ptr(v2), _ptr(t2), _ptr(s2),
+            u.data_ptr(), _ptr(gu_next), _ptr(u_prev), alpha.data_ptr(),
             _ptr(beta_next), gu.data_ptr(), _ptr(gbb), gx_out.data_ptr(), galpha.data_ptr(), _ptr(gbeta),
             *_bgfhw(gx, n_graphs), _stream(dev))
     return gu, gx_out

@@ -135,20 +135,25 @@ class _Level:
         self.gtapL, self.gtapG = z(self.tapsL), z(self.tapsG)
         self.gmu, self.gro, self.ggam = z(log_mu), z(log_ro), z(log_gamma)
 
-    def terms_bwd(self, x: Tensor, g: Tensor, coef: float, out: Tensor, glr: bool = True) -> None:
+    def terms_bwd(self, x: Tensor, g: Tensor, coef: float, out: Tensor, glr: bool = True,
+                  defer: bool = False) -> Optional[tuple]:
         """out += coef * (mu L^T + ro G^T) g, and coef * d<g, mu L x + ro G x>/d(params) into the buffers.
-        With both one-pass term reverses, the two x-gradient passes run as one sweep (grr_bwd_padj2)."""
+        With both one-pass term reverses, the two x-gradient passes run as one sweep (grr_bwd_padj2);
+        defer: that sweep's operands are returned instead (the next bwd_cg_glue applies them)."""
         acc = _acc_ok(K.TERM_PAIR, x, g, out, self.g) and (not glr or _acc_ok(K.TERM_GLR, x, g, out, self.g))
         if glr and PADJ2 and not acc and _use_fused(x, self.g) and K.padj2_ok(x):
             vl, scl = glr_term_bwd(x, g, self.tapsL, self.wL, self.mu, coef, self.g, out, self.gwL, self.gmu,
                                    self.gtapL, defer=True)
             vg, scg = gtv_term_bwd(x, g, self.tapsG, self.cG, self.ro, coef, self.g, out, self.gcG, self.gro,
                                    self.gtapG, defer=True)
+            if defer:
+                return (vl, self.tapsL, scl, vg, self.tapsG, scg)
             K.bwd_padj2(vl, self.tapsL, scl, vg, self.tapsG, scg, out, self.g)
-            return
+            return None
         if glr:
             glr_term_bwd(x, g, self.tapsL, self.wL, self.mu, coef, self.g, out, self.gwL, self.gmu, self.gtapL)
         gtv_term_bwd(x, g, self.tapsG, self.cG, self.ro, coef, self.g, out, self.gcG, self.gro, self.gtapG)
+        return None
 
     def prox_bwd(self, x: Tensor, g: Tensor, out: Tensor) -> None:
         """out += ro C^T-part reverse of the prox rhs term ro T(Ct phi(C P x)); parameter gradients."""
@@ -190,6 +195,8 @@ def _level_side(dev: torch.device) -> "torch.cuda.Stream":
 # (grr_bwd_cg_glue's gx_half: U folded into the pass that reads gx next) instead of its own
 # unpool-accumulate pass (a read + write of the full-resolution gradient)
 UNPOOL_GLUE = True
+# ... and the full level's padj2 sweep of stage k likewise (grr_bwd_cg_glue's v1 / v2), where it runs
+PADJ_GLUE = True
 
 
 def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
@@ -227,13 +234,14 @@ def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
 
 def cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Optional[Tensor], alpha: Tensor, beta: Tensor,
             gbb: Optional[Tensor], galpha: Tensor, gbeta: Tensor, k: int, g: int, owned: bool,
-            gx_half: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+            gx_half: Optional[Tensor] = None, padj: Optional[tuple] = None) -> Tuple[Tensor, Tensor]:
     """Reverse of stage k's recurrence glue (x' = x + a_k u_k, u_k = r - A x + b_k u_{k-1}) without the
     operator term: returns (gu_k, gx' - gu_k); ga_k, gb_k (when u_prev) and gbb accumulate.  owned: gx
     is this sweep's own buffer and is overwritten."""
     gu, gx2 = K.bwd_cg_glue(gx, u, gu_next, u_prev, alpha[k].contiguous(),
                             beta[k + 1].contiguous() if gu_next is not None else None, gbb, galpha[k],
-                            gbeta[k] if u_prev is not None else None, g, inplace=owned, gx_half=gx_half)
+                            gbeta[k] if u_prev is not None else None, g, inplace=owned, gx_half=gx_half,
+                            padj=padj)
     return gu, gx2
 
 
@@ -326,19 +334,28 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
     galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
 
     def a_bwd(x, gg, coef, out, glr=True, defer=False):   # out += coef * (A - I)^T gg (+ parameter gradients)
-        return _two_level(l0, l1, x, gg, out, lambda lv, xx, g2, o: lv.terms_bwd(xx, g2, coef, o, glr), defer)
+        # defer: the full level's padj2 operands and the half level's x-gradient are returned for the
+        # next bwd_cg_glue instead of being added to out here
+        pend = []
+
+        def fn(lv, xx, g2, o):
+            r = lv.terms_bwd(xx, g2, coef, o, glr, defer=defer and PADJ_GLUE and lv is l0)
+            if r is not None:
+                pend.append(r)
+        gxh = _two_level(l0, l1, x, gg, out, fn, defer)
+        return gxh, (pend[0] if pend else None)
 
     gx = gouts[0].contiguous()
     gy = torch.zeros_like(y)
     if n_st > 1:
         gbb = torch.zeros_like(y)
-        gu_next, gxh = None, None
+        gu_next, gxh, pj = None, None, None
         for k in range(n_st - 1, 0, -1):
             # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue), with the
-            # previous stage's half-level x-gradient added on the way in
+            # previous stage's full-level x-gradient pass and half-level x-gradient added on the way in
             gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
-                             galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh)
-            gxh = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1)   #   - (A - I)^T gu
+                             galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh, padj=pj)
+            gxh, pj = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1)   #   - (A - I)^T gu
             gu_next = gu
         # b_B = y + prox terms(x_1)
         K.bwd_lincomb(gbb, None, None, None, g, out=gy, accumulate=True)

@@ -381,12 +381,15 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
  * operator term): galpha[g] += <gx, u>; gu = alpha[g] gx + beta_next[g] gu_next (gu_next may be
  * NULL); gbeta[g] += <gu, u_prev> (u_prev may be NULL); gbb += gu (gbb may be NULL);
  * gx_out = gx - gu (may alias gx).  Signals [B, G*F, H, W]; alpha, beta_next, galpha, gbeta [G].
- * gx_half (may be NULL): a half-level x-gradient [B, G*F, H/2, W/2] still to be added, gx taken as
- * gx + U gx_half (grr_bwd_unpool2_acc folded into the pass; H, W even). */
-grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* u, const float* gu_next,
-                           const float* u_prev, const float* alpha, const float* beta_next, float* gu, float* gbb,
-                           float* gx_out, float* galpha, float* gbeta, int B, int G, int F, int H, int W,
-                           void* stream);
+ * Two passes of the previous reverse stage may be folded in, gx taken as
+ * ((gx + scale1[g] S1*(v1)) + scale2[g] S2*(v2)) + U gx_half:
+ * v1, v2 (both or neither; taps [G*F,5], scales [G]): grr_bwd_padj2's operands (W % 4 == 0, 16-byte
+ * aligned); gx_half: a half-level x-gradient [B, G*F, H/2, W/2] (grr_bwd_unpool2_acc; H, W even). */
+grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v1, const float* taps1,
+                           const float* scale1, const float* v2, const float* taps2, const float* scale2,
+                           const float* u, const float* gu_next, const float* u_prev, const float* alpha,
+                           const float* beta_next, float* gu, float* gbb, float* gx_out, float* galpha, float* gbeta,
+                           int B, int G, int F, int H, int W, void* stream);
 grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,
                            int accumulate, int B, int G, int F, int H, int W, void* stream);
 /* out [B,C,H,W] += U(xd): 0.25 * xd(q/2) (conv_transpose2d of scaling_kernel01, REF:676-679). */

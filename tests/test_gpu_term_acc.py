@@ -150,9 +150,45 @@ def test_cg_glue_with_half_level_equals_unpool_then_glue(K, shape):
         assert torch.equal(a, r) or rel_err(a, r) <= 1e-6, rel_err(a, r)
 
 
+@pytest.mark.parametrize("shape", [(2, 6, 8, 12), (2, 12, 32, 64)], ids=str)
+def test_cg_glue_with_padj_equals_padj2_then_glue(K, shape):
+    """grr_bwd_cg_glue with the previous stage's padj2 sweep folded in (v1 / v2) and the half level's U
+    against grr_bwd_padj2 + grr_bwd_unpool2_acc + the plain glue: the same operations in the same order."""
+    b, c, h, w = shape
+    G = 3
+    torch.manual_seed(h + w)
+    t = lambda *s: torch.randn(*s, device=DEV)  # noqa: E731
+    gx, u, gun, up, gbb, v1, v2 = (t(b, c, h, w) for _ in range(7))
+    gxh = t(b, c, h // 2, w // 2)
+    t1, t2 = t(c, 5), t(c, 5)
+    s1, s2 = torch.rand(G, device=DEV) + 0.5, torch.rand(G, device=DEV) + 0.5
+    alpha, beta = torch.rand(G, device=DEV), torch.rand(G, device=DEV)
+
+    def run(fold):
+        ga, gb, bb = torch.zeros(G, device=DEV), torch.zeros(G, device=DEV), gbb.clone()
+        x = gx.clone()
+        if not fold:
+            K.bwd_padj2(v1, t1, s1, v2, t2, s2, x, G)
+            K.bwd_unpool2_acc(gxh, x)
+        gu, gxo = K.bwd_cg_glue(x, u, gun, up, alpha, beta, bb, ga, gb, G, gx_half=gxh if fold else None,
+                                padj=(v1, t1, s1, v2, t2, s2) if fold else None)
+        torch.cuda.synchronize()
+        return [v.cpu() for v in (gu, gxo, bb, ga, gb)]
+
+    # the same operations in the same order; the compiler may contract the scale multiply into a different
+    # fma in the two kernels (one rounding), which the per-graph sums (alpha, beta) carry at fp32 level
+    n = b * (c // G) * h * w
+    for name, a, r in zip(("gu", "gx", "gbb", "galpha", "gbeta"), run(True), run(False)):
+        if name in ("galpha", "gbeta"):
+            err = float((a.double() - r.double()).abs().max())
+            assert err <= 2e-6 * max(float(r.abs().max()), n ** 0.5), (name, err)
+        else:
+            assert rel_err(a, r) <= 1e-6, (name, rel_err(a, r))
+
+
 def test_training_gradients_with_and_without_unpool_glue(K):
-    """msgf's mixture reverse with the half level's U folded into the next glue pass against the separate
-    unpool-accumulate pass: the same arithmetic, so the same gradients."""
+    """msgf's mixture reverse with the previous stage's padj2 sweep and the half level's U folded into the
+    next glue pass against the separate passes: the same arithmetic, so the same gradients."""
     import irdu_amd
     from irdu_amd import solver_grad as SG
     from tests.test_gpu_parity import perturb_mixture
@@ -160,20 +196,24 @@ def test_training_gradients_with_and_without_unpool_glue(K):
     m = irdu_amd.MultiScaleGraphFilter(3, 3, ngraphs=8, n_cgd_iters=5)
     perturb_mixture(m.localfilter, 11)
     m = m.to(DEV)
-    y = torch.rand(2, 3, 64, 64, device=DEV)
+    y = torch.rand(2, 3, 96, 256, device=DEV)   # W = 256: the full level takes the padj2 sweep
 
-    def grads(fold):
-        SG.UNPOOL_GLUE = fold
+    def grads(unpool, padj):
+        SG.UNPOOL_GLUE, SG.PADJ_GLUE = unpool, padj
         try:
             m.zero_grad(set_to_none=True)
             m(y).square().mean().backward()
             return {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
         finally:
-            SG.UNPOOL_GLUE = True
+            SG.UNPOOL_GLUE, SG.PADJ_GLUE = True, True
 
-    ref, got = grads(False), grads(True)
-    for k in ref:
-        assert torch.equal(got[k], ref[k]) or rel_err(got[k], ref[k]) <= 1e-6, (k, rel_err(got[k], ref[k]))
+    ref = grads(False, False)
+    for flags, tol in (((True, False), 1e-6), ((True, True), 1e-4)):
+        # U folded in: the same arithmetic.  padj2 folded in: the same operations, one fma contraction may
+        # differ (see above), carried through the reverse and image-wide sums that cancel
+        got = grads(*flags)
+        for k in ref:
+            assert torch.equal(got[k], ref[k]) or rel_err(got[k], ref[k]) <= tol, (flags, k, rel_err(got[k], ref[k]))
 
 
 @pytest.mark.parametrize("shape", [(2, 5, 8, 12), (3, 4, 6, 10), (16, 96, 64, 128), (1, 1, 2, 4), (2, 3, 256, 256)],
