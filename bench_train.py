@@ -31,8 +31,9 @@ HBM_PEAK_GBPS = 8000.0
 def load_traffic(kind, model, batch, size):
     """Per-launch HBM bytes (PMC, scripts/pmc_train.sh) of the reverse kernel kind at this workload,
     or None when no summary of that exact shape is committed under profiles/."""
-    for rnd in ("r04", "r03"):          # the newest round's summary of this exact workload
-        path = os.path.join(ROOT, "profiles", rnd, f"traffic_{kind}_{model}.json")
+    for rnd, name in (("r04", f"traffic_{kind}_{model}_b{batch}_s{size}.json"), ("r04", f"traffic_{kind}_{model}.json"),
+                      ("r03", f"traffic_{kind}_{model}.json")):   # the newest summary of this exact workload
+        path = os.path.join(ROOT, "profiles", rnd, name)
         if not os.path.exists(path):
             continue
         with open(path) as f:
