@@ -123,6 +123,8 @@ def main():
                     help="half level's U folded into the next glue pass (solver_grad.UNPOOL_GLUE; A/B runs)")
     ap.add_argument("--padj-glue", type=int, choices=[0, 1], default=1,
                     help="full level's x-gradient sweep folded into the next glue pass (solver_grad.PADJ_GLUE; A/B)")
+    ap.add_argument("--ln-skip", type=int, choices=[0, 1], default=1,
+                    help="LNB skip term inside the norm's reverse pass (solver_grad.LN_SKIP_FUSED; A/B runs)")
     ap.add_argument("--watchdog", type=float, default=0.0,
                     help="dump every thread's Python stack to stderr each N seconds (hang diagnosis)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU; spawned when not under torchrun)")
@@ -155,6 +157,7 @@ def main():
     SGK.TERM_ACC = bool(args.term_acc)
     SGK.UNPOOL_GLUE = bool(args.unpool_glue)
     SGK.PADJ_GLUE = bool(args.padj_glue)
+    SGK.LN_SKIP_FUSED = bool(args.ln_skip)
     torch.manual_seed(2204)
     if args.model == "abstract":
         model = irdu_amd.AbtractMultiScaleGraphFilter(3, 3, n_cgd_iters=args.stages, **D_ARGS)

@@ -108,6 +108,7 @@ SIGNATURES = {
     "grr_interleave2x2": [P, P, I, I, I, I, P],
     "grr_lnb_norm": [P, P, P, P, I, I, L, P],
     "grr_lnb_norm_bwd": [P, P, P, P, P, P, I, I, L, P],
+    "grr_lnb_norm_bwd_skip": [P, P, P, P, P, P, P, P, P, I, I, L, P],
     "grr_dwconv3": [P, P, P, I, I, I, I, P],
     "grr_dwconv3_bwd": [P, P, P, P, P, I, I, I, I, P],
     "grr_lnb_gate": [P, P, P, P, I, I, L, P],

@@ -70,9 +70,16 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(const float* __restrict__ x,
 }
 
 // gx_k (+)= ln_w_k gn_k isd - (x_k - mean) isd^3 / (C-1) * sum_c ln_w_c gn_c x_c
+// SKIP: the block's skip term in the same pass, gx_k = s0 gout_k + (...) (written, not accumulated) and
+// gdot += <gout, x> (the skip weight's gradient) -- no separate scale and dot passes over gout
+template <bool SKIP>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(const float* __restrict__ x, const float* __restrict__ lnw,
                                                     const float* __restrict__ isd, const float* __restrict__ gn,
-                                                    float* __restrict__ gx, int C, int64_t P, int64_t npix) {
+                                                    const float* __restrict__ gout, const float* __restrict__ skip,
+                                                    float* __restrict__ gx, Red gdot, int C, int64_t P,
+                                                    int64_t npix) {
+  const float s0 = SKIP ? skip[0] : 0.f;
+  float dacc = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < npix; i += (int64_t)gridDim.x * NT) {
     const int64_t b = i / P, p = i - b * P;
     const float* xp = x + b * C * P + p;
@@ -87,12 +94,24 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(const float* __restrict__ x,
     const float mean = s / (float)C, r = isd[i];
     const float k = dot * r * r * r / (float)(C - 1);
     float* gxp = gx + b * C * P + p;
+    if constexpr (SKIP) {
+      const float* op = gout + b * C * P + p;
 #pragma unroll 8
-    for (int c = 0; c < C; ++c) {
-      const int64_t o = (int64_t)c * P;
-      gxp[o] += lnw[c] * gp[o] * r - (xp[o] - mean) * k;
+      for (int c = 0; c < C; ++c) {
+        const int64_t o = (int64_t)c * P;
+        const float go = op[o];
+        dacc += go * xp[o];
+        gxp[o] = __fmul_rn(s0, go) + (lnw[c] * gp[o] * r - (xp[o] - mean) * k);
+      }
+    } else {
+#pragma unroll 8
+      for (int c = 0; c < C; ++c) {
+        const int64_t o = (int64_t)c * P;
+        gxp[o] += lnw[c] * gp[o] * r - (xp[o] - mean) * k;
+      }
     }
   }
+  if constexpr (SKIP) block_red_put(gdot, 0, blockIdx.x, dacc);
 }
 
 // gw[c] += sum_{b,p} u v isd(b,p)          grid (chunks, B*C)
@@ -867,8 +886,8 @@ grr_status grr_lnb_norm_bwd(const float* x, const float* ln_w, const float* isd,
               "grr_lnb_norm_bwd: bad args");
   GRR_REQUIRE((int64_t)B * C <= 65535, GRR_ERR_UNSUPPORTED, "grr_lnb_norm_bwd: B*C > 65535");
   const int64_t np = (int64_t)B * P;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid_for(np)), dim3(NT), 0, (hipStream_t)stream, x, ln_w, isd, gn, gx, C,
-                     P, np);
+  hipLaunchKernelGGL(ln_bwd_kernel<false>, dim3(grid_for(np)), dim3(NT), 0, (hipStream_t)stream, x, ln_w, isd, gn,
+                     nullptr, nullptr, gx, Red{nullptr, 0}, C, P, np);
   grr_status st = launch_status("grr_lnb_norm_bwd/data");
   if (st != GRR_OK) return st;
   const int chunks = chunks_for(P, (int64_t)B * C);
@@ -880,6 +899,27 @@ grr_status grr_lnb_norm_bwd(const float* x, const float* ln_w, const float* isd,
                      P);
   st = launch_status("grr_lnb_norm_bwd/weight");
   return st != GRR_OK ? st : rs.finish("grr_lnb_norm_bwd/weight");
+}
+
+grr_status grr_lnb_norm_bwd_skip(const float* x, const float* ln_w, const float* isd, const float* gn,
+                                 const float* gout, const float* skip, float* gx, float* gln_w, float* gskip0, int B,
+                                 int C, int64_t P, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && ln_w && isd && gn && gout && skip && gx && gln_w && gskip0 && gx != gout && B > 0 && C > 1 && P > 0,
+              GRR_ERR_INVALID_ARG, "grr_lnb_norm_bwd_skip: bad args");
+  GRR_REQUIRE((int64_t)B * C <= 65535, GRR_ERR_UNSUPPORTED, "grr_lnb_norm_bwd_skip: B*C > 65535");
+  const int64_t np = (int64_t)B * P;
+  const int grid = grid_for(np), chunks = chunks_for(P, (int64_t)B * C);
+  hipStream_t s = (hipStream_t)stream;
+  RedScratch rs(s);
+  const int id = rs.plan(gskip0, 1, (uint32_t)grid), iw = rs.plan(gln_w, C, (uint32_t)B * chunks);
+  grr_status st = rs.alloc("grr_lnb_norm_bwd_skip");
+  if (st != GRR_OK) return st;
+  hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3(grid), dim3(NT), 0, s, x, ln_w, isd, gn, gout, skip, gx, rs.red(id), C,
+                     P, np);
+  hipLaunchKernelGGL(ln_wgrad_kernel, dim3(chunks, B * C), dim3(NT), 0, s, gn, x, isd, rs.red(iw), C, P);
+  st = launch_status("grr_lnb_norm_bwd_skip");
+  return st != GRR_OK ? st : rs.finish("grr_lnb_norm_bwd_skip");
 }
 
 grr_status grr_dwconv3(const float* h, const float* wdw, float* out, int B, int C, int H, int W, void* stream) {

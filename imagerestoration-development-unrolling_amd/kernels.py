@@ -980,6 +980,21 @@ def lnb_norm_bwd(x: Tensor, ln_w: Tensor, isd: Tensor, gn: Tensor, gx: Tensor, g
             gn.data_ptr(), gx.data_ptr(), gln_w.data_ptr(), b, c, h * w, _stream(dev))
 
 
+def lnb_norm_bwd_skip(x: Tensor, ln_w: Tensor, isd: Tensor, gn: Tensor, gout: Tensor, skip: Tensor,
+                      gln_w: Tensor, gskip0: Tensor) -> Tensor:
+    """The LNB reverse's tail in one pass (grr_lnb_norm_bwd_skip): returns gx = skip[0] gout + d<gn, n>/dx;
+    gskip0 += <gout, x>, gln_w += sum gn x isd."""
+    dev = _check("lnb_norm_bwd", x, ln_w, isd, gn, gout, skip, gln_w, gskip0)
+    b, c, h, w = x.shape
+    if gout.shape != x.shape or gn.shape != x.shape:
+        raise ValueError("lnb_norm_bwd_skip: shapes")
+    gx = torch.empty_like(x)
+    _launch("lnb_norm_bwd", 24 * x.numel(), "grr_lnb_norm_bwd_skip", x.data_ptr(), ln_w.data_ptr(), isd.data_ptr(),
+            gn.data_ptr(), gout.data_ptr(), skip.data_ptr(), gx.data_ptr(), gln_w.data_ptr(), gskip0.data_ptr(), b, c,
+            h * w, _stream(dev))
+    return gx
+
+
 def dwconv3(h: Tensor, wdw: Tensor) -> Tensor:
     dev = _check("dwconv3", h, wdw)
     b, c, hh, ww = h.shape

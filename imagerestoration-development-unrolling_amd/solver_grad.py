@@ -197,6 +197,8 @@ def _level_side(dev: torch.device) -> "torch.cuda.Stream":
 UNPOOL_GLUE = True
 # ... and the full level's padj2 sweep of stage k likewise (grr_bwd_cg_glue's v1 / v2), where it runs
 PADJ_GLUE = True
+# LNB / FFBlock reverse: the skip term (s0 gout, <gout, x>) inside the norm's reverse pass
+LN_SKIP_FUSED = True
 
 
 def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
@@ -816,7 +818,8 @@ def _lnb_bwd(consts, inputs, outs, saved, gouts, needs):
         hp = K.dwconv3(hh, Wdw)
         gate, _ = K.lnb_gate(hp)
     gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
-    K.bwd_graph_dot(gout, x, gskip[0:1], 1)
+    if not LN_SKIP_FUSED:
+        K.bwd_graph_dot(gout, x, gskip[0:1], 1)
     s1 = skip[1:2].contiguous()
     # gw2 = s1 gout gate^T; gq = W2^T gout: the gate reverse takes s1 and returns
     # <gout, W2 gate> = <gq, gate> for the skip weight (no recomputed W2 gate)
@@ -835,10 +838,19 @@ def _lnb_bwd(consts, inputs, outs, saved, gouts, needs):
     gw1 = K.wgrad(gh.contiguous(), n.contiguous())
     gn = K.conv1x1(gh, W1.t().contiguous().view(c, hid2, 1, 1))
     del gh, n
-    gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
-    glnw = torch.zeros_like(lnw)
-    K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
+    gx, glnw = _ln_skip_bwd(x, lnw, isd, gn, gout, skip, gskip)
     return gx, glnw.view_as(ln_w), gw1.view_as(w1), gwdw.view_as(wdw), gw2.view_as(w2), gskip
+
+
+def _ln_skip_bwd(x: Tensor, lnw: Tensor, isd: Tensor, gn: Tensor, gout: Tensor, skip: Tensor, gskip: Tensor):
+    """gx = s0 gout + the norm's data gradient, gskip[0] += <gout, x> (the skip weight), and the norm's
+    weight gradient: one pass over gout (grr_lnb_norm_bwd_skip) or the dot / scale / norm passes."""
+    glnw = torch.zeros_like(lnw)
+    if LN_SKIP_FUSED:
+        return K.lnb_norm_bwd_skip(x, lnw, isd, gn, gout, skip.contiguous(), glnw, gskip[0:1]), glnw
+    gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
+    K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
+    return gx, glnw
 
 
 LNB = OpaqueFunction("lnb_train", 1, _lnb_fwd, _lnb_bwd, _lnb_fake)
@@ -876,7 +888,8 @@ def _ffn_bwd(consts, inputs, outs, saved, gouts, needs):
     hh = K.conv1x1(n, Win.view(hid2, c, 1, 1))
     gate = K.ffn_dw3_gate(hh, Wdw)
     gskip = torch.zeros(2, dtype=torch.float32, device=x.device)
-    K.bwd_graph_dot(gout, x, gskip[0:1], 1)
+    if not LN_SKIP_FUSED:
+        K.bwd_graph_dot(gout, x, gskip[0:1], 1)
     s1 = skip[1:2].contiguous()
     gw_out = K.wgrad(gout, gate) * s1                  # d/dW_out of s1 W_out gate
     del gate
@@ -887,9 +900,7 @@ def _ffn_bwd(consts, inputs, outs, saved, gouts, needs):
     gw_in = K.wgrad(gh, n)
     gn = K.conv1x1(gh, Win.t().contiguous().view(c, hid2, 1, 1))
     del gh, n
-    gx = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)          # s0 * gout
-    glnw = torch.zeros_like(lnw)
-    K.lnb_norm_bwd(x, lnw, isd, gn, gx, glnw)
+    gx, glnw = _ln_skip_bwd(x, lnw, isd, gn, gout, skip, gskip)
     return gx, glnw.view_as(ln_w), gw_in.view_as(w_in), gwdw.view_as(w_dw), gw_out.view_as(w_out), gskip
 
 

@@ -409,6 +409,12 @@ grr_status grr_lnb_norm(const float* x, const float* ln_w, float* n, float* isd,
 /* gx [B,C,P] += d<gn, n>/dx;  gln_w [C] += sum gn x isd. */
 grr_status grr_lnb_norm_bwd(const float* x, const float* ln_w, const float* isd, const float* gn, float* gx,
                             float* gln_w, int B, int C, int64_t P, void* stream);
+/* grr_lnb_norm_bwd with the block's skip term in the same pass (the LocalNonLinearBlock reverse,
+ * out = skip[0] x + skip[1] (...), REF13:541-575 under autograd): gx = skip[0] gout + the norm's data
+ * gradient (gx written, not accumulated; gx != gout), gskip0[0] += <gout, x>, gln_w += as above. */
+grr_status grr_lnb_norm_bwd_skip(const float* x, const float* ln_w, const float* isd, const float* gn,
+                                 const float* gout, const float* skip, float* gx, float* gln_w, float* gskip0, int B,
+                                 int C, int64_t P, void* stream);
 /* depthwise 3x3 with replicate padding (channels_local_linear_op, REF:934-940): wdw [C,9]. */
 grr_status grr_dwconv3(const float* h, const float* wdw, float* out, int B, int C, int H, int W, void* stream);
 /* its reverse: gh = exact adjoint of the clamped gather applied to g; gwdw [C,9] += weight gradient. */

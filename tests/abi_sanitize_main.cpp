@@ -78,6 +78,7 @@ int main() {
   EXPECT_ERR(grr_interleave2x2(n, n, 1, 4, 8, 8, s));
   EXPECT_ERR(grr_lnb_norm(n, n, n, n, 1, 4, 64, s));
   EXPECT_ERR(grr_lnb_norm_bwd(n, n, n, n, n, n, 1, 4, 64, s));
+  EXPECT_ERR(grr_lnb_norm_bwd_skip(n, n, n, n, n, n, n, n, n, 1, 4, 64, s));
   EXPECT_ERR(grr_dwconv3(n, n, n, 1, 4, 8, 8, s));
   EXPECT_ERR(grr_dwconv3_bwd(n, n, n, n, n, 1, 4, 8, 8, s));
   EXPECT_ERR(grr_lnb_gate(n, n, n, n, 1, 4, 64, s));

@@ -228,3 +228,53 @@ def test_pool2_equals_oracle_mean(K, shape):
     want = O.pool2(x.double())
     assert got.shape == want.shape
     assert rel_err(got, want) <= 1e-6
+
+
+@pytest.mark.parametrize("shape", [(2, 48, 16, 20), (1, 96, 33, 7)], ids=str)
+def test_lnb_norm_bwd_skip_equals_separate_passes(K, shape):
+    """grr_lnb_norm_bwd_skip (the LocalNonLinearBlock reverse's tail: s0 gout + the norm's data gradient,
+    <gout, x>, the norm's weight gradient in one pass over gout) against lincomb + norm_bwd + graph_dot."""
+    b, c, h, w = shape
+    torch.manual_seed(c + h)
+    x = torch.randn(b, c, h, w, device=DEV) + 0.3
+    lnw = torch.rand(c, device=DEV) + 0.5
+    gn, gout = torch.randn_like(x), torch.randn_like(x)
+    skip = torch.tensor([0.7, 1.3], device=DEV)
+    _, isd = K.lnb_norm(x, lnw)
+    gl_a, gs_a = torch.zeros_like(lnw), torch.zeros(1, device=DEV)
+    gx_a = K.lnb_norm_bwd_skip(x, lnw, isd, gn, gout, skip, gl_a, gs_a)
+    gl_r, gs_r = torch.zeros_like(lnw), torch.zeros(1, device=DEV)
+    gx_r = K.bwd_lincomb(gout, skip[0:1].contiguous(), None, None, 1)
+    K.lnb_norm_bwd(x, lnw, isd, gn, gx_r, gl_r)
+    K.bwd_graph_dot(gout, x, gs_r, 1)
+    torch.cuda.synchronize()
+    assert rel_err(gx_a, gx_r) <= 1e-6
+    assert torch.equal(gl_a.cpu(), gl_r.cpu())
+    n = x.numel()
+    assert float((gs_a.double() - gs_r.double()).abs().max()) <= 2e-6 * max(float(gs_r.abs().max()), n ** 0.5)
+
+
+def test_abstract_gradients_with_and_without_ln_skip(K):
+    """The v1.0 model's training gradients with the LNB skip term inside the norm's reverse pass against
+    the separate passes."""
+    import irdu_amd
+    from irdu_amd import solver_grad as SG
+    torch.manual_seed(3)
+    m = irdu_amd.AbtractMultiScaleGraphFilter(
+        3, 3, dims=[8, 16, 16, 32], hidden_dims=[16, 32, 32, 64], nsubnets=[1, 1, 1, 1], ngraphs=[2, 4, 4, 8],
+        num_blocks=[1, 1, 1, 1], num_blocks_out=1, n_cgd_iters=2).to(DEV)
+    y = torch.rand(2, 3, 64, 64, device=DEV)
+
+    def grads(fused):
+        SG.LN_SKIP_FUSED = fused
+        try:
+            m.zero_grad(set_to_none=True)
+            m(y).square().mean().backward()
+            return {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
+        finally:
+            SG.LN_SKIP_FUSED = True
+
+    ref, got = grads(False), grads(True)
+    assert ref.keys() == got.keys()
+    for k in ref:
+        assert rel_err(got[k], ref[k]) <= 1e-4, (k, rel_err(got[k], ref[k]))
