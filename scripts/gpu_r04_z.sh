@@ -2,7 +2,7 @@
 # Round 4: PMC traffic of the term reverse at the C4 workload, then the C4 training line reading it
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-out=gpurun_out/r04final3; mkdir -p $out
+out=gpurun_out/${R04_OUT:-r04final3}; mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 900 bash scripts/pmc_train_c4.sh > $out/pmct_c4.log 2>&1 || { tail -20 $out/pmct_c4.log; exit 1; }
 cp gpurun_out/pmct/traffic_bwd_term_fused_abstract_b32_s512.json $out/
