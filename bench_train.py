@@ -101,6 +101,8 @@ def cpu_baseline(model, model_kind, size, runs=3):
 
 
 def main():
+    # process-wide MIOpen setting of the training entry points, before any convolution (training.py)
+    os.environ.setdefault("MIOPEN_DEBUG_DISABLE_FIND_DB", "1")
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", choices=["abstract", "msgf"], default="abstract")
     ap.add_argument("--size", type=int, default=256)

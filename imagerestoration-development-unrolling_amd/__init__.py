@@ -8,17 +8,6 @@ module ``deep_multiscale_GGLR_GGTV_v1x0`` so callers can swap the import:
     import irdu_amd as model_structure
     model = model_structure.AbtractMultiScaleGraphFilter(...).cuda()
 """
-import os as _os
-
-# The stock convolutions outside the graph path (the v1.0 model's embedding, down/up-sampling and
-# channel combines) run on MIOpen.  With MIOpen's user find-db filled by an earlier process, its
-# immediate mode spends host time per call: the C4 training step (v1.0, 32 x 512^2) went 1.03 s
-# (fresh box) -> 2.7-4.0 s (every later run), GPU kernel time unchanged at 1.09 s per step; with the
-# find-db off every run stays at 1.02-1.03 s (DESIGN.md §4.r4, profiles/r04/miopen/).  A default
-# only: an explicit MIOPEN_DEBUG_DISABLE_FIND_DB in the environment wins.  MIOpen reads it at its
-# first convolution, so it must be set before any runs.
-_os.environ.setdefault("MIOPEN_DEBUG_DISABLE_FIND_DB", "1")
-
 from ._native import GrrError, NativeUnavailable, load as load_native  # noqa: F401
 from .graph_filter import (  # noqa: F401
     AbtractMultiScaleGraphFilter,
@@ -39,5 +28,7 @@ from . import glr_v10 as v10  # noqa: F401  (GLR-only drop-ins of lib/model_GLR_
 from .glr_v10 import GLRImageFilter, MixtureGLR, MultiScaleGLRImageFilter, MultiScaleMixtureGLR  # noqa: F401
 from . import window_graph  # noqa: F401  (window-graph MixtureGTV of lib/model_GLR_GTV_deep_v7.py)
 from . import window_graph_v1  # noqa: F401  (multiblock window denoiser of lib/model_GLR_GTV_deep_v1.py)
+
+from .training import miopen_training_defaults  # noqa: F401
 
 __version__ = "0.1.0"

@@ -46,6 +46,9 @@ SIGNATURES = {
     "grr_set_kernel_variant": [I],
     "grr_lnb_set_phases": [I],
     "grr_lnb_rep_fused": [I, I, I, I],
+    "grr_set_scratch_allocator": [P, P, P],
+    "grr_release_scratch": [],
+    "grr_scratch_bytes": [],
     "grr_neighbor_table": [P, I, I, P],
     "grr_stream_copy": [P, P, L, P],
     "grr_edge_weights": [P, L, P, P, P, I, I, I, I, I, P],
@@ -132,7 +135,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64, "grr_wgrad_workspace_bytes": c_int64,
-             "grr_ffn_workspace_bytes": c_int64}
+             "grr_ffn_workspace_bytes": c_int64, "grr_scratch_bytes": c_int64}
 
 _lib = None
 
@@ -153,8 +156,50 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = _RESTYPES.get(name, c_int)
+    _register_scratch_allocator(lib)
     _lib = lib
     return lib
+
+
+# The training reverse's reduction scratch (grr_set_scratch_allocator): PyTorch's caching allocator, on
+# the stream the library asks for, so the scratch is ordinary PyTorch memory (torch.cuda.memory_allocated
+# counts it, empty_cache can return it once grr_release_scratch gave it back).  The callbacks run only
+# when a stream's scratch first appears or grows (a handful of times per process).
+_SCRATCH_ALLOC_FN = ctypes.CFUNCTYPE(c_void_p, ctypes.c_uint64, c_int, c_void_p, c_void_p)
+_SCRATCH_FREE_FN = ctypes.CFUNCTYPE(None, c_void_p, c_int, c_void_p, c_void_p)
+
+
+def _scratch_alloc(nbytes, device, stream, _ctx):
+    try:
+        import torch
+        return int(torch.cuda.caching_allocator_alloc(int(nbytes), device, int(stream or 0)))
+    except Exception:      # noqa: BLE001 -- the library reports the failed allocation as GRR_ERR_HIP
+        return None
+
+
+def _scratch_free(ptr, _device, _stream, _ctx):
+    try:
+        import torch
+        torch.cuda.caching_allocator_delete(int(ptr))
+    except Exception:      # noqa: BLE001
+        pass
+
+
+_scratch_cbs = (_SCRATCH_ALLOC_FN(_scratch_alloc), _SCRATCH_FREE_FN(_scratch_free))   # kept alive
+
+
+def _register_scratch_allocator(lib) -> None:
+    st = lib.grr_set_scratch_allocator(ctypes.cast(_scratch_cbs[0], c_void_p), ctypes.cast(_scratch_cbs[1], c_void_p),
+                                       None)
+    if st != 0:   # pragma: no cover
+        raise NativeUnavailable(f"grr_set_scratch_allocator failed: {lib.grr_last_error()!r}")
+
+
+def release_scratch() -> None:
+    """Give the reverse's reduction scratch back to PyTorch's cache (synchronises the device first)."""
+    import torch
+    torch.cuda.synchronize()
+    call("grr_release_scratch")
 
 
 def call(name: str, *args) -> None:

@@ -1738,21 +1738,101 @@ __global__ __launch_bounds__(64) void red_finish_kernel(RedFinishArgs a) {
 }  // namespace
 
 // ---- RedScratch (grr_common.h) ---------------------------------------------
+// Scratch leases.  Each (device, stream) owns grow-only buffers, each leased by one RedScratch at a time
+// (alloc() to finish()); normally one per stream, a second one only while a lease is nested inside
+// another on the same stream.  Later calls on the same stream reuse a buffer: their kernels run after
+// the earlier finish kernel in stream order.  Memory comes from the allocator registered by
+// grr_set_scratch_allocator (the Python package registers PyTorch's caching allocator, so the scratch
+// is visible to and reclaimable through torch), else from hipMalloc / hipFree.  An outgrown buffer is
+// retired, not freed (a queued kernel may still read it), until grr_release_scratch.
 namespace {
-// the default pool keeps freed blocks (release threshold: unbounded), once per device
-bool pool_ready[64];
-std::mutex pool_mu;
-grr_status prepare_pool() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return GRR_ERR_HIP;
-  std::lock_guard<std::mutex> lk(pool_mu);
-  if (pool_ready[dev]) return GRR_OK;
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return GRR_ERR_HIP;
-  uint64_t thr = ~0ull;
-  if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) != hipSuccess) return GRR_ERR_HIP;
-  pool_ready[dev] = true;
+struct ScratchBuf {
+  int dev;
+  hipStream_t s;
+  void* p;
+  size_t bytes;
+  bool cb;        // from the registered allocator
+  bool leased;
+};
+struct ScratchState {
+  grr_scratch_alloc_fn alloc = nullptr;
+  grr_scratch_free_fn free = nullptr;
+  void* ctx = nullptr;
+  std::vector<ScratchBuf> bufs;      // live buffers, by (device, stream)
+  std::vector<ScratchBuf> retired;   // outgrown, freed by grr_release_scratch
+  size_t total = 0;
+};
+ScratchState g_scratch;
+std::mutex g_scratch_mu;
+
+grr_status scratch_raw_alloc(int dev, hipStream_t s, size_t bytes, ScratchBuf* out, const char* what) {
+  void* p = nullptr;
+  bool cb = false;
+  if (g_scratch.alloc) {
+    p = g_scratch.alloc((uint64_t)bytes, dev, (void*)s, g_scratch.ctx);
+    cb = true;
+  } else if (hipMalloc(&p, bytes) != hipSuccess) {
+    p = nullptr;
+  }
+  if (!p) {
+    set_error("%s: reduction scratch of %zu bytes: allocation failed", what, bytes);
+    return GRR_ERR_HIP;
+  }
+  *out = ScratchBuf{dev, s, p, bytes, cb, false};
+  g_scratch.total += bytes;
   return GRR_OK;
+}
+void scratch_raw_free(const ScratchBuf& b) {
+  if (b.cb) {
+    if (g_scratch.free) g_scratch.free(b.p, b.dev, (void*)b.s, g_scratch.ctx);
+  } else {
+    (void)hipFree(b.p);
+  }
+  g_scratch.total -= b.bytes;
+}
+
+// lease >= bytes for stream s (returned by scratch_return)
+grr_status scratch_lease(hipStream_t s, size_t bytes, void** out, const char* what) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    set_error("%s: hipGetDevice failed", what);
+    return GRR_ERR_HIP;
+  }
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  ScratchBuf* small = nullptr;
+  for (auto& b : g_scratch.bufs) {
+    if (b.dev != dev || b.s != s || b.leased) continue;
+    if (b.bytes >= bytes) {
+      b.leased = true;
+      *out = b.p;
+      return GRR_OK;
+    }
+    small = &b;
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cap);
+  GRR_REQUIRE(cap == hipStreamCaptureStatusNone, GRR_ERR_UNSUPPORTED,
+              "%s: the reduction scratch would grow inside a stream capture (run the call once before capturing)",
+              what);
+  size_t want = std::max<size_t>(bytes, (size_t)1 << 20);
+  if (small) want = std::max(want, 2 * small->bytes);
+  ScratchBuf nb{};
+  grr_status st = scratch_raw_alloc(dev, s, want, &nb, what);
+  if (st != GRR_OK) return st;
+  nb.leased = true;
+  if (small) {   // outgrown: retired (queued kernels may still read it), replaced
+    g_scratch.retired.push_back(*small);
+    *small = nb;
+  } else {       // first lease on this stream, or nested inside a live one
+    g_scratch.bufs.push_back(nb);
+  }
+  *out = nb.p;
+  return GRR_OK;
+}
+void scratch_return(void* p) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (auto& b : g_scratch.bufs)
+    if (b.p == p) b.leased = false;
 }
 }  // namespace
 
@@ -1769,15 +1849,10 @@ grr_status RedScratch::alloc(const char* what) {
   for (int i = 0; i < k_; ++i)
     if (dst_[i]) total += (size_t)n_[i] * nslot_[i];
   if (total == 0) return GRR_OK;
-  if (prepare_pool() != GRR_OK) {
-    set_error("%s: reduction scratch pool unavailable", what);
-    return GRR_ERR_HIP;
-  }
-  hipError_t e = hipMallocAsync(&base_, total * sizeof(float), s_);
-  if (e != hipSuccess) {
+  grr_status st = scratch_lease(s_, total * sizeof(float), &base_, what);
+  if (st != GRR_OK) {
     base_ = nullptr;
-    set_error("%s: reduction scratch (%zu floats): %s", what, total, hipGetErrorString(e));
-    return GRR_ERR_HIP;
+    return st;
   }
   float* p = static_cast<float*>(base_);
   for (int i = 0; i < k_; ++i)
@@ -1805,18 +1880,14 @@ grr_status RedScratch::finish(const char* what) {
   if (total > 0) hipLaunchKernelGGL(red_finish_kernel, dim3(total), dim3(64), 0, s_, a);
   grr_status st = launch_status(what);
   if (base_) {
-    const hipError_t e = hipFreeAsync(base_, s_);
+    scratch_return(base_);
     base_ = nullptr;
-    if (e != hipSuccess && st == GRR_OK) {
-      set_error("%s: reduction scratch free: %s", what, hipGetErrorString(e));
-      st = GRR_ERR_HIP;
-    }
   }
   return st;
 }
 
 RedScratch::~RedScratch() {
-  if (base_) (void)hipFreeAsync(base_, s_);   // an error path before finish(): nothing was added
+  if (base_) scratch_return(base_);   // an error path before finish(): nothing was added
 }
 
 }  // namespace grr
@@ -1824,6 +1895,36 @@ RedScratch::~RedScratch() {
 using namespace grr;
 
 extern "C" {
+
+grr_status grr_set_scratch_allocator(grr_scratch_alloc_fn alloc, grr_scratch_free_fn free_fn, void* ctx) {
+  clear_error();
+  GRR_REQUIRE((alloc == nullptr) == (free_fn == nullptr), GRR_ERR_INVALID_ARG,
+              "grr_set_scratch_allocator: give both functions or neither");
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  // buffers already handed out stay with the allocator that made them (ScratchBuf::cb); a buffer made
+  // by the previous registered allocator is freed through the new one only if that is the same pair
+  g_scratch.alloc = alloc;
+  g_scratch.free = free_fn;
+  g_scratch.ctx = ctx;
+  return GRR_OK;
+}
+
+grr_status grr_release_scratch(void) {
+  clear_error();
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (const auto& b : g_scratch.bufs)
+    GRR_REQUIRE(!b.leased, GRR_ERR_INVALID_ARG, "grr_release_scratch: a reduction scratch is in use");
+  for (const auto& b : g_scratch.bufs) scratch_raw_free(b);
+  for (const auto& b : g_scratch.retired) scratch_raw_free(b);
+  g_scratch.bufs.clear();
+  g_scratch.retired.clear();
+  return GRR_OK;
+}
+
+int64_t grr_scratch_bytes(void) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  return (int64_t)g_scratch.total;
+}
 
 grr_status grr_bwd_set_term_rows(int enable) {
   clear_error();

@@ -68,11 +68,11 @@ __device__ __forceinline__ void red_put(const Red& r, int idx, uint32_t slot, fl
   if (r.p) r.p[(size_t)idx * r.nslot + slot] = v;
 }
 
-// Host side: the partial arrays of one launch, carved from one stream-ordered allocation
-// (hipMallocAsync from the device's default pool, whose release threshold is raised once, so the
-// steady state reuses pool memory; capturable in a HIP graph), then finished (one launch for all of
-// them) and freed on the same stream.  Every kernel stores every slot of its plan (zero partials
-// included), so the scratch needs no fill.
+// Host side: the partial arrays of one launch, carved from a scratch buffer leased for the stream (a
+// per-stream grow-only buffer from the registered allocator -- PyTorch's caching allocator in the
+// Python package -- or hipMalloc; grr_set_scratch_allocator, graph_bwd.hip), then finished (one launch
+// for all of them) and returned.  Every kernel stores every slot of its plan (zero partials included),
+// so the scratch needs no fill.
 class RedScratch {
  public:
   static constexpr int kMax = 4;

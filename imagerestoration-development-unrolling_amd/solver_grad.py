@@ -761,13 +761,26 @@ def _mat(w: Tensor, rows: int) -> Tensor:
 # per weight gradient)
 # The eager forward keeps the head's gated activation g (a view of the launch's workspace) for the
 # reverse's W2 weight gradient, which then skips recomputing the depthwise + gate.  g costs hid floats
-# per pixel, so the gates alive at once are capped (KEEP_GATE_BYTES, 32 GB: all of the msgf step's,
-# about three quarters of the C4 shape's C <= 128 blocks, whose step already holds ~142 GB of the
-# 288); a kept gate leaves the budget when its tensor is freed.  Compiled graphs always recompute (the
-# custom op's saved list is fixed).
+# per pixel, so the gates alive at once are capped by a budget derived from the device's memory
+# (KEEP_GATE_FRACTION of it: 32 GB of a 288 GB MI355X -- all of the msgf step's gates, about three
+# quarters of the C4 shape's C <= 128 blocks, whose step already holds ~142 GB -- and proportionally
+# less on a smaller device; KEEP_GATE_BYTES, when set, overrides it); a kept gate leaves the budget when
+# its tensor is freed.  Compiled graphs always recompute (the custom op's saved list is fixed).
 KEEP_GATE = True
-KEEP_GATE_BYTES = 32 << 30
+KEEP_GATE_FRACTION = 1.0 / 9.0
+KEEP_GATE_BYTES = None
 _KEPT = [0]
+_GATE_BUDGET = {}
+
+
+def keep_gate_budget(device) -> int:
+    """Bytes of kept gates allowed alive at once on ``device``."""
+    if KEEP_GATE_BYTES is not None:
+        return int(KEEP_GATE_BYTES)
+    idx = torch.device(device).index or 0
+    if idx not in _GATE_BUDGET:
+        _GATE_BUDGET[idx] = int(KEEP_GATE_FRACTION * torch.cuda.get_device_properties(idx).total_memory)
+    return _GATE_BUDGET[idx]
 
 
 def _unkeep(nbytes: int) -> None:
@@ -786,7 +799,7 @@ def _lnb_fwd(consts, x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tenso
     if consts and consts[0] and _lnb_keeps_gate(x, w2):
         b, _, h, w = x.shape
         nbytes = 4 * b * w2.shape[1] * h * w
-        if _KEPT[0] + nbytes <= KEEP_GATE_BYTES:
+        if _KEPT[0] + nbytes <= keep_gate_budget(x.device):
             out, gate = K.lnb_forward_keep(*args)
             _KEPT[0] += nbytes
             weakref.finalize(gate, _unkeep, nbytes)

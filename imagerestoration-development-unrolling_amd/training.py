@@ -45,6 +45,18 @@ from . import sharding, stream_guard
 LOG = logging.getLogger("irdu_amd.train")
 
 
+def miopen_training_defaults() -> None:
+    """Process-wide MIOpen setting for the training entry points (run_train.py / training.main,
+    bench_train.py), never applied on import: MIOPEN_DEBUG_DISABLE_FIND_DB=1 unless the environment
+    already sets it.  The stock convolutions outside the graph path (the v1.0 model's embedding,
+    down/up-sampling and channel combines) run on MIOpen; with MIOpen's user find-db filled by an earlier
+    process its immediate mode spends host time per call -- the C4 training step (v1.0, 32 x 512^2) went
+    1.03 s (fresh box) -> 2.7-4.0 s on every later run, GPU kernel time unchanged at 1.09 s; with the
+    find-db off every run stays at 1.02-1.03 s (profiles/r04/miopen/).  MIOpen reads the
+    variable at its first convolution, so call this before any convolution runs in the process."""
+    os.environ.setdefault("MIOPEN_DEBUG_DISABLE_FIND_DB", "1")
+
+
 # ---------------------------------------------------------------------------
 # options (run_train.py:20-36, custom_parser.py:23-30, small_utils.py:12-18)
 # ---------------------------------------------------------------------------
@@ -206,9 +218,15 @@ VAL_DATASETS = {c.__name__: c for c in (TestImagesCSV, SyntheticTestImages)}
 
 
 def _img_as_ubyte(x: np.ndarray) -> np.ndarray:
-    """skimage.util.img_as_ubyte of a float image in [0, 1] (the reference's :269): x * 255 rounded to
-    the nearest integer (half to even), as uint8."""
-    return np.clip(np.rint(x.astype(np.float64) * 255.0), 0, 255).astype(np.uint8)
+    """skimage.util.img_as_ubyte of a float32 image in [0, 1] (the reference's :279): skimage's
+    float -> uint8 ``_convert`` multiplies in the smallest float type of at least the input's size that
+    holds the output (float32 here: ``np.multiply(x, 255, dtype=float32)``), rounds half to even
+    (``np.rint``), clips to [0, 255] and casts.  The float32 product matters at ties: a value whose
+    float64 product lies just below k + 0.5 can round to k + 0.5 in float32 and go to the even k."""
+    y = np.multiply(np.asarray(x, dtype=np.float32), np.float32(255.0), dtype=np.float32)
+    np.rint(y, out=y)
+    np.clip(y, 0, 255, out=y)
+    return y.astype(np.uint8)
 
 
 @torch.no_grad()
@@ -324,6 +342,39 @@ def create_dataloader(dataset, sampler, dataset_conf: dict, environ_conf: dict):
     return torch.utils.data.DataLoader(dataset=dataset, sampler=sampler, **args)
 
 
+class TrainStage:
+    """One loader of the training curriculum: dataset + resumable sampler + dataloader, and the
+    optimisation steps it holds per epoch."""
+
+    def __init__(self, index: int, ds_conf: dict, environ_conf: dict, rank: int, world: int):
+        self.index = index
+        self.dataset = create_dataset(ds_conf, environ_conf)
+        self.batch_size = int(ds_conf["dataloader_args"].get("batch_size", 1))
+        self.drop_last = bool(ds_conf["dataloader_args"].get("drop_last", False))
+        self.sampler = ResumeableSampler(self.dataset, self.batch_size, rank, world)
+        self.loader = create_dataloader(self.dataset, self.sampler, ds_conf, environ_conf)
+        self.steps = self.sampler.steps_per_epoch(self.drop_last)
+        if self.steps <= 0:
+            raise ValueError(f"training stage {index}: dataset of {len(self.dataset)} samples holds no batch of "
+                             f"{self.batch_size} x {world} ranks")
+
+
+def train_stage_confs(conf: dict) -> List[dict]:
+    """``datasets.train`` as a list of stage configurations: one dict (one loader), or a list of them --
+    the v2 script's curriculum, four loaders chained per epoch (128^2 x 4, 192^2 x 3, 256^2 x 2,
+    384^2 x 1; scripts_v2/run_abtract_lightformer_GGTV_GGLR_sigma25.py:50-115, :185)."""
+    tr = conf["datasets"]["train"]
+    return list(tr) if isinstance(tr, (list, tuple)) else [tr]
+
+
+def build_train_stages(conf: dict, rank: int = 0, world: int = 1) -> List[TrainStage]:
+    """The stages of an epoch, in order.  Data-parallel policy: a stage's ``batch_size`` is per rank (its
+    global batch is batch_size x world) and each stage's epoch is cut to whole global batches, so every
+    rank runs the same number of steps in every stage and all ranks stay in one all-reduce sequence --
+    the 384^2 x 1 stage on 8 GPUs is a global batch of 8, one patch per rank."""
+    return [TrainStage(k, dc, conf, rank, world) for k, dc in enumerate(train_stage_confs(conf))]
+
+
 # ---------------------------------------------------------------------------
 # model / optimiser / schedule (v2 script :120-171)
 # ---------------------------------------------------------------------------
@@ -374,10 +425,19 @@ class Trainer:
         self.reducer = sharding.OverlappedGradReducer(self.model.parameters(), bucket_mb=self.bucket_mb)
         self.i = 0
         self.val_history: List[Tuple[int, float]] = []     # (iteration, mean test PSNR)
+        # training-time PSNR / MSE (:212-223): per step the batch's squared-error sum (float64, on the
+        # device, no host sync) and its element count; summarised by train_metrics()
+        self.track_metrics = bool(tconf.get("train_metrics", True))
+        self._sse: List[torch.Tensor] = []
+        self._n: List[int] = []
+        self.train_history: List[Tuple[int, float, float]] = []   # (iteration, mean PSNR, mean MSE)
 
-    def loss(self, noisy: torch.Tensor, clean: torch.Tensor) -> torch.Tensor:
+    def loss(self, noisy: torch.Tensor, clean: torch.Tensor, _out: Optional[list] = None) -> torch.Tensor:
         m = self.model
-        loss = nn.functional.l1_loss(m(noisy), clean)
+        out = m(noisy)
+        if _out is not None:
+            _out.append(out)
+        loss = nn.functional.l1_loss(out, clean)
         if hasattr(m, "encode") and (self.w_encdec or self.w_perturb):
             latent = m.encode(clean)
             rec = m.decode(latent)
@@ -394,14 +454,38 @@ class Trainer:
         self.reducer.prepare()
         noisy = noisy_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
         clean = clean_hwc.to(self.device, non_blocking=True).permute(0, 3, 1, 2).contiguous()
+        outs: list = []
         with stream_guard.maybe_guard():       # GRR_STREAM_GUARD=1: check the internal-stream invariant
-            loss = self.loss(noisy, clean)
+            loss = self.loss(noisy, clean, outs)
             loss.backward()
         self.reducer.finish()
         self.optimizer.step()
         self.lr_scheduler.step()
+        if self.track_metrics:
+            # :212-214: both images clipped to [0, 1], squared error in float64 (summed here, divided at
+            # summary time, so several ranks' shares add up to the global batch's MSE)
+            with torch.no_grad():
+                d = outs[0].detach().clamp(0.0, 1.0).double() - clean.clamp(0.0, 1.0).double()
+                self._sse.append(torch.sum(d * d))
+            self._n.append(d.numel())
+            del self._sse[:-100], self._n[:-100]
         self.i += 1
         return float(loss.detach())
+
+    def train_metrics(self) -> Tuple[float, float]:
+        """Mean PSNR and mean MSE over the last <= 100 steps (the reference's running window, :221-223):
+        step k's MSE = its squared-error sum / element count over the global batch (summed over ranks,
+        one all-reduce of the window), PSNR_k = 10 log10(1 / MSE_k).  Every rank must call it at the same
+        iteration (it is collective when world > 1)."""
+        if not self._sse:
+            return float("nan"), float("nan")
+        acc = torch.stack([torch.stack(self._sse), torch.tensor(self._n, dtype=torch.float64,
+                                                                 device=self._sse[0].device)])
+        rank, world = sharding.world()
+        if world > 1:
+            torch.distributed.all_reduce(acc)
+        mse = (acc[0] / acc[1]).cpu().numpy()
+        return float(np.mean(10.0 * np.log10(1.0 / mse))), float(np.mean(mse))
 
     def state_dict(self) -> dict:
         return {"i": self.i, "model": self.model.state_dict(), "optimizer": self.optimizer.state_dict(),
@@ -432,11 +516,7 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
         device = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', 0))}") if torch.cuda.is_available() \
             else torch.device("cpu")
     tconf = conf.get("train", {})
-    ds_conf = conf["datasets"]["train"]
-    dataset = create_dataset(ds_conf, conf)
-    bs = int(ds_conf["dataloader_args"].get("batch_size", 1))
-    sampler = ResumeableSampler(dataset, bs, rank, world)
-    loader = create_dataloader(dataset, sampler, ds_conf, conf)
+    stages = build_train_stages(conf, rank, world)
     trainer = Trainer(build_model(conf.get("model", {})), tconf, device)
     ckpt_path = conf["path"].get("latest_checkpoint_path") or latest_checkpoint(conf)
     if world > 1:
@@ -446,9 +526,7 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
         choice = [ckpt_path]
         torch.distributed.broadcast_object_list(choice, src=0)
         ckpt_path = choice[0]
-    spe = sampler.steps_per_epoch(bool(ds_conf["dataloader_args"].get("drop_last", False)))
-    if spe <= 0:
-        raise ValueError(f"dataset of {len(dataset)} samples holds no batch of {bs} x {world} ranks")
+    spe = sum(st.steps for st in stages)
     if ckpt_path:
         trainer.load_state_dict(torch.load(ckpt_path, map_location=device, weights_only=True))
         LOG.info("resumed from %s at iteration %d", ckpt_path, trainer.i)
@@ -471,33 +549,46 @@ def run(conf: dict, device=None, max_iters: Optional[int] = None) -> Trainer:
         if rank == 0:
             torch.save(trainer.state_dict(), os.path.join(checkpoint_dir(conf), f"checkpoint_iter{trainer.i:08d}.pt"))
 
-    # epoch e visits the dataset permuted with seed 2024 + e (data_sampler.py:28-31), for a fresh
-    # run and a resumed one alike, so resuming at iteration i continues exactly the order the
+    # epoch e visits every stage's dataset permuted with seed 2024 + e (data_sampler.py:28-31), for a
+    # fresh run and a resumed one alike, so resuming at iteration i continues exactly the order the
     # uninterrupted run would have seen (the reference permutes a fresh run with 2204 instead,
-    # images_pair_restoration_dataset.py:41, which makes its resume skip a different order)
+    # images_pair_restoration_dataset.py:41, which makes its resume skip a different order).  An epoch
+    # runs the stages in order (the reference's itertools.chain of its loaders, :185); iteration i of
+    # the epoch lies in the first stage whose cumulative step count exceeds it.
     epoch, done_in_epoch = divmod(trainer.i, spe)
     start_i, saved_at = trainer.i, None
     while trainer.i < total:
-        sampler.set_epoch_and_current_sample(epoch, done_in_epoch * bs * world - 1)
-        stepped = False
-        for noisy, clean in loader:
+        for st in stages:
             if trainer.i >= total:
                 break
-            loss = trainer.step(noisy, clean)
-            stepped = True
-            if rank == 0 and trainer.i % verbose == 0:
-                LOG.info("iter=%d loss=%.6f lr=%.3e", trainer.i, loss, trainer.optimizer.param_groups[0]["lr"])
-            if trainer.i % every == 0:
-                save()
-                saved_at = trainer.i
-            if val_every and trainer.i % val_every == 0:
-                psnr = validate(trainer.model, val_set, device=device, **val_args)
-                trainer.val_history.append((trainer.i, psnr))
-                if rank == 0:
-                    LOG.info("FINISH VAL EPOCH %d - iter=%d - psnr_testing=%.4f", epoch, trainer.i, psnr)
-        if not stepped and trainer.i < total:
-            raise RuntimeError(f"epoch {epoch} yielded no batch (dataset {len(dataset)}, batch {bs}, "
-                               f"{world} ranks, drop_last {ds_conf['dataloader_args'].get('drop_last', False)})")
+            if done_in_epoch >= st.steps:
+                done_in_epoch -= st.steps
+                continue
+            st.sampler.set_epoch_and_current_sample(epoch, done_in_epoch * st.batch_size * world - 1)
+            stepped = False
+            for noisy, clean in st.loader:
+                if trainer.i >= total:
+                    break
+                loss = trainer.step(noisy, clean)
+                stepped = True
+                if trainer.i % verbose == 0:
+                    psnr_tr, mse_tr = trainer.train_metrics() if trainer.track_metrics else (float("nan"),) * 2
+                    trainer.train_history.append((trainer.i, psnr_tr, mse_tr))
+                    if rank == 0:
+                        LOG.info("iter=%d loss=%.6f lr=%.3e psnr=%.4f mse=%.6e", trainer.i, loss,
+                                 trainer.optimizer.param_groups[0]["lr"], psnr_tr, mse_tr)
+                if trainer.i % every == 0:
+                    save()
+                    saved_at = trainer.i
+                if val_every and trainer.i % val_every == 0:
+                    psnr = validate(trainer.model, val_set, device=device, **val_args)
+                    trainer.val_history.append((trainer.i, psnr))
+                    if rank == 0:
+                        LOG.info("FINISH VAL EPOCH %d - iter=%d - psnr_testing=%.4f", epoch, trainer.i, psnr)
+            if not stepped and trainer.i < total:
+                raise RuntimeError(f"epoch {epoch} stage {st.index} yielded no batch (dataset {len(st.dataset)}, "
+                                   f"batch {st.batch_size}, {world} ranks, drop_last {st.drop_last})")
+            done_in_epoch = 0
         epoch, done_in_epoch = epoch + 1, 0
     if trainer.i > start_i and saved_at != trainer.i:     # the final state is always on disk
         save()
@@ -531,15 +622,15 @@ def plumbing(conf: dict) -> dict:
     logger.addHandler(fh)
     try:
         logger.info("environ_conf=%s", json.dumps(conf, indent=1, default=str))
-        ds_conf = conf["datasets"]["train"]
-        dataset = create_dataset(ds_conf, conf)
-        sampler = ResumeableSampler(dataset, int(ds_conf["dataloader_args"].get("batch_size", 1)))
-        loader = create_dataloader(dataset, sampler, ds_conf, conf)
-        logger.info("train dataset: %d samples", len(dataset))
+        stages = build_train_stages(conf)
+        for st in stages:
+            logger.info("train dataset: %d samples", len(st.dataset))
     finally:
         logger.removeHandler(fh)
         fh.close()
-    return {"latest_checkpoint_path": ckpt, "dataset": dataset, "sampler": sampler, "dataloader": loader}
+    st = stages[0]
+    return {"latest_checkpoint_path": ckpt, "dataset": st.dataset, "sampler": st.sampler, "dataloader": st.loader,
+            "stages": stages}
 
 
 def main(argv: Optional[Sequence[str]] = None) -> None:
@@ -549,6 +640,7 @@ def main(argv: Optional[Sequence[str]] = None) -> None:
     ap.add_argument("-plumbing_only", action="store_true",
                     help="the reference run_train.py's steps only (no model); the default without a GPU")
     args = ap.parse_args(argv)
+    miopen_training_defaults()
     conf = parse_options(args.yaml_path)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s: %(message)s")
     if args.plumbing_only or not torch.cuda.is_available():

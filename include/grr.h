@@ -4,8 +4,9 @@
  * One shared library (libgrr.so) built with hipcc for gfx950.  Every entry point
  * takes raw DEVICE pointers (fp32, contiguous NCHW unless stated), explicit sizes
  * and the caller's hipStream_t (passed as void*).  The caller allocates every
- * tensor; the library keeps no state, never allocates, never synchronises, and
- * is safe to call from several host threads (re-entrant).  Each call returns a
+ * tensor it computes on; the only library state is the training reverse's per-stream reduction
+ * scratch (grr_set_scratch_allocator).  It never synchronises, and is safe to call from several host
+ * threads (re-entrant).  Each call returns a
  * grr_status; on failure grr_last_error() (thread-local) holds a message.
  *
  * Reference interfaces replaced (REF = exploration/GGTV_GGLR_v1.0/
@@ -49,6 +50,24 @@ grr_status grr_set_kernel_variant(int variant);
  * depthwise + gate -> the workspace's g), 4 mix (W2 g + skip -> out).  7 (default) = all; a caller
  * times head and mix apart by running mask 3 then mask 4 on the same workspace. */
 grr_status grr_lnb_set_phases(int mask);
+
+/* Reduction scratch of the training reverse (no reference counterpart: the reference reverses through
+ * autograd).  The reverse entry points (grr_bwd_*, grr_lnb_*_bwd, grr_dwconv3_bwd, grr_win_bwd_*, the
+ * sub-API *_bwd) reduce per-graph scalars, taps and LN / depthwise weights in a fixed order through a
+ * small device scratch of partial sums.  The library keeps one grow-only scratch buffer per (device,
+ * stream) -- a second one only while calls nest on a stream -- and reuses it for later calls on that
+ * stream (stream order makes the reuse safe).  The buffers come from the allocator registered here
+ * (alloc(bytes, device, stream, ctx) returns a device pointer or NULL; free(ptr, device, stream, ctx)),
+ * or from hipMalloc when none is registered (both NULL).  The Python package registers PyTorch's
+ * caching allocator, so the scratch is PyTorch memory.  A call that would grow the scratch while its
+ * stream is being captured fails with GRR_ERR_UNSUPPORTED (run it once before capturing).
+ * grr_release_scratch frees every buffer (the caller synchronises the streams first);
+ * grr_scratch_bytes reports the bytes held. */
+typedef void* (*grr_scratch_alloc_fn)(uint64_t bytes, int device, void* stream, void* ctx);
+typedef void (*grr_scratch_free_fn)(void* ptr, int device, void* stream, void* ctx);
+grr_status grr_set_scratch_allocator(grr_scratch_alloc_fn alloc, grr_scratch_free_fn free_fn, void* ctx);
+grr_status grr_release_scratch(void);
+int64_t grr_scratch_bytes(void);
 
 /* Measurement helper (not a reference interface): float4 streaming copy of n floats
  * (n % 4 == 0, 16-byte aligned), the HBM ceiling bench.py reports beside the step kernel. */

@@ -96,3 +96,27 @@ def test_stage_count_parameter_shapes():
     assert "localfilter.scaling_kernel01" not in m.state_dict()
     assert m.localfilter.GLRmodule00.edge_delta.dtype == torch.int32
     assert np.array_equal(m.localfilter.GLRmodule00.edge_delta.numpy(), [[-1, 0], [0, -1], [0, 1], [1, 0]])
+
+
+def test_import_leaves_the_environment_unchanged():
+    """Importing the package sets no process-wide variable (MIOpen's find-db default belongs to the
+    training entry points: irdu_amd.miopen_training_defaults, training.main, bench_train.py)."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, %r); before = dict(os.environ); import irdu_amd; "
+            "after = dict(os.environ); d = {k for k in set(before) | set(after) if before.get(k) != after.get(k)}; "
+            "print(sorted(d)); sys.exit(1 if d else 0)") % ROOT
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MIOPEN_")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run([sys.executable, "-c", "import os, sys; sys.path.insert(0, %r); import irdu_amd; "
+                        "irdu_amd.miopen_training_defaults(); print(os.environ['MIOPEN_DEBUG_DISABLE_FIND_DB'])" % ROOT],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "1", r.stdout + r.stderr
+
+
+def test_scratch_allocator_is_registered_and_empty_without_gpu():
+    lib = _native.load()
+    assert lib.grr_scratch_bytes() == 0
+    assert lib.grr_release_scratch() == 0
+    assert lib.grr_set_scratch_allocator(None, 0x1000, None) == 1   # one function without the other

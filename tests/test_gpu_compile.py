@@ -114,11 +114,12 @@ def test_compiled_training_matches_eager(irdu):
     assert metrics.generated_kernel_count == 0, metrics.generated_kernel_count
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) <= 1e-6 * abs(b), (losses, ref_losses)
-    # step 0: same weights, so only fp32 summation order differs (float atomics in the reverse
-    # reductions, Inductor's fused encoder/decoder ops): 1e-5.  Step 1 starts from weights after one
-    # Adam step, whose first update is ~lr * sign(g): an entry with |g| near eps takes an update that
-    # depends on that rounding noise, so step 1 is held to the training tolerance of DESIGN.md §5.
-    for step, tol in ((0, 1e-5), (1, 2e-4)):
+    # step 0: same weights; the HIP reverse is fixed-order (no float atomics) and no code is generated, so
+    # what can differ is AOTAutograd's decomposition of the stock ops' backward (losses, convolutions,
+    # layer norms) against eager autograd's kernels: 1e-6.  Step 1 starts from weights after one Adam
+    # step, whose first update is ~lr * sign(g): an entry with |g| near eps takes an update that depends
+    # on that rounding, so step 1 is held to the training tolerance of DESIGN.md §5.
+    for step, tol in ((0, 1e-6), (1, 2e-4)):
         for k, ref in ref_grads[step].items():
             got = grads[step][k]
             err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))

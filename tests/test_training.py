@@ -289,6 +289,138 @@ def test_data_parallel_run_over_epochs_stays_in_sync(tmp_path):
         assert np.array_equal(res[0][1][k], res[1][1][k]), k
 
 
+class _ShapeTiny(TinyModel):
+    """TinyModel that records the spatial size of every training forward (the curriculum's stage)."""
+    seen: list = []
+
+    def forward(self, x):
+        if self.training:
+            _ShapeTiny.seen.append((x.shape[0], x.shape[2]))
+        return super().forward(x)
+
+
+def _stage(ps, bs, n):
+    return {"type": "SyntheticNoisyPatches", "dataset_args": {"patch_size": ps, "max_num_patchs": n,
+                                                              "lambda_noise": 25.0},
+            "dataloader_args": {"batch_size": bs}}
+
+
+def _chain_conf(root, total, stages, verbose=1000):
+    return {"name": "chain", "manual_seed": 1, "path": {"root_dir": str(root)},
+            "datasets": {"train": stages},
+            "train": {"total_iters": total, "checkpoint_every": 1000, "verbose_every": verbose,
+                      "loss03_weight": 0.0, "milestones": [100]}}
+
+
+def test_curriculum_stages_chain_per_epoch_and_resume(tmp_path, monkeypatch):
+    """datasets.train as a list: the v2 script's curriculum (itertools.chain of its loaders, :185).  An
+    epoch runs stage 0 (16^2 x 4, 2 steps) then stage 1 (24^2 x 2, 3 steps); training past one epoch
+    starts the chain again; a run interrupted inside stage 1 and resumed equals the uninterrupted run."""
+    stages = [_stage(16, 4, 8), _stage(24, 2, 6)]
+
+    def build(_conf):
+        torch.manual_seed(0)
+        return _ShapeTiny()
+    monkeypatch.setattr(T, "build_model", build)
+    _ShapeTiny.seen = []
+    full = T.run(_chain_conf(tmp_path / "a", 12, stages), device=torch.device("cpu"))
+    assert full.i == 12
+    assert _ShapeTiny.seen == ([(4, 16)] * 2 + [(2, 24)] * 3) * 2 + [(4, 16)] * 2
+    T.run(_chain_conf(tmp_path / "b", 3, stages), device=torch.device("cpu"))     # stops inside stage 1
+    _ShapeTiny.seen = []
+    resumed = T.run(_chain_conf(tmp_path / "b", 12, stages), device=torch.device("cpu"))
+    assert resumed.i == 12 and _ShapeTiny.seen == [(2, 24)] * 2 + ([(4, 16)] * 2 + [(2, 24)] * 3) + [(4, 16)] * 2
+    for (k, v), (k2, v2) in zip(full.model.state_dict().items(), resumed.model.state_dict().items()):
+        assert k == k2 and torch.allclose(v, v2, rtol=1e-6, atol=1e-8), k
+    short = _stage(24, 8, 6)
+    short["dataloader_args"]["drop_last"] = True
+    with pytest.raises(ValueError, match="stage 1: .* holds no batch"):
+        T.run(_chain_conf(tmp_path / "c", 2, [_stage(16, 4, 8), short]), device=torch.device("cpu"))
+
+
+def test_train_metrics_window_matches_reference_formula(tmp_path, monkeypatch):
+    """Training-time PSNR / MSE (:212-223): per step MSE of the clipped output against the clipped
+    clean patch (float64), PSNR = 10 log10(1 / MSE), logged as the running mean of the last <= 100 steps."""
+    monkeypatch.setattr(T, "build_model", lambda _c: (torch.manual_seed(0), TinyModel())[1])
+    tr = T.run(_chain_conf(tmp_path, 4, [_stage(16, 4, 8)], verbose=2), device=torch.device("cpu"))
+    assert [i for i, _, _ in tr.train_history] == [2, 4]
+    # recompute steps 1..4 with the reference's numpy formula from a replay of the same run
+    torch.manual_seed(0)
+    ref = T.Trainer(TinyModel(), _chain_conf(tmp_path, 4, [])["train"], torch.device("cpu"))
+    ds = T.SyntheticNoisyPatches(patch_size=16, max_num_patchs=8, lambda_noise=25.0)
+    ds.random_permute(seed=2024)
+    psnrs, mses = [], []
+    for step in range(4):
+        idx = [(4 * step + j) % 8 for j in range(4)]
+        if step == 2:
+            ds.random_permute(seed=2025)
+        noisy, clean = [torch.stack(x) for x in zip(*[ds[i] for i in idx])]
+        ref.model.eval()
+        with torch.no_grad():
+            out = ref.model(noisy.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+        ref.step(noisy, clean)
+        a = np.clip(clean.numpy(), 0, 1).astype(np.float64)
+        b = np.clip(out.numpy(), 0, 1).astype(np.float64)
+        mse = np.square(a - b).mean()
+        mses.append(mse)
+        psnrs.append(10 * np.log10(1 / mse))
+    assert tr.train_history[-1][1] == pytest.approx(np.mean(psnrs), rel=1e-6)
+    assert tr.train_history[-1][2] == pytest.approx(np.mean(mses), rel=1e-6)
+    assert tr.train_history[0][1] == pytest.approx(np.mean(psnrs[:2]), rel=1e-6)
+
+
+def _chain_worker(rank, world, port, root, q):
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        T.build_model = lambda _c: (torch.manual_seed(0), _ShapeTiny())[1]
+        _ShapeTiny.seen = []
+        tr = T.run(_chain_conf(root, 7, [_stage(16, 2, 8), _stage(24, 1, 6)], verbose=7),
+                   device=torch.device("cpu"))
+        q.put((rank, tr.i, list(_ShapeTiny.seen), tr.train_history,
+               {k: v.detach().numpy() for k, v in tr.model.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_curriculum_splits_each_stage_batch(tmp_path, monkeypatch):
+    """Curriculum under data parallelism (gloo, 2 ranks): a stage's batch_size is per rank, so its global
+    batch is batch_size x world (stage 1, 24^2 x 1 per rank: global batch 2) and every rank runs the same
+    steps per stage (2 + 3 per epoch), in one all-reduce sequence.  The result equals one process
+    training on the global batches (16^2 x 4, then 24^2 x 2), and so do the training PSNR / MSE."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, 2, port, str(tmp_path / f"r{r}"), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert res[r][0] == 7
+        assert res[r][1] == [(2, 16)] * 2 + [(1, 24)] * 3 + [(2, 16)] * 2
+    monkeypatch.setattr(T, "build_model", lambda _c: (torch.manual_seed(0), TinyModel())[1])
+    one = T.run(_chain_conf(tmp_path / "one", 7, [_stage(16, 4, 8), _stage(24, 2, 6)], verbose=7),
+                device=torch.device("cpu"))
+    for k, v in one.model.state_dict().items():
+        for r in (0, 1):
+            assert np.allclose(res[r][3][k], v.numpy(), rtol=1e-5, atol=1e-7), (k, r)
+    for r in (0, 1):
+        assert res[r][2][-1][1] == pytest.approx(one.train_history[-1][1], rel=1e-9)
+        assert res[r][2][-1][2] == pytest.approx(one.train_history[-1][2], rel=1e-9)
+
+
+def test_v2_curriculum_yaml_states_the_reference_stages():
+    conf = T.parse(os.path.join(ROOT, "experiment_conf", "v2_curriculum.yaml"))
+    stages = T.train_stage_confs(conf)
+    got = [(s["dataset_args"]["patch_size"], s["dataloader_args"]["batch_size"], s["dataset_args"]["max_num_patchs"])
+           for s in stages]
+    assert got == [(128, 4, 800000), (192, 3, 600000), (256, 2, 400000), (384, 1, 200000)]
+    assert conf["model"]["type"] == "AbtractMultiScaleGraphFilter"
+
+
 class _PadProbe(torch.nn.Module):
     """Identity that records the shapes it sees (the validation recipe pads to multiples of 16)."""
 
@@ -311,11 +443,29 @@ def _reference_val_psnr(images, sigma=25.0, seed=2204):
         img_true = np.asarray(img, dtype=np.float32)
         noisy = img_true.copy()
         noisy += rs.normal(0, sigma / 255.0, img_true.shape)
-        restored = np.clip(noisy, 0, 1)
-        restored = np.clip(np.rint(restored.astype(np.float64) * 255), 0, 255).astype(np.uint8).astype(np.float32)
+        restored = np.clip(noisy, 0, 1).astype(np.float32)
+        restored = np.clip(np.rint(np.multiply(restored, 255, dtype=np.float32)), 0, 255).astype(np.uint8).astype(np.float32)
         mse = np.square(np.rint(img_true.astype(np.float64) * 255).astype(np.float32) - restored).mean()
         out.append(20 * np.log10(255.0 / np.sqrt(mse)))
     return float(np.mean(out))
+
+
+def test_img_as_ubyte_rounds_the_float32_product():
+    """skimage's img_as_ubyte (the reference's :279) multiplies a float32 image by 255 in float32, then
+    rint (half to even): at the float32 value nearest (k + 0.5) / 255 the float32 product is exactly
+    k + 0.5 and goes to the even neighbour, where a float64 product (just above k + 0.5) would round up."""
+    ks = np.arange(0, 255)
+    ties = ((ks + 0.5) / 255.0).astype(np.float32)
+    f32 = np.multiply(ties, np.float32(255.0), dtype=np.float32)
+    f64 = ties.astype(np.float64) * 255.0
+    exact = f32 == ks + 0.5                                         # exact ties in float32 ...
+    straddle = exact & (f64 > ks + 0.5) & (ks % 2 == 0)             # ... whose float64 product lies above
+    assert straddle.sum() >= 30, straddle.sum()
+    got = T._img_as_ubyte(ties)
+    assert np.array_equal(got[straddle], ks[straddle].astype(np.uint8))          # half to even: down to k
+    assert np.array_equal(np.rint(f64[straddle]), ks[straddle] + 1.0)             # float64 would give k + 1
+    assert np.array_equal(got, np.clip(np.rint(f32), 0, 255).astype(np.uint8))
+    assert np.array_equal(T._img_as_ubyte(np.array([0.0, 1.0, 0.2], np.float32)), np.array([0, 255, 51], np.uint8))
 
 
 def test_validation_recipe_pads_crops_and_scores():
