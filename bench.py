@@ -344,17 +344,29 @@ def main():
                 "mfma_tflops": round(mx["tflops"], 2), "mfma_peak": round(SPLIT_BF16_PEAK_TFLOPS, 1),
                 "traffic": load_traffic_file("traffic_lnb_mix.json", "lnb_mix_kernel", b),
                 "note": "algorithmic bytes (g + skip operand + out) / HIP-event time; W2 on 6 bf16 products"}}
-        if "lnb_rep_fused" in kern:   # the first block, on the replicated RGB input: one fused pass
-            rp = kern["lnb_rep_fused"]
-            res["roofline_secondary"]["lnb_rep_fused"] = {
-                "bound": "mfma", "kernel": "lnb_rep_kernel (+ lnb_rep_pack_kernel)",
-                "achieved": round(rp["tflops"], 2), "peak": round(SPLIT_F16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
-                "frac": round(rp["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": rp["flops_per_launch"],
-                "mean_launch_ms": round(rp["mean_ms"], 4), "launches": rp["launches"],
-                "hbm_gbps": round(rp["gbps"], 1), "bytes_per_launch": rp["bytes_per_launch"],
-                "note": "algorithmic fp32 flops (LN, W1, depthwise, gate, W2, skip) / HIP-event time against the "
-                        "dense fp16 rate / 3 (both GEMMs on exact fp16 two-term splits; the depthwise folded into "
-                        "GEMM1 as a 27-deep im2col operand); bytes: src in, out written"}
+    if "lnb_fused" in kern:   # the C = 96 blocks as one fused pass (lnb_fused16_kernel)
+        fu = kern["lnb_fused"]
+        res.setdefault("roofline_secondary", {})["lnb_fused"] = {
+            "bound": "mfma", "kernel": "lnb_fused16_kernel (+ lnb_fused_pack_kernel)",
+            "achieved": round(fu["tflops"], 2), "peak": round(SPLIT_F16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
+            "frac": round(fu["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": fu["flops_per_launch"],
+            "mean_launch_ms": round(fu["mean_ms"], 4), "launches": fu["launches"],
+            "hbm_gbps": round(fu["gbps"], 1), "bytes_per_launch": fu["bytes_per_launch"],
+            "traffic": load_traffic_file("traffic_lnb_fused.json", "lnb_fused16_kernel", b),
+            "note": "algorithmic fp32 flops (LN, W1, depthwise, gate, W2, skip) / HIP-event time against the dense "
+                    "fp16 rate / 3 (both GEMMs on exact fp16 two-term splits, three products each); bytes: x in, out "
+                    "written (compulsory); the gated activation stays on chip"}
+    if "lnb_rep_fused" in kern:   # the first block, on the replicated RGB input: one fused pass
+        rp = kern["lnb_rep_fused"]
+        res.setdefault("roofline_secondary", {})["lnb_rep_fused"] = {
+            "bound": "mfma", "kernel": "lnb_rep_kernel (+ lnb_rep_pack_kernel)",
+            "achieved": round(rp["tflops"], 2), "peak": round(SPLIT_F16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
+            "frac": round(rp["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": rp["flops_per_launch"],
+            "mean_launch_ms": round(rp["mean_ms"], 4), "launches": rp["launches"],
+            "hbm_gbps": round(rp["gbps"], 1), "bytes_per_launch": rp["bytes_per_launch"],
+            "note": "algorithmic fp32 flops (LN, W1, depthwise, gate, W2, skip) / HIP-event time against the "
+                    "dense fp16 rate / 3 (both GEMMs on exact fp16 two-term splits; the depthwise folded into "
+                    "GEMM1 as a 27-deep im2col operand); bytes: src in, out written"}
     kernels_ms = {k: round(v["total_ms"] / n_inst, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms
     if args.breakdown:

@@ -59,6 +59,34 @@ def reverse_roofline(kern, model, batch, size):
             "launches": v["launches"]}
 
 
+BF16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 / fp16 MFMA
+SPLIT_BF16_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6   # six bf16 products per fp32-accurate product
+
+
+def secondary_rooflines(kern):
+    """Rooflines of the training step's other large kernel families: the split-bf16 GEMMs (conv1x1: every
+    1x1 conv / LNB GEMM data path; wgrad: the weight gradients) against the dense bf16 MFMA rate / 6 (each
+    fp32-accurate product = six bf16 products of exact three-term splits), and the LNB gate + depthwise
+    reverse (a streaming row kernel) against HBM; algorithmic flops / bytes over HIP-event time."""
+    out = {}
+    for kind, label in (("conv1x1", "gemm_x3_kernel / gemm_x3k_kernel (1x1 convs, LNB GEMMs, 2x2 data grads)"),
+                        ("wgrad", "wgrad_kernel + its fixed-order chunk reduction (weight gradients)")):
+        v = kern.get(kind)
+        if v and v["flops_per_launch"] > 0:
+            out[kind] = {"bound": "mfma", "kernel": label, "achieved": round(v["tflops"], 2),
+                         "peak": round(SPLIT_BF16_PEAK_TFLOPS, 1), "unit": "TFLOP/s",
+                         "frac": round(v["tflops"] / SPLIT_BF16_PEAK_TFLOPS, 4),
+                         "flops_per_launch": v["flops_per_launch"], "mean_launch_ms": round(v["mean_ms"], 4),
+                         "launches": v["launches"], "hbm_gbps": round(v["gbps"], 1)}
+    for kind in ("lnb_gate_dw3_bwd", "lnb_norm_bwd", "bwd_cg_glue"):
+        v = kern.get(kind)
+        if v and v["bytes_per_launch"] > 0:
+            out[kind] = {"bound": "hbm", "achieved": round(v["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(v["gbps"] / HBM_PEAK_GBPS, 4), "bytes_per_launch": v["bytes_per_launch"],
+                         "mean_launch_ms": round(v["mean_ms"], 4), "launches": v["launches"]}
+    return out
+
+
 def cpu_baseline(model, model_kind, size, runs=3):
     """The oracle's differentiable restatement of the same model (PyTorch-CPU fp32, the
     reference's op sequence) for one optimisation step -- forward, L1 loss, autograd reverse,
@@ -204,6 +232,7 @@ def main():
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                "kernel_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}}
         res["roofline"] = reverse_roofline(kern, args.model, args.batch, args.size)
+        res["roofline_secondary"] = secondary_rooflines(kern)
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(model, args.model, args.cpu_size or (args.size if args.model == "msgf" else 128))
             res["cpu_baseline"] = cb

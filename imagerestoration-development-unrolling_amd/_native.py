@@ -75,6 +75,9 @@ SIGNATURES = {
     "grr_wgrad": [P, P, P, P, I, I, I, L, P],
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_lnb_forward_keep": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_lnb_fused": [I, I],
+    "grr_lnb_set_fused": [I],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
     "grr_lnb_forward_rep": [P, I, I, P, P, P, P, P, P, P, P, I, I, I, I, P],
     # GLRFast / GTVFast sub-API

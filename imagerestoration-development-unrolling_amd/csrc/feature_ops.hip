@@ -944,6 +944,21 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
   return grr::block_x3_forward<false>(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
 }
 
+grr_status grr_lnb_forward_keep(const float* x, const float* ln_w, const float* w1, const float* wdw,
+                                const float* w2, const float* skip, float* out, void* workspace, int B, int C,
+                                int hid, int H, int W, void* stream) {
+  grr::clear_error();
+  GRR_REQUIRE(x && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && C > 1 && hid > 0 && H > 0 &&
+                  W > 0,
+              GRR_ERR_INVALID_ARG, "grr_lnb_forward_keep: bad args");
+  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward_keep: out aliases x");
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0, GRR_ERR_INVALID_ARG,
+              "grr_lnb_forward_keep: workspace not 256-B aligned");
+  GRR_REQUIRE(C <= 128, GRR_ERR_UNSUPPORTED, "grr_lnb_forward_keep: C=%d > 128", C);
+  return grr::lnb_forward_mfma(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W,
+                               (hipStream_t)stream, true);
+}
+
 grr_status grr_lnb_forward_rep(const float* src, int Cs, int R, const float* x, const float* ln_w, const float* w1,
                                const float* wdw, const float* w2, const float* skip, float* out, void* workspace,
                                int B, int hid, int H, int W, void* stream) {

@@ -42,9 +42,12 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t n) {
 
 // LocalNonLinearBlock on the split-bf16 MFMA kernels (lnb_ops.hip), C <= 128
 int64_t lnb_mfma_workspace_floats(int B, int C, int hid, int H, int W);
+// C <= 96 runs the whole block as one fused pass (lnb_fused16_kernel); keep_g: it also stores the gated
+// activation g [B, hid, H, W] at the workspace's start (where the two-kernel path leaves it anyway)
+bool lnb_fused(int C, int hid);
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                             const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
-                            hipStream_t s);
+                            hipStream_t s, bool keep_g = false);
 // the same block when x holds R stacked copies of the Ch-channel image xh (GEMM1 runs on xh)
 grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
                                 const float* wdw, const float* w2, const float* skip, float* out, float* ws, int B,

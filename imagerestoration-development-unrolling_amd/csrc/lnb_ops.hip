@@ -1023,6 +1023,623 @@ __global__ __launch_bounds__(64 * LR_NW, MT <= 3 ? 4 : 3) void lnb_rep_kernel(Ln
 }
 
 // ---------------------------------------------------------------------------
+// fused16: the whole block for C <= 96 in one pass -- LN + W1 + depthwise 3x3 + gate + W2 + skip --
+// with the gated activation kept on chip (no g round trip through HBM, no mix launch).
+//
+// Persistent, wave-specialised workgroups (8 waves, one workgroup per CU, 148 KB of LDS): waves 0-3 are
+// producers, waves 4-7 consumers; wave w and w + 4 share a SIMD.  A tile is 32 output columns x 8 output
+// rows with its 34 x 10 halo (340 pixels in 11 blocks of 32); hidden channels go in chunks of 16 (mask,
+// value) pairs.  A workgroup walks its tiles' chunks as one sequence of steps; step i:
+//   producers  GEMM1 of step i's (tile, chunk) (v_mfma_f32_32x32x16_f16 on exact two-term fp16 splits,
+//              head16's arithmetic and scaling; x / sigma of the wave's halo blocks in registers, loaded,
+//              normalised and split at the tile's first chunk) -> the chunk's h planes in LDS buffer i & 1;
+//   consumers  depthwise 3x3 + gate of step i - 1 (buffer (i - 1) & 1) in the GEMM2 B-operand layout:
+//              lane = (column l % 32, pair half l / 32), two output rows per wave, the half's 8 pairs in
+//              turn (taps from the ring, the same for a lane half; the window of both rows' pixels, 4 x 3
+//              h pairs, read once); GEMM2 (W2 g, v_mfma_f32_32x32x16_f16, two-term fp16 splits) with rep's
+//              running per-pixel exponent (largest |g| so far into [2^13, 2^14); a lower one scales the
+//              pixel's accumulators down exactly); the W2 accumulators (2 rows x MT tiles) stay in the
+//              consumer's registers over the tile's chunks; after the tile's last chunk the epilogue
+//              out = skip0 x + skip1 2^-(s2_row + E) acc, while the producers already load the next tile;
+//   one barrier; the W1 / W2 fragments and taps of step i + 1 arrive by LDS-DMA in a 3-slot ring meanwhile.
+// With a gate buffer given (training's kept gate) the consumers also store g [B, hid, H, W] (fp32).
+// Against head16 + mix: no g write + read (2 KB per pixel at hid 256), half the GEMM2 products (fp16
+// two-term instead of the bf16 three-term split), one launch, and the x prologue / output epilogue of a
+// tile overlap the other role's work.
+constexpr int LF_TW = 32;                   // output columns per tile
+constexpr int LF_TH = 8;                    // output rows per tile (2 per consumer wave)
+constexpr int LF_HWD = LF_TW + 2;           // halo columns
+constexpr int LF_HR = LF_TH + 2;            // halo rows
+constexpr int LF_NQ = LF_HWD * LF_HR;       // halo pixels (340)
+constexpr int LF_NBLK = (LF_NQ + 31) / 32;  // 32-pixel GEMM1 blocks (11)
+constexpr int LF_PP = 2 * LF_NBLK * 32;     // floats per pair plane (m, v interleaved)
+constexpr int LF_HBUF = 16 * LF_PP;         // floats per h buffer
+constexpr int LF_NSLOT = 3;                 // ring slots (step i + 1 loading, GEMM1(i), GEMM2(i - 1))
+constexpr int LF_XE = 10;                   // common power-of-two scale of the fp16 x operand
+constexpr int LF_TAPS = 16 * 18;            // tap floats per chunk (two 1-KB images)
+__host__ __device__ constexpr int fused_images(int KS, int MT) { return 2 * KS + 2 * MT + 2; }
+
+struct LnbFusedArgs {
+  const float* x;        // [B, C, H, W]
+  const char* pack;      // [nch][fused_images] 1-KB images: W1 frags (hi, lo per k-step), W2 frags (hi, lo per
+                         // row tile), taps ([pair][tap][mask, value], scaled and exp2-folded)
+  const float* r2;       // [C]: 2^-s2_row
+  const float* skip;     // [2]
+  float* out;            // [B, C, H, W]
+  float* g;              // [B, hid, H, W] or nullptr
+  float var_den;
+  int C, hid, H, W, tiles_x, tiles_y, nch, ntiles;
+};
+
+// W1 images as lnb_w1_pack16_kernel's (rows 2^s_row-scaled, fp16 hi / lo); W2 images: row tile t, term q,
+// lane l, element j: m = 32 t + (l & 31), k = 8 (l >> 5) + j = pair 16 c + k, W2[m][16 c + k] 2^s2_row(m);
+// taps as head16's (2^-(s_row + XE), exp2 fold); r2[m] = 2^-s2_row(m)
+__global__ void lnb_fused_pack_kernel(const float* __restrict__ w1, const float* __restrict__ ln_w,
+                                      const float* __restrict__ wdw, const float* __restrict__ w2,
+                                      char* __restrict__ pack, float* __restrict__ r2, int C, int hid, int KS,
+                                      int MT, int nch) {
+  const int NI = fused_images(KS, MT);
+  const int64_t n_img = (int64_t)nch * NI * 256;
+  const int64_t n = n_img + C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i >= n_img) {
+      const int m = (int)(i - n_img);
+      r2[m] = ldexpf(1.0f, -rep_w2_exp(w2, m, hid));
+      continue;
+    }
+    const int64_t img = i >> 8;
+    const int e = (int)(i & 255), c = (int)(img / NI), im = (int)(img % NI), l = e >> 2;
+    uint32_t word = 0;
+    if (im < 2 * KS) {
+      const int q = im & 1, s = im >> 1, r = l & 31, pj = 16 * c + (r >> 1);
+      if (pj < hid) {
+        const int row = (r & 1 ? hid : 0) + pj;
+        const int sc = head16_row_exp(w1, ln_w, row, C, 1);
+        float v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int k = 16 * s + 8 * (l >> 5) + 2 * (e & 3) + u;
+          v[u] = k < C ? ldexpf(w1[(int64_t)row * C + k] * ln_w[k], sc) : 0.f;
+        }
+        word = f16_pair_word(v[0], v[1], q);
+      }
+    } else if (im < 2 * KS + 2 * MT) {
+      const int t = (im - 2 * KS) >> 1, q = (im - 2 * KS) & 1, m = 32 * t + (l & 31);
+      if (m < C) {
+        const int sc = rep_w2_exp(w2, m, hid);
+        float v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int pj = 16 * c + 8 * (l >> 5) + 2 * (e & 3) + u;
+          v[u] = pj < hid ? ldexpf(w2[(int64_t)m * hid + pj], sc) : 0.f;
+        }
+        word = f16_pair_word(v[0], v[1], q);
+      }
+    } else {
+      const int r = (im - 2 * KS - 2 * MT) * 256 + e;
+      if (r < LF_TAPS) {
+        const int w = r / 18, t = (r % 18) >> 1, comp = r & 1, pj = 16 * c + w;
+        if (pj < hid) {
+          const int row = (comp ? hid : 0) + pj;
+          const float fold = comp ? -0.69314718055994531f : -1.44269504088896341f;
+          word = __float_as_uint(ldexpf(wdw[(int64_t)row * 9 + t], -(head16_row_exp(w1, ln_w, row, C, 1) + LF_XE)) *
+                                 fold);
+        }
+      }
+    }
+    reinterpret_cast<uint32_t*>(pack)[i] = word;
+  }
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const float* const_f32_t;
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// exact two-term fp16 split of (a, b) with packed round-to-nearest conversions (v_cvt_pk_f16_f32): hi, lo
+__device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const f32x2v v = f32x2v{a, b};
+  const f16x2 h = __builtin_convertvector(v, f16x2);
+  const f16x2 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2v), f16x2);
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+// consumer mapping (A/B build macro): 0 = lane per pixel, pairs in turn with scalar taps, B operands by
+// v_permlane32_swap; 1 = lane per (column, pair half), two rows per lane, taps from the LDS ring
+#ifndef GRR_FUSED_MAP
+#define GRR_FUSED_MAP 1
+#endif
+
+// timing-only diagnostic builds (wrong results): 1 = consumers skip their work, 2 = producers skip theirs
+#ifndef GRR_FUSED_DIAG
+#define GRR_FUSED_DIAG 0
+#endif
+#ifndef GRR_FUSED_PRIO   // consumer waves' static priority (A/B: 0 -> 1 took 3 % off at 256^2 and 128^2)
+#define GRR_FUSED_PRIO 1
+#endif
+
+// tile t of the launch -> (b, ty, tx): consecutive tiles of a workgroup walk along rows of one image
+struct FusedTile {
+  int b, y0, x0;
+};
+__device__ __forceinline__ FusedTile fused_tile(const LnbFusedArgs& a, int t) {
+  const int tx = t % a.tiles_x, r = t / a.tiles_x;
+  return FusedTile{r / a.tiles_y, (r % a.tiles_y) * LF_TH, tx * LF_TW};
+}
+
+template <int KS, int MT>
+__global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
+  constexpr int NI = fused_images(KS, MT), SLOTF = NI * 256;
+  constexpr int DPW = (NI + 7) / 8;      // LDS-DMA instructions per wave per step
+  __shared__ __attribute__((aligned(16))) float smem[2 * LF_HBUF + LF_NSLOT * SLOTF + 32 * MT];
+  float* const ring = smem + 2 * LF_HBUF;
+  float* const r2s = ring + LF_NSLOT * SLOTF;    // 2^-s2_row of the W2 rows (0 past C)
+
+  const int tid = threadIdx.x, lane = tid & 63, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, W = a.W, C = a.C, hid = a.hid, nch = a.nch;
+  if (tid < 32 * MT) r2s[tid] = tid < C ? a.r2[tid] : 0.f;   // read after the first barrier
+  const int HW = H * W;
+  // the workgroup's tiles: blockIdx.x, + gridDim.x, ...; steps = tiles x chunks (+ 1: the last gate)
+  const int G = gridDim.x, wg = blockIdx.x;
+  const int my_tiles = wg < a.ntiles ? (a.ntiles - wg + G - 1) / G : 0;
+  const int nsteps = my_tiles * nch;
+
+  // the chunk `chunk` into ring slot `sl` (the offsets recomputed per call: hoisted out of the step loop
+  // they would hold 2 DPW x 3 SGPRs for the whole kernel)
+  auto issue = [&](int sl, int chunk) {
+    int sv = sl, cv = chunk, wv = wave;
+    asm volatile("" : "+s"(sv), "+s"(cv), "+s"(wv));
+    float* slot = ring + sv * SLOTF;
+    const char* src = a.pack + (int64_t)cv * NI * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int img = min(i * 8 + wv, NI - 1);   // surplus waves repeat the last image
+      dma16_opaque(src + img * 1024, slot + img * 256);
+    }
+  };
+  // step counters without divisions: (chunk, ring slot) of the next step's DMA
+  int dch = nch > 1 ? 1 : 0, dsl = 1;
+  auto advance_dma = [&]() {
+    dch = dch + 1 == nch ? 0 : dch + 1;
+    dsl = dsl == LF_NSLOT - 1 ? 0 : dsl + 1;
+  };
+  if (nsteps == 0) return;   // workgroup-uniform: no barrier is left waiting
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  if (wave < 4) {
+    // ---------------- producer: GEMM1 of the halo blocks wave, wave + 4, wave + 8 (< LF_NBLK)
+    constexpr int NBW = (LF_NBLK + 3) / 4;
+    const bool has_last = wave + 4 * (NBW - 1) < LF_NBLK;   // wave-uniform
+    f16x8 xh[NBW][KS], xl[NBW][KS];
+    float corr[NBW];
+    bool wave_corr = false;
+    int c = 0, tile = wg, sl = 0;                  // step i's chunk, tile and ring slot
+    for (int i = 0; i <= nsteps; ++i) {
+      issue(dsl, dch);                             // slot of step i + 1 last served step i - 2 (steps i - 2, i - 1)
+      advance_dma();
+      if (i < nsteps && !(GRR_FUSED_DIAG & 2)) {
+        if (c == 0) {
+          // the tile's halo pixels: raw x, LayerNorm statistics (REF:916-922), x / sigma split in fp16 terms
+          const FusedTile T = fused_tile(a, tile);
+          // x of the image through a buffer descriptor: channel 16 s + 8 kh + j of the lane's pixel at
+          // voffset (pixel + 8 kh HW) 4 + soffset (16 s + j) HW 4 -- the uniform part in an SGPR, no
+          // per-element address arithmetic -- and channels >= C past num_records read as 0
+          const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<float*>(a.x + (int64_t)T.b * C * HW), 0, (int)((int64_t)C * HW * 4), 0x00020000);
+          bool any_corr = false;
+#pragma unroll
+          for (int k = 0; k < NBW; ++k) {
+            const int q = min((wave + 4 * k) * 32 + (lane & 31), LF_NQ - 1);
+            const int hy = q / LF_HWD, hx = q - hy * LF_HWD;
+            const int gy = clampi(T.y0 - 1 + hy, 0, H - 1), gx = clampi(T.x0 - 1 + hx, 0, W - 1);
+            const int vo = (8 * kh * HW + gy * W + gx) * 4;
+            // (a copy per block the compiler cannot see through: otherwise it hoists the 8 KS soffsets out
+            // of the step loop and holds them in SGPRs for the whole kernel)
+            int hw4 = HW * 4;
+            asm volatile("" : "+s"(hw4));
+            float xv[KS][8];
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                xv[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
+            float sum = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) sum += xv[s][j];
+            sum += __shfl_xor(sum, 32);
+            const float mean = sum / (float)C;
+            float sq = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float d = 16 * s + 8 * kh + j < C ? xv[s][j] - mean : 0.f;
+                sq += d * d;
+              }
+            sq += __shfl_xor(sq, 32);
+            const float rstd = 1.0f / sqrtf(sq / a.var_den + 1e-5f);
+            float mx = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                xv[s][j] *= rstd;                       // x / sigma (REF:921)
+                mx = fmaxf(mx, fabsf(xv[s][j]));
+              }
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            int ep = LF_XE;
+            if (mx != 0.f) {
+              int e;
+              frexpf(mx, &e);
+              if (e > 14 - LF_XE || e < -LF_XE) ep = clampi(14 - e, -100, 100);
+            }
+            corr[k] = ldexpf(1.0f, LF_XE - ep);
+            any_corr |= ep != LF_XE;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              uint32_t hw[4], lw[4];
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                split2_f16(ldexpf(xv[s][2 * j], ep), ldexpf(xv[s][2 * j + 1], ep), hw[j], lw[j]);
+              xh[k][s] = __builtin_bit_cast(f16x8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+              xl[k][s] = __builtin_bit_cast(f16x8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+            }
+            // one block's raw x (8 KS floats per lane) at a time: the scheduler would issue every block's
+            // loads up front, and the raw values + the split blocks exceed the register file
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          wave_corr = __builtin_amdgcn_readfirstlane((int)__any(any_corr)) != 0;
+        }
+        const float* slot = ring + sl * SLOTF + lane * 4;
+        f32x16 acc[NBW];
+#pragma unroll
+        for (int k = 0; k < NBW; ++k) acc[k] = f32x16{};
+        // k-step s's W1 fragments in registers while step s + 1's load (the scheduling barrier keeps the
+        // compiler from reading every k-step's fragments up front: 8 KS registers on top of the x operands)
+        f16x8 ah = *reinterpret_cast<const f16x8*>(slot);
+        f16x8 al = *reinterpret_cast<const f16x8*>(slot + 256);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          f16x8 bh, bl;
+          if (s + 1 < KS) {
+            bh = *reinterpret_cast<const f16x8*>(slot + (2 * s + 2) * 256);
+            bl = *reinterpret_cast<const f16x8*>(slot + (2 * s + 3) * 256);
+          }
+#pragma unroll
+          for (int k = 0; k < NBW; ++k) {
+            if (k == NBW - 1 && !has_last) continue;
+            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh[k][s], acc[k], 0, 0, 0);
+            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl[k][s], acc[k], 0, 0, 0);
+            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[k][s], acc[k], 0, 0, 0);
+          }
+          if (s + 1 < KS) {
+            ah = bh;
+            al = bl;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        float* hb = smem + (i & 1) * LF_HBUF;
+#pragma unroll
+        for (int k = 0; k < NBW; ++k) {
+          if (k == NBW - 1 && !has_last) continue;
+          if (wave_corr) acc[k] *= corr[k];
+          const int q = (wave + 4 * k) * 32 + (lane & 31);
+          // registers 2u, 2u + 1 = rows r, r + 1 (r even: mask, value of chunk pair r / 2)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int r = ((2 * u) & 3) + 8 * ((2 * u) >> 2) + 4 * kh;
+            *reinterpret_cast<f32x2*>(hb + (r >> 1) * LF_PP + 2 * q) = f32x2{acc[k][2 * u], acc[k][2 * u + 1]};
+          }
+        }
+        if (++c == nch) {
+          c = 0;
+          tile += G;
+        }
+        sl = sl == LF_NSLOT - 1 ? 0 : sl + 1;
+      }
+      // step i + 1's chunk landed (this wave's DMAs), h(i) written; then every wave's
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
+
+  // ---------------- consumer: depthwise + gate + GEMM2 of output rows 2 cw, 2 cw + 1 of the tile
+#if GRR_FUSED_PRIO
+  __builtin_amdgcn_s_setprio(GRR_FUSED_PRIO);      // the VALU-bound role first at the SIMD's issue arbiter
+#endif
+  const int cw = wave - 4;
+  const int col = lane & 31;
+  f32x16 acc2[2][MT];
+  int E[2] = {1000, 1000};                           // the column pixel's GEMM2 scale exponent per row (none yet)
+  int ch = 0, ctile = wg, csl = 0;                   // step i - 1's chunk, tile and ring slot
+  for (int i = 0; i <= nsteps; ++i) {
+    issue(dsl, dch);
+    advance_dma();
+    if (i >= 1 && !(GRR_FUSED_DIAG & 1)) {
+      const int st = i - 1;
+      if (ch == 0) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc2[rb][t] = f32x16{};
+          E[rb] = 1000;
+        }
+      }
+      const float* slot = ring + csl * SLOTF;
+      const FusedTile T = fused_tile(a, ctile);
+      const int gxo = T.x0 + col;
+      const float* w2s = slot + 2 * KS * 256 + lane * 4;
+#if GRR_FUSED_MAP == 0
+      // lane = pixel (output row 2 cw + lane / 32, column lane % 32); the 16 pairs in turn, each pair's taps
+      // the same for the whole wave: scalar loads, SGPR operands of the FMAs.  The next pair's taps (SMEM)
+      // and window (LDS) are issued right after the current pair's first product -- SMEM and LDS share
+      // lgkmcnt and SMEM completes out of order, so the wait the compiler puts before that product (lgkmcnt
+      // 0) must not cover them -- and land while the rest of the pair computes.
+      const float* hwin = smem + (st & 1) * LF_HBUF + 2 * ((2 * cw + kh) * LF_HWD + col);
+      const_f32_t tp = (const_f32_t)(a.pack + (int64_t)ch * NI * 1024) + (2 * KS + 2 * MT) * 256;
+      float g[16];
+      float tA[18];
+      f32x2 wA[9];
+#pragma unroll
+      for (int u = 0; u < 18; ++u) tA[u] = tp[u];
+#pragma unroll
+      for (int u = 0; u < 9; ++u) wA[u] = *reinterpret_cast<const f32x2*>(hwin + 2 * ((u / 3) * LF_HWD + u % 3));
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        float m = tA[0] * wA[0][0], v = tA[1] * wA[0][1];
+        __builtin_amdgcn_sched_barrier(0);
+        float tB[18];
+        f32x2 wB[9];
+        if (j < 15) {
+#pragma unroll
+          for (int u = 0; u < 18; ++u) tB[u] = tp[(j + 1) * 18 + u];
+          const float* hp = hwin + (j + 1) * LF_PP;
+#pragma unroll
+          for (int u = 0; u < 9; ++u) wB[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 1; t < 9; ++t) {
+          m = __builtin_fmaf(tA[2 * t], wA[t][0], m);
+          v = __builtin_fmaf(tA[2 * t + 1], wA[t][1], v);
+        }
+        // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
+        g[j] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+        if (j < 15) {
+#pragma unroll
+          for (int u = 0; u < 18; ++u) tA[u] = tB[u];
+#pragma unroll
+          for (int u = 0; u < 9; ++u) wA[u] = wB[u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (a.g) {   // kept gate (training): the unscaled fp32 values, [B, hid, H, W]; pairs >= hid past num_records
+        const int yy = T.y0 + 2 * cw + kh;
+        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+            a.g + (int64_t)T.b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
+        const uint32_t vo = yy < H && gxo < W ? (uint32_t)(yy * W + gxo) * 4u : 0x80000000u;
+        int hw4 = HW * 4;
+        asm volatile("" : "+s"(hw4));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g[j]), grs, vo, (16 * ch + j) * hw4, 0);
+      }
+      // the pixel's running exponent: largest |g| so far into [2^13, 2^14)
+      float gm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) gm = fmaxf(gm, fabsf(g[j]));
+      const int Eo = E[0];                           // this lane's pixel (E[1] unused in this mapping)
+      int eg = Eo;
+      if (gm != 0.f) {
+        int e;
+        frexpf(gm, &e);
+        eg = min(Eo, clampi(14 - e, -100, 100));
+      }
+      if (__builtin_amdgcn_readfirstlane((int)__any(eg != Eo && Eo != 1000)) != 0) {
+        // accumulator column = lane % 32 holds the pixel of row 2 cw (block 0) / 2 cw + 1 (block 1) in both
+        // lane halves: the factor of the lane half that computed that pixel
+        const float f = Eo != 1000 ? ldexpf(1.0f, eg - Eo) : 1.0f;
+        const auto fs = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc2[0][t] *= __uint_as_float(fs[0]);
+          acc2[1][t] *= __uint_as_float(fs[1]);
+        }
+      }
+      E[0] = eg;
+      const int Eu = eg == 1000 ? 0 : eg;
+      // two-term fp16 split of 2^Eu g, packed (pair 2q, 2q + 1); v_permlane32_swap turns the lane-per-pixel
+      // layout into the B operands of the two rows: lanes 0-31 keep pairs 0-7 of row 2 cw and take pairs
+      // 8-15 of it from lanes 0-31 of the other register; lanes 32-63 likewise for row 2 cw + 1
+      uint32_t hx[8], lx[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) split2_f16(ldexpf(g[2 * q], Eu), ldexpf(g[2 * q + 1], Eu), hx[q], lx[q]);
+      uint32_t bh[2][4], bl[2][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto sh = __builtin_amdgcn_permlane32_swap(hx[q], hx[q + 4], false, false);
+        const auto sl = __builtin_amdgcn_permlane32_swap(lx[q], lx[q + 4], false, false);
+        bh[0][q] = sh[0];
+        bh[1][q] = sh[1];
+        bl[0][q] = sl[0];
+        bl[1][q] = sl[1];
+      }
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(w2s + (2 * t + 0) * 256);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(w2s + (2 * t + 1) * 256);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const f16x8 gh = __builtin_bit_cast(f16x8, u32x4{bh[rb][0], bh[rb][1], bh[rb][2], bh[rb][3]});
+          const f16x8 gl = __builtin_bit_cast(f16x8, u32x4{bl[rb][0], bl[rb][1], bl[rb][2], bl[rb][3]});
+          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc2[rb][t], 0, 0, 0);
+          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc2[rb][t], 0, 0, 0);
+          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc2[rb][t], 0, 0, 0);
+        }
+      }
+#else
+      // the window of both rows' pixels: halo rows 2 cw .. 2 cw + 3, columns col .. col + 2, pair 8 kh + jj
+      const float* hwin = smem + (st & 1) * LF_HBUF + 8 * kh * LF_PP + 2 * (2 * cw * LF_HWD + col);
+      const float* tap0 = slot + (2 * KS + 2 * MT) * 256 + 8 * kh * 18;
+      float g[2][8];
+      // One pair per step, the next pair's taps and window in flight (LDS reads count in order: the
+      // compiler waits for this pair's only); the scheduling barrier keeps each step's loads in it
+      float tA[18];
+      f32x2 wA[12];
+      auto load = [&](int jj, float (&t)[18], f32x2 (&w)[12]) {
+        const float* tp = tap0 + jj * 18;
+#pragma unroll
+        for (int u = 0; u < 18; ++u) t[u] = tp[u];
+        const float* hp = hwin + jj * LF_PP;
+#pragma unroll
+        for (int u = 0; u < 12; ++u) w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
+      };
+      load(0, tA, wA);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        float tB[18];
+        f32x2 wB[12];
+        if (jj < 7) load(jj + 1, tB, wB);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          float m = tA[0] * wA[3 * rb][0], v = tA[1] * wA[3 * rb][1];
+#pragma unroll
+          for (int t = 1; t < 9; ++t) {
+            const f32x2 hv = wA[3 * (rb + t / 3) + t % 3];
+            m = __builtin_fmaf(tA[2 * t], hv[0], m);
+            v = __builtin_fmaf(tA[2 * t + 1], hv[1], v);
+          }
+          // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
+          g[rb][jj] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+        }
+        if (jj < 7) {
+#pragma unroll
+          for (int u = 0; u < 18; ++u) tA[u] = tB[u];
+#pragma unroll
+          for (int u = 0; u < 12; ++u) wA[u] = wB[u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (a.g) {   // kept gate (training): the unscaled fp32 values, [B, hid, H, W]
+        float* gb = a.g + (int64_t)T.b * hid * HW;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int yy = T.y0 + 2 * cw + rb;
+          if (yy < H && gxo < W) {
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              const int pj = 16 * ch + 8 * kh + jj;
+              if (pj < hid) gb[(int64_t)pj * HW + yy * W + gxo] = g[rb][jj];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        // the pixel's running exponent: largest |g| over the chunk's 16 pairs (both lane halves) into
+        // [2^13, 2^14); a lower one scales the pixel's accumulated sums down by the exact power of two
+        float gm = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) gm = fmaxf(gm, fabsf(g[rb][jj]));
+        const auto gs = __builtin_amdgcn_permlane32_swap(__float_as_uint(gm), __float_as_uint(gm), false, false);
+        gm = fmaxf(__uint_as_float(gs[0]), __uint_as_float(gs[1]));
+        int eg = E[rb];
+        if (gm != 0.f) {
+          int e;
+          frexpf(gm, &e);
+          eg = min(E[rb], clampi(14 - e, -100, 100));
+        }
+        if (__builtin_amdgcn_readfirstlane((int)__any(eg != E[rb] && E[rb] != 1000)) != 0) {
+          const float f = E[rb] != 1000 ? ldexpf(1.0f, eg - E[rb]) : 1.0f;
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc2[rb][t] *= f;
+        }
+        E[rb] = eg;
+        const int Eu = eg == 1000 ? 0 : eg;
+        f16x8 gh, gl;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float v = ldexpf(g[rb][jj], Eu);
+          const _Float16 h0 = (_Float16)v;
+          gh[jj] = h0;
+          gl[jj] = (_Float16)(v - (float)h0);
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(w2s + (2 * t + 0) * 256);
+          const f16x8 al = *reinterpret_cast<const f16x8*>(w2s + (2 * t + 1) * 256);
+          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc2[rb][t], 0, 0, 0);
+          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc2[rb][t], 0, 0, 0);
+          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc2[rb][t], 0, 0, 0);
+        }
+      }
+#endif
+      if (ch == nch - 1) {
+        // epilogue (REF:962-964): out[m, p] = skip0 x[m, p] + skip1 2^-E_p r2[m] acc; accumulator block rb
+        // holds output row 2 cw + rb, column lane % 32, rows m = 32 t + (i & 3) + 8 (i >> 2) + 4 kh
+        const float s0 = a.skip[0], s1 = a.skip[1];
+        // skip operand and output through buffer descriptors: row m = 32 t + (u & 3) + 8 (u >> 2) + 4 kh of
+        // the lane's pixel at voffset (pixel + 4 kh HW) 4 + soffset (32 t + (u & 3) + 8 (u >> 2)) HW 4; rows
+        // >= C fall past num_records (loads 0, stores dropped), pixels outside the image take an
+        // out-of-range voffset
+        const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.x + (int64_t)T.b * C * HW), 0, (int)((int64_t)C * HW * 4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)T.b * C * HW, 0,
+                                                                              (int)((int64_t)C * HW * 4), 0x00020000);
+#if GRR_FUSED_MAP == 0
+        const auto es = __builtin_amdgcn_permlane32_swap((uint32_t)E[0], (uint32_t)E[0], false, false);
+        const int Eb[2] = {(int)es[0], (int)es[1]};
+#else
+        const int Eb[2] = {E[0], E[1]};
+#endif
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const float sc = s1 * ldexpf(1.0f, Eb[rb] == 1000 ? 0 : -Eb[rb]);
+          const int yy = T.y0 + 2 * cw + rb;
+          const bool ok = yy < H && gxo < W;
+          const uint32_t vx = (uint32_t)(4 * kh * HW + min(yy, H - 1) * W + min(gxo, W - 1)) * 4u;
+          const uint32_t vo = ok ? vx : 0x80000000u;
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            int hw4 = HW * 4;                      // (not hoisted: see the producer's x loads)
+            asm volatile("" : "+s"(hw4));
+            float xv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              xv[u] = __uint_as_float(
+                  __builtin_amdgcn_raw_buffer_load_b32(xrs, vx, (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0));
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const float r2 = r2s[32 * t + (u & 3) + 8 * (u >> 2) + 4 * kh];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[u] + sc * (acc2[rb][t][u] * r2)), ors, vo,
+                                                    (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0);
+            }
+            // one row tile's skip operands at a time (the scheduler would load all of them up front: 2 x MT
+            // x 16 more live registers, the kernel's peak)
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if (++ch == nch) {
+        ch = 0;
+        ctile += G;
+      }
+      csl = csl == LF_NSLOT - 1 ? 0 : csl + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+// ---------------------------------------------------------------------------
 // mix: out = skip0 x + skip1 W2 g
 constexpr int LM_NBB = 2;                 // 32-pixel blocks per wave
 constexpr int LM_PX = 4 * LM_NBB * 32;    // pixels per workgroup
@@ -1194,9 +1811,20 @@ static int64_t mix_pack_floats(int C, int hid) {
   return align64((int64_t)((hid + LM_KD - 1) / LM_KD) * ((C + 31) / 32) * 3 * 256);
 }
 
-// workspace (floats): [g: B*hid*P][W1 images][W2 images], each 256-B aligned
+// the fused block (lnb_fused16_kernel): C <= 96 (GEMM1's x of three halo blocks, 6 k-steps, in registers)
+int g_lnb_fused_on = 1;   // grr_lnb_set_fused (A/B measurement knob)
+bool lnb_fused(int C, int hid) { return g_lnb_fused_on && C >= 2 && C <= 96 && hid >= 1; }
+static int64_t fused_pack_floats(int C, int hid) {
+  const int KS = (C + 15) / 16, MT = (C + 31) / 32, nch = (hid + 15) / 16;
+  return align64((int64_t)nch * fused_images(KS, MT) * 256) + align64(C);
+}
+
+// workspace (floats): [g: B*hid*P][W1 images][W2 images], each 256-B aligned; the fused block's images,
+// taps and W2 row scales where the two-kernel path keeps its W1 images (after the g region, which the
+// fused block fills only for grr_lnb_forward_keep)
 int64_t lnb_mfma_workspace_floats(int B, int C, int hid, int H, int W) {
-  const int64_t two_kernel = align64((int64_t)B * hid * H * W) + head_pack_floats(C, hid) + mix_pack_floats(C, hid);
+  const int64_t two_kernel = align64((int64_t)B * hid * H * W) +
+                             std::max(head_pack_floats(C, hid) + mix_pack_floats(C, hid), fused_pack_floats(C, hid));
   const int64_t rep = align64((int64_t)((hid + 15) / 16) * rep_images((C + 31) / 32) * 256);   // lnb_rep_kernel's chunk images
   return std::max(two_kernel, rep);
 }
@@ -1219,10 +1847,66 @@ static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
 // a caller can time the head and the mix of one block apart on a shared workspace
 int g_lnb_phases = 7;
 
+template <int KS>
+static void launch_fused(const LnbFusedArgs& f, unsigned grid, hipStream_t s) {
+  hipLaunchKernelGGL((lnb_fused16_kernel<KS, (KS + 1) / 2>), dim3(grid), dim3(512), 0, s, f);
+}
+// compute units of the current device (cached per device)
+static int num_cus() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                             const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
-                            hipStream_t s) {
-  return lnb_forward_mfma_rep(x, C, 1, x, ln_w, w1, wdw, w2, skip, out, ws, B, hid, H, W, s);
+                            hipStream_t s, bool keep_g) {
+  if (!lnb_fused(C, hid)) {
+    // the two-kernel path leaves g at the workspace's start anyway
+    return lnb_forward_mfma_rep(x, C, 1, x, ln_w, w1, wdw, w2, skip, out, ws, B, hid, H, W, s);
+  }
+  GRR_REQUIRE((int64_t)std::max(hid, C) * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_forward: max(hid, C)*H*W too large for one image's 32-bit offsets");
+  const int KS = (C + 15) / 16, MT = (C + 31) / 32, nch = (hid + 15) / 16;
+  const int64_t P = (int64_t)H * W;
+  float* base = ws + align64((int64_t)B * hid * P);
+  char* pack = reinterpret_cast<char*>(base);
+  float* r2 = base + align64((int64_t)nch * fused_images(KS, MT) * 256);
+  if (g_lnb_phases & 1) {
+    const int64_t n = (int64_t)nch * fused_images(KS, MT) * 256 + C;
+    hipLaunchKernelGGL(lnb_fused_pack_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256),
+                       0, s, w1, ln_w, wdw, w2, pack, r2, C, hid, KS, MT, nch);
+    grr_status st = launch_status("grr_lnb_forward/fused_pack");
+    if (st != GRR_OK) return st;
+  }
+  if (!(g_lnb_phases & 2)) return GRR_OK;
+  LnbFusedArgs f{};
+  f.x = x; f.pack = pack; f.r2 = r2; f.skip = skip; f.out = out;
+  f.g = keep_g ? ws : nullptr;
+  f.var_den = (float)(C - 1);
+  f.C = C; f.hid = hid; f.H = H; f.W = W; f.nch = nch;
+  f.tiles_x = (W + LF_TW - 1) / LF_TW;
+  f.tiles_y = (H + LF_TH - 1) / LF_TH;
+  const uint64_t nt = (uint64_t)B * f.tiles_x * f.tiles_y;
+  GRR_REQUIRE(nt < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_lnb_forward: grid too large");
+  f.ntiles = (int)nt;
+  // persistent: one workgroup per CU (its LDS), each walking tiles blockIdx.x, + gridDim.x, ...
+  const unsigned grid = (unsigned)std::min<uint64_t>(nt, (uint64_t)num_cus());
+  switch (KS) {
+    case 1: launch_fused<1>(f, grid, s); break;
+    case 2: launch_fused<2>(f, grid, s); break;
+    case 3: launch_fused<3>(f, grid, s); break;
+    case 4: launch_fused<4>(f, grid, s); break;
+    case 5: launch_fused<5>(f, grid, s); break;
+    default: launch_fused<6>(f, grid, s); break;
+  }
+  return launch_status("grr_lnb_forward/fused");
 }
 
 // the replicated first block runs as one fused pass (lnb_rep_kernel) when its im2col depth 9 Cs fits two
@@ -1347,6 +2031,14 @@ grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, 
 }  // namespace grr
 
 extern "C" int grr_lnb_rep_fused(int Cs, int R, int C, int hid) { return grr::lnb_rep_fused(Cs, R, C, hid) ? 1 : 0; }
+extern "C" int grr_lnb_fused(int C, int hid) { return grr::lnb_fused(C, hid) ? 1 : 0; }
+
+extern "C" grr_status grr_lnb_set_fused(int enable) {
+  grr::clear_error();
+  GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_lnb_set_fused: 0 or 1");
+  grr::g_lnb_fused_on = enable;
+  return GRR_OK;
+}
 
 extern "C" grr_status grr_lnb_set_phases(int mask) {
   grr::clear_error();

@@ -520,10 +520,10 @@ def conv1x1(x: Tensor, weight: Tensor) -> Tensor:
     if ws_bytes > 0:   # split-bf16 MFMA path (fp32-accurate); K > 128 streams K (gemm_x3k_kernel)
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)  # allocator: 512-B aligned
         _launch(kind, 4 * b * h * w * (k + m), "grr_conv1x1_ws", x.data_ptr(), weight.data_ptr(),
-                out.data_ptr(), ws.data_ptr(), b, k, m, h * w, _stream(dev))
+                out.data_ptr(), ws.data_ptr(), b, k, m, h * w, _stream(dev), flops=2 * b * h * w * k * m)
     else:
         _launch(kind, 4 * b * h * w * (k + m), "grr_conv1x1", x.data_ptr(), weight.data_ptr(),
-                out.data_ptr(), b, k, m, h * w, _stream(dev))
+                out.data_ptr(), b, k, m, h * w, _stream(dev), flops=2 * b * h * w * k * m)
     return out
 
 
@@ -616,6 +616,11 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     out = torch.empty_like(x)
     args = (x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
             out.data_ptr(), ws.data_ptr(), b, c, hid, h, w, _stream(dev))
+    if _native.load().grr_lnb_fused(c, hid):
+        # one fused pass (lnb_fused16_kernel): x in (its halo and the skip read once), out written; the
+        # gated activation stays on chip
+        _launch("lnb_fused", 4 * b * h * w * 2 * c, "grr_lnb_forward", *args, flops=lnb_flops(b * h * w, c, c, hid))
+        return out
     if _lnb_split(c):
         _lnb_timed_parts("grr_lnb_forward", args, b * h * w, c, c, hid, c)
         return out
@@ -645,10 +650,14 @@ def lnb_forward_keep(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tenso
     out = torch.empty_like(x)
     args = (x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
             out.data_ptr(), ws.data_ptr(), b, c, hid, h, w, _stream(dev))
-    if _lnb_split(c):
-        _lnb_timed_parts("grr_lnb_forward", args, b * h * w, c, c, hid, c)
+    if _native.load().grr_lnb_fused(c, hid):
+        # the fused pass also stores g (fp32) at the workspace's start: x in, out and g written
+        _launch("lnb_fused", 4 * b * h * w * (2 * c + hid), "grr_lnb_forward_keep", *args,
+                flops=lnb_flops(b * h * w, c, c, hid))
+    elif _lnb_split(c):
+        _lnb_timed_parts("grr_lnb_forward_keep", args, b * h * w, c, c, hid, c)
     else:
-        _launch("lnb", 4 * b * h * w * (3 * c + 2 * hid), "grr_lnb_forward", *args,
+        _launch("lnb", 4 * b * h * w * (3 * c + 2 * hid), "grr_lnb_forward_keep", *args,
                 flops=lnb_flops(b * h * w, c, c, hid))
     return out, ws[:b * hid * h * w].view(b, hid, h, w)
 

@@ -304,6 +304,19 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
                            const float* w2, const float* skip, float* out, void* workspace,
                            int B, int C, int hid, int H, int W, void* stream);
 
+/* grr_lnb_forward that also leaves the gated activation g = sigmoid(m) m v [B, hid, H, W] (fp32) at the
+ * start of the workspace, for the training reverse's W2 weight gradient (the eager LocalNonLinearBlock
+ * forward keeps it instead of recomputing the depthwise + gate).  C <= 128. */
+grr_status grr_lnb_forward_keep(const float* x, const float* ln_w, const float* w1, const float* wdw,
+                                const float* w2, const float* skip, float* out, void* workspace, int B, int C,
+                                int hid, int H, int W, void* stream);
+/* 1 when grr_lnb_forward runs the block as one fused pass for these sizes (C <= 96: LN, W1, depthwise,
+ * gate and W2 in one kernel, the gated activation kept on chip).  Phase mask 2 of grr_lnb_set_phases then
+ * launches the whole block and mask 4 nothing. */
+int grr_lnb_fused(int C, int hid);
+/* Measurement knob (process-wide): 0 runs C <= 96 blocks on the two-kernel head + mix path instead of
+ * the fused pass (same results to fp32 rounding); 1 (default) fused. */
+grr_status grr_lnb_set_fused(int enable);
 /* grr_lnb_forward for an input x [B, R*Cs, H, W] that is R stacked copies of src [B, Cs, H, W]
  * (the first feature block of MultiScaleGraphFilter, whose input replicates RGB over the graphs,
  * REF13:918-921): LN statistics and W1 are evaluated on src with W1 diag(ln_w) folded over the

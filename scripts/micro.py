@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--graphs", type=int, default=32)
     ap.add_argument("--fts", type=int, default=3)
     ap.add_argument("--split", action="store_true", help="LNB: time the head and the mix apart")
+    ap.add_argument("--lnb-fused", type=int, default=1, choices=[0, 1],
+                    help="LNB, C <= 96: 1 the fused pass, 0 the head + mix kernels (grr_lnb_set_fused)")
+    ap.add_argument("--hid", type=int, default=256, help="LNB hidden width")
     ap.add_argument("--mode", type=int, default=0, help="term: 0 GLR, 1 pair Laplacian, 2 prox")
     ap.add_argument("--width", type=int, default=0, help="image width (default: --size)")
     ap.add_argument("--acc", type=int, default=0, choices=[0, 1, 2],
@@ -33,6 +36,8 @@ def main():
                          "2 the term pass + the stencil x-gradient pass")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
+    from irdu_amd._native import call
+    call("grr_lnb_set_fused", args.lnb_fused)
     dev = torch.device("cuda", 0)
     b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.width or args.size
     c = g * f
@@ -67,7 +72,7 @@ def main():
         cg1 = torch.rand(b, g, 2, h // 2, w // 2, device=dev)
         fn = lambda: K.system_half(xd, wl1, cg1, sl, sg, p(mix.muys01), p(mix.ro01), g)  # noqa: E731
     elif args.kernel == "lnb":
-        blk = irdu_amd.LocalNonLinearBlock(c, 256, 1).to(dev)
+        blk = irdu_amd.LocalNonLinearBlock(c, args.hid, 1).to(dev)
         fn = lambda: blk(x)  # noqa: E731
     elif args.kernel == "lnb_rep":   # first block of the image filter: RGB replicated over the graphs
         blk = irdu_amd.LocalNonLinearBlock(c, 256, 1).to(dev)

@@ -28,6 +28,8 @@ int main() {
   void* s = nullptr;
   EXPECT_ERR(grr_set_kernel_variant(7));
   EXPECT_ERR(grr_bwd_set_term_rows(5));
+  EXPECT_ERR(grr_lnb_set_fused(2));
+  EXPECT_ERR(grr_lnb_forward_keep(n, n, n, n, n, n, n, n, 1, 8, 16, 8, 8, s));
   EXPECT_ERR(grr_stream_copy(n, n, 3, s));
   EXPECT_ERR(grr_neighbor_table(nullptr, 0, 4, s));
   EXPECT_ERR(grr_edge_weights(n, 0, n, n, n, 1, 1, 1, 8, 8, s));

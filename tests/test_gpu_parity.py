@@ -339,6 +339,59 @@ def test_local_nonlinear_block(irdu, chw):
     assert_close(got, ref)
 
 
+def _lnb_gate64(x64, p64):
+    """The block's gated activation sigmoid(m) m v in float64 (the oracle's op sequence)."""
+    n = O.custom_layer_norm(x64, p64, "norm.", 1)
+    h = torch.nn.functional.conv2d(n, p64["local_linear.channels_linear_op.weight"])
+    hp = torch.nn.functional.pad(h, (1, 1, 1, 1), mode="replicate")
+    h = torch.nn.functional.conv2d(hp, p64["local_linear.channels_local_linear_op.weight"], groups=h.shape[1])
+    m, v = h.chunk(2, dim=1)
+    return torch.sigmoid(m) * m * v
+
+
+# C <= 96: the whole block in one fused pass (lnb_fused16_kernel: GEMM1 / depthwise / gate / GEMM2 with the
+# gated activation on chip).  Against float64 with fp32-class error: every k-step count (C = 6 ... 96),
+# hid not a multiple of 16 (a partial last chunk), tiles past the image's right / bottom edge, one-row and
+# one-column images, and a chunk-to-chunk magnitude ramp of the gated values (later chunks up to 2^12 x
+# larger: the consumer's running exponent has to scale its accumulators down) plus gray pixels (equal
+# channels: the large-|x / sigma| exponent correction of GEMM1's operand).
+@pytest.mark.parametrize("c_hid_hw", [(96, 256, (40, 36)), (48, 96, (33, 70)), (6, 20, (5, 4)), (33, 40, (9, 44)),
+                                      (96, 48, (1, 97)), (80, 64, (17, 1)), (64, 256, (8, 32)), (24, 64, (13, 30))])
+@pytest.mark.parametrize("ramp", [False, True])
+def test_fused_lnb_fp32_accurate(irdu, c_hid_hw, ramp):
+    c, hid, (h, w) = c_hid_hw
+    assert irdu._native.load().grr_lnb_fused(c, hid) == 1
+    torch.manual_seed(11)
+    blk = irdu.LocalNonLinearBlock(c, hid, 1)
+    with torch.no_grad():
+        blk.skip_weight.copy_(torch.tensor([0.7, 1.4]))
+        blk.norm.weighted_transform.weight.mul_(1.0 + 0.2 * torch.randn_like(blk.norm.weighted_transform.weight))
+        if ramp:
+            w1 = blk.local_linear.channels_linear_op.weight
+            scale = torch.pow(2.0, torch.arange(hid, dtype=torch.float32) // 16 * 1.5).clamp(max=4096.0)
+            w1[:hid] *= scale.view(-1, 1, 1, 1)
+            w1[hid:] *= scale.view(-1, 1, 1, 1)
+    x = rand(2, c, h, w, seed=41, scale=2.0, offset=-0.3)
+    if ramp:
+        x[:, :, : max(1, h // 2)] = x[:, :1, : max(1, h // 2)]       # gray rows
+    p64 = {k: v.double() for k, v in sd_cpu(blk).items()}
+    ref64 = O.local_nonlinear_block(x.double(), p64, "")
+    err32 = rel_err(O.local_nonlinear_block(x, sd_cpu(blk), ""), ref64)
+    with torch.no_grad():
+        got = blk.to(DEV)(x.to(DEV))
+    err = rel_err(got, ref64)
+    assert err <= 4 * err32 + 1e-6, (err, err32)
+    # the training forward's kept gate (grr_lnb_forward_keep): the same pass also stores g
+    ll = blk.local_linear
+    with torch.no_grad():
+        out_k, gate = irdu.kernels.lnb_forward_keep(
+            x.to(DEV), blk.norm.weighted_transform.weight.view(c), ll.channels_linear_op.weight.view(2 * hid, c),
+            ll.channels_local_linear_op.weight.view(2 * hid, 9), ll.project_out.weight.view(c, hid), blk.skip_weight)
+    assert torch.equal(out_k, got)
+    g64 = _lnb_gate64(x.double(), {k[len(""):]: v for k, v in p64.items()})
+    assert rel_err(gate, g64) <= 1e-5, rel_err(gate, g64)
+
+
 # ---------------------------------------------------------------------------
 # full solver against the reference's golden vectors
 @pytest.mark.parametrize("name", ["mixture_v1.npz", "mixture_v1_rect.npz"])
