@@ -112,7 +112,7 @@ def load_traffic(kernel, batch):
 def load_traffic_file(name, kernel_prefix, batch):
     """Per-launch HBM bytes (mean over the bench's launches of that kernel): the newest round's summary
     under profiles/ of this workload."""
-    for rnd in ("r04", "r03"):
+    for rnd in ("r05", "r04", "r03"):
         t = _traffic(os.path.join(ROOT, "profiles", rnd, name), kernel_prefix, batch)
         if t is not None:
             return t

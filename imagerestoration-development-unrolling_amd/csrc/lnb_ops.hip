@@ -1153,6 +1153,31 @@ __device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint3
 #ifndef GRR_FUSED_DIAG
 #define GRR_FUSED_DIAG 0
 #endif
+// GRR_FUSED_STAMP=1: diagnostic build -- each wave sums s_memtime deltas of its phases (producer: DMA issue,
+// x prologue, GEMM1, h stores, wait, barrier; consumer: DMA issue, gate, GEMM2, epilogue, wait, barrier)
+// into g_fused_stamps[workgroup][wave][phase] (grr_lnb_fused_stamps copies them out)
+#ifndef GRR_FUSED_STAMP
+#define GRR_FUSED_STAMP 0
+#endif
+#if GRR_FUSED_STAMP
+__device__ unsigned long long g_fused_stamps[1024 * 8 * 8];
+#define FSTAMP(k)                                              \
+  do {                                                         \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_prev;                                 \
+    st_prev = t_;                                              \
+  } while (0)
+#else
+#define FSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+#ifndef GRR_FUSED_AHEAD   // pairs of taps + windows in flight ahead of the consumer's gate (1 or 2)
+#define GRR_FUSED_AHEAD 1
+#endif
+#ifndef GRR_FUSED_PRO_SERIAL   // 1: the producer's tile prologue loads one halo block at a time
+#define GRR_FUSED_PRO_SERIAL 0
+#endif
 #ifndef GRR_FUSED_PRIO   // consumer waves' static priority (A/B: 0 -> 1 took 3 % off at 256^2 and 128^2)
 #define GRR_FUSED_PRIO 1
 #endif
@@ -1204,6 +1229,17 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
     dsl = dsl == LF_NSLOT - 1 ? 0 : dsl + 1;
   };
   if (nsteps == 0) return;   // workgroup-uniform: no barrier is left waiting
+#if GRR_FUSED_STAMP
+  unsigned long long st_acc[8] = {}, st_prev = __builtin_amdgcn_s_memtime();
+  auto stamp_out = [&]() {
+    if (lane < 8 && blockIdx.x < 1024) {
+      unsigned long long v = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v = lane == k ? st_acc[k] : v;
+      g_fused_stamps[(blockIdx.x * 8 + wave) * 8 + lane] = v;
+    }
+  };
+#endif
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1220,6 +1256,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
     for (int i = 0; i <= nsteps; ++i) {
       issue(dsl, dch);                             // slot of step i + 1 last served step i - 2 (steps i - 2, i - 1)
       advance_dma();
+      FSTAMP(0);
       if (i < nsteps && !(GRR_FUSED_DIAG & 2)) {
         if (c == 0) {
           // the tile's halo pixels: raw x, LayerNorm statistics (REF:916-922), x / sigma split in fp16 terms
@@ -1289,12 +1326,14 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
               xh[k][s] = __builtin_bit_cast(f16x8, u32x4{hw[0], hw[1], hw[2], hw[3]});
               xl[k][s] = __builtin_bit_cast(f16x8, u32x4{lw[0], lw[1], lw[2], lw[3]});
             }
-            // one block's raw x (8 KS floats per lane) at a time: the scheduler would issue every block's
-            // loads up front, and the raw values + the split blocks exceed the register file
+#if GRR_FUSED_PRO_SERIAL
+            // one block's raw x (8 KS floats per lane) at a time
             __builtin_amdgcn_sched_barrier(0);
+#endif
           }
           wave_corr = __builtin_amdgcn_readfirstlane((int)__any(any_corr)) != 0;
         }
+        FSTAMP(1);
         const float* slot = ring + sl * SLOTF + lane * 4;
         f32x16 acc[NBW];
 #pragma unroll
@@ -1323,6 +1362,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        FSTAMP(2);
         float* hb = smem + (i & 1) * LF_HBUF;
 #pragma unroll
         for (int k = 0; k < NBW; ++k) {
@@ -1342,11 +1382,17 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
         }
         sl = sl == LF_NSLOT - 1 ? 0 : sl + 1;
       }
+      FSTAMP(3);
       // step i + 1's chunk landed (this wave's DMAs), h(i) written; then every wave's
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      FSTAMP(4);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      FSTAMP(5);
     }
+#if GRR_FUSED_STAMP
+    stamp_out();
+#endif
     return;
   }
 
@@ -1362,6 +1408,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
   for (int i = 0; i <= nsteps; ++i) {
     issue(dsl, dch);
     advance_dma();
+    FSTAMP(0);
     if (i >= 1 && !(GRR_FUSED_DIAG & 1)) {
       const int st = i - 1;
       if (ch == 0) {
@@ -1502,11 +1549,21 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
         for (int u = 0; u < 12; ++u) w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
       };
       load(0, tA, wA);
+#if GRR_FUSED_AHEAD == 2
+      float tN[18];
+      f32x2 wN[12];
+      load(1, tN, wN);
+#endif
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         float tB[18];
         f32x2 wB[12];
+#if GRR_FUSED_AHEAD == 2
+        // two pairs in flight: pair jj + 2 issued, pair jj + 1 (tN, wN) landing, pair jj computed
+        if (jj < 6) load(jj + 2, tB, wB);
+#else
         if (jj < 7) load(jj + 1, tB, wB);
+#endif
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           float m = tA[0] * wA[3 * rb][0], v = tA[1] * wA[3 * rb][1];
@@ -1519,14 +1576,30 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
           // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
           g[rb][jj] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
         }
+#if GRR_FUSED_AHEAD == 2
+        if (jj < 7) {
+#pragma unroll
+          for (int u = 0; u < 18; ++u) tA[u] = tN[u];
+#pragma unroll
+          for (int u = 0; u < 12; ++u) wA[u] = wN[u];
+        }
+        if (jj < 6) {
+#pragma unroll
+          for (int u = 0; u < 18; ++u) tN[u] = tB[u];
+#pragma unroll
+          for (int u = 0; u < 12; ++u) wN[u] = wB[u];
+        }
+#else
         if (jj < 7) {
 #pragma unroll
           for (int u = 0; u < 18; ++u) tA[u] = tB[u];
 #pragma unroll
           for (int u = 0; u < 12; ++u) wA[u] = wB[u];
         }
+#endif
         __builtin_amdgcn_sched_barrier(0);
       }
+      FSTAMP(1);
       if (a.g) {   // kept gate (training): the unscaled fp32 values, [B, hid, H, W]
         float* gb = a.g + (int64_t)T.b * hid * HW;
 #pragma unroll
@@ -1581,6 +1654,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
         }
       }
 #endif
+      FSTAMP(2);
       if (ch == nch - 1) {
         // epilogue (REF:962-964): out[m, p] = skip0 x[m, p] + skip1 2^-E_p r2[m] acc; accumulator block rb
         // holds output row 2 cw + rb, column lane % 32, rows m = 32 t + (i & 3) + 8 (i >> 2) + 4 kh
@@ -1599,33 +1673,43 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
 #else
         const int Eb[2] = {E[0], E[1]};
 #endif
+        // the W2 row scales and 2^-E into the accumulators first, then every skip operand of both rows in one
+        // round of loads (the gate's registers are dead here: acc2 + 2 MT x 16 fit), then the stores
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const float sc = s1 * ldexpf(1.0f, Eb[rb] == 1000 ? 0 : -Eb[rb]);
-          const int yy = T.y0 + 2 * cw + rb;
-          const bool ok = yy < H && gxo < W;
-          const uint32_t vx = (uint32_t)(4 * kh * HW + min(yy, H - 1) * W + min(gxo, W - 1)) * 4u;
-          const uint32_t vo = ok ? vx : 0x80000000u;
 #pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            int hw4 = HW * 4;                      // (not hoisted: see the producer's x loads)
-            asm volatile("" : "+s"(hw4));
-            float xv[16];
+          for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc2[rb][t][u] *= sc * r2s[32 * t + (u & 3) + 8 * (u >> 2) + 4 * kh];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        int hw4 = HW * 4;                          // (not hoisted: see the producer's x loads)
+        asm volatile("" : "+s"(hw4));
+        uint32_t vx[2], vo[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int yy = T.y0 + 2 * cw + rb;
+          vx[rb] = (uint32_t)(4 * kh * HW + min(yy, H - 1) * W + min(gxo, W - 1)) * 4u;
+          vo[rb] = yy < H && gxo < W ? vx[rb] : 0x80000000u;
+        }
+        float xv[2][MT][16];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
 #pragma unroll
             for (int u = 0; u < 16; ++u)
-              xv[u] = __uint_as_float(
-                  __builtin_amdgcn_raw_buffer_load_b32(xrs, vx, (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0));
+              xv[rb][t][u] = __uint_as_float(
+                  __builtin_amdgcn_raw_buffer_load_b32(xrs, vx[rb], (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0));
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              const float r2 = r2s[32 * t + (u & 3) + 8 * (u >> 2) + 4 * kh];
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[u] + sc * (acc2[rb][t][u] * r2)), ors, vo,
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[rb][t][u] + acc2[rb][t][u]), ors, vo[rb],
                                                     (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0);
-            }
-            // one row tile's skip operands at a time (the scheduler would load all of them up front: 2 x MT
-            // x 16 more live registers, the kernel's peak)
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
       }
       if (++ch == nch) {
         ch = 0;
@@ -1633,11 +1717,24 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
       }
       csl = csl == LF_NSLOT - 1 ? 0 : csl + 1;
     }
+    FSTAMP(3);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    FSTAMP(4);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    FSTAMP(5);
   }
+#if GRR_FUSED_STAMP
+  stamp_out();
+#endif
 }
+
+#if GRR_FUSED_STAMP
+extern "C" int grr_lnb_fused_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_stamps), sizeof(unsigned long long) * std::min(n, 1024 * 64),
+                             0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // mix: out = skip0 x + skip1 W2 g

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--lnb-fused", type=int, default=1, choices=[0, 1],
                     help="LNB, C <= 96: 1 the fused pass, 0 the head + mix kernels (grr_lnb_set_fused)")
     ap.add_argument("--hid", type=int, default=256, help="LNB hidden width")
+    ap.add_argument("--stamps", action="store_true",
+                    help="LNB fused, GRR_FUSED_STAMP build: print the per-phase s_memtime sums of each wave role")
     ap.add_argument("--mode", type=int, default=0, help="term: 0 GLR, 1 pair Laplacian, 2 prox")
     ap.add_argument("--width", type=int, default=0, help="image width (default: --size)")
     ap.add_argument("--acc", type=int, default=0, choices=[0, 1, 2],
@@ -132,6 +134,22 @@ def main():
         for kind, v in timer.summary().items():
             print(f"{args.kernel}: {kind:16s} launches={v['launches']} mean={v['mean_ms']:.4f} ms "
                   f"algo={v['gbps']:.1f} GB/s bytes/launch={v['bytes_per_launch']:.4e}")
+    if args.stamps:
+        import ctypes
+        import numpy as np
+        lib = irdu_amd.load_native()
+        buf = (ctypes.c_ulonglong * (1024 * 64))()
+        assert lib.grr_lnb_fused_stamps(buf, 1024 * 64) == 0
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8, 8).astype(np.float64)
+        nwg = int((a.sum(axis=(1, 2)) > 0).sum())
+        a = a[:nwg]
+        prod = ["dma", "prologue", "gemm1", "h_store", "wait", "barrier"]
+        cons = ["dma", "gate", "gemm2", "epilogue", "wait", "barrier"]
+        for name, waves, labels in (("producer", slice(0, 4), prod), ("consumer", slice(4, 8), cons)):
+            m = a[:, waves, :6].mean(axis=(0, 1))
+            tot = m.sum()
+            print(f"stamps {name} ({nwg} workgroups, cycles per wave per launch): total {tot:.0f} " +
+                  " ".join(f"{l}={v:.0f} ({v / tot:.0%})" for l, v in zip(labels, m)))
 
 
 if __name__ == "__main__":
