@@ -28,6 +28,7 @@
 //   0 centre (0,0), 1 up (-1,0), 2 left (0,-1), 3 right (0,+1), 4 down (+1,0).
 // Edge order (REF:42-53): 0 up, 1 left, 2 right, 3 down; opposite(e) = 3 - e.
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "grr_common.h"
@@ -935,7 +936,9 @@ __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
 // gw written once per launch (the per-pixel kernel re-reads every operand 5-25 times from
 // L1/L2 and runs at ≈ 1.7 TB/s).
 // ---------------------------------------------------------------------------
-int g_term_rows = 1;   // grr_bwd_set_term_rows: 0 = per-pixel term reverses (A/B and tests)
+// grr_bwd_set_term_rows: 0 = per-pixel term reverses, 1 = the register-prefetch row kernel, 2 (default) = the
+// LDS-ring row kernel where it applies (A/B and tests)
+int g_term_rows = 2;
 
 template <int V> struct RowT;
 template <> struct RowT<1> { typedef float T; };
@@ -999,14 +1002,57 @@ __device__ __forceinline__ void dma_dword(const float* src, float* lds_wave_base
 // padj2) runs in the kernel one row behind v: v rows go to an LDS ring (P* reaches one row and one
 // column), gx rows come one row ahead by LDS-DMA, and each segment computes v for the rows either side
 // of it (their weight-gradient partials and reductions are not taken).
-template <int MODE, int V, bool STRIPS = false, bool PADJ = false>
-__global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
+//
+// RING (round 5): every operand row reaches the channel waves through an LDS ring filled by one extra
+// producer wave (wave F) with 16-byte LDS-DMA, ring_d - 1 steps ahead: per step the x and g rows of the
+// F channels, the graph's WPL weight rows and the WPL gw rows of the read-modify-write.  The channel
+// waves issue no loads in the row loop (no prefetch registers, no load latency on their path): the
+// register-prefetch kernel was latency-bound (one row of prefetch; waves waiting 59 % of their cycles,
+// sq_term_row_512.json).  Each step has exactly one barrier (the partials'), which the producer joins:
+// it waits (counted vmcnt) until the next step's rows have landed, passes the barrier, then refills the
+// slot the previous step read.  Column strips (W > 64 V) start on 16-byte boundaries: 64 V - 8 owned
+// columns, 4 halo columns per side.  Same arithmetic, same order: results equal the non-ring kernel's.
+constexpr int kRingRows(int V) { return 4 / V; }   // rows one 64-lane 16-byte DMA moves
+// scalar base + a loop-invariant per-lane byte offset: the VGPR operand is never rewritten while DMAs that
+// read it are in flight (a rewritten address VGPR drew compiler vmcnt(0) waits inside the issue loop)
+__device__ __forceinline__ void dma_row16(const float* sbase, uint32_t voff, float* lds_dst) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)lds_dst;
+  asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
+               : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (the immediate is 6 bits)
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+#define GRR_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    GRR_VMW(0) GRR_VMW(1) GRR_VMW(2) GRR_VMW(3) GRR_VMW(4) GRR_VMW(5) GRR_VMW(6) GRR_VMW(7) GRR_VMW(8)
+    GRR_VMW(9) GRR_VMW(10) GRR_VMW(11) GRR_VMW(12) GRR_VMW(13) GRR_VMW(14) GRR_VMW(15) GRR_VMW(16)
+    GRR_VMW(17) GRR_VMW(18) GRR_VMW(19) GRR_VMW(20) GRR_VMW(21) GRR_VMW(22) GRR_VMW(23) GRR_VMW(24)
+    GRR_VMW(25) GRR_VMW(26) GRR_VMW(27) GRR_VMW(28) GRR_VMW(29) GRR_VMW(30) GRR_VMW(31) GRR_VMW(32)
+    GRR_VMW(33) GRR_VMW(34) GRR_VMW(35) GRR_VMW(36) GRR_VMW(37) GRR_VMW(38) GRR_VMW(39) GRR_VMW(40)
+    GRR_VMW(41) GRR_VMW(42) GRR_VMW(43) GRR_VMW(44) GRR_VMW(45) GRR_VMW(46) GRR_VMW(47) GRR_VMW(48)
+    GRR_VMW(49) GRR_VMW(50) GRR_VMW(51) GRR_VMW(52) GRR_VMW(53) GRR_VMW(54) GRR_VMW(55) GRR_VMW(56)
+    GRR_VMW(57) GRR_VMW(58) GRR_VMW(59) GRR_VMW(60) GRR_VMW(61) GRR_VMW(62)
+#undef GRR_VMW
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+}
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// channel waves per workgroup of the ring kernel: F + 1 <= 8 waves for V = 4 (two per SIMD: 256 VGPRs),
+// <= 13 for V <= 2 (128 VGPRs)
+template <int V> struct TermRingMax { static constexpr int F = V == 4 ? 7 : 12; };
+template <int MODE, int V, bool STRIPS = false, bool PADJ = false, bool RING = false>
+__global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowMax<V>::F) void term_row_kernel(
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
     float* __restrict__ v_out, float* __restrict__ gx_out, float* __restrict__ gw, Red ggam, Red gdot,
-    Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk) {
+    Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk, int ring_d) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
-  constexpr bool kGwDma = term_gw_dma(MODE, V, STRIPS);
+  constexpr bool kGwDma = !RING && term_gw_dma(MODE, V, STRIPS);
+  static_assert(!(RING && PADJ), "the ring kernel has no x-gradient pass");
   // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats),
   // then (GRR_TERM_GW_DMA) the gw row ring [row parity][plane][element j][lane] (2 WPL 64 V floats)
   extern __shared__ __attribute__((aligned(16))) float part_dyn[];
@@ -1021,8 +1067,10 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   uint32_t unit = xcd_remap(blockIdx.x, nblk);
   // W > 64 V: column strips owning 62 V columns with V halo columns per side (the term's reach is two
   // columns: s = P x and a = T* g at the pixel's neighbours), as the depthwise row kernels
-  // (a separate instance, so that the one-strip kernel keeps its registers)
-  constexpr int STEP = 62 * V;
+  // (a separate instance, so that the one-strip kernel keeps its registers).  RING: 64 V - 8 owned
+  // columns, 4 halo columns per side (16-byte aligned DMA chunks)
+  constexpr int STEP = RING ? 64 * V - 8 : 62 * V;
+  constexpr int HALO = RING ? 4 : V;
   int strip = 0, nstrips = 1;
   if constexpr (STRIPS) {
     nstrips = (W + STEP - 1) / STEP;
@@ -1037,14 +1085,90 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   int c0 = lc0;                              // global column
   bool on = c0 < W;
   int cl0 = on ? c0 : W - V;
+  int x0 = 0;                                // the strip's first column
   if constexpr (STRIPS) {
-    const int x0 = strip == 0 ? 0 : strip * STEP - V;
+    x0 = strip == 0 ? 0 : strip * STEP - HALO;
     const int lo = strip * STEP, hi = min(lo + STEP, W);
     c0 = x0 + lc0;
     on = c0 >= lo && c0 < hi;
     cl0 = clampi(c0, 0, W - V);
   }
   const int64_t HW = (int64_t)H * W;
+  // RING: rows per ring slot (x, g of the F channels, WPL weight rows, WPL gw rows; padded to whole DMAs)
+  const int ring_fx = (F + kRingRows(V) - 1) / kRingRows(V) * kRingRows(V);     // x, g block rows
+  const int ring_wx = (WPL + kRingRows(V) - 1) / kRingRows(V) * kRingRows(V);   // w, gw block rows
+  const int ring_rows = 2 * (ring_fx + ring_wx);
+  float* const ring = part_dyn + 2 * F * WPL * (64 * V);
+  auto rslot = [&](int sl) { return ring + sl * ring_rows * (64 * V); };
+  const int t0 = rs - 1, te = re + 1;        // the row loop's steps (output row t - 2)
+  if constexpr (RING) {
+    if (f == F) {   // producer: the operand rows of step t into slot (t - t0) mod ring_d
+      // The slot's rows come in four blocks (x, g: F rows each; w, gw: WPL rows each), each padded to
+      // whole DMAs of RPD = 4 / V rows (16 V lanes per row): DMA q of a block moves its rows q RPD ..
+      // q RPD + RPD - 1, the lane row sub's 16-byte chunk ck.  Scalar base: the block's plane q RPD at
+      // the step's row; per-lane offset: plane sub and the column (the last DMA of a block clamps the
+      // plane: padding rows repeat the block's last row).  The w block's plane 0 (MODE 0 / 2) is the
+      // row t - 1 one: its own scalar row at V = 4, one row down in the lane offset at V < 4.
+      constexpr int RPD = kRingRows(V);
+      const int sub = lane / (16 * V), ck = lane % (16 * V);
+      const int col = min(x0 + 4 * ck, W - 4);
+      const int nfx = (F + RPD - 1) / RPD, nfw = (WPL + RPD - 1) / RPD;
+      auto lane_off = [&](int q, int np) {
+        return (uint32_t)(((min(q * RPD + sub, np - 1) - q * RPD) * HW + col) * 4);
+      };
+      const uint32_t vo_main = (uint32_t)((sub * HW + col) * 4);
+      const uint32_t vo_lastf = lane_off(nfx - 1, F), vo_lastw = lane_off(nfw - 1, WPL);
+      constexpr bool kLag1 = MODE != 1;
+      // V < 4: the DMA holding plane 0 reads row clamp(t - 2) + delta at lane row 0, delta = clamp(t - 1) -
+      // clamp(t - 2) in {0, 1} (uniform per step: one of two loop-invariant offsets)
+      const uint32_t vo_w0 = nfw == 1 ? vo_lastw : vo_main;
+      const uint32_t vo_w0d = vo_w0 + ((V < 4 && kLag1 && sub == 0) ? (uint32_t)W * 4u : 0u);
+      const float* const xb = x + (int64_t)bg * F * HW;
+      const float* const gb = g + (int64_t)bg * F * HW;
+      const float* const wb0 = w + (int64_t)bg * WPL * HW;
+      const float* const gwb0 = gw + (int64_t)bg * WPL * HW;
+      const int64_t qstep = (int64_t)RPD * HW;   // floats between consecutive DMAs of a block
+      auto issue = [&](int t, int sl) {
+        float* dst = rslot(sl);
+        constexpr int DS = RPD * (64 * V);
+        const int64_t ro0 = (int64_t)clampi(t, 0, H - 1) * W, ro2 = (int64_t)clampi(t - 2, 0, H - 1) * W;
+        // x, g: rows t
+        for (int q = 0; q < nfx - 1; ++q, dst += DS) dma_row16(xb + q * qstep + ro0, vo_main, dst);
+        dma_row16(xb + (nfx - 1) * qstep + ro0, vo_lastf, dst);
+        dst += DS;
+        for (int q = 0; q < nfx - 1; ++q, dst += DS) dma_row16(gb + q * qstep + ro0, vo_main, dst);
+        dma_row16(gb + (nfx - 1) * qstep + ro0, vo_lastf, dst);
+        dst += DS;
+        // w: rows t - 2 (plane 0 of MODE 0 / 2: t - 1)
+        const int64_t ro_w0 = (V == 4 && kLag1) ? (int64_t)clampi(t - 1, 0, H - 1) * W : ro2;
+        if (V < 4 && kLag1 && clampi(t - 1, 0, H - 1) != clampi(t - 2, 0, H - 1)) dma_row16(wb0 + ro_w0, vo_w0d, dst);
+        else dma_row16(wb0 + ro_w0, vo_w0, dst);
+        dst += DS;
+        for (int q = 1; q < nfw - 1; ++q, dst += DS) dma_row16(wb0 + q * qstep + ro2, vo_main, dst);
+        if (nfw > 1) {
+          dma_row16(wb0 + (nfw - 1) * qstep + ro2, vo_lastw, dst);
+          dst += DS;
+        }
+        // gw: rows t - 2
+        for (int q = 0; q < nfw - 1; ++q, dst += DS) dma_row16(gwb0 + q * qstep + ro2, vo_main, dst);
+        dma_row16(gwb0 + (nfw - 1) * qstep + ro2, vo_lastw, dst);
+      };
+      const int ndma = 2 * nfx + 2 * nfw;
+      const int D = ring_d;
+      for (int k = 0; k < D - 1; ++k) issue(t0 + k, k);
+      vm_wait_rt(ndma * (D - 2));   // step t0's rows landed
+      ring_barrier();
+      int sl = D - 1;
+      for (int t = t0; t <= te; ++t) {
+        vm_wait_rt(ndma * (D - 3));   // step t + 1's rows landed
+        ring_barrier();               // (the partials' barrier of step t)
+        issue(t + D - 1, sl);         // the slot step t - 1 read
+        sl = sl + 1 == D ? 0 : sl + 1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
   const float sc = scale ? scale[gi] : 1.f;
   const float gm = MODE == 2 ? expf(log_gamma[gi]) : 0.f;
   float k[5];
@@ -1089,7 +1213,6 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
   };
   // prefetched operands of the next step
   float NX[V], NG[V], NW0[V], NW3[V], NW1[V], NW2[V];
-  const int t0 = rs - 1;
   auto prefetch = [&](int t) {   // step t: x, g row t; weights of output row t - 2 (plane 0 row t - 1)
     xrow(NX, t);
     grow(NG, t);
@@ -1157,9 +1280,32 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
 #pragma unroll
     for (int j = 0; j < V; ++j) dma_dword(gxp + (int64_t)q * W + j, oring(q) + j * 64);
   };
-  prefetch(t0);
+  if constexpr (RING) ring_barrier();   // step t0's rows have landed
+  else prefetch(t0);
   int par = 0;
-  for (int t = t0; t <= re + 1; ++t) {
+  int sl = 0;   // (RING) this step's ring slot
+  for (int t = t0; t <= te; ++t) {
+    const float* const slot_lane = rslot(sl) + lc0;
+    if constexpr (RING) {
+      sl = sl + 1 == ring_d ? 0 : sl + 1;
+      rload<V>(NX, slot_lane + f * (64 * V));
+      if (t >= 0 && t < H) {
+        rload<V>(NG, slot_lane + (ring_fx + f) * (64 * V));
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) NG[j] = 0.f;
+      }
+      const float* const wr = slot_lane + 2 * ring_fx * (64 * V);
+      if constexpr (MODE == 1) {
+        rload<V>(NW0, wr);
+        rload<V>(NW3, wr + 64 * V);
+      } else {
+        rload<V>(NW0, wr);
+        rload<V>(NW1, wr + 64 * V);
+        rload<V>(NW2, wr + 2 * (64 * V));
+        rload<V>(NW3, wr + 3 * (64 * V));
+      }
+    }
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       X[0][j] = X[1][j]; X[1][j] = X[2][j]; X[2][j] = X[3][j]; X[3][j] = NX[j];
@@ -1173,7 +1319,9 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
         W1[j] = NW1[j]; W2[j] = NW2[j];
       }
     }
-    if (t + 1 <= re + 1) prefetch(t + 1);
+    if constexpr (!RING) {
+      if (t + 1 <= re + 1) prefetch(t + 1);
+    }
     // s = P x (replicate) and a = T* g (zero frame) at row t - 1
     {
       const float xp_ = lprev(X[2][V - 1]), xn_ = lnext(X[2][0]);
@@ -1192,7 +1340,10 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       }
     }
     const int r = t - 2;
-    if (r < rs) continue;   // pipeline fill (uniform over the workgroup)
+    if (r < rs) {   // pipeline fill (uniform over the workgroup)
+      if constexpr (RING) ring_barrier();
+      continue;
+    }
     const bool own = !PADJ || (r >= r0 && r < r1);   // (PADJ) rows r0 - 1 and r1: v only
     // output row r: s, a rows r-1, r, r+1 = S[0..2]; x, g rows r-1, r, r+1 = X[0..2], Gr[0..2]
     const bool in0 = r > 0, in3 = r + 1 < H;
@@ -1301,7 +1452,8 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
     if (own) {
 #pragma unroll
       for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
-      __syncthreads();
+      if constexpr (RING) ring_barrier();
+      else __syncthreads();
     }
     if constexpr (kGwDma || PADJ) {
       // gw row r / gx row r - 1 landed: copied before this step's prefetch loads (>= 1 + WPL of them,
@@ -1324,7 +1476,9 @@ __global__ __launch_bounds__(64 * TermRowMax<V>::F) void term_row_kernel(
       if (on) {
         float* dst = gwb + e * HW + (int64_t)r * W;
         float cv[V];
-        if constexpr (kGwDma) {
+        if constexpr (RING) {
+          rload<V>(cv, slot_lane + (ring_rows - ring_wx + e) * (64 * V));
+        } else if constexpr (kGwDma) {
           const float* sl = gring(r & 1, e) + lane;
 #pragma unroll
           for (int j = 0; j < V; ++j) cv[j] = sl[j * 64];
@@ -1620,19 +1774,52 @@ size_t term_row_lds(int mode, int V, int F, bool strips, bool padj) {
   return (size_t)rows * 64 * V * sizeof(float);
 }
 constexpr size_t kTermLdsMax = 160 * 1024;
+// Shapes the ring kernel takes (g_term_rows == 2): W % 4 == 0 (16-byte DMAs), F + 1 waves within its
+// launch bound, and not the one-column lanes where it measured slower (W <= 32, and the prox term at
+// W <= 64: profiles/r05/term/ab_depth.txt)
+bool term_ring_shape_ok(int mode, int F, int W) {
+  const int V = term_strip_vec(W, mode);
+  if (g_term_rows != 2 || V == 0 || W % 4 != 0 || F > (V == 4 ? TermRingMax<4>::F : TermRingMax<1>::F)) return false;
+  return V >= 2 || (W >= 64 && mode != 2);
+}
+// The ring kernel's depth (steps of rows in LDS) where it applies, else 0: the shape (above) and 16-byte
+// aligned planes.  Depth 4 (three steps of rows ahead): deeper rings measured no faster and cost
+// workgroups per CU (GRR_TERM_RING_D overrides it for A/B).
+int term_ring_depth(int mode, int V, int F, int W, const float* x, const float* g, const float* w, const float* gw,
+                    size_t* lds_out) {
+  if (!term_ring_shape_ok(mode, F, W)) return 0;
+  const void* ptrs[] = {x, g, w, gw};
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16u != 0) return 0;
+  const int wpl = mode == 1 ? 2 : 4, rpd = 4 / V;
+  const int rows = 2 * ((F + rpd - 1) / rpd + (wpl + rpd - 1) / rpd) * rpd, ndma = rows / rpd;
+  const size_t row_b = (size_t)64 * V * sizeof(float);
+  const size_t part_b = (size_t)2 * F * wpl * row_b, slot_b = (size_t)rows * row_b;
+  static const int forced = [] {
+    const char* e = getenv("GRR_TERM_RING_D");
+    return e ? atoi(e) : 0;
+  }();
+  const int d = forced >= 4 ? forced : 4;
+  if (ndma * (d - 3) > 63 || part_b + d * slot_b > kTermLdsMax) return 0;
+  if (lds_out) *lds_out = part_b + d * slot_b;
+  return d;
+}
 template <int MODE, int V>
 grr_status launch_term_row(int B, int F, const float* x, const float* g, const float* taps, const float* w,
                            const float* lg, const float* scale, float coef, float* v, float* gx, float* gw,
                            float* ggam, float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
+  size_t ring_lds = 0;
+  const int ring_d = (g_term_rows == 2 && gx == nullptr) ? term_ring_depth(MODE, V, F, W, x, g, w, gw, &ring_lds) : 0;
   // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
   int sseg = H;
-  const int nstrips = W <= 64 * V ? 1 : (W + 62 * V - 1) / (62 * V);
+  const int step = ring_d ? 64 * V - 8 : 62 * V;   // owned columns per strip
+  const int nstrips = W <= 64 * V ? 1 : (W + step - 1) / step;
   const int64_t graphs = (int64_t)B * G * nstrips;   // (b, graph, strip) units
   while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
   const bool padj = gx != nullptr;
-  const size_t lds = term_row_lds(MODE, V, F, nstrips > 1, padj);
+  const size_t lds = ring_d ? ring_lds : term_row_lds(MODE, V, F, nstrips > 1, padj);
   // slots: one per (b, segment, strip) workgroup for the taps, one per channel wave of it for the
   // per-graph scalars
   const uint32_t wgs = (uint32_t)((int64_t)B * nsegs * nstrips);
@@ -1642,8 +1829,15 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
 #define GRR_TERM_ROW_LAUNCH(STRIPS, PADJ)                                                                   \
   hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, PADJ>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, \
                      scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg,   \
-                     nsegs, nblk)
-  if (padj) {
+                     nsegs, nblk, 0)
+#define GRR_TERM_RING_LAUNCH(STRIPS)                                                                         \
+  hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, false, true>), dim3(nblk), dim3(64 * (F + 1)), lds, s, x, g, \
+                     taps, w, lg, scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, \
+                     W, sseg, nsegs, nblk, ring_d)
+  if (ring_d) {
+    if (nstrips > 1) GRR_TERM_RING_LAUNCH(true);
+    else GRR_TERM_RING_LAUNCH(false);
+  } else if (padj) {
     if constexpr (V < 4) GRR_TERM_ROW_LAUNCH(false, true);   // term_acc_shape_ok: one strip, V <= 2
   } else if (nstrips > 1) {
     GRR_TERM_ROW_LAUNCH(true, false);
@@ -1651,6 +1845,7 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
     GRR_TERM_ROW_LAUNCH(false, false);
   }
 #undef GRR_TERM_ROW_LAUNCH
+#undef GRR_TERM_RING_LAUNCH
   st = launch_status("grr_bwd_term_fused");
   if (st != GRR_OK) return st;
   return R.rs.finish("grr_bwd_term_fused");
@@ -1928,7 +2123,7 @@ int64_t grr_scratch_bytes(void) {
 
 grr_status grr_bwd_set_term_rows(int enable) {
   clear_error();
-  GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_rows: 0 or 1");
+  GRR_REQUIRE(enable >= 0 && enable <= 2, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_rows: 0, 1 or 2");
   g_term_rows = enable;
   return GRR_OK;
 }
@@ -1971,7 +2166,12 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
 }
 
 int grr_bwd_term_acc_supported(int mode, int F, int H, int W) {
-  return mode >= 0 && mode <= 2 && F > 0 && H > 0 && W > 0 && g_term_rows && term_acc_shape_ok(mode, F, W) ? 1 : 0;
+  // the ring kernel (+ the x-gradient pass apart, or folded into the CG glue) measured faster than the
+  // register kernel with the pass inside wherever it applies
+  return mode >= 0 && mode <= 2 && F > 0 && H > 0 && W > 0 && g_term_rows && term_acc_shape_ok(mode, F, W) &&
+                 !term_ring_shape_ok(mode, F, W)
+             ? 1
+             : 0;
 }
 
 grr_status grr_bwd_term_fused_acc(int mode, const float* x, const float* g, const float* taps, const float* w,

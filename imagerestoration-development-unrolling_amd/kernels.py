@@ -121,11 +121,14 @@ NO_STENCIL = Stencil(None, None, None, None)
 TERM_ROWS = True
 
 
-def set_term_rows(enable: bool) -> None:
-    """Row-streaming (True, default) or per-pixel (False) term reverses (grr_bwd_term_fused)."""
+def set_term_rows(enable) -> None:
+    """Row-streaming (True / 2, default: the LDS-ring row kernel where the shape allows, else the
+    register-prefetch one; 1: always the register-prefetch row kernel) or per-pixel (False / 0) term
+    reverses (grr_bwd_term_fused)."""
     global TERM_ROWS
-    _native.call("grr_bwd_set_term_rows", int(bool(enable)))
-    TERM_ROWS = bool(enable)
+    level = 2 if enable is True else int(enable)
+    _native.call("grr_bwd_set_term_rows", level)
+    TERM_ROWS = level > 0
 
 
 def term_rows_ok(w: int, f: int) -> bool:

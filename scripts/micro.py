@@ -36,8 +36,11 @@ def main():
     ap.add_argument("--acc", type=int, default=0, choices=[0, 1, 2],
                     help="term: 0 the term pass, 1 with the x-gradient pass inside (grr_bwd_term_fused_acc), "
                          "2 the term pass + the stencil x-gradient pass")
+    ap.add_argument("--term-rows", type=int, default=2, choices=[0, 1, 2],
+                    help="term: 0 per-pixel, 1 register-prefetch row kernel, 2 LDS-ring row kernel (default)")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
+    K.set_term_rows(args.term_rows)
     from irdu_amd._native import call
     call("grr_lnb_set_fused", args.lnb_fused)
     dev = torch.device("cuda", 0)
