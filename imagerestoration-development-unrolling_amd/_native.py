@@ -62,6 +62,8 @@ SIGNATURES = {
     "grr_system_step": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_system_step2": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P, P, P,
                          P, P, P, I, I, I, I, I, P],
+    "grr_system_first_pair": [P, P, P, I, P, P, P, Stencil, Stencil, P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P,
+                              P, P, P, P, I, I, I, I, I, P],
     "grr_system_step2_train": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P,
                                P, P, P, P, P, I, I, I, I, I, P],
     "grr_glr_stage": [P, P, P, P, Stencil, P, P, P, P, P, I, I, I, I, I, P],

@@ -1380,6 +1380,14 @@ struct Step2Args {
   float* xd_out;
   float* x_mid;          // training: x_{k+1} and u_{k+1} (the reverse sweep's saved iterates), or NULL
   float* u_mid;
+  // first pair (graph_step2_kernel<false, false, true>): stage 0, the prox right-hand side B, stage 1
+  const float* wG0;      // raw GTV weights [B,G,4,H,W] / [B,G,4,h,w] of the prox terms
+  const float* wG1;
+  const float* log_gamma0;
+  const float* log_gamma1;
+  const float* yr;       // y of right-hand side B: [B,C,H,W], or the [B,F,H,W] image it replicates (yr_rep)
+  int yr_rep;
+  float* b_out;          // right-hand side B
   int G, F, H, nsegs, sseg;
   int W, nstrips;       // image width; column strips of S2_W lanes (1 at W = S2_W)
   int FG, ngrp;         // channel groups of <= S2_FMAX channels per (b, graph): FG channels each (the last may hold fewer)
@@ -1502,6 +1510,77 @@ struct OpPipe {
   }
 };
 
+// The GTV proximal term C^T phi_gamma(C s) of the same input rows an OpPipe streams (the first-pair
+// kernel's right-hand side B, REF:757-781): s = S_G x is the pipe's SG rows (same stencil), so this adds
+// only the prox rows o and their S_G^T.  The arithmetic of graph_row_kernel's GTV_PROX consume.
+// Weight rows of l / o row r = t-2: W4 = the four raw planes at row r, wup = plane 0 (up) at row r+1,
+// wdn = plane 3 (down) at row r-1.
+template <int V>
+struct ProxExt {
+  float O[4][V];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < V; ++j) O[k][j] = 0.f;
+  }
+  template <int P, int W, bool EDGE = true>
+  __device__ __forceinline__ void advance(const OpPipe<V>& pp, const float (&W4)[4][V], const float (&wup)[V],
+                                          const float (&wdn)[V], int t, int H, int c0, const Taps& tG, float gam,
+                                          float (&tp)[V]) {
+    constexpr int K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
+    {  // o at row r = t-2 from s rows t-3, t-2, t-1 = the pipe's SG slots K1, K2, K3
+      const int r = t - 2;
+      const bool rin = r >= 0 && r < H;
+      const float (&G0)[V] = pp.SG[K1];
+      const float (&G1)[V] = pp.SG[K2];
+      const float (&G2)[V] = pp.SG[K3];
+      const float sp = lane_prev(G1[V - 1]), sn = lane_next(G1[0]);
+      const float w1n = lane_next(W4[1][0]), w2p = lane_prev(W4[2][V - 1]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        const float sv = G1[j];
+        const float su = (!EDGE || r > 0) ? G0[j] : sv, sd = (!EDGE || r < H - 1) ? G2[j] : sv;
+        const float spv = j > 0 ? G1[j - 1] : sp, snx = j < V - 1 ? G1[j + 1] : sn;
+        const float sl = col > 0 ? spv : sv, sr = col < W - 1 ? snx : sv;
+        const float w0 = W4[0][j], w1 = W4[1][j], w2 = W4[2][j], w3 = W4[3][j];
+        const float z0 = prox_phi(w0 * sv - w0 * su, gam) * w0;
+        const float z1 = prox_phi(w1 * sv - w1 * sl, gam) * w1;
+        const float z2 = prox_phi(w2 * sv - w2 * sr, gam) * w2;
+        const float z3 = prox_phi(w3 * sv - w3 * sd, gam) * w3;
+        float ov = ((z0 + z1) + z2) + z3;
+        const float wupb = wup[j];                                   // w_up(q + down)
+        const float wlfr = j < V - 1 ? W4[1][j + 1] : w1n;           // w_left(q + right)
+        const float wrtl = j > 0 ? W4[2][j - 1] : w2p;               // w_right(q - right)
+        const float wdna = wdn[j];                                   // w_down(q - down)
+        const float o1 = ov - prox_phi(wupb * G2[j] - wupb * sv, gam) * wupb;
+        ov = (!EDGE || r < H - 1) ? o1 : ov;
+        const float o2 = ov - prox_phi(wlfr * snx - wlfr * sv, gam) * wlfr;
+        ov = col < W - 1 ? o2 : ov;
+        const float o3 = ov - prox_phi(wrtl * spv - wrtl * sv, gam) * wrtl;
+        ov = col > 0 ? o3 : ov;
+        const float o4 = ov - prox_phi(wdna * G0[j] - wdna * sv, gam) * wdna;
+        ov = (!EDGE || r > 0) ? o4 : ov;
+        O[K3][j] = (!EDGE || rin) ? ov : 0.f;
+      }
+    }
+    {  // S_G^T at row t-3 from o rows t-4, t-3, t-2 = slots K1, K2, K3
+      const float (&O0)[V] = O[K1];
+      const float (&O1)[V] = O[K2];
+      const float (&O2)[V] = O[K3];
+      const float op = lane_prev(O1[V - 1]), on = lane_next(O1[0]);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float gx = j < V - 1 ? O1[j + 1] : on, gp = j > 0 ? O1[j - 1] : op;
+        float w = tG.u * O2[j];
+        w += tG.l * gx; w += tG.c * O1[j]; w += tG.r * gp; w += tG.d * O0[j];
+        tp[j] = w;
+      }
+    }
+  }
+};
+
 constexpr int S2_W = 256, S2_HW = 128;    // full / half row width
 constexpr int S2_WP = 7;                   // weight-ring row pairs
 constexpr int S2_HR = 4;                   // half-weight ring rows
@@ -1525,6 +1604,16 @@ constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipe
 constexpr int S2_AHEAD = GRR_STEP2_AHEAD;  // iterations between a channel wave's row loads and their use (1 or 2)
 static_assert(S2_AHEAD == 1 || S2_AHEAD == 2, "step2 load distance");
 static_assert(S2_LDS * 4 <= 163840, "step2 LDS");
+// First pair (stage 0, right-hand side B, stage 1; graph_step2_kernel<.., FIRST>): stage 1 has no heavy-ball
+// term (no u ring); x_1 ring of 7 rows; the half-weight ring row holds 12 planes (wL1 x4, cG1 x2, the prox
+// level's wG1 x4 at the row, plane 0 one row down, plane 3 one row up); the prox weight ring holds two
+// row pairs of wG0 (4 planes x 2 rows, plane 0 two rows down, plane 3 one row up: 10 rows each).
+constexpr int S2F_XR = 7;
+constexpr int S2F_HPL = 12;
+constexpr int S2F_PR = 10;
+constexpr int S2F_LDS = S2_WP * S2_PAIR + S2_HR * S2F_HPL * S2_HW + S2_FMAX * (S2F_XR * S2_W + S2_DR * S2_HW + S2_TR * S2_HW) +
+                        2 * S2F_PR * S2_W;
+static_assert(S2F_LDS * 4 <= 163840, "first-pair LDS");
 // Waves (wave w runs on SIMD w mod 4): stage B of channel f = wave f, the producer = wave
 // S2_FMAX, stage A of channel f = wave S2_FMAX + 1 + f, stage A's half level (all channels) =
 // wave 2 S2_FMAX + 1.  The two waves of channel f share a SIMD, so each of SIMDs 0-2 issues its
@@ -1541,19 +1630,29 @@ constexpr int S2_THREADS = 64 * (2 * S2_FMAX + 2);
 // 16-column halo covers that.
 constexpr int S2_HALO = 16, S2_SOWN = S2_W - 2 * S2_HALO;
 
-template <bool MID, bool STRIPS>
+// FIRST: stage A = stage 0 (x_0 = b = the right-hand side A, no u), stage B = the prox right-hand side B
+// (REF:757-781) of x_1 and stage 1 on it: the prox terms reuse the stage-B pipes' s rows (same stencils,
+// same input rows), b_B is formed in registers at the row stage 1 emits and stored beside x_2, u_2; x_1
+// never leaves the CU.  W = S2_W only (no strips), no training instance.
+template <bool MID, bool STRIPS, bool FIRST = false>
 __global__ __launch_bounds__(S2_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void graph_step2_kernel(Step2Args a) {
+  static_assert(!FIRST || (!MID && !STRIPS), "first pair: inference, W = 256");
   constexpr int V = 4, VH = 2, W = S2_W, hw = S2_HW;
   typedef typename VecT<4>::type F4;
   typedef typename VecT<2>::type F2;
-  __shared__ __attribute__((aligned(16))) float lds[S2_LDS];
+  constexpr int XR = FIRST ? S2F_XR : S2_XR;            // x_{k+1} ring rows
+  constexpr int UR = FIRST ? 0 : S2_UR;                 // u_{k+1} ring rows
+  constexpr int HPL = FIRST ? S2F_HPL : 6;              // planes per half-weight ring row
+  constexpr int HROW = HPL * S2_HW;
+  __shared__ __attribute__((aligned(16))) float lds[FIRST ? S2F_LDS : S2_LDS];
   float* const wring = lds;
   float* const hring = wring + S2_WP * S2_PAIR;
-  float* const xring = hring + S2_HR * S2_HROW;
-  float* const uring = xring + S2_FMAX * S2_XR * S2_W;
-  float* const dring = uring + S2_FMAX * S2_UR * S2_W;
+  float* const xring = hring + S2_HR * HROW;
+  float* const uring = xring + S2_FMAX * XR * S2_W;
+  float* const dring = uring + S2_FMAX * UR * S2_W;
   float* const tring = dring + S2_FMAX * S2_DR * S2_HW;
+  float* const pring = tring + S2_FMAX * S2_TR * S2_HW;   // (FIRST) prox weight pairs
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int F = a.F;
@@ -1616,30 +1715,55 @@ void graph_step2_kernel(Step2Args a) {
           dma(e < 4 ? pwl0 + e * HW + rw : pcg0 + (e - 4) * HW + rw, slot + (par * 6 + e) * S2_W);
       }
     };
+    // (FIRST) the prox level's raw weights
+    const float* pwg0 = FIRST ? a.wG0 + (int64_t)(b * a.G + g) * 4 * HW : nullptr;
+    const float* pwg1 = FIRST ? a.wG1 + (int64_t)(b * a.G + g) * 4 * hHW : nullptr;
     auto dma_half = [&](int p) {   // half-level weight row of iteration p (the stage-B half level's l/o row)
-      const int hr = clampi((ts + 2 * p - 3) / 2 - 3, 0, h - 1);
-      float* slot = hring + (p % S2_HR) * S2_HROW;
+      const int hr0 = (ts + 2 * p - 3) / 2 - 3;
+      const int hr = clampi(hr0, 0, h - 1);
+      float* slot = hring + (p % S2_HR) * HROW;
       const int pl = lane >> 5;   // lanes 0-31: plane 2e, lanes 32-63: plane 2e+1
 #pragma unroll
-      for (int e = 0; e < 3; ++e) {
+      for (int e = 0; e < HPL / 2; ++e) {
         const int plane = 2 * e + pl;
         const int hc = STRIPS ? clampi(x0 / 2 + (lane & 31) * 4, 0, hwi - 4) : (lane & 31) * 4;
-        const float* src = (plane < 4 ? pwl1 + plane * hHW : pcg1 + (plane - 4) * hHW) + (int64_t)hr * hwi + hc;
-        dma(src, slot + e * 2 * S2_HW);
+        const float* src;
+        if (plane < 4) src = pwl1 + plane * hHW + (int64_t)hr * hwi;
+        else if (plane < 6) src = pcg1 + (plane - 4) * hHW + (int64_t)hr * hwi;
+        else if (plane < 10) src = pwg1 + (plane - 6) * hHW + (int64_t)hr * hwi;
+        else if (plane == 10) src = pwg1 + (int64_t)clampi(hr0 + 1, 0, h - 1) * hwi;          // w_up, row + 1
+        else src = pwg1 + 3 * hHW + (int64_t)clampi(hr0 - 1, 0, h - 1) * hwi;                  // w_down, row - 1
+        dma(src + hc, slot + e * 2 * S2_HW);
       }
     };
+    // (FIRST) prox weight pair of iteration p: stage B's o rows ra = t - 10, ra + 1 (t = ts + 2p), four planes
+    // each, then plane 0 at ra + 2 and plane 3 at ra - 1; into slot p mod 2 (one iteration ahead)
+    auto dma_prox = [&](int p) {
+      const int ra = ts + 2 * p - 10;
+      float* slot = pring + (p & 1) * (S2F_PR * S2_W);
+#pragma unroll
+      for (int k = 0; k < S2F_PR; ++k) {
+        const int e = k < 8 ? (k & 3) : (k == 8 ? 0 : 3);
+        const int rr = k < 8 ? ra + (k >> 2) : (k == 8 ? ra + 2 : ra - 1);
+        dma(pwg0 + e * HW + (int64_t)clampi(rr, 0, H - 1) * Wi + vo / 4u, slot + k * S2_W);
+      }
+    };
+    // vmcnt immediate: the DMAs of the newest pair + half row may be in flight (15 / 18)
+    constexpr int kAheadDmas = 12 + HPL / 2;
+    if constexpr (FIRST) dma_prox(0);
     dma_pair(0);
     dma_half(0);
     dma_pair(1);
     dma_half(1);
-    asm volatile("s_waitcnt vmcnt(15)" ::: "memory");   // iteration 0's rows landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kAheadDmas) : "memory");   // iteration 0's rows landed
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     for (int i = 0; i < NI; ++i) {
+      if constexpr (FIRST) dma_prox(i + 1);   // the slot iteration i - 1 read
       dma_pair(i + 2);
       dma_half(i + 2);
       if (i == i_top) __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt vmcnt(15)" ::: "memory");  // iteration i+1's rows landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kAheadDmas) : "memory");  // iteration i+1's rows landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
@@ -1775,9 +1899,12 @@ void graph_step2_kernel(Step2Args a) {
   const bool use_beta_a = a.beta_a != nullptr && a.u_prev != nullptr;
   const bool use_skip = a.skip != nullptr;
   const rsrc_t rx = make_rsrc(a.x + plane, PB);
-  const rsrc_t rb = make_rsrc(a.b + plane, PB);
-  const rsrc_t ru = make_rsrc(use_beta_a ? a.u_prev + plane : nullptr, PB);   // absent: reads 0
-  const rsrc_t ry = make_rsrc(use_skip ? a.y + plane : nullptr, PB);
+  const rsrc_t rb = make_rsrc(FIRST ? nullptr : a.b + plane, PB);
+  const rsrc_t ru = make_rsrc(use_beta_a && !FIRST ? a.u_prev + plane : nullptr, PB);   // absent: reads 0
+  // y: the block skip's (step2) or right-hand side B's (FIRST; [B,F,H,W] when it replicates an image)
+  const int64_t yplane = FIRST && a.yr_rep ? ((int64_t)b * F + fb + f) * HW : plane;
+  const rsrc_t ry = make_rsrc(FIRST ? a.yr + yplane : (use_skip ? a.y + plane : nullptr), PB);
+  const rsrc_t rbo = make_rsrc(FIRST ? a.b_out + plane : nullptr, FIRST ? PB : 0);
   const rsrc_t rout = make_rsrc(a.out + plane, PB);
   const rsrc_t ruo = make_rsrc(a.u_out ? a.u_out + plane : nullptr, PB);
   const rsrc_t rxd = make_rsrc(a.xd_out ? a.xd_out + hplane : nullptr, HPB);
@@ -1794,9 +1921,10 @@ void graph_step2_kernel(Step2Args a) {
   if (use_skip) { sk0 = a.skip[0]; sk1 = a.skip[1]; }
   const Taps tL0 = make_taps(a.sL0, ch), tG0 = make_taps(a.sG0, ch);
   const Taps tL1 = make_taps(a.sL1, ch), tG1 = make_taps(a.sG1, ch);
+  const float gam0 = FIRST ? expf(a.log_gamma0[g]) : 0.f, gam1 = FIRST ? expf(a.log_gamma1[g]) : 0.f;
 
-  float* const xr = xring + f * S2_XR * S2_W + c0;
-  float* const ur = uring + f * S2_UR * S2_W + c0;
+  float* const xr = xring + f * XR * S2_W + c0;
+  float* const ur = uring + f * UR * S2_W + c0;
   float* const dr = dring + f * S2_DR * S2_HW + ch0;
   const float* const tr = tring + f * S2_TR * S2_HW + ch0;
   const float* const wl_lane = wring + c0;
@@ -1808,15 +1936,18 @@ void graph_step2_kernel(Step2Args a) {
   // read-once streams (x_k, u_k, weights) are non-temporal so that b's rows stay in L2 for
   // stage B's second read 8 rows later (one HBM read of b per launch)
   auto issue_a = [&](int t, Ld& S) {
+    // (FIRST: b = x_0 is the row the pipe already holds; no u)
     bload<V, S2_NT>(S.x, rx, vo + clampi(t, 0, H - 1) * RB);
-    const int re = clampi(t - 3, 0, H - 1);
-    bload(S.eb, rb, vo + re * RB);
-    bload<V, S2_NT>(S.eu, ru, vo + re * RB);
+    if constexpr (!FIRST) {
+      const int re = clampi(t - 3, 0, H - 1);
+      bload(S.eb, rb, vo + re * RB);
+      bload<V, S2_NT>(S.eu, ru, vo + re * RB);
+    }
   };
   auto issue_b = [&](int t, Ld& S) {
     const int r2 = clampi(t - 11, 0, H - 1);
-    bload(S.b2, rb, vo + r2 * RB);
-    bload(S.y2, ry, vo + r2 * RB);
+    if constexpr (!FIRST) bload(S.b2, rb, vo + r2 * RB);
+    bload<V, FIRST ? S2_NT : 0>(S.y2, ry, vo + r2 * RB);
   };
   auto ring_w = [&](const float* row, float (&WL)[4][V], float (&WG)[2][V]) {
 #pragma unroll
@@ -1850,11 +1981,19 @@ void graph_step2_kernel(Step2Args a) {
   PQ.zero();
   PH.zero();
   float TH[VH] = {};
+  // (FIRST) the prox terms of right-hand side B on stage B's pipes: full level (x_1) and half level (D x_1)
+  ProxExt<V> XQ;
+  ProxExt<VH> XH;
+  float TP[VH] = {};
+  if constexpr (FIRST) {
+    XQ.zero();
+    XH.zero();
+  }
   float xa0[V], xb0[V];   // the even row of the current iteration (2x2 pooling)
 
   // stage A (stage k) at step t: emits row t-3 into the x / u rings, D x half rows at odd rows;
   // th = t_k at half row (t-3) >> 1 (from the t ring)
-  auto stage_a = [&](int t, const Ld& S, const float (&thv)[VH], int q, auto par_tag, auto ph_tag, auto edge_tag) {
+  auto stage_a = [&](int t, const Ld& S, const float (&thv)[VH], int q, auto par_tag, auto ph_tag, auto edge_tag) __attribute__((always_inline)) {
     constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
     constexpr bool EDGE = decltype(edge_tag)::value;
     float WL[4][V], WG[2][V], tl[V], tg[V];
@@ -1870,14 +2009,19 @@ void graph_step2_kernel(Step2Args a) {
       ax = ax + tl[j] * scl0;
       ax = ax + tg[j] * scg0;
       ax = ax + th;
-      float uv = S.eb[j] - ax;
-      uv = uv + beta_a * S.eu[j];
+      float uv;
+      if constexpr (FIRST) {
+        uv = x0[j] - ax;                                  // stage 0: b = x_0 (REF:751-753)
+      } else {
+        uv = S.eb[j] - ax;
+        uv = uv + beta_a * S.eu[j];
+      }
       u[j] = uv;
       xn[j] = x0[j] + alpha_a * uv;
     }
     if (y >= 0 && y < H) {   // uniform: rows outside the image never enter the rings
-      st4(xr + (y & (S2_XR - 1)) * S2_W, xn);
-      st4(ur + (y % S2_UR) * S2_W, u);
+      st4(xr + (FIRST ? y % XR : y & (XR - 1)) * S2_W, xn);
+      if constexpr (!FIRST) st4(ur + (y % UR) * S2_W, u);
     }
     if constexpr (MID) {     // training: the middle iterate's rows of this segment to HBM
       const uint32_t so = (y >= r0 && y < r1 && own) ? vo + (uint32_t)y * RB : GRR_OOB;
@@ -1900,7 +2044,7 @@ void graph_step2_kernel(Step2Args a) {
   };
 
   // half level of D x_{k+1}: input half row hA - 1 (clamped), emits t_{k+1} half row hA - 4
-  auto stage_h = [&](int hA, int qh, auto ph_tag, auto edge_tag) {
+  auto stage_h = [&](int hA, int qh, auto ph_tag, auto edge_tag) __attribute__((always_inline)) {
     constexpr int P = decltype(ph_tag)::value;
     constexpr bool EDGE = decltype(edge_tag)::value;
     const int hin = hA - 1;
@@ -1909,7 +2053,7 @@ void graph_step2_kernel(Step2Args a) {
       const F2 q = *reinterpret_cast<const F2*>(dr + (clampi(hin, 0, h - 1) & (S2_DR - 1)) * S2_HW);
       xh[0] = q[0]; xh[1] = q[1];
     }
-    const float* row = hw_lane + qh * S2_HROW;
+    const float* row = hw_lane + qh * HROW;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const F2 q = *reinterpret_cast<const F2*>(row + e * S2_HW);
@@ -1927,20 +2071,58 @@ void graph_step2_kernel(Step2Args a) {
       rv = rv + tg[k] * scg1;
       TH[k] = rv;
     }
+    if constexpr (FIRST) {   // right-hand side B's half level: C^T phi(C s) of D x_1 (grr_gtv_rhs_half, prox)
+      float W4[4][VH], wup[VH], wdn[VH], tp[VH];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const F2 q = *reinterpret_cast<const F2*>(row + (6 + e) * S2_HW);
+        W4[e][0] = q[0]; W4[e][1] = q[1];
+      }
+      {
+        const F2 q = *reinterpret_cast<const F2*>(row + 10 * S2_HW);
+        wup[0] = q[0]; wup[1] = q[1];
+        const F2 r = *reinterpret_cast<const F2*>(row + 11 * S2_HW);
+        wdn[0] = r[0]; wdn[1] = r[1];
+      }
+      XH.template advance<P, hw, EDGE>(PH, W4, wup, wdn, hin, h, ch0, tG1, gam1, tp);
+#pragma unroll
+      for (int k = 0; k < VH; ++k) TP[k] = tp[k];
+    }
   };
 
   // stage B (stage k+1) at step t: input x_{k+1} row t-8, emits row t-11 to HBM
-  auto stage_b = [&](int t, const Ld& S, int q, auto par_tag, auto ph_tag, auto edge_tag) {
+  // FIRST: b = right-hand side B at that row, y + ro0 C^T phi(C s) + ro1 U(t') (grr_gtv_rhs_full's
+  // expression), formed from the same x_1 rows (prox weights: pring slot qp) and stored beside x_{k+2}
+  auto stage_b = [&](int t, const Ld& S, int q, int qp, auto par_tag, auto ph_tag, auto edge_tag) __attribute__((always_inline)) {
     constexpr int PAR = decltype(par_tag)::value, P = decltype(ph_tag)::value;
     constexpr bool EDGE = decltype(edge_tag)::value;
     const int tb = t - 8;
     float xin[V], WL[4][V], WG[2][V], tl[V], tg[V], up[V];
-    ld4(xr + (clampi(tb, 0, H - 1) & (S2_XR - 1)) * S2_W, xin);
+    ld4(xr + (FIRST ? clampi(tb, 0, H - 1) % XR : clampi(tb, 0, H - 1) & (XR - 1)) * S2_W, xin);
     ring_w(wl_lane + q * S2_PAIR + PAR * 6 * S2_W, WL, WG);
     const int y = t - 11;
-    ld4(ur + (((y % S2_UR) + S2_UR) % S2_UR) * S2_W, up);
+    if constexpr (!FIRST) ld4(ur + (((y % UR) + UR) % UR) * S2_W, up);
     PQ.template advance<P, W, EDGE, STRIPS>(xin, WL, WG, tb, H, STRIPS ? cg : c0, tL0, tG0, tl, tg, Wi);
     const float (&x0)[V] = PQ.template x_out<P>();
+    float bv[V];
+    if constexpr (FIRST) {
+      const float* prow = pring + qp * (S2F_PR * S2_W) + c0;
+      float W4[4][V], wup[V], wdn[V], tp[V];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ld4(prow + (PAR * 4 + e) * S2_W, W4[e]);
+      ld4(prow + (PAR == 0 ? 4 : 8) * S2_W, wup);
+      ld4(prow + (PAR == 0 ? 9 : 3) * S2_W, wdn);
+      XQ.template advance<P, W, EDGE>(PQ, W4, wup, wdn, tb, H, c0, tG0, gam0, tp);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float rv = S.y2[j] + tp[j] * scg0;
+        rv = rv + (0.25f * TP[j >> 1]) * scg1;
+        bv[j] = rv;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) bv[j] = S.b2[j];
+    }
     float res[V], xn[V], u[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -1949,16 +2131,17 @@ void graph_step2_kernel(Step2Args a) {
       ax = ax + tl[j] * scl0;
       ax = ax + tg[j] * scg0;
       ax = ax + th;
-      float uv = S.b2[j] - ax;
-      uv = uv + beta_b * up[j];
+      float uv = bv[j] - ax;
+      if constexpr (!FIRST) uv = uv + beta_b * up[j];
       u[j] = uv;
       xn[j] = x0[j] + alpha_b * uv;
-      res[j] = sk0 * S.y2[j] + sk1 * xn[j];
+      res[j] = FIRST ? xn[j] : sk0 * S.y2[j] + sk1 * xn[j];
     }
     const bool yv = y >= r0 && y < r1 && own;
     const uint32_t so = yv ? vo + (uint32_t)y * RB : GRR_OOB;
     bstore<V, S2_NT>(rout, so, res);
     bstore<V, S2_NT>(ruo, so, u);
+    if constexpr (FIRST) bstore<V, S2_NT>(rbo, so, bv);
     if constexpr (PAR == 0) {
 #pragma unroll
       for (int j = 0; j < V; ++j) xb0[j] = xn[j];
@@ -1985,9 +2168,9 @@ void graph_step2_kernel(Step2Args a) {
     // filled after the barrier below.
     const float zero4[V] = {};
 #pragma unroll
-    for (int r = 0; r < S2_XR; ++r) st4(xr + r * S2_W, zero4);
+    for (int r = 0; r < XR; ++r) st4(xr + r * S2_W, zero4);
 #pragma unroll
-    for (int r = 0; r < S2_UR; ++r) st4(ur + r * S2_W, zero4);
+    for (int r = 0; r < UR; ++r) st4(ur + r * S2_W, zero4);
     *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
     *reinterpret_cast<F4*>(dring + f * S2_DR * S2_HW + S2_W + 4 * lane) = F4{0.f, 0.f, 0.f, 0.f};
     for (int r = f; r < (S2_WP - 2) * 12; r += Fg) st4(wring + 2 * S2_PAIR + r * S2_W + c0, zero4);
@@ -2007,7 +2190,7 @@ void graph_step2_kernel(Step2Args a) {
   // stage k+1 (8 rows behind, its inputs written into the rings at least one barrier earlier).
   // PI = the iteration's phase in the unrolled body (pipelines A, B advance two slots per
   // iteration, the half level one)
-  auto iteration_a = [&](int i, auto pi_tag, auto edge_tag) {
+  auto iteration_a = [&](int i, auto pi_tag, auto edge_tag) __attribute__((always_inline)) {
     constexpr int PI = decltype(pi_tag)::value;
     using P0 = std::integral_constant<int, (2 * PI) & 3>;
     using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
@@ -2033,7 +2216,7 @@ void graph_step2_kernel(Step2Args a) {
     asm volatile("" ::: "memory");
     qa = qa == S2_WP - 1 ? 0 : qa + 1;
   };
-  auto iteration_b = [&](int i, auto pi_tag, auto edge_tag) {
+  auto iteration_b = [&](int i, auto pi_tag, auto edge_tag) __attribute__((always_inline)) {
     constexpr int PI = decltype(pi_tag)::value;
     using P0 = std::integral_constant<int, (2 * PI) & 3>;
     using P1 = std::integral_constant<int, (2 * PI + 1) & 3>;
@@ -2045,9 +2228,9 @@ void graph_step2_kernel(Step2Args a) {
     stage_h((t - 3) / 2, i & (S2_HR - 1), PHh{}, E{});
     Ld& LX = (S2_AHEAD == 2 && (PI & 1)) ? LC : LA;
     Ld& LY = (S2_AHEAD == 2 && (PI & 1)) ? LD : LB;
-    stage_b(t, LX, qb, std::integral_constant<int, 0>{}, P0{}, E{});
+    stage_b(t, LX, qb, PI & 1, std::integral_constant<int, 0>{}, P0{}, E{});
     issue_b(t + 2 * S2_AHEAD, LX);
-    stage_b(t + 1, LY, qb, std::integral_constant<int, 1>{}, P1{}, E{});
+    stage_b(t + 1, LY, qb, PI & 1, std::integral_constant<int, 1>{}, P1{}, E{});
     issue_b(t + 2 * S2_AHEAD + 1, LY);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -2347,6 +2530,59 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   return system_step2_impl(x, b, u_prev, xd, wL0, cG0, sL0, sG0, log_mu0, log_ro0, wL1, cG1, sL1, sG1, log_mu1,
                            log_ro1, alpha_a, beta_a, alpha_b, beta_b, skip, y_skip, x_out, u_out, xd_out, nullptr,
                            nullptr, B, G, F, H, W, stream);
+}
+
+// Stage 0, the prox right-hand side B and stage 1 in one pass (graph_step2_kernel<false, false, true>):
+// REF:751-753 (x_1 = b_A + alpha_0 (b_A - A b_A)), REF:757-781 (b_B = y + ro0 C^T phi(C S x_1) +
+// ro1 U(C^T phi(C S D x_1))), REF:784-790 at k = 1 (no heavy-ball term).  In: b_A, D b_A (the right-hand
+// side A pass's pooled output), y ([B,C,H,W], or the [B,F,H,W] image it replicates: y_rep).  Out: b_B,
+// x_2, u_2 (stage 1's residual direction, the next stage's heavy-ball term), D x_2.  x_1 stays on chip.
+grr_status grr_system_first_pair(const float* b_a, const float* xd_a, const float* y, int y_rep, const float* wL0,
+                                 const float* cG0, const float* wG0, grr_stencil sL0, grr_stencil sG0,
+                                 const float* log_mu0, const float* log_ro0, const float* log_gamma0,
+                                 const float* wL1, const float* cG1, const float* wG1, grr_stencil sL1,
+                                 grr_stencil sG1, const float* log_mu1, const float* log_ro1,
+                                 const float* log_gamma1, const float* alpha0, const float* alpha1, float* b_out,
+                                 float* x_out, float* u_out, float* xd_out, int B, int G, int F, int H, int W,
+                                 void* stream) {
+  clear_error();
+  GRR_REQUIRE(b_a && xd_a && y && wL0 && cG0 && wG0 && log_mu0 && log_ro0 && log_gamma0 && wL1 && cG1 && wG1 &&
+                  log_mu1 && log_ro1 && log_gamma1 && alpha0 && alpha1 && b_out && x_out && u_out && xd_out &&
+                  B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
+              GRR_ERR_INVALID_ARG, "grr_system_first_pair: bad args");
+  GRR_REQUIRE(stencil_ok(sL0) && stencil_ok(sG0) && stencil_ok(sL1) && stencil_ok(sG1), GRR_ERR_INVALID_ARG,
+              "grr_system_first_pair: stencil missing");
+  GRR_REQUIRE(W == S2_W && H % 2 == 0 && H >= 2, GRR_ERR_UNSUPPORTED,
+              "grr_system_first_pair: needs W = %d and even H (got H %d, W %d)", S2_W, H, W);
+  const void* outs[] = {b_out, x_out, u_out, xd_out};
+  const void* ins[] = {b_a, xd_a, y};
+  for (const void* o : outs)
+    for (const void* i : ins)
+      GRR_REQUIRE(o != i, GRR_ERR_INVALID_ARG, "grr_system_first_pair: outputs must not alias the inputs");
+  const void* ptrs[] = {b_a, xd_a, y, wL0, cG0, wG0, wL1, cG1, wG1, b_out, x_out, u_out, xd_out};
+  for (const void* q : ptrs)
+    GRR_REQUIRE((uintptr_t)q % 16 == 0, GRR_ERR_INVALID_ARG, "grr_system_first_pair: operands must be 16-byte aligned");
+  Step2Args a{};
+  a.x = b_a; a.xd = xd_a;
+  a.wL0 = wL0; a.cG0 = cG0; a.wL1 = wL1; a.cG1 = cG1;
+  a.sL0 = sL0; a.sG0 = sG0; a.sL1 = sL1; a.sG1 = sG1;
+  a.log_mu0 = log_mu0; a.log_ro0 = log_ro0; a.log_mu1 = log_mu1; a.log_ro1 = log_ro1;
+  a.alpha_a = alpha0; a.alpha_b = alpha1;
+  a.out = x_out; a.u_out = u_out; a.xd_out = xd_out;
+  a.wG0 = wG0; a.wG1 = wG1; a.log_gamma0 = log_gamma0; a.log_gamma1 = log_gamma1;
+  a.yr = y; a.yr_rep = y_rep != 0; a.b_out = b_out;
+  a.G = G; a.F = F; a.H = H; a.W = W;
+  a.nstrips = 1;
+  a.ngrp = (F + S2_FMAX - 1) / S2_FMAX;
+  a.FG = (F + a.ngrp - 1) / a.ngrp;
+  a.sseg = step2_seg_rows(H, (uint64_t)B * G * a.ngrp);
+  a.nsegs = (H + a.sseg - 1) / a.sseg;
+  const uint64_t nblk = (uint64_t)B * G * a.ngrp * a.nsegs;
+  GRR_REQUIRE(nblk < (1ull << 32) - 4, GRR_ERR_UNSUPPORTED, "grr_system_first_pair: grid too large");
+  a.nblk = (uint32_t)nblk;
+  hipLaunchKernelGGL((graph_step2_kernel<false, false, true>), dim3(a.nblk), dim3(S2_THREADS), 0,
+                     (hipStream_t)stream, a);
+  return launch_status("grr_system_first_pair");
 }
 
 grr_status grr_system_step2_train(const float* x, const float* b, const float* u_prev, const float* xd,

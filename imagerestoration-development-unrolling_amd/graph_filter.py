@@ -468,25 +468,35 @@ class MixtureGTVGLR(HipModule):
             b_a, xd = OPS.gtv_rhs_full(src, True, src, True, cG0, G0, False, None, ro0, t, ro1, g, want_pool=True)
         else:
             b_a, xd = OPS.gtv_rhs_full(y, False, y, False, cG0, G0, False, None, ro0, t, ro1, g, want_pool=True)
-        # stage 0: x1 = b_A + alpha0 (b_A - A b_A)                     (REF:751-753)
-        last = n_st == 1
-        t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
-        x, _, xd = OPS.system_step(b_a, b_a, None, t, wL0, cG0, L0, G0, mu0, ro0, alpha[0], None, g,
-                                   want_u=False, want_pool=not last, skip=skip if last else None,
-                                   y_skip=y if last else None)
-        del b_a
-        if last:
-            return x
-        # GTV proximal step -> rhs B                                   (REF:757-781)
-        t = OPS.gtv_rhs_half(xd, wG1, G1, True, self.gamma01, g)
-        if y is None:
-            b_b, _ = OPS.gtv_rhs_full(x, False, src, True, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
-        else:
-            b_b, _ = OPS.gtv_rhs_full(x, False, y, False, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
-        del wG0, wG1
         u, u_spare = None, None
-        pair = OPS.step2_supported(x, g)
-        k = 1
+        if n_st >= 3 and OPS.first_pair_supported(b_a, g):
+            # stage 0, the prox rhs B and stage 1 in one pass: x1, D x1, t0, t1 and both prox terms stay on
+            # chip (REF:751-790 at k = 0, 1); the pairs below then end on stage S-1 with its skip
+            b_b, x, u, xd = OPS.system_first_pair(b_a, xd, src if y is None else y, y is None, wL0, cG0, wG0, L0, G0,
+                                                  mu0, ro0, self.gamma00, wL1, cG1, wG1, L1, G1, mu1, ro1,
+                                                  self.gamma01, alpha[0], alpha[1], g)
+            del b_a, wG0, wG1
+            pair = OPS.step2_supported(x, g)
+            k = 2
+        else:
+            # stage 0: x1 = b_A + alpha0 (b_A - A b_A)                     (REF:751-753)
+            last = n_st == 1
+            t = OPS.system_half(xd, wL1, cG1, L1, G1, mu1, ro1, g)
+            x, _, xd = OPS.system_step(b_a, b_a, None, t, wL0, cG0, L0, G0, mu0, ro0, alpha[0], None, g,
+                                       want_u=False, want_pool=not last, skip=skip if last else None,
+                                       y_skip=y if last else None)
+            del b_a
+            if last:
+                return x
+            # GTV proximal step -> rhs B                                   (REF:757-781)
+            t = OPS.gtv_rhs_half(xd, wG1, G1, True, self.gamma01, g)
+            if y is None:
+                b_b, _ = OPS.gtv_rhs_full(x, False, src, True, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
+            else:
+                b_b, _ = OPS.gtv_rhs_full(x, False, y, False, wG0, G0, True, self.gamma00, ro0, t, ro1, g)
+            del wG0, wG1
+            pair = OPS.step2_supported(x, g)
+            k = 1
         while k < n_st:                                              # (REF:784-790, :797-807)
             if pair and k + 1 < n_st:
                 # stages k, k+1 in one pass, both half levels inside: t_k, x_{k+1}, u_{k+1},

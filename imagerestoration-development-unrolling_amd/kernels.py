@@ -319,6 +319,48 @@ def system_step2(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: Tensor
     return out, u_out, xd
 
 
+def system_first_pair(b_a: Tensor, xd_a: Tensor, y: Tensor, y_rep: bool,
+                      wL0: Tensor, cG0: Tensor, wG0: Tensor, sL0: Stencil, sG0: Stencil, log_mu0: Tensor,
+                      log_ro0: Tensor, log_gamma0: Tensor, wL1: Tensor, cG1: Tensor, wG1: Tensor, sL1: Stencil,
+                      sG1: Stencil, log_mu1: Tensor, log_ro1: Tensor, log_gamma1: Tensor, alpha0: Tensor,
+                      alpha1: Tensor, n_graphs: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Stage 0, the prox right-hand side B and stage 1 in one pass (grr_system_first_pair); xd_a = D b_A.
+    y: [B, C, H, W], or the [B, F, H, W] image it replicates (y_rep).  Returns (b_B, x_2, u_2, D x_2)."""
+    dev = _check("system_first_pair", b_a, xd_a, y, wL0, cG0, wG0, log_mu0, log_ro0, log_gamma0, wL1, cG1, wG1,
+                 log_mu1, log_ro1, log_gamma1, alpha0, alpha1)
+    b, c, h, w = b_a.shape
+    b_out, x_out, u_out = (torch.empty_like(b_a) for _ in range(3))
+    xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev)
+    _launch("system_first_pair", first_pair_bytes(b, c, n_graphs, h, w, y_rep),
+            "grr_system_first_pair", b_a.data_ptr(), xd_a.data_ptr(), y.data_ptr(), int(y_rep), wL0.data_ptr(),
+            cG0.data_ptr(), wG0.data_ptr(), sL0, sG0, log_mu0.data_ptr(), log_ro0.data_ptr(), log_gamma0.data_ptr(),
+            wL1.data_ptr(), cG1.data_ptr(), wG1.data_ptr(), sL1, sG1, log_mu1.data_ptr(), log_ro1.data_ptr(),
+            log_gamma1.data_ptr(), alpha0.data_ptr(), alpha1.data_ptr(), b_out.data_ptr(), x_out.data_ptr(),
+            u_out.data_ptr(), xd.data_ptr(), b, n_graphs, c // n_graphs, h, w, _stream(dev))
+    return b_out, x_out, u_out, xd
+
+
+def first_pair_bytes(b, c, g, h, w, y_rep):
+    """Compulsory HBM bytes of one grr_system_first_pair launch: b_A, D b_A, y read once, the full- and
+    half-level GLR + pair weights and the prox raw weights read once per channel group; b_B, x_2, u_2, D x_2
+    written once (t_0, x_1, D x_1, the prox terms and t_1 stay on chip)."""
+    f = c * (1 + 3) + (c // g if y_rep else c)                         # b_A in; b_B, x_2, u_2 out; y in
+    f += (c // 4) * 2                                                  # D b_A in, D x_2 out
+    ngrp = -(-(c // g) // 3)
+    f += (6 * g + 4 * g + (6 * g + 4 * g) // 4) * ngrp                 # wL0, cG0, wG0; wL1, cG1, wG1
+    return 4 * b * h * w * f
+
+
+# stage 0, right-hand side B and stage 1 in one pass where the shape allows (tests set False for the
+# per-stage sequence)
+FIRST_PAIR = True
+
+
+def first_pair_supported(x: Tensor, n_graphs: int) -> bool:
+    b, c, h, w = x.shape
+    return FIRST_PAIR and w == 256 and h % 2 == 0 and c % n_graphs == 0
+
+
 # two CG stages per launch where the shape allows (tests set False to run one launch per stage)
 STEP2 = True
 

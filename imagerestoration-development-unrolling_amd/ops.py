@@ -256,6 +256,27 @@ def _(x, rhs, u_prev, xd, wL0, cG0, sL01, sL02a, sL02b, sL03, sG01, sG02a, sG02b
             _half(x) if want_pool else x.new_empty(0))
 
 
+@custom_op(f"{NS}::system_first_pair", mutates_args=())
+def system_first_pair_op(b_a: Tensor, xd_a: Tensor, y: Tensor, y_rep: bool, wL0: Tensor, cG0: Tensor, wG0: Tensor,
+                         sL01: Tensor, sL02a: Tensor, sL02b: Tensor, sL03: Tensor,
+                         sG01: Tensor, sG02a: Tensor, sG02b: Tensor, sG03: Tensor, log_mu0: Tensor, log_ro0: Tensor,
+                         log_gamma0: Tensor, wL1: Tensor, cG1: Tensor, wG1: Tensor,
+                         tL01: Tensor, tL02a: Tensor, tL02b: Tensor, tL03: Tensor,
+                         tG01: Tensor, tG02a: Tensor, tG02b: Tensor, tG03: Tensor, log_mu1: Tensor, log_ro1: Tensor,
+                         log_gamma1: Tensor, alpha0: Tensor, alpha1: Tensor,
+                         n_graphs: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    c = lambda t: t.contiguous()  # noqa: E731
+    return K.system_first_pair(c(b_a), c(xd_a), c(y), y_rep, c(wL0), c(cG0), c(wG0), _st(sL01, sL02a, sL02b, sL03),
+                               _st(sG01, sG02a, sG02b, sG03), c(log_mu0), c(log_ro0), c(log_gamma0), c(wL1), c(cG1),
+                               c(wG1), _st(tL01, tL02a, tL02b, tL03), _st(tG01, tG02a, tG02b, tG03), c(log_mu1),
+                               c(log_ro1), c(log_gamma1), c(alpha0), c(alpha1), n_graphs)
+
+
+@system_first_pair_op.register_fake
+def _(b_a, xd_a, y, y_rep, *args):
+    return torch.empty_like(b_a), torch.empty_like(b_a), torch.empty_like(b_a), _half(b_a)
+
+
 @custom_op(f"{NS}::glr_stage", mutates_args=())
 def glr_stage_op(x: Tensor, b: Tensor, u_prev: Optional[Tensor], wL: Tensor, s01: Tensor, s02a: Tensor, s02b: Tensor,
                  s03: Tensor, mu: Tensor, alpha: Tensor, beta: Optional[Tensor], n_graphs: int,
@@ -338,7 +359,7 @@ def _(e6, w, *args):
 
 OPS = [conv1x1_op, conv2x2s2_op, lnb_forward_op, lnb_forward_rep_op, repeat_graphs_op, pool2_op, edge_weights_op,
        edge_weights_block_op, gtv_pair_weights_op, system_half_op, gtv_rhs_half_op, gtv_rhs_full_op, system_step_op,
-       system_step2_op, glr_stage_op, neighbor_gather_op, normalize_features_op, stats_conv_op, glr_op_L_norm_op, gtv_op_C_op,
+       system_step2_op, system_first_pair_op, glr_stage_op, neighbor_gather_op, normalize_features_op, stats_conv_op, glr_op_L_norm_op, gtv_op_C_op,
        gtv_op_C_transpose_op]
 
 
@@ -461,6 +482,23 @@ def system_step2(x, rhs, u_prev, xd, wL0, cG0, modL0, modG0, log_mu0, log_ro0, w
     return K.system_step2(x, rhs, u_prev, xd, wL0, cG0, K.stencil(modL0), K.stencil(modG0), log_mu0, log_ro0,
                           wL1, cG1, K.stencil(modL1), K.stencil(modG1), log_mu1, log_ro1, alpha_a, beta_a, alpha_b,
                           beta_b, n_graphs, want_u, want_pool, skip=skip, y_skip=y_skip, u_out=u_out)
+
+
+def system_first_pair(b_a, xd_a, y, y_rep, wL0, cG0, wG0, modL0, modG0, log_mu0, log_ro0, log_gamma0, wL1, cG1, wG1,
+                      modL1, modG1, log_mu1, log_ro1, log_gamma1, alpha0, alpha1, n_graphs):
+    """kernels.system_first_pair (stage 0, right-hand side B, stage 1 in one pass; xd_a = D b_A).
+    Returns (b_B, x_2, u_2, D x_2)."""
+    if _tracing():
+        return torch.ops.irdu.system_first_pair(b_a, xd_a, y, y_rep, wL0, cG0, wG0, *_sp(modL0), *_sp(modG0), log_mu0,
+                                                log_ro0, log_gamma0, wL1, cG1, wG1, *_sp(modL1), *_sp(modG1), log_mu1,
+                                                log_ro1, log_gamma1, alpha0, alpha1, n_graphs)
+    return K.system_first_pair(b_a, xd_a, y, y_rep, wL0, cG0, wG0, K.stencil(modL0), K.stencil(modG0), log_mu0,
+                               log_ro0, log_gamma0, wL1, cG1, wG1, K.stencil(modL1), K.stencil(modG1), log_mu1,
+                               log_ro1, log_gamma1, alpha0, alpha1, n_graphs)
+
+
+def first_pair_supported(x, n_graphs) -> bool:
+    return K.STEP2 and K.first_pair_supported(x, n_graphs)
 
 
 def step2_supported(x, n_graphs) -> bool:

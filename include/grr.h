@@ -184,6 +184,27 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
                             const float* alpha_a, const float* beta_a, const float* alpha_b, const float* beta_b,
                             const float* skip, const float* y_skip, float* x_out, float* u_out, float* xd_out,
                             int B, int G, int F, int H, int W, void* stream);
+/* Stage 0, right-hand side B and stage 1 in one pass (the first pair of the loop: REF:751-753, :757-781,
+ * :784-790 at k = 1; x_1 never leaves the chip):
+ *   half level 0:  t_0 = exp(log_mu1) L1 xd_a + exp(log_ro1) G1 xd_a, xd_a = D b_A (grr_gtv_rhs_full's
+ *                  xd_out of right-hand side A; what grr_system_half computes)
+ *   stage 0:       x_1 = b_A + alpha0 (b_A - A b_A)                       (grr_system_step, x = b = b_A)
+ *   rhs B:         b_out = y + exp(log_ro0) C0^T phi(C0 S x_1) + exp(log_ro1) U(C1^T phi(C1 S D x_1)), the
+ *                  soft threshold at exp(log_gamma0) / exp(log_gamma1), raw weights wG0 [B,G,4,H,W] /
+ *                  wG1 [B,G,4,H/2,W/2]                     (grr_gtv_rhs_half + grr_gtv_rhs_full, prox)
+ *   stage 1:       x_out = x_2, u_out = u_2 = b_B - A x_1, xd_out = D x_2  (grr_system_step, no heavy-ball)
+ * y: [B,C,H,W], or the [B,F,H,W] image it replicates over the graphs (y_rep != 0).  Same values as
+ * grr_system_half -> grr_system_step -> grr_gtv_rhs_half -> grr_gtv_rhs_full -> grr_system_half ->
+ * grr_system_step up to fp32 rounding order.  W = 256, even H; F > 3 as groups of <= 3 channels; 16-byte
+ * aligned operands; outputs must not alias inputs. */
+grr_status grr_system_first_pair(const float* b_a, const float* xd_a, const float* y, int y_rep, const float* wL0,
+                                 const float* cG0, const float* wG0, grr_stencil sL0, grr_stencil sG0,
+                                 const float* log_mu0, const float* log_ro0, const float* log_gamma0,
+                                 const float* wL1, const float* cG1, const float* wG1, grr_stencil sL1,
+                                 grr_stencil sG1, const float* log_mu1, const float* log_ro1,
+                                 const float* log_gamma1, const float* alpha0, const float* alpha1, float* b_out,
+                                 float* x_out, float* u_out, float* xd_out, int B, int G, int F, int H, int W,
+                                 void* stream);
 /* grr_system_step2 for training: also writes the middle iterate x_{k+1} (x_mid) and its direction
  * u_{k+1} (u_mid) -- the reverse sweep's saved iterates -- besides x_{k+2}, u_{k+2} (u_out required) and
  * D x_{k+2}; no skip.  Same shape limits. */
