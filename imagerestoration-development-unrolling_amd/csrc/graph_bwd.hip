@@ -939,6 +939,11 @@ __global__ __launch_bounds__(NT) void term_bwd_fused_kernel(
 // grr_bwd_set_term_rows: 0 = per-pixel term reverses, 1 = the register-prefetch row kernel, 2 (default) = the
 // LDS-ring row kernel where it applies (A/B and tests)
 int g_term_rows = 2;
+// ring kernel: the x-gradient pass inside up to this width (the half levels, where it replaces a stencil
+// pass); wider levels fold it into the CG glue pass instead (training steps, same box,
+// profiles/r05/term/ab_acc_policy.txt: msgf 65.2 -> 63.8 ms, C4 942 -> 933 ms against the pass inside at
+// every width).  grr_bwd_set_term_acc_max_w (A/B and tests)
+int g_term_acc_max_w = 128;
 
 template <int V> struct RowT;
 template <> struct RowT<1> { typedef float T; };
@@ -1052,7 +1057,6 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
     Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk, int ring_d) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
   constexpr bool kGwDma = !RING && term_gw_dma(MODE, V, STRIPS);
-  static_assert(!(RING && PADJ), "the ring kernel has no x-gradient pass");
   // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats),
   // then (GRR_TERM_GW_DMA) the gw row ring [row parity][plane][element j][lane] (2 WPL 64 V floats)
   extern __shared__ __attribute__((aligned(16))) float part_dyn[];
@@ -1060,8 +1064,12 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   auto gring = [&](int pr, int e) { return part_dyn + (2 * F * WPL + pr * WPL + e) * (64 * V); };
   const int lane = threadIdx.x & 63;
   const int f = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // (PADJ) then this wave's v rows [3][64 V] (lane-major) and gx rows [2][element j][lane]
-  const int ring0 = 2 * F * WPL + (kGwDma ? 2 * WPL : 0);
+  // (PADJ) then this wave's v rows [3][64 V] (lane-major) and gx rows [2][element j][lane]; RING: the v rows
+  // after the ring's slots (gx rows come in the slots)
+  const int ring_fx0 = (F + kRingRows(V) - 1) / kRingRows(V) * kRingRows(V);
+  const int ring_wx0 = (WPL + kRingRows(V) - 1) / kRingRows(V) * kRingRows(V);
+  const int ring0 = RING ? 2 * F * WPL + ring_d * (2 * (ring_fx0 + ring_wx0) + (PADJ ? ring_fx0 : 0))
+                         : 2 * F * WPL + (kGwDma ? 2 * WPL : 0);
   auto vring = [&](int q) { return part_dyn + (ring0 + f * 3 + q % 3) * (64 * V); };
   auto oring = [&](int q) { return part_dyn + (ring0 + 3 * F + f * 2 + (q & 1)) * (64 * V); };
   uint32_t unit = xcd_remap(blockIdx.x, nblk);
@@ -1094,10 +1102,10 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
     cl0 = clampi(c0, 0, W - V);
   }
   const int64_t HW = (int64_t)H * W;
-  // RING: rows per ring slot (x, g of the F channels, WPL weight rows, WPL gw rows; padded to whole DMAs)
-  const int ring_fx = (F + kRingRows(V) - 1) / kRingRows(V) * kRingRows(V);     // x, g block rows
-  const int ring_wx = (WPL + kRingRows(V) - 1) / kRingRows(V) * kRingRows(V);   // w, gw block rows
-  const int ring_rows = 2 * (ring_fx + ring_wx);
+  // RING: rows per ring slot (x, g of the F channels, WPL weight rows, WPL gw rows, (PADJ) the F channels'
+  // gx rows; each block padded to whole DMAs)
+  const int ring_fx = ring_fx0, ring_wx = ring_wx0;   // x, g (gx) / w, gw block rows
+  const int ring_rows = 2 * (ring_fx + ring_wx) + (PADJ ? ring_fx : 0);
   float* const ring = part_dyn + 2 * F * WPL * (64 * V);
   auto rslot = [&](int sl) { return ring + sl * ring_rows * (64 * V); };
   const int t0 = rs - 1, te = re + 1;        // the row loop's steps (output row t - 2)
@@ -1127,6 +1135,7 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
       const float* const gb = g + (int64_t)bg * F * HW;
       const float* const wb0 = w + (int64_t)bg * WPL * HW;
       const float* const gwb0 = gw + (int64_t)bg * WPL * HW;
+      const float* const gxb = PADJ ? gx_out + (int64_t)bg * F * HW : nullptr;
       const int64_t qstep = (int64_t)RPD * HW;   // floats between consecutive DMAs of a block
       auto issue = [&](int t, int sl) {
         float* dst = rslot(sl);
@@ -1152,8 +1161,14 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
         // gw: rows t - 2
         for (int q = 0; q < nfw - 1; ++q, dst += DS) dma_row16(gwb0 + q * qstep + ro2, vo_main, dst);
         dma_row16(gwb0 + (nfw - 1) * qstep + ro2, vo_lastw, dst);
+        if constexpr (PADJ) {   // gx: rows t - 3 (the row P*(v) reaches this step)
+          dst += DS;
+          const int64_t ro3 = (int64_t)clampi(t - 3, 0, H - 1) * W;
+          for (int q = 0; q < nfx - 1; ++q, dst += DS) dma_row16(gxb + q * qstep + ro3, vo_main, dst);
+          dma_row16(gxb + (nfx - 1) * qstep + ro3, vo_lastf, dst);
+        }
       };
-      const int ndma = 2 * nfx + 2 * nfw;
+      const int ndma = 2 * nfx + 2 * nfw + (PADJ ? nfx : 0);
       const int D = ring_d;
       for (int k = 0; k < D - 1; ++k) issue(t0 + k, k);
       vm_wait_rt(ndma * (D - 2));   // step t0's rows landed
@@ -1200,10 +1215,11 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   float dot = 0.f, dgam = 0.f;
 
   auto xrow = [&](float (&d)[V], int rr) { rload<V>(d, xp + (int64_t)clampi(rr, 0, H - 1) * W); };
+  // always one load (a clamped row, zeroed outside the image): the prefetch's load count is fixed, which
+  // the counted vmcnt of the gw / gx LDS-DMA rings below relies on (kAfter)
   auto grow = [&](float (&d)[V], int rr) {
-    if (rr >= 0 && rr < H) {
-      rload<V>(d, gp + (int64_t)rr * W);
-    } else {
+    rload<V>(d, gp + (int64_t)clampi(rr, 0, H - 1) * W);
+    if (rr < 0 || rr >= H) {
 #pragma unroll
       for (int j = 0; j < V; ++j) d[j] = 0.f;
     }
@@ -1241,7 +1257,7 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   if constexpr (kGwDma) gw_dma(r0);
   // (PADJ) gx row q += scale P*(v) (grr_bwd_stencil mode 3's expression, term by term), v rows q - 1 .. q + 1
   // from the ring, gx row q from its LDS-DMA slot
-  auto padj_row = [&](int q) {
+  auto padj_row = [&](int q, const float* gx_lane) {   // gx_lane: RING, this lane's V columns of gx row q
     const float* vc = vring(q);
     const bool top = q == 0, bot = q == H - 1;
     float cv[V], uv[V], dv[V];
@@ -1261,6 +1277,13 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
     const float lv = (c0 > 0 && lane > 0) ? vc[lc0 - 1] : 0.f;
     const float rv = (c0 + V < W && lane < 63) ? vc[lc0 + V] : 0.f;
     const float* os = oring(q) + lane;
+    float gq[V];
+    if constexpr (RING) {
+      rload<V>(gq, gx_lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) gq[j] = os[j * 64];
+    }
     float o[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -1272,7 +1295,7 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
       if (bot) y += k[4] * cv[j];
       if (col == 0) y += k[2] * cv[j];
       if (col == W - 1) y += k[3] * cv[j];
-      o[j] = os[j * 64] + y * sc;
+      o[j] = gq[j] + y * sc;
     }
     if (on) rstore<V>(gxp + (int64_t)q * W, o);
   };
@@ -1452,14 +1475,16 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
     if (own) {
 #pragma unroll
       for (int e = 0; e < WPL; ++e) rstore<V>(part(par, f, e) + lc0, gwa[e]);
-      if constexpr (RING) ring_barrier();
-      else __syncthreads();
+      if constexpr (!RING) __syncthreads();
     }
-    if constexpr (kGwDma || PADJ) {
-      // gw row r / gx row r - 1 landed: copied before this step's prefetch loads (>= 1 + WPL of them,
-      // + the v row store without PADJ; none in the last steps) -- the vector memory counter drains in
-      // order
+    if constexpr (RING) ring_barrier();   // every step, halo rows included (the producer counts them)
+    if constexpr (kGwDma || (PADJ && !RING)) {
+      // gw row r / gx row r - 1 landed: copied before this step's prefetch loads, which issue exactly
+      // 2 + WPL vector loads (x row, g row -- clamped, never skipped --, WPL weight rows: prefetch()), + the v
+      // row store without PADJ; none in the last steps -- the vector memory counter drains in order.  kAfter
+      // counts 1 + WPL of them (<= the issued count: a conservative wait)
       constexpr int kAfter = (MODE == 1 ? 3 : 5) + (PADJ ? 0 : 1);
+      static_assert(kAfter <= 2 + WPL + (PADJ ? 0 : 1), "kAfter must not exceed the loads issued after the DMA");
       if (t + 1 <= re + 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kAfter) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PADJ ? 0 : 1) : "memory");
     }
@@ -1477,7 +1502,7 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
         float* dst = gwb + e * HW + (int64_t)r * W;
         float cv[V];
         if constexpr (RING) {
-          rload<V>(cv, slot_lane + (ring_rows - ring_wx + e) * (64 * V));
+          rload<V>(cv, slot_lane + (2 * ring_fx + ring_wx + e) * (64 * V));
         } else if constexpr (kGwDma) {
           const float* sl = gring(r & 1, e) + lane;
 #pragma unroll
@@ -1500,14 +1525,20 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
     par ^= 1;
     }
     if constexpr (PADJ) {
-      if (r - 1 >= r0 && r - 1 < r1) padj_row(r - 1);
-      if (r >= r0 && r < r1) gx_dma(r);
+      if (r - 1 >= r0 && r - 1 < r1) padj_row(r - 1, slot_lane + (2 * (ring_fx + ring_wx) + f) * (64 * V));
+      if constexpr (!RING) {
+        if (r >= r0 && r < r1) gx_dma(r);
+      }
     }
   }
   if constexpr (PADJ) {
     if (r1 == H) {   // the image's last row: no v row below it
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      padj_row(H - 1);
+      if constexpr (RING) {
+        padj_row(H - 1, gxp + (int64_t)(H - 1) * W);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        padj_row(H - 1, nullptr);
+      }
     }
   }
   // per-graph / per-channel reductions: wave sums into this wave's slots.  Slot of the workgroup:
@@ -1776,7 +1807,7 @@ size_t term_row_lds(int mode, int V, int F, bool strips, bool padj) {
 constexpr size_t kTermLdsMax = 160 * 1024;
 // Shapes the ring kernel takes (g_term_rows == 2): W % 4 == 0 (16-byte DMAs), F + 1 waves within its
 // launch bound, and not the one-column lanes where it measured slower (W <= 32, and the prox term at
-// W <= 64: profiles/r05/term/ab_depth.txt)
+// W <= 64: profiles/r05/term/ab_ring_vs_register.txt)
 bool term_ring_shape_ok(int mode, int F, int W) {
   const int V = term_strip_vec(W, mode);
   if (g_term_rows != 2 || V == 0 || W % 4 != 0 || F > (V == 4 ? TermRingMax<4>::F : TermRingMax<1>::F)) return false;
@@ -1785,23 +1816,30 @@ bool term_ring_shape_ok(int mode, int F, int W) {
 // The ring kernel's depth (steps of rows in LDS) where it applies, else 0: the shape (above) and 16-byte
 // aligned planes.  Depth 4 (three steps of rows ahead): deeper rings measured no faster and cost
 // workgroups per CU (GRR_TERM_RING_D overrides it for A/B).
+// padj: the x-gradient pass inside (gx rows in the slots, three v rows per channel wave after them)
+size_t term_ring_lds(int mode, int V, int F, bool padj, int d, int* ndma_out) {
+  const int wpl = mode == 1 ? 2 : 4, rpd = 4 / V;
+  const int fx = (F + rpd - 1) / rpd, wx = (wpl + rpd - 1) / rpd;
+  const int rows = (2 * (fx + wx) + (padj ? fx : 0)) * rpd;
+  if (ndma_out) *ndma_out = rows / rpd;
+  const size_t row_b = (size_t)64 * V * sizeof(float);
+  return (size_t)2 * F * wpl * row_b + (size_t)d * rows * row_b + (padj ? (size_t)3 * F * row_b : 0);
+}
 int term_ring_depth(int mode, int V, int F, int W, const float* x, const float* g, const float* w, const float* gw,
-                    size_t* lds_out) {
+                    const float* gx, size_t* lds_out) {
   if (!term_ring_shape_ok(mode, F, W)) return 0;
-  const void* ptrs[] = {x, g, w, gw};
+  const void* ptrs[] = {x, g, w, gw, gx};
   for (const void* p : ptrs)
     if ((uintptr_t)p % 16u != 0) return 0;
-  const int wpl = mode == 1 ? 2 : 4, rpd = 4 / V;
-  const int rows = 2 * ((F + rpd - 1) / rpd + (wpl + rpd - 1) / rpd) * rpd, ndma = rows / rpd;
-  const size_t row_b = (size_t)64 * V * sizeof(float);
-  const size_t part_b = (size_t)2 * F * wpl * row_b, slot_b = (size_t)rows * row_b;
   static const int forced = [] {
     const char* e = getenv("GRR_TERM_RING_D");
     return e ? atoi(e) : 0;
   }();
   const int d = forced >= 4 ? forced : 4;
-  if (ndma * (d - 3) > 63 || part_b + d * slot_b > kTermLdsMax) return 0;
-  if (lds_out) *lds_out = part_b + d * slot_b;
+  int ndma = 0;
+  const size_t lds = term_ring_lds(mode, V, F, gx != nullptr, d, &ndma);
+  if (ndma * (d - 3) > 63 || lds > kTermLdsMax) return 0;
+  if (lds_out) *lds_out = lds;
   return d;
 }
 template <int MODE, int V>
@@ -1809,7 +1847,10 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
                            const float* lg, const float* scale, float coef, float* v, float* gx, float* gw,
                            float* ggam, float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
   size_t ring_lds = 0;
-  const int ring_d = (g_term_rows == 2 && gx == nullptr) ? term_ring_depth(MODE, V, F, W, x, g, w, gw, &ring_lds) : 0;
+  const int ring_d = g_term_rows == 2 ? term_ring_depth(MODE, V, F, W, x, g, w, gw, gx, &ring_lds) : 0;
+  GRR_REQUIRE(ring_d || gx == nullptr || (V < 4 && W <= 64 * V), GRR_ERR_UNSUPPORTED,
+              "grr_bwd_term_fused_acc: the x-gradient pass at this width needs the LDS-ring kernel "
+              "(16-byte aligned planes, W %% 4 == 0)");
   // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
   int sseg = H;
   const int step = ring_d ? 64 * V - 8 : 62 * V;   // owned columns per strip
@@ -1830,13 +1871,18 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
   hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, PADJ>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, \
                      scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg,   \
                      nsegs, nblk, 0)
-#define GRR_TERM_RING_LAUNCH(STRIPS)                                                                         \
-  hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, false, true>), dim3(nblk), dim3(64 * (F + 1)), lds, s, x, g, \
+#define GRR_TERM_RING_LAUNCH(STRIPS, PADJ)                                                                   \
+  hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, PADJ, true>), dim3(nblk), dim3(64 * (F + 1)), lds, s, x, g, \
                      taps, w, lg, scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, \
                      W, sseg, nsegs, nblk, ring_d)
   if (ring_d) {
-    if (nstrips > 1) GRR_TERM_RING_LAUNCH(true);
-    else GRR_TERM_RING_LAUNCH(false);
+    if (padj) {
+      if (nstrips > 1) GRR_TERM_RING_LAUNCH(true, true);
+      else GRR_TERM_RING_LAUNCH(false, true);
+    } else {
+      if (nstrips > 1) GRR_TERM_RING_LAUNCH(true, false);
+      else GRR_TERM_RING_LAUNCH(false, false);
+    }
   } else if (padj) {
     if constexpr (V < 4) GRR_TERM_ROW_LAUNCH(false, true);   // term_acc_shape_ok: one strip, V <= 2
   } else if (nstrips > 1) {
@@ -2121,6 +2167,13 @@ int64_t grr_scratch_bytes(void) {
   return (int64_t)g_scratch.total;
 }
 
+grr_status grr_bwd_set_term_acc_max_w(int w) {
+  clear_error();
+  GRR_REQUIRE(w >= 0, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_acc_max_w: w >= 0");
+  g_term_acc_max_w = w;
+  return GRR_OK;
+}
+
 grr_status grr_bwd_set_term_rows(int enable) {
   clear_error();
   GRR_REQUIRE(enable >= 0 && enable <= 2, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_rows: 0, 1 or 2");
@@ -2166,12 +2219,12 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
 }
 
 int grr_bwd_term_acc_supported(int mode, int F, int H, int W) {
-  // the ring kernel (+ the x-gradient pass apart, or folded into the CG glue) measured faster than the
-  // register kernel with the pass inside wherever it applies
-  return mode >= 0 && mode <= 2 && F > 0 && H > 0 && W > 0 && g_term_rows && term_acc_shape_ok(mode, F, W) &&
-                 !term_ring_shape_ok(mode, F, W)
-             ? 1
-             : 0;
+  // the LDS-ring kernel takes the pass wherever it applies (any width: gx rows come in its slots), the
+  // register kernel at one strip of <= 2-column lanes
+  if (mode < 0 || mode > 2 || F <= 0 || H <= 0 || W <= 0 || !g_term_rows) return 0;
+  if (term_ring_shape_ok(mode, F, W))
+    return W <= g_term_acc_max_w && term_ring_lds(mode, term_strip_vec(W, mode), F, true, 4, nullptr) <= kTermLdsMax ? 1 : 0;
+  return term_acc_shape_ok(mode, F, W) ? 1 : 0;
 }
 
 grr_status grr_bwd_term_fused_acc(int mode, const float* x, const float* g, const float* taps, const float* w,

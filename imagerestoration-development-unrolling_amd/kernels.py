@@ -131,6 +131,11 @@ def set_term_rows(enable) -> None:
     TERM_ROWS = level > 0
 
 
+def set_term_acc_max_w(w: int) -> None:
+    """Widest image where the LDS-ring term reverse takes the x-gradient pass inside (default 128)."""
+    _native.call("grr_bwd_set_term_acc_max_w", int(w))
+
+
 def term_rows_ok(w: int, f: int) -> bool:
     """Widths / channel counts the row-streaming term reverse takes (16-byte aligned planes assumed)."""
     if w <= 64:

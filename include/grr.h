@@ -393,9 +393,13 @@ grr_status grr_bwd_pair(const float* s, const float* a, const float* c, const fl
 grr_status grr_bwd_prox(const float* s, const float* a, const float* w, const float* log_gamma,
                         const float* scale, float coef, float* o_out, float* gs_out, float* gw,
                         float* ggamma, float* gdot, int B, int G, int F, int H, int W, void* stream);
-/* Kernel knob for tests and benchmarks (no reference counterpart): 1 (default) runs
- * grr_bwd_term_fused and grr_bwd_edge_weights as row-streaming kernels where W <= 256, 0 always as
- * the per-pixel kernels.
+/* Widest image at which grr_bwd_term_acc_supported offers the LDS-ring row kernel with the x-gradient pass
+ * inside (default 128; wider levels fold that pass into grr_bwd_cg_glue).  A/B and test knob. */
+grr_status grr_bwd_set_term_acc_max_w(int w);
+/* Kernel knob for tests and benchmarks (no reference counterpart): 2 (default) runs grr_bwd_term_fused
+ * (and _acc) as the LDS-ring row kernel where the shape allows (W % 4 == 0, F <= 7 at 4-column lanes /
+ * 12 below, 16-byte aligned planes), else as the register-prefetch row kernel; 1 always the register
+ * kernel; 0 the per-pixel kernels.  grr_bwd_edge_weights: row kernel for 1 and 2.
  * Process-wide; results agree to fp32 rounding. */
 grr_status grr_bwd_set_term_rows(int enable);
 

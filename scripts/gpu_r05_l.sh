@@ -15,10 +15,10 @@ timeout -k 10 300 python -u bench_train.py --model abstract --batch 8 --steps 5 
 timeout -k 10 600 python -u bench_train.py --model abstract --size 512 --batch 32 --steps 3 --warmup 1 --no-cpu-baseline \
   > $out/train_c4.json 2> $out/train_c4.err || { tail $out/train_c4.err; exit 1; }
 for f in train_msgf train_abstract train_c4; do echo "$f $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"peak_mem_gb": [0-9.]*' $out/$f.json | tr '\n' ' ')"; done
-python - <<'PY'
-import json
+python - $out <<'PY'
+import json, sys
 for n in ("train_msgf", "train_abstract", "train_c4"):
-    d = json.load(open(f"gpurun_out/r05l/{n}.json"))
+    d = json.load(open(f"{sys.argv[1]}/{n}.json"))
     k = d.get("kernel_ms_per_step", {})
     print(n, {x: k[x] for x in ("bwd_term_fused", "bwd_cg_glue", "bwd_stencil", "wgrad", "conv1x1", "lnb_gate_dw3_bwd") if x in k})
 PY

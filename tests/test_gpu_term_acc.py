@@ -28,11 +28,15 @@ def K():
     import irdu_amd
     irdu_amd.load_native()
     from irdu_amd import kernels
-    # the pass runs in the register-prefetch row kernel (level 1); the default LDS-ring kernel (level 2)
-    # declines it where the ring applies (measured faster with the x-gradient pass apart)
-    kernels.set_term_rows(1)
+    kernels.set_term_acc_max_w(1 << 20)   # the ring kernel's pass at every width (default: W <= 128)
     yield kernels
+    kernels.set_term_acc_max_w(128)
     kernels.set_term_rows(True)
+
+
+# level 1: the register-prefetch row kernel (one strip of <= 2-column lanes); level 2 (default): the
+# LDS-ring kernel wherever it applies (gx rows in its slots: every width, strips included), else level 1
+LEVELS = [1, 2]
 
 
 def _inputs(mode, case):
@@ -56,12 +60,14 @@ def _bufs(mode, w, taps, G):
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_term_acc_equals_two_pass(K, case, mode):
+@pytest.mark.parametrize("level", LEVELS)
+def test_term_acc_equals_two_pass(K, case, mode, level):
     b, G, F, h, w_ = case
+    K.set_term_rows(level)
     x, g, taps, w, lg, scale, gx0 = _inputs(mode, case)
     if not K.term_acc_ok(mode, x, G, g, gx0):
-        # W > 128 (4-column lanes, strips) stays on the two-pass path (measured slower fused)
-        assert w_ > 128, (mode, case)
+        # register kernel: W > 128 (4-column lanes, strips) stays on the two-pass path
+        assert level == 1 and w_ > 128, (mode, case)
         return
     gw_r, gg_r, gd_r, gt_r = _bufs(mode, w, taps, G)
     v = K.bwd_term_fused(mode, x, g, taps, w, lg, scale, 0.7, gw_r, gg_r, gd_r, gt_r, G)
@@ -81,9 +87,11 @@ def test_term_acc_equals_two_pass(K, case, mode):
         assert err <= 1e-5 * max(float(r.abs().max()), 1.0), (name, err)
 
 
-def test_glr_then_pair_equals_padj2(K):
+@pytest.mark.parametrize("level,case", [(1, (2, 4, 3, 70, 128)), (2, (2, 4, 3, 70, 128)), (2, (1, 2, 6, 40, 512)),
+                                        (2, (2, 4, 3, 33, 256))])
+def test_glr_then_pair_equals_padj2(K, level, case):
     """Two accumulating calls on one gx (GLR, then pair: the level's terms_bwd) equal the padj2 sweep."""
-    case = (2, 4, 3, 70, 128)
+    K.set_term_rows(level)
     b, G, F, h, w_ = case
     x, g, taps0, w0, _, s0, gx0 = _inputs(0, case)
     _, _, taps1, w1, _, s1, _ = _inputs(1, case)
@@ -99,8 +107,10 @@ def test_glr_then_pair_equals_padj2(K):
     assert rel_err(gx_a.cpu(), gx_r.cpu()) <= 1e-6
 
 
-def test_training_gradients_with_and_without_acc(K):
+@pytest.mark.parametrize("level", LEVELS)
+def test_training_gradients_with_and_without_acc(K, level):
     """msgf's mixture reverse with the fused x-gradient passes against the two-pass path."""
+    K.set_term_rows(level)
     import irdu_amd
     from irdu_amd import solver_grad as SG
     from tests.test_gpu_parity import perturb_mixture
