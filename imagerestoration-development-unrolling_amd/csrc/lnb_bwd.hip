@@ -758,6 +758,195 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
   if (q.lane == 0) red_put(gdot, 0, q.wid, d);
 }
 
+// The same reverse (recomputing the depthwise output from hh, the training path) with its operand rows
+// through a per-wave LDS ring (round 5): each wave DMAs the rows of iteration r + 3 -- gq row r + 4 and the
+// two hh rows r + 5 -- into slot (r + 3) mod 4 of its own ring (16-byte LDS-DMA, one scalar base per row,
+// a loop-invariant lane offset; lanes >= 16 V idle at V < 4) and waits with a counted vmcnt, so no load
+// latency sits on the row loop (the register kernel loaded its hh rows and used them at once: 0.34 of HBM
+// at C4).  The hh rows of the window (r - 1 .. r + 2) serve both the recomputed depthwise output and the
+// weight gradient (the register kernel loaded them twice).  Same expressions and order as
+// dw3_gate_row_bwd_kernel<V, true>: the outputs agree to fp32 contraction, the reductions bitwise.
+constexpr int DW3R_D = 4;   // ring slots (DMAs DW3R_D - 1 iterations ahead)
+// grr_lnb_set_bwd_ring: 1 (default) the ring kernel where it applies (W % 4 == 0, 16-byte aligned planes),
+// 0 the register kernel (A/B and tests)
+int g_dw3_bwd_ring = 1;
+#define HW_ALIGNED(H, W) (((int64_t)(H) * (W)) % 4 == 0)
+__device__ __forceinline__ void dma_row16s(const float* sbase, uint32_t voff, float* lds_dst) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_dst;
+  asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
+               : "memory");
+}
+// a wave-uniform pointer the compiler cannot prove uniform (derived from threadIdx.x >> 6) into SGPRs
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+template <int V>
+__global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
+    const float* __restrict__ gq, const float* __restrict__ scale, const float* __restrict__ hh,
+    const float* __restrict__ wdw, float* __restrict__ gh, Red gw, Red gdot, int hid, int H, int W, int sseg,
+    int nsegs, uint32_t nwaves) {
+  extern __shared__ __attribute__((aligned(16))) float dw3_ring[];
+  Dw3RowGeom q;
+  if (!dw3_row_geom<V>(q, hid, H, W, sseg, nsegs, nwaves)) return;   // q.plane = b hid + j, q.c = j
+  constexpr int RW = 64 * V;                                          // floats per ring row
+  float* const ring = dw3_ring + (threadIdx.x >> 6) * (DW3R_D * 3 * RW);
+  const int64_t HW = (int64_t)H * W;
+  const int64_t bq = q.plane / hid, j = q.c;
+  const int64_t pm0 = (bq * 2 * hid + j) * HW, pv0 = pm0 + (int64_t)hid * HW;
+  const float* const gq0 = gq + (int64_t)q.plane * HW;   // plane bases (wave-uniform; SGPRs at the DMA)
+  const float* const hm0 = hh + pm0;
+  const float* const hv0 = hh + pv0;
+  // the lane's 16-byte chunk of a row (16 V lanes per row; W % 4 == 0): the strip's columns x0 + 4 lane
+  const int x0 = q.c0 - V * q.lane;
+  const uint32_t voff = (uint32_t)min(x0 + 4 * q.lane, W - 4) * 4u;
+  const bool dma_lane = q.lane < 16 * V;
+  auto issue = [&](int r, int sl) {   // rows of iteration r: gq row r + 1, hh rows r + 2
+    if (dma_lane) {
+      float* dst = ring + sl * (3 * RW);
+      dma_row16s(uniform_ptr(gq0 + (int64_t)clampi(r + 1, 0, H - 1) * W), voff, dst);
+      dma_row16s(uniform_ptr(hm0 + (int64_t)clampi(r + 2, 0, H - 1) * W), voff, dst + RW);
+      dma_row16s(uniform_ptr(hv0 + (int64_t)clampi(r + 2, 0, H - 1) * W), voff, dst + 2 * RW);
+    }
+  };
+  // the first DW3R_D - 1 iterations' rows
+#pragma unroll
+  for (int k = 0; k < DW3R_D - 1; ++k) issue(q.r0 + k, k);
+  const float s = scale[0];
+  float wm[9], wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wm[t] = wdw[j * 9 + t];
+    wv[t] = wdw[(hid + j) * 9 + t];
+  }
+  float accm[9], accv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) accm[t] = accv[t] = 0.f;
+  float dot = 0.f;
+  const float* const qp = gq0 + q.cl0;
+  const float* const hmp = hm0 + q.cl0;
+  const float* const hvp = hv0 + q.cl0;
+  // windows: hh rows r-1 .. r+2 (Hm / Hv[0..3]), ghp rows r-1 .. r+1 (Gm / Gv[0..2])
+  float Hm[4][V], Hv[4][V], Gm[3][V], Gv[3][V];
+  auto ghp_row = [&](int rr, const float (&g)[V], const float (&R0m)[V], const float (&R1m)[V], const float (&R2m)[V],
+                     const float (&R0v)[V], const float (&R1v)[V], const float (&R2v)[V], float (&dm)[V],
+                     float (&dv)[V]) {
+    float NM[V], NV[V];
+    dw3_row_out<V, false>(R0m, R1m, R2m, wm, q.c0, W, NM);
+    dw3_row_out<V, false>(R0v, R1v, R2v, wv, q.c0, W, NV);
+    const bool in = rr >= 0 && rr < H;
+    const bool own = q.on && rr >= q.r0 && rr < q.r1;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float m = NM[k], v = NV[k], gg0 = g[k];
+      float gf, dgf;
+      gate_d<false>(m, gf, dgf);
+      if (own) dot += gg0 * (gf * v);
+      const float gg = s * gg0;
+      dm[k] = in ? gg * v * dgf : 0.f;
+      dv[k] = in ? gg * gf : 0.f;
+    }
+  };
+  {   // prologue: hh rows r0-2 .. r0+1 and gq rows r0-1, r0 by plain loads; ghp rows r0-1, r0
+    float X0m[V], X0v[V], g0[V], g1[V];
+    row_load_pad<V, false>(X0m, hmp, q.r0 - 2, H, W);
+    row_load_pad<V, false>(X0v, hvp, q.r0 - 2, H, W);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      row_load_pad<V, false>(Hm[d], hmp, q.r0 - 1 + d, H, W);
+      row_load_pad<V, false>(Hv[d], hvp, q.r0 - 1 + d, H, W);
+    }
+    row_load_pad<V, false>(g0, qp, q.r0 - 1, H, W);
+    row_load_pad<V, false>(g1, qp, q.r0, H, W);
+    ghp_row(q.r0 - 1, g0, X0m, Hm[0], Hm[1], X0v, Hv[0], Hv[1], Gm[0], Gv[0]);
+    ghp_row(q.r0, g1, Hm[0], Hm[1], Hm[2], Hv[0], Hv[1], Hv[2], Gm[1], Gv[1]);
+  }
+  // one plane's data adjoint (row r) and weight-gradient contribution: dw3_gate_row_bwd_kernel's
+  auto plane = [&](const float (&G)[3][V], const float (&Hp0)[V], const float (&Hp1)[V], const float (&Hp2)[V],
+                   const float (&wt)[9], float (&acc)[9], int r, float* dst) {
+    const float* Hp[3] = {Hp0, Hp1, Hp2};
+    float A[3][V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      A[0][k] = r == 0 ? G[2][k] + G[1][k] : G[2][k];
+      A[1][k] = G[1][k];
+      A[2][k] = r == H - 1 ? G[0][k] + G[1][k] : G[0][k];
+    }
+    float o[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float pvv = dpp_prev(A[dy][V - 1]), nx = dpp_next(A[dy][0]);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const int col = q.c0 + k;
+        const float a = A[dy][k];
+        const float al = k > 0 ? A[dy][k - 1] : pvv;
+        const float ar = k < V - 1 ? A[dy][k + 1] : nx;
+        const float sm = col + 1 < W ? (col == 0 ? ar + a : ar) : (col == 0 ? a : 0.f);
+        const float sp = col >= 1 ? (col == W - 1 ? al + a : al) : (col == W - 1 ? a : 0.f);
+        o[k] += wt[dy * 3 + 0] * sm;
+        o[k] += wt[dy * 3 + 1] * a;
+        o[k] += wt[dy * 3 + 2] * sp;
+      }
+    }
+    if (q.on) row_store<V>(dst + (int64_t)r * W, o);
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float* Hd = Hp[dy];
+      const float pvv = dpp_prev(Hd[V - 1]), nx = dpp_next(Hd[0]);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const int col = q.c0 + k;
+        const float gv = q.on ? G[1][k] : 0.f;
+        const float l = col > 0 ? (k > 0 ? Hd[k - 1] : pvv) : Hd[k];
+        const float rr = col < W - 1 ? (k < V - 1 ? Hd[k + 1] : nx) : Hd[k];
+        acc[dy * 3 + 0] += gv * l;
+        acc[dy * 3 + 1] += gv * Hd[k];
+        acc[dy * 3 + 2] += gv * rr;
+      }
+    }
+  };
+  float* const ghm = gh + pm0 + q.cl0;
+  float* const ghv = gh + pv0 + q.cl0;
+  int sl = 0;
+  for (int r = q.r0; r < q.r1; ++r) {
+    // iteration r's rows landed: after them the wave issued the next DW3R_D - 2 iterations' DMAs (3 each)
+    // and its own stores (vmcnt counts those too: the wait is conservative)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (DW3R_D - 2)) : "memory");
+    const float* slot = ring + sl * (3 * RW) + V * q.lane;
+    float g2[V];
+    row_load<V>(g2, slot);                  // gq row r + 1
+    row_load<V>(Hm[3], slot + RW);          // hh rows r + 2
+    row_load<V>(Hv[3], slot + 2 * RW);
+    ghp_row(r + 1, g2, Hm[1], Hm[2], Hm[3], Hv[1], Hv[2], Hv[3], Gm[2], Gv[2]);
+    plane(Gm, Hm[0], Hm[1], Hm[2], wm, accm, r, ghm);
+    plane(Gv, Hv[0], Hv[1], Hv[2], wv, accv, r, ghv);
+    issue(r + DW3R_D - 1, sl == 0 ? DW3R_D - 1 : sl - 1);   // the slot iteration r - 1 read
+    sl = sl == DW3R_D - 1 ? 0 : sl + 1;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      Gm[0][k] = Gm[1][k]; Gm[1][k] = Gm[2][k];
+      Gv[0][k] = Gv[1][k]; Gv[1][k] = Gv[2][k];
+      Hm[0][k] = Hm[1][k]; Hm[1][k] = Hm[2][k]; Hm[2][k] = Hm[3][k];
+      Hv[0][k] = Hv[1][k]; Hv[1][k] = Hv[2][k]; Hv[2][k] = Hv[3][k];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into LDS at the wave's end
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const float a = wave_sum(accm[t]), b = wave_sum(accv[t]);
+    if (q.lane == 0) {
+      red_put(gw, (int)j * 9 + t, q.slot, a);
+      red_put(gw, (hid + (int)j) * 9 + t, q.slot, b);
+    }
+  }
+  const float d = wave_sum(dot);
+  if (q.lane == 0) red_put(gdot, 0, q.wid, d);
+}
+
 // V for the row kernels (0: not applicable -> per-pixel kernels)
 // W > 256: column strips of GRR_DW3_WIDE_V-wide lanes with a V-column halo (the fused gate + depthwise
 // reverse reaches two columns: V >= 2)
@@ -832,7 +1021,11 @@ grr_status launch_dw3_gate_row(const float* hp, const float* gq, const float* sc
   grr_status st = rs.alloc(what);
   if (st != GRR_OK) return st;
   const Red gw = rs.red(iw), gdot = rs.red(id);
-  if constexpr (FFN) {   // the FeedForward reverse always recomputes the depthwise output
+  if (!FFN && !hp && g_dw3_bwd_ring && W % 4 == 0 && (uintptr_t)gq % 16 == 0 && (uintptr_t)hh % 16 == 0 &&
+      HW_ALIGNED(H, W)) {
+    hipLaunchKernelGGL(dw3_gate_row_bwd_ring_kernel<V>, grid, dim3(NT), (NT / 64) * DW3R_D * 3 * 64 * V * sizeof(float),
+                       s, gq, scale, hh, wdw, gh, gw, gdot, hid, H, W, sseg, nsegs, nwaves);
+  } else if constexpr (FFN) {   // the FeedForward reverse always recomputes the depthwise output
     hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, true, true>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw,
                        gdot, hid, H, W, sseg, nsegs, nwaves);
   } else if (hp) {
@@ -989,6 +1182,13 @@ grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int 
     default: launch_dw3_gate_fwd_row<4>(hh, wdw, gate, B, hid, H, W, s); break;
   }
   return launch_status("grr_lnb_dw3_gate");
+}
+
+grr_status grr_lnb_set_bwd_ring(int enable) {
+  clear_error();
+  GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_lnb_set_bwd_ring: 0 or 1");
+  g_dw3_bwd_ring = enable;
+  return GRR_OK;
 }
 
 grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* scale, const float* hh,

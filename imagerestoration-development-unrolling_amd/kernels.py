@@ -1091,6 +1091,11 @@ def lnb_gate_dw3_ok(h: int, w: int) -> bool:
     return (w <= 64) or (w <= 128 and w % 2 == 0) or (w % 4 == 0)
 
 
+def set_lnb_bwd_ring(enable: bool) -> None:
+    """The LDS-ring gate + depthwise reverse (True, default) or the register row kernel (grr_lnb_set_bwd_ring)."""
+    _native.call("grr_lnb_set_bwd_ring", int(bool(enable)))
+
+
 def lnb_gate_dw3_bwd(hp: Optional[Tensor], gq: Tensor, scale: Tensor, hh: Tensor, wdw: Tensor, gwdw: Tensor,
                      gdot: Tensor) -> Tensor:
     """Gate reverse + depthwise reverse in one row pass (grr_lnb_gate_dw3_bwd): returns gh.

@@ -489,6 +489,10 @@ grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float
  * depthwise output itself is not stored).  W <= 256 with W % V == 0, else GRR_ERR_UNSUPPORTED. */
 grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
                             void* stream);
+/* Kernel knob (no reference counterpart): 1 (default) runs grr_lnb_gate_dw3_bwd's recomputing variant (hp NULL)
+ * with its operand rows through a per-wave LDS-DMA ring where W % 4 == 0 and the planes are 16-byte aligned,
+ * 0 the register-prefetch row kernel.  Process-wide; results agree to fp32 rounding.  A/B and tests. */
+grr_status grr_lnb_set_bwd_ring(int enable);
 /* grr_lnb_gate_bwd_scaled and grr_dwconv3_bwd in one row pass (ghp stays on chip): hp [B,2hid,H,W]
  * (depthwise output; NULL = recomputed from hh in-kernel), gq [B,hid,H,W], hh [B,2hid,H,W]
  * (depthwise input), wdw [2hid,9] ->

@@ -92,3 +92,37 @@ def test_gate_dw3_rows_vs_autograd(K, shape, ffn):
     assert rel_err(gh.cpu(), hr.grad) <= 2e-5
     assert rel_err(gw.cpu(), wr.grad) <= 2e-5
     assert abs(float(gdot) - float((gq * gate).sum())) <= 2e-5 * float((gq * gate).abs().sum())
+
+
+RING_SHAPES = [(2, 3, 9, 32), (1, 4, 20, 100), (1, 2, 33, 256), (1, 2, 10, 300), (1, 3, 12, 512), (1, 1, 6, 744),
+               (1, 2, 300, 64), (1, 2, 1, 64), (1, 2, 2, 128), (2, 1, 5, 1000), (1, 5, 40, 200), (1, 2, 7, 102)]
+
+
+@pytest.mark.parametrize("shape", RING_SHAPES, ids=lambda s: "b{}hid{}h{}w{}".format(*s))
+def test_gate_dw3_bwd_ring_equals_register_kernel(K, shape):
+    """grr_lnb_gate_dw3_bwd's per-wave LDS-ring kernel (default) against the register row kernel: the same
+    expressions in the same order (gh to fp32 contraction, the weight-gradient and <gq, gate> reductions to
+    summation order); segmented grids (300 rows), 1- and 2-row images, strips (W > 256), W % 4 != 0 (the ring
+    declines: the register kernel runs both)."""
+    b, hid, hh_, ww = shape
+    torch.manual_seed(hh_ * 13 + ww)
+    hh = torch.randn(b, 2 * hid, hh_, ww, device=DEV)
+    w = torch.randn(2 * hid, 9, device=DEV) * 0.5
+    gq = torch.randn(b, hid, hh_, ww, device=DEV)
+    sc = torch.tensor([0.7], device=DEV)
+    res = {}
+    try:
+        for ring in (False, True):
+            K.set_lnb_bwd_ring(ring)
+            gw = torch.zeros(2 * hid, 9, device=DEV)
+            gdot = torch.zeros(1, device=DEV)
+            gh = K.lnb_gate_dw3_bwd(None, gq, sc, hh, w, gw, gdot)
+            torch.cuda.synchronize()
+            res[ring] = (gh.cpu(), gw.cpu(), gdot.cpu())
+    finally:
+        K.set_lnb_bwd_ring(True)
+    (g1, w1, d1), (g0, w0, d0) = res[True], res[False]
+    assert torch.isfinite(g1).all()
+    assert rel_err(g1, g0) <= 2e-6, rel_err(g1, g0)
+    assert rel_err(w1, w0) <= 1e-5, rel_err(w1, w0)
+    assert abs(float(d1) - float(d0)) <= 1e-5 * max(1.0, abs(float(d0))) * (b * hid * hh_ * ww) ** 0.5
