@@ -367,6 +367,16 @@ def main():
             "note": "algorithmic fp32 flops (LN, W1, depthwise, gate, W2, skip) / HIP-event time against the "
                     "dense fp16 rate / 3 (both GEMMs on exact fp16 two-term splits; the depthwise folded into "
                     "GEMM1 as a 27-deep im2col operand); bytes: src in, out written"}
+    if "system_first_pair" in kern:   # stage 0 + prox rhs B + stage 1 in one pass
+        fp = kern["system_first_pair"]
+        res.setdefault("roofline_secondary", {})["system_first_pair"] = {
+            "bound": "hbm", "kernel": "graph_step2_kernel<false, false, true> (grr_system_first_pair)",
+            "achieved": round(fp["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(fp["gbps"] / HBM_PEAK_GBPS, 4), "bytes_per_launch": fp["bytes_per_launch"],
+            "mean_launch_ms": round(fp["mean_ms"], 4), "launches": fp["launches"],
+            "traffic": load_traffic_file("traffic_system_first_pair.json", "graph_step2_kernel", b),
+            "note": "algorithmic bytes (kernels.first_pair_bytes: b_A, D b_A, y, three full- and three half-level "
+                    "weight planes sets read once; b_B, x_2, u_2, D x_2 written) / HIP-event time"}
     kernels_ms = {k: round(v["total_ms"] / n_inst, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms
     if args.breakdown:

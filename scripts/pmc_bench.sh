@@ -15,8 +15,9 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $CMD \
   > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail -5 $OUT/trace.log; exit 1; }
-for spec in "graph_step2_kernel:profiles/traffic_system_step2.json" "lnb_fused16_kernel:profiles/r05/traffic_lnb_fused.json" \
-            "lnb_rep_kernel:profiles/r05/traffic_lnb_rep.json"; do
+for spec in "graph_step2_kernel<false, false, false>:profiles/traffic_system_step2.json" \
+            "graph_step2_kernel<false, false, true>:profiles/r05/traffic_system_first_pair.json" \
+            "lnb_fused16_kernel:profiles/r05/traffic_lnb_fused.json" "lnb_rep_kernel:profiles/r05/traffic_lnb_rep.json"; do
   python scripts/collect_traffic.py $OUT/FETCH_SIZE $OUT/WRITE_SIZE --kernel "${spec%%:*}" --out "$OUT/$(basename ${spec#*:})" \
     --batch $B --size 256 || exit 1
 done
