@@ -1172,6 +1172,9 @@ __device__ unsigned long long g_fused_stamps[1024 * 8 * 8];
   do {            \
   } while (0)
 #endif
+#ifndef GRR_FUSED_PKFMA   // the gate's depthwise sums of the mask and value planes as packed FMAs (A/B: 0)
+#define GRR_FUSED_PKFMA 1
+#endif
 #ifndef GRR_FUSED_AHEAD   // pairs of taps + windows in flight ahead of the consumer's gate (1 or 2)
 #define GRR_FUSED_AHEAD 1
 #endif
@@ -1538,25 +1541,27 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
       float g[2][8];
       // One pair per step, the next pair's taps and window in flight (LDS reads count in order: the
       // compiler waits for this pair's only); the scheduling barrier keeps each step's loads in it
-      float tA[18];
+      // taps as (mask, value) pairs: the two planes' depthwise sums run as one packed FMA chain
+      // (v_pk_fma_f32: the same fp32 fma per component, half the instructions)
+      f32x2 tA[9];
       f32x2 wA[12];
-      auto load = [&](int jj, float (&t)[18], f32x2 (&w)[12]) {
+      auto load = [&](int jj, f32x2 (&t)[9], f32x2 (&w)[12]) {
         const float* tp = tap0 + jj * 18;
 #pragma unroll
-        for (int u = 0; u < 18; ++u) t[u] = tp[u];
+        for (int u = 0; u < 9; ++u) t[u] = *reinterpret_cast<const f32x2*>(tp + 2 * u);
         const float* hp = hwin + jj * LF_PP;
 #pragma unroll
         for (int u = 0; u < 12; ++u) w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
       };
       load(0, tA, wA);
 #if GRR_FUSED_AHEAD == 2
-      float tN[18];
+      f32x2 tN[9];
       f32x2 wN[12];
       load(1, tN, wN);
 #endif
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        float tB[18];
+        f32x2 tB[9];
         f32x2 wB[12];
 #if GRR_FUSED_AHEAD == 2
         // two pairs in flight: pair jj + 2 issued, pair jj + 1 (tN, wN) landing, pair jj computed
@@ -1566,33 +1571,40 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
 #endif
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
-          float m = tA[0] * wA[3 * rb][0], v = tA[1] * wA[3 * rb][1];
+#if GRR_FUSED_PKFMA
+          f32x2 mv = tA[0] * wA[3 * rb];
+#pragma unroll
+          for (int t = 1; t < 9; ++t) mv = __builtin_elementwise_fma(tA[t], wA[3 * (rb + t / 3) + t % 3], mv);
+          const float m = mv[0], v = mv[1];
+#else
+          float m = tA[0][0] * wA[3 * rb][0], v = tA[0][1] * wA[3 * rb][1];
 #pragma unroll
           for (int t = 1; t < 9; ++t) {
             const f32x2 hv = wA[3 * (rb + t / 3) + t % 3];
-            m = __builtin_fmaf(tA[2 * t], hv[0], m);
-            v = __builtin_fmaf(tA[2 * t + 1], hv[1], v);
+            m = __builtin_fmaf(tA[t][0], hv[0], m);
+            v = __builtin_fmaf(tA[t][1], hv[1], v);
           }
+#endif
           // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
           g[rb][jj] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
         }
 #if GRR_FUSED_AHEAD == 2
         if (jj < 7) {
 #pragma unroll
-          for (int u = 0; u < 18; ++u) tA[u] = tN[u];
+          for (int u = 0; u < 9; ++u) tA[u] = tN[u];
 #pragma unroll
           for (int u = 0; u < 12; ++u) wA[u] = wN[u];
         }
         if (jj < 6) {
 #pragma unroll
-          for (int u = 0; u < 18; ++u) tN[u] = tB[u];
+          for (int u = 0; u < 9; ++u) tN[u] = tB[u];
 #pragma unroll
           for (int u = 0; u < 12; ++u) wN[u] = wB[u];
         }
 #else
         if (jj < 7) {
 #pragma unroll
-          for (int u = 0; u < 18; ++u) tA[u] = tB[u];
+          for (int u = 0; u < 9; ++u) tA[u] = tB[u];
 #pragma unroll
           for (int u = 0; u < 12; ++u) wA[u] = wB[u];
         }
