@@ -65,7 +65,7 @@ SIGNATURES = {
     "grr_system_first_pair": [P, P, P, I, P, P, P, Stencil, Stencil, P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, P,
                               P, P, P, P, I, I, I, I, I, P],
     "grr_system_step2_train": [P, P, P, P, P, P, Stencil, Stencil, P, P, P, P, Stencil, Stencil, P, P, P, P, P, P,
-                               P, P, P, P, P, I, I, I, I, I, P],
+                               P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_glr_stage": [P, P, P, P, Stencil, P, P, P, P, P, I, I, I, I, I, P],
     "grr_conv1x1": [P, P, P, I, I, I, L, P],
     "grr_conv1x1_workspace_bytes": [I, I],

@@ -1380,6 +1380,7 @@ struct Step2Args {
   float* xd_out;
   float* x_mid;          // training: x_{k+1} and u_{k+1} (the reverse sweep's saved iterates), or NULL
   float* u_mid;
+  float* xd_mid;         // training: D x_{k+1} (the reverse sweep's half-level operand), or NULL
   // first pair (graph_step2_kernel<false, false, true>): stage 0, the prox right-hand side B, stage 1
   const float* wG0;      // raw GTV weights [B,G,4,H,W] / [B,G,4,h,w] of the prox terms
   const float* wG1;
@@ -1912,6 +1913,7 @@ void graph_step2_kernel(Step2Args a) {
   // inference kernel keeps its registers)
   const rsrc_t rxm = make_rsrc(MID ? a.x_mid + plane : nullptr, MID ? PB : 0);
   const rsrc_t rum = make_rsrc(MID ? a.u_mid + plane : nullptr, MID ? PB : 0);
+  const rsrc_t rxdm = make_rsrc(MID && a.xd_mid ? a.xd_mid + hplane : nullptr, MID && a.xd_mid ? HPB : 0);
 
   const float scl0 = expf(a.log_mu0[g]), scg0 = expf(a.log_ro0[g]);
   // absent terms enter as exact zeros / ones: u_prev reads 0 (beta 0), y reads 0 (skip 0, 1)
@@ -2033,13 +2035,14 @@ void graph_step2_kernel(Step2Args a) {
       for (int j = 0; j < V; ++j) xa0[j] = xn[j];
     } else {
       const int hA = (y - 1) / 2;
-      if (hA >= 0 && hA < h) {
-        F2 qv;
+      float d[VH];
 #pragma unroll
-        for (int k = 0; k < VH; ++k)
-          qv[k] = 0.25f * xa0[2 * k] + 0.25f * xa0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
-        *reinterpret_cast<F2*>(dr + (hA & (S2_DR - 1)) * S2_HW) = qv;
-      }
+      for (int k = 0; k < VH; ++k)
+        d[k] = 0.25f * xa0[2 * k] + 0.25f * xa0[2 * k + 1] + 0.25f * xn[2 * k] + 0.25f * xn[2 * k + 1];
+      if (hA >= 0 && hA < h) *reinterpret_cast<F2*>(dr + (hA & (S2_DR - 1)) * S2_HW) = F2{d[0], d[1]};
+      // training: D x_{k+1} to HBM (the reverse sweep's half-level operand), the values stage B read
+      if constexpr (MID)
+        bstore<VH>(rxdm, (y >= r0 && y < r1 && own) ? vo_half + (uint32_t)hA * HRB : GRR_OOB, d);
     }
   };
 
@@ -2473,8 +2476,8 @@ static grr_status system_step2_impl(const float* x, const float* b, const float*
                                     grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
                                     const float* alpha_a, const float* beta_a, const float* alpha_b,
                                     const float* beta_b, const float* skip, const float* y_skip, float* x_out,
-                                    float* u_out, float* xd_out, float* x_mid, float* u_mid, int B, int G, int F,
-                                    int H, int W, void* stream) {
+                                    float* u_out, float* xd_out, float* x_mid, float* u_mid, float* xd_mid, int B,
+                                    int G, int F, int H, int W, void* stream) {
   GRR_REQUIRE(x && b && xd && wL0 && cG0 && wL1 && cG1 && log_mu0 && log_ro0 && log_mu1 && log_ro1 && alpha_a &&
                   alpha_b && x_out && B > 0 && G > 0 && F > 0 && H > 0 && W > 0,
               GRR_ERR_INVALID_ARG, "grr_system_step2: bad args");
@@ -2487,11 +2490,11 @@ static grr_status system_step2_impl(const float* x, const float* b, const float*
   GRR_REQUIRE((int64_t)H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED, "grr_system_step2: plane too large");
   GRR_REQUIRE(x_out != x && x_out != b && x_out != u_prev && (!u_out || (u_out != u_prev && u_out != x && u_out != b)),
               GRR_ERR_INVALID_ARG, "grr_system_step2: outputs must not alias the inputs (rows are read ahead)");
-  const void* ptrs[] = {x, b, u_prev, xd, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out, x_mid, u_mid};
+  const void* ptrs[] = {x, b, u_prev, xd, wL0, cG0, wL1, cG1, y_skip, x_out, u_out, xd_out, x_mid, u_mid, xd_mid};
   for (const void* q : ptrs)
     GRR_REQUIRE((uintptr_t)q % 16 == 0, GRR_ERR_INVALID_ARG, "grr_system_step2: operands must be 16-byte aligned");
   Step2Args a{};
-  a.x_mid = x_mid; a.u_mid = u_mid;
+  a.x_mid = x_mid; a.u_mid = u_mid; a.xd_mid = xd_mid;
   a.x = x; a.b = b; a.u_prev = u_prev; a.xd = xd;
   a.wL0 = wL0; a.cG0 = cG0; a.wL1 = wL1; a.cG1 = cG1;
   a.sL0 = sL0; a.sG0 = sG0; a.sL1 = sL1; a.sG1 = sG1;
@@ -2529,7 +2532,7 @@ grr_status grr_system_step2(const float* x, const float* b, const float* u_prev,
   clear_error();
   return system_step2_impl(x, b, u_prev, xd, wL0, cG0, sL0, sG0, log_mu0, log_ro0, wL1, cG1, sL1, sG1, log_mu1,
                            log_ro1, alpha_a, beta_a, alpha_b, beta_b, skip, y_skip, x_out, u_out, xd_out, nullptr,
-                           nullptr, B, G, F, H, W, stream);
+                           nullptr, nullptr, B, G, F, H, W, stream);
 }
 
 // Stage 0, the prox right-hand side B and stage 1 in one pass (graph_step2_kernel<false, false, true>):
@@ -2591,7 +2594,8 @@ grr_status grr_system_step2_train(const float* x, const float* b, const float* u
                                   grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
                                   const float* alpha_a, const float* beta_a, const float* alpha_b,
                                   const float* beta_b, float* x_out, float* u_out, float* xd_out, float* x_mid,
-                                  float* u_mid, int B, int G, int F, int H, int W, void* stream) {
+                                  float* u_mid, float* xd_mid, int B, int G, int F, int H, int W,
+                                  void* stream) {
   clear_error();
   GRR_REQUIRE(x_mid && u_mid && u_out, GRR_ERR_INVALID_ARG, "grr_system_step2_train: x_mid, u_mid, u_out required");
   GRR_REQUIRE(x_mid != x && x_mid != b && x_mid != u_prev && x_mid != x_out && x_mid != u_out && u_mid != x &&
@@ -2599,7 +2603,7 @@ grr_status grr_system_step2_train(const float* x, const float* b, const float* u
               GRR_ERR_INVALID_ARG, "grr_system_step2_train: x_mid / u_mid must not alias other operands");
   return system_step2_impl(x, b, u_prev, xd, wL0, cG0, sL0, sG0, log_mu0, log_ro0, wL1, cG1, sL1, sG1, log_mu1,
                            log_ro1, alpha_a, beta_a, alpha_b, beta_b, nullptr, nullptr, x_out, u_out, xd_out, x_mid,
-                           u_mid, B, G, F, H, W, stream);
+                           u_mid, xd_mid, B, G, F, H, W, stream);
 }
 
 grr_status grr_glr_stage(const float* x, const float* b, const float* u_prev, const float* wL, grr_stencil sL,

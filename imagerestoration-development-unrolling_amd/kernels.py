@@ -374,23 +374,25 @@ def system_step2_train(x: Tensor, rhs: Tensor, u_prev: Optional[Tensor], xd_in: 
                        wL0: Tensor, cG0: Tensor, sL0: Stencil, sG0: Stencil, log_mu0: Tensor, log_ro0: Tensor,
                        wL1: Tensor, cG1: Tensor, sL1: Stencil, sG1: Stencil, log_mu1: Tensor, log_ro1: Tensor,
                        alpha_a: Tensor, beta_a: Optional[Tensor], alpha_b: Tensor, beta_b: Optional[Tensor],
-                       n_graphs: int, want_pool: bool
-                       ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Optional[Tensor]]:
+                       n_graphs: int, want_pool: bool, want_mid_pool: bool = False
+                       ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Optional[Tensor], Optional[Tensor]]:
     """Stages k, k+1 in one pass keeping the middle iterate (grr_system_step2_train, the training
-    forward).  Returns (x_{k+1}, u_{k+1}, x_{k+2}, u_{k+2}, D x_{k+2})."""
+    forward).  Returns (x_{k+1}, u_{k+1}, x_{k+2}, u_{k+2}, D x_{k+2}, D x_{k+1}); the pooled
+    outputs are None unless asked for."""
     dev = _check("system_step2_train", x, rhs, u_prev, xd_in, wL0, cG0, log_mu0, log_ro0, wL1, cG1, log_mu1,
                  log_ro1, alpha_a, beta_a, alpha_b, beta_b)
     b, c, h, w = x.shape
     x_mid, u_mid, out, u_out = (torch.empty_like(x) for _ in range(4))
     xd = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_pool else None
+    xdm = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev) if want_mid_pool else None
     _launch("system_step2", step2_bytes(b, c, n_graphs, h, w, u_prev is not None, True, want_pool, False)
-            + 8 * x.numel(),
+            + 8 * x.numel() + (x.numel() if want_mid_pool else 0),
             "grr_system_step2_train", x.data_ptr(), rhs.data_ptr(), _ptr(u_prev), xd_in.data_ptr(), wL0.data_ptr(),
             cG0.data_ptr(), sL0, sG0, log_mu0.data_ptr(), log_ro0.data_ptr(), wL1.data_ptr(), cG1.data_ptr(), sL1, sG1,
             log_mu1.data_ptr(), log_ro1.data_ptr(), alpha_a.data_ptr(), _ptr(beta_a), alpha_b.data_ptr(),
-            _ptr(beta_b), out.data_ptr(), u_out.data_ptr(), _ptr(xd), x_mid.data_ptr(), u_mid.data_ptr(), b,
-            n_graphs, c // n_graphs, h, w, _stream(dev))
-    return x_mid, u_mid, out, u_out, xd
+            _ptr(beta_b), out.data_ptr(), u_out.data_ptr(), _ptr(xd), x_mid.data_ptr(), u_mid.data_ptr(),
+            _ptr(xdm), b, n_graphs, c // n_graphs, h, w, _stream(dev))
+    return x_mid, u_mid, out, u_out, xd, xdm
 
 
 # W != 256 (W % 8 == 0) runs the two-stage pass in column strips of 256 lanes with a 16-column halo

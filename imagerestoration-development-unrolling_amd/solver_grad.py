@@ -197,22 +197,25 @@ def _level_side(dev: torch.device) -> "torch.cuda.Stream":
 UNPOOL_GLUE = True
 # ... and the full level's padj2 sweep of stage k likewise (grr_bwd_cg_glue's v1 / v2), where it runs
 PADJ_GLUE = True
+# The training forward keeps D x_k (its kernels form them anyway) for the reverse sweep's half level:
+# no pool2 of the saved iterates there (C/4 floats per pixel per stage of extra saved memory)
+SAVE_POOLED = os.environ.get("GRR_SAVE_POOLED", "1") == "1"
 # LNB / FFBlock reverse: the skip term (s0 gout, <gout, x>) inside the norm's reverse pass
 LN_SKIP_FUSED = True
 
 
 def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
-               defer: bool = False) -> Optional[Tensor]:
+               defer: bool = False, xd: Optional[Tensor] = None) -> Optional[Tensor]:
     """Apply a per-level reverse at full resolution and, through D / U, at half resolution.
     defer: return the half level's x-gradient instead of adding U of it to out (the caller passes it
-    to the next bwd_cg_glue)."""
+    to the next bwd_cg_glue).  xd: D x saved by the forward (else pooled here)."""
     if LEVEL_STREAMS and x.is_cuda and not torch.compiler.is_compiling() \
             and not torch.cuda.is_current_stream_capturing():
         main = torch.cuda.current_stream(x.device)
         side = _level_side(x.device)
         side.wait_stream(main)                # x, g (and every buffer the half level accumulates into) ready
         with torch.cuda.stream(side):
-            xd, gd = K.pool2(x), K.pool2(g)
+            xd, gd = K.pool2(x) if xd is None else xd, K.pool2(g)
             gxd = torch.zeros_like(xd)
             fn(l1, xd, gd, gxd)
         x.record_stream(side)
@@ -225,7 +228,7 @@ def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
         K.bwd_unpool2_acc(gxd, out)           # D^T = U
         return None
     fn(l0, x, g, out)
-    xd, gd = K.pool2(x), K.pool2(g)          # half level sees D x; U^T = D
+    xd, gd = K.pool2(x) if xd is None else xd, K.pool2(g)   # half level sees D x; U^T = D
     gxd = torch.zeros_like(xd)
     fn(l1, xd, gd, gxd)
     if defer:
@@ -274,12 +277,17 @@ def _mixture_fwd(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
     alpha, beta = p["alphaCGD"], p["betaCGD"]
     n_st = alpha.shape[0]
 
-    t = K.gtv_rhs_half(K.pool2(y), cG1, sG1, False, None, g)
+    keep = bool(consts[1])
+    dy = K.pool2(y)
+    t = K.gtv_rhs_half(dy, cG1, sG1, False, None, g)
     b_a, xd = K.gtv_rhs_full(y, y, cG0, sG0, False, None, ro0, t, ro1, g, want_pool=True)
+    xds = [xd]
     t = K.system_half(xd, wL1, cG1, sL1, sG1, mu1, ro1, g)
     x, r0, xd = K.system_step(b_a, b_a, None, t, wL0, cG0, sL0, sG0, mu0, ro0, alpha[0], None, g,
                               want_u=True, want_pool=n_st > 1)
     xs, us = [b_a, x], [r0]
+    if n_st > 1:
+        xds.append(xd)
     if n_st > 1:
         t = K.gtv_rhs_half(xd, wG1, sG1, True, p["gamma01"], g)
         b_b, _ = K.gtv_rhs_full(x, y, wG0, sG0, True, p["gamma00"], ro0, t, ro1, g)
@@ -290,11 +298,13 @@ def _mixture_fwd(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
             if pair and k + 1 < n_st:
                 # stages k, k+1 in one pass; the middle iterate is written for the reverse sweep
                 last = k + 1 == n_st - 1
-                xm, um, x, u, xd = K.system_step2_train(x, b_b, u, xd, wL0, cG0, sL0, sG0, mu0, ro0, wL1, cG1, sL1,
-                                                        sG1, mu1, ro1, alpha[k], beta[k] if k >= 2 else None,
-                                                        alpha[k + 1], beta[k + 1], g, want_pool=not last)
+                xm, um, x, u, xd, xdm = K.system_step2_train(x, b_b, u, xd, wL0, cG0, sL0, sG0, mu0, ro0, wL1, cG1,
+                                                             sL1, sG1, mu1, ro1, alpha[k], beta[k] if k >= 2 else None,
+                                                             alpha[k + 1], beta[k + 1], g, want_pool=not last,
+                                                             want_mid_pool=keep)
                 xs += [xm, x]
                 us += [um, u]
+                xds += [xdm, xd]
                 k += 2
                 continue
             last = k == n_st - 1
@@ -303,9 +313,12 @@ def _mixture_fwd(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
                                      beta[k] if k >= 2 else None, g, want_u=True, want_pool=not last)
             xs.append(x)
             us.append(u)
+            xds.append(xd)
             k += 1
         del b_b
-    return [xs[-1]], [wG0, wL0, wG1, wL1, cG0, cG1, *xs[:-1], *us]
+    # keep: D x_0 ... D x_{S-1} and D y, the half-level operands of the reverse sweep (no pool2 of them there)
+    pooled = [*xds[:n_st], dy] if keep else []
+    return [xs[-1]], [wG0, wL0, wG1, wL1, cG0, cG1, *xs[:-1], *us, *pooled]
 
 
 def _mixture_fake(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
@@ -313,19 +326,23 @@ def _mixture_fake(consts, y: Tensor, f0: Tensor, f1: Tensor, *params: Tensor):
     b, c, h, w = y.shape
     n_st = dict(zip(PARAM_NAMES, params))["alphaCGD"].shape[0]
     e0, e1 = _new(y, b, g, 4, h, w), _new(y, b, g, 4, h // 2, w // 2)
+    pooled = [_new(y, b, c, h // 2, w // 2) for _ in range(n_st + 1)] if consts[1] else []
     return [_new(y, b, c, h, w)], [e0, _new(y, b, g, 4, h, w), e1, _new(y, b, g, 4, h // 2, w // 2),
                                    _new(y, b, g, 2, h, w), _new(y, b, g, 2, h // 2, w // 2),
-                                   *[_new(y, b, c, h, w) for _ in range(2 * n_st)]]
+                                   *[_new(y, b, c, h, w) for _ in range(2 * n_st)], *pooled]
 
 
 def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
     g = consts[0]
     y, f0, f1 = inputs[:3]
     params = inputs[3:]
-    n_st = (len(saved) - 6) // 2
+    keep = bool(consts[1])
+    n_st = (len(saved) - 6 - int(keep)) // (3 if keep else 2)
     wG0, wL0, wG1, wL1, cG0, cG1 = saved[:6]
     xs = saved[6:6 + n_st]          # x_0 = b_A, x_1, ..., x_{S-1}
-    us = saved[6 + n_st:]           # r_0, u_1, ..., u_{S-1}
+    us = saved[6 + n_st:6 + 2 * n_st]   # r_0, u_1, ..., u_{S-1}
+    # D x_0 ... D x_{S-1}, D y from the forward (keep), else pooled here
+    xds = saved[6 + 2 * n_st:] if keep else [None] * (n_st + 1)
     p = dict(zip(PARAM_NAMES, params))
     c = y.shape[1]
     nf = c // g
@@ -335,7 +352,7 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
     alpha, beta = p["alphaCGD"], p["betaCGD"]
     galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
 
-    def a_bwd(x, gg, coef, out, glr=True, defer=False):   # out += coef * (A - I)^T gg (+ parameter gradients)
+    def a_bwd(x, gg, coef, out, glr=True, defer=False, xd=None):   # out += coef * (A - I)^T gg (+ parameter gradients)
         # defer: the full level's padj2 operands and the half level's x-gradient are returned for the
         # next bwd_cg_glue instead of being added to out here
         pend = []
@@ -344,7 +361,7 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
             r = lv.terms_bwd(xx, g2, coef, o, glr, defer=defer and PADJ_GLUE and lv is l0)
             if r is not None:
                 pend.append(r)
-        gxh = _two_level(l0, l1, x, gg, out, fn, defer)
+        gxh = _two_level(l0, l1, x, gg, out, fn, defer, xd)
         return gxh, (pend[0] if pend else None)
 
     gx = gouts[0].contiguous()
@@ -357,21 +374,21 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
             # previous stage's full-level x-gradient pass and half-level x-gradient added on the way in
             gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
                              galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh, padj=pj)
-            gxh, pj = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1)   #   - (A - I)^T gu
+            gxh, pj = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1, xd=xds[k])   #   - (A - I)^T gu
             gu_next = gu
         # b_B = y + prox terms(x_1)
         K.bwd_lincomb(gbb, None, None, None, g, out=gy, accumulate=True)
-        _two_level(l0, l1, xs[1], gbb, gx, lambda lv, xx, g2, o: lv.prox_bwd(xx, g2, o))
+        _two_level(l0, l1, xs[1], gbb, gx, lambda lv, xx, g2, o: lv.prox_bwd(xx, g2, o), xd=xds[1])
         del gbb
     # x_1 = b_A + alpha_0 r_0, r_0 = b_A - A b_A
     K.bwd_graph_dot(gx, us[0], galpha[0], g)
     ga = K.bwd_lincomb(gx, alpha[0], None, None, g)
     gba = gx.clone()
-    a_bwd(xs[0], ga, -1.0, gba)                                 # gx_1 - (A - I)^T (alpha_0 gx_1)
+    a_bwd(xs[0], ga, -1.0, gba, xd=xds[0])                      # gx_1 - (A - I)^T (alpha_0 gx_1)
     del ga
     # b_A = y + ro0 G0 y + U ro1 G1 D y
     K.bwd_lincomb(gba, None, None, None, g, out=gy, accumulate=True)
-    a_bwd(y, gba, 1.0, gy, glr=False)
+    a_bwd(y, gba, 1.0, gy, glr=False, xd=xds[n_st])
     del gba
 
     # weights -> features
@@ -402,7 +419,7 @@ MIXTURE = OpaqueFunction("mixture_solve_train", 1, _mixture_fwd, _mixture_bwd, _
 
 def mixture_solve(mod, y: Tensor, f0: Tensor, f1: Tensor) -> Tensor:
     """Differentiable MixtureGTVGLR solve (features given); all work on the HIP kernels."""
-    return MIXTURE([mod.n_graphs], y, f0.contiguous(), f1.contiguous(), *solver_params(mod))
+    return MIXTURE([mod.n_graphs, int(SAVE_POOLED)], y, f0.contiguous(), f1.contiguous(), *solver_params(mod))
 
 
 # ---- feature convolutions ----------------------------------------------------

@@ -207,14 +207,16 @@ grr_status grr_system_first_pair(const float* b_a, const float* xd_a, const floa
                                  void* stream);
 /* grr_system_step2 for training: also writes the middle iterate x_{k+1} (x_mid) and its direction
  * u_{k+1} (u_mid) -- the reverse sweep's saved iterates -- besides x_{k+2}, u_{k+2} (u_out required) and
- * D x_{k+2}; no skip.  Same shape limits. */
+ * D x_{k+2}; no skip.  xd_mid (may be NULL): D x_{k+1}, the pooled middle iterate the kernel's half level
+ * already forms, for the reverse sweep's half-level terms (no pool2 of x_{k+1} there).  Same shape
+ * limits. */
 grr_status grr_system_step2_train(const float* x, const float* b, const float* u_prev, const float* xd,
                                   const float* wL0, const float* cG0, grr_stencil sL0, grr_stencil sG0,
                                   const float* log_mu0, const float* log_ro0, const float* wL1, const float* cG1,
                                   grr_stencil sL1, grr_stencil sG1, const float* log_mu1, const float* log_ro1,
                                   const float* alpha_a, const float* beta_a, const float* alpha_b,
                                   const float* beta_b, float* x_out, float* u_out, float* xd_out, float* x_mid,
-                                  float* u_mid, int B, int G, int F, int H, int W, void* stream);
+                                  float* u_mid, float* xd_mid, int B, int G, int F, int H, int W, void* stream);
 
 /* One unrolled stage of the GLR-only v10 block (exploration/model_multiscale_mixture_GLR/lib/
  * model_GLR_GTV_deep_v10.py:241-335, MixtureGLR): single scale, A x = x + mu[g] L x with mu

@@ -92,7 +92,7 @@ int main() {
   EXPECT_ERR(grr_ffn_forward(n, n, n, n, n, n, n, n, 1, 8, 16, 8, 8, s));
   EXPECT_ERR(grr_wgrad(n, n, n, n, 1, 8, 8, 64, s));
   EXPECT_ERR(grr_system_step2_train(n, n, n, n, n, n, ns, ns, n, n, n, n, ns, ns, n, n, n, n, n, n, n, n, n, n, n,
-                                    1, 2, 3, 8, 256, s));
+                                    n, 1, 2, 3, 8, 256, s));
   const int32_t delta[4] = {-1, 0, 0, -1};
   EXPECT_ERR(grr_win_edge_weights(n, 0, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_solver(0, n, 0, n, n, n, n, n, n, n, n, n, n, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));

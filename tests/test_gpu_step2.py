@@ -200,3 +200,64 @@ def test_training_forward_with_step2_matches_per_stage(irdu, n_st, w):
     assert p1.keys() == p0.keys()
     for k in p0:
         assert rel_err(p1[k], p0[k]) <= 1e-4, k
+
+
+def test_training_step2_mid_pool_equals_pool2(irdu):
+    """grr_system_step2_train's xd_mid (D x_{k+1}, the pooled rows stage B's half level reads) against
+    grr_pool2 of the middle iterate it writes; without xd_mid the other outputs are unchanged."""
+    from irdu_amd import kernels as K
+    torch.manual_seed(77)
+    G, F, B, H, W = 4, 3, 2, 64, 256
+    m = irdu.MixtureGTVGLR(G, F, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]], n_cgd_iters=10)
+    perturb_mixture(m, 77)
+    m = m.to(DEV)
+    f0 = torch.randn(B, 2 * G * F, H, W, device=DEV)
+    f1 = torch.randn(B, 2 * G * F, H // 2, W // 2, device=DEV)
+    wG0, cG0, wL0 = K.edge_weights_block(f0, G, F, m.GTVmodule00.multiM, m.GLRmodule00.multiM)
+    wG1, cG1, wL1 = K.edge_weights_block(f1, G, F, m.GTVmodule01.multiM, m.GLRmodule01.multiM)
+    x = torch.rand(B, G * F, H, W, device=DEV)
+    rhs = torch.rand_like(x)
+    u = torch.randn_like(x)
+    xd = K.pool2(x)
+    args = (x, rhs, u, xd, wL0, cG0, K.stencil(m.GLRmodule00), K.stencil(m.GTVmodule00), m.muys00, m.ro00, wL1,
+            cG1, K.stencil(m.GLRmodule01), K.stencil(m.GTVmodule01), m.muys01, m.ro01, m.alphaCGD[2],
+            m.betaCGD[2], m.alphaCGD[3], m.betaCGD[3], G)
+    with torch.no_grad():
+        got = K.system_step2_train(*args, want_pool=True, want_mid_pool=True)
+        ref = K.system_step2_train(*args, want_pool=True, want_mid_pool=False)
+    torch.cuda.synchronize()
+    assert ref[5] is None
+    for a, r in zip(got[:5], ref[:5]):
+        assert torch.equal(a, r)
+    assert rel_err(got[5], K.pool2(got[0])) <= 1e-6
+
+
+@pytest.mark.parametrize("n_st", [4, 5])
+def test_training_saved_pooled_iterates_match_repooling(irdu, n_st):
+    """solver_grad.SAVE_POOLED (the reverse's half level reads D x_k saved by the forward) against
+    pooling the saved iterates in the reverse: input and parameter gradients."""
+    from irdu_amd import solver_grad as SG
+    torch.manual_seed(2500 + n_st)
+    m = irdu.MultiScaleGraphFilter(3, 3, ngraphs=4, n_cgd_iters=n_st)
+    perturb_mixture(m.localfilter, 25 + n_st)
+    x = torch.rand(2, 3, 32, 256)
+    gout = torch.randn(2, 3, 32, 256)
+    md = m.to(DEV).train()
+    saved = SG.SAVE_POOLED
+    res = {}
+    try:
+        for flag in (True, False):
+            SG.SAVE_POOLED = flag
+            md.zero_grad(set_to_none=True)
+            xd = x.to(DEV).requires_grad_(True)
+            out = md(xd)
+            out.backward(gout.to(DEV))
+            res[flag] = (out.detach().cpu(), xd.grad.cpu(),
+                         {k: p.grad.detach().cpu() for k, p in md.named_parameters() if p.grad is not None})
+    finally:
+        SG.SAVE_POOLED = saved
+    (o1, g1, p1), (o0, g0, p0) = res[True], res[False]
+    assert torch.equal(o1, o0)
+    assert rel_err(g1, g0) <= 1e-5
+    for k in p0:
+        assert rel_err(p1[k], p0[k]) <= 1e-4, k
