@@ -113,6 +113,7 @@ SIGNATURES = {
     "grr_bwd_graph_dot": [P, P, Fl, P, I, I, I, I, I, P],
     "grr_bwd_lincomb": [P, P, P, P, P, I, I, I, I, I, I, P],
     "grr_bwd_cg_glue": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_bwd_cg_glue_pool": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_unpool2_acc": [P, P, I, I, I, I, P],
     "grr_conv2x2s2_bwd_data": [P, P, P, I, I, I, I, I, P],
     "grr_interleave2x2": [P, P, I, I, I, I, P],

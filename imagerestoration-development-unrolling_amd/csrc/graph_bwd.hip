@@ -624,14 +624,17 @@ __global__ __launch_bounds__(NT) void lincomb_kernel(const float* __restrict__ x
 struct GluePadj {
   const float *v1, *t1, *s1, *v2, *t2, *s2;
 };
+// gud (optional, V4, even H): D gu as well (pool2_kernel's arithmetic), the half-level operand of the
+// operator reverse that reads gu next -- each thread takes the same four columns of a row pair.
 template <bool V4>
 __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const float* __restrict__ gxh, GluePadj pj,
                                                      int F, const float* __restrict__ u,
                                                      const float* __restrict__ gun, const float* __restrict__ up,
                                                      const float* __restrict__ alpha,
                                                      const float* __restrict__ beta_next, float* __restrict__ gu_out,
-                                                     float* __restrict__ gbb, float* gx_out, Red galpha,
-                                                     Red gbeta, int G, int64_t n, int H, int W) {
+                                                     float* __restrict__ gbb, float* gx_out,
+                                                     float* __restrict__ gud, Red galpha, Red gbeta, int G,
+                                                     int64_t n, int H, int W) {
   const int bg = blockIdx.y, g = bg % G;
   const int64_t base = (int64_t)bg * n;
   const float al = alpha[g], be = gun ? beta_next[g] : 0.f;
@@ -645,13 +648,13 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
   if constexpr (V4) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef float f2 __attribute__((ext_vector_type(2)));
-    const int64_t n4 = n / 4;
-    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
-      const int64_t o = base + 4 * i;
+    // four columns at slab element li (W % 4 == 0 where pj / gxh / gud are given)
+    auto glue4 = [&](int li) __attribute__((always_inline)) {
+      const int64_t o = base + li;
       f4 x = *reinterpret_cast<const f4*>(gx + o);
       const f4 uv = *reinterpret_cast<const f4*>(u + o);
-      if (pj.v1) {   // W % 4 == 0
-        const int li = (int)(4 * i), f = li / HW, p = li - f * HW, r = p / W, c = p - r * W;
+      if (pj.v1) {
+        const int f = li / HW, p = li - f * HW, r = p / W, c = p - r * W;
         const int ch = g * F + f;
         const int64_t po = ((int64_t)bg * F + f) * HW;
         const float *k1 = pj.t1 + ch * 5, *k2 = pj.t2 + ch * 5;
@@ -661,8 +664,8 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
         y2 *= pj.s2[g];
         x = (x + y1) + y2;
       }
-      if (gxh) {   // W % 4 == 0: the four columns sit over two half-level columns
-        const f2 q = *reinterpret_cast<const f2*>(gxh + half_at((int)(4 * i)));
+      if (gxh) {   // the four columns sit over two half-level columns
+        const f2 q = *reinterpret_cast<const f2*>(gxh + half_at(li));
         x.x += 0.25f * q.x; x.y += 0.25f * q.x; x.z += 0.25f * q.y; x.w += 0.25f * q.y;
       }
       f4 gu = al * x;
@@ -675,6 +678,24 @@ __global__ __launch_bounds__(NT) void cg_glue_kernel(const float* gx, const floa
       if (gbb) *reinterpret_cast<f4*>(gbb + o) += gu;
       *reinterpret_cast<f4*>(gu_out + o) = gu;
       *reinterpret_cast<f4*>(gx_out + o) = x - gu;
+      return gu;
+    };
+    if (gud) {   // (f, half row, column quad) per step
+      const int W4 = W / 4, hq = (H / 2) * W4;
+      const int64_t nq = n / 8;
+      for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nq; i += (int64_t)gridDim.x * NT) {
+        const int q = (int)i, f = q / hq, rem = q - f * hq, hr = rem / W4, c4 = rem - hr * W4;
+        const int li = f * HW + 2 * hr * W + 4 * c4;
+        const f4 g0 = glue4(li), g1 = glue4(li + W);
+        f2 d;
+        d.x = 0.25f * g0.x + 0.25f * g0.y + 0.25f * g1.x + 0.25f * g1.y;
+        d.y = 0.25f * g0.z + 0.25f * g0.w + 0.25f * g1.z + 0.25f * g1.w;
+        *reinterpret_cast<f2*>(gud + hbase + (int64_t)f * (HW / 4) + hr * w2 + 2 * c4) = d;
+      }
+    } else {
+      const int64_t n4 = n / 4;
+      for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT)
+        glue4((int)(4 * i));
     }
   } else {
     for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
@@ -2420,12 +2441,11 @@ grr_status grr_bwd_graph_dot(const float* u, const float* v, float coef, float* 
   return st != GRR_OK ? st : rs.finish("grr_bwd_graph_dot");
 }
 
-grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v1, const float* taps1,
-                           const float* scale1, const float* v2, const float* taps2, const float* scale2,
-                           const float* u, const float* gu_next, const float* u_prev, const float* alpha,
-                           const float* beta_next, float* gu, float* gbb, float* gx_out, float* galpha, float* gbeta,
-                           int B, int G, int F, int H, int W, void* stream) {
-  clear_error();
+static grr_status cg_glue_impl(const float* gx, const float* gx_half, const float* v1, const float* taps1,
+                               const float* scale1, const float* v2, const float* taps2, const float* scale2,
+                               const float* u, const float* gu_next, const float* u_prev, const float* alpha,
+                               const float* beta_next, float* gu, float* gbb, float* gx_out, float* gu_half,
+                               float* galpha, float* gbeta, int B, int G, int F, int H, int W, void* stream) {
   GRR_REQUIRE(gx && u && alpha && gu && gx_out && galpha && (!gu_next || beta_next) && (!u_prev || gbeta) && B > 0 &&
                   G > 0 && F > 0 && H > 0 && W > 0 && (!gx_half || (H % 2 == 0 && W % 2 == 0)),
               GRR_ERR_INVALID_ARG, "grr_bwd_cg_glue: bad args");
@@ -2441,8 +2461,10 @@ grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v
                   (!v1 || (W % 4 == 0 && al16(v1) && al16(v2)));
   GRR_REQUIRE(!v1 || v4, GRR_ERR_UNSUPPORTED,
               "grr_bwd_cg_glue: the x-gradient pass needs W %% 4 == 0 and 16-byte aligned planes (W = %d)", W);
+  GRR_REQUIRE(!gu_half || (v4 && W % 4 == 0 && H % 2 == 0 && ((uintptr_t)gu_half & 7) == 0), GRR_ERR_UNSUPPORTED,
+              "grr_bwd_cg_glue_pool: needs W %% 4 == 0, even H, 16-byte aligned planes, 8-byte aligned gu_half (H %d, W %d)", H, W);
   const GluePadj pj{v1, taps1, scale1, v2, taps2, scale2};
-  const int chunks = chunks_for(v4 ? n / 4 : n, (int64_t)B * G);
+  const int chunks = chunks_for(v4 ? n / (gu_half ? 8 : 4) : n, (int64_t)B * G);
   const dim3 grid(chunks, B * G);
   RedScratch rs((hipStream_t)stream);
   const int ia = rs.plan(galpha, G, (uint32_t)B * chunks), ib = rs.plan(u_prev ? gbeta : nullptr, G, (uint32_t)B * chunks);
@@ -2450,12 +2472,33 @@ grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v
   if (st != GRR_OK) return st;
   if (v4)
     hipLaunchKernelGGL(cg_glue_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, pj, F, u, gu_next,
-                       u_prev, alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
+                       u_prev, alpha, beta_next, gu, gbb, gx_out, gu_half, rs.red(ia), rs.red(ib), G, n, H, W);
   else
     hipLaunchKernelGGL(cg_glue_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, gx, gx_half, pj, F, u, gu_next,
-                       u_prev, alpha, beta_next, gu, gbb, gx_out, rs.red(ia), rs.red(ib), G, n, H, W);
+                       u_prev, alpha, beta_next, gu, gbb, gx_out, nullptr, rs.red(ia), rs.red(ib), G, n, H, W);
   st = launch_status("grr_bwd_cg_glue");
   return st != GRR_OK ? st : rs.finish("grr_bwd_cg_glue");
+}
+
+grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v1, const float* taps1,
+                           const float* scale1, const float* v2, const float* taps2, const float* scale2,
+                           const float* u, const float* gu_next, const float* u_prev, const float* alpha,
+                           const float* beta_next, float* gu, float* gbb, float* gx_out, float* galpha, float* gbeta,
+                           int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  return cg_glue_impl(gx, gx_half, v1, taps1, scale1, v2, taps2, scale2, u, gu_next, u_prev, alpha, beta_next, gu,
+                      gbb, gx_out, nullptr, galpha, gbeta, B, G, F, H, W, stream);
+}
+
+grr_status grr_bwd_cg_glue_pool(const float* gx, const float* gx_half, const float* v1, const float* taps1,
+                                const float* scale1, const float* v2, const float* taps2, const float* scale2,
+                                const float* u, const float* gu_next, const float* u_prev, const float* alpha,
+                                const float* beta_next, float* gu, float* gbb, float* gx_out, float* gu_half,
+                                float* galpha, float* gbeta, int B, int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(gu_half, GRR_ERR_INVALID_ARG, "grr_bwd_cg_glue_pool: gu_half required");
+  return cg_glue_impl(gx, gx_half, v1, taps1, scale1, v2, taps2, scale2, u, gu_next, u_prev, alpha, beta_next, gu,
+                      gbb, gx_out, gu_half, galpha, gbeta, B, G, F, H, W, stream);
 }
 
 grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,

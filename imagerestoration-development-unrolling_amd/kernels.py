@@ -944,8 +944,9 @@ def bwd_lincomb(x: Tensor, sa: Optional[Tensor], y: Optional[Tensor], sb: Option
 def bwd_cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Optional[Tensor], alpha: Tensor,
                 beta_next: Optional[Tensor], gbb: Optional[Tensor], galpha: Tensor, gbeta: Optional[Tensor],
                 n_graphs: int, inplace: bool = False, gx_half: Optional[Tensor] = None,
-                padj: Optional[tuple] = None) -> Tuple[Tensor, Tensor]:
-    """One reverse step of the stage recurrence glue (grr_bwd_cg_glue): returns (gu, gx - gu);
+                padj: Optional[tuple] = None, want_pool: bool = False):
+    """One reverse step of the stage recurrence glue (grr_bwd_cg_glue): returns (gu, gx - gu), and
+    D gu third when want_pool (grr_bwd_cg_glue_pool; glue_pool_ok must hold);
     galpha / gbeta accumulate <gx, u> / <gu, u_prev>, gbb += gu.  inplace: gx - gu overwrites gx.
     Passes of the previous stage folded in (gx taken as ((gx + s1 P1*(v1)) + s2 P2*(v2)) + U gx_half):
     padj = (v1, taps1, s1, v2, taps2, s2), bwd_padj2's operands (padj2_ok); gx_half, bwd_unpool2_acc's."""
@@ -965,12 +966,24 @@ def bwd_cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Option
     gx_out = gx if inplace else torch.empty_like(gx)
     n_rw = 2 + int(gu_next is not None) + int(u_prev is not None) + 2 * int(gbb is not None) + 2
     n_rw += 2 * int(v1 is not None)
-    _launch("bwd_cg_glue", 4 * (gx.numel() * n_rw + (0 if gx_half is None else gx_half.numel())), "grr_bwd_cg_glue",
-            gx.data_ptr(), _ptr(gx_half), _ptr(v1), _ptr(t1), _ptr(s1), _ptr(v2), _ptr(t2), _ptr(s2),
-            u.data_ptr(), _ptr(gu_next), _ptr(u_prev), alpha.data_ptr(),
-            _ptr(beta_next), gu.data_ptr(), _ptr(gbb), gx_out.data_ptr(), galpha.data_ptr(), _ptr(gbeta),
+    nbytes = 4 * (gx.numel() * n_rw + (0 if gx_half is None else gx_half.numel()))
+    ptrs = (gx.data_ptr(), _ptr(gx_half), _ptr(v1), _ptr(t1), _ptr(s1), _ptr(v2), _ptr(t2), _ptr(s2),
+            u.data_ptr(), _ptr(gu_next), _ptr(u_prev), alpha.data_ptr(), _ptr(beta_next), gu.data_ptr(), _ptr(gbb),
+            gx_out.data_ptr())
+    if want_pool:
+        gud = torch.empty((b, c, h // 2, w // 2), dtype=torch.float32, device=dev)
+        _launch("bwd_cg_glue", nbytes + gx.numel(), "grr_bwd_cg_glue_pool", *ptrs, gud.data_ptr(),
+                galpha.data_ptr(), _ptr(gbeta), *_bgfhw(gx, n_graphs), _stream(dev))
+        return gu, gx_out, gud
+    _launch("bwd_cg_glue", nbytes, "grr_bwd_cg_glue", *ptrs, galpha.data_ptr(), _ptr(gbeta),
             *_bgfhw(gx, n_graphs), _stream(dev))
     return gu, gx_out
+
+
+def glue_pool_ok(x: Tensor) -> bool:
+    """Where grr_bwd_cg_glue_pool takes the glue (W % 4 == 0, even H; planes 16-byte aligned by torch)."""
+    b, c, h, w = x.shape
+    return w % 4 == 0 and h % 2 == 0 and x.data_ptr() % 16 == 0
 
 
 def bwd_unpool2_acc(xd: Tensor, out: Tensor) -> None:

@@ -200,22 +200,26 @@ PADJ_GLUE = True
 # The training forward keeps D x_k (its kernels form them anyway) for the reverse sweep's half level:
 # no pool2 of the saved iterates there (C/4 floats per pixel per stage of extra saved memory)
 SAVE_POOLED = os.environ.get("GRR_SAVE_POOLED", "1") == "1"
+# ... and the glue pass that writes gu_k also writes D gu_k (grr_bwd_cg_glue_pool): no pool2 of gu_k
+GLUE_POOL = os.environ.get("GRR_GLUE_POOL", "1") == "1"
 # LNB / FFBlock reverse: the skip term (s0 gout, <gout, x>) inside the norm's reverse pass
 LN_SKIP_FUSED = True
 
 
 def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
-               defer: bool = False, xd: Optional[Tensor] = None) -> Optional[Tensor]:
+               defer: bool = False, xd: Optional[Tensor] = None, gd: Optional[Tensor] = None) -> Optional[Tensor]:
     """Apply a per-level reverse at full resolution and, through D / U, at half resolution.
     defer: return the half level's x-gradient instead of adding U of it to out (the caller passes it
-    to the next bwd_cg_glue).  xd: D x saved by the forward (else pooled here)."""
+    to the next bwd_cg_glue).  xd, gd: D x saved by the forward, D g formed by the pass that wrote g
+    (else pooled here)."""
     if LEVEL_STREAMS and x.is_cuda and not torch.compiler.is_compiling() \
             and not torch.cuda.is_current_stream_capturing():
         main = torch.cuda.current_stream(x.device)
         side = _level_side(x.device)
         side.wait_stream(main)                # x, g (and every buffer the half level accumulates into) ready
         with torch.cuda.stream(side):
-            xd, gd = K.pool2(x) if xd is None else xd, K.pool2(g)
+            xd = K.pool2(x) if xd is None else xd
+            gd = K.pool2(g) if gd is None else gd
             gxd = torch.zeros_like(xd)
             fn(l1, xd, gd, gxd)
         x.record_stream(side)
@@ -228,7 +232,8 @@ def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
         K.bwd_unpool2_acc(gxd, out)           # D^T = U
         return None
     fn(l0, x, g, out)
-    xd, gd = K.pool2(x) if xd is None else xd, K.pool2(g)   # half level sees D x; U^T = D
+    xd = K.pool2(x) if xd is None else xd          # half level sees D x; U^T = D
+    gd = K.pool2(g) if gd is None else gd
     gxd = torch.zeros_like(xd)
     fn(l1, xd, gd, gxd)
     if defer:
@@ -239,15 +244,14 @@ def _two_level(l0: _Level, l1: _Level, x: Tensor, g: Tensor, out: Tensor, fn,
 
 def cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Optional[Tensor], alpha: Tensor, beta: Tensor,
             gbb: Optional[Tensor], galpha: Tensor, gbeta: Tensor, k: int, g: int, owned: bool,
-            gx_half: Optional[Tensor] = None, padj: Optional[tuple] = None) -> Tuple[Tensor, Tensor]:
+            gx_half: Optional[Tensor] = None, padj: Optional[tuple] = None, want_pool: bool = False):
     """Reverse of stage k's recurrence glue (x' = x + a_k u_k, u_k = r - A x + b_k u_{k-1}) without the
-    operator term: returns (gu_k, gx' - gu_k); ga_k, gb_k (when u_prev) and gbb accumulate.  owned: gx
-    is this sweep's own buffer and is overwritten."""
-    gu, gx2 = K.bwd_cg_glue(gx, u, gu_next, u_prev, alpha[k].contiguous(),
-                            beta[k + 1].contiguous() if gu_next is not None else None, gbb, galpha[k],
-                            gbeta[k] if u_prev is not None else None, g, inplace=owned, gx_half=gx_half,
-                            padj=padj)
-    return gu, gx2
+    operator term: returns (gu_k, gx' - gu_k), and D gu_k third when want_pool; ga_k, gb_k (when
+    u_prev) and gbb accumulate.  owned: gx is this sweep's own buffer and is overwritten."""
+    return K.bwd_cg_glue(gx, u, gu_next, u_prev, alpha[k].contiguous(),
+                         beta[k + 1].contiguous() if gu_next is not None else None, gbb, galpha[k],
+                         gbeta[k] if u_prev is not None else None, g, inplace=owned, gx_half=gx_half,
+                         padj=padj, want_pool=want_pool)
 
 
 def _stencil(t4) -> Stencil:
@@ -352,7 +356,7 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
     alpha, beta = p["alphaCGD"], p["betaCGD"]
     galpha, gbeta = torch.zeros_like(alpha), torch.zeros_like(beta)
 
-    def a_bwd(x, gg, coef, out, glr=True, defer=False, xd=None):   # out += coef * (A - I)^T gg (+ parameter gradients)
+    def a_bwd(x, gg, coef, out, glr=True, defer=False, xd=None, gd=None):   # out += coef * (A - I)^T gg (+ params)
         # defer: the full level's padj2 operands and the half level's x-gradient are returned for the
         # next bwd_cg_glue instead of being added to out here
         pend = []
@@ -361,7 +365,7 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
             r = lv.terms_bwd(xx, g2, coef, o, glr, defer=defer and PADJ_GLUE and lv is l0)
             if r is not None:
                 pend.append(r)
-        gxh = _two_level(l0, l1, x, gg, out, fn, defer, xd)
+        gxh = _two_level(l0, l1, x, gg, out, fn, defer, xd, gd)
         return gxh, (pend[0] if pend else None)
 
     gx = gouts[0].contiguous()
@@ -372,9 +376,12 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
         for k in range(n_st - 1, 0, -1):
             # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue), with the
             # previous stage's full-level x-gradient pass and half-level x-gradient added on the way in
-            gu, gx = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
-                             galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh, padj=pj)
-            gxh, pj = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1, xd=xds[k])   #   - (A - I)^T gu
+            pool = GLUE_POOL and K.glue_pool_ok(gx)
+            gu, gx, *gud = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
+                                   galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh, padj=pj, want_pool=pool)
+            gxh, pj = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1, xd=xds[k],
+                            gd=gud[0] if gud else None)                   #   - (A - I)^T gu
+            del gud
             gu_next = gu
         # b_B = y + prox terms(x_1)
         K.bwd_lincomb(gbb, None, None, None, g, out=gy, accumulate=True)

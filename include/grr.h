@@ -449,6 +449,14 @@ grr_status grr_bwd_cg_glue(const float* gx, const float* gx_half, const float* v
                            const float* u, const float* gu_next, const float* u_prev, const float* alpha,
                            const float* beta_next, float* gu, float* gbb, float* gx_out, float* galpha, float* gbeta,
                            int B, int G, int F, int H, int W, void* stream);
+/* grr_bwd_cg_glue that also writes gu_half = D gu [B, G*F, H/2, W/2] (grr_pool2's arithmetic): the
+ * half-level operand of the operator reverse that reads gu next, formed in the pass that writes gu
+ * (no separate pool of it).  W % 4 == 0, even H, 16-byte aligned planes. */
+grr_status grr_bwd_cg_glue_pool(const float* gx, const float* gx_half, const float* v1, const float* taps1,
+                                const float* scale1, const float* v2, const float* taps2, const float* scale2,
+                                const float* u, const float* gu_next, const float* u_prev, const float* alpha,
+                                const float* beta_next, float* gu, float* gbb, float* gx_out, float* gu_half,
+                                float* galpha, float* gbeta, int B, int G, int F, int H, int W, void* stream);
 grr_status grr_bwd_lincomb(const float* x, const float* sa, const float* y, const float* sb, float* out,
                            int accumulate, int B, int G, int F, int H, int W, void* stream);
 /* out [B,C,H,W] += U(xd): 0.25 * xd(q/2) (conv_transpose2d of scaling_kernel01, REF:676-679). */

@@ -75,6 +75,7 @@ int main() {
   EXPECT_ERR(grr_bwd_graph_dot(n, n, 1.f, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_lincomb(n, n, n, n, n, 0, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_cg_glue(n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_bwd_cg_glue_pool(n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_bwd_unpool2_acc(n, n, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_conv2x2s2_bwd_data(n, n, n, 1, 4, 4, 8, 8, s));
   EXPECT_ERR(grr_interleave2x2(n, n, 1, 4, 8, 8, s));

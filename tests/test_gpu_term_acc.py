@@ -291,3 +291,49 @@ def test_abstract_gradients_with_and_without_ln_skip(K):
     assert ref.keys() == got.keys()
     for k in ref:
         assert rel_err(got[k], ref[k]) <= 1e-4, (k, rel_err(got[k], ref[k]))
+
+
+@pytest.mark.parametrize("shape", [(2, 6, 8, 12), (2, 12, 32, 64), (1, 3, 2, 4), (2, 6, 6, 20)], ids=str)
+@pytest.mark.parametrize("fold", [False, True])
+def test_cg_glue_pool_equals_glue_then_pool2(K, shape, fold):
+    """grr_bwd_cg_glue_pool (D gu written by the glue pass, row pairs per thread) against the plain glue
+    followed by grr_pool2 of gu; with and without the previous stage's padj2 / U passes folded in.  The
+    element-wise outputs are the same expressions; the per-graph sums run in another order."""
+    b, c, h, w = shape
+    G = 3
+    torch.manual_seed(h * w + int(fold))
+    t = lambda *s: torch.randn(*s, device=DEV)  # noqa: E731
+    gx, u, gun, up, gbb, v1, v2 = (t(b, c, h, w) for _ in range(7))
+    gxh = t(b, c, h // 2, w // 2)
+    t1, t2 = t(c, 5), t(c, 5)
+    s1, s2 = torch.rand(G, device=DEV) + 0.5, torch.rand(G, device=DEV) + 0.5
+    alpha, beta = torch.rand(G, device=DEV), torch.rand(G, device=DEV)
+    assert K.glue_pool_ok(gx)
+
+    def run(pool):
+        ga, gb, bb = torch.zeros(G, device=DEV), torch.zeros(G, device=DEV), gbb.clone()
+        x = gx.clone()
+        r = K.bwd_cg_glue(x, u, gun, up, alpha, beta, bb, ga, gb, G, gx_half=gxh if fold else None,
+                          padj=(v1, t1, s1, v2, t2, s2) if fold else None, want_pool=pool)
+        gu, gxo = r[:2]
+        gud = r[2] if pool else K.pool2(gu)
+        torch.cuda.synchronize()
+        return [v.cpu() for v in (gu, gxo, gud, bb, ga, gb)]
+
+    n = b * (c // G) * h * w
+    for name, a, r in zip(("gu", "gx", "gud", "gbb", "galpha", "gbeta"), run(True), run(False)):
+        if name in ("galpha", "gbeta"):
+            err = float((a.double() - r.double()).abs().max())
+            assert err <= 2e-6 * max(float(r.abs().max()), n ** 0.5), (name, err)
+        else:
+            assert rel_err(a, r) <= 1e-6, (name, rel_err(a, r))
+
+
+def test_cg_glue_pool_rejects_odd_shapes(K):
+    from irdu_amd._native import GrrError
+    G = 3
+    x = torch.randn(1, 6, 5, 8, device=DEV)      # odd H
+    a = torch.rand(G, device=DEV)
+    assert not K.glue_pool_ok(x)
+    with pytest.raises(GrrError):
+        K.bwd_cg_glue(x, x.clone(), None, None, a, None, None, torch.zeros(G, device=DEV), None, G, want_pool=True)
