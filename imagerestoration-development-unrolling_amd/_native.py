@@ -74,6 +74,7 @@ SIGNATURES = {
     "grr_ffn_workspace_bytes": [I, I, I, I, I],
     "grr_ffn_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_wgrad_workspace_bytes": [I, I, I, L],
+    "grr_wgrad_set_tiles": [I],
     "grr_wgrad": [P, P, P, P, I, I, I, L, P],
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],

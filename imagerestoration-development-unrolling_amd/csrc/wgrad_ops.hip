@@ -38,8 +38,9 @@ struct WgArgs {
   uint32_t nblk;
 };
 
-// output tile per wave: 128 x 96 (12 accumulators in AGPRs, one wave per SIMD).  A 64 x 96 tile at two
-// waves per SIMD measured slower (1.03 vs 0.86 ms at 512 x 96) and is not built.
+// output tile per wave: 32 TA x 32 TB (TA TB accumulators in AGPRs); wgrad_plan picks the tile.  (A
+// 64 x 96 tile at two waves per SIMD measured slower than 128 x 96 on a 512 x 96 output, 1.03 vs 0.86 ms,
+// it is taken only where 128 x 96 would be mostly padding.)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // exact split v = v0 + v1 + v2 of 8 values into bf16 terms (RNE casts: v_cvt_pk_bf16_f32)
@@ -242,32 +243,54 @@ __global__ __launch_bounds__(64 * WG_RW) void wgrad_reduce_kernel(const float* _
 
 struct WgPlan {
   int ta, tb;          // 32-row tiles per wave along the a / bop rows
+  int wps;             // waves per SIMD the instance is built for
   bool swap;           // operands exchanged (out^T = sum bop a^T): less tile padding
   int64_t CP;
   int cpi, nta, ntb;
   int64_t nchunk, nwaves;
 };
 
-// chunks of whole 32-pixel steps sized for ~3 rounds of waves over the 1024 SIMDs, at most 1024
-// chunks and kWgradWsBudget bytes of workspace (the wide v1.0 LNB weights, 2 hid x C = 1536 x 384,
-// would otherwise take 1024 x 2.4 MB); the operand order that pads the output tiles least
+// wave tiles built: 128 x 96 (the default), 192 x 64 (M x K = 192 x 48, the v1.0 model's first-level
+// W1 gradient: one tile holds the whole output at 75 % use instead of two at 37.5 %) and 64 x 96 at
+// two waves per SIMD (48 x 96, its W2 gradient).  The plan takes the cover of the output with the
+// least measured cost: tiles x the tile's cost per pixel step relative to 128 x 96 (192 x 64: 1.05,
+// its MFMA work plus eight operand blocks to split; 64 x 96: 0.8, measured at 96 x 192 on 256^2 x 32,
+// where three of them ran 0.754 ms against two 128 x 96 tiles' 0.657 ms; profiles/r05/wgrad).
+struct WgTile {
+  int ta, tb, wps;
+  float cost;
+};
+static constexpr WgTile kWgTiles[] = {{4, 3, 1, 1.0f}, {6, 2, 1, 1.05f}, {2, 3, 2, 0.8f}};
+// 0: the 128 x 96 tile only (A/B and test knob; GRR_WGRAD_TILES=0 sets it for a whole run)
+static int g_wgrad_tiles = [] {
+  const char* e = std::getenv("GRR_WGRAD_TILES");
+  return e && *e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+}();
+
+// chunks of whole 32-pixel steps sized for ~3 rounds of waves over the SIMDs, at most 4096 chunks and
+// kWgradWsBudget bytes of workspace (the wide v1.0 LNB weights, 2 hid x C = 1536 x 384, would otherwise
+// take 1024 x 2.4 MB); the operand order that pads the output tiles least
 static constexpr int64_t kWgradWsBudget = 128ll << 20;
 
 static WgPlan wgrad_plan(int B, int M, int K, int64_t P) {
   WgPlan p{};
-  p.ta = 4;
-  p.tb = 3;
-  const int wps = 1;
-  auto padded = [&](int rows_a, int rows_b) {
-    const int64_t ra = 32 * p.ta, rb = 32 * p.tb;
-    return ((rows_a + ra - 1) / ra * ra) * ((rows_b + rb - 1) / rb * rb);
-  };
-  p.swap = padded(K, M) < padded(M, K);
-  const int ma = p.swap ? K : M, kb = p.swap ? M : K;
-  p.nta = (ma + 32 * p.ta - 1) / (32 * p.ta);
-  p.ntb = (kb + 32 * p.tb - 1) / (32 * p.tb);
+  double best = 0.0;
+  const int ntiles = g_wgrad_tiles ? (int)(sizeof(kWgTiles) / sizeof(kWgTiles[0])) : 1;
+  for (int ti = 0; ti < ntiles; ++ti) {
+    const WgTile t = kWgTiles[ti];
+    for (int sw = 0; sw < 2; ++sw) {
+      const int ma = sw ? K : M, kb = sw ? M : K;
+      const int64_t na = (ma + 32 * t.ta - 1) / (32 * t.ta), nb = (kb + 32 * t.tb - 1) / (32 * t.tb);
+      const double cost = (double)(na * nb) * t.cost;
+      if (best == 0.0 || cost < best) {
+        best = cost;
+        p.ta = t.ta; p.tb = t.tb; p.wps = t.wps; p.swap = sw != 0;
+        p.nta = (int)na; p.ntb = (int)nb;
+      }
+    }
+  }
   const int64_t tiles = (int64_t)p.nta * p.ntb;
-  const int64_t target = 3072 * wps;
+  const int64_t target = 3072 * p.wps;
   int64_t cp = ((int64_t)B * P * tiles + target - 1) / target;
   cp = (cp + 31) / 32 * 32;
   const int64_t pmax = (P + 31) / 32 * 32;
@@ -276,7 +299,7 @@ static WgPlan wgrad_plan(int B, int M, int K, int64_t P) {
   for (;;) {
     p.cpi = (int)((P + cp - 1) / cp);
     p.nchunk = (int64_t)B * p.cpi;
-    if ((p.nchunk <= 1024 && p.nchunk * (int64_t)M * K * (int64_t)sizeof(float) <= kWgradWsBudget) || cp >= pmax)
+    if ((p.nchunk <= 4096 && p.nchunk * (int64_t)M * K * (int64_t)sizeof(float) <= kWgradWsBudget) || cp >= pmax)
       break;
     cp = std::min<int64_t>(pmax, cp * 2);
   }
@@ -290,6 +313,11 @@ static WgPlan wgrad_plan(int B, int M, int K, int64_t P) {
 using namespace grr;
 
 extern "C" {
+
+grr_status grr_wgrad_set_tiles(int enable) {
+  g_wgrad_tiles = enable ? 1 : 0;
+  return GRR_OK;
+}
 
 int64_t grr_wgrad_workspace_bytes(int B, int M, int K, int64_t P) {
   if (B <= 0 || M <= 0 || K <= 0 || P <= 0) return 0;
@@ -314,8 +342,16 @@ grr_status grr_wgrad(const float* a, const float* bop, float* out, void* workspa
   w.P = P; w.CP = p.CP; w.cpi = p.cpi; w.nta = p.nta; w.ntb = p.ntb; w.nblk = (uint32_t)p.nwaves;
   // 16-byte row loads need 4-aligned rows and chunk starts (CP is a multiple of 32)
   const dim3 g(w.nblk), t(64);
-  if (P % 4 == 0) hipLaunchKernelGGL((wgrad_x3_kernel<4, 3, true, 1>), g, t, 0, s, w);
-  else hipLaunchKernelGGL((wgrad_x3_kernel<4, 3, false, 1>), g, t, 0, s, w);
+  const bool vec = P % 4 == 0;
+#define GRR_WG_LAUNCH(TA, TB, WPS)                                                       \
+  if (p.ta == TA && p.tb == TB) {                                                        \
+    if (vec) hipLaunchKernelGGL((wgrad_x3_kernel<TA, TB, true, WPS>), g, t, 0, s, w);   \
+    else hipLaunchKernelGGL((wgrad_x3_kernel<TA, TB, false, WPS>), g, t, 0, s, w);      \
+  }
+  GRR_WG_LAUNCH(4, 3, 1)
+  else GRR_WG_LAUNCH(6, 2, 1)
+  else GRR_WG_LAUNCH(2, 3, 2)
+#undef GRR_WG_LAUNCH
   grr_status st = launch_status("grr_wgrad");
   if (st != GRR_OK) return st;
   const int64_t n = (int64_t)M * K;

@@ -629,6 +629,11 @@ def wgrad(a: Tensor, bop: Tensor) -> Tensor:
     return out
 
 
+def set_wgrad_tiles(enable: bool) -> None:
+    """grr_wgrad's per-shape wave tile (True, default) or the 128 x 96 tile only (grr_wgrad_set_tiles)."""
+    _native.call("grr_wgrad_set_tiles", int(bool(enable)))
+
+
 _WS_CACHE = {}
 
 

@@ -312,6 +312,10 @@ grr_status grr_ffn_forward(const float* x, const float* ln_w, const float* w_in,
  * atomics).  Replaces the library GEMM torch.matmul(g, x^T).sum(0) of the reference's autograd.
  * workspace: grr_wgrad_workspace_bytes(B, M, K, P) bytes of device memory; a, bop 16-B aligned. */
 int64_t grr_wgrad_workspace_bytes(int B, int M, int K, int64_t P);
+/* grr_wgrad's wave tiles: 1 (default) the plan picks 128 x 96, 192 x 64 or 64 x 96 per output shape
+ * (least padded MFMA work), 0 the 128 x 96 tile only.  Results are identical up to the fp32 summation
+ * order of the pixel chunks.  A/B and test knob. */
+grr_status grr_wgrad_set_tiles(int enable);
 grr_status grr_wgrad(const float* a, const float* bop, float* out, void* workspace, int B, int M, int K, int64_t P,
                      void* stream);
 

@@ -79,3 +79,32 @@ def test_conv_weight_gradients_match_autograd(K):
         fn.apply(x.float().to(DEV).contiguous(), wd).backward(gy.float().to(DEV))
         err = float((wd.grad.double().cpu() - wr.grad).abs().max() / wr.grad.abs().max())
         assert err <= 1e-5, (fn, err)
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 192, 48, 64, 64),      # v1.0 first-level W1 gradient: the 192 x 64 tile
+    (2, 48, 192, 64, 64),      # ... transposed (the plan swaps the operands)
+    (2, 48, 96, 64, 64),       # v1.0 first-level W2 gradient: the 64 x 96 tile, two waves per SIMD
+    (1, 40, 70, 13, 11),       # 64 x 96 tile with rows past the tile, P % 4 != 0, ragged step
+    (3, 170, 33, 9, 20),       # 192 x 64 tile with rows past it
+    (1, 12, 7, 3, 3),          # tiny
+])
+@pytest.mark.parametrize("tiles", [True, False])
+def test_wgrad_tile_plans_match_float64(K, shape, tiles):
+    """Every wave tile the plan can take (grr_wgrad_set_tiles(1)) and the 128 x 96 tile alone (0), against
+    the float64 reduction; each deterministic."""
+    b, m, k, h, w = shape
+    g = torch.Generator().manual_seed(m * 17 + k + h)
+    a = torch.randn(b, m, h, w, generator=g)
+    x = torch.randn(b, k, h, w, generator=g)
+    ref = _ref(a, x)
+    try:
+        K.set_wgrad_tiles(tiles)
+        got = K.wgrad(a.to(DEV), x.to(DEV))
+        got2 = K.wgrad(a.to(DEV), x.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        K.set_wgrad_tiles(True)
+    assert torch.equal(got, got2)
+    err = float((got.double().cpu() - ref).abs().max() / ref.abs().max())
+    assert err <= 1e-5, err
