@@ -598,6 +598,17 @@ static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, in
 // ---------------------------------------------------------------------------
 constexpr int X3K_KC = 2;   // k-steps per ring slot (3 slots: 72 KB at 4 row tiles, two workgroups per CU)
 
+// 16-byte LDS-DMA (lane l -> LDS m0 + 16 l) as an asm statement: hipcc answers the LDS-DMA builtin with
+// vmcnt(0) before every later LDS read (it cannot order the DMA's LDS write against them), which drains
+// the x loads the k-loop keeps two steps ahead.  The ring is ordered by the kernel itself (counted
+// vmcnt + barrier per chunk); the compiler's own counted waits stay correct with these extra,
+// uncounted operations in flight (vmcnt retires loads in order: a wait only gets stricter).
+typedef __attribute__((address_space(3))) float* x3_lds_t;
+__device__ __forceinline__ void x3_dma16(const void* src, const float* lds_wave_base) {
+  const uint32_t m0v = (uint32_t)(uintptr_t)(x3_lds_t)lds_wave_base;
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v)) : "memory");
+}
+
 enum { X3K_STORE = 0, X3K_LN = 1, X3K_SKIP = 2 };
 struct X3KArgs {
   const float* x;          // [B, K, P]
@@ -631,34 +642,47 @@ __global__ __launch_bounds__(64 * X3_WV, 4) void gemm_x3k_kernel(X3KArgs a) {
   constexpr int SLOT = X3K_KC * TM * 3 * 256;    // floats per ring slot (1 KB images)
   const int nch = (KS + X3K_KC - 1) / X3K_KC;
 
-  // chunk c -> slot c % 3: images [s][t][q] for k-steps c KC .. c KC + KC - 1, row tiles t < TM
-  auto issue = [&](int c) {
-    float* slot = x3_lds + (c % 3) * SLOT;
-    for (int i = wave; i < X3K_KC * TM * 3; i += X3_WV) {
-      const int q = i % 3, t = (i / 3) % TM, s = c * X3K_KC + i / (3 * TM);
-      int g = mt * TM + t;
-      if (g >= a.ngroups) g = a.ngroups - 1;     // rows past M: any valid image (never stored)
-      const int ss = s < KS ? s : KS - 1;
-      __builtin_amdgcn_global_load_lds((const void*)(fragb + g * a.CB + (int64_t)(ss * 3 + q) * 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void*)(slot + i * 256), 16, 0, 0);
+  // chunk c -> slot c % 3: images [s][t][q] for k-steps c KC .. c KC + KC - 1, row tiles t < TM.  This
+  // wave's images i = wave + X3_WV n and their fragment offsets are fixed across chunks (computed once:
+  // the per-chunk address is one clamp and one multiply-add, not a div / mod chain in the scalar unit)
+  constexpr int NIMG = X3K_KC * TM * 3, NI = (NIMG + X3_WV - 1) / X3_WV;
+  int64_t img_src[NI];                          // wave-uniform (the lane's 16 bytes added at issue)
+  int img_si[NI];
+#pragma unroll
+  for (int n = 0; n < NI; ++n) {
+    const int i = wave + X3_WV * n;
+    const int q = i % 3, t = (i / 3) % TM;
+    int g = mt * TM + t;
+    if (g >= a.ngroups) g = a.ngroups - 1;     // rows past M: any valid image (never stored)
+    img_src[n] = (int64_t)g * a.CB + q * 1024;
+    img_si[n] = i / (3 * TM);
+  }
+  auto issue = [&](int c, int slot_idx) {
+    float* slot = x3_lds + slot_idx * SLOT;
+#pragma unroll
+    for (int n = 0; n < NI; ++n) {
+      const int i = wave + X3_WV * n;
+      if (NIMG % X3_WV == 0 || i < NIMG) {
+        const int s = c * X3K_KC + img_si[n];
+        const int ss = s < KS ? s : KS - 1;
+        x3_dma16(fragb + img_src[n] + (int64_t)ss * 3072 + lane * 16, slot + i * 256);
+      }
     }
   };
 
-  // wave-uniform slab base + 32-bit lane offsets (K P < 2^30, checked on the host); rows past K load
-  // row K - 1 and are zeroed by a select (no per-load branches)
+  // the image's [K, P] slab as a buffer resource: row 16 s + j + 8 hf of pixel pc at voffset
+  // 4 (8 hf P + pc) + soffset 4 (16 s + j) P (wave-uniform, SGPR) -- no per-row address arithmetic in
+  // the vector or scalar units; rows past K fall past num_records and read 0 ((K + 16) P < 2^30,
+  // checked on the host)
   const float* xs = a.x + (int64_t)b * K * P;
   const uint32_t P32 = (uint32_t)P, pc32 = (uint32_t)pc;
-  const uint32_t loff = (uint32_t)(8 * hf) * P32 + pc32;   // lane offset within a 16-row k-step
-  // row 16 s + j + 8 hf: a wave-uniform row base (SGPRs) plus the lane offset; rows past K read a valid
-  // row (the base clamped, the half-wave offset dropped) and are zeroed by a select -- no branches
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xs), (short)0, (int)(4u * (uint32_t)K * P32), 0x00020000);
+  const uint32_t voff = 4u * ((uint32_t)(8 * hf) * P32 + pc32), Pb = 4u * P32;
   auto load = [&](int s, float (&v)[8]) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int rb = 16 * s + j;
-      const float* rp = xs + (int64_t)(rb < K ? rb : K - 1) * P;
-      const float t = rp[(hf && rb + 8 < K) ? loff : pc32];
-      v[j] = rb + 8 * hf < K ? t : 0.f;
-    }
+    for (int j = 0; j < 8; ++j)
+      v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, voff, (uint32_t)(16 * s + j) * Pb, 0));
   };
 
   f32x16 acc[TM];
@@ -668,49 +692,59 @@ __global__ __launch_bounds__(64 * X3_WV, 4) void gemm_x3k_kernel(X3KArgs a) {
   // 3-slot ring, chunks two ahead.  Per wave and chunk: its DMAs of chunk c + 2 (at least DMIN),
   // then 8 KC dword x loads (the k-steps one chunk ahead), in that order.
   constexpr int DMIN = X3K_KC * TM * 3 / X3_WV;
-  issue(0);
-  if (nch > 1) issue(1);
+  issue(0, 0);
+  if (nch > 1) issue(1, 1);
   float x0[8], x1[8];
   load(0, x0);
   load(1 < KS ? 1 : 0, x1);
-  for (int c = 0; c < nch; ++c) {
-    // this wave's DMAs of chunk c landed (younger: chunk c - 2's x loads, chunk c + 1's DMAs if any,
-    // chunk c - 1's x loads), then every wave's; one barrier per chunk: a wave at it has finished
-    // reading the slot the next issue() overwrites
+  static_assert(X3K_KC == 2, "two k-steps per chunk: x0 / x1 alternate by step parity");
+  // one k-step: split this step's x (loaded two steps ago), reload the buffer two steps ahead, multiply
+  auto kstep = [&](const float* slot, int s, int si, float (&xb)[8]) __attribute__((always_inline)) {
+    bf16x8 bq0, bq1, bq2;
+    split3x8(xb, bq0, bq1, bq2);
+    // the scheduler would otherwise sink the reload below the other buffer's split (which then waits on
+    // loads issued just before it, vmcnt(0))
+    __builtin_amdgcn_sched_barrier(0);
+    load(s + 2 < KS ? s + 2 : KS - 1, xb);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const float* im = slot + (si * TM * 3 + t * 3) * 256 + lane * 4;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(im);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(im + 256);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(im + 512);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq1, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, bq0, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq2, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq0, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq1, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq0, acc[t], 0, 0, 0);
+    }
+  };
+  // chunk c: this wave's DMAs of chunk c landed (younger: chunk c - 2's x loads, chunk c + 1's DMAs if
+  // any, chunk c - 1's x loads), then every wave's; one barrier per chunk: a wave at it has finished
+  // reading the slot the next issue() overwrites
+  auto chunk_top = [&](int c) __attribute__((always_inline)) {
     if (c == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if (c + 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(32 + DMIN) : "memory");
     else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (c + 2 < nch) issue(c + 2);               // slot (c + 2) % 3 was last read in chunk c - 1
-    const float* slot = x3_lds + (c % 3) * SLOT;
-    static_assert(X3K_KC == 2, "two k-steps per chunk: x0 / x1 alternate by step parity");
-#pragma unroll
-    for (int si = 0; si < X3K_KC; ++si) {
-      const int s = c * X3K_KC + si;
-      if (s < KS) {   // wave-uniform (only the last chunk can be short)
-      bf16x8 bq0, bq1, bq2;
-      if (si == 0) {
-        split3x8(x0, bq0, bq1, bq2);
-        load(s + 2 < KS ? s + 2 : KS - 1, x0);
-      } else {
-        split3x8(x1, bq0, bq1, bq2);
-        load(s + 2 < KS ? s + 2 : KS - 1, x1);
-      }
-#pragma unroll
-      for (int t = 0; t < TM; ++t) {
-        const float* im = slot + (si * TM * 3 + t * 3) * 256 + lane * 4;
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(im);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(im + 256);
-        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(im + 512);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq1, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, bq0, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq2, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq0, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq1, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq0, acc[t], 0, 0, 0);
-      }
-      }
-    }
+    asm volatile("" ::: "memory");               // the slot's LDS reads stay below the barrier
+    const int sc = c % 3;
+    if (c + 2 < nch) issue(c + 2, sc == 0 ? 2 : sc - 1);   // slot (c + 2) % 3 was last read in chunk c - 1
+    return x3_lds + sc * SLOT;
+  };
+  // whole chunks in a branch-free body (x0 / x1 always in the same order, so the compiler's counted
+  // waits before each split allow the other buffer's eight loads in flight), the odd k-step after
+  const int nfull = KS / X3K_KC;
+  for (int c = 0; c < nfull; ++c) {
+    const float* slot = chunk_top(c);
+    kstep(slot, c * X3K_KC, 0, x0);
+    kstep(slot, c * X3K_KC + 1, 1, x1);
+  }
+  if (nfull < nch) {
+    const float* slot = chunk_top(nfull);
+    kstep(slot, nfull * X3K_KC, 0, x0);
   }
   float* const obase = a.out + (int64_t)b * M * P;
   float cs = 1.f, s0 = 0.f, s1 = 1.f;
@@ -738,7 +772,7 @@ template <int EPI = X3K_STORE>
 static grr_status launch_x3k(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
                              hipStream_t s, const char* name, const float* sd = nullptr, const float* res = nullptr,
                              const float* skip = nullptr) {
-  GRR_REQUIRE((int64_t)K * P < (1ll << 30) && (int64_t)M * P < (1ll << 30), GRR_ERR_UNSUPPORTED,
+  GRR_REQUIRE((int64_t)(K + 16) * P < (1ll << 30) && (int64_t)M * P < (1ll << 30), GRR_ERR_UNSUPPORTED,
               "%s: K*P or M*P too large for 32-bit offsets", name);
   X3KArgs a{};
   a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M; a.sd = sd; a.res = res; a.skip = skip;

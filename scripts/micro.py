@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--lnb-fused", type=int, default=1, choices=[0, 1],
                     help="LNB, C <= 96: 1 the fused pass, 0 the head + mix kernels (grr_lnb_set_fused)")
     ap.add_argument("--hid", type=int, default=256, help="LNB hidden width")
+    ap.add_argument("--cin", type=int, default=192, help="conv_mk: input channels")
+    ap.add_argument("--cout", type=int, default=48, help="conv_mk: output channels")
     ap.add_argument("--stamps", action="store_true",
                     help="LNB fused, GRR_FUSED_STAMP build: print the per-phase s_memtime sums of each wave role")
     ap.add_argument("--mode", type=int, default=0, help="term: 0 GLR, 1 pair Laplacian, 2 prox")
@@ -90,6 +92,10 @@ def main():
     elif args.kernel == "conv1x1":
         wt = torch.rand(2 * c, c, 1, 1, device=dev)
         fn = lambda: K.conv1x1(x, wt)  # noqa: E731
+    elif args.kernel == "conv_mk":     # conv1x1 at --cin -> --cout channels
+        xk = torch.rand(b, args.cin, h, w, device=dev)
+        wt = torch.rand(args.cout, args.cin, 1, 1, device=dev)
+        fn = lambda: K.conv1x1(xk, wt)  # noqa: E731
     elif args.kernel == "conv_deep":   # the window FFBlock's W_in (K = 256 -> M = 1364), K-streaming x3 GEMM
         xd = torch.rand(b, 256, h, w, device=dev)
         wt = torch.rand(1364, 256, 1, 1, device=dev)
