@@ -429,7 +429,6 @@ struct X3Args {
   uint32_t nblk;
 };
 
-__device__ float g_x3_scratch[64];
 
 #ifndef GRR_X3_WAVES   // waves (32-pixel columns) per workgroup: the W chunk images DMA'd once serve them all
 #define GRR_X3_WAVES 8
@@ -468,15 +467,15 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3_kernel(X3Args a) {
   float xv[KS][8];
   // wave-uniform slab base + 32-bit lane offsets (K P < 2^30, checked on the host); rows past K load
   // row K - 1 and are zeroed by a select (no per-load branches)
-  const float* xs = a.x + (int64_t)b * K * P;
+  // (through a buffer descriptor: row 16 s + j in soffset, rows >= K past num_records read 0)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x + (int64_t)b * K * P), (short)0, (int)(4u * (uint32_t)K * (uint32_t)P), 0x00020000);
+  const uint32_t xvo = 4u * ((uint32_t)(8 * hf) * (uint32_t)P + (uint32_t)pc), xPb = 4u * (uint32_t)P;
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 16 * s + 8 * hf + j;
-      const float v = xs[(uint32_t)(k < K ? k : K - 1) * (uint32_t)P + (uint32_t)pc];
-      xv[s][j] = k < K ? v : 0.f;
-    }
+    for (int j = 0; j < 8; ++j)
+      xv[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, xvo, (uint32_t)(16 * s + j) * xPb, 0));
   float rstd = 1.f;
   if constexpr (LN) {                          // CustomLayerNorm statistics (REF:916-922)
     float sum = 0.f;
@@ -502,10 +501,11 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3_kernel(X3Args a) {
   for (int s = 0; s < KS; ++s)
     split3x8(xv[s], bq[s][0], bq[s][1], bq[s][2]);
 
-  float* const obase = a.out + (int64_t)b * M * P;
-  // full tile: every lane's pixel in range -> stores through a uniform row base + 32-bit offset
-  const bool full_px = (int64_t)tile * X3_PX + X3_PX <= P;
-  const uint32_t so = (uint32_t)((4 * hf) * P + r) * 4u;
+  // the image's [M, P] output slab as a buffer resource ((M + 32) P < 2^30, checked on the host)
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * M * P, (short)0,
+                                                                       (int)(4u * (uint32_t)M * (uint32_t)P), 0x00020000);
+  const uint32_t Pb = 4u * (uint32_t)P;
+  const uint32_t so = (uint32_t)((4 * hf) * P + pc) * 4u;
   for (int c = 0; c < nch; ++c) {
     // chunk c landed (this wave's DMAs; later ops: the previous chunk's stores), then all waves'
     if (c == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -539,26 +539,16 @@ __global__ __launch_bounds__(64 * X3_WV) void gemm_x3_kernel(X3Args a) {
         a0 = n0; a1 = n1; a2 = n2;
       }
     }
-    // epilogue: 16 stores per tile, every one issued (rows >= M / pixels >= P -> scratch)
-    if (full_px && (c + 1) * X3_MCH <= M) {
+    // epilogue: 16 buffer stores per tile, row m0 in soffset; rows >= M fall past num_records and are
+    // dropped; lanes past P (the image's last pixel tile) computed pixel P - 1 from the same x column
+    // and store that same value there
 #pragma unroll
-      for (int t = 0; t < X3_NT; ++t)
+    for (int t = 0; t < X3_NT; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int m0 = c * X3_MCH + t * 32 + (i & 3) + 8 * (i >> 2);
-          float* row = obase + (int64_t)m0 * P + (int64_t)tile * X3_PX + wave * 32;
-          *reinterpret_cast<float*>(reinterpret_cast<char*>(row) + so) = acc[t][i] * rstd;
-        }
-    } else {
-#pragma unroll
-      for (int t = 0; t < X3_NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int m = c * X3_MCH + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-          float* dst = (m < M && pin) ? obase + (int64_t)m * P + p : g_x3_scratch + lane;
-          *dst = acc[t][i] * rstd;
-        }
-    }
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t m0 = (uint32_t)(c * X3_MCH + t * 32 + (i & 3) + 8 * (i >> 2));
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[t][i] * rstd), ors, so, m0 * Pb, 0);
+      }
   }
 }
 
@@ -566,7 +556,8 @@ template <bool LN>
 static grr_status launch_x3(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
                             hipStream_t s, const char* name) {
   GRR_REQUIRE(K >= 1 && K <= 128, GRR_ERR_UNSUPPORTED, "%s: K=%d outside [1, 128]", name, K);
-  GRR_REQUIRE((int64_t)K * P < (1ll << 30), GRR_ERR_UNSUPPORTED, "%s: K*P too large for 32-bit offsets", name);
+  GRR_REQUIRE((int64_t)(K + 16) * P < (1ll << 30) && (int64_t)(M + 32) * P < (1ll << 30), GRR_ERR_UNSUPPORTED,
+              "%s: K*P or M*P too large for 32-bit offsets", name);
   X3Args a{};
   a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M;
   a.nch = (M + X3_MCH - 1) / X3_MCH;
@@ -746,25 +737,30 @@ __global__ __launch_bounds__(64 * X3_WV, 4) void gemm_x3k_kernel(X3KArgs a) {
     const float* slot = chunk_top(nfull);
     kstep(slot, nfull * X3K_KC, 0, x0);
   }
-  float* const obase = a.out + (int64_t)b * M * P;
   float cs = 1.f, s0 = 0.f, s1 = 1.f;
   if constexpr (EPI == X3K_LN) cs = a.sd[(int64_t)b * P + pc];   // CustomLayerNorm 1/sigma (REF:921-922)
   if constexpr (EPI == X3K_SKIP) { s0 = a.skip[0]; s1 = a.skip[1]; }
-  // row m = 32 g + (i & 3) + 8 (i >> 2) + 4 hf: a wave-uniform row base per (tile, i) plus the lane's
-  // offset 4 hf P + p (M P < 2^30, checked on the host)
-  const float* rbase = a.res + (int64_t)b * M * P;
-  const uint32_t eoff = (uint32_t)(4 * hf) * P32 + (uint32_t)p;
+  // row m = 32 g + (i & 3) + 8 (i >> 2) + 4 hf through buffer descriptors of the image's [M, P] slabs: the
+  // lane's 4 (4 hf P + pc) in voffset, the row's 4 m P in soffset ((M + 32) P < 2^30, checked on the
+  // host); rows >= M fall past num_records (stores dropped); lanes past P computed pixel P - 1 from the
+  // same x column and store that same value there
+  const uint32_t MPb = 4u * (uint32_t)M * P32;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)b * M * P, (short)0, (int)MPb,
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(EPI == X3K_SKIP ? a.res + (int64_t)b * M * P : a.out), (short)0,
+      EPI == X3K_SKIP ? (int)MPb : 0, 0x00020000);
+  const uint32_t eoff = 4u * ((uint32_t)(4 * hf) * P32 + pc32);
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int mr = (mt * TM + t) * 32 + (i & 3) + 8 * (i >> 2);
-      if (mr + 4 * hf < M && pin) {
-        float v = acc[t][i];
-        if constexpr (EPI == X3K_LN) v *= cs;
-        if constexpr (EPI == X3K_SKIP) v = s0 * (rbase + (int64_t)mr * P)[eoff] + s1 * v;   // REF:962-964
-        (obase + (int64_t)mr * P)[eoff] = v;
-      }
+      const uint32_t mr = (uint32_t)((mt * TM + t) * 32 + (i & 3) + 8 * (i >> 2));
+      float v = acc[t][i];
+      if constexpr (EPI == X3K_LN) v *= cs;
+      if constexpr (EPI == X3K_SKIP)   // REF:962-964
+        v = s0 * __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, eoff, mr * Pb, 0)) + s1 * v;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, eoff, mr * Pb, 0);
     }
 }
 
@@ -772,7 +768,7 @@ template <int EPI = X3K_STORE>
 static grr_status launch_x3k(const float* x, const uint16_t* frag, float* out, int B, int K, int M, int64_t P,
                              hipStream_t s, const char* name, const float* sd = nullptr, const float* res = nullptr,
                              const float* skip = nullptr) {
-  GRR_REQUIRE((int64_t)(K + 16) * P < (1ll << 30) && (int64_t)M * P < (1ll << 30), GRR_ERR_UNSUPPORTED,
+  GRR_REQUIRE((int64_t)(K + 16) * P < (1ll << 30) && (int64_t)(M + 128) * P < (1ll << 30), GRR_ERR_UNSUPPORTED,
               "%s: K*P or M*P too large for 32-bit offsets", name);
   X3KArgs a{};
   a.x = x; a.frag = frag; a.out = out; a.P = P; a.K = K; a.M = M; a.sd = sd; a.res = res; a.skip = skip;
