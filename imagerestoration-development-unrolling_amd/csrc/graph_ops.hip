@@ -1395,6 +1395,14 @@ struct Step2Args {
   uint32_t nblk;
 };
 
+typedef float pk2f __attribute__((ext_vector_type(2)));
+// GRR_S2_PK=1: the pair kernel's operator pipeline on column pairs (v_pk_fma_f32 & co., ~20 % fewer vector
+// instructions in the stage loops, no loop spills).  Measured no gain (same box, profiles/r05/pk: bench
+// 136.8 / 137.1 scalar vs 135.4 / 135.1 packed MPix/s, step2 0.627 vs 0.620 of HBM): the pass is not
+// bound by vector-instruction issue.  Kept as an A/B build, off.
+#ifndef GRR_S2_PK
+#define GRR_S2_PK 0
+#endif
 template <int V>
 struct OpPipe {
   // Register slots of the row pipeline, 4-periodic: at phase P (step t with t = P mod 4 in
@@ -1427,7 +1435,7 @@ struct OpPipe {
   // CE (column strips of a wider image): c0 is the image column, the image is Wr wide (columns
   // >= Wr are lanes past the right edge: their l / o are zeroed like rows outside the image)
   template <int P, int W, bool EDGE = true, bool CE = false>
-  __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
+  __device__ __forceinline__ void advance_scalar(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
                                           int t, int H, int c0, const Taps& tL, const Taps& tG,
                                           float (&tl)[V], float (&tg)[V], int Wr = W) {
     constexpr int K0 = P & 3, K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
@@ -1509,6 +1517,142 @@ struct OpPipe {
       }
     }
   }
+
+  // The same arithmetic on column pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two columns per
+  // vector instruction; the operations, operands and their order per column are the scalar version's,
+  // so the roundings are too).  Neighbour columns and the boundary selects are formed per column as
+  // there, then paired.
+  // GRR_S2_PK: the pair kernel at W = 256 (its column-strip instances, CE, stay scalar: packed, their
+  // register pressure spills ~400 B per lane)
+  template <int P, int W, bool EDGE = true, bool CE = false>
+  __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
+                                          int t, int H, int c0, const Taps& tL, const Taps& tG,
+                                          float (&tl)[V], float (&tg)[V], int Wr = W) {
+    if constexpr (CE || GRR_S2_PK == 0) {
+      advance_scalar<P, W, EDGE, CE>(xin, WL, WG, t, H, c0, tL, tG, tl, tg, Wr);
+      return;
+    }
+    static_assert(V % 2 == 0, "column pairs");
+    typedef pk2f f2;
+    constexpr int NP = V / 2;
+    constexpr int K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
+    const int WW = CE ? Wr : W;
+#define pr(a, q) pk2f{(a)[2 * (q)], (a)[2 * (q) + 1]}
+#define sp(v) pk2f{(v), (v)}
+#define fma2(a, b, c) __builtin_elementwise_fma((a), (b), (c))
+#pragma unroll
+    for (int j = 0; j < V; ++j) X[K3][j] = xin[j];
+    const float (&X1)[V] = X[K1];
+    const float (&X2)[V] = X[K2];
+    const float (&X3)[V] = X[K3];
+    {  // s at row t-1 -> slot K3 (rows t-3, t-2 in K1, K2)
+      const float xp = lane_prev(X2[V - 1]), xq = lane_next(X2[0]);
+      float xl[V], xr[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        xl[j] = col > 0 ? (j > 0 ? X2[j - 1] : xp) : X2[j];
+        xr[j] = col < WW - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
+      }
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const f2 x1 = pr(X1, q), x2 = pr(X2, q), x3 = pr(X3, q), l2 = pr(xl, q), r2 = pr(xr, q);
+        f2 sv = sp(tL.u) * x1;
+        sv = fma2(sp(tL.l), l2, sv); sv = fma2(sp(tL.c), x2, sv); sv = fma2(sp(tL.r), r2, sv);
+        sv = fma2(sp(tL.d), x3, sv);
+        SL[K3][2 * q] = sv.x; SL[K3][2 * q + 1] = sv.y;
+        f2 sg = sp(tG.u) * x1;
+        sg = fma2(sp(tG.l), l2, sg); sg = fma2(sp(tG.c), x2, sg); sg = fma2(sp(tG.r), r2, sg);
+        sg = fma2(sp(tG.d), x3, sg);
+        SG[K3][2 * q] = sg.x; SG[K3][2 * q + 1] = sg.y;
+      }
+    }
+    {  // l and o at row r = t-2 -> slot K3 (zero outside the image); s rows t-3, t-2, t-1 = K1, K2, K3
+      const int r = t - 2;
+      const bool rin = r >= 0 && r < H;
+      const float (&S0)[V] = SL[K1];
+      const float (&S1)[V] = SL[K2];
+      const float (&S2)[V] = SL[K3];
+      const float (&G0)[V] = SG[K1];
+      const float (&G1)[V] = SG[K2];
+      const float (&G2)[V] = SG[K3];
+      const float pv = lane_prev(S1[V - 1]), nx = lane_next(S1[0]);
+      const float spn = lane_prev(G1[V - 1]), snn = lane_next(G1[0]);
+      const float wp = lane_prev(WG[0][V - 1]);
+      const float (&cvp)[V] = cv[(P + 1) & 1];
+      float up[V], dn[V], lf[V], rt[V], snx[V], spv[V], chl[V], cvu[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int col = c0 + j;
+        up[j] = (!EDGE || r > 0) ? S0[j] : S1[j];
+        dn[j] = (!EDGE || r < H - 1) ? S2[j] : S1[j];
+        lf[j] = col > 0 ? (j > 0 ? S1[j - 1] : pv) : S1[j];
+        rt[j] = col < WW - 1 ? (j < V - 1 ? S1[j + 1] : nx) : S1[j];
+        snx[j] = j < V - 1 ? G1[j + 1] : snn;
+        spv[j] = j > 0 ? G1[j - 1] : spn;
+        chl[j] = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
+        cvu[j] = (!EDGE || r > 0) ? cvp[j] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const f2 w0 = pr(WL[0], q), w1 = pr(WL[1], q), w2 = pr(WL[2], q), w3 = pr(WL[3], q);
+        f2 wx = w0 * pr(up, q);
+        wx = fma2(w1, pr(lf, q), wx);
+        wx = fma2(w2, pr(rt, q), wx);
+        wx = fma2(w3, pr(dn, q), wx);
+        const f2 s1 = pr(S1, q);
+        const f2 lv = s1 - wx;
+        const f2 sv = pr(G1, q);
+        f2 ov = pr(WG[0], q) * (sv - pr(snx, q));
+        ov = fma2(pr(chl, q), sv - pr(spv, q), ov);
+        ov = fma2(pr(WG[1], q), sv - pr(G2, q), ov);
+        ov = fma2(pr(cvu, q), sv - pr(G0, q), ov);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * q + e;
+          const int col = c0 + j;
+          const bool in = (!EDGE || rin) && (!CE || col < WW);
+          L[K3][j] = in ? lv[e] : 0.f;
+          O[K3][j] = in ? ov[e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) cv[P & 1][j] = WG[1][j];
+    }
+    {  // S^T at row t-3 from l / o rows t-4, t-3, t-2 = slots K1, K2, K3
+      const float (&L0)[V] = L[K1];
+      const float (&L1)[V] = L[K2];
+      const float (&L2)[V] = L[K3];
+      const float (&O0)[V] = O[K1];
+      const float (&O1)[V] = O[K2];
+      const float (&O2)[V] = O[K3];
+      const float lp = lane_prev(L1[V - 1]), ln = lane_next(L1[0]);
+      const float op = lane_prev(O1[V - 1]), on = lane_next(O1[0]);
+      float nx[V], pv[V], gx[V], gp[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        nx[j] = j < V - 1 ? L1[j + 1] : ln;
+        pv[j] = j > 0 ? L1[j - 1] : lp;
+        gx[j] = j < V - 1 ? O1[j + 1] : on;
+        gp[j] = j > 0 ? O1[j - 1] : op;
+      }
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        f2 v = sp(tL.u) * pr(L2, q);
+        v = fma2(sp(tL.l), pr(nx, q), v); v = fma2(sp(tL.c), pr(L1, q), v); v = fma2(sp(tL.r), pr(pv, q), v);
+        v = fma2(sp(tL.d), pr(L0, q), v);
+        tl[2 * q] = v.x; tl[2 * q + 1] = v.y;
+        f2 w = sp(tG.u) * pr(O2, q);
+        w = fma2(sp(tG.l), pr(gx, q), w); w = fma2(sp(tG.c), pr(O1, q), w); w = fma2(sp(tG.r), pr(gp, q), w);
+        w = fma2(sp(tG.d), pr(O0, q), w);
+        tg[2 * q] = w.x; tg[2 * q + 1] = w.y;
+      }
+    }
+#undef pr
+#undef sp
+#undef fma2
+  }
+
 };
 
 // The GTV proximal term C^T phi_gamma(C s) of the same input rows an OpPipe streams (the first-pair
