@@ -1006,18 +1006,15 @@ __device__ __forceinline__ float lnext(float v) {   // lane + 1 (0 at lane 63)
 // VGPRs = 3 waves per SIMD, which also gives 4 three-wave workgroups per CU instead of 2 at the
 // 176-182 VGPRs the compiler picks unconstrained), up to 16 for V <= 2 (128 VGPRs).
 template <int V> struct TermRowMax { static constexpr int F = V == 4 ? 12 : 16; };
-// gw rows of the read-modify-write through LDS-DMA one row ahead (GRR_TERM_GW_DMA, default on): the
-// summing wave copies gw row r + 1 of its planes into an LDS ring right after adding row r, so the
-// next row's read-modify-write reads LDS instead of waiting on a global load after the partials'
-// barrier; no registers are held across the step (an early global read into VGPRs spilled, §4.r4)
-#ifndef GRR_TERM_GW_DMA
-#define GRR_TERM_GW_DMA 1
-#endif
+// gw rows of the read-modify-write through LDS-DMA one row ahead: the summing wave copies gw row r + 1 of
+// its planes into an LDS ring right after adding row r, so the next row's read-modify-write reads LDS
+// instead of waiting on a global load after the partials' barrier; no registers are held across the
+// step (an early global read into VGPRs spilled, §4.r4)
 // Only where it measured faster (profiles/r04/term/ab_gw_dma.txt): not in GGTV's instance (MODE 2, the
 // register-heaviest: the ring costs it spills) nor in the one-strip 4-column instances (W = 256, 3-4 %
 // slower); 12 % faster at W = 128, 7 % at W = 512 (strips)
 __host__ __device__ constexpr bool term_gw_dma(int mode, int v, bool strips) {
-  return GRR_TERM_GW_DMA && mode != 2 && (strips || v < 4);
+  return mode != 2 && (strips || v < 4);
 }
 typedef __attribute__((address_space(3))) float* lds_f32_t;
 __device__ __forceinline__ void dma_dword(const float* src, float* lds_wave_base) {
@@ -1079,7 +1076,7 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
   constexpr bool kGwDma = !RING && term_gw_dma(MODE, V, STRIPS);
   // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats),
-  // then (GRR_TERM_GW_DMA) the gw row ring [row parity][plane][element j][lane] (2 WPL 64 V floats)
+  // then (term_gw_dma) the gw row ring [row parity][plane][element j][lane] (2 WPL 64 V floats)
   extern __shared__ __attribute__((aligned(16))) float part_dyn[];
   auto part = [&](int pr, int ff, int e) { return part_dyn + ((pr * F + ff) * WPL + e) * (64 * V); };
   auto gring = [&](int pr, int e) { return part_dyn + (2 * F * WPL + pr * WPL + e) * (64 * V); };

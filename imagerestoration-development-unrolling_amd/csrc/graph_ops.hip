@@ -650,15 +650,11 @@ struct RowLoadsV {
   float th[(V + 1) / 2];   // half-resolution operand at row (t-3)/2
 };
 
-// Minimum waves per SIMD asked of the LDS-ring step kernel (LW below).  Without its weight
-// registers it needs 178 VGPRs (2 waves/SIMD); forcing 3 (168 VGPRs) spills 10-12 VGPRs of
-// store addresses into the row loop and measured 2.37 -> 2.81 ms per launch, so 1 (no bound).
-#ifndef GRR_ROW_WPE
-#define GRR_ROW_WPE 1
-#endif
+// No minimum waves per SIMD asked of the row kernel: without its weight registers the LDS-ring
+// step kernel needs 178 VGPRs (2 waves/SIMD); forcing 3 (168 VGPRs) spilled 10-12 VGPRs of store
+// addresses into the row loop and measured 2.37 -> 2.81 ms per launch.
 template <bool GLR, int GTV, int EPI, int V>
-__global__ __launch_bounds__(NT) __attribute__((
-    amdgpu_waves_per_eu((GLR && GTV == GTV_PAIR && EPI == EPI_STEP && V == 4) ? GRR_ROW_WPE : 1)))
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1)))
 void graph_row_kernel(OpArgs a) {
   constexpr int NH = (V + 1) / 2;    // half-resolution values per lane
   const int lane = threadIdx.x & 63;
@@ -1130,10 +1126,6 @@ static grr_status launch_op(const OpArgs& a0, int B, hipStream_t s, const char* 
 // w_up of row r+1, so it is written one row late.  Same arithmetic order as
 // edge_weights_kernel (REF:146-175).
 // ---------------------------------------------------------------------------
-// GRR_EDGE_FASTDIV (A/B build): hardware reciprocal and exp in the normalisation and the softmax
-#ifndef GRR_EDGE_FASTDIV
-#define GRR_EDGE_FASTDIV 0
-#endif
 #ifndef GRR_EDGE_MIN_WAVES
 #define GRR_EDGE_MIN_WAVES 8192
 #endif
@@ -1193,14 +1185,8 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
       // (a segment's first rows are normalised by the prologue, elsewhere by the loop)
       for (int f = 0; f < F; ++f) ss = __builtin_fmaf(raw[f][j], raw[f][j], ss);
       const float den = fmaxf(sqrtf(ss), 1e-12f);
-#if GRR_EDGE_FASTDIV
-      const float rd = __builtin_amdgcn_rcpf(den);
-#pragma unroll
-      for (int f = 0; f < F; ++f) dst[f][j] = (raw[f][j] * rd) * M[f];
-#else
 #pragma unroll
       for (int f = 0; f < F; ++f) dst[f][j] = (raw[f][j] / den) * M[f];
-#endif
     }
   };
   load_raw(r0 - 1);                                  // clamped: row 0 is its own up neighbour
@@ -1235,16 +1221,9 @@ __global__ __launch_bounds__(NT) void edge_row_kernel(EdgeArgs a) {
         s3 += v * fN[f][j];
       }
       const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
-#if GRR_EDGE_FASTDIV
-      const float e0 = __expf(s0 - m), e1 = __expf(s1 - m), e2 = __expf(s2 - m), e3 = __expf(s3 - m);
-      const float sum = ((e0 + e1) + e2) + e3;
-      const float rs = __builtin_amdgcn_rcpf(sum);
-      w0[j] = e0 * rs; w1[j] = e1 * rs; w2[j] = e2 * rs; w3[j] = e3 * rs;
-#else
       const float e0 = expf(s0 - m), e1 = expf(s1 - m), e2 = expf(s2 - m), e3 = expf(s3 - m);
       const float sum = ((e0 + e1) + e2) + e3;
       w0[j] = e0 / sum; w1[j] = e1 / sum; w2[j] = e2 / sum; w3[j] = e3 / sum;
-#endif
     }
     const int64_t ro = (int64_t)r * W;
     if (lane_on && own) {
@@ -1395,14 +1374,6 @@ struct Step2Args {
   uint32_t nblk;
 };
 
-typedef float pk2f __attribute__((ext_vector_type(2)));
-// GRR_S2_PK=1: the pair kernel's operator pipeline on column pairs (v_pk_fma_f32 & co., ~20 % fewer vector
-// instructions in the stage loops, no loop spills).  Measured no gain (same box, profiles/r05/pk: bench
-// 136.8 / 137.1 scalar vs 135.4 / 135.1 packed MPix/s, step2 0.627 vs 0.620 of HBM): the pass is not
-// bound by vector-instruction issue.  Kept as an A/B build, off.
-#ifndef GRR_S2_PK
-#define GRR_S2_PK 0
-#endif
 template <int V>
 struct OpPipe {
   // Register slots of the row pipeline, 4-periodic: at phase P (step t with t = P mod 4 in
@@ -1435,7 +1406,7 @@ struct OpPipe {
   // CE (column strips of a wider image): c0 is the image column, the image is Wr wide (columns
   // >= Wr are lanes past the right edge: their l / o are zeroed like rows outside the image)
   template <int P, int W, bool EDGE = true, bool CE = false>
-  __device__ __forceinline__ void advance_scalar(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
+  __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
                                           int t, int H, int c0, const Taps& tL, const Taps& tG,
                                           float (&tl)[V], float (&tg)[V], int Wr = W) {
     constexpr int K0 = P & 3, K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
@@ -1517,142 +1488,6 @@ struct OpPipe {
       }
     }
   }
-
-  // The same arithmetic on column pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two columns per
-  // vector instruction; the operations, operands and their order per column are the scalar version's,
-  // so the roundings are too).  Neighbour columns and the boundary selects are formed per column as
-  // there, then paired.
-  // GRR_S2_PK: the pair kernel at W = 256 (its column-strip instances, CE, stay scalar: packed, their
-  // register pressure spills ~400 B per lane)
-  template <int P, int W, bool EDGE = true, bool CE = false>
-  __device__ __forceinline__ void advance(const float (&xin)[V], const float (&WL)[4][V], const float (&WG)[2][V],
-                                          int t, int H, int c0, const Taps& tL, const Taps& tG,
-                                          float (&tl)[V], float (&tg)[V], int Wr = W) {
-    if constexpr (CE || GRR_S2_PK == 0) {
-      advance_scalar<P, W, EDGE, CE>(xin, WL, WG, t, H, c0, tL, tG, tl, tg, Wr);
-      return;
-    }
-    static_assert(V % 2 == 0, "column pairs");
-    typedef pk2f f2;
-    constexpr int NP = V / 2;
-    constexpr int K1 = (P + 1) & 3, K2 = (P + 2) & 3, K3 = (P + 3) & 3;
-    const int WW = CE ? Wr : W;
-#define pr(a, q) pk2f{(a)[2 * (q)], (a)[2 * (q) + 1]}
-#define sp(v) pk2f{(v), (v)}
-#define fma2(a, b, c) __builtin_elementwise_fma((a), (b), (c))
-#pragma unroll
-    for (int j = 0; j < V; ++j) X[K3][j] = xin[j];
-    const float (&X1)[V] = X[K1];
-    const float (&X2)[V] = X[K2];
-    const float (&X3)[V] = X[K3];
-    {  // s at row t-1 -> slot K3 (rows t-3, t-2 in K1, K2)
-      const float xp = lane_prev(X2[V - 1]), xq = lane_next(X2[0]);
-      float xl[V], xr[V];
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int col = c0 + j;
-        xl[j] = col > 0 ? (j > 0 ? X2[j - 1] : xp) : X2[j];
-        xr[j] = col < WW - 1 ? (j < V - 1 ? X2[j + 1] : xq) : X2[j];
-      }
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        const f2 x1 = pr(X1, q), x2 = pr(X2, q), x3 = pr(X3, q), l2 = pr(xl, q), r2 = pr(xr, q);
-        f2 sv = sp(tL.u) * x1;
-        sv = fma2(sp(tL.l), l2, sv); sv = fma2(sp(tL.c), x2, sv); sv = fma2(sp(tL.r), r2, sv);
-        sv = fma2(sp(tL.d), x3, sv);
-        SL[K3][2 * q] = sv.x; SL[K3][2 * q + 1] = sv.y;
-        f2 sg = sp(tG.u) * x1;
-        sg = fma2(sp(tG.l), l2, sg); sg = fma2(sp(tG.c), x2, sg); sg = fma2(sp(tG.r), r2, sg);
-        sg = fma2(sp(tG.d), x3, sg);
-        SG[K3][2 * q] = sg.x; SG[K3][2 * q + 1] = sg.y;
-      }
-    }
-    {  // l and o at row r = t-2 -> slot K3 (zero outside the image); s rows t-3, t-2, t-1 = K1, K2, K3
-      const int r = t - 2;
-      const bool rin = r >= 0 && r < H;
-      const float (&S0)[V] = SL[K1];
-      const float (&S1)[V] = SL[K2];
-      const float (&S2)[V] = SL[K3];
-      const float (&G0)[V] = SG[K1];
-      const float (&G1)[V] = SG[K2];
-      const float (&G2)[V] = SG[K3];
-      const float pv = lane_prev(S1[V - 1]), nx = lane_next(S1[0]);
-      const float spn = lane_prev(G1[V - 1]), snn = lane_next(G1[0]);
-      const float wp = lane_prev(WG[0][V - 1]);
-      const float (&cvp)[V] = cv[(P + 1) & 1];
-      float up[V], dn[V], lf[V], rt[V], snx[V], spv[V], chl[V], cvu[V];
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int col = c0 + j;
-        up[j] = (!EDGE || r > 0) ? S0[j] : S1[j];
-        dn[j] = (!EDGE || r < H - 1) ? S2[j] : S1[j];
-        lf[j] = col > 0 ? (j > 0 ? S1[j - 1] : pv) : S1[j];
-        rt[j] = col < WW - 1 ? (j < V - 1 ? S1[j + 1] : nx) : S1[j];
-        snx[j] = j < V - 1 ? G1[j + 1] : snn;
-        spv[j] = j > 0 ? G1[j - 1] : spn;
-        chl[j] = col > 0 ? (j > 0 ? WG[0][j - 1] : wp) : 0.f;
-        cvu[j] = (!EDGE || r > 0) ? cvp[j] : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        const f2 w0 = pr(WL[0], q), w1 = pr(WL[1], q), w2 = pr(WL[2], q), w3 = pr(WL[3], q);
-        f2 wx = w0 * pr(up, q);
-        wx = fma2(w1, pr(lf, q), wx);
-        wx = fma2(w2, pr(rt, q), wx);
-        wx = fma2(w3, pr(dn, q), wx);
-        const f2 s1 = pr(S1, q);
-        const f2 lv = s1 - wx;
-        const f2 sv = pr(G1, q);
-        f2 ov = pr(WG[0], q) * (sv - pr(snx, q));
-        ov = fma2(pr(chl, q), sv - pr(spv, q), ov);
-        ov = fma2(pr(WG[1], q), sv - pr(G2, q), ov);
-        ov = fma2(pr(cvu, q), sv - pr(G0, q), ov);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int j = 2 * q + e;
-          const int col = c0 + j;
-          const bool in = (!EDGE || rin) && (!CE || col < WW);
-          L[K3][j] = in ? lv[e] : 0.f;
-          O[K3][j] = in ? ov[e] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < V; ++j) cv[P & 1][j] = WG[1][j];
-    }
-    {  // S^T at row t-3 from l / o rows t-4, t-3, t-2 = slots K1, K2, K3
-      const float (&L0)[V] = L[K1];
-      const float (&L1)[V] = L[K2];
-      const float (&L2)[V] = L[K3];
-      const float (&O0)[V] = O[K1];
-      const float (&O1)[V] = O[K2];
-      const float (&O2)[V] = O[K3];
-      const float lp = lane_prev(L1[V - 1]), ln = lane_next(L1[0]);
-      const float op = lane_prev(O1[V - 1]), on = lane_next(O1[0]);
-      float nx[V], pv[V], gx[V], gp[V];
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        nx[j] = j < V - 1 ? L1[j + 1] : ln;
-        pv[j] = j > 0 ? L1[j - 1] : lp;
-        gx[j] = j < V - 1 ? O1[j + 1] : on;
-        gp[j] = j > 0 ? O1[j - 1] : op;
-      }
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        f2 v = sp(tL.u) * pr(L2, q);
-        v = fma2(sp(tL.l), pr(nx, q), v); v = fma2(sp(tL.c), pr(L1, q), v); v = fma2(sp(tL.r), pr(pv, q), v);
-        v = fma2(sp(tL.d), pr(L0, q), v);
-        tl[2 * q] = v.x; tl[2 * q + 1] = v.y;
-        f2 w = sp(tG.u) * pr(O2, q);
-        w = fma2(sp(tG.l), pr(gx, q), w); w = fma2(sp(tG.c), pr(O1, q), w); w = fma2(sp(tG.r), pr(gp, q), w);
-        w = fma2(sp(tG.d), pr(O0, q), w);
-        tg[2 * q] = w.x; tg[2 * q + 1] = w.y;
-      }
-    }
-#undef pr
-#undef sp
-#undef fma2
-  }
-
 };
 
 // The GTV proximal term C^T phi_gamma(C s) of the same input rows an OpPipe streams (the first-pair
@@ -1738,10 +1573,7 @@ constexpr int S2_PAIR = 2 * 6 * S2_W;      // floats per weight-ring pair
 constexpr int S2_HROW = 6 * S2_HW;         // floats per half-weight ring row
 constexpr int S2_LDS = S2_WP * S2_PAIR + S2_HR * S2_HROW +
                        S2_FMAX * (S2_XR * S2_W + S2_UR * S2_W + S2_DR * S2_HW + S2_TR * S2_HW);
-#ifndef GRR_STEP2_NT
-#define GRR_STEP2_NT 1
-#endif
-constexpr int S2_NT = GRR_STEP2_NT ? 2 : 0;   // cache policy of step2's read-once / write-once streams
+constexpr int S2_NT = 2;                   // cache policy (nt) of step2's read-once / write-once streams
 constexpr int S2_UNROLL = 4;               // iterations per loop body (the pipelines' slot period)
 #ifndef GRR_STEP2_AHEAD
 #define GRR_STEP2_AHEAD 2
@@ -1842,13 +1674,8 @@ void graph_step2_kernel(Step2Args a) {
     const float* pcg1 = a.cG1 + (int64_t)(b * a.G + g) * 2 * hHW;
     auto dma = [&](const float* src, float* dst) {
       const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)dst;
-#if GRR_STEP2_NT
       asm volatile("global_load_lds_dwordx4 %0, off nt" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
                    : "memory");
-#else
-      asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v))
-                   : "memory");
-#endif
     };
     auto dma_pair = [&](int p) {   // full-level weight rows of steps ts+2p, ts+2p+1 (rows t-2)
       float* slot = wring + (p % S2_WP) * S2_PAIR;

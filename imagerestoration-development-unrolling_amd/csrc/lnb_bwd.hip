@@ -948,16 +948,11 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
 }
 
 // V for the row kernels (0: not applicable -> per-pixel kernels)
-// W > 256: column strips of GRR_DW3_WIDE_V-wide lanes with a V-column halo (the fused gate + depthwise
-// reverse reaches two columns: V >= 2)
-#ifndef GRR_DW3_WIDE_V
-#define GRR_DW3_WIDE_V 4
-#endif
-static_assert(GRR_DW3_WIDE_V == 2 || GRR_DW3_WIDE_V == 4, "strip lanes: 2 or 4 columns");
+// W > 256: column strips of 4-wide lanes with a V-column halo (the fused gate + depthwise reverse reaches
+// two columns: V >= 2)
 int dw3_row_vec(int W) {
   if (W <= 64) return 1;
   if (W <= 128 && W % 2 == 0) return 2;
-  if (W > 256 && W % GRR_DW3_WIDE_V == 0) return GRR_DW3_WIDE_V;
   if (W % 4 == 0) return 4;
   return 0;
 }

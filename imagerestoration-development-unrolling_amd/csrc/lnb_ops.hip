@@ -95,9 +95,6 @@ __device__ __forceinline__ void dma16_opaque(const void* src, float* lds_wave_ba
   const uint32_t m0v = (uint32_t)(uintptr_t)(lds_f32_t)lds_wave_base;
   asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(__builtin_amdgcn_readfirstlane(m0v)) : "memory");
 }
-#ifndef GRR_HEAD_OPAQUE_DMA
-#define GRR_HEAD_OPAQUE_DMA 1
-#endif
 
 // ---------------------------------------------------------------------------
 // head: LN + W1 + dw3x3 + gate
@@ -197,8 +194,7 @@ __global__ __launch_bounds__(512, head_wgs(KS)) void lnb_head_kernel(LnbHeadArgs
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
       const int img = min(i * 8 + wave, NI - 1);   // surplus waves repeat the last image
-      if constexpr (GRR_HEAD_OPAQUE_DMA) dma16_opaque(src + img * 1024, slot + img * 256);
-      else dma16(src + img * 1024, slot + img * 256);
+      dma16_opaque(src + img * 1024, slot + img * 256);
     }
   };
   issue(0, 0);
@@ -335,10 +331,7 @@ __global__ __launch_bounds__(512, head_wgs(KS)) void lnb_head_kernel(LnbHeadArgs
   // Iteration c: GEMM1 of chunk c and the gate of chunk c - 1 (independent LDS planes).  The two
   // waves sharing a SIMD (w, w + 4) run them in opposite orders, so one wave's matrix work
   // overlaps the other's vector / LDS work (MI355X_MICROARCH.md, two waves per SIMD: stagger).
-#ifndef GRR_HEAD_STAGGER
-#define GRR_HEAD_STAGGER 1
-#endif
-  const bool gate_first = GRR_HEAD_STAGGER ? wave < 4 : true;
+  const bool gate_first = wave < 4;
   for (int c = 0; c <= nch; ++c) {
     // chunk c + AHEAD -> slot (c + AHEAD) % NSLOT, last read (gate of chunk c - 2) before the previous barrier
     issue(min(c + AHEAD, nch - 1), (c + AHEAD) % NSLOT);
@@ -1143,11 +1136,8 @@ __device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint3
   hi = __builtin_bit_cast(uint32_t, h);
   lo = __builtin_bit_cast(uint32_t, l);
 }
-// consumer mapping (A/B build macro): 0 = lane per pixel, pairs in turn with scalar taps, B operands by
-// v_permlane32_swap; 1 = lane per (column, pair half), two rows per lane, taps from the LDS ring
-#ifndef GRR_FUSED_MAP
-#define GRR_FUSED_MAP 1
-#endif
+// consumer mapping: lane per (column, pair half), two rows per lane, taps from the LDS ring (a lane per
+// pixel with scalar taps and B operands by v_permlane32_swap measured slower)
 
 // timing-only diagnostic builds (wrong results): 1 = consumers skip their work, 2 = producers skip theirs
 #ifndef GRR_FUSED_DIAG
@@ -1171,18 +1161,6 @@ __device__ unsigned long long g_fused_stamps[1024 * 8 * 8];
 #define FSTAMP(k) \
   do {            \
   } while (0)
-#endif
-#ifndef GRR_FUSED_PKFMA   // the gate's depthwise sums of the mask and value planes as packed FMAs (A/B: 0)
-#define GRR_FUSED_PKFMA 1
-#endif
-#ifndef GRR_FUSED_AHEAD   // pairs of taps + windows in flight ahead of the consumer's gate (1 or 2)
-#define GRR_FUSED_AHEAD 1
-#endif
-#ifndef GRR_FUSED_PRO_SERIAL   // 1: the producer's tile prologue loads one halo block at a time
-#define GRR_FUSED_PRO_SERIAL 0
-#endif
-#ifndef GRR_FUSED_PRIO   // consumer waves' static priority (A/B: 0 -> 1 took 3 % off at 256^2 and 128^2)
-#define GRR_FUSED_PRIO 1
 #endif
 
 // tile t of the launch -> (b, ty, tx): consecutive tiles of a workgroup walk along rows of one image
@@ -1329,10 +1307,6 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
               xh[k][s] = __builtin_bit_cast(f16x8, u32x4{hw[0], hw[1], hw[2], hw[3]});
               xl[k][s] = __builtin_bit_cast(f16x8, u32x4{lw[0], lw[1], lw[2], lw[3]});
             }
-#if GRR_FUSED_PRO_SERIAL
-            // one block's raw x (8 KS floats per lane) at a time
-            __builtin_amdgcn_sched_barrier(0);
-#endif
           }
           wave_corr = __builtin_amdgcn_readfirstlane((int)__any(any_corr)) != 0;
         }
@@ -1400,9 +1374,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
   }
 
   // ---------------- consumer: depthwise + gate + GEMM2 of output rows 2 cw, 2 cw + 1 of the tile
-#if GRR_FUSED_PRIO
-  __builtin_amdgcn_s_setprio(GRR_FUSED_PRIO);      // the VALU-bound role first at the SIMD's issue arbiter
-#endif
+  __builtin_amdgcn_s_setprio(1);   // the VALU-bound role first at the SIMD's issue arbiter (3 % at 256^2, 128^2)
   const int cw = wave - 4;
   const int col = lane & 31;
   f32x16 acc2[2][MT];
@@ -1426,115 +1398,6 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
       const FusedTile T = fused_tile(a, ctile);
       const int gxo = T.x0 + col;
       const float* w2s = slot + 2 * KS * 256 + lane * 4;
-#if GRR_FUSED_MAP == 0
-      // lane = pixel (output row 2 cw + lane / 32, column lane % 32); the 16 pairs in turn, each pair's taps
-      // the same for the whole wave: scalar loads, SGPR operands of the FMAs.  The next pair's taps (SMEM)
-      // and window (LDS) are issued right after the current pair's first product -- SMEM and LDS share
-      // lgkmcnt and SMEM completes out of order, so the wait the compiler puts before that product (lgkmcnt
-      // 0) must not cover them -- and land while the rest of the pair computes.
-      const float* hwin = smem + (st & 1) * LF_HBUF + 2 * ((2 * cw + kh) * LF_HWD + col);
-      const_f32_t tp = (const_f32_t)(a.pack + (int64_t)ch * NI * 1024) + (2 * KS + 2 * MT) * 256;
-      float g[16];
-      float tA[18];
-      f32x2 wA[9];
-#pragma unroll
-      for (int u = 0; u < 18; ++u) tA[u] = tp[u];
-#pragma unroll
-      for (int u = 0; u < 9; ++u) wA[u] = *reinterpret_cast<const f32x2*>(hwin + 2 * ((u / 3) * LF_HWD + u % 3));
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        float m = tA[0] * wA[0][0], v = tA[1] * wA[0][1];
-        __builtin_amdgcn_sched_barrier(0);
-        float tB[18];
-        f32x2 wB[9];
-        if (j < 15) {
-#pragma unroll
-          for (int u = 0; u < 18; ++u) tB[u] = tp[(j + 1) * 18 + u];
-          const float* hp = hwin + (j + 1) * LF_PP;
-#pragma unroll
-          for (int u = 0; u < 9; ++u) wB[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 1; t < 9; ++t) {
-          m = __builtin_fmaf(tA[2 * t], wA[t][0], m);
-          v = __builtin_fmaf(tA[2 * t + 1], wA[t][1], v);
-        }
-        // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
-        g[j] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
-        if (j < 15) {
-#pragma unroll
-          for (int u = 0; u < 18; ++u) tA[u] = tB[u];
-#pragma unroll
-          for (int u = 0; u < 9; ++u) wA[u] = wB[u];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (a.g) {   // kept gate (training): the unscaled fp32 values, [B, hid, H, W]; pairs >= hid past num_records
-        const int yy = T.y0 + 2 * cw + kh;
-        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
-            a.g + (int64_t)T.b * hid * HW, 0, (int)((int64_t)hid * HW * 4), 0x00020000);
-        const uint32_t vo = yy < H && gxo < W ? (uint32_t)(yy * W + gxo) * 4u : 0x80000000u;
-        int hw4 = HW * 4;
-        asm volatile("" : "+s"(hw4));
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g[j]), grs, vo, (16 * ch + j) * hw4, 0);
-      }
-      // the pixel's running exponent: largest |g| so far into [2^13, 2^14)
-      float gm = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) gm = fmaxf(gm, fabsf(g[j]));
-      const int Eo = E[0];                           // this lane's pixel (E[1] unused in this mapping)
-      int eg = Eo;
-      if (gm != 0.f) {
-        int e;
-        frexpf(gm, &e);
-        eg = min(Eo, clampi(14 - e, -100, 100));
-      }
-      if (__builtin_amdgcn_readfirstlane((int)__any(eg != Eo && Eo != 1000)) != 0) {
-        // accumulator column = lane % 32 holds the pixel of row 2 cw (block 0) / 2 cw + 1 (block 1) in both
-        // lane halves: the factor of the lane half that computed that pixel
-        const float f = Eo != 1000 ? ldexpf(1.0f, eg - Eo) : 1.0f;
-        const auto fs = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          acc2[0][t] *= __uint_as_float(fs[0]);
-          acc2[1][t] *= __uint_as_float(fs[1]);
-        }
-      }
-      E[0] = eg;
-      const int Eu = eg == 1000 ? 0 : eg;
-      // two-term fp16 split of 2^Eu g, packed (pair 2q, 2q + 1); v_permlane32_swap turns the lane-per-pixel
-      // layout into the B operands of the two rows: lanes 0-31 keep pairs 0-7 of row 2 cw and take pairs
-      // 8-15 of it from lanes 0-31 of the other register; lanes 32-63 likewise for row 2 cw + 1
-      uint32_t hx[8], lx[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) split2_f16(ldexpf(g[2 * q], Eu), ldexpf(g[2 * q + 1], Eu), hx[q], lx[q]);
-      uint32_t bh[2][4], bl[2][4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const auto sh = __builtin_amdgcn_permlane32_swap(hx[q], hx[q + 4], false, false);
-        const auto sl = __builtin_amdgcn_permlane32_swap(lx[q], lx[q + 4], false, false);
-        bh[0][q] = sh[0];
-        bh[1][q] = sh[1];
-        bl[0][q] = sl[0];
-        bl[1][q] = sl[1];
-      }
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(w2s + (2 * t + 0) * 256);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(w2s + (2 * t + 1) * 256);
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          const f16x8 gh = __builtin_bit_cast(f16x8, u32x4{bh[rb][0], bh[rb][1], bh[rb][2], bh[rb][3]});
-          const f16x8 gl = __builtin_bit_cast(f16x8, u32x4{bl[rb][0], bl[rb][1], bl[rb][2], bl[rb][3]});
-          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc2[rb][t], 0, 0, 0);
-          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc2[rb][t], 0, 0, 0);
-          acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc2[rb][t], 0, 0, 0);
-        }
-      }
-#else
       // the window of both rows' pixels: halo rows 2 cw .. 2 cw + 3, columns col .. col + 2, pair 8 kh + jj
       const float* hwin = smem + (st & 1) * LF_HBUF + 8 * kh * LF_PP + 2 * (2 * cw * LF_HWD + col);
       const float* tap0 = slot + (2 * KS + 2 * MT) * 256 + 8 * kh * 18;
@@ -1554,61 +1417,26 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
         for (int u = 0; u < 12; ++u) w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
       };
       load(0, tA, wA);
-#if GRR_FUSED_AHEAD == 2
-      f32x2 tN[9];
-      f32x2 wN[12];
-      load(1, tN, wN);
-#endif
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         f32x2 tB[9];
         f32x2 wB[12];
-#if GRR_FUSED_AHEAD == 2
-        // two pairs in flight: pair jj + 2 issued, pair jj + 1 (tN, wN) landing, pair jj computed
-        if (jj < 6) load(jj + 2, tB, wB);
-#else
         if (jj < 7) load(jj + 1, tB, wB);
-#endif
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
-#if GRR_FUSED_PKFMA
           f32x2 mv = tA[0] * wA[3 * rb];
 #pragma unroll
           for (int t = 1; t < 9; ++t) mv = __builtin_elementwise_fma(tA[t], wA[3 * (rb + t / 3) + t % 3], mv);
           const float m = mv[0], v = mv[1];
-#else
-          float m = tA[0][0] * wA[3 * rb][0], v = tA[0][1] * wA[3 * rb][1];
-#pragma unroll
-          for (int t = 1; t < 9; ++t) {
-            const f32x2 hv = wA[3 * (rb + t / 3) + t % 3];
-            m = __builtin_fmaf(tA[t][0], hv[0], m);
-            v = __builtin_fmaf(tA[t][1], hv[1], v);
-          }
-#endif
           // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
           g[rb][jj] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
         }
-#if GRR_FUSED_AHEAD == 2
-        if (jj < 7) {
-#pragma unroll
-          for (int u = 0; u < 9; ++u) tA[u] = tN[u];
-#pragma unroll
-          for (int u = 0; u < 12; ++u) wA[u] = wN[u];
-        }
-        if (jj < 6) {
-#pragma unroll
-          for (int u = 0; u < 9; ++u) tN[u] = tB[u];
-#pragma unroll
-          for (int u = 0; u < 12; ++u) wN[u] = wB[u];
-        }
-#else
         if (jj < 7) {
 #pragma unroll
           for (int u = 0; u < 9; ++u) tA[u] = tB[u];
 #pragma unroll
           for (int u = 0; u < 12; ++u) wA[u] = wB[u];
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);
       }
       FSTAMP(1);
@@ -1665,7 +1493,6 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
           acc2[rb][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc2[rb][t], 0, 0, 0);
         }
       }
-#endif
       FSTAMP(2);
       if (ch == nch - 1) {
         // epilogue (REF:962-964): out[m, p] = skip0 x[m, p] + skip1 2^-E_p r2[m] acc; accumulator block rb
@@ -1679,12 +1506,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
             const_cast<float*>(a.x + (int64_t)T.b * C * HW), 0, (int)((int64_t)C * HW * 4), 0x00020000);
         const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)T.b * C * HW, 0,
                                                                               (int)((int64_t)C * HW * 4), 0x00020000);
-#if GRR_FUSED_MAP == 0
-        const auto es = __builtin_amdgcn_permlane32_swap((uint32_t)E[0], (uint32_t)E[0], false, false);
-        const int Eb[2] = {(int)es[0], (int)es[1]};
-#else
         const int Eb[2] = {E[0], E[1]};
-#endif
         // the W2 row scales and 2^-E into the accumulators first, then every skip operand of both rows in one
         // round of loads (the gate's registers are dead here: acc2 + 2 MT x 16 fit), then the stores
 #pragma unroll
