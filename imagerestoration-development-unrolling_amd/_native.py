@@ -139,6 +139,7 @@ SIGNATURES = {
     "grr_win_bwd_glr": [P, P, P, P, I, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
     "grr_win_bwd_gtv": [P, P, P, P, I, I, P, P, Fl, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_win_bwd_gather": [P, P, P, I, P, P, I, I, I, I, I, P],
+    "grr_win_bwd_gather_fused": [P, P, P, P, I, I, I, P, P, P, P, I, I, I, I, I, P],
     "grr_win_bwd_edge_weights": [P, L, P, P, P, P, I, P, L, P, I, I, I, I, I, P],
     "grr_win_bwd_mix": [P, P, P, P, P, I, I, I, I, I, P],
 }

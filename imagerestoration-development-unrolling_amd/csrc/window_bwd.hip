@@ -193,7 +193,7 @@ __global__ __launch_bounds__(NTB) void win_glr_bwd_kernel(const float* __restric
         const float we = wq[e * HW], sn = sp[nq];
         wx += we * sn;
         gwa[e] -= gl * sn;
-        E[((bg * Fs + ch) * K + e) * HW + q] = gl * we;
+        if (E) E[((bg * Fs + ch) * K + e) * HW + q] = gl * we;
       }
       const float lv = sp[q] - wx;
       l_out[plane + q] = lv;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
         const bool in = ry >= 0 && ry < H && cx >= 0 && cx < W;
         const int nq = clampi(ry, 0, H - 1) * W + clampi(cx, 0, W - 1);
         const float we = wp[e * HW], sn = sp[nq];
-        const float z = we * sv - we * sn;
+        const float z = __builtin_fmaf(sv, we, -__fmul_rn(we, sn));   // (win_gather_fused_kernel rounds z alike)
         float ph = z, gz;
         const float bd = bv - (in ? bp[ry * W + cx] : 0.f);
         const float gph = we * (sc * bd);
@@ -259,8 +259,8 @@ __global__ __launch_bounds__(NTB) void win_gtv_bwd_kernel(const float* __restric
         }
         gwa[e] += ph * (sc * bd) + gz * (sv - sn);
         gs += gz * we;
-        E[((bg * Fs + ch) * K + e) * HW + p] = gz * we;
-        PW[((bg * Fs + ch) * K + e) * HW + p] = we * ph;
+        if (E) E[((bg * Fs + ch) * K + e) * HW + p] = gz * we;
+        if (PW) PW[((bg * Fs + ch) * K + e) * HW + p] = we * ph;
         dot += ph * we * bd;
       }
       gsd[plane + p] = gs;
@@ -299,6 +299,104 @@ __global__ __launch_bounds__(NTB) void win_gather_bwd_kernel(const float* __rest
       for (int e = 0; e < K; ++e) {
         const int py = r - d.dy[e], px = c - d.dx[e];
         if (py >= 0 && py < H && px >= 0 && px < W) o -= Pp[e * HW + py * W + px];
+      }
+      o_out[i] = o;
+    }
+  }
+}
+
+// ---- pass 2 without the E / PW planes: each E_e(p) / PW_e(p) the gather needs is recomputed at its
+// target from s, b and w (pass 1's expressions, in its order).  Every source p of q under edge e has
+// clamp(p + d_e) = q, so s(n_e(p)) = s(q), and p + d_e is inside exactly when it equals q (then
+// b(p + d_e) = b(q)).  Pass 1 then writes neither plane set (2 Fs K floats per pixel written and read back).
+//   GLR: E_e(p) = (sc b(p)) w_e(p)
+//   GTV: E_e(p) = gz_e(p) w_e(p), PW_e(p) = w_e(p) ph_e(p)  (win_gtv_bwd_kernel)
+template <bool GTV>
+__global__ __launch_bounds__(NTB) void win_gather_fused_kernel(const float* __restrict__ s, const float* __restrict__ b,
+                                                               const float* __restrict__ w, WinDeltaB d, int K,
+                                                               int prox, const float* __restrict__ log_gamma,
+                                                               const float* __restrict__ scale,
+                                                               float* __restrict__ gs, float* __restrict__ o_out, int G,
+                                                               int Fs, int H, int W, int64_t n) {
+  const int64_t HW = (int64_t)H * W;
+  for (int64_t i = blockIdx.x * (int64_t)NTB + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTB) {
+    const int64_t plane = i / HW;                   // (b, g, channel)
+    const int64_t bg = plane / Fs;
+    const int g = (int)(bg % G);
+    const float sc = scale ? scale[g] : 1.f;
+    const float gm = GTV && prox ? expf(log_gamma[g]) : 0.f;
+    const int q = (int)(i - plane * HW);
+    const int r = q / W, c = q - r * W;
+    const float* sp = s + plane * HW;
+    const float* bp = b + plane * HW;
+    const float* wb = w + bg * K * HW;
+    const float sq = sp[q], bq = bp[q];
+    // E_e(p) (and PW_e(p) for GTV) of source p of q under edge e
+    auto edge = [&](int e, int p, bool in, float& pw) {
+      const float we = wb[e * HW + p];
+      if constexpr (!GTV) {
+        pw = 0.f;
+        const float gl = sc * bp[p];
+        return gl * we;
+      } else {
+        const float sv = sp[p], sn = sq;
+        // pass 1's rounding of z exactly (it compiles to fma(s(p), w, -round(w s(n)))): at tiny gamma the soft
+        // threshold's branch follows the last bit of z, so both passes must see the same z
+        const float z = __builtin_fmaf(sv, we, -__fmul_rn(we, sn));
+        float ph = z, gz;
+        const float bd = bp[p] - (in ? bq : 0.f);
+        const float gph = we * (sc * bd);
+        if (prox) {
+          const float lo = z < -gm ? z + gm : 0.f, hi = z > gm ? z - gm : 0.f;
+          const float eps = lo + hi;
+          ph = eps - (z - eps);
+          const bool beyond = z < -gm || z > gm;
+          gz = beyond ? gph : -gph;
+        } else {
+          gz = gph;
+        }
+        pw = we * ph;
+        return gz * we;
+      }
+    };
+    float acc = 0.f;
+    for (int e = 0; e < K; ++e) {
+      int sy[3], sx[3];
+      const int dy = d.dy[e], dx = d.dx[e];
+      const int ny = clamp_sources(r, dy, H, sy), nx = clamp_sources(c, dx, W, sx);
+      for (int a = 0; a < ny; ++a)
+        for (int bb = 0; bb < nx; ++bb) {
+          const int py = sy[a], px = sx[bb];
+          const bool in = py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
+          float pw;
+          acc += edge(e, py * W + px, in, pw);
+        }
+    }
+    gs[i] -= acc;
+    if (GTV && o_out) {
+      // o(q) = sum_e PW_e(q) - sum_e [q - d_e inside] PW_e(q - d_e)  (pass 2's order: the first sum, then
+      // the subtraction term by term)
+      float o = 0.f;
+      for (int e = 0; e < K; ++e) {
+        const int ny2 = clampi(r + d.dy[e], 0, H - 1), nx2 = clampi(c + d.dx[e], 0, W - 1);
+        const float we = wb[e * HW + q], sv = sq, sn = sp[ny2 * W + nx2];
+        const float z = __builtin_fmaf(sv, we, -__fmul_rn(we, sn));
+        float ph = z;
+        if (prox) {
+          const float lo = z < -gm ? z + gm : 0.f, hi = z > gm ? z - gm : 0.f;
+          const float eps = lo + hi;
+          ph = eps - (z - eps);
+        }
+        o += we * ph;
+      }
+      for (int e = 0; e < K; ++e) {
+        const int py = r - d.dy[e], px = c - d.dx[e];
+        if (py >= 0 && py < H && px >= 0 && px < W) {
+          float pw;
+          const bool in = true;   // p + d_e = q
+          edge(e, py * W + px, in, pw);
+          o -= pw;
+        }
       }
       o_out[i] = o;
     }
@@ -488,7 +586,7 @@ grr_status grr_win_bwd_glr(const float* s, const float* b, const float* w, const
                            int B, int G, int Fs, int H, int W, void* stream) {
   clear_error();
   WinDeltaB d{};
-  GRR_REQUIRE(s && b && w && l_out && E && gsd && gw && B > 0 && G > 0 && Fs > 0 && H > 1 && W > 1 &&
+  GRR_REQUIRE(s && b && w && l_out && gsd && gw && B > 0 && G > 0 && Fs > 0 && H > 1 && W > 1 &&
                   fill_delta(delta, K, d),
               GRR_ERR_INVALID_ARG, "grr_win_bwd_glr: bad args");
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_glr: B*G > 65535");
@@ -509,7 +607,7 @@ grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const
                            void* stream) {
   clear_error();
   WinDeltaB d{};
-  GRR_REQUIRE(s && b && w && PW && E && gsd && gw && B > 0 && G > 0 && Fs > 0 && H > 1 && W > 1 &&
+  GRR_REQUIRE(s && b && w && gsd && gw && B > 0 && G > 0 && Fs > 0 && H > 1 && W > 1 &&
                   (!prox || log_gamma) && fill_delta(delta, K, d),
               GRR_ERR_INVALID_ARG, "grr_win_bwd_gtv: bad args");
   GRR_REQUIRE((int64_t)B * G <= 65535, GRR_ERR_UNSUPPORTED, "grr_win_bwd_gtv: B*G > 65535");
@@ -534,6 +632,24 @@ grr_status grr_win_bwd_gather(const float* E, const float* PW, const int32_t* de
   hipLaunchKernelGGL(win_gather_bwd_kernel, dim3(grid_1d(n)), dim3(NTB), 0, (hipStream_t)stream, E, PW, d, K, gs, o_out,
                      H, W, n);
   return launch_status("grr_win_bwd_gather");
+}
+
+grr_status grr_win_bwd_gather_fused(const float* s, const float* b, const float* w, const int32_t* delta, int K,
+                                    int gtv, int prox, const float* log_gamma, const float* scale, float* gs,
+                                    float* o_out, int B, int G, int Fs, int H, int W, void* stream) {
+  clear_error();
+  WinDeltaB d{};
+  GRR_REQUIRE(s && b && w && gs && (gtv || !o_out) && (!gtv || !prox || log_gamma) && B > 0 && G > 0 && Fs > 0 &&
+                  H > 1 && W > 1 && fill_delta(delta, K, d),
+              GRR_ERR_INVALID_ARG, "grr_win_bwd_gather_fused: bad args");
+  const int64_t n = (int64_t)B * G * Fs * H * W;
+  if (gtv)
+    hipLaunchKernelGGL(win_gather_fused_kernel<true>, dim3(grid_1d(n)), dim3(NTB), 0, (hipStream_t)stream, s, b, w, d,
+                       K, prox, log_gamma, scale, gs, o_out, G, Fs, H, W, n);
+  else
+    hipLaunchKernelGGL(win_gather_fused_kernel<false>, dim3(grid_1d(n)), dim3(NTB), 0, (hipStream_t)stream, s, b, w,
+                       d, K, 0, nullptr, scale, gs, nullptr, G, Fs, H, W, n);
+  return launch_status("grr_win_bwd_gather_fused");
 }
 
 grr_status grr_win_bwd_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM, const float* w,

@@ -1375,6 +1375,12 @@ def _edge_shape_ok(w: Tensor, dims, k: int) -> None:
         raise ValueError(f"window reverse: edge weights of shape {tuple(w.shape)}, expected {(b, g, k, h, ww)}")
 
 
+# The window term reverses' second pass recomputes the E / PW planes where they are gathered
+# (grr_win_bwd_gather_fused) instead of pass 1 writing 2 Fs K floats per pixel for it to read back;
+# False: the planes (the A/B and parity reference)
+WIN_FUSED_GATHER = True
+
+
 def win_bwd_glr(s: Tensor, bt: Tensor, w: Tensor, edge_delta, sc: Tensor, coef: float, gw: Tensor,
                 gdot: Optional[Tensor], n_graphs: int) -> Tuple[Tensor, Tensor]:
     """GLR term reverse, both passes: returns (l = (I - W) s, gs = (I - W)^T (sc * bt))."""
@@ -1387,6 +1393,14 @@ def win_bwd_glr(s: Tensor, bt: Tensor, w: Tensor, edge_delta, sc: Tensor, coef: 
     _check_win_scalars(n_graphs, sc=sc, gdot=gdot)
     b, g, fs, h, ww = dims
     l_out, gs = torch.empty_like(s), torch.empty_like(s)
+    if WIN_FUSED_GATHER:   # no E planes: the gather recomputes them (grr_win_bwd_gather_fused)
+        _launch("win_bwd_glr", 4 * (4 * s.numel() + 3 * w.numel()), "grr_win_bwd_glr",
+                s.data_ptr(), bt.data_ptr(), w.data_ptr(), delta, k, sc.data_ptr(), float(coef), l_out.data_ptr(),
+                None, gs.data_ptr(), gw.data_ptr(), _ptr(gdot), *dims, _stream(dev))
+        _launch("win_bwd_gather", 4 * (4 * s.numel() + w.numel()), "grr_win_bwd_gather_fused", s.data_ptr(),
+                bt.data_ptr(), w.data_ptr(), delta, k, 0, 0, None, sc.data_ptr(), gs.data_ptr(), None, *dims,
+                _stream(dev))
+        return l_out, gs
     E = torch.empty((b, g, fs, k, h, ww), dtype=torch.float32, device=dev)
     _launch("win_bwd_glr", 4 * (3 * s.numel() + 3 * w.numel() + (k + 2) * s.numel()), "grr_win_bwd_glr",
             s.data_ptr(), bt.data_ptr(), w.data_ptr(), delta, k, sc.data_ptr(), float(coef), l_out.data_ptr(),
@@ -1409,6 +1423,15 @@ def win_bwd_gtv(s: Tensor, bt: Tensor, w: Tensor, edge_delta, prox: bool, log_ga
     _check_win_scalars(n_graphs, sc=sc, gdot=gdot, log_gamma=log_gamma, ggamma=ggamma)
     b, g, fs, h, ww = dims
     o, gs = torch.empty_like(s), torch.empty_like(s)
+    if WIN_FUSED_GATHER:   # no E / PW planes: the gather recomputes them (grr_win_bwd_gather_fused)
+        _launch("win_bwd_gtv", 4 * (3 * s.numel() + 3 * w.numel()), "grr_win_bwd_gtv",
+                s.data_ptr(), bt.data_ptr(), w.data_ptr(), delta, k, int(prox), _ptr(log_gamma), sc.data_ptr(),
+                float(coef), None, None, gs.data_ptr(), gw.data_ptr(), _ptr(gdot), _ptr(ggamma), *dims,
+                _stream(dev))
+        _launch("win_bwd_gather", 4 * (5 * s.numel() + w.numel()), "grr_win_bwd_gather_fused", s.data_ptr(),
+                bt.data_ptr(), w.data_ptr(), delta, k, 1, int(prox), _ptr(log_gamma), sc.data_ptr(), gs.data_ptr(),
+                o.data_ptr(), *dims, _stream(dev))
+        return o, gs
     E = torch.empty((b, g, fs, k, h, ww), dtype=torch.float32, device=dev)
     PW = torch.empty_like(E)
     _launch("win_bwd_gtv", 4 * (3 * s.numel() + 3 * w.numel() + (2 * k + 1) * s.numel()), "grr_win_bwd_gtv",

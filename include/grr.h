@@ -588,12 +588,14 @@ grr_status grr_win_bwd_stencil(const float* x, const float* taps, int mode, cons
 grr_status grr_win_bwd_tapgrad(const float* u, const float* z, int mode, const float* scale, float* gtaps, int B,
                                int G, int Fs, int H, int W, void* stream);
 /* GLR term reverse, pass 1 (s = S x, b = S^T* g): l_out = (I - W) s, gsd = scale b,
- * E [B,G,Fs,K,H,W] = scale b w_e (gathered by grr_win_bwd_gather), gw += -scale b s(n_e),
+ * E [B,G,Fs,K,H,W] = scale b w_e (gathered by grr_win_bwd_gather; may be NULL with
+ * grr_win_bwd_gather_fused), gw += -scale b s(n_e),
  * gdot[g] += coef <b, l>. */
 grr_status grr_win_bwd_glr(const float* s, const float* b, const float* w, const int32_t* delta, int K,
                            const float* scale, float coef, float* l_out, float* E, float* gsd, float* gw, float* gdot,
                            int B, int G, int Fs, int H, int W, void* stream);
-/* GTV term reverse, pass 1 (C^T C, or with prox C^T phi(C .)): gsd, E as above, PW [B,G,Fs,K,H,W]
+/* GTV term reverse, pass 1 (C^T C, or with prox C^T phi(C .)): gsd, E as above, PW [B,G,Fs,K,H,W] (E, PW
+ * may be NULL with grr_win_bwd_gather_fused)
  * = w_e phi(z_e) (the gather rebuilds o = C^T phi from it), gw, gdot[g] += coef <b, o>,
  * ggamma[g] += dL/dgamma (prox). */
 grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const int32_t* delta, int K, int prox,
@@ -602,6 +604,14 @@ grr_status grr_win_bwd_gtv(const float* s, const float* b, const float* w, const
 /* Pass 2: gs -= sum_e sum_{p: clamp(p + delta_e) = q} E_e(p) (in place); with PW also o_out. */
 grr_status grr_win_bwd_gather(const float* E, const float* PW, const int32_t* delta, int K, float* gs, float* o_out,
                               int B, int G, int Fs, int H, int W, void* stream);
+/* Pass 2 without the E / PW planes (pass 1 then runs with E = PW = NULL): each E_e(p) / PW_e(p) is
+ * recomputed at the pixel that gathers it from s, b, w (gtv = 0: the GLR term's E; gtv = 1: the GTV
+ * term's E and, with o_out, o = C^T phi(C s); prox, log_gamma, scale as in pass 1).  Same result as
+ * grr_win_bwd_glr / _gtv writing the planes + grr_win_bwd_gather, without 2 Fs K floats per pixel
+ * written and read back. */
+grr_status grr_win_bwd_gather_fused(const float* s, const float* b, const float* w, const int32_t* delta, int K,
+                                    int gtv, int prox, const float* log_gamma, const float* scale, float* gs,
+                                    float* o_out, int B, int G, int Fs, int H, int W, void* stream);
 /* Edge-weight reverse of grr_win_edge_weights: gw is overwritten (softmax reverse in place);
  * the [G*F] slab of gfeat and gmultiM [G,F] accumulate (the GTV and GLR graphs share features). */
 grr_status grr_win_bwd_edge_weights(const float* feat, int64_t feat_bstride, const float* multiM, const float* w,

@@ -104,6 +104,7 @@ int main() {
   EXPECT_ERR(grr_win_bwd_glr(n, n, n, delta, 2, n, 1.f, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_gtv(n, n, n, delta, 2, 1, n, n, 1.f, n, n, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_gather(n, n, delta, 2, n, n, 1, 1, 1, 8, 8, s));
+  EXPECT_ERR(grr_win_bwd_gather_fused(n, n, n, delta, 2, 1, 0, n, n, n, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_edge_weights(n, 0, n, n, n, delta, 2, n, 0, n, 1, 1, 1, 8, 8, s));
   EXPECT_ERR(grr_win_bwd_mix(n, n, n, n, n, 1, 1, 1, 8, 8, s));
   // non-positive sizes with non-NULL (never dereferenced) pointers

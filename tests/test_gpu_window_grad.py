@@ -10,6 +10,8 @@ Tolerances: max-abs error / max-abs reference <= 2e-4 where every soft-threshold
 stable (gamma far from |C x| or tiny); relative L2 <= 2e-3 where a few of the millions of
 |C x| ~ gamma comparisons may legitimately flip between fp32 and fp64.
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -324,3 +326,47 @@ def test_window_module_calls_differentiable(wg, version, name):
         for m_, to in ((glr, tlo), (gtv, tgo)):
             for q, v in to.items():
                 assert rel_inf(getattr(m_, q).grad, v.grad) <= 2e-4, q
+
+
+@pytest.mark.parametrize("hw", [(21, 37), (2, 3), (3, 2), (64, 64)])
+@pytest.mark.parametrize("name", sorted(WINDOWS))
+@pytest.mark.parametrize("term", ["glr", "gtv", "prox", "prox_tiny"])
+def test_window_fused_gather_equals_planes(wg, name, term, hw):
+    """grr_win_bwd_gather_fused (the E / PW terms recomputed where they are gathered; pass 1 writes no
+    planes) against pass 1 writing E / PW + grr_win_bwd_gather: l or o, gs, and the weight / scalar
+    gradients pass 1 accumulates, to fp32 rounding (the same expressions in two kernels)."""
+    K = wg[0].K
+    delta = O.window_edges(WINDOWS[name])
+    dl = tuple((int(a), int(c)) for a, c in delta)
+    b, g, fs = 2, 3, 3
+    h, w = hw
+    k = len(delta)
+    gen = torch.Generator().manual_seed(501 + k + len(term) + h)
+    s = _dev(torch.randn((b, g, fs, h, w), generator=gen, dtype=torch.float64))
+    bt = _dev(torch.randn((b, g, fs, h, w), generator=gen, dtype=torch.float64))
+    wt = _dev(_weights(b, g, k, h, w, gen))
+    sc = _dev(0.2 + torch.rand(g, generator=gen, dtype=torch.float64))
+    lg = _dev(torch.log(0.05 + 0.5 * torch.rand(g, generator=gen, dtype=torch.float64)))
+    if term == "prox_tiny":                     # gamma 1e-9: the soft threshold's branch at z = 0 matters
+        lg = torch.full_like(lg, math.log(1e-9))
+        term = "prox"
+    res = {}
+    saved = K.WIN_FUSED_GATHER
+    try:
+        for fused in (False, True):
+            K.WIN_FUSED_GATHER = fused
+            gw = torch.full_like(wt, 0.25)
+            gdot = torch.zeros(g, device=DEV)
+            ggam = torch.zeros(g, device=DEV)
+            if term == "glr":
+                out = K.win_bwd_glr(s, bt, wt, dl, sc, -1.0, gw, gdot, g)
+            else:
+                out = K.win_bwd_gtv(s, bt, wt, dl, term == "prox", lg if term == "prox" else None, sc, 1.0, gw, gdot,
+                                    ggam if term == "prox" else None, g)
+            torch.cuda.synchronize()
+            res[fused] = [t.cpu() for t in (*out, gw, gdot, ggam)]
+    finally:
+        K.WIN_FUSED_GATHER = saved
+    for nm, a, r in zip(("l/o", "gs", "gw", "gdot", "ggamma"), res[True], res[False]):
+        assert torch.isfinite(a).all(), nm
+        assert rel_inf(a, r) <= 1e-6, (nm, rel_inf(a, r))
