@@ -120,3 +120,21 @@ def test_scratch_allocator_is_registered_and_empty_without_gpu():
     assert lib.grr_scratch_bytes() == 0
     assert lib.grr_release_scratch() == 0
     assert lib.grr_set_scratch_allocator(None, 0x1000, None) == 1   # one function without the other
+
+
+def test_wgrad_tile_plan_without_gpu():
+    """grr_wgrad's host plan (no launch): the per-shape tile makes the v1.0 first level's 192 x 48 gradient
+    one output tile per pixel chunk instead of two, so it plans twice the chunks (and workspace) of the
+    128 x 96 tile at the same wave budget; a 512 x 96 output keeps the 128 x 96 tile either way."""
+    lib = _native.load()
+    try:
+        lib.grr_wgrad_set_tiles(0)
+        base_small = lib.grr_wgrad_workspace_bytes(32, 192, 48, 512 * 512)
+        base_wide = lib.grr_wgrad_workspace_bytes(16, 512, 96, 256 * 256)
+        lib.grr_wgrad_set_tiles(1)
+        tiled_small = lib.grr_wgrad_workspace_bytes(32, 192, 48, 512 * 512)
+        tiled_wide = lib.grr_wgrad_workspace_bytes(16, 512, 96, 256 * 256)
+    finally:
+        lib.grr_wgrad_set_tiles(1)
+    assert tiled_small > base_small > 0
+    assert tiled_wide == base_wide > 0
