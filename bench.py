@@ -236,6 +236,7 @@ def main():
         benchlib.dry_run_report(world, rank, local)
         return
     dev = benchlib.init(world, local)
+    ranks = benchlib.check_ranks(world, dev)     # every rank in the group, over the data backend
 
     import irdu_amd
     from irdu_amd import kernels as K
@@ -322,7 +323,8 @@ def main():
                       "parallelism": f"batch-sharded x{world}, no collective in the data path"},
            "roofline": roofline}
     if world > 1:
-        res["ranks"] = {"backend": benchlib.backend(), "visible_gpus": torch.cuda.device_count(),
+        res.update(ranks)
+        res["ranks"] = {"backend": ranks["backend"], "visible_gpus": torch.cuda.device_count(),
                         "ms_per_step_per_rank": [round(d / args.steps * 1e3, 3) for d in rank_dts]}
     if "lnb_head" in kern:   # the feature CNN: head (LN + W1 + depthwise + gate) and mix (W2 + skip) apart
         hd, mx = kern["lnb_head"], kern["lnb_mix"]

@@ -39,6 +39,7 @@ def main():
         benchlib.dry_run_report(world, rank, local)
         return
     dev = benchlib.init(world, local)
+    ranks = benchlib.check_ranks(world, dev)     # every rank in the group, over the data backend
     import irdu_amd
     from irdu_amd import tiling
     from bench import TRAINED, build_model, synthetic_patches
@@ -79,7 +80,7 @@ def main():
                                      else "reference init",
                                      "parallelism": f"(image, window) units sharded x{world}, "
                                                     + ("cores gathered to rank 0" if args.gather else "no collective")},
-                          "tiled_vs_whole": parity}), flush=True)
+                          "tiled_vs_whole": parity, **(ranks if world > 1 else {})}), flush=True)
     benchlib.finish(world)
 
 

@@ -174,6 +174,7 @@ def main():
         benchlib.dry_run_report(world, rank, local)
         return
     dev = benchlib.init(world, local)
+    ranks = benchlib.check_ranks(world, dev)     # every rank in the group, over the data backend
 
     import irdu_amd
     from irdu_amd import kernels as K
@@ -231,6 +232,8 @@ def main():
                "loss": loss, "hip_kernel_ms_per_step": round(hip_ms, 2),
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                "kernel_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in kern.items()}}
+        if world > 1:
+            res.update(ranks)
         res["roofline"] = reverse_roofline(kern, args.model, args.batch, args.size)
         res["roofline_secondary"] = secondary_rooflines(kern)
         if not args.no_cpu_baseline and world == 1:

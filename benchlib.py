@@ -116,10 +116,20 @@ def _check_devices(world: int, dry_run: bool) -> None:
 
 
 def dry_run_report(world: int, rank: int, local: int) -> None:
-    """--dry-run: each rank reports itself (no HIP, no process group)."""
-    print(json.dumps({"dry_run": True, "rank": rank, "local_rank": local, "world": world,
-                      "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
-          flush=True)
+    """--dry-run: each rank reports itself without HIP.  For world > 1 the ranks still join a gloo
+    process group on the CPU and count each other with the same ones all-reduce ``ranks_seen`` runs
+    on the real backend, so the launcher test checks the fields an N > 1 bench line carries."""
+    rep = {"dry_run": True, "rank": rank, "local_rank": local, "world": world,
+           "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}
+    if world > 1:
+        import torch
+        torch.distributed.init_process_group("gloo")
+        try:
+            rep["ranks_seen"] = ranks_seen(world, torch.device("cpu"))
+            rep["backend"] = torch.distributed.get_backend()
+        finally:
+            torch.distributed.destroy_process_group()
+    print(json.dumps(rep), flush=True)
 
 
 def init(world: int, local: int):
@@ -134,6 +144,29 @@ def init(world: int, local: int):
         else:
             torch.distributed.init_process_group(backend())
     return dev
+
+
+def ranks_seen(world: int, dev) -> int:
+    """Ranks that took part in one all-reduce of ones over the process group (== world when every
+    rank joined the group the timing is reduced over).  On the nccl backend the tensor lives on the
+    rank's GPU, so the count has crossed RCCL.  1 without a process group."""
+    import torch
+    if world == 1:
+        return 1
+    on = dev if torch.distributed.get_backend() == "nccl" else "cpu"
+    t = torch.ones(1, dtype=torch.int64, device=on)
+    torch.distributed.all_reduce(t)
+    return int(t.item())
+
+
+def check_ranks(world: int, dev) -> dict:
+    """The fields every N > 1 bench line carries: ranks_seen (== N, else the run fails) and the
+    process group's backend."""
+    import torch
+    seen = ranks_seen(world, dev)
+    if seen != world:
+        raise LaunchError(f"ranks_seen={seen} != world {world}: a rank is missing from the process group")
+    return {"ranks_seen": seen, "backend": torch.distributed.get_backend() if world > 1 else "none"}
 
 
 def barrier(world: int, dev) -> None:

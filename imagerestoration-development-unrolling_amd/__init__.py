@@ -7,6 +7,12 @@ module ``deep_multiscale_GGLR_GGTV_v1x0`` so callers can swap the import:
 
     import irdu_amd as model_structure
     model = model_structure.AbtractMultiScaleGraphFilter(...).cuda()
+
+Importing changes no process-wide setting.  A drop-in training script with its own loop calls
+``irdu_amd.miopen_training_defaults()`` before its first convolution (MIOpen's find-db otherwise costs
+seconds of host time per step on the v1.0 model's stock convolutions after a box's first run,
+DESIGN.md §4.r4); the first training-mode forward of AbtractMultiScaleGraphFilter warns once when
+MIOPEN_DEBUG_DISABLE_FIND_DB is unset.
 """
 from ._native import GrrError, NativeUnavailable, load as load_native  # noqa: F401
 from .graph_filter import (  # noqa: F401

@@ -80,6 +80,7 @@ SIGNATURES = {
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_lnb_forward_keep": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_lnb_fused": [I, I],
+    "grr_lnb_fused_workspace_bytes": [I, I],
     "grr_lnb_set_fused": [I],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
     "grr_lnb_forward_rep": [P, I, I, P, P, P, P, P, P, P, P, I, I, I, I, P],
@@ -145,7 +146,8 @@ SIGNATURES = {
 }
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64, "grr_wgrad_workspace_bytes": c_int64,
-             "grr_ffn_workspace_bytes": c_int64, "grr_scratch_bytes": c_int64}
+             "grr_ffn_workspace_bytes": c_int64, "grr_scratch_bytes": c_int64,
+             "grr_lnb_fused_workspace_bytes": c_int64}
 
 _lib = None
 

@@ -958,6 +958,11 @@ int64_t grr_lnb_workspace_bytes(int B, int C, int hid, int H, int W) {
   return f * (int64_t)sizeof(float);
 }
 
+int64_t grr_lnb_fused_workspace_bytes(int C, int hid) {
+  if (!grr::lnb_fused(C, hid)) return 0;
+  return grr::fused_pack_floats(C, hid) * (int64_t)sizeof(float);
+}
+
 grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                            const float* skip, float* out, void* workspace, int B, int C, int hid, int H, int W,
                            void* stream) {

@@ -1843,20 +1843,29 @@ size_t term_ring_lds(int mode, int V, int F, bool padj, int d, int* ndma_out) {
   const size_t row_b = (size_t)64 * V * sizeof(float);
   return (size_t)2 * F * wpl * row_b + (size_t)d * rows * row_b + (padj ? (size_t)3 * F * row_b : 0);
 }
+int term_ring_setting() {
+  static const int forced = [] {
+    const char* e = getenv("GRR_TERM_RING_D");
+    return e ? atoi(e) : 0;
+  }();
+  return forced >= 4 ? forced : 4;
+}
+// the ring's shape-only conditions at depth d: the counted vmcnt of d - 3 steps of DMAs, the LDS
+bool term_ring_fits(int mode, int V, int F, bool padj, int d, size_t* lds_out) {
+  int ndma = 0;
+  const size_t lds = term_ring_lds(mode, V, F, padj, d, &ndma);
+  if (lds_out) *lds_out = lds;
+  return ndma * (d - 3) <= 63 && lds <= kTermLdsMax;
+}
 int term_ring_depth(int mode, int V, int F, int W, const float* x, const float* g, const float* w, const float* gw,
                     const float* gx, size_t* lds_out) {
   if (!term_ring_shape_ok(mode, F, W)) return 0;
   const void* ptrs[] = {x, g, w, gw, gx};
   for (const void* p : ptrs)
     if ((uintptr_t)p % 16u != 0) return 0;
-  static const int forced = [] {
-    const char* e = getenv("GRR_TERM_RING_D");
-    return e ? atoi(e) : 0;
-  }();
-  const int d = forced >= 4 ? forced : 4;
-  int ndma = 0;
-  const size_t lds = term_ring_lds(mode, V, F, gx != nullptr, d, &ndma);
-  if (ndma * (d - 3) > 63 || lds > kTermLdsMax) return 0;
+  const int d = term_ring_setting();
+  size_t lds = 0;
+  if (!term_ring_fits(mode, V, F, gx != nullptr, d, &lds)) return 0;
   if (lds_out) *lds_out = lds;
   return d;
 }
@@ -2004,6 +2013,10 @@ __global__ __launch_bounds__(64) void red_finish_kernel(RedFinishArgs a) {
 // grr_set_scratch_allocator (the Python package registers PyTorch's caching allocator, so the scratch
 // is visible to and reclaimable through torch), else from hipMalloc / hipFree.  An outgrown buffer is
 // retired, not freed (a queued kernel may still read it), until grr_release_scratch.
+// A lease taken while its stream is being captured into a HIP graph is the graph's own: a
+// hipMallocAsync / hipFreeAsync pair on the capturing stream (memory nodes of the graph), never one of
+// the stream's buffers, so replays do not share memory with eager calls on that stream or with another
+// graph, and grr_release_scratch cannot free memory a graph still points at.
 namespace {
 struct ScratchBuf {
   int dev;
@@ -2023,6 +2036,11 @@ struct ScratchState {
 };
 ScratchState g_scratch;
 std::mutex g_scratch_mu;
+struct CaptureLease {
+  void* p;
+  hipStream_t s;
+};
+std::vector<CaptureLease> g_capture_leases;   // leased inside a stream capture, freed by scratch_return
 
 grr_status scratch_raw_alloc(int dev, hipStream_t s, size_t bytes, ScratchBuf* out, const char* what) {
   void* p = nullptr;
@@ -2058,6 +2076,19 @@ grr_status scratch_lease(hipStream_t s, size_t bytes, void** out, const char* wh
     return GRR_ERR_HIP;
   }
   std::lock_guard<std::mutex> lk(g_scratch_mu);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  GRR_REQUIRE(hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusInvalidated,
+              GRR_ERR_HIP, "%s: the stream's capture state is invalid", what);
+  if (cap == hipStreamCaptureStatusActive) {
+    void* p = nullptr;
+    if (hipMallocAsync(&p, std::max<size_t>(bytes, 256), s) != hipSuccess || !p) {
+      set_error("%s: reduction scratch of %zu bytes inside a stream capture: hipMallocAsync failed", what, bytes);
+      return GRR_ERR_HIP;
+    }
+    g_capture_leases.push_back(CaptureLease{p, s});
+    *out = p;
+    return GRR_OK;
+  }
   ScratchBuf* small = nullptr;
   for (auto& b : g_scratch.bufs) {
     if (b.dev != dev || b.s != s || b.leased) continue;
@@ -2068,11 +2099,6 @@ grr_status scratch_lease(hipStream_t s, size_t bytes, void** out, const char* wh
     }
     small = &b;
   }
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(s, &cap);
-  GRR_REQUIRE(cap == hipStreamCaptureStatusNone, GRR_ERR_UNSUPPORTED,
-              "%s: the reduction scratch would grow inside a stream capture (run the call once before capturing)",
-              what);
   size_t want = std::max<size_t>(bytes, (size_t)1 << 20);
   if (small) want = std::max(want, 2 * small->bytes);
   ScratchBuf nb{};
@@ -2090,6 +2116,12 @@ grr_status scratch_lease(hipStream_t s, size_t bytes, void** out, const char* wh
 }
 void scratch_return(void* p) {
   std::lock_guard<std::mutex> lk(g_scratch_mu);
+  for (size_t i = 0; i < g_capture_leases.size(); ++i)
+    if (g_capture_leases[i].p == p) {   // after the finish kernel on the capturing stream: a free node
+      (void)hipFreeAsync(p, g_capture_leases[i].s);
+      g_capture_leases.erase(g_capture_leases.begin() + (std::ptrdiff_t)i);
+      return;
+    }
   for (auto& b : g_scratch.bufs)
     if (b.p == p) b.leased = false;
 }
@@ -2239,9 +2271,18 @@ grr_status grr_bwd_term_fused(int mode, const float* x, const float* g, const fl
 int grr_bwd_term_acc_supported(int mode, int F, int H, int W) {
   // the LDS-ring kernel takes the pass wherever it applies (any width: gx rows come in its slots), the
   // register kernel at one strip of <= 2-column lanes
+  // (16-byte aligned planes are the caller's part: kernels.term_acc_ok checks them).  Everything else
+  // grr_bwd_term_fused_acc and launch_term_row ask for is checked here, so a shape this accepts with
+  // aligned planes never fails with GRR_ERR_UNSUPPORTED: term_row_ok's channel bound, then either the
+  // ring (enabled, within the width cap, its DMA count and LDS at the depth it will run) or the
+  // register kernel's one strip of <= 2-column lanes
   if (mode < 0 || mode > 2 || F <= 0 || H <= 0 || W <= 0 || !g_term_rows) return 0;
-  if (term_ring_shape_ok(mode, F, W))
-    return W <= g_term_acc_max_w && term_ring_lds(mode, term_strip_vec(W, mode), F, true, 4, nullptr) <= kTermLdsMax ? 1 : 0;
+  const int V = term_strip_vec(W, mode);
+  if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return 0;
+  if (term_ring_shape_ok(mode, F, W)) {
+    if (W > g_term_acc_max_w) return 0;   // the policy cap (wider levels fold the pass into the CG glue)
+    if (g_term_rows == 2 && term_ring_fits(mode, V, F, true, term_ring_setting(), nullptr)) return 1;
+  }
   return term_acc_shape_ok(mode, F, W) ? 1 : 0;
 }
 

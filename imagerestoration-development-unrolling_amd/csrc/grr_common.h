@@ -42,6 +42,8 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t n) {
 
 // LocalNonLinearBlock on the split-bf16 MFMA kernels (lnb_ops.hip), C <= 128
 int64_t lnb_mfma_workspace_floats(int B, int C, int hid, int H, int W);
+int64_t fused_pack_floats(int C, int hid);   // the fused block's chunk images + W2 row scales
+bool lnb_fused(int C, int hid);
 // C <= 96 runs the whole block as one fused pass (lnb_fused16_kernel); keep_g: it also stores the gated
 // activation g [B, hid, H, W] at the workspace's start (where the two-kernel path leaves it anyway)
 bool lnb_fused(int C, int hid);

@@ -1745,7 +1745,7 @@ static int64_t mix_pack_floats(int C, int hid) {
 // the fused block (lnb_fused16_kernel): C <= 96 (GEMM1's x of three halo blocks, 6 k-steps, in registers)
 int g_lnb_fused_on = 1;   // grr_lnb_set_fused (A/B measurement knob)
 bool lnb_fused(int C, int hid) { return g_lnb_fused_on && C >= 2 && C <= 96 && hid >= 1; }
-static int64_t fused_pack_floats(int C, int hid) {
+int64_t fused_pack_floats(int C, int hid) {
   const int KS = (C + 15) / 16, MT = (C + 31) / 32, nch = (hid + 15) / 16;
   return align64((int64_t)nch * fused_images(KS, MT) * 256) + align64(C);
 }
@@ -1806,7 +1806,9 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
               "grr_lnb_forward: max(hid, C)*H*W too large for one image's 32-bit offsets");
   const int KS = (C + 15) / 16, MT = (C + 31) / 32, nch = (hid + 15) / 16;
   const int64_t P = (int64_t)H * W;
-  float* base = ws + align64((int64_t)B * hid * P);
+  // the chunk images at the workspace's start (grr_lnb_fused_workspace_bytes), after the g region when the
+  // pass also keeps g
+  float* base = keep_g ? ws + align64((int64_t)B * hid * P) : ws;
   char* pack = reinterpret_cast<char*>(base);
   float* r2 = base + align64((int64_t)nch * fused_images(KS, MT) * 256);
   if (g_lnb_phases & 1) {

@@ -22,6 +22,7 @@ training can never silently skip gradients.
 from __future__ import annotations
 
 import os
+import warnings
 from typing import List, Optional, Sequence
 
 import torch
@@ -611,6 +612,25 @@ class Upsampling(HipModule):
         return self.local_linear(x)
 
 
+_MIOPEN_CHECKED = False
+
+
+def _warn_miopen_find_db() -> None:
+    """Once per process: a drop-in training script that never called irdu_amd.miopen_training_defaults()
+    (and does not set MIOPEN_DEBUG_DISABLE_FIND_DB itself) trains the v1.0 model's stock convolutions
+    with MIOpen's user find-db, 2.7-4.0 s per C4 step instead of 1.03 s after a box's first run
+    (DESIGN.md §4.r4).  Importing the package changes no process-wide setting, so this only warns."""
+    global _MIOPEN_CHECKED
+    if _MIOPEN_CHECKED or torch.compiler.is_compiling():
+        return
+    _MIOPEN_CHECKED = True
+    if "MIOPEN_DEBUG_DISABLE_FIND_DB" not in os.environ:
+        warnings.warn("irdu_amd: training AbtractMultiScaleGraphFilter without MIOPEN_DEBUG_DISABLE_FIND_DB set; "
+                      "call irdu_amd.miopen_training_defaults() before the first convolution (MIOpen's find-db "
+                      "costs seconds of host time per step on later runs, DESIGN.md §4.r4)", RuntimeWarning,
+                      stacklevel=3)
+
+
 class AbtractMultiScaleGraphFilter(HipModule):
     def __init__(self, n_channels_in=3, n_channels_out=3, dims=(48, 64, 96, 128), hidden_dims=(128, 192, 256, 384),
                  nsubnets=(1, 1, 1, 1), ngraphs=(4, 4, 8, 8), num_blocks=(4, 6, 6, 8), num_blocks_out=4,
@@ -671,4 +691,6 @@ class AbtractMultiScaleGraphFilter(HipModule):
         return self.decode(self.encode(img))
 
     def forward(self, img):
+        if self.training and torch.is_grad_enabled():
+            _warn_miopen_find_db()
         return self.decode(self.filtering(self.encode(img)))

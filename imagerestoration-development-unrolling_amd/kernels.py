@@ -668,12 +668,15 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     rows = _lnb_band_rows(c, hid, h, w)
     if rows < h:
         return _lnb_banded(lambda xb: lnb_forward(xb, ln_w, w1, wdw, w2, skip), [x], h, rows)
-    nbytes = _native.load().grr_lnb_workspace_bytes(b, c, hid, h, w)
+    lib = _native.load()
+    fused = bool(lib.grr_lnb_fused(c, hid))
+    # the fused pass needs only its chunk images (g stays on chip); the two-kernel path g + images
+    nbytes = lib.grr_lnb_fused_workspace_bytes(c, hid) if fused else lib.grr_lnb_workspace_bytes(b, c, hid, h, w)
     ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
     out = torch.empty_like(x)
     args = (x.data_ptr(), ln_w.data_ptr(), w1.data_ptr(), wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(),
             out.data_ptr(), ws.data_ptr(), b, c, hid, h, w, _stream(dev))
-    if _native.load().grr_lnb_fused(c, hid):
+    if fused:
         # one fused pass (lnb_fused16_kernel): x in (its halo and the skip read once), out written; the
         # gated activation stays on chip
         _launch("lnb_fused", 4 * b * h * w * 2 * c, "grr_lnb_forward", *args, flops=lnb_flops(b * h * w, c, c, hid))
@@ -985,10 +988,14 @@ def bwd_cg_glue(gx: Tensor, u: Tensor, gu_next: Optional[Tensor], u_prev: Option
     return gu, gx_out
 
 
-def glue_pool_ok(x: Tensor) -> bool:
-    """Where grr_bwd_cg_glue_pool takes the glue (W % 4 == 0, even H; planes 16-byte aligned by torch)."""
+def glue_pool_ok(x: Tensor, *planes: Optional[Tensor], gx_half: Optional[Tensor] = None) -> bool:
+    """Where grr_bwd_cg_glue_pool takes the glue: W % 4 == 0, even H, and every operand plane the pass
+    reads on its float4 path (x = gx, then u, gu_next, u_prev, gbb, the padj v planes: None = absent)
+    16-byte aligned, gx_half 8-byte aligned (the outputs are fresh torch allocations)."""
     b, c, h, w = x.shape
-    return w % 4 == 0 and h % 2 == 0 and x.data_ptr() % 16 == 0
+    if w % 4 or h % 2 or any(t is not None and t.data_ptr() % 16 for t in (x, *planes)):
+        return False
+    return gx_half is None or gx_half.data_ptr() % 8 == 0
 
 
 def bwd_unpool2_acc(xd: Tensor, out: Tensor) -> None:

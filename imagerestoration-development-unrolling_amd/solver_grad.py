@@ -376,7 +376,8 @@ def _mixture_bwd(consts, inputs, outs, saved, gouts, needs):
         for k in range(n_st - 1, 0, -1):
             # ga_k, gu_k, gb_k, gb_B += gu_k, gx_{k+1} - gu_k in one pass (grr_bwd_cg_glue), with the
             # previous stage's full-level x-gradient pass and half-level x-gradient added on the way in
-            pool = GLUE_POOL and K.glue_pool_ok(gx)
+            pool = GLUE_POOL and K.glue_pool_ok(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, gbb,
+                                                *((pj[0], pj[3]) if pj is not None else ()), gx_half=gxh)
             gu, gx, *gud = cg_glue(gx, us[k], gu_next, us[k - 1] if k >= 2 else None, alpha, beta, gbb,
                                    galpha, gbeta, k, g, owned=k < n_st - 1, gx_half=gxh, padj=pj, want_pool=pool)
             gxh, pj = a_bwd(xs[k], gu, -1.0, gx, defer=UNPOOL_GLUE and k > 1, xd=xds[k],

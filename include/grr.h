@@ -59,9 +59,11 @@ grr_status grr_lnb_set_phases(int mask);
  * stream (stream order makes the reuse safe).  The buffers come from the allocator registered here
  * (alloc(bytes, device, stream, ctx) returns a device pointer or NULL; free(ptr, device, stream, ctx)),
  * or from hipMalloc when none is registered (both NULL).  The Python package registers PyTorch's
- * caching allocator, so the scratch is PyTorch memory.  A call that would grow the scratch while its
- * stream is being captured fails with GRR_ERR_UNSUPPORTED (run it once before capturing).
- * grr_release_scratch frees every buffer (the caller synchronises the streams first);
+ * caching allocator, so the scratch is PyTorch memory.  A call made while its stream is being captured
+ * into a HIP graph takes its own scratch as a hipMallocAsync / hipFreeAsync pair on that stream (memory
+ * nodes the graph owns): a replayed graph shares no scratch with eager calls on the stream or with
+ * another graph, and grr_release_scratch never frees memory a graph uses.
+ * grr_release_scratch frees every stream buffer (the caller synchronises the streams first);
  * grr_scratch_bytes reports the bytes held. */
 typedef void* (*grr_scratch_alloc_fn)(uint64_t bytes, int device, void* stream, void* ctx);
 typedef void (*grr_scratch_free_fn)(void* ptr, int device, void* stream, void* ctx);
@@ -341,6 +343,10 @@ grr_status grr_lnb_forward_keep(const float* x, const float* ln_w, const float* 
  * gate and W2 in one kernel, the gated activation kept on chip).  Phase mask 2 of grr_lnb_set_phases then
  * launches the whole block and mask 4 nothing. */
 int grr_lnb_fused(int C, int hid);
+/* Workspace bytes grr_lnb_forward needs when grr_lnb_fused(C, hid) holds (the fused pass's chunk images
+ * only: no gated tensor, no batch or image size), else 0.  grr_lnb_forward_keep still needs
+ * grr_lnb_workspace_bytes (g at the workspace's start). */
+int64_t grr_lnb_fused_workspace_bytes(int C, int hid);
 /* Measurement knob (process-wide): 0 runs C <= 96 blocks on the two-kernel head + mix path instead of
  * the fused pass (same results to fp32 rounding); 1 (default) fused. */
 grr_status grr_lnb_set_fused(int enable);

@@ -28,6 +28,9 @@ def test_library_loads_and_exports_every_header_symbol():
     assert set(syms) == set(_native.SIGNATURES), "ctypes signature table out of sync with include/grr.h"
     assert lib.grr_version() >= 1
     assert lib.grr_lnb_workspace_bytes(2, 96, 256, 64, 64) > 0
+    # the fused C <= 96 block needs its chunk images only, far below the gated tensor's 2*256*64*64 floats
+    assert 0 < lib.grr_lnb_fused_workspace_bytes(96, 256) < 4 * 2 * 256 * 64 * 64
+    assert lib.grr_lnb_fused_workspace_bytes(128, 256) == 0
 
 
 def test_invalid_args_report_status_without_gpu():

@@ -31,6 +31,8 @@ def test_plain_start_spawns_n_ranks(script):
     assert sorted(d["rank"] for d in lines) == [0, 1]
     assert all(d["world"] == 2 and d["local_rank"] == d["rank"] for d in lines)
     assert len({d["master"] for d in lines}) == 1 and lines[0]["master"].startswith("127.0.0.1:")
+    # the fields an N > 1 bench line carries: every rank counted by the ones all-reduce, and the backend
+    assert all(d["ranks_seen"] == 2 and d["backend"] == "gloo" for d in lines)
 
 
 def test_single_gpu_dry_run_does_not_spawn():
@@ -47,11 +49,29 @@ def test_torchrun_world_must_match_gpus():
 
 
 def test_torchrun_rank_reports_itself():
-    r = _run("bench.py", ["--gpus", "2", "--dry-run"],
-             _env(WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29555"))
-    assert r.returncode == 0, r.stderr
-    d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert (d["rank"], d["world"], d["master"]) == (1, 2, "127.0.0.1:29555")
+    # both ranks under torchrun's environment (started by hand here): each reports itself and the group
+    port = _free_port()
+    env = dict(WORLD_SIZE="2", LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                              cwd=ROOT, env=_env(RANK=str(r), LOCAL_RANK=str(r), **env), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in (0, 1)]
+    outs = [p.communicate(timeout=180) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1] for o in outs]
+    d = json.loads(outs[1][0].strip().splitlines()[-1])
+    assert (d["rank"], d["world"], d["master"]) == (1, 2, f"127.0.0.1:{port}")
+    assert d["ranks_seen"] == 2 and d["backend"] == "gloo"
+
+
+def test_check_ranks_single_process():
+    import benchlib
+    assert benchlib.check_ranks(1, None) == {"ranks_seen": 1, "backend": "none"}
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def test_more_ranks_than_gpus_is_refused():

@@ -97,9 +97,9 @@ def test_two_rank_hip_training_step_equals_full_batch():
                 p.kill()
     for r in (0, 1):
         assert not isinstance(res[r][0], str), res[r][0]
+        assert res[r][1] >= 1, ("no bucket was reduced inside backward", r)
     for k in res[0][2]:
         assert np.array_equal(res[0][2][k], res[1][2][k]), k     # the replicas stay identical
-        assert res[r][1] >= 1, "no bucket was reduced inside backward"
     for p in procs:
         assert p.exitcode == 0
 
