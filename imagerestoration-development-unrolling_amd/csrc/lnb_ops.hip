@@ -1062,6 +1062,7 @@ struct LnbFusedArgs {
   float* g;              // [B, hid, H, W] or nullptr
   float var_den;
   int C, hid, H, W, tiles_x, tiles_y, nch, ntiles;
+  int stagger_groups, stagger_unit;   // start-phase stagger (grr_lnb_set_stagger)
 };
 
 // W1 images as lnb_w1_pack16_kernel's (rows 2^s_row-scaled, fp16 hi / lo); W2 images: row tile t, term q,
@@ -1210,6 +1211,14 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
     dsl = dsl == LF_NSLOT - 1 ? 0 : dsl + 1;
   };
   if (nsteps == 0) return;   // workgroup-uniform: no barrier is left waiting
+  // Start-phase stagger: every workgroup walks identical tiles, so left alone they run in lockstep and all
+  // of them load their next tile's x halo (producers) and store the finished tile (consumers: skip x in,
+  // out) in the same step -- one chip-wide HBM burst per tile while the other 15 steps move almost no
+  // bytes.  Workgroup group k = (wg / 8) % groups (consecutive workgroups go to the 8 XCDs in turn) sleeps
+  // k units of 2048 cycles first, which spreads the bursts over the tile's steps.
+  if (a.stagger_groups > 1) {
+    for (int r = ((wg >> 3) % a.stagger_groups) * a.stagger_unit; r > 0; --r) __builtin_amdgcn_s_sleep(32);
+  }
 #if GRR_FUSED_STAMP
   unsigned long long st_acc[8] = {}, st_prev = __builtin_amdgcn_s_memtime();
   auto stamp_out = [&]() {
@@ -1744,6 +1753,7 @@ static int64_t mix_pack_floats(int C, int hid) {
 
 // the fused block (lnb_fused16_kernel): C <= 96 (GEMM1's x of three halo blocks, 6 k-steps, in registers)
 int g_lnb_fused_on = 1;   // grr_lnb_set_fused (A/B measurement knob)
+int g_lnb_stagger_groups = 0, g_lnb_stagger_unit = 3;   // grr_lnb_set_stagger
 bool lnb_fused(int C, int hid) { return g_lnb_fused_on && C >= 2 && C <= 96 && hid >= 1; }
 int64_t fused_pack_floats(int C, int hid) {
   const int KS = (C + 15) / 16, MT = (C + 31) / 32, nch = (hid + 15) / 16;
@@ -1823,6 +1833,8 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
   f.x = x; f.pack = pack; f.r2 = r2; f.skip = skip; f.out = out;
   f.g = keep_g ? ws : nullptr;
   f.var_den = (float)(C - 1);
+  f.stagger_groups = g_lnb_stagger_groups;
+  f.stagger_unit = g_lnb_stagger_unit;
   f.C = C; f.hid = hid; f.H = H; f.W = W; f.nch = nch;
   f.tiles_x = (W + LF_TW - 1) / LF_TW;
   f.tiles_y = (H + LF_TH - 1) / LF_TH;
@@ -1970,6 +1982,15 @@ extern "C" grr_status grr_lnb_set_fused(int enable) {
   grr::clear_error();
   GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_lnb_set_fused: 0 or 1");
   grr::g_lnb_fused_on = enable;
+  return GRR_OK;
+}
+
+extern "C" grr_status grr_lnb_set_stagger(int groups, int unit) {
+  grr::clear_error();
+  GRR_REQUIRE(groups >= 0 && groups <= 64 && unit >= 0 && unit <= 64, GRR_ERR_INVALID_ARG,
+              "grr_lnb_set_stagger: groups in [0, 64], unit in [0, 64]");
+  grr::g_lnb_stagger_groups = groups;
+  grr::g_lnb_stagger_unit = unit;
   return GRR_OK;
 }
 

@@ -350,6 +350,11 @@ int64_t grr_lnb_fused_workspace_bytes(int C, int hid);
 /* Measurement knob (process-wide): 0 runs C <= 96 blocks on the two-kernel head + mix path instead of
  * the fused pass (same results to fp32 rounding); 1 (default) fused. */
 grr_status grr_lnb_set_fused(int enable);
+/* Measurement knob (process-wide) of the fused C <= 96 pass: its persistent workgroups start in
+ * `groups` phases, group k (of workgroups wg, (wg / 8) % groups) after k * unit * 2048 cycles, so the
+ * per-tile HBM bursts of the workgroups do not coincide.  groups <= 1: no stagger.  Results are
+ * independent of it. */
+grr_status grr_lnb_set_stagger(int groups, int unit);
 /* grr_lnb_forward for an input x [B, R*Cs, H, W] that is R stacked copies of src [B, Cs, H, W]
  * (the first feature block of MultiScaleGraphFilter, whose input replicates RGB over the graphs,
  * REF13:918-921): LN statistics and W1 are evaluated on src with W1 diag(ln_w) folded over the

@@ -40,11 +40,13 @@ def main():
                          "2 the term pass + the stencil x-gradient pass")
     ap.add_argument("--term-rows", type=int, default=2, choices=[0, 1, 2],
                     help="term: 0 per-pixel, 1 register-prefetch row kernel, 2 LDS-ring row kernel (default)")
+    ap.add_argument("--stagger", default="0,3", help="LNB fused: groups,unit (grr_lnb_set_stagger)")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
     K.set_term_rows(args.term_rows)
     from irdu_amd._native import call
     call("grr_lnb_set_fused", args.lnb_fused)
+    call("grr_lnb_set_stagger", *[int(v) for v in args.stagger.split(",")])
     dev = torch.device("cuda", 0)
     b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.width or args.size
     c = g * f
