@@ -1150,6 +1150,9 @@ __device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint3
 #ifndef GRR_FUSED_STAMP
 #define GRR_FUSED_STAMP 0
 #endif
+#ifndef GRR_FUSED_PRO_ALL
+#define GRR_FUSED_PRO_ALL 0
+#endif
 #if GRR_FUSED_STAMP
 __device__ unsigned long long g_fused_stamps[1024 * 8 * 8];
 #define FSTAMP(k)                                              \
@@ -1257,8 +1260,34 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
           const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
               const_cast<float*>(a.x + (int64_t)T.b * C * HW), 0, (int)((int64_t)C * HW * 4), 0x00020000);
           bool any_corr = false;
+#if GRR_FUSED_PRO_ALL
+          // every block's loads first (one round trip of HBM latency instead of one per block)
+          float xva[NBW][KS][8];
 #pragma unroll
           for (int k = 0; k < NBW; ++k) {
+            const int q = min((wave + 4 * k) * 32 + (lane & 31), LF_NQ - 1);
+            const int hy = q / LF_HWD, hx = q - hy * LF_HWD;
+            const int gy = clampi(T.y0 - 1 + hy, 0, H - 1), gx = clampi(T.x0 - 1 + hx, 0, W - 1);
+            const int vo = (8 * kh * HW + gy * W + gx) * 4;
+            int hw4 = HW * 4;
+            asm volatile("" : "+s"(hw4));
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+#if GRR_FUSED_DIAG & 4   // timing only: a quarter of the loads (the others repeat them)
+                if (j & 3) { xva[k][s][j] = xva[k][s][j & 4]; continue; }
+#endif
+                xva[k][s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
+              }
+          }
+          __builtin_amdgcn_sched_barrier(0);   // (else the scheduler sinks blocks 1, 2's loads past block 0's math)
+#endif
+#pragma unroll
+          for (int k = 0; k < NBW; ++k) {
+#if GRR_FUSED_PRO_ALL
+            float (&xv)[KS][8] = xva[k];
+#else
             const int q = min((wave + 4 * k) * 32 + (lane & 31), LF_NQ - 1);
             const int hy = q / LF_HWD, hx = q - hy * LF_HWD;
             const int gy = clampi(T.y0 - 1 + hy, 0, H - 1), gx = clampi(T.x0 - 1 + hx, 0, W - 1);
@@ -1273,6 +1302,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
 #pragma unroll
               for (int j = 0; j < 8; ++j)
                 xv[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
+#endif
             float sum = 0.f;
 #pragma unroll
             for (int s = 0; s < KS; ++s)
