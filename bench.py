@@ -224,8 +224,6 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary workload (v1.0 AbtractMultiScaleGraphFilter, SURVEY.md §8d 'D')")
     ap.add_argument("--breakdown", action="store_true", help="print the per-kernel table to stderr")
-    ap.add_argument("--lnb-stagger", default=None,
-                    help="A/B knob: 'groups,unit' of the fused LNB's start-phase stagger (grr_lnb_set_stagger)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check: every rank prints its rank / world and exits (no HIP)")
     args = ap.parse_args()
@@ -243,9 +241,6 @@ def main():
     import irdu_amd
     from irdu_amd import kernels as K
     irdu_amd.load_native()
-    if args.lnb_stagger:
-        from irdu_amd._native import call
-        call("grr_lnb_set_stagger", *[int(v) for v in args.lnb_stagger.split(",")])
     model = build_model(dev, trained=os.path.exists(TRAINED))
     b = args.batch
     # each rank its own shard of patches (seed by rank): resident in HBM before timing

@@ -79,8 +79,9 @@ SIGNATURES = {
     "grr_lnb_workspace_bytes": [I, I, I, I, I],
     "grr_lnb_forward": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_lnb_forward_keep": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grr_lnb_forward_c8": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
+    "grr_c8_convert": [P, P, I, I, I, I, I, P],
     "grr_lnb_fused": [I, I],
-    "grr_lnb_set_stagger": [I, I],
     "grr_lnb_fused_workspace_bytes": [I, I],
     "grr_lnb_set_fused": [I],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],

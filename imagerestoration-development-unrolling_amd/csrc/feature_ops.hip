@@ -979,6 +979,69 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
   return grr::block_x3_forward<false>(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W, s);
 }
 
+grr_status grr_lnb_forward_c8(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
+                              const float* skip, float* out, void* workspace, int B, int C, int hid, int H, int W,
+                              int layout, void* stream) {
+  grr::clear_error();
+  GRR_REQUIRE(x && ln_w && w1 && wdw && w2 && skip && out && workspace && B > 0 && C > 1 && hid > 0 && H > 0 &&
+                  W > 0 && layout >= 0 && layout <= 3,
+              GRR_ERR_INVALID_ARG, "grr_lnb_forward_c8: bad args");
+  GRR_REQUIRE(out != x, GRR_ERR_INVALID_ARG, "grr_lnb_forward_c8: out aliases x");
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0,
+              GRR_ERR_INVALID_ARG, "grr_lnb_forward_c8: workspace 256-B, x and out 16-B aligned");
+  GRR_REQUIRE(grr_lnb_fused(C, hid) && (int64_t)((C + 7) / 8) * 8 * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_forward_c8: needs the fused pass (grr_lnb_fused) and 2^31 bytes per blocked image");
+  return grr::lnb_forward_mfma(x, ln_w, w1, wdw, w2, skip, out, (float*)workspace, B, C, hid, H, W,
+                               (hipStream_t)stream, false, layout);
+}
+
+// [B, C, H, W] <-> [B, ceil(C / 8), H, W, 8] (pad channels written as 0 / skipped)
+namespace grr {
+__global__ __launch_bounds__(256) void c8_pack_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int64_t HW,
+                                                     int64_t n) {   // n = B * NB * HW (one thread: 8 channels)
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i % HW, r = i / HW;
+    const int nb = (C + 7) / 8, blk = (int)(r % nb);
+    const int64_t b = r / nb;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * blk + j;
+      v[j] = c < C ? x[(b * C + c) * HW + p] : 0.f;
+    }
+    float4* o = reinterpret_cast<float4*>(y + i * 8);
+    o[0] = make_float4(v[0], v[1], v[2], v[3]);
+    o[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+__global__ __launch_bounds__(256) void c8_unpack_kernel(const float* __restrict__ y, float* __restrict__ x, int C,
+                                                       int64_t HW, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i % HW, r = i / HW;
+    const int nb = (C + 7) / 8, blk = (int)(r % nb);
+    const int64_t b = r / nb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * blk + j;
+      if (c < C) x[(b * C + c) * HW + p] = y[i * 8 + j];
+    }
+  }
+}
+}  // namespace grr
+
+grr_status grr_c8_convert(const float* src, float* dst, int B, int C, int H, int W, int to_blocked, void* stream) {
+  grr::clear_error();
+  GRR_REQUIRE(src && dst && src != dst && B > 0 && C > 0 && H > 0 && W > 0 && ((uintptr_t)(to_blocked ? dst : src) & 15) == 0,
+              GRR_ERR_INVALID_ARG, "grr_c8_convert: bad args (the blocked tensor 16-B aligned)");
+  const int64_t HW = (int64_t)H * W, n = (int64_t)B * ((C + 7) / 8) * HW;
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65536);
+  if (to_blocked)
+    hipLaunchKernelGGL(grr::c8_pack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, dst, C, HW, n);
+  else
+    hipLaunchKernelGGL(grr::c8_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src, dst, C, HW, n);
+  return grr::launch_status("grr_c8_convert");
+}
+
 grr_status grr_lnb_forward_keep(const float* x, const float* ln_w, const float* w1, const float* wdw,
                                 const float* w2, const float* skip, float* out, void* workspace, int B, int C,
                                 int hid, int H, int W, void* stream) {

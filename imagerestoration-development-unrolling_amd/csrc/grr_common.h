@@ -49,7 +49,7 @@ bool lnb_fused(int C, int hid);
 bool lnb_fused(int C, int hid);
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                             const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
-                            hipStream_t s, bool keep_g = false);
+                            hipStream_t s, bool keep_g = false, int io = 0);
 // the same block when x holds R stacked copies of the Ch-channel image xh (GEMM1 runs on xh)
 grr_status lnb_forward_mfma_rep(const float* xh, int Ch, int R, const float* x, const float* ln_w, const float* w1,
                                 const float* wdw, const float* w2, const float* skip, float* out, float* ws, int B,

@@ -1062,7 +1062,6 @@ struct LnbFusedArgs {
   float* g;              // [B, hid, H, W] or nullptr
   float var_den;
   int C, hid, H, W, tiles_x, tiles_y, nch, ntiles;
-  int stagger_groups, stagger_unit;   // start-phase stagger (grr_lnb_set_stagger)
 };
 
 // W1 images as lnb_w1_pack16_kernel's (rows 2^s_row-scaled, fp16 hi / lo); W2 images: row tile t, term q,
@@ -1150,9 +1149,6 @@ __device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint3
 #ifndef GRR_FUSED_STAMP
 #define GRR_FUSED_STAMP 0
 #endif
-#ifndef GRR_FUSED_PRO_ALL
-#define GRR_FUSED_PRO_ALL 0
-#endif
 #if GRR_FUSED_STAMP
 __device__ unsigned long long g_fused_stamps[1024 * 8 * 8];
 #define FSTAMP(k)                                              \
@@ -1176,8 +1172,16 @@ __device__ __forceinline__ FusedTile fused_tile(const LnbFusedArgs& a, int t) {
   return FusedTile{r / a.tiles_y, (r % a.tiles_y) * LF_TH, tx * LF_TW};
 }
 
-template <int KS, int MT>
+// IO: bit 0 -- x (and the skip operand) in the channel-blocked layout [B][NB][H][W][8] (NB = ceil(C / 8), the
+// pad channels 0; grr_lnb_forward_c8), bit 1 -- out in it; else [B, C, H, W].  The blocked layout serves the
+// kernel's memory instructions: the producer's 8 channels of a pixel per k-step are 32 contiguous bytes (two
+// dwordx4 loads instead of eight dword loads) and the consumer's four consecutive accumulator rows of a pixel
+// are 16 contiguous bytes (one dwordx4 load / store instead of four).  The prologue / epilogue step of a tile
+// is bound by the count of those instructions (phase stamps: a quarter of the prologue loads halved the
+// prologue), not by bytes.  Same values in the same registers either way: the results are bitwise equal.
+template <int KS, int MT, int IO>
 __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
+  constexpr bool IN8 = (IO & 1) != 0, OUT8 = (IO & 2) != 0;
   constexpr int NI = fused_images(KS, MT), SLOTF = NI * 256;
   constexpr int DPW = (NI + 7) / 8;      // LDS-DMA instructions per wave per step
   __shared__ __attribute__((aligned(16))) float smem[2 * LF_HBUF + LF_NSLOT * SLOTF + 32 * MT];
@@ -1214,14 +1218,6 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
     dsl = dsl == LF_NSLOT - 1 ? 0 : dsl + 1;
   };
   if (nsteps == 0) return;   // workgroup-uniform: no barrier is left waiting
-  // Start-phase stagger: every workgroup walks identical tiles, so left alone they run in lockstep and all
-  // of them load their next tile's x halo (producers) and store the finished tile (consumers: skip x in,
-  // out) in the same step -- one chip-wide HBM burst per tile while the other 15 steps move almost no
-  // bytes.  Workgroup group k = (wg / 8) % groups (consecutive workgroups go to the 8 XCDs in turn) sleeps
-  // k units of 2048 cycles first, which spreads the bursts over the tile's steps.
-  if (a.stagger_groups > 1) {
-    for (int r = ((wg >> 3) % a.stagger_groups) * a.stagger_unit; r > 0; --r) __builtin_amdgcn_s_sleep(32);
-  }
 #if GRR_FUSED_STAMP
   unsigned long long st_acc[8] = {}, st_prev = __builtin_amdgcn_s_memtime();
   auto stamp_out = [&]() {
@@ -1257,37 +1253,12 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
           // x of the image through a buffer descriptor: channel 16 s + 8 kh + j of the lane's pixel at
           // voffset (pixel + 8 kh HW) 4 + soffset (16 s + j) HW 4 -- the uniform part in an SGPR, no
           // per-element address arithmetic -- and channels >= C past num_records read as 0
+          const int cx = IN8 ? 8 * ((C + 7) / 8) : C;   // channels of one image in x (blocked: the pads too)
           const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-              const_cast<float*>(a.x + (int64_t)T.b * C * HW), 0, (int)((int64_t)C * HW * 4), 0x00020000);
+              const_cast<float*>(a.x + (int64_t)T.b * cx * HW), 0, (int)((int64_t)cx * HW * 4), 0x00020000);
           bool any_corr = false;
-#if GRR_FUSED_PRO_ALL
-          // every block's loads first (one round trip of HBM latency instead of one per block)
-          float xva[NBW][KS][8];
 #pragma unroll
           for (int k = 0; k < NBW; ++k) {
-            const int q = min((wave + 4 * k) * 32 + (lane & 31), LF_NQ - 1);
-            const int hy = q / LF_HWD, hx = q - hy * LF_HWD;
-            const int gy = clampi(T.y0 - 1 + hy, 0, H - 1), gx = clampi(T.x0 - 1 + hx, 0, W - 1);
-            const int vo = (8 * kh * HW + gy * W + gx) * 4;
-            int hw4 = HW * 4;
-            asm volatile("" : "+s"(hw4));
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-#if GRR_FUSED_DIAG & 4   // timing only: a quarter of the loads (the others repeat them)
-                if (j & 3) { xva[k][s][j] = xva[k][s][j & 4]; continue; }
-#endif
-                xva[k][s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
-              }
-          }
-          __builtin_amdgcn_sched_barrier(0);   // (else the scheduler sinks blocks 1, 2's loads past block 0's math)
-#endif
-#pragma unroll
-          for (int k = 0; k < NBW; ++k) {
-#if GRR_FUSED_PRO_ALL
-            float (&xv)[KS][8] = xva[k];
-#else
             const int q = min((wave + 4 * k) * 32 + (lane & 31), LF_NQ - 1);
             const int hy = q / LF_HWD, hx = q - hy * LF_HWD;
             const int gy = clampi(T.y0 - 1 + hy, 0, H - 1), gx = clampi(T.x0 - 1 + hx, 0, W - 1);
@@ -1297,12 +1268,27 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
             int hw4 = HW * 4;
             asm volatile("" : "+s"(hw4));
             float xv[KS][8];
+            if constexpr (IN8) {
+              // blocked: channels 16 s + 8 kh + j = block 2 s + kh, lane j of it -- 32 bytes at voffset
+              // (kh HW + pixel) 32 + soffset 2 s HW 32; blocks >= NB past num_records read as 0
+              const uint32_t vo8 = (uint32_t)((kh * HW + gy * W + gx) * 32);
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
+              for (int s = 0; s < KS; ++s) {
+                const u32x4 lo = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo8, 16 * s * hw4, 0));
+                const u32x4 hi = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo8 + 16, 16 * s * hw4, 0));
 #pragma unroll
-              for (int j = 0; j < 8; ++j)
-                xv[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
-#endif
+                for (int j = 0; j < 4; ++j) {
+                  xv[s][j] = __uint_as_float(lo[j]);
+                  xv[s][4 + j] = __uint_as_float(hi[j]);
+                }
+              }
+            } else {
+#pragma unroll
+              for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                  xv[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
+            }
             float sum = 0.f;
 #pragma unroll
             for (int s = 0; s < KS; ++s)
@@ -1541,10 +1527,12 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
         // the lane's pixel at voffset (pixel + 4 kh HW) 4 + soffset (32 t + (u & 3) + 8 (u >> 2)) HW 4; rows
         // >= C fall past num_records (loads 0, stores dropped), pixels outside the image take an
         // out-of-range voffset
+        const int c8 = 8 * ((C + 7) / 8);
+        const int cx = IN8 ? c8 : C, co = OUT8 ? c8 : C;
         const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(a.x + (int64_t)T.b * C * HW), 0, (int)((int64_t)C * HW * 4), 0x00020000);
-        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)T.b * C * HW, 0,
-                                                                              (int)((int64_t)C * HW * 4), 0x00020000);
+            const_cast<float*>(a.x + (int64_t)T.b * cx * HW), 0, (int)((int64_t)cx * HW * 4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out + (int64_t)T.b * co * HW, 0,
+                                                                              (int)((int64_t)co * HW * 4), 0x00020000);
         const int Eb[2] = {E[0], E[1]};
         // the W2 row scales and 2^-E into the accumulators first, then every skip operand of both rows in one
         // round of loads (the gate's registers are dead here: acc2 + 2 MT x 16 fit), then the stores
@@ -1559,30 +1547,61 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         int hw4 = HW * 4;                          // (not hoisted: see the producer's x loads)
         asm volatile("" : "+s"(hw4));
-        uint32_t vx[2], vo[2];
+        // NCHW: row m at voffset (pixel + 4 kh HW) 4 + soffset (32 t + (u & 3) + 8 (u >> 2)) HW 4; blocked: rows
+        // 32 t + 8 q + 4 kh + 0..3 (u = 4 q + 0..3) are block 4 t + q, lanes 4 kh .. 4 kh + 3 of the pixel --
+        // 16 bytes at voffset pixel 32 + 16 kh + soffset (4 t + q) HW 32
+        uint32_t vx[2], vo[2], vx8[2], vo8[2];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int yy = T.y0 + 2 * cw + rb;
-          vx[rb] = (uint32_t)(4 * kh * HW + min(yy, H - 1) * W + min(gxo, W - 1)) * 4u;
-          vo[rb] = yy < H && gxo < W ? vx[rb] : 0x80000000u;
+          const uint32_t pix = (uint32_t)(min(yy, H - 1) * W + min(gxo, W - 1));
+          const bool in = yy < H && gxo < W;
+          vx[rb] = (uint32_t)(4 * kh * HW + pix) * 4u;
+          vo[rb] = in ? vx[rb] : 0x80000000u;
+          vx8[rb] = pix * 32u + 16u * kh;
+          vo8[rb] = in ? vx8[rb] : 0x80000000u;
         }
         float xv[2][MT][16];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-          for (int t = 0; t < MT; ++t)
+          for (int t = 0; t < MT; ++t) {
+            if constexpr (IN8) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-              xv[rb][t][u] = __uint_as_float(
-                  __builtin_amdgcn_raw_buffer_load_b32(xrs, vx[rb], (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0));
+              for (int q = 0; q < 4; ++q) {
+                const u32x4 v = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vx8[rb], (4 * t + q) * 8 * hw4, 0));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xv[rb][t][4 * q + r] = __uint_as_float(v[r]);
+              }
+            } else {
+#pragma unroll
+              for (int u = 0; u < 16; ++u)
+                xv[rb][t][u] = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(xrs, vx[rb], (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0));
+            }
+          }
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-          for (int t = 0; t < MT; ++t)
+          for (int t = 0; t < MT; ++t) {
+            if constexpr (OUT8) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[rb][t][u] + acc2[rb][t][u]), ors, vo[rb],
-                                                    (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0);
+              for (int q = 0; q < 4; ++q) {
+                u32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = __float_as_uint(s0 * xv[rb][t][4 * q + r] + acc2[rb][t][4 * q + r]);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b128(
+                                                           ors, 0, 0, 0)), v),
+                                                       ors, vo8[rb], (4 * t + q) * 8 * hw4, 0);
+              }
+            } else {
+#pragma unroll
+              for (int u = 0; u < 16; ++u)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0 * xv[rb][t][u] + acc2[rb][t][u]), ors, vo[rb],
+                                                      (32 * t + (u & 3) + 8 * (u >> 2)) * hw4, 0);
+            }
+          }
       }
       if (++ch == nch) {
         ch = 0;
@@ -1783,7 +1802,6 @@ static int64_t mix_pack_floats(int C, int hid) {
 
 // the fused block (lnb_fused16_kernel): C <= 96 (GEMM1's x of three halo blocks, 6 k-steps, in registers)
 int g_lnb_fused_on = 1;   // grr_lnb_set_fused (A/B measurement knob)
-int g_lnb_stagger_groups = 0, g_lnb_stagger_unit = 3;   // grr_lnb_set_stagger
 bool lnb_fused(int C, int hid) { return g_lnb_fused_on && C >= 2 && C <= 96 && hid >= 1; }
 int64_t fused_pack_floats(int C, int hid) {
   const int KS = (C + 15) / 16, MT = (C + 31) / 32, nch = (hid + 15) / 16;
@@ -1819,8 +1837,13 @@ static void launch_mix(const LnbMixArgs& m, bool v4, hipStream_t s) {
 int g_lnb_phases = 7;
 
 template <int KS>
-static void launch_fused(const LnbFusedArgs& f, unsigned grid, hipStream_t s) {
-  hipLaunchKernelGGL((lnb_fused16_kernel<KS, (KS + 1) / 2>), dim3(grid), dim3(512), 0, s, f);
+static void launch_fused(const LnbFusedArgs& f, unsigned grid, int io, hipStream_t s) {
+  switch (io) {
+    case 1: hipLaunchKernelGGL((lnb_fused16_kernel<KS, (KS + 1) / 2, 1>), dim3(grid), dim3(512), 0, s, f); break;
+    case 2: hipLaunchKernelGGL((lnb_fused16_kernel<KS, (KS + 1) / 2, 2>), dim3(grid), dim3(512), 0, s, f); break;
+    case 3: hipLaunchKernelGGL((lnb_fused16_kernel<KS, (KS + 1) / 2, 3>), dim3(grid), dim3(512), 0, s, f); break;
+    default: hipLaunchKernelGGL((lnb_fused16_kernel<KS, (KS + 1) / 2, 0>), dim3(grid), dim3(512), 0, s, f);
+  }
 }
 // compute units of the current device (cached per device)
 static int num_cus() {
@@ -1837,7 +1860,9 @@ static int num_cus() {
 
 grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, const float* wdw, const float* w2,
                             const float* skip, float* out, float* ws, int B, int C, int hid, int H, int W,
-                            hipStream_t s, bool keep_g) {
+                            hipStream_t s, bool keep_g, int io) {
+  GRR_REQUIRE(io == 0 || (lnb_fused(C, hid) && !keep_g), GRR_ERR_UNSUPPORTED,
+              "grr_lnb_forward_c8: the channel-blocked layout needs the fused pass (C <= 96) without the kept gate");
   if (!lnb_fused(C, hid)) {
     // the two-kernel path leaves g at the workspace's start anyway
     return lnb_forward_mfma_rep(x, C, 1, x, ln_w, w1, wdw, w2, skip, out, ws, B, hid, H, W, s);
@@ -1863,8 +1888,6 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
   f.x = x; f.pack = pack; f.r2 = r2; f.skip = skip; f.out = out;
   f.g = keep_g ? ws : nullptr;
   f.var_den = (float)(C - 1);
-  f.stagger_groups = g_lnb_stagger_groups;
-  f.stagger_unit = g_lnb_stagger_unit;
   f.C = C; f.hid = hid; f.H = H; f.W = W; f.nch = nch;
   f.tiles_x = (W + LF_TW - 1) / LF_TW;
   f.tiles_y = (H + LF_TH - 1) / LF_TH;
@@ -1874,12 +1897,12 @@ grr_status lnb_forward_mfma(const float* x, const float* ln_w, const float* w1, 
   // persistent: one workgroup per CU (its LDS), each walking tiles blockIdx.x, + gridDim.x, ...
   const unsigned grid = (unsigned)std::min<uint64_t>(nt, (uint64_t)num_cus());
   switch (KS) {
-    case 1: launch_fused<1>(f, grid, s); break;
-    case 2: launch_fused<2>(f, grid, s); break;
-    case 3: launch_fused<3>(f, grid, s); break;
-    case 4: launch_fused<4>(f, grid, s); break;
-    case 5: launch_fused<5>(f, grid, s); break;
-    default: launch_fused<6>(f, grid, s); break;
+    case 1: launch_fused<1>(f, grid, io, s); break;
+    case 2: launch_fused<2>(f, grid, io, s); break;
+    case 3: launch_fused<3>(f, grid, io, s); break;
+    case 4: launch_fused<4>(f, grid, io, s); break;
+    case 5: launch_fused<5>(f, grid, io, s); break;
+    default: launch_fused<6>(f, grid, io, s); break;
   }
   return launch_status("grr_lnb_forward/fused");
 }
@@ -2012,15 +2035,6 @@ extern "C" grr_status grr_lnb_set_fused(int enable) {
   grr::clear_error();
   GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_lnb_set_fused: 0 or 1");
   grr::g_lnb_fused_on = enable;
-  return GRR_OK;
-}
-
-extern "C" grr_status grr_lnb_set_stagger(int groups, int unit) {
-  grr::clear_error();
-  GRR_REQUIRE(groups >= 0 && groups <= 64 && unit >= 0 && unit <= 64, GRR_ERR_INVALID_ARG,
-              "grr_lnb_set_stagger: groups in [0, 64], unit in [0, 64]");
-  grr::g_lnb_stagger_groups = groups;
-  grr::g_lnb_stagger_unit = unit;
   return GRR_OK;
 }
 

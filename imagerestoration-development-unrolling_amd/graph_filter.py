@@ -71,6 +71,38 @@ def records_grad(module: nn.Module, *tensors) -> bool:
                                         or any(p.requires_grad for p in module.parameters()))
 
 
+# Chains of fused LocalNonLinearBlocks hand their intermediate tensors on in the channel-blocked layout
+# (kernels.lnb_forward_c8: bitwise equal, fewer and wider memory instructions in each block).  Eager
+# inference only; compiled graphs and training keep [B, C, H, W].
+BLOCKED_CHAINS = True
+
+
+def run_blocks(blocks, x, first=None):
+    """x through the LocalNonLinearBlocks `blocks` in order; `first`, when given, replaces the first block's
+    call (x -> its output, [B, C, H, W]).  Inference chains of fused blocks pass the blocked layout between
+    the blocks; the result is [B, C, H, W] either way."""
+    blocks = list(blocks)
+    out = first(x) if first is not None else None
+    rest = blocks[1:] if first is not None else blocks
+    if out is None:
+        out, rest = x, blocks
+    b, c, h, w = out.shape
+    chain = (BLOCKED_CHAINS and out.is_cuda and len(rest) >= 2
+             and not torch.compiler.is_compiling()
+             and all(isinstance(k, LocalNonLinearBlock) and k._blockable(h, w) and k.dim == c for k in rest)
+             and not any(records_grad(k, out) for k in rest))
+    if not chain:
+        for k in rest:
+            out = k(out)
+        return out
+    blocked = False
+    for i, k in enumerate(rest):
+        last = i == len(rest) - 1
+        out = k._forward_c8(out, blocked, not last)
+        blocked = not last
+    return out
+
+
 def hip_forward(fn):
     """Run a HIP-backed forward; when autograd is recording, attach a node whose
     backward raises, so a training loop can never silently drop gradients."""
@@ -282,6 +314,18 @@ class LocalNonLinearBlock(HipModule):
                                    ll.channels_local_linear_op.weight.view(2 * hid, 9),
                                    ll.project_out.weight.view(c, hid), self.skip_weight)
 
+    def _blockable(self, h: int, w: int) -> bool:
+        return self.nsubnets == 1 and K.lnb_c8_ok(self.dim, self.hidden_dim, h, w)
+
+    def _forward_c8(self, x, in_c8: bool, out_c8: bool):
+        """Inference forward with x / out in the channel-blocked layout (kernels.lnb_forward_c8)."""
+        ll = self.local_linear
+        c, hid = self.dim, self.hidden_dim
+        return K.lnb_forward_c8(x, c, self.norm.weighted_transform.weight.view(c),
+                                ll.channels_linear_op.weight.view(2 * hid, c),
+                                ll.channels_local_linear_op.weight.view(2 * hid, 9),
+                                ll.project_out.weight.view(c, hid), self.skip_weight, in_c8, out_c8)
+
     @hip_forward
     def _forward_hip(self, x):
         ll = self.local_linear
@@ -362,9 +406,7 @@ class MixtureGTVGLR(HipModule):
         ref = y if y is not None else src
 
         def half():
-            f1 = self._down(y, s1[0].weight, src)
-            for blk in list(s1)[1:4]:
-                f1 = blk(f1)
+            f1 = run_blocks(list(s1)[1:4], self._down(y, s1[0].weight, src))
             f1 = OPS.conv1x1(f1, s1[4].weight)
             return half_tail(f1) if half_tail is not None else f1
 
@@ -380,9 +422,7 @@ class MixtureGTVGLR(HipModule):
             f1 = half()
         blocks = list(s0)[:3]
         # the first block's input replicates src over the graphs: its GEMM1 runs on src (K = F)
-        f0 = blocks[0].forward_replicated(src, y) if src is not None else blocks[0](y)
-        for blk in blocks[1:]:
-            f0 = blk(f0)
+        f0 = run_blocks(blocks, y, first=(lambda _y: blocks[0].forward_replicated(src, _y)) if src is not None else None)
         f0 = OPS.conv1x1(f0, s0[3].weight)
         if side is not None:
             main.wait_stream(side)

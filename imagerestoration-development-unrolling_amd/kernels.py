@@ -690,6 +690,59 @@ def lnb_forward(x: Tensor, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, sk
     return out
 
 
+def c8_shape(b: int, c: int, h: int, w: int) -> Tuple[int, int, int, int, int]:
+    """Shape of the channel-blocked layout of a [B, C, H, W] tensor: [B, ceil(C / 8), H, W, 8]."""
+    return (b, (c + 7) // 8, h, w, 8)
+
+
+def to_c8(x: Tensor) -> Tensor:
+    """[B, C, H, W] -> the channel-blocked layout (grr_c8_convert; pad channels 0)."""
+    dev = _check("to_c8", x)
+    b, c, h, w = x.shape
+    y = torch.empty(c8_shape(b, c, h, w), dtype=torch.float32, device=dev)
+    _launch("c8_convert", 8 * y.numel(), "grr_c8_convert", x.contiguous().data_ptr(), y.data_ptr(), b, c, h, w, 1,
+            _stream(dev))
+    return y
+
+
+def from_c8(y: Tensor, c: int) -> Tensor:
+    """The channel-blocked layout -> [B, C, H, W]."""
+    dev = _check("from_c8", y)
+    b, nb, h, w, _ = y.shape
+    x = torch.empty((b, c, h, w), dtype=torch.float32, device=dev)
+    _launch("c8_convert", 8 * x.numel(), "grr_c8_convert", y.data_ptr(), x.data_ptr(), b, c, h, w, 0, _stream(dev))
+    return x
+
+
+def lnb_c8_ok(c: int, hid: int, h: int, w: int) -> bool:
+    """Where lnb_forward_c8 applies: the fused C <= 96 pass, one band."""
+    return bool(_native.load().grr_lnb_fused(c, hid)) and _lnb_band_rows(c, hid, h, w) >= h and \
+        ((c + 7) // 8) * 8 * h * w * 4 < (1 << 31)
+
+
+def lnb_forward_c8(x: Tensor, c: int, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor,
+                   in_c8: bool, out_c8: bool) -> Tensor:
+    """lnb_forward with x and / or out in the channel-blocked layout (grr_lnb_forward_c8): a chain of fused
+    blocks hands the blocked tensor on, the kernel then loads and stores 16 / 32 bytes per lane instead of
+    dwords.  Bitwise equal to lnb_forward.  lnb_c8_ok must hold."""
+    dev = _check("lnb_forward_c8", x, ln_w, w1, wdw, w2, skip)
+    if in_c8:
+        b, _, h, w, _ = x.shape
+    else:
+        b, c_in, h, w = x.shape
+        if c_in != c:
+            raise ValueError("lnb_forward_c8: channels")
+    hid = w2.shape[1]
+    lib = _native.load()
+    ws = torch.empty((lib.grr_lnb_fused_workspace_bytes(c, hid) + 3) // 4, dtype=torch.float32, device=dev)
+    out = torch.empty(c8_shape(b, c, h, w) if out_c8 else (b, c, h, w), dtype=torch.float32, device=dev)
+    xc = x.contiguous()
+    _launch("lnb_fused", 4 * b * h * w * 2 * c, "grr_lnb_forward_c8", xc.data_ptr(), ln_w.data_ptr(), w1.data_ptr(),
+            wdw.data_ptr(), w2.data_ptr(), skip.data_ptr(), out.data_ptr(), ws.data_ptr(), b, c, hid, h, w,
+            int(in_c8) | 2 * int(out_c8), _stream(dev), flops=lnb_flops(b * h * w, c, c, hid))
+    return out
+
+
 def lnb_gate_keepable(c: int, hid: int, h: int, w: int) -> bool:
     """lnb_forward_keep's shapes: the C <= 128 head + mix pipeline in one band (its workspace starts
     with the gated activation g [B, hid, H, W])."""

@@ -333,6 +333,19 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
                            const float* w2, const float* skip, float* out, void* workspace,
                            int B, int C, int hid, int H, int W, void* stream);
 
+/* grr_lnb_forward with either side in the channel-blocked layout [B, ceil(C / 8), H, W, 8] (channel
+ * 8 k + j of pixel p at ((b ceil(C / 8) + k) H W + p) 8 + j; pad channels 0): layout bit 0 -- x (read for
+ * LN / W1 and the skip term) blocked, bit 1 -- out blocked.  Needs grr_lnb_fused(C, hid); x and out 16-B
+ * aligned; workspace as grr_lnb_forward's.  Results equal grr_lnb_forward's bitwise (same arithmetic; the
+ * layout only changes the kernel's memory instructions: 16- and 32-byte accesses per lane instead of
+ * dwords).  A chain of blocks passes the blocked tensor from one to the next (no reference counterpart:
+ * an internal layout of the feature CNN between its LocalNonLinearBlocks, REF13:541-575). */
+grr_status grr_lnb_forward_c8(const float* x, const float* ln_w, const float* w1, const float* wdw,
+                              const float* w2, const float* skip, float* out, void* workspace, int B, int C,
+                              int hid, int H, int W, int layout, void* stream);
+/* [B, C, H, W] -> blocked (to_blocked = 1, pads written 0) or back (0). */
+grr_status grr_c8_convert(const float* src, float* dst, int B, int C, int H, int W, int to_blocked, void* stream);
+
 /* grr_lnb_forward that also leaves the gated activation g = sigmoid(m) m v [B, hid, H, W] (fp32) at the
  * start of the workspace, for the training reverse's W2 weight gradient (the eager LocalNonLinearBlock
  * forward keeps it instead of recomputing the depthwise + gate).  C <= 128. */
@@ -350,11 +363,6 @@ int64_t grr_lnb_fused_workspace_bytes(int C, int hid);
 /* Measurement knob (process-wide): 0 runs C <= 96 blocks on the two-kernel head + mix path instead of
  * the fused pass (same results to fp32 rounding); 1 (default) fused. */
 grr_status grr_lnb_set_fused(int enable);
-/* Measurement knob (process-wide) of the fused C <= 96 pass: its persistent workgroups start in
- * `groups` phases, group k (of workgroups wg, (wg / 8) % groups) after k * unit * 2048 cycles, so the
- * per-tile HBM bursts of the workgroups do not coincide.  groups <= 1: no stagger.  Results are
- * independent of it. */
-grr_status grr_lnb_set_stagger(int groups, int unit);
 /* grr_lnb_forward for an input x [B, R*Cs, H, W] that is R stacked copies of src [B, Cs, H, W]
  * (the first feature block of MultiScaleGraphFilter, whose input replicates RGB over the graphs,
  * REF13:918-921): LN statistics and W1 are evaluated on src with W1 diag(ln_w) folded over the

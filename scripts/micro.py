@@ -40,13 +40,13 @@ def main():
                          "2 the term pass + the stencil x-gradient pass")
     ap.add_argument("--term-rows", type=int, default=2, choices=[0, 1, 2],
                     help="term: 0 per-pixel, 1 register-prefetch row kernel, 2 LDS-ring row kernel (default)")
-    ap.add_argument("--stagger", default="0,3", help="LNB fused: groups,unit (grr_lnb_set_stagger)")
+    ap.add_argument("--c8", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="LNB fused: channel-blocked layout of x (1), out (2) or both (3)")
     args = ap.parse_args()
     K.set_kernel_variant(args.variant)
     K.set_term_rows(args.term_rows)
     from irdu_amd._native import call
     call("grr_lnb_set_fused", args.lnb_fused)
-    call("grr_lnb_set_stagger", *[int(v) for v in args.stagger.split(",")])
     dev = torch.device("cuda", 0)
     b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.width or args.size
     c = g * f
@@ -82,7 +82,11 @@ def main():
         fn = lambda: K.system_half(xd, wl1, cg1, sl, sg, p(mix.muys01), p(mix.ro01), g)  # noqa: E731
     elif args.kernel == "lnb":
         blk = irdu_amd.LocalNonLinearBlock(c, args.hid, 1).to(dev)
-        fn = lambda: blk(x)  # noqa: E731
+        if args.c8:   # the channel-blocked layout on the input (bit 0) / output (bit 1) side
+            xin = K.to_c8(x) if args.c8 & 1 else x
+            fn = lambda: blk._forward_c8(xin, bool(args.c8 & 1), bool(args.c8 & 2))  # noqa: E731
+        else:
+            fn = lambda: blk(x)  # noqa: E731
     elif args.kernel == "lnb_rep":   # first block of the image filter: RGB replicated over the graphs
         blk = irdu_amd.LocalNonLinearBlock(c, 256, 1).to(dev)
         src = torch.rand(b, 3, h, w, device=dev)
