@@ -81,6 +81,9 @@ SIGNATURES = {
     "grr_lnb_forward_keep": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grr_lnb_forward_c8": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
     "grr_c8_convert": [P, P, I, I, I, I, I, P],
+    "grr_feature_edges_supported": [I, I, I, I, I],
+    "grr_feature_edges_workspace_bytes": [I],
+    "grr_feature_edges": [P, I, P, P, P, P, P, P, P, I, I, I, I, I, I, P],
     "grr_lnb_fused": [I, I],
     "grr_lnb_fused_workspace_bytes": [I, I],
     "grr_lnb_set_fused": [I],
@@ -149,7 +152,7 @@ SIGNATURES = {
 _RESTYPES = {"grr_version": c_int, "grr_last_error": ctypes.c_char_p, "grr_lnb_workspace_bytes": c_int64,
              "grr_conv1x1_workspace_bytes": c_int64, "grr_wgrad_workspace_bytes": c_int64,
              "grr_ffn_workspace_bytes": c_int64, "grr_scratch_bytes": c_int64,
-             "grr_lnb_fused_workspace_bytes": c_int64}
+             "grr_lnb_fused_workspace_bytes": c_int64, "grr_feature_edges_workspace_bytes": c_int64}
 
 _lib = None
 

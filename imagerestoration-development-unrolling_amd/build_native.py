@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrr.so")
-SOURCES = ["graph_ops.hip", "feature_ops.hip", "lnb_ops.hip", "graph_bwd.hip", "lnb_bwd.hip", "window_ops.hip", "window_bwd.hip", "subapi_ops.hip", "subapi_bwd.hip", "wgrad_ops.hip"]
+SOURCES = ["graph_ops.hip", "feature_ops.hip", "lnb_ops.hip", "graph_bwd.hip", "lnb_bwd.hip", "window_ops.hip", "window_bwd.hip", "subapi_ops.hip", "subapi_bwd.hip", "wgrad_ops.hip", "feature_edge.hip"]
 HEADERS = [os.path.join(CSRC, "grr_common.h"), os.path.join(ROOT, "include", "grr.h")]
 ARCH = "gfx950"
 # lnb_ops, graph_ops: no SLP packing of independent f32 FMAs into v_pk_fma_f32 (the packing

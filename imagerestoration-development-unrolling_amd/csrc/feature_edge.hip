@@ -1,0 +1,435 @@
+// The image filter's last feature 1x1 conv and the edge weights of both graph modules of a level in one pass
+// (REF:146-175 extract_edge_weights / normalize_and_transform_features on the features of REF13:887-926's
+// patchs_features_extraction 1x1 output).  Before, the 1x1 conv (C -> 2C, gemm_x3_kernel) wrote the [B, 2C, H, W]
+// feature tensor and the edge-row kernel read it back: 768 + 768 B per pixel of HBM traffic between two
+// launches.  Here the features never leave the CU.
+//
+// Workgroup = (b, 29-column strip, row segment), 9 waves:
+//  * wave 8 (loader) streams the strip's input rows (the LocalNonLinearBlock output x, [B, C, H, W] or the
+//    channel-blocked [B, C/8, H, W, 8] of grr_lnb_forward_c8) one row ahead, scales each pixel by a power of two
+//    (its largest |x| into [2^13, 2^14)), splits it into exact-sum fp16 hi / lo terms in the layout of the
+//    32x32x16 MFMA's B operand, and writes them into a 2-slot LDS ring;
+//  * waves 0..7 each own 8 graphs of one slab (waves 0-3 the GTV features, 4-7 the GLR features; lane half kh
+//    holds graphs 8 t + 4 kh .. + 3): per row, the 1x1 conv of the strip's 32 columns (x0 - 1 .. x0 + 30) on
+//    v_mfma_f32_32x32x16_f16 (three products of the two-term splits, A = the wave's weight rows resident in
+//    registers, scaled by a power of two per (slab, graph)) leaves each lane the 12 features (4 graphs x 3) of
+//    its column; normalisation (F.normalize * multiM), the four neighbour similarities (left / right by DPP
+//    lane shifts, up / down from the previous rows' registers), the softmax and (GTV) the pair weights follow
+//    in registers, edge_row_kernel's expressions.  Lanes 0, 30 and 31 of a half are the strip's halo columns.
+// The power-of-two scales need no undoing: F.normalize is exact under them (sqrt and division commute with a
+// power-of-two factor; the 1e-12 floor is scaled alike).
+#include <type_traits>
+
+#include "grr_common.h"
+
+namespace grr {
+namespace {
+
+typedef _Float16 fe_f16x8 __attribute__((ext_vector_type(8)));
+typedef float fe_f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t fe_u32x4 __attribute__((ext_vector_type(4)));
+typedef float fe_f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 fe_f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int FE_KS = 6;                 // k-steps of 16: input channels <= 96
+constexpr int FE_GH = 4;                 // graphs per lane half (12 of the 16 accumulator rows)
+constexpr int FE_TPS = 4;                // tiles (waves) per slab: G <= 32
+constexpr int FE_NT = 2 * FE_TPS;        // compute waves
+constexpr int FE_THREADS = 64 * (FE_NT + 1);
+// output columns per strip: window columns 1..29 (column 30 is computed too: its w_left is the pair weight
+// c_h of column 29; column 31's softmax reads past the window)
+constexpr int FE_OWN = 29;
+constexpr int FE_SLOT = FE_KS * 2 * 256 + 32;   // floats per ring slot: the B images (hi, lo per k-step) + ep
+constexpr uint32_t FE_OOB = 0x80000000u;
+
+struct FeArgs {
+  const float* x;          // [B, C, H, W], or channel-blocked
+  const char* pack;        // [tile][k-step][term] 1-KB A images (fe_pack_kernel)
+  const int* sexp;         // [2][G] power-of-two scale of each (slab, graph)'s weight rows
+  const float* multiM[2];  // [G, 3] per slab (GTV, GLR)
+  float* w[2];             // raw weights [B, G, 4, H, W] per slab
+  float* c;                // GTV pair weights [B, G, 2, H, W]
+  int C, G, H, W, nstrips, sseg, nsegs;
+  uint32_t nblk;
+};
+
+__device__ __forceinline__ int fe_scale_exp(float mx) {   // mx 2^s in [2^13, 2^14)
+  if (mx == 0.f) return 0;
+  int e;
+  frexpf(mx, &e);
+  return clampi(14 - e, -100, 100);
+}
+// (slab, graph) -> the exponent of its three weight rows
+__device__ __forceinline__ int fe_graph_exp(const float* __restrict__ wf, int slab, int g, int G, int K) {
+  float mx = 0.f;
+  for (int f = 0; f < 3; ++f) {
+    const float* row = wf + (int64_t)(slab * 3 * G + 3 * g + f) * K;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, fabsf(row[k]));
+  }
+  return fe_scale_exp(mx);
+}
+
+// A images: tile T (slab T / 4, graphs 8 (T % 4) ..), k-step s, term q; lane l, element j: A row i = l & 31
+// (lane half kh = (i >> 2) & 1, accumulator register r = ((i >> 3) << 2) | (i & 3): graph 8 (T % 4) + 4 kh + r / 3,
+// feature r % 3 for r < 12, else zero), k = 16 s + 8 (l >> 5) + j
+__global__ void fe_pack_kernel(const float* __restrict__ wf, char* __restrict__ pack, int* __restrict__ sexp, int G,
+                               int K) {
+  const int n_img = FE_NT * FE_KS * 2 * 256;
+  const int n = n_img + 2 * G;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (i >= n_img) {
+      const int sg = i - n_img;
+      sexp[sg] = fe_graph_exp(wf, sg / G, sg % G, G, K);
+      continue;
+    }
+    const int img = i >> 8, e = i & 255;
+    const int T = img / (FE_KS * 2), s = (img >> 1) % FE_KS, q = img & 1;
+    const int l = e >> 2, jw = e & 3;
+    const int ir = l & 31, khr = (ir >> 2) & 1, r = ((ir >> 3) << 2) | (ir & 3);
+    const int slab = T / FE_TPS, g = 8 * (T % FE_TPS) + 4 * khr + r / 3;
+    uint32_t word = 0;
+    if (r < 3 * FE_GH && g < G) {
+      const int row = slab * 3 * G + 3 * g + r % 3, sc = fe_graph_exp(wf, slab, g, G, K);
+      float v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = 16 * s + 8 * (l >> 5) + 2 * jw + u;
+        v[u] = k < K ? ldexpf(wf[(int64_t)row * K + k], sc) : 0.f;
+      }
+      const _Float16 h0 = (_Float16)v[0], h1 = (_Float16)v[1];
+      const _Float16 t0 = q == 0 ? h0 : (_Float16)(v[0] - (float)h0), t1 = q == 0 ? h1 : (_Float16)(v[1] - (float)h1);
+      word = (uint32_t)__builtin_bit_cast(uint16_t, t0) | ((uint32_t)__builtin_bit_cast(uint16_t, t1) << 16);
+    }
+    reinterpret_cast<uint32_t*>(pack)[i] = word;
+  }
+}
+
+__device__ __forceinline__ float fe_prev(float v) {   // lane - 1 (DPP wave shift; whole wave active)
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ float fe_next(float v) {   // lane + 1
+  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+template <bool IN8>
+__global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
+  __shared__ __attribute__((aligned(16))) float ring[2 * FE_SLOT];
+  const int lane = threadIdx.x & 63, kh = lane >> 5, n = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t unit = xcd_remap(blockIdx.x, a.nblk);
+  const int strip = unit % a.nstrips;
+  unit /= a.nstrips;
+  const int seg = unit % a.nsegs;
+  const int b = unit / a.nsegs;
+  const int H = a.H, W = a.W, G = a.G, C = a.C;
+  const int HW = H * W;
+  const int x0 = strip * FE_OWN;   // first owned column; window column n = image column x0 - 1 + n
+  const int col = x0 - 1 + n;
+  const int colc = clampi(col, 0, W - 1);
+  const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
+  // a segment ending inside the image runs one more edge row (not stored) for its last row's c_v
+  const int rend = r1 < H ? r1 + 1 : H;
+  // iteration k: the conv of row r0 - 1 + k (clamped into the image; k <= rend - r0 + 1) and the edges of row
+  // r0 - 3 + k (k >= 3)
+  const int NI = rend - r0 + 3;
+  const int NI3 = (NI + 2) / 3 * 3;
+
+  if (wave == FE_NT) {
+    // ---------------- loader
+    const int cx = IN8 ? 8 * ((C + 7) / 8) : C;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x + (int64_t)b * cx * HW), 0, (int)((int64_t)cx * HW * 4), 0x00020000);
+    float v[FE_KS][8];
+    auto issue = [&](int k) {   // input row of iteration k
+      const int gy = clampi(r0 - 1 + k, 0, H - 1);
+      int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
+      asm volatile("" : "+s"(hw4));
+      if constexpr (IN8) {
+        const uint32_t vo = (uint32_t)((kh * HW + gy * W + colc) * 32);
+#pragma unroll
+        for (int s = 0; s < FE_KS; ++s) {
+          const fe_u32x4 lo = __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, 16 * s * hw4, 0));
+          const fe_u32x4 hi = __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 16, 16 * s * hw4, 0));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[s][j] = __uint_as_float(lo[j]);
+            v[s][4 + j] = __uint_as_float(hi[j]);
+          }
+        }
+      } else {
+        const uint32_t vo = (uint32_t)((8 * kh * HW + gy * W + colc) * 4);
+#pragma unroll
+        for (int s = 0; s < FE_KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
+      }
+    };
+    auto put = [&](int sl) {   // the loaded row -> ring slot sl
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      float mx = 0.f;
+#pragma unroll
+      for (int s = 0; s < FE_KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[s][j]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const int ep = fe_scale_exp(mx);
+      float* slot = ring + sl * FE_SLOT;
+#pragma unroll
+      for (int s = 0; s < FE_KS; ++s) {
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const fe_f32x2 p = fe_f32x2{ldexpf(v[s][2 * j], ep), ldexpf(v[s][2 * j + 1], ep)};
+          const fe_f16x2 h = __builtin_convertvector(p, fe_f16x2);
+          const fe_f16x2 l = __builtin_convertvector(p - __builtin_convertvector(h, fe_f32x2), fe_f16x2);
+          hw[j] = __builtin_bit_cast(uint32_t, h);
+          lw[j] = __builtin_bit_cast(uint32_t, l);
+        }
+        *reinterpret_cast<fe_u32x4*>(slot + (2 * s) * 256 + 4 * lane) = fe_u32x4{hw[0], hw[1], hw[2], hw[3]};
+        *reinterpret_cast<fe_u32x4*>(slot + (2 * s + 1) * 256 + 4 * lane) = fe_u32x4{lw[0], lw[1], lw[2], lw[3]};
+      }
+      if (kh == 0) reinterpret_cast<int*>(slot + FE_KS * 2 * 256)[n] = ep;
+    };
+    issue(0);
+    put(0);
+    issue(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int k = 0; k < NI3; ++k) {
+      if (k + 1 <= NI - 2) {   // uniform: iterations 0 .. NI - 2 run a conv
+        put((k + 1) & 1);
+        if (k + 2 <= NI - 2) issue(k + 2);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---------------- compute wave: slab, tile
+  const int slab = wave >> 2, t4 = wave & 3;
+  const int gbase = 8 * t4 + 4 * kh;                 // the lane half's first graph
+  if (8 * t4 >= G) {                                 // no graph in this tile: the barriers only
+    for (int k = 0; k <= NI3; ++k) __builtin_amdgcn_s_barrier();
+    return;
+  }
+  fe_f16x8 ah[FE_KS], al[FE_KS];
+  {
+    const char* pk = a.pack + (int64_t)wave * FE_KS * 2 * 1024 + lane * 16;
+#pragma unroll
+    for (int s = 0; s < FE_KS; ++s) {
+      ah[s] = *reinterpret_cast<const fe_f16x8*>(pk + (2 * s) * 1024);
+      al[s] = *reinterpret_cast<const fe_f16x8*>(pk + (2 * s + 1) * 1024);
+    }
+  }
+  float M[FE_GH][3];
+  int sg[FE_GH];
+#pragma unroll
+  for (int gi = 0; gi < FE_GH; ++gi) {
+    const int g = min(gbase + gi, G - 1);
+    sg[gi] = a.sexp[slab * G + g];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) M[gi][f] = a.multiM[slab][g * 3 + f];
+  }
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      a.w[slab] + (int64_t)b * G * 4 * HW, 0, (int)((int64_t)G * 4 * HW * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      slab == 0 ? a.c + (int64_t)b * G * 2 * HW : nullptr, 0, slab == 0 ? (int)((int64_t)G * 2 * HW * 4) : 0,
+      0x00020000);
+  // the lane stores its column (window columns 1..30 inside the image), graphs of its half only
+  const bool lane_out = n >= 1 && n <= FE_OWN && col < W;
+  float fw[3][FE_GH][3];   // normalised features of three consecutive rows (rotating)
+  float wdn_prev[FE_GH];
+#pragma unroll
+  for (int gi = 0; gi < FE_GH; ++gi) wdn_prev[gi] = 0.f;
+
+  // normalise the conv of iteration k's row into fw[P]
+  auto normalise = [&](const fe_f32x16& acc, int ep, auto p_tag) __attribute__((always_inline)) {
+    constexpr int P = decltype(p_tag)::value;
+#pragma unroll
+    for (int gi = 0; gi < FE_GH; ++gi) {
+      const float f0 = acc[3 * gi], f1 = acc[3 * gi + 1], f2 = acc[3 * gi + 2];
+      float ss = __builtin_fmaf(f0, f0, 0.f);
+      ss = __builtin_fmaf(f1, f1, ss);
+      ss = __builtin_fmaf(f2, f2, ss);
+      const float den = fmaxf(sqrtf(ss), ldexpf(1e-12f, ep + sg[gi]));   // the scaled 1e-12 floor
+      fw[P][gi][0] = (f0 / den) * M[gi][0];
+      fw[P][gi][1] = (f1 / den) * M[gi][1];
+      fw[P][gi][2] = (f2 / den) * M[gi][2];
+    }
+  };
+  // edges of row ey from rows P (ey - 1), Q (ey), N (ey + 1); edge_row_kernel's arithmetic (V = 1)
+  auto edges = [&](int ey, auto p_tag, auto q_tag, auto n_tag) __attribute__((always_inline)) {
+    constexpr int P = decltype(p_tag)::value, Q = decltype(q_tag)::value, N = decltype(n_tag)::value;
+    const bool own = ey < r1;
+    const uint32_t row_off = (uint32_t)(ey * W + col);
+    const uint32_t vo = lane_out && own ? (row_off + 16u * kh * HW) * 4u : FE_OOB;
+    const uint32_t voc = lane_out && own ? (row_off + 8u * kh * HW) * 4u : FE_OOB;
+    const uint32_t vcv = lane_out && ey > r0 ? (row_off - W + 8u * kh * HW) * 4u : FE_OOB;   // row ey - 1
+    int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
+    asm volatile("" : "+s"(hw4));
+#pragma unroll
+    for (int gi = 0; gi < FE_GH; ++gi) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const float v = fw[Q][gi][f];
+        const float pl = fe_prev(v), pr = fe_next(v);
+        const float lv = col > 0 ? pl : v;
+        const float rv = col < W - 1 ? pr : v;
+        s0 += v * fw[P][gi][f];
+        s1 += v * lv;
+        s2 += v * rv;
+        s3 += v * fw[N][gi][f];
+      }
+      const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
+      const float e0 = expf(s0 - m), e1 = expf(s1 - m), e2 = expf(s2 - m), e3 = expf(s3 - m);
+      const float sum = ((e0 + e1) + e2) + e3;
+      const float w0 = e0 / sum, w1 = e1 / sum, w2 = e2 / sum, w3 = e3 / sum;
+      const bool gok = gbase + gi < G;
+      const uint32_t so = (uint32_t)((8 * t4 + gi) * 4) * hw4;
+      const uint32_t vg = gok ? vo : FE_OOB;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w0), wr, vg, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w1), wr, vg, so + hw4, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w2), wr, vg, so + 2 * hw4, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w3), wr, vg, so + 3 * hw4, 0);
+      if (slab == 0) {   // wave-uniform: pair weights (REF:452-516's C^T C as pair weights)
+        const float wln = fe_next(w1);   // w_left(p + right)
+        const float ch = col + 1 < W ? w2 * w2 + wln * wln : 0.f;
+        const float cv = wdn_prev[gi] * wdn_prev[gi] + w0 * w0;   // row ey - 1: w_down(p)^2 + w_up(p + down)^2
+        wdn_prev[gi] = w3;
+        const uint32_t soc = (uint32_t)((8 * t4 + gi) * 2) * hw4;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ch), crs, gok ? voc : FE_OOB, soc, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cv), crs, gok ? vcv : FE_OOB, soc + hw4, 0);
+      }
+    }
+  };
+
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // ring slot 0 holds row r0 - 1
+  asm volatile("" ::: "memory");
+  // phase PH = k mod 3: the row of iteration k goes to fw[PH]; the edge row's rows are fw[PH] (= k - 3),
+  // fw[(PH + 1) % 3] (k - 2), fw[(PH + 2) % 3] (k - 1)
+  auto iteration = [&](int k, auto ph_tag) __attribute__((always_inline)) {
+    constexpr int PH = decltype(ph_tag)::value;
+    using IP = std::integral_constant<int, PH>;
+    using IQ = std::integral_constant<int, (PH + 1) % 3>;
+    using IN = std::integral_constant<int, (PH + 2) % 3>;
+    if (k < NI) {   // uniform
+      const bool conv = k <= NI - 2;
+      fe_f32x16 acc = fe_f32x16{};
+      int ep = 0;
+      if (conv) {
+        const float* slot = ring + (k & 1) * FE_SLOT;
+#pragma unroll
+        for (int s = 0; s < FE_KS; ++s) {
+          const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256 + 4 * lane);
+          const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256 + 4 * lane);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc, 0, 0, 0);
+        }
+        ep = reinterpret_cast<const int*>(slot + FE_KS * 2 * 256)[n];
+      }
+      if (k >= 3) edges(r0 - 3 + k, IP{}, IQ{}, IN{});   // rows k - 3, k - 2, k - 1
+      if (conv) normalise(acc, ep, IP{});                // row k replaces row k - 3
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (int k = 0; k < NI3; k += 3) {
+    iteration(k, std::integral_constant<int, 0>{});
+    iteration(k + 1, std::integral_constant<int, 1>{});
+    iteration(k + 2, std::integral_constant<int, 2>{});
+  }
+  if (slab == 0 && r1 == H) {   // the image's last row: no lower neighbour, c_v = 0
+    int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
+    const uint32_t vz = lane_out ? ((uint32_t)((H - 1) * W + col) + 8u * kh * HW) * 4u : FE_OOB;
+#pragma unroll
+    for (int gi = 0; gi < FE_GH; ++gi)
+      __builtin_amdgcn_raw_buffer_store_b32(0u, crs, gbase + gi < G ? vz : FE_OOB, (uint32_t)((8 * t4 + gi) * 2 + 1) * hw4,
+                                            0);
+  }
+}
+
+}  // namespace
+}  // namespace grr
+
+using namespace grr;
+
+extern "C" {
+
+int64_t grr_feature_edges_workspace_bytes(int G) {
+  return G <= 0 ? 0 : (int64_t)FE_NT * FE_KS * 2 * 1024 + 256 * (((int64_t)2 * G * 4 + 255) / 256);
+}
+
+int grr_feature_edges_supported(int C, int G, int F, int H, int W) {
+  return F == 3 && G >= 1 && G <= FE_TPS * 8 && C == G * F && C <= 16 * FE_KS && H >= 1 && W >= 1 &&
+                 (int64_t)G * 4 * H * W * 4 < (1ll << 31)
+             ? 1
+             : 0;
+}
+
+grr_status grr_feature_edges(const float* x, int x_blocked, const float* wf, const float* multiM_gtv,
+                             const float* multiM_glr, float* wG, float* cG, float* wL, void* workspace, int B, int C,
+                             int G, int F, int H, int W, void* stream) {
+  clear_error();
+  GRR_REQUIRE(x && wf && multiM_gtv && multiM_glr && wG && cG && wL && workspace && B > 0, GRR_ERR_INVALID_ARG,
+              "grr_feature_edges: bad args");
+  GRR_REQUIRE(grr_feature_edges_supported(C, G, F, H, W), GRR_ERR_UNSUPPORTED,
+              "grr_feature_edges: needs F = 3, G <= %d, C = G F <= %d (got C %d, G %d, F %d)", FE_TPS * 8, 16 * FE_KS, C,
+              G, F);
+  GRR_REQUIRE(((uintptr_t)workspace & 255) == 0 && (!x_blocked || ((uintptr_t)x & 15) == 0), GRR_ERR_INVALID_ARG,
+              "grr_feature_edges: workspace 256-B aligned, a blocked x 16-B aligned");
+  GRR_REQUIRE((int64_t)((C + 7) / 8) * 8 * H * W * 4 < (1ll << 31), GRR_ERR_UNSUPPORTED,
+              "grr_feature_edges: image too large for 32-bit offsets");
+  hipStream_t s = (hipStream_t)stream;
+  char* pack = static_cast<char*>(workspace);
+  int* sexp = reinterpret_cast<int*>(pack + (int64_t)FE_NT * FE_KS * 2 * 1024);
+  {
+    const int n = FE_NT * FE_KS * 2 * 256 + 2 * G;
+    hipLaunchKernelGGL(fe_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, wf, pack, sexp, G, C);
+    grr_status st = launch_status("grr_feature_edges/pack");
+    if (st != GRR_OK) return st;
+  }
+  FeArgs a{};
+  a.x = x;
+  a.pack = pack;
+  a.sexp = sexp;
+  a.multiM[0] = multiM_gtv;
+  a.multiM[1] = multiM_glr;
+  a.w[0] = wG;
+  a.w[1] = wL;
+  a.c = cG;
+  a.C = C;
+  a.G = G;
+  a.H = H;
+  a.W = W;
+  a.nstrips = (W + FE_OWN - 1) / FE_OWN;
+  // row segments: >= 4 workgroups per CU where the batch allows, segments of >= 32 rows (each costs 3 extra
+  // conv rows and 1 extra edge row)
+  int sseg = H;
+  const int64_t strips = (int64_t)B * a.nstrips;
+  while (sseg > 32 && strips * ((H + sseg - 1) / sseg) < 1024) sseg = (sseg + 1) / 2;
+  a.sseg = sseg;
+  a.nsegs = (H + sseg - 1) / sseg;
+  const uint64_t nblk = (uint64_t)strips * a.nsegs;
+  GRR_REQUIRE(nblk < (1ull << 31), GRR_ERR_UNSUPPORTED, "grr_feature_edges: grid too large");
+  a.nblk = (uint32_t)nblk;
+  if (x_blocked)
+    hipLaunchKernelGGL(feat_edge_kernel<true>, dim3(a.nblk), dim3(FE_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL(feat_edge_kernel<false>, dim3(a.nblk), dim3(FE_THREADS), 0, s, a);
+  return launch_status("grr_feature_edges");
+}
+
+}  // extern "C"

@@ -72,35 +72,40 @@ def records_grad(module: nn.Module, *tensors) -> bool:
 
 
 # Chains of fused LocalNonLinearBlocks hand their intermediate tensors on in the channel-blocked layout
-# (kernels.lnb_forward_c8: bitwise equal, fewer and wider memory instructions in each block).  Eager
-# inference only; compiled graphs and training keep [B, C, H, W].
+# (kernels.lnb_forward_c8: bitwise equal, fewer and wider memory instructions in each block).  Inference
+# (eager and compiled: the irdu::lnb_forward_c8 op); training keeps [B, C, H, W].
 BLOCKED_CHAINS = True
+# The image filter's last feature 1x1 conv + the level's edge weights as one pass (kernels.feature_edges; v13
+# feature CNN, F = 3, G <= 32, inference, eager and compiled).  Off: the two-pass path (conv1x1,
+# edge_weights_block).
+FUSED_FEATURE_EDGES = True
 
 
-def run_blocks(blocks, x, first=None):
+def run_blocks(blocks, x, first=None, out_blocked: bool = False):
     """x through the LocalNonLinearBlocks `blocks` in order; `first`, when given, replaces the first block's
     call (x -> its output, [B, C, H, W]).  Inference chains of fused blocks pass the blocked layout between
-    the blocks; the result is [B, C, H, W] either way."""
+    the blocks.  Returns the output in [B, C, H, W]; with out_blocked, (output, is_blocked) where the last
+    block may leave it blocked (for feature_edges)."""
     blocks = list(blocks)
     out = first(x) if first is not None else None
     rest = blocks[1:] if first is not None else blocks
     if out is None:
         out, rest = x, blocks
     b, c, h, w = out.shape
-    chain = (BLOCKED_CHAINS and out.is_cuda and len(rest) >= 2
-             and not torch.compiler.is_compiling()
+    chain = (BLOCKED_CHAINS and out.is_cuda and len(rest) >= (1 if out_blocked else 2)
              and all(isinstance(k, LocalNonLinearBlock) and k._blockable(h, w) and k.dim == c for k in rest)
              and not any(records_grad(k, out) for k in rest))
     if not chain:
         for k in rest:
             out = k(out)
-        return out
+        return (out, False) if out_blocked else out
     blocked = False
     for i, k in enumerate(rest):
         last = i == len(rest) - 1
-        out = k._forward_c8(out, blocked, not last)
-        blocked = not last
-    return out
+        keep = not last or out_blocked
+        out = k._forward_c8(out, blocked, keep)
+        blocked = keep
+    return (out, blocked) if out_blocked else out
 
 
 def hip_forward(fn):
@@ -321,7 +326,7 @@ class LocalNonLinearBlock(HipModule):
         """Inference forward with x / out in the channel-blocked layout (kernels.lnb_forward_c8)."""
         ll = self.local_linear
         c, hid = self.dim, self.hidden_dim
-        return K.lnb_forward_c8(x, c, self.norm.weighted_transform.weight.view(c),
+        return OPS.lnb_forward_c8(x, c, self.norm.weighted_transform.weight.view(c),
                                 ll.channels_linear_op.weight.view(2 * hid, c),
                                 ll.channels_local_linear_op.weight.view(2 * hid, 9),
                                 ll.project_out.weight.view(c, hid), self.skip_weight, in_c8, out_c8)
@@ -395,9 +400,11 @@ class MixtureGTVGLR(HipModule):
             return OPS.conv2x2s2(y, weight)
         return OPS.conv2x2s2(src, weight, fold=True)
 
-    def features(self, y: torch.Tensor, src: Optional[torch.Tensor] = None, half_tail=None):
+    def features(self, y: torch.Tensor, src: Optional[torch.Tensor] = None, half_tail=None, project: bool = True):
         """f0, f1 (a13).  half_tail(f1), when given, runs right after the half-resolution branch on
-        the same stream and its tuple of tensors is returned in place of f1."""
+        the same stream and its tuple of tensors is returned in place of f1.  project=False (v13, inference):
+        each branch stops before its last 1x1 conv and yields (x, is_blocked), the last block's output for
+        feature_edges."""
         s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
         if self.feature_extractor == "v1":
             f0 = OPS.conv1x1(y, s0[0].weight)
@@ -406,8 +413,10 @@ class MixtureGTVGLR(HipModule):
         ref = y if y is not None else src
 
         def half():
-            f1 = run_blocks(list(s1)[1:4], self._down(y, s1[0].weight, src))
-            f1 = OPS.conv1x1(f1, s1[4].weight)
+            if project:
+                f1 = OPS.conv1x1(run_blocks(list(s1)[1:4], self._down(y, s1[0].weight, src)), s1[4].weight)
+            else:
+                f1 = run_blocks(list(s1)[1:4], self._down(y, s1[0].weight, src), out_blocked=True)
             return half_tail(f1) if half_tail is not None else f1
 
         side = None
@@ -422,12 +431,16 @@ class MixtureGTVGLR(HipModule):
             f1 = half()
         blocks = list(s0)[:3]
         # the first block's input replicates src over the graphs: its GEMM1 runs on src (K = F)
-        f0 = run_blocks(blocks, y, first=(lambda _y: blocks[0].forward_replicated(src, _y)) if src is not None else None)
-        f0 = OPS.conv1x1(f0, s0[3].weight)
+        first = (lambda _y: blocks[0].forward_replicated(src, _y)) if src is not None else None
+        if project:
+            f0 = OPS.conv1x1(run_blocks(blocks, y, first=first), s0[3].weight)
+        else:
+            f0 = run_blocks(blocks, y, first=first, out_blocked=True)
         if side is not None:
             main.wait_stream(side)
             for t in (f1 if isinstance(f1, tuple) else (f1,)):
-                t.record_stream(main)
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(main)
         return f0, f1
 
     def features_train(self, y: torch.Tensor):
@@ -491,14 +504,25 @@ class MixtureGTVGLR(HipModule):
             raise ValueError("MixtureGTVGLR: src must be [B, F, H, W]")
         G0, L0, G1, L1 = self.GTVmodule00, self.GLRmodule00, self.GTVmodule01, self.GLRmodule01
 
+        # the last 1x1 conv of each feature branch and the level's edge weights in one pass (v13, eager)
+        fuse = (FUSED_FEATURE_EDGES and self.feature_extractor == "v13" and ref.is_cuda
+                and K.feature_edges_ok(g * f, g, f, h, w) and K.feature_edges_ok(g * f, g, f, h // 2, w // 2))
+        s0, s1 = self.patchs_features_extraction00, self.patchs_features_extraction01
+
         def half_tail(f1):
             # the half level's edge weights and its part of rhs A (ro1 G1 D y, REF:738-749)
-            wG1, cG1, wL1 = OPS.edge_weights_block(f1, g, f, G1.multiM, L1.multiM)
+            if fuse:
+                wG1, cG1, wL1 = OPS.feature_edges(f1[0], f1[1], s1[4].weight, g, f, G1.multiM, L1.multiM)
+            else:
+                wG1, cG1, wL1 = OPS.edge_weights_block(f1, g, f, G1.multiM, L1.multiM)
             yd = OPS.pool2(y) if src is None else OPS.repeat_graphs(OPS.pool2(src), g)   # D y
             return wG1, cG1, wL1, OPS.gtv_rhs_half(yd, cG1, G1, False, None, g)
 
-        f0, (wG1, cG1, wL1, t) = self.features(y, src, half_tail)
-        wG0, cG0, wL0 = OPS.edge_weights_block(f0, g, f, G0.multiM, L0.multiM)
+        f0, (wG1, cG1, wL1, t) = self.features(y, src, half_tail, project=not fuse)
+        if fuse:
+            wG0, cG0, wL0 = OPS.feature_edges(f0[0], f0[1], s0[3].weight, g, f, G0.multiM, L0.multiM)
+        else:
+            wG0, cG0, wL0 = OPS.edge_weights_block(f0, g, f, G0.multiM, L0.multiM)
         del f0
         mu0, mu1, ro0, ro1 = self.muys00, self.muys01, self.ro00, self.ro01
         alpha, beta = self.alphaCGD, self.betaCGD

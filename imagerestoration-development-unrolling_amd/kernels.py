@@ -199,6 +199,39 @@ def edge_weights_block(feat: Tensor, n_graphs: int, n_fts: int, multiM_gtv: Tens
     return wG, cG, wL
 
 
+def feature_edges_ok(c: int, n_graphs: int, n_fts: int, h: int, w: int) -> bool:
+    """Where feature_edges applies: grr_feature_edges_supported's conditions (F = 3, G <= 32, C = G F) in plain
+    Python (traceable; tests/test_abi.py checks the two agree)."""
+    return (n_fts == 3 and 1 <= n_graphs <= 32 and c == n_graphs * n_fts and c <= 96 and h >= 1 and w >= 1
+            and n_graphs * 4 * h * w * 4 < (1 << 31) and ((c + 7) // 8) * 8 * h * w * 4 < (1 << 31))
+
+
+def feature_edges(x: Tensor, x_blocked: bool, weight: Tensor, n_graphs: int, n_fts: int, multiM_gtv: Tensor,
+                  multiM_glr: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """edge_weights_block(conv1x1(x, weight), ...) in one pass (grr_feature_edges): the [B, 2C, H, W]
+    features stay on chip.  x: [B, C, H, W], or the channel-blocked layout (x_blocked, lnb_forward_c8's).
+    Returns (wG raw [B,G,4,H,W], cG pair [B,G,2,H,W], wL [B,G,4,H,W])."""
+    dev = _check("feature_edges", x, weight, multiM_gtv, multiM_glr)
+    if x_blocked:
+        b, _, h, w, _ = x.shape
+        c = n_graphs * n_fts
+    else:
+        b, c, h, w = x.shape
+    if tuple(weight.shape[:2]) != (2 * n_graphs * n_fts, c):
+        raise ValueError(f"feature_edges: weight {tuple(weight.shape)} for {c} -> {2 * n_graphs * n_fts} channels")
+    wG = torch.empty((b, n_graphs, 4, h, w), dtype=torch.float32, device=dev)
+    wL = torch.empty_like(wG)
+    cG = torch.empty((b, n_graphs, 2, h, w), dtype=torch.float32, device=dev)
+    lib = _native.load()
+    ws = torch.empty((lib.grr_feature_edges_workspace_bytes(n_graphs) + 3) // 4, dtype=torch.float32, device=dev)
+    nbytes = 4 * b * h * w * (c + 10 * n_graphs)   # x in; wG, wL, cG out
+    _launch("feature_edges", nbytes, "grr_feature_edges", x.contiguous().data_ptr(), int(x_blocked),
+            weight.contiguous().data_ptr(), multiM_gtv.contiguous().data_ptr(), multiM_glr.contiguous().data_ptr(),
+            wG.data_ptr(), cG.data_ptr(), wL.data_ptr(), ws.data_ptr(), b, c, n_graphs, n_fts, h, w, _stream(dev),
+            flops=2 * b * h * w * c * 2 * c)
+    return wG, cG, wL
+
+
 def gtv_pair_weights(w: Tensor) -> Tensor:
     dev = _check("gtv_pair_weights", w)
     b, g, four, h, ww = w.shape
@@ -714,9 +747,22 @@ def from_c8(y: Tensor, c: int) -> Tensor:
     return x
 
 
+# Python mirror of grr_lnb_set_fused (set_lnb_fused keeps both): the layout decisions below are plain Python so
+# that Dynamo traces them (a ctypes query would break the graph); a stale mirror fails loudly in the C entry
+# point (GRR_ERR_UNSUPPORTED), never silently
+LNB_FUSED = True
+
+
+def set_lnb_fused(enable: bool) -> None:
+    """C <= 96 blocks as one fused pass (default) or on the head + mix kernels (grr_lnb_set_fused)."""
+    global LNB_FUSED
+    _native.call("grr_lnb_set_fused", int(bool(enable)))
+    LNB_FUSED = bool(enable)
+
+
 def lnb_c8_ok(c: int, hid: int, h: int, w: int) -> bool:
-    """Where lnb_forward_c8 applies: the fused C <= 96 pass, one band."""
-    return bool(_native.load().grr_lnb_fused(c, hid)) and _lnb_band_rows(c, hid, h, w) >= h and \
+    """Where lnb_forward_c8 applies: the fused C <= 96 pass (grr_lnb_fused), one band."""
+    return LNB_FUSED and 2 <= c <= 96 and hid >= 1 and _lnb_band_rows(c, hid, h, w) >= h and \
         ((c + 7) // 8) * 8 * h * w * 4 < (1 << 31)
 
 

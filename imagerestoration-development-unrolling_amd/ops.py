@@ -99,6 +99,33 @@ def _(src, x, ln_w, w1, wdw, w2, skip):
     return src.new_empty((src.shape[0], ln_w.numel(), src.shape[2], src.shape[3]))
 
 
+@custom_op(f"{NS}::lnb_forward_c8", mutates_args=())
+def lnb_forward_c8_op(x: Tensor, c: int, ln_w: Tensor, w1: Tensor, wdw: Tensor, w2: Tensor, skip: Tensor,
+                      in_c8: bool, out_c8: bool) -> Tensor:
+    return K.lnb_forward_c8(x.contiguous(), c, ln_w.contiguous(), w1.contiguous(), wdw.contiguous(), w2.contiguous(),
+                            skip.contiguous(), in_c8, out_c8)
+
+
+@lnb_forward_c8_op.register_fake
+def _(x, c, ln_w, w1, wdw, w2, skip, in_c8, out_c8):
+    b, h, w = (x.shape[0], x.shape[2], x.shape[3])
+    return x.new_empty(K.c8_shape(b, c, h, w) if out_c8 else (b, c, h, w))
+
+
+@custom_op(f"{NS}::feature_edges", mutates_args=())
+def feature_edges_op(x: Tensor, x_blocked: bool, weight: Tensor, n_graphs: int, n_fts: int, multiM_gtv: Tensor,
+                     multiM_glr: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    return K.feature_edges(x.contiguous(), x_blocked, weight.contiguous(), n_graphs, n_fts, multiM_gtv.contiguous(),
+                           multiM_glr.contiguous())
+
+
+@feature_edges_op.register_fake
+def _(x, x_blocked, weight, n_graphs, n_fts, multiM_gtv, multiM_glr):
+    b, h, w = (x.shape[0], x.shape[2], x.shape[3])
+    return (x.new_empty((b, n_graphs, 4, h, w)), x.new_empty((b, n_graphs, 2, h, w)),
+            x.new_empty((b, n_graphs, 4, h, w)))
+
+
 @custom_op(f"{NS}::repeat_graphs", mutates_args=())
 def repeat_graphs_op(img: Tensor, n_graphs: int) -> Tensor:
     return K.repeat_graphs(img.contiguous(), n_graphs)
@@ -402,6 +429,18 @@ def lnb_forward_rep(src, x, ln_w, w1, wdw, w2, skip):
     if _tracing():
         return torch.ops.irdu.lnb_forward_rep(src, x, ln_w, w1, wdw, w2, skip)
     return K.lnb_forward_rep(src, x, ln_w, w1, wdw, w2, skip)
+
+
+def lnb_forward_c8(x, c, ln_w, w1, wdw, w2, skip, in_c8, out_c8):
+    if _tracing():
+        return torch.ops.irdu.lnb_forward_c8(x, c, ln_w, w1, wdw, w2, skip, in_c8, out_c8)
+    return K.lnb_forward_c8(x, c, ln_w, w1, wdw, w2, skip, in_c8, out_c8)
+
+
+def feature_edges(x, x_blocked, weight, n_graphs, n_fts, multiM_gtv, multiM_glr):
+    if _tracing():
+        return torch.ops.irdu.feature_edges(x, x_blocked, weight, n_graphs, n_fts, multiM_gtv, multiM_glr)
+    return K.feature_edges(x, x_blocked, weight, n_graphs, n_fts, multiM_gtv, multiM_glr)
 
 
 def repeat_graphs(img, n_graphs):

@@ -333,6 +333,20 @@ grr_status grr_lnb_forward(const float* x, const float* ln_w, const float* w1, c
                            const float* w2, const float* skip, float* out, void* workspace,
                            int B, int C, int hid, int H, int W, void* stream);
 
+/* The feature CNN's last 1x1 conv and the edge weights of both graph modules of a level in one pass
+ * (REF:146-175, :556-612 -- REF13:887-926's patchs_features_extraction[-1] followed by extract_edge_weights
+ * for the GTV and the GLR module): feat = wf x (wf [2 G F, C]: rows 0 .. G F - 1 the GTV features, then
+ * the GLR features), then grr_edge_weights_block's outputs (wG, cG, wL) from feat -- without feat in memory.
+ * x is [B, C, H, W], or the channel-blocked layout of grr_lnb_forward_c8 when x_blocked.  F = 3, G <= 32,
+ * C = G F (grr_feature_edges_supported).  The conv runs as fp16 two-term splits of both operands (three
+ * products), fp32-class like the fused LocalNonLinearBlock's GEMMs, so the weights agree with the two-pass
+ * path to fp32-class rounding, not bitwise.  workspace: grr_feature_edges_workspace_bytes(G), 256-B aligned. */
+int grr_feature_edges_supported(int C, int G, int F, int H, int W);
+int64_t grr_feature_edges_workspace_bytes(int G);
+grr_status grr_feature_edges(const float* x, int x_blocked, const float* wf, const float* multiM_gtv,
+                             const float* multiM_glr, float* wG, float* cG, float* wL, void* workspace, int B,
+                             int C, int G, int F, int H, int W, void* stream);
+
 /* grr_lnb_forward with either side in the channel-blocked layout [B, ceil(C / 8), H, W, 8] (channel
  * 8 k + j of pixel p at ((b ceil(C / 8) + k) H W + p) 8 + j; pad channels 0): layout bit 0 -- x (read for
  * LN / W1 and the skip term) blocked, bit 1 -- out blocked.  Needs grr_lnb_fused(C, hid); x and out 16-B

@@ -7,7 +7,7 @@ mkdir -p exp
 H=/opt/rocm/bin/hipcc
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I include"
 S=imagerestoration-development-unrolling_amd/csrc
-SRCS="graph_ops feature_ops wgrad_ops lnb_ops graph_bwd lnb_bwd window_ops window_bwd subapi_ops subapi_bwd"
+SRCS="graph_ops feature_ops wgrad_ops lnb_ops graph_bwd lnb_bwd window_ops window_bwd subapi_ops subapi_bwd feature_edge"
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   objs=""

@@ -46,7 +46,7 @@ def main():
     K.set_kernel_variant(args.variant)
     K.set_term_rows(args.term_rows)
     from irdu_amd._native import call
-    call("grr_lnb_set_fused", args.lnb_fused)
+    K.set_lnb_fused(bool(args.lnb_fused))
     dev = torch.device("cuda", 0)
     b, g, f, h, w = args.batch, args.graphs, args.fts, args.size, args.width or args.size
     c = g * f

@@ -33,6 +33,19 @@ def test_library_loads_and_exports_every_header_symbol():
     assert lib.grr_lnb_fused_workspace_bytes(128, 256) == 0
 
 
+def test_python_mirrors_of_native_shape_queries():
+    """kernels.feature_edges_ok / lnb_c8_ok are plain Python (traceable by Dynamo); they must agree with the
+    library's own queries."""
+    from irdu_amd import _native
+    from irdu_amd import kernels as K
+    lib = _native.load()
+    for c, g, f, h, w in [(96, 32, 3, 256, 256), (96, 32, 3, 128, 128), (15, 5, 3, 9, 29), (96, 16, 6, 64, 64),
+                          (99, 33, 3, 8, 8), (48, 16, 3, 1, 1), (12, 4, 3, 8192, 8192), (6, 2, 3, 3, 5)]:
+        assert K.feature_edges_ok(c, g, f, h, w) == bool(lib.grr_feature_edges_supported(c, g, f, h, w)), (c, g, f)
+    for c, hid in [(96, 256), (97, 256), (2, 1), (1, 4), (64, 128)]:
+        assert K.lnb_c8_ok(c, hid, 64, 64) == bool(lib.grr_lnb_fused(c, hid)), (c, hid)
+
+
 def test_invalid_args_report_status_without_gpu():
     lib = _native.load()
     st = lib.grr_pool2(None, None, 1, 1, 4, 4, None)
