@@ -4,18 +4,23 @@
 // feature tensor and the edge-row kernel read it back: 768 + 768 B per pixel of HBM traffic between two
 // launches.  Here the features never leave the CU.
 //
-// Workgroup = (b, 29-column strip, row segment), 9 waves:
+// Workgroup = (b, 32-column strip, row segment), 9 waves:
 //  * wave 8 (loader) streams the strip's input rows (the LocalNonLinearBlock output x, [B, C, H, W] or the
 //    channel-blocked [B, C/8, H, W, 8] of grr_lnb_forward_c8) one row ahead, scales each pixel by a power of two
 //    (its largest |x| into [2^13, 2^14)), splits it into exact-sum fp16 hi / lo terms in the layout of the
-//    32x32x16 MFMA's B operand, and writes them into a 2-slot LDS ring;
+//    32x32x16 MFMA's B operand and writes them into a 2-slot LDS ring -- for the strip's 32 columns (main image)
+//    and for its halo columns x0 - 1, x0 + 32, x0 + 33 (halo image, lanes 0, 31, 30);
 //  * waves 0..7 each own 8 graphs of one slab (waves 0-3 the GTV features, 4-7 the GLR features; lane half kh
-//    holds graphs 8 t + 4 kh .. + 3): per row, the 1x1 conv of the strip's 32 columns (x0 - 1 .. x0 + 30) on
-//    v_mfma_f32_32x32x16_f16 (three products of the two-term splits, A = the wave's weight rows resident in
-//    registers, scaled by a power of two per (slab, graph)) leaves each lane the 12 features (4 graphs x 3) of
-//    its column; normalisation (F.normalize * multiM), the four neighbour similarities (left / right by DPP
-//    lane shifts, up / down from the previous rows' registers), the softmax and (GTV) the pair weights follow
-//    in registers, edge_row_kernel's expressions.  Lanes 0, 30 and 31 of a half are the strip's halo columns.
+//    holds graphs 8 t + 4 kh .. + 3): per row, the 1x1 conv of both images on v_mfma_f32_32x32x16_f16 (three
+//    products of the two-term splits; A = the wave's weight rows, staged in LDS, scaled by a power of two per
+//    (slab, graph)) leaves each lane the 12 features (4 graphs x 3) of its column; normalisation (F.normalize *
+//    multiM), the four neighbour similarities (left / right by DPP lane shifts, the strip-edge lanes from the
+//    halo features, which a small per-wave LDS ring keeps for three rows; up / down from the previous rows'
+//    registers), the softmax and (GTV) the pair weights follow in registers -- edge_row_kernel's expressions
+//    with hardware reciprocal / sqrt / exp2 in place of the IEEE division sequences and expf (<= 2 ulp; the
+//    conv's fp16 splits already make the weights fp32-class, not bitwise).
+// Strips are 32-column aligned so that every store fills whole 128-B lines: 29-column strips (halo inside the
+// window) wrote each line from two workgroups and ran 3.19 ms against 1.57 ms aligned (64 x 256^2).
 // The power-of-two scales need no undoing: F.normalize is exact under them (sqrt and division commute with a
 // power-of-two factor; the 1e-12 floor is scaled alike).
 #include <type_traits>
@@ -36,11 +41,17 @@ constexpr int FE_GH = 4;                 // graphs per lane half (12 of the 16 a
 constexpr int FE_TPS = 4;                // tiles (waves) per slab: G <= 32
 constexpr int FE_NT = 2 * FE_TPS;        // compute waves
 constexpr int FE_THREADS = 64 * (FE_NT + 1);
-// output columns per strip: window columns 1..29 (column 30 is computed too: its w_left is the pair weight
-// c_h of column 29; column 31's softmax reads past the window)
-constexpr int FE_OWN = 29;
-constexpr int FE_SLOT = FE_KS * 2 * 256 + 32;   // floats per ring slot: the B images (hi, lo per k-step) + ep
+constexpr int FE_OWN = 32;                      // output columns per strip (32-aligned: whole 128-B lines)
+constexpr int FE_IMG = FE_KS * 2 * 256;         // floats of one B image set (hi, lo per k-step)
+constexpr int FE_SLOT = 2 * FE_IMG + 64;        // ring slot: main + halo image sets, ep of their pixels
+constexpr int FE_AIMG = FE_KS * 2 * 256;        // floats of one tile's A images
+constexpr int FE_HR = 3, FE_HROW = 2 * 3 * 12;  // halo feature ring: rows, floats per row ([kh][L, R1, R2][12])
+constexpr int FE_LDS = FE_NT * FE_AIMG + 2 * FE_SLOT + FE_NT * FE_HR * FE_HROW;
+static_assert(FE_LDS * 4 <= 163840, "feature_edges LDS");
 constexpr uint32_t FE_OOB = 0x80000000u;
+#ifndef FE_DIAG
+#define FE_DIAG 0   // timing-only builds: 1 no stores, 2 no edge arithmetic, 4 no loads (loader), 8 no conv
+#endif
 
 struct FeArgs {
   const float* x;          // [B, C, H, W], or channel-blocked
@@ -117,7 +128,10 @@ __device__ __forceinline__ float fe_next(float v) {   // lane + 1
 
 template <bool IN8>
 __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
-  __shared__ __attribute__((aligned(16))) float ring[2 * FE_SLOT];
+  __shared__ __attribute__((aligned(16))) float lds[FE_LDS];
+  float* const aimg = lds;                         // [tile][k-step][term] A images
+  float* const ring = aimg + FE_NT * FE_AIMG;      // [slot]: main images, halo images, ep of their pixels
+  float* const hring = ring + 2 * FE_SLOT;         // [wave][row % 3][kh][L, R1, R2][12]: halo features
   const int lane = threadIdx.x & 63, kh = lane >> 5, n = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t unit = xcd_remap(blockIdx.x, a.nblk);
@@ -127,8 +141,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   const int b = unit / a.nsegs;
   const int H = a.H, W = a.W, G = a.G, C = a.C;
   const int HW = H * W;
-  const int x0 = strip * FE_OWN;   // first owned column; window column n = image column x0 - 1 + n
-  const int col = x0 - 1 + n;
+  const int x0 = strip * FE_OWN, col = x0 + n;     // the lane's column (main image)
   const int colc = clampi(col, 0, W - 1);
   const int r0 = seg * a.sseg, r1 = min(r0 + a.sseg, H);
   // a segment ending inside the image runs one more edge row (not stored) for its last row's c_v
@@ -138,68 +151,86 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   const int NI = rend - r0 + 3;
   const int NI3 = (NI + 2) / 3 * 3;
 
+  // the tiles' A images into LDS (every workgroup reads the same 96 KB: L2)
+  for (int i = threadIdx.x; i < FE_NT * FE_AIMG / 4; i += FE_THREADS)
+    reinterpret_cast<fe_u32x4*>(aimg)[i] = reinterpret_cast<const fe_u32x4*>(a.pack)[i];
+
   if (wave == FE_NT) {
-    // ---------------- loader
+    // ---------------- loader: the main and the halo pixels of a row, one row ahead
+    // halo image lanes: 0 = the left neighbour column x0 - 1, 31 = x0 + 32, 30 = x0 + 33 (the right neighbour
+    // and its right neighbour, for the pair weight of column x0 + 31); the other lanes repeat lane 0's pixel
+    const int hcol = clampi(n == 31 ? x0 + 32 : (n == 30 ? x0 + 33 : x0 - 1), 0, W - 1);
     const int cx = IN8 ? 8 * ((C + 7) / 8) : C;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.x + (int64_t)b * cx * HW), 0, (int)((int64_t)cx * HW * 4), 0x00020000);
-    float v[FE_KS][8];
+    float v[2][FE_KS][8];
     auto issue = [&](int k) {   // input row of iteration k
+      if (FE_DIAG & 4) return;
       const int gy = clampi(r0 - 1 + k, 0, H - 1);
       int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
       asm volatile("" : "+s"(hw4));
-      if constexpr (IN8) {
-        const uint32_t vo = (uint32_t)((kh * HW + gy * W + colc) * 32);
 #pragma unroll
-        for (int s = 0; s < FE_KS; ++s) {
-          const fe_u32x4 lo = __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, 16 * s * hw4, 0));
-          const fe_u32x4 hi = __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 16, 16 * s * hw4, 0));
+      for (int set = 0; set < 2; ++set) {
+        const int cc = set ? hcol : colc;
+        if constexpr (IN8) {
+          const uint32_t vo = (uint32_t)((kh * HW + gy * W + cc) * 32);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[s][j] = __uint_as_float(lo[j]);
-            v[s][4 + j] = __uint_as_float(hi[j]);
+          for (int s = 0; s < FE_KS; ++s) {
+            const fe_u32x4 lo =
+                __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, 16 * s * hw4, 0));
+            const fe_u32x4 hi =
+                __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 16, 16 * s * hw4, 0));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[set][s][j] = __uint_as_float(lo[j]);
+              v[set][s][4 + j] = __uint_as_float(hi[j]);
+            }
           }
+        } else {
+          const uint32_t vo = (uint32_t)((8 * kh * HW + gy * W + cc) * 4);
+#pragma unroll
+          for (int s = 0; s < FE_KS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              v[set][s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
         }
-      } else {
-        const uint32_t vo = (uint32_t)((8 * kh * HW + gy * W + colc) * 4);
-#pragma unroll
-        for (int s = 0; s < FE_KS; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
       }
     };
     auto put = [&](int sl) {   // the loaded row -> ring slot sl
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      float mx = 0.f;
-#pragma unroll
-      for (int s = 0; s < FE_KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[s][j]));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const int ep = fe_scale_exp(mx);
       float* slot = ring + sl * FE_SLOT;
 #pragma unroll
-      for (int s = 0; s < FE_KS; ++s) {
-        uint32_t hw[4], lw[4];
+      for (int set = 0; set < 2; ++set) {
+        float mx = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const fe_f32x2 p = fe_f32x2{ldexpf(v[s][2 * j], ep), ldexpf(v[s][2 * j + 1], ep)};
-          const fe_f16x2 h = __builtin_convertvector(p, fe_f16x2);
-          const fe_f16x2 l = __builtin_convertvector(p - __builtin_convertvector(h, fe_f32x2), fe_f16x2);
-          hw[j] = __builtin_bit_cast(uint32_t, h);
-          lw[j] = __builtin_bit_cast(uint32_t, l);
+        for (int s = 0; s < FE_KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[set][s][j]));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const int ep = fe_scale_exp(mx);
+        float* img = slot + set * FE_IMG;
+#pragma unroll
+        for (int s = 0; s < FE_KS; ++s) {
+          uint32_t hw[4], lw[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const fe_f32x2 p = fe_f32x2{ldexpf(v[set][s][2 * j], ep), ldexpf(v[set][s][2 * j + 1], ep)};
+            const fe_f16x2 h = __builtin_convertvector(p, fe_f16x2);
+            const fe_f16x2 l = __builtin_convertvector(p - __builtin_convertvector(h, fe_f32x2), fe_f16x2);
+            hw[j] = __builtin_bit_cast(uint32_t, h);
+            lw[j] = __builtin_bit_cast(uint32_t, l);
+          }
+          *reinterpret_cast<fe_u32x4*>(img + (2 * s) * 256 + 4 * lane) = fe_u32x4{hw[0], hw[1], hw[2], hw[3]};
+          *reinterpret_cast<fe_u32x4*>(img + (2 * s + 1) * 256 + 4 * lane) = fe_u32x4{lw[0], lw[1], lw[2], lw[3]};
         }
-        *reinterpret_cast<fe_u32x4*>(slot + (2 * s) * 256 + 4 * lane) = fe_u32x4{hw[0], hw[1], hw[2], hw[3]};
-        *reinterpret_cast<fe_u32x4*>(slot + (2 * s + 1) * 256 + 4 * lane) = fe_u32x4{lw[0], lw[1], lw[2], lw[3]};
+        if (kh == 0) reinterpret_cast<int*>(slot + 2 * FE_IMG)[set * 32 + n] = ep;
       }
-      if (kh == 0) reinterpret_cast<int*>(slot + FE_KS * 2 * 256)[n] = ep;
     };
     issue(0);
     put(0);
     issue(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();   // A images and slot 0
     asm volatile("" ::: "memory");
     for (int k = 0; k < NI3; ++k) {
       if (k + 1 <= NI - 2) {   // uniform: iterations 0 .. NI - 2 run a conv
@@ -218,17 +249,9 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   const int slab = wave >> 2, t4 = wave & 3;
   const int gbase = 8 * t4 + 4 * kh;                 // the lane half's first graph
   if (8 * t4 >= G) {                                 // no graph in this tile: the barriers only
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     for (int k = 0; k <= NI3; ++k) __builtin_amdgcn_s_barrier();
     return;
-  }
-  fe_f16x8 ah[FE_KS], al[FE_KS];
-  {
-    const char* pk = a.pack + (int64_t)wave * FE_KS * 2 * 1024 + lane * 16;
-#pragma unroll
-    for (int s = 0; s < FE_KS; ++s) {
-      ah[s] = *reinterpret_cast<const fe_f16x8*>(pk + (2 * s) * 1024);
-      al[s] = *reinterpret_cast<const fe_f16x8*>(pk + (2 * s + 1) * 1024);
-    }
   }
   float M[FE_GH][3];
   int sg[FE_GH];
@@ -244,38 +267,64 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
       slab == 0 ? a.c + (int64_t)b * G * 2 * HW : nullptr, 0, slab == 0 ? (int)((int64_t)G * 2 * HW * 4) : 0,
       0x00020000);
-  // the lane stores its column (window columns 1..30 inside the image), graphs of its half only
-  const bool lane_out = n >= 1 && n <= FE_OWN && col < W;
+  const bool lane_out = col < W;
+  const float* const at = aimg + wave * FE_AIMG + 4 * lane;
+  float* const hw_wave = hring + wave * FE_HR * FE_HROW;
   float fw[3][FE_GH][3];   // normalised features of three consecutive rows (rotating)
   float wdn_prev[FE_GH];
 #pragma unroll
   for (int gi = 0; gi < FE_GH; ++gi) wdn_prev[gi] = 0.f;
 
-  // normalise the conv of iteration k's row into fw[P]
-  auto normalise = [&](const fe_f32x16& acc, int ep, auto p_tag) __attribute__((always_inline)) {
-    constexpr int P = decltype(p_tag)::value;
+  // F.normalize * multiM of one pixel's 4 x 3 features (REF:146-157): one hardware reciprocal per (pixel,
+  // graph) instead of three IEEE divisions (the IEEE sequence serialises on VCC); <= 1.5 ulp
+  auto norm4 = [&](const fe_f32x16& acc, int ep, float (&out)[FE_GH][3]) __attribute__((always_inline)) {
 #pragma unroll
     for (int gi = 0; gi < FE_GH; ++gi) {
       const float f0 = acc[3 * gi], f1 = acc[3 * gi + 1], f2 = acc[3 * gi + 2];
       float ss = __builtin_fmaf(f0, f0, 0.f);
       ss = __builtin_fmaf(f1, f1, ss);
       ss = __builtin_fmaf(f2, f2, ss);
-      const float den = fmaxf(sqrtf(ss), ldexpf(1e-12f, ep + sg[gi]));   // the scaled 1e-12 floor
-      fw[P][gi][0] = (f0 / den) * M[gi][0];
-      fw[P][gi][1] = (f1 / den) * M[gi][1];
-      fw[P][gi][2] = (f2 / den) * M[gi][2];
+      const float den = fmaxf(__builtin_amdgcn_sqrtf(ss), ldexpf(1e-12f, ep + sg[gi]));   // the scaled 1e-12 floor
+      const float inv = __builtin_amdgcn_rcpf(den);
+      out[gi][0] = (f0 * inv) * M[gi][0];
+      out[gi][1] = (f1 * inv) * M[gi][1];
+      out[gi][2] = (f2 * inv) * M[gi][2];
     }
   };
-  // edges of row ey from rows P (ey - 1), Q (ey), N (ey + 1); edge_row_kernel's arithmetic (V = 1)
+  // softmax of four similarities with v_exp_f32 (2^x of the log2(e)-scaled argument, <= 0) and one reciprocal
+  auto softmax4 = [&](float s0, float s1, float s2, float s3, float& w0, float& w1, float& w2, float& w3)
+      __attribute__((always_inline)) {
+    constexpr float L2E = 1.4426950408889634f;
+    const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
+    const float e0 = __builtin_amdgcn_exp2f((s0 - m) * L2E), e1 = __builtin_amdgcn_exp2f((s1 - m) * L2E);
+    const float e2 = __builtin_amdgcn_exp2f((s2 - m) * L2E), e3 = __builtin_amdgcn_exp2f((s3 - m) * L2E);
+    const float sum = ((e0 + e1) + e2) + e3;
+    const float rs = __builtin_amdgcn_rcpf(sum);
+    w0 = e0 * rs;
+    w1 = e1 * rs;
+    w2 = e2 * rs;
+    w3 = e3 * rs;
+  };
+  // edges of row ey from the main rows P (ey - 1), Q (ey), N (ey + 1) and the halo ring rows of the same slots
   auto edges = [&](int ey, auto p_tag, auto q_tag, auto n_tag) __attribute__((always_inline)) {
     constexpr int P = decltype(p_tag)::value, Q = decltype(q_tag)::value, N = decltype(n_tag)::value;
-    const bool own = ey < r1;
+    const bool own = ey < r1 && !(FE_DIAG & 1);
     const uint32_t row_off = (uint32_t)(ey * W + col);
     const uint32_t vo = lane_out && own ? (row_off + 16u * kh * HW) * 4u : FE_OOB;
     const uint32_t voc = lane_out && own ? (row_off + 8u * kh * HW) * 4u : FE_OOB;
-    const uint32_t vcv = lane_out && ey > r0 ? (row_off - W + 8u * kh * HW) * 4u : FE_OOB;   // row ey - 1
+    const uint32_t vcv = lane_out && ey > r0 && !(FE_DIAG & 1) ? (row_off - W + 8u * kh * HW) * 4u : FE_OOB;   // row ey - 1
     int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
     asm volatile("" : "+s"(hw4));
+    // the lane's neighbour across the strip edge, row ey: lane 0 the left pixel L, lane 31 the right R1
+    const float* hq = hw_wave + Q * FE_HROW + kh * 36;
+    float hb[FE_GH][3];
+    {
+      const float* src = hq + (n == 31 ? 12 : 0);
+#pragma unroll
+      for (int gi = 0; gi < FE_GH; ++gi)
+#pragma unroll
+        for (int f = 0; f < 3; ++f) hb[gi][f] = src[3 * gi + f];
+    }
 #pragma unroll
     for (int gi = 0; gi < FE_GH; ++gi) {
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -283,17 +332,15 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       for (int f = 0; f < 3; ++f) {
         const float v = fw[Q][gi][f];
         const float pl = fe_prev(v), pr = fe_next(v);
-        const float lv = col > 0 ? pl : v;
-        const float rv = col < W - 1 ? pr : v;
+        const float lv = col > 0 ? (n == 0 ? hb[gi][f] : pl) : v;
+        const float rv = col < W - 1 ? (n == 31 ? hb[gi][f] : pr) : v;
         s0 += v * fw[P][gi][f];
         s1 += v * lv;
         s2 += v * rv;
         s3 += v * fw[N][gi][f];
       }
-      const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
-      const float e0 = expf(s0 - m), e1 = expf(s1 - m), e2 = expf(s2 - m), e3 = expf(s3 - m);
-      const float sum = ((e0 + e1) + e2) + e3;
-      const float w0 = e0 / sum, w1 = e1 / sum, w2 = e2 / sum, w3 = e3 / sum;
+      float w0, w1, w2, w3;
+      softmax4(s0, s1, s2, s3, w0, w1, w2, w3);
       const bool gok = gbase + gi < G;
       const uint32_t so = (uint32_t)((8 * t4 + gi) * 4) * hw4;
       const uint32_t vg = gok ? vo : FE_OOB;
@@ -302,7 +349,29 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w2), wr, vg, so + 2 * hw4, 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w3), wr, vg, so + 3 * hw4, 0);
       if (slab == 0) {   // wave-uniform: pair weights (REF:452-516's C^T C as pair weights)
-        const float wln = fe_next(w1);   // w_left(p + right)
+        // w_left(p + right): lane n + 1's w1; for lane 31 the softmax of R1 = x0 + 32 from the halo rows (R1's
+        // up / down rows, R2 = x0 + 33 to its right, this lane's column to its left)
+        float w1r;
+        {
+          const float* hp = hw_wave + P * FE_HROW + kh * 36 + 12 + 3 * gi;   // R1, row ey - 1
+          const float* hn = hw_wave + N * FE_HROW + kh * 36 + 12 + 3 * gi;   // R1, row ey + 1
+          const float* hr = hq + 24 + 3 * gi;                                // R2, row ey
+          const int cr = x0 + 32;
+          float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+#pragma unroll
+          for (int f = 0; f < 3; ++f) {
+            const float v = hb[gi][f];   // R1 (lane 31's hb)
+            const float rv = cr < W - 1 ? hr[f] : v;
+            t0 += v * hp[f];
+            t1 += v * fw[Q][gi][f];
+            t2 += v * rv;
+            t3 += v * hn[f];
+          }
+          float u0, u2, u3;
+          softmax4(t0, t1, t2, t3, u0, w1r, u2, u3);
+        }
+        const float w1n = fe_next(w1);   // (outside the select: a DPP read in a branch sees inactive lanes as 0)
+        const float wln = n == 31 ? w1r : w1n;
         const float ch = col + 1 < W ? w2 * w2 + wln * wln : 0.f;
         const float cv = wdn_prev[gi] * wdn_prev[gi] + w0 * w0;   // row ey - 1: w_down(p)^2 + w_up(p + down)^2
         wdn_prev[gi] = w3;
@@ -313,11 +382,11 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     }
   };
 
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();   // ring slot 0 holds row r0 - 1
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // A images and ring slot 0 (row r0 - 1)
   asm volatile("" ::: "memory");
-  // phase PH = k mod 3: the row of iteration k goes to fw[PH]; the edge row's rows are fw[PH] (= k - 3),
-  // fw[(PH + 1) % 3] (k - 2), fw[(PH + 2) % 3] (k - 1)
+  // phase PH = k mod 3: the row of iteration k goes to fw[PH] (and halo ring row PH); the edge row's rows are
+  // slot PH (= k - 3), (PH + 1) % 3 (k - 2), (PH + 2) % 3 (k - 1)
   auto iteration = [&](int k, auto ph_tag) __attribute__((always_inline)) {
     constexpr int PH = decltype(ph_tag)::value;
     using IP = std::integral_constant<int, PH>;
@@ -325,22 +394,42 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     using IN = std::integral_constant<int, (PH + 2) % 3>;
     if (k < NI) {   // uniform
       const bool conv = k <= NI - 2;
-      fe_f32x16 acc = fe_f32x16{};
-      int ep = 0;
-      if (conv) {
-        const float* slot = ring + (k & 1) * FE_SLOT;
+      fe_f32x16 am = fe_f32x16{}, ax = fe_f32x16{};
+      int epm = 0, eph = 0;
+      if (conv && !(FE_DIAG & 8)) {
+        const float* slot = ring + (k & 1) * FE_SLOT + 4 * lane;
 #pragma unroll
         for (int s = 0; s < FE_KS; ++s) {
-          const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256 + 4 * lane);
-          const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256 + 4 * lane);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc, 0, 0, 0);
+          const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
+          const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
+          const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
+          const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
+          const fe_f16x8 ch = *reinterpret_cast<const fe_f16x8*>(slot + FE_IMG + (2 * s) * 256);
+          const fe_f16x8 cl = *reinterpret_cast<const fe_f16x8*>(slot + FE_IMG + (2 * s + 1) * 256);
+          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
+          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, ax, 0, 0, 0);
+          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
+          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, ax, 0, 0, 0);
+          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
+          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, ax, 0, 0, 0);
         }
-        ep = reinterpret_cast<const int*>(slot + FE_KS * 2 * 256)[n];
+        const int* eps = reinterpret_cast<const int*>(ring + (k & 1) * FE_SLOT + 2 * FE_IMG);
+        epm = eps[n];
+        eph = eps[32 + n];
       }
-      if (k >= 3) edges(r0 - 3 + k, IP{}, IQ{}, IN{});   // rows k - 3, k - 2, k - 1
-      if (conv) normalise(acc, ep, IP{});                // row k replaces row k - 3
+      if (k >= 3 && !(FE_DIAG & 2)) edges(r0 - 3 + k, IP{}, IQ{}, IN{});   // rows k - 3, k - 2, k - 1
+      if (conv) {                                                            // row k replaces row k - 3
+        norm4(am, epm, fw[PH]);
+        float hf[FE_GH][3];
+        norm4(ax, eph, hf);
+        if (n == 0 || n >= 30) {   // the halo ring row: L (lane 0), R1 (lane 31), R2 (lane 30)
+          float* dst = hw_wave + PH * FE_HROW + kh * 36 + (n == 0 ? 0 : (n == 31 ? 12 : 24));
+#pragma unroll
+          for (int gi = 0; gi < FE_GH; ++gi)
+#pragma unroll
+            for (int f = 0; f < 3; ++f) dst[3 * gi + f] = hf[gi][f];
+        }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

@@ -95,6 +95,15 @@ def main():
                p(ll.channels_local_linear_op.weight).view(2 * hid, 9), p(ll.project_out.weight).view(c, hid),
                p(blk.skip_weight))
         fn = lambda: K.lnb_forward_rep(src, None, *wts)  # noqa: E731
+    elif args.kernel in ("feature_edges", "feature_edges_c8", "conv_edges"):   # a level's features -> edge weights
+        wt = torch.rand(2 * c, c, 1, 1, device=dev) * 0.2
+        mG, mL = torch.rand(g, f, device=dev) + 0.5, torch.rand(g, f, device=dev) + 0.5
+        if args.kernel == "conv_edges":   # the two-pass path
+            fn = lambda: K.edge_weights_block(K.conv1x1(x, wt), g, f, mG, mL)  # noqa: E731
+        else:
+            blocked = args.kernel.endswith("c8")
+            xin = K.to_c8(x) if blocked else x
+            fn = lambda: K.feature_edges(xin, blocked, wt, g, f, mG, mL)  # noqa: E731
     elif args.kernel == "conv1x1":
         wt = torch.rand(2 * c, c, 1, 1, device=dev)
         fn = lambda: K.conv1x1(x, wt)  # noqa: E731
