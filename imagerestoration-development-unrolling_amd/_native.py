@@ -87,6 +87,7 @@ SIGNATURES = {
     "grr_lnb_fused": [I, I],
     "grr_lnb_fused_workspace_bytes": [I, I],
     "grr_lnb_set_fused": [I],
+    "grr_dw3_ring_check": [I],
     "grr_repeat_graphs": [P, P, I, I, I, L, P],
     "grr_lnb_forward_rep": [P, I, I, P, P, P, P, P, P, P, P, I, I, I, I, P],
     # GLRFast / GTVFast sub-API

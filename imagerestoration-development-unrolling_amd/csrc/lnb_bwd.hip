@@ -782,6 +782,30 @@ __device__ __forceinline__ const float* uniform_ptr(const float* p) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
+// DMA geometry of a ring row (shared by the kernel and the host replay grr_dw3_ring_check): a ring row holds
+// RW = 64 V floats; one global_load_lds_dwordx4 moves 16 bytes per lane into consecutive LDS, so a row takes
+// NDMA instructions of LANES lanes, DMA d lane l writing row bytes [16 (d LANES + l), + 16) from image column
+// x0 + 4 (d LANES + l), clamped into [0, W - 4].  The invariants (static_assert below, replayed on the host
+// over every strip of a launch): every DMA byte lands inside its ring row, every source lies inside its image
+// row.  Round 5's fault (r05v8: hipErrorIllegalAddress in test_gate_dw3_rows_vs_autograd[b2hid3h9w32-lnb], the
+// V = 1 instance, right after a change that let the issue path run two DMAs per ring row for an 8-column
+// lane) is the violation of both at V < 4: one 1-KB DMA already covers 4 V rows' worth of lanes' data at V = 1,
+// so a second DMA per row (or all 64 lanes in the first) writes past the 256-B ring row into the next slot --
+// for the last wave's last slot past the workgroup's LDS -- and reads 1 KB past the image row, off the end of
+// the tensor at its last row (the test's 9 x 32 planes end 1 KB before the next page boundary only by chance).
+// The faulting diff was not kept; this reconstruction rests on the arithmetic above, which the replay checks.
+template <int V>
+struct Dw3RingGeom {
+  static constexpr int RW = 64 * V;
+  static constexpr int NDMA = (RW * 4 + 1023) / 1024;
+  static constexpr int LANES = RW / 4 / NDMA;
+  static_assert(NDMA * LANES * 16 == RW * 4 && LANES <= 64, "ring row DMAs must tile the row exactly");
+};
+__host__ __device__ inline int dw3_ring_src_col(int x0, int dl, int W) {   // dl = d LANES + l
+  const int c = x0 + 4 * dl;
+  return c < W - 4 ? c : W - 4;
+}
+
 template <int V>
 __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
     const float* __restrict__ gq, const float* __restrict__ scale, const float* __restrict__ hh,
@@ -798,10 +822,12 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
   const float* const gq0 = gq + (int64_t)q.plane * HW;   // plane bases (wave-uniform; SGPRs at the DMA)
   const float* const hm0 = hh + pm0;
   const float* const hv0 = hh + pv0;
-  // the lane's 16-byte chunk of a row (16 V lanes per row; W % 4 == 0): the strip's columns x0 + 4 lane
+  // the lane's 16-byte chunk of a row (Dw3RingGeom; W % 4 == 0): the strip's columns x0 + 4 lane
+  typedef Dw3RingGeom<V> RG;
+  static_assert(RG::RW == RW && RG::NDMA == 1, "the ring kernel's issue path moves one DMA per ring row");
   const int x0 = q.c0 - V * q.lane;
-  const uint32_t voff = (uint32_t)min(x0 + 4 * q.lane, W - 4) * 4u;
-  const bool dma_lane = q.lane < 16 * V;
+  const uint32_t voff = (uint32_t)dw3_ring_src_col(x0, q.lane, W) * 4u;
+  const bool dma_lane = q.lane < RG::LANES;
   auto issue = [&](int r, int sl) {   // rows of iteration r: gq row r + 1, hh rows r + 2
     if (dma_lane) {
       float* dst = ring + sl * (3 * RW);
@@ -962,6 +988,27 @@ int dw3_row_seg(int H, int64_t planes) {
   while (sseg > 32 && planes * ((H + sseg - 1) / sseg) < 4096) sseg = (sseg + 1) / 2;
   return sseg;
 }
+// Host replay of the ring kernel's DMA geometry for a launch shape (Dw3RingGeom, dw3_row_geom's strips):
+// 0 when every DMA of every strip lands inside its ring row and reads inside its image row, else the first
+// violation as GRR_ERR_SHAPE.  Cheap integer arithmetic; tests/test_abi.py runs it over the test shapes.
+template <int V>
+static grr_status dw3_ring_replay(int W) {
+  typedef Dw3RingGeom<V> RG;
+  const int nstrips = dw3_row_strips(W, V), step = 62 * V;
+  for (int strip = 0; strip < nstrips; ++strip) {
+    const int x0 = strip == 0 ? 0 : strip * step - V;
+    for (int d = 0; d < RG::NDMA; ++d)
+      for (int l = 0; l < RG::LANES; ++l) {
+        const int dl = d * RG::LANES + l, lds_end = 16 * (dl + 1), c = dw3_ring_src_col(x0, dl, W);
+        GRR_REQUIRE(lds_end <= RG::RW * 4, GRR_ERR_SHAPE, "dw3 ring: V=%d W=%d strip %d DMA %d lane %d writes byte %d of a %d-byte ring row",
+                    V, W, strip, d, l, lds_end, RG::RW * 4);
+        GRR_REQUIRE(c >= 0 && c + 4 <= W, GRR_ERR_SHAPE, "dw3 ring: V=%d W=%d strip %d DMA %d lane %d reads columns %d..%d",
+                    V, W, strip, d, l, c, c + 3);
+      }
+  }
+  return GRR_OK;
+}
+
 template <int V>
 grr_status launch_dw3_row(bool bwd, const float* g, const float* h, const float* wdw, float* out, float* gwd, int B,
                           int C, int H, int W, hipStream_t s, const char* what) {
@@ -1177,6 +1224,17 @@ grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int 
     default: launch_dw3_gate_fwd_row<4>(hh, wdw, gate, B, hid, H, W, s); break;
   }
   return launch_status("grr_lnb_dw3_gate");
+}
+
+grr_status grr_dw3_ring_check(int W) {
+  clear_error();
+  GRR_REQUIRE(W >= 4 && W % 4 == 0, GRR_ERR_INVALID_ARG, "grr_dw3_ring_check: the ring kernel needs W %% 4 == 0");
+  switch (grr::dw3_row_vec(W)) {
+    case 1: return grr::dw3_ring_replay<1>(W);
+    case 2: return grr::dw3_ring_replay<2>(W);
+    case 4: return grr::dw3_ring_replay<4>(W);
+    default: return GRR_ERR_UNSUPPORTED;
+  }
 }
 
 grr_status grr_lnb_set_bwd_ring(int enable) {

@@ -540,6 +540,11 @@ grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int 
  * with its operand rows through a per-wave LDS-DMA ring where W % 4 == 0 and the planes are 16-byte aligned,
  * 0 the register-prefetch row kernel.  Process-wide; results agree to fp32 rounding.  A/B and tests. */
 grr_status grr_lnb_set_bwd_ring(int enable);
+/* Host replay of the gate + depthwise reverse ring kernel's DMA geometry at image width W (W % 4 == 0): GRR_OK
+ * when every ring-row DMA of every column strip writes inside its ring row and reads inside its image row
+ * (the invariant whose violation faulted round 5's two-DMAs-per-row attempt), else GRR_ERR_SHAPE with the
+ * first violation in grr_last_error.  No device work. */
+grr_status grr_dw3_ring_check(int W);
 /* grr_lnb_gate_bwd_scaled and grr_dwconv3_bwd in one row pass (ghp stays on chip): hp [B,2hid,H,W]
  * (depthwise output; NULL = recomputed from hh in-kernel), gq [B,hid,H,W], hh [B,2hid,H,W]
  * (depthwise input), wdw [2hid,9] ->

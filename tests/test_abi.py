@@ -154,3 +154,14 @@ def test_wgrad_tile_plan_without_gpu():
         lib.grr_wgrad_set_tiles(1)
     assert tiled_small > base_small > 0
     assert tiled_wide == base_wide > 0
+
+
+def test_dw3_ring_dma_geometry_replay():
+    """The gate + depthwise reverse ring kernel's DMAs stay inside their ring row and image row at every width
+    it takes (W % 4 == 0), including round 5's faulting case W = 32 (V = 1) and the C4 width 512 (strips)."""
+    from irdu_amd import _native
+    lib = _native.load()
+    for w in list(range(4, 1028, 4)) + [32, 100, 256, 300, 512, 744]:
+        if w % 4 == 0:
+            assert lib.grr_dw3_ring_check(w) == 0, (w, lib.grr_last_error())
+    assert lib.grr_dw3_ring_check(30) != 0          # W % 4 != 0 is not a ring shape
