@@ -43,10 +43,12 @@ constexpr int FE_NT = 2 * FE_TPS;        // compute waves
 constexpr int FE_THREADS = 64 * (FE_NT + 1);
 constexpr int FE_OWN = 32;                      // output columns per strip (32-aligned: whole 128-B lines)
 constexpr int FE_IMG = FE_KS * 2 * 256;         // floats of one B image set (hi, lo per k-step)
-constexpr int FE_SLOT = 2 * FE_IMG + 64;        // ring slot: main + halo image sets, ep of their pixels
+constexpr int FE_SLOT = FE_IMG + 32;            // image set + the ep of its 32 pixels
 constexpr int FE_AIMG = FE_KS * 2 * 256;        // floats of one tile's A images
-constexpr int FE_HR = 3, FE_HROW = 2 * 3 * 12;  // halo feature ring: rows, floats per row ([kh][L, R1, R2][12])
-constexpr int FE_LDS = FE_NT * FE_AIMG + 2 * FE_SLOT + FE_NT * FE_HR * FE_HROW;
+constexpr int FE_HB = 8;                        // conv rows per halo batch (3 halo pixels a row: 24 B columns)
+constexpr int FE_HR = FE_HB + 3, FE_HROW = 2 * 3 * 12;   // halo feature ring: rows, floats per row ([kh][L, R1, R2][12])
+// A images, 2 main ring slots, 1 halo batch slot, per-wave halo feature rings
+constexpr int FE_LDS = FE_NT * FE_AIMG + 3 * FE_SLOT + FE_NT * FE_HR * FE_HROW;
 static_assert(FE_LDS * 4 <= 163840, "feature_edges LDS");
 constexpr uint32_t FE_OOB = 0x80000000u;
 #ifndef FE_DIAG
@@ -130,8 +132,9 @@ template <bool IN8>
 __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[FE_LDS];
   float* const aimg = lds;                         // [tile][k-step][term] A images
-  float* const ring = aimg + FE_NT * FE_AIMG;      // [slot]: main images, halo images, ep of their pixels
-  float* const hring = ring + 2 * FE_SLOT;         // [wave][row % 3][kh][L, R1, R2][12]: halo features
+  float* const ring = aimg + FE_NT * FE_AIMG;      // [slot 0, 1]: main images + ep of their pixels
+  float* const himg = ring + 2 * FE_SLOT;          // the halo batch image + ep
+  float* const hring = himg + FE_SLOT;             // [wave][conv row % FE_HR][kh][L, R1, R2][12]: halo features
   const int lane = threadIdx.x & 63, kh = lane >> 5, n = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t unit = xcd_remap(blockIdx.x, a.nblk);
@@ -156,86 +159,86 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     reinterpret_cast<fe_u32x4*>(aimg)[i] = reinterpret_cast<const fe_u32x4*>(a.pack)[i];
 
   if (wave == FE_NT) {
-    // ---------------- loader: the main and the halo pixels of a row, one row ahead
-    // halo image lanes: 0 = the left neighbour column x0 - 1, 31 = x0 + 32, 30 = x0 + 33 (the right neighbour
-    // and its right neighbour, for the pair weight of column x0 + 31); the other lanes repeat lane 0's pixel
-    const int hcol = clampi(n == 31 ? x0 + 32 : (n == 30 ? x0 + 33 : x0 - 1), 0, W - 1);
+    // ---------------- loader: the main pixels of a row, one row ahead; the halo pixels of FE_HB rows at a time
+    // halo batch m = conv rows (iterations) FE_HB m .. + FE_HB - 1: lane n < 24 holds row FE_HB m + n / 3, column
+    // x0 - 1 (n % 3 = 0, the left neighbour L), x0 + 32 (1, the right neighbour R1), x0 + 33 (2, R1's right
+    // neighbour R2, for the pair weight of column x0 + 31); lanes 24..31 repeat lane 23's pixel
+    const int hn = min(n, 3 * FE_HB - 1);
+    const int hcol = clampi(hn % 3 == 0 ? x0 - 1 : (hn % 3 == 1 ? x0 + 32 : x0 + 33), 0, W - 1);
     const int cx = IN8 ? 8 * ((C + 7) / 8) : C;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.x + (int64_t)b * cx * HW), 0, (int)((int64_t)cx * HW * 4), 0x00020000);
     float v[2][FE_KS][8];
-    auto issue = [&](int k) {   // input row of iteration k
+    auto load = [&](int set, int gy, int cc) __attribute__((always_inline)) {
       if (FE_DIAG & 4) return;
-      const int gy = clampi(r0 - 1 + k, 0, H - 1);
       int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
       asm volatile("" : "+s"(hw4));
+      if constexpr (IN8) {
+        const uint32_t vo = (uint32_t)((kh * HW + gy * W + cc) * 32);
 #pragma unroll
-      for (int set = 0; set < 2; ++set) {
-        const int cc = set ? hcol : colc;
-        if constexpr (IN8) {
-          const uint32_t vo = (uint32_t)((kh * HW + gy * W + cc) * 32);
+        for (int s = 0; s < FE_KS; ++s) {
+          const fe_u32x4 lo =
+              __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, 16 * s * hw4, 0));
+          const fe_u32x4 hi =
+              __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 16, 16 * s * hw4, 0));
 #pragma unroll
-          for (int s = 0; s < FE_KS; ++s) {
-            const fe_u32x4 lo =
-                __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, 16 * s * hw4, 0));
-            const fe_u32x4 hi =
-                __builtin_bit_cast(fe_u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 16, 16 * s * hw4, 0));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              v[set][s][j] = __uint_as_float(lo[j]);
-              v[set][s][4 + j] = __uint_as_float(hi[j]);
-            }
+          for (int j = 0; j < 4; ++j) {
+            v[set][s][j] = __uint_as_float(lo[j]);
+            v[set][s][4 + j] = __uint_as_float(hi[j]);
           }
-        } else {
-          const uint32_t vo = (uint32_t)((8 * kh * HW + gy * W + cc) * 4);
-#pragma unroll
-          for (int s = 0; s < FE_KS; ++s)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              v[set][s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
         }
-      }
-    };
-    auto put = [&](int sl) {   // the loaded row -> ring slot sl
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      float* slot = ring + sl * FE_SLOT;
-#pragma unroll
-      for (int set = 0; set < 2; ++set) {
-        float mx = 0.f;
+      } else {
+        const uint32_t vo = (uint32_t)((8 * kh * HW + gy * W + cc) * 4);
 #pragma unroll
         for (int s = 0; s < FE_KS; ++s)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[set][s][j]));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const int ep = fe_scale_exp(mx);
-        float* img = slot + set * FE_IMG;
-#pragma unroll
-        for (int s = 0; s < FE_KS; ++s) {
-          uint32_t hw[4], lw[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const fe_f32x2 p = fe_f32x2{ldexpf(v[set][s][2 * j], ep), ldexpf(v[set][s][2 * j + 1], ep)};
-            const fe_f16x2 h = __builtin_convertvector(p, fe_f16x2);
-            const fe_f16x2 l = __builtin_convertvector(p - __builtin_convertvector(h, fe_f32x2), fe_f16x2);
-            hw[j] = __builtin_bit_cast(uint32_t, h);
-            lw[j] = __builtin_bit_cast(uint32_t, l);
-          }
-          *reinterpret_cast<fe_u32x4*>(img + (2 * s) * 256 + 4 * lane) = fe_u32x4{hw[0], hw[1], hw[2], hw[3]};
-          *reinterpret_cast<fe_u32x4*>(img + (2 * s + 1) * 256 + 4 * lane) = fe_u32x4{lw[0], lw[1], lw[2], lw[3]};
-        }
-        if (kh == 0) reinterpret_cast<int*>(slot + 2 * FE_IMG)[set * 32 + n] = ep;
+          for (int j = 0; j < 8; ++j)
+            v[set][s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (16 * s + j) * hw4, 0));
       }
     };
-    issue(0);
-    put(0);
-    issue(1);
+    auto issue_main = [&](int k) { load(0, clampi(r0 - 1 + k, 0, H - 1), colc); };
+    auto issue_halo = [&](int m) { load(1, clampi(r0 - 1 + FE_HB * m + hn / 3, 0, H - 1), hcol); };
+    auto put = [&](int set, float* slot) {   // the loaded pixels of set -> an image slot
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      float mx = 0.f;
+#pragma unroll
+      for (int s = 0; s < FE_KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[set][s][j]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const int ep = fe_scale_exp(mx);
+#pragma unroll
+      for (int s = 0; s < FE_KS; ++s) {
+        uint32_t hw[4], lw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const fe_f32x2 p = fe_f32x2{ldexpf(v[set][s][2 * j], ep), ldexpf(v[set][s][2 * j + 1], ep)};
+          const fe_f16x2 h = __builtin_convertvector(p, fe_f16x2);
+          const fe_f16x2 l = __builtin_convertvector(p - __builtin_convertvector(h, fe_f32x2), fe_f16x2);
+          hw[j] = __builtin_bit_cast(uint32_t, h);
+          lw[j] = __builtin_bit_cast(uint32_t, l);
+        }
+        *reinterpret_cast<fe_u32x4*>(slot + (2 * s) * 256 + 4 * lane) = fe_u32x4{hw[0], hw[1], hw[2], hw[3]};
+        *reinterpret_cast<fe_u32x4*>(slot + (2 * s + 1) * 256 + 4 * lane) = fe_u32x4{lw[0], lw[1], lw[2], lw[3]};
+      }
+      if (kh == 0) reinterpret_cast<int*>(slot + FE_IMG)[n] = ep;
+    };
+    issue_main(0);
+    issue_halo(0);
+    put(0, ring);
+    put(1, himg);
+    issue_main(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // A images and slot 0
+    __builtin_amdgcn_s_barrier();   // A images, slot 0 and halo batch 0
     asm volatile("" ::: "memory");
     for (int k = 0; k < NI3; ++k) {
       if (k + 1 <= NI - 2) {   // uniform: iterations 0 .. NI - 2 run a conv
-        put((k + 1) & 1);
-        if (k + 2 <= NI - 2) issue(k + 2);
+        put(0, ring + ((k + 1) & 1) * FE_SLOT);
+        if ((k + 1) % FE_HB == 0) put(1, himg);   // read by the compute waves in iteration k + 1 only
+        if (k + 2 <= NI - 2) {
+          issue_main(k + 2);
+          if ((k + 2) % FE_HB == 0) issue_halo((k + 2) / FE_HB);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -305,8 +308,9 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     w2 = e2 * rs;
     w3 = e3 * rs;
   };
-  // edges of row ey from the main rows P (ey - 1), Q (ey), N (ey + 1) and the halo ring rows of the same slots
-  auto edges = [&](int ey, auto p_tag, auto q_tag, auto n_tag) __attribute__((always_inline)) {
+  // edges of row ey from the main rows P (ey - 1), Q (ey), N (ey + 1) and the halo ring rows hP, hQ, hN
+  auto edges = [&](int ey, auto p_tag, auto q_tag, auto n_tag, const float* hP, const float* hQ, const float* hN)
+      __attribute__((always_inline)) {
     constexpr int P = decltype(p_tag)::value, Q = decltype(q_tag)::value, N = decltype(n_tag)::value;
     const bool own = ey < r1 && !(FE_DIAG & 1);
     const uint32_t row_off = (uint32_t)(ey * W + col);
@@ -316,7 +320,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
     asm volatile("" : "+s"(hw4));
     // the lane's neighbour across the strip edge, row ey: lane 0 the left pixel L, lane 31 the right R1
-    const float* hq = hw_wave + Q * FE_HROW + kh * 36;
+    const float* hq = hQ + kh * 36;
     float hb[FE_GH][3];
     {
       const float* src = hq + (n == 31 ? 12 : 0);
@@ -353,8 +357,8 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
         // up / down rows, R2 = x0 + 33 to its right, this lane's column to its left)
         float w1r;
         {
-          const float* hp = hw_wave + P * FE_HROW + kh * 36 + 12 + 3 * gi;   // R1, row ey - 1
-          const float* hn = hw_wave + N * FE_HROW + kh * 36 + 12 + 3 * gi;   // R1, row ey + 1
+          const float* hp = hP + kh * 36 + 12 + 3 * gi;   // R1, row ey - 1
+          const float* hn = hN + kh * 36 + 12 + 3 * gi;   // R1, row ey + 1
           const float* hr = hq + 24 + 3 * gi;                                // R2, row ey
           const int cr = x0 + 32;
           float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
@@ -385,8 +389,10 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // A images and ring slot 0 (row r0 - 1)
   asm volatile("" ::: "memory");
-  // phase PH = k mod 3: the row of iteration k goes to fw[PH] (and halo ring row PH); the edge row's rows are
-  // slot PH (= k - 3), (PH + 1) % 3 (k - 2), (PH + 2) % 3 (k - 1)
+  // phase PH = k mod 3: the row of iteration k goes to fw[PH]; the edge row's rows are slot PH (= k - 3),
+  // (PH + 1) % 3 (k - 2), (PH + 2) % 3 (k - 1).  The halo features of conv row j sit in halo ring row j % FE_HR:
+  // iteration FE_HB m writes rows FE_HB m .. + FE_HB - 1 while rows FE_HB m - 3 .. - 1 are still read (FE_HR =
+  // FE_HB + 3 keeps them apart)
   auto iteration = [&](int k, auto ph_tag) __attribute__((always_inline)) {
     constexpr int PH = decltype(ph_tag)::value;
     using IP = std::integral_constant<int, PH>;
@@ -394,36 +400,54 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     using IN = std::integral_constant<int, (PH + 2) % 3>;
     if (k < NI) {   // uniform
       const bool conv = k <= NI - 2;
+      const bool hconv = conv && k % FE_HB == 0;
       fe_f32x16 am = fe_f32x16{}, ax = fe_f32x16{};
       int epm = 0, eph = 0;
       if (conv && !(FE_DIAG & 8)) {
         const float* slot = ring + (k & 1) * FE_SLOT + 4 * lane;
+        if (hconv) {   // uniform: the halo batch with this row (the product order of the main image's)
+          const float* hs = himg + 4 * lane;
 #pragma unroll
-        for (int s = 0; s < FE_KS; ++s) {
-          const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
-          const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
-          const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
-          const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
-          const fe_f16x8 ch = *reinterpret_cast<const fe_f16x8*>(slot + FE_IMG + (2 * s) * 256);
-          const fe_f16x8 cl = *reinterpret_cast<const fe_f16x8*>(slot + FE_IMG + (2 * s + 1) * 256);
-          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
-          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, ax, 0, 0, 0);
-          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
-          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, ax, 0, 0, 0);
-          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
-          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, ax, 0, 0, 0);
+          for (int s = 0; s < FE_KS; ++s) {
+            const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
+            const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
+            const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
+            const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
+            const fe_f16x8 ch = *reinterpret_cast<const fe_f16x8*>(hs + (2 * s) * 256);
+            const fe_f16x8 cl = *reinterpret_cast<const fe_f16x8*>(hs + (2 * s + 1) * 256);
+            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, ax, 0, 0, 0);
+            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, ax, 0, 0, 0);
+            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, ax, 0, 0, 0);
+          }
+          eph = reinterpret_cast<const int*>(himg + FE_IMG)[n];
+        } else {
+#pragma unroll
+          for (int s = 0; s < FE_KS; ++s) {
+            const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
+            const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
+            const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
+            const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
+            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
+            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
+            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
+          }
         }
-        const int* eps = reinterpret_cast<const int*>(ring + (k & 1) * FE_SLOT + 2 * FE_IMG);
-        epm = eps[n];
-        eph = eps[32 + n];
+        epm = reinterpret_cast<const int*>(ring + (k & 1) * FE_SLOT + FE_IMG)[n];
       }
-      if (k >= 3 && !(FE_DIAG & 2)) edges(r0 - 3 + k, IP{}, IQ{}, IN{});   // rows k - 3, k - 2, k - 1
-      if (conv) {                                                            // row k replaces row k - 3
-        norm4(am, epm, fw[PH]);
+      if (k >= 3 && !(FE_DIAG & 2)) {   // rows k - 3, k - 2, k - 1
+        const int j = k % FE_HR;          // (k - 3, k - 2, k - 1) % FE_HR
+        const int jp = j >= 3 ? j - 3 : j + FE_HR - 3, jq = j >= 2 ? j - 2 : j + FE_HR - 2, jn = j >= 1 ? j - 1 : FE_HR - 1;
+        edges(r0 - 3 + k, IP{}, IQ{}, IN{}, hw_wave + jp * FE_HROW, hw_wave + jq * FE_HROW, hw_wave + jn * FE_HROW);
+      }
+      if (conv) norm4(am, epm, fw[PH]);   // row k replaces row k - 3
+      if (hconv) {
         float hf[FE_GH][3];
         norm4(ax, eph, hf);
-        if (n == 0 || n >= 30) {   // the halo ring row: L (lane 0), R1 (lane 31), R2 (lane 30)
-          float* dst = hw_wave + PH * FE_HROW + kh * 36 + (n == 0 ? 0 : (n == 31 ? 12 : 24));
+        if (n < 3 * FE_HB) {   // lane n: conv row k + n / 3, pixel L / R1 / R2
+          float* dst = hw_wave + ((k + n / 3) % FE_HR) * FE_HROW + kh * 36 + 12 * (n % 3);
 #pragma unroll
           for (int gi = 0; gi < FE_GH; ++gi)
 #pragma unroll
