@@ -51,6 +51,12 @@ constexpr int FE_HR = FE_HB + 3, FE_HROW = 2 * 3 * 12;   // halo feature ring: r
 constexpr int FE_LDS = FE_NT * FE_AIMG + 3 * FE_SLOT + FE_NT * FE_HR * FE_HROW;
 static_assert(FE_LDS * 4 <= 163840, "feature_edges LDS");
 constexpr uint32_t FE_OOB = 0x80000000u;
+// features carry sqrt(log2 e) (folded into multiM): a similarity is then log2(e) times REF's, the argument of
+// v_exp_f32 (2^x) directly
+constexpr float FE_SQRT_L2E = 1.2011224087864498f;
+#ifndef FE_SWAP
+#define FE_SWAP 1   // GLR waves: edges before the conv (see iteration)
+#endif
 #ifndef FE_DIAG
 #define FE_DIAG 0   // timing-only builds: 1 no stores, 2 no edge arithmetic, 4 no loads (loader), 8 no conv
 #endif
@@ -117,15 +123,20 @@ __global__ void fe_pack_kernel(const float* __restrict__ wf, char* __restrict__ 
   }
 }
 
+// (DPP moves are convergent: never sunk into a branch, where inactive lanes would read as 0.  No inline asm in
+// the edge arithmetic: an asm statement ends the scheduling region and the conv MFMAs could not be spread over it)
 __device__ __forceinline__ float fe_prev(float v) {   // lane - 1 (DPP wave shift; whole wave active)
-  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
-  asm volatile("" : "+v"(r));
-  return r;
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float fe_next(float v) {   // lane + 1
-  float r = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
-  asm volatile("" : "+v"(r));
-  return r;
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
+}
+template <int E>
+__device__ __forceinline__ float fe_quad_e(float v) {   // every lane of a quad takes the quad's element E
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), E * 0x55, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float fe_quad(float v, int e) {   // e a compile-time constant after unrolling
+  return e == 0 ? fe_quad_e<0>(v) : e == 1 ? fe_quad_e<1>(v) : e == 2 ? fe_quad_e<2>(v) : fe_quad_e<3>(v);
 }
 
 template <bool IN8>
@@ -256,6 +267,10 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     for (int k = 0; k <= NI3; ++k) __builtin_amdgcn_s_barrier();
     return;
   }
+  // the compute of one slab, slab a compile-time constant so that a steady-state iteration (conv MFMAs, edge
+  // arithmetic) is one basic block and the scheduler can overlap the MFMAs with the edges' VALU work
+  auto run = [&](auto sl_tag) __attribute__((always_inline)) {
+  constexpr int slab = decltype(sl_tag)::value;
   float M[FE_GH][3];
   int sg[FE_GH];
 #pragma unroll
@@ -263,7 +278,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     const int g = min(gbase + gi, G - 1);
     sg[gi] = a.sexp[slab * G + g];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) M[gi][f] = a.multiM[slab][g * 3 + f];
+    for (int f = 0; f < 3; ++f) M[gi][f] = a.multiM[slab][g * 3 + f] * FE_SQRT_L2E;
   }
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       a.w[slab] + (int64_t)b * G * 4 * HW, 0, (int)((int64_t)G * 4 * HW * 4), 0x00020000);
@@ -294,13 +309,12 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       out[gi][2] = (f2 * inv) * M[gi][2];
     }
   };
-  // softmax of four similarities with v_exp_f32 (2^x of the log2(e)-scaled argument, <= 0) and one reciprocal
+  // softmax of four (log2(e)-scaled) similarities with v_exp_f32 (2^x, x <= 0) and one reciprocal
   auto softmax4 = [&](float s0, float s1, float s2, float s3, float& w0, float& w1, float& w2, float& w3)
       __attribute__((always_inline)) {
-    constexpr float L2E = 1.4426950408889634f;
     const float m = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
-    const float e0 = __builtin_amdgcn_exp2f((s0 - m) * L2E), e1 = __builtin_amdgcn_exp2f((s1 - m) * L2E);
-    const float e2 = __builtin_amdgcn_exp2f((s2 - m) * L2E), e3 = __builtin_amdgcn_exp2f((s3 - m) * L2E);
+    const float e0 = __builtin_amdgcn_exp2f(s0 - m), e1 = __builtin_amdgcn_exp2f(s1 - m);
+    const float e2 = __builtin_amdgcn_exp2f(s2 - m), e3 = __builtin_amdgcn_exp2f(s3 - m);
     const float sum = ((e0 + e1) + e2) + e3;
     const float rs = __builtin_amdgcn_rcpf(sum);
     w0 = e0 * rs;
@@ -317,8 +331,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     const uint32_t vo = lane_out && own ? (row_off + 16u * kh * HW) * 4u : FE_OOB;
     const uint32_t voc = lane_out && own ? (row_off + 8u * kh * HW) * 4u : FE_OOB;
     const uint32_t vcv = lane_out && ey > r0 && !(FE_DIAG & 1) ? (row_off - W + 8u * kh * HW) * 4u : FE_OOB;   // row ey - 1
-    int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
-    asm volatile("" : "+s"(hw4));
+    const int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
     // the lane's neighbour across the strip edge, row ey: lane 0 the left pixel L, lane 31 the right R1
     const float* hq = hQ + kh * 36;
     float hb[FE_GH][3];
@@ -329,6 +342,39 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
 #pragma unroll
         for (int f = 0; f < 3; ++f) hb[gi][f] = src[3 * gi + f];
     }
+    // GTV: the softmax of R1 = x0 + 32 (lane 31's right neighbour, whose w_left lane 31's pair weight needs), one
+    // graph per lane of the DPP quad 28..31 (lane 28 + j: graph 3 - j) instead of all four graphs in every lane.
+    // Inputs: R1's rows ey - 1, ey, ey + 1 and R2 = x0 + 33 (R1 itself at the image's right edge) from the halo
+    // ring; R1 . (x0 + 31) from lane 31 (its hb and its own features) by a quad broadcast
+    float w1r[FE_GH];
+    if constexpr (slab == 0) {
+      const int gl = 3 - (n & 3);
+      float t1 = 0.f;
+#pragma unroll
+      for (int gi = 0; gi < FE_GH; ++gi) {
+        float d = 0.f;
+#pragma unroll
+        for (int f = 0; f < 3; ++f) d += hb[gi][f] * fw[Q][gi][f];
+        const float b31 = fe_quad(d, 3);
+        t1 = gl == gi ? b31 : t1;
+      }
+      const float* r1q = hq + 12 + 3 * gl;
+      const float* r1p = hP + kh * 36 + 12 + 3 * gl;
+      const float* r1n = hN + kh * 36 + 12 + 3 * gl;
+      const float* r2 = hq + (x0 + 32 < W - 1 ? 24 : 12) + 3 * gl;
+      float t0 = 0.f, t2 = 0.f, t3 = 0.f;
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const float v = r1q[f];
+        t0 += v * r1p[f];
+        t2 += v * r2[f];
+        t3 += v * r1n[f];
+      }
+      float u0, u1, u2, u3;
+      softmax4(t0, t1, t2, t3, u0, u1, u2, u3);
+#pragma unroll
+      for (int gi = 0; gi < FE_GH; ++gi) w1r[gi] = fe_quad(u1, 3 - gi);   // lane 31: graph gi from lane 31 - gi
+    }
 #pragma unroll
     for (int gi = 0; gi < FE_GH; ++gi) {
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -336,8 +382,10 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       for (int f = 0; f < 3; ++f) {
         const float v = fw[Q][gi][f];
         const float pl = fe_prev(v), pr = fe_next(v);
-        const float lv = col > 0 ? (n == 0 ? hb[gi][f] : pl) : v;
-        const float rv = col < W - 1 ? (n == 31 ? hb[gi][f] : pr) : v;
+        // at the image's edges the neighbour is the pixel itself (REF's replicate padding): the halo columns and
+        // the lanes past W are clamped into the image, so their features already equal v bitwise
+        const float lv = n == 0 ? hb[gi][f] : pl;
+        const float rv = n == 31 ? hb[gi][f] : pr;
         s0 += v * fw[P][gi][f];
         s1 += v * lv;
         s2 += v * rv;
@@ -355,27 +403,8 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       if (slab == 0) {   // wave-uniform: pair weights (REF:452-516's C^T C as pair weights)
         // w_left(p + right): lane n + 1's w1; for lane 31 the softmax of R1 = x0 + 32 from the halo rows (R1's
         // up / down rows, R2 = x0 + 33 to its right, this lane's column to its left)
-        float w1r;
-        {
-          const float* hp = hP + kh * 36 + 12 + 3 * gi;   // R1, row ey - 1
-          const float* hn = hN + kh * 36 + 12 + 3 * gi;   // R1, row ey + 1
-          const float* hr = hq + 24 + 3 * gi;                                // R2, row ey
-          const int cr = x0 + 32;
-          float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
-#pragma unroll
-          for (int f = 0; f < 3; ++f) {
-            const float v = hb[gi][f];   // R1 (lane 31's hb)
-            const float rv = cr < W - 1 ? hr[f] : v;
-            t0 += v * hp[f];
-            t1 += v * fw[Q][gi][f];
-            t2 += v * rv;
-            t3 += v * hn[f];
-          }
-          float u0, u2, u3;
-          softmax4(t0, t1, t2, t3, u0, w1r, u2, u3);
-        }
         const float w1n = fe_next(w1);   // (outside the select: a DPP read in a branch sees inactive lanes as 0)
-        const float wln = n == 31 ? w1r : w1n;
+        const float wln = n == 31 ? w1r[gi] : w1n;
         const float ch = col + 1 < W ? w2 * w2 + wln * wln : 0.f;
         const float cv = wdn_prev[gi] * wdn_prev[gi] + w0 * w0;   // row ey - 1: w_down(p)^2 + w_up(p + down)^2
         wdn_prev[gi] = w3;
@@ -387,83 +416,113 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   };
 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();   // A images and ring slot 0 (row r0 - 1)
+  __builtin_amdgcn_s_barrier();   // A images, ring slot 0 (row r0 - 1), halo batch 0
   asm volatile("" ::: "memory");
-  // phase PH = k mod 3: the row of iteration k goes to fw[PH]; the edge row's rows are slot PH (= k - 3),
-  // (PH + 1) % 3 (k - 2), (PH + 2) % 3 (k - 1).  The halo features of conv row j sit in halo ring row j % FE_HR:
-  // iteration FE_HB m writes rows FE_HB m .. + FE_HB - 1 while rows FE_HB m - 3 .. - 1 are still read (FE_HR =
-  // FE_HB + 3 keeps them apart)
-  auto iteration = [&](int k, auto ph_tag) __attribute__((always_inline)) {
+  // the halo batch of conv rows k .. k + FE_HB - 1 into the halo feature ring (the main image's product order)
+  auto halo = [&](int k) __attribute__((always_inline)) {
+    fe_f32x16 ax = fe_f32x16{};
+    const float* hs = himg + 4 * lane;
+#pragma unroll
+    for (int s = 0; s < FE_KS; ++s) {
+      const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
+      const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
+      const fe_f16x8 ch = *reinterpret_cast<const fe_f16x8*>(hs + (2 * s) * 256);
+      const fe_f16x8 cl = *reinterpret_cast<const fe_f16x8*>(hs + (2 * s + 1) * 256);
+      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, ax, 0, 0, 0);
+      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, ax, 0, 0, 0);
+      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, ax, 0, 0, 0);
+    }
+    float hf[FE_GH][3];
+    norm4(ax, reinterpret_cast<const int*>(himg + FE_IMG)[n], hf);
+    if (n < 3 * FE_HB) {   // lane n: conv row k + n / 3, pixel L / R1 / R2
+      float* dst = hw_wave + ((k + n / 3) % FE_HR) * FE_HROW + kh * 36 + 12 * (n % 3);
+#pragma unroll
+      for (int gi = 0; gi < FE_GH; ++gi)
+#pragma unroll
+        for (int f = 0; f < 3; ++f) dst[3 * gi + f] = hf[gi][f];
+    }
+  };
+  // iteration k: phase PH = k mod 3: the row of iteration k goes to fw[PH]; the edge row's rows are slot PH
+  // (= k - 3), (PH + 1) % 3 (k - 2), (PH + 2) % 3 (k - 1).  The halo features of conv row j sit in halo ring row
+  // j % FE_HR: iteration FE_HB m writes rows FE_HB m .. + FE_HB - 1 while rows FE_HB m - 3 .. - 1 are still read
+  // (FE_HR = FE_HB + 3 keeps them apart).  EDGE / CONV are compile-time (k >= 3 / k <= NI - 2).
+  auto iteration = [&](int k, auto ph_tag, auto edge_tag, auto conv_tag) __attribute__((always_inline)) {
     constexpr int PH = decltype(ph_tag)::value;
+    constexpr bool EDGE = decltype(edge_tag)::value, CONV = decltype(conv_tag)::value;
     using IP = std::integral_constant<int, PH>;
     using IQ = std::integral_constant<int, (PH + 1) % 3>;
     using IN = std::integral_constant<int, (PH + 2) % 3>;
-    if (k < NI) {   // uniform
-      const bool conv = k <= NI - 2;
-      const bool hconv = conv && k % FE_HB == 0;
-      fe_f32x16 am = fe_f32x16{}, ax = fe_f32x16{};
-      int epm = 0, eph = 0;
-      if (conv && !(FE_DIAG & 8)) {
+    fe_f32x16 am = fe_f32x16{};
+    int epm = 0;
+    auto conv = [&]() __attribute__((always_inline)) {
+      if (CONV && !(FE_DIAG & 8)) {
         const float* slot = ring + (k & 1) * FE_SLOT + 4 * lane;
-        if (hconv) {   // uniform: the halo batch with this row (the product order of the main image's)
-          const float* hs = himg + 4 * lane;
 #pragma unroll
-          for (int s = 0; s < FE_KS; ++s) {
-            const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
-            const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
-            const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
-            const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
-            const fe_f16x8 ch = *reinterpret_cast<const fe_f16x8*>(hs + (2 * s) * 256);
-            const fe_f16x8 cl = *reinterpret_cast<const fe_f16x8*>(hs + (2 * s + 1) * 256);
-            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, ax, 0, 0, 0);
-            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, ax, 0, 0, 0);
-            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, ax, 0, 0, 0);
-          }
-          eph = reinterpret_cast<const int*>(himg + FE_IMG)[n];
-        } else {
-#pragma unroll
-          for (int s = 0; s < FE_KS; ++s) {
-            const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
-            const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
-            const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
-            const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
-            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
-            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
-            am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
-          }
+        for (int s = 0; s < FE_KS; ++s) {
+          const fe_f16x8 ah = *reinterpret_cast<const fe_f16x8*>(at + (2 * s) * 256);
+          const fe_f16x8 al = *reinterpret_cast<const fe_f16x8*>(at + (2 * s + 1) * 256);
+          const fe_f16x8 bh = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s) * 256);
+          const fe_f16x8 bl = *reinterpret_cast<const fe_f16x8*>(slot + (2 * s + 1) * 256);
+          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, am, 0, 0, 0);
+          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, am, 0, 0, 0);
+          am = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, am, 0, 0, 0);
         }
         epm = reinterpret_cast<const int*>(ring + (k & 1) * FE_SLOT + FE_IMG)[n];
       }
-      if (k >= 3 && !(FE_DIAG & 2)) {   // rows k - 3, k - 2, k - 1
-        const int j = k % FE_HR;          // (k - 3, k - 2, k - 1) % FE_HR
+    };
+    auto edge = [&]() __attribute__((always_inline)) {
+      if (EDGE && !(FE_DIAG & 2)) {   // rows k - 3, k - 2, k - 1
+        const int j = k % FE_HR;
         const int jp = j >= 3 ? j - 3 : j + FE_HR - 3, jq = j >= 2 ? j - 2 : j + FE_HR - 2, jn = j >= 1 ? j - 1 : FE_HR - 1;
         edges(r0 - 3 + k, IP{}, IQ{}, IN{}, hw_wave + jp * FE_HROW, hw_wave + jq * FE_HROW, hw_wave + jn * FE_HROW);
       }
-      if (conv) norm4(am, epm, fw[PH]);   // row k replaces row k - 3
-      if (hconv) {
-        float hf[FE_GH][3];
-        norm4(ax, eph, hf);
-        if (n < 3 * FE_HB) {   // lane n: conv row k + n / 3, pixel L / R1 / R2
-          float* dst = hw_wave + ((k + n / 3) % FE_HR) * FE_HROW + kh * 36 + 12 * (n % 3);
-#pragma unroll
-          for (int gi = 0; gi < FE_GH; ++gi)
-#pragma unroll
-            for (int f = 0; f < 3; ++f) dst[3 * gi + f] = hf[gi][f];
-        }
-      }
+    };
+    // the two compute waves of a SIMD (one GTV, one GLR: waves w, w + 4) run the phases in opposite orders, so
+    // that one's dependent MFMA chain overlaps the other's edge arithmetic (both in lockstep after the barrier)
+    if constexpr (slab == 0 || !FE_SWAP) {
+      conv();
+      __builtin_amdgcn_sched_barrier(0);
+      edge();
+    } else {
+      edge();
+      __builtin_amdgcn_sched_barrier(0);
+      conv();
+    }
+    if (CONV) {
+      if (k % FE_HB == 0 && !(FE_DIAG & 8)) halo(k);   // uniform
+      norm4(am, epm, fw[PH]);                           // row k replaces row k - 3
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  for (int k = 0; k < NI3; k += 3) {
-    iteration(k, std::integral_constant<int, 0>{});
-    iteration(k + 1, std::integral_constant<int, 1>{});
-    iteration(k + 2, std::integral_constant<int, 2>{});
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using T = std::true_type;
+  using F = std::false_type;
+  // NI >= 4: iterations 0..2 conv only, 3..NI-2 both, NI-1 edges only
+  iteration(0, I0{}, F{}, T{});
+  iteration(1, I1{}, F{}, T{});
+  iteration(2, I2{}, F{}, T{});
+  int k = 3;
+  for (; k + 2 <= NI - 2; k += 3) {
+    iteration(k, I0{}, T{}, T{});
+    iteration(k + 1, I1{}, T{}, T{});
+    iteration(k + 2, I2{}, T{}, T{});
   }
+  const int rem = NI - 1 - k;   // 0..2 conv rows left (k % 3 == 0), then the edge-only iteration NI - 1
+  if (rem == 0) {
+    iteration(k, I0{}, T{}, F{});
+  } else if (rem == 1) {
+    iteration(k, I0{}, T{}, T{});
+    iteration(k + 1, I1{}, T{}, F{});
+  } else {
+    iteration(k, I0{}, T{}, T{});
+    iteration(k + 1, I1{}, T{}, T{});
+    iteration(k + 2, I2{}, T{}, F{});
+  }
+  for (int i = NI; i < NI3; ++i) __builtin_amdgcn_s_barrier();   // the loader's NI3 iteration barriers
   if (slab == 0 && r1 == H) {   // the image's last row: no lower neighbour, c_v = 0
     int hw4 = __builtin_amdgcn_readfirstlane(HW * 4);
     const uint32_t vz = lane_out ? ((uint32_t)((H - 1) * W + col) + 8u * kh * HW) * 4u : FE_OOB;
@@ -472,6 +531,11 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       __builtin_amdgcn_raw_buffer_store_b32(0u, crs, gbase + gi < G ? vz : FE_OOB, (uint32_t)((8 * t4 + gi) * 2 + 1) * hw4,
                                             0);
   }
+  };
+  if (slab == 0)
+    run(std::integral_constant<int, 0>{});
+  else
+    run(std::integral_constant<int, 1>{});
 }
 
 }  // namespace
