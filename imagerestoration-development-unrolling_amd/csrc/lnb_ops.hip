@@ -1049,7 +1049,16 @@ constexpr int LF_PP = 2 * LF_NBLK * 32;     // floats per pair plane (m, v inter
 constexpr int LF_HBUF = 16 * LF_PP;         // floats per h buffer
 constexpr int LF_NSLOT = 3;                 // ring slots (step i + 1 loading, GEMM1(i), GEMM2(i - 1))
 constexpr int LF_XE = 10;                   // common power-of-two scale of the fp16 x operand
-constexpr int LF_TAPS = 16 * 18;            // tap floats per chunk (two 1-KB images)
+#ifndef GRR_WIN_B64
+#define GRR_WIN_B64 1
+#endif
+#ifndef GRR_TAP20
+#define GRR_TAP20 1
+#endif
+// tap floats per pair: 9 (mask, value) pairs, padded to 20 so that a pair's taps are five 16-byte LDS reads
+// (ds_read_b128 runs at the LDS array's rate with one wave per SIMD, ds_read_b64 does not)
+constexpr int LF_TSTR = GRR_TAP20 ? 20 : 18;
+constexpr int LF_TAPS = 16 * LF_TSTR;       // tap floats per chunk (two 1-KB images)
 __host__ __device__ constexpr int fused_images(int KS, int MT) { return 2 * KS + 2 * MT + 2; }
 
 struct LnbFusedArgs {
@@ -1111,8 +1120,8 @@ __global__ void lnb_fused_pack_kernel(const float* __restrict__ w1, const float*
     } else {
       const int r = (im - 2 * KS - 2 * MT) * 256 + e;
       if (r < LF_TAPS) {
-        const int w = r / 18, t = (r % 18) >> 1, comp = r & 1, pj = 16 * c + w;
-        if (pj < hid) {
+        const int w = r / LF_TSTR, t = (r % LF_TSTR) >> 1, comp = r & 1, pj = 16 * c + w;
+        if (pj < hid && t < 9) {
           const int row = (comp ? hid : 0) + pj;
           const float fold = comp ? -0.69314718055994531f : -1.44269504088896341f;
           word = __float_as_uint(ldexpf(wdw[(int64_t)row * 9 + t], -(head16_row_exp(w1, ln_w, row, C, 1) + LF_XE)) *
@@ -1141,7 +1150,8 @@ __device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint3
 
 // timing-only diagnostic builds (wrong results): 1 = consumers skip their work, 2 = producers skip theirs
 #ifndef GRR_FUSED_DIAG
-#define GRR_FUSED_DIAG 0
+#define GRR_FUSED_DIAG 0   // timing-only knock-outs: 1 consumer work, 2 producer work, 4 gate LDS reads after
+                           // the first pair, 8 the gate's exp / rcp
 #endif
 // GRR_FUSED_STAMP=1: diagnostic build -- each wave sums s_memtime deltas of its phases (producer: DMA issue,
 // x prologue, GEMM1, h stores, wait, barrier; consumer: DMA issue, gate, GEMM2, epilogue, wait, barrier)
@@ -1425,7 +1435,7 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
       const float* w2s = slot + 2 * KS * 256 + lane * 4;
       // the window of both rows' pixels: halo rows 2 cw .. 2 cw + 3, columns col .. col + 2, pair 8 kh + jj
       const float* hwin = smem + (st & 1) * LF_HBUF + 8 * kh * LF_PP + 2 * (2 * cw * LF_HWD + col);
-      const float* tap0 = slot + (2 * KS + 2 * MT) * 256 + 8 * kh * 18;
+      const float* tap0 = slot + (2 * KS + 2 * MT) * 256 + 8 * kh * LF_TSTR;
       float g[2][8];
       // One pair per step, the next pair's taps and window in flight (LDS reads count in order: the
       // compiler waits for this pair's only); the scheduling barrier keeps each step's loads in it
@@ -1433,30 +1443,54 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
       // (v_pk_fma_f32: the same fp32 fma per component, half the instructions)
       f32x2 tA[9];
       f32x2 wA[12];
-      auto load = [&](int jj, f32x2 (&t)[9], f32x2 (&w)[12]) {
-        const float* tp = tap0 + jj * 18;
+      auto load_t = [&](int jj, f32x2 (&t)[9]) {
+        const float* tp = tap0 + jj * LF_TSTR;
+        if constexpr (GRR_TAP20) {
 #pragma unroll
-        for (int u = 0; u < 9; ++u) t[u] = *reinterpret_cast<const f32x2*>(tp + 2 * u);
+          for (int u = 0; u < 5; ++u) {
+            const f32x4 q = *reinterpret_cast<const f32x4*>(tp + 4 * u);
+            t[2 * u] = f32x2{q[0], q[1]};
+            if (2 * u + 1 < 9) t[2 * u + 1] = f32x2{q[2], q[3]};
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 9; ++u) t[u] = *reinterpret_cast<const f32x2*>(tp + 2 * u);
+        }
+      };
+      auto load_w = [&](int jj, f32x2 (&w)[12]) {
         const float* hp = hwin + jj * LF_PP;
 #pragma unroll
-        for (int u = 0; u < 12; ++u) w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
+        for (int u = 0; u < 12; ++u) {
+#if GRR_WIN_B64
+          // volatile: one ds_read_b64 each (2 LDS cycles, 256 B/clk); the load combiner's ds_read2_b64 pairs
+          // take 8 cycles (128 B/clk) and an address add each
+          w[u] = *(const volatile __attribute__((address_space(3))) f32x2*)(hp + 2 * ((u / 3) * LF_HWD + u % 3));
+#else
+          w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
+#endif
+        }
       };
-      load(0, tA, wA);
+      auto row = [&](int jj, int rb) __attribute__((always_inline)) {
+        f32x2 mv = tA[0] * wA[3 * rb];
+#pragma unroll
+        for (int t = 1; t < 9; ++t) mv = __builtin_elementwise_fma(tA[t], wA[3 * (rb + t / 3) + t % 3], mv);
+        const float m = mv[0], v = mv[1];
+        // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
+        g[rb][jj] = (GRR_FUSED_DIAG & 8) ? (m * v) : (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+      };
+      load_t(0, tA);
+      load_w(0, wA);
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         f32x2 tB[9];
         f32x2 wB[12];
-        if (jj < 7) load(jj + 1, tB, wB);
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          f32x2 mv = tA[0] * wA[3 * rb];
-#pragma unroll
-          for (int t = 1; t < 9; ++t) mv = __builtin_elementwise_fma(tA[t], wA[3 * (rb + t / 3) + t % 3], mv);
-          const float m = mv[0], v = mv[1];
-          // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
-          g[rb][jj] = (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
+        if (jj < 7 && !(GRR_FUSED_DIAG & 4)) {
+          load_t(jj + 1, tB);
+          load_w(jj + 1, wB);
         }
-        if (jj < 7) {
+        row(jj, 0);
+        row(jj, 1);
+        if (jj < 7 && !(GRR_FUSED_DIAG & 4)) {
 #pragma unroll
           for (int u = 0; u < 9; ++u) tA[u] = tB[u];
 #pragma unroll
