@@ -141,6 +141,10 @@ __device__ __forceinline__ float fe_quad(float v, int e) {   // e a compile-time
 
 template <bool IN8>
 __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
+  // Explicit fmas only: an iteration is instantiated several times (phase, edge / conv flags), and contraction
+  // left to the backend fused differently per instance -- a row's weights then depended on where its segment
+  // started (1 ulp), which breaks bitwise batch independence (the segment length follows the batch size)
+#pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float lds[FE_LDS];
   float* const aimg = lds;                         // [tile][k-step][term] A images
   float* const ring = aimg + FE_NT * FE_AIMG;      // [slot 0, 1]: main images + ep of their pixels
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       for (int gi = 0; gi < FE_GH; ++gi) {
         float d = 0.f;
 #pragma unroll
-        for (int f = 0; f < 3; ++f) d += hb[gi][f] * fw[Q][gi][f];
+        for (int f = 0; f < 3; ++f) d = __builtin_fmaf(hb[gi][f], fw[Q][gi][f], d);
         const float b31 = fe_quad(d, 3);
         t1 = gl == gi ? b31 : t1;
       }
@@ -366,9 +370,9 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
 #pragma unroll
       for (int f = 0; f < 3; ++f) {
         const float v = r1q[f];
-        t0 += v * r1p[f];
-        t2 += v * r2[f];
-        t3 += v * r1n[f];
+        t0 = __builtin_fmaf(v, r1p[f], t0);
+        t2 = __builtin_fmaf(v, r2[f], t2);
+        t3 = __builtin_fmaf(v, r1n[f], t3);
       }
       float u0, u1, u2, u3;
       softmax4(t0, t1, t2, t3, u0, u1, u2, u3);
@@ -386,10 +390,10 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
         // the lanes past W are clamped into the image, so their features already equal v bitwise
         const float lv = n == 0 ? hb[gi][f] : pl;
         const float rv = n == 31 ? hb[gi][f] : pr;
-        s0 += v * fw[P][gi][f];
-        s1 += v * lv;
-        s2 += v * rv;
-        s3 += v * fw[N][gi][f];
+        s0 = __builtin_fmaf(v, fw[P][gi][f], s0);
+        s1 = __builtin_fmaf(v, lv, s1);
+        s2 = __builtin_fmaf(v, rv, s2);
+        s3 = __builtin_fmaf(v, fw[N][gi][f], s3);
       }
       float w0, w1, w2, w3;
       softmax4(s0, s1, s2, s3, w0, w1, w2, w3);
@@ -405,8 +409,9 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
         // up / down rows, R2 = x0 + 33 to its right, this lane's column to its left)
         const float w1n = fe_next(w1);   // (outside the select: a DPP read in a branch sees inactive lanes as 0)
         const float wln = n == 31 ? w1r[gi] : w1n;
-        const float ch = col + 1 < W ? w2 * w2 + wln * wln : 0.f;
-        const float cv = wdn_prev[gi] * wdn_prev[gi] + w0 * w0;   // row ey - 1: w_down(p)^2 + w_up(p + down)^2
+        const float ch = col + 1 < W ? __builtin_fmaf(w2, w2, wln * wln) : 0.f;
+        // row ey - 1: w_down(p)^2 + w_up(p + down)^2
+        const float cv = __builtin_fmaf(wdn_prev[gi], wdn_prev[gi], w0 * w0);
         wdn_prev[gi] = w3;
         const uint32_t soc = (uint32_t)((8 * t4 + gi) * 2) * hw4;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ch), crs, gok ? voc : FE_OOB, soc, 0);

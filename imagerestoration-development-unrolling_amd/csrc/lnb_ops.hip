@@ -1049,16 +1049,12 @@ constexpr int LF_PP = 2 * LF_NBLK * 32;     // floats per pair plane (m, v inter
 constexpr int LF_HBUF = 16 * LF_PP;         // floats per h buffer
 constexpr int LF_NSLOT = 3;                 // ring slots (step i + 1 loading, GEMM1(i), GEMM2(i - 1))
 constexpr int LF_XE = 10;                   // common power-of-two scale of the fp16 x operand
-#ifndef GRR_WIN_B64
-#define GRR_WIN_B64 1
-#endif
-#ifndef GRR_TAP20
-#define GRR_TAP20 1
-#endif
-// tap floats per pair: 9 (mask, value) pairs, padded to 20 so that a pair's taps are five 16-byte LDS reads
-// (ds_read_b128 runs at the LDS array's rate with one wave per SIMD, ds_read_b64 does not)
-constexpr int LF_TSTR = GRR_TAP20 ? 20 : 18;
-constexpr int LF_TAPS = 16 * LF_TSTR;       // tap floats per chunk (two 1-KB images)
+// h planes and taps in pair duos: per halo pixel the (mask, value) of pairs 2d, 2d + 1 in 16 bytes, as GEMM1's
+// accumulator holds them (registers 4q .. 4q + 3 = pairs 4q + 2 kh, + 1), so the gate reads its window and taps
+// as ds_read_b128 -- 21 reads per two pairs; one pair at a time took 2 x (12 ds_read_b64 + 5): 64 x 256^2
+// 3.71 -> 3.67 ms (with the b64 reads merged into ds_read2_b64, which run at half the LDS rate: 3.76)
+constexpr int LF_DSTR = 36;                 // tap floats per duo: 9 taps x (m_a, v_a, m_b, v_b)
+constexpr int LF_TAPS = 8 * LF_DSTR;        // tap floats per chunk (two 1-KB images)
 __host__ __device__ constexpr int fused_images(int KS, int MT) { return 2 * KS + 2 * MT + 2; }
 
 struct LnbFusedArgs {
@@ -1120,7 +1116,7 @@ __global__ void lnb_fused_pack_kernel(const float* __restrict__ w1, const float*
     } else {
       const int r = (im - 2 * KS - 2 * MT) * 256 + e;
       if (r < LF_TAPS) {
-        const int w = r / LF_TSTR, t = (r % LF_TSTR) >> 1, comp = r & 1, pj = 16 * c + w;
+        const int w = 2 * (r / LF_DSTR) + ((r >> 1) & 1), t = (r % LF_DSTR) >> 2, comp = r & 1, pj = 16 * c + w;
         if (pj < hid && t < 9) {
           const int row = (comp ? hid : 0) + pj;
           const float fold = comp ? -0.69314718055994531f : -1.44269504088896341f;
@@ -1148,10 +1144,10 @@ __device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint3
 // consumer mapping: lane per (column, pair half), two rows per lane, taps from the LDS ring (a lane per
 // pixel with scalar taps and B operands by v_permlane32_swap measured slower)
 
-// timing-only diagnostic builds (wrong results): 1 = consumers skip their work, 2 = producers skip theirs
+// timing-only diagnostic builds (wrong results): 1 = consumers skip their work, 2 = producers skip theirs,
+// 8 = the gate without its exp / rcp
 #ifndef GRR_FUSED_DIAG
-#define GRR_FUSED_DIAG 0   // timing-only knock-outs: 1 consumer work, 2 producer work, 4 gate LDS reads after
-                           // the first pair, 8 the gate's exp / rcp
+#define GRR_FUSED_DIAG 0
 #endif
 // GRR_FUSED_STAMP=1: diagnostic build -- each wave sums s_memtime deltas of its phases (producer: DMA issue,
 // x prologue, GEMM1, h stores, wait, barrier; consumer: DMA issue, gate, GEMM2, epilogue, wait, barrier)
@@ -1381,12 +1377,11 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
           if (k == NBW - 1 && !has_last) continue;
           if (wave_corr) acc[k] *= corr[k];
           const int q = (wave + 4 * k) * 32 + (lane & 31);
-          // registers 2u, 2u + 1 = rows r, r + 1 (r even: mask, value of chunk pair r / 2)
+          // registers 4u .. 4u + 3 = rows 8 u + 4 kh .. + 3: (mask, value) of pairs 4 u + 2 kh, + 1 = duo 2 u + kh
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int r = ((2 * u) & 3) + 8 * ((2 * u) >> 2) + 4 * kh;
-            *reinterpret_cast<f32x2*>(hb + (r >> 1) * LF_PP + 2 * q) = f32x2{acc[k][2 * u], acc[k][2 * u + 1]};
-          }
+          for (int u = 0; u < 4; ++u)
+            *reinterpret_cast<f32x4*>(hb + (2 * u + kh) * 2 * LF_PP + 4 * q) =
+                f32x4{acc[k][4 * u], acc[k][4 * u + 1], acc[k][4 * u + 2], acc[k][4 * u + 3]};
         }
         if (++c == nch) {
           c = 0;
@@ -1433,68 +1428,36 @@ __global__ __launch_bounds__(512, 1) void lnb_fused16_kernel(LnbFusedArgs a) {
       const FusedTile T = fused_tile(a, ctile);
       const int gxo = T.x0 + col;
       const float* w2s = slot + 2 * KS * 256 + lane * 4;
-      // the window of both rows' pixels: halo rows 2 cw .. 2 cw + 3, columns col .. col + 2, pair 8 kh + jj
-      const float* hwin = smem + (st & 1) * LF_HBUF + 8 * kh * LF_PP + 2 * (2 * cw * LF_HWD + col);
-      const float* tap0 = slot + (2 * KS + 2 * MT) * 256 + 8 * kh * LF_TSTR;
       float g[2][8];
-      // One pair per step, the next pair's taps and window in flight (LDS reads count in order: the
-      // compiler waits for this pair's only); the scheduling barrier keeps each step's loads in it
-      // taps as (mask, value) pairs: the two planes' depthwise sums run as one packed FMA chain
-      // (v_pk_fma_f32: the same fp32 fma per component, half the instructions)
-      f32x2 tA[9];
-      f32x2 wA[12];
-      auto load_t = [&](int jj, f32x2 (&t)[9]) {
-        const float* tp = tap0 + jj * LF_TSTR;
-        if constexpr (GRR_TAP20) {
+      // the gate, a pair duo at a time (taps and window of both output rows as 16-byte reads): the window is
+      // halo rows 2 cw .. 2 cw + 3, columns col .. col + 2; the two planes' depthwise sums of both pairs run
+      // as packed FMA chains (v_pk_fma_f32: the same fp32 fma per component)
+      // duo dd = pairs 8 kh + 2 dd, + 1
+      const float* hwin4 = smem + (st & 1) * LF_HBUF + 4 * kh * 2 * LF_PP + 4 * (2 * cw * LF_HWD + col);
+      const float* tapd = slot + (2 * KS + 2 * MT) * 256 + 4 * kh * LF_DSTR;
+      auto load_d = [&](int dd, f32x4 (&t4)[9], f32x4 (&w4)[12]) __attribute__((always_inline)) {
 #pragma unroll
-          for (int u = 0; u < 5; ++u) {
-            const f32x4 q = *reinterpret_cast<const f32x4*>(tp + 4 * u);
-            t[2 * u] = f32x2{q[0], q[1]};
-            if (2 * u + 1 < 9) t[2 * u + 1] = f32x2{q[2], q[3]};
+        for (int u = 0; u < 9; ++u) t4[u] = *reinterpret_cast<const f32x4*>(tapd + dd * LF_DSTR + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 12; ++u)
+          w4[u] = *reinterpret_cast<const f32x4*>(hwin4 + dd * 2 * LF_PP + 4 * ((u / 3) * LF_HWD + u % 3));
+      };
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        f32x4 t4[9], w4[12];
+        load_d(dd, t4, w4);   // (the next duo's reads in flight too spill at the 256-register bound)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          f32x4 mv = t4[0] * w4[3 * rb];
+#pragma unroll
+          for (int t = 1; t < 9; ++t) mv = __builtin_elementwise_fma(t4[t], w4[3 * (rb + t / 3) + t % 3], mv);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
+            const float m = mv[2 * e], v = mv[2 * e + 1];
+            g[rb][2 * dd + e] = (GRR_FUSED_DIAG & 8) ? (m * v)
+                                                      : (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
           }
-        } else {
-#pragma unroll
-          for (int u = 0; u < 9; ++u) t[u] = *reinterpret_cast<const f32x2*>(tp + 2 * u);
-        }
-      };
-      auto load_w = [&](int jj, f32x2 (&w)[12]) {
-        const float* hp = hwin + jj * LF_PP;
-#pragma unroll
-        for (int u = 0; u < 12; ++u) {
-#if GRR_WIN_B64
-          // volatile: one ds_read_b64 each (2 LDS cycles, 256 B/clk); the load combiner's ds_read2_b64 pairs
-          // take 8 cycles (128 B/clk) and an address add each
-          w[u] = *(const volatile __attribute__((address_space(3))) f32x2*)(hp + 2 * ((u / 3) * LF_HWD + u % 3));
-#else
-          w[u] = *reinterpret_cast<const f32x2*>(hp + 2 * ((u / 3) * LF_HWD + u % 3));
-#endif
-        }
-      };
-      auto row = [&](int jj, int rb) __attribute__((always_inline)) {
-        f32x2 mv = tA[0] * wA[3 * rb];
-#pragma unroll
-        for (int t = 1; t < 9; ++t) mv = __builtin_elementwise_fma(tA[t], wA[3 * (rb + t / 3) + t % 3], mv);
-        const float m = mv[0], v = mv[1];
-        // m' = -log2(e) m, v' = -ln(2) v (the taps' fold): sigmoid(m) m v = m' v' / (1 + 2^m')
-        g[rb][jj] = (GRR_FUSED_DIAG & 8) ? (m * v) : (m * v) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(m));
-      };
-      load_t(0, tA);
-      load_w(0, wA);
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        f32x2 tB[9];
-        f32x2 wB[12];
-        if (jj < 7 && !(GRR_FUSED_DIAG & 4)) {
-          load_t(jj + 1, tB);
-          load_w(jj + 1, wB);
-        }
-        row(jj, 0);
-        row(jj, 1);
-        if (jj < 7 && !(GRR_FUSED_DIAG & 4)) {
-#pragma unroll
-          for (int u = 0; u < 9; ++u) tA[u] = tB[u];
-#pragma unroll
-          for (int u = 0; u < 12; ++u) wA[u] = wB[u];
         }
         __builtin_amdgcn_sched_barrier(0);
       }
