@@ -1,13 +1,13 @@
 #!/bin/bash
-# round 6 (o): fused LNB window reads as single ds_read_b64 (GRR_WIN_B64) -- parity of the candidate, A/B
+# round 6 (o): fused LNB gate software-pipelined over tap rows (GRR_GATE_PIPE) -- parity of the candidate, A/B
 set -o pipefail
 O=gpurun_out/r06o
 mkdir -p $O
-GRR_LIB=exp/libgrr_wb.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "fused_lnb or local_nonlinear" -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
+GRR_LIB=exp/libgrr_gp.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "fused_lnb or local_nonlinear" -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
 tail -1 $O/t.log
 for rep in 1 2; do
 for sz in 256 128; do
-  for v in base t20 wb; do
+  for v in base gp; do
     lib=imagerestoration-development-unrolling_amd/libgrr.so; [ $v = base ] || lib=exp/libgrr_$v.so
     GRR_LIB=$lib timeout -k 10 120 python scripts/micro.py --kernel lnb --size $sz --iters 20 --c8 1 > $O/m_${v}_$sz.txt 2>&1 || exit 1
     echo "$sz $v: $(grep -h 'mean=' $O/m_${v}_$sz.txt | tr '\n' ' ')"
