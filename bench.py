@@ -112,7 +112,7 @@ def load_traffic(kernel, batch):
 def load_traffic_file(name, kernel_prefix, batch):
     """Per-launch HBM bytes (mean over the bench's launches of that kernel): the newest round's summary
     under profiles/ of this workload."""
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         t = _traffic(os.path.join(ROOT, "profiles", rnd, name), kernel_prefix, batch)
         if t is not None:
             return t
@@ -379,6 +379,17 @@ def main():
             "traffic": load_traffic_file("traffic_system_first_pair.json", "graph_step2_kernel", b),
             "note": "algorithmic bytes (kernels.first_pair_bytes: b_A, D b_A, y, three full- and three half-level "
                     "weight planes sets read once; b_B, x_2, u_2, D x_2 written) / HIP-event time"}
+    if "feature_edges" in kern:   # a level's feature 1x1 + both graph modules' edge weights in one pass
+        fe = kern["feature_edges"]
+        res.setdefault("roofline_secondary", {})["feature_edges"] = {
+            "bound": "hbm", "kernel": "feat_edge_kernel (grr_feature_edges)",
+            "achieved": round(fe["gbps"], 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(fe["gbps"] / HBM_PEAK_GBPS, 4), "bytes_per_launch": fe["bytes_per_launch"],
+            "mean_launch_ms": round(fe["mean_ms"], 4), "launches": fe["launches"],
+            "traffic": load_traffic_file("traffic_feature_edges.json", "feat_edge_kernel", b),
+            "note": "algorithmic bytes (kernels.feature_edges: 4 (C + 10 G) per pixel -- the LocalNonLinearBlock output "
+                    "in, the GTV raw and pair weights and the GLR raw weights out; the 2C features never reach HBM) / "
+                    "HIP-event time"}
     kernels_ms = {k: round(v["total_ms"] / n_inst, 3) for k, v in kern.items()}
     res["kernel_ms_per_step"] = kernels_ms
     if args.breakdown:
