@@ -10,7 +10,7 @@
 //    (its largest |x| into [2^13, 2^14)), splits it into exact-sum fp16 hi / lo terms in the layout of the
 //    32x32x16 MFMA's B operand and writes them into a 2-slot LDS ring -- for the strip's 32 columns (main image)
 //    and for its halo columns x0 - 1, x0 + 32, x0 + 33 (halo image, lanes 0, 31, 30);
-//  * waves 0..7 each own 8 graphs of one slab (waves 0-3 the GTV features, 4-7 the GLR features; lane half kh
+//  * waves 0..7 each own 8 graphs of one slab (4 tiles of GTV features, 4 of GLR features; lane half kh
 //    holds graphs 8 t + 4 kh .. + 3): per row, the 1x1 conv of both images on v_mfma_f32_32x32x16_f16 (three
 //    products of the two-term splits; A = the wave's weight rows, staged in LDS, scaled by a power of two per
 //    (slab, graph)) leaves each lane the 12 features (4 graphs x 3) of its column; normalisation (F.normalize *
@@ -54,6 +54,9 @@ constexpr uint32_t FE_OOB = 0x80000000u;
 // features carry sqrt(log2 e) (folded into multiM): a similarity is then log2(e) times REF's, the argument of
 // v_exp_f32 (2^x) directly
 constexpr float FE_SQRT_L2E = 1.2011224087864498f;
+#ifndef FE_REMAP
+#define FE_REMAP 0   // 1: GLR tiles on the loader's SIMD (see the compute waves' role map; A/B pending)
+#endif
 #ifndef FE_SWAP
 #define FE_SWAP 1   // GLR waves: edges before the conv (see iteration)
 #endif
@@ -264,7 +267,15 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   }
 
   // ---------------- compute wave: slab, tile
+  // wave -> (slab, tile): waves w and w + 4 share a SIMD (a workgroup's waves cycle over the four), and the
+  // loader (wave 8) joins waves 0 and 4 -- so those two take the lighter GLR tiles (no pair weights, no R1
+  // softmax) and the GTV tiles go to the loader-free SIMDs
+#if FE_REMAP
+  const int slab = (0xD1 >> wave) & 1;                 // GLR: waves 0, 4, 6, 7 (tiles 0..3), GTV: 1, 5, 2, 3
+  const int t4 = (0xE5E0 >> (2 * wave)) & 3;
+#else
   const int slab = wave >> 2, t4 = wave & 3;
+#endif
   const int gbase = 8 * t4 + 4 * kh;                 // the lane half's first graph
   if (8 * t4 >= G) {                                 // no graph in this tile: the barriers only
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -275,6 +286,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
   // arithmetic) is one basic block and the scheduler can overlap the MFMAs with the edges' VALU work
   auto run = [&](auto sl_tag) __attribute__((always_inline)) {
   constexpr int slab = decltype(sl_tag)::value;
+  constexpr bool EDGES_FIRST = FE_SWAP && slab == 1;
   float M[FE_GH][3];
   int sg[FE_GH];
 #pragma unroll
@@ -290,7 +302,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       slab == 0 ? a.c + (int64_t)b * G * 2 * HW : nullptr, 0, slab == 0 ? (int)((int64_t)G * 2 * HW * 4) : 0,
       0x00020000);
   const bool lane_out = col < W;
-  const float* const at = aimg + wave * FE_AIMG + 4 * lane;
+  const float* const at = aimg + (4 * slab + t4) * FE_AIMG + 4 * lane;   // the tile's A images
   float* const hw_wave = hring + wave * FE_HR * FE_HROW;
   float fw[3][FE_GH][3];   // normalised features of three consecutive rows (rotating)
   float wdn_prev[FE_GH];
@@ -482,9 +494,9 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
         edges(r0 - 3 + k, IP{}, IQ{}, IN{}, hw_wave + jp * FE_HROW, hw_wave + jq * FE_HROW, hw_wave + jn * FE_HROW);
       }
     };
-    // the two compute waves of a SIMD (one GTV, one GLR: waves w, w + 4) run the phases in opposite orders, so
-    // that one's dependent MFMA chain overlaps the other's edge arithmetic (both in lockstep after the barrier)
-    if constexpr (slab == 0 || !FE_SWAP) {
+    // GTV waves conv first, GLR waves edges first: where a SIMD holds one of each, one's dependent MFMA chain
+    // overlaps the other's edge arithmetic (both in lockstep after the barrier)
+    if constexpr (!EDGES_FIRST) {
       conv();
       __builtin_amdgcn_sched_barrier(0);
       edge();

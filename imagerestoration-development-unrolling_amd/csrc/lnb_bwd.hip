@@ -260,6 +260,7 @@ template <int V> struct RowVec;
 template <> struct RowVec<1> { typedef float T; };
 template <> struct RowVec<2> { typedef float __attribute__((ext_vector_type(2))) T; };
 template <> struct RowVec<4> { typedef float __attribute__((ext_vector_type(4))) T; };
+template <> struct RowVec<8> { typedef float __attribute__((ext_vector_type(8))) T; };
 
 template <int V>
 __device__ __forceinline__ void row_load(float (&d)[V], const float* p) {
@@ -767,6 +768,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_kernel(
 // weight gradient (the register kernel loaded them twice).  Same expressions and order as
 // dw3_gate_row_bwd_kernel<V, true>: the outputs agree to fp32 contraction, the reductions bitwise.
 constexpr int DW3R_D = 4;   // ring slots (DMAs DW3R_D - 1 iterations ahead)
+// ring slots per V: three at V = 8 (2-KB rows: 72 KB per 4-wave workgroup, two workgroups per CU)
+__host__ __device__ constexpr int dw3_ring_depth(int V) { return V == 8 ? 3 : DW3R_D; }
 // grr_lnb_set_bwd_ring: 1 (default) the ring kernel where it applies (W % 4 == 0, 16-byte aligned planes),
 // 0 the register kernel (A/B and tests)
 int g_dw3_bwd_ring = 1;
@@ -815,18 +818,21 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
   Dw3RowGeom q;
   if (!dw3_row_geom<V>(q, hid, H, W, sseg, nsegs, nwaves)) return;   // q.plane = b hid + j, q.c = j
   constexpr int RW = 64 * V;                                          // floats per ring row
-  float* const ring = dw3_ring + (threadIdx.x >> 6) * (DW3R_D * 3 * RW);
+  constexpr int D = dw3_ring_depth(V);                                // ring slots
+  float* const ring = dw3_ring + (threadIdx.x >> 6) * (D * 3 * RW);
   const int64_t HW = (int64_t)H * W;
   const int64_t bq = q.plane / hid, j = q.c;
   const int64_t pm0 = (bq * 2 * hid + j) * HW, pv0 = pm0 + (int64_t)hid * HW;
   const float* const gq0 = gq + (int64_t)q.plane * HW;   // plane bases (wave-uniform; SGPRs at the DMA)
   const float* const hm0 = hh + pm0;
   const float* const hv0 = hh + pv0;
-  // the lane's 16-byte chunk of a row (Dw3RingGeom; W % 4 == 0): the strip's columns x0 + 4 lane
+  // DMA d of a ring row, lane l: the 16-byte chunk d LANES + l, the strip's columns x0 + 4 (d LANES + l)
+  // (Dw3RingGeom; W % 4 == 0): one DMA per row at V <= 4, two at V = 8
   typedef Dw3RingGeom<V> RG;
-  static_assert(RG::RW == RW && RG::NDMA == 1, "the ring kernel's issue path moves one DMA per ring row");
+  static_assert(RG::RW == RW, "ring row size");
   const int x0 = q.c0 - V * q.lane;
-  const uint32_t voff = (uint32_t)dw3_ring_src_col(x0, q.lane, W) * 4u;
+  const uint32_t voff = (uint32_t)dw3_ring_src_col(x0, q.lane, W) * 4u;                    // DMA 0
+  const uint32_t voff1 = (uint32_t)dw3_ring_src_col(x0, RG::LANES + q.lane, W) * 4u;      // DMA 1 (V = 8)
   const bool dma_lane = q.lane < RG::LANES;
   auto issue = [&](int r, int sl) {   // rows of iteration r: gq row r + 1, hh rows r + 2
     if (dma_lane) {
@@ -834,11 +840,17 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
       dma_row16s(uniform_ptr(gq0 + (int64_t)clampi(r + 1, 0, H - 1) * W), voff, dst);
       dma_row16s(uniform_ptr(hm0 + (int64_t)clampi(r + 2, 0, H - 1) * W), voff, dst + RW);
       dma_row16s(uniform_ptr(hv0 + (int64_t)clampi(r + 2, 0, H - 1) * W), voff, dst + 2 * RW);
+      if constexpr (RG::NDMA == 2) {   // the second KB of each 2-KB row
+        dma_row16s(uniform_ptr(gq0 + (int64_t)clampi(r + 1, 0, H - 1) * W), voff1, dst + RG::LANES * 4);
+        dma_row16s(uniform_ptr(hm0 + (int64_t)clampi(r + 2, 0, H - 1) * W), voff1, dst + RW + RG::LANES * 4);
+        dma_row16s(uniform_ptr(hv0 + (int64_t)clampi(r + 2, 0, H - 1) * W), voff1, dst + 2 * RW + RG::LANES * 4);
+      }
     }
   };
-  // the first DW3R_D - 1 iterations' rows
+  static_assert(RG::NDMA <= 2, "ring kernel issue path: one or two DMAs per ring row");
+  // the first D - 1 iterations' rows
 #pragma unroll
-  for (int k = 0; k < DW3R_D - 1; ++k) issue(q.r0 + k, k);
+  for (int k = 0; k < D - 1; ++k) issue(q.r0 + k, k);
   const float s = scale[0];
   float wm[9], wv[9];
 #pragma unroll
@@ -939,9 +951,9 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
   float* const ghv = gh + pv0 + q.cl0;
   int sl = 0;
   for (int r = q.r0; r < q.r1; ++r) {
-    // iteration r's rows landed: after them the wave issued the next DW3R_D - 2 iterations' DMAs (3 each)
+    // iteration r's rows landed: after them the wave issued the next D - 2 iterations' DMAs (3 NDMA each)
     // and its own stores (vmcnt counts those too: the wait is conservative)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (DW3R_D - 2)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * RG::NDMA * (D - 2)) : "memory");
     const float* slot = ring + sl * (3 * RW) + V * q.lane;
     float g2[V];
     row_load<V>(g2, slot);                  // gq row r + 1
@@ -950,8 +962,8 @@ __global__ __launch_bounds__(NT) void dw3_gate_row_bwd_ring_kernel(
     ghp_row(r + 1, g2, Hm[1], Hm[2], Hm[3], Hv[1], Hv[2], Hv[3], Gm[2], Gv[2]);
     plane(Gm, Hm[0], Hm[1], Hm[2], wm, accm, r, ghm);
     plane(Gv, Hv[0], Hv[1], Hv[2], wv, accv, r, ghv);
-    issue(r + DW3R_D - 1, sl == 0 ? DW3R_D - 1 : sl - 1);   // the slot iteration r - 1 read
-    sl = sl == DW3R_D - 1 ? 0 : sl + 1;
+    issue(r + D - 1, sl == 0 ? D - 1 : sl - 1);   // the slot iteration r - 1 read
+    sl = sl == D - 1 ? 0 : sl + 1;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       Gm[0][k] = Gm[1][k]; Gm[1][k] = Gm[2][k];
@@ -982,6 +994,13 @@ int dw3_row_vec(int W) {
   if (W % 4 == 0) return 4;
   return 0;
 }
+// the ring kernel's one-strip instance: 256 < W <= 512, W % 8 == 0 -- 8 columns per lane cover the row, no halo
+// columns (round 5's V = 4 strips read 1.5x the columns at W = 512)
+#ifndef GRR_DW3_V8
+#define GRR_DW3_V8 0   // (A/B pending on the GPU)
+#endif
+bool dw3_ring_v8_shape(int W) { return W > 256 && W <= 512 && W % 8 == 0; }
+bool dw3_ring_v8(int W) { return GRR_DW3_V8 && dw3_ring_v8_shape(W); }
 // rows per wave: whole planes while the grid has >= 4096 waves, else segments of >= 32 rows
 int dw3_row_seg(int H, int64_t planes) {
   int sseg = H;
@@ -1063,10 +1082,15 @@ grr_status launch_dw3_gate_row(const float* hp, const float* gq, const float* sc
   grr_status st = rs.alloc(what);
   if (st != GRR_OK) return st;
   const Red gw = rs.red(iw), gdot = rs.red(id);
-  if (!FFN && !hp && g_dw3_bwd_ring && W % 4 == 0 && (uintptr_t)gq % 16 == 0 && (uintptr_t)hh % 16 == 0 &&
+  if constexpr (V == 8) {   // ring kernel only (grr_lnb_gate_dw3_bwd checked dw3_ring_v8)
+    hipLaunchKernelGGL(dw3_gate_row_bwd_ring_kernel<8>, grid, dim3(NT),
+                       (NT / 64) * dw3_ring_depth(8) * 3 * 64 * 8 * sizeof(float), s, gq, scale, hh, wdw, gh, gw, gdot,
+                       hid, H, W, sseg, nsegs, nwaves);
+  } else if (!FFN && !hp && g_dw3_bwd_ring && W % 4 == 0 && (uintptr_t)gq % 16 == 0 && (uintptr_t)hh % 16 == 0 &&
       HW_ALIGNED(H, W)) {
-    hipLaunchKernelGGL(dw3_gate_row_bwd_ring_kernel<V>, grid, dim3(NT), (NT / 64) * DW3R_D * 3 * 64 * V * sizeof(float),
-                       s, gq, scale, hh, wdw, gh, gw, gdot, hid, H, W, sseg, nsegs, nwaves);
+    hipLaunchKernelGGL(dw3_gate_row_bwd_ring_kernel<V>, grid, dim3(NT),
+                       (NT / 64) * dw3_ring_depth(V) * 3 * 64 * V * sizeof(float), s, gq, scale, hh, wdw, gh, gw, gdot,
+                       hid, H, W, sseg, nsegs, nwaves);
   } else if constexpr (FFN) {   // the FeedForward reverse always recomputes the depthwise output
     hipLaunchKernelGGL((dw3_gate_row_bwd_kernel<V, true, true>), grid, dim3(NT), 0, s, hp, gq, scale, hh, wdw, gh, gw,
                        gdot, hid, H, W, sseg, nsegs, nwaves);
@@ -1229,6 +1253,10 @@ grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int 
 grr_status grr_dw3_ring_check(int W) {
   clear_error();
   GRR_REQUIRE(W >= 4 && W % 4 == 0, GRR_ERR_INVALID_ARG, "grr_dw3_ring_check: the ring kernel needs W %% 4 == 0");
+  if (grr::dw3_ring_v8_shape(W)) {   // (checked whether or not the build launches it)
+    const grr_status st = grr::dw3_ring_replay<8>(W);
+    if (st != GRR_OK) return st;
+  }
   switch (grr::dw3_row_vec(W)) {
     case 1: return grr::dw3_ring_replay<1>(W);
     case 2: return grr::dw3_ring_replay<2>(W);
@@ -1258,6 +1286,9 @@ grr_status grr_lnb_gate_dw3_bwd(const float* hp, const float* gq, const float* s
               "grr_lnb_gate_dw3_bwd: needs W <= 64, even W <= 128 or W %% 4 == 0, and 4V-byte aligned planes");
   hipStream_t s = (hipStream_t)stream;
   const char* what = "grr_lnb_gate_dw3_bwd";
+  if (!hp && g_dw3_bwd_ring && dw3_ring_v8(W) && (uintptr_t)gq % 32 == 0 && (uintptr_t)hh % 32 == 0 &&
+      (uintptr_t)gh % 32 == 0)
+    return launch_dw3_gate_row<8>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
   switch (V) {
     case 1: return launch_dw3_gate_row<1>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);
     case 2: return launch_dw3_gate_row<2>(hp, gq, scale, hh, wdw, gh, gwdw, gdot, B, hid, H, W, s, what);

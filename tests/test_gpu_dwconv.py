@@ -95,7 +95,8 @@ def test_gate_dw3_rows_vs_autograd(K, shape, ffn):
 
 
 RING_SHAPES = [(2, 3, 9, 32), (1, 4, 20, 100), (1, 2, 33, 256), (1, 2, 10, 300), (1, 3, 12, 512), (1, 1, 6, 744),
-               (1, 2, 300, 64), (1, 2, 1, 64), (1, 2, 2, 128), (2, 1, 5, 1000), (1, 5, 40, 200), (1, 2, 7, 102)]
+               (1, 2, 300, 64), (1, 2, 1, 64), (1, 2, 2, 128), (2, 1, 5, 1000), (1, 5, 40, 200), (1, 2, 7, 102),
+               (1, 2, 9, 264), (2, 3, 70, 512)]   # the one-strip V = 8 instance: 33 of 64 lanes, a whole row
 
 
 @pytest.mark.parametrize("shape", RING_SHAPES, ids=lambda s: "b{}hid{}h{}w{}".format(*s))
