@@ -997,7 +997,7 @@ int dw3_row_vec(int W) {
 // the ring kernel's one-strip instance: 256 < W <= 512, W % 8 == 0 -- 8 columns per lane cover the row, no halo
 // columns (round 5's V = 4 strips read 1.5x the columns at W = 512)
 #ifndef GRR_DW3_V8
-#define GRR_DW3_V8 0   // (A/B pending on the GPU)
+#define GRR_DW3_V8 1   // 32 x 512^2: hid 96 5.61 -> 4.58 ms, hid 192 11.16 -> 9.03 ms per launch (scripts/gpu_r06_u.sh)
 #endif
 bool dw3_ring_v8_shape(int W) { return W > 256 && W <= 512 && W % 8 == 0; }
 bool dw3_ring_v8(int W) { return GRR_DW3_V8 && dw3_ring_v8_shape(W); }

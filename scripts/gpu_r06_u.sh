@@ -10,7 +10,7 @@ for rep in 1 2; do
 for hid in 96 192; do
   for v in base v8; do
     lib=imagerestoration-development-unrolling_amd/libgrr.so; [ $v = base ] || lib=exp/libgrr_$v.so
-    GRR_LIB=$lib timeout -k 10 120 python scripts/micro.py --kernel gate_dw3_bwd --size 512 --batch 32 --fts $hid --iters 10 > $O/m_${v}_$hid.txt 2>&1 || exit 1
+    GRR_LIB=$lib timeout -k 10 120 python scripts/micro.py --kernel gate_dw3_bwd --size 512 --batch 32 --graphs 1 --fts $hid --iters 10 > $O/m_${v}_$hid.txt 2>&1 || exit 1
     echo "hid $hid $v: $(grep -h 'mean=' $O/m_${v}_$hid.txt | tr '\n' ' ')"
   done
 done
