@@ -366,6 +366,7 @@ def main():
             "frac": round(rp["tflops"] / SPLIT_F16_PEAK_TFLOPS, 4), "flops_per_launch": rp["flops_per_launch"],
             "mean_launch_ms": round(rp["mean_ms"], 4), "launches": rp["launches"],
             "hbm_gbps": round(rp["gbps"], 1), "bytes_per_launch": rp["bytes_per_launch"],
+            "traffic": load_traffic_file("traffic_lnb_rep.json", "lnb_rep_kernel", b),
             "note": "algorithmic fp32 flops (LN, W1, depthwise, gate, W2, skip) / HIP-event time against the "
                     "dense fp16 rate / 3 (both GEMMs on exact fp16 two-term splits; the depthwise folded into "
                     "GEMM1 as a 27-deep im2col operand); bytes: src in, out written"}
