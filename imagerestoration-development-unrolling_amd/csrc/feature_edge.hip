@@ -54,9 +54,6 @@ constexpr uint32_t FE_OOB = 0x80000000u;
 // features carry sqrt(log2 e) (folded into multiM): a similarity is then log2(e) times REF's, the argument of
 // v_exp_f32 (2^x) directly
 constexpr float FE_SQRT_L2E = 1.2011224087864498f;
-#ifndef FE_AHEAD2
-#define FE_AHEAD2 0   // 1: loader with main rows two ahead (halo batches loaded on their own; A/B pending)
-#endif
 #ifndef FE_REMAP
 #define FE_REMAP 1   // GLR tiles on the loader's SIMD (the compute waves' role map): 1.637 -> 1.604 ms at 64 x 256^2
 #endif
@@ -220,7 +217,7 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
     auto issue_main = [&](int k) { load(0, clampi(r0 - 1 + k, 0, H - 1), colc); };
     auto issue_halo = [&](int m) { load(1, clampi(r0 - 1 + FE_HB * m + hn / 3, 0, H - 1), hcol); };
     auto put = [&](int set, float* slot) __attribute__((always_inline)) {   // the loaded pixels of set -> a slot
-      if (!FE_AHEAD2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (FE_AHEAD2: the caller waits)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       float mx = 0.f;
 #pragma unroll
       for (int s = 0; s < FE_KS; ++s)
@@ -244,55 +241,6 @@ __global__ __launch_bounds__(FE_THREADS, 1) void feat_edge_kernel(FeArgs a) {
       }
       if (kh == 0) reinterpret_cast<int*>(slot + FE_IMG)[n] = ep;
     };
-#if FE_AHEAD2
-    // Main rows two ahead: rows r + 1 and r + 2 in flight in the two register sets (row parity); a halo batch
-    // is loaded on its own into the set a put just freed (once per FE_HB rows: that load's latency is exposed)
-    constexpr int LROW = IN8 ? 2 * FE_KS : 8 * FE_KS;   // loads per row
-    static_assert(LROW <= 63, "vmcnt");
-    auto ld_main = [&](int k) __attribute__((always_inline)) {   // (set index compile-time in each branch)
-      if (k & 1) load(1, clampi(r0 - 1 + k, 0, H - 1), colc);
-      else load(0, clampi(r0 - 1 + k, 0, H - 1), colc);
-    };
-    auto ld_halo = [&](int m, int set) __attribute__((always_inline)) {
-      if (set) load(1, clampi(r0 - 1 + FE_HB * m + hn / 3, 0, H - 1), hcol);
-      else load(0, clampi(r0 - 1 + FE_HB * m + hn / 3, 0, H - 1), hcol);
-    };
-    auto put_set = [&](int set, float* slot) __attribute__((always_inline)) {
-      if (set) put(1, slot);
-      else put(0, slot);
-    };
-    ld_main(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    put_set(0, ring);
-    ld_halo(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    put_set(0, himg);
-    if (1 <= NI - 2) ld_main(1);
-    if (2 <= NI - 2) ld_main(2);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // A images, slot 0 and halo batch 0
-    asm volatile("" ::: "memory");
-    for (int k = 0; k < NI3; ++k) {
-      const int r = k + 1;   // the row put in this iteration, read by the compute waves in iteration r
-      if (r <= NI - 2) {
-        // row r + 1 (issued an iteration later) may stay in flight
-        if (r + 1 <= NI - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LROW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        put_set(r & 1, ring + (r & 1) * FE_SLOT);
-        if (r % FE_HB == 0) {   // batch r / FE_HB, read in iteration r only, through the set just freed
-          ld_halo(r / FE_HB, r & 1);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          put_set(r & 1, himg);
-        }
-        if (r + 2 <= NI - 2) ld_main(r + 2);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-#endif
     issue_main(0);
     issue_halo(0);
     put(0, ring);
