@@ -537,13 +537,16 @@ grr_status grr_lnb_gate_bwd_scaled(const float* hp, const float* gq, const float
 grr_status grr_lnb_dw3_gate(const float* hh, const float* wdw, float* gate, int B, int hid, int H, int W,
                             void* stream);
 /* Kernel knob (no reference counterpart): 1 (default) runs grr_lnb_gate_dw3_bwd's recomputing variant (hp NULL)
- * with its operand rows through a per-wave LDS-DMA ring where W % 4 == 0 and the planes are 16-byte aligned,
- * 0 the register-prefetch row kernel.  Process-wide; results agree to fp32 rounding.  A/B and tests. */
+ * with its operand rows through a per-wave LDS-DMA ring where W % 4 == 0 and the planes are 16-byte aligned
+ * (one strip of 8-column lanes for 256 < W <= 512, W % 8 == 0, 32-byte aligned planes), 0 the
+ * register-prefetch row kernel.  Process-wide; results agree to fp32 rounding.  A/B and tests. */
 grr_status grr_lnb_set_bwd_ring(int enable);
 /* Host replay of the gate + depthwise reverse ring kernel's DMA geometry at image width W (W % 4 == 0): GRR_OK
  * when every ring-row DMA of every column strip writes inside its ring row and reads inside its image row
  * (the invariant whose violation faulted round 5's two-DMAs-per-row attempt), else GRR_ERR_SHAPE with the
- * first violation in grr_last_error.  No device work. */
+ * first violation in grr_last_error.  Covers the strip instance of the width (V = 1, 2, 4) and, for
+ * 256 < W <= 512 with W % 8 == 0, the one-strip V = 8 instance (two DMAs per 2-KB ring row) that
+ * grr_lnb_gate_dw3_bwd runs there.  No device work. */
 grr_status grr_dw3_ring_check(int W);
 /* grr_lnb_gate_bwd_scaled and grr_dwconv3_bwd in one row pass (ghp stays on chip): hp [B,2hid,H,W]
  * (depthwise output; NULL = recomputed from hh in-kernel), gq [B,hid,H,W], hh [B,2hid,H,W]
