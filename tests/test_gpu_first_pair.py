@@ -144,3 +144,38 @@ def test_filter_with_first_pair_matches_without(irdu, model):
         K.FIRST_PAIR = saved
     assert math.isfinite(float(fused.abs().max()))
     assert rel_err(fused, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("bh", [(1, 256), (2, 130)], ids=["b1h256", "b2h130"])
+def test_first_pair_f6_segmented_vs_oracle(irdu, bh):
+    """MixtureGTVGLR at F = 6 (the v1.0 first filter block: two channel groups of 3), S = 10, W = 256 so the
+    first-pair pass runs, on a segmented grid (B G groups far below the step-2 grid floor: 64-row segments at
+    H = 256, a ragged last segment at H = 130) against the CPU oracle (REF:707-811) at the north_star
+    tolerance (1e-4 normwise), not against the HIP launch sequence it replaces."""
+    from oracle import graph_oracle as O
+    from irdu_amd import kernels as K
+    from tests.test_gpu_parity import assert_close, sd_cpu
+    B, H = bh
+    G, F = 2, 6
+    torch.manual_seed(4600 + H)
+    m = irdu.MixtureGTVGLR(G, F, 0.5, 0.1, [[1e-3], [1e-4]], [[1e-4], [1e-4]], [[1e-4], [1e-4]], n_cgd_iters=10)
+    perturb_mixture(m, 46 + B)
+    g = torch.Generator().manual_seed(46 + B)
+    with torch.no_grad():   # mu, rho in [0.01, 0.06]: the ten-stage iteration stays bounded at F = 6 and
+        for q in (m.muys00, m.muys01, m.ro00, m.ro01):   # still moves the output by ~0.2 (perturb_mixture's
+            q.copy_(torch.log(0.01 + 0.05 * torch.rand(q.shape, generator=g)))   # 0.05-0.6 diverges here)
+    x = torch.rand(B, G * F, H, 256)
+    ref = O.mixture_forward(x, sd_cpu(m), G, "v1")
+    md = m.to(DEV).eval()
+    xd = x.to(DEV)
+    assert K.first_pair_supported(xd, G) == K.FIRST_PAIR
+    saved = K.FIRST_PAIR
+    try:
+        with torch.no_grad():
+            K.FIRST_PAIR = True
+            got = md(xd)
+    finally:
+        K.FIRST_PAIR = saved
+    assert float(ref.abs().max()) < 2.0 and float((ref - x).abs().max()) > 0.05
+    assert torch.isfinite(got).all()
+    assert_close(got, ref)
