@@ -111,6 +111,7 @@ SIGNATURES = {
     "grr_bwd_pair": [P, P, P, P, Fl, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_prox": [P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],
     "grr_bwd_set_term_rows": [I],
+    "grr_bwd_set_term_tail": [I],
     "grr_bwd_set_term_acc_max_w": [I],
     "grr_lnb_set_bwd_ring": [I],
     "grr_bwd_term_fused": [I, P, P, P, P, P, P, Fl, P, P, P, P, P, I, I, I, I, I, P],

@@ -965,6 +965,12 @@ int g_term_rows = 2;
 // profiles/r05/term/ab_acc_policy.txt: msgf 65.2 -> 63.8 ms, C4 942 -> 933 ms against the pass inside at
 // every width).  grr_bwd_set_term_acc_max_w (A/B and tests)
 int g_term_acc_max_w = 128;
+// ring kernel: the narrow V = 1 tail launch for a row's last strip (launch_term_row); GRR_TERM_TAIL=0 or
+// grr_bwd_set_term_tail(0) turns it off (A/B and tests)
+int g_term_tail = [] {
+  const char* e = getenv("GRR_TERM_TAIL");
+  return e ? atoi(e) : 1;
+}();
 
 template <int V> struct RowT;
 template <> struct RowT<1> { typedef float T; };
@@ -1072,7 +1078,8 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
     const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ taps,
     const float* __restrict__ w, const float* __restrict__ log_gamma, const float* __restrict__ scale, float coef,
     float* __restrict__ v_out, float* __restrict__ gx_out, float* __restrict__ gw, Red ggam, Red gdot,
-    Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk, int ring_d) {
+    Red gtaps, int G, int F, int H, int W, int sseg, int nsegs, uint32_t nblk, int ring_d, int cbeg, int nstr,
+    uint32_t slot0) {
   constexpr int WPL = MODE == 1 ? 2 : 4;   // weight planes per graph
   constexpr bool kGwDma = !RING && term_gw_dma(MODE, V, STRIPS);
   // weight-gradient partials [row parity][channel][plane][64 V columns] (dynamic: 2 F WPL 64 V floats),
@@ -1097,9 +1104,11 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   // columns, 4 halo columns per side (16-byte aligned DMA chunks)
   constexpr int STEP = RING ? 64 * V - 8 : 62 * V;
   constexpr int HALO = RING ? 4 : V;
+  // (STRIPS) nstr strips owning columns cbeg + STEP s ..; a launch may cover only part of the row (the
+  // ring kernel's narrow tail launch, launch_term_row)
   int strip = 0, nstrips = 1;
   if constexpr (STRIPS) {
-    nstrips = (W + STEP - 1) / STEP;
+    nstrips = nstr;
     strip = (int)(unit % (uint32_t)nstrips);
     unit /= (uint32_t)nstrips;
   }
@@ -1113,8 +1122,8 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   int cl0 = on ? c0 : W - V;
   int x0 = 0;                                // the strip's first column
   if constexpr (STRIPS) {
-    x0 = strip == 0 ? 0 : strip * STEP - HALO;
-    const int lo = strip * STEP, hi = min(lo + STEP, W);
+    const int lo = cbeg + strip * STEP, hi = min(lo + STEP, W);
+    x0 = lo == 0 ? 0 : lo - HALO;
     c0 = x0 + lc0;
     on = c0 >= lo && c0 < hi;
     cl0 = clampi(c0, 0, W - V);
@@ -1561,7 +1570,7 @@ __global__ __launch_bounds__(RING ? 64 * (TermRingMax<V>::F + 1) : 64 * TermRowM
   }
   // per-graph / per-channel reductions: wave sums into this wave's slots.  Slot of the workgroup:
   // (b, segment, strip); the per-graph scalars take one slot per channel wave of it.
-  const uint32_t wslot = ((uint32_t)(bg / G) * nsegs + seg) * nstrips + strip;
+  const uint32_t wslot = slot0 + ((uint32_t)(bg / G) * nsegs + seg) * nstrips + strip;
   {
     const float d = wave_sum(dot);
     if (lane == 0) red_put(gdot, gi, wslot * F + f, coef * d);
@@ -1894,21 +1903,38 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
   TermReds R(s);
   grr_status st = R.setup(MODE, gdot, ggam, gtaps, G, F, wgs * F, wgs);
   if (st != GRR_OK) return st;
+  // Narrow tail (ring kernel, V > 1): when the last strip owns no more columns than a one-column-lane strip
+  // (64 - 8), the row's first nstrips - 1 strips run here and the last one as a V = 1 launch on the same
+  // stream (W = 512: 2 x 256 + 64 lane columns instead of 3 x 256 at V = 4, 4 x 128 + 64 instead of 5 x 128
+  // at V = 2); its reduction slots follow the main launch's.  Same per-column arithmetic.
+  size_t tail_lds = 0;
+  const bool tail = ring_d && V > 1 && nstrips > 1 && W - (nstrips - 1) * step <= 56 && g_term_tail &&
+                    F <= TermRingMax<1>::F && term_ring_fits(MODE, 1, F, padj, ring_d, &tail_lds);
+  const int nmain = tail ? nstrips - 1 : nstrips;
+  const uint32_t nblk_main = (uint32_t)((int64_t)B * G * nmain * nsegs);
 #define GRR_TERM_ROW_LAUNCH(STRIPS, PADJ)                                                                   \
   hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, PADJ>), dim3(nblk), dim3(64 * F), lds, s, x, g, taps, w, lg, \
                      scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, W, sseg,   \
-                     nsegs, nblk, 0)
-#define GRR_TERM_RING_LAUNCH(STRIPS, PADJ)                                                                   \
-  hipLaunchKernelGGL((term_row_kernel<MODE, V, STRIPS, PADJ, true>), dim3(nblk), dim3(64 * (F + 1)), lds, s, x, g, \
+                     nsegs, nblk, 0, 0, nstrips, 0u)
+#define GRR_TERM_RING_LAUNCH(VV, STRIPS, PADJ, NB, LDS, CB, NS, SL0)                                           \
+  hipLaunchKernelGGL((term_row_kernel<MODE, VV, STRIPS, PADJ, true>), dim3(NB), dim3(64 * (F + 1)), LDS, s, x, g, \
                      taps, w, lg, scale, coef, v, gx, gw, R.rs.red(R.ig), R.rs.red(R.id), R.rs.red(R.it), G, F, H, \
-                     W, sseg, nsegs, nblk, ring_d)
+                     W, sseg, nsegs, NB, ring_d, CB, NS, SL0)
   if (ring_d) {
     if (padj) {
-      if (nstrips > 1) GRR_TERM_RING_LAUNCH(true, true);
-      else GRR_TERM_RING_LAUNCH(false, true);
+      if (nstrips > 1) GRR_TERM_RING_LAUNCH(V, true, true, nblk_main, lds, 0, nmain, 0u);
+      else GRR_TERM_RING_LAUNCH(V, false, true, nblk, lds, 0, 1, 0u);
     } else {
-      if (nstrips > 1) GRR_TERM_RING_LAUNCH(true, false);
-      else GRR_TERM_RING_LAUNCH(false, false);
+      if (nstrips > 1) GRR_TERM_RING_LAUNCH(V, true, false, nblk_main, lds, 0, nmain, 0u);
+      else GRR_TERM_RING_LAUNCH(V, false, false, nblk, lds, 0, 1, 0u);
+    }
+    if constexpr (V > 1) {
+      if (tail) {
+        const uint32_t nblk_tail = (uint32_t)((int64_t)B * G * nsegs);
+        const uint32_t slot_tail = (uint32_t)((int64_t)B * nsegs * nmain);
+        if (padj) GRR_TERM_RING_LAUNCH(1, true, true, nblk_tail, tail_lds, nmain * step, 1, slot_tail);
+        else GRR_TERM_RING_LAUNCH(1, true, false, nblk_tail, tail_lds, nmain * step, 1, slot_tail);
+      }
     }
   } else if (padj) {
     if constexpr (V < 4) GRR_TERM_ROW_LAUNCH(false, true);   // term_acc_shape_ok: one strip, V <= 2
@@ -2221,6 +2247,13 @@ grr_status grr_bwd_set_term_acc_max_w(int w) {
   clear_error();
   GRR_REQUIRE(w >= 0, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_acc_max_w: w >= 0");
   g_term_acc_max_w = w;
+  return GRR_OK;
+}
+
+grr_status grr_bwd_set_term_tail(int enable) {
+  clear_error();
+  GRR_REQUIRE(enable == 0 || enable == 1, GRR_ERR_INVALID_ARG, "grr_bwd_set_term_tail: 0 or 1");
+  g_term_tail = enable;
   return GRR_OK;
 }
 

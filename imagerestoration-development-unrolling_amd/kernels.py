@@ -131,6 +131,11 @@ def set_term_rows(enable) -> None:
     TERM_ROWS = level > 0
 
 
+def set_term_tail(enable: bool) -> None:
+    """The wide ring-kernel term reverse's last column strip as a one-column-lane launch (default on)."""
+    _native.call("grr_bwd_set_term_tail", int(bool(enable)))
+
+
 def set_term_acc_max_w(w: int) -> None:
     """Widest image where the LDS-ring term reverse takes the x-gradient pass inside (default 128)."""
     _native.call("grr_bwd_set_term_acc_max_w", int(w))

@@ -441,6 +441,11 @@ grr_status grr_bwd_set_term_acc_max_w(int w);
  * kernel; 0 the per-pixel kernels.  grr_bwd_edge_weights: row kernel for 1 and 2.
  * Process-wide; results agree to fp32 rounding. */
 grr_status grr_bwd_set_term_rows(int enable);
+/* Kernel knob for tests and benchmarks (no reference counterpart): 1 (default; env GRR_TERM_TAIL) runs the
+ * last column strip of a wide ring-kernel term reverse (W > 64 V, the last strip owning <= 56 columns) as
+ * a second, one-column-lane launch; 0 keeps every strip at V columns per lane.  Process-wide; results
+ * agree to fp32 rounding (the per-strip wave sums differ). */
+grr_status grr_bwd_set_term_tail(int enable);
 
 /* The three reverses above in one pass each, from x and g directly (s = S x and a = adjoint-S^T g
  * recomputed on the fly) with both tap gradients fused: mode 0 GLR (w raw), 1 pair Laplacian

@@ -93,3 +93,44 @@ def test_term_ring_bitwise_reproducible(K, mode):
     for ta, tb in zip(a, bb):
         if ta is not None:
             assert torch.equal(ta, tb)
+
+
+# W > 64 V whose last column strip owns <= 56 columns: the ring kernel runs that strip as a second,
+# one-column-lane launch (grr_bwd_set_term_tail(1), the default).  (b, G, F, H, W): W = 512 (4-column lanes:
+# 2 strips + a 16-column tail for the pair term; 2-column lanes: 4 + a 32-column tail for GLR / prox), W = 300
+# (pair term: 248 + a 52-column tail), W = 744 (2-column lanes: 6 strips + 24), W = 400 (no tail: 152 / 40 owned)
+TAIL_CASES = [(1, 2, 6, 7, 512), (2, 1, 3, 33, 512), (1, 2, 4, 8, 300), (1, 1, 2, 6, 744), (1, 2, 3, 5, 400)]
+
+
+@pytest.mark.parametrize("case", TAIL_CASES, ids=lambda c: "b{}g{}f{}h{}w{}".format(*c))
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_term_ring_tail_equals_full_strips(K, case, mode):
+    b, G, F, h, w_ = case
+    torch.manual_seed(5000 + mode * 100 + h + w_)
+    C = G * F
+    x = torch.randn(b, C, h, w_, device=DEV)
+    g = torch.randn(b, C, h, w_, device=DEV)
+    taps = torch.randn(C, 5, device=DEV) * 0.5
+    w = torch.rand(b, G, 2 if mode == 1 else 4, h, w_, device=DEV)
+    lg = torch.log(torch.linspace(0.05, 0.5, G, device=DEV)) if mode == 2 else None
+    scale = torch.rand(G, device=DEV) + 0.5
+    try:
+        K.set_term_tail(False)
+        ref = _run(K, 2, mode, x, g, taps, w, lg, scale, G)
+        K.set_term_tail(True)
+        got = _run(K, 2, mode, x, g, taps, w, lg, scale, G)
+        again = _run(K, 2, mode, x, g, taps, w, lg, scale, G)
+    finally:
+        K.set_term_tail(True)
+    for name, a, r, a2 in zip(["v", "gw", "gdot", "ggamma", "gtaps"], got, ref, again):
+        if r is None:
+            continue
+        assert torch.equal(a, a2), name           # fixed-order reductions across the two launches
+        assert torch.isfinite(a).all(), name
+        if name in ("v", "gw"):
+            assert rel_err(a, r) <= 2e-6, (name, rel_err(a, r))
+        else:
+            n = b * F * h * w_
+            sc = max(float(r.abs().max()), n ** 0.5)
+            err = float((a.double() - r.double()).abs().max())
+            assert err <= 2e-5 * sc, (name, err, sc)
