@@ -2,7 +2,7 @@
 # round 6 end: full GPU suite, smoke, the default bench line (with the round-6 traffic files), the C4 training line
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-out=gpurun_out/r06e; mkdir -p $out
+out=gpurun_out/${R06E_OUT:-r06e}; mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $out/gpu_tests.log 2>&1
 rc=$?
