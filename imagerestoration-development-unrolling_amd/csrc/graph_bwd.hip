@@ -1597,8 +1597,22 @@ int term_row_vec(int W) {
 // loaded for W = 512 against 768 with 4-column lanes, and 128 VGPRs, four waves per SIMD), the pair term
 // on 4-column lanes (measured, B32 G8 F6 512^2: GLR 4.15 -> 3.64 ms, prox 6.69 -> 4.61, pair 2.88 -> 3.33;
 // profiles/r04/term/ab_wide_v.txt); the edge-weight reverse on 4-column lanes
-int term_strip_vec(int W, int mode = 1) {
+// Round 6 (the LDS-ring kernel with the tail launch, C4 shapes, scripts/term_sweep.py, profiles/r06/tv/): the GLR
+// term at W > 256 on 4-column lanes where the ring takes it (F <= 7) without the x-gradient pass (W above the
+// pass's width cap: at 4-column lanes that pass no longer fits the ring's LDS) (512^2 F = 6: 2.15 -> 1.97 ms;
+// prox unchanged, stays on 2-column lanes), and the ring for the prox term at one-column lanes too (64^2
+// F = 12: 0.37 -> 0.24 ms, 0.72 -> 0.41; 32^2: 0.30 -> 0.21).  GRR_TERM_POLICY=0 restores the round-5
+// choices (A/B).
+static int term_policy() {
+  static const int v = [] {
+    const char* e = getenv("GRR_TERM_POLICY");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+int term_strip_vec(int W, int mode = 1, int F = 0) {
   if (term_row_vec(W)) return term_row_vec(W);
+  if (term_policy() != 0 && mode == 0 && W % 4 == 0 && F <= TermRingMax<4>::F && W > g_term_acc_max_w) return 4;
   if (mode != 1 && W % 2 == 0) return 2;
   return W % 4 == 0 ? 4 : 0;
 }
@@ -1833,12 +1847,13 @@ size_t term_row_lds(int mode, int V, int F, bool strips, bool padj) {
 }
 constexpr size_t kTermLdsMax = 160 * 1024;
 // Shapes the ring kernel takes (g_term_rows == 2): W % 4 == 0 (16-byte DMAs), F + 1 waves within its
-// launch bound, and not the one-column lanes where it measured slower (W <= 32, and the prox term at
-// W <= 64: profiles/r05/term/ab_ring_vs_register.txt)
+// launch bound, and not the one-column lanes where it measured slower for the GLR and pair terms (W <= 32:
+// profiles/r05/term/ab_ring_vs_register.txt; the prox term takes the ring there since round 6, term_policy)
 bool term_ring_shape_ok(int mode, int F, int W) {
-  const int V = term_strip_vec(W, mode);
+  const int V = term_strip_vec(W, mode, F);
   if (g_term_rows != 2 || V == 0 || W % 4 != 0 || F > (V == 4 ? TermRingMax<4>::F : TermRingMax<1>::F)) return false;
-  return V >= 2 || (W >= 64 && mode != 2);
+  if (term_policy() == 0) return V >= 2 || (W >= 64 && mode != 2);
+  return V >= 2 || W >= 64 || mode == 2;
 }
 // The ring kernel's depth (steps of rows in LDS) where it applies, else 0: the shape (above) and 16-byte
 // aligned planes.  Depth 4 (three steps of rows ahead): deeper rings measured no faster and cost
@@ -1951,7 +1966,7 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
 }
 bool term_row_ok(int mode, int F, const float* x, const float* g, const float* w, const float* v, const float* gw,
                  int W) {
-  const int V = term_strip_vec(W, mode);
+  const int V = term_strip_vec(W, mode, F);
   if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return false;
   const void* ptrs[] = {x, g, w, v, gw};
   for (const void* p : ptrs)
@@ -1965,7 +1980,7 @@ bool term_row_ok(int mode, int F, const float* x, const float* g, const float* w
 // 1.22 at B16 G32 F3 256^2 (profiles/r04/term/ab_term_acc.txt).  (Strips would also need V >= 3: P* at
 // an owned edge column reads v one halo column out.)
 bool term_acc_shape_ok(int mode, int F, int W) {
-  const int V = term_strip_vec(W, mode);
+  const int V = term_strip_vec(W, mode, F);
   if (V == 0 || V == 4 || W > 64 * V || F > TermRowMax<1>::F) return false;
   return term_row_lds(mode, V, F, false, true) <= kTermLdsMax;
 }
@@ -1973,7 +1988,7 @@ template <int MODE>
 grr_status launch_term_row_v(int B, int F, const float* x, const float* g, const float* taps, const float* w,
                              const float* lg, const float* scale, float coef, float* v, float* gx, float* gw,
                              float* ggam, float* gdot, float* gtaps, int G, int H, int W, hipStream_t s) {
-  switch (term_strip_vec(W, MODE)) {
+  switch (term_strip_vec(W, MODE, F)) {
     case 1: return launch_term_row<MODE, 1>(B, F, x, g, taps, w, lg, scale, coef, v, gx, gw, ggam, gdot, gtaps, G, H, W, s);
     case 2: return launch_term_row<MODE, 2>(B, F, x, g, taps, w, lg, scale, coef, v, gx, gw, ggam, gdot, gtaps, G, H, W, s);
     default: return launch_term_row<MODE, 4>(B, F, x, g, taps, w, lg, scale, coef, v, gx, gw, ggam, gdot, gtaps, G, H, W, s);
@@ -2310,7 +2325,7 @@ int grr_bwd_term_acc_supported(int mode, int F, int H, int W) {
   // ring (enabled, within the width cap, its DMA count and LDS at the depth it will run) or the
   // register kernel's one strip of <= 2-column lanes
   if (mode < 0 || mode > 2 || F <= 0 || H <= 0 || W <= 0 || !g_term_rows) return 0;
-  const int V = term_strip_vec(W, mode);
+  const int V = term_strip_vec(W, mode, F);
   if (V == 0 || F > (V == 4 ? TermRowMax<4>::F : TermRowMax<1>::F)) return 0;
   if (term_ring_shape_ok(mode, F, W)) {
     if (W > g_term_acc_max_w) return 0;   // the policy cap (wider levels fold the pass into the CG glue)

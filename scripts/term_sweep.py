@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rows", default="1,2")
     ap.add_argument("--modes", default="0,1,2")
+    ap.add_argument("--levels", default="", help="comma list of shapes to run (L0f,L0h,...; default all)")
+    ap.add_argument("--tail", default="1", help="comma list of grr_bwd_set_term_tail settings (0,1)")
     args = ap.parse_args()
     irdu_amd.load_native()
     dev = torch.device("cuda", 0)
@@ -33,6 +35,8 @@ def main():
     for lvl, (c, g) in enumerate(zip(DIMS, GRAPHS)):
         for half in (0, 1):
             s = args.size >> (lvl + half)
+            if args.levels and f"L{lvl}{'h' if half else 'f'}" not in args.levels.split(","):
+                continue
             b = args.batch
             x = torch.randn(b, c, s, s, device=dev)
             gg = torch.randn_like(x)
@@ -46,8 +50,9 @@ def main():
                 gx = torch.zeros_like(x)
                 nbytes = 4 * (3 * x.numel() + 3 * wt.numel())
                 line = f"L{lvl}{'h' if half else 'f'} C={c:3d} G={g:2d} F={c // g:2d} {s:3d}^2 mode {mode}:"
-                for rows in map(int, args.rows.split(",")):
+                for rows, tail in [(r, t) for r in map(int, args.rows.split(",")) for t in map(int, args.tail.split(","))]:
                     K.set_term_rows(rows)
+                    K.set_term_tail(bool(tail))
                     acc = K.term_acc_ok(mode, x, g, gg, wt)
                     if acc:
                         fn = lambda: K.bwd_term_fused_acc(mode, x, gg, taps, wt, lg, sc, 0.5, gx, gw, ggam, gdot, gt, g)  # noqa: E731
@@ -64,12 +69,14 @@ def main():
                         e1.record()
                         torch.cuda.synchronize()
                     ms = e0.elapsed_time(e1) / args.iters
-                    total[rows] = total.get(rows, 0.0) + ms
-                    line += f"  rows{rows}{'+acc' if acc else ''} {ms:7.3f} ms {nbytes / ms / 1e6:7.1f} GB/s"
+                    key = (rows, tail)
+                    total[key] = total.get(key, 0.0) + ms
+                    line += f"  rows{rows}{'+acc' if acc else ''} t{tail} {ms:7.3f} ms {nbytes / ms / 1e6:7.1f} GB/s"
                 print(line, flush=True)
                 del wt, gw
     K.set_term_rows(True)
-    print("sum of one launch per (shape, mode):", {k: round(v, 3) for k, v in total.items()})
+    K.set_term_tail(True)
+    print("sum of one launch per (shape, mode):", {f"rows{k[0]} t{k[1]}": round(v, 3) for k, v in total.items()})
 
 
 if __name__ == "__main__":
