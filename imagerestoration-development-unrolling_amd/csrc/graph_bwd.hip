@@ -1902,12 +1902,23 @@ grr_status launch_term_row(int B, int F, const float* x, const float* g, const f
   GRR_REQUIRE(ring_d || gx == nullptr || (V < 4 && W <= 64 * V), GRR_ERR_UNSUPPORTED,
               "grr_bwd_term_fused_acc: the x-gradient pass at this width needs the LDS-ring kernel "
               "(16-byte aligned planes, W %% 4 == 0)");
-  // rows per workgroup: whole planes while the grid holds >= 8192 waves, else segments >= 32 rows
+  // rows per workgroup: segments of <= 128 rows, halved further while the grid holds < 2048 waves (floor 32
+  // rows).  Round 6 on the ring kernel (C4 shapes, sum of one launch per shape and term,
+  // profiles/r06/seg/): 16.19 ms at the round-5 rule (whole planes while >= 8192 waves) against 15.40 here;
+  // GRR_TERM_MIN_WAVES / GRR_TERM_MAX_SEG override both (A/B)
   int sseg = H;
   const int step = ring_d ? 64 * V - 8 : 62 * V;   // owned columns per strip
   const int nstrips = W <= 64 * V ? 1 : (W + step - 1) / step;
   const int64_t graphs = (int64_t)B * G * nstrips;   // (b, graph, strip) units
-  while (sseg > 32 && graphs * F * ((H + sseg - 1) / sseg) < 8192) sseg = (sseg + 1) / 2;
+  static const int64_t min_waves = [] {
+    const char* e = getenv("GRR_TERM_MIN_WAVES");
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
+  }();
+  static const int max_seg = [] {
+    const char* e = getenv("GRR_TERM_MAX_SEG");
+    return e ? atoi(e) : 128;
+  }();
+  while (sseg > 32 && (graphs * F * ((H + sseg - 1) / sseg) < min_waves || sseg > max_seg)) sseg = (sseg + 1) / 2;
   const int nsegs = (H + sseg - 1) / sseg;
   const uint32_t nblk = (uint32_t)(graphs * nsegs);
   const bool padj = gx != nullptr;
