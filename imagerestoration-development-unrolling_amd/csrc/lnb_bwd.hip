@@ -1003,8 +1003,16 @@ bool dw3_ring_v8_shape(int W) { return W > 256 && W <= 512 && W % 8 == 0; }
 bool dw3_ring_v8(int W) { return GRR_DW3_V8 && dw3_ring_v8_shape(W); }
 // rows per wave: whole planes while the grid has >= 4096 waves, else segments of >= 32 rows
 int dw3_row_seg(int H, int64_t planes) {
+  static const int64_t min_waves = [] {   // GRR_DW3_MIN_WAVES / GRR_DW3_MAX_SEG: A/B of the segment split
+    const char* e = getenv("GRR_DW3_MIN_WAVES");
+    return e ? (int64_t)atoll(e) : (int64_t)4096;
+  }();
+  static const int max_seg = [] {
+    const char* e = getenv("GRR_DW3_MAX_SEG");
+    return e ? atoi(e) : (1 << 30);
+  }();
   int sseg = H;
-  while (sseg > 32 && planes * ((H + sseg - 1) / sseg) < 4096) sseg = (sseg + 1) / 2;
+  while (sseg > 32 && (planes * ((H + sseg - 1) / sseg) < min_waves || sseg > max_seg)) sseg = (sseg + 1) / 2;
   return sseg;
 }
 // Host replay of the ring kernel's DMA geometry for a launch shape (Dw3RingGeom, dw3_row_geom's strips):
